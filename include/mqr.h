@@ -1,0 +1,128 @@
+/*
+ * mqr.h -- C ABI of libmqr_hip.so, the MI355X (gfx950) TSDF fusion path.
+ *
+ * Drop-in boundary for the reference's Open3D VoxelBlockGrid usage and its numpy confidence
+ * estimator (lszmer/metaquest-3d-reconstruction).  Each entry point names the reference
+ * interface it replaces.  Conventions:
+ *   - every function returns 0 on success, non-zero on error; mqr_last_error() returns a
+ *     thread-local message (the Python layer raises RuntimeError with it, as Open3D does);
+ *   - plain pointers and sizes only; `loc` arguments say where a buffer lives:
+ *     MQR_HOST (caller-owned host memory, read/written during the call only) or
+ *     MQR_DEVICE (device pointer on the volume's device, e.g. from mqr_device_alloc);
+ *   - matrices are row-major: K = 3x3 intrinsic (Open3D convention, cx already flipped),
+ *     T_wc = 4x4 world->camera extrinsic, both float64 as the reference passes them
+ *     (o3d_utils.py:203-210);
+ *   - a volume handle is not re-entrant; several handles per process/device are fine.
+ */
+#ifndef MQR_H
+#define MQR_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MQR_HOST 0
+#define MQR_DEVICE 1
+
+typedef struct mqr_vbg mqr_vbg;    /* voxel-block-hashed TSDF volume resident in HBM */
+typedef struct mqr_geom mqr_geom;  /* extracted point cloud or triangle mesh (device-resident) */
+
+int mqr_version(void);
+const char* mqr_last_error(void);
+int mqr_device_count(int* n);
+
+/* Device memory helpers (so callers can keep inputs resident in HBM without any framework). */
+int mqr_device_alloc(int device, int64_t bytes, void** ptr);
+int mqr_device_free(int device, void* ptr);
+int mqr_memcpy(void* dst, int dst_loc, const void* src, int src_loc, int64_t bytes, int device);
+int mqr_device_synchronize(int device);
+
+/* o3d.t.geometry.VoxelBlockGrid(attr_names=('tsdf','weight'), attr_dtypes=(f32,f32), attr_channels=(1,1),
+ *                               voxel_size, block_resolution, block_count, device)
+ * -- reference call site scripts/processing/reconstruction/utils/o3d_utils.py:170-179.
+ * block_count is the initial capacity; the volume grows automatically like Open3D's hash map. */
+int mqr_vbg_create(float voxel_size, int block_resolution, int64_t block_count, int device, mqr_vbg** out);
+int mqr_vbg_destroy(mqr_vbg* v);
+/* Empty the volume in place (keeps its allocations): the state of a freshly created grid. */
+int mqr_vbg_reset(mqr_vbg* v);
+int mqr_vbg_size(mqr_vbg* v, int64_t* n_blocks);
+int mqr_vbg_capacity(mqr_vbg* v, int64_t* block_capacity);
+int mqr_vbg_params(mqr_vbg* v, float* voxel_size, int* block_resolution, int* device);
+
+/* vbg.compute_unique_block_coordinates(depth, intrinsic, extrinsic, depth_scale, depth_max,
+ *                                      trunc_voxel_multiplier)  -- o3d_utils.py:212-219.
+ * keys_out (host) must hold 4*(H/4)*(W/4) int32 triplets.  Returns 3 ("no block is touched")
+ * when nothing is touched, like upstream.  The main volume is not modified. */
+int mqr_touch(mqr_vbg* v, const float* depth, int depth_loc, int H, int W, const double* K, const double* T_wc,
+              float depth_scale, float depth_max, float trunc_mult, int32_t* keys_out, int64_t* n_out);
+
+/* vbg.integrate(block_coords, depth, intrinsic, extrinsic, depth_scale, depth_max,
+ *               trunc_voxel_multiplier)  -- o3d_utils.py:221-229.  keys: n int32 triplets (host). */
+int mqr_integrate(mqr_vbg* v, const int32_t* keys, int64_t n, const float* depth, int depth_loc, int H, int W,
+                  const double* K, const double* T_wc, float depth_scale, float depth_max, float trunc_mult);
+
+/* The whole per-frame loop of o3d_utils.integrate (:188-236): touch + integrate for B frames in
+ * order, batched on device (results identical to B sequential touch+integrate calls).
+ * depths: B*H*W float32 metric depth (0 = invalid), K: B*9, T_wc: B*16 (host float64).
+ * frame_ok (host, may be NULL): frames with frame_ok[i]==0 are skipped (missing/invalid loads).
+ * Returns 3 if a valid frame touches no block (upstream raises). */
+int mqr_integrate_frames(mqr_vbg* v, const float* depths, int depth_loc, int B, int H, int W, const double* K,
+                         const double* T_wc, const uint8_t* frame_ok, float depth_scale, float depth_max,
+                         float trunc_mult);
+
+/* Volume contents (VoxelBlockGrid.save / load payload, and the multi-GPU merge).  Blocks are in
+ * buffer order: keys n*3 int32, tsdf / weight n*R^3 float32 ([z][y][x] within a block). */
+int mqr_vbg_export(mqr_vbg* v, int32_t* keys, float* tsdf, float* weight, int loc);
+int mqr_vbg_import(mqr_vbg* v, const int32_t* keys, const float* tsdf, const float* weight, int64_t n, int loc);
+
+/* Multi-GPU merge: pack the volume against a shared, sorted union key table into
+ * [U][R^3][2] = (weight*tsdf, weight) float32 (zeros where a block is absent), and the inverse
+ * after a sum-reduce: tsdf = sum(w*tsdf)/sum(w), weight = sum(w).  Device pointers. */
+int mqr_vbg_pack_weighted(mqr_vbg* v, const int32_t* union_keys, int64_t U, float* packed);
+int mqr_vbg_unpack_weighted(mqr_vbg* v, const int32_t* union_keys, int64_t U, const float* packed);
+
+/* vbg.extract_point_cloud(weight_threshold=3.0)   -- reconstruct_scene.py:90, refine_fragment_poses.py:39
+ * vbg.extract_triangle_mesh(weight_threshold)       -- reconstruct_scene.py:105-108, 186-189 */
+int mqr_extract_points(mqr_vbg* v, float weight_threshold, mqr_geom** out);
+int mqr_extract_mesh(mqr_vbg* v, float weight_threshold, mqr_geom** out);
+int mqr_geom_counts(mqr_geom* g, int64_t* n_vertices, int64_t* n_triangles);
+/* Copy to caller buffers (positions / normals n*3 float32, triangles n*3 int32); NULL skips. */
+int mqr_geom_copy(mqr_geom* g, float* positions, float* normals, int32_t* triangles, int loc);
+int mqr_geom_free(mqr_geom* g);
+
+/* build_confidence_map / compute_pixel_error_map
+ * (confidence_estimation/estimate_depth_confidences.py:15-79, compute_pixel_error_map.py:120-220)
+ * for reference frames [ref_begin, ref_end) of an N-frame sequence, all on the device at once.
+ * depths: N*H*W float32 metric; K: N*9, T_cw: N*16, T_cw_inv: N*16 float32 (host);
+ * frame_ok: N bytes (host, may be NULL).  conf: (ref_end-ref_begin)*H*W float64,
+ * valid: same int32, both in `out_loc` memory.  float64 arithmetic as numpy does it. */
+int mqr_confidence(int device, const float* depths, int depth_loc, int N, int H, int W, const float* K,
+                   const float* T_cw, const float* T_cw_inv, const uint8_t* frame_ok, int ref_begin, int ref_end,
+                   int frame_range, double depth_max, double error_threshold, double* conf, int32_t* valid,
+                   int out_loc);
+int mqr_pixel_error_map(int device, const float* ref_depth, const float* tgt_depth, int H, int W, const float* K_ref,
+                        const float* K_tgt, const float* T_cw_ref, const float* T_cw_inv_tgt, const float* T_cw_tgt,
+                        double depth_max, float* err_out);
+
+/* Kernel timing (HIP events on the volume's own stream).  enable=1 starts recording every
+ * integrate-kernel launch; stats: launches, total kernel ms, union blocks, frame-blocks
+ * (sum of per-frame touched blocks), frames, and the same for touch. */
+typedef struct mqr_stats {
+    int64_t integrate_launches;
+    double integrate_ms;
+    int64_t union_blocks;
+    int64_t frame_blocks;
+    int64_t frames;
+    int64_t touch_launches;
+    double touch_ms;
+    int64_t pixels;
+} mqr_stats;
+int mqr_vbg_profile(mqr_vbg* v, int enable);
+int mqr_vbg_stats(mqr_vbg* v, mqr_stats* out, int reset);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MQR_H */

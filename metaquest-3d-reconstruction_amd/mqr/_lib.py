@@ -1,0 +1,155 @@
+"""ctypes binding of libmqr_hip.so (the C ABI declared in include/mqr.h).
+
+There is no CPU fallback: if the HIP library is missing or no MI355X is visible, the product
+raises.  (The CPU restatement under oracle/ is test infrastructure only.)
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("MQR_HIP_LIB", os.path.join(_HERE, "libmqr_hip.so"))
+
+MQR_HOST = 0
+MQR_DEVICE = 1
+
+_f32p = ctypes.POINTER(ctypes.c_float)
+_f64p = ctypes.POINTER(ctypes.c_double)
+_i32p = ctypes.POINTER(ctypes.c_int32)
+_i64p = ctypes.POINTER(ctypes.c_int64)
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_vp = ctypes.c_void_p
+
+
+class MqrStats(ctypes.Structure):
+    _fields_ = [("integrate_launches", ctypes.c_int64), ("integrate_ms", ctypes.c_double),
+                ("union_blocks", ctypes.c_int64), ("frame_blocks", ctypes.c_int64), ("frames", ctypes.c_int64),
+                ("touch_launches", ctypes.c_int64), ("touch_ms", ctypes.c_double), ("pixels", ctypes.c_int64)]
+
+
+# name -> (restype, argtypes); every function returns int status
+SIGNATURES = {
+    "mqr_version": (ctypes.c_int, []),
+    "mqr_last_error": (ctypes.c_char_p, []),
+    "mqr_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+    "mqr_device_alloc": (ctypes.c_int, [ctypes.c_int, ctypes.c_int64, ctypes.POINTER(_vp)]),
+    "mqr_device_free": (ctypes.c_int, [ctypes.c_int, _vp]),
+    "mqr_memcpy": (ctypes.c_int, [_vp, ctypes.c_int, _vp, ctypes.c_int, ctypes.c_int64, ctypes.c_int]),
+    "mqr_device_synchronize": (ctypes.c_int, [ctypes.c_int]),
+    "mqr_vbg_create": (ctypes.c_int, [ctypes.c_float, ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.POINTER(_vp)]),
+    "mqr_vbg_destroy": (ctypes.c_int, [_vp]),
+    "mqr_vbg_reset": (ctypes.c_int, [_vp]),
+    "mqr_vbg_size": (ctypes.c_int, [_vp, _i64p]),
+    "mqr_vbg_capacity": (ctypes.c_int, [_vp, _i64p]),
+    "mqr_vbg_params": (ctypes.c_int, [_vp, _f32p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
+    "mqr_touch": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, _f64p, _f64p, ctypes.c_float,
+                                 ctypes.c_float, ctypes.c_float, _i32p, _i64p]),
+    "mqr_integrate": (ctypes.c_int, [_vp, _i32p, ctypes.c_int64, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, _f64p,
+                                     _f64p, ctypes.c_float, ctypes.c_float, ctypes.c_float]),
+    "mqr_integrate_frames": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _f64p,
+                                            _f64p, _u8p, ctypes.c_float, ctypes.c_float, ctypes.c_float]),
+    "mqr_vbg_export": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_int]),
+    "mqr_vbg_import": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_int64, ctypes.c_int]),
+    "mqr_vbg_pack_weighted": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp]),
+    "mqr_vbg_unpack_weighted": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp]),
+    "mqr_extract_points": (ctypes.c_int, [_vp, ctypes.c_float, ctypes.POINTER(_vp)]),
+    "mqr_extract_mesh": (ctypes.c_int, [_vp, ctypes.c_float, ctypes.POINTER(_vp)]),
+    "mqr_geom_counts": (ctypes.c_int, [_vp, _i64p, _i64p]),
+    "mqr_geom_copy": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_int]),
+    "mqr_geom_free": (ctypes.c_int, [_vp]),
+    "mqr_confidence": (ctypes.c_int, [ctypes.c_int, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _f32p,
+                                      _f32p, _f32p, _u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double,
+                                      ctypes.c_double, _vp, _vp, ctypes.c_int]),
+    "mqr_pixel_error_map": (ctypes.c_int, [ctypes.c_int, _f32p, _f32p, ctypes.c_int, ctypes.c_int, _f32p, _f32p,
+                                           _f32p, _f32p, _f32p, ctypes.c_double, _f32p]),
+    "mqr_vbg_profile": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "mqr_vbg_stats": (ctypes.c_int, [_vp, ctypes.POINTER(MqrStats), ctypes.c_int]),
+}
+
+_lib = None
+
+
+class MqrError(RuntimeError):
+    """Raised for any non-zero status from the HIP library (Open3D raises RuntimeError too)."""
+
+    def __init__(self, msg, code):
+        super().__init__(msg)
+        self.code = code
+
+
+def load(path: str = LIB_PATH):
+    """Load libmqr_hip.so (no compute happens here)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise ImportError(f"libmqr_hip.so not found at {path}; build it with "
+                          "`python -c 'import __graft_entry__ as g; g.build()'` (there is no CPU fallback)")
+    L = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def call(name, *args):
+    L = load()
+    rc = getattr(L, name)(*args)
+    if rc != 0:
+        msg = L.mqr_last_error().decode(errors="replace")
+        raise MqrError(f"{name} failed ({rc}): {msg}", rc)
+    return rc
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    try:
+        call("mqr_device_count", ctypes.byref(n))
+    except MqrError:
+        return 0
+    return n.value
+
+
+def ptr(a: np.ndarray, t=None):
+    if t is None:
+        return ctypes.c_void_p(a.ctypes.data)
+    return a.ctypes.data_as(t)
+
+
+class DeviceBuffer:
+    """Raw HBM allocation owned by Python (keeps inputs resident without any framework)."""
+
+    def __init__(self, nbytes: int, device: int = 0):
+        self.device = device
+        self.nbytes = int(nbytes)
+        p = ctypes.c_void_p()
+        call("mqr_device_alloc", device, max(self.nbytes, 4), ctypes.byref(p))
+        self.ptr = p
+
+    @classmethod
+    def from_array(cls, a: np.ndarray, device: int = 0):
+        a = np.ascontiguousarray(a)
+        buf = cls(a.nbytes, device)
+        call("mqr_memcpy", buf.ptr, MQR_DEVICE, ptr(a), MQR_HOST, a.nbytes, device)
+        return buf
+
+    def to_array(self, shape, dtype):
+        out = np.empty(shape, dtype)
+        call("mqr_memcpy", ptr(out), MQR_HOST, self.ptr, MQR_DEVICE, out.nbytes, self.device)
+        return out
+
+    def free(self):
+        if self.ptr is not None and self.ptr.value:
+            call("mqr_device_free", self.device, self.ptr)
+        self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass

@@ -1,0 +1,130 @@
+"""Drop-in for the reference's multi-view depth-confidence estimator on the MI355X.
+
+    estimate_depth_confidences(depth_data_io, config)   estimate_depth_confidences.py:120-153
+    build_confidence_map(...)                           estimate_depth_confidences.py:15-79
+    compute_pixel_error_map(...)                        compute_pixel_error_map.py:120-220
+
+The reference runs one numpy task per reference frame on a process pool and re-reads every
+neighbour frame from disk (~21x per frame).  Here each side's frames are decoded once, kept in
+HBM, and one kernel launch computes a chunk of reference frames (thread per pixel, neighbour
+loop in registers, float64 like numpy).  Outputs, file names and resume rules are the
+reference's: ``<side>_depth_confidence/<timestamp>.npz`` with confidence_map f64 / valid_count i32,
+existing per-frame files are kept, a side whose directory exists is skipped when
+``skip_if_output_dir_exists``.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+
+from . import _lib
+from ._lib import MQR_HOST, call, ptr
+from .models import ConfidenceMap, CoordinateSystem, Side
+from .o3d_utils import compute_o3d_intrinsic_matrices
+
+REF_CHUNK = 64
+
+
+@dataclass
+class DepthConfidenceEstimationConfig:
+    """reconstruction_config.py:33-39 (defaults), config/pipeline_config.yml:30-35 (pipeline values)."""
+    target_frame_range: int = 10
+    depth_max: float = 3.0
+    error_threshold: float = 0.05
+    skip_if_output_dir_exists: bool = True
+    use_dataset_cache: bool = True
+    use_multi_threading: bool = True
+    device: int = 0
+
+
+def confidence_maps(depths, intrinsics, T_cw, T_cw_inv, ref_begin=0, ref_end=None, target_frame_range=10,
+                    depth_max=3.0, error_threshold=0.05, frame_ok=None, device=0):
+    """(conf (n,H,W) f64, valid (n,H,W) i32) for reference frames [ref_begin, ref_end)."""
+    d = np.ascontiguousarray(depths, dtype=np.float32)
+    N, H, W = d.shape
+    ref_end = N if ref_end is None else ref_end
+    K = np.ascontiguousarray(intrinsics, dtype=np.float32).reshape(N, 9)
+    Tc = np.ascontiguousarray(T_cw, dtype=np.float32).reshape(N, 16)
+    Ti = np.ascontiguousarray(T_cw_inv, dtype=np.float32).reshape(N, 16)
+    ok = None if frame_ok is None else np.ascontiguousarray(frame_ok, dtype=np.uint8)
+    nref = ref_end - ref_begin
+    conf = np.empty((nref, H, W), np.float64)
+    valid = np.empty((nref, H, W), np.int32)
+    call("mqr_confidence", int(device), ptr(d), MQR_HOST, N, H, W, ptr(K, _lib._f32p), ptr(Tc, _lib._f32p),
+         ptr(Ti, _lib._f32p), None if ok is None else ptr(ok, _lib._u8p), int(ref_begin), int(ref_end),
+         int(target_frame_range), float(depth_max), float(error_threshold), ptr(conf), ptr(valid), MQR_HOST)
+    return conf, valid
+
+
+def compute_pixel_error_map(intrinsic_matrices, extrinsic_matrices, extrinsic_matrices_inv, ref_frame_idx,
+                            ref_depth_map, target_frame_idx, target_depth_map, depth_max=3.0, device=0):
+    ref = np.ascontiguousarray(ref_depth_map, dtype=np.float32)
+    tgt = np.ascontiguousarray(target_depth_map, dtype=np.float32)
+    H, W = ref.shape
+    K = np.ascontiguousarray(intrinsic_matrices, dtype=np.float32)
+    Tc = np.ascontiguousarray(extrinsic_matrices, dtype=np.float32)
+    Ti = np.ascontiguousarray(extrinsic_matrices_inv, dtype=np.float32)
+    out = np.empty((H, W), np.float32)
+    f = _lib._f32p
+    call("mqr_pixel_error_map", int(device), ptr(ref, f), ptr(tgt, f), H, W, ptr(K[ref_frame_idx], f),
+         ptr(K[target_frame_idx], f), ptr(Tc[ref_frame_idx], f), ptr(Ti[target_frame_idx], f),
+         ptr(Tc[target_frame_idx], f), float(depth_max), ptr(out, f))
+    return out
+
+
+def build_confidence_map(depth_data_io, dataset, intrinsic_matrices, extrinsic_matrices, extrinsic_matrices_inv,
+                         side, ref_frame_idx, target_frame_range=10, depth_max=3.0,
+                         error_threshold=0.05) -> Optional[ConfidenceMap]:
+    ref = depth_data_io.load_depth_map_by_index(side=side, dataset=dataset, index=ref_frame_idx)
+    if ref is None:
+        return None
+    lo = max(0, ref_frame_idx - target_frame_range)
+    hi = min(len(dataset), ref_frame_idx + target_frame_range + 1)
+    frames, ok = [], []
+    for i in range(lo, hi):
+        d = ref if i == ref_frame_idx else depth_data_io.load_depth_map_by_index(side=side, dataset=dataset, index=i)
+        ok.append(d is not None and d.shape == ref.shape)
+        frames.append(d if ok[-1] else np.zeros_like(ref))
+    conf, valid = confidence_maps(np.stack(frames), np.asarray(intrinsic_matrices)[lo:hi],
+                                  np.asarray(extrinsic_matrices)[lo:hi], np.asarray(extrinsic_matrices_inv)[lo:hi],
+                                  ref_frame_idx - lo, ref_frame_idx - lo + 1, target_frame_range, depth_max,
+                                  error_threshold, np.array(ok))
+    return ConfidenceMap(confidence_map=conf[0], valid_count=valid[0])
+
+
+def estimate_depth_confidences(depth_data_io, config: DepthConfidenceEstimationConfig, sides=None):
+    for side in (sides or list(Side)):
+        if config.skip_if_output_dir_exists and depth_data_io.exists_depth_confidence_map_dir(side=side):
+            print(f"[{side.name}] Skipping confidence map estimation: output directory already exists. "
+                  "Set skip_if_output_dir_exists = False to force re-estimation.")
+            continue
+        dataset = depth_data_io.load_depth_dataset(side=side)
+        n = len(dataset)
+        if n == 0:
+            continue
+        K = compute_o3d_intrinsic_matrices(dataset)
+        T_cw = dataset.transforms.convert_coordinate_system(target_coordinate_system=CoordinateSystem.OPEN3D,
+                                                            is_camera=True).extrinsics_cw
+        T_inv = np.linalg.inv(T_cw)
+        frames = [depth_data_io.load_depth_map_by_index(side=side, dataset=dataset, index=i) for i in range(n)]
+        shape = next((f.shape for f in frames if f is not None), None)
+        if shape is None:
+            continue
+        ok = np.array([f is not None and f.shape == shape for f in frames])
+        depths = np.stack([f if o else np.zeros(shape, np.float32) for f, o in zip(frames, ok)])
+        todo = [i for i in range(n) if ok[i]
+                and depth_data_io.load_confidence_map(side=side, timestamp=dataset.timestamps[i]) is None]
+        r = int(config.target_frame_range)
+        for c0 in range(0, len(todo), REF_CHUNK):
+            chunk = todo[c0:c0 + REF_CHUNK]
+            a, b = chunk[0], chunk[-1] + 1
+            lo, hi = max(0, a - r), min(n, b + r)
+            conf, valid = confidence_maps(depths[lo:hi], K[lo:hi], T_cw[lo:hi], T_inv[lo:hi], a - lo, b - lo, r,
+                                          config.depth_max, config.error_threshold, ok[lo:hi],
+                                          device=getattr(config, "device", 0))
+            for i in chunk:
+                depth_data_io.save_confidence_map(side=side, timestamp=dataset.timestamps[i],
+                                                  confidence_map=ConfidenceMap(conf[i - a], valid[i - a]))

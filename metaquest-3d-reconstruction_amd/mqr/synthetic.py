@@ -114,6 +114,89 @@ def render_depth(scene, K, R, t, height, width):
     return z.reshape(height, width).astype(np.float32)
 
 
+def render_depth_torch(scene, K, poses, height, width, device="cuda"):
+    """Batched torch version of render_depth (float64 on the GPU; synthetic-input generation only).
+
+    Returns (N,H,W) float32 torch tensor on `device`."""
+    import torch
+    fx, fy, cx, cy = (float(K[0, 0]), float(K[1, 1]), float(K[0, 2]), float(K[1, 2]))
+    v, u = torch.meshgrid(torch.arange(height, device=device, dtype=torch.float64),
+                          torch.arange(width, device=device, dtype=torch.float64), indexing="ij")
+    dc = torch.stack([(u - cx) / fx, (v - cy) / fy, torch.ones_like(u)], dim=-1).reshape(-1, 3)
+    out = torch.empty((len(poses), height, width), dtype=torch.float32, device=device)
+    inf = torch.tensor(float("inf"), dtype=torch.float64, device=device)
+    for i, (R, t) in enumerate(poses):
+        d = dc @ torch.as_tensor(np.asarray(R).T, dtype=torch.float64, device=device)
+        o = torch.as_tensor(np.asarray(t), dtype=torch.float64, device=device)
+        best = torch.full((d.shape[0],), float("inf"), dtype=torch.float64, device=device)
+        a = (d * d).sum(1)
+        for c, r in scene["spheres"]:
+            oc = o - torch.as_tensor(c, dtype=torch.float64, device=device)
+            b = 2 * d @ oc
+            cc = oc @ oc - r * r
+            disc = b * b - 4 * a * cc
+            ok = disc >= 0
+            sq = torch.sqrt(torch.clamp(disc, min=0))
+            s0 = (-b - sq) / (2 * a)
+            s1 = (-b + sq) / (2 * a)
+            s = torch.where(s0 > 1e-6, s0, torch.where(s1 > 1e-6, s1, inf))
+            best = torch.minimum(best, torch.where(ok, s, inf))
+        inv = 1.0 / d
+        for lo, hi in scene["boxes"]:
+            t0 = (torch.as_tensor(lo, dtype=torch.float64, device=device) - o) * inv
+            t1 = (torch.as_tensor(hi, dtype=torch.float64, device=device) - o) * inv
+            tn = torch.nan_to_num(torch.minimum(t0, t1), nan=-float("inf")).amax(1)
+            tf = torch.nan_to_num(torch.maximum(t0, t1), nan=float("inf")).amin(1)
+            hit = (tf >= tn) & (tn > 1e-6)
+            best = torch.minimum(best, torch.where(hit, tn, inf))
+        if scene["room"] is not None:
+            lo, hi = scene["room"]
+            t0 = (torch.as_tensor(lo, dtype=torch.float64, device=device) - o) * inv
+            t1 = (torch.as_tensor(hi, dtype=torch.float64, device=device) - o) * inv
+            tf = torch.nan_to_num(torch.maximum(t0, t1), nan=float("inf")).amin(1)
+            best = torch.minimum(best, torch.where(tf > 1e-6, tf, inf))
+        out[i] = torch.where(torch.isfinite(best), best, torch.zeros_like(best)).reshape(height, width).float()
+    return out
+
+
+def make_sequence_fast(scene="room", poses=None, n=500, height=480, width=640, f=525.0, noise=True, seed=0,
+                       near=NEAR, far=FAR, device="cuda"):
+    """make_sequence for benchmark-sized inputs: GPU (torch) ray casting, same decode/pose path.
+
+    Noise comes from a torch generator (so it differs from make_sequence's numpy stream)."""
+    import torch
+    cx_o3d, cy = (width - 1) / 2.0, (height - 1) / 2.0
+    l, r, t, b = fov_tangents(f, cx_o3d, f, cy, width, height)
+    fx, fy = width / (r + l), height / (t + b)
+    cx_desc, cy_desc = width * r / (r + l), height * t / (t + b)
+    K64 = np.array([[fx, 0, width - cx_desc], [0, fy, cy_desc], [0, 0, 1]])
+    if poses is None:
+        poses = sphere_ring_poses(n) if scene == "sphere" else room_loop_poses(n)
+    z = render_depth_torch(SCENES[scene], K64, poses, height, width, device).double()
+    if noise:
+        g = torch.Generator(device=device).manual_seed(seed)
+        noisy = z + torch.randn(z.shape, generator=g, device=device, dtype=torch.float64) * 0.002 * z
+        drop = torch.rand(z.shape, generator=g, device=device) < 0.01
+        z = torch.where((z > 0) & ~drop & (noisy > 0), noisy, torch.zeros_like(z))
+    # encode to the Quest NDC buffer and decode exactly like the reference loader
+    x, y = (-2.0 * near, -1.0) if np.isinf(far) or far < near else (-2.0 * far * near / (far - near),
+                                                                        -(far + near) / (far - near))
+    ndc = torch.where(z > 0, x / torch.where(z > 0, z, torch.ones_like(z)) - y, torch.ones_like(z))
+    raw = torch.clamp((ndc + 1.0) * 0.5, 0.0, 1.0).float()
+    ndc32 = raw * 2.0 - 1.0
+    denom = ndc32 + np.float32(y)
+    depth = torch.where(denom != 0, np.float32(x) / torch.where(denom != 0, denom, torch.ones_like(denom)),
+                        torch.zeros_like(denom)).float()
+    unity = o3d_poses_to_unity(poses)
+    o3d = unity.convert_coordinate_system(CoordinateSystem.OPEN3D, is_camera=True)
+    K = np.zeros((len(poses), 3, 3), np.float32)
+    K[:, 0, 0], K[:, 1, 1], K[:, 2, 2] = fx, fy, 1.0
+    K[:, 0, 2], K[:, 1, 2] = cx_desc, cy_desc
+    K[:, 0, 2] = width - K[:, 0, 2]
+    return {"depth_t": depth, "K": K, "T_wc": o3d.extrinsics_wc, "T_cw": o3d.extrinsics_cw, "unity": unity,
+            "width": width, "height": height}
+
+
 def corrupt(z, rng, sigma_rel=0.002, dropout=0.01):
     z = z.astype(np.float64)
     noisy = z + rng.standard_normal(z.shape) * sigma_rel * z

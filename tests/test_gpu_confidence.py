@@ -1,0 +1,55 @@
+"""GPU parity of the confidence estimator against golden vectors produced by the reference itself."""
+import numpy as np
+import pytest
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def golden(golden_dir):
+    import os
+    from mqr import _lib
+    _lib.load()
+    return np.load(os.path.join(golden_dir, "confidence_golden.npz"))
+
+
+@pytest.mark.parametrize("name", ["sphere", "room"])
+@pytest.mark.parametrize("tag,params", [("a", (3, 3.0, 0.05)), ("b", (10, 4.0, 0.08))])
+def test_confidence_matches_reference_golden(golden, name, tag, params):
+    from mqr.confidence import confidence_maps
+    r, dmax, thr = params
+    d = golden[f"{name}_depth"]
+    conf, valid = confidence_maps(d, golden[f"{name}_K"], golden[f"{name}_T_cw"], golden[f"{name}_T_cw_inv"], 0,
+                                  d.shape[0], r, dmax, thr)
+    assert np.array_equal(valid, golden[f"{name}_valid_{tag}"])
+    assert np.array_equal(conf, golden[f"{name}_conf_{tag}"])
+
+
+@pytest.mark.parametrize("name", ["sphere", "room"])
+def test_pixel_error_map_matches_reference_golden(golden, name):
+    from mqr.confidence import compute_pixel_error_map
+    d = golden[f"{name}_depth"]
+    for (a, b), e in zip(golden[f"{name}_pairs"], golden[f"{name}_err"]):
+        g = compute_pixel_error_map(golden[f"{name}_K"], golden[f"{name}_T_cw"], golden[f"{name}_T_cw_inv"], a, d[a],
+                                    b, d[b], depth_max=3.0)
+        assert np.array_equal(np.isnan(g), np.isnan(e))
+        m = ~np.isnan(e)
+        assert np.array_equal(g[m], e[m])
+
+
+def test_confidence_full_resolution_vs_oracle():
+    """640x480 room frames, skipped neighbour frames, window clipping at both ends."""
+    from mqr import synthetic
+    from mqr.confidence import confidence_maps
+    seq = synthetic.make_sequence("room", n=14, height=480, width=640, noise=True, seed=5)
+    Ti = np.linalg.inv(seq["T_cw"])
+    ok = np.ones(14, np.uint8)
+    ok[4] = 0
+    conf, valid = confidence_maps(seq["depth"], seq["K"], seq["T_cw"], Ti, 0, 14, 10, 4.0, 0.08, frame_ok=ok)
+    for i in (0, 5, 13):
+        oc, ov = oracle.confidence(seq["depth"], seq["K"], seq["T_cw"], Ti, i, 10, 4.0, 0.08, frame_valid=ok)
+        assert np.array_equal(valid[i], ov)
+        assert np.array_equal(conf[i], oc)
+    assert valid.max() > 0
