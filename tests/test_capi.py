@@ -1,0 +1,48 @@
+"""The C ABI library loads and exports every entry point include/mqr.h declares (no GPU needed)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared():
+    src = open(os.path.join(ROOT, "include", "mqr.h")).read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+char\s*\*|int)\s+(mqr_\w+)\s*\(", src, flags=re.M)))
+
+
+def test_header_declares_the_boundary():
+    names = _declared()
+    for must in ("mqr_vbg_create", "mqr_touch", "mqr_integrate", "mqr_integrate_frames", "mqr_extract_mesh",
+                 "mqr_extract_points", "mqr_confidence", "mqr_vbg_export", "mqr_vbg_import", "mqr_last_error",
+                 "mqr_vbg_pack_weighted", "mqr_vbg_unpack_weighted"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol():
+    from mqr import _lib
+    path = _lib.LIB_PATH
+    if not os.path.exists(path):
+        pytest.fail(f"{path} missing: run __graft_entry__.build()")
+    L = ctypes.CDLL(path)
+    missing = [n for n in _declared() if not hasattr(L, n)]
+    assert not missing, missing
+    assert set(_declared()) == set(_lib.SIGNATURES), "ctypes binding out of sync with mqr.h"
+
+
+def test_version_and_error_plumbing_without_gpu():
+    from mqr import _lib
+    L = _lib.load()
+    assert L.mqr_version() >= 100
+    assert isinstance(L.mqr_last_error(), bytes)
+
+
+def test_product_never_imports_the_oracle():
+    pkg = os.path.join(ROOT, "metaquest-3d-reconstruction_amd")
+    for dirpath, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith((".py", ".hip", ".hpp", ".cpp", ".h")):
+                txt = open(os.path.join(dirpath, f), errors="ignore").read()
+                assert "import oracle" not in txt and "liborc" not in txt and "mqr_oracle" not in txt, f

@@ -1,0 +1,103 @@
+"""Known-answer tests pinning the CPU oracle's TSDF semantics.
+
+Open3D is not installed and cannot be fetched, so the TSDF oracle is pinned here by hand-computed
+answers: a single voxel update, the touched-block set of one pixel, a fronto-parallel plane with
+an analytic TSDF, the sphere mesh against the analytic surface, and the no-block error.
+"""
+import numpy as np
+import pytest
+
+import oracle
+
+f32 = np.float32
+
+
+def _frame(d, H=16, W=16, f=100.0):
+    K = np.array([[f, 0, W / 2], [0, f, H / 2], [0, 0, 1]], np.float64)
+    return np.full((H, W), d, np.float32), K, np.eye(4)
+
+
+def test_single_voxel_running_average():
+    depth, K, T = _frame(1.0)
+    vs, R, tm = 0.1, 4, 2.0  # tau = 0.2
+    v = oracle.OracleVBG(vs, R, 16)
+    key = np.array([[0, 0, 2]], np.int32)  # voxels z = 8..11 -> 0.8 .. 1.1 m on the optical axis
+    v.integrate(key, depth, K, T, 1.0, 3.0, tm)
+    v.integrate(key, depth, K, T, 1.0, 3.0, tm)
+    keys, tsdf, w = v.export()
+    tau = f32(vs) * f32(tm)
+    for zl, zv in enumerate(range(8, 12)):
+        zc = f32(zv) * f32(vs)
+        sdf = f32(1.0) - zc
+        exp = min(sdf, tau) / tau
+        # two identical frames: (0*0 + s)/1 = s, then (1*s + s) * (1/2)
+        exp2 = (f32(1) * f32(exp) + f32(exp)) * (f32(1) / f32(2))
+        assert w[0, zl, 0, 0] == 2.0
+        assert tsdf[0, zl, 0, 0] == exp2
+    # behind the surface: updated only while sdf >= -tau (float32 compare), never beyond
+    v2 = oracle.OracleVBG(vs, R, 16)
+    v2.integrate(np.array([[0, 0, 3]], np.int32), depth, K, T, 1.0, 3.0, tm)
+    _, t2, w2 = v2.export()
+    for zl, zv in enumerate(range(12, 16)):
+        sdf = f32(1.0) - f32(zv) * f32(vs)
+        assert w2[0, zl, 0, 0] == (0.0 if sdf < -tau else 1.0)
+    assert w2[0, 1:, 0, 0].sum() == 0.0  # 1.3 m and beyond: never
+
+
+def test_touch_single_pixel_known_keys():
+    H = W = 8
+    depth = np.zeros((H, W), np.float32)
+    depth[4, 4] = 1.0  # the stride-4 pixel (u=4, v=4)
+    K = np.array([[100.0, 0, 4.0], [0, 100.0, 4.0], [0, 0, 1]])
+    keys = oracle.touch(depth, K, np.eye(4), 0.05, 8, 1.0, 3.0, 4.0)  # block 0.4 m, tau 0.2
+    # ray through the principal point: samples at t = 0.8, 0.9333, 1.0667, 1.2 on the z axis
+    assert sorted(map(tuple, keys)) == [(0, 0, 2), (0, 0, 3)]
+
+
+def test_no_block_touched_raises():
+    depth = np.zeros((16, 16), np.float32)
+    with pytest.raises(RuntimeError, match="No block is touched"):
+        oracle.touch(depth, np.eye(3), np.eye(4), 0.01, 16, 1.0, 3.0, 8.0)
+
+
+def test_fronto_parallel_plane_analytic_tsdf():
+    H, W, f = 64, 64, 64.0
+    depth = np.full((H, W), 1.0, np.float32)
+    K = np.array([[f, 0, W / 2], [0, f, H / 2], [0, 0, 1]])
+    vs, R, tm = 0.02, 8, 5.0  # tau 0.1
+    v = oracle.OracleVBG(vs, R, 64)
+    v.integrate_frame(depth, K, np.eye(4), 1.0, 3.0, tm)
+    keys, tsdf, w = v.export()
+    tau = f32(vs) * f32(tm)
+    zz = (keys[:, 2, None, None, None] * R + np.arange(R)[None, :, None, None]) * f32(vs)
+    zz = np.broadcast_to(zz.astype(np.float32), tsdf.shape)
+    m = w > 0
+    assert m.sum() > 1000
+    expected = np.minimum(f32(1.0) - zz, tau) / tau
+    assert np.abs(tsdf[m] - expected[m]).max() == 0.0
+    # nothing updated beyond the truncation band behind the surface
+    assert (zz[m] <= f32(1.0) + tau + 1e-6).all()
+
+
+def test_sphere_mesh_lies_on_the_surface():
+    import sys, os
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "metaquest-3d-reconstruction_amd"))
+    from mqr import synthetic
+    seq = synthetic.make_sequence("sphere", n=16, height=120, width=160, f=131.25, noise=False, seed=0)
+    v = oracle.OracleVBG(0.01, 8, 256)
+    for i in range(16):
+        v.integrate_frame(seq["depth"][i], seq["K"][i].astype(np.float64), seq["T_wc"][i].astype(np.float64),
+                          1.0, 3.0, 4.0)
+    verts, nrm, tris = v.extract_mesh(0.0)
+    assert len(tris) > 1000
+    r = np.linalg.norm(verts, axis=1)
+    assert np.abs(r - 0.5).max() < 0.01          # within one voxel of the analytic sphere
+    # normals point outward (tsdf gradient: positive outside)
+    assert (np.einsum("ij,ij->i", nrm, verts / r[:, None]) > 0.5).mean() > 0.95
+    # every triangle edge shared by at most two triangles (manifold patches)
+    e = np.sort(np.concatenate([tris[:, [0, 1]], tris[:, [1, 2]], tris[:, [2, 0]]]), axis=1)
+    _, c = np.unique(e, axis=0, return_counts=True)
+    assert c.max() <= 2
+    pts, pn = v.extract_points(0.0)
+    assert np.abs(np.linalg.norm(pts, axis=1) - 0.5).max() < 0.01
