@@ -120,6 +120,14 @@ typedef struct mqr_stats {
     int64_t pixels;
 } mqr_stats;
 int mqr_vbg_profile(mqr_vbg* v, int enable);
+
+/* Test / tuning hooks.  mqr_vbg_set_variant: 0 = R-specialised integrate kernel (default),
+ * 1 = generic kernel (A/B).  mqr_check_division: exhaustive bit-pattern check of the division
+ * shortcut used on device (which=0: 1/b over float bit patterns [lo_bits, lo_bits+count);
+ * which=1: a/b for those patterns as a); returns the mismatch count and the first bad pattern. */
+int mqr_vbg_set_variant(mqr_vbg* v, int variant);
+int mqr_check_division(int device, int which, float b, uint32_t lo_bits, uint64_t count, uint32_t* mismatches,
+                       uint32_t* first_bad);
 int mqr_vbg_stats(mqr_vbg* v, mqr_stats* out, int reset);
 
 #ifdef __cplusplus

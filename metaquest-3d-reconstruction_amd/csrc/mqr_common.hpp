@@ -118,6 +118,7 @@ struct mqr_vbg {
     float* d_depth = nullptr;          // staging for host depth frames
     int64_t depth_cap = 0;             // floats
 
+    int kernel_variant = 0;            // 0 = R-specialised integrate, 1 = generic (A/B)
     // profiling
     bool profile = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> int_events, touch_events;

@@ -238,6 +238,161 @@ __global__ __launch_bounds__(256) void k_integrate(const int32_t* __restrict__ l
     }
 }
 
+// ---- correctly rounded division without the v_div_scale / v_div_fixup wrapper ----------------
+// The instruction sequence below is exactly what hipcc emits for IEEE float division
+// (v_rcp_f32, Newton step, two residual corrections, final FMA = v_div_fmas without scaling).
+// v_div_scale only rescales operands whose exponents put the quotient near over/underflow, and
+// v_div_fixup only rewrites 0/inf/NaN cases, so for |num|, |den| in [2^-60, 2^60] the result
+// equals a/b bit for bit; outside that range we call the real division.  Verified
+// exhaustively on the GPU by tests/test_gpu_numerics.py.
+__device__ __forceinline__ float div_rn_core(float a, float b) {
+    const float y0 = __builtin_amdgcn_rcpf(b);
+    const float nb = -b;
+    const float e0 = __builtin_fmaf(nb, y0, 1.0f);
+    const float y1 = __builtin_fmaf(e0, y0, y0);
+    const float q0 = a * y1;
+    const float r0 = __builtin_fmaf(nb, q0, a);
+    const float q1 = __builtin_fmaf(r0, y1, q0);
+    const float r1 = __builtin_fmaf(nb, q1, a);
+    return __builtin_fmaf(r1, y1, q1);
+}
+
+__device__ __forceinline__ bool div_safe(float v) {
+    const float m = fabsf(v);
+    return m >= 0x1p-60f && m <= 0x1p60f;
+}
+
+__device__ __forceinline__ float div_rn(float a, float b) {
+    return (div_safe(a) && div_safe(b)) ? div_rn_core(a, b) : a / b;
+}
+
+__device__ __forceinline__ float rcp_rn(float b) { return div_safe(b) ? div_rn_core(1.0f, b) : 1.0f / b; }
+
+// Integrate, R known at compile time (R = 16 / 8): thread t owns the voxel column (x, y) =
+// (t % R, t / R % R) for z in its z-range, keeps those voxels' (tsdf, weight) in registers for
+// all frames of the batch, and evaluates Open3D's transform ((xs*e0 + ys*e1) + zs*e2) + e3 with
+// the z-independent partial product hoisted per frame -- the same float operations in the same
+// order, so the result is bit-identical to k_integrate.
+template <int R, int G>
+__global__ __launch_bounds__(256) void k_integrate_t(const int32_t* __restrict__ list, const int* __restrict__ counters,
+                                                     int64_t list_cap, Table t, float2* __restrict__ pool,
+                                                     float voxel_size, const float* __restrict__ depths, int64_t HW,
+                                                     int H, int W, const FrameParams* __restrict__ fps,
+                                                     const int64_t* __restrict__ depth_frame, float depth_scale,
+                                                     float depth_max, float sdf_trunc) {
+    constexpr int R2 = R * R;
+    constexpr int R3 = R2 * R;
+    constexpr int ZPER = R3 / 256;         // voxels per thread (16 at R=16, 2 at R=8)
+    constexpr int ZSTEP = 256 / R2;        // z stride between a thread's voxels (1 at R=16, 4 at R=8)
+    static_assert(R3 % 256 == 0, "R^3 must be a multiple of 256");
+    static_assert(ZPER % G == 0, "group size must divide the voxels per thread");
+    const bool unit_scale = depth_scale == 1.0f;  // d / 1 == d exactly: skip the division
+    const int64_t n = min((int64_t)counters[kListCount], list_cap);
+    const float hm1 = (float)H - 1.0f, wm1 = (float)W - 1.0f;
+    const int tid = threadIdx.x;
+    const int xv = tid % R, yv = (tid / R) % R, z0 = tid / R2;
+    for (int64_t i = blockIdx.x; i < n; i += gridDim.x) {
+        const int32_t slot = list[i];
+        const int buf = t.vals[slot];
+        const uint32_t mask = __builtin_amdgcn_readfirstlane(t.mask[slot]);
+        int xb, yb, zb;
+        unpack_key(t.keys[slot], xb, yb, zb);
+        if (buf >= 0) {
+            float2* vox = pool + (int64_t)buf * R3;
+            float2 tw[ZPER];
+            float zs[ZPER];
+#pragma unroll
+            for (int k = 0; k < ZPER; ++k) {
+                tw[k] = vox[k * 256 + tid];
+                zs[k] = (float)(zb * R + z0 + k * ZSTEP) * voxel_size;
+            }
+            const float xs = (float)(xb * R + xv) * voxel_size;
+            const float ys = (float)(yb * R + yv) * voxel_size;
+            uint32_t dirty = 0;
+            uint32_t m = mask;
+            while (m) {
+                const int f = __builtin_ctz(m);
+                m &= m - 1;
+                const FrameParams& fp = fps[f];
+                const float* __restrict__ dep = depths + depth_frame[f] * HW;
+                const float ax = xs * fp.ext[0] + ys * fp.ext[1];
+                const float ay = xs * fp.ext[4] + ys * fp.ext[5];
+                const float az = xs * fp.ext[8] + ys * fp.ext[9];
+                // Groups of G voxels: project all, issue all G depth gathers (branch-free, out-of-image
+                // lanes read pixel 0 and are masked), then update -- G loads in flight per wave.
+#pragma unroll
+                for (int g = 0; g < ZPER; g += G) {
+                    int pix[G];
+                    float zcs[G];
+                    bool in[G];
+#pragma unroll
+                    for (int j = 0; j < G; ++j) {
+                        const int k = g + j;
+                        const float xc = (ax + zs[k] * fp.ext[2]) + fp.ext[3];
+                        const float yc = (ay + zs[k] * fp.ext[6]) + fp.ext[7];
+                        const float zc = (az + zs[k] * fp.ext[10]) + fp.ext[11];
+                        const float inv_z = rcp_rn(zc);
+                        const float u = fp.fx * xc * inv_z + fp.cx;
+                        const float v = fp.fy * yc * inv_z + fp.cy;
+                        in[j] = v >= 0 && u >= 0 && v <= hm1 && u <= wm1;
+                        const int ui = (int)(in[j] ? u : 0.f), vi = (int)(in[j] ? v : 0.f);
+                        pix[j] = vi * W + ui;
+                        zcs[j] = zc;
+                    }
+                    float dv[G];
+#pragma unroll
+                    for (int j = 0; j < G; ++j) dv[j] = dep[pix[j]];
+#pragma unroll
+                    for (int j = 0; j < G; ++j) {
+                        const int k = g + j;
+                        const float d = unit_scale ? dv[j] : div_rn(dv[j], depth_scale);
+                        const float zc = zcs[j];
+                        float sdf = d - zc;
+                        if (!in[j] || d <= 0 || d > depth_max || zc <= 0 || sdf < -sdf_trunc) continue;
+                        sdf = sdf < sdf_trunc ? sdf : sdf_trunc;
+                        sdf = div_rn(sdf, sdf_trunc);
+                        const float wgt = tw[k].y;
+                        const float inv_wsum = rcp_rn(wgt + 1);
+                        tw[k].x = (wgt * tw[k].x + sdf) * inv_wsum;
+                        tw[k].y = wgt + 1;
+                        dirty |= 1u << k;
+                    }
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < ZPER; ++k)
+                if (dirty & (1u << k)) vox[k * 256 + tid] = tw[k];
+        }
+        __syncthreads();
+        if (tid == 0) t.mask[slot] = 0;
+    }
+}
+
+// Exhaustive-check kernels for the division shortcut (tests/test_gpu_numerics.py).
+__global__ void k_check_rcp(uint32_t lo_bits, uint64_t count, uint32_t* mismatches, uint32_t* first_bad) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    const uint32_t bits = lo_bits + (uint32_t)i;
+    const float b = __uint_as_float(bits);
+    const float fast = rcp_rn(b), ref = 1.0f / b;
+    if (__float_as_uint(fast) != __float_as_uint(ref)) {
+        atomicAdd(mismatches, 1u);
+        atomicMin(first_bad, bits);
+    }
+}
+
+__global__ void k_check_div(float b, uint32_t lo_bits, uint64_t count, uint32_t* mismatches, uint32_t* first_bad) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    const uint32_t bits = lo_bits + (uint32_t)i;
+    const float a = __uint_as_float(bits);
+    const float fast = div_rn(a, b), ref = a / b;
+    if (__float_as_uint(fast) != __float_as_uint(ref) && !(isnan(fast) && isnan(ref))) {
+        atomicAdd(mismatches, 1u);
+        atomicMin(first_bad, bits);
+    }
+}
+
 __global__ void k_rehash(Table src, Table dst) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= src.cap) return;
@@ -505,9 +660,24 @@ static int launch_integrate(mqr_vbg* v, const float* depths, int64_t HW, int H, 
         MQR_CHECK_HIP(hipEventCreate(&e1));
         MQR_CHECK_HIP(hipEventRecord(e0, v->stream));
     }
-    hipLaunchKernelGGL(k_integrate, dim3(grid), dim3(256), 0, v->stream, v->list, v->counters, v->list_cap, v->tab,
-                       v->pool, v->R, v->voxel_size, depths, HW, H, W, v->d_fp, depth_frame, depth_scale, depth_max,
-                       sdf_trunc);
+#define MQR_LAUNCH_INT(RR, GG)                                                                                \
+    hipLaunchKernelGGL((k_integrate_t<RR, GG>), dim3(grid), dim3(256), 0, v->stream, v->list, v->counters,          \
+                       v->list_cap, v->tab, v->pool, v->voxel_size, depths, HW, H, W, v->d_fp, depth_frame,          \
+                       depth_scale, depth_max, sdf_trunc)
+    if (v->R == 16 && v->kernel_variant == 0)
+        MQR_LAUNCH_INT(16, 8);
+    else if (v->R == 16 && v->kernel_variant == 2)
+        MQR_LAUNCH_INT(16, 4);
+    else if (v->R == 16 && v->kernel_variant == 3)
+        MQR_LAUNCH_INT(16, 16);
+    else if (v->R == 16 && v->kernel_variant == 4)
+        MQR_LAUNCH_INT(16, 2);
+    else if (v->R == 8 && v->kernel_variant != 1)
+        MQR_LAUNCH_INT(8, 2);
+    else
+        hipLaunchKernelGGL(k_integrate, dim3(grid), dim3(256), 0, v->stream, v->list, v->counters, v->list_cap,
+                           v->tab, v->pool, v->R, v->voxel_size, depths, HW, H, W, v->d_fp, depth_frame, depth_scale,
+                           depth_max, sdf_trunc);
     MQR_CHECK_HIP(hipGetLastError());
     if (v->profile) {
         MQR_CHECK_HIP(hipEventRecord(e1, v->stream));
@@ -927,6 +1097,38 @@ int mqr_vbg_unpack_weighted(mqr_vbg* v, const int32_t* union_keys, int64_t U, co
                        (int)v->R3, reinterpret_cast<const float2*>(packed));
     MQR_CHECK_HIP(hipGetLastError());
     MQR_CHECK_HIP(hipStreamSynchronize(v->stream));
+    return 0;
+}
+
+int mqr_vbg_set_variant(mqr_vbg* v, int variant) {
+    MQR_REQUIRE(v, "null volume");
+    v->kernel_variant = variant;
+    return 0;
+}
+
+int mqr_check_division(int device, int which, float b, uint32_t lo_bits, uint64_t count, uint32_t* mismatches,
+                       uint32_t* first_bad) {
+    MQR_REQUIRE(mismatches && first_bad, "null argument");
+    MQR_CHECK_HIP(hipSetDevice(device));
+    uint32_t* d = nullptr;
+    MQR_CHECK_HIP(hipMalloc(&d, 2 * sizeof(uint32_t)));
+    const uint32_t init[2] = {0u, 0xffffffffu};
+    MQR_CHECK_HIP(hipMemcpy(d, init, sizeof(init), hipMemcpyHostToDevice));
+    const uint64_t chunk = 1ull << 30;
+    for (uint64_t off = 0; off < count; off += chunk) {
+        const uint64_t c = std::min<uint64_t>(chunk, count - off);
+        const unsigned blocks = (unsigned)((c + 255) / 256);
+        if (which == 0)
+            hipLaunchKernelGGL(k_check_rcp, dim3(blocks), dim3(256), 0, 0, lo_bits + (uint32_t)off, c, d, d + 1);
+        else
+            hipLaunchKernelGGL(k_check_div, dim3(blocks), dim3(256), 0, 0, b, lo_bits + (uint32_t)off, c, d, d + 1);
+        MQR_CHECK_HIP(hipGetLastError());
+    }
+    uint32_t out[2];
+    MQR_CHECK_HIP(hipMemcpy(out, d, sizeof(out), hipMemcpyDeviceToHost));
+    (void)hipFree(d);
+    *mismatches = out[0];
+    *first_bad = out[1];
     return 0;
 }
 

@@ -66,6 +66,9 @@ SIGNATURES = {
     "mqr_pixel_error_map": (ctypes.c_int, [ctypes.c_int, _f32p, _f32p, ctypes.c_int, ctypes.c_int, _f32p, _f32p,
                                            _f32p, _f32p, _f32p, ctypes.c_double, _f32p]),
     "mqr_vbg_profile": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "mqr_vbg_set_variant": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "mqr_check_division": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_uint32, ctypes.c_uint64,
+                                          ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]),
     "mqr_vbg_stats": (ctypes.c_int, [_vp, ctypes.POINTER(MqrStats), ctypes.c_int]),
 }
 

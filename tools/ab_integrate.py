@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""Interleaved A/B of integrate-kernel variants on the bench workload (one process, same data).
+
+python tools/ab_integrate.py --variants 0,2,3,4 --rounds 5
+Prints per-variant median integrate-kernel ms per launch, touch ms, and step ms.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "metaquest-3d-reconstruction_amd"))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--variants", default="0,1")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--frames", type=int, default=500)
+    ap.add_argument("--batch", type=int, default=0, help="frames per integrate_frames call (0 = all)")
+    a = ap.parse_args()
+    import numpy as np
+    import torch
+    from bench import _DevPtr
+    from mqr import _lib, synthetic
+    from mqr.vbg import VoxelBlockGrid
+    seq = synthetic.make_sequence_fast("room", poses=synthetic.room_loop_poses(a.frames), device="cuda:0")
+    d = seq["depth_t"].contiguous()
+    B, H, W = d.shape
+    K, T = seq["K"].astype(np.float64), seq["T_wc"].astype(np.float64)
+    torch.cuda.synchronize()
+    vbg = VoxelBlockGrid(voxel_size=0.005, block_resolution=16, block_count=40000, device=0)
+    variants = [int(x) for x in a.variants.split(",")]
+    res = {v: {"int": [], "touch": [], "step": []} for v in variants}
+    for r in range(a.rounds + 1):
+        for v in variants:
+            _lib.call("mqr_vbg_set_variant", vbg.handle, v)
+            vbg.reset()
+            vbg.stats(reset=True)
+            vbg.profile(True)
+            t0 = time.perf_counter()
+            vbg.integrate_frames((_DevPtr(d.data_ptr()), B, H, W), K, T, depth_scale=1.0, depth_max=4.0,
+                                 trunc_voxel_multiplier=10.0)
+            dt = time.perf_counter() - t0
+            vbg.profile(False)
+            st = vbg.stats(reset=True)
+            if r == 0:
+                continue  # warm-up round
+            res[v]["int"].append(st["integrate_ms"] / max(st["integrate_launches"], 1))
+            res[v]["touch"].append(st["touch_ms"] / max(st["touch_launches"], 1))
+            res[v]["step"].append(dt * 1e3)
+    out = {v: {k: float(np.median(x)) for k, x in r.items()} for v, r in res.items()}
+    print(json.dumps({"variants": out, "blocks": vbg.size()}))
+
+
+if __name__ == "__main__":
+    main()
