@@ -90,6 +90,10 @@ struct FrameParams {
 
 void make_frame_params(const double* K, const double* T_wc, FrameParams* fp);
 
+constexpr int kMaxBatch = 32;         // frames per device batch (one bit each in the slot mask)
+constexpr int kFrameCounterBase = 8;  // per-frame raw touch counts live at counters[8 + f]
+constexpr int kCountersTotal = kFrameCounterBase + kMaxBatch;
+
 // ---------------------------------------------------------------- volume
 }  // namespace mqr
 
@@ -98,36 +102,52 @@ struct mqr_vbg {
     float voxel_size = 0.f;
     int R = 16;
     int64_t R3 = 4096;
+    // Two streams: touch(b+1) on `stream` overlaps integrate(b) on `stream2`.  Per-batch state
+    // (slot masks, slot lists, counters, frame parameters, staged depth) is double-buffered by
+    // batch parity; the hash table, pool and pool counter are shared.
     hipStream_t stream = nullptr;
+    hipStream_t stream2 = nullptr;
+    hipEvent_t ev_touch[2] = {nullptr, nullptr};
+    hipEvent_t ev_int[2] = {nullptr, nullptr};
+    bool int_pending[2] = {false, false};
 
-    mqr::Table tab{};          // main block table
+    mqr::Table tab{};          // main block table (tab.mask == mask[0])
+    uint32_t* mask1 = nullptr; // parity-1 slot masks
     mqr::Table ftab{};         // frustum table for mqr_touch (Open3D's separate frustum hash map)
     float2* pool = nullptr;    // [pool_cap][R3] (tsdf, weight)
     uint64_t* bkeys = nullptr; // [pool_cap] packed key of each buffer
     int64_t pool_cap = 0;
     int64_t pool_count = 0;    // host mirror (valid after each batch)
 
-    int32_t* list = nullptr;   // batch slot list, capacity list_cap
+    int32_t* lists[2] = {nullptr, nullptr};  // batch slot lists, capacity list_cap each
     int64_t list_cap = 0;
-    int* counters = nullptr;   // device counters
-    int* h_counters = nullptr; // pinned mirror
+    int* counters = nullptr;   // device: 2 x kCountersTotal per-parity sets, then the pool counter
+    int* h_counters = nullptr; // pinned mirror, same layout
 
-    mqr::FrameParams* d_fp = nullptr;  // per-batch frame parameters (+ int64 depth-frame index array)
-    mqr::FrameParams* h_fp = nullptr;  // pinned host mirror of d_fp
+    mqr::FrameParams* d_fp[2] = {nullptr, nullptr};  // frame params (+ int64 depth-frame index array)
+    mqr::FrameParams* h_fp[2] = {nullptr, nullptr};  // pinned mirrors
     int fp_cap = 0;
-    float* d_depth = nullptr;          // staging for host depth frames
-    int64_t depth_cap = 0;             // floats
+    float* d_depth[2] = {nullptr, nullptr};          // staging for host depth frames
+    int64_t depth_cap = 0;                           // floats per parity
 
-    int kernel_variant = 0;            // 0 = R-specialised integrate, 1 = generic (A/B)
+    int kernel_variant = 0;    // 0 = R-specialised integrate, 1 = generic, 2 = G=4 (A/B)
+    bool pipelined = true;     // overlap touch(b+1) with integrate(b)
     // profiling
     bool profile = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> int_events, touch_events;
     mqr_stats stats{};
+
+    mqr::Table table(int parity) const {
+        mqr::Table t = tab;
+        t.mask = parity ? mask1 : tab.mask;
+        return t;
+    }
+    int* ctr(int parity) const { return counters + parity * mqr::kCountersTotal; }
+    int* hctr(int parity) const { return h_counters + parity * mqr::kCountersTotal; }
+    int* pool_ctr() const { return counters + 2 * mqr::kCountersTotal; }
 };
 
 namespace mqr {
-int ensure_fp(mqr_vbg* v, int n);
-int ensure_depth(mqr_vbg* v, int64_t floats);
 int grow_pool(mqr_vbg* v, int64_t need);
-int sync_counters(mqr_vbg* v);
+int sync_all(mqr_vbg* v);
 }  // namespace mqr

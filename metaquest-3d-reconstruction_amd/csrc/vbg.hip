@@ -1,32 +1,30 @@
-// vbg.hip -- the HBM-resident voxel-block TSDF volume: block hash, touch, integrate,
-// export/import and the multi-GPU pack/unpack.  Replaces Open3D 0.19's VoxelBlockGrid
-// (reference call sites: scripts/processing/reconstruction/utils/o3d_utils.py:170-229).
+// vbg.hip -- host side of the HBM-resident voxel-block TSDF volume: block hash, touch,
+// integrate, export/import and the multi-GPU pack/unpack.  Replaces Open3D 0.19's
+// VoxelBlockGrid (reference call sites: scripts/processing/reconstruction/utils/o3d_utils.py:170-229).
 //
 // Data layout in HBM (one volume):
 //   pool   [pool_cap][R^3] float2 (tsdf, weight), voxel [z][y][x] inside a block -> 32 KiB/block at R=16
 //   bkeys  [pool_cap] packed block key of each buffer (for extraction / export)
-//   table  keys u64 / vals i32 / mask u32, open addressing, capacity >= 2x live keys
-//   list   slots touched by the current batch (appended once per batch, on first touch)
+//   table  keys u64 / vals i32 / mask u32 x2 (batch parity), open addressing, capacity >= 2x live keys
+//   lists  slots touched by the current batch (appended once per batch, on first touch), x2
 //
 // Per batch of <= 32 frames: k_touch (one thread per stride-4 pixel per frame, 4 ray samples,
-// hash insert, per-slot frame bitmask) -> host reads 8 counters (pool growth) -> k_integrate
-// (one workgroup per touched block, every voxel applies that block's frames in frame order =
-// bit-identical to sequential per-frame integration).
+// hash insert, per-slot frame bitmask) -> host reads the batch counters (pool growth, empty-frame
+// error) -> k_integrate (one workgroup per touched block, every voxel applies that block's frames
+// in frame order = bit-identical to sequential per-frame integration).
+// touch(b+1) runs on a second stream while integrate(b) runs (double-buffered batch state).
 #include <algorithm>
 #include <cmath>
 #include <cstring>
 
 #include "mqr_common.hpp"
+#include "vbg_kernels.hpp"
 
 namespace mqr {
 
 static thread_local std::string g_err;
 void set_error(const std::string& msg) { g_err = msg; }
 const char* get_error() { return g_err.c_str(); }
-
-constexpr int kMaxBatch = 32;
-constexpr int kFrameCounterBase = 8;  // per-frame raw touch counts live at counters[8 + f]
-constexpr int kCountersTotal = kFrameCounterBase + kMaxBatch;
 
 void make_frame_params(const double* K, const double* T, FrameParams* fp) {
     fp->fx = (float)K[0];
@@ -42,468 +40,6 @@ void make_frame_params(const double* K, const double* T, FrameParams* fp) {
     for (int i = 0; i < 3; ++i)
         P[i * 4 + 3] = -(P[i * 4 + 0] * T[0 * 4 + 3] + P[i * 4 + 1] * T[1 * 4 + 3] + P[i * 4 + 2] * T[2 * 4 + 3]);
     for (int k = 0; k < 12; ++k) fp->pose[k] = (float)P[k];
-}
-
-// ------------------------------------------------------------------ device helpers
-__device__ inline int64_t table_find(const Table t, uint64_t k) {
-    const uint64_t m = (uint64_t)t.cap - 1;
-    uint64_t h = mix64(k) & m;
-    for (int64_t p = 0; p < t.cap; ++p) {
-        const uint64_t cur = t.keys[h];
-        if (cur == k) return (int64_t)h;
-        if (cur == kEmpty) return -1;
-        h = (h + 1) & m;
-    }
-    return -1;
-}
-
-// Insert-or-find.  A CAS winner allocates a pool buffer when `alloc`.
-__device__ inline int64_t table_insert(Table t, uint64_t k, bool alloc, int* counters, int64_t pool_cap,
-                                       uint64_t* bkeys) {
-    const uint64_t m = (uint64_t)t.cap - 1;
-    uint64_t h = mix64(k) & m;
-    for (int64_t p = 0; p < t.cap; ++p) {
-        const uint64_t cur = t.keys[h];
-        if (cur == k) return (int64_t)h;
-        if (cur == kEmpty) {
-            const uint64_t old = atomicCAS((unsigned long long*)&t.keys[h], (unsigned long long)kEmpty,
-                                           (unsigned long long)k);
-            if (old == kEmpty) {
-                if (alloc) {
-                    const int b = atomicAdd(&counters[kPoolCount], 1);
-                    if (b < pool_cap) {
-                        t.vals[h] = b;
-                        bkeys[b] = k;
-                    } else {
-                        t.vals[h] = -2;
-                        atomicOr(&counters[kOverflow], 1);
-                    }
-                }
-                return (int64_t)h;
-            }
-            if (old == k) return (int64_t)h;
-        }
-        h = (h + 1) & m;
-    }
-    atomicOr(&counters[kOverflow], 2);
-    return -1;
-}
-
-__device__ inline void mark_slot(Table t, int64_t slot, int f, int* counters, int32_t* list, int64_t list_cap) {
-    const uint32_t bit = 1u << f;
-    const uint32_t old = atomicOr(&t.mask[slot], bit);
-    if (!(old & bit)) atomicAdd(&counters[kFrameBlocks], 1);
-    if (old == 0) {
-        const int pos = atomicAdd(&counters[kListCount], 1);
-        if (pos < list_cap)
-            list[pos] = (int32_t)slot;
-        else
-            atomicOr(&counters[kOverflow], 4);
-    }
-}
-
-__device__ inline uint64_t shfl_up_u64(uint64_t v, int d) {
-    const int lo = __shfl_up((int)(uint32_t)v, d, 64);
-    const int hi = __shfl_up((int)(uint32_t)(v >> 32), d, 64);
-    return ((uint64_t)(uint32_t)hi << 32) | (uint64_t)(uint32_t)lo;
-}
-
-// ------------------------------------------------------------------ kernels
-// compute_unique_block_coordinates for a batch: blockIdx.y = batch frame (bit), one thread per
-// stride-4 pixel, 4 samples over [max(d - trunc, 0), min(d + trunc, depth_max)] (Appendix A.2).
-__global__ __launch_bounds__(256) void k_touch(const float* __restrict__ depths, int64_t HW, int H, int W,
-                                               const FrameParams* __restrict__ fps,
-                                               const int64_t* __restrict__ depth_frame, float depth_scale,
-                                               float depth_max, float sdf_trunc, float block_size, Table t,
-                                               int alloc, int* counters, int64_t pool_cap, uint64_t* bkeys,
-                                               int32_t* list, int64_t list_cap) {
-    const int f = blockIdx.y;
-    const FrameParams& fp = fps[f];
-    const int cols = W / 4, rows = H / 4, n = rows * cols;
-    const int w = blockIdx.x * blockDim.x + threadIdx.x;
-    const int lane = threadIdx.x & 63;
-    uint64_t key[4] = {kEmpty, kEmpty, kEmpty, kEmpty};
-    if (w < n) {
-        const int y = (w / cols) * 4, x = (w % cols) * 4;
-        const float d = depths[depth_frame[f] * HW + (int64_t)y * W + x] / depth_scale;
-        if (d > 0 && d < depth_max) {
-            const float xc = ((float)x - fp.cx) * 1.0f / fp.fx;
-            const float yc = ((float)y - fp.cy) * 1.0f / fp.fy;
-            const float zc = 1.0f;
-            const float xg = xc * fp.pose[0] + yc * fp.pose[1] + zc * fp.pose[2] + fp.pose[3];
-            const float yg = xc * fp.pose[4] + yc * fp.pose[5] + zc * fp.pose[6] + fp.pose[7];
-            const float zg = xc * fp.pose[8] + yc * fp.pose[9] + zc * fp.pose[10] + fp.pose[11];
-            const float xo = fp.pose[3], yo = fp.pose[7], zo = fp.pose[11];
-            const float xd = xg - xo, yd = yg - yo, zd = zg - zo;
-            const float t_min = fmaxf(d - sdf_trunc, 0.0f);
-            const float t_max = fminf(d + sdf_trunc, depth_max);
-            const float t_step = (t_max - t_min) / 3;
-            float tt = t_min;
-#pragma unroll
-            for (int s = 0; s < 4; ++s) {
-                const int xb = (int)floorf((xo + tt * xd) / block_size);
-                const int yb = (int)floorf((yo + tt * yd) / block_size);
-                const int zb = (int)floorf((zo + tt * zd) / block_size);
-                if (key_in_range(xb, yb, zb))
-                    key[s] = pack_key(xb, yb, zb);
-                else
-                    atomicOr(&counters[kOverflow], 8);
-                tt += t_step;
-            }
-            atomicAdd(&counters[kFrameCounterBase + f], 4);
-        }
-    }
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-        const uint64_t k = key[s];
-        const uint64_t up = shfl_up_u64(k, 1);
-        bool dup = (lane > 0 && up == k);
-        if (s > 0 && key[s - 1] == k) dup = true;
-        if (k != kEmpty && !dup) {
-            const int64_t slot = table_insert(t, k, alloc != 0, counters, pool_cap, bkeys);
-            if (slot >= 0) mark_slot(t, slot, f, counters, list, list_cap);
-        }
-    }
-}
-
-// Activate explicit keys (vbg.integrate(block_coords, ...)); marks frame bit 0.
-__global__ void k_activate(const int32_t* __restrict__ keys, int64_t n, Table t, int* counters, int64_t pool_cap,
-                           uint64_t* bkeys, int32_t* list, int64_t list_cap, int mark) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const int x = keys[3 * i], y = keys[3 * i + 1], z = keys[3 * i + 2];
-    if (!key_in_range(x, y, z)) {
-        atomicOr(&counters[kOverflow], 8);
-        return;
-    }
-    const int64_t slot = table_insert(t, pack_key(x, y, z), true, counters, pool_cap, bkeys);
-    if (slot >= 0 && mark) mark_slot(t, slot, 0, counters, list, list_cap);
-}
-
-// Projective TSDF update of every voxel of every listed block, frames applied in bit order.
-// Arithmetic = Open3D 0.19 Integrate kernel (Appendix A.3), float32, no contraction.
-__global__ __launch_bounds__(256) void k_integrate(const int32_t* __restrict__ list, const int* __restrict__ counters,
-                                                   int64_t list_cap, Table t, float2* __restrict__ pool, int R,
-                                                   float voxel_size, const float* __restrict__ depths, int64_t HW,
-                                                   int H, int W, const FrameParams* __restrict__ fps,
-                                                   const int64_t* __restrict__ depth_frame, float depth_scale,
-                                                   float depth_max, float sdf_trunc) {
-    const int64_t n = min((int64_t)counters[kListCount], list_cap);
-    const int R3 = R * R * R;
-    const float hm1 = (float)H - 1.0f, wm1 = (float)W - 1.0f;
-    for (int64_t i = blockIdx.x; i < n; i += gridDim.x) {
-        const int32_t slot = list[i];
-        const int buf = t.vals[slot];
-        const uint32_t mask = t.mask[slot];
-        int xb, yb, zb;
-        unpack_key(t.keys[slot], xb, yb, zb);
-        if (buf >= 0) {
-            float2* vox = pool + (int64_t)buf * R3;
-            for (int p = threadIdx.x; p < R3; p += blockDim.x) {
-                const int xv = p % R, yv = (p / R) % R, zv = p / (R * R);
-                const float xs = (float)(xb * R + xv) * voxel_size;
-                const float ys = (float)(yb * R + yv) * voxel_size;
-                const float zs = (float)(zb * R + zv) * voxel_size;
-                float2 tw = vox[p];
-                bool dirty = false;
-                uint32_t m = mask;
-                while (m) {
-                    const int f = __builtin_ctz(m);
-                    m &= m - 1;
-                    const FrameParams& fp = fps[f];
-                    const float xc = xs * fp.ext[0] + ys * fp.ext[1] + zs * fp.ext[2] + fp.ext[3];
-                    const float yc = xs * fp.ext[4] + ys * fp.ext[5] + zs * fp.ext[6] + fp.ext[7];
-                    const float zc = xs * fp.ext[8] + ys * fp.ext[9] + zs * fp.ext[10] + fp.ext[11];
-                    const float inv_z = 1.0f / zc;
-                    const float u = fp.fx * xc * inv_z + fp.cx;
-                    const float v = fp.fy * yc * inv_z + fp.cy;
-                    if (!(v >= 0 && u >= 0 && v <= hm1 && u <= wm1)) continue;
-                    const int ui = (int)u, vi = (int)v;
-                    const float d = depths[depth_frame[f] * HW + (int64_t)vi * W + ui] / depth_scale;
-                    float sdf = d - zc;
-                    if (d <= 0 || d > depth_max || zc <= 0 || sdf < -sdf_trunc) continue;
-                    sdf = sdf < sdf_trunc ? sdf : sdf_trunc;
-                    sdf /= sdf_trunc;
-                    const float inv_wsum = 1.0f / (tw.y + 1);
-                    const float wgt = tw.y;
-                    tw.x = (wgt * tw.x + sdf) * inv_wsum;
-                    tw.y = wgt + 1;
-                    dirty = true;
-                }
-                if (dirty) vox[p] = tw;
-            }
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) t.mask[slot] = 0;
-    }
-}
-
-// ---- correctly rounded division without the v_div_scale / v_div_fixup wrapper ----------------
-// The instruction sequence below is exactly what hipcc emits for IEEE float division
-// (v_rcp_f32, Newton step, two residual corrections, final FMA = v_div_fmas without scaling).
-// v_div_scale only rescales operands whose exponents put the quotient near over/underflow, and
-// v_div_fixup only rewrites 0/inf/NaN cases, so for |num|, |den| in [2^-60, 2^60] the result
-// equals a/b bit for bit; outside that range we call the real division.  Verified
-// exhaustively on the GPU by tests/test_gpu_numerics.py.
-__device__ __forceinline__ float div_rn_core(float a, float b) {
-    const float y0 = __builtin_amdgcn_rcpf(b);
-    const float nb = -b;
-    const float e0 = __builtin_fmaf(nb, y0, 1.0f);
-    const float y1 = __builtin_fmaf(e0, y0, y0);
-    const float q0 = a * y1;
-    const float r0 = __builtin_fmaf(nb, q0, a);
-    const float q1 = __builtin_fmaf(r0, y1, q0);
-    const float r1 = __builtin_fmaf(nb, q1, a);
-    return __builtin_fmaf(r1, y1, q1);
-}
-
-__device__ __forceinline__ bool div_safe(float v) {
-    const float m = fabsf(v);
-    return m >= 0x1p-60f && m <= 0x1p60f;
-}
-
-__device__ __forceinline__ float div_rn(float a, float b) {
-    return (div_safe(a) && div_safe(b)) ? div_rn_core(a, b) : a / b;
-}
-
-__device__ __forceinline__ float rcp_rn(float b) { return div_safe(b) ? div_rn_core(1.0f, b) : 1.0f / b; }
-
-// Integrate, R known at compile time (R = 16 / 8): thread t owns the voxel column (x, y) =
-// (t % R, t / R % R) for z in its z-range, keeps those voxels' (tsdf, weight) in registers for
-// all frames of the batch, and evaluates Open3D's transform ((xs*e0 + ys*e1) + zs*e2) + e3 with
-// the z-independent partial product hoisted per frame -- the same float operations in the same
-// order, so the result is bit-identical to k_integrate.
-template <int R, int G>
-__global__ __launch_bounds__(256) void k_integrate_t(const int32_t* __restrict__ list, const int* __restrict__ counters,
-                                                     int64_t list_cap, Table t, float2* __restrict__ pool,
-                                                     float voxel_size, const float* __restrict__ depths, int64_t HW,
-                                                     int H, int W, const FrameParams* __restrict__ fps,
-                                                     const int64_t* __restrict__ depth_frame, float depth_scale,
-                                                     float depth_max, float sdf_trunc) {
-    constexpr int R2 = R * R;
-    constexpr int R3 = R2 * R;
-    constexpr int ZPER = R3 / 256;         // voxels per thread (16 at R=16, 2 at R=8)
-    constexpr int ZSTEP = 256 / R2;        // z stride between a thread's voxels (1 at R=16, 4 at R=8)
-    static_assert(R3 % 256 == 0, "R^3 must be a multiple of 256");
-    static_assert(ZPER % G == 0, "group size must divide the voxels per thread");
-    const bool unit_scale = depth_scale == 1.0f;  // d / 1 == d exactly: skip the division
-    const int64_t n = min((int64_t)counters[kListCount], list_cap);
-    const float hm1 = (float)H - 1.0f, wm1 = (float)W - 1.0f;
-    const int tid = threadIdx.x;
-    const int xv = tid % R, yv = (tid / R) % R, z0 = tid / R2;
-    for (int64_t i = blockIdx.x; i < n; i += gridDim.x) {
-        const int32_t slot = list[i];
-        const int buf = t.vals[slot];
-        const uint32_t mask = __builtin_amdgcn_readfirstlane(t.mask[slot]);
-        int xb, yb, zb;
-        unpack_key(t.keys[slot], xb, yb, zb);
-        if (buf >= 0) {
-            float2* vox = pool + (int64_t)buf * R3;
-            float2 tw[ZPER];
-            float zs[ZPER];
-#pragma unroll
-            for (int k = 0; k < ZPER; ++k) {
-                tw[k] = vox[k * 256 + tid];
-                zs[k] = (float)(zb * R + z0 + k * ZSTEP) * voxel_size;
-            }
-            const float xs = (float)(xb * R + xv) * voxel_size;
-            const float ys = (float)(yb * R + yv) * voxel_size;
-            uint32_t dirty = 0;
-            uint32_t m = mask;
-            while (m) {
-                const int f = __builtin_ctz(m);
-                m &= m - 1;
-                const FrameParams& fp = fps[f];
-                const float* __restrict__ dep = depths + depth_frame[f] * HW;
-                const float ax = xs * fp.ext[0] + ys * fp.ext[1];
-                const float ay = xs * fp.ext[4] + ys * fp.ext[5];
-                const float az = xs * fp.ext[8] + ys * fp.ext[9];
-                // Groups of G voxels: project all, issue all G depth gathers (branch-free, out-of-image
-                // lanes read pixel 0 and are masked), then update -- G loads in flight per wave.
-#pragma unroll
-                for (int g = 0; g < ZPER; g += G) {
-                    int pix[G];
-                    float zcs[G];
-                    bool in[G];
-#pragma unroll
-                    for (int j = 0; j < G; ++j) {
-                        const int k = g + j;
-                        const float xc = (ax + zs[k] * fp.ext[2]) + fp.ext[3];
-                        const float yc = (ay + zs[k] * fp.ext[6]) + fp.ext[7];
-                        const float zc = (az + zs[k] * fp.ext[10]) + fp.ext[11];
-                        const float inv_z = rcp_rn(zc);
-                        const float u = fp.fx * xc * inv_z + fp.cx;
-                        const float v = fp.fy * yc * inv_z + fp.cy;
-                        in[j] = v >= 0 && u >= 0 && v <= hm1 && u <= wm1;
-                        const int ui = (int)(in[j] ? u : 0.f), vi = (int)(in[j] ? v : 0.f);
-                        pix[j] = vi * W + ui;
-                        zcs[j] = zc;
-                    }
-                    float dv[G];
-#pragma unroll
-                    for (int j = 0; j < G; ++j) dv[j] = dep[pix[j]];
-#pragma unroll
-                    for (int j = 0; j < G; ++j) {
-                        const int k = g + j;
-                        const float d = unit_scale ? dv[j] : div_rn(dv[j], depth_scale);
-                        const float zc = zcs[j];
-                        float sdf = d - zc;
-                        if (!in[j] || d <= 0 || d > depth_max || zc <= 0 || sdf < -sdf_trunc) continue;
-                        sdf = sdf < sdf_trunc ? sdf : sdf_trunc;
-                        sdf = div_rn(sdf, sdf_trunc);
-                        const float wgt = tw[k].y;
-                        const float inv_wsum = rcp_rn(wgt + 1);
-                        tw[k].x = (wgt * tw[k].x + sdf) * inv_wsum;
-                        tw[k].y = wgt + 1;
-                        dirty |= 1u << k;
-                    }
-                }
-            }
-#pragma unroll
-            for (int k = 0; k < ZPER; ++k)
-                if (dirty & (1u << k)) vox[k * 256 + tid] = tw[k];
-        }
-        __syncthreads();
-        if (tid == 0) t.mask[slot] = 0;
-    }
-}
-
-// Exhaustive-check kernels for the division shortcut (tests/test_gpu_numerics.py).
-__global__ void k_check_rcp(uint32_t lo_bits, uint64_t count, uint32_t* mismatches, uint32_t* first_bad) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= count) return;
-    const uint32_t bits = lo_bits + (uint32_t)i;
-    const float b = __uint_as_float(bits);
-    const float fast = rcp_rn(b), ref = 1.0f / b;
-    if (__float_as_uint(fast) != __float_as_uint(ref)) {
-        atomicAdd(mismatches, 1u);
-        atomicMin(first_bad, bits);
-    }
-}
-
-__global__ void k_check_div(float b, uint32_t lo_bits, uint64_t count, uint32_t* mismatches, uint32_t* first_bad) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= count) return;
-    const uint32_t bits = lo_bits + (uint32_t)i;
-    const float a = __uint_as_float(bits);
-    const float fast = div_rn(a, b), ref = a / b;
-    if (__float_as_uint(fast) != __float_as_uint(ref) && !(isnan(fast) && isnan(ref))) {
-        atomicAdd(mismatches, 1u);
-        atomicMin(first_bad, bits);
-    }
-}
-
-__global__ void k_rehash(Table src, Table dst) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= src.cap) return;
-    const uint64_t k = src.keys[i];
-    if (k == kEmpty) return;
-    const uint64_t m = (uint64_t)dst.cap - 1;
-    uint64_t h = mix64(k) & m;
-    for (;;) {
-        const uint64_t old =
-            atomicCAS((unsigned long long*)&dst.keys[h], (unsigned long long)kEmpty, (unsigned long long)k);
-        if (old == kEmpty) break;
-        h = (h + 1) & m;
-    }
-    dst.vals[h] = src.vals[i];
-    dst.mask[h] = src.mask[i];
-}
-
-__global__ void k_set_counter(int* counters, int which, int value) { counters[which] = value; }
-
-__global__ void k_fixup_alloc(Table t, int* counters, int64_t pool_cap, uint64_t* bkeys) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= t.cap) return;
-    if (t.keys[i] == kEmpty || t.vals[i] != -2) return;
-    const int b = atomicAdd(&counters[kPoolCount], 1);
-    if (b < pool_cap) {
-        t.vals[i] = b;
-        bkeys[b] = t.keys[i];
-    } else {
-        atomicOr(&counters[kOverflow], 1);
-    }
-}
-
-__global__ void k_gather_keys(const int32_t* __restrict__ list, int64_t n, const Table t, int32_t* keys_out) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    int x, y, z;
-    unpack_key(t.keys[list[i]], x, y, z);
-    keys_out[3 * i] = x;
-    keys_out[3 * i + 1] = y;
-    keys_out[3 * i + 2] = z;
-}
-
-__global__ void k_clear_slots(const int32_t* __restrict__ list, int64_t n, Table t, int clear_keys) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const int32_t s = list[i];
-    t.mask[s] = 0;
-    if (clear_keys) {
-        t.keys[s] = kEmpty;
-        t.vals[s] = -1;
-    }
-}
-
-__global__ void k_export(const float2* __restrict__ pool, const uint64_t* __restrict__ bkeys, int64_t n, int R3,
-                         int32_t* keys, float* tsdf, float* weight) {
-    const int64_t b = blockIdx.x;
-    if (b >= n) return;
-    if (threadIdx.x == 0 && keys) {
-        int x, y, z;
-        unpack_key(bkeys[b], x, y, z);
-        keys[3 * b] = x;
-        keys[3 * b + 1] = y;
-        keys[3 * b + 2] = z;
-    }
-    for (int p = threadIdx.x; p < R3; p += blockDim.x) {
-        const float2 tw = pool[b * R3 + p];
-        if (tsdf) tsdf[b * R3 + p] = tw.x;
-        if (weight) weight[b * R3 + p] = tw.y;
-    }
-}
-
-__global__ void k_import(const int32_t* __restrict__ keys, int64_t n, const Table t, float2* pool, int R3,
-                         const float* __restrict__ tsdf, const float* __restrict__ weight) {
-    const int64_t b = blockIdx.x;
-    if (b >= n) return;
-    const int64_t slot = table_find(t, pack_key(keys[3 * b], keys[3 * b + 1], keys[3 * b + 2]));
-    if (slot < 0) return;
-    const int buf = t.vals[slot];
-    if (buf < 0) return;
-    for (int p = threadIdx.x; p < R3; p += blockDim.x)
-        pool[(int64_t)buf * R3 + p] = make_float2(tsdf[b * R3 + p], weight[b * R3 + p]);
-}
-
-__global__ void k_pack(const int32_t* __restrict__ ukeys, int64_t U, const Table t, const float2* __restrict__ pool,
-                       int R3, float2* out) {
-    const int64_t b = blockIdx.x;
-    if (b >= U) return;
-    const int64_t slot = table_find(t, pack_key(ukeys[3 * b], ukeys[3 * b + 1], ukeys[3 * b + 2]));
-    const int buf = slot >= 0 ? t.vals[slot] : -1;
-    for (int p = threadIdx.x; p < R3; p += blockDim.x) {
-        float2 r = make_float2(0.f, 0.f);
-        if (buf >= 0) {
-            const float2 tw = pool[(int64_t)buf * R3 + p];
-            r = make_float2(tw.y * tw.x, tw.y);
-        }
-        out[b * R3 + p] = r;
-    }
-}
-
-__global__ void k_unpack(const int32_t* __restrict__ ukeys, int64_t U, const Table t, float2* pool, int R3,
-                         const float2* __restrict__ in) {
-    const int64_t b = blockIdx.x;
-    if (b >= U) return;
-    const int64_t slot = table_find(t, pack_key(ukeys[3 * b], ukeys[3 * b + 1], ukeys[3 * b + 2]));
-    if (slot < 0) return;
-    const int buf = t.vals[slot];
-    if (buf < 0) return;
-    for (int p = threadIdx.x; p < R3; p += blockDim.x) {
-        const float2 s = in[b * R3 + p];
-        pool[(int64_t)buf * R3 + p] = make_float2(s.y > 0.f ? s.x / s.y : 0.f, s.y);
-    }
 }
 
 // ------------------------------------------------------------------ host helpers
@@ -531,20 +67,35 @@ static void free_table(Table& t) {
     t = Table{};
 }
 
-static int ensure_list(mqr_vbg* v, int64_t cap) {
+int sync_all(mqr_vbg* v) {
+    MQR_CHECK_HIP(hipStreamSynchronize(v->stream2));
+    MQR_CHECK_HIP(hipStreamSynchronize(v->stream));
+    v->int_pending[0] = v->int_pending[1] = false;
+    return 0;
+}
+
+static int ensure_lists(mqr_vbg* v, int64_t cap) {
     if (v->list_cap >= cap) return 0;
-    if (v->list) MQR_CHECK_HIP(hipFree(v->list));
-    MQR_CHECK_HIP(hipMalloc(&v->list, sizeof(int32_t) * cap));
+    if (sync_all(v)) return 1;
+    for (int p = 0; p < 2; ++p) {
+        if (v->lists[p]) MQR_CHECK_HIP(hipFree(v->lists[p]));
+        MQR_CHECK_HIP(hipMalloc(&v->lists[p], sizeof(int32_t) * cap));
+    }
     v->list_cap = cap;
     return 0;
 }
 
-// Grow the main table (between batches only: masks clear, list empty) to hold `live` keys at <= 50 % load.
+// Grow the main table to hold `live` keys at <= 50 % load.  Only between batches: waits for any
+// in-flight integrate (its lists hold slot indices of the old table) and all masks are zero then.
 static int ensure_table(mqr_vbg* v, int64_t live) {
     const int64_t want = next_pow2(2 * live);
-    if (v->tab.cap >= want) return ensure_list(v, v->tab.cap);
+    if (v->tab.cap >= want) return ensure_lists(v, v->tab.cap);
+    if (sync_all(v)) return 1;
     Table nt{};
     if (alloc_table(nt, want, v->stream)) return 1;
+    uint32_t* nm1 = nullptr;
+    MQR_CHECK_HIP(hipMalloc(&nm1, sizeof(uint32_t) * want));
+    MQR_CHECK_HIP(hipMemsetAsync(nm1, 0, sizeof(uint32_t) * want, v->stream));
     if (v->tab.cap) {
         const int64_t blocks = (v->tab.cap + 255) / 256;
         hipLaunchKernelGGL(k_rehash, dim3((unsigned)blocks), dim3(256), 0, v->stream, v->tab, nt);
@@ -552,12 +103,15 @@ static int ensure_table(mqr_vbg* v, int64_t live) {
         MQR_CHECK_HIP(hipStreamSynchronize(v->stream));
         free_table(v->tab);
     }
+    if (v->mask1) MQR_CHECK_HIP(hipFree(v->mask1));
     v->tab = nt;
-    return ensure_list(v, v->tab.cap);
+    v->mask1 = nm1;
+    return ensure_lists(v, v->tab.cap);
 }
 
 int grow_pool(mqr_vbg* v, int64_t need) {
     if (need <= v->pool_cap) return 0;
+    if (sync_all(v)) return 1;
     int64_t ncap = std::max<int64_t>(need, v->pool_cap + v->pool_cap / 2);
     float2* np = nullptr;
     uint64_t* nk = nullptr;
@@ -579,43 +133,72 @@ int grow_pool(mqr_vbg* v, int64_t need) {
     return 0;
 }
 
-int ensure_fp(mqr_vbg* v, int n) {
+static int ensure_fp(mqr_vbg* v, int n) {
     if (v->fp_cap >= n) return 0;
-    if (v->d_fp) MQR_CHECK_HIP(hipFree(v->d_fp));
-    if (v->h_fp) MQR_CHECK_HIP(hipHostFree(v->h_fp));
+    if (sync_all(v)) return 1;
     const int cap = std::max(n, kMaxBatch);
-    // FrameParams followed by the int64 depth-frame index array
-    MQR_CHECK_HIP(hipMalloc(&v->d_fp, (sizeof(FrameParams) + sizeof(int64_t)) * cap));
-    MQR_CHECK_HIP(hipHostMalloc(&v->h_fp, (sizeof(FrameParams) + sizeof(int64_t)) * cap, hipHostMallocDefault));
+    for (int p = 0; p < 2; ++p) {
+        if (v->d_fp[p]) MQR_CHECK_HIP(hipFree(v->d_fp[p]));
+        if (v->h_fp[p]) MQR_CHECK_HIP(hipHostFree(v->h_fp[p]));
+        // FrameParams followed by the int64 depth-frame index array
+        MQR_CHECK_HIP(hipMalloc(&v->d_fp[p], (sizeof(FrameParams) + sizeof(int64_t)) * cap));
+        MQR_CHECK_HIP(hipHostMalloc(&v->h_fp[p], (sizeof(FrameParams) + sizeof(int64_t)) * cap, hipHostMallocDefault));
+    }
     v->fp_cap = cap;
     return 0;
 }
 
-int ensure_depth(mqr_vbg* v, int64_t floats) {
+static int ensure_depth(mqr_vbg* v, int64_t floats) {
     if (v->depth_cap >= floats) return 0;
-    if (v->d_depth) MQR_CHECK_HIP(hipFree(v->d_depth));
-    MQR_CHECK_HIP(hipMalloc(&v->d_depth, sizeof(float) * floats));
+    if (sync_all(v)) return 1;
+    for (int p = 0; p < 2; ++p) {
+        if (v->d_depth[p]) MQR_CHECK_HIP(hipFree(v->d_depth[p]));
+        MQR_CHECK_HIP(hipMalloc(&v->d_depth[p], sizeof(float) * floats));
+    }
     v->depth_cap = floats;
     return 0;
 }
 
-int sync_counters(mqr_vbg* v) {
-    MQR_CHECK_HIP(hipMemcpyAsync(v->h_counters, v->counters, sizeof(int) * kCountersTotal, hipMemcpyDeviceToHost,
+static const int64_t* dframe_dev(const mqr_vbg* v, int p) {
+    return reinterpret_cast<const int64_t*>(v->d_fp[p] + v->fp_cap);
+}
+
+// Stage B frames' parameters into parity p (on `stream`; the caller made sure batch p is free).
+static int upload_frames(mqr_vbg* v, int p, const double* K, const double* T, const int* idx, int b,
+                         const int64_t* dframe) {
+    if (ensure_fp(v, b)) return 1;
+    int64_t* h_dframe = reinterpret_cast<int64_t*>(v->h_fp[p] + v->fp_cap);
+    for (int f = 0; f < b; ++f) {
+        make_frame_params(K + 9 * idx[f], T + 16 * idx[f], &v->h_fp[p][f]);
+        h_dframe[f] = dframe[f];
+    }
+    MQR_CHECK_HIP(hipMemcpyAsync(v->d_fp[p], v->h_fp[p], sizeof(FrameParams) * b, hipMemcpyHostToDevice, v->stream));
+    MQR_CHECK_HIP(hipMemcpyAsync(v->d_fp[p] + v->fp_cap, h_dframe, sizeof(int64_t) * b, hipMemcpyHostToDevice,
                                  v->stream));
-    MQR_CHECK_HIP(hipStreamSynchronize(v->stream));
     return 0;
 }
 
-static int reset_batch_counters(mqr_vbg* v) {
-    // keep kPoolCount; zero list/overflow/touch/frame-block and per-frame counters
-    MQR_CHECK_HIP(hipMemsetAsync(v->counters + 1, 0, sizeof(int) * (kCountersTotal - 1), v->stream));
+// Counters of parity p: zero (pool counter untouched).
+static int reset_batch_counters(mqr_vbg* v, int p) {
+    MQR_CHECK_HIP(hipMemsetAsync(v->ctr(p), 0, sizeof(int) * kCountersTotal, v->stream));
     return 0;
 }
 
-// After a touch/activate: allocate pool buffers that did not fit, if any.
-static int resolve_pool_overflow(mqr_vbg* v) {
-    if (sync_counters(v)) return 1;
-    int* c = v->h_counters;
+// Copy parity p's counters and the pool counter to the pinned mirror and wait (on `stream`).
+static int read_counters(mqr_vbg* v, int p) {
+    MQR_CHECK_HIP(hipMemcpyAsync(v->hctr(p), v->ctr(p), sizeof(int) * kCountersTotal, hipMemcpyDeviceToHost,
+                                 v->stream));
+    MQR_CHECK_HIP(hipMemcpyAsync(v->h_counters + 2 * kCountersTotal, v->pool_ctr(), sizeof(int),
+                                 hipMemcpyDeviceToHost, v->stream));
+    MQR_CHECK_HIP(hipEventRecord(v->ev_touch[p], v->stream));
+    MQR_CHECK_HIP(hipEventSynchronize(v->ev_touch[p]));
+    return 0;
+}
+
+// After a touch/activate of parity p: allocate pool buffers that did not fit, if any.
+static int resolve_pool_overflow(mqr_vbg* v, int p) {
+    if (read_counters(v, p)) return 1;
+    int* c = v->hctr(p);
     if (c[kOverflow] & 2) {
         set_error("internal: block table full");
         return 1;
@@ -628,64 +211,79 @@ static int resolve_pool_overflow(mqr_vbg* v) {
         set_error("block coordinate out of the supported range (|key| < 2^20 blocks)");
         return 2;
     }
+    int64_t pc = v->h_counters[2 * kCountersTotal];
     if (c[kOverflow] & 1) {
-        const int64_t attempted = c[kPoolCount];
         const int64_t old_cap = v->pool_cap;
-        if (grow_pool(v, std::max<int64_t>(attempted, old_cap * 2))) return 1;
-        hipLaunchKernelGGL(k_set_counter, dim3(1), dim3(1), 0, v->stream, v->counters, (int)kPoolCount, (int)old_cap);
-        MQR_CHECK_HIP(hipMemsetAsync(v->counters + kOverflow, 0, sizeof(int), v->stream));
+        if (grow_pool(v, std::max<int64_t>(pc, old_cap * 2))) return 1;  // waits for in-flight work
+        // every allocation < old_cap succeeded; those >= old_cap are retried on the new pool
+        hipLaunchKernelGGL(k_set_counter, dim3(1), dim3(1), 0, v->stream, v->pool_ctr(), (int)old_cap);
+        MQR_CHECK_HIP(hipMemsetAsync(v->ctr(p) + kOverflow, 0, sizeof(int), v->stream));
         const int64_t blocks = (v->tab.cap + 255) / 256;
-        hipLaunchKernelGGL(k_fixup_alloc, dim3((unsigned)blocks), dim3(256), 0, v->stream, v->tab, v->counters,
-                           v->pool_cap, v->bkeys);
+        hipLaunchKernelGGL(k_fixup_alloc, dim3((unsigned)blocks), dim3(256), 0, v->stream, v->tab, v->ctr(p),
+                           v->pool_ctr(), v->pool_cap, v->bkeys);
         MQR_CHECK_HIP(hipGetLastError());
-        if (sync_counters(v)) return 1;
+        if (read_counters(v, p)) return 1;
         if (c[kOverflow] & 1) {
             set_error("internal: pool growth failed");
             return 1;
         }
+        pc = v->h_counters[2 * kCountersTotal];
     }
-    v->pool_count = c[kPoolCount];
+    v->pool_count = pc;
     return 0;
 }
 
-static int launch_integrate(mqr_vbg* v, const float* depths, int64_t HW, int H, int W, int nframes,
+// Launch the integrate kernel for parity p on `stream2`, after touch(p) (event) completed.
+static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, int H, int W, int nframes,
                             float depth_scale, float depth_max, float sdf_trunc) {
-    const int64_t n = std::min<int64_t>(v->h_counters[kListCount], v->list_cap);
+    const int64_t n = std::min<int64_t>(v->hctr(p)[kListCount], v->list_cap);
     if (n == 0) return 0;
+    hipStream_t s = v->pipelined ? v->stream2 : v->stream;
+    if (v->pipelined) MQR_CHECK_HIP(hipStreamWaitEvent(s, v->ev_touch[p], 0));
     const unsigned grid = (unsigned)std::min<int64_t>(n, 8192);
-    const int64_t* depth_frame = reinterpret_cast<const int64_t*>(v->d_fp + v->fp_cap);
+    const int64_t* depth_frame = dframe_dev(v, p);
+    const Table t = v->table(p);
+    const int32_t* list = v->lists[p];
+    const int* counters = v->ctr(p);
+    const FrameParams* fp = v->d_fp[p];
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (v->profile) {
         MQR_CHECK_HIP(hipEventCreate(&e0));
         MQR_CHECK_HIP(hipEventCreate(&e1));
-        MQR_CHECK_HIP(hipEventRecord(e0, v->stream));
+        MQR_CHECK_HIP(hipEventRecord(e0, s));
     }
 #define MQR_LAUNCH_INT(RR, GG)                                                                                \
-    hipLaunchKernelGGL((k_integrate_t<RR, GG>), dim3(grid), dim3(256), 0, v->stream, v->list, v->counters,          \
-                       v->list_cap, v->tab, v->pool, v->voxel_size, depths, HW, H, W, v->d_fp, depth_frame,          \
-                       depth_scale, depth_max, sdf_trunc)
+    hipLaunchKernelGGL((k_integrate_t<RR, GG>), dim3(grid), dim3(256), 0, s, list, counters, v->list_cap, t,  \
+                       v->pool, v->voxel_size, depths, HW, H, W, fp, depth_frame, depth_scale, depth_max, sdf_trunc)
     if (v->R == 16 && v->kernel_variant == 0)
         MQR_LAUNCH_INT(16, 8);
     else if (v->R == 16 && v->kernel_variant == 2)
         MQR_LAUNCH_INT(16, 4);
-    else if (v->R == 16 && v->kernel_variant == 3)
-        MQR_LAUNCH_INT(16, 16);
-    else if (v->R == 16 && v->kernel_variant == 4)
-        MQR_LAUNCH_INT(16, 2);
     else if (v->R == 8 && v->kernel_variant != 1)
         MQR_LAUNCH_INT(8, 2);
     else
-        hipLaunchKernelGGL(k_integrate, dim3(grid), dim3(256), 0, v->stream, v->list, v->counters, v->list_cap,
-                           v->tab, v->pool, v->R, v->voxel_size, depths, HW, H, W, v->d_fp, depth_frame, depth_scale,
-                           depth_max, sdf_trunc);
+        hipLaunchKernelGGL(k_integrate, dim3(grid), dim3(256), 0, s, list, counters, v->list_cap, t, v->pool, v->R,
+                           v->voxel_size, depths, HW, H, W, fp, depth_frame, depth_scale, depth_max, sdf_trunc);
+#undef MQR_LAUNCH_INT
     MQR_CHECK_HIP(hipGetLastError());
     if (v->profile) {
-        MQR_CHECK_HIP(hipEventRecord(e1, v->stream));
+        MQR_CHECK_HIP(hipEventRecord(e1, s));
         v->int_events.emplace_back(e0, e1);
         v->stats.integrate_launches += 1;
         v->stats.union_blocks += n;
-        v->stats.frame_blocks += v->h_counters[kFrameBlocks];
+        v->stats.frame_blocks += v->hctr(p)[kFrameBlocks];
         v->stats.frames += nframes;
+    }
+    MQR_CHECK_HIP(hipEventRecord(v->ev_int[p], s));
+    v->int_pending[p] = true;
+    return 0;
+}
+
+// Before reusing parity p's batch state on `stream`: the integrate that last used it must be done.
+static int wait_parity_free(mqr_vbg* v, int p) {
+    if (v->int_pending[p]) {
+        MQR_CHECK_HIP(hipStreamWaitEvent(v->stream, v->ev_int[p], 0));
+        v->int_pending[p] = false;  // ordered behind it on `stream` from here on
     }
     return 0;
 }
@@ -708,6 +306,33 @@ static void drain_events(mqr_vbg* v) {
     }
     v->touch_events.clear();
 }
+
+static int touch_launch(mqr_vbg* v, int p, const float* dbase, int64_t HW, int H, int W, int b, float depth_scale,
+                        float depth_max, float sdf_trunc, float block_size, const Table& t, int alloc) {
+    const int n = (H / 4) * (W / 4);
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (v->profile) {
+        MQR_CHECK_HIP(hipEventCreate(&e0));
+        MQR_CHECK_HIP(hipEventCreate(&e1));
+        MQR_CHECK_HIP(hipEventRecord(e0, v->stream));
+    }
+    if (n > 0)
+        hipLaunchKernelGGL(k_touch, dim3((n + 255) / 256, b), dim3(256), 0, v->stream, dbase, HW, H, W, v->d_fp[p],
+                           dframe_dev(v, p), depth_scale, depth_max, sdf_trunc, block_size, t, alloc, v->ctr(p),
+                           v->pool_ctr(), v->pool_cap, v->bkeys, v->lists[p], v->list_cap);
+    MQR_CHECK_HIP(hipGetLastError());
+    if (v->profile) {
+        MQR_CHECK_HIP(hipEventRecord(e1, v->stream));
+        v->touch_events.emplace_back(e0, e1);
+        v->stats.touch_launches += 1;
+        v->stats.pixels += (int64_t)b * HW;
+    }
+    return 0;
+}
+
+static const char* kNoBlock =
+    "No block is touched in TSDF volume, abort integration. Please check specified parameters, especially "
+    "depth_scale and voxel_size";
 
 }  // namespace mqr
 
@@ -764,10 +389,16 @@ int mqr_vbg_create(float voxel_size, int block_resolution, int64_t block_count, 
     v->voxel_size = voxel_size;
     v->R = block_resolution;
     v->R3 = (int64_t)block_resolution * block_resolution * block_resolution;
-    if (hipStreamCreateWithFlags(&v->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc(&v->counters, sizeof(int) * kCountersTotal) != hipSuccess ||
-        hipHostMalloc(&v->h_counters, sizeof(int) * kCountersTotal, hipHostMallocDefault) != hipSuccess ||
-        hipMemsetAsync(v->counters, 0, sizeof(int) * kCountersTotal, v->stream) != hipSuccess) {
+    const size_t nctr = 2 * kCountersTotal + 8;
+    bool ok = hipStreamCreateWithFlags(&v->stream, hipStreamNonBlocking) == hipSuccess &&
+              hipStreamCreateWithFlags(&v->stream2, hipStreamNonBlocking) == hipSuccess &&
+              hipMalloc(&v->counters, sizeof(int) * nctr) == hipSuccess &&
+              hipHostMalloc(&v->h_counters, sizeof(int) * nctr, hipHostMallocDefault) == hipSuccess &&
+              hipMemsetAsync(v->counters, 0, sizeof(int) * nctr, v->stream) == hipSuccess;
+    for (int p = 0; p < 2 && ok; ++p)
+        ok = hipEventCreateWithFlags(&v->ev_touch[p], hipEventDisableTiming) == hipSuccess &&
+             hipEventCreateWithFlags(&v->ev_int[p], hipEventDisableTiming) == hipSuccess;
+    if (!ok) {
         set_error("mqr_vbg_create: device allocation failed");
         mqr_vbg_destroy(v);
         return 1;
@@ -784,18 +415,25 @@ int mqr_vbg_destroy(mqr_vbg* v) {
     if (!v) return 0;
     (void)hipSetDevice(v->device);
     if (v->stream) (void)hipStreamSynchronize(v->stream);
+    if (v->stream2) (void)hipStreamSynchronize(v->stream2);
     drain_events(v);
     free_table(v->tab);
     free_table(v->ftab);
+    if (v->mask1) (void)hipFree(v->mask1);
     if (v->pool) (void)hipFree(v->pool);
     if (v->bkeys) (void)hipFree(v->bkeys);
-    if (v->list) (void)hipFree(v->list);
+    for (int p = 0; p < 2; ++p) {
+        if (v->lists[p]) (void)hipFree(v->lists[p]);
+        if (v->d_fp[p]) (void)hipFree(v->d_fp[p]);
+        if (v->h_fp[p]) (void)hipHostFree(v->h_fp[p]);
+        if (v->d_depth[p]) (void)hipFree(v->d_depth[p]);
+        if (v->ev_touch[p]) (void)hipEventDestroy(v->ev_touch[p]);
+        if (v->ev_int[p]) (void)hipEventDestroy(v->ev_int[p]);
+    }
     if (v->counters) (void)hipFree(v->counters);
     if (v->h_counters) (void)hipHostFree(v->h_counters);
-    if (v->d_fp) (void)hipFree(v->d_fp);
-    if (v->h_fp) (void)hipHostFree(v->h_fp);
-    if (v->d_depth) (void)hipFree(v->d_depth);
     if (v->stream) (void)hipStreamDestroy(v->stream);
+    if (v->stream2) (void)hipStreamDestroy(v->stream2);
     delete v;
     return 0;
 }
@@ -803,12 +441,14 @@ int mqr_vbg_destroy(mqr_vbg* v) {
 int mqr_vbg_reset(mqr_vbg* v) {
     MQR_REQUIRE(v, "null volume");
     MQR_CHECK_HIP(hipSetDevice(v->device));
+    if (sync_all(v)) return 1;
     MQR_CHECK_HIP(hipMemsetAsync(v->tab.keys, 0xff, sizeof(uint64_t) * v->tab.cap, v->stream));
     MQR_CHECK_HIP(hipMemsetAsync(v->tab.vals, 0xff, sizeof(int32_t) * v->tab.cap, v->stream));
     MQR_CHECK_HIP(hipMemsetAsync(v->tab.mask, 0, sizeof(uint32_t) * v->tab.cap, v->stream));
+    MQR_CHECK_HIP(hipMemsetAsync(v->mask1, 0, sizeof(uint32_t) * v->tab.cap, v->stream));
     if (v->pool_count > 0)
         MQR_CHECK_HIP(hipMemsetAsync(v->pool, 0, sizeof(float2) * v->pool_count * v->R3, v->stream));
-    MQR_CHECK_HIP(hipMemsetAsync(v->counters, 0, sizeof(int) * kCountersTotal, v->stream));
+    MQR_CHECK_HIP(hipMemsetAsync(v->counters, 0, sizeof(int) * (2 * kCountersTotal + 8), v->stream));
     MQR_CHECK_HIP(hipStreamSynchronize(v->stream));
     v->pool_count = 0;
     return 0;
@@ -834,20 +474,6 @@ int mqr_vbg_params(mqr_vbg* v, float* voxel_size, int* R, int* device) {
     return 0;
 }
 
-// Upload B frames' parameters; depth_frame[f] = index of frame f in the depth array.
-static int upload_frames(mqr_vbg* v, const double* K, const double* T, const int* idx, int b, const int64_t* dframe) {
-    if (ensure_fp(v, b)) return 1;
-    // The stream was synchronised after the previous batch's touch, so the pinned mirror is free.
-    int64_t* h_dframe = reinterpret_cast<int64_t*>(v->h_fp + v->fp_cap);
-    for (int f = 0; f < b; ++f) {
-        make_frame_params(K + 9 * idx[f], T + 16 * idx[f], &v->h_fp[f]);
-        h_dframe[f] = dframe[f];
-    }
-    MQR_CHECK_HIP(hipMemcpyAsync(v->d_fp, v->h_fp, sizeof(FrameParams) * b, hipMemcpyHostToDevice, v->stream));
-    MQR_CHECK_HIP(hipMemcpyAsync(v->d_fp + v->fp_cap, h_dframe, sizeof(int64_t) * b, hipMemcpyHostToDevice, v->stream));
-    return 0;
-}
-
 int mqr_integrate_frames(mqr_vbg* v, const float* depths, int depth_loc, int B, int H, int W, const double* K,
                          const double* T_wc, const uint8_t* frame_ok, float depth_scale, float depth_max,
                          float trunc_mult) {
@@ -861,62 +487,55 @@ int mqr_integrate_frames(mqr_vbg* v, const float* depths, int depth_loc, int B, 
     std::vector<int> valid;
     for (int i = 0; i < B; ++i)
         if (!frame_ok || frame_ok[i]) valid.push_back(i);
-    for (size_t s = 0; s < valid.size(); s += kMaxBatch) {
+    int rc = 0;
+    int batch = 0;
+    for (size_t s = 0; s < valid.size(); s += kMaxBatch, ++batch) {
+        const int p = v->pipelined ? (batch & 1) : 0;
         const int b = (int)std::min<size_t>(kMaxBatch, valid.size() - s);
         const int* idx = valid.data() + s;
-        // table headroom for every key this batch could add (so no rehash mid-batch)
-        if (ensure_table(v, v->pool_count + b * max_touch)) return 1;
+        // table headroom for every key this batch could add (a rehash waits for in-flight work)
+        if (ensure_table(v, v->pool_count + b * max_touch) || ensure_fp(v, b)) return 1;
+        if (depth_loc != MQR_DEVICE && ensure_depth(v, b * HW)) return 1;
+        if (wait_parity_free(v, p)) return 1;
         const float* dbase = depths;
-        std::vector<int64_t> dframe(b);
+        int64_t dframe[kMaxBatch];
         if (depth_loc == MQR_DEVICE) {
             for (int f = 0; f < b; ++f) dframe[f] = idx[f];
         } else {
-            if (ensure_depth(v, b * HW)) return 1;
             for (int f = 0; f < b; ++f) {
-                MQR_CHECK_HIP(hipMemcpyAsync(v->d_depth + f * HW, depths + (int64_t)idx[f] * HW, sizeof(float) * HW,
-                                             hipMemcpyHostToDevice, v->stream));
+                MQR_CHECK_HIP(hipMemcpyAsync(v->d_depth[p] + f * HW, depths + (int64_t)idx[f] * HW,
+                                             sizeof(float) * HW, hipMemcpyHostToDevice, v->stream));
                 dframe[f] = f;
             }
-            dbase = v->d_depth;
+            dbase = v->d_depth[p];
         }
-        if (upload_frames(v, K, T_wc, idx, b, dframe.data())) return 1;
-        if (reset_batch_counters(v)) return 1;
-        const int64_t* d_dframe = reinterpret_cast<const int64_t*>(v->d_fp + v->fp_cap);
-        const int n = (H / 4) * (W / 4);
-        hipEvent_t e0 = nullptr, e1 = nullptr;
-        if (v->profile) {
-            MQR_CHECK_HIP(hipEventCreate(&e0));
-            MQR_CHECK_HIP(hipEventCreate(&e1));
-            MQR_CHECK_HIP(hipEventRecord(e0, v->stream));
-        }
-        if (n > 0)
-            hipLaunchKernelGGL(k_touch, dim3((n + 255) / 256, b), dim3(256), 0, v->stream, dbase, HW, H, W, v->d_fp,
-                               d_dframe, depth_scale, depth_max, sdf_trunc, block_size, v->tab, 1, v->counters,
-                               v->pool_cap, v->bkeys, v->list, v->list_cap);
-        MQR_CHECK_HIP(hipGetLastError());
-        if (v->profile) {
-            MQR_CHECK_HIP(hipEventRecord(e1, v->stream));
-            v->touch_events.emplace_back(e0, e1);
-            v->stats.touch_launches += 1;
-            v->stats.pixels += (int64_t)b * HW;
-        }
-        if (resolve_pool_overflow(v)) return 1;
+        if (upload_frames(v, p, K, T_wc, idx, b, dframe) || reset_batch_counters(v, p)) return 1;
+        if (touch_launch(v, p, dbase, HW, H, W, b, depth_scale, depth_max, sdf_trunc, block_size, v->table(p), 1))
+            return 1;
+        if (resolve_pool_overflow(v, p)) return 1;
         for (int f = 0; f < b; ++f)
-            if (v->h_counters[kFrameCounterBase + f] == 0) {
-                set_error("No block is touched in TSDF volume, abort integration. Please check specified parameters, "
-                          "especially depth_scale and voxel_size");
-                return 3;
+            if (v->hctr(p)[kFrameCounterBase + f] == 0) {
+                set_error(kNoBlock);
+                rc = 3;
             }
-        if (launch_integrate(v, dbase, HW, H, W, b, depth_scale, depth_max, sdf_trunc)) return 1;
+        if (rc) {  // leave the volume consistent: clear this batch's slot marks before failing
+            const int64_t n = std::min<int64_t>(v->hctr(p)[kListCount], v->list_cap);
+            if (n > 0)
+                hipLaunchKernelGGL(k_clear_slots, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, v->stream,
+                                   v->lists[p], n, v->table(p), 0);
+            break;
+        }
+        if (launch_integrate(v, p, dbase, HW, H, W, b, depth_scale, depth_max, sdf_trunc)) return 1;
     }
-    MQR_CHECK_HIP(hipStreamSynchronize(v->stream));
-    return 0;
+    if (sync_all(v)) return 1;
+    return rc;
 }
 
 int mqr_touch(mqr_vbg* v, const float* depth, int depth_loc, int H, int W, const double* K, const double* T_wc,
               float depth_scale, float depth_max, float trunc_mult, int32_t* keys_out, int64_t* n_out) {
     MQR_REQUIRE(v && depth && K && T_wc && keys_out && n_out, "null argument");
     MQR_CHECK_HIP(hipSetDevice(v->device));
+    if (sync_all(v)) return 1;
     const int64_t HW = (int64_t)H * W;
     const int64_t max_touch = 4LL * (H / 4) * (W / 4);
     const int64_t want = next_pow2(2 * std::max<int64_t>(max_touch, 1));
@@ -924,41 +543,35 @@ int mqr_touch(mqr_vbg* v, const float* depth, int depth_loc, int H, int W, const
         free_table(v->ftab);
         if (alloc_table(v->ftab, want, v->stream)) return 1;
     }
-    if (ensure_list(v, std::max(v->tab.cap, v->ftab.cap))) return 1;
+    if (ensure_lists(v, std::max(v->tab.cap, v->ftab.cap))) return 1;
     const float* dptr = depth;
     if (depth_loc != MQR_DEVICE) {
         if (ensure_depth(v, HW)) return 1;
-        MQR_CHECK_HIP(hipMemcpyAsync(v->d_depth, depth, sizeof(float) * HW, hipMemcpyHostToDevice, v->stream));
-        dptr = v->d_depth;
+        MQR_CHECK_HIP(hipMemcpyAsync(v->d_depth[0], depth, sizeof(float) * HW, hipMemcpyHostToDevice, v->stream));
+        dptr = v->d_depth[0];
     }
     const int idx = 0;
     const int64_t dframe = 0;
-    if (upload_frames(v, K, T_wc, &idx, 1, &dframe)) return 1;
-    if (reset_batch_counters(v)) return 1;
-    const int n = (H / 4) * (W / 4);
-    if (n > 0)
-        hipLaunchKernelGGL(k_touch, dim3((n + 255) / 256, 1), dim3(256), 0, v->stream, dptr, HW, H, W, v->d_fp,
-                           reinterpret_cast<const int64_t*>(v->d_fp + v->fp_cap), depth_scale, depth_max,
-                           v->voxel_size * trunc_mult, v->voxel_size * v->R, v->ftab, 0, v->counters, v->pool_cap,
-                           v->bkeys, v->list, v->list_cap);
-    MQR_CHECK_HIP(hipGetLastError());
-    if (sync_counters(v)) return 1;
-    const int64_t cnt = v->h_counters[kListCount];
+    if (upload_frames(v, 0, K, T_wc, &idx, 1, &dframe) || reset_batch_counters(v, 0)) return 1;
+    if (touch_launch(v, 0, dptr, HW, H, W, 1, depth_scale, depth_max, v->voxel_size * trunc_mult,
+                     v->voxel_size * v->R, v->ftab, 0))
+        return 1;
+    if (read_counters(v, 0)) return 1;
+    const int64_t cnt = v->hctr(0)[kListCount];
     int32_t* dkeys = nullptr;
     if (cnt > 0) {
         MQR_CHECK_HIP(hipMalloc(&dkeys, sizeof(int32_t) * 3 * cnt));
-        hipLaunchKernelGGL(k_gather_keys, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, v->stream, v->list, cnt,
-                           v->ftab, dkeys);
+        hipLaunchKernelGGL(k_gather_keys, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, v->stream, v->lists[0],
+                           cnt, v->ftab, dkeys);
         MQR_CHECK_HIP(hipMemcpyAsync(keys_out, dkeys, sizeof(int32_t) * 3 * cnt, hipMemcpyDeviceToHost, v->stream));
-        hipLaunchKernelGGL(k_clear_slots, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, v->stream, v->list, cnt,
-                           v->ftab, 1);
+        hipLaunchKernelGGL(k_clear_slots, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, v->stream, v->lists[0],
+                           cnt, v->ftab, 1);
         MQR_CHECK_HIP(hipStreamSynchronize(v->stream));
         MQR_CHECK_HIP(hipFree(dkeys));
     }
     *n_out = cnt;
-    if (v->h_counters[kFrameCounterBase] == 0) {
-        set_error("No block is touched in TSDF volume, abort integration. Please check specified parameters, "
-                  "especially depth_scale and voxel_size");
+    if (v->hctr(0)[kFrameCounterBase] == 0) {
+        set_error(kNoBlock);
         return 3;
     }
     return 0;
@@ -969,30 +582,30 @@ int mqr_integrate(mqr_vbg* v, const int32_t* keys, int64_t n, const float* depth
     MQR_REQUIRE(v && depth && K && T_wc && (keys || n == 0), "null argument");
     MQR_CHECK_HIP(hipSetDevice(v->device));
     if (n == 0) return 0;
+    if (sync_all(v)) return 1;
     const int64_t HW = (int64_t)H * W;
     if (ensure_table(v, v->pool_count + n)) return 1;
     const float* dptr = depth;
     if (depth_loc != MQR_DEVICE) {
         if (ensure_depth(v, HW)) return 1;
-        MQR_CHECK_HIP(hipMemcpyAsync(v->d_depth, depth, sizeof(float) * HW, hipMemcpyHostToDevice, v->stream));
-        dptr = v->d_depth;
+        MQR_CHECK_HIP(hipMemcpyAsync(v->d_depth[0], depth, sizeof(float) * HW, hipMemcpyHostToDevice, v->stream));
+        dptr = v->d_depth[0];
     }
     int32_t* dkeys = nullptr;
     MQR_CHECK_HIP(hipMalloc(&dkeys, sizeof(int32_t) * 3 * n));
     MQR_CHECK_HIP(hipMemcpyAsync(dkeys, keys, sizeof(int32_t) * 3 * n, hipMemcpyHostToDevice, v->stream));
     const int idx = 0;
     const int64_t dframe = 0;
-    if (upload_frames(v, K, T_wc, &idx, 1, &dframe)) return 1;
-    if (reset_batch_counters(v)) return 1;
-    hipLaunchKernelGGL(k_activate, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, v->stream, dkeys, n, v->tab,
-                       v->counters, v->pool_cap, v->bkeys, v->list, v->list_cap, 1);
+    if (upload_frames(v, 0, K, T_wc, &idx, 1, &dframe) || reset_batch_counters(v, 0)) return 1;
+    hipLaunchKernelGGL(k_activate, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, v->stream, dkeys, n, v->table(0),
+                       v->ctr(0), v->pool_ctr(), v->pool_cap, v->bkeys, v->lists[0], v->list_cap, 1);
     MQR_CHECK_HIP(hipGetLastError());
-    if (resolve_pool_overflow(v)) {
+    if (resolve_pool_overflow(v, 0)) {
         (void)hipFree(dkeys);
         return 1;
     }
-    int rc = launch_integrate(v, dptr, HW, H, W, 1, depth_scale, depth_max, v->voxel_size * trunc_mult);
-    MQR_CHECK_HIP(hipStreamSynchronize(v->stream));
+    int rc = launch_integrate(v, 0, dptr, HW, H, W, 1, depth_scale, depth_max, v->voxel_size * trunc_mult);
+    if (sync_all(v)) rc = 1;
     MQR_CHECK_HIP(hipFree(dkeys));
     return rc;
 }
@@ -1000,6 +613,7 @@ int mqr_integrate(mqr_vbg* v, const int32_t* keys, int64_t n, const float* depth
 int mqr_vbg_export(mqr_vbg* v, int32_t* keys, float* tsdf, float* weight, int loc) {
     MQR_REQUIRE(v, "null volume");
     MQR_CHECK_HIP(hipSetDevice(v->device));
+    if (sync_all(v)) return 1;
     const int64_t n = v->pool_count;
     if (n == 0) return 0;
     int32_t* dk = keys;
@@ -1033,13 +647,12 @@ int mqr_vbg_export(mqr_vbg* v, int32_t* keys, float* tsdf, float* weight, int lo
 
 // Activate `ukeys` (device, U triplets) without marking frames.
 static int activate_device_keys(mqr_vbg* v, const int32_t* dkeys, int64_t U) {
-    if (ensure_table(v, v->pool_count + U)) return 1;
-    if (reset_batch_counters(v)) return 1;
+    if (sync_all(v) || ensure_table(v, v->pool_count + U) || reset_batch_counters(v, 0)) return 1;
     if (U > 0)
-        hipLaunchKernelGGL(k_activate, dim3((unsigned)((U + 255) / 256)), dim3(256), 0, v->stream, dkeys, U, v->tab,
-                           v->counters, v->pool_cap, v->bkeys, v->list, v->list_cap, 0);
+        hipLaunchKernelGGL(k_activate, dim3((unsigned)((U + 255) / 256)), dim3(256), 0, v->stream, dkeys, U,
+                           v->table(0), v->ctr(0), v->pool_ctr(), v->pool_cap, v->bkeys, v->lists[0], v->list_cap, 0);
     MQR_CHECK_HIP(hipGetLastError());
-    return resolve_pool_overflow(v);
+    return resolve_pool_overflow(v, 0);
 }
 
 int mqr_vbg_import(mqr_vbg* v, const int32_t* keys, const float* tsdf, const float* weight, int64_t n, int loc) {
@@ -1081,6 +694,7 @@ int mqr_vbg_pack_weighted(mqr_vbg* v, const int32_t* union_keys, int64_t U, floa
     MQR_REQUIRE(v && (U == 0 || (union_keys && packed)), "null argument");
     MQR_CHECK_HIP(hipSetDevice(v->device));
     if (U == 0) return 0;
+    if (sync_all(v)) return 1;
     hipLaunchKernelGGL(k_pack, dim3((unsigned)U), dim3(256), 0, v->stream, union_keys, U, v->tab, v->pool, (int)v->R3,
                        reinterpret_cast<float2*>(packed));
     MQR_CHECK_HIP(hipGetLastError());
@@ -1102,7 +716,9 @@ int mqr_vbg_unpack_weighted(mqr_vbg* v, const int32_t* union_keys, int64_t U, co
 
 int mqr_vbg_set_variant(mqr_vbg* v, int variant) {
     MQR_REQUIRE(v, "null volume");
-    v->kernel_variant = variant;
+    if (sync_all(v)) return 1;
+    v->kernel_variant = variant & 0xff;
+    v->pipelined = (variant & 0x100) == 0;  // bit 8: serialise touch and integrate (A/B of the overlap)
     return 0;
 }
 
@@ -1121,7 +737,8 @@ int mqr_check_division(int device, int which, float b, uint32_t lo_bits, uint64_
         if (which == 0)
             hipLaunchKernelGGL(k_check_rcp, dim3(blocks), dim3(256), 0, 0, lo_bits + (uint32_t)off, c, d, d + 1);
         else
-            hipLaunchKernelGGL(k_check_div, dim3(blocks), dim3(256), 0, 0, b, lo_bits + (uint32_t)off, c, d, d + 1);
+            hipLaunchKernelGGL(k_check_div, dim3(blocks), dim3(256), 0, 0, which == 2 ? 1 : 0, b,
+                               lo_bits + (uint32_t)off, c, d, d + 1);
         MQR_CHECK_HIP(hipGetLastError());
     }
     uint32_t out[2];
@@ -1141,6 +758,7 @@ int mqr_vbg_profile(mqr_vbg* v, int enable) {
 int mqr_vbg_stats(mqr_vbg* v, mqr_stats* out, int reset) {
     MQR_REQUIRE(v && out, "null argument");
     MQR_CHECK_HIP(hipSetDevice(v->device));
+    if (sync_all(v)) return 1;
     drain_events(v);
     *out = v->stats;
     if (reset) v->stats = mqr_stats{};

@@ -1,0 +1,470 @@
+// vbg_kernels.hpp -- device code of the TSDF volume (included once, by vbg.hip).
+// Open3D 0.19 VoxelBlockGrid semantics; float32 with no FMA contraction.
+#pragma once
+#include "mqr_common.hpp"
+
+namespace mqr {
+
+// ------------------------------------------------------------------ device helpers
+__device__ inline int64_t table_find(const Table t, uint64_t k) {
+    const uint64_t m = (uint64_t)t.cap - 1;
+    uint64_t h = mix64(k) & m;
+    for (int64_t p = 0; p < t.cap; ++p) {
+        const uint64_t cur = t.keys[h];
+        if (cur == k) return (int64_t)h;
+        if (cur == kEmpty) return -1;
+        h = (h + 1) & m;
+    }
+    return -1;
+}
+
+// Insert-or-find.  A CAS winner allocates a pool buffer when `alloc`.
+__device__ inline int64_t table_insert(Table t, uint64_t k, bool alloc, int* counters, int* pool_ctr,
+                                       int64_t pool_cap, uint64_t* bkeys) {
+    const uint64_t m = (uint64_t)t.cap - 1;
+    uint64_t h = mix64(k) & m;
+    for (int64_t p = 0; p < t.cap; ++p) {
+        const uint64_t cur = t.keys[h];
+        if (cur == k) return (int64_t)h;
+        if (cur == kEmpty) {
+            const uint64_t old = atomicCAS((unsigned long long*)&t.keys[h], (unsigned long long)kEmpty,
+                                           (unsigned long long)k);
+            if (old == kEmpty) {
+                if (alloc) {
+                    const int b = atomicAdd(pool_ctr, 1);
+                    if (b < pool_cap) {
+                        t.vals[h] = b;
+                        bkeys[b] = k;
+                    } else {
+                        t.vals[h] = -2;
+                        atomicOr(&counters[kOverflow], 1);
+                    }
+                }
+                return (int64_t)h;
+            }
+            if (old == k) return (int64_t)h;
+        }
+        h = (h + 1) & m;
+    }
+    atomicOr(&counters[kOverflow], 2);
+    return -1;
+}
+
+__device__ inline void mark_slot(Table t, int64_t slot, int f, int* counters, int32_t* list, int64_t list_cap) {
+    const uint32_t bit = 1u << f;
+    const uint32_t old = atomicOr(&t.mask[slot], bit);
+    if (!(old & bit)) atomicAdd(&counters[kFrameBlocks], 1);
+    if (old == 0) {
+        const int pos = atomicAdd(&counters[kListCount], 1);
+        if (pos < list_cap)
+            list[pos] = (int32_t)slot;
+        else
+            atomicOr(&counters[kOverflow], 4);
+    }
+}
+
+__device__ inline uint64_t shfl_up_u64(uint64_t v, int d) {
+    const int lo = __shfl_up((int)(uint32_t)v, d, 64);
+    const int hi = __shfl_up((int)(uint32_t)(v >> 32), d, 64);
+    return ((uint64_t)(uint32_t)hi << 32) | (uint64_t)(uint32_t)lo;
+}
+
+// ------------------------------------------------------------------ kernels
+// compute_unique_block_coordinates for a batch: blockIdx.y = batch frame (bit), one thread per
+// stride-4 pixel, 4 samples over [max(d - trunc, 0), min(d + trunc, depth_max)] (Appendix A.2).
+__global__ __launch_bounds__(256) void k_touch(const float* __restrict__ depths, int64_t HW, int H, int W,
+                                               const FrameParams* __restrict__ fps,
+                                               const int64_t* __restrict__ depth_frame, float depth_scale,
+                                               float depth_max, float sdf_trunc, float block_size, Table t,
+                                               int alloc, int* counters, int* pool_ctr, int64_t pool_cap,
+                                               uint64_t* bkeys, int32_t* list, int64_t list_cap) {
+    const int f = blockIdx.y;
+    const FrameParams& fp = fps[f];
+    const int cols = W / 4, rows = H / 4, n = rows * cols;
+    const int w = blockIdx.x * blockDim.x + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    uint64_t key[4] = {kEmpty, kEmpty, kEmpty, kEmpty};
+    if (w < n) {
+        const int y = (w / cols) * 4, x = (w % cols) * 4;
+        const float d = depths[depth_frame[f] * HW + (int64_t)y * W + x] / depth_scale;
+        if (d > 0 && d < depth_max) {
+            const float xc = ((float)x - fp.cx) * 1.0f / fp.fx;
+            const float yc = ((float)y - fp.cy) * 1.0f / fp.fy;
+            const float zc = 1.0f;
+            const float xg = xc * fp.pose[0] + yc * fp.pose[1] + zc * fp.pose[2] + fp.pose[3];
+            const float yg = xc * fp.pose[4] + yc * fp.pose[5] + zc * fp.pose[6] + fp.pose[7];
+            const float zg = xc * fp.pose[8] + yc * fp.pose[9] + zc * fp.pose[10] + fp.pose[11];
+            const float xo = fp.pose[3], yo = fp.pose[7], zo = fp.pose[11];
+            const float xd = xg - xo, yd = yg - yo, zd = zg - zo;
+            const float t_min = fmaxf(d - sdf_trunc, 0.0f);
+            const float t_max = fminf(d + sdf_trunc, depth_max);
+            const float t_step = (t_max - t_min) / 3;
+            float tt = t_min;
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const int xb = (int)floorf((xo + tt * xd) / block_size);
+                const int yb = (int)floorf((yo + tt * yd) / block_size);
+                const int zb = (int)floorf((zo + tt * zd) / block_size);
+                if (key_in_range(xb, yb, zb))
+                    key[s] = pack_key(xb, yb, zb);
+                else
+                    atomicOr(&counters[kOverflow], 8);
+                tt += t_step;
+            }
+            atomicAdd(&counters[kFrameCounterBase + f], 4);
+        }
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        const uint64_t k = key[s];
+        const uint64_t up = shfl_up_u64(k, 1);
+        bool dup = (lane > 0 && up == k);
+        if (s > 0 && key[s - 1] == k) dup = true;
+        if (k != kEmpty && !dup) {
+            const int64_t slot = table_insert(t, k, alloc != 0, counters, pool_ctr, pool_cap, bkeys);
+            if (slot >= 0) mark_slot(t, slot, f, counters, list, list_cap);
+        }
+    }
+}
+
+// Activate explicit keys (vbg.integrate(block_coords, ...)); marks frame bit 0.
+__global__ void k_activate(const int32_t* __restrict__ keys, int64_t n, Table t, int* counters, int* pool_ctr,
+                           int64_t pool_cap, uint64_t* bkeys, int32_t* list, int64_t list_cap, int mark) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int x = keys[3 * i], y = keys[3 * i + 1], z = keys[3 * i + 2];
+    if (!key_in_range(x, y, z)) {
+        atomicOr(&counters[kOverflow], 8);
+        return;
+    }
+    const int64_t slot = table_insert(t, pack_key(x, y, z), true, counters, pool_ctr, pool_cap, bkeys);
+    if (slot >= 0 && mark) mark_slot(t, slot, 0, counters, list, list_cap);
+}
+
+// Projective TSDF update of every voxel of every listed block, frames applied in bit order.
+// Arithmetic = Open3D 0.19 Integrate kernel (Appendix A.3), float32, no contraction.
+__global__ __launch_bounds__(256) void k_integrate(const int32_t* __restrict__ list, const int* __restrict__ counters,
+                                                   int64_t list_cap, Table t, float2* __restrict__ pool, int R,
+                                                   float voxel_size, const float* __restrict__ depths, int64_t HW,
+                                                   int H, int W, const FrameParams* __restrict__ fps,
+                                                   const int64_t* __restrict__ depth_frame, float depth_scale,
+                                                   float depth_max, float sdf_trunc) {
+    const int64_t n = min((int64_t)counters[kListCount], list_cap);
+    const int R3 = R * R * R;
+    const float hm1 = (float)H - 1.0f, wm1 = (float)W - 1.0f;
+    for (int64_t i = blockIdx.x; i < n; i += gridDim.x) {
+        const int32_t slot = list[i];
+        const int buf = t.vals[slot];
+        const uint32_t mask = t.mask[slot];
+        int xb, yb, zb;
+        unpack_key(t.keys[slot], xb, yb, zb);
+        if (buf >= 0) {
+            float2* vox = pool + (int64_t)buf * R3;
+            for (int p = threadIdx.x; p < R3; p += blockDim.x) {
+                const int xv = p % R, yv = (p / R) % R, zv = p / (R * R);
+                const float xs = (float)(xb * R + xv) * voxel_size;
+                const float ys = (float)(yb * R + yv) * voxel_size;
+                const float zs = (float)(zb * R + zv) * voxel_size;
+                float2 tw = vox[p];
+                bool dirty = false;
+                uint32_t m = mask;
+                while (m) {
+                    const int f = __builtin_ctz(m);
+                    m &= m - 1;
+                    const FrameParams& fp = fps[f];
+                    const float xc = xs * fp.ext[0] + ys * fp.ext[1] + zs * fp.ext[2] + fp.ext[3];
+                    const float yc = xs * fp.ext[4] + ys * fp.ext[5] + zs * fp.ext[6] + fp.ext[7];
+                    const float zc = xs * fp.ext[8] + ys * fp.ext[9] + zs * fp.ext[10] + fp.ext[11];
+                    const float inv_z = 1.0f / zc;
+                    const float u = fp.fx * xc * inv_z + fp.cx;
+                    const float v = fp.fy * yc * inv_z + fp.cy;
+                    if (!(v >= 0 && u >= 0 && v <= hm1 && u <= wm1)) continue;
+                    const int ui = (int)u, vi = (int)v;
+                    const float d = depths[depth_frame[f] * HW + (int64_t)vi * W + ui] / depth_scale;
+                    float sdf = d - zc;
+                    if (d <= 0 || d > depth_max || zc <= 0 || sdf < -sdf_trunc) continue;
+                    sdf = sdf < sdf_trunc ? sdf : sdf_trunc;
+                    sdf /= sdf_trunc;
+                    const float inv_wsum = 1.0f / (tw.y + 1);
+                    const float wgt = tw.y;
+                    tw.x = (wgt * tw.x + sdf) * inv_wsum;
+                    tw.y = wgt + 1;
+                    dirty = true;
+                }
+                if (dirty) vox[p] = tw;
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) t.mask[slot] = 0;
+    }
+}
+
+// ---- correctly rounded division without the v_div_scale / v_div_fixup wrapper ----------------
+// The instruction sequence below is exactly what hipcc emits for IEEE float division
+// (v_rcp_f32, Newton step, two residual corrections, final FMA = v_div_fmas without scaling).
+// v_div_scale only rescales operands whose exponents put the quotient near over/underflow, and
+// v_div_fixup only rewrites 0/inf/NaN cases, so for |num|, |den| in [2^-60, 2^60] the result
+// equals a/b bit for bit; outside that range we call the real division.  Verified
+// exhaustively on the GPU by tests/test_gpu_numerics.py.
+__device__ __forceinline__ float div_rn_core(float a, float b) {
+    const float y0 = __builtin_amdgcn_rcpf(b);
+    const float nb = -b;
+    const float e0 = __builtin_fmaf(nb, y0, 1.0f);
+    const float y1 = __builtin_fmaf(e0, y0, y0);
+    const float q0 = a * y1;
+    const float r0 = __builtin_fmaf(nb, q0, a);
+    const float q1 = __builtin_fmaf(r0, y1, q0);
+    const float r1 = __builtin_fmaf(nb, q1, a);
+    return __builtin_fmaf(r1, y1, q1);
+}
+
+__device__ __forceinline__ bool div_safe(float v) {
+    const float m = fabsf(v);
+    return m >= 0x1p-60f && m <= 0x1p60f;
+}
+
+__device__ __forceinline__ float div_rn(float a, float b) {
+    return (div_safe(a) && div_safe(b)) ? div_rn_core(a, b) : a / b;
+}
+
+__device__ __forceinline__ float rcp_rn(float b) { return div_safe(b) ? div_rn_core(1.0f, b) : 1.0f / b; }
+
+// Integrate, R known at compile time (R = 16 / 8): thread t owns the voxel column (x, y) =
+// (t % R, t / R % R) for z in its z-range, keeps those voxels' (tsdf, weight) in registers for
+// all frames of the batch, and evaluates Open3D's transform ((xs*e0 + ys*e1) + zs*e2) + e3 with
+// the z-independent partial product hoisted per frame -- the same float operations in the same
+// order, so the result is bit-identical to k_integrate.
+template <int R, int G>
+__global__ __launch_bounds__(256) void k_integrate_t(const int32_t* __restrict__ list, const int* __restrict__ counters,
+                                                     int64_t list_cap, Table t, float2* __restrict__ pool,
+                                                     float voxel_size, const float* __restrict__ depths, int64_t HW,
+                                                     int H, int W, const FrameParams* __restrict__ fps,
+                                                     const int64_t* __restrict__ depth_frame, float depth_scale,
+                                                     float depth_max, float sdf_trunc) {
+    constexpr int R2 = R * R;
+    constexpr int R3 = R2 * R;
+    constexpr int ZPER = R3 / 256;         // voxels per thread (16 at R=16, 2 at R=8)
+    constexpr int ZSTEP = 256 / R2;        // z stride between a thread's voxels (1 at R=16, 4 at R=8)
+    static_assert(R3 % 256 == 0, "R^3 must be a multiple of 256");
+    static_assert(ZPER % G == 0, "group size must divide the voxels per thread");
+    const bool unit_scale = depth_scale == 1.0f;  // d / 1 == d exactly: skip the division
+    const int64_t n = min((int64_t)counters[kListCount], list_cap);
+    const float hm1 = (float)H - 1.0f, wm1 = (float)W - 1.0f;
+    const int tid = threadIdx.x;
+    const int xv = tid % R, yv = (tid / R) % R, z0 = tid / R2;
+    for (int64_t i = blockIdx.x; i < n; i += gridDim.x) {
+        const int32_t slot = list[i];
+        const int buf = t.vals[slot];
+        const uint32_t mask = __builtin_amdgcn_readfirstlane(t.mask[slot]);
+        int xb, yb, zb;
+        unpack_key(t.keys[slot], xb, yb, zb);
+        if (buf >= 0) {
+            float2* vox = pool + (int64_t)buf * R3;
+            float2 tw[ZPER];
+            float zs[ZPER];
+#pragma unroll
+            for (int k = 0; k < ZPER; ++k) {
+                tw[k] = vox[k * 256 + tid];
+                zs[k] = (float)(zb * R + z0 + k * ZSTEP) * voxel_size;
+            }
+            const float xs = (float)(xb * R + xv) * voxel_size;
+            const float ys = (float)(yb * R + yv) * voxel_size;
+            uint32_t dirty = 0;
+            uint32_t m = mask;
+            while (m) {
+                const int f = __builtin_ctz(m);
+                m &= m - 1;
+                const FrameParams& fp = fps[f];
+                const float* __restrict__ dep = depths + depth_frame[f] * HW;
+                const float ax = xs * fp.ext[0] + ys * fp.ext[1];
+                const float ay = xs * fp.ext[4] + ys * fp.ext[5];
+                const float az = xs * fp.ext[8] + ys * fp.ext[9];
+                // Groups of G voxels: project all, issue all G depth gathers (branch-free, out-of-image
+                // lanes read pixel 0 and are masked), then update -- G loads in flight per wave.
+#pragma unroll
+                for (int g = 0; g < ZPER; g += G) {
+                    int pix[G];
+                    float zcs[G];
+                    bool in[G];
+#pragma unroll
+                    for (int j = 0; j < G; ++j) {
+                        const int k = g + j;
+                        const float xc = (ax + zs[k] * fp.ext[2]) + fp.ext[3];
+                        const float yc = (ay + zs[k] * fp.ext[6]) + fp.ext[7];
+                        const float zc = (az + zs[k] * fp.ext[10]) + fp.ext[11];
+                        const float inv_z = rcp_rn(zc);
+                        const float u = fp.fx * xc * inv_z + fp.cx;
+                        const float v = fp.fy * yc * inv_z + fp.cy;
+                        in[j] = v >= 0 && u >= 0 && v <= hm1 && u <= wm1;
+                        const int ui = (int)(in[j] ? u : 0.f), vi = (int)(in[j] ? v : 0.f);
+                        pix[j] = vi * W + ui;
+                        zcs[j] = zc;
+                    }
+                    float dv[G];
+#pragma unroll
+                    for (int j = 0; j < G; ++j) dv[j] = dep[pix[j]];
+#pragma unroll
+                    for (int j = 0; j < G; ++j) {
+                        const int k = g + j;
+                        const float d = unit_scale ? dv[j] : div_rn(dv[j], depth_scale);
+                        const float zc = zcs[j];
+                        float sdf = d - zc;
+                        if (!in[j] || d <= 0 || d > depth_max || zc <= 0 || sdf < -sdf_trunc) continue;
+                        sdf = sdf < sdf_trunc ? sdf : sdf_trunc;
+                        sdf = div_rn(sdf, sdf_trunc);
+                        const float wgt = tw[k].y;
+                        const float inv_wsum = rcp_rn(wgt + 1);
+                        tw[k].x = (wgt * tw[k].x + sdf) * inv_wsum;
+                        tw[k].y = wgt + 1;
+                        dirty |= 1u << k;
+                    }
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < ZPER; ++k)
+                if (dirty & (1u << k)) vox[k * 256 + tid] = tw[k];
+        }
+        __syncthreads();
+        if (tid == 0) t.mask[slot] = 0;
+    }
+}
+
+// Exhaustive-check kernels for the division shortcut (tests/test_gpu_numerics.py).
+__global__ void k_check_rcp(uint32_t lo_bits, uint64_t count, uint32_t* mismatches, uint32_t* first_bad) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    const uint32_t bits = lo_bits + (uint32_t)i;
+    const float b = __uint_as_float(bits);
+    const float fast = rcp_rn(b), ref = 1.0f / b;
+    if (__float_as_uint(fast) != __float_as_uint(ref)) {
+        atomicAdd(mismatches, 1u);
+        atomicMin(first_bad, bits);
+    }
+}
+
+__global__ void k_check_div(int which_core, float b, uint32_t lo_bits, uint64_t count, uint32_t* mismatches, uint32_t* first_bad) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    const uint32_t bits = lo_bits + (uint32_t)i;
+    const float a = __uint_as_float(bits);
+    const float fast = which_core ? div_rn_core(a, b) : div_rn(a, b), ref = a / b;
+    if (__float_as_uint(fast) != __float_as_uint(ref) && !(isnan(fast) && isnan(ref))) {
+        atomicAdd(mismatches, 1u);
+        atomicMin(first_bad, bits);
+    }
+}
+
+__global__ void k_rehash(Table src, Table dst) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= src.cap) return;
+    const uint64_t k = src.keys[i];
+    if (k == kEmpty) return;
+    const uint64_t m = (uint64_t)dst.cap - 1;
+    uint64_t h = mix64(k) & m;
+    for (;;) {
+        const uint64_t old =
+            atomicCAS((unsigned long long*)&dst.keys[h], (unsigned long long)kEmpty, (unsigned long long)k);
+        if (old == kEmpty) break;
+        h = (h + 1) & m;
+    }
+    dst.vals[h] = src.vals[i];
+    dst.mask[h] = src.mask[i];
+}
+
+__global__ void k_set_counter(int* ctr, int value) { *ctr = value; }
+
+__global__ void k_fixup_alloc(Table t, int* counters, int* pool_ctr, int64_t pool_cap, uint64_t* bkeys) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= t.cap) return;
+    if (t.keys[i] == kEmpty || t.vals[i] != -2) return;
+    const int b = atomicAdd(pool_ctr, 1);
+    if (b < pool_cap) {
+        t.vals[i] = b;
+        bkeys[b] = t.keys[i];
+    } else {
+        atomicOr(&counters[kOverflow], 1);
+    }
+}
+
+__global__ void k_gather_keys(const int32_t* __restrict__ list, int64_t n, const Table t, int32_t* keys_out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int x, y, z;
+    unpack_key(t.keys[list[i]], x, y, z);
+    keys_out[3 * i] = x;
+    keys_out[3 * i + 1] = y;
+    keys_out[3 * i + 2] = z;
+}
+
+__global__ void k_clear_slots(const int32_t* __restrict__ list, int64_t n, Table t, int clear_keys) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int32_t s = list[i];
+    t.mask[s] = 0;
+    if (clear_keys) {
+        t.keys[s] = kEmpty;
+        t.vals[s] = -1;
+    }
+}
+
+__global__ void k_export(const float2* __restrict__ pool, const uint64_t* __restrict__ bkeys, int64_t n, int R3,
+                         int32_t* keys, float* tsdf, float* weight) {
+    const int64_t b = blockIdx.x;
+    if (b >= n) return;
+    if (threadIdx.x == 0 && keys) {
+        int x, y, z;
+        unpack_key(bkeys[b], x, y, z);
+        keys[3 * b] = x;
+        keys[3 * b + 1] = y;
+        keys[3 * b + 2] = z;
+    }
+    for (int p = threadIdx.x; p < R3; p += blockDim.x) {
+        const float2 tw = pool[b * R3 + p];
+        if (tsdf) tsdf[b * R3 + p] = tw.x;
+        if (weight) weight[b * R3 + p] = tw.y;
+    }
+}
+
+__global__ void k_import(const int32_t* __restrict__ keys, int64_t n, const Table t, float2* pool, int R3,
+                         const float* __restrict__ tsdf, const float* __restrict__ weight) {
+    const int64_t b = blockIdx.x;
+    if (b >= n) return;
+    const int64_t slot = table_find(t, pack_key(keys[3 * b], keys[3 * b + 1], keys[3 * b + 2]));
+    if (slot < 0) return;
+    const int buf = t.vals[slot];
+    if (buf < 0) return;
+    for (int p = threadIdx.x; p < R3; p += blockDim.x)
+        pool[(int64_t)buf * R3 + p] = make_float2(tsdf[b * R3 + p], weight[b * R3 + p]);
+}
+
+__global__ void k_pack(const int32_t* __restrict__ ukeys, int64_t U, const Table t, const float2* __restrict__ pool,
+                       int R3, float2* out) {
+    const int64_t b = blockIdx.x;
+    if (b >= U) return;
+    const int64_t slot = table_find(t, pack_key(ukeys[3 * b], ukeys[3 * b + 1], ukeys[3 * b + 2]));
+    const int buf = slot >= 0 ? t.vals[slot] : -1;
+    for (int p = threadIdx.x; p < R3; p += blockDim.x) {
+        float2 r = make_float2(0.f, 0.f);
+        if (buf >= 0) {
+            const float2 tw = pool[(int64_t)buf * R3 + p];
+            r = make_float2(tw.y * tw.x, tw.y);
+        }
+        out[b * R3 + p] = r;
+    }
+}
+
+__global__ void k_unpack(const int32_t* __restrict__ ukeys, int64_t U, const Table t, float2* pool, int R3,
+                         const float2* __restrict__ in) {
+    const int64_t b = blockIdx.x;
+    if (b >= U) return;
+    const int64_t slot = table_find(t, pack_key(ukeys[3 * b], ukeys[3 * b + 1], ukeys[3 * b + 2]));
+    if (slot < 0) return;
+    const int buf = t.vals[slot];
+    if (buf < 0) return;
+    for (int p = threadIdx.x; p < R3; p += blockDim.x) {
+        const float2 s = in[b * R3 + p];
+        pool[(int64_t)buf * R3 + p] = make_float2(s.y > 0.f ? s.x / s.y : 0.f, s.y);
+    }
+}
+
+}  // namespace mqr

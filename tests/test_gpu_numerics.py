@@ -41,7 +41,7 @@ def test_specialised_integrate_equals_generic():
     from mqr.vbg import VoxelBlockGrid
     seq = synthetic.make_sequence("room", n=20, height=240, width=320, f=262.5, noise=True, seed=21)
     out = []
-    for R, variant in ((16, 0), (16, 1), (8, 0), (8, 1)):
+    for R, variant in ((16, 0), (16, 1), (8, 0), (8, 1), (16, 2), (16, 0x100), (8, 0x101)):
         v = VoxelBlockGrid(voxel_size=0.01, block_resolution=R, block_count=64)
         _lib.call("mqr_vbg_set_variant", v.handle, variant)
         v.integrate_frames(seq["depth"], seq["K"], seq["T_wc"], depth_scale=1.0, depth_max=4.0,
@@ -49,3 +49,13 @@ def test_specialised_integrate_equals_generic():
         out.append(v.export())
     assert compare_volumes(out[0], out[1], 0.0) == 0.0
     assert compare_volumes(out[2], out[3], 0.0) == 0.0
+    assert compare_volumes(out[0], out[4], 0.0) == 0.0
+    assert compare_volumes(out[0], out[5], 0.0) == 0.0
+    assert compare_volumes(out[2], out[6], 0.0) == 0.0
+
+
+def test_division_core_on_positive_zero():
+    """The branch-free update divides s = +0 (d == zc) through the core sequence: must give +0."""
+    for b in (0.05, 1.0, 3.0):
+        mm, _ = _check(2, b, 0.0, 2.0 ** -149)  # bit pattern 0 only
+        assert mm == 0
