@@ -57,24 +57,29 @@ def merge_to_root(vbg, group=None, root: int = 0, all_ranks: bool = False):
     Returns the union block count."""
     import torch
     import torch.distributed as dist
-    on_gpu = dist.get_backend(group) == "nccl"
-    dev = torch.device("cuda", vbg.device_id) if on_gpu else torch.device("cpu")
-    keys = union_keys(vbg.export_keys(), group=group, device=dev)
+    nccl = dist.get_backend(group) == "nccl"
+    on_device = getattr(vbg, "on_device", True)   # the numpy stand-in of the CPU tests says False
+    vdev = torch.device("cuda", vbg.device_id) if on_device else torch.device("cpu")
+    cdev = vdev if nccl else torch.device("cpu")  # gloo collectives run on host tensors
+    keys = union_keys(vbg.export_keys(), group=group, device=cdev)
     U = len(keys)
     if U == 0:
         return 0
     R3 = vbg.block_resolution ** 3
-    dkeys = torch.as_tensor(keys, device=dev).contiguous()
-    packed = torch.empty((U, R3, 2), dtype=torch.float32, device=dev)
-    if on_gpu:
-        torch.cuda.synchronize(dev)
+    dkeys = torch.as_tensor(keys, device=vdev).contiguous()
+    packed = torch.empty((U, R3, 2), dtype=torch.float32, device=vdev)
+    if on_device:
+        torch.cuda.synchronize(vdev)
     vbg.pack_weighted(dkeys.data_ptr(), U, packed.data_ptr())
+    buf = packed if cdev == vdev else packed.to(cdev)
     if all_ranks:
-        dist.all_reduce(packed, op=dist.ReduceOp.SUM, group=group)
+        dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
     else:
-        dist.reduce(packed, dst=root, op=dist.ReduceOp.SUM, group=group)
-    if on_gpu:
-        torch.cuda.synchronize(dev)
+        dist.reduce(buf, dst=root, op=dist.ReduceOp.SUM, group=group)
     if all_ranks or dist.get_rank(group) == root:
+        if buf is not packed:
+            packed.copy_(buf)
+        if on_device:
+            torch.cuda.synchronize(vdev)
         vbg.unpack_weighted(dkeys.data_ptr(), U, packed.data_ptr())
     return U

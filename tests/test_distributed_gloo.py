@@ -16,6 +16,7 @@ R3 = R ** 3
 class NumpyVolume:
     block_resolution = R
     device_id = 0
+    on_device = False
 
     def __init__(self, blocks):
         self.blocks = {tuple(k): (t.copy(), w.copy()) for k, (t, w) in blocks.items()}

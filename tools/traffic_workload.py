@@ -1,0 +1,49 @@
+#!/usr/bin/env python3
+"""Workload for the rocprofv3 --pmc traffic passes: the bench's integrate step (one 500-frame
+pass, default kernel) followed by k_pack over every block (known bytes: U*R^3*8 read + written)
+which calibrates FETCH_SIZE / WRITE_SIZE for 8-byte-per-lane accesses (MI355X_MICROARCH.md §HBM:
+other widths are uncalibrated).  Writes gpurun_out/pmc/workload.json with the known byte counts."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "metaquest-3d-reconstruction_amd"))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import numpy as np
+    import torch
+    from bench import _DevPtr
+    from mqr import synthetic
+    from mqr.vbg import VoxelBlockGrid
+    seq = synthetic.make_sequence_fast("room", poses=synthetic.room_loop_poses(500), device="cuda:0")
+    d = seq["depth_t"].contiguous()
+    B, H, W = d.shape
+    K, T = seq["K"].astype(np.float64), seq["T_wc"].astype(np.float64)
+    torch.cuda.synchronize()
+    vbg = VoxelBlockGrid(voxel_size=0.005, block_resolution=16, block_count=40000, device=0)
+    vbg.profile(True)
+    vbg.integrate_frames((_DevPtr(d.data_ptr()), B, H, W), K, T, depth_scale=1.0, depth_max=4.0,
+                         trunc_voxel_multiplier=10.0)
+    st = vbg.stats(reset=True)
+    keys = torch.as_tensor(np.unique(vbg.export_keys(), axis=0), device="cuda:0").contiguous()
+    U = keys.shape[0]
+    out = torch.empty((U, 4096, 2), dtype=torch.float32, device="cuda:0")
+    torch.cuda.synchronize()
+    vbg.pack_weighted(keys.data_ptr(), U, out.data_ptr())
+    torch.cuda.synchronize()
+    R3 = 4096
+    info = {"integrate_launches": st["integrate_launches"], "union_blocks": st["union_blocks"],
+            "frame_blocks": st["frame_blocks"], "frames": st["frames"], "H": H, "W": W,
+            "alg_bytes_total": 16 * R3 * st["union_blocks"] + 4 * H * W * st["frames"] + 16 * st["frame_blocks"],
+            "pack_blocks": U, "pack_read_bytes": U * R3 * 8, "pack_write_bytes": U * R3 * 8}
+    os.makedirs(os.path.join(ROOT, "gpurun_out", "pmc"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", "pmc", "workload.json"), "w") as f:
+        json.dump(info, f)
+    print(json.dumps(info))
+
+
+if __name__ == "__main__":
+    main()
