@@ -68,6 +68,22 @@ def extract_ms(vbg, thr, reps):
     return times[len(times) // 2], counts
 
 
+def pmc_traffic(H, W, frames):
+    """HBM bytes per integrate launch from the committed rocprofv3 --pmc passes of this workload
+    (tools/traffic_workload.py + tools/pmc_summary.py; FETCH_SIZE/WRITE_SIZE calibrated on k_pack)."""
+    import glob
+    recs = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
+    for path in reversed(recs):
+        try:
+            rec = json.load(open(path))
+            wl = rec["workload"]
+            if (wl["H"], wl["W"], wl["frames"]) == (H, W, frames):
+                return rec["traffic_bytes_per_launch"], os.path.relpath(path, ROOT)
+        except (OSError, KeyError, ValueError):
+            continue
+    return None, None
+
+
 def cpu_baseline(seq_host, K, T, args):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # the checker / CPU restatement (port) -- timed here as the baseline only
@@ -163,6 +179,8 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(depth_t.cpu().numpy(), K, T, args)
 
+    traffic, traffic_src = pmc_traffic(H, W, B)
+
     if rank == 0:
         total_frames = B * world * args.steps
         out = {
@@ -188,7 +206,8 @@ def main():
             "extract": {"weight_threshold": args.extract_threshold, "vertices": nv, "triangles": nt,
                         "blocks": blocks, "note": "device-resident extract_triangle_mesh, median of reps"},
             "roofline": {"bound": "hbm", "kernel": "k_integrate", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "alg_bytes_per_launch": alg_bytes / launches, "avg_launch_ms": avg_ms,
                          "launches": st["integrate_launches"], "union_blocks_per_launch":
                              st["union_blocks"] / launches, "frame_blocks_per_frame":
