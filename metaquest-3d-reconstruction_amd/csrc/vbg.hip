@@ -252,15 +252,17 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
         MQR_CHECK_HIP(hipEventCreate(&e1));
         MQR_CHECK_HIP(hipEventRecord(e0, s));
     }
-#define MQR_LAUNCH_INT(RR, GG)                                                                                \
-    hipLaunchKernelGGL((k_integrate_t<RR, GG>), dim3(grid), dim3(256), 0, s, list, counters, v->list_cap, t,  \
+#define MQR_LAUNCH_INT(RR, GG, SW)                                                                            \
+    hipLaunchKernelGGL((k_integrate_t<RR, GG, SW>), dim3(grid), dim3(256), 0, s, list, counters, v->list_cap, t, \
                        v->pool, v->voxel_size, depths, HW, H, W, fp, depth_frame, depth_scale, depth_max, sdf_trunc)
     if (v->R == 16 && v->kernel_variant == 0)
-        MQR_LAUNCH_INT(16, 8);
+        MQR_LAUNCH_INT(16, 8, false);
+    else if (v->R == 16 && v->kernel_variant == 5)
+        MQR_LAUNCH_INT(16, 8, true);
     else if (v->R == 16 && v->kernel_variant == 2)
-        MQR_LAUNCH_INT(16, 4);
+        MQR_LAUNCH_INT(16, 4, false);
     else if (v->R == 8 && v->kernel_variant != 1)
-        MQR_LAUNCH_INT(8, 2);
+        MQR_LAUNCH_INT(8, 2, false);
     else
         hipLaunchKernelGGL(k_integrate, dim3(grid), dim3(256), 0, s, list, counters, v->list_cap, t, v->pool, v->R,
                            v->voxel_size, depths, HW, H, W, fp, depth_frame, depth_scale, depth_max, sdf_trunc);

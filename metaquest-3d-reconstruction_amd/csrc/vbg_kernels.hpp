@@ -234,7 +234,18 @@ __device__ __forceinline__ float rcp_rn(float b) { return div_safe(b) ? div_rn_c
 // all frames of the batch, and evaluates Open3D's transform ((xs*e0 + ys*e1) + zs*e2) + e3 with
 // the z-independent partial product hoisted per frame -- the same float operations in the same
 // order, so the result is bit-identical to k_integrate.
-template <int R, int G>
+// XCD-aware list order: consecutive workgroups are dealt round-robin over the 8 XCDs, so give XCD
+// x (= L % 8) one contiguous 1/8 of the list.  List entries are appended in pixel order, so a
+// contiguous range is a spatially coherent set of blocks whose depth gathers share pixels, and
+// each XCD's L2 then holds its region of the batch's depth frames.  Bijective on [0, n);
+// affects speed only (placement is not a correctness assumption).
+__device__ __forceinline__ int64_t xcd_swizzle(int64_t L, int64_t n) {
+    const int64_t q = n >> 3, r = n & 7;
+    const int64_t x = L & 7, j = L >> 3;
+    return x * q + (x < r ? x : r) + j;
+}
+
+template <int R, int G, bool SWZ = false>
 __global__ __launch_bounds__(256) void k_integrate_t(const int32_t* __restrict__ list, const int* __restrict__ counters,
                                                      int64_t list_cap, Table t, float2* __restrict__ pool,
                                                      float voxel_size, const float* __restrict__ depths, int64_t HW,
@@ -252,7 +263,8 @@ __global__ __launch_bounds__(256) void k_integrate_t(const int32_t* __restrict__
     const float hm1 = (float)H - 1.0f, wm1 = (float)W - 1.0f;
     const int tid = threadIdx.x;
     const int xv = tid % R, yv = (tid / R) % R, z0 = tid / R2;
-    for (int64_t i = blockIdx.x; i < n; i += gridDim.x) {
+    for (int64_t L = blockIdx.x; L < n; L += gridDim.x) {
+        const int64_t i = SWZ ? xcd_swizzle(L, n) : L;
         const int32_t slot = list[i];
         const int buf = t.vals[slot];
         const uint32_t mask = __builtin_amdgcn_readfirstlane(t.mask[slot]);
