@@ -159,6 +159,12 @@ static int ensure_depth(mqr_vbg* v, int64_t floats) {
     return 0;
 }
 
+// Host twin of den_unsafe(): true unless 2^-60 <= |x| <= 2^60.
+static bool div_unsafe_host(float x) {
+    const float m = std::fabs(x);
+    return !(m >= 0x1p-60f && m <= 0x1p60f);
+}
+
 static const int64_t* dframe_dev(const mqr_vbg* v, int p) {
     return reinterpret_cast<const int64_t*>(v->d_fp[p] + v->fp_cap);
 }
@@ -252,21 +258,57 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
         MQR_CHECK_HIP(hipEventCreate(&e1));
         MQR_CHECK_HIP(hipEventRecord(e0, s));
     }
-#define MQR_LAUNCH_INT(RR, GG, SW)                                                                            \
-    hipLaunchKernelGGL((k_integrate_t<RR, GG, SW>), dim3(grid), dim3(256), 0, s, list, counters, v->list_cap, t, \
-                       v->pool, v->voxel_size, depths, HW, H, W, fp, depth_frame, depth_scale, depth_max, sdf_trunc)
-    if (v->R == 16 && v->kernel_variant == 0)
-        MQR_LAUNCH_INT(16, 8, false);
-    else if (v->R == 16 && v->kernel_variant == 5)
-        MQR_LAUNCH_INT(16, 8, true);
-    else if (v->R == 16 && v->kernel_variant == 2)
-        MQR_LAUNCH_INT(16, 4, false);
-    else if (v->R == 8 && v->kernel_variant != 1)
-        MQR_LAUNCH_INT(8, 2, false);
-    else
+    // the unguarded division core needs its constant denominators in range (see div_rn_core)
+    const bool fast_ok = !div_unsafe_host(sdf_trunc) && (depth_scale == 1.0f || !div_unsafe_host(depth_scale));
+#define MQR_LAUNCH_INT(RR, GG, SW, FAST, NT)                                                                      \
+    hipLaunchKernelGGL((k_integrate_t<RR, GG, SW, FAST, NT>), dim3(grid), dim3(NT), 0, s, list, counters,        \
+                       v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp, depth_frame, depth_scale,      \
+                       depth_max, sdf_trunc)
+#define MQR_LAUNCH_PK(RR, GG, NT)                                                                              \
+    hipLaunchKernelGGL((k_integrate_pk<RR, GG, NT>), dim3(grid), dim3(NT), 0, s, list, counters, v->list_cap, t, \
+                       v->pool, v->voxel_size, depths, HW, H, W, fp, depth_frame, depth_max, sdf_trunc)
+    const bool pk_ok = fast_ok && depth_scale == 1.0f;
+    // Variants (mqr_vbg_set_variant; all bit-identical, tests/test_gpu_numerics.py): 1 generic k_integrate;
+    // k_integrate_t<R, G, SWZ, FAST, NT> and packed-f32 k_integrate_pk<R, G, NT> configurations
+    // below, kept for A/B on new hardware (tools/ab_integrate.py).  FAST / packed fall back to the
+    // default when their preconditions on sdf_trunc / depth_scale do not hold.
+    int var = v->kernel_variant;
+    if ((var == 6 || var == 7 || var == 18 || var == 19) && !fast_ok) var = 0;
+    if ((var == 8 || var == 9 || (var >= 13 && var <= 16) || var == 20) && !pk_ok) var = 0;
+    if (v->R == 16 && var != 1) {
+        switch (var) {
+            case 2: MQR_LAUNCH_INT(16, 4, false, false, 256); break;
+            case 5: MQR_LAUNCH_INT(16, 8, true, false, 256); break;
+            case 6: MQR_LAUNCH_INT(16, 8, false, true, 256); break;
+            case 7: MQR_LAUNCH_INT(16, 4, false, true, 256); break;
+            case 8: MQR_LAUNCH_PK(16, 8, 256); break;
+            case 9: MQR_LAUNCH_PK(16, 4, 256); break;
+            case 10: MQR_LAUNCH_INT(16, 8, false, false, 512); break;
+            case 11: MQR_LAUNCH_INT(16, 8, false, false, 256); break;
+            case 12: MQR_LAUNCH_INT(16, 4, false, false, 1024); break;
+            case 13: MQR_LAUNCH_PK(16, 8, 512); break;
+            case 14: MQR_LAUNCH_PK(16, 4, 512); break;
+            case 15: MQR_LAUNCH_PK(16, 4, 1024); break;
+            case 16: MQR_LAUNCH_PK(16, 2, 1024); break;
+            case 17: MQR_LAUNCH_INT(16, 2, false, false, 1024); break;
+            case 18: MQR_LAUNCH_INT(16, 4, false, true, 512); break;
+            case 19: MQR_LAUNCH_INT(16, 8, false, true, 512); break;
+            case 20: MQR_LAUNCH_PK(16, 2, 512); break;
+            // default: 512 threads x 8 voxels, gathers in groups of 4 (fastest on MI355X)
+            default: MQR_LAUNCH_INT(16, 4, false, false, 512); break;
+        }
+    } else if (v->R == 8 && var != 1) {
+        if (var >= 8 && pk_ok)
+            MQR_LAUNCH_PK(8, 2, 256);
+        else if (var == 6)
+            MQR_LAUNCH_INT(8, 2, false, true, 256);
+        else
+            MQR_LAUNCH_INT(8, 2, false, false, 256);
+    } else
         hipLaunchKernelGGL(k_integrate, dim3(grid), dim3(256), 0, s, list, counters, v->list_cap, t, v->pool, v->R,
                            v->voxel_size, depths, HW, H, W, fp, depth_frame, depth_scale, depth_max, sdf_trunc);
 #undef MQR_LAUNCH_INT
+#undef MQR_LAUNCH_PK
     MQR_CHECK_HIP(hipGetLastError());
     if (v->profile) {
         MQR_CHECK_HIP(hipEventRecord(e1, s));

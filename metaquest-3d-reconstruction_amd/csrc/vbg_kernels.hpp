@@ -245,8 +245,113 @@ __device__ __forceinline__ int64_t xcd_swizzle(int64_t L, int64_t n) {
     return x * q + (x < r ? x : r) + j;
 }
 
-template <int R, int G, bool SWZ = false>
-__global__ __launch_bounds__(256) void k_integrate_t(const int32_t* __restrict__ list, const int* __restrict__ counters,
+// Operand checks of the unguarded division core, on the float bits (|x| = e):
+//   denominator / reciprocal: 2^-60 <= |x| <= 2^60 (also rejects 0, inf, NaN);
+//   numerator below a safe denominator: 0 or |x| >= 2^-60 (the clamp keeps it <= the denominator).
+__device__ __forceinline__ bool den_unsafe(float v) {
+    return ((__float_as_uint(v) & 0x7fffffffu) - 0x21800000u) > 0x3c000000u;
+}
+__device__ __forceinline__ bool num_unsafe(float v) {
+    return ((__float_as_uint(v) & 0x7fffffffu) - 1u) < 0x217fffffu;
+}
+
+// All frames of the batch over one thread's voxel column (see k_integrate_t).  EXACT = false
+// evaluates every division with the bare core and returns whether any operand left the range in
+// which the core is exact (den_unsafe / num_unsafe); the caller then discards the column results
+// of the whole block and re-runs it with EXACT = true.  The flag is data-independent of which
+// path ran, so the exact pass reproduces k_integrate bit for bit, and the fast pass has no
+// per-voxel branches around its divisions.
+template <int ZPER, int G, bool EXACT>
+__device__ __forceinline__ bool integrate_column(float2 (&tw)[ZPER], uint32_t& dirty, uint32_t mask,
+                                                 const float (&zs)[ZPER], float xs, float ys,
+                                                 const float* __restrict__ depths, int64_t HW, int W, float hm1,
+                                                 float wm1, const FrameParams* __restrict__ fps,
+                                                 const int64_t* __restrict__ depth_frame, float depth_scale,
+                                                 bool unit_scale, float depth_max, float sdf_trunc) {
+    bool bad = false;
+    uint32_t m = mask;
+    while (m) {
+        const int f = __builtin_ctz(m);
+        m &= m - 1;
+        const FrameParams& fp = fps[f];
+        const float* __restrict__ dep = depths + depth_frame[f] * HW;
+        const float ax = xs * fp.ext[0] + ys * fp.ext[1];
+        const float ay = xs * fp.ext[4] + ys * fp.ext[5];
+        const float az = xs * fp.ext[8] + ys * fp.ext[9];
+        // Groups of G voxels: project all, issue all G depth gathers (branch-free, out-of-image
+        // lanes read pixel 0 and are masked), then update -- G loads in flight per wave.
+#pragma unroll
+        for (int g = 0; g < ZPER; g += G) {
+            int pix[G];
+            float zcs[G];
+            bool in[G];
+#pragma unroll
+            for (int j = 0; j < G; ++j) {
+                const int k = g + j;
+                const float xc = (ax + zs[k] * fp.ext[2]) + fp.ext[3];
+                const float yc = (ay + zs[k] * fp.ext[6]) + fp.ext[7];
+                const float zc = (az + zs[k] * fp.ext[10]) + fp.ext[11];
+                float inv_z;
+                if (EXACT) {
+                    inv_z = rcp_rn(zc);
+                } else {
+                    inv_z = div_rn_core(1.0f, zc);
+                    bad |= den_unsafe(zc);
+                }
+                const float u = fp.fx * xc * inv_z + fp.cx;
+                const float v = fp.fy * yc * inv_z + fp.cy;
+                in[j] = v >= 0 && u >= 0 && v <= hm1 && u <= wm1;
+                const int ui = (int)(in[j] ? u : 0.f), vi = (int)(in[j] ? v : 0.f);
+                pix[j] = vi * W + ui;
+                zcs[j] = zc;
+            }
+            float dv[G];
+#pragma unroll
+            for (int j = 0; j < G; ++j) dv[j] = dep[pix[j]];
+#pragma unroll
+            for (int j = 0; j < G; ++j) {
+                const int k = g + j;
+                float d;
+                if (unit_scale) {
+                    d = dv[j];
+                } else if (EXACT) {
+                    d = div_rn(dv[j], depth_scale);
+                } else {
+                    d = div_rn_core(dv[j], depth_scale);
+                    bad |= in[j] && dv[j] != 0.0f && den_unsafe(dv[j]);  // 0 / s = +0 in the core
+                }
+                const float zc = zcs[j];
+                float sdf = d - zc;
+                if (!in[j] || d <= 0 || d > depth_max || zc <= 0 || sdf < -sdf_trunc) continue;
+                sdf = sdf < sdf_trunc ? sdf : sdf_trunc;
+                const float wgt = tw[k].y;
+                float inv_wsum;
+                if (EXACT) {
+                    sdf = div_rn(sdf, sdf_trunc);
+                    inv_wsum = rcp_rn(wgt + 1);
+                } else {
+                    bad |= num_unsafe(sdf) || den_unsafe(wgt + 1);
+                    sdf = div_rn_core(sdf, sdf_trunc);
+                    inv_wsum = div_rn_core(1.0f, wgt + 1);
+                }
+                tw[k].x = (wgt * tw[k].x + sdf) * inv_wsum;
+                tw[k].y = wgt + 1;
+                dirty |= 1u << k;
+            }
+        }
+    }
+    return bad;
+}
+
+// Integrate, R known at compile time (R = 16 / 8): thread t owns the voxel column (x, y) =
+// (t % R, t / R % R) for z in its z-range, keeps those voxels' (tsdf, weight) in registers for
+// all frames of the batch, and evaluates Open3D's transform ((xs*e0 + ys*e1) + zs*e2) + e3 with
+// the z-independent partial product hoisted per frame -- the same float operations in the same
+// order, so the result is bit-identical to k_integrate.  FAST: unguarded division core with a
+// block-level exact re-run when any operand is out of its range (host guarantees sdf_trunc and
+// depth_scale are in range).
+template <int R, int G, bool SWZ = false, bool FAST = false, int NT = 256>
+__global__ __launch_bounds__(NT) void k_integrate_t(const int32_t* __restrict__ list, const int* __restrict__ counters,
                                                      int64_t list_cap, Table t, float2* __restrict__ pool,
                                                      float voxel_size, const float* __restrict__ depths, int64_t HW,
                                                      int H, int W, const FrameParams* __restrict__ fps,
@@ -254,9 +359,9 @@ __global__ __launch_bounds__(256) void k_integrate_t(const int32_t* __restrict__
                                                      float depth_max, float sdf_trunc) {
     constexpr int R2 = R * R;
     constexpr int R3 = R2 * R;
-    constexpr int ZPER = R3 / 256;         // voxels per thread (16 at R=16, 2 at R=8)
-    constexpr int ZSTEP = 256 / R2;        // z stride between a thread's voxels (1 at R=16, 4 at R=8)
-    static_assert(R3 % 256 == 0, "R^3 must be a multiple of 256");
+    constexpr int ZPER = R3 / NT;          // voxels per thread (16 at R=16, NT=256; 2 at R=8)
+    constexpr int ZSTEP = NT / R2;         // z stride between a thread's voxels (1 at R=16, NT=256)
+    static_assert(R3 % NT == 0 && NT % R2 == 0, "NT must divide R^3 and be a multiple of R^2");
     static_assert(ZPER % G == 0, "group size must divide the voxels per thread");
     const bool unit_scale = depth_scale == 1.0f;  // d / 1 == d exactly: skip the division
     const int64_t n = min((int64_t)counters[kListCount], list_cap);
@@ -276,65 +381,210 @@ __global__ __launch_bounds__(256) void k_integrate_t(const int32_t* __restrict__
             float zs[ZPER];
 #pragma unroll
             for (int k = 0; k < ZPER; ++k) {
-                tw[k] = vox[k * 256 + tid];
+                tw[k] = vox[k * NT + tid];
                 zs[k] = (float)(zb * R + z0 + k * ZSTEP) * voxel_size;
             }
             const float xs = (float)(xb * R + xv) * voxel_size;
             const float ys = (float)(yb * R + yv) * voxel_size;
             uint32_t dirty = 0;
-            uint32_t m = mask;
-            while (m) {
-                const int f = __builtin_ctz(m);
-                m &= m - 1;
-                const FrameParams& fp = fps[f];
-                const float* __restrict__ dep = depths + depth_frame[f] * HW;
-                const float ax = xs * fp.ext[0] + ys * fp.ext[1];
-                const float ay = xs * fp.ext[4] + ys * fp.ext[5];
-                const float az = xs * fp.ext[8] + ys * fp.ext[9];
-                // Groups of G voxels: project all, issue all G depth gathers (branch-free, out-of-image
-                // lanes read pixel 0 and are masked), then update -- G loads in flight per wave.
+            const bool bad = integrate_column<ZPER, G, !FAST>(tw, dirty, mask, zs, xs, ys, depths, HW, W, hm1, wm1,
+                                                           fps, depth_frame, depth_scale, unit_scale, depth_max,
+                                                           sdf_trunc);
+            if (FAST && __syncthreads_or(bad)) {  // block-uniform: redo this block exactly
 #pragma unroll
-                for (int g = 0; g < ZPER; g += G) {
-                    int pix[G];
-                    float zcs[G];
-                    bool in[G];
-#pragma unroll
-                    for (int j = 0; j < G; ++j) {
-                        const int k = g + j;
-                        const float xc = (ax + zs[k] * fp.ext[2]) + fp.ext[3];
-                        const float yc = (ay + zs[k] * fp.ext[6]) + fp.ext[7];
-                        const float zc = (az + zs[k] * fp.ext[10]) + fp.ext[11];
-                        const float inv_z = rcp_rn(zc);
-                        const float u = fp.fx * xc * inv_z + fp.cx;
-                        const float v = fp.fy * yc * inv_z + fp.cy;
-                        in[j] = v >= 0 && u >= 0 && v <= hm1 && u <= wm1;
-                        const int ui = (int)(in[j] ? u : 0.f), vi = (int)(in[j] ? v : 0.f);
-                        pix[j] = vi * W + ui;
-                        zcs[j] = zc;
-                    }
-                    float dv[G];
-#pragma unroll
-                    for (int j = 0; j < G; ++j) dv[j] = dep[pix[j]];
-#pragma unroll
-                    for (int j = 0; j < G; ++j) {
-                        const int k = g + j;
-                        const float d = unit_scale ? dv[j] : div_rn(dv[j], depth_scale);
-                        const float zc = zcs[j];
-                        float sdf = d - zc;
-                        if (!in[j] || d <= 0 || d > depth_max || zc <= 0 || sdf < -sdf_trunc) continue;
-                        sdf = sdf < sdf_trunc ? sdf : sdf_trunc;
-                        sdf = div_rn(sdf, sdf_trunc);
-                        const float wgt = tw[k].y;
-                        const float inv_wsum = rcp_rn(wgt + 1);
-                        tw[k].x = (wgt * tw[k].x + sdf) * inv_wsum;
-                        tw[k].y = wgt + 1;
-                        dirty |= 1u << k;
-                    }
-                }
+                for (int k = 0; k < ZPER; ++k) tw[k] = vox[k * NT + tid];
+                dirty = 0;
+                integrate_column<ZPER, G, true>(tw, dirty, mask, zs, xs, ys, depths, HW, W, hm1, wm1, fps,
+                                                depth_frame, depth_scale, unit_scale, depth_max, sdf_trunc);
             }
 #pragma unroll
             for (int k = 0; k < ZPER; ++k)
-                if (dirty & (1u << k)) vox[k * 256 + tid] = tw[k];
+                if (dirty & (1u << k)) vox[k * NT + tid] = tw[k];
+        }
+        __syncthreads();
+        if (tid == 0) t.mask[slot] = 0;
+    }
+}
+
+// ---- packed-f32 integrate (v_pk_mul/add/fma_f32: two voxels per VALU instruction) ------------
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f2v fma2(f2v a, f2v b, f2v c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f2v splat2(float x) { return f2v{x, x}; }
+
+// 1 / b through the core sequence (q0 = 1 * y1 = y1), elementwise; exact for 2^-60 <= |b| <= 2^60.
+__device__ __forceinline__ f2v rcp_core2(f2v b) {
+    const f2v one = splat2(1.0f);
+    const f2v y0 = {__builtin_amdgcn_rcpf(b.x), __builtin_amdgcn_rcpf(b.y)};
+    const f2v nb = -b;
+    const f2v y1 = fma2(fma2(nb, y0, one), y0, y0);
+    const f2v q1 = fma2(fma2(nb, y1, one), y1, y1);
+    return fma2(fma2(nb, q1, one), y1, q1);
+}
+
+// a / t for a launch-constant t with its refined reciprocal y1t precomputed (same core sequence).
+__device__ __forceinline__ f2v div_const2(f2v a, f2v nbt, f2v y1t) {
+    const f2v q0 = a * y1t;
+    const f2v q1 = fma2(fma2(nbt, q0, a), y1t, q0);
+    return fma2(fma2(nbt, q1, a), y1t, q1);
+}
+
+// Fast pass of one column with the (tsdf, weight) of voxels (2q, 2q+1) packed in T[q], Wt[q].
+// Preconditions (checked by the caller): depth_scale == 1, sdf_trunc in [2^-60, 2^60], every
+// weight in [0, 2^59].  Returns true if some |zc| left [2^-36, 2^60]; the caller then re-runs the
+// block exactly.  Inside that range the core divisions are exact: 1/zc directly, and the numerator
+// sdf = d - zc is 0 or >= 2^-60 in magnitude (zc >= 2^-36 => the difference is a multiple of
+// 2^-60 or at least zc / 2), so the result is bit-identical to integrate_column<.., true>.
+template <int ZPER, int G>
+__device__ __forceinline__ bool integrate_column_pk(f2v (&T)[ZPER / 2], f2v (&Wt)[ZPER / 2],
+                                                    uint32_t& dirty, uint32_t mask,
+                                                    const f2v (&zs2)[ZPER / 2], float xs, float ys,
+                                                    const float* __restrict__ depths, int64_t HW, int W,
+                                                    float hm1, float wm1, const FrameParams* __restrict__ fps,
+                                                    const int64_t* __restrict__ depth_frame, float depth_max,
+                                                    float sdf_trunc) {
+    const float y0t = __builtin_amdgcn_rcpf(sdf_trunc);
+    const float y1t_s = __builtin_fmaf(__builtin_fmaf(-sdf_trunc, y0t, 1.0f), y0t, y0t);
+    const f2v y1t = splat2(y1t_s), nbt = splat2(-sdf_trunc), one = splat2(1.0f);
+    float zmin = 0x1p100f, zmax = 0.0f;
+    uint32_t m = mask;
+    while (m) {
+        const int f = __builtin_ctz(m);
+        m &= m - 1;
+        const FrameParams& fp = fps[f];
+        const float* __restrict__ dep = depths + depth_frame[f] * HW;
+        const f2v ax = splat2(xs * fp.ext[0] + ys * fp.ext[1]);
+        const f2v ay = splat2(xs * fp.ext[4] + ys * fp.ext[5]);
+        const f2v az = splat2(xs * fp.ext[8] + ys * fp.ext[9]);
+        const f2v e2 = splat2(fp.ext[2]), e3 = splat2(fp.ext[3]), e6 = splat2(fp.ext[6]);
+        const f2v e7 = splat2(fp.ext[7]), e10 = splat2(fp.ext[10]), e11 = splat2(fp.ext[11]);
+        const f2v fx = splat2(fp.fx), fy = splat2(fp.fy), cx = splat2(fp.cx), cy = splat2(fp.cy);
+#pragma unroll
+        for (int g = 0; g < ZPER; g += G) {
+            constexpr int GP = G / 2;
+            int pix[G];
+            bool in[G];
+            f2v zc[GP];
+#pragma unroll
+            for (int q = 0; q < GP; ++q) {
+                const f2v zz = zs2[g / 2 + q];
+                const f2v xc = (ax + zz * e2) + e3;
+                const f2v yc = (ay + zz * e6) + e7;
+                zc[q] = (az + zz * e10) + e11;
+                zmin = fminf(zmin, fminf(fabsf(zc[q].x), fabsf(zc[q].y)));
+                zmax = fmaxf(zmax, fmaxf(fabsf(zc[q].x), fabsf(zc[q].y)));
+                const f2v inv = rcp_core2(zc[q]);
+                const f2v u = fx * xc * inv + cx;
+                const f2v v = fy * yc * inv + cy;
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    const float ue = e ? u.y : u.x, ve = e ? v.y : v.x;
+                    const bool ok = ve >= 0 && ue >= 0 && ve <= hm1 && ue <= wm1;
+                    in[2 * q + e] = ok;
+                    pix[2 * q + e] = (int)(ok ? ve : 0.f) * W + (int)(ok ? ue : 0.f);
+                }
+            }
+            float dv[G];
+#pragma unroll
+            for (int j = 0; j < G; ++j) dv[j] = dep[pix[j]];
+#pragma unroll
+            for (int q = 0; q < GP; ++q) {
+                const int qq = g / 2 + q;
+                const f2v d = {dv[2 * q], dv[2 * q + 1]};
+                const f2v sdf = d - zc[q];
+                bool up[2];
+                f2v s;
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    const float de = e ? d.y : d.x, ze = e ? zc[q].y : zc[q].x, se = e ? sdf.y : sdf.x;
+                    up[e] = !(!in[2 * q + e] || de <= 0 || de > depth_max || ze <= 0 || se < -sdf_trunc);
+                    s[e] = se < sdf_trunc ? se : sdf_trunc;
+                }
+                const f2v sn = div_const2(s, nbt, y1t);
+                const f2v wp = Wt[qq] + one;
+                const f2v nt = (Wt[qq] * T[qq] + sn) * rcp_core2(wp);
+                T[qq].x = up[0] ? nt.x : T[qq].x;
+                T[qq].y = up[1] ? nt.y : T[qq].y;
+                Wt[qq].x = up[0] ? wp.x : Wt[qq].x;
+                Wt[qq].y = up[1] ? wp.y : Wt[qq].y;
+                dirty |= (up[0] ? 1u << (2 * qq) : 0u) | (up[1] ? 2u << (2 * qq) : 0u);
+            }
+        }
+    }
+    return !(zmin >= 0x1p-36f) || zmax > 0x1p60f;
+}
+
+// Packed-f32 integrate (R = 16 / 8, unit depth scale): fast pass with exact block re-run, exact
+// pass directly for blocks whose weights are outside [0, 2^59] (imported volumes).
+template <int R, int G, int NT = 256>
+__global__ __launch_bounds__(NT) void k_integrate_pk(const int32_t* __restrict__ list,
+                                                      const int* __restrict__ counters, int64_t list_cap, Table t,
+                                                      float2* __restrict__ pool, float voxel_size,
+                                                      const float* __restrict__ depths, int64_t HW, int H, int W,
+                                                      const FrameParams* __restrict__ fps,
+                                                      const int64_t* __restrict__ depth_frame, float depth_max,
+                                                      float sdf_trunc) {
+    constexpr int R2 = R * R;
+    constexpr int R3 = R2 * R;
+    constexpr int ZPER = R3 / NT;
+    constexpr int NP = ZPER / 2;
+    constexpr int ZSTEP = NT / R2;
+    static_assert(R3 % NT == 0 && NT % R2 == 0, "NT must divide R^3 and be a multiple of R^2");
+    static_assert(ZPER % G == 0 && G % 2 == 0, "group size must be even and divide the voxels per thread");
+    const int64_t n = min((int64_t)counters[kListCount], list_cap);
+    const float hm1 = (float)H - 1.0f, wm1 = (float)W - 1.0f;
+    const int tid = threadIdx.x;
+    const int xv = tid % R, yv = (tid / R) % R, z0 = tid / R2;
+    for (int64_t i = blockIdx.x; i < n; i += gridDim.x) {
+        const int32_t slot = list[i];
+        const int buf = t.vals[slot];
+        const uint32_t mask = __builtin_amdgcn_readfirstlane(t.mask[slot]);
+        int xb, yb, zb;
+        unpack_key(t.keys[slot], xb, yb, zb);
+        if (buf >= 0) {
+            float2* vox = pool + (int64_t)buf * R3;
+            float2 tw[ZPER];
+            float zs[ZPER];
+            bool wbad = false;
+#pragma unroll
+            for (int k = 0; k < ZPER; ++k) {
+                tw[k] = vox[k * NT + tid];
+                zs[k] = (float)(zb * R + z0 + k * ZSTEP) * voxel_size;
+                wbad |= !(tw[k].y >= 0.0f && tw[k].y <= 0x1p59f);
+            }
+            const float xs = (float)(xb * R + xv) * voxel_size;
+            const float ys = (float)(yb * R + yv) * voxel_size;
+            uint32_t dirty = 0;
+            bool exact = __syncthreads_or(wbad);
+            if (!exact) {
+                f2v T[NP], Wt[NP], zs2[NP];
+#pragma unroll
+                for (int q = 0; q < NP; ++q) {
+                    T[q] = f2v{tw[2 * q].x, tw[2 * q + 1].x};
+                    Wt[q] = f2v{tw[2 * q].y, tw[2 * q + 1].y};
+                    zs2[q] = f2v{zs[2 * q], zs[2 * q + 1]};
+                }
+                const bool zbad = integrate_column_pk<ZPER, G>(T, Wt, dirty, mask, zs2, xs, ys, depths, HW, W, hm1,
+                                                            wm1, fps, depth_frame, depth_max, sdf_trunc);
+                exact = __syncthreads_or(zbad);
+                if (!exact) {
+#pragma unroll
+                    for (int q = 0; q < NP; ++q) {
+                        tw[2 * q] = make_float2(T[q].x, Wt[q].x);
+                        tw[2 * q + 1] = make_float2(T[q].y, Wt[q].y);
+                    }
+                } else {
+#pragma unroll
+                    for (int k = 0; k < ZPER; ++k) tw[k] = vox[k * NT + tid];
+                    dirty = 0;
+                }
+            }
+            if (exact)
+                integrate_column<ZPER, G, true>(tw, dirty, mask, zs, xs, ys, depths, HW, W, hm1, wm1, fps,
+                                                depth_frame, 1.0f, true, depth_max, sdf_trunc);
+#pragma unroll
+            for (int k = 0; k < ZPER; ++k)
+                if (dirty & (1u << k)) vox[k * NT + tid] = tw[k];
         }
         __syncthreads();
         if (tid == 0) t.mask[slot] = 0;

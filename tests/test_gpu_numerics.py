@@ -35,23 +35,56 @@ def test_division_shortcut_exact(b):
         assert mm == 0, f"b={b}: {mm} mismatches, first bit pattern {first:#x}"
 
 
+INTEGRATE_VARIANTS = {16: (0, 2, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 0x100, 0x106, 0x108),
+                      8: (0, 6, 8, 0x101)}
+
+
 def test_specialised_integrate_equals_generic():
+    """Every integrate-kernel variant (R-specialised, packed f32, 256/512/1024 threads, fast
+    division with exact re-run, serial or pipelined) equals the generic kernel (variant 1) bit for bit."""
     from gpu_helpers import compare_volumes
     from mqr import _lib, synthetic
     from mqr.vbg import VoxelBlockGrid
     seq = synthetic.make_sequence("room", n=20, height=240, width=320, f=262.5, noise=True, seed=21)
+    for R, variants in INTEGRATE_VARIANTS.items():
+        out = {}
+        for variant in (1,) + variants:
+            v = VoxelBlockGrid(voxel_size=0.01, block_resolution=R, block_count=64)
+            _lib.call("mqr_vbg_set_variant", v.handle, variant)
+            v.integrate_frames(seq["depth"], seq["K"], seq["T_wc"], depth_scale=1.0, depth_max=4.0,
+                               trunc_voxel_multiplier=10.0)
+            out[variant] = v.export()
+        for variant in variants:
+            assert compare_volumes(out[1], out[variant], 0.0) == 0.0, (R, variant)
+
+
+def test_fast_integrate_exact_fallback():
+    """Operands outside the division core's exact range (a tiny non-zero depth read in millimetres,
+    weights near 2^61 from an imported volume) make the fast kernel redo the block exactly."""
+    from gpu_helpers import compare_volumes
+    from mqr import _lib, synthetic
+    from mqr.vbg import VoxelBlockGrid
+    seq = synthetic.make_sequence("room", n=8, height=240, width=320, f=262.5, noise=True, seed=5)
+    depth_mm = [np.asarray(d, np.float32) * 1000.0 for d in seq["depth"]]
+    for d in depth_mm:
+        d[::7, ::5] = np.float32(1e-30)   # in-image, > 0, below 2^-60 -> fallback
     out = []
-    for R, variant in ((16, 0), (16, 1), (8, 0), (8, 1), (16, 2), (16, 0x100), (8, 0x101)):
+    for R, variant in ((16, 1), (16, 0), (16, 6), (16, 7), (16, 18), (8, 1), (8, 6)):
         v = VoxelBlockGrid(voxel_size=0.01, block_resolution=R, block_count=64)
         _lib.call("mqr_vbg_set_variant", v.handle, variant)
-        v.integrate_frames(seq["depth"], seq["K"], seq["T_wc"], depth_scale=1.0, depth_max=4.0,
+        v.integrate_frames(depth_mm[:4], seq["K"][:4], seq["T_wc"][:4], depth_scale=1000.0, depth_max=4.0,
+                           trunc_voxel_multiplier=10.0)
+        keys, tsdf, wgt = v.export()
+        wgt = wgt.copy()
+        wgt[keys.sum(axis=1) % 3 == 0] = np.float32(2.0 ** 61)   # w + 1 out of range (key-chosen blocks)
+        v.reset()
+        v.import_blocks(keys, tsdf, wgt)
+        v.integrate_frames(depth_mm[4:], seq["K"][4:], seq["T_wc"][4:], depth_scale=1000.0, depth_max=4.0,
                            trunc_voxel_multiplier=10.0)
         out.append(v.export())
-    assert compare_volumes(out[0], out[1], 0.0) == 0.0
-    assert compare_volumes(out[2], out[3], 0.0) == 0.0
-    assert compare_volumes(out[0], out[4], 0.0) == 0.0
-    assert compare_volumes(out[0], out[5], 0.0) == 0.0
-    assert compare_volumes(out[2], out[6], 0.0) == 0.0
+    for i in (1, 2, 3, 4):
+        assert compare_volumes(out[0], out[i], 0.0) == 0.0
+    assert compare_volumes(out[5], out[6], 0.0) == 0.0
 
 
 def test_division_core_on_positive_zero():
@@ -59,3 +92,32 @@ def test_division_core_on_positive_zero():
     for b in (0.05, 1.0, 3.0):
         mm, _ = _check(2, b, 0.0, 2.0 ** -149)  # bit pattern 0 only
         assert mm == 0
+
+
+def test_packed_integrate_exact_fallback():
+    """Packed kernel (variants 8/9): a camera at the origin looking at a 1 cm plane touches the block
+    holding voxels with zc == 0 (block re-run), imported weights of 2^61 force the exact pass."""
+    from gpu_helpers import compare_volumes
+    from mqr import _lib, synthetic
+    from mqr.vbg import VoxelBlockGrid
+    seq = synthetic.make_sequence("room", n=6, height=240, width=320, f=262.5, noise=True, seed=9)
+    near = np.full((240, 320), 0.01, np.float32)
+    depths = [near] + [np.asarray(d, np.float32) for d in seq["depth"]]
+    Ks = np.concatenate([seq["K"][:1], seq["K"]])
+    Ts = np.concatenate([np.eye(4)[None], seq["T_wc"]])
+    out = []
+    for R, variant in ((16, 1), (16, 8), (16, 9), (16, 14), (16, 15), (8, 1), (8, 8)):
+        v = VoxelBlockGrid(voxel_size=0.005, block_resolution=R, block_count=64)
+        _lib.call("mqr_vbg_set_variant", v.handle, variant)
+        v.integrate_frames(depths[:4], Ks[:4], Ts[:4], depth_scale=1.0, depth_max=4.0, trunc_voxel_multiplier=10.0)
+        keys, tsdf, wgt = v.export()
+        assert (keys == 0).all(axis=1).any(), "origin block not touched"
+        wgt = wgt.copy()
+        wgt[keys.sum(axis=1) % 3 == 1] = np.float32(2.0 ** 61)
+        v.reset()
+        v.import_blocks(keys, tsdf, wgt)
+        v.integrate_frames(depths[3:], Ks[3:], Ts[3:], depth_scale=1.0, depth_max=4.0, trunc_voxel_multiplier=10.0)
+        out.append(v.export())
+    for i in (1, 2, 3, 4):
+        assert compare_volumes(out[0], out[i], 0.0) == 0.0
+    assert compare_volumes(out[5], out[6], 0.0) == 0.0

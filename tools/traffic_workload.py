@@ -13,6 +13,11 @@ sys.path.insert(0, ROOT)
 
 
 def main():
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--variant", type=int, default=-1, help="integrate kernel variant (-1 = library default)")
+    ap.add_argument("--out", default="pmc")
+    a = ap.parse_args()
     import numpy as np
     import torch
     from bench import _DevPtr
@@ -24,6 +29,9 @@ def main():
     K, T = seq["K"].astype(np.float64), seq["T_wc"].astype(np.float64)
     torch.cuda.synchronize()
     vbg = VoxelBlockGrid(voxel_size=0.005, block_resolution=16, block_count=40000, device=0)
+    if a.variant >= 0:
+        from mqr import _lib
+        _lib.call("mqr_vbg_set_variant", vbg.handle, a.variant)
     vbg.profile(True)
     vbg.integrate_frames((_DevPtr(d.data_ptr()), B, H, W), K, T, depth_scale=1.0, depth_max=4.0,
                          trunc_voxel_multiplier=10.0)
@@ -39,8 +47,10 @@ def main():
             "frame_blocks": st["frame_blocks"], "frames": st["frames"], "H": H, "W": W,
             "alg_bytes_total": 16 * R3 * st["union_blocks"] + 4 * H * W * st["frames"] + 16 * st["frame_blocks"],
             "pack_blocks": U, "pack_read_bytes": U * R3 * 8, "pack_write_bytes": U * R3 * 8}
-    os.makedirs(os.path.join(ROOT, "gpurun_out", "pmc"), exist_ok=True)
-    with open(os.path.join(ROOT, "gpurun_out", "pmc", "workload.json"), "w") as f:
+    info["variant"] = a.variant
+    info["voxel_frames_per_launch"] = R3 * st["frame_blocks"] / max(st["integrate_launches"], 1)
+    os.makedirs(os.path.join(ROOT, "gpurun_out", a.out), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", a.out, "workload.json"), "w") as f:
         json.dump(info, f)
     print(json.dumps(info))
 
