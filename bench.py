@@ -48,7 +48,12 @@ def parse():
     ap.add_argument("--extract-threshold", type=float, default=1.5)
     ap.add_argument("--extract-reps", type=int, default=3)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu1-seconds", type=float, default=8.0, help="bounded 1-thread CPU sample")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--conf-range", type=int, default=10, help="C3 confidence window r")
+    ap.add_argument("--conf-depth-max", type=float, default=4.0)
+    ap.add_argument("--conf-error", type=float, default=0.08)
+    ap.add_argument("--no-extras", action="store_true", help="skip confidence / copy-peak / host-input legs")
     return ap.parse_args()
 
 
@@ -66,6 +71,58 @@ def extract_ms(vbg, thr, reps):
         _lib.call("mqr_geom_free", g)
     times.sort()
     return times[len(times) // 2], counts
+
+
+def copy_peak_gbs(device, nbytes=2 << 30, reps=5):
+    """Achievable HBM rate on this box: device-to-device copy (read + write bytes) / time."""
+    import torch
+    a = torch.empty(nbytes // 4, dtype=torch.float32, device=device)
+    b = torch.empty_like(a)
+    a.fill_(1.0)
+    b.copy_(a)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    best = None
+    for _ in range(reps):
+        e0.record()
+        b.copy_(a)
+        e1.record()
+        e1.synchronize()
+        ms = e0.elapsed_time(e1)
+        best = ms if best is None else min(best, ms)
+    del a, b
+    return 2 * nbytes / (best * 1e-3) / 1e9
+
+
+def confidence_leg(depth_t, K, T_wc, args, device):
+    """C3: depth-confidence maps of every frame of the sequence (window r), device-resident
+    inputs/outputs, median of 3; algorithmic bytes per ref frame = 4HW(1 + n_nb) + 12HW."""
+    import numpy as np
+    import torch
+    from mqr import _lib
+    B, H, W = depth_t.shape
+    T_cw = np.linalg.inv(T_wc).astype(np.float32)
+    T_cw_inv = np.linalg.inv(T_cw).astype(np.float32)
+    K32 = np.ascontiguousarray(K, dtype=np.float32).reshape(B, 9)
+    conf = torch.empty((B, H, W), dtype=torch.float64, device=device)
+    valid = torch.empty((B, H, W), dtype=torch.int32, device=device)
+    times = []
+    for _ in range(3):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        _lib.call("mqr_confidence", int(device.index or 0), ctypes.c_void_p(depth_t.data_ptr()), 1, B, H, W,
+                  _lib.ptr(K32, _lib._f32p), _lib.ptr(np.ascontiguousarray(T_cw.reshape(B, 16)), _lib._f32p),
+                  _lib.ptr(np.ascontiguousarray(T_cw_inv.reshape(B, 16)), _lib._f32p), None, 0, B,
+                  int(args.conf_range), float(args.conf_depth_max), float(args.conf_error),
+                  ctypes.c_void_p(conf.data_ptr()), ctypes.c_void_p(valid.data_ptr()), 1)
+        torch.cuda.synchronize()
+        times.append(time.perf_counter() - t0)
+    times.sort()
+    t = times[1]
+    n_nb = sum(min(B, i + args.conf_range + 1) - max(0, i - args.conf_range) - 1 for i in range(B))
+    alg = 4 * H * W * (B + n_nb) + 12 * H * W * B
+    return {"ref_frames": B, "window_r": args.conf_range, "ms": t * 1e3, "ref_frames_per_s": B / t,
+            "alg_gbs": alg / t / 1e9, "depth_max": args.conf_depth_max, "error_threshold": args.conf_error,
+            "note": "mqr_confidence over all frames, device-resident depth in/out, wall time of the call"}
 
 
 def pmc_traffic(H, W, frames):
@@ -100,9 +157,21 @@ def cpu_baseline(seq_host, K, T, args):
         ref.integrate_frame(seq_host[n], K[n], T[n], 1.0, args.depth_max, args.trunc)
         n += 1
     dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "frames/s", "cores": cores, "kind": "port",
-            "sample": f"first {n} of the {len(seq_host)} frames, touch+integrate per frame (oracle/mqr_oracle.c, "
-                      f"OpenMP over blocks), {dt:.1f} s"}
+    out = {"value": n / dt, "unit": "frames/s", "cores": cores, "kind": "port",
+           "sample": f"first {n} of the {len(seq_host)} frames, touch+integrate per frame (oracle/mqr_oracle.c, "
+                     f"OpenMP over blocks), {dt:.1f} s"}
+    if args.cpu1_seconds > 0:
+        oracle.set_threads(1)
+        ref1 = oracle.OracleVBG(args.voxel, args.block_resolution, args.block_count)
+        t0 = time.perf_counter()
+        n1 = 0
+        while n1 < len(seq_host) and time.perf_counter() - t0 < args.cpu1_seconds:
+            ref1.integrate_frame(seq_host[n1], K[n1], T[n1], 1.0, args.depth_max, args.trunc)
+            n1 += 1
+        dt1 = time.perf_counter() - t0
+        out["one_thread"] = {"value": n1 / dt1, "frames": n1, "seconds": dt1}
+        oracle.set_threads(cores)
+    return out
 
 
 def main():
@@ -165,6 +234,7 @@ def main():
         elapsed = float(e.item())
 
     blocks = vbg.size()
+    R3_ = args.block_resolution ** 3
     ext_ms, (nv, nt) = (None, (0, 0))
     if rank == 0:
         ext_ms, (nv, nt) = extract_ms(vbg, args.extract_threshold, args.extract_reps)
@@ -174,6 +244,24 @@ def main():
     launches = max(st["integrate_launches"], 1)
     avg_ms = st["integrate_ms"] / launches
     achieved = alg_bytes / launches / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+
+    extras = {}
+    if rank == 0 and not args.no_extras:
+        dev = torch.device("cuda", local)
+        extras["hbm_copy_gbs"] = copy_peak_gbs(dev)
+        extras["confidence"] = confidence_leg(depth_t, K, T, args, dev)
+        # PCIe-inclusive: the same step from host (numpy) frames, H2D inside integrate_frames
+        host = depth_t.cpu().numpy()
+        vbg.reset()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        vbg.integrate_frames(host, K, T, depth_scale=1.0, depth_max=args.depth_max,
+                             trunc_voxel_multiplier=args.trunc)
+        torch.cuda.synchronize()
+        extras["host_input_frames_per_s"] = B / (time.perf_counter() - t0)
+    ext_alg = None
+    if ext_ms:
+        ext_alg = (8 * R3_ * blocks + 4 * 27 * blocks + 24 * nv + 12 * nt) / (ext_ms * 1e-3) / 1e9
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -204,8 +292,13 @@ def main():
                        "parallelism": f"frame-shard x{world}" + (" + RCCL reduce" if world > 1 else "")},
             "extract_ms": ext_ms,
             "extract": {"weight_threshold": args.extract_threshold, "vertices": nv, "triangles": nt,
-                        "blocks": blocks, "note": "device-resident extract_triangle_mesh, median of reps"},
+                        "blocks": blocks, "alg_gbs": ext_alg,
+                        "note": "device-resident extract_triangle_mesh, median of reps; alg bytes = "
+                                "8R^3 N + 108 N + 24 V + 12 T"},
+            "confidence": extras.get("confidence"),
+            "host_input_frames_per_s": extras.get("host_input_frames_per_s"),
             "roofline": {"bound": "hbm", "kernel": "k_integrate", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "peak_measured_copy": extras.get("hbm_copy_gbs"),
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_source": traffic_src,
                          "alg_bytes_per_launch": alg_bytes / launches, "avg_launch_ms": avg_ms,
