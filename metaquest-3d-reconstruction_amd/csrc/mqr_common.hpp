@@ -129,8 +129,11 @@ struct mqr_vbg {
     int fp_cap = 0;
     float* d_depth[2] = {nullptr, nullptr};          // staging for host depth frames
     int64_t depth_cap = 0;                           // floats per parity
+    void* ex_scratch = nullptr;                      // extraction scratch (grow-only, extract.hip)
+    size_t ex_scratch_bytes = 0;
+    int64_t* h_ex = nullptr;                         // pinned totals of the extraction scans
 
-    int kernel_variant = 0;    // 0 = R-specialised integrate, 1 = generic, 2 = G=4 (A/B)
+    int kernel_variant = 0;    // integrate kernel configuration (launch_integrate in vbg.hip), 1 = generic
     bool pipelined = true;     // overlap touch(b+1) with integrate(b)
     // profiling
     bool profile = false;

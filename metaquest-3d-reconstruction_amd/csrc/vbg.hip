@@ -476,6 +476,8 @@ int mqr_vbg_destroy(mqr_vbg* v) {
     }
     if (v->counters) (void)hipFree(v->counters);
     if (v->h_counters) (void)hipHostFree(v->h_counters);
+    if (v->ex_scratch) (void)hipFree(v->ex_scratch);
+    if (v->h_ex) (void)hipHostFree(v->h_ex);
     if (v->stream) (void)hipStreamDestroy(v->stream);
     if (v->stream2) (void)hipStreamDestroy(v->stream2);
     delete v;
