@@ -35,7 +35,7 @@ struct mqr_geom {
 namespace mqr {
 
 constexpr int kMaxR = 16;
-constexpr int kThreads = 256;
+constexpr int kThreads = 512;  // 8 waves per workgroup: two LDS-resident blocks per CU keep 16 waves busy
 
 __device__ inline int64_t dev_find(const Table t, uint64_t k) {
     const uint64_t m = (uint64_t)t.cap - 1;
@@ -117,8 +117,8 @@ __device__ void load_tile(uint8_t* __restrict__ flag, float* __restrict__ tsdf, 
     }
 }
 
-// Block-wide exclusive scan of one int per thread (256 threads = 4 waves of 64).
-__device__ inline int block_exclusive_scan(int v, int* scratch /* >= 4 ints */, int& total) {
+// Block-wide exclusive scan of one int per thread (blockDim / 64 waves of 64, <= 16).
+__device__ inline int block_exclusive_scan(int v, int* scratch /* >= blockDim / 64 ints */, int& total) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     int incl = v;
 #pragma unroll
@@ -146,7 +146,7 @@ struct MeshLocal {
     uint16_t cube[Dims<RT>::CM * Dims<RT>::CM * Dims<RT>::CM];  // origins [-1, R-1]^3: bit8 valid | index
     uint8_t emask[R3M];                                          // owned edges with a vertex (bits x,y,z)
     uint16_t vbase[R3M];                                         // local vertex id of the voxel's first vertex
-    int scratch[8];
+    int scratch[16];
 };
 
 template <int RT>
@@ -195,7 +195,7 @@ __device__ void classify_mesh(const uint8_t* __restrict__ flag, MeshLocal<RT>& m
     }
     int vtot, ttot;
     int voff = block_exclusive_scan(vsum, ml.scratch, vtot);
-    tstart = block_exclusive_scan(tsum, ml.scratch + 4, ttot);
+    tstart = block_exclusive_scan(tsum, ml.scratch + 8, ttot);
     for (int p = p0; p < p1; ++p) {
         ml.vbase[p] = (uint16_t)voff;
         voff += __popc(ml.emask[p]);

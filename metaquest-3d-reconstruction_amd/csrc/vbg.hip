@@ -278,7 +278,11 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
     if (v->R == 16 && var != 1) {
         switch (var) {
             case 2: MQR_LAUNCH_INT(16, 4, false, false, 256); break;
-            case 5: MQR_LAUNCH_INT(16, 8, true, false, 256); break;
+            case 5: MQR_LAUNCH_INT(16, 8, 64, false, 256); break;
+            case 22: MQR_LAUNCH_INT(16, 4, 16, false, 512); break;
+            case 23: MQR_LAUNCH_INT(16, 4, 64, false, 512); break;
+            case 24: MQR_LAUNCH_INT(16, 4, 256, false, 512); break;
+            case 25: MQR_LAUNCH_INT(16, 4, 4, false, 512); break;
             case 6: MQR_LAUNCH_INT(16, 8, false, true, 256); break;
             case 7: MQR_LAUNCH_INT(16, 4, false, true, 256); break;
             case 8: MQR_LAUNCH_PK(16, 8, 256); break;

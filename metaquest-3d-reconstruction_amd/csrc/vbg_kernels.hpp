@@ -229,20 +229,17 @@ __device__ __forceinline__ float div_rn(float a, float b) {
 
 __device__ __forceinline__ float rcp_rn(float b) { return div_safe(b) ? div_rn_core(1.0f, b) : 1.0f / b; }
 
-// Integrate, R known at compile time (R = 16 / 8): thread t owns the voxel column (x, y) =
-// (t % R, t / R % R) for z in its z-range, keeps those voxels' (tsdf, weight) in registers for
-// all frames of the batch, and evaluates Open3D's transform ((xs*e0 + ys*e1) + zs*e2) + e3 with
-// the z-independent partial product hoisted per frame -- the same float operations in the same
-// order, so the result is bit-identical to k_integrate.
-// XCD-aware list order: consecutive workgroups are dealt round-robin over the 8 XCDs, so give XCD
-// x (= L % 8) one contiguous 1/8 of the list.  List entries are appended in pixel order, so a
-// contiguous range is a spatially coherent set of blocks whose depth gathers share pixels, and
-// each XCD's L2 then holds its region of the batch's depth frames.  Bijective on [0, n);
-// affects speed only (placement is not a correctness assumption).
+// XCD-aware list order: consecutive workgroups are dealt round-robin over the 8 XCDs, so hand XCD
+// x (= L % 8) chunks of C consecutive list entries in turn.  List entries are appended in touch
+// (pixel) order, so a chunk is a spatially coherent set of blocks whose depth gathers share
+// pixels and can hit in that XCD's L2; interleaving the chunks keeps the XCDs' loads balanced.
+// Bijective on [0, n) (the tail past the last full round keeps its order); speed only.
+template <int C>
 __device__ __forceinline__ int64_t xcd_swizzle(int64_t L, int64_t n) {
-    const int64_t q = n >> 3, r = n & 7;
-    const int64_t x = L & 7, j = L >> 3;
-    return x * q + (x < r ? x : r) + j;
+    const int64_t full = n / (8 * C) * (8 * C);
+    if (L >= full) return L;
+    const int64_t x = L & 7, s = L >> 3;
+    return ((s / C) * 8 + x) * C + s % C;
 }
 
 // Operand checks of the unguarded division core, on the float bits (|x| = e):
@@ -350,7 +347,7 @@ __device__ __forceinline__ bool integrate_column(float2 (&tw)[ZPER], uint32_t& d
 // order, so the result is bit-identical to k_integrate.  FAST: unguarded division core with a
 // block-level exact re-run when any operand is out of its range (host guarantees sdf_trunc and
 // depth_scale are in range).
-template <int R, int G, bool SWZ = false, bool FAST = false, int NT = 256>
+template <int R, int G, int SWZ = 0, bool FAST = false, int NT = 256>
 __global__ __launch_bounds__(NT) void k_integrate_t(const int32_t* __restrict__ list, const int* __restrict__ counters,
                                                      int64_t list_cap, Table t, float2* __restrict__ pool,
                                                      float voxel_size, const float* __restrict__ depths, int64_t HW,
@@ -369,7 +366,7 @@ __global__ __launch_bounds__(NT) void k_integrate_t(const int32_t* __restrict__ 
     const int tid = threadIdx.x;
     const int xv = tid % R, yv = (tid / R) % R, z0 = tid / R2;
     for (int64_t L = blockIdx.x; L < n; L += gridDim.x) {
-        const int64_t i = SWZ ? xcd_swizzle(L, n) : L;
+        const int64_t i = SWZ > 0 ? xcd_swizzle<(SWZ > 0 ? SWZ : 1)>(L, n) : L;
         const int32_t slot = list[i];
         const int buf = t.vals[slot];
         const uint32_t mask = __builtin_amdgcn_readfirstlane(t.mask[slot]);

@@ -35,7 +35,8 @@ def test_division_shortcut_exact(b):
         assert mm == 0, f"b={b}: {mm} mismatches, first bit pattern {first:#x}"
 
 
-INTEGRATE_VARIANTS = {16: (0, 2, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 0x100, 0x106, 0x108),
+INTEGRATE_VARIANTS = {16: (0, 2, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 22, 23, 24, 25, 0x100, 0x106,
+                          0x108),
                       8: (0, 6, 8, 0x101)}
 
 
