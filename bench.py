@@ -125,6 +125,36 @@ def confidence_leg(depth_t, K, T_wc, args, device):
             "note": "mqr_confidence over all frames, device-resident depth in/out, wall time of the call"}
 
 
+def ingest_leg(B, H, W, device):
+    """Row f4: device decode of B raw NDC frames + validity + confidence mask (every frame masked),
+    all buffers in HBM; algorithmic bytes = HW * (4 raw + 8 conf + 4 count + 4 out) per frame."""
+    import numpy as np
+    import torch
+    from mqr import _lib
+    g = torch.Generator(device=device).manual_seed(0)
+    raw = torch.rand((B, H, W), generator=g, device=device)
+    conf = torch.rand((B, H, W), generator=g, device=device, dtype=torch.float64)
+    vc = torch.randint(0, 8, (B, H, W), generator=g, device=device, dtype=torch.int32)
+    out = torch.empty_like(raw)
+    nears = np.full(B, 0.1)
+    fars = np.full(B, np.inf)
+    strong = np.full(B, 3, np.uint8)
+    has = np.ones(B, np.uint8)
+    ok = np.zeros(B, np.uint8)
+    times = []
+    for _ in range(4):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        _lib.call("mqr_decode_depth", int(device.index or 0), ctypes.c_void_p(raw.data_ptr()), 1, B, H, W,
+                  _lib.ptr(nears, _lib._f64p), _lib.ptr(fars, _lib._f64p), _lib.ptr(strong, _lib._u8p),
+                  ctypes.c_void_p(conf.data_ptr()), ctypes.c_void_p(vc.data_ptr()), _lib.ptr(has, _lib._u8p), 1,
+                  0.3, 2, ctypes.c_void_p(out.data_ptr()), 1, _lib.ptr(ok, _lib._u8p))
+        times.append(time.perf_counter() - t0)
+    t = sorted(times[1:])[1]
+    return {"frames": B, "ms": t * 1e3, "frames_per_s": B / t, "alg_gbs": 20 * H * W * B / t / 1e9,
+            "note": "mqr_decode_depth, device raw/conf/count in, depth out, wall time of the call"}
+
+
 def pmc_traffic(H, W, frames):
     """HBM bytes per integrate launch from the committed rocprofv3 --pmc passes of this workload
     (tools/traffic_workload.py + tools/pmc_summary.py; FETCH_SIZE/WRITE_SIZE calibrated on k_pack)."""
@@ -250,6 +280,7 @@ def main():
         dev = torch.device("cuda", local)
         extras["hbm_copy_gbs"] = copy_peak_gbs(dev)
         extras["confidence"] = confidence_leg(depth_t, K, T, args, dev)
+        extras["ingest"] = ingest_leg(B, H, W, dev)
         # PCIe-inclusive: the same step from host (numpy) frames, H2D inside integrate_frames
         host = depth_t.cpu().numpy()
         vbg.reset()
@@ -296,6 +327,7 @@ def main():
                         "note": "device-resident extract_triangle_mesh, median of reps; alg bytes = "
                                 "8R^3 N + 108 N + 24 V + 12 T"},
             "confidence": extras.get("confidence"),
+            "ingest": extras.get("ingest"),
             "host_input_frames_per_s": extras.get("host_input_frames_per_s"),
             "roofline": {"bound": "hbm", "kernel": "k_integrate", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "peak_measured_copy": extras.get("hbm_copy_gbs"),

@@ -106,6 +106,21 @@ int mqr_pixel_error_map(int device, const float* ref_depth, const float* tgt_dep
                         const float* K_tgt, const float* T_cw_ref, const float* T_cw_inv_tgt, const float* T_cw_tgt,
                         double depth_max, float* err_out);
 
+/* Device-side depth ingestion.  N raw Quest NDC buffers (H*W float32, raw_loc
+ * MQR_HOST / MQR_DEVICE) -> metric depth (depth_out, out_loc) + per-frame validity frame_ok[N]
+ * (host).  Replaces DepthDataIO.load_depth_map + is_depth_map_valid
+ * (scripts/dataio/depth_data_io.py:33-53, 80-85), convert_depth_to_linear
+ * (scripts/utils/depth_utils.py:21-46) and the confidence mask of load_depth_map
+ * (processing/reconstruction/utils/o3d_utils.py:131-142).  strong[f] (nullable): bit 0 / bit 1 =
+ * near / far were numpy float64 scalars (numpy >= 2 then divides in float64; Python floats keep
+ * the decode in float32).  has_mask[f] (nullable) selects frames whose conf (float64) /
+ * valid_count (int32) maps, laid out like the depth, are applied: depth = 0 where
+ * conf < conf_thr or valid_count < count_thr. */
+int mqr_decode_depth(int device, const float* raw, int raw_loc, int N, int H, int W, const double* nears,
+                     const double* fars, const uint8_t* strong, const double* conf, const int32_t* valid_count,
+                     const uint8_t* has_mask, int mask_loc, double conf_thr, int count_thr, float* depth_out,
+                     int out_loc, uint8_t* frame_ok);
+
 /* Kernel timing (HIP events on the volume's own stream).  enable=1 starts recording every
  * integrate-kernel launch; stats: launches, total kernel ms, union blocks, frame-blocks
  * (sum of per-frame touched blocks), frames, and the same for touch. */

@@ -65,6 +65,9 @@ SIGNATURES = {
                                       ctypes.c_double, _vp, _vp, ctypes.c_int]),
     "mqr_pixel_error_map": (ctypes.c_int, [ctypes.c_int, _f32p, _f32p, ctypes.c_int, ctypes.c_int, _f32p, _f32p,
                                            _f32p, _f32p, _f32p, ctypes.c_double, _f32p]),
+    "mqr_decode_depth": (ctypes.c_int, [ctypes.c_int, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                        _f64p, _f64p, _u8p, _vp, _vp, _u8p, ctypes.c_int, ctypes.c_double,
+                                        ctypes.c_int, _vp, ctypes.c_int, _u8p]),
     "mqr_vbg_profile": (ctypes.c_int, [_vp, ctypes.c_int]),
     "mqr_vbg_set_variant": (ctypes.c_int, [_vp, ctypes.c_int]),
     "mqr_check_division": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_uint32, ctypes.c_uint64,

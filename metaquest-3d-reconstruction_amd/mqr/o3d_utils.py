@@ -51,6 +51,22 @@ def _masked_depth(depth_data_io, side, index, dataset, use_confidence_filtered_d
     return depth
 
 
+def _raw_reader(depth_data_io, side):
+    """fn(timestamp, width, height) -> raw float32 NDC buffer or None (missing file), from either
+    this package's DepthDataIO or the reference's (via its depth_path_config); None if neither."""
+    if hasattr(depth_data_io, "load_raw_depth"):
+        return lambda ts, w, h: depth_data_io.load_raw_depth(side, ts, w, h)
+    cfg = getattr(depth_data_io, "depth_path_config", None)
+    if cfg is not None and hasattr(cfg, "get_depth_map_path"):
+        def read(ts, w, h):
+            path = cfg.get_depth_map_path(side=side, timestamp=ts)
+            if not path.exists():
+                return None
+            return np.fromfile(path, dtype="<f4").reshape((int(h), int(w)))
+        return read
+    return None
+
+
 def load_depth_map(depth_data_io, side, index: int, dataset, device, use_confidence_filtered_depth: bool,
                    confidence_threshold: float, valid_count_threshold: int) -> Optional[Image]:
     d = _masked_depth(depth_data_io, side, index, dataset, use_confidence_filtered_depth, confidence_threshold,
@@ -68,16 +84,62 @@ def integrate(dataset, depth_data_io, side, use_confidence_filtered_depth: bool,
     n = len(dataset.timestamps)
     extrinsic_wc = dataset.transforms.extrinsics_wc
     intrinsics = compute_o3d_intrinsic_matrices(dataset)
+    read_raw = _raw_reader(depth_data_io, side)
 
     def load_chunk(lo):
+        """Host side of one chunk: file reads only (decode + mask run on the device), or the
+        caller's own DataIO decode when it exposes no raw-buffer access."""
         hi = min(n, lo + CHUNK)
-        frames, ok = [], []
+        items = []
         for i in range(lo, hi):
-            d = _masked_depth(depth_data_io, side, i, dataset, use_confidence_filtered_depth, confidence_threshold,
-                              valid_count_threshold)
-            ok.append(d is not None)
-            frames.append(d)
-        return lo, hi, frames, ok
+            if read_raw is None:
+                d = _masked_depth(depth_data_io, side, i, dataset, use_confidence_filtered_depth,
+                                  confidence_threshold, valid_count_threshold)
+                if d is not None:
+                    items.append((i, d, None))
+                continue
+            raw = read_raw(dataset.timestamps[i], dataset.widths[i], dataset.heights[i])
+            if raw is None:
+                continue
+            cm = None
+            if use_confidence_filtered_depth:
+                cm = depth_data_io.load_confidence_map(side=side, timestamp=dataset.timestamps[i])
+                if cm is None:
+                    print(f"[Warning] Confidence map not found for timestamp {dataset.timestamps[i]}")
+            items.append((i, raw, cm))
+        return lo, hi, items
+
+    stage = {}  # (H, W) -> DeviceBuffer of CHUNK decoded frames
+
+    def run(idx, frames, cms, H, W):
+        K = intrinsics[idx].astype(np.float64)
+        T = extrinsic_wc[idx].astype(np.float64)
+        kw = dict(depth_scale=1.0, depth_max=float(depth_max), trunc_voxel_multiplier=float(trunc_voxel_multiplier))
+        if read_raw is None:
+            vbg.integrate_frames(np.stack(frames), K, T, **kw)
+            return
+        from ._lib import DeviceBuffer
+        from .ingest import decode_depth_frames
+        B = len(idx)
+        buf = stage.get((H, W))
+        if buf is None:
+            buf = stage[(H, W)] = DeviceBuffer(4 * CHUNK * H * W, vbg.device_id)
+        has = np.array([cm is not None for cm in cms], bool)
+        conf = vc = None
+        if has.any():
+            conf = np.zeros((B, H, W), np.float64)
+            vc = np.zeros((B, H, W), np.int32)
+            for j, cm in enumerate(cms):
+                if cm is not None:
+                    conf[j] = cm.confidence_map
+                    vc[j] = cm.valid_count
+        _, ok = decode_depth_frames(np.stack(frames), [dataset.nears[i] for i in idx], [dataset.fars[i] for i in idx],
+                                    conf=conf, valid_count=vc, has_mask=has,
+                                    confidence_threshold=confidence_threshold,
+                                    valid_count_threshold=valid_count_threshold, device=vbg.device_id,
+                                    out_ptr=buf.ptr)
+        if ok.any():
+            vbg.integrate_frames((buf, B, H, W), K, T, frame_ok=ok.astype(np.uint8), **kw)
 
     bar = None
     if show_progress:
@@ -86,18 +148,15 @@ def integrate(dataset, depth_data_io, side, use_confidence_filtered_depth: bool,
     with ThreadPoolExecutor(max_workers=1) as pool:
         fut = pool.submit(load_chunk, 0) if n else None
         while fut is not None:
-            lo, hi, frames, ok = fut.result()
+            lo, hi, items = fut.result()
             fut = pool.submit(load_chunk, hi) if hi < n else None
-            shapes = {f.shape for f in frames if f is not None}
-            for shape in shapes:  # frames of one capture share a size; group defensively
-                sel = [j for j, f in enumerate(frames) if f is not None and f.shape == shape]
-                depths = np.stack([frames[j] for j in sel])
-                idx = np.array([lo + j for j in sel])
-                vbg.integrate_frames(depths, intrinsics[idx].astype(np.float64), extrinsic_wc[idx].astype(np.float64),
-                                     depth_scale=1.0, depth_max=float(depth_max),
-                                     trunc_voxel_multiplier=float(trunc_voxel_multiplier))
+            for shape in dict.fromkeys(f.shape for _, f, _ in items):  # one size per capture; group defensively
+                sel = [it for it in items if it[1].shape == shape]
+                run(np.array([i for i, _, _ in sel]), [f for _, f, _ in sel], [c for _, _, c in sel], *shape)
             if bar is not None:
                 bar.update(hi - lo)
     if bar is not None:
         bar.close()
+    for b in stage.values():
+        b.free()
     return vbg

@@ -1,6 +1,6 @@
 """Generate the golden fixtures in tests/golden/ by running the REFERENCE's own Python code.
 
-Run here (this container) only:  python tests/golden/make_golden.py
+Run here (this container) only:  python tests/golden/make_golden.py [decode]
 It imports /root/reference/scripts (read-only) with ``open3d`` and ``cv2`` stubbed by
 MagicMock (neither is installed; the functions exercised never touch them), feeds it synthetic
 captures, and stores inputs + reference outputs as .npz data.  Nothing from the reference is
@@ -61,7 +61,12 @@ def make_decode(ref):
     io = ref["DepthDataIO"](depth_path_config=None)
     valid = np.array([io.is_depth_map_valid(r) for r in raw])
     out = np.stack([np.stack([ref["convert_depth_to_linear"](r, float(n), float(f)) for r in raw]) for n, f in params])
-    np.savez_compressed(HERE / "decode_golden.npz", raw=raw, params=params, valid=valid, linear=out)
+    # the pipeline passes DepthDataset.nears[i] / fars[i], numpy float64 scalars: under numpy >= 2
+    # (NEP 50) they are strongly typed and the decode's division runs in float64 -> separate vectors
+    out64 = np.stack([np.stack([ref["convert_depth_to_linear"](r, np.float64(n), np.float64(f)) for r in raw])
+                      for n, f in params])
+    np.savez_compressed(HERE / "decode_golden.npz", raw=raw, params=params, valid=valid, linear=out,
+                        linear64=out64, numpy_version=np.array(np.__version__))
 
 
 def capture_to_reference(ref, project_dir):
@@ -124,6 +129,7 @@ def make_dataset_and_confidence(ref):
 if __name__ == "__main__":
     ref = import_reference()
     make_decode(ref)
-    make_dataset_and_confidence(ref)
+    if "decode" not in sys.argv[1:]:
+        make_dataset_and_confidence(ref)
     for f in sorted(HERE.glob("*.npz")):
         print(f.name, os.path.getsize(f))

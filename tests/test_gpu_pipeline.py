@@ -1,0 +1,72 @@
+"""The drop-in boundary end to end: mqr.o3d_utils.integrate(dataset, depth_data_io, side, ...)
+(reference o3d_utils.py:153-238) on a capture written in the reference's layout, with device
+ingestion (raw files -> mqr_decode_depth -> batched touch/integrate), against the CPU oracle fed
+by the numpy decode path frame by frame.  Covers missing files, invalid buffers, confidence
+masking and a missing confidence map.  Bit-identical volumes."""
+import numpy as np
+import pytest
+
+import oracle  # the test-only checker (tests/conftest.py puts oracle/ on the path)
+
+pytestmark = pytest.mark.gpu
+
+
+def _capture(tmp_path, n=14, seed=31):
+    from mqr import synthetic
+    from mqr.dataio import DepthDataIO
+    from mqr.models import ConfidenceMap, Side
+    seq = synthetic.make_sequence("room", n=n, height=240, width=320, f=262.5, noise=True, seed=seed)
+    synthetic.write_capture(tmp_path, seq)
+    io = DepthDataIO(tmp_path)
+    ds = io.build_depth_dataset(Side.LEFT)
+    assert len(ds) == n
+    rng = np.random.default_rng(seed)
+    for i, ts in enumerate(ds.timestamps):
+        if i == 6:
+            continue  # no confidence map: warn, integrate unmasked
+        conf = rng.random((240, 320))
+        vc = rng.integers(0, 8, (240, 320)).astype(np.int32)
+        io.save_confidence_map(Side.LEFT, int(ts), ConfidenceMap(conf, vc))
+    files = sorted((tmp_path / "left_depth").glob("*.raw"))
+    files[3].unlink()                                 # missing after the dataset was built
+    np.ones((240, 320), "<f4").tofile(files[9])       # all-one buffer: invalid, dropped
+    return io, ds, Side
+
+
+@pytest.mark.parametrize("use_conf", [False, True])
+def test_integrate_dropin_matches_oracle(tmp_path, use_conf, capsys):
+    from gpu_helpers import compare_volumes
+    from mqr.o3d_utils import _masked_depth, compute_o3d_intrinsic_matrices, integrate
+    io, ds, Side = _capture(tmp_path)
+    kw = dict(use_confidence_filtered_depth=use_conf, confidence_threshold=0.2, valid_count_threshold=2)
+    vbg = integrate(ds, io, Side.LEFT, voxel_size=0.01, block_resolution=16, block_count=500, depth_max=4.0,
+                    trunc_voxel_multiplier=10.0, device="CUDA:0", **kw)
+    out = capsys.readouterr().out
+    assert ("[Warning] Confidence map not found" in out) == use_conf
+    ref = oracle.OracleVBG(0.01, 16, 256)
+    K = compute_o3d_intrinsic_matrices(ds).astype(np.float64)
+    T = ds.transforms.extrinsics_wc.astype(np.float64)
+    used = 0
+    for i in range(len(ds)):
+        d = _masked_depth(io, Side.LEFT, i, ds, **kw)
+        if d is None:
+            continue
+        ref.integrate_frame(d, K[i], T[i], 1.0, 4.0, 10.0)
+        used += 1
+    assert used == len(ds) - 2
+    capsys.readouterr()
+    assert compare_volumes(vbg.export(), ref.export(), 0.0) == 0.0
+
+
+def test_integrate_dropin_chains_volumes(tmp_path):
+    """vbg_opt chaining (reconstruct_scene.py:65-81): a second call continues the same volume."""
+    from gpu_helpers import compare_volumes
+    from mqr.o3d_utils import integrate
+    io, ds, Side = _capture(tmp_path, n=10, seed=5)
+    kw = dict(use_confidence_filtered_depth=False, confidence_threshold=0.0, valid_count_threshold=0,
+              voxel_size=0.01, block_resolution=8, block_count=100, depth_max=4.0, trunc_voxel_multiplier=10.0,
+              device=0)
+    a = integrate(ds[list(range(5))], io, Side.LEFT, **kw)
+    a = integrate(ds[list(range(5, 10))], io, Side.LEFT, vbg_opt=a, **kw)
+    b = integrate(ds, io, Side.LEFT, **kw)
+    assert compare_volumes(a.export(), b.export(), 0.0) == 0.0
