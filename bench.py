@@ -155,6 +155,32 @@ def ingest_leg(B, H, W, device):
             "note": "mqr_decode_depth, device raw/conf/count in, depth out, wall time of the call"}
 
 
+def raycast_leg(vbg, K, T, H, W, thr, frames=64):
+    """Row f1: colour-aligned depth by ray casting the extracted mesh (RaycastingScene.cast_rays
+    stand-in): BVH build + `frames` pinhole casts at H x W from the sequence's poses."""
+    import numpy as np
+    from mqr.raycasting import RaycastingScene
+    m = vbg.extract_triangle_mesh(weight_threshold=thr)
+    scene = RaycastingScene(device=vbg.device_id)
+    scene.add_triangles(m.vertices, m.triangles)
+    from mqr import _lib
+    t0 = time.perf_counter()
+    _lib.call("mqr_scene_build", scene._h)
+    build_ms = (time.perf_counter() - t0) * 1e3
+    idx = np.linspace(0, len(K) - 1, frames).astype(int)
+    scene.cast_pinhole(K[idx[:4]], T[idx[:4]], W, H)  # warm-up
+    times = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        out = scene.cast_pinhole(K[idx], T[idx], W, H)["t_hit"].numpy()
+        times.append(time.perf_counter() - t0)
+    t = sorted(times)[1]
+    return {"triangles": int(m.triangles.shape[0]), "bvh_build_ms": build_ms, "frames": frames,
+            "frames_per_s": frames / t, "mrays_per_s": frames * H * W / t / 1e6,
+            "hit_fraction": float(np.isfinite(out).mean()),
+            "note": "mqr_scene_cast_pinhole, t_hit copied to host (PCIe included), median of 3"}
+
+
 def pmc_traffic(H, W, frames):
     """HBM bytes per integrate launch from the committed rocprofv3 --pmc passes of this workload
     (tools/traffic_workload.py + tools/pmc_summary.py; FETCH_SIZE/WRITE_SIZE calibrated on k_pack)."""
@@ -281,6 +307,7 @@ def main():
         extras["hbm_copy_gbs"] = copy_peak_gbs(dev)
         extras["confidence"] = confidence_leg(depth_t, K, T, args, dev)
         extras["ingest"] = ingest_leg(B, H, W, dev)
+        extras["raycast"] = raycast_leg(vbg, K, T, H, W, args.extract_threshold)
         # PCIe-inclusive: the same step from host (numpy) frames, H2D inside integrate_frames
         host = depth_t.cpu().numpy()
         vbg.reset()
@@ -328,6 +355,7 @@ def main():
                                 "8R^3 N + 108 N + 24 V + 12 T"},
             "confidence": extras.get("confidence"),
             "ingest": extras.get("ingest"),
+            "raycast": extras.get("raycast"),
             "host_input_frames_per_s": extras.get("host_input_frames_per_s"),
             "roofline": {"bound": "hbm", "kernel": "k_integrate", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "peak_measured_copy": extras.get("hbm_copy_gbs"),

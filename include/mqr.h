@@ -28,6 +28,7 @@ extern "C" {
 
 typedef struct mqr_vbg mqr_vbg;    /* voxel-block-hashed TSDF volume resident in HBM */
 typedef struct mqr_geom mqr_geom;  /* extracted point cloud or triangle mesh (device-resident) */
+typedef struct mqr_scene mqr_scene;  /* triangle-mesh ray-casting scene (device BVH) */
 
 int mqr_version(void);
 const char* mqr_last_error(void);
@@ -144,6 +145,27 @@ int mqr_vbg_set_variant(mqr_vbg* v, int variant);
 int mqr_check_division(int device, int which, float b, uint32_t lo_bits, uint64_t count, uint32_t* mismatches,
                        uint32_t* first_bad);
 int mqr_vbg_stats(mqr_vbg* v, mqr_stats* out, int reset);
+
+/* Ray casting: replaces o3d.t.geometry.RaycastingScene as used for colour-aligned
+ * depth (reconstruct_scene.py:197-201, o3d_utils.py:324-341, optimize_color_pose.py:24-47).
+ * add_triangles ~ RaycastingScene.add_triangles (vertices float32 (nv,3), triangles int32 (nt,3),
+ * loc MQR_HOST/MQR_DEVICE; returns the geometry id); the device BVH is (re)built on the first
+ * query after a change (mqr_scene_build forces it).  cast_pinhole ~ create_rays_pinhole(K, T_wc,
+ * W, H) + cast_rays for n_frames cameras (K (n,3,3) and T_wc (n,4,4) float64 row-major);
+ * cast_rays takes explicit rays (n,6) float32 (origin, direction).  Outputs: t_hit (inf on miss)
+ * and the optional geometry / primitive ids (0xffffffff on miss), barycentric uvs (n,2) and unit
+ * geometric normals (n,3); out_loc says where all output buffers live. */
+int mqr_scene_create(int device, mqr_scene** out);
+int mqr_scene_destroy(mqr_scene* s);
+int mqr_scene_add_triangles(mqr_scene* s, const float* vertices, int64_t nv, const int32_t* triangles, int64_t nt,
+                            int loc, uint32_t* geom_id);
+int mqr_scene_build(mqr_scene* s);
+int mqr_scene_triangle_count(mqr_scene* s, int64_t* n);
+int mqr_scene_cast_pinhole(mqr_scene* s, const double* K, const double* T_wc, int n_frames, int H, int W,
+                           float* t_hit, uint32_t* geom_ids, uint32_t* prim_ids, float* uvs, float* normals,
+                           int out_loc);
+int mqr_scene_cast_rays(mqr_scene* s, const float* rays, int64_t nrays, int rays_loc, float* t_hit,
+                        uint32_t* geom_ids, uint32_t* prim_ids, float* uvs, float* normals, int out_loc);
 
 #ifdef __cplusplus
 }

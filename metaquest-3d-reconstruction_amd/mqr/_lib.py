@@ -68,6 +68,16 @@ SIGNATURES = {
     "mqr_decode_depth": (ctypes.c_int, [ctypes.c_int, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                         _f64p, _f64p, _u8p, _vp, _vp, _u8p, ctypes.c_int, ctypes.c_double,
                                         ctypes.c_int, _vp, ctypes.c_int, _u8p]),
+    "mqr_scene_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(_vp)]),
+    "mqr_scene_destroy": (ctypes.c_int, [_vp]),
+    "mqr_scene_add_triangles": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp, ctypes.c_int64, ctypes.c_int,
+                                               ctypes.POINTER(ctypes.c_uint32)]),
+    "mqr_scene_build": (ctypes.c_int, [_vp]),
+    "mqr_scene_triangle_count": (ctypes.c_int, [_vp, _i64p]),
+    "mqr_scene_cast_pinhole": (ctypes.c_int, [_vp, _f64p, _f64p, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp, _vp,
+                                              _vp, _vp, _vp, ctypes.c_int]),
+    "mqr_scene_cast_rays": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_int, _vp, _vp, _vp, _vp, _vp,
+                                           ctypes.c_int]),
     "mqr_vbg_profile": (ctypes.c_int, [_vp, ctypes.c_int]),
     "mqr_vbg_set_variant": (ctypes.c_int, [_vp, ctypes.c_int]),
     "mqr_check_division": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_uint32, ctypes.c_uint64,

@@ -647,3 +647,47 @@ int orc_confidence(const float* depths, const uint8_t* frame_valid, const float*
     }
     return 0;
 }
+
+/* ------------------------------------------------------------------ ray casting (row f1)
+ * Restates what the reference reads from Open3D's RaycastingScene (o3d_utils.py:324-341):
+ * closest hit t in (0, inf) of each ray (origin, direction) against every triangle, inf on a
+ * miss, with the primitive index.  Brute force, Moeller-Trumbore in float64 (the exact geometric
+ * answer up to float64 rounding), OpenMP over rays.  Parity against Embree itself is unpinned
+ * (Open3D is not installed); the GPU kernel is checked against this to a tolerance. */
+int orc_raycast(const float* V, int64_t nv, const int32_t* T, int64_t nt, const float* rays, int64_t nrays,
+                float* t_hit, int32_t* prim) {
+    (void)nv;
+#pragma omp parallel for schedule(dynamic, 64)
+    for (int64_t r = 0; r < nrays; ++r) {
+        const double o[3] = {rays[6 * r], rays[6 * r + 1], rays[6 * r + 2]};
+        const double d[3] = {rays[6 * r + 3], rays[6 * r + 4], rays[6 * r + 5]};
+        double best = INFINITY;
+        int32_t bp = -1;
+        for (int64_t i = 0; i < nt; ++i) {
+            const float* a = V + 3 * (int64_t)T[3 * i];
+            const float* b = V + 3 * (int64_t)T[3 * i + 1];
+            const float* c = V + 3 * (int64_t)T[3 * i + 2];
+            const double e1[3] = {(double)b[0] - a[0], (double)b[1] - a[1], (double)b[2] - a[2]};
+            const double e2[3] = {(double)c[0] - a[0], (double)c[1] - a[1], (double)c[2] - a[2]};
+            const double p[3] = {d[1] * e2[2] - d[2] * e2[1], d[2] * e2[0] - d[0] * e2[2], d[0] * e2[1] - d[1] * e2[0]};
+            const double det = e1[0] * p[0] + e1[1] * p[1] + e1[2] * p[2];
+            if (det == 0.0) continue;
+            const double inv = 1.0 / det;
+            const double tv[3] = {o[0] - a[0], o[1] - a[1], o[2] - a[2]};
+            const double u = (tv[0] * p[0] + tv[1] * p[1] + tv[2] * p[2]) * inv;
+            if (u < 0.0 || u > 1.0) continue;
+            const double q[3] = {tv[1] * e1[2] - tv[2] * e1[1], tv[2] * e1[0] - tv[0] * e1[2],
+                                 tv[0] * e1[1] - tv[1] * e1[0]};
+            const double v = (d[0] * q[0] + d[1] * q[1] + d[2] * q[2]) * inv;
+            if (v < 0.0 || u + v > 1.0) continue;
+            const double t = (e2[0] * q[0] + e2[1] * q[1] + e2[2] * q[2]) * inv;
+            if (t > 0.0 && t < best) {
+                best = t;
+                bp = (int32_t)i;
+            }
+        }
+        t_hit[r] = (float)best;
+        if (prim) prim[r] = bp;
+    }
+    return 0;
+}

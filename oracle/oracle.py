@@ -66,6 +66,8 @@ def lib():
         L.orc_confidence.restype = ctypes.c_int
         L.orc_confidence.argtypes = [_f32p, _u8p, _f32p, _f32p, _f32p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                      ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_double, _f64p, _i32p]
+        L.orc_raycast.restype = ctypes.c_int
+        L.orc_raycast.argtypes = [_f32p, ctypes.c_int64, _i32p, ctypes.c_int64, _f32p, ctypes.c_int64, _f32p, _i32p]
         _lib = L
     return _lib
 
@@ -202,3 +204,17 @@ def confidence(depths, K, Tcw, Tcw_inv, ref, target_frame_range=10, depth_max=3.
                          _p(Tcw_inv, _f32p), N, H, W, int(ref), int(target_frame_range), float(depth_max),
                          float(error_threshold), _p(conf, _f64p), _p(valid, _i32p))
     return conf, valid
+
+
+def raycast(vertices, triangles, rays):
+    """Closest-hit t (inf on miss) and primitive index (-1) per ray, brute force in float64."""
+    V = np.ascontiguousarray(vertices, dtype=np.float32).reshape(-1, 3)
+    T = np.ascontiguousarray(triangles, dtype=np.int32).reshape(-1, 3)
+    r = np.ascontiguousarray(rays, dtype=np.float32)
+    shape = r.shape[:-1]
+    r = r.reshape(-1, 6)
+    t = np.empty(r.shape[0], np.float32)
+    pr = np.empty(r.shape[0], np.int32)
+    lib().orc_raycast(_p(V, _f32p), V.shape[0], _p(T, _i32p), T.shape[0], _p(r, _f32p), r.shape[0], _p(t, _f32p),
+                      _p(pr, _i32p))
+    return t.reshape(shape), pr.reshape(shape)
