@@ -62,9 +62,10 @@ __global__ __launch_bounds__(256) void k_decode_depth(const float* __restrict__ 
         }
         out[base + i] = z;
     }
-    // wave-level OR, one atomic per wave
+    // wave-level OR, then one atomic per wave only for bits the frame's word does not have yet
+    // (every wave of a frame would otherwise hit the same address: thousands of serialised atomics)
     for (int o = 32; o > 0; o >>= 1) fl |= (uint32_t)__shfl_xor((int)fl, o, 64);
-    if ((threadIdx.x & 63) == 0 && fl) atomicOr(&flags[f], fl);
+    if ((threadIdx.x & 63) == 0 && (fl & ~__atomic_load_n(&flags[f], __ATOMIC_RELAXED))) atomicOr(&flags[f], fl);
 }
 
 }  // namespace mqr
