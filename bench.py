@@ -181,6 +181,37 @@ def raycast_leg(vbg, K, T, H, W, thr, frames=64):
             "note": "mqr_scene_cast_pinhole, t_hit copied to host (PCIe included), median of 3"}
 
 
+def meshfilter_leg(vbg, thr, min_count=2000, reps=3):
+    """Row f3: filter_mesh_components (o3d_utils.py:241-321) on the extracted mesh, device-resident
+    input (the extraction's own buffers), result left on the device."""
+    import ctypes
+    import numpy as np
+    from mqr import _lib
+    m = vbg.extract_triangle_mesh(weight_threshold=thr)
+    nv, nt = int(m.vertices.shape[0]), int(m.triangles.shape[0])
+    import torch
+    dev = torch.device("cuda", vbg.device_id)
+    v = torch.from_numpy(np.ascontiguousarray(m.vertices)).to(dev)
+    n = torch.from_numpy(np.ascontiguousarray(m.vertex_normals)).to(dev)
+    t = torch.from_numpy(np.ascontiguousarray(m.triangles, dtype=np.int32)).to(dev)
+    torch.cuda.synchronize()
+    stats = np.zeros(8, np.int64)
+    times = []
+    for _ in range(reps + 1):
+        g = ctypes.c_void_p()
+        t0 = time.perf_counter()
+        _lib.call("mqr_mesh_filter_components", vbg.device_id, ctypes.c_void_p(v.data_ptr()),
+                  ctypes.c_void_p(n.data_ptr()), nv, ctypes.c_void_p(t.data_ptr()), nt, 1, min_count,
+                  ctypes.byref(g), _lib.ptr(stats, _lib._i64p))
+        times.append(time.perf_counter() - t0)
+        _lib.call("mqr_geom_free", g)
+    ms = sorted(times[1:])[len(times[1:]) // 2] * 1e3
+    return {"triangles_in": nt, "vertices_in": nv, "clusters": int(stats[1]), "kept_clusters": int(stats[2]),
+            "triangles_out": int(stats[6]), "min_triangle_count": min_count, "ms": ms,
+            "mtris_per_s": nt / ms / 1e3,
+            "note": "mqr_mesh_filter_components, device-resident mesh in/out, wall time of the call, median"}
+
+
 def pmc_traffic(H, W, frames):
     """HBM bytes per integrate launch from the committed rocprofv3 --pmc passes of this workload
     (tools/traffic_workload.py + tools/pmc_summary.py; FETCH_SIZE/WRITE_SIZE calibrated on k_pack)."""
@@ -308,6 +339,7 @@ def main():
         extras["confidence"] = confidence_leg(depth_t, K, T, args, dev)
         extras["ingest"] = ingest_leg(B, H, W, dev)
         extras["raycast"] = raycast_leg(vbg, K, T, H, W, args.extract_threshold)
+        extras["meshfilter"] = meshfilter_leg(vbg, args.extract_threshold)
         # PCIe-inclusive: the same step from host (numpy) frames, H2D inside integrate_frames
         host = depth_t.cpu().numpy()
         vbg.reset()
@@ -356,6 +388,7 @@ def main():
             "confidence": extras.get("confidence"),
             "ingest": extras.get("ingest"),
             "raycast": extras.get("raycast"),
+            "meshfilter": extras.get("meshfilter"),
             "host_input_frames_per_s": extras.get("host_input_frames_per_s"),
             "roofline": {"bound": "hbm", "kernel": "k_integrate", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "peak_measured_copy": extras.get("hbm_copy_gbs"),

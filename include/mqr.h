@@ -167,6 +167,19 @@ int mqr_scene_cast_pinhole(mqr_scene* s, const double* K, const double* T_wc, in
 int mqr_scene_cast_rays(mqr_scene* s, const float* rays, int64_t nrays, int rays_loc, float* t_hit,
                         uint32_t* geom_ids, uint32_t* prim_ids, float* uvs, float* normals, int out_loc);
 
+/* filter_mesh_components (processing/reconstruction/utils/o3d_utils.py:241-321) on the device:
+ * edge-connected triangle clusters (Open3D cluster_connected_triangles order), keep clusters with
+ * >= min_triangle_count triangles (else the largest), then remove_unreferenced_vertices,
+ * remove_degenerate_triangles, remove_duplicated_triangles, remove_duplicated_vertices and
+ * remove_non_manifold_edges with Open3D's legacy semantics (non-manifold edges visited in
+ * ascending vertex-pair order).  vertices / normals (nullable) nv*3 float32, triangles nt*3 int32
+ * in `loc` memory.  Result: a device geometry (mqr_geom_counts / _copy / _free).  stats[8]:
+ * input triangles, clusters, kept clusters, triangles removed with small clusters, largest
+ * cluster, triangles removed by the non-manifold pass, final triangles, final vertices. */
+int mqr_mesh_filter_components(int device, const float* vertices, const float* normals, int64_t nv,
+                               const int32_t* triangles, int64_t nt, int loc, int64_t min_triangle_count,
+                               mqr_geom** out, int64_t* stats);
+
 #ifdef __cplusplus
 }
 #endif

@@ -24,14 +24,6 @@
 #include "mqr_common.hpp"
 #include "mqr_mc_tables.h"
 
-struct mqr_geom {
-    int device = 0;
-    int64_t nv = 0, nt = 0;
-    float* pos = nullptr;
-    float* nrm = nullptr;
-    int32_t* tri = nullptr;
-};
-
 namespace mqr {
 
 constexpr int kMaxR = 16;

@@ -150,6 +150,15 @@ struct mqr_vbg {
     int* pool_ctr() const { return counters + 2 * mqr::kCountersTotal; }
 };
 
+// Device-resident geometry result (extract.hip, meshfilter.hip); released by mqr_geom_free.
+struct mqr_geom {
+    int device = 0;
+    int64_t nv = 0, nt = 0;
+    float* pos = nullptr;
+    float* nrm = nullptr;
+    int32_t* tri = nullptr;
+};
+
 namespace mqr {
 int grow_pool(mqr_vbg* v, int64_t need);
 int sync_all(mqr_vbg* v);

@@ -78,6 +78,8 @@ SIGNATURES = {
                                               _vp, _vp, _vp, ctypes.c_int]),
     "mqr_scene_cast_rays": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_int, _vp, _vp, _vp, _vp, _vp,
                                            ctypes.c_int]),
+    "mqr_mesh_filter_components": (ctypes.c_int, [ctypes.c_int, _vp, _vp, ctypes.c_int64, _vp, ctypes.c_int64,
+                                                  ctypes.c_int, ctypes.c_int64, ctypes.POINTER(_vp), _i64p]),
     "mqr_vbg_profile": (ctypes.c_int, [_vp, ctypes.c_int]),
     "mqr_vbg_set_variant": (ctypes.c_int, [_vp, ctypes.c_int]),
     "mqr_check_division": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_uint32, ctypes.c_uint64,

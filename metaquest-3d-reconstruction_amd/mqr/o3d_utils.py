@@ -21,6 +21,8 @@ from typing import Optional
 import numpy as np
 
 from .geometry import Image
+from .meshfilter import filter_mesh_components  # noqa: F401  (re-exported: o3d_utils.py:241-321)
+from .raycasting import raycast_in_color_view  # noqa: F401  (re-exported: o3d_utils.py:324-341)
 from .vbg import VoxelBlockGrid
 
 CHUNK = 64  # frames per host->device hand-off (device batches are <= 32 frames)
