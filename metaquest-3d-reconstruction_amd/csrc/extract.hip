@@ -84,30 +84,94 @@ struct Tile {
 };
 
 // Stage the (R+3)^3 tile [-1, R+1]^3 from the block and its 26 neighbours (nbrow: buffer or -1).
+// Compile-time R: every thread first issues all of its ceil(S^3 / kThreads) pool loads into
+// registers and only then writes LDS, so a workgroup has ~14 loads per lane in flight instead of
+// one latency-serialised load per loop trip.
 template <int RT, bool TSDF>
 __device__ void load_tile(uint8_t* __restrict__ flag, float* __restrict__ tsdf, const int32_t* __restrict__ nbrow,
                           const float2* __restrict__ pool, const Dims<RT>& d, float thr) {
-    const int R = d.R, S = d.S;
-    const int S3 = S * S * S;
-    const int R3 = R * R * R;
-    for (int i = threadIdx.x; i < S3; i += blockDim.x) {
-        const int lx = i % S - 1, ly = (i / S) % S - 1, lz = i / (S * S) - 1;
-        const int dx = lx < 0 ? -1 : (lx >= R ? 1 : 0);
-        const int dy = ly < 0 ? -1 : (ly >= R ? 1 : 0);
-        const int dz = lz < 0 ? -1 : (lz >= R ? 1 : 0);
-        const int nbuf = nbrow[(dx + 1) + 3 * (dy + 1) + 9 * (dz + 1)];
-        uint8_t f = 0;
-        float ts = 0.f;
-        if (nbuf >= 0) {
-            const float2 tw =
-                pool[(int64_t)nbuf * R3 + ((lz - dz * R) * R + (ly - dy * R)) * R + (lx - dx * R)];
-            ts = tw.x;
-            f = 1 | (tw.y > thr ? 2 : 0) | (tw.x < 0 ? 4 : 0);
+    if constexpr (RT > 0) {
+        constexpr int R = RT, S = RT + 3, S3 = S * S * S, R3 = R * R * R;
+        constexpr int NIT = (S3 + kThreads - 1) / kThreads;
+        float2 v[NIT];
+        uint32_t present = 0;
+#pragma unroll
+        for (int k = 0; k < NIT; ++k) {
+            const int i = threadIdx.x + k * kThreads;
+            v[k] = make_float2(0.f, 0.f);
+            if (i < S3) {
+                const int lx = i % S - 1, ly = (i / S) % S - 1, lz = i / (S * S) - 1;
+                const int dx = lx < 0 ? -1 : (lx >= R ? 1 : 0);
+                const int dy = ly < 0 ? -1 : (ly >= R ? 1 : 0);
+                const int dz = lz < 0 ? -1 : (lz >= R ? 1 : 0);
+                const int nbuf = nbrow[(dx + 1) + 3 * (dy + 1) + 9 * (dz + 1)];
+                if (nbuf >= 0) {
+                    v[k] = pool[(int64_t)nbuf * R3 + ((lz - dz * R) * R + (ly - dy * R)) * R + (lx - dx * R)];
+                    present |= 1u << k;
+                }
+            }
         }
-        flag[i] = f;
-        if (TSDF) tsdf[i] = ts;
+#pragma unroll
+        for (int k = 0; k < NIT; ++k) {
+            const int i = threadIdx.x + k * kThreads;
+            if (i < S3) {
+                const bool p = (present >> k) & 1u;
+                flag[i] = p ? (uint8_t)(1 | (v[k].y > thr ? 2 : 0) | (v[k].x < 0 ? 4 : 0)) : (uint8_t)0;
+                if (TSDF) tsdf[i] = v[k].x;
+            }
+        }
+        (void)d;
+    } else {
+        const int R = d.R, S = d.S;
+        const int S3 = S * S * S;
+        const int R3 = R * R * R;
+        for (int i = threadIdx.x; i < S3; i += blockDim.x) {
+            const int lx = i % S - 1, ly = (i / S) % S - 1, lz = i / (S * S) - 1;
+            const int dx = lx < 0 ? -1 : (lx >= R ? 1 : 0);
+            const int dy = ly < 0 ? -1 : (ly >= R ? 1 : 0);
+            const int dz = lz < 0 ? -1 : (lz >= R ? 1 : 0);
+            const int nbuf = nbrow[(dx + 1) + 3 * (dy + 1) + 9 * (dz + 1)];
+            uint8_t f = 0;
+            float ts = 0.f;
+            if (nbuf >= 0) {
+                const float2 tw =
+                    pool[(int64_t)nbuf * R3 + ((lz - dz * R) * R + (ly - dy * R)) * R + (lx - dx * R)];
+                ts = tw.x;
+                f = 1 | (tw.y > thr ? 2 : 0) | (tw.x < 0 ? 4 : 0);
+            }
+            flag[i] = f;
+            if (TSDF) tsdf[i] = ts;
+        }
     }
 }
+
+// Marching-cubes tables staged in LDS: the lookups below are lane-divergent (one cube index per
+// lane), which from __constant__ memory become serialised vector loads.
+struct McLds {
+    int8_t tri[256 * 16];
+    uint8_t count[256];
+};
+
+__device__ inline void load_mc_tables(McLds& mc, bool tri) {
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+        mc.count[i] = (uint8_t)mqr_tri_count[i];
+        if (tri) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) mc.tri[i * 16 + r] = mqr_tri_table[i][r];
+        }
+    }
+}
+
+// Edge e's owning-voxel shift (dx, dy, dz) and axis packed 5 bits per edge (mqr_edge_shifts).
+__host__ __device__ constexpr uint64_t pack_edge_shifts() {
+    constexpr int es[12][4] = {{0, 0, 0, 0}, {1, 0, 0, 1}, {0, 1, 0, 0}, {0, 0, 0, 1}, {0, 0, 1, 0}, {1, 0, 1, 1},
+                               {0, 1, 1, 0}, {0, 0, 1, 1}, {0, 0, 0, 2}, {1, 0, 0, 2}, {1, 1, 0, 2}, {0, 1, 0, 2}};
+    uint64_t r = 0;
+    for (int e = 0; e < 12; ++e)
+        r |= (uint64_t)(es[e][0] | es[e][1] << 1 | es[e][2] << 2 | es[e][3] << 3) << (5 * e);
+    return r;
+}
+constexpr uint64_t kEdgeShifts = pack_edge_shifts();
 
 // Block-wide exclusive scan of one int per thread (blockDim / 64 waves of 64, <= 16).
 __device__ inline int block_exclusive_scan(int v, int* scratch /* >= blockDim / 64 ints */, int& total) {
@@ -142,8 +206,8 @@ struct MeshLocal {
 };
 
 template <int RT>
-__device__ void classify_mesh(const uint8_t* __restrict__ flag, MeshLocal<RT>& ml, const Dims<RT>& d, int& nverts,
-                              int& ntris, int& tstart) {
+__device__ void classify_mesh(const uint8_t* __restrict__ flag, MeshLocal<RT>& ml, const McLds& mc, const Dims<RT>& d,
+                              int& nverts, int& ntris, int& tstart) {
     const int R = d.R, C = d.C;
     for (int i = threadIdx.x; i < C * C * C; i += blockDim.x) {
         const int cx = i % C - 1, cy = (i / C) % C - 1, cz = i / (C * C) - 1;
@@ -183,7 +247,7 @@ __device__ void classify_mesh(const uint8_t* __restrict__ flag, MeshLocal<RT>& m
         ml.emask[p] = (uint8_t)m;
         vsum += __popc(m);
         const uint16_t c = ml.cube[d.cidx(x, y, z)];
-        if (c & 0x100) tsum += mqr_tri_count[c & 0xff];
+        if (c & 0x100) tsum += mc.count[c & 0xff];
     }
     int vtot, ttot;
     int voff = block_exclusive_scan(vsum, ml.scratch, vtot);
@@ -209,16 +273,18 @@ __global__ __launch_bounds__(kThreads) void k_mesh_count(const int32_t* __restri
                                                          int32_t* vcount, int32_t* tcount, uint32_t* faces) {
     __shared__ FlagTile<RT> tl;
     __shared__ MeshLocal<RT> ml;
+    __shared__ McLds mc;
     __shared__ int32_t nbrow[27];
     const Dims<RT> d(Rrt);
     const int R = d.R;
     const int64_t b = blockIdx.x;
     if (threadIdx.x < 27) nbrow[threadIdx.x] = nb[b * 27 + threadIdx.x];
+    load_mc_tables(mc, false);
     __syncthreads();
     load_tile<RT, false>(tl.flag, nullptr, nbrow, pool, d, thr);
     __syncthreads();
     int nv, nt, ts;
-    classify_mesh<RT>(tl.flag, ml, d, nv, nt, ts);
+    classify_mesh<RT>(tl.flag, ml, mc, d, nv, nt, ts);
     if (threadIdx.x == 0) {
         vcount[b] = nv;
         tcount[b] = nt;
@@ -265,6 +331,7 @@ __global__ __launch_bounds__(kThreads) void k_mesh_emit(const int32_t* __restric
                                                         int32_t* tri) {
     __shared__ Tile<RT> tl;
     __shared__ MeshLocal<RT> ml;
+    __shared__ McLds mc;
     __shared__ int32_t nbrow[27];
     __shared__ int32_t nbvoff[27];
     const int64_t b = blockIdx.x;
@@ -276,11 +343,12 @@ __global__ __launch_bounds__(kThreads) void k_mesh_emit(const int32_t* __restric
         nbrow[threadIdx.x] = q;
         nbvoff[threadIdx.x] = q >= 0 ? voff[q] : 0;
     }
+    load_mc_tables(mc, true);
     __syncthreads();
     load_tile<RT, true>(tl.flag, tl.tsdf, nbrow, pool, d, thr);
     __syncthreads();
     int nv, nt, tstart;
-    classify_mesh<RT>(tl.flag, ml, d, nv, nt, tstart);
+    classify_mesh<RT>(tl.flag, ml, mc, d, nv, nt, tstart);
     const int R3 = R * R * R;
     const int RR = R * R;
     int xb, yb, zb;
@@ -318,13 +386,14 @@ __global__ __launch_bounds__(kThreads) void k_mesh_emit(const int32_t* __restric
         const uint16_t c = ml.cube[d.cidx(x, y, z)];
         if (!(c & 0x100)) continue;
         const int ci = c & 0xff;
+        const int8_t* trow = mc.tri + ci * 16;
         for (int r = 0; r < 16; r += 3) {
-            if (mqr_tri_table[ci][r] == -1) break;
+            if (trow[r] == -1) break;
             for (int k = 0; k < 3; ++k) {
-                const int edge = mqr_tri_table[ci][r + k];
-                const int ox = x + mqr_edge_shifts[edge][0], oy = y + mqr_edge_shifts[edge][1],
-                          oz = z + mqr_edge_shifts[edge][2];
-                const int axis = mqr_edge_shifts[edge][3];
+                const int edge = trow[r + k];
+                const uint32_t es = (uint32_t)(kEdgeShifts >> (5 * edge));
+                const int ox = x + (int)(es & 1u), oy = y + (int)((es >> 1) & 1u), oz = z + (int)((es >> 2) & 1u);
+                const int axis = (int)((es >> 3) & 3u);
                 int32_t vid;
                 if (ox < R && oy < R && oz < R) {
                     const int q = (oz * R + oy) * R + ox;
@@ -350,6 +419,358 @@ __global__ __launch_bounds__(kThreads) void k_mesh_emit(const int32_t* __restric
                 tri[3 * (int64_t)t + (2 - k)] = vid;
             }
             ++t;
+        }
+    }
+}
+
+// ================================================================ bit-row marching cubes (R = 8 / 16)
+// The tile's per-voxel predicates are kept as bit rows: for tile row q = (z + 1) * S + (y + 1),
+// bit (x + 1) of rowV[q] / rowN[q] is "weight > thr" / "tsdf < 0" of voxel x in [-1, R + 1]
+// (absent voxels: 0, 0).  Cube validity (AND of the four corner rows and of adjacent bits), the cube
+// index and the owned crossing edges of a whole x-row then take a few word operations instead of
+// per-voxel byte lookups in LDS (which the byte-granular bank conflicts made the bottleneck of the
+// per-voxel kernels above: SQ_LDS_IDX_ACTIVE ~ 80 % of k_mesh_count's time).  Vertices and
+// triangles are emitted by a balanced thread-per-output loop (binary search over the per-row
+// prefix), in the same (block, voxel, edge) / (block, cube, triangle) order as the kernels above.
+template <int R>
+struct Mc {
+    static constexpr int S = R + 3, S2 = S * S, C = R + 1, C2 = C * C, R2 = R * R, R3 = R * R * R;
+    static constexpr int RPW = 64 / R;                 // tile rows per wave-wide ballot
+    static constexpr int NG = (S2 + RPW - 1) / RPW;    // ballot groups
+    static constexpr int NW = kThreads / 64;
+    static constexpr int NIT = (NG + NW - 1) / NW;     // ballot groups per wave
+    static constexpr uint32_t RMASK = (1u << R) - 1;
+    static constexpr uint32_t CMASK = (1u << C) - 1;
+    static_assert(R == 8 || R == 16, "bit-row kernels: R = 8 or 16");
+    static_assert(R2 <= kThreads, "one thread per voxel row");
+    __device__ static int q(int y, int z) { return (z + 1) * S + (y + 1); }
+    __device__ static int c(int y, int z) { return (z + 1) * C + (y + 1); }
+    __device__ static int t(int x, int y, int z) { return q(y, z) * S + (x + 1); }
+    __device__ static int blk(int v) { return v < 0 ? -1 : (v >= R ? 1 : 0); }
+    __device__ static int k27(int x, int y, int z) { return (blk(x) + 1) + 3 * (blk(y) + 1) + 9 * (blk(z) + 1); }
+};
+
+// Stage the bit rows (and, for the emit pass, the tsdf tile [-1, R+1]^3).  Columns x in [0, R) come
+// from row-contiguous loads combined by wave ballots; the halo columns x = -1, R, R+1 are loaded by
+// one thread per tile row.  All loads of a thread are issued before any LDS write.
+template <int R, bool TSDF>
+__device__ void mc_stage(const int32_t* __restrict__ nbrow, const float2* __restrict__ pool, float thr,
+                         uint32_t* rowV, uint32_t* rowN, float* tile) {
+    using M = Mc<R>;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    float2 h[3] = {make_float2(0.f, 0.f), make_float2(0.f, 0.f), make_float2(0.f, 0.f)};
+    uint32_t hp = 0;
+    if (tid < M::S2) {
+        const int ty = tid % M::S - 1, tz = tid / M::S - 1;
+        const int dy = M::blk(ty), dz = M::blk(tz);
+#pragma unroll
+        for (int s = 0; s < 3; ++s) {
+            const int x = s == 0 ? -1 : R + s - 1, dx = s == 0 ? -1 : 1;
+            const int nbuf = nbrow[(dx + 1) + 3 * (dy + 1) + 9 * (dz + 1)];
+            if (nbuf >= 0) {
+                h[s] = pool[(int64_t)nbuf * M::R3 + ((tz - dz * R) * R + (ty - dy * R)) * R + (x - dx * R)];
+                hp |= 1u << s;
+            }
+        }
+    }
+    float2 mv[M::NIT];
+    uint32_t mp = 0;
+#pragma unroll
+    for (int it = 0; it < M::NIT; ++it) {
+        const int g = wave + it * M::NW;
+        const int qq = g * M::RPW + lane / R;
+        mv[it] = make_float2(0.f, 0.f);
+        if (g < M::NG && qq < M::S2) {
+            const int ty = qq % M::S - 1, tz = qq / M::S - 1;
+            const int dy = M::blk(ty), dz = M::blk(tz);
+            const int nbuf = nbrow[1 + 3 * (dy + 1) + 9 * (dz + 1)];
+            if (nbuf >= 0) {
+                mv[it] = pool[(int64_t)nbuf * M::R3 + ((tz - dz * R) * R + (ty - dy * R)) * R + lane % R];
+                mp |= 1u << it;
+            }
+        }
+    }
+#pragma unroll
+    for (int it = 0; it < M::NIT; ++it) {
+        const int g = wave + it * M::NW;
+        if (g >= M::NG) break;  // wave-uniform
+        const int qq = g * M::RPW + lane / R;
+        const bool p = (mp >> it) & 1u;
+        const uint64_t bv = __ballot(p && mv[it].y > thr);
+        const uint64_t bn = __ballot(p && mv[it].x < 0.f);
+        if (qq < M::S2) {
+            if (lane % R == 0) {
+                rowV[qq] = (uint32_t)((bv >> lane) & M::RMASK) << 1;
+                rowN[qq] = (uint32_t)((bn >> lane) & M::RMASK) << 1;
+            }
+            if (TSDF) tile[qq * M::S + lane % R + 1] = mv[it].x;
+        }
+    }
+    __syncthreads();
+    if (tid < M::S2) {
+        uint32_t v = 0, n = 0;
+#pragma unroll
+        for (int s = 0; s < 3; ++s) {
+            const int bit = s == 0 ? 0 : R + s;
+            if ((hp >> s) & 1u) {
+                v |= (uint32_t)(h[s].y > thr) << bit;
+                n |= (uint32_t)(h[s].x < 0.f) << bit;
+            }
+        }
+        rowV[tid] |= v;
+        rowN[tid] |= n;
+        if (TSDF) {
+            tile[tid * M::S] = h[0].x;
+            tile[tid * M::S + R + 1] = h[1].x;
+            tile[tid * M::S + R + 2] = h[2].x;
+        }
+    }
+    __syncthreads();
+}
+
+// Surface cubes per cube row (origins y, z in [-1, R-1]): bit (x + 1) set iff the cube at origin x
+// has all 8 corners with weight > thr and an index other than 0 / 255.  (An edge with a sign change
+// next to a valid cube makes that cube mixed, so edge ownership can test these bits.)
+template <int R>
+__device__ void mc_cubes(const uint32_t* rowV, const uint32_t* rowN, uint32_t* cs) {
+    using M = Mc<R>;
+    for (int i = threadIdx.x; i < M::C2; i += blockDim.x) {
+        const int cy = i % M::C - 1, cz = i / M::C - 1;
+        const int q00 = M::q(cy, cz), q10 = M::q(cy + 1, cz), q01 = M::q(cy, cz + 1), q11 = M::q(cy + 1, cz + 1);
+        const uint32_t v4 = rowV[q00] & rowV[q10] & rowV[q01] & rowV[q11];
+        const uint32_t no = rowN[q00] | rowN[q10] | rowN[q01] | rowN[q11];
+        const uint32_t na = rowN[q00] & rowN[q10] & rowN[q01] & rowN[q11];
+        cs[i] = (v4 & (v4 >> 1)) & (no | (no >> 1)) & ~(na & (na >> 1)) & M::CMASK;
+    }
+}
+
+// Owned crossing edges (bit x = voxel x of row (y, z) owns a vertex on its +x / +y / +z edge) and
+// owned surface cubes (oc) of one voxel row.
+struct RowEdges {
+    uint32_t ex, ey, ez, oc;
+};
+
+template <int R>
+__device__ inline RowEdges mc_row(const uint32_t* rowN, const uint32_t* cs, int y, int z) {
+    using M = Mc<R>;
+    const uint32_t n0 = rowN[M::q(y, z)];
+    const uint32_t c00 = cs[M::c(y, z)], cym = cs[M::c(y - 1, z)], czm = cs[M::c(y, z - 1)];
+    const uint32_t cyzm = cs[M::c(y - 1, z - 1)];
+    RowEdges e;
+    e.ex = (((n0 ^ (n0 >> 1)) & (c00 | cym | czm | cyzm)) >> 1) & M::RMASK;  // cubes (x,y,z) (x,y-1,z) (x,y,z-1) (x,y-1,z-1)
+    const uint32_t a = c00 | czm;                                             // + the same at x - 1
+    e.ey = (((n0 ^ rowN[M::q(y + 1, z)]) & (a | (a << 1))) >> 1) & M::RMASK;
+    const uint32_t b = c00 | cym;
+    e.ez = (((n0 ^ rowN[M::q(y, z + 1)]) & (b | (b << 1))) >> 1) & M::RMASK;
+    e.oc = (c00 >> 1) & M::RMASK;
+    return e;
+}
+
+// Cube index of the cube at origin x from the four corner rows shifted right by x + 1.
+__device__ inline int mc_index(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    return (int)((a & 1) | (a & 2) | ((b & 2) << 1) | ((b & 1) << 3) | ((c & 1) << 4) | ((c & 2) << 4) |
+                 ((d & 2) << 5) | ((d & 1) << 7));
+}
+__device__ inline int mc_tri_count(int ci) { return (int)((mqr_tri_count_packed[ci >> 3] >> ((ci & 7) * 4)) & 0xFu); }
+
+template <int R>
+__device__ inline int mc_row_tris(const uint32_t* rowN, uint32_t oc, int y, int z) {
+    using M = Mc<R>;
+    const uint32_t a = rowN[M::q(y, z)], b = rowN[M::q(y + 1, z)], c = rowN[M::q(y, z + 1)];
+    const uint32_t d = rowN[M::q(y + 1, z + 1)];
+    int n = 0;
+    while (oc) {
+        const int x = __builtin_ctz(oc);
+        oc &= oc - 1;
+        n += mc_tri_count(mc_index(a >> (x + 1), b >> (x + 1), c >> (x + 1), d >> (x + 1)));
+    }
+    return n;
+}
+
+// Per-block counts + per-row vertex base and edge masks (rowinfo: {vbase | ez << 16, ex | ey << 16}),
+// which the emit pass of this block and of its -x / -y / -z neighbours read.
+template <int R>
+__global__ __launch_bounds__(kThreads) void k_mc_count(const int32_t* __restrict__ nb, const float2* __restrict__ pool,
+                                                       float thr, int32_t* vcount, int32_t* tcount, uint2* rowinfo) {
+    using M = Mc<R>;
+    __shared__ uint32_t rowV[M::S2], rowN[M::S2], cs[M::C2];
+    __shared__ int32_t nbrow[27];
+    __shared__ int scratch[16];
+    const int64_t b = blockIdx.x;
+    if (threadIdx.x < 27) nbrow[threadIdx.x] = nb[b * 27 + threadIdx.x];
+    __syncthreads();
+    mc_stage<R, false>(nbrow, pool, thr, rowV, rowN, nullptr);
+    mc_cubes<R>(rowV, rowN, cs);
+    __syncthreads();
+    const int r = threadIdx.x;
+    RowEdges e{0, 0, 0, 0};
+    int nv = 0, nt = 0;
+    if (r < M::R2) {
+        e = mc_row<R>(rowN, cs, r % R, r / R);
+        nv = __popc(e.ex) + __popc(e.ey) + __popc(e.ez);
+        nt = mc_row_tris<R>(rowN, e.oc, r % R, r / R);
+    }
+    int vtot, ttot;
+    const int vb = block_exclusive_scan(nv, scratch, vtot);
+    block_exclusive_scan(nt, scratch + 8, ttot);
+    if (r < M::R2) rowinfo[b * M::R2 + r] = make_uint2((uint32_t)vb | (e.ez << 16), e.ex | (e.ey << 16));
+    if (threadIdx.x == 0) {
+        vcount[b] = vtot;
+        tcount[b] = ttot;
+    }
+}
+
+// Central-difference normal at tile point (x, y, z), components left untouched where a side's
+// block is absent (upstream DeviceGetNormal; presence is per block: bit k27 of pres).
+template <int R>
+__device__ inline void mc_normal(const float* tile, uint32_t pres, int x, int y, int z, float* n) {
+    using M = Mc<R>;
+    auto present = [&](int a, int b, int c) { return (pres >> M::k27(a, b, c)) & 1u; };
+    if (present(x + 1, y, z) && present(x - 1, y, z)) n[0] = tile[M::t(x + 1, y, z)] - tile[M::t(x - 1, y, z)];
+    if (present(x, y + 1, z) && present(x, y - 1, z)) n[1] = tile[M::t(x, y + 1, z)] - tile[M::t(x, y - 1, z)];
+    if (present(x, y, z + 1) && present(x, y, z - 1)) n[2] = tile[M::t(x, y, z + 1)] - tile[M::t(x, y, z - 1)];
+}
+
+// Global vertex id of the edge owned by voxel (ox, oy, oz) (may lie in a +x/+y/+z neighbour) along axis.
+__device__ inline int32_t mc_vid(uint32_t vbase, uint32_t ex, uint32_t ey, uint32_t ez, int x, int axis) {
+    const uint32_t low = (1u << x) - 1;
+    return (int32_t)(vbase + __popc(ex & low) + __popc(ey & low) + __popc(ez & low) +
+                     (axis > 0 ? (ex >> x) & 1u : 0u) + (axis > 1 ? (ey >> x) & 1u : 0u));
+}
+
+template <int R>
+__global__ __launch_bounds__(kThreads) void k_mc_emit(const int32_t* __restrict__ nb, const uint64_t* __restrict__ bkeys,
+                                                      const float2* __restrict__ pool, float voxel_size, float thr,
+                                                      const int32_t* __restrict__ vcount,
+                                                      const int32_t* __restrict__ tcount,
+                                                      const int32_t* __restrict__ voff,
+                                                      const int32_t* __restrict__ toff,
+                                                      const uint2* __restrict__ rowinfo, float* pos, float* nrm,
+                                                      int32_t* tri) {
+    using M = Mc<R>;
+    __shared__ float tile[M::S2 * M::S];
+    __shared__ uint32_t rowV[M::S2], rowN[M::S2], cs[M::C2];
+    __shared__ uint4 rows[M::R2];  // vbase, tbase, ex | ey << 16, ez | oc << 16
+    __shared__ int32_t nbrow[27], nbvoff[27];
+    __shared__ int scratch[16];
+    const int64_t b = blockIdx.x;
+    const int nvb = vcount[b], ntb = tcount[b];
+    if (nvb == 0 && ntb == 0) return;  // block-uniform: nothing to write
+    if (threadIdx.x < 27) {
+        const int32_t q = nb[b * 27 + threadIdx.x];
+        nbrow[threadIdx.x] = q;
+        nbvoff[threadIdx.x] = q >= 0 ? voff[q] : 0;
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const uint32_t pres = (uint32_t)__ballot(lane < 27 && nbrow[lane < 27 ? lane : 0] >= 0);
+    mc_stage<R, true>(nbrow, pool, thr, rowV, rowN, tile);
+    mc_cubes<R>(rowV, rowN, cs);
+    __syncthreads();
+    const int r = threadIdx.x;
+    RowEdges e{0, 0, 0, 0};
+    int nt = 0;
+    uint32_t vbase = 0;
+    if (r < M::R2) {
+        e = mc_row<R>(rowN, cs, r % R, r / R);
+        nt = mc_row_tris<R>(rowN, e.oc, r % R, r / R);
+        vbase = rowinfo[b * M::R2 + r].x & 0xffffu;
+    }
+    int ttot;
+    const int tb = block_exclusive_scan(nt, scratch, ttot);
+    if (r < M::R2) rows[r] = make_uint4(vbase, (uint32_t)tb, e.ex | (e.ey << 16), e.ez | (e.oc << 16));
+    __syncthreads();
+
+    int xb, yb, zb;
+    unpack_key(bkeys[b], xb, yb, zb);
+    const int32_t vb0 = voff[b], tb0 = toff[b];
+    for (int i = threadIdx.x; i < nvb; i += blockDim.x) {
+        int lo = 0, hi = M::R2 - 1;  // last row whose vertex base is <= i (non-empty)
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if ((int)rows[mid].x <= i) lo = mid; else hi = mid - 1;
+        }
+        const uint4 rw = rows[lo];
+        const uint32_t ex = rw.z & 0xffffu, ey = rw.z >> 16, ez = rw.w & 0xffffu;
+        int k = i - (int)rw.x, x = 0;
+        for (; x < R; ++x) {
+            const int c = (int)(((ex >> x) & 1u) + ((ey >> x) & 1u) + ((ez >> x) & 1u));
+            if (k < c) break;
+            k -= c;
+        }
+        const uint32_t m3 = ((ex >> x) & 1u) | (((ey >> x) & 1u) << 1) | (((ez >> x) & 1u) << 2);
+        const int y = lo % R, z = lo / R;
+        const float tsdf_o = tile[M::t(x, y, z)];
+        float no[3] = {0.f, 0.f, 0.f}, ne[3] = {0.f, 0.f, 0.f};
+        mc_normal<R>(tile, pres, x, y, z, no);
+        // upstream keeps one per-voxel normal scratch across the voxel's edges: replay the earlier ones
+        uint32_t mm = m3;
+        int axis = 0;
+        for (int j = 0;; ++j) {
+            axis = __builtin_ctz(mm);
+            mc_normal<R>(tile, pres, x + (axis == 0), y + (axis == 1), z + (axis == 2), ne);
+            if (j == k) break;
+            mm &= mm - 1;
+        }
+        const int ex_ = x + (axis == 0), ey_ = y + (axis == 1), ez_ = z + (axis == 2);
+        const float tsdf_e = tile[M::t(ex_, ey_, ez_)];
+        const float ratio = (0 - tsdf_o) / (tsdf_e - tsdf_o);
+        const float rx = ratio * (int)(axis == 0), ry = ratio * (int)(axis == 1), rz = ratio * (int)(axis == 2);
+        const int gx = xb * R + x, gy = yb * R + y, gz = zb * R + z;
+        const int64_t id = (int64_t)vb0 + i;
+        pos[3 * id + 0] = voxel_size * (gx + rx);
+        pos[3 * id + 1] = voxel_size * (gy + ry);
+        pos[3 * id + 2] = voxel_size * (gz + rz);
+        const float nx = (1 - ratio) * no[0] + ratio * ne[0];
+        const float ny = (1 - ratio) * no[1] + ratio * ne[1];
+        const float nz = (1 - ratio) * no[2] + ratio * ne[2];
+        write_normal(nx, ny, nz, nrm + 3 * id);
+    }
+    for (int i = threadIdx.x; i < ntb; i += blockDim.x) {
+        int lo = 0, hi = M::R2 - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if ((int)rows[mid].y <= i) lo = mid; else hi = mid - 1;
+        }
+        const uint4 rw = rows[lo];
+        const int y = lo % R, z = lo / R;
+        const uint32_t a = rowN[M::q(y, z)], bb = rowN[M::q(y + 1, z)], c = rowN[M::q(y, z + 1)];
+        const uint32_t d = rowN[M::q(y + 1, z + 1)];
+        uint32_t oc = rw.w >> 16;
+        int k = i - (int)rw.y, x = 0, ci = 0;
+        while (oc) {
+            x = __builtin_ctz(oc);
+            ci = mc_index(a >> (x + 1), bb >> (x + 1), c >> (x + 1), d >> (x + 1));
+            const int n = mc_tri_count(ci);
+            if (k < n) break;
+            k -= n;
+            oc &= oc - 1;
+        }
+        const uint64_t te = mqr_tri_packed[ci] >> (12 * k);
+        const int64_t t = (int64_t)tb0 + i;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const int edge = (int)((te >> (4 * j)) & 0xFu);
+            const uint32_t es = (uint32_t)(kEdgeShifts >> (5 * edge));
+            const int ox = x + (int)(es & 1u), oy = y + (int)((es >> 1) & 1u), oz = z + (int)((es >> 2) & 1u);
+            const int axis = (int)((es >> 3) & 3u);
+            int32_t vid;
+            if (ox < R && oy < R && oz < R) {
+                const uint4 ow = rows[oz * R + oy];
+                vid = vb0 + mc_vid(ow.x, ow.z & 0xffffu, ow.z >> 16, ow.w & 0xffffu, ox, axis);
+            } else {
+                const int dx = ox >= R, dy = oy >= R, dz = oz >= R;
+                const int k27 = (dx + 1) + 3 * (dy + 1) + 9 * (dz + 1);
+                const int32_t nbuf = nbrow[k27];
+                if (nbuf < 0) {
+                    vid = -1;  // cannot happen for a valid cube (all corners exist); stay in bounds
+                } else {
+                    const int lx = ox - dx * R, ly = oy - dy * R, lz = oz - dz * R;
+                    const uint2 ri = rowinfo[(int64_t)nbuf * M::R2 + lz * R + ly];
+                    vid = nbvoff[k27] + mc_vid(ri.x & 0xffffu, ri.y & 0xffffu, ri.y >> 16, ri.x >> 16, lx, axis);
+                }
+            }
+            tri[3 * t + (2 - j)] = vid;
         }
     }
 }
@@ -497,8 +918,13 @@ static int build_nb(mqr_vbg* v, int32_t* nb) {
 template <int RT>
 static int mesh_passes(mqr_vbg* v, float thr, const ExScratch& e, mqr_geom* g) {
     const int64_t n = v->pool_count;
-    hipLaunchKernelGGL(k_mesh_count<RT>, dim3((unsigned)n), dim3(kThreads), 0, v->stream, e.nb, n, v->pool, v->R,
-                       thr, e.c0, e.c1, e.faces);
+    uint2* rowinfo = reinterpret_cast<uint2*>(e.faces);  // R^2 uint2 per block fit in the 3 R^2 u32 faces slot
+    if constexpr (RT > 0)
+        hipLaunchKernelGGL(k_mc_count<RT>, dim3((unsigned)n), dim3(kThreads), 0, v->stream, e.nb, v->pool, thr, e.c0,
+                           e.c1, rowinfo);
+    else
+        hipLaunchKernelGGL(k_mesh_count<RT>, dim3((unsigned)n), dim3(kThreads), 0, v->stream, e.nb, n, v->pool, v->R,
+                           thr, e.c0, e.c1, e.faces);
     MQR_CHECK_HIP(hipGetLastError());
     int64_t nv = 0, nt = 0;
     if (scan_totals(v, e, n, 2, &nv, &nt)) return 1;
@@ -508,8 +934,12 @@ static int mesh_passes(mqr_vbg* v, float thr, const ExScratch& e, mqr_geom* g) {
     MQR_CHECK_HIP(hipMalloc(&g->pos, sizeof(float) * 3 * std::max<int64_t>(nv, 1)));
     MQR_CHECK_HIP(hipMalloc(&g->nrm, sizeof(float) * 3 * std::max<int64_t>(nv, 1)));
     MQR_CHECK_HIP(hipMalloc(&g->tri, sizeof(int32_t) * 3 * std::max<int64_t>(nt, 1)));
-    hipLaunchKernelGGL(k_mesh_emit<RT>, dim3((unsigned)n), dim3(kThreads), 0, v->stream, e.nb, n, v->bkeys, v->pool,
-                       v->R, v->voxel_size, thr, e.c0, e.c1, e.o0, e.o1, e.faces, g->pos, g->nrm, g->tri);
+    if constexpr (RT > 0)
+        hipLaunchKernelGGL(k_mc_emit<RT>, dim3((unsigned)n), dim3(kThreads), 0, v->stream, e.nb, v->bkeys, v->pool,
+                           v->voxel_size, thr, e.c0, e.c1, e.o0, e.o1, rowinfo, g->pos, g->nrm, g->tri);
+    else
+        hipLaunchKernelGGL(k_mesh_emit<RT>, dim3((unsigned)n), dim3(kThreads), 0, v->stream, e.nb, n, v->bkeys,
+                           v->pool, v->R, v->voxel_size, thr, e.c0, e.c1, e.o0, e.o1, e.faces, g->pos, g->nrm, g->tri);
     MQR_CHECK_HIP(hipGetLastError());
     MQR_CHECK_HIP(hipStreamSynchronize(v->stream));
     return 0;

@@ -97,12 +97,13 @@ def test_skipped_frames_and_empty_frame_error(mqr_mod, sphere_seq):
         vbg.integrate_frames(empty, K[:1], T[:1], depth_scale=1.0, depth_max=3.0, trunc_voxel_multiplier=4.0)
 
 
-@pytest.mark.parametrize("thr", [0.0, 1.5, 3.0])
-def test_mesh_matches_oracle(mqr_mod, room_seq, thr):
-    vbg = mqr_mod.VoxelBlockGrid(voxel_size=0.01, block_resolution=16, block_count=512)
+# R = 16 / 8: bit-row kernels (k_mc_count / k_mc_emit); R = 12: runtime-R per-voxel kernels
+@pytest.mark.parametrize("R,thr", [(16, 0.0), (16, 1.5), (16, 3.0), (8, 1.5), (8, 0.0), (12, 1.5)])
+def test_mesh_matches_oracle(mqr_mod, room_seq, R, thr):
+    vbg = mqr_mod.VoxelBlockGrid(voxel_size=0.01, block_resolution=R, block_count=512)
     vbg.integrate_frames(room_seq["depth"], room_seq["K"], room_seq["T_wc"], depth_scale=1.0, depth_max=4.0,
                          trunc_voxel_multiplier=10.0)
-    ref = _oracle_run(room_seq, 0.01, 16, 4.0, 10.0)
+    ref = _oracle_run(room_seq, 0.01, R, 4.0, 10.0)
     mesh = vbg.extract_triangle_mesh(weight_threshold=thr)
     ov, on, ot = ref.extract_mesh(thr)
     assert len(ot) > 1000

@@ -364,6 +364,19 @@ def write_header(path):
     for r in TRI_TABLE:
         lines.append("    {" + ", ".join(str(v) for v in r) + "},")
     lines.append("};")
+    # Packed forms for lane-divergent lookups (one 8-byte / 4-byte load instead of 16 / 1 byte loads):
+    # nibble j of mqr_tri_packed[ci] = tri_table[ci][j] (15 = end), nibble (ci % 8) of
+    # mqr_tri_count_packed[ci / 8] = tri_count[ci].
+    lines.append("MQR_MC_CONST unsigned long long mqr_tri_packed[256] = {")
+    packed = [sum(((v & 0xF) << (4 * j)) for j, v in enumerate(r)) for r in TRI_TABLE]
+    for i in range(0, 256, 4):
+        lines.append("    " + ", ".join("0x%016xull" % v for v in packed[i:i + 4]) + ",")
+    lines.append("};")
+    lines.append("MQR_MC_CONST unsigned int mqr_tri_count_packed[32] = {")
+    cp = [sum(TRI_COUNT[8 * i + j] << (4 * j) for j in range(8)) for i in range(32)]
+    for i in range(0, 32, 8):
+        lines.append("    " + ", ".join("0x%08xu" % v for v in cp[i:i + 8]) + ",")
+    lines.append("};")
     lines.append("#endif  // MQR_MC_TABLES_H")
     with open(path, "w") as f:
         f.write("\n".join(lines) + "\n")

@@ -17,6 +17,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--variant", type=int, default=-1, help="integrate kernel variant (-1 = library default)")
     ap.add_argument("--out", default="pmc")
+    ap.add_argument("--extract", type=int, default=0, help="extract_triangle_mesh(1.5) calls after the pack")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -41,6 +42,10 @@ def main():
     out = torch.empty((U, 4096, 2), dtype=torch.float32, device="cuda:0")
     torch.cuda.synchronize()
     vbg.pack_weighted(keys.data_ptr(), U, out.data_ptr())
+    torch.cuda.synchronize()
+    if a.extract:
+        from bench import extract_ms
+        extract_ms(vbg, 1.5, a.extract)  # device-resident mqr_extract_mesh, result freed
     torch.cuda.synchronize()
     R3 = 4096
     info = {"integrate_launches": st["integrate_launches"], "union_blocks": st["union_blocks"],
