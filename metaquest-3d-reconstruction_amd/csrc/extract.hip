@@ -432,9 +432,11 @@ __global__ __launch_bounds__(kThreads) void k_mesh_emit(const int32_t* __restric
 // per-voxel kernels above: SQ_LDS_IDX_ACTIVE ~ 80 % of k_mesh_count's time).  Vertices and
 // triangles are emitted by a balanced thread-per-output loop (binary search over the per-row
 // prefix), in the same (block, voxel, edge) / (block, cube, triangle) order as the kernels above.
-template <int R>
+// HI = 1: tile [-1, R]^3 (classification only, count pass); HI = 2: [-1, R + 1]^3 (normals, emit pass).
+template <int R, int HI>
 struct Mc {
-    static constexpr int S = R + 3, S2 = S * S, C = R + 1, C2 = C * C, R2 = R * R, R3 = R * R * R;
+    static constexpr int S = R + 1 + HI, S2 = S * S, C = R + 1, C2 = C * C, R2 = R * R, R3 = R * R * R;
+    static constexpr int NH = 1 + HI;                  // halo columns x = -1 and x = R .. R + HI - 1
     static constexpr int RPW = 64 / R;                 // tile rows per wave-wide ballot
     static constexpr int NG = (S2 + RPW - 1) / RPW;    // ballot groups
     static constexpr int NW = kThreads / 64;
@@ -442,6 +444,7 @@ struct Mc {
     static constexpr uint32_t RMASK = (1u << R) - 1;
     static constexpr uint32_t CMASK = (1u << C) - 1;
     static_assert(R == 8 || R == 16, "bit-row kernels: R = 8 or 16");
+    static_assert(HI == 1 || HI == 2, "tile upper halo: 1 or 2");
     static_assert(R2 <= kThreads, "one thread per voxel row");
     __device__ static int q(int y, int z) { return (z + 1) * S + (y + 1); }
     __device__ static int c(int y, int z) { return (z + 1) * C + (y + 1); }
@@ -453,10 +456,10 @@ struct Mc {
 // Stage the bit rows (and, for the emit pass, the tsdf tile [-1, R+1]^3).  Columns x in [0, R) come
 // from row-contiguous loads combined by wave ballots; the halo columns x = -1, R, R+1 are loaded by
 // one thread per tile row.  All loads of a thread are issued before any LDS write.
-template <int R, bool TSDF>
+template <class M, bool TSDF>
 __device__ void mc_stage(const int32_t* __restrict__ nbrow, const float2* __restrict__ pool, float thr,
                          uint32_t* rowV, uint32_t* rowN, float* tile) {
-    using M = Mc<R>;
+    constexpr int R = M::C - 1;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     float2 h[3] = {make_float2(0.f, 0.f), make_float2(0.f, 0.f), make_float2(0.f, 0.f)};
     uint32_t hp = 0;
@@ -464,7 +467,7 @@ __device__ void mc_stage(const int32_t* __restrict__ nbrow, const float2* __rest
         const int ty = tid % M::S - 1, tz = tid / M::S - 1;
         const int dy = M::blk(ty), dz = M::blk(tz);
 #pragma unroll
-        for (int s = 0; s < 3; ++s) {
+        for (int s = 0; s < M::NH; ++s) {
             const int x = s == 0 ? -1 : R + s - 1, dx = s == 0 ? -1 : 1;
             const int nbuf = nbrow[(dx + 1) + 3 * (dy + 1) + 9 * (dz + 1)];
             if (nbuf >= 0) {
@@ -510,7 +513,7 @@ __device__ void mc_stage(const int32_t* __restrict__ nbrow, const float2* __rest
     if (tid < M::S2) {
         uint32_t v = 0, n = 0;
 #pragma unroll
-        for (int s = 0; s < 3; ++s) {
+        for (int s = 0; s < M::NH; ++s) {
             const int bit = s == 0 ? 0 : R + s;
             if ((hp >> s) & 1u) {
                 v |= (uint32_t)(h[s].y > thr) << bit;
@@ -521,8 +524,8 @@ __device__ void mc_stage(const int32_t* __restrict__ nbrow, const float2* __rest
         rowN[tid] |= n;
         if (TSDF) {
             tile[tid * M::S] = h[0].x;
-            tile[tid * M::S + R + 1] = h[1].x;
-            tile[tid * M::S + R + 2] = h[2].x;
+#pragma unroll
+            for (int s = 1; s < M::NH; ++s) tile[tid * M::S + R + s] = h[s].x;
         }
     }
     __syncthreads();
@@ -531,9 +534,8 @@ __device__ void mc_stage(const int32_t* __restrict__ nbrow, const float2* __rest
 // Surface cubes per cube row (origins y, z in [-1, R-1]): bit (x + 1) set iff the cube at origin x
 // has all 8 corners with weight > thr and an index other than 0 / 255.  (An edge with a sign change
 // next to a valid cube makes that cube mixed, so edge ownership can test these bits.)
-template <int R>
+template <class M>
 __device__ void mc_cubes(const uint32_t* rowV, const uint32_t* rowN, uint32_t* cs) {
-    using M = Mc<R>;
     for (int i = threadIdx.x; i < M::C2; i += blockDim.x) {
         const int cy = i % M::C - 1, cz = i / M::C - 1;
         const int q00 = M::q(cy, cz), q10 = M::q(cy + 1, cz), q01 = M::q(cy, cz + 1), q11 = M::q(cy + 1, cz + 1);
@@ -550,9 +552,8 @@ struct RowEdges {
     uint32_t ex, ey, ez, oc;
 };
 
-template <int R>
+template <class M>
 __device__ inline RowEdges mc_row(const uint32_t* rowN, const uint32_t* cs, int y, int z) {
-    using M = Mc<R>;
     const uint32_t n0 = rowN[M::q(y, z)];
     const uint32_t c00 = cs[M::c(y, z)], cym = cs[M::c(y - 1, z)], czm = cs[M::c(y, z - 1)];
     const uint32_t cyzm = cs[M::c(y - 1, z - 1)];
@@ -573,9 +574,8 @@ __device__ inline int mc_index(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
 }
 __device__ inline int mc_tri_count(int ci) { return (int)((mqr_tri_count_packed[ci >> 3] >> ((ci & 7) * 4)) & 0xFu); }
 
-template <int R>
+template <class M>
 __device__ inline int mc_row_tris(const uint32_t* rowN, uint32_t oc, int y, int z) {
-    using M = Mc<R>;
     const uint32_t a = rowN[M::q(y, z)], b = rowN[M::q(y + 1, z)], c = rowN[M::q(y, z + 1)];
     const uint32_t d = rowN[M::q(y + 1, z + 1)];
     int n = 0;
@@ -592,23 +592,23 @@ __device__ inline int mc_row_tris(const uint32_t* rowN, uint32_t oc, int y, int 
 template <int R>
 __global__ __launch_bounds__(kThreads) void k_mc_count(const int32_t* __restrict__ nb, const float2* __restrict__ pool,
                                                        float thr, int32_t* vcount, int32_t* tcount, uint2* rowinfo) {
-    using M = Mc<R>;
+    using M = Mc<R, 1>;
     __shared__ uint32_t rowV[M::S2], rowN[M::S2], cs[M::C2];
     __shared__ int32_t nbrow[27];
     __shared__ int scratch[16];
     const int64_t b = blockIdx.x;
     if (threadIdx.x < 27) nbrow[threadIdx.x] = nb[b * 27 + threadIdx.x];
     __syncthreads();
-    mc_stage<R, false>(nbrow, pool, thr, rowV, rowN, nullptr);
-    mc_cubes<R>(rowV, rowN, cs);
+    mc_stage<M, false>(nbrow, pool, thr, rowV, rowN, nullptr);
+    mc_cubes<M>(rowV, rowN, cs);
     __syncthreads();
     const int r = threadIdx.x;
     RowEdges e{0, 0, 0, 0};
     int nv = 0, nt = 0;
     if (r < M::R2) {
-        e = mc_row<R>(rowN, cs, r % R, r / R);
+        e = mc_row<M>(rowN, cs, r % R, r / R);
         nv = __popc(e.ex) + __popc(e.ey) + __popc(e.ez);
-        nt = mc_row_tris<R>(rowN, e.oc, r % R, r / R);
+        nt = mc_row_tris<M>(rowN, e.oc, r % R, r / R);
     }
     int vtot, ttot;
     const int vb = block_exclusive_scan(nv, scratch, vtot);
@@ -622,9 +622,8 @@ __global__ __launch_bounds__(kThreads) void k_mc_count(const int32_t* __restrict
 
 // Central-difference normal at tile point (x, y, z), components left untouched where a side's
 // block is absent (upstream DeviceGetNormal; presence is per block: bit k27 of pres).
-template <int R>
+template <class M>
 __device__ inline void mc_normal(const float* tile, uint32_t pres, int x, int y, int z, float* n) {
-    using M = Mc<R>;
     auto present = [&](int a, int b, int c) { return (pres >> M::k27(a, b, c)) & 1u; };
     if (present(x + 1, y, z) && present(x - 1, y, z)) n[0] = tile[M::t(x + 1, y, z)] - tile[M::t(x - 1, y, z)];
     if (present(x, y + 1, z) && present(x, y - 1, z)) n[1] = tile[M::t(x, y + 1, z)] - tile[M::t(x, y - 1, z)];
@@ -647,7 +646,7 @@ __global__ __launch_bounds__(kThreads) void k_mc_emit(const int32_t* __restrict_
                                                       const int32_t* __restrict__ toff,
                                                       const uint2* __restrict__ rowinfo, float* pos, float* nrm,
                                                       int32_t* tri) {
-    using M = Mc<R>;
+    using M = Mc<R, 2>;
     __shared__ float tile[M::S2 * M::S];
     __shared__ uint32_t rowV[M::S2], rowN[M::S2], cs[M::C2];
     __shared__ uint4 rows[M::R2];  // vbase, tbase, ex | ey << 16, ez | oc << 16
@@ -664,16 +663,16 @@ __global__ __launch_bounds__(kThreads) void k_mc_emit(const int32_t* __restrict_
     __syncthreads();
     const int lane = threadIdx.x & 63;
     const uint32_t pres = (uint32_t)__ballot(lane < 27 && nbrow[lane < 27 ? lane : 0] >= 0);
-    mc_stage<R, true>(nbrow, pool, thr, rowV, rowN, tile);
-    mc_cubes<R>(rowV, rowN, cs);
+    mc_stage<M, true>(nbrow, pool, thr, rowV, rowN, tile);
+    mc_cubes<M>(rowV, rowN, cs);
     __syncthreads();
     const int r = threadIdx.x;
     RowEdges e{0, 0, 0, 0};
     int nt = 0;
     uint32_t vbase = 0;
     if (r < M::R2) {
-        e = mc_row<R>(rowN, cs, r % R, r / R);
-        nt = mc_row_tris<R>(rowN, e.oc, r % R, r / R);
+        e = mc_row<M>(rowN, cs, r % R, r / R);
+        nt = mc_row_tris<M>(rowN, e.oc, r % R, r / R);
         vbase = rowinfo[b * M::R2 + r].x & 0xffffu;
     }
     int ttot;
@@ -702,13 +701,13 @@ __global__ __launch_bounds__(kThreads) void k_mc_emit(const int32_t* __restrict_
         const int y = lo % R, z = lo / R;
         const float tsdf_o = tile[M::t(x, y, z)];
         float no[3] = {0.f, 0.f, 0.f}, ne[3] = {0.f, 0.f, 0.f};
-        mc_normal<R>(tile, pres, x, y, z, no);
+        mc_normal<M>(tile, pres, x, y, z, no);
         // upstream keeps one per-voxel normal scratch across the voxel's edges: replay the earlier ones
         uint32_t mm = m3;
         int axis = 0;
         for (int j = 0;; ++j) {
             axis = __builtin_ctz(mm);
-            mc_normal<R>(tile, pres, x + (axis == 0), y + (axis == 1), z + (axis == 2), ne);
+            mc_normal<M>(tile, pres, x + (axis == 0), y + (axis == 1), z + (axis == 2), ne);
             if (j == k) break;
             mm &= mm - 1;
         }
@@ -908,6 +907,18 @@ static int scan_totals(mqr_vbg* v, const ExScratch& e, int64_t n, int arrays, in
     return 0;
 }
 
+// One allocation for positions, normals and triangles (one hipMalloc instead of three).
+static int alloc_geom(mqr_geom* g, int64_t nv, int64_t nt) {
+    const size_t sv = align256(sizeof(float) * 3 * std::max<int64_t>(nv, 1));
+    const size_t st = align256(sizeof(int32_t) * 3 * std::max<int64_t>(nt, 1));
+    MQR_CHECK_HIP(hipMalloc(&g->blk, 2 * sv + st));
+    char* p = static_cast<char*>(g->blk);
+    g->pos = reinterpret_cast<float*>(p);
+    g->nrm = reinterpret_cast<float*>(p + sv);
+    g->tri = reinterpret_cast<int32_t*>(p + 2 * sv);
+    return 0;
+}
+
 static int build_nb(mqr_vbg* v, int32_t* nb) {
     const int64_t n = v->pool_count;
     hipLaunchKernelGGL(k_nb, dim3((unsigned)((n * 27 + 255) / 256)), dim3(256), 0, v->stream, v->bkeys, n, v->tab, nb);
@@ -931,9 +942,7 @@ static int mesh_passes(mqr_vbg* v, float thr, const ExScratch& e, mqr_geom* g) {
     MQR_REQUIRE(nv < (int64_t)1 << 31 && nt < (int64_t)1 << 31, "mesh exceeds int32 vertex / triangle ids");
     g->nv = nv;
     g->nt = nt;
-    MQR_CHECK_HIP(hipMalloc(&g->pos, sizeof(float) * 3 * std::max<int64_t>(nv, 1)));
-    MQR_CHECK_HIP(hipMalloc(&g->nrm, sizeof(float) * 3 * std::max<int64_t>(nv, 1)));
-    MQR_CHECK_HIP(hipMalloc(&g->tri, sizeof(int32_t) * 3 * std::max<int64_t>(nt, 1)));
+    if (alloc_geom(g, nv, nt)) return 1;
     if constexpr (RT > 0)
         hipLaunchKernelGGL(k_mc_emit<RT>, dim3((unsigned)n), dim3(kThreads), 0, v->stream, e.nb, v->bkeys, v->pool,
                            v->voxel_size, thr, e.c0, e.c1, e.o0, e.o1, rowinfo, g->pos, g->nrm, g->tri);
@@ -1023,9 +1032,13 @@ int mqr_geom_copy(mqr_geom* g, float* positions, float* normals, int32_t* triang
 int mqr_geom_free(mqr_geom* g) {
     if (!g) return 0;
     (void)hipSetDevice(g->device);
-    if (g->pos) (void)hipFree(g->pos);
-    if (g->nrm) (void)hipFree(g->nrm);
-    if (g->tri) (void)hipFree(g->tri);
+    if (g->blk) {
+        (void)hipFree(g->blk);
+    } else {
+        if (g->pos) (void)hipFree(g->pos);
+        if (g->nrm) (void)hipFree(g->nrm);
+        if (g->tri) (void)hipFree(g->tri);
+    }
     delete g;
     return 0;
 }

@@ -157,6 +157,7 @@ struct mqr_geom {
     float* pos = nullptr;
     float* nrm = nullptr;
     int32_t* tri = nullptr;
+    void* blk = nullptr;  // when set, pos / nrm / tri are carved from this one allocation
 };
 
 namespace mqr {
