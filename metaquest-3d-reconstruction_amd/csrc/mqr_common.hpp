@@ -120,6 +120,7 @@ struct mqr_vbg {
     int64_t pool_count = 0;    // host mirror (valid after each batch)
 
     int32_t* lists[2] = {nullptr, nullptr};  // batch slot lists, capacity list_cap each
+    int32_t* lpt[2] = {nullptr, nullptr};    // the same lists in longest-first order (k_lpt_order)
     int64_t list_cap = 0;
     int* counters = nullptr;   // device: 2 x kCountersTotal per-parity sets, then the pool counter
     int* h_counters = nullptr; // pinned mirror, same layout
@@ -135,6 +136,7 @@ struct mqr_vbg {
 
     int kernel_variant = 0;    // integrate kernel configuration (launch_integrate in vbg.hip), 1 = generic
     bool pipelined = true;     // overlap touch(b+1) with integrate(b)
+    bool lpt_order = true;     // integrate blocks in longest-first order
     // profiling
     bool profile = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> int_events, touch_events;

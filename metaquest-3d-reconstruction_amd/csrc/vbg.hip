@@ -79,7 +79,10 @@ static int ensure_lists(mqr_vbg* v, int64_t cap) {
     if (sync_all(v)) return 1;
     for (int p = 0; p < 2; ++p) {
         if (v->lists[p]) MQR_CHECK_HIP(hipFree(v->lists[p]));
+        if (v->lpt[p]) MQR_CHECK_HIP(hipFree(v->lpt[p]));
+        v->lists[p] = v->lpt[p] = nullptr;
         MQR_CHECK_HIP(hipMalloc(&v->lists[p], sizeof(int32_t) * cap));
+        MQR_CHECK_HIP(hipMalloc(&v->lpt[p], 2 * sizeof(int32_t) * cap));  // slots, then their masks
     }
     v->list_cap = cap;
     return 0;
@@ -245,12 +248,23 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
     const int64_t n = std::min<int64_t>(v->hctr(p)[kListCount], v->list_cap);
     if (n == 0) return 0;
     hipStream_t s = v->pipelined ? v->stream2 : v->stream;
-    if (v->pipelined) MQR_CHECK_HIP(hipStreamWaitEvent(s, v->ev_touch[p], 0));
     const unsigned grid = (unsigned)std::min<int64_t>(n, 8192);
+    const unsigned grid2 = (unsigned)std::min<int64_t>(2 * n, 16384);
     const int64_t* depth_frame = dframe_dev(v, p);
     const Table t = v->table(p);
-    const int32_t* list = v->lists[p];
     const int* counters = v->ctr(p);
+    const int32_t* list = v->lists[p];
+    const uint32_t* lmask = nullptr;
+    if (v->lpt_order && n > 1) {  // on the touch stream: overlaps the previous integrate
+        uint32_t* om = reinterpret_cast<uint32_t*>(v->lpt[p] + v->list_cap);
+        hipLaunchKernelGGL(k_lpt_order, dim3(1), dim3(1024), 0, v->stream, list, counters, v->list_cap, t.mask,
+                           v->lpt[p], om);
+        MQR_CHECK_HIP(hipGetLastError());
+        if (v->pipelined) MQR_CHECK_HIP(hipEventRecord(v->ev_touch[p], v->stream));
+        list = v->lpt[p];
+        lmask = om;
+    }
+    if (v->pipelined) MQR_CHECK_HIP(hipStreamWaitEvent(s, v->ev_touch[p], 0));
     const FrameParams* fp = v->d_fp[p];
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (v->profile) {
@@ -260,10 +274,16 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
     }
     // the unguarded division core needs its constant denominators in range (see div_rn_core)
     const bool fast_ok = !div_unsafe_host(sdf_trunc) && (depth_scale == 1.0f || !div_unsafe_host(depth_scale));
-#define MQR_LAUNCH_INT(RR, GG, SW, FAST, NT)                                                                      \
-    hipLaunchKernelGGL((k_integrate_t<RR, GG, SW, FAST, NT>), dim3(grid), dim3(NT), 0, s, list, counters,        \
+#define MQR_LAUNCH_INT(RR, GG, SW, FAST, NT) MQR_LAUNCH_INTW(RR, GG, SW, FAST, NT, 1)
+#define MQR_LAUNCH_INTW(RR, GG, SW, FAST, NT, WPE)                                                                \
+    hipLaunchKernelGGL((k_integrate_t<RR, GG, SW, FAST, NT, WPE>), dim3(grid), dim3(NT), 0, s, list, lmask,      \
+                       counters,                                                                                  \
                        v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp, depth_frame, depth_scale,      \
                        depth_max, sdf_trunc)
+#define MQR_LAUNCH_SPLIT(RR, GG, NT)                                                                              \
+    hipLaunchKernelGGL((k_integrate_t<RR, GG, 0, false, NT, 1, 2>), dim3(grid2), dim3(NT), 0, s, list, lmask,     \
+                       counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp, depth_frame,       \
+                       depth_scale, depth_max, sdf_trunc)
 #define MQR_LAUNCH_PK(RR, GG, NT)                                                                              \
     hipLaunchKernelGGL((k_integrate_pk<RR, GG, NT>), dim3(grid), dim3(NT), 0, s, list, counters, v->list_cap, t, \
                        v->pool, v->voxel_size, depths, HW, H, W, fp, depth_frame, depth_max, sdf_trunc)
@@ -273,8 +293,9 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
     // below, kept for A/B on new hardware (tools/ab_integrate.py).  FAST / packed fall back to the
     // default when their preconditions on sdf_trunc / depth_scale do not hold.
     int var = v->kernel_variant;
-    if ((var == 6 || var == 7 || var == 18 || var == 19) && !fast_ok) var = 0;
+    if ((var == 6 || var == 7 || var == 18 || var == 19 || var == 27) && !fast_ok) var = 0;
     if ((var == 8 || var == 9 || (var >= 13 && var <= 16) || var == 20) && !pk_ok) var = 0;
+    if (var >= 30 && var <= 33 && !lmask) var = 0;  // split blocks need the longest-first mask copy
     if (v->R == 16 && var != 1) {
         switch (var) {
             case 2: MQR_LAUNCH_INT(16, 4, false, false, 256); break;
@@ -298,6 +319,14 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
             case 18: MQR_LAUNCH_INT(16, 4, false, true, 512); break;
             case 19: MQR_LAUNCH_INT(16, 8, false, true, 512); break;
             case 20: MQR_LAUNCH_PK(16, 2, 512); break;
+            case 26: MQR_LAUNCH_INTW(16, 4, false, false, 512, 8); break;
+            case 30: MQR_LAUNCH_SPLIT(16, 4, 256); break;
+            case 31: MQR_LAUNCH_SPLIT(16, 4, 512); break;
+            case 32: MQR_LAUNCH_SPLIT(16, 8, 256); break;
+            case 33: MQR_LAUNCH_SPLIT(16, 2, 512); break;
+            case 27: MQR_LAUNCH_INTW(16, 4, false, true, 512, 8); break;
+            case 28: MQR_LAUNCH_INTW(16, 8, false, false, 512, 8); break;
+            case 29: MQR_LAUNCH_INTW(16, 2, false, false, 256, 8); break;
             // default: 512 threads x 8 voxels, gathers in groups of 4 (fastest on MI355X)
             default: MQR_LAUNCH_INT(16, 4, false, false, 512); break;
         }
@@ -312,6 +341,8 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
         hipLaunchKernelGGL(k_integrate, dim3(grid), dim3(256), 0, s, list, counters, v->list_cap, t, v->pool, v->R,
                            v->voxel_size, depths, HW, H, W, fp, depth_frame, depth_scale, depth_max, sdf_trunc);
 #undef MQR_LAUNCH_INT
+#undef MQR_LAUNCH_INTW
+#undef MQR_LAUNCH_SPLIT
 #undef MQR_LAUNCH_PK
     MQR_CHECK_HIP(hipGetLastError());
     if (v->profile) {
@@ -472,6 +503,7 @@ int mqr_vbg_destroy(mqr_vbg* v) {
     if (v->bkeys) (void)hipFree(v->bkeys);
     for (int p = 0; p < 2; ++p) {
         if (v->lists[p]) (void)hipFree(v->lists[p]);
+        if (v->lpt[p]) (void)hipFree(v->lpt[p]);
         if (v->d_fp[p]) (void)hipFree(v->d_fp[p]);
         if (v->h_fp[p]) (void)hipHostFree(v->h_fp[p]);
         if (v->d_depth[p]) (void)hipFree(v->d_depth[p]);
@@ -769,6 +801,7 @@ int mqr_vbg_set_variant(mqr_vbg* v, int variant) {
     if (sync_all(v)) return 1;
     v->kernel_variant = variant & 0xff;
     v->pipelined = (variant & 0x100) == 0;  // bit 8: serialise touch and integrate (A/B of the overlap)
+    v->lpt_order = (variant & 0x200) == 0;  // bit 9: integrate in touch order instead of longest-first
     return 0;
 }
 

@@ -347,8 +347,14 @@ __device__ __forceinline__ bool integrate_column(float2 (&tw)[ZPER], uint32_t& d
 // order, so the result is bit-identical to k_integrate.  FAST: unguarded division core with a
 // block-level exact re-run when any operand is out of its range (host guarantees sdf_trunc and
 // depth_scale are in range).
-template <int R, int G, int SWZ = 0, bool FAST = false, int NT = 256>
-__global__ __launch_bounds__(NT) void k_integrate_t(const int32_t* __restrict__ list, const int* __restrict__ counters,
+//
+// SPLIT > 1: SPLIT workgroups per block, each on R / SPLIT consecutive z-layers (finer grain for the
+// longest-first schedule); needs lmask, the batch masks in list order (k_lpt_order), because the
+// part-0 workgroup clears the table mask while its sibling may not have read it yet.
+template <int R, int G, int SWZ = 0, bool FAST = false, int NT = 256, int WPE = 1, int SPLIT = 1>
+__global__ __launch_bounds__(NT, WPE) void k_integrate_t(const int32_t* __restrict__ list,
+                                                     const uint32_t* __restrict__ lmask,
+                                                     const int* __restrict__ counters,
                                                      int64_t list_cap, Table t, float2* __restrict__ pool,
                                                      float voxel_size, const float* __restrict__ depths, int64_t HW,
                                                      int H, int W, const FrameParams* __restrict__ fps,
@@ -356,24 +362,28 @@ __global__ __launch_bounds__(NT) void k_integrate_t(const int32_t* __restrict__ 
                                                      float depth_max, float sdf_trunc) {
     constexpr int R2 = R * R;
     constexpr int R3 = R2 * R;
-    constexpr int ZPER = R3 / NT;          // voxels per thread (16 at R=16, NT=256; 2 at R=8)
-    constexpr int ZSTEP = NT / R2;         // z stride between a thread's voxels (1 at R=16, NT=256)
-    static_assert(R3 % NT == 0 && NT % R2 == 0, "NT must divide R^3 and be a multiple of R^2");
+    constexpr int ZPER = R3 / (NT * SPLIT);  // voxels per thread (16 at R=16, NT=256; 2 at R=8)
+    constexpr int ZSTEP = NT / R2;           // z stride between a thread's voxels (1 at R=16, NT=256)
+    static_assert(R3 % (NT * SPLIT) == 0 && NT % R2 == 0, "NT * SPLIT must divide R^3, NT a multiple of R^2");
+    static_assert(SPLIT == 1 || SWZ == 0, "split blocks use the plain list order");
     static_assert(ZPER % G == 0, "group size must divide the voxels per thread");
     const bool unit_scale = depth_scale == 1.0f;  // d / 1 == d exactly: skip the division
     const int64_t n = min((int64_t)counters[kListCount], list_cap);
     const float hm1 = (float)H - 1.0f, wm1 = (float)W - 1.0f;
     const int tid = threadIdx.x;
-    const int xv = tid % R, yv = (tid / R) % R, z0 = tid / R2;
-    for (int64_t L = blockIdx.x; L < n; L += gridDim.x) {
+    const int xv = tid % R, yv = (tid / R) % R;
+    for (int64_t U = blockIdx.x; U < n * SPLIT; U += gridDim.x) {
+        const int64_t L = SPLIT > 1 ? U / SPLIT : U;
+        const int part = SPLIT > 1 ? (int)(U % SPLIT) : 0;
+        const int z0 = tid / R2 + part * (R / SPLIT);
         const int64_t i = SWZ > 0 ? xcd_swizzle<(SWZ > 0 ? SWZ : 1)>(L, n) : L;
         const int32_t slot = list[i];
         const int buf = t.vals[slot];
-        const uint32_t mask = __builtin_amdgcn_readfirstlane(t.mask[slot]);
+        const uint32_t mask = __builtin_amdgcn_readfirstlane(lmask ? lmask[i] : t.mask[slot]);
         int xb, yb, zb;
         unpack_key(t.keys[slot], xb, yb, zb);
         if (buf >= 0) {
-            float2* vox = pool + (int64_t)buf * R3;
+            float2* vox = pool + (int64_t)buf * R3 + part * (R3 / SPLIT);
             float2 tw[ZPER];
             float zs[ZPER];
 #pragma unroll
@@ -399,7 +409,38 @@ __global__ __launch_bounds__(NT) void k_integrate_t(const int32_t* __restrict__ 
                 if (dirty & (1u << k)) vox[k * NT + tid] = tw[k];
         }
         __syncthreads();
-        if (tid == 0) t.mask[slot] = 0;
+        if (tid == 0 && part == 0) t.mask[slot] = 0;
+    }
+}
+
+// Longest-processing-time order of a batch list: counting sort by the number of the batch's frames
+// that touched each block (popcount of its slot mask), descending.  The integrate grid then ends on
+// short blocks instead of whichever long blocks the touch order happened to put last.  One
+// workgroup; order within a bin is arbitrary (blocks are independent, results unchanged).
+__global__ __launch_bounds__(1024) void k_lpt_order(const int32_t* __restrict__ list, const int* __restrict__ counters,
+                                                    int64_t list_cap, const uint32_t* __restrict__ mask,
+                                                    int32_t* __restrict__ out, uint32_t* __restrict__ out_mask) {
+    __shared__ int hist[kMaxBatch + 1];
+    const int n = (int)min((int64_t)counters[kListCount], list_cap);
+    if (threadIdx.x <= kMaxBatch) hist[threadIdx.x] = 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += blockDim.x) atomicAdd(&hist[__popc(mask[list[i]])], 1);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int acc = 0;
+        for (int c = kMaxBatch; c >= 0; --c) {
+            const int h = hist[c];
+            hist[c] = acc;
+            acc += h;
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const int32_t s = list[i];
+        const uint32_t m = mask[s];
+        const int pos = atomicAdd(&hist[__popc(m)], 1);
+        out[pos] = s;
+        out_mask[pos] = m;
     }
 }
 

@@ -36,8 +36,8 @@ def test_division_shortcut_exact(b):
 
 
 INTEGRATE_VARIANTS = {16: (0, 2, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 22, 23, 24, 25, 0x100, 0x106,
-                          0x108),
-                      8: (0, 6, 8, 0x101)}
+                          0x108, 26, 27, 28, 29, 0x200, 0x300, 30, 31, 32, 33, 0x21e),
+                      8: (0, 6, 8, 0x101, 0x200)}
 
 
 def test_specialised_integrate_equals_generic():
