@@ -77,6 +77,7 @@ enum Counter : int {
     kOverflow = 2,    // bit0 pool overflow, bit1 table full, bit2 list overflow, bit3 key range
     kTouched = 3,     // raw (pre-dedup) touched samples
     kFrameBlocks = 4, // sum over frames of touched blocks (per-frame unique)
+    kBadCount = 5,    // blocks the fast integrate kernel handed to the exact fix-up launch
     kNumCounters = 8
 };
 
@@ -121,6 +122,7 @@ struct mqr_vbg {
 
     int32_t* lists[2] = {nullptr, nullptr};  // batch slot lists, capacity list_cap each
     int32_t* lpt[2] = {nullptr, nullptr};    // the same lists in longest-first order (k_lpt_order)
+    int32_t* bad[2] = {nullptr, nullptr};    // fast-kernel fix-up list: slots, then their masks
     int64_t list_cap = 0;
     int* counters = nullptr;   // device: 2 x kCountersTotal per-parity sets, then the pool counter
     int* h_counters = nullptr; // pinned mirror, same layout

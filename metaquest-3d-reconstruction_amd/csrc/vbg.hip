@@ -83,6 +83,9 @@ static int ensure_lists(mqr_vbg* v, int64_t cap) {
         v->lists[p] = v->lpt[p] = nullptr;
         MQR_CHECK_HIP(hipMalloc(&v->lists[p], sizeof(int32_t) * cap));
         MQR_CHECK_HIP(hipMalloc(&v->lpt[p], 2 * sizeof(int32_t) * cap));  // slots, then their masks
+        if (v->bad[p]) MQR_CHECK_HIP(hipFree(v->bad[p]));
+        v->bad[p] = nullptr;
+        MQR_CHECK_HIP(hipMalloc(&v->bad[p], 2 * sizeof(int32_t) * cap));
     }
     v->list_cap = cap;
     return 0;
@@ -252,7 +255,7 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
     const unsigned grid2 = (unsigned)std::min<int64_t>(2 * n, 16384);
     const int64_t* depth_frame = dframe_dev(v, p);
     const Table t = v->table(p);
-    const int* counters = v->ctr(p);
+    int* counters = v->ctr(p);
     const int32_t* list = v->lists[p];
     const uint32_t* lmask = nullptr;
     if (v->lpt_order && n > 1) {  // on the touch stream: overlaps the previous integrate
@@ -277,13 +280,23 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
 #define MQR_LAUNCH_INT(RR, GG, SW, FAST, NT) MQR_LAUNCH_INTW(RR, GG, SW, FAST, NT, 1)
 #define MQR_LAUNCH_INTW(RR, GG, SW, FAST, NT, WPE)                                                                \
     hipLaunchKernelGGL((k_integrate_t<RR, GG, SW, FAST, NT, WPE>), dim3(grid), dim3(NT), 0, s, list, lmask,      \
-                       counters,                                                                                  \
+                       (int32_t*)nullptr, counters,                                                               \
                        v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp, depth_frame, depth_scale,      \
                        depth_max, sdf_trunc)
 #define MQR_LAUNCH_SPLIT(RR, GG, NT)                                                                              \
     hipLaunchKernelGGL((k_integrate_t<RR, GG, 0, false, NT, 1, 2>), dim3(grid2), dim3(NT), 0, s, list, lmask,     \
-                       counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp, depth_frame,       \
+                       (int32_t*)nullptr, counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp, depth_frame,       \
                        depth_scale, depth_max, sdf_trunc)
+// fast kernel + exact fix-up launch over the blocks it handed back (usually none: the fix-up grid
+// reads a zero count and exits).  counters + (kBadCount - kListCount): the fix-up's list length.
+#define MQR_LAUNCH_FIX(RR, GG, NT, WPE)                                                                           \
+    hipLaunchKernelGGL((k_integrate_t<RR, GG, 0, true, NT, WPE, 1, true>), dim3(grid), dim3(NT), 0, s, list, lmask, \
+                       v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp,        \
+                       depth_frame, depth_scale, depth_max, sdf_trunc);                                            \
+    hipLaunchKernelGGL((k_integrate_t<RR, 4, 0, false, 512>), dim3(64), dim3(512), 0, s, v->bad[p],                \
+                       reinterpret_cast<const uint32_t*>(v->bad[p] + v->list_cap), (int32_t*)nullptr,             \
+                       counters + (kBadCount - kListCount), v->list_cap, t, v->pool, v->voxel_size, depths, HW,   \
+                       H, W, fp, depth_frame, depth_scale, depth_max, sdf_trunc)
 #define MQR_LAUNCH_PK(RR, GG, NT)                                                                              \
     hipLaunchKernelGGL((k_integrate_pk<RR, GG, NT>), dim3(grid), dim3(NT), 0, s, list, counters, v->list_cap, t, \
                        v->pool, v->voxel_size, depths, HW, H, W, fp, depth_frame, depth_max, sdf_trunc)
@@ -293,7 +306,8 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
     // below, kept for A/B on new hardware (tools/ab_integrate.py).  FAST / packed fall back to the
     // default when their preconditions on sdf_trunc / depth_scale do not hold.
     int var = v->kernel_variant;
-    if ((var == 6 || var == 7 || var == 18 || var == 19 || var == 27) && !fast_ok) var = 0;
+    if ((var == 6 || var == 7 || var == 18 || var == 19 || var == 27 || (var >= 34 && var <= 37)) && !fast_ok)
+        var = 0;
     if ((var == 8 || var == 9 || (var >= 13 && var <= 16) || var == 20) && !pk_ok) var = 0;
     if (var >= 30 && var <= 33 && !lmask) var = 0;  // split blocks need the longest-first mask copy
     if (v->R == 16 && var != 1) {
@@ -321,6 +335,10 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
             case 20: MQR_LAUNCH_PK(16, 2, 512); break;
             case 26: MQR_LAUNCH_INTW(16, 4, false, false, 512, 8); break;
             case 30: MQR_LAUNCH_SPLIT(16, 4, 256); break;
+            case 34: MQR_LAUNCH_FIX(16, 4, 512, 1); break;
+            case 35: MQR_LAUNCH_FIX(16, 8, 512, 1); break;
+            case 36: MQR_LAUNCH_FIX(16, 4, 256, 1); break;
+            case 37: MQR_LAUNCH_FIX(16, 4, 512, 8); break;
             case 31: MQR_LAUNCH_SPLIT(16, 4, 512); break;
             case 32: MQR_LAUNCH_SPLIT(16, 8, 256); break;
             case 33: MQR_LAUNCH_SPLIT(16, 2, 512); break;
@@ -343,6 +361,7 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
 #undef MQR_LAUNCH_INT
 #undef MQR_LAUNCH_INTW
 #undef MQR_LAUNCH_SPLIT
+#undef MQR_LAUNCH_FIX
 #undef MQR_LAUNCH_PK
     MQR_CHECK_HIP(hipGetLastError());
     if (v->profile) {
@@ -504,6 +523,7 @@ int mqr_vbg_destroy(mqr_vbg* v) {
     for (int p = 0; p < 2; ++p) {
         if (v->lists[p]) (void)hipFree(v->lists[p]);
         if (v->lpt[p]) (void)hipFree(v->lpt[p]);
+        if (v->bad[p]) (void)hipFree(v->bad[p]);
         if (v->d_fp[p]) (void)hipFree(v->d_fp[p]);
         if (v->h_fp[p]) (void)hipHostFree(v->h_fp[p]);
         if (v->d_depth[p]) (void)hipFree(v->d_depth[p]);

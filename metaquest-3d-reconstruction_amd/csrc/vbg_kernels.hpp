@@ -351,10 +351,16 @@ __device__ __forceinline__ bool integrate_column(float2 (&tw)[ZPER], uint32_t& d
 // SPLIT > 1: SPLIT workgroups per block, each on R / SPLIT consecutive z-layers (finer grain for the
 // longest-first schedule); needs lmask, the batch masks in list order (k_lpt_order), because the
 // part-0 workgroup clears the table mask while its sibling may not have read it yet.
-template <int R, int G, int SWZ = 0, bool FAST = false, int NT = 256, int WPE = 1, int SPLIT = 1>
+//
+// FAST with bad_out != nullptr: a block whose operands left the core's exact range is not written
+// back; its (slot, mask) goes to bad_out (count at counters[kBadCount]) for an exact re-run by a
+// follow-up launch of the exact kernel over that list.  The fast kernel then carries no second,
+// exact copy of the column loop (fewer registers, no per-voxel branches).
+template <int R, int G, int SWZ = 0, bool FAST = false, int NT = 256, int WPE = 1, int SPLIT = 1, bool EXTFIX = false>
 __global__ __launch_bounds__(NT, WPE) void k_integrate_t(const int32_t* __restrict__ list,
                                                      const uint32_t* __restrict__ lmask,
-                                                     const int* __restrict__ counters,
+                                                     int32_t* __restrict__ bad_out,
+                                                     int* __restrict__ counters,
                                                      int64_t list_cap, Table t, float2* __restrict__ pool,
                                                      float voxel_size, const float* __restrict__ depths, int64_t HW,
                                                      int H, int W, const FrameParams* __restrict__ fps,
@@ -397,12 +403,21 @@ __global__ __launch_bounds__(NT, WPE) void k_integrate_t(const int32_t* __restri
             const bool bad = integrate_column<ZPER, G, !FAST>(tw, dirty, mask, zs, xs, ys, depths, HW, W, hm1, wm1,
                                                            fps, depth_frame, depth_scale, unit_scale, depth_max,
                                                            sdf_trunc);
-            if (FAST && __syncthreads_or(bad)) {  // block-uniform: redo this block exactly
+            if (FAST && __syncthreads_or(bad)) {  // block-uniform
+                if (EXTFIX) {  // hand the block to the exact fix-up launch, leave it unwritten
+                    if (tid == 0) {
+                        const int j = atomicAdd(&counters[kBadCount], 1);
+                        bad_out[j] = slot;
+                        bad_out[list_cap + j] = (int32_t)mask;
+                    }
+                    dirty = 0;
+                } else {  // redo this block exactly
 #pragma unroll
-                for (int k = 0; k < ZPER; ++k) tw[k] = vox[k * NT + tid];
-                dirty = 0;
-                integrate_column<ZPER, G, true>(tw, dirty, mask, zs, xs, ys, depths, HW, W, hm1, wm1, fps,
-                                                depth_frame, depth_scale, unit_scale, depth_max, sdf_trunc);
+                    for (int k = 0; k < ZPER; ++k) tw[k] = vox[k * NT + tid];
+                    dirty = 0;
+                    integrate_column<ZPER, G, true>(tw, dirty, mask, zs, xs, ys, depths, HW, W, hm1, wm1, fps,
+                                                    depth_frame, depth_scale, unit_scale, depth_max, sdf_trunc);
+                }
             }
 #pragma unroll
             for (int k = 0; k < ZPER; ++k)

@@ -36,7 +36,7 @@ def test_division_shortcut_exact(b):
 
 
 INTEGRATE_VARIANTS = {16: (0, 2, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 22, 23, 24, 25, 0x100, 0x106,
-                          0x108, 26, 27, 28, 29, 0x200, 0x300, 30, 31, 32, 33, 0x21e),
+                          0x108, 26, 27, 28, 29, 0x200, 0x300, 30, 31, 32, 33, 0x21e, 34, 35, 36, 37),
                       8: (0, 6, 8, 0x101, 0x200)}
 
 
@@ -70,7 +70,8 @@ def test_fast_integrate_exact_fallback():
     for d in depth_mm:
         d[::7, ::5] = np.float32(1e-30)   # in-image, > 0, below 2^-60 -> fallback
     out = []
-    for R, variant in ((16, 1), (16, 0), (16, 6), (16, 7), (16, 18), (8, 1), (8, 6)):
+    # 34 / 37: fast kernel handing out-of-range blocks to the exact fix-up launch
+    for R, variant in ((16, 1), (16, 0), (16, 6), (16, 7), (16, 18), (16, 34), (16, 37), (8, 1), (8, 6)):
         v = VoxelBlockGrid(voxel_size=0.01, block_resolution=R, block_count=64)
         _lib.call("mqr_vbg_set_variant", v.handle, variant)
         v.integrate_frames(depth_mm[:4], seq["K"][:4], seq["T_wc"][:4], depth_scale=1000.0, depth_max=4.0,
@@ -83,9 +84,9 @@ def test_fast_integrate_exact_fallback():
         v.integrate_frames(depth_mm[4:], seq["K"][4:], seq["T_wc"][4:], depth_scale=1000.0, depth_max=4.0,
                            trunc_voxel_multiplier=10.0)
         out.append(v.export())
-    for i in (1, 2, 3, 4):
+    for i in (1, 2, 3, 4, 5, 6):
         assert compare_volumes(out[0], out[i], 0.0) == 0.0
-    assert compare_volumes(out[5], out[6], 0.0) == 0.0
+    assert compare_volumes(out[7], out[8], 0.0) == 0.0
 
 
 def test_division_core_on_positive_zero():
