@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--conf-depth-max", type=float, default=4.0)
     ap.add_argument("--conf-error", type=float, default=0.08)
     ap.add_argument("--no-extras", action="store_true", help="skip confidence / copy-peak / host-input legs")
+    ap.add_argument("--merge", default="sparse", choices=["sparse", "reduce"],
+                    help="N>1 volume merge: all-to-all to union-slice owners + gather, or one dense reduce")
     return ap.parse_args()
 
 
@@ -292,15 +294,21 @@ def main():
     vbg = VoxelBlockGrid(voxel_size=args.voxel, block_resolution=args.block_resolution,
                          block_count=args.block_count, device=local)
 
+    merge_times = []
+
     def step():
         vbg.reset()
         vbg.integrate_frames(dptr, K, T, depth_scale=1.0, depth_max=args.depth_max,
                              trunc_voxel_multiplier=args.trunc)
         if world > 1:
-            merge_to_root(vbg)
+            t = time.perf_counter()
+            merge_to_root(vbg, method=args.merge)
+            torch.cuda.synchronize()
+            merge_times.append(time.perf_counter() - t)
 
     for _ in range(args.warmup):
         step()
+    merge_times.clear()
     vbg.stats(reset=True)
     vbg.profile(True)
     if dist:
@@ -379,7 +387,10 @@ def main():
                        "frames_per_gpu": B, "height": H, "width": W, "voxel_size": args.voxel,
                        "block_resolution": args.block_resolution, "depth_max": args.depth_max,
                        "trunc_voxel_multiplier": args.trunc, "frame_batch": 32,
-                       "parallelism": f"frame-shard x{world}" + (" + RCCL reduce" if world > 1 else "")},
+                       "parallelism": f"frame-shard x{world}" + (
+                           f" + RCCL merge ({args.merge})" if world > 1 else "")},
+            "merge_ms": (sum(merge_times) / len(merge_times) * 1e3) if merge_times else None,
+            "union_blocks": blocks if world > 1 else None,
             "extract_ms": ext_ms,
             "extract": {"weight_threshold": args.extract_threshold, "vertices": nv, "triangles": nt,
                         "blocks": blocks, "alg_gbs": ext_alg,

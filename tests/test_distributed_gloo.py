@@ -46,12 +46,12 @@ class NumpyVolume:
 
 def _make(rank):
     rng = np.random.default_rng(rank)
-    keys = [(0, 0, 0), (1, 0, 0)] if rank == 0 else [(1, 0, 0), (0, -1, 2)]
+    keys = [[(0, 0, 0), (1, 0, 0)], [(1, 0, 0), (0, -1, 2)], [(1, 0, 0), (5, 5, -5), (0, 0, 0)]][rank]
     return {k: (rng.uniform(-1, 1, R3).astype(np.float32), rng.integers(0, 5, R3).astype(np.float32))
             for k in keys}
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, method="reduce"):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -59,7 +59,7 @@ def _worker(rank, world, port, q):
         from mqr.distributed import merge_to_root, shard_range, union_keys
         vol = NumpyVolume(_make(rank))
         u = union_keys(vol.export_keys())
-        U = merge_to_root(vol, root=0)
+        U = merge_to_root(vol, root=0, method=method)
         q.put((rank, len(u), U, {k: (t.tolist(), w.tolist()) for k, (t, w) in vol.blocks.items()},
                shard_range(10, rank, world)))
     finally:
@@ -103,3 +103,37 @@ def test_merge_two_ranks_gloo():
     assert np.abs(got_t - want).max() < 1e-6
     # non-root keeps its own partial volume
     assert set(res[1][3]) == {(1, 0, 0), (0, -1, 2)}
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sparse_merge_gloo(world):
+    """all-to-all to the union-slice owners + gather to root == the dense reduce (uneven slices at 3)."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, "sparse")) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r = q.get(timeout=120)
+        res[r[0]] = r
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    parts = [_make(r) for r in range(world)]
+    keys = set().union(*parts)
+    assert res[0][2] == len(keys)
+    merged = res[0][3]
+    assert set(merged) == keys
+    for k in keys:
+        ws = [p[k][1] for p in parts if k in p]
+        ts = [p[k][0] for p in parts if k in p]
+        w = np.sum(ws, axis=0)
+        want = np.where(w > 0, np.sum([a * b for a, b in zip(ws, ts)], axis=0) / np.where(w > 0, w, 1), 0)
+        got_t, got_w = map(np.asarray, merged[k])
+        assert np.array_equal(got_w, w)
+        assert np.abs(got_t - want).max() < 1e-6
+    for r in range(1, world):  # non-root ranks keep their partial volumes
+        assert set(res[r][3]) == set(parts[r])

@@ -1,6 +1,6 @@
-"""Two ranks (gloo, both on GPU 0) run the real multi-GPU merge path: frame-sharded integration
-through libmqr_hip.so, key union + one sum-reduce + unpack; rank 0's volume must equal a single
-sequential pass (same keys and weights, tsdf within 1e-4)."""
+"""2-3 ranks (gloo, all on GPU 0) run the real multi-GPU merge path: frame-sharded integration
+through libmqr_hip.so, key union, then the sparse all-to-all + gather (or the dense sum-reduce) and
+unpack; rank 0's volume must equal a single sequential pass (same keys and weights, tsdf within 1e-4)."""
 import os
 import socket
 
@@ -10,7 +10,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, method):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -23,7 +23,7 @@ def _worker(rank, world, port, q):
         v = VoxelBlockGrid(voxel_size=0.01, block_resolution=16, block_count=64, device=0)
         v.integrate_frames(seq["depth"][lo:hi], seq["K"][lo:hi], seq["T_wc"][lo:hi], depth_scale=1.0,
                            depth_max=4.0, trunc_voxel_multiplier=10.0)
-        U = merge_to_root(v, root=0)
+        U = merge_to_root(v, root=0, method=method)
         if rank == 0:
             k, t, w = v.export()
             q.put((rank, U, k, t, w))
@@ -33,7 +33,8 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_two_rank_merge_on_gpu():
+@pytest.mark.parametrize("world,method", [(2, "sparse"), (2, "reduce"), (3, "sparse")])
+def test_multi_rank_merge_on_gpu(world, method):
     import oracle
     import torch.multiprocessing as mp
     from gpu_helpers import compare_volumes
@@ -44,11 +45,11 @@ def test_two_rank_merge_on_gpu():
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, method)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}
-    for _ in range(2):
+    for _ in range(world):
         r = q.get(timeout=300)
         res[r[0]] = r
     for p in procs:
@@ -60,5 +61,5 @@ def test_two_rank_merge_on_gpu():
         ref.integrate_frame(seq["depth"][i], seq["K"][i].astype(np.float64), seq["T_wc"][i].astype(np.float64),
                             1.0, 4.0, 10.0)
     _, U, k, t, w = res[0]
-    assert U == res[1][1] == ref.size()
+    assert all(res[r][1] == U for r in range(world)) and U == ref.size()
     assert compare_volumes((k, t, w), ref.export(), 1e-4) < 1e-5
