@@ -27,6 +27,7 @@
 #include <cmath>
 #include <limits>
 #include <map>
+#include <mutex>
 #include <vector>
 
 #include "mqr_common.hpp"
@@ -78,12 +79,28 @@ __global__ void k_union_edges(const uint64_t* __restrict__ keys, const int32_t* 
     }
 }
 
+// Cluster sizes: lanes of a wave mostly share one root (neighbouring triangles), so the wave adds
+// each distinct root's lane count with one atomic (per-lane atomics on the root of a 2 M-triangle
+// cluster serialised this kernel to ~20 ms).
 __global__ void k_roots(int32_t* parent, int64_t n, int32_t* count, int32_t* is_root) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const int32_t r = uf_find(parent, (int32_t)i);
-    atomicAdd(&count[r], 1);
-    is_root[i] = r == (int32_t)i;
+    const int lane = threadIdx.x & 63;
+    int32_t r = -1;
+    if (i < n) {
+        r = uf_find(parent, (int32_t)i);
+        is_root[i] = r == (int32_t)i;
+    }
+    bool todo = i < n;
+    while (true) {
+        const uint64_t pending = __ballot(todo);
+        if (!pending) break;
+        const int leader = __ffsll((unsigned long long)pending) - 1;
+        const int32_t lr = __shfl(r, leader, 64);
+        const bool same = todo && r == lr;
+        const uint64_t peers = __ballot(same);
+        if (lane == leader) atomicAdd(&count[lr], __popcll(peers));
+        if (same) todo = false;
+    }
 }
 
 // Read-only final find into a separate array: compressing `parent` in place here would race with
@@ -276,25 +293,92 @@ __global__ void k_gather_f64(const double* __restrict__ a, const int32_t* __rest
 // ------------------------------------------------------------------ host helpers
 inline unsigned nb(int64_t n) { return (unsigned)std::max<int64_t>((n + 255) / 256, 1); }
 
+// Scratch: a bump arena over one grow-only device buffer cached per device (the ~40 buffers of a
+// filter pass cost no hipMalloc / hipFree -- each hipFree synchronises the device, and the
+// stream-ordered pool still spent ~66 us per hipFreeAsync); release() pops the top allocation.
+// Requests past the arena fall back to hipMallocAsync.  One call owns the cached arena at a time
+// (a concurrent call on another thread gets a private one).
+struct Arena {
+    char* base = nullptr;
+    size_t cap = 0;
+    bool busy = false;
+    hipStream_t s = nullptr;  // cached with the arena: creating a stream costs ~2 ms
+};
+static std::mutex g_arena_mu;
+static Arena g_arena[64];
+
 struct Ctx {
     hipStream_t s = nullptr;
-    std::vector<void*> owned;
+    int device = 0;
+    Arena* ar = nullptr;
+    Arena priv;
+    size_t top = 0;
+    std::vector<std::pair<size_t, size_t>> stack;  // (offset, size) of live arena allocations
+    std::vector<void*> owned;                        // fallback allocations
+
+    int open(int dev, size_t want) {
+        device = dev;
+        {
+            std::lock_guard<std::mutex> lk(g_arena_mu);
+            if (dev >= 0 && dev < 64 && !g_arena[dev].busy) {
+                ar = &g_arena[dev];
+                ar->busy = true;
+            }
+        }
+        if (!ar) ar = &priv;
+        if (!ar->s && hipStreamCreateWithFlags(&ar->s, hipStreamNonBlocking) != hipSuccess) return 1;
+        s = ar->s;
+        if (ar->cap < want) {
+            if (ar->base) (void)hipFree(ar->base);
+            ar->base = nullptr;
+            ar->cap = 0;
+            if (hipMalloc(&ar->base, want) != hipSuccess) return 1;
+            ar->cap = want;
+        }
+        return 0;
+    }
     template <class T>
     T* alloc(int64_t n) {
+        const size_t bytes = (sizeof(T) * (size_t)std::max<int64_t>(n, 1) + 255) & ~(size_t)255;
+        if (ar && top + bytes <= ar->cap) {
+            stack.emplace_back(top, bytes);
+            void* p = ar->base + top;
+            top += bytes;
+            return static_cast<T*>(p);
+        }
         void* p = nullptr;
-        if (hipMalloc(&p, sizeof(T) * std::max<int64_t>(n, 1)) != hipSuccess) return nullptr;
+        if (hipMallocAsync(&p, bytes, s) != hipSuccess) return nullptr;
         owned.push_back(p);
         return static_cast<T*>(p);
     }
     void release(void* p) {
+        if (ar && p >= (void*)ar->base && p < (void*)(ar->base + ar->cap)) {
+            const size_t off = static_cast<char*>(p) - ar->base;
+            for (size_t i = stack.size(); i-- > 0;)
+                if (stack[i].first == off) {
+                    stack.erase(stack.begin() + (std::ptrdiff_t)i);
+                    break;
+                }
+            top = stack.empty() ? 0 : stack.back().first + stack.back().second;  // pops freed tops
+            return;
+        }
         auto it = std::find(owned.begin(), owned.end(), p);
         if (it != owned.end()) {
-            (void)hipFree(p);
+            (void)hipFreeAsync(p, s);
             owned.erase(it);
         }
     }
     ~Ctx() {
-        for (void* p : owned) (void)hipFree(p);
+        if (!s) return;
+        for (void* p : owned) (void)hipFreeAsync(p, s);
+        (void)hipStreamSynchronize(s);
+        if (ar == &priv) {
+            if (priv.base) (void)hipFree(priv.base);
+            (void)hipStreamDestroy(priv.s);
+        } else if (ar) {
+            std::lock_guard<std::mutex> lk(g_arena_mu);
+            ar->busy = false;
+        }
     }
 };
 
@@ -344,8 +428,7 @@ static int exclusive_sum(Ctx& c, const int32_t* in, int32_t* out, int64_t n) {
         return 1;
     }
     MF_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tb, in, out, (int)n, c.s));
-    MF_CHECK(hipStreamSynchronize(c.s));
-    c.release(tmp);
+    c.release(tmp);  // stream-ordered reuse: later work on c.s runs after the scan
     return 0;
 }
 
@@ -359,7 +442,6 @@ static int sort_pairs(Ctx& c, const K* kin, K* kout, const int32_t* vin, int32_t
         return 1;
     }
     MF_CHECK(hipcub::DeviceRadixSort::SortPairs(tmp, tb, kin, kout, vin, vout, (int)n, 0, bits, c.s));
-    MF_CHECK(hipStreamSynchronize(c.s));
     c.release(tmp);
     return 0;
 }
@@ -383,7 +465,6 @@ static int keep_triangles(Ctx& c, Mesh& m, const uint8_t* keep) {
     MF_ALLOC(tri2, int32_t, 3 * k);
     if (k) hipLaunchKernelGGL(k_gather_tris, dim3(nb(k)), dim3(256), 0, c.s, m.tri, sel, k, tri2);
     MF_CHECK(hipGetLastError());
-    MF_CHECK(hipStreamSynchronize(c.s));
     c.release(sel);
     c.release(m.tri);
     m.tri = tri2;
@@ -410,14 +491,12 @@ static int keep_vertices(Ctx& c, Mesh& m, const int32_t* keepv, const int32_t* m
         }
         if (k) hipLaunchKernelGGL(k_gather_vertices, dim3(nb(k)), dim3(256), 0, c.s, m.pos, m.nrm, sel, k, pos2, nrm2);
         MF_CHECK(hipGetLastError());
-        MF_CHECK(hipStreamSynchronize(c.s));
         c.release(m.pos);
         if (m.nrm) c.release(m.nrm);
         m.pos = pos2;
         m.nrm = nrm2;
         m.nv = k;
     }
-    MF_CHECK(hipStreamSynchronize(c.s));
     c.release(sel);
     return 0;
 }
@@ -542,13 +621,17 @@ static int remove_non_manifold_edges(Ctx& c, Mesh& m, int64_t* removed) {
         if (!manifold) {
             // bring the runs of the non-manifold edges to the host (keys + slots from each head)
             std::vector<int32_t> h_heads(nh);
-            MF_CHECK(hipMemcpy(h_heads.data(), heads, sizeof(int32_t) * nh, hipMemcpyDeviceToHost));
+            MF_CHECK(hipMemcpyAsync(h_heads.data(), heads, sizeof(int32_t) * nh, hipMemcpyDeviceToHost, c.s));
+            MF_CHECK(hipStreamSynchronize(c.s));
             std::vector<uint64_t> h_keys(ne);
             std::vector<int32_t> h_slot(ne);
-            MF_CHECK(hipMemcpy(h_keys.data(), keys_s, sizeof(uint64_t) * ne, hipMemcpyDeviceToHost));
-            MF_CHECK(hipMemcpy(h_slot.data(), slot_s, sizeof(int32_t) * ne, hipMemcpyDeviceToHost));
+            MF_CHECK(hipMemcpyAsync(h_keys.data(), keys_s, sizeof(uint64_t) * ne, hipMemcpyDeviceToHost, c.s));
+            MF_CHECK(hipStreamSynchronize(c.s));
+            MF_CHECK(hipMemcpyAsync(h_slot.data(), slot_s, sizeof(int32_t) * ne, hipMemcpyDeviceToHost, c.s));
+            MF_CHECK(hipStreamSynchronize(c.s));
             h_area.resize(n);
-            MF_CHECK(hipMemcpy(h_area.data(), area, sizeof(double) * n, hipMemcpyDeviceToHost));
+            MF_CHECK(hipMemcpyAsync(h_area.data(), area, sizeof(double) * n, hipMemcpyDeviceToHost, c.s));
+            MF_CHECK(hipStreamSynchronize(c.s));
             for (int32_t h : h_heads) {  // ascending edge key order
                 int64_t e = h;
                 std::vector<int32_t> tris;
@@ -565,7 +648,8 @@ static int remove_non_manifold_edges(Ctx& c, Mesh& m, int64_t* removed) {
                     --to_delete;
                 }
             }
-            MF_CHECK(hipMemcpy(area, h_area.data(), sizeof(double) * n, hipMemcpyHostToDevice));
+            MF_CHECK(hipMemcpyAsync(area, h_area.data(), sizeof(double) * n, hipMemcpyHostToDevice, c.s));
+            MF_CHECK(hipStreamSynchronize(c.s));
         }
         MF_ALLOC(keep, uint8_t, n);
         hipLaunchKernelGGL(k_keep_positive, dim3(nb(n)), dim3(256), 0, c.s, area, n, keep);
@@ -597,14 +681,9 @@ int mqr_mesh_filter_components(int device, const float* vertices, const float* n
     for (int i = 0; i < 8; ++i) stats[i] = 0;
     stats[0] = nt;
     Ctx c;
-    MQR_CHECK_HIP(hipStreamCreateWithFlags(&c.s, hipStreamNonBlocking));
-    struct StreamGuard {
-        hipStream_t s;
-        ~StreamGuard() {
-            (void)hipStreamSynchronize(s);
-            (void)hipStreamDestroy(s);
-        }
-    } guard{c.s};
+    // arena: ~110 B per triangle + ~90 B per vertex covers the largest stage (edge sort + keys)
+    MQR_REQUIRE(c.open(device, (size_t)(128 * nt + 96 * nv) + ((size_t)32 << 20)) == 0,
+                "mesh filter: device allocation failed");
     const hipMemcpyKind k = loc == MQR_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
     Mesh m;
     m.nv = nv;
@@ -642,8 +721,9 @@ int mqr_mesh_filter_components(int device, const float* vertices, const float* n
         MQR_CHECK_HIP(hipGetLastError());
         if (exclusive_sum(c, is_root, cid, nt)) return 1;
         int32_t last_root = 0, last_cid = 0;
-        MQR_CHECK_HIP(hipMemcpy(&last_root, is_root + nt - 1, sizeof(int32_t), hipMemcpyDeviceToHost));
-        MQR_CHECK_HIP(hipMemcpy(&last_cid, cid + nt - 1, sizeof(int32_t), hipMemcpyDeviceToHost));
+        MQR_CHECK_HIP(hipMemcpyAsync(&last_root, is_root + nt - 1, sizeof(int32_t), hipMemcpyDeviceToHost, c.s));
+        MQR_CHECK_HIP(hipMemcpyAsync(&last_cid, cid + nt - 1, sizeof(int32_t), hipMemcpyDeviceToHost, c.s));
+        MQR_CHECK_HIP(hipStreamSynchronize(c.s));
         const int64_t C = (int64_t)last_root + last_cid;
         int32_t* ccount = c.alloc<int32_t>(C);
         MQR_REQUIRE(ccount, "mesh filter: device allocation failed");
@@ -701,26 +781,27 @@ int mqr_mesh_filter_components(int device, const float* vertices, const float* n
     }
     stats[6] = m.nt;
     stats[7] = m.nv;
-    // hand the arrays over to a geometry object (detach them from the context)
+    // copy the result out of the scratch arena into one allocation owned by the geometry object
     mqr_geom* g = new mqr_geom();
     g->device = device;
     g->nv = m.nv;
     g->nt = m.nt;
-    auto detach = [&](void* p) {
-        auto it = std::find(c.owned.begin(), c.owned.end(), p);
-        if (it != c.owned.end()) c.owned.erase(it);
-    };
-    g->pos = m.pos;
-    g->tri = m.tri;
-    detach(m.pos);
-    detach(m.tri);
-    if (m.nrm) {
-        g->nrm = m.nrm;
-        detach(m.nrm);
-    } else {
-        MQR_CHECK_HIP(hipMalloc(&g->nrm, sizeof(float) * 3 * std::max<int64_t>(m.nv, 1)));
-        MQR_CHECK_HIP(hipMemsetAsync(g->nrm, 0, sizeof(float) * 3 * std::max<int64_t>(m.nv, 1), c.s));
+    const size_t sv = (sizeof(float) * 3 * (size_t)std::max<int64_t>(m.nv, 1) + 255) & ~(size_t)255;
+    const size_t stb = (sizeof(int32_t) * 3 * (size_t)std::max<int64_t>(m.nt, 1) + 255) & ~(size_t)255;
+    if (hipMalloc(&g->blk, 2 * sv + stb) != hipSuccess) {
+        delete g;
+        set_error("mesh filter: device allocation failed");
+        return 1;
     }
+    g->pos = reinterpret_cast<float*>(g->blk);
+    g->nrm = reinterpret_cast<float*>(static_cast<char*>(g->blk) + sv);
+    g->tri = reinterpret_cast<int32_t*>(static_cast<char*>(g->blk) + 2 * sv);
+    if (m.nv) MQR_CHECK_HIP(hipMemcpyAsync(g->pos, m.pos, sizeof(float) * 3 * m.nv, hipMemcpyDeviceToDevice, c.s));
+    if (m.nv && m.nrm)
+        MQR_CHECK_HIP(hipMemcpyAsync(g->nrm, m.nrm, sizeof(float) * 3 * m.nv, hipMemcpyDeviceToDevice, c.s));
+    else
+        MQR_CHECK_HIP(hipMemsetAsync(g->nrm, 0, sv, c.s));
+    if (m.nt) MQR_CHECK_HIP(hipMemcpyAsync(g->tri, m.tri, sizeof(int32_t) * 3 * m.nt, hipMemcpyDeviceToDevice, c.s));
     MQR_CHECK_HIP(hipStreamSynchronize(c.s));
     *out = g;
     return 0;

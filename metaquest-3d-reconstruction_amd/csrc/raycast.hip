@@ -55,31 +55,49 @@ struct BuildTri {
 
 // Gather every geometry's triangles into one array (prim id / geom id kept) and accumulate the
 // centroid bounds (ordered-int atomics).
+// Centroid bounds: a wave-wide min / max first, then one atomic per wave and axis (2 M per-thread
+// atomics on the same 6 words serialised this kernel to ~2 ms).
+__device__ inline uint32_t wave_min_u32(uint32_t x) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) x = min(x, (uint32_t)__shfl_xor((int)x, o, 64));
+    return x;
+}
+__device__ inline uint32_t wave_max_u32(uint32_t x) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, o, 64));
+    return x;
+}
+
 __global__ void k_gather_tris(const float* __restrict__ v, const int32_t* __restrict__ t, int64_t nt, int64_t nv,
                               int64_t base, uint32_t geom, BuildTri* tris, uint32_t* prim, uint32_t* gid,
                               uint32_t* cbounds /* 6: min xyz, max xyz (ordered) */, int* bad) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nt) return;
-    BuildTri b;
-    float c[3] = {0.f, 0.f, 0.f};
-    for (int k = 0; k < 3; ++k) {
-        int32_t vi = t[3 * i + k];
-        if (vi < 0 || vi >= nv) {
-            atomicOr(bad, 1);
-            vi = 0;
+    uint32_t lo[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, hi[3] = {0u, 0u, 0u};
+    if (i < nt) {
+        BuildTri b;
+        float c[3] = {0.f, 0.f, 0.f};
+        for (int k = 0; k < 3; ++k) {
+            int32_t vi = t[3 * i + k];
+            if (vi < 0 || vi >= nv) {
+                atomicOr(bad, 1);
+                vi = 0;
+            }
+            for (int a = 0; a < 3; ++a) {
+                b.v[3 * k + a] = v[3 * (int64_t)vi + a];
+                c[a] += b.v[3 * k + a];
+            }
         }
-        for (int a = 0; a < 3; ++a) {
-            b.v[3 * k + a] = v[3 * (int64_t)vi + a];
-            c[a] += b.v[3 * k + a];
-        }
+        tris[base + i] = b;
+        prim[base + i] = (uint32_t)i;
+        gid[base + i] = geom;
+        for (int a = 0; a < 3; ++a) lo[a] = hi[a] = f2ord(c[a] * (1.0f / 3.0f));
     }
-    tris[base + i] = b;
-    prim[base + i] = (uint32_t)i;
-    gid[base + i] = geom;
     for (int a = 0; a < 3; ++a) {
-        const float ca = c[a] * (1.0f / 3.0f);
-        atomicMin(&cbounds[a], f2ord(ca));
-        atomicMax(&cbounds[3 + a], f2ord(ca));
+        const uint32_t wl = wave_min_u32(lo[a]), wh = wave_max_u32(hi[a]);
+        if ((threadIdx.x & 63) == 0) {
+            atomicMin(&cbounds[a], wl);
+            atomicMax(&cbounds[3 + a], wh);
+        }
     }
 }
 
@@ -148,12 +166,9 @@ __global__ void k_radix_tree(const uint64_t* __restrict__ keys, int64_t n, int32
     parent[c1 >= 0 ? c1 : (n - 1) + ~c1] = (int32_t)i;
 }
 
-// Write the sorted leaves and refit boxes bottom-up: the second thread to reach a node writes its
-// two child boxes and continues to the parent.
-__global__ void k_leaves_refit(const BuildTri* __restrict__ tris, const uint32_t* __restrict__ prim,
-                               const uint32_t* __restrict__ gid, const uint32_t* __restrict__ order, int64_t n,
-                               const int32_t* __restrict__ child, const int32_t* __restrict__ parent,
-                               int* __restrict__ arrivals, float4* leaf, float4* node) {
+// Sorted leaves: v0 + primitive id, e1 + geometry id, e2.
+__global__ void k_leaves(const BuildTri* __restrict__ tris, const uint32_t* __restrict__ prim,
+                         const uint32_t* __restrict__ gid, const uint32_t* __restrict__ order, int64_t n, float4* leaf) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint32_t o = order[i];
@@ -163,12 +178,40 @@ __global__ void k_leaves_refit(const BuildTri* __restrict__ tris, const uint32_t
     leaf[3 * i + 0] = make_float4(b.v[0], b.v[1], b.v[2], __uint_as_float(prim[o]));
     leaf[3 * i + 1] = make_float4(e1[0], e1[1], e1[2], __uint_as_float(gid[o]));
     leaf[3 * i + 2] = make_float4(e2[0], e2[1], e2[2], 0.f);
-    if (n == 1) return;
-    int32_t p = parent[(n - 1) + i];
-    __threadfence();
-    while (p >= 0) {
-        if (atomicAdd(&arrivals[p], 1) == 0) return;  // first arrival: the sibling finishes the node
-        __threadfence();
+}
+
+// Depth of every internal node (root 0), for the level-by-level refit.  The bottom-up refit with
+// per-node arrival counters needs a device-scope fence per level so that a sibling on another XCD
+// (whose L2 is not coherent with this one) sees the child box: on gfx950 every such fence writes
+// back L2, which made that single kernel ~15 ms for 2 M triangles.  Kernel boundaries order the
+// levels here instead (<= 96 levels: 63 key bits + 32 index bits + 1).
+__global__ void k_node_depth(const int32_t* __restrict__ parent, int64_t m, uint32_t* depth, uint32_t* ids,
+                             int* bad) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    uint32_t d = 0;
+    for (int32_t x = parent[i]; x >= 0; x = parent[x]) ++d;
+    if (d >= 256) atomicOr(bad, 2);
+    depth[i] = d;
+    ids[i] = (uint32_t)i;
+}
+
+__global__ void k_level_bounds(const uint32_t* __restrict__ ds, int64_t m, int* start, int* end) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const uint32_t d = ds[i] & 0xffu;
+    if (i == 0 || (ds[i - 1] & 0xffu) != d) start[d] = (int)i;
+    if (i == m - 1 || (ds[i + 1] & 0xffu) != d) end[d] = (int)(i + 1);
+}
+
+// Boxes of the nodes of one level (their children are leaves or deeper, already written).
+__global__ void k_refit_level(const BuildTri* __restrict__ tris, const uint32_t* __restrict__ order,
+                              const int32_t* __restrict__ child, const uint32_t* __restrict__ ids, int64_t cnt,
+                              float4* node) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= cnt) return;
+    const int32_t p = (int32_t)ids[k];
+    {
         float lo[2][3], hi[2][3];
         for (int c = 0; c < 2; ++c) {
             const int32_t ch = child[2 * p + c];
@@ -179,7 +222,7 @@ __global__ void k_leaves_refit(const BuildTri* __restrict__ tris, const uint32_t
                     hi[c][a] = fmaxf(fmaxf(t.v[a], t.v[3 + a]), t.v[6 + a]);
                 }
             } else {
-                const float4* cn = node + 4 * (int64_t)ch;  // written by another thread before its fence
+                const float4* cn = node + 4 * (int64_t)ch;  // written by an earlier level's launch
                 const float4 l0 = cn[0], h0 = cn[1], l1 = cn[2], h1 = cn[3];
                 lo[c][0] = fminf(l0.x, l1.x), lo[c][1] = fminf(l0.y, l1.y), lo[c][2] = fminf(l0.z, l1.z);
                 hi[c][0] = fmaxf(h0.x, h1.x), hi[c][1] = fmaxf(h0.y, h1.y), hi[c][2] = fmaxf(h0.z, h1.z);
@@ -190,8 +233,6 @@ __global__ void k_leaves_refit(const BuildTri* __restrict__ tris, const uint32_t
         nd[1] = make_float4(hi[0][0], hi[0][1], hi[0][2], 0.f);
         nd[2] = make_float4(lo[1][0], lo[1][1], lo[1][2], __int_as_float(child[2 * p + 1]));
         nd[3] = make_float4(hi[1][0], hi[1][1], hi[1][2], 0.f);
-        __threadfence();
-        p = parent[p];
     }
 }
 
@@ -415,10 +456,57 @@ static int build(mqr_scene* s) {
                            child, parent);
         RC_HIP(hipGetLastError());
     }
-    hipLaunchKernelGGL(k_leaves_refit, dim3(gb), dim3(256), 0, st, tris, prim, gid, idx_sorted, n, child, parent,
-                       arrivals, s->leaf, s->node);
+    hipLaunchKernelGGL(k_leaves, dim3(gb), dim3(256), 0, st, tris, prim, gid, idx_sorted, n, s->leaf);
     RC_HIP(hipGetLastError());
     int h_bad = 0;
+    if (n > 1) {
+        // level-by-level refit: internal node depths -> sort ids by depth -> one launch per level
+        const int64_t m = n - 1;
+        uint32_t* depth = reinterpret_cast<uint32_t*>(keys);  // 2 x uint32 per former 64-bit key slot
+        uint32_t* depth_s = depth + m;
+        uint32_t* ids = reinterpret_cast<uint32_t*>(keys_sorted);
+        uint32_t* ids_s = ids + m;
+        int* lvl = arrivals;  // 512 ints: start[256], end[256] (arrivals has n - 1 >= 512 slots or is regrown)
+        if (m < 512) {
+            RC_HIP(hipFree(arrivals));
+            arrivals = nullptr;
+            RC_HIP(hipMalloc(&arrivals, sizeof(int) * 512));
+            lvl = arrivals;
+        }
+        RC_HIP(hipMemsetAsync(lvl, 0, sizeof(int) * 512, st));
+        const unsigned gm = (unsigned)((m + 255) / 256);
+        hipLaunchKernelGGL(k_node_depth, dim3(gm), dim3(256), 0, st, parent, m, depth, ids, bad);
+        RC_HIP(hipGetLastError());
+        size_t sb = 0;
+        RC_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, sb, depth, depth_s, ids, ids_s, (int)m, 0, 8, st));
+        if (sb > tmp_bytes + 16) {
+            RC_HIP(hipFree(tmp));
+            tmp = nullptr;
+            RC_HIP(hipMalloc(&tmp, sb));
+        } else {
+            sb = tmp_bytes + 16;
+        }
+        RC_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, sb, depth, depth_s, ids, ids_s, (int)m, 0, 8, st));
+        hipLaunchKernelGGL(k_level_bounds, dim3(gm), dim3(256), 0, st, depth_s, m, lvl, lvl + 256);
+        RC_HIP(hipGetLastError());
+        int h_lvl[512];
+        RC_HIP(hipMemcpyAsync(h_lvl, lvl, sizeof(h_lvl), hipMemcpyDeviceToHost, st));
+        RC_HIP(hipMemcpyAsync(&h_bad, bad, sizeof(int), hipMemcpyDeviceToHost, st));
+        RC_HIP(hipStreamSynchronize(st));
+        if (h_bad & 2) {
+            set_error("internal: BVH deeper than 255 levels");
+            cleanup();
+            free_built(s);
+            return 1;
+        }
+        for (int d = 255; d >= 0; --d) {
+            const int64_t cnt = (int64_t)h_lvl[256 + d] - h_lvl[d];
+            if (cnt <= 0) continue;
+            hipLaunchKernelGGL(k_refit_level, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, st, tris, idx_sorted,
+                               child, ids_s + h_lvl[d], cnt, s->node);
+            RC_HIP(hipGetLastError());
+        }
+    }
     RC_HIP(hipMemcpyAsync(&h_bad, bad, sizeof(int), hipMemcpyDeviceToHost, st));
     RC_HIP(hipStreamSynchronize(st));
 #undef RC_HIP
