@@ -28,6 +28,7 @@
 #include <limits>
 #include <map>
 #include <mutex>
+#include <unordered_map>
 #include <vector>
 
 #include "mqr_common.hpp"
@@ -273,11 +274,31 @@ __global__ void k_areas(const float* __restrict__ pos, const int32_t* __restrict
     area[i] = 0.5 * sqrt((c0 * c0 + c1 * c1) + c2 * c2);
 }
 
-// run starts of sorted edge keys whose run has more than 2 entries
-__global__ void k_nonmanifold_heads(const uint64_t* __restrict__ keys, int64_t m, uint8_t* flag) {
+// sorted edge entries inside a run of more than two equal keys (the entries of non-manifold edges)
+__global__ void k_nonmanifold_members(const uint64_t* __restrict__ keys, int64_t m, uint8_t* flag) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= m) return;
-    flag[i] = (i == 0 || keys[i] != keys[i - 1]) && i + 2 < m && keys[i + 2] == keys[i];
+    const uint64_t k = keys[i];
+    const bool p1 = i >= 1 && keys[i - 1] == k, p2 = i >= 2 && keys[i - 2] == k;
+    const bool n1 = i + 1 < m && keys[i + 1] == k, n2 = i + 2 < m && keys[i + 2] == k;
+    flag[i] = (p1 && p2) || (p1 && n1) || (n1 && n2);
+}
+
+// key, triangle and area of each member entry (for the host's resolution pass)
+__global__ void k_gather_members(const uint64_t* __restrict__ keys, const int32_t* __restrict__ slot,
+                                 const double* __restrict__ area, const int32_t* __restrict__ mem, int64_t n,
+                                 uint64_t* okey, int32_t* otri, double* oarea) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int32_t e = mem[i], t = slot[e] / 3;
+    okey[i] = keys[e];
+    otri[i] = t;
+    oarea[i] = area[t];
+}
+
+__global__ void k_drop_tris(const int32_t* __restrict__ del, int64_t n, double* area) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) area[del[i]] = -1.0;
 }
 
 __global__ void k_keep_positive(const double* __restrict__ area, int64_t nt, uint8_t* keep) {
@@ -591,8 +612,9 @@ static int remove_duplicated_vertices(Ctx& c, Mesh& m) {
     return 0;
 }
 
-// RemoveNonManifoldEdges: edge map on the device; the (few) non-manifold edges are resolved on the
-// host in ascending edge order with Open3D's rule; triangles with area <= 0 are dropped each round.
+// RemoveNonManifoldEdges: edge map on the device; only the entries of non-manifold edges (key,
+// triangle, area) go to the host, which resolves the edges in ascending key order with Open3D's
+// rule and returns the dropped triangles; triangles with area <= 0 are dropped each round.
 static int remove_non_manifold_edges(Ctx& c, Mesh& m, int64_t* removed) {
     *removed = 0;
     const int64_t nt0 = m.nt;
@@ -608,54 +630,68 @@ static int remove_non_manifold_edges(Ctx& c, Mesh& m, int64_t* removed) {
         MF_ALLOC(slot, int32_t, ne);
         MF_ALLOC(slot_s, int32_t, ne);
         MF_ALLOC(flag, uint8_t, ne);
-        MF_ALLOC(heads, int32_t, ne);
+        MF_ALLOC(mem, int32_t, ne);
         hipLaunchKernelGGL(k_edge_keys, dim3(nb(ne)), dim3(256), 0, c.s, m.tri, n, keys, slot);
         MF_CHECK(hipGetLastError());
         if (sort_pairs(c, keys, keys_s, slot, slot_s, ne, 64)) return 1;
-        hipLaunchKernelGGL(k_nonmanifold_heads, dim3(nb(ne)), dim3(256), 0, c.s, keys_s, ne, flag);
+        hipLaunchKernelGGL(k_nonmanifold_members, dim3(nb(ne)), dim3(256), 0, c.s, keys_s, ne, flag);
         MF_CHECK(hipGetLastError());
-        int64_t nh = 0;
-        if (select_flagged(c, flag, ne, heads, &nh)) return 1;
-        std::vector<double> h_area;
-        bool manifold = nh == 0;
+        int64_t nm = 0;
+        if (select_flagged(c, flag, ne, mem, &nm)) return 1;
+        const bool manifold = nm == 0;
         if (!manifold) {
-            // bring the runs of the non-manifold edges to the host (keys + slots from each head)
-            std::vector<int32_t> h_heads(nh);
-            MF_CHECK(hipMemcpyAsync(h_heads.data(), heads, sizeof(int32_t) * nh, hipMemcpyDeviceToHost, c.s));
+            MF_ALLOC(mkey, uint64_t, nm);
+            MF_ALLOC(mtri, int32_t, nm);
+            MF_ALLOC(marea, double, nm);
+            hipLaunchKernelGGL(k_gather_members, dim3(nb(nm)), dim3(256), 0, c.s, keys_s, slot_s, area, mem, nm, mkey,
+                               mtri, marea);
+            MF_CHECK(hipGetLastError());
+            std::vector<uint64_t> hk(nm);
+            std::vector<int32_t> ht(nm);
+            std::vector<double> ha(nm);
+            MF_CHECK(hipMemcpyAsync(hk.data(), mkey, sizeof(uint64_t) * nm, hipMemcpyDeviceToHost, c.s));
+            MF_CHECK(hipMemcpyAsync(ht.data(), mtri, sizeof(int32_t) * nm, hipMemcpyDeviceToHost, c.s));
+            MF_CHECK(hipMemcpyAsync(ha.data(), marea, sizeof(double) * nm, hipMemcpyDeviceToHost, c.s));
             MF_CHECK(hipStreamSynchronize(c.s));
-            std::vector<uint64_t> h_keys(ne);
-            std::vector<int32_t> h_slot(ne);
-            MF_CHECK(hipMemcpyAsync(h_keys.data(), keys_s, sizeof(uint64_t) * ne, hipMemcpyDeviceToHost, c.s));
-            MF_CHECK(hipStreamSynchronize(c.s));
-            MF_CHECK(hipMemcpyAsync(h_slot.data(), slot_s, sizeof(int32_t) * ne, hipMemcpyDeviceToHost, c.s));
-            MF_CHECK(hipStreamSynchronize(c.s));
-            h_area.resize(n);
-            MF_CHECK(hipMemcpyAsync(h_area.data(), area, sizeof(double) * n, hipMemcpyDeviceToHost, c.s));
-            MF_CHECK(hipStreamSynchronize(c.s));
-            for (int32_t h : h_heads) {  // ascending edge key order
-                int64_t e = h;
-                std::vector<int32_t> tris;
-                while (e < ne && h_keys[e] == h_keys[h]) tris.push_back(h_slot[e++] / 3);
+            std::unordered_map<int32_t, double> cur;  // current area of every triangle involved
+            cur.reserve((size_t)nm);
+            for (int64_t j = 0; j < nm; ++j) cur.emplace(ht[j], ha[j]);
+            std::vector<int32_t> del;
+            for (int64_t s0 = 0; s0 < nm;) {  // runs in ascending edge-key order
+                int64_t e = s0;
+                while (e < nm && hk[e] == hk[s0]) ++e;
                 int cnt = 0;
-                for (int32_t t : tris) cnt += h_area[t] > 0;
-                int to_delete = cnt - 2;
-                while (to_delete > 0) {
+                for (int64_t j = s0; j < e; ++j) cnt += cur[ht[j]] > 0;
+                for (int to_delete = cnt - 2; to_delete > 0; --to_delete) {
                     int32_t mt = -1;
                     double ma = std::numeric_limits<double>::max();
-                    for (int32_t t : tris)
-                        if (h_area[t] > 0 && h_area[t] < ma) mt = t, ma = h_area[t];
-                    h_area[mt] = -1;
-                    --to_delete;
+                    for (int64_t j = s0; j < e; ++j) {
+                        const double a = cur[ht[j]];
+                        if (a > 0 && a < ma) mt = ht[j], ma = a;
+                    }
+                    cur[mt] = -1;
+                    del.push_back(mt);
                 }
+                s0 = e;
             }
-            MF_CHECK(hipMemcpyAsync(area, h_area.data(), sizeof(double) * n, hipMemcpyHostToDevice, c.s));
-            MF_CHECK(hipStreamSynchronize(c.s));
+            if (!del.empty()) {
+                MF_ALLOC(ddel, int32_t, (int64_t)del.size());
+                MF_CHECK(hipMemcpyAsync(ddel, del.data(), sizeof(int32_t) * del.size(), hipMemcpyHostToDevice, c.s));
+                hipLaunchKernelGGL(k_drop_tris, dim3(nb((int64_t)del.size())), dim3(256), 0, c.s, ddel,
+                                   (int64_t)del.size(), area);
+                MF_CHECK(hipGetLastError());
+                MF_CHECK(hipStreamSynchronize(c.s));  // `del` is pageable host memory
+                c.release(ddel);
+            }
+            c.release(marea);
+            c.release(mtri);
+            c.release(mkey);
         }
         MF_ALLOC(keep, uint8_t, n);
         hipLaunchKernelGGL(k_keep_positive, dim3(nb(n)), dim3(256), 0, c.s, area, n, keep);
         MF_CHECK(hipGetLastError());
         if (keep_triangles(c, m, keep)) return 1;
-        for (void* p : {(void*)area, (void*)keys, (void*)keys_s, (void*)slot, (void*)slot_s, (void*)flag, (void*)heads,
+        for (void* p : {(void*)area, (void*)keys, (void*)keys_s, (void*)slot, (void*)slot_s, (void*)flag, (void*)mem,
                         (void*)keep})
             c.release(p);
         if (manifold) break;

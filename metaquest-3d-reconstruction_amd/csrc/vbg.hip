@@ -301,6 +301,18 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
     hipLaunchKernelGGL((k_integrate_pk<RR, GG, NT>), dim3(grid), dim3(NT), 0, s, list, counters, v->list_cap, t, \
                        v->pool, v->voxel_size, depths, HW, H, W, fp, depth_frame, depth_max, sdf_trunc)
     const bool pk_ok = fast_ok && depth_scale == 1.0f;
+    // lean kernel: also needs every out-of-image byte offset (>= 2^32 - 4W) past the frame's 4HW bytes
+    const bool lean_ok = pk_ok && 4 * (HW + W) <= (int64_t{1} << 31);
+// lean kernel + exact fix-up launch (FG / FNT: the fix-up kernel's group size and threads)
+#define MQR_LAUNCH_LEAN(RR, NT, PIPE, RZ, WPE, FG, FNT) MQR_LAUNCH_LEANC(RR, NT, PIPE, RZ, WPE, false, FG, FNT)
+#define MQR_LAUNCH_LEANC(RR, NT, PIPE, RZ, WPE, CUBE, FG, FNT)                                                    \
+    hipLaunchKernelGGL((k_integrate_lean<RR, NT, PIPE, RZ, WPE, CUBE>), dim3(grid), dim3(NT), 0, s, list, lmask,   \
+                       v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp,          \
+                       depth_frame, depth_max, sdf_trunc);                                                        \
+    hipLaunchKernelGGL((k_integrate_t<RR, FG, 0, false, FNT>), dim3(64), dim3(FNT), 0, s, v->bad[p],               \
+                       reinterpret_cast<const uint32_t*>(v->bad[p] + v->list_cap), (int32_t*)nullptr,             \
+                       counters + (kBadCount - kListCount), v->list_cap, t, v->pool, v->voxel_size, depths, HW,   \
+                       H, W, fp, depth_frame, depth_scale, depth_max, sdf_trunc)
     // Variants (mqr_vbg_set_variant; all bit-identical, tests/test_gpu_numerics.py): 1 generic k_integrate;
     // k_integrate_t<R, G, SWZ, FAST, NT> and packed-f32 k_integrate_pk<R, G, NT> configurations
     // below, kept for A/B on new hardware (tools/ab_integrate.py).  FAST / packed fall back to the
@@ -310,8 +322,23 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
         var = 0;
     if ((var == 8 || var == 9 || (var >= 13 && var <= 16) || var == 20) && !pk_ok) var = 0;
     if (var >= 30 && var <= 33 && !lmask) var = 0;  // split blocks need the longest-first mask copy
+    if (var >= 40 && var <= 55 && !lean_ok) var = 0;
     if (v->R == 16 && var != 1) {
         switch (var) {
+            case 40: MQR_LAUNCH_LEAN(16, 512, true, 1, 1, 4, 512); break;
+            case 41: MQR_LAUNCH_LEAN(16, 512, false, 1, 1, 4, 512); break;
+            case 42: MQR_LAUNCH_LEAN(16, 1024, true, 1, 1, 4, 512); break;
+            case 43: MQR_LAUNCH_LEAN(16, 512, true, 2, 1, 4, 512); break;
+            case 44: MQR_LAUNCH_LEAN(16, 256, false, 1, 1, 4, 512); break;
+            case 45: MQR_LAUNCH_LEAN(16, 512, true, 1, 8, 4, 512); break;
+            case 46: MQR_LAUNCH_LEAN(16, 1024, false, 1, 1, 4, 512); break;
+            case 47: MQR_LAUNCH_LEAN(16, 1024, true, 2, 1, 4, 512); break;
+            case 48: MQR_LAUNCH_LEANC(16, 512, false, 2, 1, true, 4, 512); break;
+            case 49: MQR_LAUNCH_LEANC(16, 512, true, 2, 1, true, 4, 512); break;
+            case 50: MQR_LAUNCH_LEANC(16, 1024, false, 2, 1, true, 4, 512); break;
+            case 51: MQR_LAUNCH_LEANC(16, 1024, true, 2, 1, true, 4, 512); break;
+            case 52: MQR_LAUNCH_LEANC(16, 256, false, 2, 1, true, 4, 512); break;
+            case 53: MQR_LAUNCH_LEAN(16, 512, false, 2, 1, 4, 512); break;
             case 2: MQR_LAUNCH_INT(16, 4, false, false, 256); break;
             case 5: MQR_LAUNCH_INT(16, 8, 64, false, 256); break;
             case 22: MQR_LAUNCH_INT(16, 4, 16, false, 512); break;
@@ -349,7 +376,11 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
             default: MQR_LAUNCH_INT(16, 4, false, false, 512); break;
         }
     } else if (v->R == 8 && var != 1) {
-        if (var >= 8 && pk_ok)
+        if (var >= 48 && var <= 55) {
+            MQR_LAUNCH_LEANC(8, 256, false, 2, 1, true, 2, 256);
+        } else if (var >= 40 && var <= 47) {
+            MQR_LAUNCH_LEAN(8, 256, true, 1, 1, 2, 256);
+        } else if (var >= 8 && pk_ok)
             MQR_LAUNCH_PK(8, 2, 256);
         else if (var == 6)
             MQR_LAUNCH_INT(8, 2, false, true, 256);
@@ -363,6 +394,8 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
 #undef MQR_LAUNCH_SPLIT
 #undef MQR_LAUNCH_FIX
 #undef MQR_LAUNCH_PK
+#undef MQR_LAUNCH_LEAN
+#undef MQR_LAUNCH_LEANC
     MQR_CHECK_HIP(hipGetLastError());
     if (v->profile) {
         MQR_CHECK_HIP(hipEventRecord(e1, s));
@@ -488,7 +521,12 @@ int mqr_vbg_create(float voxel_size, int block_resolution, int64_t block_count, 
     v->R = block_resolution;
     v->R3 = (int64_t)block_resolution * block_resolution * block_resolution;
     const size_t nctr = 2 * kCountersTotal + 8;
-    bool ok = hipStreamCreateWithFlags(&v->stream, hipStreamNonBlocking) == hipSuccess &&
+    // The touch stream gets the device's highest priority: touch(b+1) shares the CUs with
+    // integrate(b), and integrate(b+1) cannot be enqueued before the host has read touch(b+1)'s
+    // counters -- a touch starved by integrate waves would leave the device idle at every batch.
+    int prio_least = 0, prio_greatest = 0;
+    (void)hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest);
+    bool ok = hipStreamCreateWithPriority(&v->stream, hipStreamNonBlocking, prio_greatest) == hipSuccess &&
               hipStreamCreateWithFlags(&v->stream2, hipStreamNonBlocking) == hipSuccess &&
               hipMalloc(&v->counters, sizeof(int) * nctr) == hipSuccess &&
               hipHostMalloc(&v->h_counters, sizeof(int) * nctr, hipHostMallocDefault) == hipSuccess &&
@@ -837,8 +875,9 @@ int mqr_check_division(int device, int which, float b, uint32_t lo_bits, uint64_
     for (uint64_t off = 0; off < count; off += chunk) {
         const uint64_t c = std::min<uint64_t>(chunk, count - off);
         const unsigned blocks = (unsigned)((c + 255) / 256);
-        if (which == 0)
-            hipLaunchKernelGGL(k_check_rcp, dim3(blocks), dim3(256), 0, 0, lo_bits + (uint32_t)off, c, d, d + 1);
+        if (which == 0 || which == 3 || which == 4)
+            hipLaunchKernelGGL(k_check_rcp, dim3(blocks), dim3(256), 0, 0, which == 0 ? 0 : which - 2,
+                               lo_bits + (uint32_t)off, c, d, d + 1);
         else
             hipLaunchKernelGGL(k_check_div, dim3(blocks), dim3(256), 0, 0, which == 2 ? 1 : 0, b,
                                lo_bits + (uint32_t)off, c, d, d + 1);

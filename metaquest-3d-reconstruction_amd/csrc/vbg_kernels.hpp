@@ -50,10 +50,14 @@ __device__ inline int64_t table_insert(Table t, uint64_t k, bool alloc, int* cou
     return -1;
 }
 
-__device__ inline void mark_slot(Table t, int64_t slot, int f, int* counters, int32_t* list, int64_t list_cap) {
+// Sets frame bit f of the slot (appending the slot to the batch list at its first bit); returns
+// whether the bit was new -- the caller counts those per wave (kFrameBlocks).
+__device__ inline bool mark_slot(Table t, int64_t slot, int f, int* counters, int32_t* list, int64_t list_cap) {
     const uint32_t bit = 1u << f;
+    // every workgroup of a frame that sees the block marks it: read the word at L2 first and only
+    // the workgroups that still find the bit clear issue the (same-address, serialised) atomic
+    if (__hip_atomic_load(&t.mask[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & bit) return false;
     const uint32_t old = atomicOr(&t.mask[slot], bit);
-    if (!(old & bit)) atomicAdd(&counters[kFrameBlocks], 1);
     if (old == 0) {
         const int pos = atomicAdd(&counters[kListCount], 1);
         if (pos < list_cap)
@@ -61,12 +65,15 @@ __device__ inline void mark_slot(Table t, int64_t slot, int f, int* counters, in
         else
             atomicOr(&counters[kOverflow], 4);
     }
+    return !(old & bit);
 }
 
-__device__ inline uint64_t shfl_up_u64(uint64_t v, int d) {
-    const int lo = __shfl_up((int)(uint32_t)v, d, 64);
-    const int hi = __shfl_up((int)(uint32_t)(v >> 32), d, 64);
-    return ((uint64_t)(uint32_t)hi << 32) | (uint64_t)(uint32_t)lo;
+// Sum of a per-lane count over the wave, added to *ctr by one lane (an LDS word of the workgroup
+// here; per-thread global atomics on the batch counters serialised on a handful of addresses).
+__device__ inline void wave_add(int* ctr, int v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    if ((threadIdx.x & 63) == 0 && v) atomicAdd(ctr, v);
 }
 
 // ------------------------------------------------------------------ kernels
@@ -78,12 +85,20 @@ __global__ __launch_bounds__(256) void k_touch(const float* __restrict__ depths,
                                                float depth_max, float sdf_trunc, float block_size, Table t,
                                                int alloc, int* counters, int* pool_ctr, int64_t pool_cap,
                                                uint64_t* bkeys, int32_t* list, int64_t list_cap) {
+    // keys already inserted by this workgroup (a 256-pixel strip of one frame shares most of its
+    // blocks): only a key's first occurrence probes the global table and sets the frame bit
+    constexpr int kSeen = 2048;
+    __shared__ unsigned long long seen[kSeen];
+    __shared__ int wg_count[2];  // valid samples, new frame bits: one global atomic per workgroup
+    for (int i = threadIdx.x; i < kSeen; i += blockDim.x) seen[i] = kEmpty;
+    if (threadIdx.x < 2) wg_count[threadIdx.x] = 0;
+    __syncthreads();
     const int f = blockIdx.y;
     const FrameParams& fp = fps[f];
     const int cols = W / 4, rows = H / 4, n = rows * cols;
     const int w = blockIdx.x * blockDim.x + threadIdx.x;
-    const int lane = threadIdx.x & 63;
     uint64_t key[4] = {kEmpty, kEmpty, kEmpty, kEmpty};
+    int valid = 0, fresh = 0;
     if (w < n) {
         const int y = (w / cols) * 4, x = (w % cols) * 4;
         const float d = depths[depth_frame[f] * HW + (int64_t)y * W + x] / depth_scale;
@@ -111,19 +126,32 @@ __global__ __launch_bounds__(256) void k_touch(const float* __restrict__ depths,
                     atomicOr(&counters[kOverflow], 8);
                 tt += t_step;
             }
-            atomicAdd(&counters[kFrameCounterBase + f], 4);
+            valid = 4;
         }
     }
+    wave_add(&wg_count[0], valid);
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
         const uint64_t k = key[s];
-        const uint64_t up = shfl_up_u64(k, 1);
-        bool dup = (lane > 0 && up == k);
-        if (s > 0 && key[s - 1] == k) dup = true;
-        if (k != kEmpty && !dup) {
-            const int64_t slot = table_insert(t, k, alloc != 0, counters, pool_ctr, pool_cap, bkeys);
-            if (slot >= 0) mark_slot(t, slot, f, counters, list, list_cap);
+        if (k == kEmpty || (s > 0 && key[s - 1] == k)) continue;
+        bool first = false;
+        uint32_t h = (uint32_t)mix64(k) & (kSeen - 1);
+        for (int p = 0; p < kSeen; ++p) {  // <= 1024 keys per workgroup: at most half full
+            const unsigned long long old = atomicCAS(&seen[h], (unsigned long long)kEmpty, (unsigned long long)k);
+            if (old == kEmpty) first = true;
+            if (old == kEmpty || old == k) break;
+            h = (h + 1) & (kSeen - 1);
         }
+        if (first) {
+            const int64_t slot = table_insert(t, k, alloc != 0, counters, pool_ctr, pool_cap, bkeys);
+            if (slot >= 0) fresh += mark_slot(t, slot, f, counters, list, list_cap);
+        }
+    }
+    wave_add(&wg_count[1], fresh);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (wg_count[0]) atomicAdd(&counters[kFrameCounterBase + f], wg_count[0]);
+        if (wg_count[1]) atomicAdd(&counters[kFrameBlocks], wg_count[1]);
     }
 }
 
@@ -138,7 +166,7 @@ __global__ void k_activate(const int32_t* __restrict__ keys, int64_t n, Table t,
         return;
     }
     const int64_t slot = table_insert(t, pack_key(x, y, z), true, counters, pool_ctr, pool_cap, bkeys);
-    if (slot >= 0 && mark) mark_slot(t, slot, 0, counters, list, list_cap);
+    if (slot >= 0 && mark && mark_slot(t, slot, 0, counters, list, list_cap)) atomicAdd(&counters[kFrameBlocks], 1);
 }
 
 // Projective TSDF update of every voxel of every listed block, frames applied in bit order.
@@ -644,13 +672,230 @@ __global__ __launch_bounds__(NT) void k_integrate_pk(const int32_t* __restrict__
     }
 }
 
+// ---- lean integrate (variants 40-47) -----------------------------------------------------------
+// The exact kernel's arithmetic with (i) shortened reciprocals, (ii) gathers through a raw buffer
+// view (out-of-image voxels read past its end, which returns 0), (iii) predicated updates instead
+// of per-voxel branches and (iv) optionally the next frame's projections and gathers issued before
+// the current frame's updates (PIPE), so a wave keeps ZPER gathers in flight across a whole frame
+// of arithmetic.  Blocks whose operands leave the ranges below are handed to the exact fix-up
+// launch unwritten (as the EXTFIX variants do).
+//
+// rcp_nm: v_rcp + one Newton step + one Markstein correction (5 VALU);
+// rcp_m:  v_rcp + one Markstein correction (3 VALU).
+// Both are compared with IEEE 1.0f / b over every float of the ranges they are used on
+// (tests/test_gpu_numerics.py, mqr_check_division modes 3 / 4): 1 / zc for 2^-36 <= zc <= 2^60
+// (rcp_nm, or rcp_m when RZ == 2) and 1 / (w + 1) for integer weights w <= 2^23 + 32 (rcp_m).
+__device__ __forceinline__ float rcp_nm(float b) {
+    const float y0 = __builtin_amdgcn_rcpf(b);
+    const float y1 = __builtin_fmaf(__builtin_fmaf(-b, y0, 1.0f), y0, y0);
+    return __builtin_fmaf(__builtin_fmaf(-b, y1, 1.0f), y1, y1);
+}
+__device__ __forceinline__ float rcp_m(float b) {
+    const float y0 = __builtin_amdgcn_rcpf(b);
+    return __builtin_fmaf(__builtin_fmaf(-b, y0, 1.0f), y0, y0);
+}
+
+// Raw buffer view of one depth frame: a load at or past `bytes` returns 0 instead of faulting.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t frame_rsrc(const float* base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, (int)bytes, 0x00020000);
+}
+
+// (tsdf, weight) of a block through a buffer view: 32-bit offsets recomputed at the store, where
+// plain pointers made the compiler keep a 64-bit address per voxel live across the frame loop.
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float2 pool_load(__amdgpu_buffer_rsrc_t rs, uint32_t voff, int soff) {
+    const u32x2 r = __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, 0);
+    return make_float2(__uint_as_float(r.x), __uint_as_float(r.y));
+}
+__device__ __forceinline__ void pool_store(__amdgpu_buffer_rsrc_t rs, uint32_t voff, int soff, float2 v) {
+    u32x2 r;
+    r.x = __float_as_uint(v.x);
+    r.y = __float_as_uint(v.y);
+    __builtin_amdgcn_raw_buffer_store_b64(r, rs, voff, soff, 0);
+}
+
+// Projection and gather of one frame for a thread's column -- Open3D's transform and projection,
+// the same float operations as integrate_column.  An out-of-image voxel gets row H, whose byte
+// offset is >= 4HW, past the end of the frame (host: 4 (HW + W) <= 2^31, so the 24-bit multiply
+// is exact): its depth reads as 0 and fails the update's d > 0 test, exactly like the out-of-image
+// skip (an in-image
+// NaN depth still reaches the update, as in Open3D).  `bad` is set unless 2^-36 <= zc <= 2^60 (zc
+// <= 0 included, which the update would skip anyway): inside that range the reciprocal shortcut is
+// exact and a non-zero sdf = d - zc is >= 2^-60 in magnitude, which keeps the division core exact.
+template <int ZPER, int RZ>
+__device__ __forceinline__ void lean_gather(float (&dv)[ZPER], bool& bad, const FrameParams& fp,
+                                            __amdgpu_buffer_rsrc_t rs, const float (&xs)[ZPER],
+                                            const float (&ys)[ZPER], const float (&zs)[ZPER], uint32_t W4, float hf,
+                                            float hm1, float wm1) {
+#pragma unroll
+    for (int k = 0; k < ZPER; ++k) {
+        // z-independent partial products: one per thread in the column mapping (equal operands are
+        // merged by the compiler), one per cube column in the cube mapping
+        const float ax = xs[k] * fp.ext[0] + ys[k] * fp.ext[1];
+        const float ay = xs[k] * fp.ext[4] + ys[k] * fp.ext[5];
+        const float az = xs[k] * fp.ext[8] + ys[k] * fp.ext[9];
+        const float xc = (ax + zs[k] * fp.ext[2]) + fp.ext[3];
+        const float yc = (ay + zs[k] * fp.ext[6]) + fp.ext[7];
+        const float zc = (az + zs[k] * fp.ext[10]) + fp.ext[11];
+        bad |= (__float_as_uint(zc) - 0x2D800000u) > 0x30000000u;  // not 2^-36 <= zc <= 2^60
+        const float inv_z = RZ == 2 ? rcp_m(zc) : rcp_nm(zc);
+        const float u = fp.fx * xc * inv_z + fp.cx;
+        const float v = fp.fy * yc * inv_z + fp.cy;
+        const bool in = (v >= 0) & (u >= 0) & (v <= hm1) & (u <= wm1);
+        const int ui = (int)(in ? u : 0.f), vi = (int)(in ? v : hf);
+        const uint32_t off = __umul24((uint32_t)vi, W4) + ((uint32_t)ui << 2);
+        dv[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
+        // keep each voxel's projection next to its load: hoisting all projections above the loads
+        // (the scheduler's choice) keeps ~6 more VGPRs per voxel live and halves the occupancy
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+// Running-average update of one frame's gathered depths (zc recomputed by the same operations).
+template <int ZPER>
+__device__ __forceinline__ void lean_update(float2 (&tw)[ZPER], const float (&dv)[ZPER], const FrameParams& fp,
+                                            const float (&xs)[ZPER], const float (&ys)[ZPER],
+                                            const float (&zs)[ZPER], float depth_max, float sdf_trunc, float y1t) {
+#pragma unroll
+    for (int k = 0; k < ZPER; ++k) {
+        const float az = xs[k] * fp.ext[8] + ys[k] * fp.ext[9];
+        const float zc = (az + zs[k] * fp.ext[10]) + fp.ext[11];
+        const float d = dv[k];
+        const float sdf = d - zc;
+        // zc > 0 holds in every block that is not handed to the fix-up launch
+        const bool up = !(d <= 0) && !(d > depth_max) && !(sdf < -sdf_trunc);
+        const float s = sdf < sdf_trunc ? sdf : sdf_trunc;
+        const float q0 = s * y1t;  // s / sdf_trunc: div_rn_core with the reciprocal refinement hoisted
+        const float q1 = __builtin_fmaf(__builtin_fmaf(-sdf_trunc, q0, s), y1t, q0);
+        const float sn = __builtin_fmaf(__builtin_fmaf(-sdf_trunc, q1, s), y1t, q1);
+        const float wgt = tw[k].y, wp = wgt + 1;
+        const float nt = (wgt * tw[k].x + sn) * rcp_m(wp);
+        tw[k].x = up ? nt : tw[k].x;
+        tw[k].y = up ? wp : wgt;
+        __builtin_amdgcn_sched_barrier(0);  // one voxel's chain at a time (register pressure)
+    }
+}
+
+// Voxel (x, y, z) of a block handled by thread `tid` as its k-th voxel.  COLUMN: the layout of
+// k_integrate_t (thread = voxel column, a wave = a 16 x 4 slab of one z layer).  CUBE: a wave's 64
+// lanes form a 4 x 4 x 4 voxel cube (lane bits x:0-1, y:2-3, z:4-5) and a thread's voxels walk the
+// cubes of R/4-cube columns, so every gather instruction reads the projection of a compact cube --
+// far fewer distinct cache lines than a slab, which is what bounds the gathers (L1 tag lookups).
+template <int R, int NT, bool CUBE>
+__device__ __forceinline__ void lean_voxel(int tid, int k, int& x, int& y, int& z) {
+    constexpr int R2 = R * R, ZPER = R * R2 / NT;
+    if (CUBE) {
+        constexpr int C = R / 4, CPT = ZPER / C;  // cubes per axis, cube columns per thread
+        static_assert(R % 4 == 0 && ZPER % C == 0 && (NT / 64) * CPT == C * C, "cube mapping does not tile");
+        const int w = tid >> 6, l = tid & 63, cxy = w * CPT + k / C;
+        x = 4 * (cxy % C) + (l & 3);
+        y = 4 * (cxy / C) + ((l >> 2) & 3);
+        z = 4 * (k % C) + (l >> 4);
+    } else {
+        x = tid % R;
+        y = (tid / R) % R;
+        z = tid / R2 + k * (NT / R2);
+    }
+}
+
+// Lean integrate, unit depth scale only (host: sdf_trunc in the division core's range).  Block per
+// workgroup as in k_integrate_t; every voxel of a block that is not handed off is written back.
+template <int R, int NT, bool PIPE, int RZ, int WPE = 1, bool CUBE = false>
+__global__ __launch_bounds__(NT, WPE) void k_integrate_lean(const int32_t* __restrict__ list,
+                                                        const uint32_t* __restrict__ lmask,
+                                                        int32_t* __restrict__ bad_out, int* __restrict__ counters,
+                                                        int64_t list_cap, Table t, float2* __restrict__ pool,
+                                                        float voxel_size, const float* __restrict__ depths,
+                                                        int64_t HW, int H, int W,
+                                                        const FrameParams* __restrict__ fps,
+                                                        const int64_t* __restrict__ depth_frame, float depth_max,
+                                                        float sdf_trunc) {
+    constexpr int R2 = R * R;
+    constexpr int R3 = R2 * R;
+    constexpr int ZPER = R3 / NT;
+    static_assert(R3 % NT == 0 && NT % R2 == 0, "NT must divide R^3 and be a multiple of R^2");
+    const int64_t n = min((int64_t)counters[kListCount], list_cap);
+    const float hf = (float)H, hm1 = (float)H - 1.0f, wm1 = (float)W - 1.0f;
+    const uint32_t W4 = 4u * (uint32_t)W, bytes = 4u * (uint32_t)HW;
+    const float y0t = __builtin_amdgcn_rcpf(sdf_trunc);
+    const float y1t = __builtin_fmaf(__builtin_fmaf(-sdf_trunc, y0t, 1.0f), y0t, y0t);
+    const int tid = threadIdx.x;
+    for (int64_t i = blockIdx.x; i < n; i += gridDim.x) {
+        const int32_t slot = list[i];
+        const int buf = t.vals[slot];
+        const uint32_t mask = __builtin_amdgcn_readfirstlane(lmask ? lmask[i] : t.mask[slot]);
+        int xb, yb, zb;
+        unpack_key(t.keys[slot], xb, yb, zb);
+        if (buf >= 0 && mask) {
+            const __amdgpu_buffer_rsrc_t vox = __builtin_amdgcn_make_buffer_rsrc(
+                pool + (int64_t)buf * R3, (short)0, (int)(R3 * sizeof(float2)), 0x00020000);
+            float2 tw[ZPER];
+            float xs[ZPER], ys[ZPER], zs[ZPER];
+            bool bad = false;
+#pragma unroll
+            for (int k = 0; k < ZPER; ++k) {
+                int x, y, z;
+                lean_voxel<R, NT, CUBE>(tid, k, x, y, z);
+                tw[k] = pool_load(vox, 8u * (uint32_t)(z * R2 + y * R + x), 0);
+                xs[k] = (float)(xb * R + x) * voxel_size;
+                ys[k] = (float)(yb * R + y) * voxel_size;
+                zs[k] = (float)(zb * R + z) * voxel_size;
+                const float w = tw[k].y;  // rcp_m(w + 1) needs integer weights (this batch adds <= 32)
+                bad |= !(w >= 0.0f && w <= 0x1p23f && w == __builtin_truncf(w));
+            }
+            uint32_t m = mask;
+            int f = __builtin_ctz(m);
+            m &= m - 1;
+            float da[ZPER], db[ZPER];
+            lean_gather<ZPER, RZ>(da, bad, fps[f], frame_rsrc(depths + depth_frame[f] * HW, bytes), xs, ys, zs, W4,
+                                  hf, hm1, wm1);
+            // PIPE: the next frame's projections and gathers are issued before this frame's updates
+            while (true) {
+                const bool more = m != 0;  // wave-uniform
+                const int g = more ? __builtin_ctz(m) : 0;
+                m &= m - 1;
+                if (PIPE && more)
+                    lean_gather<ZPER, RZ>(db, bad, fps[g], frame_rsrc(depths + depth_frame[g] * HW, bytes), xs, ys,
+                                          zs, W4, hf, hm1, wm1);
+                lean_update<ZPER>(tw, da, fps[f], xs, ys, zs, depth_max, sdf_trunc, y1t);
+                if (!more) break;
+                if (PIPE) {
+#pragma unroll
+                    for (int k = 0; k < ZPER; ++k) da[k] = db[k];
+                } else {
+                    lean_gather<ZPER, RZ>(da, bad, fps[g], frame_rsrc(depths + depth_frame[g] * HW, bytes), xs, ys,
+                                          zs, W4, hf, hm1, wm1);
+                }
+                f = g;
+            }
+            if (__syncthreads_or(bad)) {  // block-uniform: the exact fix-up launch redoes it from the pool
+                if (tid == 0) {
+                    const int j = atomicAdd(&counters[kBadCount], 1);
+                    bad_out[j] = slot;
+                    bad_out[list_cap + j] = (int32_t)mask;
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < ZPER; ++k) {
+                    int x, y, z;
+                    lean_voxel<R, NT, CUBE>(tid, k, x, y, z);
+                    pool_store(vox, 8u * (uint32_t)(z * R2 + y * R + x), 0, tw[k]);
+                }
+            }
+        }
+        __syncthreads();
+        if (tid == 0) t.mask[slot] = 0;
+    }
+}
+
 // Exhaustive-check kernels for the division shortcut (tests/test_gpu_numerics.py).
-__global__ void k_check_rcp(uint32_t lo_bits, uint64_t count, uint32_t* mismatches, uint32_t* first_bad) {
+// mode 0: rcp_rn, 1: rcp_nm, 2: rcp_m.
+__global__ void k_check_rcp(int mode, uint32_t lo_bits, uint64_t count, uint32_t* mismatches, uint32_t* first_bad) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= count) return;
     const uint32_t bits = lo_bits + (uint32_t)i;
     const float b = __uint_as_float(bits);
-    const float fast = rcp_rn(b), ref = 1.0f / b;
+    const float fast = mode == 1 ? rcp_nm(b) : mode == 2 ? rcp_m(b) : rcp_rn(b), ref = 1.0f / b;
     if (__float_as_uint(fast) != __float_as_uint(ref)) {
         atomicAdd(mismatches, 1u);
         atomicMin(first_bad, bits);

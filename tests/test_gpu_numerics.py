@@ -35,9 +35,19 @@ def test_division_shortcut_exact(b):
         assert mm == 0, f"b={b}: {mm} mismatches, first bit pattern {first:#x}"
 
 
+@pytest.mark.parametrize("which,lo,hi", [(3, 2.0 ** -60, 2.0 ** 60), (4, 1.0, 2.0 ** 24), (4, 2.0 ** -60, 2.0 ** 60)])
+def test_shortened_reciprocals_exact(which, lo, hi):
+    """Lean integrate kernel: rcp_nm (v_rcp + Newton + Markstein; 1 / zc) and rcp_m (v_rcp +
+    Markstein; 1 / (w + 1), and 1 / zc in the RZ = 2 variants) equal IEEE 1.0f / b on every float
+    of the range they are used on."""
+    mm, first = _check(which, 0.0, lo, hi)
+    assert mm == 0, f"mode {which}: {mm} mismatches, first bit pattern {first:#x}"
+
+
 INTEGRATE_VARIANTS = {16: (0, 2, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 22, 23, 24, 25, 0x100, 0x106,
-                          0x108, 26, 27, 28, 29, 0x200, 0x300, 30, 31, 32, 33, 0x21e, 34, 35, 36, 37),
-                      8: (0, 6, 8, 0x101, 0x200)}
+                          0x108, 26, 27, 28, 29, 0x200, 0x300, 30, 31, 32, 33, 0x21e, 34, 35, 36, 37,
+                          40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 52, 53, 0x128, 0x228, 0x130),
+                      8: (0, 6, 8, 0x101, 0x200, 40, 48)}
 
 
 def test_specialised_integrate_equals_generic():
@@ -123,3 +133,38 @@ def test_packed_integrate_exact_fallback():
     for i in (1, 2, 3, 4):
         assert compare_volumes(out[0], out[i], 0.0) == 0.0
     assert compare_volumes(out[5], out[6], 0.0) == 0.0
+
+
+def test_lean_integrate_exact_fallback():
+    """Lean kernel (variants 40-53, column and cube lane mappings): the block holding zc == 0 voxels (camera at the origin looking at
+    a 1 cm plane) and blocks with imported weights of 2^61 or non-integer weights are handed to the
+    exact fix-up launch; every volume equals the generic kernel's bit for bit."""
+    from gpu_helpers import compare_volumes
+    from mqr import _lib, synthetic
+    from mqr.vbg import VoxelBlockGrid
+    seq = synthetic.make_sequence("room", n=6, height=240, width=320, f=262.5, noise=True, seed=9)
+    near = np.full((240, 320), 0.01, np.float32)
+    depths = [near] + [np.asarray(d, np.float32) for d in seq["depth"]]
+    Ks = np.concatenate([seq["K"][:1], seq["K"]])
+    Ts = np.concatenate([np.eye(4)[None], seq["T_wc"]])
+    cases = ((16, 1), (16, 40), (16, 41), (16, 42), (16, 43), (16, 44), (16, 45), (16, 46), (16, 47), (16, 48),
+             (16, 49), (16, 50), (16, 51), (16, 52), (16, 53), (8, 1), (8, 40), (8, 48))
+    out = []
+    for R, variant in cases:
+        v = VoxelBlockGrid(voxel_size=0.005, block_resolution=R, block_count=64)
+        _lib.call("mqr_vbg_set_variant", v.handle, variant)
+        v.integrate_frames(depths[:4], Ks[:4], Ts[:4], depth_scale=1.0, depth_max=4.0, trunc_voxel_multiplier=10.0)
+        keys, tsdf, wgt = v.export()
+        assert (keys == 0).all(axis=1).any(), "origin block not touched"
+        wgt = wgt.copy()
+        sel = keys.sum(axis=1) % 3
+        wgt[sel == 1] = np.float32(2.0 ** 61)
+        wgt[sel == 2] *= np.float32(1.5)  # odd counts become non-integer
+        v.reset()
+        v.import_blocks(keys, tsdf, wgt)
+        v.integrate_frames(depths[3:], Ks[3:], Ts[3:], depth_scale=1.0, depth_max=4.0, trunc_voxel_multiplier=10.0)
+        out.append(v.export())
+    for i in range(1, 15):
+        assert compare_volumes(out[0], out[i], 0.0) == 0.0, cases[i]
+    assert compare_volumes(out[15], out[16], 0.0) == 0.0
+    assert compare_volumes(out[15], out[17], 0.0) == 0.0
