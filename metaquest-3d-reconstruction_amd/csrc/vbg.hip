@@ -322,7 +322,7 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
         var = 0;
     if ((var == 8 || var == 9 || (var >= 13 && var <= 16) || var == 20) && !pk_ok) var = 0;
     if (var >= 30 && var <= 33 && !lmask) var = 0;  // split blocks need the longest-first mask copy
-    if (var >= 40 && var <= 55 && !lean_ok) var = 0;
+    if (var >= 40 && var <= 53 && !lean_ok) var = 0;
     if (v->R == 16 && var != 1) {
         switch (var) {
             case 40: MQR_LAUNCH_LEAN(16, 512, true, 1, 1, 4, 512); break;
@@ -372,8 +372,17 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
             case 27: MQR_LAUNCH_INTW(16, 4, false, true, 512, 8); break;
             case 28: MQR_LAUNCH_INTW(16, 8, false, false, 512, 8); break;
             case 29: MQR_LAUNCH_INTW(16, 2, false, false, 256, 8); break;
-            // default: 512 threads x 8 voxels, gathers in groups of 4 (fastest on MI355X)
-            default: MQR_LAUNCH_INT(16, 4, false, false, 512); break;
+            case 54: MQR_LAUNCH_INT(16, 4, false, false, 512); break;
+            // default: the lean kernel (512 threads x 8 voxels, column mapping, 3-op reciprocals;
+            // fastest on MI355X, tools/ab_integrate.py); the exact branchy kernel where the lean one's
+            // preconditions (unit depth scale, trunc in range, frame size) do not hold
+            default:
+                if (lean_ok) {
+                    MQR_LAUNCH_LEAN(16, 512, false, 2, 1, 4, 512);
+                } else {
+                    MQR_LAUNCH_INT(16, 4, false, false, 512);
+                }
+                break;
         }
     } else if (v->R == 8 && var != 1) {
         if (var >= 48 && var <= 55) {

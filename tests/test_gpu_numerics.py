@@ -46,7 +46,7 @@ def test_shortened_reciprocals_exact(which, lo, hi):
 
 INTEGRATE_VARIANTS = {16: (0, 2, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 22, 23, 24, 25, 0x100, 0x106,
                           0x108, 26, 27, 28, 29, 0x200, 0x300, 30, 31, 32, 33, 0x21e, 34, 35, 36, 37,
-                          40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 52, 53, 0x128, 0x228, 0x130),
+                          40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 52, 53, 54, 0x128, 0x228, 0x130),
                       8: (0, 6, 8, 0x101, 0x200, 40, 48)}
 
 
@@ -81,7 +81,7 @@ def test_fast_integrate_exact_fallback():
         d[::7, ::5] = np.float32(1e-30)   # in-image, > 0, below 2^-60 -> fallback
     out = []
     # 34 / 37: fast kernel handing out-of-range blocks to the exact fix-up launch
-    for R, variant in ((16, 1), (16, 0), (16, 6), (16, 7), (16, 18), (16, 34), (16, 37), (8, 1), (8, 6)):
+    for R, variant in ((16, 1), (16, 0), (16, 6), (16, 7), (16, 18), (16, 34), (16, 37), (8, 1), (8, 6), (16, 54)):
         v = VoxelBlockGrid(voxel_size=0.01, block_resolution=R, block_count=64)
         _lib.call("mqr_vbg_set_variant", v.handle, variant)
         v.integrate_frames(depth_mm[:4], seq["K"][:4], seq["T_wc"][:4], depth_scale=1000.0, depth_max=4.0,
@@ -94,7 +94,7 @@ def test_fast_integrate_exact_fallback():
         v.integrate_frames(depth_mm[4:], seq["K"][4:], seq["T_wc"][4:], depth_scale=1000.0, depth_max=4.0,
                            trunc_voxel_multiplier=10.0)
         out.append(v.export())
-    for i in (1, 2, 3, 4, 5, 6):
+    for i in (1, 2, 3, 4, 5, 6, 9):
         assert compare_volumes(out[0], out[i], 0.0) == 0.0
     assert compare_volumes(out[7], out[8], 0.0) == 0.0
 
