@@ -305,11 +305,19 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
     const bool lean_ok = pk_ok && 4 * (HW + W) <= (int64_t{1} << 31);
 // lean kernel + exact fix-up launch (FG / FNT: the fix-up kernel's group size and threads)
 #define MQR_LAUNCH_LEAN(RR, NT, PIPE, RZ, WPE, FG, FNT) MQR_LAUNCH_LEANC(RR, NT, PIPE, RZ, WPE, false, FG, FNT)
+#define MQR_LAUNCH_TILE(RR, NT, FG, FNT)                                                                        \
+    hipLaunchKernelGGL((k_integrate_tile<RR, NT>), dim3(grid), dim3(NT), 0, s, list, lmask, v->bad[p], counters, \
+                       v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp, depth_frame, depth_max,      \
+                       sdf_trunc);                                                                                \
+    hipLaunchKernelGGL((k_integrate_t<RR, FG, 0, false, FNT>), dim3(8), dim3(FNT), 0, s, v->bad[p],                \
+                       reinterpret_cast<const uint32_t*>(v->bad[p] + v->list_cap), (int32_t*)nullptr,             \
+                       counters + (kBadCount - kListCount), v->list_cap, t, v->pool, v->voxel_size, depths, HW,   \
+                       H, W, fp, depth_frame, depth_scale, depth_max, sdf_trunc)
 #define MQR_LAUNCH_LEANC(RR, NT, PIPE, RZ, WPE, CUBE, FG, FNT)                                                    \
     hipLaunchKernelGGL((k_integrate_lean<RR, NT, PIPE, RZ, WPE, CUBE>), dim3(grid), dim3(NT), 0, s, list, lmask,   \
                        v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp,          \
                        depth_frame, depth_max, sdf_trunc);                                                        \
-    hipLaunchKernelGGL((k_integrate_t<RR, FG, 0, false, FNT>), dim3(64), dim3(FNT), 0, s, v->bad[p],               \
+    hipLaunchKernelGGL((k_integrate_t<RR, FG, 0, false, FNT>), dim3(8), dim3(FNT), 0, s, v->bad[p],               \
                        reinterpret_cast<const uint32_t*>(v->bad[p] + v->list_cap), (int32_t*)nullptr,             \
                        counters + (kBadCount - kListCount), v->list_cap, t, v->pool, v->voxel_size, depths, HW,   \
                        H, W, fp, depth_frame, depth_scale, depth_max, sdf_trunc)
@@ -322,7 +330,7 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
         var = 0;
     if ((var == 8 || var == 9 || (var >= 13 && var <= 16) || var == 20) && !pk_ok) var = 0;
     if (var >= 30 && var <= 33 && !lmask) var = 0;  // split blocks need the longest-first mask copy
-    if (var >= 40 && var <= 53 && !lean_ok) var = 0;
+    if (((var >= 40 && var <= 53) || var == 56 || var == 57) && !lean_ok) var = 0;
     if (v->R == 16 && var != 1) {
         switch (var) {
             case 40: MQR_LAUNCH_LEAN(16, 512, true, 1, 1, 4, 512); break;
@@ -373,6 +381,8 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
             case 28: MQR_LAUNCH_INTW(16, 8, false, false, 512, 8); break;
             case 29: MQR_LAUNCH_INTW(16, 2, false, false, 256, 8); break;
             case 54: MQR_LAUNCH_INT(16, 4, false, false, 512); break;
+            case 56: MQR_LAUNCH_TILE(16, 512, 4, 512); break;
+            case 57: MQR_LAUNCH_TILE(16, 256, 4, 512); break;
             // default: the lean kernel (512 threads x 8 voxels, column mapping, 3-op reciprocals;
             // fastest on MI355X, tools/ab_integrate.py); the exact branchy kernel where the lean one's
             // preconditions (unit depth scale, trunc in range, frame size) do not hold
@@ -405,6 +415,7 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
 #undef MQR_LAUNCH_PK
 #undef MQR_LAUNCH_LEAN
 #undef MQR_LAUNCH_LEANC
+#undef MQR_LAUNCH_TILE
     MQR_CHECK_HIP(hipGetLastError());
     if (v->profile) {
         MQR_CHECK_HIP(hipEventRecord(e1, s));

@@ -727,20 +727,26 @@ __device__ __forceinline__ void lean_gather(float (&dv)[ZPER], bool& bad, const 
                                             __amdgpu_buffer_rsrc_t rs, const float (&xs)[ZPER],
                                             const float (&ys)[ZPER], const float (&zs)[ZPER], uint32_t W4, float hf,
                                             float hm1, float wm1) {
+    // frame constants as values (the scheduling barriers below would otherwise force a reload of
+    // every field per voxel and keep the partial products apart)
+    float e[12];
+#pragma unroll
+    for (int j = 0; j < 12; ++j) e[j] = fp.ext[j];
+    const float fx = fp.fx, fy = fp.fy, cx = fp.cx, cy = fp.cy;
 #pragma unroll
     for (int k = 0; k < ZPER; ++k) {
         // z-independent partial products: one per thread in the column mapping (equal operands are
         // merged by the compiler), one per cube column in the cube mapping
-        const float ax = xs[k] * fp.ext[0] + ys[k] * fp.ext[1];
-        const float ay = xs[k] * fp.ext[4] + ys[k] * fp.ext[5];
-        const float az = xs[k] * fp.ext[8] + ys[k] * fp.ext[9];
-        const float xc = (ax + zs[k] * fp.ext[2]) + fp.ext[3];
-        const float yc = (ay + zs[k] * fp.ext[6]) + fp.ext[7];
-        const float zc = (az + zs[k] * fp.ext[10]) + fp.ext[11];
+        const float ax = xs[k] * e[0] + ys[k] * e[1];
+        const float ay = xs[k] * e[4] + ys[k] * e[5];
+        const float az = xs[k] * e[8] + ys[k] * e[9];
+        const float xc = (ax + zs[k] * e[2]) + e[3];
+        const float yc = (ay + zs[k] * e[6]) + e[7];
+        const float zc = (az + zs[k] * e[10]) + e[11];
         bad |= (__float_as_uint(zc) - 0x2D800000u) > 0x30000000u;  // not 2^-36 <= zc <= 2^60
         const float inv_z = RZ == 2 ? rcp_m(zc) : rcp_nm(zc);
-        const float u = fp.fx * xc * inv_z + fp.cx;
-        const float v = fp.fy * yc * inv_z + fp.cy;
+        const float u = fx * xc * inv_z + cx;
+        const float v = fy * yc * inv_z + cy;
         const bool in = (v >= 0) & (u >= 0) & (v <= hm1) & (u <= wm1);
         const int ui = (int)(in ? u : 0.f), vi = (int)(in ? v : hf);
         const uint32_t off = __umul24((uint32_t)vi, W4) + ((uint32_t)ui << 2);
@@ -756,10 +762,11 @@ template <int ZPER>
 __device__ __forceinline__ void lean_update(float2 (&tw)[ZPER], const float (&dv)[ZPER], const FrameParams& fp,
                                             const float (&xs)[ZPER], const float (&ys)[ZPER],
                                             const float (&zs)[ZPER], float depth_max, float sdf_trunc, float y1t) {
+    const float e8 = fp.ext[8], e9 = fp.ext[9], e10 = fp.ext[10], e11 = fp.ext[11];
 #pragma unroll
     for (int k = 0; k < ZPER; ++k) {
-        const float az = xs[k] * fp.ext[8] + ys[k] * fp.ext[9];
-        const float zc = (az + zs[k] * fp.ext[10]) + fp.ext[11];
+        const float az = xs[k] * e8 + ys[k] * e9;
+        const float zc = (az + zs[k] * e10) + e11;
         const float d = dv[k];
         const float sdf = d - zc;
         // zc > 0 holds in every block that is not handed to the fix-up launch
@@ -832,13 +839,18 @@ __global__ __launch_bounds__(NT, WPE) void k_integrate_lean(const int32_t* __res
             float2 tw[ZPER];
             float xs[ZPER], ys[ZPER], zs[ZPER];
             bool bad = false;
+            // column mapping: one (x, y) per thread, shared by all its voxels (one value, not ZPER copies)
+            const float xs0 = (float)(xb * R + tid % R) * voxel_size;
+            const float ys0 = (float)(yb * R + (tid / R) % R) * voxel_size;
 #pragma unroll
             for (int k = 0; k < ZPER; ++k) {
                 int x, y, z;
                 lean_voxel<R, NT, CUBE>(tid, k, x, y, z);
-                tw[k] = pool_load(vox, 8u * (uint32_t)(z * R2 + y * R + x), 0);
-                xs[k] = (float)(xb * R + x) * voxel_size;
-                ys[k] = (float)(yb * R + y) * voxel_size;
+                // column mapping: voxel k * NT + tid, i.e. one VGPR offset and a constant per voxel
+                tw[k] = CUBE ? pool_load(vox, 8u * (uint32_t)(z * R2 + y * R + x), 0)
+                             : pool_load(vox, 8u * (uint32_t)tid, k * NT * (int)sizeof(float2));
+                xs[k] = CUBE ? (float)(xb * R + x) * voxel_size : xs0;
+                ys[k] = CUBE ? (float)(yb * R + y) * voxel_size : ys0;
                 zs[k] = (float)(zb * R + z) * voxel_size;
                 const float w = tw[k].y;  // rcp_m(w + 1) needs integer weights (this batch adds <= 32)
                 bad |= !(w >= 0.0f && w <= 0x1p23f && w == __builtin_truncf(w));
@@ -879,6 +891,177 @@ __global__ __launch_bounds__(NT, WPE) void k_integrate_lean(const int32_t* __res
                 for (int k = 0; k < ZPER; ++k) {
                     int x, y, z;
                     lean_voxel<R, NT, CUBE>(tid, k, x, y, z);
+                    if (CUBE)
+                        pool_store(vox, 8u * (uint32_t)(z * R2 + y * R + x), 0, tw[k]);
+                    else
+                        pool_store(vox, 8u * (uint32_t)tid, k * NT * (int)sizeof(float2), tw[k]);
+                }
+            }
+        }
+        __syncthreads();
+        if (tid == 0) t.mask[slot] = 0;
+    }
+}
+
+// ---- tiled lean integrate (variants 56-57) ------------------------------------------------------
+// The lean kernel spends its time in the L1 (one tag lookup per distinct line per gather lane group:
+// ~46 per 64-lane depth gather, rocprofv3 TCP_TOTAL_CACHE_ACCESSES).  Here the depth rectangle a
+// block projects to is copied into LDS once per (block, frame) with row-coalesced loads and the
+// voxel gathers read LDS.  The depth values are the same, so the result is the lean kernel's.
+constexpr int kTilePx = 12288;  // 48 KiB of depth per workgroup
+
+// Conservative pixel rectangle of block (xb, yb, zb)'s projection into one frame, computed by one
+// whole wave: the 8 corner voxel centres are projected with the kernel's own operations (corner =
+// lane & 7), padded by 2 px and clamped to the image.  Voxel centres inside the block project into
+// the convex hull of the corners when every corner is in front of the camera (float rounding moves
+// a projection by far less than the pad); a voxel that still falls outside reads global memory.
+// rect = {u0, v0, width, height}; width 0 = no tile (a corner not in 2^-36 <= zc <= 2^60, a
+// non-finite projection, or a rectangle larger than the tile).
+__device__ __forceinline__ void block_rect(const FrameParams& fp, int xb, int yb, int zb, int R, float voxel_size,
+                                           int H, int W, int (&rect)[4]) {
+    const int c = threadIdx.x & 7;
+    const float xs = (float)(xb * R + (c & 1) * (R - 1)) * voxel_size;
+    const float ys = (float)(yb * R + ((c >> 1) & 1) * (R - 1)) * voxel_size;
+    const float zs = (float)(zb * R + ((c >> 2) & 1) * (R - 1)) * voxel_size;
+    const float xc = ((xs * fp.ext[0] + ys * fp.ext[1]) + zs * fp.ext[2]) + fp.ext[3];
+    const float yc = ((xs * fp.ext[4] + ys * fp.ext[5]) + zs * fp.ext[6]) + fp.ext[7];
+    const float zc = ((xs * fp.ext[8] + ys * fp.ext[9]) + zs * fp.ext[10]) + fp.ext[11];
+    const float inv_z = rcp_m(zc);
+    const float u = fp.fx * xc * inv_z + fp.cx;
+    const float v = fp.fy * yc * inv_z + fp.cy;
+    const bool ok = zc >= 0x1p-36f && zc <= 0x1p60f && fabsf(u) < 1e7f && fabsf(v) < 1e7f;
+    float umin = u, umax = u, vmin = v, vmax = v;
+#pragma unroll
+    for (int o = 4; o >= 1; o >>= 1) {
+        umin = fminf(umin, __shfl_xor(umin, o, 64));
+        umax = fmaxf(umax, __shfl_xor(umax, o, 64));
+        vmin = fminf(vmin, __shfl_xor(vmin, o, 64));
+        vmax = fmaxf(vmax, __shfl_xor(vmax, o, 64));
+    }
+    const int u0 = max(0, (int)floorf(umin) - 2), u1 = min(W - 1, (int)floorf(umax) + 2);
+    const int v0 = max(0, (int)floorf(vmin) - 2), v1 = min(H - 1, (int)floorf(vmax) + 2);
+    const int tw = max(u1 - u0 + 1, 0), th = max(v1 - v0 + 1, 0);
+    const bool use = __ballot(!ok) == 0 && tw * th <= kTilePx;
+    rect[0] = u0;
+    rect[1] = v0;
+    rect[2] = use ? tw : 0;
+    rect[3] = use ? th : 0;
+}
+
+// lean_gather with the depth read from the staged rectangle (global memory for an in-image voxel
+// outside it, 0 for an out-of-image voxel).
+template <int ZPER>
+__device__ __forceinline__ void lean_gather_tile(float (&dv)[ZPER], bool& bad, const FrameParams& fp,
+                                                 const float* __restrict__ dep, const float* tile, int u0, int v0,
+                                                 int tlw, int tlh, const float (&xs)[ZPER], const float (&ys)[ZPER],
+                                                 const float (&zs)[ZPER], int W, float hf, float hm1, float wm1) {
+#pragma unroll
+    for (int k = 0; k < ZPER; ++k) {
+        const float ax = xs[k] * fp.ext[0] + ys[k] * fp.ext[1];
+        const float ay = xs[k] * fp.ext[4] + ys[k] * fp.ext[5];
+        const float az = xs[k] * fp.ext[8] + ys[k] * fp.ext[9];
+        const float xc = (ax + zs[k] * fp.ext[2]) + fp.ext[3];
+        const float yc = (ay + zs[k] * fp.ext[6]) + fp.ext[7];
+        const float zc = (az + zs[k] * fp.ext[10]) + fp.ext[11];
+        bad |= (__float_as_uint(zc) - 0x2D800000u) > 0x30000000u;  // not 2^-36 <= zc <= 2^60
+        const float inv_z = rcp_m(zc);
+        const float u = fp.fx * xc * inv_z + fp.cx;
+        const float v = fp.fy * yc * inv_z + fp.cy;
+        const bool in = (v >= 0) & (u >= 0) & (v <= hm1) & (u <= wm1);
+        const int ui = (int)(in ? u : 0.f), vi = (int)(in ? v : hf);
+        const uint32_t tu = (uint32_t)(ui - u0), tv = (uint32_t)(vi - v0);  // row H never lies in the tile
+        float d = 0.f;
+        if (tu < (uint32_t)tlw && tv < (uint32_t)tlh)
+            d = tile[__umul24(tv, (uint32_t)tlw) + tu];
+        else if (in)
+            d = dep[vi * W + ui];
+        dv[k] = d;
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+// Tiled lean integrate (column mapping, RZ = 2; same preconditions and fix-up hand-off as the lean
+// kernel).  Per (block, frame): wave 0 computes the rectangle, the workgroup copies it into LDS
+// (one wave per row, lanes along the row), then every thread gathers and updates its voxels.
+template <int R, int NT>
+__global__ __launch_bounds__(NT) void k_integrate_tile(const int32_t* __restrict__ list,
+                                                      const uint32_t* __restrict__ lmask,
+                                                      int32_t* __restrict__ bad_out, int* __restrict__ counters,
+                                                      int64_t list_cap, Table t, float2* __restrict__ pool,
+                                                      float voxel_size, const float* __restrict__ depths, int64_t HW,
+                                                      int H, int W, const FrameParams* __restrict__ fps,
+                                                      const int64_t* __restrict__ depth_frame, float depth_max,
+                                                      float sdf_trunc) {
+    constexpr int R2 = R * R;
+    constexpr int R3 = R2 * R;
+    constexpr int ZPER = R3 / NT;
+    constexpr int NW = NT / 64;
+    static_assert(R3 % NT == 0 && NT % R2 == 0, "NT must divide R^3 and be a multiple of R^2");
+    __shared__ float tile[kTilePx];
+    __shared__ int s_rect[4];
+    const int64_t n = min((int64_t)counters[kListCount], list_cap);
+    const float hf = (float)H, hm1 = (float)H - 1.0f, wm1 = (float)W - 1.0f;
+    const float y0t = __builtin_amdgcn_rcpf(sdf_trunc);
+    const float y1t = __builtin_fmaf(__builtin_fmaf(-sdf_trunc, y0t, 1.0f), y0t, y0t);
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    for (int64_t i = blockIdx.x; i < n; i += gridDim.x) {
+        const int32_t slot = list[i];
+        const int buf = t.vals[slot];
+        const uint32_t mask = __builtin_amdgcn_readfirstlane(lmask ? lmask[i] : t.mask[slot]);
+        int xb, yb, zb;
+        unpack_key(t.keys[slot], xb, yb, zb);
+        if (buf >= 0 && mask) {
+            const __amdgpu_buffer_rsrc_t vox = __builtin_amdgcn_make_buffer_rsrc(
+                pool + (int64_t)buf * R3, (short)0, (int)(R3 * sizeof(float2)), 0x00020000);
+            float2 tw[ZPER];
+            float xs[ZPER], ys[ZPER], zs[ZPER];
+            bool bad = false;
+#pragma unroll
+            for (int k = 0; k < ZPER; ++k) {
+                int x, y, z;
+                lean_voxel<R, NT, false>(tid, k, x, y, z);
+                tw[k] = pool_load(vox, 8u * (uint32_t)(z * R2 + y * R + x), 0);
+                xs[k] = (float)(xb * R + x) * voxel_size;
+                ys[k] = (float)(yb * R + y) * voxel_size;
+                zs[k] = (float)(zb * R + z) * voxel_size;
+                const float w = tw[k].y;
+                bad |= !(w >= 0.0f && w <= 0x1p23f && w == __builtin_truncf(w));
+            }
+            uint32_t m = mask;
+            while (m) {
+                const int f = __builtin_ctz(m);
+                m &= m - 1;
+                const FrameParams& fp = fps[f];
+                const float* __restrict__ dep = depths + depth_frame[f] * HW;
+                if (wave == 0) {
+                    int rect[4];
+                    block_rect(fp, xb, yb, zb, R, voxel_size, H, W, rect);
+                    if (lane < 4) s_rect[lane] = rect[lane];
+                }
+                __syncthreads();  // the rectangle is out, and every wave is done with the last tile
+                const int u0 = __builtin_amdgcn_readfirstlane(s_rect[0]), v0 = __builtin_amdgcn_readfirstlane(s_rect[1]);
+                const int tlw = __builtin_amdgcn_readfirstlane(s_rect[2]);
+                const int tlh = __builtin_amdgcn_readfirstlane(s_rect[3]);
+                for (int r = wave; r < tlh; r += NW) {
+                    const float* src = dep + (int64_t)(v0 + r) * W + u0;
+                    for (int c = lane; c < tlw; c += 64) tile[r * tlw + c] = src[c];
+                }
+                __syncthreads();
+                float dv[ZPER];
+                lean_gather_tile<ZPER>(dv, bad, fp, dep, tile, u0, v0, tlw, tlh, xs, ys, zs, W, hf, hm1, wm1);
+                lean_update<ZPER>(tw, dv, fp, xs, ys, zs, depth_max, sdf_trunc, y1t);
+            }
+            if (__syncthreads_or(bad)) {  // block-uniform: the exact fix-up launch redoes it from the pool
+                if (tid == 0) {
+                    const int j = atomicAdd(&counters[kBadCount], 1);
+                    bad_out[j] = slot;
+                    bad_out[list_cap + j] = (int32_t)mask;
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < ZPER; ++k) {
+                    int x, y, z;
+                    lean_voxel<R, NT, false>(tid, k, x, y, z);
                     pool_store(vox, 8u * (uint32_t)(z * R2 + y * R + x), 0, tw[k]);
                 }
             }
