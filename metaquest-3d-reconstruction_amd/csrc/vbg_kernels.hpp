@@ -1071,6 +1071,204 @@ __global__ __launch_bounds__(NT) void k_integrate_tile(const int32_t* __restrict
     }
 }
 
+// ---- double-buffered tile integrate (variant 58) --------------------------------------------------
+// The lean kernel is bound by the L1 path of its depth gathers: a scattered dword gather costs about
+// one tag lookup per in-image lane (rocprofv3: ~43 TCP accesses and ~34 TA-busy cycles per gather
+// instruction, TA busy ~80 % of the kernel).  Here the rectangle a block projects to (<= 64 x 64 px)
+// is copied into LDS by async row loads (global_load_lds, one wave-instruction per row), the next
+// frame's rectangle while the current frame is integrated, and the voxel gathers read LDS.  Same
+// depth values and arithmetic as the lean kernel.  A frame whose rectangle does not fit (block close
+// to the camera) or whose corners are not safely in front of the camera is gathered directly.
+constexpr int kTileDim = 64;
+typedef __attribute__((address_space(1))) void gvoid_t;
+typedef __attribute__((address_space(3))) void lvoid_t;
+
+// Rectangles of every frame of a block's batch mask in one pass of the workgroup (slot = thread / 8
+// = rank of the frame in the mask, corner = thread % 8; NT >= 256): the 8 corner voxel centres are
+// projected with the kernel's own operations, padded by 2 px and clamped to the image (voxel centres
+// inside the block project into the hull of the corners when all corners are in front of the
+// camera; rounding moves a projection far less than the pad, and a voxel found outside the
+// rectangle sends the block to the exact fix-up launch).  {u0, v0, w, h}; w = -1: gather directly.
+__device__ __forceinline__ void block_rects(const FrameParams* __restrict__ fps, uint32_t mask, int xb, int yb, int zb,
+                                            int R, float voxel_size, int H, int W, int4* s_rect) {
+    const int slot = threadIdx.x >> 3, c = threadIdx.x & 7;
+    uint32_t m = mask;
+    for (int q = 0; q < slot && m; ++q) m &= m - 1;
+    const bool have = m != 0;
+    const FrameParams& fp = fps[have ? __builtin_ctz(m) : 0];
+    const float xs = (float)(xb * R + (c & 1) * (R - 1)) * voxel_size;
+    const float ys = (float)(yb * R + ((c >> 1) & 1) * (R - 1)) * voxel_size;
+    const float zs = (float)(zb * R + ((c >> 2) & 1) * (R - 1)) * voxel_size;
+    const float xc = ((xs * fp.ext[0] + ys * fp.ext[1]) + zs * fp.ext[2]) + fp.ext[3];
+    const float yc = ((xs * fp.ext[4] + ys * fp.ext[5]) + zs * fp.ext[6]) + fp.ext[7];
+    const float zc = ((xs * fp.ext[8] + ys * fp.ext[9]) + zs * fp.ext[10]) + fp.ext[11];
+    const float inv_z = rcp_m(zc);
+    const float u = fp.fx * xc * inv_z + fp.cx;
+    const float v = fp.fy * yc * inv_z + fp.cy;
+    int ok = zc >= 0x1p-36f && zc <= 0x1p60f && fabsf(u) < 1e7f && fabsf(v) < 1e7f;
+    float umin = u, umax = u, vmin = v, vmax = v;
+#pragma unroll
+    for (int o = 4; o >= 1; o >>= 1) {
+        umin = fminf(umin, __shfl_xor(umin, o, 64));
+        umax = fmaxf(umax, __shfl_xor(umax, o, 64));
+        vmin = fminf(vmin, __shfl_xor(vmin, o, 64));
+        vmax = fmaxf(vmax, __shfl_xor(vmax, o, 64));
+        ok &= __shfl_xor(ok, o, 64);
+    }
+    if (have && c == 0) {
+        int4 r = make_int4(0, 0, -1, 0);
+        if (ok) {
+            const int u0 = max(0, (int)floorf(umin) - 2), u1 = min(W - 1, (int)floorf(umax) + 2);
+            const int v0 = max(0, (int)floorf(vmin) - 2), v1 = min(H - 1, (int)floorf(vmax) + 2);
+            const int w = u1 - u0 + 1, h = v1 - v0 + 1;
+            if (w <= 0 || h <= 0)
+                r = make_int4(0, 0, 0, 0);  // projection outside the image: nothing to stage
+            else if (w <= kTileDim && h <= kTileDim)
+                r = make_int4(u0, v0, w, h);
+        }
+        s_rect[slot] = r;
+    }
+}
+
+// Async copy of a rectangle (w, h > 0, inside the image) into one LDS buffer of row pitch 64: one
+// global_load_lds per row and wave (LDS destination = row base + lane * 4); lanes past the width
+// re-read the last column.
+__device__ __forceinline__ void tile_copy(const float* __restrict__ dep, int W, int4 r, float* buf, int nw) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int col = r.x + min(lane, r.z - 1);
+    for (int row = wave; row < r.w; row += nw)
+        __builtin_amdgcn_global_load_lds((gvoid_t*)(dep + (int64_t)(r.y + row) * W + col),
+                                         (lvoid_t*)(buf + row * kTileDim), 4, 0, 0);
+}
+
+// lean_gather reading the staged rectangle; an in-image voxel outside it sets `bad`.
+template <int ZPER>
+__device__ __forceinline__ void tile_gather(float (&dv)[ZPER], bool& bad, const FrameParams& fp, const float* tile,
+                                            int4 r, const float (&xs)[ZPER], const float (&ys)[ZPER],
+                                            const float (&zs)[ZPER], float hm1, float wm1) {
+    float e[12];
+#pragma unroll
+    for (int j = 0; j < 12; ++j) e[j] = fp.ext[j];
+    const float fx = fp.fx, fy = fp.fy, cx = fp.cx, cy = fp.cy;
+#pragma unroll
+    for (int k = 0; k < ZPER; ++k) {
+        const float ax = xs[k] * e[0] + ys[k] * e[1];
+        const float ay = xs[k] * e[4] + ys[k] * e[5];
+        const float az = xs[k] * e[8] + ys[k] * e[9];
+        const float xc = (ax + zs[k] * e[2]) + e[3];
+        const float yc = (ay + zs[k] * e[6]) + e[7];
+        const float zc = (az + zs[k] * e[10]) + e[11];
+        bad |= (__float_as_uint(zc) - 0x2D800000u) > 0x30000000u;  // not 2^-36 <= zc <= 2^60
+        const float inv_z = rcp_m(zc);
+        const float u = fx * xc * inv_z + cx;
+        const float v = fy * yc * inv_z + cy;
+        const bool in = (v >= 0) & (u >= 0) & (v <= hm1) & (u <= wm1);
+        const int ui = (int)(in ? u : 0.f), vi = (int)(in ? v : 0.f);
+        const uint32_t tu = (uint32_t)(ui - r.x), tv = (uint32_t)(vi - r.y);
+        const bool hit = (tu < (uint32_t)r.z) & (tv < (uint32_t)r.w);
+        bad |= in & !hit;
+        const float t = tile[hit ? tv * kTileDim + tu : 0];
+        dv[k] = (in & hit) ? t : 0.f;
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+template <int R, int NT>
+__global__ __launch_bounds__(NT) void k_integrate_dbt(const int32_t* __restrict__ list,
+                                                     const uint32_t* __restrict__ lmask,
+                                                     int32_t* __restrict__ bad_out, int* __restrict__ counters,
+                                                     int64_t list_cap, Table t, float2* __restrict__ pool,
+                                                     float voxel_size, const float* __restrict__ depths, int64_t HW,
+                                                     int H, int W, const FrameParams* __restrict__ fps,
+                                                     const int64_t* __restrict__ depth_frame, float depth_max,
+                                                     float sdf_trunc) {
+    constexpr int R2 = R * R;
+    constexpr int R3 = R2 * R;
+    constexpr int ZPER = R3 / NT;
+    constexpr int NW = NT / 64;
+    static_assert(R3 % NT == 0 && NT % R2 == 0 && NT >= 8 * kMaxBatch, "layout");
+    __shared__ float tiles[2][kTileDim * kTileDim];
+    __shared__ int4 s_rect[kMaxBatch];
+    const int64_t n = min((int64_t)counters[kListCount], list_cap);
+    const float hf = (float)H, hm1 = (float)H - 1.0f, wm1 = (float)W - 1.0f;
+    const uint32_t W4 = 4u * (uint32_t)W, bytes = 4u * (uint32_t)HW;
+    const float y0t = __builtin_amdgcn_rcpf(sdf_trunc);
+    const float y1t = __builtin_fmaf(__builtin_fmaf(-sdf_trunc, y0t, 1.0f), y0t, y0t);
+    const int tid = threadIdx.x;
+    for (int64_t i = blockIdx.x; i < n; i += gridDim.x) {
+        const int32_t slot = list[i];
+        const int buf = t.vals[slot];
+        const uint32_t mask = __builtin_amdgcn_readfirstlane(lmask ? lmask[i] : t.mask[slot]);
+        int xb, yb, zb;
+        unpack_key(t.keys[slot], xb, yb, zb);
+        if (buf >= 0 && mask) {
+            const __amdgpu_buffer_rsrc_t vox = __builtin_amdgcn_make_buffer_rsrc(
+                pool + (int64_t)buf * R3, (short)0, (int)(R3 * sizeof(float2)), 0x00020000);
+            float2 tw[ZPER];
+            float xs[ZPER], ys[ZPER], zs[ZPER];
+            bool bad = false;
+            const float xs0 = (float)(xb * R + tid % R) * voxel_size;
+            const float ys0 = (float)(yb * R + (tid / R) % R) * voxel_size;
+#pragma unroll
+            for (int k = 0; k < ZPER; ++k) {
+                tw[k] = pool_load(vox, 8u * (uint32_t)tid, k * NT * (int)sizeof(float2));
+                xs[k] = xs0;
+                ys[k] = ys0;
+                zs[k] = (float)(zb * R + tid / R2 + k * (NT / R2)) * voxel_size;
+                const float w = tw[k].y;
+                bad |= !(w >= 0.0f && w <= 0x1p23f && w == __builtin_truncf(w));
+            }
+            block_rects(fps, mask, xb, yb, zb, R, voxel_size, H, W, s_rect);
+            __syncthreads();
+            uint32_t m = mask;
+            int f = __builtin_ctz(m);
+            m &= m - 1;
+            int j = 0;
+            int4 r = s_rect[0];
+            r = make_int4(__builtin_amdgcn_readfirstlane(r.x), __builtin_amdgcn_readfirstlane(r.y),
+                          __builtin_amdgcn_readfirstlane(r.z), __builtin_amdgcn_readfirstlane(r.w));
+            if (r.z > 0 && r.w > 0) tile_copy(depths + depth_frame[f] * HW, W, r, tiles[0], NW);
+            __syncthreads();  // waits for the copy (vmcnt) as well
+            while (true) {
+                const bool more = m != 0;  // wave-uniform
+                const int g = more ? __builtin_ctz(m) : 0;
+                m &= m - 1;
+                int4 rn = make_int4(0, 0, 0, 0);
+                if (more) {
+                    rn = s_rect[j + 1];
+                    rn = make_int4(__builtin_amdgcn_readfirstlane(rn.x), __builtin_amdgcn_readfirstlane(rn.y),
+                                   __builtin_amdgcn_readfirstlane(rn.z), __builtin_amdgcn_readfirstlane(rn.w));
+                    if (rn.z > 0 && rn.w > 0) tile_copy(depths + depth_frame[g] * HW, W, rn, tiles[(j + 1) & 1], NW);
+                }
+                float dv[ZPER];
+                if (r.z >= 0)
+                    tile_gather<ZPER>(dv, bad, fps[f], tiles[j & 1], r, xs, ys, zs, hm1, wm1);
+                else
+                    lean_gather<ZPER, 2>(dv, bad, fps[f], frame_rsrc(depths + depth_frame[f] * HW, bytes), xs, ys, zs,
+                                         W4, hf, hm1, wm1);
+                lean_update<ZPER>(tw, dv, fps[f], xs, ys, zs, depth_max, sdf_trunc, y1t);
+                if (!more) break;
+                __syncthreads();  // the next rectangle has landed, this one is free
+                f = g;
+                r = rn;
+                ++j;
+            }
+            if (__syncthreads_or(bad)) {
+                if (tid == 0) {
+                    const int jj = atomicAdd(&counters[kBadCount], 1);
+                    bad_out[jj] = slot;
+                    bad_out[list_cap + jj] = (int32_t)mask;
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < ZPER; ++k) pool_store(vox, 8u * (uint32_t)tid, k * NT * (int)sizeof(float2), tw[k]);
+            }
+        }
+        __syncthreads();
+        if (tid == 0) t.mask[slot] = 0;
+    }
+}
+
 // Exhaustive-check kernels for the division shortcut (tests/test_gpu_numerics.py).
 // mode 0: rcp_rn, 1: rcp_nm, 2: rcp_m.
 __global__ void k_check_rcp(int mode, uint32_t lo_bits, uint64_t count, uint32_t* mismatches, uint32_t* first_bad) {

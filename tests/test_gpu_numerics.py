@@ -46,7 +46,7 @@ def test_shortened_reciprocals_exact(which, lo, hi):
 
 INTEGRATE_VARIANTS = {16: (0, 2, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 22, 23, 24, 25, 0x100, 0x106,
                           0x108, 26, 27, 28, 29, 0x200, 0x300, 30, 31, 32, 33, 0x21e, 34, 35, 36, 37,
-                          40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 52, 53, 54, 56, 57, 0x128, 0x228, 0x130),
+                          40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 52, 53, 54, 56, 57, 58, 0x128, 0x228, 0x130),
                       8: (0, 6, 8, 0x101, 0x200, 40, 48)}
 
 
@@ -148,7 +148,7 @@ def test_lean_integrate_exact_fallback():
     Ks = np.concatenate([seq["K"][:1], seq["K"]])
     Ts = np.concatenate([np.eye(4)[None], seq["T_wc"]])
     cases = ((16, 1), (16, 40), (16, 41), (16, 42), (16, 43), (16, 44), (16, 45), (16, 46), (16, 47), (16, 48),
-             (16, 49), (16, 50), (16, 51), (16, 52), (16, 53), (16, 56), (16, 57), (8, 1), (8, 40), (8, 48))
+             (16, 49), (16, 50), (16, 51), (16, 52), (16, 53), (16, 56), (16, 57), (16, 58), (8, 1), (8, 40), (8, 48))
     out = []
     for R, variant in cases:
         v = VoxelBlockGrid(voxel_size=0.005, block_resolution=R, block_count=64)
@@ -164,7 +164,7 @@ def test_lean_integrate_exact_fallback():
         v.import_blocks(keys, tsdf, wgt)
         v.integrate_frames(depths[3:], Ks[3:], Ts[3:], depth_scale=1.0, depth_max=4.0, trunc_voxel_multiplier=10.0)
         out.append(v.export())
-    for i in range(1, 17):
+    for i in range(1, 18):
         assert compare_volumes(out[0], out[i], 0.0) == 0.0, cases[i]
-    assert compare_volumes(out[17], out[18], 0.0) == 0.0
-    assert compare_volumes(out[17], out[19], 0.0) == 0.0
+    assert compare_volumes(out[18], out[19], 0.0) == 0.0
+    assert compare_volumes(out[18], out[20], 0.0) == 0.0
