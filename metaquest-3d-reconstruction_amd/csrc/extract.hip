@@ -21,6 +21,10 @@
 
 #include <algorithm>
 
+#include <mutex>
+#include <tuple>
+#include <vector>
+
 #include "mqr_common.hpp"
 #include "mqr_mc_tables.h"
 
@@ -907,11 +911,52 @@ static int scan_totals(mqr_vbg* v, const ExScratch& e, int64_t n, int arrays, in
     return 0;
 }
 
-// One allocation for positions, normals and triangles (one hipMalloc instead of three).
+static std::mutex g_geom_mu;
+static std::vector<std::tuple<int, void*, size_t>> g_geom_cache;  // (device, block, capacity)
+constexpr size_t kGeomCacheBlocks = 4;
+
+void* geom_block_alloc(int device, size_t bytes, size_t* cap) {
+    {
+        std::lock_guard<std::mutex> lk(g_geom_mu);
+        int best = -1;
+        for (size_t i = 0; i < g_geom_cache.size(); ++i) {
+            const auto& e = g_geom_cache[i];
+            if (std::get<0>(e) == device && std::get<2>(e) >= bytes &&
+                (best < 0 || std::get<2>(e) < std::get<2>(g_geom_cache[best])))
+                best = (int)i;
+        }
+        if (best >= 0) {
+            void* p = std::get<1>(g_geom_cache[best]);
+            *cap = std::get<2>(g_geom_cache[best]);
+            g_geom_cache.erase(g_geom_cache.begin() + best);
+            return p;
+        }
+    }
+    const size_t want = (bytes + (size_t(1) << 20) - 1) & ~((size_t(1) << 20) - 1);
+    void* p = nullptr;
+    if (hipMalloc(&p, want) != hipSuccess) return nullptr;
+    *cap = want;
+    return p;
+}
+
+void geom_block_release(int device, void* p, size_t cap) {
+    if (!p) return;
+    {
+        std::lock_guard<std::mutex> lk(g_geom_mu);
+        if (cap && g_geom_cache.size() < kGeomCacheBlocks) {
+            g_geom_cache.emplace_back(device, p, cap);
+            return;
+        }
+    }
+    (void)hipFree(p);
+}
+
+// One allocation for positions, normals and triangles, recycled across results (geom_block_alloc).
 static int alloc_geom(mqr_geom* g, int64_t nv, int64_t nt) {
     const size_t sv = align256(sizeof(float) * 3 * std::max<int64_t>(nv, 1));
     const size_t st = align256(sizeof(int32_t) * 3 * std::max<int64_t>(nt, 1));
-    MQR_CHECK_HIP(hipMalloc(&g->blk, 2 * sv + st));
+    g->blk = geom_block_alloc(g->device, 2 * sv + st, &g->blk_cap);
+    MQR_REQUIRE(g->blk, "geometry: device allocation failed");
     char* p = static_cast<char*>(g->blk);
     g->pos = reinterpret_cast<float*>(p);
     g->nrm = reinterpret_cast<float*>(p + sv);
@@ -1033,7 +1078,9 @@ int mqr_geom_free(mqr_geom* g) {
     if (!g) return 0;
     (void)hipSetDevice(g->device);
     if (g->blk) {
-        (void)hipFree(g->blk);
+        // the block may still be read by work queued on a stream (a device-side copy): drain first
+        (void)hipDeviceSynchronize();
+        geom_block_release(g->device, g->blk, g->blk_cap);
     } else {
         if (g->pos) (void)hipFree(g->pos);
         if (g->nrm) (void)hipFree(g->nrm);

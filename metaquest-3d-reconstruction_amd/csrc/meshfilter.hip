@@ -824,7 +824,8 @@ int mqr_mesh_filter_components(int device, const float* vertices, const float* n
     g->nt = m.nt;
     const size_t sv = (sizeof(float) * 3 * (size_t)std::max<int64_t>(m.nv, 1) + 255) & ~(size_t)255;
     const size_t stb = (sizeof(int32_t) * 3 * (size_t)std::max<int64_t>(m.nt, 1) + 255) & ~(size_t)255;
-    if (hipMalloc(&g->blk, 2 * sv + stb) != hipSuccess) {
+    g->blk = geom_block_alloc(device, 2 * sv + stb, &g->blk_cap);
+    if (!g->blk) {
         delete g;
         set_error("mesh filter: device allocation failed");
         return 1;

@@ -162,9 +162,15 @@ struct mqr_geom {
     float* nrm = nullptr;
     int32_t* tri = nullptr;
     void* blk = nullptr;  // when set, pos / nrm / tri are carved from this one allocation
+    size_t blk_cap = 0;   // its size (a recycled block may be larger than needed)
 };
 
 namespace mqr {
+// Device blocks for geometry results, recycled by mqr_geom_free (a few per device) instead of
+// hipFree + hipMalloc: hipFree synchronises the device and a fresh multi-10-MB hipMalloc maps new
+// pages, together 1-3 ms per extraction of a 2 M-triangle mesh.
+void* geom_block_alloc(int device, size_t bytes, size_t* cap);
+void geom_block_release(int device, void* p, size_t cap);
 int grow_pool(mqr_vbg* v, int64_t need);
 int sync_all(mqr_vbg* v);
 }  // namespace mqr
