@@ -142,6 +142,16 @@ struct mqr_vbg {
     // profiling
     bool profile = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> int_events, touch_events;
+    std::vector<hipEvent_t> ev_pool;  // timing events, created once and reused (hipEventCreate per
+    size_t ev_used = 0;               // launch added ~0.1 ms to a 500-frame step)
+    hipEvent_t pooled_event() {
+        if (ev_used == ev_pool.size()) {
+            hipEvent_t e = nullptr;
+            if (hipEventCreate(&e) != hipSuccess) return nullptr;
+            ev_pool.push_back(e);
+        }
+        return ev_pool[ev_used++];
+    }
     mqr_stats stats{};
 
     mqr::Table table(int parity) const {

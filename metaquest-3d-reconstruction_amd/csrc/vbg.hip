@@ -271,8 +271,9 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
     const FrameParams* fp = v->d_fp[p];
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (v->profile) {
-        MQR_CHECK_HIP(hipEventCreate(&e0));
-        MQR_CHECK_HIP(hipEventCreate(&e1));
+        e0 = v->pooled_event();
+        e1 = v->pooled_event();
+        MQR_REQUIRE(e0 && e1, "profiling: event creation failed");
         MQR_CHECK_HIP(hipEventRecord(e0, s));
     }
     // the unguarded division core needs its constant denominators in range (see div_rn_core)
@@ -454,18 +455,15 @@ static void drain_events(mqr_vbg* v) {
         float ms = 0.f;
         if (hipEventSynchronize(e.second) == hipSuccess && hipEventElapsedTime(&ms, e.first, e.second) == hipSuccess)
             v->stats.integrate_ms += ms;
-        (void)hipEventDestroy(e.first);
-        (void)hipEventDestroy(e.second);
     }
     v->int_events.clear();
     for (auto& e : v->touch_events) {
         float ms = 0.f;
         if (hipEventSynchronize(e.second) == hipSuccess && hipEventElapsedTime(&ms, e.first, e.second) == hipSuccess)
             v->stats.touch_ms += ms;
-        (void)hipEventDestroy(e.first);
-        (void)hipEventDestroy(e.second);
     }
     v->touch_events.clear();
+    v->ev_used = 0;
 }
 
 static int touch_launch(mqr_vbg* v, int p, const float* dbase, int64_t HW, int H, int W, int b, float depth_scale,
@@ -473,8 +471,9 @@ static int touch_launch(mqr_vbg* v, int p, const float* dbase, int64_t HW, int H
     const int n = (H / 4) * (W / 4);
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (v->profile) {
-        MQR_CHECK_HIP(hipEventCreate(&e0));
-        MQR_CHECK_HIP(hipEventCreate(&e1));
+        e0 = v->pooled_event();
+        e1 = v->pooled_event();
+        MQR_REQUIRE(e0 && e1, "profiling: event creation failed");
         MQR_CHECK_HIP(hipEventRecord(e0, v->stream));
     }
     if (n > 0)
@@ -598,6 +597,7 @@ int mqr_vbg_destroy(mqr_vbg* v) {
         if (v->ev_touch[p]) (void)hipEventDestroy(v->ev_touch[p]);
         if (v->ev_int[p]) (void)hipEventDestroy(v->ev_int[p]);
     }
+    for (hipEvent_t e : v->ev_pool) (void)hipEventDestroy(e);
     if (v->counters) (void)hipFree(v->counters);
     if (v->h_counters) (void)hipHostFree(v->h_counters);
     if (v->ex_scratch) (void)hipFree(v->ex_scratch);
@@ -924,6 +924,14 @@ int mqr_check_division(int device, int which, float b, uint32_t lo_bits, uint64_
 int mqr_vbg_profile(mqr_vbg* v, int enable) {
     MQR_REQUIRE(v, "null volume");
     v->profile = enable != 0;
+    // create the timing events now, outside any timed region (4 per batch; more are created on
+    // demand until the next stats read recycles them)
+    MQR_CHECK_HIP(hipSetDevice(v->device));
+    while (v->profile && v->ev_pool.size() < 1024) {
+        hipEvent_t e = nullptr;
+        MQR_CHECK_HIP(hipEventCreate(&e));
+        v->ev_pool.push_back(e);
+    }
     return 0;
 }
 
