@@ -3,7 +3,7 @@
 
 A "step" = integrate the rank's whole 500-frame depth sequence (640x480, procedural room = a
 512^3-voxel volume at 5 mm, R=16, depth_max 4 m, truncation 10 voxels) into an empty volume:
-per 32-frame batch one touch launch (hash insert) + one integrate launch, inputs resident in HBM.
+per 64-frame batch one touch launch (hash insert) + one integrate launch, inputs resident in HBM.
 With N > 1 ranks every rank integrates its own 500 frames of an N*500-frame walk (weak scaling)
 and the step ends with the single RCCL merge of the partial volumes into rank 0.
 
@@ -386,7 +386,7 @@ def main():
                                    "TSDF 5 mm voxels, 512^3 effective volume, R=16, depth_max 4 m, trunc 10",
                        "frames_per_gpu": B, "height": H, "width": W, "voxel_size": args.voxel,
                        "block_resolution": args.block_resolution, "depth_max": args.depth_max,
-                       "trunc_voxel_multiplier": args.trunc, "frame_batch": 32,
+                       "trunc_voxel_multiplier": args.trunc, "frame_batch": 64,
                        "parallelism": f"frame-shard x{world}" + (
                            f" + RCCL merge ({args.merge})" if world > 1 else "")},
             "merge_ms": (sum(merge_times) / len(merge_times) * 1e3) if merge_times else None,

@@ -63,10 +63,11 @@ __host__ __device__ inline uint64_t mix64(uint64_t k) {
 // ---------------------------------------------------------------- hash table (device view)
 // Open addressing, linear probing, 64-bit keys claimed by atomicCAS.  vals = pool buffer
 // index (-1 none yet, -2 pool overflow), mask = frames of the current batch that touched it.
+typedef uint64_t bmask_t;  // one bit per frame of a device batch (<= kMaxBatch frames)
 struct Table {
     uint64_t* keys;
     int32_t* vals;
-    uint32_t* mask;
+    bmask_t* mask;
     int64_t cap;  // power of two
 };
 
@@ -91,7 +92,7 @@ struct FrameParams {
 
 void make_frame_params(const double* K, const double* T_wc, FrameParams* fp);
 
-constexpr int kMaxBatch = 32;         // frames per device batch (one bit each in the slot mask)
+constexpr int kMaxBatch = 64;         // frames per device batch (one bit each in the slot mask)
 constexpr int kFrameCounterBase = 8;  // per-frame raw touch counts live at counters[8 + f]
 constexpr int kCountersTotal = kFrameCounterBase + kMaxBatch;
 
@@ -113,7 +114,7 @@ struct mqr_vbg {
     bool int_pending[2] = {false, false};
 
     mqr::Table tab{};          // main block table (tab.mask == mask[0])
-    uint32_t* mask1 = nullptr; // parity-1 slot masks
+    mqr::bmask_t* mask1 = nullptr; // parity-1 slot masks
     mqr::Table ftab{};         // frustum table for mqr_touch (Open3D's separate frustum hash map)
     float2* pool = nullptr;    // [pool_cap][R3] (tsdf, weight)
     uint64_t* bkeys = nullptr; // [pool_cap] packed key of each buffer
@@ -139,6 +140,7 @@ struct mqr_vbg {
     int kernel_variant = 0;    // integrate kernel configuration (launch_integrate in vbg.hip), 1 = generic
     bool pipelined = true;     // overlap touch(b+1) with integrate(b)
     bool lpt_order = true;     // integrate blocks in longest-first order
+    int batch_frames = mqr::kMaxBatch;  // frames per device batch (A/B: 32, variant bit 0x400)
     // profiling
     bool profile = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> int_events, touch_events;

@@ -5,10 +5,10 @@
 // Data layout in HBM (one volume):
 //   pool   [pool_cap][R^3] float2 (tsdf, weight), voxel [z][y][x] inside a block -> 32 KiB/block at R=16
 //   bkeys  [pool_cap] packed block key of each buffer (for extraction / export)
-//   table  keys u64 / vals i32 / mask u32 x2 (batch parity), open addressing, capacity >= 2x live keys
+//   table  keys u64 / vals i32 / mask u64 x2 (batch parity), open addressing, capacity >= 2x live keys
 //   lists  slots touched by the current batch (appended once per batch, on first touch), x2
 //
-// Per batch of <= 32 frames: k_touch (one thread per stride-4 pixel per frame, 4 ray samples,
+// Per batch of <= 64 frames: k_touch (one thread per stride-4 pixel per frame, 4 ray samples,
 // hash insert, per-slot frame bitmask) -> host reads the batch counters (pool growth, empty-frame
 // error) -> k_integrate (one workgroup per touched block, every voxel applies that block's frames
 // in frame order = bit-identical to sequential per-frame integration).
@@ -52,10 +52,10 @@ static int64_t next_pow2(int64_t x) {
 static int alloc_table(Table& t, int64_t cap, hipStream_t s) {
     MQR_CHECK_HIP(hipMalloc(&t.keys, sizeof(uint64_t) * cap));
     MQR_CHECK_HIP(hipMalloc(&t.vals, sizeof(int32_t) * cap));
-    MQR_CHECK_HIP(hipMalloc(&t.mask, sizeof(uint32_t) * cap));
+    MQR_CHECK_HIP(hipMalloc(&t.mask, sizeof(bmask_t) * cap));
     MQR_CHECK_HIP(hipMemsetAsync(t.keys, 0xff, sizeof(uint64_t) * cap, s));
     MQR_CHECK_HIP(hipMemsetAsync(t.vals, 0xff, sizeof(int32_t) * cap, s));
-    MQR_CHECK_HIP(hipMemsetAsync(t.mask, 0, sizeof(uint32_t) * cap, s));
+    MQR_CHECK_HIP(hipMemsetAsync(t.mask, 0, sizeof(bmask_t) * cap, s));
     t.cap = cap;
     return 0;
 }
@@ -82,10 +82,10 @@ static int ensure_lists(mqr_vbg* v, int64_t cap) {
         if (v->lpt[p]) MQR_CHECK_HIP(hipFree(v->lpt[p]));
         v->lists[p] = v->lpt[p] = nullptr;
         MQR_CHECK_HIP(hipMalloc(&v->lists[p], sizeof(int32_t) * cap));
-        MQR_CHECK_HIP(hipMalloc(&v->lpt[p], 2 * sizeof(int32_t) * cap));  // slots, then their masks
+        MQR_CHECK_HIP(hipMalloc(&v->lpt[p], (sizeof(int32_t) + sizeof(bmask_t)) * cap));  // slots, then their masks
         if (v->bad[p]) MQR_CHECK_HIP(hipFree(v->bad[p]));
         v->bad[p] = nullptr;
-        MQR_CHECK_HIP(hipMalloc(&v->bad[p], 2 * sizeof(int32_t) * cap));
+        MQR_CHECK_HIP(hipMalloc(&v->bad[p], (sizeof(int32_t) + sizeof(bmask_t)) * cap));  // slots, then masks
     }
     v->list_cap = cap;
     return 0;
@@ -99,9 +99,9 @@ static int ensure_table(mqr_vbg* v, int64_t live) {
     if (sync_all(v)) return 1;
     Table nt{};
     if (alloc_table(nt, want, v->stream)) return 1;
-    uint32_t* nm1 = nullptr;
-    MQR_CHECK_HIP(hipMalloc(&nm1, sizeof(uint32_t) * want));
-    MQR_CHECK_HIP(hipMemsetAsync(nm1, 0, sizeof(uint32_t) * want, v->stream));
+    bmask_t* nm1 = nullptr;
+    MQR_CHECK_HIP(hipMalloc(&nm1, sizeof(bmask_t) * want));
+    MQR_CHECK_HIP(hipMemsetAsync(nm1, 0, sizeof(bmask_t) * want, v->stream));
     if (v->tab.cap) {
         const int64_t blocks = (v->tab.cap + 255) / 256;
         hipLaunchKernelGGL(k_rehash, dim3((unsigned)blocks), dim3(256), 0, v->stream, v->tab, nt);
@@ -257,9 +257,9 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
     const Table t = v->table(p);
     int* counters = v->ctr(p);
     const int32_t* list = v->lists[p];
-    const uint32_t* lmask = nullptr;
+    const bmask_t* lmask = nullptr;
     if (v->lpt_order && n > 1) {  // on the touch stream: overlaps the previous integrate
-        uint32_t* om = reinterpret_cast<uint32_t*>(v->lpt[p] + v->list_cap);
+        bmask_t* om = reinterpret_cast<bmask_t*>(v->lpt[p] + v->list_cap);
         hipLaunchKernelGGL(k_lpt_order, dim3(1), dim3(1024), 0, v->stream, list, counters, v->list_cap, t.mask,
                            v->lpt[p], om);
         MQR_CHECK_HIP(hipGetLastError());
@@ -295,7 +295,7 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
                        v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp,        \
                        depth_frame, depth_scale, depth_max, sdf_trunc);                                            \
     hipLaunchKernelGGL((k_integrate_t<RR, 4, 0, false, 512>), dim3(64), dim3(512), 0, s, v->bad[p],                \
-                       reinterpret_cast<const uint32_t*>(v->bad[p] + v->list_cap), (int32_t*)nullptr,             \
+                       reinterpret_cast<const bmask_t*>(v->bad[p] + v->list_cap), (int32_t*)nullptr,             \
                        counters + (kBadCount - kListCount), v->list_cap, t, v->pool, v->voxel_size, depths, HW,   \
                        H, W, fp, depth_frame, depth_scale, depth_max, sdf_trunc)
 #define MQR_LAUNCH_PK(RR, GG, NT)                                                                              \
@@ -311,7 +311,7 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
                        v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp, depth_frame, depth_max,      \
                        sdf_trunc);                                                                                \
     hipLaunchKernelGGL((k_integrate_t<RR, 4, 0, false, 512>), dim3(8), dim3(512), 0, s, v->bad[p],                 \
-                       reinterpret_cast<const uint32_t*>(v->bad[p] + v->list_cap), (int32_t*)nullptr,             \
+                       reinterpret_cast<const bmask_t*>(v->bad[p] + v->list_cap), (int32_t*)nullptr,             \
                        counters + (kBadCount - kListCount), v->list_cap, t, v->pool, v->voxel_size, depths, HW,   \
                        H, W, fp, depth_frame, depth_scale, depth_max, sdf_trunc)
 #define MQR_LAUNCH_TILE(RR, NT, FG, FNT)                                                                        \
@@ -319,7 +319,7 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
                        v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp, depth_frame, depth_max,      \
                        sdf_trunc);                                                                                \
     hipLaunchKernelGGL((k_integrate_t<RR, FG, 0, false, FNT>), dim3(8), dim3(FNT), 0, s, v->bad[p],                \
-                       reinterpret_cast<const uint32_t*>(v->bad[p] + v->list_cap), (int32_t*)nullptr,             \
+                       reinterpret_cast<const bmask_t*>(v->bad[p] + v->list_cap), (int32_t*)nullptr,             \
                        counters + (kBadCount - kListCount), v->list_cap, t, v->pool, v->voxel_size, depths, HW,   \
                        H, W, fp, depth_frame, depth_scale, depth_max, sdf_trunc)
 #define MQR_LAUNCH_LEANC(RR, NT, PIPE, RZ, WPE, CUBE, FG, FNT)                                                    \
@@ -327,7 +327,7 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
                        v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp,          \
                        depth_frame, depth_max, sdf_trunc);                                                        \
     hipLaunchKernelGGL((k_integrate_t<RR, FG, 0, false, FNT>), dim3(8), dim3(FNT), 0, s, v->bad[p],               \
-                       reinterpret_cast<const uint32_t*>(v->bad[p] + v->list_cap), (int32_t*)nullptr,             \
+                       reinterpret_cast<const bmask_t*>(v->bad[p] + v->list_cap), (int32_t*)nullptr,             \
                        counters + (kBadCount - kListCount), v->list_cap, t, v->pool, v->voxel_size, depths, HW,   \
                        H, W, fp, depth_frame, depth_scale, depth_max, sdf_trunc)
     // Variants (mqr_vbg_set_variant; all bit-identical, tests/test_gpu_numerics.py): 1 generic k_integrate;
@@ -614,8 +614,8 @@ int mqr_vbg_reset(mqr_vbg* v) {
     if (sync_all(v)) return 1;
     MQR_CHECK_HIP(hipMemsetAsync(v->tab.keys, 0xff, sizeof(uint64_t) * v->tab.cap, v->stream));
     MQR_CHECK_HIP(hipMemsetAsync(v->tab.vals, 0xff, sizeof(int32_t) * v->tab.cap, v->stream));
-    MQR_CHECK_HIP(hipMemsetAsync(v->tab.mask, 0, sizeof(uint32_t) * v->tab.cap, v->stream));
-    MQR_CHECK_HIP(hipMemsetAsync(v->mask1, 0, sizeof(uint32_t) * v->tab.cap, v->stream));
+    MQR_CHECK_HIP(hipMemsetAsync(v->tab.mask, 0, sizeof(bmask_t) * v->tab.cap, v->stream));
+    MQR_CHECK_HIP(hipMemsetAsync(v->mask1, 0, sizeof(bmask_t) * v->tab.cap, v->stream));
     if (v->pool_count > 0)
         MQR_CHECK_HIP(hipMemsetAsync(v->pool, 0, sizeof(float2) * v->pool_count * v->R3, v->stream));
     MQR_CHECK_HIP(hipMemsetAsync(v->counters, 0, sizeof(int) * (2 * kCountersTotal + 8), v->stream));
@@ -659,9 +659,10 @@ int mqr_integrate_frames(mqr_vbg* v, const float* depths, int depth_loc, int B, 
         if (!frame_ok || frame_ok[i]) valid.push_back(i);
     int rc = 0;
     int batch = 0;
-    for (size_t s = 0; s < valid.size(); s += kMaxBatch, ++batch) {
+    const size_t nb = (size_t)std::max(1, std::min(v->batch_frames, kMaxBatch));
+    for (size_t s = 0; s < valid.size(); s += nb, ++batch) {
         const int p = v->pipelined ? (batch & 1) : 0;
-        const int b = (int)std::min<size_t>(kMaxBatch, valid.size() - s);
+        const int b = (int)std::min<size_t>(nb, valid.size() - s);
         const int* idx = valid.data() + s;
         // table headroom for every key this batch could add (a rehash waits for in-flight work)
         if (ensure_table(v, v->pool_count + b * max_touch) || ensure_fp(v, b)) return 1;
@@ -890,6 +891,7 @@ int mqr_vbg_set_variant(mqr_vbg* v, int variant) {
     v->kernel_variant = variant & 0xff;
     v->pipelined = (variant & 0x100) == 0;  // bit 8: serialise touch and integrate (A/B of the overlap)
     v->lpt_order = (variant & 0x200) == 0;  // bit 9: integrate in touch order instead of longest-first
+    v->batch_frames = (variant & 0x400) ? 32 : kMaxBatch;  // bit 10: 32-frame batches (A/B)
     return 0;
 }
 

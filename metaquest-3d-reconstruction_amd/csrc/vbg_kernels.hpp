@@ -6,6 +6,12 @@
 namespace mqr {
 
 // ------------------------------------------------------------------ device helpers
+__device__ __forceinline__ bmask_t readfirstlane_u64(bmask_t v) {
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return (bmask_t)hi << 32 | lo;
+}
+
 __device__ inline int64_t table_find(const Table t, uint64_t k) {
     const uint64_t m = (uint64_t)t.cap - 1;
     uint64_t h = mix64(k) & m;
@@ -53,11 +59,11 @@ __device__ inline int64_t table_insert(Table t, uint64_t k, bool alloc, int* cou
 // Sets frame bit f of the slot (appending the slot to the batch list at its first bit); returns
 // whether the bit was new -- the caller counts those per wave (kFrameBlocks).
 __device__ inline bool mark_slot(Table t, int64_t slot, int f, int* counters, int32_t* list, int64_t list_cap) {
-    const uint32_t bit = 1u << f;
+    const bmask_t bit = (bmask_t)1 << f;
     // every workgroup of a frame that sees the block marks it: read the word at L2 first and only
     // the workgroups that still find the bit clear issue the (same-address, serialised) atomic
     if (__hip_atomic_load(&t.mask[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & bit) return false;
-    const uint32_t old = atomicOr(&t.mask[slot], bit);
+    const bmask_t old = atomicOr((unsigned long long*)&t.mask[slot], (unsigned long long)bit);
     if (old == 0) {
         const int pos = atomicAdd(&counters[kListCount], 1);
         if (pos < list_cap)
@@ -183,7 +189,7 @@ __global__ __launch_bounds__(256) void k_integrate(const int32_t* __restrict__ l
     for (int64_t i = blockIdx.x; i < n; i += gridDim.x) {
         const int32_t slot = list[i];
         const int buf = t.vals[slot];
-        const uint32_t mask = t.mask[slot];
+        const bmask_t mask = t.mask[slot];
         int xb, yb, zb;
         unpack_key(t.keys[slot], xb, yb, zb);
         if (buf >= 0) {
@@ -195,9 +201,9 @@ __global__ __launch_bounds__(256) void k_integrate(const int32_t* __restrict__ l
                 const float zs = (float)(zb * R + zv) * voxel_size;
                 float2 tw = vox[p];
                 bool dirty = false;
-                uint32_t m = mask;
+                bmask_t m = mask;
                 while (m) {
-                    const int f = __builtin_ctz(m);
+                    const int f = __builtin_ctzll(m);
                     m &= m - 1;
                     const FrameParams& fp = fps[f];
                     const float xc = xs * fp.ext[0] + ys * fp.ext[1] + zs * fp.ext[2] + fp.ext[3];
@@ -287,16 +293,16 @@ __device__ __forceinline__ bool num_unsafe(float v) {
 // path ran, so the exact pass reproduces k_integrate bit for bit, and the fast pass has no
 // per-voxel branches around its divisions.
 template <int ZPER, int G, bool EXACT>
-__device__ __forceinline__ bool integrate_column(float2 (&tw)[ZPER], uint32_t& dirty, uint32_t mask,
+__device__ __forceinline__ bool integrate_column(float2 (&tw)[ZPER], uint32_t& dirty, bmask_t mask,
                                                  const float (&zs)[ZPER], float xs, float ys,
                                                  const float* __restrict__ depths, int64_t HW, int W, float hm1,
                                                  float wm1, const FrameParams* __restrict__ fps,
                                                  const int64_t* __restrict__ depth_frame, float depth_scale,
                                                  bool unit_scale, float depth_max, float sdf_trunc) {
     bool bad = false;
-    uint32_t m = mask;
+    bmask_t m = mask;
     while (m) {
-        const int f = __builtin_ctz(m);
+        const int f = __builtin_ctzll(m);
         m &= m - 1;
         const FrameParams& fp = fps[f];
         const float* __restrict__ dep = depths + depth_frame[f] * HW;
@@ -386,7 +392,7 @@ __device__ __forceinline__ bool integrate_column(float2 (&tw)[ZPER], uint32_t& d
 // exact copy of the column loop (fewer registers, no per-voxel branches).
 template <int R, int G, int SWZ = 0, bool FAST = false, int NT = 256, int WPE = 1, int SPLIT = 1, bool EXTFIX = false>
 __global__ __launch_bounds__(NT, WPE) void k_integrate_t(const int32_t* __restrict__ list,
-                                                     const uint32_t* __restrict__ lmask,
+                                                     const bmask_t* __restrict__ lmask,
                                                      int32_t* __restrict__ bad_out,
                                                      int* __restrict__ counters,
                                                      int64_t list_cap, Table t, float2* __restrict__ pool,
@@ -413,7 +419,7 @@ __global__ __launch_bounds__(NT, WPE) void k_integrate_t(const int32_t* __restri
         const int64_t i = SWZ > 0 ? xcd_swizzle<(SWZ > 0 ? SWZ : 1)>(L, n) : L;
         const int32_t slot = list[i];
         const int buf = t.vals[slot];
-        const uint32_t mask = __builtin_amdgcn_readfirstlane(lmask ? lmask[i] : t.mask[slot]);
+        const bmask_t mask = readfirstlane_u64(lmask ? lmask[i] : t.mask[slot]);
         int xb, yb, zb;
         unpack_key(t.keys[slot], xb, yb, zb);
         if (buf >= 0) {
@@ -436,7 +442,7 @@ __global__ __launch_bounds__(NT, WPE) void k_integrate_t(const int32_t* __restri
                     if (tid == 0) {
                         const int j = atomicAdd(&counters[kBadCount], 1);
                         bad_out[j] = slot;
-                        bad_out[list_cap + j] = (int32_t)mask;
+                        reinterpret_cast<bmask_t*>(bad_out + list_cap)[j] = mask;
                     }
                     dirty = 0;
                 } else {  // redo this block exactly
@@ -461,13 +467,13 @@ __global__ __launch_bounds__(NT, WPE) void k_integrate_t(const int32_t* __restri
 // short blocks instead of whichever long blocks the touch order happened to put last.  One
 // workgroup; order within a bin is arbitrary (blocks are independent, results unchanged).
 __global__ __launch_bounds__(1024) void k_lpt_order(const int32_t* __restrict__ list, const int* __restrict__ counters,
-                                                    int64_t list_cap, const uint32_t* __restrict__ mask,
-                                                    int32_t* __restrict__ out, uint32_t* __restrict__ out_mask) {
+                                                    int64_t list_cap, const bmask_t* __restrict__ mask,
+                                                    int32_t* __restrict__ out, bmask_t* __restrict__ out_mask) {
     __shared__ int hist[kMaxBatch + 1];
     const int n = (int)min((int64_t)counters[kListCount], list_cap);
     if (threadIdx.x <= kMaxBatch) hist[threadIdx.x] = 0;
     __syncthreads();
-    for (int i = threadIdx.x; i < n; i += blockDim.x) atomicAdd(&hist[__popc(mask[list[i]])], 1);
+    for (int i = threadIdx.x; i < n; i += blockDim.x) atomicAdd(&hist[__popcll(mask[list[i]])], 1);
     __syncthreads();
     if (threadIdx.x == 0) {
         int acc = 0;
@@ -480,8 +486,8 @@ __global__ __launch_bounds__(1024) void k_lpt_order(const int32_t* __restrict__ 
     __syncthreads();
     for (int i = threadIdx.x; i < n; i += blockDim.x) {
         const int32_t s = list[i];
-        const uint32_t m = mask[s];
-        const int pos = atomicAdd(&hist[__popc(m)], 1);
+        const bmask_t m = mask[s];
+        const int pos = atomicAdd(&hist[__popcll(m)], 1);
         out[pos] = s;
         out_mask[pos] = m;
     }
@@ -518,7 +524,7 @@ __device__ __forceinline__ f2v div_const2(f2v a, f2v nbt, f2v y1t) {
 // 2^-60 or at least zc / 2), so the result is bit-identical to integrate_column<.., true>.
 template <int ZPER, int G>
 __device__ __forceinline__ bool integrate_column_pk(f2v (&T)[ZPER / 2], f2v (&Wt)[ZPER / 2],
-                                                    uint32_t& dirty, uint32_t mask,
+                                                    uint32_t& dirty, bmask_t mask,
                                                     const f2v (&zs2)[ZPER / 2], float xs, float ys,
                                                     const float* __restrict__ depths, int64_t HW, int W,
                                                     float hm1, float wm1, const FrameParams* __restrict__ fps,
@@ -528,9 +534,9 @@ __device__ __forceinline__ bool integrate_column_pk(f2v (&T)[ZPER / 2], f2v (&Wt
     const float y1t_s = __builtin_fmaf(__builtin_fmaf(-sdf_trunc, y0t, 1.0f), y0t, y0t);
     const f2v y1t = splat2(y1t_s), nbt = splat2(-sdf_trunc), one = splat2(1.0f);
     float zmin = 0x1p100f, zmax = 0.0f;
-    uint32_t m = mask;
+    bmask_t m = mask;
     while (m) {
-        const int f = __builtin_ctz(m);
+        const int f = __builtin_ctzll(m);
         m &= m - 1;
         const FrameParams& fp = fps[f];
         const float* __restrict__ dep = depths + depth_frame[f] * HW;
@@ -619,7 +625,7 @@ __global__ __launch_bounds__(NT) void k_integrate_pk(const int32_t* __restrict__
     for (int64_t i = blockIdx.x; i < n; i += gridDim.x) {
         const int32_t slot = list[i];
         const int buf = t.vals[slot];
-        const uint32_t mask = __builtin_amdgcn_readfirstlane(t.mask[slot]);
+        const bmask_t mask = readfirstlane_u64(t.mask[slot]);
         int xb, yb, zb;
         unpack_key(t.keys[slot], xb, yb, zb);
         if (buf >= 0) {
@@ -809,7 +815,7 @@ __device__ __forceinline__ void lean_voxel(int tid, int k, int& x, int& y, int& 
 // workgroup as in k_integrate_t; every voxel of a block that is not handed off is written back.
 template <int R, int NT, bool PIPE, int RZ, int WPE = 1, bool CUBE = false>
 __global__ __launch_bounds__(NT, WPE) void k_integrate_lean(const int32_t* __restrict__ list,
-                                                        const uint32_t* __restrict__ lmask,
+                                                        const bmask_t* __restrict__ lmask,
                                                         int32_t* __restrict__ bad_out, int* __restrict__ counters,
                                                         int64_t list_cap, Table t, float2* __restrict__ pool,
                                                         float voxel_size, const float* __restrict__ depths,
@@ -830,7 +836,7 @@ __global__ __launch_bounds__(NT, WPE) void k_integrate_lean(const int32_t* __res
     for (int64_t i = blockIdx.x; i < n; i += gridDim.x) {
         const int32_t slot = list[i];
         const int buf = t.vals[slot];
-        const uint32_t mask = __builtin_amdgcn_readfirstlane(lmask ? lmask[i] : t.mask[slot]);
+        const bmask_t mask = readfirstlane_u64(lmask ? lmask[i] : t.mask[slot]);
         int xb, yb, zb;
         unpack_key(t.keys[slot], xb, yb, zb);
         if (buf >= 0 && mask) {
@@ -855,8 +861,8 @@ __global__ __launch_bounds__(NT, WPE) void k_integrate_lean(const int32_t* __res
                 const float w = tw[k].y;  // rcp_m(w + 1) needs integer weights (this batch adds <= 32)
                 bad |= !(w >= 0.0f && w <= 0x1p23f && w == __builtin_truncf(w));
             }
-            uint32_t m = mask;
-            int f = __builtin_ctz(m);
+            bmask_t m = mask;
+            int f = __builtin_ctzll(m);
             m &= m - 1;
             float da[ZPER], db[ZPER];
             lean_gather<ZPER, RZ>(da, bad, fps[f], frame_rsrc(depths + depth_frame[f] * HW, bytes), xs, ys, zs, W4,
@@ -864,7 +870,7 @@ __global__ __launch_bounds__(NT, WPE) void k_integrate_lean(const int32_t* __res
             // PIPE: the next frame's projections and gathers are issued before this frame's updates
             while (true) {
                 const bool more = m != 0;  // wave-uniform
-                const int g = more ? __builtin_ctz(m) : 0;
+                const int g = more ? __builtin_ctzll(m) : 0;
                 m &= m - 1;
                 if (PIPE && more)
                     lean_gather<ZPER, RZ>(db, bad, fps[g], frame_rsrc(depths + depth_frame[g] * HW, bytes), xs, ys,
@@ -884,7 +890,7 @@ __global__ __launch_bounds__(NT, WPE) void k_integrate_lean(const int32_t* __res
                 if (tid == 0) {
                     const int j = atomicAdd(&counters[kBadCount], 1);
                     bad_out[j] = slot;
-                    bad_out[list_cap + j] = (int32_t)mask;
+                    reinterpret_cast<bmask_t*>(bad_out + list_cap)[j] = mask;
                 }
             } else {
 #pragma unroll
@@ -985,7 +991,7 @@ __device__ __forceinline__ void lean_gather_tile(float (&dv)[ZPER], bool& bad, c
 // (one wave per row, lanes along the row), then every thread gathers and updates its voxels.
 template <int R, int NT>
 __global__ __launch_bounds__(NT) void k_integrate_tile(const int32_t* __restrict__ list,
-                                                      const uint32_t* __restrict__ lmask,
+                                                      const bmask_t* __restrict__ lmask,
                                                       int32_t* __restrict__ bad_out, int* __restrict__ counters,
                                                       int64_t list_cap, Table t, float2* __restrict__ pool,
                                                       float voxel_size, const float* __restrict__ depths, int64_t HW,
@@ -1007,7 +1013,7 @@ __global__ __launch_bounds__(NT) void k_integrate_tile(const int32_t* __restrict
     for (int64_t i = blockIdx.x; i < n; i += gridDim.x) {
         const int32_t slot = list[i];
         const int buf = t.vals[slot];
-        const uint32_t mask = __builtin_amdgcn_readfirstlane(lmask ? lmask[i] : t.mask[slot]);
+        const bmask_t mask = readfirstlane_u64(lmask ? lmask[i] : t.mask[slot]);
         int xb, yb, zb;
         unpack_key(t.keys[slot], xb, yb, zb);
         if (buf >= 0 && mask) {
@@ -1027,9 +1033,9 @@ __global__ __launch_bounds__(NT) void k_integrate_tile(const int32_t* __restrict
                 const float w = tw[k].y;
                 bad |= !(w >= 0.0f && w <= 0x1p23f && w == __builtin_truncf(w));
             }
-            uint32_t m = mask;
+            bmask_t m = mask;
             while (m) {
-                const int f = __builtin_ctz(m);
+                const int f = __builtin_ctzll(m);
                 m &= m - 1;
                 const FrameParams& fp = fps[f];
                 const float* __restrict__ dep = depths + depth_frame[f] * HW;
@@ -1055,7 +1061,7 @@ __global__ __launch_bounds__(NT) void k_integrate_tile(const int32_t* __restrict
                 if (tid == 0) {
                     const int j = atomicAdd(&counters[kBadCount], 1);
                     bad_out[j] = slot;
-                    bad_out[list_cap + j] = (int32_t)mask;
+                    reinterpret_cast<bmask_t*>(bad_out + list_cap)[j] = mask;
                 }
             } else {
 #pragma unroll
@@ -1089,13 +1095,13 @@ typedef __attribute__((address_space(3))) void lvoid_t;
 // inside the block project into the hull of the corners when all corners are in front of the
 // camera; rounding moves a projection far less than the pad, and a voxel found outside the
 // rectangle sends the block to the exact fix-up launch).  {u0, v0, w, h}; w = -1: gather directly.
-__device__ __forceinline__ void block_rects(const FrameParams* __restrict__ fps, uint32_t mask, int xb, int yb, int zb,
+__device__ __forceinline__ void block_rects(const FrameParams* __restrict__ fps, bmask_t mask, int xb, int yb, int zb,
                                             int R, float voxel_size, int H, int W, int4* s_rect) {
     const int slot = threadIdx.x >> 3, c = threadIdx.x & 7;
-    uint32_t m = mask;
+    bmask_t m = mask;
     for (int q = 0; q < slot && m; ++q) m &= m - 1;
     const bool have = m != 0;
-    const FrameParams& fp = fps[have ? __builtin_ctz(m) : 0];
+    const FrameParams& fp = fps[have ? __builtin_ctzll(m) : 0];
     const float xs = (float)(xb * R + (c & 1) * (R - 1)) * voxel_size;
     const float ys = (float)(yb * R + ((c >> 1) & 1) * (R - 1)) * voxel_size;
     const float zs = (float)(zb * R + ((c >> 2) & 1) * (R - 1)) * voxel_size;
@@ -1175,7 +1181,7 @@ __device__ __forceinline__ void tile_gather(float (&dv)[ZPER], bool& bad, const 
 
 template <int R, int NT>
 __global__ __launch_bounds__(NT) void k_integrate_dbt(const int32_t* __restrict__ list,
-                                                     const uint32_t* __restrict__ lmask,
+                                                     const bmask_t* __restrict__ lmask,
                                                      int32_t* __restrict__ bad_out, int* __restrict__ counters,
                                                      int64_t list_cap, Table t, float2* __restrict__ pool,
                                                      float voxel_size, const float* __restrict__ depths, int64_t HW,
@@ -1198,7 +1204,7 @@ __global__ __launch_bounds__(NT) void k_integrate_dbt(const int32_t* __restrict_
     for (int64_t i = blockIdx.x; i < n; i += gridDim.x) {
         const int32_t slot = list[i];
         const int buf = t.vals[slot];
-        const uint32_t mask = __builtin_amdgcn_readfirstlane(lmask ? lmask[i] : t.mask[slot]);
+        const bmask_t mask = readfirstlane_u64(lmask ? lmask[i] : t.mask[slot]);
         int xb, yb, zb;
         unpack_key(t.keys[slot], xb, yb, zb);
         if (buf >= 0 && mask) {
@@ -1220,8 +1226,8 @@ __global__ __launch_bounds__(NT) void k_integrate_dbt(const int32_t* __restrict_
             }
             block_rects(fps, mask, xb, yb, zb, R, voxel_size, H, W, s_rect);
             __syncthreads();
-            uint32_t m = mask;
-            int f = __builtin_ctz(m);
+            bmask_t m = mask;
+            int f = __builtin_ctzll(m);
             m &= m - 1;
             int j = 0;
             int4 r = s_rect[0];
@@ -1231,7 +1237,7 @@ __global__ __launch_bounds__(NT) void k_integrate_dbt(const int32_t* __restrict_
             __syncthreads();  // waits for the copy (vmcnt) as well
             while (true) {
                 const bool more = m != 0;  // wave-uniform
-                const int g = more ? __builtin_ctz(m) : 0;
+                const int g = more ? __builtin_ctzll(m) : 0;
                 m &= m - 1;
                 int4 rn = make_int4(0, 0, 0, 0);
                 if (more) {
@@ -1257,7 +1263,7 @@ __global__ __launch_bounds__(NT) void k_integrate_dbt(const int32_t* __restrict_
                 if (tid == 0) {
                     const int jj = atomicAdd(&counters[kBadCount], 1);
                     bad_out[jj] = slot;
-                    bad_out[list_cap + jj] = (int32_t)mask;
+                    reinterpret_cast<bmask_t*>(bad_out + list_cap)[jj] = mask;
                 }
             } else {
 #pragma unroll

@@ -25,7 +25,7 @@ from .meshfilter import filter_mesh_components  # noqa: F401  (re-exported: o3d_
 from .raycasting import raycast_in_color_view  # noqa: F401  (re-exported: o3d_utils.py:324-341)
 from .vbg import VoxelBlockGrid
 
-CHUNK = 64  # frames per host->device hand-off (device batches are <= 32 frames)
+CHUNK = 64  # frames per host->device hand-off (device batches are <= 64 frames)
 
 
 def compute_o3d_intrinsic_matrices(dataset) -> np.ndarray:
