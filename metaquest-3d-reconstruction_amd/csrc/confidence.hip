@@ -41,8 +41,11 @@ __device__ inline int pixel_error(const float* __restrict__ tgt, int H, int W, c
     if (!(uu >= -max_coord && uu < max_coord && vv >= -max_coord && vv < max_coord)) return 0;
     const int u0 = (int)floor(uu), v0 = (int)floor(vv), u1 = u0 + 1, v1 = v0 + 1;
     if (!(u0 >= 0 && u1 < W && v0 >= 0 && v1 < H)) return 0;
-    const float Ia = tgt[(int64_t)v0 * W + u0], Ib = tgt[(int64_t)v0 * W + u1];
-    const float Ic = tgt[(int64_t)v1 * W + u0], Id = tgt[(int64_t)v1 * W + u1];
+    // the two taps of a row in one 8-byte load (4-byte aligned; the L1 path costs per lane, not per byte)
+    float2 ab, cd;
+    __builtin_memcpy(&ab, tgt + (int64_t)v0 * W + u0, sizeof(float2));
+    __builtin_memcpy(&cd, tgt + (int64_t)v1 * W + u0, sizeof(float2));
+    const float Ia = ab.x, Ib = ab.y, Ic = cd.x, Id = cd.y;
     if (!(Ib > 0 && Ib <= dmf && Ia > 0 && Ia <= dmf && Ic > 0 && Ic <= dmf && Id > 0 && Id <= dmf)) return 0;
     const double wa = ((double)u1 - uu) * ((double)v1 - vv);
     const double wb = (uu - (double)u0) * ((double)v1 - vv);
