@@ -137,10 +137,14 @@ typedef struct mqr_stats {
 } mqr_stats;
 int mqr_vbg_profile(mqr_vbg* v, int enable);
 
-/* Test / tuning hooks.  mqr_vbg_set_variant: 0 = R-specialised integrate kernel (default),
- * 1 = generic kernel (A/B).  mqr_check_division: exhaustive bit-pattern check of the division
- * shortcut used on device (which=0: 1/b over float bit patterns [lo_bits, lo_bits+count);
- * which=1: a/b for those patterns as a); returns the mismatch count and the first bad pattern. */
+/* Test / tuning hooks.  mqr_vbg_set_variant: low byte = integrate kernel (0 default = lean kernel
+ * where its preconditions hold, 1 generic, 2-59 specialised / A/B configurations, all bit-identical,
+ * see launch_integrate in csrc/vbg.hip); bit 8 serialises touch and integrate, bit 9 keeps touch
+ * order instead of longest-first, bit 10 uses 32-frame batches instead of 64.
+ * mqr_check_division: exhaustive bit-pattern check of the division shortcuts used on device against
+ * IEEE division (which=0: 1/b via rcp_rn, 1: a/b via div_rn, 2: a/b via the bare core, 3: 1/b via
+ * rcp_nm, 4: 1/b via rcp_m, over float bit patterns [lo_bits, lo_bits+count) as b or a); returns
+ * the mismatch count and the first bad pattern. */
 int mqr_vbg_set_variant(mqr_vbg* v, int variant);
 int mqr_check_division(int device, int which, float b, uint32_t lo_bits, uint64_t count, uint32_t* mismatches,
                        uint32_t* first_bad);

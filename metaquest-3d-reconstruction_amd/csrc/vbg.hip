@@ -306,8 +306,9 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
     const bool lean_ok = pk_ok && 4 * (HW + W) <= (int64_t{1} << 31);
 // lean kernel + exact fix-up launch (FG / FNT: the fix-up kernel's group size and threads)
 #define MQR_LAUNCH_LEAN(RR, NT, PIPE, RZ, WPE, FG, FNT) MQR_LAUNCH_LEANC(RR, NT, PIPE, RZ, WPE, false, FG, FNT)
-#define MQR_LAUNCH_DBT(RR, NT)                                                                                  \
-    hipLaunchKernelGGL((k_integrate_dbt<RR, NT>), dim3(grid), dim3(NT), 0, s, list, lmask, v->bad[p], counters,  \
+#define MQR_LAUNCH_DBT(RR, NT) MQR_LAUNCH_DBTW(RR, NT, 1)
+#define MQR_LAUNCH_DBTW(RR, NT, WPE)                                                                            \
+    hipLaunchKernelGGL((k_integrate_dbt<RR, NT, WPE>), dim3(grid), dim3(NT), 0, s, list, lmask, v->bad[p], counters,  \
                        v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp, depth_frame, depth_max,      \
                        sdf_trunc);                                                                                \
     hipLaunchKernelGGL((k_integrate_t<RR, 4, 0, false, 512>), dim3(8), dim3(512), 0, s, v->bad[p],                 \
@@ -339,7 +340,7 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
         var = 0;
     if ((var == 8 || var == 9 || (var >= 13 && var <= 16) || var == 20) && !pk_ok) var = 0;
     if (var >= 30 && var <= 33 && !lmask) var = 0;  // split blocks need the longest-first mask copy
-    if (((var >= 40 && var <= 53) || (var >= 56 && var <= 58)) && !lean_ok) var = 0;
+    if (((var >= 40 && var <= 53) || (var >= 56 && var <= 59)) && !lean_ok) var = 0;
     if (v->R == 16 && var != 1) {
         switch (var) {
             case 40: MQR_LAUNCH_LEAN(16, 512, true, 1, 1, 4, 512); break;
@@ -392,6 +393,7 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
             case 54: MQR_LAUNCH_INT(16, 4, false, false, 512); break;
             case 56: MQR_LAUNCH_TILE(16, 512, 4, 512); break;
             case 58: MQR_LAUNCH_DBT(16, 512); break;
+            case 59: MQR_LAUNCH_DBTW(16, 512, 8); break;
             case 57: MQR_LAUNCH_TILE(16, 256, 4, 512); break;
             // default: the lean kernel (512 threads x 8 voxels, column mapping, 3-op reciprocals;
             // fastest on MI355X, tools/ab_integrate.py); the exact branchy kernel where the lean one's
@@ -427,6 +429,7 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
 #undef MQR_LAUNCH_LEANC
 #undef MQR_LAUNCH_TILE
 #undef MQR_LAUNCH_DBT
+#undef MQR_LAUNCH_DBTW
     MQR_CHECK_HIP(hipGetLastError());
     if (v->profile) {
         MQR_CHECK_HIP(hipEventRecord(e1, s));

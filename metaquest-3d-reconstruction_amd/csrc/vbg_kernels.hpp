@@ -1179,8 +1179,8 @@ __device__ __forceinline__ void tile_gather(float (&dv)[ZPER], bool& bad, const 
     }
 }
 
-template <int R, int NT>
-__global__ __launch_bounds__(NT) void k_integrate_dbt(const int32_t* __restrict__ list,
+template <int R, int NT, int WPE = 1>
+__global__ __launch_bounds__(NT, WPE) void k_integrate_dbt(const int32_t* __restrict__ list,
                                                      const bmask_t* __restrict__ lmask,
                                                      int32_t* __restrict__ bad_out, int* __restrict__ counters,
                                                      int64_t list_cap, Table t, float2* __restrict__ pool,

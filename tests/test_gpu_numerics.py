@@ -46,7 +46,7 @@ def test_shortened_reciprocals_exact(which, lo, hi):
 
 INTEGRATE_VARIANTS = {16: (0, 2, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 22, 23, 24, 25, 0x100, 0x106,
                           0x108, 26, 27, 28, 29, 0x200, 0x300, 30, 31, 32, 33, 0x21e, 34, 35, 36, 37,
-                          40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 52, 53, 54, 56, 57, 58, 0x128, 0x228, 0x130, 0x400, 0x436, 0x500),
+                          40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 52, 53, 54, 56, 57, 58, 59, 0x128, 0x228, 0x130, 0x400, 0x436, 0x500),
                       8: (0, 6, 8, 0x101, 0x200, 40, 48)}
 
 
