@@ -690,7 +690,7 @@ __global__ __launch_bounds__(NT) void k_integrate_pk(const int32_t* __restrict__
 // rcp_m:  v_rcp + one Markstein correction (3 VALU).
 // Both are compared with IEEE 1.0f / b over every float of the ranges they are used on
 // (tests/test_gpu_numerics.py, mqr_check_division modes 3 / 4): 1 / zc for 2^-36 <= zc <= 2^60
-// (rcp_nm, or rcp_m when RZ == 2) and 1 / (w + 1) for integer weights w <= 2^23 + 32 (rcp_m).
+// (rcp_nm, or rcp_m when RZ == 2) and 1 / (w + 1) for integer weights w <= 2^23 + 64 (rcp_m).
 __device__ __forceinline__ float rcp_nm(float b) {
     const float y0 = __builtin_amdgcn_rcpf(b);
     const float y1 = __builtin_fmaf(__builtin_fmaf(-b, y0, 1.0f), y0, y0);
@@ -858,7 +858,7 @@ __global__ __launch_bounds__(NT, WPE) void k_integrate_lean(const int32_t* __res
                 xs[k] = CUBE ? (float)(xb * R + x) * voxel_size : xs0;
                 ys[k] = CUBE ? (float)(yb * R + y) * voxel_size : ys0;
                 zs[k] = (float)(zb * R + z) * voxel_size;
-                const float w = tw[k].y;  // rcp_m(w + 1) needs integer weights (this batch adds <= 32)
+                const float w = tw[k].y;  // rcp_m(w + 1) needs integer weights (a batch adds <= 64)
                 bad |= !(w >= 0.0f && w <= 0x1p23f && w == __builtin_truncf(w));
             }
             bmask_t m = mask;
