@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Benchmark of the TSDF fusion hot path (BASELINE.json config 1 at N=1).
+"""Benchmark of the TSDF fusion hot path (SURVEY.md §8(d) workload C2 at N=1).
 
 A "step" = integrate the rank's whole 500-frame depth sequence (640x480, procedural room = a
 512^3-voxel volume at 5 mm, R=16, depth_max 4 m, truncation 10 voxels) into an empty volume:
@@ -9,7 +9,8 @@ and the step ends with the single RCCL merge of the partial volumes into rank 0.
 
 Prints ONE JSON line (rank 0): value = frames integrated per second over all ranks, the mesh
 extraction time (weight_threshold 1.5, the pipeline's setting), the integrate kernel's roofline
-(algorithmic bytes per launch / its average HIP-event duration) and the CPU-oracle baseline.
+(algorithmic bytes per launch / its average HIP-event duration), the CPU-oracle baseline and the
+parity of the last timed step's volume and mesh against the oracle's.
 """
 from __future__ import annotations
 
@@ -35,8 +36,8 @@ class _DevPtr:
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--frames", type=int, default=500)
     ap.add_argument("--height", type=int, default=480)
     ap.add_argument("--width", type=int, default=640)
@@ -54,6 +55,9 @@ def parse():
     ap.add_argument("--conf-depth-max", type=float, default=4.0)
     ap.add_argument("--conf-error", type=float, default=0.08)
     ap.add_argument("--no-extras", action="store_true", help="skip confidence / copy-peak / host-input legs")
+    ap.add_argument("--no-parity", action="store_true", help="skip the oracle comparison of the timed volume")
+    ap.add_argument("--conf-cpu-seconds", type=float, default=10.0, help="bounded CPU sample of the confidence oracle")
+    ap.add_argument("--e2e-frames", type=int, default=500, help="frames of the on-disk C3 capture (0: skip the leg)")
     ap.add_argument("--merge", default="sparse", choices=["sparse", "reduce"],
                     help="N>1 volume merge: all-to-all to union-slice owners + gather, or one dense reduce")
     return ap.parse_args()
@@ -157,6 +161,113 @@ def ingest_leg(B, H, W, device):
             "note": "mqr_decode_depth, device raw/conf/count in, depth out, wall time of the call"}
 
 
+def c3_leg(seq, vbg, args, device, reps=3):
+    """C3 on the device, inputs resident in HBM: decode the raw NDC stack (mqr_decode_depth), the
+    confidence of every frame (mqr_confidence, r = conf_range), decode again with the confidence
+    mask (0.02 / 2, o3d_utils.py:141-142) and integrate the masked frames -- the pipeline's
+    estimate_depth_confidences -> integrate(use_confidence_filtered_depth=True) order."""
+    import numpy as np
+    import torch
+    from mqr import _lib
+    raw = seq["raw_t"].contiguous()
+    B, H, W = raw.shape
+    K = seq["K"].astype(np.float64)
+    T = seq["T_wc"].astype(np.float64)
+    T_cw = np.ascontiguousarray(seq["T_cw"], dtype=np.float32).reshape(B, 16)
+    T_ci = np.ascontiguousarray(np.linalg.inv(seq["T_cw"]), dtype=np.float32).reshape(B, 16)
+    K32 = np.ascontiguousarray(seq["K"], dtype=np.float32).reshape(B, 9)
+    depth = torch.empty_like(raw)
+    masked = torch.empty_like(raw)
+    conf = torch.empty((B, H, W), dtype=torch.float64, device=device)
+    valid = torch.empty((B, H, W), dtype=torch.int32, device=device)
+    nears = np.full(B, seq["near"], np.float64)
+    fars = np.full(B, seq["far"], np.float64)
+    strong = np.full(B, 3, np.uint8)  # DepthDataset.nears / fars are numpy float64 scalars
+    has = np.ones(B, np.uint8)
+    ok = np.zeros(B, np.uint8)
+    dev = int(device.index or 0)
+
+    class _P:
+        ptr = ctypes.c_void_p(masked.data_ptr())
+
+    def run():
+        _lib.call("mqr_decode_depth", dev, ctypes.c_void_p(raw.data_ptr()), 1, B, H, W, _lib.ptr(nears, _lib._f64p),
+                  _lib.ptr(fars, _lib._f64p), _lib.ptr(strong, _lib._u8p), None, None, None, 1, 0.0, 0,
+                  ctypes.c_void_p(depth.data_ptr()), 1, _lib.ptr(ok, _lib._u8p))
+        _lib.call("mqr_confidence", dev, ctypes.c_void_p(depth.data_ptr()), 1, B, H, W, _lib.ptr(K32, _lib._f32p),
+                  _lib.ptr(T_cw, _lib._f32p), _lib.ptr(T_ci, _lib._f32p), _lib.ptr(ok, _lib._u8p), 0, B,
+                  int(args.conf_range), float(args.conf_depth_max), float(args.conf_error),
+                  ctypes.c_void_p(conf.data_ptr()), ctypes.c_void_p(valid.data_ptr()), 1)
+        _lib.call("mqr_decode_depth", dev, ctypes.c_void_p(raw.data_ptr()), 1, B, H, W, _lib.ptr(nears, _lib._f64p),
+                  _lib.ptr(fars, _lib._f64p), _lib.ptr(strong, _lib._u8p), ctypes.c_void_p(conf.data_ptr()),
+                  ctypes.c_void_p(valid.data_ptr()), _lib.ptr(has, _lib._u8p), 1, 0.02, 2,
+                  ctypes.c_void_p(masked.data_ptr()), 1, _lib.ptr(ok, _lib._u8p))
+        vbg.reset()
+        vbg.integrate_frames((_P, B, H, W), K, T, frame_ok=ok, depth_scale=1.0, depth_max=args.depth_max,
+                             trunc_voxel_multiplier=args.trunc)
+
+    run()
+    times = []
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        run()
+        torch.cuda.synchronize()
+        times.append(time.perf_counter() - t0)
+    t = sorted(times)[len(times) // 2]
+    return {"frames": B, "ms": t * 1e3, "frames_per_s": B / t, "masked_fraction": float((masked == 0).float().mean()),
+            "blocks": vbg.size(), "window_r": args.conf_range,
+            "note": "device-resident raw NDC in: decode + confidence (all frames) + masked decode + integrate, "
+                    "wall time, median of 3"}
+
+
+def dropin_e2e_leg(seq, frames, device):
+    """The reference's own loop on disk: a C3 capture (raw NDC files + descriptor CSV) in a temp dir,
+    mqr.confidence.estimate_depth_confidences writing the per-frame npz, then
+    mqr.o3d_utils.integrate(use_confidence_filtered_depth=True) reading raw + npz back
+    (o3d_utils.py:153-238 -> device decode / mask / batched integrate).  Page cache warm."""
+    import shutil
+    import tempfile
+    import numpy as np
+    from mqr import synthetic
+    from mqr.confidence import DepthConfidenceEstimationConfig, estimate_depth_confidences
+    from mqr.dataio import DepthDataIO
+    from mqr.models import CoordinateSystem, Side
+    from mqr.o3d_utils import integrate
+    cap = {"raw": seq["raw_t"][:frames].cpu().numpy(), "unity": seq["unity"], "tangents": seq["tangents"],
+           "near": seq["near"], "far": seq["far"], "width": seq["width"], "height": seq["height"]}
+    tmp = tempfile.mkdtemp(prefix="mqr_e2e_")
+    try:
+        synthetic.write_capture(tmp, cap)
+        io = DepthDataIO(tmp)
+        ds = io.load_depth_dataset(Side.LEFT)
+        n = len(ds)
+        cfg = DepthConfidenceEstimationConfig(target_frame_range=10, depth_max=4.0, error_threshold=0.08,
+                                              skip_if_output_dir_exists=False, device=int(device.index or 0))
+        t0 = time.perf_counter()
+        estimate_depth_confidences(io, cfg, sides=[Side.LEFT])
+        t_conf = time.perf_counter() - t0
+        # reconstruct_scene.py:27-53: confidences first (UNITY poses converted inside), then the
+        # integrator gets the dataset with OPEN3D camera poses
+        ds.transforms = ds.transforms.convert_coordinate_system(target_coordinate_system=CoordinateSystem.OPEN3D,
+                                                                is_camera=True)
+        kw = dict(use_confidence_filtered_depth=True, confidence_threshold=0.02, valid_count_threshold=2,
+                  voxel_size=0.005, block_resolution=16, block_count=40000, depth_max=4.0,
+                  trunc_voxel_multiplier=10.0, device=int(device.index or 0))
+        integrate(ds, io, Side.LEFT, **kw)  # warm-up (allocations, page cache)
+        t0 = time.perf_counter()
+        vbg = integrate(ds, io, Side.LEFT, **kw)
+        t_int = time.perf_counter() - t0
+        blocks = vbg.size()
+        del vbg
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    return {"frames": n, "confidence_s": t_conf, "confidence_frames_per_s": n / t_conf, "integrate_s": t_int,
+            "integrate_frames_per_s": n / t_int, "frames_per_s": n / (t_conf + t_int), "blocks": blocks,
+            "note": "on-disk capture (raw + descriptor CSV), estimate_depth_confidences (writes npz) then "
+                    "o3d_utils.integrate with confidence masking; host file I/O + PCIe included"}
+
+
 def raycast_leg(vbg, K, T, H, W, thr, frames=64):
     """Row f1: colour-aligned depth by ray casting the extracted mesh (RaycastingScene.cast_rays
     stand-in): BVH build + `frames` pinhole casts at H x W from the sequence's poses."""
@@ -230,29 +341,52 @@ def pmc_traffic(H, W, frames):
     return None, None
 
 
+def host_cores():
+    """Threads this job can run at once: the affinity set, capped by a cgroup CPU quota if any."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    use = min(aff, quota) if quota else aff
+    return use, {"nproc": os.cpu_count(), "affinity": aff, "cgroup_quota_cpus": quota, "cpu_model": model}
+
+
 def cpu_baseline(seq_host, K, T, args):
+    """The oracle (oracle/mqr_oracle.c, OpenMP over blocks) over whole passes of the sequence, a
+    fresh volume each like a bench step, for ~cpu_seconds.  Returns (record, last full volume)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # the checker / CPU restatement (port) -- timed here as the baseline only
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        cores = os.cpu_count() or 1
-    cores = max(1, min(cores, 16))
+    cores, info = host_cores()
     oracle.set_threads(cores)
-    # whole passes over the sequence (a fresh volume each, as a bench step) until ~cpu_seconds
     t0 = time.perf_counter()
     n = passes = 0
-    while time.perf_counter() - t0 < args.cpu_seconds:
+    last = None
+    while time.perf_counter() - t0 < args.cpu_seconds or last is None:
         ref = oracle.OracleVBG(args.voxel, args.block_resolution, args.block_count)
         for i in range(len(seq_host)):
             ref.integrate_frame(seq_host[i], K[i], T[i], 1.0, args.depth_max, args.trunc)
         n += len(seq_host)
         passes += 1
-        del ref
+        last = ref
     dt = time.perf_counter() - t0
     out = {"value": n / dt, "unit": "frames/s", "cores": cores, "kind": "port",
            "sample": f"{passes} pass(es) over the {len(seq_host)}-frame sequence ({n} frames), touch+integrate per "
-                     f"frame (oracle/mqr_oracle.c, OpenMP over blocks), {dt:.1f} s"}
+                     f"frame (oracle/mqr_oracle.c, OpenMP over blocks, {cores} threads), {dt:.1f} s", **info}
     if args.cpu1_seconds > 0:
         oracle.set_threads(1)
         ref1 = oracle.OracleVBG(args.voxel, args.block_resolution, args.block_count)
@@ -264,7 +398,61 @@ def cpu_baseline(seq_host, K, T, args):
         dt1 = time.perf_counter() - t0
         out["one_thread"] = {"value": n1 / dt1, "frames": n1, "seconds": dt1}
         oracle.set_threads(cores)
+    return out, last
+
+
+def parity_check(vbg, ref, thr):
+    """The last timed step's GPU volume and mesh vs the oracle's volume of the same 500 frames."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from gpu_helpers import canon_blocks, canon_triangles, canon_vertices
+    gk, gt, gw = canon_blocks(*vbg.export())
+    ok_, ot, ow = canon_blocks(*ref.export())
+    keys_equal = gk.shape == ok_.shape and bool(np.array_equal(gk, ok_))
+    out = {"blocks": int(len(gk)), "keys_equal": keys_equal}
+    if keys_equal:
+        out["weights_equal"] = bool(np.array_equal(gw, ow))
+        m = gw > 0
+        out["max_dtsdf"] = float(np.abs(gt[m] - ot[m]).max()) if m.any() else 0.0
+    del gt, gw, ot, ow
+    mesh = vbg.extract_triangle_mesh(weight_threshold=thr)
+    ov, _, otri = ref.extract_mesh(thr)
+    out["mesh_threshold"] = thr
+    out["triangles"] = int(len(mesh.triangles))
+    out["triangle_count_equal"] = len(mesh.triangles) == len(otri)
+    out["vertex_count_equal"] = len(mesh.vertices) == len(ov)
+    if out["triangle_count_equal"] and out["vertex_count_equal"]:
+        out["vertices_equal"] = bool(np.array_equal(canon_vertices(mesh.vertices)[0], canon_vertices(ov)[0]))
+        out["triangles_equal"] = bool(np.array_equal(canon_triangles(mesh.vertices, mesh.triangles),
+                                                     canon_triangles(ov, otri)))
+    out["tolerance"] = 1e-4
+    out["all_ok"] = bool(out.get("keys_equal") and out.get("weights_equal") and out.get("max_dtsdf", 1) <= 1e-4
+                         and out.get("triangles_equal") and out.get("vertices_equal"))
     return out
+
+
+def confidence_cpu(depth_host, K, T_wc, args, budget_s):
+    """CPU baseline of the confidence leg: the oracle's build_confidence_map restatement (fp64,
+    OpenMP over pixels) on as many reference frames as fit in ~budget_s."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    cores, _ = host_cores()
+    oracle.set_threads(cores)
+    T_cw = np.linalg.inv(T_wc).astype(np.float32)
+    Ti = np.linalg.inv(T_cw).astype(np.float32)
+    n = len(depth_host)
+    t0 = time.perf_counter()
+    done = 0
+    for i in np.linspace(0, n - 1, n).astype(int)[np.random.default_rng(0).permutation(n)]:
+        oracle.confidence(depth_host, K, T_cw, Ti, int(i), args.conf_range, args.conf_depth_max, args.conf_error)
+        done += 1
+        if time.perf_counter() - t0 > budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "ref frames/s", "cores": cores, "kind": "port",
+            "sample": f"{done} random reference frames of the sequence (r = {args.conf_range}), oracle.confidence "
+                      f"(oracle/mqr_oracle.c, OpenMP over pixels), {dt:.1f} s"}
 
 
 def main():
@@ -300,10 +488,13 @@ def main():
 
     merge_times = []
 
-    def step():
+    def step_integrate():
         vbg.reset()
         vbg.integrate_frames(dptr, K, T, depth_scale=1.0, depth_max=args.depth_max,
                              trunc_voxel_multiplier=args.trunc)
+
+    def step():
+        step_integrate()
         if world > 1:
             t = time.perf_counter()
             merge_to_root(vbg, method=args.merge)
@@ -352,6 +543,9 @@ def main():
         extras["ingest"] = ingest_leg(B, H, W, dev)
         extras["raycast"] = raycast_leg(vbg, K, T, H, W, args.extract_threshold)
         extras["meshfilter"] = meshfilter_leg(vbg, args.extract_threshold)
+        extras["c3"] = c3_leg(seq, vbg, args, dev)
+        if args.e2e_frames > 0:
+            extras["dropin_e2e"] = dropin_e2e_leg(seq, min(args.e2e_frames, B), dev)
         # PCIe-inclusive: the same step from host (numpy) frames, H2D inside integrate_frames
         host = depth_t.cpu().numpy()
         vbg.reset()
@@ -365,9 +559,19 @@ def main():
     if ext_ms:
         ext_alg = (8 * R3_ * blocks + 4 * 27 * blocks + 24 * nv + 12 * nt) / (ext_ms * 1e-3) / 1e9
 
-    cpu = None
+    cpu = parity = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(depth_t.cpu().numpy(), K, T, args)
+        host_depth = depth_t.cpu().numpy()
+        cpu, ref_vol = cpu_baseline(host_depth, K, T, args)
+        if not args.no_parity:
+            # the volume of the last timed step is still in vbg unless an extra leg reset it: rebuild
+            # it exactly as a step does (reset + integrate_frames) when the legs ran
+            if extras:
+                step_integrate()
+            parity = parity_check(vbg, ref_vol, args.extract_threshold)
+        del ref_vol
+        if extras.get("confidence") is not None and args.conf_cpu_seconds > 0:
+            extras["confidence"]["cpu_baseline"] = confidence_cpu(host_depth, K, T, args, args.conf_cpu_seconds)
 
     traffic, traffic_src = pmc_traffic(H, W, B)
 
@@ -386,8 +590,9 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (procedural room, GPU ray-cast, sigma=0.002z noise + 1% dropout)",
-            "config": {"workload": "BASELINE config 1: 500-frame LEFT depth sequence per GPU, 640x480, hashed "
-                                   "TSDF 5 mm voxels, 512^3 effective volume, R=16, depth_max 4 m, trunc 10",
+            "config": {"workload": "C2 (SURVEY.md §8(d); BASELINE.json configs[1]): 500-frame LEFT depth sequence "
+                                   "per GPU, 640x480, hashed TSDF 5 mm voxels, 512^3 effective volume, R=16, "
+                                   "depth_max 4 m, trunc 10",
                        "frames_per_gpu": B, "height": H, "width": W, "voxel_size": args.voxel,
                        "block_resolution": args.block_resolution, "depth_max": args.depth_max,
                        "trunc_voxel_multiplier": args.trunc, "frame_batch": 64,
@@ -415,6 +620,9 @@ def main():
                              st["frame_blocks"] / max(st["frames"], 1),
                          "touch_ms_per_launch": st["touch_ms"] / max(st["touch_launches"], 1)},
             "cpu_baseline": cpu,
+            "parity": parity,
+            "c3": extras.get("c3"),
+            "dropin_e2e": extras.get("dropin_e2e"),
         }
         print(json.dumps(out), flush=True)
     if dist:

@@ -1031,13 +1031,22 @@ int mqr_extract_mesh(mqr_vbg* v, float thr, mqr_geom** out) {
     const int64_t n = v->pool_count;
     mqr_geom* g = new mqr_geom();
     g->device = v->device;
+    *out = nullptr;
+    int rc = 0;
+    if (n > 0) {
+        ExScratch e{};
+        rc = ex_scratch(v, n, true, e) || build_nb(v, e.nb);
+        if (!rc) rc = v->R == 16 ? mesh_passes<16>(v, thr, e, g) : v->R == 8 ? mesh_passes<8>(v, thr, e, g)
+                                                                          : mesh_passes<0>(v, thr, e, g);
+    }
+    if (rc) {  // release whatever the failed passes allocated; the caller gets no handle
+        const std::string msg = get_error();
+        mqr_geom_free(g);
+        set_error(msg);
+        return rc;
+    }
     *out = g;
-    if (n == 0) return 0;
-    ExScratch e{};
-    if (ex_scratch(v, n, true, e) || build_nb(v, e.nb)) return 1;
-    if (v->R == 16) return mesh_passes<16>(v, thr, e, g);
-    if (v->R == 8) return mesh_passes<8>(v, thr, e, g);
-    return mesh_passes<0>(v, thr, e, g);
+    return 0;
 }
 
 int mqr_extract_points(mqr_vbg* v, float thr, mqr_geom** out) {
@@ -1048,13 +1057,22 @@ int mqr_extract_points(mqr_vbg* v, float thr, mqr_geom** out) {
     const int64_t n = v->pool_count;
     mqr_geom* g = new mqr_geom();
     g->device = v->device;
+    *out = nullptr;
+    int rc = 0;
+    if (n > 0) {
+        ExScratch e{};
+        rc = ex_scratch(v, n, false, e) || build_nb(v, e.nb);
+        if (!rc) rc = v->R == 16 ? point_passes<16>(v, thr, e, g) : v->R == 8 ? point_passes<8>(v, thr, e, g)
+                                                                           : point_passes<0>(v, thr, e, g);
+    }
+    if (rc) {
+        const std::string msg = get_error();
+        mqr_geom_free(g);
+        set_error(msg);
+        return rc;
+    }
     *out = g;
-    if (n == 0) return 0;
-    ExScratch e{};
-    if (ex_scratch(v, n, false, e) || build_nb(v, e.nb)) return 1;
-    if (v->R == 16) return point_passes<16>(v, thr, e, g);
-    if (v->R == 8) return point_passes<8>(v, thr, e, g);
-    return point_passes<0>(v, thr, e, g);
+    return 0;
 }
 
 int mqr_geom_counts(mqr_geom* g, int64_t* nv, int64_t* nt) {

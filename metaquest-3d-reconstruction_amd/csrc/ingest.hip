@@ -18,6 +18,7 @@
 // Mask: depth = 0 where conf < conf_thr, and where valid_count < count_thr.
 #include <algorithm>
 #include <cmath>
+#include <mutex>
 #include <vector>
 
 #include "mqr_common.hpp"
@@ -33,6 +34,32 @@ struct DecodeFrame {
 // validity flag bits accumulated per frame
 constexpr uint32_t kAnyNonZero = 1, kAnyNonOne = 2, kAnyNaN = 4, kAnyNotGE0 = 8;
 
+// One pixel: NDC decode with the frame's numpy dtype rules, then the confidence mask.
+template <bool MASK>
+__device__ __forceinline__ float decode_px(float d, const DecodeFrame& fr, double c, int32_t vc, double conf_thr,
+                                           int count_thr, uint32_t& fl) {
+    fl |= (d != 0.0f ? kAnyNonZero : 0u) | (d != 1.0f ? kAnyNonOne : 0u) | (d != d ? kAnyNaN : 0u) |
+          (!(d >= 0.0f) ? kAnyNotGE0 : 0u);
+    const float ndc = d * 2.0f - 1.0f;
+    float z = 0.0f;
+    if (fr.strong & 2) {
+        const double den = (double)ndc + fr.y;
+        if (den != 0.0) z = (float)(fr.x / den);
+    } else {
+        const float den = ndc + (float)fr.y;
+        if (den != 0.0f) z = (fr.strong & 1) ? (float)(fr.x / (double)den) : (float)fr.x / den;
+    }
+    if (MASK) {
+        if (c < conf_thr) z = 0.0f;
+        if (vc < count_thr) z = 0.0f;
+    }
+    return z;
+}
+
+// Thread per 4 consecutive pixels of one frame (blockIdx.y): 16-byte raw / count / depth
+// accesses and two 16-byte confidence loads, so every wave moves whole 1 KiB (raw) or 2 KiB
+// (confidence) runs.  VEC = false: scalar tail path for frames whose size is not a multiple of 4.
+template <bool VEC>
 __global__ __launch_bounds__(256) void k_decode_depth(const float* __restrict__ raw, int64_t HW,
                                                       const DecodeFrame* __restrict__ frames,
                                                       const double* __restrict__ conf,
@@ -43,30 +70,92 @@ __global__ __launch_bounds__(256) void k_decode_depth(const float* __restrict__ 
     const DecodeFrame fr = frames[f];
     const int64_t base = (int64_t)f * HW;
     uint32_t fl = 0;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < HW; i += (int64_t)gridDim.x * blockDim.x) {
-        const float d = raw[base + i];
-        fl |= (d != 0.0f ? kAnyNonZero : 0u) | (d != 1.0f ? kAnyNonOne : 0u) | (d != d ? kAnyNaN : 0u) |
-              (!(d >= 0.0f) ? kAnyNotGE0 : 0u);
-        const float ndc = d * 2.0f - 1.0f;
-        float z = 0.0f;
-        if (fr.strong & 2) {
-            const double den = (double)ndc + fr.y;
-            if (den != 0.0) z = (float)(fr.x / den);
-        } else {
-            const float den = ndc + (float)fr.y;
-            if (den != 0.0f) z = (fr.strong & 1) ? (float)(fr.x / (double)den) : (float)fr.x / den;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    if (VEC) {
+        const int64_t n4 = HW >> 2;
+        const float4* r4 = reinterpret_cast<const float4*>(raw + base);
+        float4* o4 = reinterpret_cast<float4*>(out + base);
+        for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+            const float4 d = r4[i];
+            float4 z;
+            if (fr.mask) {
+                const double2* c2 = reinterpret_cast<const double2*>(conf + base) + 2 * i;
+                const double2 ca = c2[0], cb = c2[1];
+                const int4 v = reinterpret_cast<const int4*>(vcount + base)[i];
+                z.x = decode_px<true>(d.x, fr, ca.x, v.x, conf_thr, count_thr, fl);
+                z.y = decode_px<true>(d.y, fr, ca.y, v.y, conf_thr, count_thr, fl);
+                z.z = decode_px<true>(d.z, fr, cb.x, v.z, conf_thr, count_thr, fl);
+                z.w = decode_px<true>(d.w, fr, cb.y, v.w, conf_thr, count_thr, fl);
+            } else {
+                z.x = decode_px<false>(d.x, fr, 0.0, 0, conf_thr, count_thr, fl);
+                z.y = decode_px<false>(d.y, fr, 0.0, 0, conf_thr, count_thr, fl);
+                z.z = decode_px<false>(d.z, fr, 0.0, 0, conf_thr, count_thr, fl);
+                z.w = decode_px<false>(d.w, fr, 0.0, 0, conf_thr, count_thr, fl);
+            }
+            o4[i] = z;
         }
-        if (fr.mask) {
-            if (conf[base + i] < conf_thr) z = 0.0f;
-            if (vcount[base + i] < count_thr) z = 0.0f;
+    } else {
+        for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < HW; i += stride) {
+            const float d = raw[base + i];
+            out[base + i] = fr.mask ? decode_px<true>(d, fr, conf[base + i], vcount[base + i], conf_thr, count_thr, fl)
+                                    : decode_px<false>(d, fr, 0.0, 0, conf_thr, count_thr, fl);
         }
-        out[base + i] = z;
     }
     // wave-level OR, then one atomic per wave only for bits the frame's word does not have yet
     // (every wave of a frame would otherwise hit the same address: thousands of serialised atomics)
     for (int o = 32; o > 0; o >>= 1) fl |= (uint32_t)__shfl_xor((int)fl, o, 64);
     if ((threadIdx.x & 63) == 0 && (fl & ~__atomic_load_n(&flags[f], __ATOMIC_RELAXED))) atomicOr(&flags[f], fl);
 }
+
+// Per-device decode context, created on first use and kept: a stream, a grow-only scratch buffer
+// (staged host inputs / output), the per-frame parameter and flag arrays and their pinned
+// mirrors.  Creating a stream and mapping fresh device pages cost milliseconds per call; the
+// kernel itself streams 20 B per pixel.  Calls on one device serialise on the context's mutex.
+struct DecodeCtx {
+    std::mutex mu;
+    hipStream_t s = nullptr;
+    char* scratch = nullptr;
+    size_t scratch_cap = 0;
+    DecodeFrame* d_fr = nullptr;
+    uint32_t* d_flags = nullptr;
+    DecodeFrame* h_fr = nullptr;
+    uint32_t* h_flags = nullptr;
+    int frame_cap = 0;
+};
+static DecodeCtx g_decode[64];
+
+static int decode_ctx_reserve(DecodeCtx& c, size_t scratch_bytes, int frames) {
+    if (!c.s) MQR_CHECK_HIP(hipStreamCreateWithFlags(&c.s, hipStreamNonBlocking));
+    if (scratch_bytes > c.scratch_cap) {
+        MQR_CHECK_HIP(hipStreamSynchronize(c.s));
+        if (c.scratch) MQR_CHECK_HIP(hipFree(c.scratch));
+        c.scratch = nullptr;
+        c.scratch_cap = 0;
+        MQR_CHECK_HIP(hipMalloc(&c.scratch, scratch_bytes));
+        c.scratch_cap = scratch_bytes;
+    }
+    if (frames > c.frame_cap) {
+        MQR_CHECK_HIP(hipStreamSynchronize(c.s));
+        const int cap = std::max(frames, 256);
+        if (c.d_fr) MQR_CHECK_HIP(hipFree(c.d_fr));
+        if (c.d_flags) MQR_CHECK_HIP(hipFree(c.d_flags));
+        if (c.h_fr) MQR_CHECK_HIP(hipHostFree(c.h_fr));
+        if (c.h_flags) MQR_CHECK_HIP(hipHostFree(c.h_flags));
+        c.d_fr = nullptr;
+        c.d_flags = nullptr;
+        c.h_fr = nullptr;
+        c.h_flags = nullptr;
+        c.frame_cap = 0;
+        MQR_CHECK_HIP(hipMalloc(&c.d_fr, sizeof(DecodeFrame) * cap));
+        MQR_CHECK_HIP(hipMalloc(&c.d_flags, sizeof(uint32_t) * cap));
+        MQR_CHECK_HIP(hipHostMalloc(&c.h_fr, sizeof(DecodeFrame) * cap, hipHostMallocDefault));
+        MQR_CHECK_HIP(hipHostMalloc(&c.h_flags, sizeof(uint32_t) * cap, hipHostMallocDefault));
+        c.frame_cap = cap;
+    }
+    return 0;
+}
+
+static size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
 }  // namespace mqr
 
@@ -80,15 +169,25 @@ int mqr_decode_depth(int device, const float* raw, int raw_loc, int N, int H, in
                      int out_loc, uint8_t* frame_ok) {
     MQR_REQUIRE(raw && nears && fars && depth_out && frame_ok, "null argument");
     MQR_REQUIRE(N >= 0 && H > 0 && W > 0, "bad frame shape");
+    MQR_REQUIRE(device >= 0 && device < 64, "device index out of range");
     if (N == 0) return 0;
     const bool any_mask = has_mask && std::any_of(has_mask, has_mask + N, [](uint8_t m) { return m != 0; });
     MQR_REQUIRE(!any_mask || (conf && valid_count), "mask requested without confidence maps");
     MQR_CHECK_HIP(hipSetDevice(device));
     const int64_t HW = (int64_t)H * W, total = HW * N;
-    std::vector<DecodeFrame> hf(N);
+    DecodeCtx& c = g_decode[device];
+    std::lock_guard<std::mutex> lock(c.mu);
+    // scratch layout: [raw f32][conf f64][count i32][out f32], only the parts that are staged
+    const bool stage_raw = raw_loc != MQR_DEVICE, stage_mask = any_mask && mask_loc != MQR_DEVICE,
+               stage_out = out_loc != MQR_DEVICE;
+    const size_t b_raw = stage_raw ? align256(sizeof(float) * total) : 0;
+    const size_t b_conf = stage_mask ? align256(sizeof(double) * total) : 0;
+    const size_t b_vc = stage_mask ? align256(sizeof(int32_t) * total) : 0;
+    const size_t b_out = stage_out ? align256(sizeof(float) * total) : 0;
+    if (decode_ctx_reserve(c, std::max<size_t>(b_raw + b_conf + b_vc + b_out, 256), N)) return 1;
     for (int f = 0; f < N; ++f) {
         const double nr = nears[f], fa = fars[f];
-        DecodeFrame& d = hf[f];
+        DecodeFrame& d = c.h_fr[f];
         if (std::isinf(fa) || fa < nr) {  // compute_ndc_to_linear_depth_params, depth_utils.py:21-28
             d.x = -2.0 * nr;
             d.y = -1.0;
@@ -100,75 +199,46 @@ int mqr_decode_depth(int device, const float* raw, int raw_loc, int N, int H, in
         }
         d.mask = any_mask && has_mask[f];
     }
-    hipStream_t s = nullptr;
-    MQR_CHECK_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-    std::vector<void*> owned;
-    auto dev_alloc = [&](size_t bytes) -> void* {
-        void* p = nullptr;
-        if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
-        owned.push_back(p);
-        return p;
-    };
-    int rc = 0;
-    do {
-        const float* d_raw = raw;
-        if (raw_loc != MQR_DEVICE) {
-            float* p = static_cast<float*>(dev_alloc(sizeof(float) * total));
-            if (!p || hipMemcpyAsync(p, raw, sizeof(float) * total, hipMemcpyHostToDevice, s) != hipSuccess) {
-                set_error("decode: raw upload failed");
-                rc = 1;
-                break;
-            }
-            d_raw = p;
-        }
-        const double* d_conf = conf;
-        const int32_t* d_vc = valid_count;
-        if (any_mask && mask_loc != MQR_DEVICE) {
-            double* pc = static_cast<double*>(dev_alloc(sizeof(double) * total));
-            int32_t* pv = static_cast<int32_t*>(dev_alloc(sizeof(int32_t) * total));
-            if (!pc || !pv || hipMemcpyAsync(pc, conf, sizeof(double) * total, hipMemcpyHostToDevice, s) ||
-                hipMemcpyAsync(pv, valid_count, sizeof(int32_t) * total, hipMemcpyHostToDevice, s)) {
-                set_error("decode: confidence upload failed");
-                rc = 1;
-                break;
-            }
-            d_conf = pc;
-            d_vc = pv;
-        }
-        float* d_out = out_loc == MQR_DEVICE ? depth_out : static_cast<float*>(dev_alloc(sizeof(float) * total));
-        DecodeFrame* d_fr = static_cast<DecodeFrame*>(dev_alloc(sizeof(DecodeFrame) * N));
-        uint32_t* d_flags = static_cast<uint32_t*>(dev_alloc(sizeof(uint32_t) * N));
-        if (!d_out || !d_fr || !d_flags || hipMemcpyAsync(d_fr, hf.data(), sizeof(DecodeFrame) * N,
-                                                          hipMemcpyHostToDevice, s) ||
-            hipMemsetAsync(d_flags, 0, sizeof(uint32_t) * N, s)) {
-            set_error("decode: device allocation failed");
-            rc = 1;
-            break;
-        }
-        const unsigned gx = (unsigned)std::min<int64_t>((HW + 255) / 256, 1024);
-        hipLaunchKernelGGL(k_decode_depth, dim3(gx, (unsigned)N), dim3(256), 0, s, d_raw, HW, d_fr, d_conf, d_vc,
-                           conf_thr, count_thr, d_out, d_flags);
-        if (hipGetLastError() != hipSuccess) {
-            set_error("decode: kernel launch failed");
-            rc = 1;
-            break;
-        }
-        std::vector<uint32_t> fl(N);
-        if (hipMemcpyAsync(fl.data(), d_flags, sizeof(uint32_t) * N, hipMemcpyDeviceToHost, s) ||
-            (out_loc != MQR_DEVICE &&
-             hipMemcpyAsync(depth_out, d_out, sizeof(float) * total, hipMemcpyDeviceToHost, s)) ||
-            hipStreamSynchronize(s)) {
-            set_error("decode: copy back failed");
-            rc = 1;
-            break;
-        }
-        for (int f = 0; f < N; ++f)
-            frame_ok[f] = (fl[f] & kAnyNonZero) && (fl[f] & kAnyNonOne) && !(fl[f] & (kAnyNaN | kAnyNotGE0));
-    } while (false);
-    (void)hipStreamSynchronize(s);
-    for (void* p : owned) (void)hipFree(p);
-    (void)hipStreamDestroy(s);
-    return rc;
+    char* sp = c.scratch;
+    const float* d_raw = raw;
+    if (stage_raw) {
+        MQR_CHECK_HIP(hipMemcpyAsync(sp, raw, sizeof(float) * total, hipMemcpyHostToDevice, c.s));
+        d_raw = reinterpret_cast<const float*>(sp);
+        sp += b_raw;
+    }
+    const double* d_conf = conf;
+    const int32_t* d_vc = valid_count;
+    if (stage_mask) {
+        MQR_CHECK_HIP(hipMemcpyAsync(sp, conf, sizeof(double) * total, hipMemcpyHostToDevice, c.s));
+        d_conf = reinterpret_cast<const double*>(sp);
+        sp += b_conf;
+        MQR_CHECK_HIP(hipMemcpyAsync(sp, valid_count, sizeof(int32_t) * total, hipMemcpyHostToDevice, c.s));
+        d_vc = reinterpret_cast<const int32_t*>(sp);
+        sp += b_vc;
+    }
+    float* d_out = stage_out ? reinterpret_cast<float*>(sp) : depth_out;
+    MQR_CHECK_HIP(hipMemcpyAsync(c.d_fr, c.h_fr, sizeof(DecodeFrame) * N, hipMemcpyHostToDevice, c.s));
+    MQR_CHECK_HIP(hipMemsetAsync(c.d_flags, 0, sizeof(uint32_t) * N, c.s));
+    auto aligned = [](const void* p, size_t a) { return (reinterpret_cast<uintptr_t>(p) & (a - 1)) == 0; };
+    const bool vec = HW % 4 == 0 && aligned(d_raw, 16) && aligned(d_out, 16) &&
+                     (!any_mask || (aligned(d_conf, 32) && aligned(d_vc, 16)));
+    const int64_t work = vec ? HW / 4 : HW;
+    const unsigned gx = (unsigned)std::min<int64_t>((work + 255) / 256, 2048);
+    if (vec)
+        hipLaunchKernelGGL(k_decode_depth<true>, dim3(gx, (unsigned)N), dim3(256), 0, c.s, d_raw, HW, c.d_fr, d_conf,
+                           d_vc, conf_thr, count_thr, d_out, c.d_flags);
+    else
+        hipLaunchKernelGGL(k_decode_depth<false>, dim3(gx, (unsigned)N), dim3(256), 0, c.s, d_raw, HW, c.d_fr, d_conf,
+                           d_vc, conf_thr, count_thr, d_out, c.d_flags);
+    MQR_CHECK_HIP(hipGetLastError());
+    MQR_CHECK_HIP(hipMemcpyAsync(c.h_flags, c.d_flags, sizeof(uint32_t) * N, hipMemcpyDeviceToHost, c.s));
+    if (stage_out) MQR_CHECK_HIP(hipMemcpyAsync(depth_out, d_out, sizeof(float) * total, hipMemcpyDeviceToHost, c.s));
+    MQR_CHECK_HIP(hipStreamSynchronize(c.s));
+    for (int f = 0; f < N; ++f) {
+        const uint32_t fl = c.h_flags[f];
+        frame_ok[f] = (fl & kAnyNonZero) && (fl & kAnyNonOne) && !(fl & (kAnyNaN | kAnyNotGE0));
+    }
+    return 0;
 }
 
 }  // extern "C"

@@ -683,25 +683,43 @@ int mqr_integrate_frames(mqr_vbg* v, const float* depths, int depth_loc, int B, 
             }
             dbase = v->d_depth[p];
         }
+        const int64_t pool_before = v->pool_count;
         if (upload_frames(v, p, K, T_wc, idx, b, dframe) || reset_batch_counters(v, p)) return 1;
         if (touch_launch(v, p, dbase, HW, H, W, b, depth_scale, depth_max, sdf_trunc, block_size, v->table(p), 1))
             return 1;
         if (resolve_pool_overflow(v, p)) return 1;
-        for (int f = 0; f < b; ++f)
-            if (v->hctr(p)[kFrameCounterBase + f] == 0) {
-                set_error(kNoBlock);
-                rc = 3;
-            }
-        if (rc) {  // leave the volume consistent: clear this batch's slot marks before failing
+        int empty = -1;  // first frame of the batch that touched no block
+        for (int f = 0; f < b && empty < 0; ++f)
+            if (v->hctr(p)[kFrameCounterBase + f] == 0) empty = f;
+        if (empty >= 0) {
+            // Open3D raises at frame `empty` (DepthTouch) after integrating the frames
+            // before it and before touching anything after it: undo the whole batch's touch (slot marks,
+            // blocks it allocated), then integrate the prefix [0, empty) as a batch of its own.
+            set_error(kNoBlock);
+            rc = 3;
             const int64_t n = std::min<int64_t>(v->hctr(p)[kListCount], v->list_cap);
             if (n > 0)
                 hipLaunchKernelGGL(k_clear_slots, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, v->stream,
                                    v->lists[p], n, v->table(p), 0);
+            hipLaunchKernelGGL(k_rollback, dim3((unsigned)((v->tab.cap + 255) / 256)), dim3(256), 0, v->stream,
+                               v->table(p), (int)pool_before);
+            hipLaunchKernelGGL(k_set_counter, dim3(1), dim3(1), 0, v->stream, v->pool_ctr(), (int)pool_before);
+            MQR_CHECK_HIP(hipGetLastError());
+            v->pool_count = pool_before;
+            if (empty > 0) {
+                if (upload_frames(v, p, K, T_wc, idx, empty, dframe) || reset_batch_counters(v, p)) return 1;
+                if (touch_launch(v, p, dbase, HW, H, W, empty, depth_scale, depth_max, sdf_trunc, block_size,
+                                 v->table(p), 1))
+                    return 1;
+                if (resolve_pool_overflow(v, p)) return 1;
+                if (launch_integrate(v, p, dbase, HW, H, W, empty, depth_scale, depth_max, sdf_trunc)) return 1;
+            }
             break;
         }
         if (launch_integrate(v, p, dbase, HW, H, W, b, depth_scale, depth_max, sdf_trunc)) return 1;
     }
     if (sync_all(v)) return 1;
+    if (rc) set_error(kNoBlock);  // the prefix re-run may have overwritten the message
     return rc;
 }
 
@@ -932,7 +950,7 @@ int mqr_vbg_profile(mqr_vbg* v, int enable) {
     // create the timing events now, outside any timed region (4 per batch; more are created on
     // demand until the next stats read recycles them)
     MQR_CHECK_HIP(hipSetDevice(v->device));
-    while (v->profile && v->ev_pool.size() < 1024) {
+    while (v->profile && v->ev_pool.size() < 12288) {
         hipEvent_t e = nullptr;
         MQR_CHECK_HIP(hipEventCreate(&e));
         v->ev_pool.push_back(e);

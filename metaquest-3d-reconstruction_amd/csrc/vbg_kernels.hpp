@@ -1333,6 +1333,22 @@ __global__ void k_fixup_alloc(Table t, int* counters, int* pool_ctr, int64_t poo
     }
 }
 
+// Undo the allocations of a batch that failed (a frame touched no block): every key whose buffer
+// index is >= `first_buf` was inserted by that batch.  Keys inserted earlier never probe through a
+// slot claimed later (linear probing), so removing exactly the later keys keeps every remaining
+// probe chain intact.  Their pool buffers were never integrated and are still zero.
+__global__ void k_rollback(Table t, int first_buf) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= t.cap) return;
+    if (t.keys[i] == kEmpty) return;
+    const int b = t.vals[i];
+    if (b >= first_buf || b == -2) {
+        t.keys[i] = kEmpty;
+        t.vals[i] = -1;
+        t.mask[i] = 0;
+    }
+}
+
 __global__ void k_gather_keys(const int32_t* __restrict__ list, int64_t n, const Table t, int32_t* keys_out) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;

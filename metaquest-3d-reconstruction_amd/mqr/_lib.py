@@ -98,6 +98,26 @@ class MqrError(RuntimeError):
         self.code = code
 
 
+def hip_runtime_path():
+    """The HIP runtime this process must use.
+
+    libamdhip64 is bound by SONAME (libamdhip64.so.7): whichever copy is mapped first serves every
+    later library that needs it.  PyTorch ships its own copy (and its own HSA runtime, loaded by
+    file name), so if /opt/rocm's copy came first -- libmqr_hip.so's RUNPATH -- a later
+    ``import torch`` maps a second HIP + HSA runtime and finds no device.  Mapping torch's copy first
+    (when torch is installed) gives ONE runtime per process in either import order.  MQR_HIP_RUNTIME
+    overrides the choice; without torch, libmqr's RUNPATH (/opt/rocm/lib) applies."""
+    env = os.environ.get("MQR_HIP_RUNTIME")
+    if env:
+        return env
+    import importlib.util
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.origin:
+        return None
+    p = os.path.join(os.path.dirname(spec.origin), "lib", "libamdhip64.so")
+    return p if os.path.exists(p) else None
+
+
 def load(path: str = LIB_PATH):
     """Load libmqr_hip.so (no compute happens here)."""
     global _lib
@@ -106,6 +126,9 @@ def load(path: str = LIB_PATH):
     if not os.path.exists(path):
         raise ImportError(f"libmqr_hip.so not found at {path}; build it with "
                           "`python -c 'import __graft_entry__ as g; g.build()'` (there is no CPU fallback)")
+    rt = hip_runtime_path()
+    if rt:
+        ctypes.CDLL(rt, mode=ctypes.RTLD_GLOBAL)
     L = ctypes.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(L, name)

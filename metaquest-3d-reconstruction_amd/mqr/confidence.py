@@ -96,6 +96,9 @@ def build_confidence_map(depth_data_io, dataset, intrinsic_matrices, extrinsic_m
 
 
 def estimate_depth_confidences(depth_data_io, config: DepthConfidenceEstimationConfig, sides=None):
+    """Per side: skip if the output directory exists (``skip_if_output_dir_exists``), keep existing
+    per-frame files, compute the rest in chunks of REF_CHUNK reference frames.  Frames are decoded
+    once each and held only while a chunk's window [first - r, last + r] needs them."""
     for side in (sides or list(Side)):
         if config.skip_if_output_dir_exists and depth_data_io.exists_depth_confidence_map_dir(side=side):
             print(f"[{side.name}] Skipping confidence map estimation: output directory already exists. "
@@ -109,22 +112,40 @@ def estimate_depth_confidences(depth_data_io, config: DepthConfidenceEstimationC
         T_cw = dataset.transforms.convert_coordinate_system(target_coordinate_system=CoordinateSystem.OPEN3D,
                                                             is_camera=True).extrinsics_cw
         T_inv = np.linalg.inv(T_cw)
-        frames = [depth_data_io.load_depth_map_by_index(side=side, dataset=dataset, index=i) for i in range(n)]
-        shape = next((f.shape for f in frames if f is not None), None)
-        if shape is None:
-            continue
-        ok = np.array([f is not None and f.shape == shape for f in frames])
-        depths = np.stack([f if o else np.zeros(shape, np.float32) for f, o in zip(frames, ok)])
-        todo = [i for i in range(n) if ok[i]
-                and depth_data_io.load_confidence_map(side=side, timestamp=dataset.timestamps[i]) is None]
         r = int(config.target_frame_range)
+        todo = [i for i in range(n) if depth_data_io.load_confidence_map(side=side, timestamp=dataset.timestamps[i])
+                is None]
+        cache = {}  # index -> decoded frame (None: missing / invalid), frames of the current window only
+
+        def frame(i):
+            if i not in cache:
+                cache[i] = depth_data_io.load_depth_map_by_index(side=side, dataset=dataset, index=i)
+            return cache[i]
+
         for c0 in range(0, len(todo), REF_CHUNK):
-            chunk = todo[c0:c0 + REF_CHUNK]
-            a, b = chunk[0], chunk[-1] + 1
-            lo, hi = max(0, a - r), min(n, b + r)
-            conf, valid = confidence_maps(depths[lo:hi], K[lo:hi], T_cw[lo:hi], T_inv[lo:hi], a - lo, b - lo, r,
-                                          config.depth_max, config.error_threshold, ok[lo:hi],
-                                          device=getattr(config, "device", 0))
-            for i in chunk:
-                depth_data_io.save_confidence_map(side=side, timestamp=dataset.timestamps[i],
-                                                  confidence_map=ConfidenceMap(conf[i - a], valid[i - a]))
+            chunk = [i for i in todo[c0:c0 + REF_CHUNK] if frame(i) is not None]  # invalid refs: no output
+            for i in [k for k in cache if chunk and k < chunk[0] - r]:
+                del cache[i]
+            # runs of one frame size spanning < REF_CHUNK indices (sparse resumes keep windows small); a
+            # neighbour of another size counts as a failed load
+            j = 0
+            while j < len(chunk):
+                shape = frame(chunk[j]).shape
+                k = j + 1
+                while k < len(chunk) and frame(chunk[k]).shape == shape and chunk[k] - chunk[j] < REF_CHUNK:
+                    k += 1
+                refs = chunk[j:k]
+                a, b = refs[0], refs[-1] + 1
+                lo, hi = max(0, a - r), min(n, b + r)
+                win = [frame(i) for i in range(lo, hi)]
+                ok = np.array([f is not None and f.shape == shape for f in win])
+                if (~ok & np.array([f is not None for f in win])).any():
+                    print(f"[Warning] {side.name}: neighbour frames of a size other than {shape} are skipped")
+                depths = np.stack([f if o else np.zeros(shape, np.float32) for f, o in zip(win, ok)])
+                conf, valid = confidence_maps(depths, K[lo:hi], T_cw[lo:hi], T_inv[lo:hi], a - lo, b - lo, r,
+                                              config.depth_max, config.error_threshold, ok,
+                                              device=getattr(config, "device", 0))
+                for i in refs:
+                    depth_data_io.save_confidence_map(side=side, timestamp=dataset.timestamps[i],
+                                                      confidence_map=ConfidenceMap(conf[i - a], valid[i - a]))
+                j = k

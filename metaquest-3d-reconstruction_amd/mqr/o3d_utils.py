@@ -152,9 +152,16 @@ def integrate(dataset, depth_data_io, side, use_confidence_filtered_depth: bool,
         while fut is not None:
             lo, hi, items = fut.result()
             fut = pool.submit(load_chunk, hi) if hi < n else None
-            for shape in dict.fromkeys(f.shape for _, f, _ in items):  # one size per capture; group defensively
-                sel = [it for it in items if it[1].shape == shape]
-                run(np.array([i for i, _, _ in sel]), [f for _, f, _ in sel], [c for _, _, c in sel], *shape)
+            # consecutive runs of one frame size, in dataset order (the running average is order-dependent)
+            j = 0
+            while j < len(items):
+                k = j + 1
+                while k < len(items) and items[k][1].shape == items[j][1].shape:
+                    k += 1
+                sel = items[j:k]
+                run(np.array([i for i, _, _ in sel]), [f for _, f, _ in sel], [c for _, _, c in sel],
+                    *sel[0][1].shape)
+                j = k
             if bar is not None:
                 bar.update(hi - lo)
     if bar is not None:

@@ -193,8 +193,8 @@ def make_sequence_fast(scene="room", poses=None, n=500, height=480, width=640, f
     K[:, 0, 0], K[:, 1, 1], K[:, 2, 2] = fx, fy, 1.0
     K[:, 0, 2], K[:, 1, 2] = cx_desc, cy_desc
     K[:, 0, 2] = width - K[:, 0, 2]
-    return {"depth_t": depth, "K": K, "T_wc": o3d.extrinsics_wc, "T_cw": o3d.extrinsics_cw, "unity": unity,
-            "width": width, "height": height}
+    return {"depth_t": depth, "raw_t": raw, "K": K, "T_wc": o3d.extrinsics_wc, "T_cw": o3d.extrinsics_cw,
+            "unity": unity, "tangents": (l, r, t, b), "near": near, "far": far, "width": width, "height": height}
 
 
 def corrupt(z, rng, sigma_rel=0.002, dropout=0.01):

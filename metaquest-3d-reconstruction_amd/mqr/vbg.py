@@ -190,7 +190,12 @@ class VoxelBlockGrid:
     # -- extraction --------------------------------------------------------------------------------
     def _geom(self, fn, thr):
         g = ctypes.c_void_p()
-        call(fn, self._h, float(thr), ctypes.byref(g))
+        try:
+            call(fn, self._h, float(thr), ctypes.byref(g))
+        except _lib.MqrError:
+            if g.value:  # a failed extraction may still have handed out its result object
+                _lib._lib.mqr_geom_free(g)
+            raise
         try:
             nv, nt = ctypes.c_int64(), ctypes.c_int64()
             call("mqr_geom_counts", g, ctypes.byref(nv), ctypes.byref(nt))

@@ -46,3 +46,18 @@ def test_product_never_imports_the_oracle():
             if f.endswith((".py", ".hip", ".hpp", ".cpp", ".h")):
                 txt = open(os.path.join(dirpath, f), errors="ignore").read()
                 assert "import oracle" not in txt and "liborc" not in txt and "mqr_oracle" not in txt, f
+
+
+def test_one_hip_runtime_per_process():
+    """libmqr first, torch second (the order that used to leave torch without a device): the process
+    maps exactly one libamdhip64 and one HSA runtime (mqr._lib preloads the copy torch ships)."""
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "from mqr import _lib; _lib.load()\n"
+            "import torch\n"
+            "m = {l.split()[-1] for l in open('/proc/self/maps') if 'amdhip64' in l or 'hsa-runtime64' in l}\n"
+            "print(len([p for p in m if 'amdhip64' in p]), len([p for p in m if 'hsa-runtime64' in p]))\n"
+            % os.path.join(ROOT, "metaquest-3d-reconstruction_amd"))
+    out = subprocess.check_output([sys.executable, "-c", code], text=True).split()
+    assert out == ["1", "1"], out

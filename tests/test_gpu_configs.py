@@ -1,0 +1,146 @@
+"""Parity at the BASELINE.json configurations' own sizes, GPU vs the CPU
+oracle on the same inputs:
+
+* C1: 32 x 640x480 procedural sphere, 2 cm voxels, R = 16, the 128^3 region (o3d_utils.py:153-238);
+* C2: 500 x 640x480 procedural room walk, 5 mm voxels, R = 16, trunc 10, depth_max 4 m;
+* C3: C2 + estimate_depth_confidences (r = 10, depth_max 4, err 0.08) -> mask (0.02 / 2) -> integrate
+  (estimate_depth_confidences.py:15-79, o3d_utils.py:109-150).
+
+Bar (north_star): identical touched-block sets and weights, |dtsdf| <= 1e-4 on w > 0 voxels
+(bit-exact in practice), identical marching-cubes vertex and triangle sets at the pipeline's mesh
+threshold 1.5 and the point-cloud default 3.0.  The oracle itself is parity-unpinned against Open3D
+(Open3D is absent offline); the confidence path is pinned by reference golden vectors.
+"""
+import numpy as np
+import pytest
+
+import oracle
+from gpu_helpers import compare_meshes, compare_volumes
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-4  # voxel TSDF tolerance, BASELINE.json north_star
+
+
+@pytest.fixture(scope="module")
+def vbg_mod():
+    import torch  # initialise torch's HIP first: the in-process runtime then serves both
+    assert torch.cuda.is_available()
+    from mqr import _lib
+    _lib.load()
+    import mqr.vbg
+    return mqr.vbg
+
+
+def _oracle_volume(depth, K, T, vs, R, dmax, tm, block_count=4096):
+    ref = oracle.OracleVBG(vs, R, block_count)
+    K = np.asarray(K, np.float64)
+    T = np.asarray(T, np.float64)
+    for i in range(len(depth)):
+        ref.integrate_frame(depth[i], K[i], T[i], 1.0, dmax, tm)
+    return ref
+
+
+def _check_mesh(vbg, ref, thr):
+    mesh = vbg.extract_triangle_mesh(weight_threshold=thr)
+    ov, _, ot = ref.extract_mesh(thr)
+    assert len(ot) > 1000
+    compare_meshes(mesh.vertices, mesh.triangles, ov, ot, pos_tol=0.0)
+    return len(ot)
+
+
+def test_c1_sphere_32_frames_2cm(vbg_mod):
+    """C1: 32 frames 640x480 on a 1.5 m ring around a r = 0.5 m sphere, 2 cm voxels (128^3 = 512
+    blocks of 16^3), noisy depth (sigma 0.002 z, 1 % dropout)."""
+    from mqr import synthetic
+    seq = synthetic.make_sequence("sphere", n=32, height=480, width=640, noise=True, seed=0)
+    vbg = vbg_mod.VoxelBlockGrid(voxel_size=0.02, block_resolution=16, block_count=512)
+    vbg.integrate_frames(seq["depth"], seq["K"], seq["T_wc"], depth_scale=1.0, depth_max=4.0,
+                         trunc_voxel_multiplier=10.0)
+    ref = _oracle_volume(seq["depth"], seq["K"], seq["T_wc"], 0.02, 16, 4.0, 10.0, 512)
+    keys = vbg.export_keys()
+    assert np.abs(keys).max() <= 4  # inside the 128^3 region around the sphere
+    assert compare_volumes(vbg.export(), ref.export(), TOL) == 0.0
+    for thr in (1.5, 3.0):
+        _check_mesh(vbg, ref, thr)
+
+
+@pytest.fixture(scope="module")
+def c2_seq(vbg_mod):
+    """The bench's C2 sequence (mqr.synthetic.make_sequence_fast, GPU ray cast) as host arrays."""
+    from mqr import synthetic
+    seq = synthetic.make_sequence_fast("room", n=500, height=480, width=640, seed=0, device="cuda:0")
+    seq["depth"] = seq.pop("depth_t").cpu().numpy()
+    return seq
+
+
+def test_c2_room_500_frames_5mm(vbg_mod, c2_seq):
+    seq = c2_seq
+    vbg = vbg_mod.VoxelBlockGrid(voxel_size=0.005, block_resolution=16, block_count=4096)  # grows
+    vbg.integrate_frames(seq["depth"], seq["K"], seq["T_wc"], depth_scale=1.0, depth_max=4.0,
+                         trunc_voxel_multiplier=10.0)
+    ref = _oracle_volume(seq["depth"], seq["K"], seq["T_wc"], 0.005, 16, 4.0, 10.0, 8192)
+    assert ref.size() > 5000
+    assert compare_volumes(vbg.export(), ref.export(), TOL) == 0.0
+    n15 = _check_mesh(vbg, ref, 1.5)
+    n30 = _check_mesh(vbg, ref, 3.0)
+    assert n15 >= n30 > 1_000_000
+
+
+def test_c3_confidence_mask_integrate(vbg_mod, c2_seq):
+    """C3: confidence of every frame (r = 10) on the GPU, checked against the oracle on reference
+    frames at both window edges and in the middle; then the masked sequence integrates
+    identically on both sides."""
+    from mqr.confidence import confidence_maps
+    seq = c2_seq
+    depth, K, Tcw = seq["depth"], seq["K"], seq["T_cw"]
+    Ti = np.linalg.inv(Tcw)
+    conf, valid = confidence_maps(depth, K, Tcw, Ti, 0, len(depth), 10, 4.0, 0.08)
+    for i in (0, 9, 10, 250, 490, 499):
+        oc, ov = oracle.confidence(depth, K, Tcw, Ti, i, 10, 4.0, 0.08)
+        assert np.array_equal(valid[i], ov), i
+        assert np.array_equal(conf[i], oc), i
+    masked = depth.copy()
+    masked[conf < 0.02] = 0.0  # o3d_utils.py:141-142 with the pipeline's thresholds
+    masked[valid < 2] = 0.0
+    assert 0.01 < (masked == 0).mean() < 0.9
+    vbg = vbg_mod.VoxelBlockGrid(voxel_size=0.005, block_resolution=16, block_count=8192)
+    vbg.integrate_frames(masked, K, seq["T_wc"], depth_scale=1.0, depth_max=4.0, trunc_voxel_multiplier=10.0)
+    ref = _oracle_volume(masked, K, seq["T_wc"], 0.005, 16, 4.0, 10.0, 8192)
+    assert compare_volumes(vbg.export(), ref.export(), TOL) == 0.0
+    _check_mesh(vbg, ref, 1.5)
+
+
+def test_empty_frame_mid_batch(vbg_mod):
+    """A frame that touches no block in the middle of a device batch: frames before it are
+    integrated, nothing of it or after it is (Open3D raises at that frame's touch)."""
+    from mqr import synthetic
+    seq = synthetic.make_sequence("sphere", n=12, height=120, width=160, f=131.25, noise=True, seed=3)
+    depth = seq["depth"].copy()
+    depth[7] = 0.0
+    K = seq["K"].astype(np.float64)
+    T = seq["T_wc"].astype(np.float64)
+    vbg = vbg_mod.VoxelBlockGrid(voxel_size=0.02, block_resolution=16, block_count=64)
+    vbg.integrate_frames(depth[:3], K[:3], T[:3], depth_scale=1.0, depth_max=3.0, trunc_voxel_multiplier=4.0)
+    with pytest.raises(RuntimeError, match="No block is touched"):
+        vbg.integrate_frames(depth[3:], K[3:], T[3:], depth_scale=1.0, depth_max=3.0, trunc_voxel_multiplier=4.0)
+    ref = _oracle_volume(depth[:7], K[:7], T[:7], 0.02, 16, 3.0, 4.0, 64)
+    assert vbg.size() == ref.size()
+    assert compare_volumes(vbg.export(), ref.export(), 0.0) == 0.0
+    # the volume stays usable: the remaining frames continue it exactly
+    vbg.integrate_frames(depth[8:], K[8:], T[8:], depth_scale=1.0, depth_max=3.0, trunc_voxel_multiplier=4.0)
+    for i in range(8, 12):
+        ref.integrate_frame(depth[i], K[i], T[i], 1.0, 3.0, 4.0)
+    assert compare_volumes(vbg.export(), ref.export(), 0.0) == 0.0
+
+
+def test_empty_first_frame_of_batch(vbg_mod):
+    from mqr import synthetic
+    seq = synthetic.make_sequence("sphere", n=4, height=120, width=160, f=131.25, noise=False, seed=3)
+    depth = seq["depth"].copy()
+    depth[0] = 0.0
+    vbg = vbg_mod.VoxelBlockGrid(voxel_size=0.02, block_resolution=16, block_count=64)
+    with pytest.raises(RuntimeError, match="No block is touched"):
+        vbg.integrate_frames(depth, seq["K"], seq["T_wc"], depth_scale=1.0, depth_max=3.0,
+                             trunc_voxel_multiplier=4.0)
+    assert vbg.size() == 0
