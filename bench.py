@@ -58,8 +58,13 @@ def parse():
     ap.add_argument("--no-parity", action="store_true", help="skip the oracle comparison of the timed volume")
     ap.add_argument("--conf-cpu-seconds", type=float, default=10.0, help="bounded CPU sample of the confidence oracle")
     ap.add_argument("--e2e-frames", type=int, default=500, help="frames of the on-disk C3 capture (0: skip the leg)")
-    ap.add_argument("--merge", default="sparse", choices=["sparse", "reduce"],
-                    help="N>1 volume merge: all-to-all to union-slice owners + gather, or one dense reduce")
+    ap.add_argument("--merge", default="sharded", choices=["sharded", "root"],
+                    help="N>1 volume merge inside libmqr over RCCL (mqr_reduce_rccl): owned slice + halo per "
+                         "rank, or the whole volume on rank 0")
+    ap.add_argument("--strong", action="store_true",
+                    help="C4: a fixed 2000-frame LEFT+RIGHT capture (1000 + 1000, stereo baseline 0.064 m) "
+                         "split over the ranks (strong scaling) instead of 500 frames per rank")
+    ap.add_argument("--strong-frames", type=int, default=1000, help="frames per side in --strong mode")
     return ap.parse_args()
 
 
@@ -462,18 +467,29 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", 0))
     import numpy as np
     import torch
+    if os.environ.get("MQR_BENCH_WRAP_DEVICES"):  # rehearsal on fewer GPUs than ranks
+        local %= torch.cuda.device_count()
     torch.cuda.set_device(local)
-    dist = None
+    dist = comm = None
     if world > 1:
+        # control plane only (barriers, the RCCL id, max-over-ranks timing); volume data moves over
+        # RCCL inside libmqr_hip.so (mqr_reduce_rccl)
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist.init_process_group("gloo")
 
     from mqr import synthetic
-    from mqr.distributed import merge_to_root
+    from mqr.distributed import make_comm, merge_rccl, shard_range
     from mqr.vbg import VoxelBlockGrid
 
-    # this rank's frames of an N*frames closed walk through the room
-    poses = synthetic.room_loop_poses(args.frames * world)[rank * args.frames:(rank + 1) * args.frames]
+    if args.strong:
+        # C4: LEFT then RIGHT (reconstruct_scene.py:64-81 order), contiguous frame ranges per rank
+        left = synthetic.room_loop_poses(args.strong_frames)
+        right = [(R_, t_ + R_[:, 0] * 0.064) for R_, t_ in left]
+        lo, hi = shard_range(2 * args.strong_frames, rank, world)
+        poses = (left + right)[lo:hi]
+    else:
+        # this rank's frames of an N*frames closed walk through the room (weak scaling)
+        poses = synthetic.room_loop_poses(args.frames * world)[rank * args.frames:(rank + 1) * args.frames]
     seq = synthetic.make_sequence_fast("room", poses=poses, height=args.height, width=args.width, seed=rank,
                                        device=f"cuda:{local}")
     depth_t = seq["depth_t"].contiguous()
@@ -487,6 +503,11 @@ def main():
                          block_count=args.block_count, device=local)
 
     merge_times = []
+    shard = {"out": None, "owned": 0}
+    if world > 1:
+        comm = make_comm(local)
+        shard["out"] = VoxelBlockGrid(voxel_size=args.voxel, block_resolution=args.block_resolution,
+                                      block_count=args.block_count, device=local)
 
     def step_integrate():
         vbg.reset()
@@ -497,7 +518,7 @@ def main():
         step_integrate()
         if world > 1:
             t = time.perf_counter()
-            merge_to_root(vbg, method=args.merge)
+            shard["out"], shard["owned"] = merge_rccl(vbg, comm, mode=args.merge, out=shard["out"])
             torch.cuda.synchronize()
             merge_times.append(time.perf_counter() - t)
 
@@ -519,14 +540,33 @@ def main():
     vbg.profile(False)
     st = vbg.stats(reset=True)
     if dist:
-        e = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        e = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
 
     blocks = vbg.size()
     R3_ = args.block_resolution ** 3
     ext_ms, (nv, nt) = (None, (0, 0))
-    if rank == 0:
+    sharded = None
+    if world > 1:
+        # every rank extracts its owned cubes (mqr_extract_mesh_owned); the mesh is the concatenation
+        from mqr.distributed import extract_mesh_owned
+        dist.barrier()
+        t = time.perf_counter()
+        m = extract_mesh_owned(shard["out"], shard["owned"], args.extract_threshold)
+        tx = time.perf_counter() - t
+        stats = torch.tensor([tx, len(m.triangles), len(m.vertices), shard["owned"]], dtype=torch.float64)
+        allst = [torch.zeros_like(stats) for _ in range(world)]
+        dist.all_gather(allst, stats)
+        allst = torch.stack(allst)
+        sharded = {"mode": args.merge, "extract_ms_max": float(allst[:, 0].max()) * 1e3,
+                   "triangles": int(allst[:, 1].sum()), "vertices_with_boundary_copies": int(allst[:, 2].sum()),
+                   "union_blocks": int(allst[:, 3].sum()) if args.merge == "sharded" else int(allst[0, 3]),
+                   "note": "per-rank owned-cube extraction of the merged shard (host copy of the shard mesh "
+                           "included); triangles add up to the single-volume mesh"}
+        blocks = sharded["union_blocks"]
+        nt = sharded["triangles"]
+    elif rank == 0:
         ext_ms, (nv, nt) = extract_ms(vbg, args.extract_threshold, args.extract_reps)
 
     R3 = args.block_resolution ** 3
@@ -576,7 +616,7 @@ def main():
     traffic, traffic_src = pmc_traffic(H, W, B)
 
     if rank == 0:
-        total_frames = B * world * args.steps
+        total_frames = (2 * args.strong_frames if args.strong else B * world) * args.steps
         out = {
             "metric": METRIC,
             "value": total_frames / elapsed,
@@ -586,18 +626,22 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.strong else "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (procedural room, GPU ray-cast, sigma=0.002z noise + 1% dropout)",
-            "config": {"workload": "C2 (SURVEY.md §8(d); BASELINE.json configs[1]): 500-frame LEFT depth sequence "
-                                   "per GPU, 640x480, hashed TSDF 5 mm voxels, 512^3 effective volume, R=16, "
-                                   "depth_max 4 m, trunc 10",
+            "config": {"workload": ("C4 (SURVEY.md §8(d); BASELINE.json configs[3]): 2000-frame LEFT+RIGHT capture "
+                                    "split over the GPUs, 640x480, 5 mm voxels, R=16, depth_max 4 m, trunc 10, merged "
+                                    "over RCCL") if args.strong else
+                                   ("C2 (SURVEY.md §8(d); BASELINE.json configs[1]): 500-frame LEFT depth sequence "
+                                    "per GPU, 640x480, hashed TSDF 5 mm voxels, 512^3 effective volume, R=16, "
+                                    "depth_max 4 m, trunc 10"),
                        "frames_per_gpu": B, "height": H, "width": W, "voxel_size": args.voxel,
                        "block_resolution": args.block_resolution, "depth_max": args.depth_max,
                        "trunc_voxel_multiplier": args.trunc, "frame_batch": 64,
                        "parallelism": f"frame-shard x{world}" + (
-                           f" + RCCL merge ({args.merge})" if world > 1 else "")},
+                           f" + libmqr RCCL merge ({args.merge})" if world > 1 else "")},
+            "sharded_extract": sharded,
             "merge_ms": (sum(merge_times) / len(merge_times) * 1e3) if merge_times else None,
             "union_blocks": blocks if world > 1 else None,
             "extract_ms": ext_ms,
@@ -625,6 +669,8 @@ def main():
             "dropin_e2e": extras.get("dropin_e2e"),
         }
         print(json.dumps(out), flush=True)
+    if comm is not None:
+        comm.close()
     if dist:
         dist.destroy_process_group()
 

@@ -29,6 +29,7 @@ extern "C" {
 typedef struct mqr_vbg mqr_vbg;    /* voxel-block-hashed TSDF volume resident in HBM */
 typedef struct mqr_geom mqr_geom;  /* extracted point cloud or triangle mesh (device-resident) */
 typedef struct mqr_scene mqr_scene;  /* triangle-mesh ray-casting scene (device BVH) */
+typedef struct mqr_comm mqr_comm;    /* RCCL communicator of one rank (one process per GPU) */
 
 int mqr_version(void);
 const char* mqr_last_error(void);
@@ -84,10 +85,36 @@ int mqr_vbg_import(mqr_vbg* v, const int32_t* keys, const float* tsdf, const flo
 int mqr_vbg_pack_weighted(mqr_vbg* v, const int32_t* union_keys, int64_t U, float* packed);
 int mqr_vbg_unpack_weighted(mqr_vbg* v, const int32_t* union_keys, int64_t U, const float* packed);
 
+/* The single exchange step of frame-sharded fusion (SURVEY §8(b) mqr_reduce_rccl, §8(e)); the
+ * reference has no distributed path -- this replaces running its integrate() loop
+ * (o3d_utils.py:153-238) over all frames in one process.  One process per GPU: rank 0 makes an id
+ * (mqr_comm_unique_id), the caller distributes it (e.g. a gloo / TCP store), every rank calls
+ * mqr_comm_init.  RCCL (librccl.so.1) is resolved at run time.
+ * mqr_reduce_rccl merges every rank's `local` volume into `out` (emptied first):
+ *   MQR_MERGE_ROOT     `out` on `root` holds the whole merged volume (others: empty);
+ *   MQR_MERGE_SHARDED  `out` holds this rank's owned slice of the sorted block union first
+ *                      (*n_owned blocks), then the one-block halo; extract it with
+ *                      mqr_extract_mesh_owned(out, thr, *n_owned): shard meshes concatenate to the
+ *                      single-volume mesh (triangle counts add exactly).
+ * Voxels seen by one rank keep its (tsdf, weight) bit for bit; others merge in rank order:
+ * tsdf = (w_a tsdf_a + w_b tsdf_b) / (w_a + w_b), weight = w_a + w_b.
+ * mqr_merge_local: the same plan and arithmetic for n volumes of one process (device copies
+ * instead of RCCL; tests and single-node fallbacks). */
+#define MQR_MERGE_ROOT 0
+#define MQR_MERGE_SHARDED 1
+int mqr_comm_unique_id(uint8_t* id_out /* 128 bytes */);
+int mqr_comm_init(int device, int rank, int world, const uint8_t* id /* 128 bytes */, mqr_comm** out);
+int mqr_comm_destroy(mqr_comm* comm);
+int mqr_reduce_rccl(mqr_vbg* local, mqr_comm* comm, int mode, int root, mqr_vbg* out, int64_t* n_owned);
+int mqr_merge_local(mqr_vbg** locals, int n, int mode, int root, mqr_vbg** outs, int64_t* n_owned);
+
 /* vbg.extract_point_cloud(weight_threshold=3.0)   -- reconstruct_scene.py:90, refine_fragment_poses.py:39
  * vbg.extract_triangle_mesh(weight_threshold)       -- reconstruct_scene.py:105-108, 186-189 */
 int mqr_extract_points(mqr_vbg* v, float weight_threshold, mqr_geom** out);
 int mqr_extract_mesh(mqr_vbg* v, float weight_threshold, mqr_geom** out);
+/* Triangles only of cubes whose origin voxel lies in blocks [0, n_owned) (a shard from
+ * mqr_reduce_rccl MQR_MERGE_SHARDED); vertices of every block (unreferenced ones may remain). */
+int mqr_extract_mesh_owned(mqr_vbg* v, float weight_threshold, int64_t n_owned, mqr_geom** out);
 int mqr_geom_counts(mqr_geom* g, int64_t* n_vertices, int64_t* n_triangles);
 /* Copy to caller buffers (positions / normals n*3 float32, triangles n*3 int32); NULL skips. */
 int mqr_geom_copy(mqr_geom* g, float* positions, float* normals, int32_t* triangles, int loc);

@@ -595,7 +595,8 @@ __device__ inline int mc_row_tris(const uint32_t* rowN, uint32_t oc, int y, int 
 // which the emit pass of this block and of its -x / -y / -z neighbours read.
 template <int R>
 __global__ __launch_bounds__(kThreads) void k_mc_count(const int32_t* __restrict__ nb, const float2* __restrict__ pool,
-                                                       float thr, int32_t* vcount, int32_t* tcount, uint2* rowinfo) {
+                                                       float thr, int64_t tri_blocks, int32_t* vcount,
+                                                       int32_t* tcount, uint2* rowinfo) {
     using M = Mc<R, 1>;
     __shared__ uint32_t rowV[M::S2], rowN[M::S2], cs[M::C2];
     __shared__ int32_t nbrow[27];
@@ -611,6 +612,7 @@ __global__ __launch_bounds__(kThreads) void k_mc_count(const int32_t* __restrict
     int nv = 0, nt = 0;
     if (r < M::R2) {
         e = mc_row<M>(rowN, cs, r % R, r / R);
+        if (b >= tri_blocks) e.oc = 0;  // halo block of a shard: its vertices, none of its cubes
         nv = __popc(e.ex) + __popc(e.ey) + __popc(e.ez);
         nt = mc_row_tris<M>(rowN, e.oc, r % R, r / R);
     }
@@ -644,7 +646,7 @@ __device__ inline int32_t mc_vid(uint32_t vbase, uint32_t ex, uint32_t ey, uint3
 template <int R>
 __global__ __launch_bounds__(kThreads) void k_mc_emit(const int32_t* __restrict__ nb, const uint64_t* __restrict__ bkeys,
                                                       const float2* __restrict__ pool, float voxel_size, float thr,
-                                                      const int32_t* __restrict__ vcount,
+                                                      int64_t tri_blocks, const int32_t* __restrict__ vcount,
                                                       const int32_t* __restrict__ tcount,
                                                       const int32_t* __restrict__ voff,
                                                       const int32_t* __restrict__ toff,
@@ -676,6 +678,7 @@ __global__ __launch_bounds__(kThreads) void k_mc_emit(const int32_t* __restrict_
     uint32_t vbase = 0;
     if (r < M::R2) {
         e = mc_row<M>(rowN, cs, r % R, r / R);
+        if (b >= tri_blocks) e.oc = 0;
         nt = mc_row_tris<M>(rowN, e.oc, r % R, r / R);
         vbase = rowinfo[b * M::R2 + r].x & 0xffffu;
     }
@@ -972,12 +975,12 @@ static int build_nb(mqr_vbg* v, int32_t* nb) {
 }
 
 template <int RT>
-static int mesh_passes(mqr_vbg* v, float thr, const ExScratch& e, mqr_geom* g) {
+static int mesh_passes(mqr_vbg* v, float thr, const ExScratch& e, mqr_geom* g, int64_t tri_blocks) {
     const int64_t n = v->pool_count;
     uint2* rowinfo = reinterpret_cast<uint2*>(e.faces);  // R^2 uint2 per block fit in the 3 R^2 u32 faces slot
     if constexpr (RT > 0)
-        hipLaunchKernelGGL(k_mc_count<RT>, dim3((unsigned)n), dim3(kThreads), 0, v->stream, e.nb, v->pool, thr, e.c0,
-                           e.c1, rowinfo);
+        hipLaunchKernelGGL(k_mc_count<RT>, dim3((unsigned)n), dim3(kThreads), 0, v->stream, e.nb, v->pool, thr,
+                           tri_blocks, e.c0, e.c1, rowinfo);
     else
         hipLaunchKernelGGL(k_mesh_count<RT>, dim3((unsigned)n), dim3(kThreads), 0, v->stream, e.nb, n, v->pool, v->R,
                            thr, e.c0, e.c1, e.faces);
@@ -990,7 +993,7 @@ static int mesh_passes(mqr_vbg* v, float thr, const ExScratch& e, mqr_geom* g) {
     if (alloc_geom(g, nv, nt)) return 1;
     if constexpr (RT > 0)
         hipLaunchKernelGGL(k_mc_emit<RT>, dim3((unsigned)n), dim3(kThreads), 0, v->stream, e.nb, v->bkeys, v->pool,
-                           v->voxel_size, thr, e.c0, e.c1, e.o0, e.o1, rowinfo, g->pos, g->nrm, g->tri);
+                           v->voxel_size, thr, tri_blocks, e.c0, e.c1, e.o0, e.o1, rowinfo, g->pos, g->nrm, g->tri);
     else
         hipLaunchKernelGGL(k_mesh_emit<RT>, dim3((unsigned)n), dim3(kThreads), 0, v->stream, e.nb, n, v->bkeys,
                            v->pool, v->R, v->voxel_size, thr, e.c0, e.c1, e.o0, e.o1, e.faces, g->pos, g->nrm, g->tri);
@@ -1023,9 +1026,13 @@ using namespace mqr;
 
 extern "C" {
 
-int mqr_extract_mesh(mqr_vbg* v, float thr, mqr_geom** out) {
+int mqr_extract_mesh(mqr_vbg* v, float thr, mqr_geom** out) { return mqr_extract_mesh_owned(v, thr, -1, out); }
+
+int mqr_extract_mesh_owned(mqr_vbg* v, float thr, int64_t n_owned, mqr_geom** out) {
     MQR_REQUIRE(v && out, "null argument");
     MQR_REQUIRE(v->R <= kMaxR, "extract_triangle_mesh supports block_resolution <= 16");
+    MQR_REQUIRE(n_owned < 0 || v->R == 16 || v->R == 8, "owned-block extraction supports block_resolution 8 / 16");
+    const int64_t tri_blocks = n_owned < 0 ? INT64_MAX : n_owned;
     MQR_CHECK_HIP(hipSetDevice(v->device));
     if (sync_all(v)) return 1;  // an integrate may still be running on the second stream
     const int64_t n = v->pool_count;
@@ -1036,8 +1043,9 @@ int mqr_extract_mesh(mqr_vbg* v, float thr, mqr_geom** out) {
     if (n > 0) {
         ExScratch e{};
         rc = ex_scratch(v, n, true, e) || build_nb(v, e.nb);
-        if (!rc) rc = v->R == 16 ? mesh_passes<16>(v, thr, e, g) : v->R == 8 ? mesh_passes<8>(v, thr, e, g)
-                                                                          : mesh_passes<0>(v, thr, e, g);
+        if (!rc) rc = v->R == 16 ? mesh_passes<16>(v, thr, e, g, tri_blocks)
+                      : v->R == 8 ? mesh_passes<8>(v, thr, e, g, tri_blocks)
+                                  : mesh_passes<0>(v, thr, e, g, tri_blocks);
     }
     if (rc) {  // release whatever the failed passes allocated; the caller gets no handle
         const std::string msg = get_error();

@@ -185,4 +185,5 @@ void* geom_block_alloc(int device, size_t bytes, size_t* cap);
 void geom_block_release(int device, void* p, size_t cap);
 int grow_pool(mqr_vbg* v, int64_t need);
 int sync_all(mqr_vbg* v);
+int activate_ordered(mqr_vbg* v, const uint64_t* dkeys, int64_t n);  // empty volume, buffer i = key i
 }  // namespace mqr

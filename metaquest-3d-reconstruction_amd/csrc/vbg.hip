@@ -469,6 +469,27 @@ static void drain_events(mqr_vbg* v) {
     v->ev_used = 0;
 }
 
+// Fill an EMPTY volume with `n` distinct packed keys (device), buffer i = keys[i], pool counter n.
+int activate_ordered(mqr_vbg* v, const uint64_t* dkeys, int64_t n) {
+    if (v->pool_count != 0) {
+        set_error("internal: ordered activation needs an empty volume");
+        return 1;
+    }
+    if (n == 0) return 0;
+    if (sync_all(v) || ensure_table(v, n) || grow_pool(v, n) || reset_batch_counters(v, 0)) return 1;
+    hipLaunchKernelGGL(k_activate_ordered, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, v->stream, dkeys, n,
+                       v->tab, v->bkeys, v->ctr(0));
+    hipLaunchKernelGGL(k_set_counter, dim3(1), dim3(1), 0, v->stream, v->pool_ctr(), (int)n);
+    MQR_CHECK_HIP(hipGetLastError());
+    if (read_counters(v, 0)) return 1;
+    if (v->hctr(0)[kOverflow] & 2) {
+        set_error("internal: block table full");
+        return 1;
+    }
+    v->pool_count = n;
+    return 0;
+}
+
 static int touch_launch(mqr_vbg* v, int p, const float* dbase, int64_t HW, int H, int W, int b, float depth_scale,
                         float depth_max, float sdf_trunc, float block_size, const Table& t, int alloc) {
     const int n = (H / 4) * (W / 4);

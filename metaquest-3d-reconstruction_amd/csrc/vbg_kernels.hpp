@@ -1349,6 +1349,28 @@ __global__ void k_rollback(Table t, int first_buf) {
     }
 }
 
+// Insert packed keys with buffer index = position (an empty volume filled in a chosen order: the
+// multi-GPU merge places owned blocks first).  Keys are distinct.
+__global__ void k_activate_ordered(const uint64_t* __restrict__ keys, int64_t n, Table t, uint64_t* bkeys,
+                                   int* counters) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t k = keys[i];
+    const uint64_t m = (uint64_t)t.cap - 1;
+    uint64_t h = mix64(k) & m;
+    for (int64_t p = 0; p < t.cap; ++p) {
+        const uint64_t old = atomicCAS((unsigned long long*)&t.keys[h], (unsigned long long)kEmpty,
+                                       (unsigned long long)k);
+        if (old == kEmpty) {
+            t.vals[h] = (int32_t)i;
+            bkeys[i] = k;
+            return;
+        }
+        h = (h + 1) & m;
+    }
+    atomicOr(&counters[kOverflow], 2);
+}
+
 __global__ void k_gather_keys(const int32_t* __restrict__ list, int64_t n, const Table t, int32_t* keys_out) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;

@@ -57,6 +57,13 @@ SIGNATURES = {
     "mqr_vbg_unpack_weighted": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp]),
     "mqr_extract_points": (ctypes.c_int, [_vp, ctypes.c_float, ctypes.POINTER(_vp)]),
     "mqr_extract_mesh": (ctypes.c_int, [_vp, ctypes.c_float, ctypes.POINTER(_vp)]),
+    "mqr_extract_mesh_owned": (ctypes.c_int, [_vp, ctypes.c_float, ctypes.c_int64, ctypes.POINTER(_vp)]),
+    "mqr_comm_unique_id": (ctypes.c_int, [_u8p]),
+    "mqr_comm_init": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, _u8p, ctypes.POINTER(_vp)]),
+    "mqr_comm_destroy": (ctypes.c_int, [_vp]),
+    "mqr_reduce_rccl": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_int, _vp, _i64p]),
+    "mqr_merge_local": (ctypes.c_int, [ctypes.POINTER(_vp), ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                       ctypes.POINTER(_vp), _i64p]),
     "mqr_geom_counts": (ctypes.c_int, [_vp, _i64p, _i64p]),
     "mqr_geom_copy": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_int]),
     "mqr_geom_free": (ctypes.c_int, [_vp]),
@@ -110,12 +117,35 @@ def hip_runtime_path():
     env = os.environ.get("MQR_HIP_RUNTIME")
     if env:
         return env
+    return _torch_lib("libamdhip64.so")
+
+
+def _torch_lib(name: str):
     import importlib.util
     spec = importlib.util.find_spec("torch")
     if spec is None or not spec.origin:
         return None
-    p = os.path.join(os.path.dirname(spec.origin), "lib", "libamdhip64.so")
+    p = os.path.join(os.path.dirname(spec.origin), "lib", name)
     return p if os.path.exists(p) else None
+
+
+_rccl_loaded = False
+
+
+def preload_rccl():
+    """Bring in the RCCL that torch links (when torch is installed) before libmqr resolves
+    librccl.so.1 at run time: torch links it by file name, so a copy from /opt/rocm mapped first
+    would be followed by a second RCCL (and ROCm SMI) instance.  It has to come in through
+    ``import torch`` itself -- mapping torch's librccl.so by hand before torch's own libraries
+    leaves the process with a double free at exit.  MQR_RCCL names another library instead."""
+    global _rccl_loaded
+    if _rccl_loaded:
+        return
+    if os.environ.get("MQR_RCCL"):
+        ctypes.CDLL(os.environ["MQR_RCCL"], mode=ctypes.RTLD_GLOBAL)
+    elif _torch_lib("librccl.so"):
+        import torch  # noqa: F401
+    _rccl_loaded = True
 
 
 def load(path: str = LIB_PATH):

@@ -14,6 +14,12 @@ volumes exactly (up to fp32 rounding), because the reference's unit-weight runni
 Only step 4 moves volume data (U * R^3 * 8 bytes).  The collective calls go through
 ``torch.distributed`` (backend "nccl" is RCCL on ROCm; "gloo" for the CPU tests), everything
 volumetric goes through libmqr_hip.so.
+
+The production path is ``merge_rccl``: the whole exchange inside libmqr_hip.so (mqr_reduce_rccl,
+RCCL resolved at run time, one sparse grouped send/recv of the blocks each rank owns or needs as
+halo), with ``torch.distributed`` (any backend, gloo is enough) only handing the RCCL id around.
+``merge_local`` runs the same plan and kernels for several volumes of one process (tests on one
+GPU), and ``extract_mesh_owned`` extracts a shard's mesh (its owned cubes only).
 """
 from __future__ import annotations
 
@@ -167,3 +173,105 @@ def _merge_sparse(vbg, group, root):
         if on_device:
             torch.cuda.synchronize(vdev)
     return U
+
+
+# ---------------------------------------------------------------- libmqr RCCL path
+MERGE_MODES = {"root": 0, "sharded": 1}
+
+
+class RcclComm:
+    """One rank's RCCL communicator inside libmqr_hip.so (mqr_comm_init)."""
+
+    def __init__(self, device: int, rank: int, world: int, uid: bytes):
+        import ctypes
+        from . import _lib
+        _lib.preload_rccl()
+        buf = (ctypes.c_uint8 * 128).from_buffer_copy(bytes(uid))
+        h = ctypes.c_void_p()
+        _lib.call("mqr_comm_init", int(device), int(rank), int(world), buf, ctypes.byref(h))
+        self._h, self.device, self.rank, self.world = h, int(device), int(rank), int(world)
+
+    @staticmethod
+    def unique_id() -> bytes:
+        import ctypes
+        from . import _lib
+        _lib.preload_rccl()
+        buf = (ctypes.c_uint8 * 128)()
+        _lib.call("mqr_comm_unique_id", buf)
+        return bytes(buf)
+
+    def close(self):
+        from . import _lib
+        if getattr(self, "_h", None) is not None and self._h.value and _lib._lib is not None:
+            _lib._lib.mqr_comm_destroy(self._h)
+        self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def make_comm(device: int, group=None) -> RcclComm:
+    """Rank 0 makes the RCCL id; torch.distributed (any backend) broadcasts it; every rank inits."""
+    import torch.distributed as dist
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    obj = [RcclComm.unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0, group=group)
+    return RcclComm(device, rank, world, obj[0])
+
+
+def _empty_like(vbg):
+    from .vbg import VoxelBlockGrid
+    return VoxelBlockGrid(voxel_size=vbg.voxel_size, block_resolution=vbg.block_resolution, block_count=1,
+                          device=vbg.device_id)
+
+
+def merge_rccl(vbg, comm: RcclComm, mode: str = "sharded", root: int = 0, out=None):
+    """mqr_reduce_rccl: returns (out volume, owned block count).  mode "root": rank `root`'s out
+    holds the merged volume; "sharded": every out holds its owned union slice first, then halo."""
+    import ctypes
+    from . import _lib
+    out = out if out is not None else _empty_like(vbg)
+    n = ctypes.c_int64()
+    _lib.call("mqr_reduce_rccl", vbg.handle, comm._h, MERGE_MODES[mode], int(root), out.handle, ctypes.byref(n))
+    return out, n.value
+
+
+def merge_local(vbgs, mode: str = "sharded", root: int = 0, outs=None):
+    """The merge of several volumes of one process (same plan and kernels, device copies instead
+    of RCCL).  Returns [(out volume, owned block count)] per input."""
+    import ctypes
+    from . import _lib
+    n = len(vbgs)
+    outs = outs if outs is not None else [_empty_like(v) for v in vbgs]
+    arr = (ctypes.c_void_p * n)(*[v.handle.value for v in vbgs])
+    oarr = (ctypes.c_void_p * n)(*[o.handle.value for o in outs])
+    owned = np.zeros(n, np.int64)
+    _lib.call("mqr_merge_local", arr, n, MERGE_MODES[mode], int(root), oarr, _lib.ptr(owned, _lib._i64p))
+    return list(zip(outs, owned.tolist()))
+
+
+def extract_mesh_owned(vbg, n_owned: int, weight_threshold: float = 1.5):
+    """A shard's mesh: triangles of the cubes whose origin lies in its owned blocks, the vertices
+    they reference (re-indexed; vertices on the shard boundary also appear in the neighbour's mesh)."""
+    import ctypes
+    from . import _lib
+    from ._lib import MQR_HOST, call, ptr
+    from .geometry import TriangleMesh
+    g = ctypes.c_void_p()
+    call("mqr_extract_mesh_owned", vbg.handle, float(weight_threshold), int(n_owned), ctypes.byref(g))
+    try:
+        nv, nt = ctypes.c_int64(), ctypes.c_int64()
+        call("mqr_geom_counts", g, ctypes.byref(nv), ctypes.byref(nt))
+        pos = np.empty((nv.value, 3), np.float32)
+        nrm = np.empty((nv.value, 3), np.float32)
+        tri = np.empty((nt.value, 3), np.int32)
+        call("mqr_geom_copy", g, ptr(pos), ptr(nrm), ptr(tri) if nt.value else None, MQR_HOST)
+    finally:
+        _lib._lib.mqr_geom_free(g)
+    used = np.zeros(len(pos), bool)
+    used[tri.reshape(-1)] = True
+    remap = np.cumsum(used) - 1
+    return TriangleMesh(pos[used], nrm[used], remap[tri].astype(np.int32), device=vbg.device)

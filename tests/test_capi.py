@@ -50,14 +50,17 @@ def test_product_never_imports_the_oracle():
 
 def test_one_hip_runtime_per_process():
     """libmqr first, torch second (the order that used to leave torch without a device): the process
-    maps exactly one libamdhip64 and one HSA runtime (mqr._lib preloads the copy torch ships)."""
+    maps exactly one libamdhip64, one HSA runtime and one RCCL (mqr._lib preloads the copies torch
+    ships)."""
     import subprocess
     import sys
     code = ("import sys; sys.path.insert(0, %r)\n"
-            "from mqr import _lib; _lib.load()\n"
+            "from mqr import _lib; _lib.load(); _lib.preload_rccl()\n"
+            "import ctypes; ctypes.CDLL('librccl.so.1')\n"  # what libmqr's mqr_comm_* resolve at run time
             "import torch\n"
-            "m = {l.split()[-1] for l in open('/proc/self/maps') if 'amdhip64' in l or 'hsa-runtime64' in l}\n"
-            "print(len([p for p in m if 'amdhip64' in p]), len([p for p in m if 'hsa-runtime64' in p]))\n"
+            "m = {l.split()[-1] for l in open('/proc/self/maps') if 'amdhip64' in l or 'hsa-runtime64' in l\n"
+            "     or 'rccl' in l}\n"
+            "print(*[len([p for p in m if s in p]) for s in ('amdhip64', 'hsa-runtime64', 'rccl')])\n"
             % os.path.join(ROOT, "metaquest-3d-reconstruction_amd"))
     out = subprocess.check_output([sys.executable, "-c", code], text=True).split()
-    assert out == ["1", "1"], out
+    assert out == ["1", "1", "1"], out

@@ -1,0 +1,186 @@
+"""Multi-GPU merge in libmqr (mqr_reduce_rccl / mqr_merge_local) on one device.
+
+* root mode: N frame shards merged into one volume == one sequential pass (identical keys and
+  weights, |dtsdf| <= 1e-4; voxels one shard saw alone are that shard's values bit for bit);
+* sharded mode: every rank's owned slice + one-block halo; the shard meshes (owned cubes only)
+  concatenate to exactly the merged volume's mesh (same triangle set, counts add up);
+* RCCL itself at world size 1 (one GPU on the test box); world size 2 over RCCL when >= 2 GPUs
+  are visible (skipped otherwise -- the driver's 8-GPU node runs bench.py --gpus N).
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+from gpu_helpers import canon_triangles, canon_vertices, compare_meshes, compare_volumes
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-4
+
+
+@pytest.fixture(scope="module")
+def seq():
+    from mqr import _lib, synthetic
+    _lib.load()
+    return synthetic.make_sequence("room", n=36, height=240, width=320, f=262.5, noise=True, seed=12)
+
+
+def _shards(seq, world, R=16, vs=0.01):
+    from mqr.distributed import shard_range
+    from mqr.vbg import VoxelBlockGrid
+    vols = []
+    n = len(seq["K"])
+    for r in range(world):
+        lo, hi = shard_range(n, r, world)
+        v = VoxelBlockGrid(voxel_size=vs, block_resolution=R, block_count=64)
+        v.integrate_frames(seq["depth"][lo:hi], seq["K"][lo:hi], seq["T_wc"][lo:hi], depth_scale=1.0,
+                           depth_max=4.0, trunc_voxel_multiplier=10.0)
+        vols.append(v)
+    return vols
+
+
+def _oracle(seq, R=16, vs=0.01):
+    ref = oracle.OracleVBG(vs, R, 256)
+    for i in range(len(seq["K"])):
+        ref.integrate_frame(seq["depth"][i], seq["K"][i].astype(np.float64), seq["T_wc"][i].astype(np.float64),
+                            1.0, 4.0, 10.0)
+    return ref
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_root_merge_matches_single_pass(seq, world):
+    from mqr.distributed import merge_local
+    vols = _shards(seq, world)
+    res = merge_local(vols, mode="root", root=world - 1)
+    merged, n_owned = res[world - 1]
+    assert n_owned == merged.size()
+    for r, (o, n) in enumerate(res):
+        if r != world - 1:
+            assert o.size() == 0 and n == 0
+    err = compare_volumes(merged.export(), _oracle(seq).export(), TOL)
+    assert err < 1e-5
+    # a voxel that only the first shard saw keeps that shard's values exactly
+    k0, t0, w0 = vols[0].export()
+    km, tm, wm = merged.export()
+    pos = {tuple(k): i for i, k in enumerate(km)}
+    others = [dict(zip(map(tuple, v.export()[0]), v.export()[2])) for v in vols[1:]]
+    for b in range(len(k0)):
+        wo = sum(o[tuple(k0[b])] if tuple(k0[b]) in o else 0 for o in others)
+        alone = (w0[b] > 0) & (np.asarray(wo) == 0)
+        j = pos[tuple(k0[b])]
+        assert np.array_equal(tm[j][alone], t0[b][alone]) and np.array_equal(wm[j][alone], w0[b][alone])
+
+
+@pytest.mark.parametrize("world,R", [(2, 16), (3, 16), (4, 8)])
+def test_sharded_meshes_concatenate_to_the_merged_mesh(seq, world, R):
+    from mqr.distributed import extract_mesh_owned, merge_local
+    vols = _shards(seq, world, R=R)
+    root = merge_local(vols, mode="root", root=0)[0][0]
+    full = root.extract_triangle_mesh(weight_threshold=1.5)
+    shards = merge_local(vols, mode="sharded")
+    owned_keys = []
+    verts, tris, nt = [], [], 0
+    off = 0
+    for out, n_owned in shards:
+        k = out.export()[0]
+        owned_keys.append(k[:n_owned])
+        m = extract_mesh_owned(out, n_owned, 1.5)
+        verts.append(m.vertices)
+        tris.append(m.triangles + off)
+        off += len(m.vertices)
+        nt += len(m.triangles)
+    allk = np.concatenate(owned_keys)
+    assert len(allk) == root.size() and len(np.unique(allk, axis=0)) == len(allk)  # owned slices partition U
+    assert nt == len(full.triangles) > 1000
+    V, T = np.concatenate(verts), np.concatenate(tris)
+    assert np.array_equal(canon_triangles(V, T), canon_triangles(full.vertices, full.triangles))
+    assert np.array_equal(canon_vertices(np.unique(V, axis=0))[0], canon_vertices(np.unique(full.vertices, axis=0))[0])
+    # the halo makes each shard's owned blocks identical to the merged volume's
+    rk, rt, rw = root.export()
+    rpos = {tuple(k): i for i, k in enumerate(rk)}
+    for out, n_owned in shards:
+        k, t, w = out.export()
+        for b in range(n_owned):
+            j = rpos[tuple(k[b])]
+            assert np.array_equal(t[b], rt[j]) and np.array_equal(w[b], rw[j])
+
+
+def test_rccl_world_one(seq):
+    """mqr_reduce_rccl through a real RCCL communicator (world size 1: the send to self)."""
+    from mqr.distributed import RcclComm, merge_rccl
+    vol = _shards(seq, 1)[0]
+    comm = RcclComm(0, 0, 1, RcclComm.unique_id())
+    try:
+        out, n = merge_rccl(vol, comm, mode="root")
+        assert n == vol.size() == out.size()
+        assert compare_volumes(out.export(), vol.export(), 0.0) == 0.0
+        out2, n2 = merge_rccl(vol, comm, mode="sharded", out=out)  # reuse: the output is emptied first
+        assert n2 == vol.size()
+        a = vol.extract_triangle_mesh(1.5)
+        from mqr.distributed import extract_mesh_owned
+        b = extract_mesh_owned(out2, n2, 1.5)
+        compare_meshes(b.vertices, b.triangles, a.vertices, a.triangles)
+    finally:
+        comm.close()
+
+
+def _rccl_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from mqr import synthetic
+        from mqr.distributed import extract_mesh_owned, make_comm, merge_rccl, shard_range
+        from mqr.vbg import VoxelBlockGrid
+        torch.cuda.set_device(rank)
+        s = synthetic.make_sequence("room", n=36, height=240, width=320, f=262.5, noise=True, seed=12)
+        lo, hi = shard_range(36, rank, world)
+        v = VoxelBlockGrid(voxel_size=0.01, block_resolution=16, block_count=64, device=rank)
+        v.integrate_frames(s["depth"][lo:hi], s["K"][lo:hi], s["T_wc"][lo:hi], depth_scale=1.0, depth_max=4.0,
+                           trunc_voxel_multiplier=10.0)
+        comm = make_comm(rank)
+        out, n = merge_rccl(v, comm, mode="sharded")
+        m = extract_mesh_owned(out, n, 1.5)
+        got = [None] * world
+        dist.all_gather_object(got, (m.vertices, m.triangles))
+        comm.close()
+        q.put((rank, got if rank == 0 else None))
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_two_gpus(seq):
+    import torch
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs 2 GPUs (RCCL cannot put two ranks on one device)")
+    import socket
+    import torch.multiprocessing as mp
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_rccl_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in ps)
+    for p in ps:
+        p.join(60)
+    assert not isinstance(res[1], str), res[1]
+    got = res[0]
+    assert not isinstance(got, str), got
+    from mqr.distributed import merge_local
+    full = merge_local(_shards(seq, 2), mode="root")[0][0].extract_triangle_mesh(1.5)
+    off, V, T = 0, [], []
+    for v, t in got:
+        V.append(v)
+        T.append(t + off)
+        off += len(v)
+    V, T = np.concatenate(V), np.concatenate(T)
+    assert np.array_equal(canon_triangles(V, T), canon_triangles(full.vertices, full.triangles))
