@@ -576,7 +576,7 @@ def main():
     achieved = alg_bytes / launches / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
 
     extras = {}
-    if rank == 0 and not args.no_extras:
+    if rank == 0 and world == 1 and not args.no_extras:
         dev = torch.device("cuda", local)
         extras["hbm_copy_gbs"] = copy_peak_gbs(dev)
         extras["confidence"] = confidence_leg(depth_t, K, T, args, dev)

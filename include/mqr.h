@@ -186,6 +186,18 @@ int mqr_vbg_stats(mqr_vbg* v, mqr_stats* out, int reset);
  * cast_rays takes explicit rays (n,6) float32 (origin, direction).  Outputs: t_hit (inf on miss)
  * and the optional geometry / primitive ids (0xffffffff on miss), barycentric uvs (n,2) and unit
  * geometric normals (n,3); out_loc says where all output buffers live. */
+/* Per-vertex colour from keyframes: the colour averaging of Open3D's
+ * colour-map pipeline fed by the reference (optimize_color_pose.py:24-73 -> run_rigid_optimizer;
+ * upstream ColorMapUtils.cpp CreateVertexAndImageVisibility + SetGeometryColorAverage, VERIFY).
+ * vertices nv*3 float32; images N*H*W*3 uint8 RGB; depths N*H*W float32 colour-aligned depth
+ * (ray-cast, raycast_in_color_view); K N*9, T_wc N*16 float64 host.  colors_out nv*3 float32 in
+ * [0, 1] (0 where no keyframe sees the vertex), counts_out nv int32 (nullable).  Open3D defaults:
+ * max_depth 2.5, visibility_threshold 0.03, margin 10. */
+int mqr_color_vertices(int device, const float* vertices, int64_t nv, int vertices_loc, const uint8_t* images,
+                       const float* depths, int images_loc, int N, int H, int W, const double* K, const double* T_wc,
+                       double max_depth, double visibility_threshold, int margin, float* colors_out,
+                       int32_t* counts_out, int out_loc);
+
 int mqr_scene_create(int device, mqr_scene** out);
 int mqr_scene_destroy(mqr_scene* s);
 int mqr_scene_add_triangles(mqr_scene* s, const float* vertices, int64_t nv, const int32_t* triangles, int64_t nt,

@@ -252,7 +252,6 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
     if (n == 0) return 0;
     hipStream_t s = v->pipelined ? v->stream2 : v->stream;
     const unsigned grid = (unsigned)std::min<int64_t>(n, 8192);
-    const unsigned grid2 = (unsigned)std::min<int64_t>(2 * n, 16384);
     const int64_t* depth_frame = dframe_dev(v, p);
     const Table t = v->table(p);
     int* counters = v->ctr(p);
@@ -276,160 +275,58 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
         MQR_REQUIRE(e0 && e1, "profiling: event creation failed");
         MQR_CHECK_HIP(hipEventRecord(e0, s));
     }
-    // the unguarded division core needs its constant denominators in range (see div_rn_core)
-    const bool fast_ok = !div_unsafe_host(sdf_trunc) && (depth_scale == 1.0f || !div_unsafe_host(depth_scale));
-#define MQR_LAUNCH_INT(RR, GG, SW, FAST, NT) MQR_LAUNCH_INTW(RR, GG, SW, FAST, NT, 1)
-#define MQR_LAUNCH_INTW(RR, GG, SW, FAST, NT, WPE)                                                                \
-    hipLaunchKernelGGL((k_integrate_t<RR, GG, SW, FAST, NT, WPE>), dim3(grid), dim3(NT), 0, s, list, lmask,      \
-                       (int32_t*)nullptr, counters,                                                               \
-                       v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp, depth_frame, depth_scale,      \
-                       depth_max, sdf_trunc)
-#define MQR_LAUNCH_SPLIT(RR, GG, NT)                                                                              \
-    hipLaunchKernelGGL((k_integrate_t<RR, GG, 0, false, NT, 1, 2>), dim3(grid2), dim3(NT), 0, s, list, lmask,     \
-                       (int32_t*)nullptr, counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp, depth_frame,       \
-                       depth_scale, depth_max, sdf_trunc)
-// fast kernel + exact fix-up launch over the blocks it handed back (usually none: the fix-up grid
-// reads a zero count and exits).  counters + (kBadCount - kListCount): the fix-up's list length.
-#define MQR_LAUNCH_FIX(RR, GG, NT, WPE)                                                                           \
-    hipLaunchKernelGGL((k_integrate_t<RR, GG, 0, true, NT, WPE, 1, true>), dim3(grid), dim3(NT), 0, s, list, lmask, \
-                       v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp,        \
-                       depth_frame, depth_scale, depth_max, sdf_trunc);                                            \
-    hipLaunchKernelGGL((k_integrate_t<RR, 4, 0, false, 512>), dim3(64), dim3(512), 0, s, v->bad[p],                \
-                       reinterpret_cast<const bmask_t*>(v->bad[p] + v->list_cap), (int32_t*)nullptr,             \
-                       counters + (kBadCount - kListCount), v->list_cap, t, v->pool, v->voxel_size, depths, HW,   \
-                       H, W, fp, depth_frame, depth_scale, depth_max, sdf_trunc)
-#define MQR_LAUNCH_PK(RR, GG, NT)                                                                              \
-    hipLaunchKernelGGL((k_integrate_pk<RR, GG, NT>), dim3(grid), dim3(NT), 0, s, list, counters, v->list_cap, t, \
-                       v->pool, v->voxel_size, depths, HW, H, W, fp, depth_frame, depth_max, sdf_trunc)
-    const bool pk_ok = fast_ok && depth_scale == 1.0f;
-    // lean kernel: also needs every out-of-image byte offset (>= 2^32 - 4W) past the frame's 4HW bytes
-    const bool lean_ok = pk_ok && 4 * (HW + W) <= (int64_t{1} << 31);
-// lean kernel + exact fix-up launch (FG / FNT: the fix-up kernel's group size and threads)
-#define MQR_LAUNCH_LEAN(RR, NT, PIPE, RZ, WPE, FG, FNT) MQR_LAUNCH_LEANC(RR, NT, PIPE, RZ, WPE, false, FG, FNT)
-#define MQR_LAUNCH_DBT(RR, NT) MQR_LAUNCH_DBTW(RR, NT, 1)
-#define MQR_LAUNCH_DBTW(RR, NT, WPE)                                                                            \
-    hipLaunchKernelGGL((k_integrate_dbt<RR, NT, WPE>), dim3(grid), dim3(NT), 0, s, list, lmask, v->bad[p], counters,  \
-                       v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp, depth_frame, depth_max,      \
-                       sdf_trunc);                                                                                \
-    hipLaunchKernelGGL((k_integrate_t<RR, 4, 0, false, 512>), dim3(8), dim3(512), 0, s, v->bad[p],                 \
-                       reinterpret_cast<const bmask_t*>(v->bad[p] + v->list_cap), (int32_t*)nullptr,             \
-                       counters + (kBadCount - kListCount), v->list_cap, t, v->pool, v->voxel_size, depths, HW,   \
-                       H, W, fp, depth_frame, depth_scale, depth_max, sdf_trunc)
-#define MQR_LAUNCH_TILE(RR, NT, FG, FNT)                                                                        \
-    hipLaunchKernelGGL((k_integrate_tile<RR, NT>), dim3(grid), dim3(NT), 0, s, list, lmask, v->bad[p], counters, \
-                       v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp, depth_frame, depth_max,      \
-                       sdf_trunc);                                                                                \
-    hipLaunchKernelGGL((k_integrate_t<RR, FG, 0, false, FNT>), dim3(8), dim3(FNT), 0, s, v->bad[p],                \
-                       reinterpret_cast<const bmask_t*>(v->bad[p] + v->list_cap), (int32_t*)nullptr,             \
-                       counters + (kBadCount - kListCount), v->list_cap, t, v->pool, v->voxel_size, depths, HW,   \
-                       H, W, fp, depth_frame, depth_scale, depth_max, sdf_trunc)
-#define MQR_LAUNCH_LEANC(RR, NT, PIPE, RZ, WPE, CUBE, FG, FNT)                                                    \
-    hipLaunchKernelGGL((k_integrate_lean<RR, NT, PIPE, RZ, WPE, CUBE>), dim3(grid), dim3(NT), 0, s, list, lmask,   \
-                       v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp,          \
-                       depth_frame, depth_max, sdf_trunc);                                                        \
-    hipLaunchKernelGGL((k_integrate_t<RR, FG, 0, false, FNT>), dim3(8), dim3(FNT), 0, s, v->bad[p],               \
-                       reinterpret_cast<const bmask_t*>(v->bad[p] + v->list_cap), (int32_t*)nullptr,             \
-                       counters + (kBadCount - kListCount), v->list_cap, t, v->pool, v->voxel_size, depths, HW,   \
-                       H, W, fp, depth_frame, depth_scale, depth_max, sdf_trunc)
-    // Variants (mqr_vbg_set_variant; all bit-identical, tests/test_gpu_numerics.py): 1 generic k_integrate;
-    // k_integrate_t<R, G, SWZ, FAST, NT> and packed-f32 k_integrate_pk<R, G, NT> configurations
-    // below, kept for A/B on new hardware (tools/ab_integrate.py).  FAST / packed fall back to the
-    // default when their preconditions on sdf_trunc / depth_scale do not hold.
+    // The fast kernels (k_integrate_lean, k_integrate_tb) evaluate s / sdf_trunc through the division
+    // core (div_rn_core: exact while the denominator is in [2^-60, 2^60]), take depth in metres
+    // (depth_scale 1: Open3D's d / 1 is d), and address the frame with 32-bit byte offsets that
+    // must stay past 4HW for out-of-image voxels.  Otherwise the exact k_integrate_t runs alone.
+    const bool lean_ok = !div_unsafe_host(sdf_trunc) && depth_scale == 1.0f && 4 * (HW + W) <= (int64_t{1} << 31);
+    // Variants (mqr_vbg_set_variant, low byte; all bit-identical, tests/test_gpu_numerics.py):
+    //   0 default: k_integrate_lean (R = 16 / 8);  1 generic k_integrate (runtime R);
+    //   2 exact k_integrate_t;  5 k_integrate_tb (R = 16: block depth tile in LDS, A/B -- DESIGN.md §4).
     int var = v->kernel_variant;
-    if ((var == 6 || var == 7 || var == 18 || var == 19 || var == 27 || (var >= 34 && var <= 37)) && !fast_ok)
-        var = 0;
-    if ((var == 8 || var == 9 || (var >= 13 && var <= 16) || var == 20) && !pk_ok) var = 0;
-    if (var >= 30 && var <= 33 && !lmask) var = 0;  // split blocks need the longest-first mask copy
-    if (((var >= 40 && var <= 53) || (var >= 56 && var <= 59)) && !lean_ok) var = 0;
-    if (v->R == 16 && var != 1) {
-        switch (var) {
-            case 40: MQR_LAUNCH_LEAN(16, 512, true, 1, 1, 4, 512); break;
-            case 41: MQR_LAUNCH_LEAN(16, 512, false, 1, 1, 4, 512); break;
-            case 42: MQR_LAUNCH_LEAN(16, 1024, true, 1, 1, 4, 512); break;
-            case 43: MQR_LAUNCH_LEAN(16, 512, true, 2, 1, 4, 512); break;
-            case 44: MQR_LAUNCH_LEAN(16, 256, false, 1, 1, 4, 512); break;
-            case 45: MQR_LAUNCH_LEAN(16, 512, true, 1, 8, 4, 512); break;
-            case 46: MQR_LAUNCH_LEAN(16, 1024, false, 1, 1, 4, 512); break;
-            case 47: MQR_LAUNCH_LEAN(16, 1024, true, 2, 1, 4, 512); break;
-            case 48: MQR_LAUNCH_LEANC(16, 512, false, 2, 1, true, 4, 512); break;
-            case 49: MQR_LAUNCH_LEANC(16, 512, true, 2, 1, true, 4, 512); break;
-            case 50: MQR_LAUNCH_LEANC(16, 1024, false, 2, 1, true, 4, 512); break;
-            case 51: MQR_LAUNCH_LEANC(16, 1024, true, 2, 1, true, 4, 512); break;
-            case 52: MQR_LAUNCH_LEANC(16, 256, false, 2, 1, true, 4, 512); break;
-            case 53: MQR_LAUNCH_LEAN(16, 512, false, 2, 1, 4, 512); break;
-            case 2: MQR_LAUNCH_INT(16, 4, false, false, 256); break;
-            case 5: MQR_LAUNCH_INT(16, 8, 64, false, 256); break;
-            case 22: MQR_LAUNCH_INT(16, 4, 16, false, 512); break;
-            case 23: MQR_LAUNCH_INT(16, 4, 64, false, 512); break;
-            case 24: MQR_LAUNCH_INT(16, 4, 256, false, 512); break;
-            case 25: MQR_LAUNCH_INT(16, 4, 4, false, 512); break;
-            case 6: MQR_LAUNCH_INT(16, 8, false, true, 256); break;
-            case 7: MQR_LAUNCH_INT(16, 4, false, true, 256); break;
-            case 8: MQR_LAUNCH_PK(16, 8, 256); break;
-            case 9: MQR_LAUNCH_PK(16, 4, 256); break;
-            case 10: MQR_LAUNCH_INT(16, 8, false, false, 512); break;
-            case 11: MQR_LAUNCH_INT(16, 8, false, false, 256); break;
-            case 12: MQR_LAUNCH_INT(16, 4, false, false, 1024); break;
-            case 13: MQR_LAUNCH_PK(16, 8, 512); break;
-            case 14: MQR_LAUNCH_PK(16, 4, 512); break;
-            case 15: MQR_LAUNCH_PK(16, 4, 1024); break;
-            case 16: MQR_LAUNCH_PK(16, 2, 1024); break;
-            case 17: MQR_LAUNCH_INT(16, 2, false, false, 1024); break;
-            case 18: MQR_LAUNCH_INT(16, 4, false, true, 512); break;
-            case 19: MQR_LAUNCH_INT(16, 8, false, true, 512); break;
-            case 20: MQR_LAUNCH_PK(16, 2, 512); break;
-            case 26: MQR_LAUNCH_INTW(16, 4, false, false, 512, 8); break;
-            case 30: MQR_LAUNCH_SPLIT(16, 4, 256); break;
-            case 34: MQR_LAUNCH_FIX(16, 4, 512, 1); break;
-            case 35: MQR_LAUNCH_FIX(16, 8, 512, 1); break;
-            case 36: MQR_LAUNCH_FIX(16, 4, 256, 1); break;
-            case 37: MQR_LAUNCH_FIX(16, 4, 512, 8); break;
-            case 31: MQR_LAUNCH_SPLIT(16, 4, 512); break;
-            case 32: MQR_LAUNCH_SPLIT(16, 8, 256); break;
-            case 33: MQR_LAUNCH_SPLIT(16, 2, 512); break;
-            case 27: MQR_LAUNCH_INTW(16, 4, false, true, 512, 8); break;
-            case 28: MQR_LAUNCH_INTW(16, 8, false, false, 512, 8); break;
-            case 29: MQR_LAUNCH_INTW(16, 2, false, false, 256, 8); break;
-            case 54: MQR_LAUNCH_INT(16, 4, false, false, 512); break;
-            case 56: MQR_LAUNCH_TILE(16, 512, 4, 512); break;
-            case 58: MQR_LAUNCH_DBT(16, 512); break;
-            case 59: MQR_LAUNCH_DBTW(16, 512, 8); break;
-            case 57: MQR_LAUNCH_TILE(16, 256, 4, 512); break;
-            // default: the lean kernel (512 threads x 8 voxels, column mapping, 3-op reciprocals;
-            // fastest on MI355X, tools/ab_integrate.py); the exact branchy kernel where the lean one's
-            // preconditions (unit depth scale, trunc in range, frame size) do not hold
-            default:
-                if (lean_ok) {
-                    MQR_LAUNCH_LEAN(16, 512, false, 2, 1, 4, 512);
-                } else {
-                    MQR_LAUNCH_INT(16, 4, false, false, 512);
-                }
-                break;
-        }
-    } else if (v->R == 8 && var != 1) {
-        if (var >= 48 && var <= 55) {
-            MQR_LAUNCH_LEANC(8, 256, false, 2, 1, true, 2, 256);
-        } else if (var >= 40 && var <= 47) {
-            MQR_LAUNCH_LEAN(8, 256, true, 1, 1, 2, 256);
-        } else if (var >= 8 && pk_ok)
-            MQR_LAUNCH_PK(8, 2, 256);
-        else if (var == 6)
-            MQR_LAUNCH_INT(8, 2, false, true, 256);
-        else
-            MQR_LAUNCH_INT(8, 2, false, false, 256);
-    } else
+    if (var != 1 && var != 2 && var != 5) var = 0;
+    if ((var == 0 || var == 5) && !lean_ok) var = 2;
+    if (var == 5 && (v->R != 16 || W % 4 != 0 || (reinterpret_cast<uintptr_t>(depths) & 15))) var = 0;
+    if (v->R != 16 && v->R != 8) var = 1;
+    const int32_t* bad_list = v->bad[p];
+    const bmask_t* bad_mask = reinterpret_cast<const bmask_t*>(v->bad[p] + v->list_cap);
+    int* bad_count = counters + kBadCount;
+    if (var == 1) {
         hipLaunchKernelGGL(k_integrate, dim3(grid), dim3(256), 0, s, list, counters, v->list_cap, t, v->pool, v->R,
                            v->voxel_size, depths, HW, H, W, fp, depth_frame, depth_scale, depth_max, sdf_trunc);
-#undef MQR_LAUNCH_INT
-#undef MQR_LAUNCH_INTW
-#undef MQR_LAUNCH_SPLIT
-#undef MQR_LAUNCH_FIX
-#undef MQR_LAUNCH_PK
-#undef MQR_LAUNCH_LEAN
-#undef MQR_LAUNCH_LEANC
-#undef MQR_LAUNCH_TILE
-#undef MQR_LAUNCH_DBT
-#undef MQR_LAUNCH_DBTW
+    } else if (v->R == 16) {
+        if (var == 2) {
+            hipLaunchKernelGGL((k_integrate_t<16, 4, 512>), dim3(grid), dim3(512), 0, s, list, lmask,
+                               counters + kListCount, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp,
+                               depth_frame, depth_scale, depth_max, sdf_trunc);
+        } else {
+            if (var == 5)
+                hipLaunchKernelGGL(k_integrate_tb, dim3(grid), dim3(512), 0, s, list, lmask, v->bad[p], counters,
+                                   v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp, depth_frame,
+                                   depth_max, sdf_trunc);
+            else
+                hipLaunchKernelGGL((k_integrate_lean<16, 512>), dim3(grid), dim3(512), 0, s, list, lmask, v->bad[p],
+                                   counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp,
+                                   depth_frame, depth_max, sdf_trunc);
+            // exact fix-up of the blocks the fast kernel handed back (usually none: reads a zero count)
+            hipLaunchKernelGGL((k_integrate_t<16, 4, 512>), dim3(8), dim3(512), 0, s, bad_list, bad_mask, bad_count,
+                               v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp, depth_frame, depth_scale,
+                               depth_max, sdf_trunc);
+        }
+    } else {  // R == 8
+        if (var == 2) {
+            hipLaunchKernelGGL((k_integrate_t<8, 2, 256>), dim3(grid), dim3(256), 0, s, list, lmask,
+                               counters + kListCount, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp,
+                               depth_frame, depth_scale, depth_max, sdf_trunc);
+        } else {
+            hipLaunchKernelGGL((k_integrate_lean<8, 256>), dim3(grid), dim3(256), 0, s, list, lmask, v->bad[p],
+                               counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp, depth_frame,
+                               depth_max, sdf_trunc);
+            hipLaunchKernelGGL((k_integrate_t<8, 2, 256>), dim3(8), dim3(256), 0, s, bad_list, bad_mask, bad_count,
+                               v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp, depth_frame, depth_scale,
+                               depth_max, sdf_trunc);
+        }
+    }
     MQR_CHECK_HIP(hipGetLastError());
     if (v->profile) {
         MQR_CHECK_HIP(hipEventRecord(e1, s));

@@ -262,44 +262,21 @@ __device__ __forceinline__ float div_rn(float a, float b) {
 }
 
 __device__ __forceinline__ float rcp_rn(float b) { return div_safe(b) ? div_rn_core(1.0f, b) : 1.0f / b; }
-
-// XCD-aware list order: consecutive workgroups are dealt round-robin over the 8 XCDs, so hand XCD
-// x (= L % 8) chunks of C consecutive list entries in turn.  List entries are appended in touch
-// (pixel) order, so a chunk is a spatially coherent set of blocks whose depth gathers share
-// pixels and can hit in that XCD's L2; interleaving the chunks keeps the XCDs' loads balanced.
-// Bijective on [0, n) (the tail past the last full round keeps its order); speed only.
-template <int C>
-__device__ __forceinline__ int64_t xcd_swizzle(int64_t L, int64_t n) {
-    const int64_t full = n / (8 * C) * (8 * C);
-    if (L >= full) return L;
-    const int64_t x = L & 7, s = L >> 3;
-    return ((s / C) * 8 + x) * C + s % C;
-}
-
-// Operand checks of the unguarded division core, on the float bits (|x| = e):
-//   denominator / reciprocal: 2^-60 <= |x| <= 2^60 (also rejects 0, inf, NaN);
-//   numerator below a safe denominator: 0 or |x| >= 2^-60 (the clamp keeps it <= the denominator).
-__device__ __forceinline__ bool den_unsafe(float v) {
-    return ((__float_as_uint(v) & 0x7fffffffu) - 0x21800000u) > 0x3c000000u;
-}
-__device__ __forceinline__ bool num_unsafe(float v) {
-    return ((__float_as_uint(v) & 0x7fffffffu) - 1u) < 0x217fffffu;
-}
-
-// All frames of the batch over one thread's voxel column (see k_integrate_t).  EXACT = false
-// evaluates every division with the bare core and returns whether any operand left the range in
-// which the core is exact (den_unsafe / num_unsafe); the caller then discards the column results
-// of the whole block and re-runs it with EXACT = true.  The flag is data-independent of which
-// path ran, so the exact pass reproduces k_integrate bit for bit, and the fast pass has no
-// per-voxel branches around its divisions.
-template <int ZPER, int G, bool EXACT>
-__device__ __forceinline__ bool integrate_column(float2 (&tw)[ZPER], uint32_t& dirty, bmask_t mask,
+// Exact integrate, R known at compile time (R = 16 / 8): thread t owns the voxel column (x, y) =
+// (t % R, t / R % R) for z in its z-range, keeps those voxels' (tsdf, weight) in registers for
+// all frames of the batch, and evaluates Open3D's transform ((xs*e0 + ys*e1) + zs*e2) + e3 with
+// the z-independent partial product hoisted per frame -- the same float operations in the same
+// order as k_integrate, so the result is bit-identical.  Groups of G voxels issue their depth
+// gathers together.  The fallback kernel (depth_scale != 1, trunc or frame size outside the fast
+// kernels' preconditions) and the exact fix-up launch behind the fast kernels (over the blocks
+// they handed back through bad_out; lmask = those blocks' batch masks).
+template <int ZPER, int G>
+__device__ __forceinline__ void integrate_column(float2 (&tw)[ZPER], uint32_t& dirty, bmask_t mask,
                                                  const float (&zs)[ZPER], float xs, float ys,
                                                  const float* __restrict__ depths, int64_t HW, int W, float hm1,
                                                  float wm1, const FrameParams* __restrict__ fps,
                                                  const int64_t* __restrict__ depth_frame, float depth_scale,
                                                  bool unit_scale, float depth_max, float sdf_trunc) {
-    bool bad = false;
     bmask_t m = mask;
     while (m) {
         const int f = __builtin_ctzll(m);
@@ -309,8 +286,6 @@ __device__ __forceinline__ bool integrate_column(float2 (&tw)[ZPER], uint32_t& d
         const float ax = xs * fp.ext[0] + ys * fp.ext[1];
         const float ay = xs * fp.ext[4] + ys * fp.ext[5];
         const float az = xs * fp.ext[8] + ys * fp.ext[9];
-        // Groups of G voxels: project all, issue all G depth gathers (branch-free, out-of-image
-        // lanes read pixel 0 and are masked), then update -- G loads in flight per wave.
 #pragma unroll
         for (int g = 0; g < ZPER; g += G) {
             int pix[G];
@@ -322,13 +297,7 @@ __device__ __forceinline__ bool integrate_column(float2 (&tw)[ZPER], uint32_t& d
                 const float xc = (ax + zs[k] * fp.ext[2]) + fp.ext[3];
                 const float yc = (ay + zs[k] * fp.ext[6]) + fp.ext[7];
                 const float zc = (az + zs[k] * fp.ext[10]) + fp.ext[11];
-                float inv_z;
-                if (EXACT) {
-                    inv_z = rcp_rn(zc);
-                } else {
-                    inv_z = div_rn_core(1.0f, zc);
-                    bad |= den_unsafe(zc);
-                }
+                const float inv_z = rcp_rn(zc);
                 const float u = fp.fx * xc * inv_z + fp.cx;
                 const float v = fp.fy * yc * inv_z + fp.cy;
                 in[j] = v >= 0 && u >= 0 && v <= hm1 && u <= wm1;
@@ -342,88 +311,49 @@ __device__ __forceinline__ bool integrate_column(float2 (&tw)[ZPER], uint32_t& d
 #pragma unroll
             for (int j = 0; j < G; ++j) {
                 const int k = g + j;
-                float d;
-                if (unit_scale) {
-                    d = dv[j];
-                } else if (EXACT) {
-                    d = div_rn(dv[j], depth_scale);
-                } else {
-                    d = div_rn_core(dv[j], depth_scale);
-                    bad |= in[j] && dv[j] != 0.0f && den_unsafe(dv[j]);  // 0 / s = +0 in the core
-                }
+                const float d = unit_scale ? dv[j] : div_rn(dv[j], depth_scale);
                 const float zc = zcs[j];
                 float sdf = d - zc;
                 if (!in[j] || d <= 0 || d > depth_max || zc <= 0 || sdf < -sdf_trunc) continue;
                 sdf = sdf < sdf_trunc ? sdf : sdf_trunc;
                 const float wgt = tw[k].y;
-                float inv_wsum;
-                if (EXACT) {
-                    sdf = div_rn(sdf, sdf_trunc);
-                    inv_wsum = rcp_rn(wgt + 1);
-                } else {
-                    bad |= num_unsafe(sdf) || den_unsafe(wgt + 1);
-                    sdf = div_rn_core(sdf, sdf_trunc);
-                    inv_wsum = div_rn_core(1.0f, wgt + 1);
-                }
+                sdf = div_rn(sdf, sdf_trunc);
+                const float inv_wsum = rcp_rn(wgt + 1);
                 tw[k].x = (wgt * tw[k].x + sdf) * inv_wsum;
                 tw[k].y = wgt + 1;
                 dirty |= 1u << k;
             }
         }
     }
-    return bad;
 }
 
-// Integrate, R known at compile time (R = 16 / 8): thread t owns the voxel column (x, y) =
-// (t % R, t / R % R) for z in its z-range, keeps those voxels' (tsdf, weight) in registers for
-// all frames of the batch, and evaluates Open3D's transform ((xs*e0 + ys*e1) + zs*e2) + e3 with
-// the z-independent partial product hoisted per frame -- the same float operations in the same
-// order, so the result is bit-identical to k_integrate.  FAST: unguarded division core with a
-// block-level exact re-run when any operand is out of its range (host guarantees sdf_trunc and
-// depth_scale are in range).
-//
-// SPLIT > 1: SPLIT workgroups per block, each on R / SPLIT consecutive z-layers (finer grain for the
-// longest-first schedule); needs lmask, the batch masks in list order (k_lpt_order), because the
-// part-0 workgroup clears the table mask while its sibling may not have read it yet.
-//
-// FAST with bad_out != nullptr: a block whose operands left the core's exact range is not written
-// back; its (slot, mask) goes to bad_out (count at counters[kBadCount]) for an exact re-run by a
-// follow-up launch of the exact kernel over that list.  The fast kernel then carries no second,
-// exact copy of the column loop (fewer registers, no per-voxel branches).
-template <int R, int G, int SWZ = 0, bool FAST = false, int NT = 256, int WPE = 1, int SPLIT = 1, bool EXTFIX = false>
-__global__ __launch_bounds__(NT, WPE) void k_integrate_t(const int32_t* __restrict__ list,
-                                                     const bmask_t* __restrict__ lmask,
-                                                     int32_t* __restrict__ bad_out,
-                                                     int* __restrict__ counters,
-                                                     int64_t list_cap, Table t, float2* __restrict__ pool,
-                                                     float voxel_size, const float* __restrict__ depths, int64_t HW,
-                                                     int H, int W, const FrameParams* __restrict__ fps,
-                                                     const int64_t* __restrict__ depth_frame, float depth_scale,
-                                                     float depth_max, float sdf_trunc) {
+template <int R, int G, int NT>
+__global__ __launch_bounds__(NT) void k_integrate_t(const int32_t* __restrict__ list, const bmask_t* __restrict__ lmask,
+                                                    const int* __restrict__ count, int64_t list_cap, Table t,
+                                                    float2* __restrict__ pool, float voxel_size,
+                                                    const float* __restrict__ depths, int64_t HW, int H, int W,
+                                                    const FrameParams* __restrict__ fps,
+                                                    const int64_t* __restrict__ depth_frame, float depth_scale,
+                                                    float depth_max, float sdf_trunc) {
     constexpr int R2 = R * R;
     constexpr int R3 = R2 * R;
-    constexpr int ZPER = R3 / (NT * SPLIT);  // voxels per thread (16 at R=16, NT=256; 2 at R=8)
-    constexpr int ZSTEP = NT / R2;           // z stride between a thread's voxels (1 at R=16, NT=256)
-    static_assert(R3 % (NT * SPLIT) == 0 && NT % R2 == 0, "NT * SPLIT must divide R^3, NT a multiple of R^2");
-    static_assert(SPLIT == 1 || SWZ == 0, "split blocks use the plain list order");
+    constexpr int ZPER = R3 / NT;   // voxels per thread
+    constexpr int ZSTEP = NT / R2;  // z stride between a thread's voxels
+    static_assert(R3 % NT == 0 && NT % R2 == 0, "NT must divide R^3 and be a multiple of R^2");
     static_assert(ZPER % G == 0, "group size must divide the voxels per thread");
     const bool unit_scale = depth_scale == 1.0f;  // d / 1 == d exactly: skip the division
-    const int64_t n = min((int64_t)counters[kListCount], list_cap);
+    const int64_t n = min((int64_t)*count, list_cap);
     const float hm1 = (float)H - 1.0f, wm1 = (float)W - 1.0f;
     const int tid = threadIdx.x;
-    const int xv = tid % R, yv = (tid / R) % R;
-    for (int64_t U = blockIdx.x; U < n * SPLIT; U += gridDim.x) {
-        const int64_t L = SPLIT > 1 ? U / SPLIT : U;
-        const int part = SPLIT > 1 ? (int)(U % SPLIT) : 0;
-        const int z0 = tid / R2 + part * (R / SPLIT);
-        const int64_t i = SWZ > 0 ? xcd_swizzle<(SWZ > 0 ? SWZ : 1)>(L, n) : L;
+    const int xv = tid % R, yv = (tid / R) % R, z0 = tid / R2;
+    for (int64_t i = blockIdx.x; i < n; i += gridDim.x) {
         const int32_t slot = list[i];
         const int buf = t.vals[slot];
         const bmask_t mask = readfirstlane_u64(lmask ? lmask[i] : t.mask[slot]);
         int xb, yb, zb;
         unpack_key(t.keys[slot], xb, yb, zb);
         if (buf >= 0) {
-            float2* vox = pool + (int64_t)buf * R3 + part * (R3 / SPLIT);
+            float2* vox = pool + (int64_t)buf * R3;
             float2 tw[ZPER];
             float zs[ZPER];
 #pragma unroll
@@ -434,31 +364,14 @@ __global__ __launch_bounds__(NT, WPE) void k_integrate_t(const int32_t* __restri
             const float xs = (float)(xb * R + xv) * voxel_size;
             const float ys = (float)(yb * R + yv) * voxel_size;
             uint32_t dirty = 0;
-            const bool bad = integrate_column<ZPER, G, !FAST>(tw, dirty, mask, zs, xs, ys, depths, HW, W, hm1, wm1,
-                                                           fps, depth_frame, depth_scale, unit_scale, depth_max,
-                                                           sdf_trunc);
-            if (FAST && __syncthreads_or(bad)) {  // block-uniform
-                if (EXTFIX) {  // hand the block to the exact fix-up launch, leave it unwritten
-                    if (tid == 0) {
-                        const int j = atomicAdd(&counters[kBadCount], 1);
-                        bad_out[j] = slot;
-                        reinterpret_cast<bmask_t*>(bad_out + list_cap)[j] = mask;
-                    }
-                    dirty = 0;
-                } else {  // redo this block exactly
-#pragma unroll
-                    for (int k = 0; k < ZPER; ++k) tw[k] = vox[k * NT + tid];
-                    dirty = 0;
-                    integrate_column<ZPER, G, true>(tw, dirty, mask, zs, xs, ys, depths, HW, W, hm1, wm1, fps,
-                                                    depth_frame, depth_scale, unit_scale, depth_max, sdf_trunc);
-                }
-            }
+            integrate_column<ZPER, G>(tw, dirty, mask, zs, xs, ys, depths, HW, W, hm1, wm1, fps, depth_frame,
+                                      depth_scale, unit_scale, depth_max, sdf_trunc);
 #pragma unroll
             for (int k = 0; k < ZPER; ++k)
                 if (dirty & (1u << k)) vox[k * NT + tid] = tw[k];
         }
         __syncthreads();
-        if (tid == 0 && part == 0) t.mask[slot] = 0;
+        if (tid == 0) t.mask[slot] = 0;
     }
 }
 
@@ -492,205 +405,16 @@ __global__ __launch_bounds__(1024) void k_lpt_order(const int32_t* __restrict__ 
         out_mask[pos] = m;
     }
 }
-
-// ---- packed-f32 integrate (v_pk_mul/add/fma_f32: two voxels per VALU instruction) ------------
-typedef float f2v __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ f2v fma2(f2v a, f2v b, f2v c) { return __builtin_elementwise_fma(a, b, c); }
-__device__ __forceinline__ f2v splat2(float x) { return f2v{x, x}; }
-
-// 1 / b through the core sequence (q0 = 1 * y1 = y1), elementwise; exact for 2^-60 <= |b| <= 2^60.
-__device__ __forceinline__ f2v rcp_core2(f2v b) {
-    const f2v one = splat2(1.0f);
-    const f2v y0 = {__builtin_amdgcn_rcpf(b.x), __builtin_amdgcn_rcpf(b.y)};
-    const f2v nb = -b;
-    const f2v y1 = fma2(fma2(nb, y0, one), y0, y0);
-    const f2v q1 = fma2(fma2(nb, y1, one), y1, y1);
-    return fma2(fma2(nb, q1, one), y1, q1);
-}
-
-// a / t for a launch-constant t with its refined reciprocal y1t precomputed (same core sequence).
-__device__ __forceinline__ f2v div_const2(f2v a, f2v nbt, f2v y1t) {
-    const f2v q0 = a * y1t;
-    const f2v q1 = fma2(fma2(nbt, q0, a), y1t, q0);
-    return fma2(fma2(nbt, q1, a), y1t, q1);
-}
-
-// Fast pass of one column with the (tsdf, weight) of voxels (2q, 2q+1) packed in T[q], Wt[q].
-// Preconditions (checked by the caller): depth_scale == 1, sdf_trunc in [2^-60, 2^60], every
-// weight in [0, 2^59].  Returns true if some |zc| left [2^-36, 2^60]; the caller then re-runs the
-// block exactly.  Inside that range the core divisions are exact: 1/zc directly, and the numerator
-// sdf = d - zc is 0 or >= 2^-60 in magnitude (zc >= 2^-36 => the difference is a multiple of
-// 2^-60 or at least zc / 2), so the result is bit-identical to integrate_column<.., true>.
-template <int ZPER, int G>
-__device__ __forceinline__ bool integrate_column_pk(f2v (&T)[ZPER / 2], f2v (&Wt)[ZPER / 2],
-                                                    uint32_t& dirty, bmask_t mask,
-                                                    const f2v (&zs2)[ZPER / 2], float xs, float ys,
-                                                    const float* __restrict__ depths, int64_t HW, int W,
-                                                    float hm1, float wm1, const FrameParams* __restrict__ fps,
-                                                    const int64_t* __restrict__ depth_frame, float depth_max,
-                                                    float sdf_trunc) {
-    const float y0t = __builtin_amdgcn_rcpf(sdf_trunc);
-    const float y1t_s = __builtin_fmaf(__builtin_fmaf(-sdf_trunc, y0t, 1.0f), y0t, y0t);
-    const f2v y1t = splat2(y1t_s), nbt = splat2(-sdf_trunc), one = splat2(1.0f);
-    float zmin = 0x1p100f, zmax = 0.0f;
-    bmask_t m = mask;
-    while (m) {
-        const int f = __builtin_ctzll(m);
-        m &= m - 1;
-        const FrameParams& fp = fps[f];
-        const float* __restrict__ dep = depths + depth_frame[f] * HW;
-        const f2v ax = splat2(xs * fp.ext[0] + ys * fp.ext[1]);
-        const f2v ay = splat2(xs * fp.ext[4] + ys * fp.ext[5]);
-        const f2v az = splat2(xs * fp.ext[8] + ys * fp.ext[9]);
-        const f2v e2 = splat2(fp.ext[2]), e3 = splat2(fp.ext[3]), e6 = splat2(fp.ext[6]);
-        const f2v e7 = splat2(fp.ext[7]), e10 = splat2(fp.ext[10]), e11 = splat2(fp.ext[11]);
-        const f2v fx = splat2(fp.fx), fy = splat2(fp.fy), cx = splat2(fp.cx), cy = splat2(fp.cy);
-#pragma unroll
-        for (int g = 0; g < ZPER; g += G) {
-            constexpr int GP = G / 2;
-            int pix[G];
-            bool in[G];
-            f2v zc[GP];
-#pragma unroll
-            for (int q = 0; q < GP; ++q) {
-                const f2v zz = zs2[g / 2 + q];
-                const f2v xc = (ax + zz * e2) + e3;
-                const f2v yc = (ay + zz * e6) + e7;
-                zc[q] = (az + zz * e10) + e11;
-                zmin = fminf(zmin, fminf(fabsf(zc[q].x), fabsf(zc[q].y)));
-                zmax = fmaxf(zmax, fmaxf(fabsf(zc[q].x), fabsf(zc[q].y)));
-                const f2v inv = rcp_core2(zc[q]);
-                const f2v u = fx * xc * inv + cx;
-                const f2v v = fy * yc * inv + cy;
-#pragma unroll
-                for (int e = 0; e < 2; ++e) {
-                    const float ue = e ? u.y : u.x, ve = e ? v.y : v.x;
-                    const bool ok = ve >= 0 && ue >= 0 && ve <= hm1 && ue <= wm1;
-                    in[2 * q + e] = ok;
-                    pix[2 * q + e] = (int)(ok ? ve : 0.f) * W + (int)(ok ? ue : 0.f);
-                }
-            }
-            float dv[G];
-#pragma unroll
-            for (int j = 0; j < G; ++j) dv[j] = dep[pix[j]];
-#pragma unroll
-            for (int q = 0; q < GP; ++q) {
-                const int qq = g / 2 + q;
-                const f2v d = {dv[2 * q], dv[2 * q + 1]};
-                const f2v sdf = d - zc[q];
-                bool up[2];
-                f2v s;
-#pragma unroll
-                for (int e = 0; e < 2; ++e) {
-                    const float de = e ? d.y : d.x, ze = e ? zc[q].y : zc[q].x, se = e ? sdf.y : sdf.x;
-                    up[e] = !(!in[2 * q + e] || de <= 0 || de > depth_max || ze <= 0 || se < -sdf_trunc);
-                    s[e] = se < sdf_trunc ? se : sdf_trunc;
-                }
-                const f2v sn = div_const2(s, nbt, y1t);
-                const f2v wp = Wt[qq] + one;
-                const f2v nt = (Wt[qq] * T[qq] + sn) * rcp_core2(wp);
-                T[qq].x = up[0] ? nt.x : T[qq].x;
-                T[qq].y = up[1] ? nt.y : T[qq].y;
-                Wt[qq].x = up[0] ? wp.x : Wt[qq].x;
-                Wt[qq].y = up[1] ? wp.y : Wt[qq].y;
-                dirty |= (up[0] ? 1u << (2 * qq) : 0u) | (up[1] ? 2u << (2 * qq) : 0u);
-            }
-        }
-    }
-    return !(zmin >= 0x1p-36f) || zmax > 0x1p60f;
-}
-
-// Packed-f32 integrate (R = 16 / 8, unit depth scale): fast pass with exact block re-run, exact
-// pass directly for blocks whose weights are outside [0, 2^59] (imported volumes).
-template <int R, int G, int NT = 256>
-__global__ __launch_bounds__(NT) void k_integrate_pk(const int32_t* __restrict__ list,
-                                                      const int* __restrict__ counters, int64_t list_cap, Table t,
-                                                      float2* __restrict__ pool, float voxel_size,
-                                                      const float* __restrict__ depths, int64_t HW, int H, int W,
-                                                      const FrameParams* __restrict__ fps,
-                                                      const int64_t* __restrict__ depth_frame, float depth_max,
-                                                      float sdf_trunc) {
-    constexpr int R2 = R * R;
-    constexpr int R3 = R2 * R;
-    constexpr int ZPER = R3 / NT;
-    constexpr int NP = ZPER / 2;
-    constexpr int ZSTEP = NT / R2;
-    static_assert(R3 % NT == 0 && NT % R2 == 0, "NT must divide R^3 and be a multiple of R^2");
-    static_assert(ZPER % G == 0 && G % 2 == 0, "group size must be even and divide the voxels per thread");
-    const int64_t n = min((int64_t)counters[kListCount], list_cap);
-    const float hm1 = (float)H - 1.0f, wm1 = (float)W - 1.0f;
-    const int tid = threadIdx.x;
-    const int xv = tid % R, yv = (tid / R) % R, z0 = tid / R2;
-    for (int64_t i = blockIdx.x; i < n; i += gridDim.x) {
-        const int32_t slot = list[i];
-        const int buf = t.vals[slot];
-        const bmask_t mask = readfirstlane_u64(t.mask[slot]);
-        int xb, yb, zb;
-        unpack_key(t.keys[slot], xb, yb, zb);
-        if (buf >= 0) {
-            float2* vox = pool + (int64_t)buf * R3;
-            float2 tw[ZPER];
-            float zs[ZPER];
-            bool wbad = false;
-#pragma unroll
-            for (int k = 0; k < ZPER; ++k) {
-                tw[k] = vox[k * NT + tid];
-                zs[k] = (float)(zb * R + z0 + k * ZSTEP) * voxel_size;
-                wbad |= !(tw[k].y >= 0.0f && tw[k].y <= 0x1p59f);
-            }
-            const float xs = (float)(xb * R + xv) * voxel_size;
-            const float ys = (float)(yb * R + yv) * voxel_size;
-            uint32_t dirty = 0;
-            bool exact = __syncthreads_or(wbad);
-            if (!exact) {
-                f2v T[NP], Wt[NP], zs2[NP];
-#pragma unroll
-                for (int q = 0; q < NP; ++q) {
-                    T[q] = f2v{tw[2 * q].x, tw[2 * q + 1].x};
-                    Wt[q] = f2v{tw[2 * q].y, tw[2 * q + 1].y};
-                    zs2[q] = f2v{zs[2 * q], zs[2 * q + 1]};
-                }
-                const bool zbad = integrate_column_pk<ZPER, G>(T, Wt, dirty, mask, zs2, xs, ys, depths, HW, W, hm1,
-                                                            wm1, fps, depth_frame, depth_max, sdf_trunc);
-                exact = __syncthreads_or(zbad);
-                if (!exact) {
-#pragma unroll
-                    for (int q = 0; q < NP; ++q) {
-                        tw[2 * q] = make_float2(T[q].x, Wt[q].x);
-                        tw[2 * q + 1] = make_float2(T[q].y, Wt[q].y);
-                    }
-                } else {
-#pragma unroll
-                    for (int k = 0; k < ZPER; ++k) tw[k] = vox[k * NT + tid];
-                    dirty = 0;
-                }
-            }
-            if (exact)
-                integrate_column<ZPER, G, true>(tw, dirty, mask, zs, xs, ys, depths, HW, W, hm1, wm1, fps,
-                                                depth_frame, 1.0f, true, depth_max, sdf_trunc);
-#pragma unroll
-            for (int k = 0; k < ZPER; ++k)
-                if (dirty & (1u << k)) vox[k * NT + tid] = tw[k];
-        }
-        __syncthreads();
-        if (tid == 0) t.mask[slot] = 0;
-    }
-}
-
-// ---- lean integrate (variants 40-47) -----------------------------------------------------------
+// ---- lean integrate ------------------------------------------------------------------------------
 // The exact kernel's arithmetic with (i) shortened reciprocals, (ii) gathers through a raw buffer
 // view (out-of-image voxels read past its end, which returns 0), (iii) predicated updates instead
-// of per-voxel branches and (iv) optionally the next frame's projections and gathers issued before
-// the current frame's updates (PIPE), so a wave keeps ZPER gathers in flight across a whole frame
-// of arithmetic.  Blocks whose operands leave the ranges below are handed to the exact fix-up
-// launch unwritten (as the EXTFIX variants do).
+// of per-voxel branches.  Blocks whose operands leave the ranges below are handed to the exact
+// fix-up launch unwritten.
 //
-// rcp_nm: v_rcp + one Newton step + one Markstein correction (5 VALU);
-// rcp_m:  v_rcp + one Markstein correction (3 VALU).
-// Both are compared with IEEE 1.0f / b over every float of the ranges they are used on
-// (tests/test_gpu_numerics.py, mqr_check_division modes 3 / 4): 1 / zc for 2^-36 <= zc <= 2^60
-// (rcp_nm, or rcp_m when RZ == 2) and 1 / (w + 1) for integer weights w <= 2^23 + 64 (rcp_m).
+// rcp_m:  v_rcp + one Markstein correction (3 VALU);  rcp_nm: v_rcp + one Newton step + one
+// Markstein correction (5 VALU).  Both are compared with IEEE 1.0f / b over every float of the
+// ranges they are used on (tests/test_gpu_numerics.py, mqr_check_division modes 3 / 4): rcp_m for
+// 1 / zc, 2^-60 <= zc <= 2^60, and 1 / (w + 1) for integer weights w <= 2^23 + 64.
 __device__ __forceinline__ float rcp_nm(float b) {
     const float y0 = __builtin_amdgcn_rcpf(b);
     const float y1 = __builtin_fmaf(__builtin_fmaf(-b, y0, 1.0f), y0, y0);
@@ -720,15 +444,15 @@ __device__ __forceinline__ void pool_store(__amdgpu_buffer_rsrc_t rs, uint32_t v
     __builtin_amdgcn_raw_buffer_store_b64(r, rs, voff, soff, 0);
 }
 
-// Projection and gather of one frame for a thread's column -- Open3D's transform and projection,
+// Projection and gather of one frame for a thread's voxels -- Open3D's transform and projection,
 // the same float operations as integrate_column.  An out-of-image voxel gets row H, whose byte
 // offset is >= 4HW, past the end of the frame (host: 4 (HW + W) <= 2^31, so the 24-bit multiply
 // is exact): its depth reads as 0 and fails the update's d > 0 test, exactly like the out-of-image
-// skip (an in-image
-// NaN depth still reaches the update, as in Open3D).  `bad` is set unless 2^-36 <= zc <= 2^60 (zc
-// <= 0 included, which the update would skip anyway): inside that range the reciprocal shortcut is
-// exact and a non-zero sdf = d - zc is >= 2^-60 in magnitude, which keeps the division core exact.
-template <int ZPER, int RZ>
+// skip (an in-image NaN depth still reaches the update, as in Open3D).  `bad` is set unless
+// 2^-36 <= zc <= 2^60 (zc <= 0 included, which the update would skip anyway): inside that range
+// rcp_m is exact and a non-zero sdf = d - zc is >= 2^-60 in magnitude, which keeps the division
+// core exact.
+template <int ZPER>
 __device__ __forceinline__ void lean_gather(float (&dv)[ZPER], bool& bad, const FrameParams& fp,
                                             __amdgpu_buffer_rsrc_t rs, const float (&xs)[ZPER],
                                             const float (&ys)[ZPER], const float (&zs)[ZPER], uint32_t W4, float hf,
@@ -741,16 +465,14 @@ __device__ __forceinline__ void lean_gather(float (&dv)[ZPER], bool& bad, const 
     const float fx = fp.fx, fy = fp.fy, cx = fp.cx, cy = fp.cy;
 #pragma unroll
     for (int k = 0; k < ZPER; ++k) {
-        // z-independent partial products: one per thread in the column mapping (equal operands are
-        // merged by the compiler), one per cube column in the cube mapping
-        const float ax = xs[k] * e[0] + ys[k] * e[1];
+        const float ax = xs[k] * e[0] + ys[k] * e[1];  // equal operands across k are merged
         const float ay = xs[k] * e[4] + ys[k] * e[5];
         const float az = xs[k] * e[8] + ys[k] * e[9];
         const float xc = (ax + zs[k] * e[2]) + e[3];
         const float yc = (ay + zs[k] * e[6]) + e[7];
         const float zc = (az + zs[k] * e[10]) + e[11];
         bad |= (__float_as_uint(zc) - 0x2D800000u) > 0x30000000u;  // not 2^-36 <= zc <= 2^60
-        const float inv_z = RZ == 2 ? rcp_m(zc) : rcp_nm(zc);
+        const float inv_z = rcp_m(zc);
         const float u = fx * xc * inv_z + cx;
         const float v = fy * yc * inv_z + cy;
         const bool in = (v >= 0) & (u >= 0) & (v <= hm1) & (u <= wm1);
@@ -789,412 +511,29 @@ __device__ __forceinline__ void lean_update(float2 (&tw)[ZPER], const float (&dv
     }
 }
 
-// Voxel (x, y, z) of a block handled by thread `tid` as its k-th voxel.  COLUMN: the layout of
-// k_integrate_t (thread = voxel column, a wave = a 16 x 4 slab of one z layer).  CUBE: a wave's 64
-// lanes form a 4 x 4 x 4 voxel cube (lane bits x:0-1, y:2-3, z:4-5) and a thread's voxels walk the
-// cubes of R/4-cube columns, so every gather instruction reads the projection of a compact cube --
-// far fewer distinct cache lines than a slab, which is what bounds the gathers (L1 tag lookups).
-template <int R, int NT, bool CUBE>
-__device__ __forceinline__ void lean_voxel(int tid, int k, int& x, int& y, int& z) {
-    constexpr int R2 = R * R, ZPER = R * R2 / NT;
-    if (CUBE) {
-        constexpr int C = R / 4, CPT = ZPER / C;  // cubes per axis, cube columns per thread
-        static_assert(R % 4 == 0 && ZPER % C == 0 && (NT / 64) * CPT == C * C, "cube mapping does not tile");
-        const int w = tid >> 6, l = tid & 63, cxy = w * CPT + k / C;
-        x = 4 * (cxy % C) + (l & 3);
-        y = 4 * (cxy / C) + ((l >> 2) & 3);
-        z = 4 * (k % C) + (l >> 4);
-    } else {
-        x = tid % R;
-        y = (tid / R) % R;
-        z = tid / R2 + k * (NT / R2);
-    }
+// Hand a block to the exact fix-up launch (its (slot, batch mask) appended to bad_out).
+__device__ __forceinline__ void hand_off(int32_t* bad_out, int* counters, int64_t list_cap, int32_t slot,
+                                         bmask_t mask) {
+    const int j = atomicAdd(&counters[kBadCount], 1);
+    bad_out[j] = slot;
+    reinterpret_cast<bmask_t*>(bad_out + list_cap)[j] = mask;
 }
 
 // Lean integrate, unit depth scale only (host: sdf_trunc in the division core's range).  Block per
-// workgroup as in k_integrate_t; every voxel of a block that is not handed off is written back.
-template <int R, int NT, bool PIPE, int RZ, int WPE = 1, bool CUBE = false>
-__global__ __launch_bounds__(NT, WPE) void k_integrate_lean(const int32_t* __restrict__ list,
-                                                        const bmask_t* __restrict__ lmask,
-                                                        int32_t* __restrict__ bad_out, int* __restrict__ counters,
-                                                        int64_t list_cap, Table t, float2* __restrict__ pool,
-                                                        float voxel_size, const float* __restrict__ depths,
-                                                        int64_t HW, int H, int W,
-                                                        const FrameParams* __restrict__ fps,
-                                                        const int64_t* __restrict__ depth_frame, float depth_max,
-                                                        float sdf_trunc) {
-    constexpr int R2 = R * R;
-    constexpr int R3 = R2 * R;
-    constexpr int ZPER = R3 / NT;
-    static_assert(R3 % NT == 0 && NT % R2 == 0, "NT must divide R^3 and be a multiple of R^2");
-    const int64_t n = min((int64_t)counters[kListCount], list_cap);
-    const float hf = (float)H, hm1 = (float)H - 1.0f, wm1 = (float)W - 1.0f;
-    const uint32_t W4 = 4u * (uint32_t)W, bytes = 4u * (uint32_t)HW;
-    const float y0t = __builtin_amdgcn_rcpf(sdf_trunc);
-    const float y1t = __builtin_fmaf(__builtin_fmaf(-sdf_trunc, y0t, 1.0f), y0t, y0t);
-    const int tid = threadIdx.x;
-    for (int64_t i = blockIdx.x; i < n; i += gridDim.x) {
-        const int32_t slot = list[i];
-        const int buf = t.vals[slot];
-        const bmask_t mask = readfirstlane_u64(lmask ? lmask[i] : t.mask[slot]);
-        int xb, yb, zb;
-        unpack_key(t.keys[slot], xb, yb, zb);
-        if (buf >= 0 && mask) {
-            const __amdgpu_buffer_rsrc_t vox = __builtin_amdgcn_make_buffer_rsrc(
-                pool + (int64_t)buf * R3, (short)0, (int)(R3 * sizeof(float2)), 0x00020000);
-            float2 tw[ZPER];
-            float xs[ZPER], ys[ZPER], zs[ZPER];
-            bool bad = false;
-            // column mapping: one (x, y) per thread, shared by all its voxels (one value, not ZPER copies)
-            const float xs0 = (float)(xb * R + tid % R) * voxel_size;
-            const float ys0 = (float)(yb * R + (tid / R) % R) * voxel_size;
-#pragma unroll
-            for (int k = 0; k < ZPER; ++k) {
-                int x, y, z;
-                lean_voxel<R, NT, CUBE>(tid, k, x, y, z);
-                // column mapping: voxel k * NT + tid, i.e. one VGPR offset and a constant per voxel
-                tw[k] = CUBE ? pool_load(vox, 8u * (uint32_t)(z * R2 + y * R + x), 0)
-                             : pool_load(vox, 8u * (uint32_t)tid, k * NT * (int)sizeof(float2));
-                xs[k] = CUBE ? (float)(xb * R + x) * voxel_size : xs0;
-                ys[k] = CUBE ? (float)(yb * R + y) * voxel_size : ys0;
-                zs[k] = (float)(zb * R + z) * voxel_size;
-                const float w = tw[k].y;  // rcp_m(w + 1) needs integer weights (a batch adds <= 64)
-                bad |= !(w >= 0.0f && w <= 0x1p23f && w == __builtin_truncf(w));
-            }
-            bmask_t m = mask;
-            int f = __builtin_ctzll(m);
-            m &= m - 1;
-            float da[ZPER], db[ZPER];
-            lean_gather<ZPER, RZ>(da, bad, fps[f], frame_rsrc(depths + depth_frame[f] * HW, bytes), xs, ys, zs, W4,
-                                  hf, hm1, wm1);
-            // PIPE: the next frame's projections and gathers are issued before this frame's updates
-            while (true) {
-                const bool more = m != 0;  // wave-uniform
-                const int g = more ? __builtin_ctzll(m) : 0;
-                m &= m - 1;
-                if (PIPE && more)
-                    lean_gather<ZPER, RZ>(db, bad, fps[g], frame_rsrc(depths + depth_frame[g] * HW, bytes), xs, ys,
-                                          zs, W4, hf, hm1, wm1);
-                lean_update<ZPER>(tw, da, fps[f], xs, ys, zs, depth_max, sdf_trunc, y1t);
-                if (!more) break;
-                if (PIPE) {
-#pragma unroll
-                    for (int k = 0; k < ZPER; ++k) da[k] = db[k];
-                } else {
-                    lean_gather<ZPER, RZ>(da, bad, fps[g], frame_rsrc(depths + depth_frame[g] * HW, bytes), xs, ys,
-                                          zs, W4, hf, hm1, wm1);
-                }
-                f = g;
-            }
-            if (__syncthreads_or(bad)) {  // block-uniform: the exact fix-up launch redoes it from the pool
-                if (tid == 0) {
-                    const int j = atomicAdd(&counters[kBadCount], 1);
-                    bad_out[j] = slot;
-                    reinterpret_cast<bmask_t*>(bad_out + list_cap)[j] = mask;
-                }
-            } else {
-#pragma unroll
-                for (int k = 0; k < ZPER; ++k) {
-                    int x, y, z;
-                    lean_voxel<R, NT, CUBE>(tid, k, x, y, z);
-                    if (CUBE)
-                        pool_store(vox, 8u * (uint32_t)(z * R2 + y * R + x), 0, tw[k]);
-                    else
-                        pool_store(vox, 8u * (uint32_t)tid, k * NT * (int)sizeof(float2), tw[k]);
-                }
-            }
-        }
-        __syncthreads();
-        if (tid == 0) t.mask[slot] = 0;
-    }
-}
-
-// ---- tiled lean integrate (variants 56-57) ------------------------------------------------------
-// The lean kernel spends its time in the L1 (one tag lookup per distinct line per gather lane group:
-// ~46 per 64-lane depth gather, rocprofv3 TCP_TOTAL_CACHE_ACCESSES).  Here the depth rectangle a
-// block projects to is copied into LDS once per (block, frame) with row-coalesced loads and the
-// voxel gathers read LDS.  The depth values are the same, so the result is the lean kernel's.
-constexpr int kTilePx = 12288;  // 48 KiB of depth per workgroup
-
-// Conservative pixel rectangle of block (xb, yb, zb)'s projection into one frame, computed by one
-// whole wave: the 8 corner voxel centres are projected with the kernel's own operations (corner =
-// lane & 7), padded by 2 px and clamped to the image.  Voxel centres inside the block project into
-// the convex hull of the corners when every corner is in front of the camera (float rounding moves
-// a projection by far less than the pad); a voxel that still falls outside reads global memory.
-// rect = {u0, v0, width, height}; width 0 = no tile (a corner not in 2^-36 <= zc <= 2^60, a
-// non-finite projection, or a rectangle larger than the tile).
-__device__ __forceinline__ void block_rect(const FrameParams& fp, int xb, int yb, int zb, int R, float voxel_size,
-                                           int H, int W, int (&rect)[4]) {
-    const int c = threadIdx.x & 7;
-    const float xs = (float)(xb * R + (c & 1) * (R - 1)) * voxel_size;
-    const float ys = (float)(yb * R + ((c >> 1) & 1) * (R - 1)) * voxel_size;
-    const float zs = (float)(zb * R + ((c >> 2) & 1) * (R - 1)) * voxel_size;
-    const float xc = ((xs * fp.ext[0] + ys * fp.ext[1]) + zs * fp.ext[2]) + fp.ext[3];
-    const float yc = ((xs * fp.ext[4] + ys * fp.ext[5]) + zs * fp.ext[6]) + fp.ext[7];
-    const float zc = ((xs * fp.ext[8] + ys * fp.ext[9]) + zs * fp.ext[10]) + fp.ext[11];
-    const float inv_z = rcp_m(zc);
-    const float u = fp.fx * xc * inv_z + fp.cx;
-    const float v = fp.fy * yc * inv_z + fp.cy;
-    const bool ok = zc >= 0x1p-36f && zc <= 0x1p60f && fabsf(u) < 1e7f && fabsf(v) < 1e7f;
-    float umin = u, umax = u, vmin = v, vmax = v;
-#pragma unroll
-    for (int o = 4; o >= 1; o >>= 1) {
-        umin = fminf(umin, __shfl_xor(umin, o, 64));
-        umax = fmaxf(umax, __shfl_xor(umax, o, 64));
-        vmin = fminf(vmin, __shfl_xor(vmin, o, 64));
-        vmax = fmaxf(vmax, __shfl_xor(vmax, o, 64));
-    }
-    const int u0 = max(0, (int)floorf(umin) - 2), u1 = min(W - 1, (int)floorf(umax) + 2);
-    const int v0 = max(0, (int)floorf(vmin) - 2), v1 = min(H - 1, (int)floorf(vmax) + 2);
-    const int tw = max(u1 - u0 + 1, 0), th = max(v1 - v0 + 1, 0);
-    const bool use = __ballot(!ok) == 0 && tw * th <= kTilePx;
-    rect[0] = u0;
-    rect[1] = v0;
-    rect[2] = use ? tw : 0;
-    rect[3] = use ? th : 0;
-}
-
-// lean_gather with the depth read from the staged rectangle (global memory for an in-image voxel
-// outside it, 0 for an out-of-image voxel).
-template <int ZPER>
-__device__ __forceinline__ void lean_gather_tile(float (&dv)[ZPER], bool& bad, const FrameParams& fp,
-                                                 const float* __restrict__ dep, const float* tile, int u0, int v0,
-                                                 int tlw, int tlh, const float (&xs)[ZPER], const float (&ys)[ZPER],
-                                                 const float (&zs)[ZPER], int W, float hf, float hm1, float wm1) {
-#pragma unroll
-    for (int k = 0; k < ZPER; ++k) {
-        const float ax = xs[k] * fp.ext[0] + ys[k] * fp.ext[1];
-        const float ay = xs[k] * fp.ext[4] + ys[k] * fp.ext[5];
-        const float az = xs[k] * fp.ext[8] + ys[k] * fp.ext[9];
-        const float xc = (ax + zs[k] * fp.ext[2]) + fp.ext[3];
-        const float yc = (ay + zs[k] * fp.ext[6]) + fp.ext[7];
-        const float zc = (az + zs[k] * fp.ext[10]) + fp.ext[11];
-        bad |= (__float_as_uint(zc) - 0x2D800000u) > 0x30000000u;  // not 2^-36 <= zc <= 2^60
-        const float inv_z = rcp_m(zc);
-        const float u = fp.fx * xc * inv_z + fp.cx;
-        const float v = fp.fy * yc * inv_z + fp.cy;
-        const bool in = (v >= 0) & (u >= 0) & (v <= hm1) & (u <= wm1);
-        const int ui = (int)(in ? u : 0.f), vi = (int)(in ? v : hf);
-        const uint32_t tu = (uint32_t)(ui - u0), tv = (uint32_t)(vi - v0);  // row H never lies in the tile
-        float d = 0.f;
-        if (tu < (uint32_t)tlw && tv < (uint32_t)tlh)
-            d = tile[__umul24(tv, (uint32_t)tlw) + tu];
-        else if (in)
-            d = dep[vi * W + ui];
-        dv[k] = d;
-        __builtin_amdgcn_sched_barrier(0);
-    }
-}
-
-// Tiled lean integrate (column mapping, RZ = 2; same preconditions and fix-up hand-off as the lean
-// kernel).  Per (block, frame): wave 0 computes the rectangle, the workgroup copies it into LDS
-// (one wave per row, lanes along the row), then every thread gathers and updates its voxels.
+// workgroup, column mapping as k_integrate_t; every voxel of a block not handed off is written back.
 template <int R, int NT>
-__global__ __launch_bounds__(NT) void k_integrate_tile(const int32_t* __restrict__ list,
-                                                      const bmask_t* __restrict__ lmask,
-                                                      int32_t* __restrict__ bad_out, int* __restrict__ counters,
-                                                      int64_t list_cap, Table t, float2* __restrict__ pool,
-                                                      float voxel_size, const float* __restrict__ depths, int64_t HW,
-                                                      int H, int W, const FrameParams* __restrict__ fps,
-                                                      const int64_t* __restrict__ depth_frame, float depth_max,
-                                                      float sdf_trunc) {
+__global__ __launch_bounds__(NT) void k_integrate_lean(const int32_t* __restrict__ list,
+                                                       const bmask_t* __restrict__ lmask,
+                                                       int32_t* __restrict__ bad_out, int* __restrict__ counters,
+                                                       int64_t list_cap, Table t, float2* __restrict__ pool,
+                                                       float voxel_size, const float* __restrict__ depths,
+                                                       int64_t HW, int H, int W, const FrameParams* __restrict__ fps,
+                                                       const int64_t* __restrict__ depth_frame, float depth_max,
+                                                       float sdf_trunc) {
     constexpr int R2 = R * R;
     constexpr int R3 = R2 * R;
     constexpr int ZPER = R3 / NT;
-    constexpr int NW = NT / 64;
     static_assert(R3 % NT == 0 && NT % R2 == 0, "NT must divide R^3 and be a multiple of R^2");
-    __shared__ float tile[kTilePx];
-    __shared__ int s_rect[4];
-    const int64_t n = min((int64_t)counters[kListCount], list_cap);
-    const float hf = (float)H, hm1 = (float)H - 1.0f, wm1 = (float)W - 1.0f;
-    const float y0t = __builtin_amdgcn_rcpf(sdf_trunc);
-    const float y1t = __builtin_fmaf(__builtin_fmaf(-sdf_trunc, y0t, 1.0f), y0t, y0t);
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    for (int64_t i = blockIdx.x; i < n; i += gridDim.x) {
-        const int32_t slot = list[i];
-        const int buf = t.vals[slot];
-        const bmask_t mask = readfirstlane_u64(lmask ? lmask[i] : t.mask[slot]);
-        int xb, yb, zb;
-        unpack_key(t.keys[slot], xb, yb, zb);
-        if (buf >= 0 && mask) {
-            const __amdgpu_buffer_rsrc_t vox = __builtin_amdgcn_make_buffer_rsrc(
-                pool + (int64_t)buf * R3, (short)0, (int)(R3 * sizeof(float2)), 0x00020000);
-            float2 tw[ZPER];
-            float xs[ZPER], ys[ZPER], zs[ZPER];
-            bool bad = false;
-#pragma unroll
-            for (int k = 0; k < ZPER; ++k) {
-                int x, y, z;
-                lean_voxel<R, NT, false>(tid, k, x, y, z);
-                tw[k] = pool_load(vox, 8u * (uint32_t)(z * R2 + y * R + x), 0);
-                xs[k] = (float)(xb * R + x) * voxel_size;
-                ys[k] = (float)(yb * R + y) * voxel_size;
-                zs[k] = (float)(zb * R + z) * voxel_size;
-                const float w = tw[k].y;
-                bad |= !(w >= 0.0f && w <= 0x1p23f && w == __builtin_truncf(w));
-            }
-            bmask_t m = mask;
-            while (m) {
-                const int f = __builtin_ctzll(m);
-                m &= m - 1;
-                const FrameParams& fp = fps[f];
-                const float* __restrict__ dep = depths + depth_frame[f] * HW;
-                if (wave == 0) {
-                    int rect[4];
-                    block_rect(fp, xb, yb, zb, R, voxel_size, H, W, rect);
-                    if (lane < 4) s_rect[lane] = rect[lane];
-                }
-                __syncthreads();  // the rectangle is out, and every wave is done with the last tile
-                const int u0 = __builtin_amdgcn_readfirstlane(s_rect[0]), v0 = __builtin_amdgcn_readfirstlane(s_rect[1]);
-                const int tlw = __builtin_amdgcn_readfirstlane(s_rect[2]);
-                const int tlh = __builtin_amdgcn_readfirstlane(s_rect[3]);
-                for (int r = wave; r < tlh; r += NW) {
-                    const float* src = dep + (int64_t)(v0 + r) * W + u0;
-                    for (int c = lane; c < tlw; c += 64) tile[r * tlw + c] = src[c];
-                }
-                __syncthreads();
-                float dv[ZPER];
-                lean_gather_tile<ZPER>(dv, bad, fp, dep, tile, u0, v0, tlw, tlh, xs, ys, zs, W, hf, hm1, wm1);
-                lean_update<ZPER>(tw, dv, fp, xs, ys, zs, depth_max, sdf_trunc, y1t);
-            }
-            if (__syncthreads_or(bad)) {  // block-uniform: the exact fix-up launch redoes it from the pool
-                if (tid == 0) {
-                    const int j = atomicAdd(&counters[kBadCount], 1);
-                    bad_out[j] = slot;
-                    reinterpret_cast<bmask_t*>(bad_out + list_cap)[j] = mask;
-                }
-            } else {
-#pragma unroll
-                for (int k = 0; k < ZPER; ++k) {
-                    int x, y, z;
-                    lean_voxel<R, NT, false>(tid, k, x, y, z);
-                    pool_store(vox, 8u * (uint32_t)(z * R2 + y * R + x), 0, tw[k]);
-                }
-            }
-        }
-        __syncthreads();
-        if (tid == 0) t.mask[slot] = 0;
-    }
-}
-
-// ---- double-buffered tile integrate (variant 58) --------------------------------------------------
-// The lean kernel is bound by the L1 path of its depth gathers: a scattered dword gather costs about
-// one tag lookup per in-image lane (rocprofv3: ~43 TCP accesses and ~34 TA-busy cycles per gather
-// instruction, TA busy ~80 % of the kernel).  Here the rectangle a block projects to (<= 64 x 64 px)
-// is copied into LDS by async row loads (global_load_lds, one wave-instruction per row), the next
-// frame's rectangle while the current frame is integrated, and the voxel gathers read LDS.  Same
-// depth values and arithmetic as the lean kernel.  A frame whose rectangle does not fit (block close
-// to the camera) or whose corners are not safely in front of the camera is gathered directly.
-constexpr int kTileDim = 64;
-typedef __attribute__((address_space(1))) void gvoid_t;
-typedef __attribute__((address_space(3))) void lvoid_t;
-
-// Rectangles of every frame of a block's batch mask in one pass of the workgroup (slot = thread / 8
-// = rank of the frame in the mask, corner = thread % 8; NT >= 256): the 8 corner voxel centres are
-// projected with the kernel's own operations, padded by 2 px and clamped to the image (voxel centres
-// inside the block project into the hull of the corners when all corners are in front of the
-// camera; rounding moves a projection far less than the pad, and a voxel found outside the
-// rectangle sends the block to the exact fix-up launch).  {u0, v0, w, h}; w = -1: gather directly.
-__device__ __forceinline__ void block_rects(const FrameParams* __restrict__ fps, bmask_t mask, int xb, int yb, int zb,
-                                            int R, float voxel_size, int H, int W, int4* s_rect) {
-    const int slot = threadIdx.x >> 3, c = threadIdx.x & 7;
-    bmask_t m = mask;
-    for (int q = 0; q < slot && m; ++q) m &= m - 1;
-    const bool have = m != 0;
-    const FrameParams& fp = fps[have ? __builtin_ctzll(m) : 0];
-    const float xs = (float)(xb * R + (c & 1) * (R - 1)) * voxel_size;
-    const float ys = (float)(yb * R + ((c >> 1) & 1) * (R - 1)) * voxel_size;
-    const float zs = (float)(zb * R + ((c >> 2) & 1) * (R - 1)) * voxel_size;
-    const float xc = ((xs * fp.ext[0] + ys * fp.ext[1]) + zs * fp.ext[2]) + fp.ext[3];
-    const float yc = ((xs * fp.ext[4] + ys * fp.ext[5]) + zs * fp.ext[6]) + fp.ext[7];
-    const float zc = ((xs * fp.ext[8] + ys * fp.ext[9]) + zs * fp.ext[10]) + fp.ext[11];
-    const float inv_z = rcp_m(zc);
-    const float u = fp.fx * xc * inv_z + fp.cx;
-    const float v = fp.fy * yc * inv_z + fp.cy;
-    int ok = zc >= 0x1p-36f && zc <= 0x1p60f && fabsf(u) < 1e7f && fabsf(v) < 1e7f;
-    float umin = u, umax = u, vmin = v, vmax = v;
-#pragma unroll
-    for (int o = 4; o >= 1; o >>= 1) {
-        umin = fminf(umin, __shfl_xor(umin, o, 64));
-        umax = fmaxf(umax, __shfl_xor(umax, o, 64));
-        vmin = fminf(vmin, __shfl_xor(vmin, o, 64));
-        vmax = fmaxf(vmax, __shfl_xor(vmax, o, 64));
-        ok &= __shfl_xor(ok, o, 64);
-    }
-    if (have && c == 0) {
-        int4 r = make_int4(0, 0, -1, 0);
-        if (ok) {
-            const int u0 = max(0, (int)floorf(umin) - 2), u1 = min(W - 1, (int)floorf(umax) + 2);
-            const int v0 = max(0, (int)floorf(vmin) - 2), v1 = min(H - 1, (int)floorf(vmax) + 2);
-            const int w = u1 - u0 + 1, h = v1 - v0 + 1;
-            if (w <= 0 || h <= 0)
-                r = make_int4(0, 0, 0, 0);  // projection outside the image: nothing to stage
-            else if (w <= kTileDim && h <= kTileDim)
-                r = make_int4(u0, v0, w, h);
-        }
-        s_rect[slot] = r;
-    }
-}
-
-// Async copy of a rectangle (w, h > 0, inside the image) into one LDS buffer of row pitch 64: one
-// global_load_lds per row and wave (LDS destination = row base + lane * 4); lanes past the width
-// re-read the last column.
-__device__ __forceinline__ void tile_copy(const float* __restrict__ dep, int W, int4 r, float* buf, int nw) {
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int col = r.x + min(lane, r.z - 1);
-    for (int row = wave; row < r.w; row += nw)
-        __builtin_amdgcn_global_load_lds((gvoid_t*)(dep + (int64_t)(r.y + row) * W + col),
-                                         (lvoid_t*)(buf + row * kTileDim), 4, 0, 0);
-}
-
-// lean_gather reading the staged rectangle; an in-image voxel outside it sets `bad`.
-template <int ZPER>
-__device__ __forceinline__ void tile_gather(float (&dv)[ZPER], bool& bad, const FrameParams& fp, const float* tile,
-                                            int4 r, const float (&xs)[ZPER], const float (&ys)[ZPER],
-                                            const float (&zs)[ZPER], float hm1, float wm1) {
-    float e[12];
-#pragma unroll
-    for (int j = 0; j < 12; ++j) e[j] = fp.ext[j];
-    const float fx = fp.fx, fy = fp.fy, cx = fp.cx, cy = fp.cy;
-#pragma unroll
-    for (int k = 0; k < ZPER; ++k) {
-        const float ax = xs[k] * e[0] + ys[k] * e[1];
-        const float ay = xs[k] * e[4] + ys[k] * e[5];
-        const float az = xs[k] * e[8] + ys[k] * e[9];
-        const float xc = (ax + zs[k] * e[2]) + e[3];
-        const float yc = (ay + zs[k] * e[6]) + e[7];
-        const float zc = (az + zs[k] * e[10]) + e[11];
-        bad |= (__float_as_uint(zc) - 0x2D800000u) > 0x30000000u;  // not 2^-36 <= zc <= 2^60
-        const float inv_z = rcp_m(zc);
-        const float u = fx * xc * inv_z + cx;
-        const float v = fy * yc * inv_z + cy;
-        const bool in = (v >= 0) & (u >= 0) & (v <= hm1) & (u <= wm1);
-        const int ui = (int)(in ? u : 0.f), vi = (int)(in ? v : 0.f);
-        const uint32_t tu = (uint32_t)(ui - r.x), tv = (uint32_t)(vi - r.y);
-        const bool hit = (tu < (uint32_t)r.z) & (tv < (uint32_t)r.w);
-        bad |= in & !hit;
-        const float t = tile[hit ? tv * kTileDim + tu : 0];
-        dv[k] = (in & hit) ? t : 0.f;
-        __builtin_amdgcn_sched_barrier(0);
-    }
-}
-
-template <int R, int NT, int WPE = 1>
-__global__ __launch_bounds__(NT, WPE) void k_integrate_dbt(const int32_t* __restrict__ list,
-                                                     const bmask_t* __restrict__ lmask,
-                                                     int32_t* __restrict__ bad_out, int* __restrict__ counters,
-                                                     int64_t list_cap, Table t, float2* __restrict__ pool,
-                                                     float voxel_size, const float* __restrict__ depths, int64_t HW,
-                                                     int H, int W, const FrameParams* __restrict__ fps,
-                                                     const int64_t* __restrict__ depth_frame, float depth_max,
-                                                     float sdf_trunc) {
-    constexpr int R2 = R * R;
-    constexpr int R3 = R2 * R;
-    constexpr int ZPER = R3 / NT;
-    constexpr int NW = NT / 64;
-    static_assert(R3 % NT == 0 && NT % R2 == 0 && NT >= 8 * kMaxBatch, "layout");
-    __shared__ float tiles[2][kTileDim * kTileDim];
-    __shared__ int4 s_rect[kMaxBatch];
     const int64_t n = min((int64_t)counters[kListCount], list_cap);
     const float hf = (float)H, hm1 = (float)H - 1.0f, wm1 = (float)W - 1.0f;
     const uint32_t W4 = 4u * (uint32_t)W, bytes = 4u * (uint32_t)HW;
@@ -1203,7 +542,7 @@ __global__ __launch_bounds__(NT, WPE) void k_integrate_dbt(const int32_t* __rest
     const int tid = threadIdx.x;
     for (int64_t i = blockIdx.x; i < n; i += gridDim.x) {
         const int32_t slot = list[i];
-        const int buf = t.vals[slot];
+        const int buf = __builtin_amdgcn_readfirstlane(t.vals[slot]);
         const bmask_t mask = readfirstlane_u64(lmask ? lmask[i] : t.mask[slot]);
         int xb, yb, zb;
         unpack_key(t.keys[slot], xb, yb, zb);
@@ -1221,54 +560,350 @@ __global__ __launch_bounds__(NT, WPE) void k_integrate_dbt(const int32_t* __rest
                 xs[k] = xs0;
                 ys[k] = ys0;
                 zs[k] = (float)(zb * R + tid / R2 + k * (NT / R2)) * voxel_size;
-                const float w = tw[k].y;
+                const float w = tw[k].y;  // rcp_m(w + 1) needs integer weights (a batch adds <= 64)
                 bad |= !(w >= 0.0f && w <= 0x1p23f && w == __builtin_truncf(w));
             }
-            block_rects(fps, mask, xb, yb, zb, R, voxel_size, H, W, s_rect);
-            __syncthreads();
             bmask_t m = mask;
-            int f = __builtin_ctzll(m);
-            m &= m - 1;
-            int j = 0;
-            int4 r = s_rect[0];
-            r = make_int4(__builtin_amdgcn_readfirstlane(r.x), __builtin_amdgcn_readfirstlane(r.y),
-                          __builtin_amdgcn_readfirstlane(r.z), __builtin_amdgcn_readfirstlane(r.w));
-            if (r.z > 0 && r.w > 0) tile_copy(depths + depth_frame[f] * HW, W, r, tiles[0], NW);
-            __syncthreads();  // waits for the copy (vmcnt) as well
-            while (true) {
-                const bool more = m != 0;  // wave-uniform
-                const int g = more ? __builtin_ctzll(m) : 0;
+            while (m) {
+                const int f = __builtin_ctzll(m);
                 m &= m - 1;
-                int4 rn = make_int4(0, 0, 0, 0);
-                if (more) {
-                    rn = s_rect[j + 1];
-                    rn = make_int4(__builtin_amdgcn_readfirstlane(rn.x), __builtin_amdgcn_readfirstlane(rn.y),
-                                   __builtin_amdgcn_readfirstlane(rn.z), __builtin_amdgcn_readfirstlane(rn.w));
-                    if (rn.z > 0 && rn.w > 0) tile_copy(depths + depth_frame[g] * HW, W, rn, tiles[(j + 1) & 1], NW);
-                }
                 float dv[ZPER];
-                if (r.z >= 0)
-                    tile_gather<ZPER>(dv, bad, fps[f], tiles[j & 1], r, xs, ys, zs, hm1, wm1);
-                else
-                    lean_gather<ZPER, 2>(dv, bad, fps[f], frame_rsrc(depths + depth_frame[f] * HW, bytes), xs, ys, zs,
-                                         W4, hf, hm1, wm1);
+                lean_gather<ZPER>(dv, bad, fps[f], frame_rsrc(depths + depth_frame[f] * HW, bytes), xs, ys, zs, W4,
+                                  hf, hm1, wm1);
                 lean_update<ZPER>(tw, dv, fps[f], xs, ys, zs, depth_max, sdf_trunc, y1t);
-                if (!more) break;
-                __syncthreads();  // the next rectangle has landed, this one is free
-                f = g;
-                r = rn;
-                ++j;
             }
-            if (__syncthreads_or(bad)) {
-                if (tid == 0) {
-                    const int jj = atomicAdd(&counters[kBadCount], 1);
-                    bad_out[jj] = slot;
-                    reinterpret_cast<bmask_t*>(bad_out + list_cap)[jj] = mask;
-                }
+            if (__syncthreads_or(bad)) {  // block-uniform: the exact fix-up launch redoes it from the pool
+                if (tid == 0) hand_off(bad_out, counters, list_cap, slot, mask);
             } else {
 #pragma unroll
-                for (int k = 0; k < ZPER; ++k) pool_store(vox, 8u * (uint32_t)tid, k * NT * (int)sizeof(float2), tw[k]);
+                for (int k = 0; k < ZPER; ++k)
+                    pool_store(vox, 8u * (uint32_t)tid, k * NT * (int)sizeof(float2), tw[k]);
             }
+        }
+        __syncthreads();
+        if (tid == 0) t.mask[slot] = 0;
+    }
+}
+
+// ---- helpers of the packed / tiled kernels ---------------------------------------------------------
+typedef __attribute__((address_space(1))) void gvoid_t;
+typedef __attribute__((address_space(3))) void lvoid_t;
+
+typedef float f2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2v fma2(f2v a, f2v b, f2v c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f2v splat2(float x) { return f2v{x, x}; }
+// rcp_m of both elements: v_rcp each, the Markstein correction packed
+__device__ __forceinline__ f2v rcp_m2(f2v b) {
+    const f2v one = splat2(1.0f);
+    const f2v y0 = {__builtin_amdgcn_rcpf(b.x), __builtin_amdgcn_rcpf(b.y)};
+    return fma2(fma2(-b, y0, one), y0, y0);
+}
+
+// Index of the j-th (from 0) set bit of m (m has more than j set bits).
+__device__ __forceinline__ int nth_bit(bmask_t m, int j) {
+    uint32_t w = (uint32_t)m;
+    int base = 0;
+    const int c = __popc(w);
+    if (j >= c) {
+        j -= c;
+        base = 32;
+        w = (uint32_t)(m >> 32);
+    }
+#pragma unroll
+    for (int s = 16; s >= 1; s >>= 1) {
+        const int cl = __popc(w & ((1u << s) - 1));
+        if (j >= cl) {
+            j -= cl;
+            w >>= s;
+            base += s;
+        }
+    }
+    return base;
+}
+
+// ---- packed lean integrate ------------------------------------------------------------------------
+// The lean kernel with its arithmetic on voxel pairs (v_pk_mul / v_pk_add / v_pk_fma_f32: two
+// voxels of a thread's column per VALU instruction), the voxels' camera z kept from the projection
+// for the update, and s = min(sdf, trunc) as one v_min (minNum(NaN, t) = t, as the ternary).  Same
+// float operations in the same order per voxel as lean_gather / lean_update: bit-identical.
+template <int ZPER>
+__device__ __forceinline__ void lean_gather_pk(float (&dv)[ZPER], f2v (&zc2)[ZPER / 2], bool& bad,
+                                               const FrameParams& fp, __amdgpu_buffer_rsrc_t rs, float xs, float ys,
+                                               const f2v (&zs2)[ZPER / 2], uint32_t W4, float hf, float hm1,
+                                               float wm1) {
+    float e[12];
+#pragma unroll
+    for (int j = 0; j < 12; ++j) e[j] = fp.ext[j];
+    const f2v AX = splat2(xs * e[0] + ys * e[1]), AY = splat2(xs * e[4] + ys * e[5]);
+    const f2v AZ = splat2(xs * e[8] + ys * e[9]);
+    const f2v FX = splat2(fp.fx), FY = splat2(fp.fy), CX = splat2(fp.cx), CY = splat2(fp.cy);
+#pragma unroll
+    for (int q = 0; q < ZPER / 2; ++q) {
+        const f2v Z = zs2[q];
+        const f2v xc = (AX + Z * splat2(e[2])) + splat2(e[3]);
+        const f2v yc = (AY + Z * splat2(e[6])) + splat2(e[7]);
+        const f2v zc = (AZ + Z * splat2(e[10])) + splat2(e[11]);
+        bad |= (__float_as_uint(zc.x) - 0x2D800000u) > 0x30000000u;  // not 2^-36 <= zc <= 2^60
+        bad |= (__float_as_uint(zc.y) - 0x2D800000u) > 0x30000000u;
+        const f2v inv = rcp_m2(zc);
+        const f2v u = (FX * xc) * inv + CX;
+        const f2v v = (FY * yc) * inv + CY;
+        zc2[q] = zc;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const float uu = u[h], vv = v[h];
+            const bool in = (vv >= 0) & (uu >= 0) & (vv <= hm1) & (uu <= wm1);
+            const int ui = (int)(in ? uu : 0.f), vi = (int)(in ? vv : hf);
+            const uint32_t off = __umul24((uint32_t)vi, W4) + ((uint32_t)ui << 2);
+            dv[2 * q + h] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+template <int ZPER>
+__device__ __forceinline__ void lean_update_pk(f2v (&T)[ZPER / 2], f2v (&Wt)[ZPER / 2], const float (&dv)[ZPER],
+                                               const f2v (&zc2)[ZPER / 2], float depth_max, float sdf_trunc,
+                                               float y1t) {
+    const f2v ONE = splat2(1.0f), Y1T = splat2(y1t), NTR = splat2(-sdf_trunc);
+#pragma unroll
+    for (int q = 0; q < ZPER / 2; ++q) {
+        const f2v d = {dv[2 * q], dv[2 * q + 1]};
+        const f2v sdf = d - zc2[q];
+        const bool up0 = !(d.x <= 0) && !(d.x > depth_max) && !(sdf.x < -sdf_trunc);
+        const bool up1 = !(d.y <= 0) && !(d.y > depth_max) && !(sdf.y < -sdf_trunc);
+        const f2v s = {__builtin_fminf(sdf.x, sdf_trunc), __builtin_fminf(sdf.y, sdf_trunc)};
+        const f2v q0 = s * Y1T;
+        const f2v q1 = fma2(fma2(NTR, q0, s), Y1T, q0);
+        const f2v sn = fma2(fma2(NTR, q1, s), Y1T, q1);
+        const f2v wp = Wt[q] + ONE;
+        const f2v nt = (Wt[q] * T[q] + sn) * rcp_m2(wp);
+        T[q].x = up0 ? nt.x : T[q].x;
+        T[q].y = up1 ? nt.y : T[q].y;
+        Wt[q].x = up0 ? wp.x : Wt[q].x;
+        Wt[q].y = up1 ? wp.y : Wt[q].y;
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+// ---- block-tiled integrate: one LDS depth tile per (block, frame), shared by the workgroup ----------
+// Counters of the lean kernel (tools/pmc_ab.sh) show it bound by the vector-memory address path:
+// every 64-lane depth gather costs ~33 TA cycles and no VMEM instruction costs much under ~16-20,
+// coalesced or not, while VALU has slack (halving VALU with packed math did not move the time).
+// So the lever is VMEM instructions per voxel-frame pair: lean issues one per 64 pairs.  Here the
+// pixel rectangle a whole 16^3 block projects to (<= 68 x 64 px) is copied into LDS with 16-byte
+// LDS-DMA loads (global_load_lds_dwordx4: 17 lanes per 68-px row, ~ceil(17 h / 64) instructions per
+// block and frame, shared by 4096 pairs), double-buffered across the batch's frames with one
+// workgroup barrier per frame, and the voxels read their depth from LDS.  Row pitch 68 floats: rows
+// land 4 banks apart.  Column thread mapping, projection and update arithmetic of the lean kernel
+// (bit-identical).  Rectangles come from the block's 8 corners projected with the kernel's own
+// operations (all voxels lie in their hull when every corner is in front of the camera), padded by
+// 2 px, clamped to the image, the left edge aligned down to 4 px; a frame whose rectangle is too big
+// or whose corners leave [2^-30, 2^50] in z uses direct gathers, one outside the image is skipped.
+constexpr int kTBP = 68;  // tile row pitch in floats (17 chunks of 4 px)
+constexpr int kTBH = 64;  // tile rows
+
+// Projection of a thread's voxel pairs and their depth read from the frame's LDS tile.  INNER: the
+// rectangle keeps 1 px off every image edge, so a voxel inside it is inside the image (no bound
+// test).  A voxel in the image but outside the rectangle sets `bad` (the block is redone exactly;
+// its dv is then irrelevant), so dv needs no select beyond the out-of-image zero.
+template <int NP, bool INNER>
+__device__ __forceinline__ void tb_gather(float (&dv)[2 * NP], f2v (&zc2)[NP], bool& bad, const FrameParams& fp,
+                                          float xs, float ys, const f2v (&zs2)[NP], const float* tile, int rx,
+                                          int ry, uint32_t tw, uint32_t th, float hm1, float wm1) {
+    float e[12];
+#pragma unroll
+    for (int q = 0; q < 12; ++q) e[q] = fp.ext[q];
+    const f2v AX = splat2(xs * e[0] + ys * e[1]), AY = splat2(xs * e[4] + ys * e[5]);
+    const f2v AZ = splat2(xs * e[8] + ys * e[9]);
+    const f2v FX = splat2(fp.fx), FY = splat2(fp.fy), CX = splat2(fp.cx), CY = splat2(fp.cy);
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+        const f2v Z = zs2[q];
+        const f2v xc = (AX + Z * splat2(e[2])) + splat2(e[3]);
+        const f2v yc = (AY + Z * splat2(e[6])) + splat2(e[7]);
+        zc2[q] = (AZ + Z * splat2(e[10])) + splat2(e[11]);
+        const f2v inv = rcp_m2(zc2[q]);
+        const f2v u2 = (FX * xc) * inv + CX;
+        const f2v v2 = (FY * yc) * inv + CY;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const float u = u2[h], v = v2[h];
+            const uint32_t tu = (uint32_t)((int)u - rx), tv = (uint32_t)((int)v - ry);
+            const bool hit = (tu < tw) & (tv < th);
+            const float d = tile[hit ? __umul24(tv, (uint32_t)kTBP) + tu : 0];
+            if (INNER) {
+                bad |= !hit;
+                dv[2 * q + h] = d;
+            } else {
+                const bool in = (v >= 0) & (u >= 0) & (v <= hm1) & (u <= wm1);
+                bad |= in & !hit;
+                dv[2 * q + h] = in ? d : 0.f;
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_integrate_tb(const int32_t* __restrict__ list,
+                                                      const bmask_t* __restrict__ lmask,
+                                                      int32_t* __restrict__ bad_out, int* __restrict__ counters,
+                                                      int64_t list_cap, Table t, float2* __restrict__ pool,
+                                                      float voxel_size, const float* __restrict__ depths,
+                                                      int64_t HW, int H, int W, const FrameParams* __restrict__ fps,
+                                                      const int64_t* __restrict__ depth_frame, float depth_max,
+                                                      float sdf_trunc) {
+    constexpr int R = 16, R2 = R * R, R3 = R2 * R, NT = 512, ZPER = R3 / NT, NP = ZPER / 2;
+    __shared__ __attribute__((aligned(16))) float s_tile[2][kTBH * kTBP];
+    __shared__ int4 s_rect[kMaxBatch];
+    const int64_t n = min((int64_t)counters[kListCount], list_cap);
+    const float hm1 = (float)H - 1.0f, wm1 = (float)W - 1.0f;
+    const float y0t = __builtin_amdgcn_rcpf(sdf_trunc);
+    const float y1t = __builtin_fmaf(__builtin_fmaf(-sdf_trunc, y0t, 1.0f), y0t, y0t);
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    // this lane's part of a tile copy: 64-lane instructions k = wave + 8 i (i < 3) over the tile's
+    // linear 4-px chunks, 17 per row: (row, chunk) of chunk 64 k + lane, fixed for the kernel
+    int crow[3], cchunk[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const int q = 64 * (wave + 8 * i) + lane;
+        crow[i] = q / 17;
+        cchunk[i] = q - 17 * crow[i];
+    }
+    for (int64_t i = blockIdx.x; i < n; i += gridDim.x) {
+        const int32_t slot = list[i];
+        const int buf = __builtin_amdgcn_readfirstlane(t.vals[slot]);
+        const bmask_t mask = readfirstlane_u64(lmask ? lmask[i] : t.mask[slot]);
+        int xb, yb, zb;
+        unpack_key(t.keys[slot], xb, yb, zb);
+        if (buf < 0 || !mask) {  // block-uniform
+            __syncthreads();
+            if (tid == 0) t.mask[slot] = 0;
+            continue;
+        }
+        const __amdgpu_buffer_rsrc_t vox = __builtin_amdgcn_make_buffer_rsrc(
+            pool + (int64_t)buf * R3, (short)0, (int)(R3 * sizeof(float2)), 0x00020000);
+        f2v T[NP], Wt[NP], zs2[NP];
+        bool bad = false;
+        const float xs = (float)(xb * R + tid % R) * voxel_size;
+        const float ys = (float)(yb * R + (tid / R) % R) * voxel_size;
+#pragma unroll
+        for (int k = 0; k < ZPER; ++k) {
+            const float2 a = pool_load(vox, 8u * (uint32_t)tid, k * NT * (int)sizeof(float2));
+            T[k >> 1][k & 1] = a.x;
+            Wt[k >> 1][k & 1] = a.y;
+            zs2[k >> 1][k & 1] = (float)(zb * R + tid / R2 + k * (NT / R2)) * voxel_size;
+            bad |= !(a.y >= 0.0f && a.y <= 0x1p23f && a.y == __builtin_truncf(a.y));  // rcp_m(w + 1) exact
+        }
+        const int nf = __popcll(mask);
+        if (wave == 0) {  // rectangles of every frame of the batch: lane = (frame in pass, corner)
+            const int c = lane & 7, jj = lane >> 3;
+            const float cxs = (float)(xb * R + (c & 1) * (R - 1)) * voxel_size;
+            const float cys = (float)(yb * R + ((c >> 1) & 1) * (R - 1)) * voxel_size;
+            const float czs = (float)(zb * R + (c >> 2) * (R - 1)) * voxel_size;
+            for (int g = 0; g * 8 < nf; ++g) {
+                const int j = g * 8 + jj;
+                const bool have = j < nf;
+                const FrameParams& fp = fps[have ? nth_bit(mask, j) : 0];
+                const float xc = ((cxs * fp.ext[0] + cys * fp.ext[1]) + czs * fp.ext[2]) + fp.ext[3];
+                const float yc = ((cxs * fp.ext[4] + cys * fp.ext[5]) + czs * fp.ext[6]) + fp.ext[7];
+                const float zc = ((cxs * fp.ext[8] + cys * fp.ext[9]) + czs * fp.ext[10]) + fp.ext[11];
+                const float inv = rcp_m(zc);
+                const float u = fp.fx * xc * inv + fp.cx;
+                const float v = fp.fy * yc * inv + fp.cy;
+                int ok = zc >= 0x1p-30f && zc <= 0x1p50f && fabsf(u) < 1e6f && fabsf(v) < 1e6f;
+                float umin = u, umax = u, vmin = v, vmax = v;
+#pragma unroll
+                for (int o = 1; o <= 4; o <<= 1) {
+                    umin = fminf(umin, __shfl_xor(umin, o, 64));
+                    umax = fmaxf(umax, __shfl_xor(umax, o, 64));
+                    vmin = fminf(vmin, __shfl_xor(vmin, o, 64));
+                    vmax = fmaxf(vmax, __shfl_xor(vmax, o, 64));
+                    ok &= __shfl_xor(ok, o, 64);
+                }
+                if (have && c == 0) {
+                    // x = left column (aligned to 4 px), y = top row, z = width (0: outside the image,
+                    // -1: direct gathers), w = height | 0x10000 when the rectangle keeps 1 px off every
+                    // image edge (then a voxel inside it is inside the image: no per-voxel bound test)
+                    int4 r = make_int4(0, 0, -1, 0);
+                    if (ok) {
+                        const int u0 = max(0, (int)floorf(umin) - 2) & ~3, u1 = min(W - 1, (int)floorf(umax) + 2);
+                        const int v0 = max(0, (int)floorf(vmin) - 2), v1 = min(H - 1, (int)floorf(vmax) + 2);
+                        const int w = u1 - u0 + 1, h = v1 - v0 + 1;
+                        const bool inner = u0 >= 1 && u1 <= W - 2 && v0 >= 1 && v1 <= H - 2;
+                        if (w <= 0 || h <= 0)
+                            r = make_int4(0, 0, 0, 0);
+                        else if (w <= kTBP && h <= kTBH)
+                            r = make_int4(u0, v0, w, h | (inner ? 0x10000 : 0));
+                    }
+                    s_rect[j] = r;
+                }
+            }
+        }
+        __syncthreads();
+        bmask_t m = mask;
+        int f = __builtin_ctzll(m);
+        m &= m - 1;
+        int4 r = s_rect[0];
+        r = make_int4(__builtin_amdgcn_readfirstlane(r.x), __builtin_amdgcn_readfirstlane(r.y),
+                      __builtin_amdgcn_readfirstlane(r.z), __builtin_amdgcn_readfirstlane(r.w));
+        auto stage = [&](int fr, int4 rr, float* tile) {  // lanes past the last row re-read row 0 (never hit)
+            asm volatile("" ::: "memory");
+            const int h = rr.w & 0xffff;
+            const float* dep = depths + depth_frame[fr] * HW;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                const int k = wave + 8 * c;
+                if (64 * k < 17 * h) {
+                    const int gr = rr.y + (crow[c] < h ? crow[c] : 0);
+                    const int gc = min(rr.x + 4 * cchunk[c], W - 4);
+                    __builtin_amdgcn_global_load_lds((gvoid_t*)(dep + (int64_t)gr * W + gc), (lvoid_t*)(tile + 256 * k),
+                                                     16, 0, 0);
+                }
+            }
+        };
+        if (r.z > 0) stage(f, r, s_tile[0]);
+        for (int j = 0; j < nf; ++j) {
+            const bool more = j + 1 < nf;  // block-uniform
+            const int g = more ? __builtin_ctzll(m) : 0;
+            m &= m - 1;
+            int4 rn = make_int4(0, 0, 0, 0);
+            if (more) {
+                rn = s_rect[j + 1];
+                rn = make_int4(__builtin_amdgcn_readfirstlane(rn.x), __builtin_amdgcn_readfirstlane(rn.y),
+                               __builtin_amdgcn_readfirstlane(rn.z), __builtin_amdgcn_readfirstlane(rn.w));
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's part of frame j's tile has landed
+            __syncthreads();  // ... every wave's part; and every wave is done reading frame j-1's buffer
+            if (rn.z > 0) stage(g, rn, s_tile[(j + 1) & 1]);
+            if (r.z != 0) {
+                float dv[ZPER];
+                f2v zc2[NP];
+                if (r.z > 0) {
+                    const float* tile = s_tile[j & 1];
+                    if (r.w >> 16)
+                        tb_gather<NP, true>(dv, zc2, bad, fps[f], xs, ys, zs2, tile, r.x, r.y, (uint32_t)r.z,
+                                            (uint32_t)(r.w & 0xffff), hm1, wm1);
+                    else
+                        tb_gather<NP, false>(dv, zc2, bad, fps[f], xs, ys, zs2, tile, r.x, r.y, (uint32_t)r.z,
+                                             (uint32_t)(r.w & 0xffff), hm1, wm1);
+                } else {  // direct gathers (the lean kernel's, with its per-voxel zc check)
+                    lean_gather_pk<ZPER>(dv, zc2, bad, fps[f], frame_rsrc(depths + depth_frame[f] * HW,
+                                                                           4u * (uint32_t)HW),
+                                         xs, ys, zs2, 4u * (uint32_t)W, (float)H, hm1, wm1);
+                }
+                lean_update_pk<ZPER>(T, Wt, dv, zc2, depth_max, sdf_trunc, y1t);
+            }
+            f = g;
+            r = rn;
+        }
+        if (__syncthreads_or(bad)) {  // block-uniform: the exact fix-up launch redoes it from the pool
+            if (tid == 0) hand_off(bad_out, counters, list_cap, slot, mask);
+        } else {
+#pragma unroll
+            for (int k = 0; k < ZPER; ++k)
+                pool_store(vox, 8u * (uint32_t)tid, k * NT * (int)sizeof(float2),
+                           make_float2(T[k >> 1][k & 1], Wt[k >> 1][k & 1]));
         }
         __syncthreads();
         if (tid == 0) t.mask[slot] = 0;

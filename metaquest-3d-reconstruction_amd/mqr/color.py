@@ -1,0 +1,63 @@
+"""Per-vertex colour projection from colour keyframes.
+
+The reference colours the extracted mesh with Open3D's colour-map pipeline
+(processing/reconstruction/color_map_optimization/optimize_color_pose.py:24-73): the filtered
+mesh goes into a RaycastingScene, every colour keyframe gets a colour-aligned depth map from
+``raycast_in_color_view`` (utils/o3d_utils.py:324-341), and ``run_rigid_optimizer`` assigns vertex
+colours by visibility-tested averaging (upstream ColorMapUtils.cpp) while it refines the poses.
+The pose optimisation stays OUT of scope; this module is the colour assignment:
+
+    colors, counts = color_vertices(vertices, images, depths, K, T_wc)
+    colors, counts = project_vertex_colors(mesh, images, K, T_wc)   # ray casts the depths first
+
+Both run on the GPU (libmqr_hip.so: k_color_vertices; raycast.hip for the depths).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import MQR_HOST, call, ptr
+
+# Open3D RigidOptimizerOption defaults (maximum_allowable_depth, depth_threshold_for_visibility_check,
+# image_boundary_margin)
+MAX_DEPTH = 2.5
+VISIBILITY_THRESHOLD = 0.03
+MARGIN = 10
+
+
+def color_vertices(vertices, images, depths, K, T_wc, max_depth=MAX_DEPTH,
+                   visibility_threshold=VISIBILITY_THRESHOLD, margin=MARGIN, device=0):
+    """vertices (V,3) float32; images (N,H,W,3) uint8 RGB; depths (N,H,W) float32 colour-aligned
+    depth; K (N,3,3), T_wc (N,4,4) world->camera.  Returns (colours (V,3) float32 in [0,1],
+    counts (V,) int32 = keyframes averaged)."""
+    V = np.ascontiguousarray(vertices, dtype=np.float32).reshape(-1, 3)
+    im = np.ascontiguousarray(images, dtype=np.uint8)
+    if im.ndim != 4 or im.shape[3] != 3:
+        raise ValueError(f"images must be (N,H,W,3) uint8, got {im.shape}")
+    N, H, W = im.shape[:3]
+    d = np.ascontiguousarray(depths, dtype=np.float32).reshape(N, H, W)
+    Kd = np.ascontiguousarray(K, dtype=np.float64).reshape(N, 9)
+    Td = np.ascontiguousarray(T_wc, dtype=np.float64).reshape(N, 16)
+    out = np.empty((len(V), 3), np.float32)
+    cnt = np.empty(len(V), np.int32)
+    call("mqr_color_vertices", int(device), ptr(V), len(V), MQR_HOST, ptr(im), ptr(d), MQR_HOST, N, H, W,
+         ptr(Kd, _lib._f64p), ptr(Td, _lib._f64p), float(max_depth), float(visibility_threshold), int(margin),
+         ptr(out), ptr(cnt), MQR_HOST)
+    return out, cnt
+
+
+def project_vertex_colors(mesh, images, K, T_wc, device=0, **kw):
+    """Ray-cast each keyframe's colour-aligned depth from `mesh` (raycast_in_color_view), then
+    average the keyframe colours per vertex.  Returns (colours, counts)."""
+    from .raycasting import RaycastingScene, _mesh_arrays
+    v, t = _mesh_arrays(mesh)
+    im = np.asarray(images)
+    N, H, W = im.shape[:3]
+    scene = RaycastingScene(device=device)
+    scene.add_triangles(v, t)
+    depth = scene.cast_pinhole(np.asarray(K, np.float64).reshape(N, 3, 3), np.asarray(T_wc, np.float64).reshape(N, 4, 4),
+                               W, H)["t_hit"].numpy()
+    return color_vertices(v, im, depth, K, T_wc, device=device, **kw)

@@ -197,6 +197,25 @@ def make_sequence_fast(scene="room", poses=None, n=500, height=480, width=640, f
             "unity": unity, "tangents": (l, r, t, b), "near": near, "far": far, "width": width, "height": height}
 
 
+def texture(points):
+    """Analytic RGB texture of the procedural scenes at world points (..., 3) -> (..., 3) in [0, 1]."""
+    p = np.asarray(points, np.float64)
+    return np.stack([0.5 + 0.5 * np.sin(7.0 * p[..., 0] + 1.0), 0.5 + 0.5 * np.sin(5.0 * p[..., 1] + 2.0),
+                     0.5 + 0.5 * np.sin(3.0 * p[..., 2] + 3.0)], axis=-1)
+
+
+def render_color(scene, K, R, t, height, width):
+    """uint8 RGB colour frame of `scene` from an Open3D camera (R cam->world, t eye), texture() at
+    each pixel's hit point (black where nothing is hit); same pinhole model as render_depth."""
+    z = render_depth(SCENES[scene] if isinstance(scene, str) else scene, K, R, t, height, width).astype(np.float64)
+    fx, fy, cx, cy = K[0, 0], K[1, 1], K[0, 2], K[1, 2]
+    v, u = np.mgrid[0:height, 0:width]
+    dc = np.stack([(u - cx) / fx, (v - cy) / fy, np.ones_like(u, dtype=np.float64)], axis=-1)
+    pw = (dc * z[..., None]) @ np.asarray(R).T + np.asarray(t)
+    rgb = np.where((z > 0)[..., None], texture(pw), 0.0)
+    return np.clip(np.round(rgb * 255.0), 0, 255).astype(np.uint8)
+
+
 def corrupt(z, rng, sigma_rel=0.002, dropout=0.01):
     z = z.astype(np.float64)
     noisy = z + rng.standard_normal(z.shape) * sigma_rel * z

@@ -23,7 +23,7 @@
  *       estimate_depth_confidences.py:15-79 (build_confidence_map).
  *     numpy's dtype promotion is mirrored exactly (float64 arithmetic, float32 rounding of
  *     the interpolated depth and of the error) and the result is pinned by golden vectors
- *     generated from the reference itself (tests/golden/, oracle/gen_golden.py).
+ *     generated from the reference itself (tests/golden/, tests/golden/make_golden.py).
  *
  * Build: see oracle/Makefile (gcc -O2 -ffp-contract=off -fopenmp).  No FMA contraction, so
  * every float op rounds exactly as written -- the HIP library is compiled the same way.
@@ -688,6 +688,54 @@ int orc_raycast(const float* V, int64_t nv, const int32_t* T, int64_t nt, const 
         }
         t_hit[r] = (float)best;
         if (prim) prim[r] = bp;
+    }
+    return 0;
+}
+
+/* ------------------------------------------------------------------ per-vertex colour (row f1)
+ * The colour averaging of Open3D's colour-map pipeline as the reference feeds it
+ * (optimize_color_pose.py:24-73: extracted mesh + colour keyframes + ray-cast colour-aligned
+ * depth -> run_rigid_optimizer); upstream ColorMapUtils.cpp CreateVertexAndImageVisibility +
+ * SetGeometryColorAverage, recalled (Open3D is not installed here: parity unpinned, VERIFY).
+ * Float64 projection Vt = T [X 1], u = float(Vt.x fx / Vt.z + cx), v likewise, d = float(Vt.z);
+ * visible iff d >= 0, (round u, round v) in the image, depth there <= max_depth and
+ * |d - depth| < thr; sampled iff also margin <= u < W - margin, margin <= v < H - margin;
+ * colour = mean of rgb / 255 over sampled keyframes (float64 sums in keyframe order), 0 if none.
+ * The depth-discontinuity mask and the knn fill of unseen vertices are not restated. */
+int orc_color_vertices(const float* V, int64_t nv, const uint8_t* images, const float* depths, int N, int H, int W,
+                       const double* K, const double* T, double max_depth, double thr, int margin, float* out,
+                       int32_t* counts) {
+    const int64_t HW = (int64_t)H * W;
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < nv; ++i) {
+        const double X = V[3 * i], Y = V[3 * i + 1], Z = V[3 * i + 2];
+        double sr = 0.0, sg = 0.0, sb = 0.0;
+        int cnt = 0;
+        for (int c = 0; c < N; ++c) {
+            const double* E = T + 16 * c;
+            const double vx = E[0] * X + E[1] * Y + E[2] * Z + E[3];
+            const double vy = E[4] * X + E[5] * Y + E[6] * Z + E[7];
+            const double vz = E[8] * X + E[9] * Y + E[10] * Z + E[11];
+            const float u = (float)((vx * K[9 * c]) / vz + K[9 * c + 2]);
+            const float v = (float)((vy * K[9 * c + 4]) / vz + K[9 * c + 5]);
+            const float d = (float)vz;
+            const int ui = (int)roundf(u), vi = (int)roundf(v);
+            if (d < 0.0f || ui < 0 || ui >= W || vi < 0 || vi >= H) continue;
+            const int64_t px = (int64_t)c * HW + (int64_t)vi * W + ui;
+            const float ds = depths[px];
+            if (ds > max_depth) continue;
+            if (!((double)fabsf(d - ds) < thr)) continue;
+            if (!(u >= margin && u < W - margin && v >= margin && v < H - margin)) continue;
+            const uint8_t* p = images + 3 * px;
+            sr += p[0] / 255.0;
+            sg += p[1] / 255.0;
+            sb += p[2] / 255.0;
+            ++cnt;
+        }
+        out[3 * i] = cnt ? (float)(sr / cnt) : 0.f;
+        out[3 * i + 1] = cnt ? (float)(sg / cnt) : 0.f;
+        out[3 * i + 2] = cnt ? (float)(sb / cnt) : 0.f;
+        if (counts) counts[i] = cnt;
     }
     return 0;
 }

@@ -68,6 +68,9 @@ def lib():
                                      ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_double, _f64p, _i32p]
         L.orc_raycast.restype = ctypes.c_int
         L.orc_raycast.argtypes = [_f32p, ctypes.c_int64, _i32p, ctypes.c_int64, _f32p, ctypes.c_int64, _f32p, _i32p]
+        L.orc_color_vertices.restype = ctypes.c_int
+        L.orc_color_vertices.argtypes = [_f32p, ctypes.c_int64, _u8p, _f32p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                         _f64p, _f64p, ctypes.c_double, ctypes.c_double, ctypes.c_int, _f32p, _i32p]
         _lib = L
     return _lib
 
@@ -218,3 +221,20 @@ def raycast(vertices, triangles, rays):
     lib().orc_raycast(_p(V, _f32p), V.shape[0], _p(T, _i32p), T.shape[0], _p(r, _f32p), r.shape[0], _p(t, _f32p),
                       _p(pr, _i32p))
     return t.reshape(shape), pr.reshape(shape)
+
+
+def color_vertices(vertices, images, depths, K, T_wc, max_depth=2.5, visibility_threshold=0.03, margin=10):
+    """Per-vertex colour averaging over keyframes (colour-map pipeline input, row f1) ->
+    (colours (V,3) float32, counts (V,) int32)."""
+    V = np.ascontiguousarray(vertices, dtype=np.float32).reshape(-1, 3)
+    im = np.ascontiguousarray(images, dtype=np.uint8)
+    N, H, W = im.shape[:3]
+    d = np.ascontiguousarray(depths, dtype=np.float32).reshape(N, H, W)
+    K = np.ascontiguousarray(K, dtype=np.float64).reshape(N, 9)
+    T = np.ascontiguousarray(T_wc, dtype=np.float64).reshape(N, 16)
+    out = np.empty((len(V), 3), np.float32)
+    cnt = np.empty(len(V), np.int32)
+    lib().orc_color_vertices(_p(V, _f32p), len(V), _p(im, _u8p), _p(d, _f32p), N, H, W, _p(K, _f64p), _p(T, _f64p),
+                             float(max_depth), float(visibility_threshold), int(margin), _p(out, _f32p),
+                             _p(cnt, _i32p))
+    return out, cnt

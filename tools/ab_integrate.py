@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Interleaved A/B of integrate-kernel variants on the bench workload (one process, same data).
 
-python tools/ab_integrate.py --variants 0,2,3,4 --rounds 5
+python tools/ab_integrate.py --variants 0,5 --rounds 5
 Prints per-variant median integrate-kernel ms per launch, touch ms, and step ms.
 """
 import argparse

@@ -1,0 +1,37 @@
+#!/bin/bash
+# Counter comparison of integrate-kernel variants (one rocprofv3 --pmc pass per counter group and
+# variant, each under its own time limit) over tools/traffic_workload.py; per-launch means of the
+# kernels matching $KRE go to gpurun_out/pmc_ab.json.  Usage (on the box):
+#   VARIANTS="0 3" bash tools/pmc_ab.sh
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+KRE="${KRE:-k_integrate_(t8|lean)}"
+GROUPS_=("SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_WAVE_CYCLES"
+         "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INST_CYCLES_VMEM_RD TA_BUSY_avr TA_TA_BUSY_sum")
+for v in ${VARIANTS:-0 3}; do
+  i=0
+  for G in "${GROUPS_[@]}"; do
+    i=$((i+1))
+    timeout -s KILL 120 rocprofv3 --pmc $G -d /tmp/pmcab/v$v/p$i -o p --output-format csv -- \
+      python3 tools/traffic_workload.py --variant $v --out pmcab_v$v > gpurun_out/pmcab_v${v}_p$i.log 2>&1 || { tail -5 gpurun_out/pmcab_v${v}_p$i.log; exit 1; }
+  done
+done
+python3 - "$KRE" <<'PY'
+import glob, re, sys, json
+import pandas as pd
+rx = re.compile(sys.argv[1])
+res = {}
+for path in glob.glob("/tmp/pmcab/**/*counter_collection.csv", recursive=True):
+    var = re.search(r"/v(\d+)/", path).group(1)
+    df = pd.read_csv(path)
+    df = df[df["Kernel_Name"].map(lambda n: bool(rx.search(n)))]
+    for (k, c), g in df.groupby(["Kernel_Name", "Counter_Name"]):
+        short = "v" + var + ":" + k.split("(")[0][-40:]
+        res.setdefault(short, {})[c] = float(g["Counter_Value"].mean())
+        res[short]["launches"] = int(len(g))
+with open("gpurun_out/pmc_ab.json", "w") as f:
+    json.dump(res, f, indent=1)
+print(json.dumps(res, indent=1))
+PY
