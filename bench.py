@@ -65,6 +65,7 @@ def parse():
                     help="C4: a fixed 2000-frame LEFT+RIGHT capture (1000 + 1000, stereo baseline 0.064 m) "
                          "split over the ranks (strong scaling) instead of 500 frames per rank")
     ap.add_argument("--strong-frames", type=int, default=1000, help="frames per side in --strong mode")
+    ap.add_argument("--no-c5", action="store_true", help="skip the 1-GPU C5 leg (4000 frames @ 3 mm + colour)")
     return ap.parse_args()
 
 
@@ -273,6 +274,85 @@ def dropin_e2e_leg(seq, frames, device):
                     "o3d_utils.integrate with confidence masking; host file I/O + PCIe included"}
 
 
+def c5_leg(args, device, frames_per_side=2000, voxel=0.003, key_every=40):
+    """C5 on one GPU (BASELINE.json configs[4] minus the 8-GPU split): a 2000 + 2000
+    frame LEFT+RIGHT walk through an 8 x 8 x 3 m hall, 3 mm voxels (R = 16), integrated in
+    reconstruct_scene.py's order (all LEFT, then all RIGHT) into one volume grown from a small
+    capacity (multi-GB pool growth), the mesh extracted at 1.5, and per-vertex colour projected from
+    every key_every-th frame's 640x480 colour image with ray-cast colour-aligned depth."""
+    import numpy as np
+    import torch
+    from mqr import synthetic
+    from mqr.color import color_vertices
+    from mqr.raycasting import RaycastingScene
+    from mqr.vbg import VoxelBlockGrid
+    dev = int(device.index or 0)
+    left = synthetic.hall_loop_poses(frames_per_side)
+    right = [(R_, t_ + R_[:, 0] * 0.064) for R_, t_ in left]
+    poses = left + right
+    t0 = time.perf_counter()
+    seq = synthetic.make_sequence_fast("hall", poses=poses, height=args.height, width=args.width, seed=5,
+                                       device=f"cuda:{dev}")
+    depth = seq["depth_t"].contiguous()
+    gen_s = time.perf_counter() - t0
+    B, H, W = depth.shape
+    K = seq["K"].astype(np.float64)
+    T = seq["T_wc"].astype(np.float64)
+
+    class _P:
+        ptr = ctypes.c_void_p(depth.data_ptr())
+
+    vbg = VoxelBlockGrid(voxel_size=voxel, block_resolution=16, block_count=16384, device=dev)
+    times = []
+    for _ in range(2):
+        vbg.reset()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        vbg.integrate_frames((_P, B, H, W), K, T, depth_scale=1.0, depth_max=args.depth_max,
+                             trunc_voxel_multiplier=args.trunc)
+        torch.cuda.synchronize()
+        times.append(time.perf_counter() - t0)
+    t_int = min(times)
+    blocks = vbg.size()
+    pool_gb = vbg.capacity() * 16 ** 3 * 8 / 1e9
+    del depth, seq
+    torch.cuda.empty_cache()
+    ext = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        mesh = vbg.extract_triangle_mesh(weight_threshold=1.5)
+        ext.append(time.perf_counter() - t0)
+    key = list(range(0, B, key_every))
+    Ko = K[0]
+    imgs = synthetic.render_color_torch("hall", Ko, [poses[i] for i in key], H, W, device=f"cuda:{dev}").cpu().numpy()
+    scene = RaycastingScene(device=dev)
+    scene.add_triangles(mesh.vertices, mesh.triangles)
+    from mqr import _lib
+    t0 = time.perf_counter()
+    _lib.call("mqr_scene_build", scene._h)
+    bvh_s = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    cad = scene.cast_pinhole(K[key], T[key], W, H)["t_hit"].numpy()
+    cast_s = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    col, cnt = color_vertices(mesh.vertices, imgs, cad, K[key], T[key], device=dev)
+    col_s = time.perf_counter() - t0
+    seen = cnt > 0
+    err = float(np.abs(col[seen] - synthetic.texture(mesh.vertices[seen])).mean()) if seen.any() else None
+    out = {"frames": B, "voxel_size": voxel, "integrate_ms": t_int * 1e3, "frames_per_s": B / t_int,
+           "blocks": blocks, "pool_gb": pool_gb, "extract_ms": sorted(ext)[1] * 1e3,
+           "vertices": int(len(mesh.vertices)), "triangles": int(len(mesh.triangles)),
+           "keyframes": len(key), "bvh_build_ms": bvh_s * 1e3, "colour_depth_cast_ms": cast_s * 1e3,
+           "colour_ms": col_s * 1e3, "coloured_fraction": float(seen.mean()), "colour_mean_abs_err": err,
+           "generation_s": gen_s,
+           "note": "integrate: device-resident depth, best of 2 passes from an emptied volume (capacity grows "
+                   "from 16384 blocks); extract: host copy included, median of 3; colour: host arrays in/out "
+                   "(PCIe included), error vs the analytic texture the colour frames were rendered with"}
+    del vbg, mesh, scene
+    torch.cuda.empty_cache()
+    return out
+
+
 def raycast_leg(vbg, K, T, H, W, thr, frames=64):
     """Row f1: colour-aligned depth by ray casting the extracted mesh (RaycastingScene.cast_rays
     stand-in): BVH build + `frames` pinhole casts at H x W from the sequence's poses."""
@@ -460,6 +540,11 @@ def confidence_cpu(depth_host, K, T_wc, args, budget_s):
                       f"(oracle/mqr_oracle.c, OpenMP over pixels), {dt:.1f} s"}
 
 
+def log(msg):
+    """Progress on stderr (long legs must not look hung to a supervisor watching the output)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def main():
     args = parse()
     rank = int(os.environ.get("RANK", 0))
@@ -522,6 +607,7 @@ def main():
             torch.cuda.synchronize()
             merge_times.append(time.perf_counter() - t)
 
+    log(f"rank {rank}: {B} frames {H}x{W} generated; warm-up {args.warmup} steps")
     for _ in range(args.warmup):
         step()
     merge_times.clear()
@@ -537,6 +623,7 @@ def main():
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    log(f"rank {rank}: {args.steps} timed steps in {elapsed:.3f} s")
     vbg.profile(False)
     st = vbg.stats(reset=True)
     if dist:
@@ -578,12 +665,17 @@ def main():
     extras = {}
     if rank == 0 and world == 1 and not args.no_extras:
         dev = torch.device("cuda", local)
+        log("extra legs: copy peak, confidence, ingest, raycast, mesh filter, C3, drop-in")
         extras["hbm_copy_gbs"] = copy_peak_gbs(dev)
         extras["confidence"] = confidence_leg(depth_t, K, T, args, dev)
         extras["ingest"] = ingest_leg(B, H, W, dev)
         extras["raycast"] = raycast_leg(vbg, K, T, H, W, args.extract_threshold)
         extras["meshfilter"] = meshfilter_leg(vbg, args.extract_threshold)
         extras["c3"] = c3_leg(seq, vbg, args, dev)
+        log("C5 leg (4000 frames @ 3 mm, extract, colour)")
+        if not args.no_c5:
+            extras["c5"] = c5_leg(args, dev)
+        log("C3 / C5 legs done; drop-in leg (on-disk capture)")
         if args.e2e_frames > 0:
             extras["dropin_e2e"] = dropin_e2e_leg(seq, min(args.e2e_frames, B), dev)
         # PCIe-inclusive: the same step from host (numpy) frames, H2D inside integrate_frames
@@ -602,7 +694,9 @@ def main():
     cpu = parity = None
     if rank == 0 and world == 1 and not args.no_cpu:
         host_depth = depth_t.cpu().numpy()
+        log("CPU baseline (oracle)")
         cpu, ref_vol = cpu_baseline(host_depth, K, T, args)
+        log("parity check of the timed volume")
         if not args.no_parity:
             # the volume of the last timed step is still in vbg unless an extra leg reset it: rebuild
             # it exactly as a step does (reset + integrate_frames) when the legs ran
@@ -666,6 +760,7 @@ def main():
             "cpu_baseline": cpu,
             "parity": parity,
             "c3": extras.get("c3"),
+            "c5": extras.get("c5"),
             "dropin_e2e": extras.get("dropin_e2e"),
         }
         print(json.dumps(out), flush=True)

@@ -56,7 +56,7 @@ __device__ __forceinline__ float decode_px(float d, const DecodeFrame& fr, doubl
     return z;
 }
 
-// Thread per 4 consecutive pixels of one frame (blockIdx.y): 16-byte raw / count / depth
+// Workgroups stride over 4-pixel groups of one frame (blockIdx.y): 16-byte raw / count / depth
 // accesses and two 16-byte confidence loads, so every wave moves whole 1 KiB (raw) or 2 KiB
 // (confidence) runs.  VEC = false: scalar tail path for frames whose size is not a multiple of 4.
 template <bool VEC>
@@ -101,10 +101,16 @@ __global__ __launch_bounds__(256) void k_decode_depth(const float* __restrict__ 
                                     : decode_px<false>(d, fr, 0.0, 0, conf_thr, count_thr, fl);
         }
     }
-    // wave-level OR, then one atomic per wave only for bits the frame's word does not have yet
-    // (every wave of a frame would otherwise hit the same address: thousands of serialised atomics)
+    // workgroup-level OR (wave shuffle, then LDS), then ONE device atomic per workgroup.  A device
+    // atomic (or atomic load) per wave on the frame's word serialises at that word's memory
+    // channel: with a workgroup per 1024 pixels it capped the whole kernel at ~0.4 TB/s.
+    __shared__ uint32_t wg_fl;
+    if (threadIdx.x == 0) wg_fl = 0;
     for (int o = 32; o > 0; o >>= 1) fl |= (uint32_t)__shfl_xor((int)fl, o, 64);
-    if ((threadIdx.x & 63) == 0 && (fl & ~__atomic_load_n(&flags[f], __ATOMIC_RELAXED))) atomicOr(&flags[f], fl);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0 && fl) atomicOr(&wg_fl, fl);
+    __syncthreads();
+    if (threadIdx.x == 0 && wg_fl) atomicOr(&flags[f], wg_fl);
 }
 
 // Per-device decode context, created on first use and kept: a stream, a grow-only scratch buffer
@@ -223,7 +229,10 @@ int mqr_decode_depth(int device, const float* raw, int raw_loc, int N, int H, in
     const bool vec = HW % 4 == 0 && aligned(d_raw, 16) && aligned(d_out, 16) &&
                      (!any_mask || (aligned(d_conf, 32) && aligned(d_vc, 16)));
     const int64_t work = vec ? HW / 4 : HW;
-    const unsigned gx = (unsigned)std::min<int64_t>((work + 255) / 256, 2048);
+    // ~4096 workgroups in all (16 per CU), each a long grid-stride run over its frame: enough
+    // to fill the chip with few enough workgroups that the per-frame flag atomics stay rare
+    const int64_t per_frame = std::max<int64_t>(1, (4096 + N - 1) / N);
+    const unsigned gx = (unsigned)std::min<int64_t>((work + 255) / 256, per_frame);
     if (vec)
         hipLaunchKernelGGL(k_decode_depth<true>, dim3(gx, (unsigned)N), dim3(256), 0, c.s, d_raw, HW, c.d_fr, d_conf,
                            d_vc, conf_thr, count_thr, d_out, c.d_flags);

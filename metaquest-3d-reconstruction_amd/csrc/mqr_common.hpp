@@ -109,9 +109,21 @@ struct mqr_vbg {
     // batch parity; the hash table, pool and pool counter are shared.
     hipStream_t stream = nullptr;
     hipStream_t stream2 = nullptr;
+    // Ordering events between the two streams are recorded with a DEVICE-scope release
+    // (hipEventDisableSystemFence): a default (system-scope) event makes the packet processor write
+    // back and invalidate every XCD's L2 at the record -- ~20 us between consecutive integrate
+    // launches, and the next kernel starts cold.  Only ev_host (the host's read of the batch
+    // counters through pinned memory) keeps the system-scope release.  sys_fence (variant bit
+    // 0x800) records the system-scope twins instead, for the A/B.
     hipEvent_t ev_touch[2] = {nullptr, nullptr};
     hipEvent_t ev_int[2] = {nullptr, nullptr};
+    hipEvent_t ev_touch_sys[2] = {nullptr, nullptr};
+    hipEvent_t ev_int_sys[2] = {nullptr, nullptr};
+    hipEvent_t ev_host[2] = {nullptr, nullptr};
+    bool sys_fence = false;
     bool int_pending[2] = {false, false};
+    hipEvent_t touch_ev(int p) const { return sys_fence ? ev_touch_sys[p] : ev_touch[p]; }
+    hipEvent_t int_ev(int p) const { return sys_fence ? ev_int_sys[p] : ev_int[p]; }
 
     mqr::Table tab{};          // main block table (tab.mask == mask[0])
     mqr::bmask_t* mask1 = nullptr; // parity-1 slot masks
@@ -145,11 +157,13 @@ struct mqr_vbg {
     bool profile = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> int_events, touch_events;
     std::vector<hipEvent_t> ev_pool;  // timing events, created once and reused (hipEventCreate per
-    size_t ev_used = 0;               // launch added ~0.1 ms to a 500-frame step)
+    size_t ev_used = 0;               // launch added ~0.1 ms to a 500-frame step); device-scope
+    bool ev_pool_sys = false;         // release unless sys_fence (then a pool of default events)
+    unsigned timing_event_flags() const { return sys_fence ? hipEventDefault : hipEventDisableSystemFence; }
     hipEvent_t pooled_event() {
         if (ev_used == ev_pool.size()) {
             hipEvent_t e = nullptr;
-            if (hipEventCreate(&e) != hipSuccess) return nullptr;
+            if (hipEventCreateWithFlags(&e, timing_event_flags()) != hipSuccess) return nullptr;
             ev_pool.push_back(e);
         }
         return ev_pool[ev_used++];

@@ -202,8 +202,8 @@ static int read_counters(mqr_vbg* v, int p) {
                                  v->stream));
     MQR_CHECK_HIP(hipMemcpyAsync(v->h_counters + 2 * kCountersTotal, v->pool_ctr(), sizeof(int),
                                  hipMemcpyDeviceToHost, v->stream));
-    MQR_CHECK_HIP(hipEventRecord(v->ev_touch[p], v->stream));
-    MQR_CHECK_HIP(hipEventSynchronize(v->ev_touch[p]));
+    MQR_CHECK_HIP(hipEventRecord(v->ev_host[p], v->stream));
+    MQR_CHECK_HIP(hipEventSynchronize(v->ev_host[p]));
     return 0;
 }
 
@@ -262,11 +262,11 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
         hipLaunchKernelGGL(k_lpt_order, dim3(1), dim3(1024), 0, v->stream, list, counters, v->list_cap, t.mask,
                            v->lpt[p], om);
         MQR_CHECK_HIP(hipGetLastError());
-        if (v->pipelined) MQR_CHECK_HIP(hipEventRecord(v->ev_touch[p], v->stream));
+        if (v->pipelined) MQR_CHECK_HIP(hipEventRecord(v->touch_ev(p), v->stream));
         list = v->lpt[p];
         lmask = om;
     }
-    if (v->pipelined) MQR_CHECK_HIP(hipStreamWaitEvent(s, v->ev_touch[p], 0));
+    if (v->pipelined) MQR_CHECK_HIP(hipStreamWaitEvent(s, v->touch_ev(p), 0));
     const FrameParams* fp = v->d_fp[p];
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (v->profile) {
@@ -281,12 +281,14 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
     // must stay past 4HW for out-of-image voxels.  Otherwise the exact k_integrate_t runs alone.
     const bool lean_ok = !div_unsafe_host(sdf_trunc) && depth_scale == 1.0f && 4 * (HW + W) <= (int64_t{1} << 31);
     // Variants (mqr_vbg_set_variant, low byte; all bit-identical, tests/test_gpu_numerics.py):
-    //   0 default: k_integrate_lean (R = 16 / 8);  1 generic k_integrate (runtime R);
-    //   2 exact k_integrate_t;  5 k_integrate_tb (R = 16: block depth tile in LDS, A/B -- DESIGN.md §4).
+    //   0 default: k_integrate_lean -- R = 16: brick map, >= 8 waves per SIMD, 2 interleaved voxel
+    //     chains; R = 8: plate map;  1 generic k_integrate (runtime R);  2 exact k_integrate_t;
+    //   3 k_integrate_lean with the plate map (round-1 default, A/B);  5 k_integrate_tb (R = 16:
+    //     block depth tile in LDS, A/B).  DESIGN.md §4 has the measurements behind the choice.
     int var = v->kernel_variant;
-    if (var != 1 && var != 2 && var != 5) var = 0;
-    if ((var == 0 || var == 5) && !lean_ok) var = 2;
-    if (var == 5 && (v->R != 16 || W % 4 != 0 || (reinterpret_cast<uintptr_t>(depths) & 15))) var = 0;
+    if (var != 1 && var != 2 && var != 3 && var != 5) var = 0;
+    if (var != 1 && var != 2 && !lean_ok) var = 2;
+    if (var == 5 && (v->R != 16 || W % 4 != 0 || W < 4 || (reinterpret_cast<uintptr_t>(depths) & 15))) var = 0;
     if (v->R != 16 && v->R != 8) var = 1;
     const int32_t* bad_list = v->bad[p];
     const bmask_t* bad_mask = reinterpret_cast<const bmask_t*>(v->bad[p] + v->list_cap);
@@ -304,9 +306,13 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
                 hipLaunchKernelGGL(k_integrate_tb, dim3(grid), dim3(512), 0, s, list, lmask, v->bad[p], counters,
                                    v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp, depth_frame,
                                    depth_max, sdf_trunc);
-            else
+            else if (var == 3)
                 hipLaunchKernelGGL((k_integrate_lean<16, 512>), dim3(grid), dim3(512), 0, s, list, lmask, v->bad[p],
                                    counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp,
+                                   depth_frame, depth_max, sdf_trunc);
+            else
+                hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 8, 2>), dim3(grid), dim3(512), 0, s, list, lmask,
+                                   v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp,
                                    depth_frame, depth_max, sdf_trunc);
             // exact fix-up of the blocks the fast kernel handed back (usually none: reads a zero count)
             hipLaunchKernelGGL((k_integrate_t<16, 4, 512>), dim3(8), dim3(512), 0, s, bad_list, bad_mask, bad_count,
@@ -336,7 +342,7 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
         v->stats.frame_blocks += v->hctr(p)[kFrameBlocks];
         v->stats.frames += nframes;
     }
-    MQR_CHECK_HIP(hipEventRecord(v->ev_int[p], s));
+    MQR_CHECK_HIP(hipEventRecord(v->int_ev(p), s));
     v->int_pending[p] = true;
     return 0;
 }
@@ -344,7 +350,7 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
 // Before reusing parity p's batch state on `stream`: the integrate that last used it must be done.
 static int wait_parity_free(mqr_vbg* v, int p) {
     if (v->int_pending[p]) {
-        MQR_CHECK_HIP(hipStreamWaitEvent(v->stream, v->ev_int[p], 0));
+        MQR_CHECK_HIP(hipStreamWaitEvent(v->stream, v->int_ev(p), 0));
         v->int_pending[p] = false;  // ordered behind it on `stream` from here on
     }
     return 0;
@@ -482,8 +488,13 @@ int mqr_vbg_create(float voxel_size, int block_resolution, int64_t block_count, 
               hipHostMalloc(&v->h_counters, sizeof(int) * nctr, hipHostMallocDefault) == hipSuccess &&
               hipMemsetAsync(v->counters, 0, sizeof(int) * nctr, v->stream) == hipSuccess;
     for (int p = 0; p < 2 && ok; ++p)
-        ok = hipEventCreateWithFlags(&v->ev_touch[p], hipEventDisableTiming) == hipSuccess &&
-             hipEventCreateWithFlags(&v->ev_int[p], hipEventDisableTiming) == hipSuccess;
+        ok = hipEventCreateWithFlags(&v->ev_touch[p], hipEventDisableTiming | hipEventDisableSystemFence) ==
+                 hipSuccess &&
+             hipEventCreateWithFlags(&v->ev_int[p], hipEventDisableTiming | hipEventDisableSystemFence) ==
+                 hipSuccess &&
+             hipEventCreateWithFlags(&v->ev_touch_sys[p], hipEventDisableTiming) == hipSuccess &&
+             hipEventCreateWithFlags(&v->ev_int_sys[p], hipEventDisableTiming) == hipSuccess &&
+             hipEventCreateWithFlags(&v->ev_host[p], hipEventDisableTiming) == hipSuccess;
     if (!ok) {
         set_error("mqr_vbg_create: device allocation failed");
         mqr_vbg_destroy(v);
@@ -515,8 +526,8 @@ int mqr_vbg_destroy(mqr_vbg* v) {
         if (v->d_fp[p]) (void)hipFree(v->d_fp[p]);
         if (v->h_fp[p]) (void)hipHostFree(v->h_fp[p]);
         if (v->d_depth[p]) (void)hipFree(v->d_depth[p]);
-        if (v->ev_touch[p]) (void)hipEventDestroy(v->ev_touch[p]);
-        if (v->ev_int[p]) (void)hipEventDestroy(v->ev_int[p]);
+        for (hipEvent_t e : {v->ev_touch[p], v->ev_int[p], v->ev_touch_sys[p], v->ev_int_sys[p], v->ev_host[p]})
+            if (e) (void)hipEventDestroy(e);
     }
     for (hipEvent_t e : v->ev_pool) (void)hipEventDestroy(e);
     if (v->counters) (void)hipFree(v->counters);
@@ -831,6 +842,7 @@ int mqr_vbg_set_variant(mqr_vbg* v, int variant) {
     v->pipelined = (variant & 0x100) == 0;  // bit 8: serialise touch and integrate (A/B of the overlap)
     v->lpt_order = (variant & 0x200) == 0;  // bit 9: integrate in touch order instead of longest-first
     v->batch_frames = (variant & 0x400) ? 32 : kMaxBatch;  // bit 10: 32-frame batches (A/B)
+    v->sys_fence = (variant & 0x800) != 0;  // bit 11: system-scope ordering / timing events (A/B)
     return 0;
 }
 
@@ -868,9 +880,16 @@ int mqr_vbg_profile(mqr_vbg* v, int enable) {
     // create the timing events now, outside any timed region (4 per batch; more are created on
     // demand until the next stats read recycles them)
     MQR_CHECK_HIP(hipSetDevice(v->device));
+    if (v->profile && v->ev_pool_sys != v->sys_fence) {  // the fence scope changed: rebuild the pool
+        if (sync_all(v)) return 1;
+        drain_events(v);
+        for (hipEvent_t e : v->ev_pool) (void)hipEventDestroy(e);
+        v->ev_pool.clear();
+        v->ev_pool_sys = v->sys_fence;
+    }
     while (v->profile && v->ev_pool.size() < 12288) {
         hipEvent_t e = nullptr;
-        MQR_CHECK_HIP(hipEventCreate(&e));
+        MQR_CHECK_HIP(hipEventCreateWithFlags(&e, v->timing_event_flags()));
         v->ev_pool.push_back(e);
     }
     return 0;

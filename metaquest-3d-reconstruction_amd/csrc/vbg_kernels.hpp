@@ -1,6 +1,9 @@
 // vbg_kernels.hpp -- device code of the TSDF volume (included once, by vbg.hip).
 // Open3D 0.19 VoxelBlockGrid semantics; float32 with no FMA contraction.
 #pragma once
+#ifndef MQR_DIAG
+#define MQR_DIAG 0  // 1 / 2: timing-only builds of the lean kernel (wrong results; never shipped)
+#endif
 #include "mqr_common.hpp"
 
 namespace mqr {
@@ -452,7 +455,7 @@ __device__ __forceinline__ void pool_store(__amdgpu_buffer_rsrc_t rs, uint32_t v
 // 2^-36 <= zc <= 2^60 (zc <= 0 included, which the update would skip anyway): inside that range
 // rcp_m is exact and a non-zero sdf = d - zc is >= 2^-60 in magnitude, which keeps the division
 // core exact.
-template <int ZPER>
+template <int ZPER, int ILP = 1>
 __device__ __forceinline__ void lean_gather(float (&dv)[ZPER], bool& bad, const FrameParams& fp,
                                             __amdgpu_buffer_rsrc_t rs, const float (&xs)[ZPER],
                                             const float (&ys)[ZPER], const float (&zs)[ZPER], uint32_t W4, float hf,
@@ -478,19 +481,29 @@ __device__ __forceinline__ void lean_gather(float (&dv)[ZPER], bool& bad, const 
         const bool in = (v >= 0) & (u >= 0) & (v <= hm1) & (u <= wm1);
         const int ui = (int)(in ? u : 0.f), vi = (int)(in ? v : hf);
         const uint32_t off = __umul24((uint32_t)vi, W4) + ((uint32_t)ui << 2);
+#if MQR_DIAG == 1  // timing diagnostics only (tools/diag_integrate.sh): projection without the gather
+        dv[k] = zc + (float)(off & 1u) * 1e-30f;
+#else
         dv[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
-        // keep each voxel's projection next to its load: hoisting all projections above the loads
-        // (the scheduler's choice) keeps ~6 more VGPRs per voxel live and halves the occupancy
-        __builtin_amdgcn_sched_barrier(0);
+#endif
+        // keep each group of ILP voxels' projections next to their loads: hoisting all projections
+        // above the loads (the scheduler's choice) keeps ~6 more VGPRs per voxel live and halves the
+        // occupancy; ILP > 1 lets the scheduler interleave that many independent chains
+        if ((k + 1) % ILP == 0) __builtin_amdgcn_sched_barrier(0);
     }
 }
 
 // Running-average update of one frame's gathered depths (zc recomputed by the same operations).
-template <int ZPER>
+template <int ZPER, int ILP = 1>
 __device__ __forceinline__ void lean_update(float2 (&tw)[ZPER], const float (&dv)[ZPER], const FrameParams& fp,
                                             const float (&xs)[ZPER], const float (&ys)[ZPER],
                                             const float (&zs)[ZPER], float depth_max, float sdf_trunc, float y1t) {
     const float e8 = fp.ext[8], e9 = fp.ext[9], e10 = fp.ext[10], e11 = fp.ext[11];
+#if MQR_DIAG == 2  // timing diagnostics only: the gather without the update
+#pragma unroll
+    for (int k = 0; k < ZPER; ++k) tw[k].x += dv[k];
+    return;
+#endif
 #pragma unroll
     for (int k = 0; k < ZPER; ++k) {
         const float az = xs[k] * e8 + ys[k] * e9;
@@ -507,7 +520,7 @@ __device__ __forceinline__ void lean_update(float2 (&tw)[ZPER], const float (&dv
         const float nt = (wgt * tw[k].x + sn) * rcp_m(wp);
         tw[k].x = up ? nt : tw[k].x;
         tw[k].y = up ? wp : wgt;
-        __builtin_amdgcn_sched_barrier(0);  // one voxel's chain at a time (register pressure)
+        if ((k + 1) % ILP == 0) __builtin_amdgcn_sched_barrier(0);  // ILP chains at a time (registers)
     }
 }
 
@@ -517,72 +530,6 @@ __device__ __forceinline__ void hand_off(int32_t* bad_out, int* counters, int64_
     const int j = atomicAdd(&counters[kBadCount], 1);
     bad_out[j] = slot;
     reinterpret_cast<bmask_t*>(bad_out + list_cap)[j] = mask;
-}
-
-// Lean integrate, unit depth scale only (host: sdf_trunc in the division core's range).  Block per
-// workgroup, column mapping as k_integrate_t; every voxel of a block not handed off is written back.
-template <int R, int NT>
-__global__ __launch_bounds__(NT) void k_integrate_lean(const int32_t* __restrict__ list,
-                                                       const bmask_t* __restrict__ lmask,
-                                                       int32_t* __restrict__ bad_out, int* __restrict__ counters,
-                                                       int64_t list_cap, Table t, float2* __restrict__ pool,
-                                                       float voxel_size, const float* __restrict__ depths,
-                                                       int64_t HW, int H, int W, const FrameParams* __restrict__ fps,
-                                                       const int64_t* __restrict__ depth_frame, float depth_max,
-                                                       float sdf_trunc) {
-    constexpr int R2 = R * R;
-    constexpr int R3 = R2 * R;
-    constexpr int ZPER = R3 / NT;
-    static_assert(R3 % NT == 0 && NT % R2 == 0, "NT must divide R^3 and be a multiple of R^2");
-    const int64_t n = min((int64_t)counters[kListCount], list_cap);
-    const float hf = (float)H, hm1 = (float)H - 1.0f, wm1 = (float)W - 1.0f;
-    const uint32_t W4 = 4u * (uint32_t)W, bytes = 4u * (uint32_t)HW;
-    const float y0t = __builtin_amdgcn_rcpf(sdf_trunc);
-    const float y1t = __builtin_fmaf(__builtin_fmaf(-sdf_trunc, y0t, 1.0f), y0t, y0t);
-    const int tid = threadIdx.x;
-    for (int64_t i = blockIdx.x; i < n; i += gridDim.x) {
-        const int32_t slot = list[i];
-        const int buf = __builtin_amdgcn_readfirstlane(t.vals[slot]);
-        const bmask_t mask = readfirstlane_u64(lmask ? lmask[i] : t.mask[slot]);
-        int xb, yb, zb;
-        unpack_key(t.keys[slot], xb, yb, zb);
-        if (buf >= 0 && mask) {
-            const __amdgpu_buffer_rsrc_t vox = __builtin_amdgcn_make_buffer_rsrc(
-                pool + (int64_t)buf * R3, (short)0, (int)(R3 * sizeof(float2)), 0x00020000);
-            float2 tw[ZPER];
-            float xs[ZPER], ys[ZPER], zs[ZPER];
-            bool bad = false;
-            const float xs0 = (float)(xb * R + tid % R) * voxel_size;
-            const float ys0 = (float)(yb * R + (tid / R) % R) * voxel_size;
-#pragma unroll
-            for (int k = 0; k < ZPER; ++k) {
-                tw[k] = pool_load(vox, 8u * (uint32_t)tid, k * NT * (int)sizeof(float2));
-                xs[k] = xs0;
-                ys[k] = ys0;
-                zs[k] = (float)(zb * R + tid / R2 + k * (NT / R2)) * voxel_size;
-                const float w = tw[k].y;  // rcp_m(w + 1) needs integer weights (a batch adds <= 64)
-                bad |= !(w >= 0.0f && w <= 0x1p23f && w == __builtin_truncf(w));
-            }
-            bmask_t m = mask;
-            while (m) {
-                const int f = __builtin_ctzll(m);
-                m &= m - 1;
-                float dv[ZPER];
-                lean_gather<ZPER>(dv, bad, fps[f], frame_rsrc(depths + depth_frame[f] * HW, bytes), xs, ys, zs, W4,
-                                  hf, hm1, wm1);
-                lean_update<ZPER>(tw, dv, fps[f], xs, ys, zs, depth_max, sdf_trunc, y1t);
-            }
-            if (__syncthreads_or(bad)) {  // block-uniform: the exact fix-up launch redoes it from the pool
-                if (tid == 0) hand_off(bad_out, counters, list_cap, slot, mask);
-            } else {
-#pragma unroll
-                for (int k = 0; k < ZPER; ++k)
-                    pool_store(vox, 8u * (uint32_t)tid, k * NT * (int)sizeof(float2), tw[k]);
-            }
-        }
-        __syncthreads();
-        if (tid == 0) t.mask[slot] = 0;
-    }
 }
 
 // ---- helpers of the packed / tiled kernels ---------------------------------------------------------
@@ -628,17 +575,18 @@ __device__ __forceinline__ int nth_bit(bmask_t m, int j) {
 // float operations in the same order per voxel as lean_gather / lean_update: bit-identical.
 template <int ZPER>
 __device__ __forceinline__ void lean_gather_pk(float (&dv)[ZPER], f2v (&zc2)[ZPER / 2], bool& bad,
-                                               const FrameParams& fp, __amdgpu_buffer_rsrc_t rs, float xs, float ys,
-                                               const f2v (&zs2)[ZPER / 2], uint32_t W4, float hf, float hm1,
-                                               float wm1) {
+                                               const FrameParams& fp, __amdgpu_buffer_rsrc_t rs, float xs,
+                                               const float (&ys2)[ZPER / 2], const f2v (&zs2)[ZPER / 2], uint32_t W4,
+                                               float hf, float hm1, float wm1) {
     float e[12];
 #pragma unroll
     for (int j = 0; j < 12; ++j) e[j] = fp.ext[j];
-    const f2v AX = splat2(xs * e[0] + ys * e[1]), AY = splat2(xs * e[4] + ys * e[5]);
-    const f2v AZ = splat2(xs * e[8] + ys * e[9]);
     const f2v FX = splat2(fp.fx), FY = splat2(fp.fy), CX = splat2(fp.cx), CY = splat2(fp.cy);
 #pragma unroll
     for (int q = 0; q < ZPER / 2; ++q) {
+        const float ys = ys2[q];  // equal operands across q are merged
+        const f2v AX = splat2(xs * e[0] + ys * e[1]), AY = splat2(xs * e[4] + ys * e[5]);
+        const f2v AZ = splat2(xs * e[8] + ys * e[9]);
         const f2v Z = zs2[q];
         const f2v xc = (AX + Z * splat2(e[2])) + splat2(e[3]);
         const f2v yc = (AY + Z * splat2(e[6])) + splat2(e[7]);
@@ -683,6 +631,103 @@ __device__ __forceinline__ void lean_update_pk(f2v (&T)[ZPER / 2], f2v (&Wt)[ZPE
         Wt[q].x = up0 ? wp.x : Wt[q].x;
         Wt[q].y = up1 ? wp.y : Wt[q].y;
         __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+// Thread -> voxels of the lean kernel.
+// MAP 0 (plate): thread t owns column (x, y) = (t % R, t / R % R), voxels z = t / R^2 + k NT / R^2;
+//   a wave's k-th voxels form a 16 x 4 x 1 plate (R = 16).
+// MAP 1 (brick, R = 16, NT = 512): lane l of wave w owns x = l % 8 + 8 (w % 2), y = (l / 8) % 2 +
+//   2 (w / 2), z = l / 16, and its voxel k sits at (x, y + 8 (k / 4), z + 4 (k % 4)); a wave's k-th
+//   voxels form an 8 x 2 x 4 brick.  Voxels along a viewing ray share pixels, so a brick projects to
+//   fewer image rows than a plate (5.8 vs 10.3 distinct cache lines per 64-lane gather on the C2
+//   walk); with the occupancy hint below this is the faster map.
+template <int R, int NT, int MAP>
+__device__ __forceinline__ void lean_map(int tid, int& x, int& y, int& z) {
+    if (MAP == 1) {
+        const int l = tid & 63, w = tid >> 6;
+        x = (l & 7) + 8 * (w & 1);
+        y = ((l >> 3) & 1) + 2 * (w >> 1);
+        z = l >> 4;
+    } else {
+        x = tid % R;
+        y = (tid / R) % R;
+        z = tid / (R * R);
+    }
+}
+// Offsets (voxels along y and z) of a thread's voxel k from its voxel 0.
+template <int R, int NT, int MAP>
+__host__ __device__ constexpr int lean_dy(int k) { return MAP == 1 ? 8 * (k >> 2) : 0; }
+template <int R, int NT, int MAP>
+__host__ __device__ constexpr int lean_dz(int k) { return MAP == 1 ? 4 * (k & 3) : k * (NT / (R * R)); }
+
+// Lean integrate, unit depth scale only (host: sdf_trunc in the division core's range).  Block per
+// workgroup, voxels per lean_map<MAP>; every voxel of a block not handed off is written back.
+// WPE: minimum waves per SIMD the register allocation must allow; ILP: voxel chains the scheduler
+// may interleave (lean_gather / lean_update).
+template <int R, int NT, int MAP = 0, int WPE = 1, int ILP = 1>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void k_integrate_lean(
+    const int32_t* __restrict__ list, const bmask_t* __restrict__ lmask, int32_t* __restrict__ bad_out,
+    int* __restrict__ counters, int64_t list_cap, Table t, float2* __restrict__ pool, float voxel_size,
+    const float* __restrict__ depths, int64_t HW, int H, int W, const FrameParams* __restrict__ fps,
+    const int64_t* __restrict__ depth_frame, float depth_max, float sdf_trunc) {
+    constexpr int R2 = R * R;
+    constexpr int R3 = R2 * R;
+    constexpr int ZPER = R3 / NT;
+    static_assert(R3 % NT == 0 && NT % R2 == 0, "NT must divide R^3 and be a multiple of R^2");
+    static_assert(MAP == 0 || (R == 16 && NT == 512), "the brick map is for R = 16, NT = 512");
+    const int64_t n = min((int64_t)counters[kListCount], list_cap);
+    const float hf = (float)H, hm1 = (float)H - 1.0f, wm1 = (float)W - 1.0f;
+    const uint32_t W4 = 4u * (uint32_t)W, bytes = 4u * (uint32_t)HW;
+    const float y0t = __builtin_amdgcn_rcpf(sdf_trunc);
+    const float y1t = __builtin_fmaf(__builtin_fmaf(-sdf_trunc, y0t, 1.0f), y0t, y0t);
+    const int tid = threadIdx.x;
+    int vx, vy, vz;
+    lean_map<R, NT, MAP>(tid, vx, vy, vz);
+    const uint32_t voff = 8u * (uint32_t)(vx + R * vy + R2 * vz);  // byte offset of voxel 0 in its block
+    for (int64_t i = blockIdx.x; i < n; i += gridDim.x) {
+        const int32_t slot = list[i];
+        const int buf = __builtin_amdgcn_readfirstlane(t.vals[slot]);
+        const bmask_t mask = readfirstlane_u64(lmask ? lmask[i] : t.mask[slot]);
+        int xb, yb, zb;
+        unpack_key(t.keys[slot], xb, yb, zb);
+        if (buf >= 0 && mask) {
+            const __amdgpu_buffer_rsrc_t vox = __builtin_amdgcn_make_buffer_rsrc(
+                pool + (int64_t)buf * R3, (short)0, (int)(R3 * sizeof(float2)), 0x00020000);
+            float2 tw[ZPER];
+            float xs[ZPER], ys[ZPER], zs[ZPER];
+            bool bad = false;
+            const float xs0 = (float)(xb * R + vx) * voxel_size;
+#pragma unroll
+            for (int k = 0; k < ZPER; ++k) {
+                const int dy = lean_dy<R, NT, MAP>(k), dz = lean_dz<R, NT, MAP>(k);
+                tw[k] = pool_load(vox, voff, (R * dy + R2 * dz) * (int)sizeof(float2));
+                xs[k] = xs0;
+                ys[k] = (float)(yb * R + vy + dy) * voxel_size;
+                zs[k] = (float)(zb * R + vz + dz) * voxel_size;
+                const float w = tw[k].y;  // rcp_m(w + 1) needs integer weights (a batch adds <= 64)
+                bad |= !(w >= 0.0f && w <= 0x1p23f && w == __builtin_truncf(w));
+            }
+            bmask_t m = mask;
+            while (m) {
+                const int f = __builtin_ctzll(m);
+                m &= m - 1;
+                float dv[ZPER];
+                lean_gather<ZPER, ILP>(dv, bad, fps[f], frame_rsrc(depths + depth_frame[f] * HW, bytes), xs, ys, zs,
+                                       W4, hf, hm1, wm1);
+                lean_update<ZPER, ILP>(tw, dv, fps[f], xs, ys, zs, depth_max, sdf_trunc, y1t);
+            }
+            if (__syncthreads_or(bad)) {  // block-uniform: the exact fix-up launch redoes it from the pool
+                if (tid == 0) hand_off(bad_out, counters, list_cap, slot, mask);
+            } else {
+#pragma unroll
+                for (int k = 0; k < ZPER; ++k)
+                    pool_store(vox, voff, (R * lean_dy<R, NT, MAP>(k) + R2 * lean_dz<R, NT, MAP>(k)) * (int)sizeof(float2),
+                               tw[k]);
+            }
+        }
+        __syncthreads();
+        if (tid == 0) t.mask[slot] = 0;
     }
 }
 
@@ -888,9 +933,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
                         tb_gather<NP, false>(dv, zc2, bad, fps[f], xs, ys, zs2, tile, r.x, r.y, (uint32_t)r.z,
                                              (uint32_t)(r.w & 0xffff), hm1, wm1);
                 } else {  // direct gathers (the lean kernel's, with its per-voxel zc check)
+                    float ys2[NP];
+#pragma unroll
+                    for (int q = 0; q < NP; ++q) ys2[q] = ys;
                     lean_gather_pk<ZPER>(dv, zc2, bad, fps[f], frame_rsrc(depths + depth_frame[f] * HW,
                                                                            4u * (uint32_t)HW),
-                                         xs, ys, zs2, 4u * (uint32_t)W, (float)H, hm1, wm1);
+                                         xs, ys2, zs2, 4u * (uint32_t)W, (float)H, hm1, wm1);
                 }
                 lean_update_pk<ZPER>(T, Wt, dv, zc2, depth_max, sdf_trunc, y1t);
             }

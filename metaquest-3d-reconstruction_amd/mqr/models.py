@@ -6,7 +6,7 @@ Host-side mirror of the reference's ``scripts/models`` surface that the TSDF pat
 ``Side`` (models/side.py).  The arithmetic order (float32 4x4 extrinsics, ``np.linalg.inv``
 for world->camera, scipy quaternions in (x, y, z, w) order) follows the reference so the
 matrices handed to the kernels are bit-identical to what the reference hands to Open3D
-(pinned by tests/golden/transforms_golden.npz).
+(pinned by the dataset fields in tests/golden/confidence_golden.npz, tests/test_dataio_golden.py).
 """
 from __future__ import annotations
 

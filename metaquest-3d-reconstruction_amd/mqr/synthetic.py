@@ -34,6 +34,13 @@ SCENES = {
         "boxes": [((-1.1, 0.0, 0.5), (-0.5, 0.75, 1.1)), ((0.5, 0.0, -1.2), (1.2, 1.2, -0.7))],
         "room": ((-1.28, 0.0, -1.28), (1.28, 2.56, 1.28)),
     },
+    # C5: an 8 x 8 x 3 m hall with furniture-sized boxes and spheres
+    "hall": {
+        "spheres": [((1.5, 0.6, 1.0), 0.6), ((-2.0, 0.4, -1.5), 0.4), ((0.5, 2.2, -2.5), 0.3), ((-2.8, 1.2, 2.6), 0.5)],
+        "boxes": [((-3.5, 0.0, 1.0), (-2.0, 0.9, 3.5)), ((2.0, 0.0, -3.5), (3.8, 2.0, -2.5)),
+                  ((-0.8, 0.0, -0.6), (0.6, 0.75, 0.6)), ((2.8, 0.0, 2.0), (3.6, 1.2, 3.8))],
+        "room": ((-4.0, 0.0, -4.0), (4.0, 3.0, 4.0)),
+    },
 }
 
 
@@ -156,6 +163,31 @@ def render_depth_torch(scene, K, poses, height, width, device="cuda"):
             tf = torch.nan_to_num(torch.maximum(t0, t1), nan=float("inf")).amin(1)
             best = torch.minimum(best, torch.where(tf > 1e-6, tf, inf))
         out[i] = torch.where(torch.isfinite(best), best, torch.zeros_like(best)).reshape(height, width).float()
+    return out
+
+
+def hall_loop_poses(n, radius=2.2, height=1.6, sweep_deg=70.0, sweeps=6, pitch_deg=-15.0):
+    """C5 walk: a closed loop through the hall, looking outwards and across with a yaw sweep."""
+    return room_loop_poses(n, radius=radius, height=height, sweep_deg=sweep_deg, sweeps=sweeps, pitch_deg=pitch_deg)
+
+
+def render_color_torch(scene, K, poses, height, width, device="cuda"):
+    """(N,H,W,3) uint8 colour frames (texture() at the ray hits, black on a miss) on `device`."""
+    import torch
+    z = render_depth_torch(SCENES[scene] if isinstance(scene, str) else scene, K, poses, height, width, device)
+    z = z.double()
+    fx, fy, cx, cy = (float(K[0, 0]), float(K[1, 1]), float(K[0, 2]), float(K[1, 2]))
+    v, u = torch.meshgrid(torch.arange(height, device=device, dtype=torch.float64),
+                          torch.arange(width, device=device, dtype=torch.float64), indexing="ij")
+    dc = torch.stack([(u - cx) / fx, (v - cy) / fy, torch.ones_like(u)], dim=-1)
+    out = torch.empty((len(poses), height, width, 3), dtype=torch.uint8, device=device)
+    for i, (R, t) in enumerate(poses):
+        Rt = torch.as_tensor(np.asarray(R).T, dtype=torch.float64, device=device)
+        pw = (dc * z[i][..., None]) @ Rt + torch.as_tensor(np.asarray(t), dtype=torch.float64, device=device)
+        rgb = torch.stack([0.5 + 0.5 * torch.sin(7.0 * pw[..., 0] + 1.0), 0.5 + 0.5 * torch.sin(5.0 * pw[..., 1] + 2.0),
+                           0.5 + 0.5 * torch.sin(3.0 * pw[..., 2] + 3.0)], dim=-1)
+        rgb = torch.where((z[i] > 0)[..., None], rgb, torch.zeros_like(rgb))
+        out[i] = torch.clamp(torch.round(rgb * 255.0), 0, 255).to(torch.uint8)
     return out
 
 

@@ -9,12 +9,13 @@ copied; the GPU box never sees the reference -- only these vectors.
 Fixtures:
   decode_golden.npz      raw NDC buffers x (near, far) -> convert_depth_to_linear (depth_utils.py:21-46)
                          + is_depth_map_valid verdicts (depth_data_io.py:80-85)
-  dataset_golden.npz     a 12-frame capture (raw buffers + descriptor rows) -> DepthDataset fields,
-                         compute_o3d_intrinsic_matrices (o3d_utils.py:14-19), OPEN3D extrinsics_wc/_cw
-                         (transforms.py:57-72, 164-220), np.linalg.inv(extrinsics_cw), decoded depth
-  confidence_golden.npz  build_confidence_map (estimate_depth_confidences.py:15-79) for every ref frame of
-                         two sequences and two parameter sets, + compute_pixel_error_map
-                         (compute_pixel_error_map.py:120-220) for 4 frame pairs
+  confidence_golden.npz  per sequence (sphere / room): the capture (raw buffers + descriptor rows), the
+                         DepthDataset fields and compute_o3d_intrinsic_matrices (o3d_utils.py:14-19,
+                         <seq>_fx / _cx / _K), the OPEN3D extrinsics_wc / _cw (transforms.py:57-72,
+                         164-220) and np.linalg.inv(extrinsics_cw), the decoded depth; then
+                         build_confidence_map (estimate_depth_confidences.py:15-79) for every ref frame
+                         under two parameter sets (_conf_a/_valid_a, _conf_b/_valid_b) and
+                         compute_pixel_error_map (compute_pixel_error_map.py:120-220) for frame pairs
 """
 from __future__ import annotations
 

@@ -144,3 +144,36 @@ def test_empty_first_frame_of_batch(vbg_mod):
         vbg.integrate_frames(depth, seq["K"], seq["T_wc"], depth_scale=1.0, depth_max=3.0,
                              trunc_voxel_multiplier=4.0)
     assert vbg.size() == 0
+
+
+def test_c5_structure_hall_3mm(vbg_mod):
+    """C5's structure at test size: LEFT then RIGHT (stereo baseline 0.064 m) through the 8 x 8 x 3 m
+    hall at 3 mm voxels, volume grown from a small capacity, mesh at 1.5 and per-vertex colour from
+    keyframes with ray-cast colour-aligned depth -- all against the oracle."""
+    from mqr import synthetic
+    from mqr.color import MARGIN, MAX_DEPTH, VISIBILITY_THRESHOLD, color_vertices
+    from mqr.raycasting import RaycastingScene
+    left = synthetic.hall_loop_poses(24)
+    right = [(R, t + R[:, 0] * 0.064) for R, t in left]
+    seq = synthetic.make_sequence("hall", poses=left + right, height=240, width=320, f=262.5, noise=True, seed=8)
+    vbg = vbg_mod.VoxelBlockGrid(voxel_size=0.003, block_resolution=16, block_count=256)
+    vbg.integrate_frames(seq["depth"], seq["K"], seq["T_wc"], depth_scale=1.0, depth_max=4.0,
+                         trunc_voxel_multiplier=10.0)
+    ref = _oracle_volume(seq["depth"], seq["K"], seq["T_wc"], 0.003, 16, 4.0, 10.0, 256)
+    assert ref.size() > 4 * 256  # grew several times
+    assert compare_volumes(vbg.export(), ref.export(), TOL) == 0.0
+    _check_mesh(vbg, ref, 1.5)
+    mesh = vbg.extract_triangle_mesh(weight_threshold=1.5)
+    key = list(range(0, 48, 4))
+    K = seq["K"][key].astype(np.float64)
+    T = seq["T_wc"][key].astype(np.float64)
+    poses = left + right
+    imgs = np.stack([synthetic.render_color("hall", K[0], poses[i][0], poses[i][1], 240, 320) for i in key])
+    rs = RaycastingScene()
+    rs.add_triangles(mesh.vertices, mesh.triangles)
+    depth = rs.cast_pinhole(K, T, 320, 240)["t_hit"].numpy()
+    gc, gn = color_vertices(mesh.vertices, imgs, depth, K, T)
+    oc, on = oracle.color_vertices(mesh.vertices, imgs, depth, K, T, MAX_DEPTH, VISIBILITY_THRESHOLD, MARGIN)
+    assert np.array_equal(gn, on) and np.array_equal(gc, oc)
+    # colour max depth 2.5 m in an 8 x 8 m hall: only the near walls and floor are coloured
+    assert (gn > 0).mean() > 0.02

@@ -4,7 +4,7 @@
 set -e
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-ROUND=${ROUND:-r01}
+ROUND=${ROUND:-r02}
 mkdir -p gpurun_out/pmc
 for c in FETCH_SIZE WRITE_SIZE; do
   n=$(echo $c | cut -d_ -f1 | tr A-Z a-z)
