@@ -123,8 +123,7 @@ int grow_pool(mqr_vbg* v, int64_t need) {
     uint64_t* nk = nullptr;
     MQR_CHECK_HIP(hipMalloc(&np, sizeof(float2) * ncap * v->R3));
     MQR_CHECK_HIP(hipMalloc(&nk, sizeof(uint64_t) * ncap));
-    MQR_CHECK_HIP(hipMemsetAsync(np, 0, sizeof(float2) * ncap * v->R3, v->stream));
-    if (v->pool_cap) {
+    if (v->pool_cap) {  // buffers past the old capacity are not cleared (see mqr_vbg_reset)
         MQR_CHECK_HIP(hipMemcpyAsync(np, v->pool, sizeof(float2) * v->pool_cap * v->R3, hipMemcpyDeviceToDevice,
                                      v->stream));
         MQR_CHECK_HIP(
@@ -246,8 +245,9 @@ static int resolve_pool_overflow(mqr_vbg* v, int p) {
 }
 
 // Launch the integrate kernel for parity p on `stream2`, after touch(p) (event) completed.
+// first_new: the pool size before this batch's allocations (its blocks start at (0, 0)).
 static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, int H, int W, int nframes,
-                            float depth_scale, float depth_max, float sdf_trunc) {
+                            float depth_scale, float depth_max, float sdf_trunc, int first_new) {
     const int64_t n = std::min<int64_t>(v->hctr(p)[kListCount], v->list_cap);
     if (n == 0) return 0;
     hipStream_t s = v->pipelined ? v->stream2 : v->stream;
@@ -295,42 +295,42 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
     int* bad_count = counters + kBadCount;
     if (var == 1) {
         hipLaunchKernelGGL(k_integrate, dim3(grid), dim3(256), 0, s, list, counters, v->list_cap, t, v->pool, v->R,
-                           v->voxel_size, depths, HW, H, W, fp, depth_frame, depth_scale, depth_max, sdf_trunc);
+                           v->voxel_size, depths, HW, H, W, fp, depth_frame, depth_scale, depth_max, sdf_trunc, first_new);
     } else if (v->R == 16) {
         if (var == 2) {
             hipLaunchKernelGGL((k_integrate_t<16, 4, 512>), dim3(grid), dim3(512), 0, s, list, lmask,
                                counters + kListCount, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp,
-                               depth_frame, depth_scale, depth_max, sdf_trunc);
+                               depth_frame, depth_scale, depth_max, sdf_trunc, first_new);
         } else {
             if (var == 5)
                 hipLaunchKernelGGL(k_integrate_tb, dim3(grid), dim3(512), 0, s, list, lmask, v->bad[p], counters,
                                    v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp, depth_frame,
-                                   depth_max, sdf_trunc);
+                                   depth_max, sdf_trunc, first_new);
             else if (var == 3)
                 hipLaunchKernelGGL((k_integrate_lean<16, 512>), dim3(grid), dim3(512), 0, s, list, lmask, v->bad[p],
                                    counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp,
-                                   depth_frame, depth_max, sdf_trunc);
+                                   depth_frame, depth_max, sdf_trunc, first_new);
             else
                 hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 8, 2>), dim3(grid), dim3(512), 0, s, list, lmask,
                                    v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp,
-                                   depth_frame, depth_max, sdf_trunc);
+                                   depth_frame, depth_max, sdf_trunc, first_new);
             // exact fix-up of the blocks the fast kernel handed back (usually none: reads a zero count)
             hipLaunchKernelGGL((k_integrate_t<16, 4, 512>), dim3(8), dim3(512), 0, s, bad_list, bad_mask, bad_count,
                                v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp, depth_frame, depth_scale,
-                               depth_max, sdf_trunc);
+                               depth_max, sdf_trunc, first_new);
         }
     } else {  // R == 8
         if (var == 2) {
             hipLaunchKernelGGL((k_integrate_t<8, 2, 256>), dim3(grid), dim3(256), 0, s, list, lmask,
                                counters + kListCount, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp,
-                               depth_frame, depth_scale, depth_max, sdf_trunc);
+                               depth_frame, depth_scale, depth_max, sdf_trunc, first_new);
         } else {
             hipLaunchKernelGGL((k_integrate_lean<8, 256>), dim3(grid), dim3(256), 0, s, list, lmask, v->bad[p],
                                counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp, depth_frame,
-                               depth_max, sdf_trunc);
+                               depth_max, sdf_trunc, first_new);
             hipLaunchKernelGGL((k_integrate_t<8, 2, 256>), dim3(8), dim3(256), 0, s, bad_list, bad_mask, bad_count,
                                v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp, depth_frame, depth_scale,
-                               depth_max, sdf_trunc);
+                               depth_max, sdf_trunc, first_new);
         }
     }
     MQR_CHECK_HIP(hipGetLastError());
@@ -380,6 +380,8 @@ int activate_ordered(mqr_vbg* v, const uint64_t* dkeys, int64_t n) {
     }
     if (n == 0) return 0;
     if (sync_all(v) || ensure_table(v, n) || grow_pool(v, n) || reset_batch_counters(v, 0)) return 1;
+    // the merge accumulates into these buffers (k_merge_blocks): they start at (0, 0)
+    MQR_CHECK_HIP(hipMemsetAsync(v->pool, 0, sizeof(float2) * n * v->R3, v->stream));
     hipLaunchKernelGGL(k_activate_ordered, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, v->stream, dkeys, n,
                        v->tab, v->bkeys, v->ctr(0));
     hipLaunchKernelGGL(k_set_counter, dim3(1), dim3(1), 0, v->stream, v->pool_ctr(), (int)n);
@@ -544,14 +546,13 @@ int mqr_vbg_reset(mqr_vbg* v) {
     MQR_REQUIRE(v, "null volume");
     MQR_CHECK_HIP(hipSetDevice(v->device));
     if (sync_all(v)) return 1;
-    MQR_CHECK_HIP(hipMemsetAsync(v->tab.keys, 0xff, sizeof(uint64_t) * v->tab.cap, v->stream));
-    MQR_CHECK_HIP(hipMemsetAsync(v->tab.vals, 0xff, sizeof(int32_t) * v->tab.cap, v->stream));
-    MQR_CHECK_HIP(hipMemsetAsync(v->tab.mask, 0, sizeof(bmask_t) * v->tab.cap, v->stream));
-    MQR_CHECK_HIP(hipMemsetAsync(v->mask1, 0, sizeof(bmask_t) * v->tab.cap, v->stream));
-    if (v->pool_count > 0)
-        MQR_CHECK_HIP(hipMemsetAsync(v->pool, 0, sizeof(float2) * v->pool_count * v->R3, v->stream));
-    MQR_CHECK_HIP(hipMemsetAsync(v->counters, 0, sizeof(int) * (2 * kCountersTotal + 8), v->stream));
-    MQR_CHECK_HIP(hipStreamSynchronize(v->stream));
+    // one launch, ordered on `stream` before anything that uses the volume next; the pool is not
+    // cleared: a block starts at (0, 0) in the batch that allocates it (launch_integrate first_new)
+    const int nctr = 2 * kCountersTotal + 8;
+    const int64_t cells = std::max<int64_t>(v->tab.cap, nctr);
+    hipLaunchKernelGGL(k_reset_table, dim3((unsigned)((cells + 255) / 256)), dim3(256), 0, v->stream, v->tab, v->mask1,
+                       v->counters, nctr);
+    MQR_CHECK_HIP(hipGetLastError());
     v->pool_count = 0;
     return 0;
 }
@@ -641,11 +642,12 @@ int mqr_integrate_frames(mqr_vbg* v, const float* depths, int depth_loc, int B, 
                                  v->table(p), 1))
                     return 1;
                 if (resolve_pool_overflow(v, p)) return 1;
-                if (launch_integrate(v, p, dbase, HW, H, W, empty, depth_scale, depth_max, sdf_trunc)) return 1;
+                if (launch_integrate(v, p, dbase, HW, H, W, empty, depth_scale, depth_max, sdf_trunc, (int)pool_before))
+                    return 1;
             }
             break;
         }
-        if (launch_integrate(v, p, dbase, HW, H, W, b, depth_scale, depth_max, sdf_trunc)) return 1;
+        if (launch_integrate(v, p, dbase, HW, H, W, b, depth_scale, depth_max, sdf_trunc, (int)pool_before)) return 1;
     }
     if (sync_all(v)) return 1;
     if (rc) set_error(kNoBlock);  // the prefix re-run may have overwritten the message
@@ -717,6 +719,7 @@ int mqr_integrate(mqr_vbg* v, const int32_t* keys, int64_t n, const float* depth
     MQR_CHECK_HIP(hipMemcpyAsync(dkeys, keys, sizeof(int32_t) * 3 * n, hipMemcpyHostToDevice, v->stream));
     const int idx = 0;
     const int64_t dframe = 0;
+    const int64_t pool_before = v->pool_count;
     if (upload_frames(v, 0, K, T_wc, &idx, 1, &dframe) || reset_batch_counters(v, 0)) return 1;
     hipLaunchKernelGGL(k_activate, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, v->stream, dkeys, n, v->table(0),
                        v->ctr(0), v->pool_ctr(), v->pool_cap, v->bkeys, v->lists[0], v->list_cap, 1);
@@ -725,7 +728,8 @@ int mqr_integrate(mqr_vbg* v, const int32_t* keys, int64_t n, const float* depth
         (void)hipFree(dkeys);
         return 1;
     }
-    int rc = launch_integrate(v, 0, dptr, HW, H, W, 1, depth_scale, depth_max, v->voxel_size * trunc_mult);
+    int rc = launch_integrate(v, 0, dptr, HW, H, W, 1, depth_scale, depth_max, v->voxel_size * trunc_mult,
+                              (int)pool_before);
     if (sync_all(v)) rc = 1;
     MQR_CHECK_HIP(hipFree(dkeys));
     return rc;

@@ -185,7 +185,7 @@ __global__ __launch_bounds__(256) void k_integrate(const int32_t* __restrict__ l
                                                    float voxel_size, const float* __restrict__ depths, int64_t HW,
                                                    int H, int W, const FrameParams* __restrict__ fps,
                                                    const int64_t* __restrict__ depth_frame, float depth_scale,
-                                                   float depth_max, float sdf_trunc) {
+                                                   float depth_max, float sdf_trunc, int first_new) {
     const int64_t n = min((int64_t)counters[kListCount], list_cap);
     const int R3 = R * R * R;
     const float hm1 = (float)H - 1.0f, wm1 = (float)W - 1.0f;
@@ -202,8 +202,9 @@ __global__ __launch_bounds__(256) void k_integrate(const int32_t* __restrict__ l
                 const float xs = (float)(xb * R + xv) * voxel_size;
                 const float ys = (float)(yb * R + yv) * voxel_size;
                 const float zs = (float)(zb * R + zv) * voxel_size;
-                float2 tw = vox[p];
-                bool dirty = false;
+                const bool fresh = buf >= first_new;  // allocated by this batch: starts at (0, 0)
+                float2 tw = fresh ? make_float2(0.f, 0.f) : vox[p];
+                bool dirty = fresh;
                 bmask_t m = mask;
                 while (m) {
                     const int f = __builtin_ctzll(m);
@@ -337,7 +338,7 @@ __global__ __launch_bounds__(NT) void k_integrate_t(const int32_t* __restrict__ 
                                                     const float* __restrict__ depths, int64_t HW, int H, int W,
                                                     const FrameParams* __restrict__ fps,
                                                     const int64_t* __restrict__ depth_frame, float depth_scale,
-                                                    float depth_max, float sdf_trunc) {
+                                                    float depth_max, float sdf_trunc, int first_new) {
     constexpr int R2 = R * R;
     constexpr int R3 = R2 * R;
     constexpr int ZPER = R3 / NT;   // voxels per thread
@@ -361,12 +362,12 @@ __global__ __launch_bounds__(NT) void k_integrate_t(const int32_t* __restrict__ 
             float zs[ZPER];
 #pragma unroll
             for (int k = 0; k < ZPER; ++k) {
-                tw[k] = vox[k * NT + tid];
+                tw[k] = buf >= first_new ? make_float2(0.f, 0.f) : vox[k * NT + tid];
                 zs[k] = (float)(zb * R + z0 + k * ZSTEP) * voxel_size;
             }
             const float xs = (float)(xb * R + xv) * voxel_size;
             const float ys = (float)(yb * R + yv) * voxel_size;
-            uint32_t dirty = 0;
+            uint32_t dirty = buf >= first_new ? 0xffffffffu : 0u;  // a fresh block is written whole
             integrate_column<ZPER, G>(tw, dirty, mask, zs, xs, ys, depths, HW, W, hm1, wm1, fps, depth_frame,
                                       depth_scale, unit_scale, depth_max, sdf_trunc);
 #pragma unroll
@@ -670,7 +671,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
     const int32_t* __restrict__ list, const bmask_t* __restrict__ lmask, int32_t* __restrict__ bad_out,
     int* __restrict__ counters, int64_t list_cap, Table t, float2* __restrict__ pool, float voxel_size,
     const float* __restrict__ depths, int64_t HW, int H, int W, const FrameParams* __restrict__ fps,
-    const int64_t* __restrict__ depth_frame, float depth_max, float sdf_trunc) {
+    const int64_t* __restrict__ depth_frame, float depth_max, float sdf_trunc, int first_new) {
     constexpr int R2 = R * R;
     constexpr int R3 = R2 * R;
     constexpr int ZPER = R3 / NT;
@@ -701,7 +702,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
 #pragma unroll
             for (int k = 0; k < ZPER; ++k) {
                 const int dy = lean_dy<R, NT, MAP>(k), dz = lean_dz<R, NT, MAP>(k);
-                tw[k] = pool_load(vox, voff, (R * dy + R2 * dz) * (int)sizeof(float2));
+                // a block allocated by this batch (buffer >= first_new) starts at (0, 0): the pool is
+                // not cleared on reset or growth
+                tw[k] = buf >= first_new ? make_float2(0.f, 0.f)
+                                         : pool_load(vox, voff, (R * dy + R2 * dz) * (int)sizeof(float2));
                 xs[k] = xs0;
                 ys[k] = (float)(yb * R + vy + dy) * voxel_size;
                 zs[k] = (float)(zb * R + vz + dz) * voxel_size;
@@ -797,7 +801,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
                                                       float voxel_size, const float* __restrict__ depths,
                                                       int64_t HW, int H, int W, const FrameParams* __restrict__ fps,
                                                       const int64_t* __restrict__ depth_frame, float depth_max,
-                                                      float sdf_trunc) {
+                                                      float sdf_trunc, int first_new) {
     constexpr int R = 16, R2 = R * R, R3 = R2 * R, NT = 512, ZPER = R3 / NT, NP = ZPER / 2;
     __shared__ __attribute__((aligned(16))) float s_tile[2][kTBH * kTBP];
     __shared__ int4 s_rect[kMaxBatch];
@@ -834,7 +838,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
         const float ys = (float)(yb * R + (tid / R) % R) * voxel_size;
 #pragma unroll
         for (int k = 0; k < ZPER; ++k) {
-            const float2 a = pool_load(vox, 8u * (uint32_t)tid, k * NT * (int)sizeof(float2));
+            const float2 a = buf >= first_new ? make_float2(0.f, 0.f)
+                                              : pool_load(vox, 8u * (uint32_t)tid, k * NT * (int)sizeof(float2));
             T[k >> 1][k & 1] = a.x;
             Wt[k >> 1][k & 1] = a.y;
             zs2[k >> 1][k & 1] = (float)(zb * R + tid / R2 + k * (NT / R2)) * voxel_size;
@@ -1002,6 +1007,18 @@ __global__ void k_rehash(Table src, Table dst) {
 }
 
 __global__ void k_set_counter(int* ctr, int value) { *ctr = value; }
+
+// Empty table: keys empty, values -1, both parities' slot masks 0; and `nctr` counters 0.
+__global__ void k_reset_table(Table t, bmask_t* mask1, int* counters, int nctr) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < t.cap) {
+        t.keys[i] = kEmpty;
+        t.vals[i] = -1;
+        t.mask[i] = 0;
+        mask1[i] = 0;
+    }
+    if (i < nctr) counters[i] = 0;
+}
 
 __global__ void k_fixup_alloc(Table t, int* counters, int* pool_ctr, int64_t pool_cap, uint64_t* bkeys) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
