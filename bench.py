@@ -426,6 +426,35 @@ def pmc_traffic(H, W, frames):
     return None, None
 
 
+def pmc_binding(avg_launch_ms):
+    """The integrate kernel's binding resource from the committed rocprofv3 counter passes of the
+    default kernel (tools/pmc_ab.sh -> profiles/*_pmc_integrate_counters.json, entry "v0:..."):
+    busy fractions of the texture addresser (TA), L1 tag lookups per CU-cycle, VALU issue share.
+    The counters are per launch of this same workload; the live launch time rescales the rate."""
+    import glob
+    for path in reversed(sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_integrate_counters.json")))):
+        try:
+            rec = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        for name, r in rec.items():
+            d = r.get("derived")
+            if not name.startswith("v0:") or not d:
+                continue
+            live_cycles = avg_launch_ms * 1e-3 * d["clock_ghz"] * 1e9 if avg_launch_ms else None
+            return {"bound": "vector-memory gather path (TA address / TCP tag lookups)",
+                    "kernel": name[3:].strip(), "source": os.path.relpath(path, ROOT),
+                    "ta_busy_frac": d["ta_busy_frac"], "tcp_lookups_per_cu_cycle": d["tcp_lookups_per_cu_cycle"],
+                    "valu_issue_frac": d["valu_issue_frac"],
+                    "tcp_lookups_per_launch": r.get("TCP_TOTAL_CACHE_ACCESSES_sum"),
+                    "tcp_lookups_per_cu_cycle_live": (r.get("TCP_TOTAL_CACHE_ACCESSES_sum", 0.0) / 256 / live_cycles
+                                                      if live_cycles else None),
+                    "note": "fractions of the launch's GPU cycles (GRBM_GUI_ACTIVE) in the counter run; "
+                            "diagnostic builds (tools/diag_integrate.sh): no gathers 0.20 ms, no update ~0.34 "
+                            "of ~0.35 ms -- the gathers, not HBM or VALU, set the time (DESIGN.md §4)"}
+    return None
+
+
 def host_cores():
     """Threads this job can run at once: the affinity set, capped by a cgroup CPU quota if any."""
     try:
@@ -748,7 +777,8 @@ def main():
             "raycast": extras.get("raycast"),
             "meshfilter": extras.get("meshfilter"),
             "host_input_frames_per_s": extras.get("host_input_frames_per_s"),
-            "roofline": {"bound": "hbm", "kernel": "k_integrate", "achieved": achieved, "peak": HBM_PEAK_GBS,
+            "roofline_binding": pmc_binding(avg_ms),
+            "roofline": {"bound": "hbm", "kernel": "k_integrate_lean", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "peak_measured_copy": extras.get("hbm_copy_gbs"),
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_source": traffic_src,

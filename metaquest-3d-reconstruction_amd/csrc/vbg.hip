@@ -314,7 +314,8 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
                 hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 8, 2>), dim3(grid), dim3(512), 0, s, list, lmask,
                                    v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp,
                                    depth_frame, depth_max, sdf_trunc, first_new);
-            // exact fix-up of the blocks the fast kernel handed back (usually none: reads a zero count)
+            // exact fix-up of the blocks the fast kernel handed back (usually none: reads a zero count;
+            // redoing them inside the fast kernel costs it registers in the hot loop)
             hipLaunchKernelGGL((k_integrate_t<16, 4, 512>), dim3(8), dim3(512), 0, s, bad_list, bad_mask, bad_count,
                                v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp, depth_frame, depth_scale,
                                depth_max, sdf_trunc, first_new);

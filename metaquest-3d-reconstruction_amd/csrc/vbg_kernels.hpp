@@ -331,6 +331,35 @@ __device__ __forceinline__ void integrate_column(float2 (&tw)[ZPER], uint32_t& d
     }
 }
 
+// One block, exact arithmetic (k_integrate_t's body; also the in-kernel fallback of the lean
+// kernel): thread tid owns column (tid % R, tid / R % R), voxels z = tid / R^2 + k NT / R^2.
+template <int R, int G, int NT>
+__device__ __forceinline__ void exact_block(float2* __restrict__ vox, bool fresh, bmask_t mask, int xb, int yb, int zb,
+                                            int tid, float voxel_size, const float* __restrict__ depths, int64_t HW,
+                                            int W, float hm1, float wm1, const FrameParams* __restrict__ fps,
+                                            const int64_t* __restrict__ depth_frame, float depth_scale,
+                                            float depth_max, float sdf_trunc) {
+    constexpr int R2 = R * R;
+    constexpr int ZPER = R2 * R / NT;  // voxels per thread
+    constexpr int ZSTEP = NT / R2;     // z stride between a thread's voxels
+    const int xv = tid % R, yv = (tid / R) % R, z0 = tid / R2;
+    float2 tw[ZPER];
+    float zs[ZPER];
+#pragma unroll
+    for (int k = 0; k < ZPER; ++k) {
+        tw[k] = fresh ? make_float2(0.f, 0.f) : vox[k * NT + tid];
+        zs[k] = (float)(zb * R + z0 + k * ZSTEP) * voxel_size;
+    }
+    const float xs = (float)(xb * R + xv) * voxel_size;
+    const float ys = (float)(yb * R + yv) * voxel_size;
+    uint32_t dirty = fresh ? 0xffffffffu : 0u;  // a fresh block is written whole
+    integrate_column<ZPER, G>(tw, dirty, mask, zs, xs, ys, depths, HW, W, hm1, wm1, fps, depth_frame, depth_scale,
+                              depth_scale == 1.0f, depth_max, sdf_trunc);
+#pragma unroll
+    for (int k = 0; k < ZPER; ++k)
+        if (dirty & (1u << k)) vox[k * NT + tid] = tw[k];
+}
+
 template <int R, int G, int NT>
 __global__ __launch_bounds__(NT) void k_integrate_t(const int32_t* __restrict__ list, const bmask_t* __restrict__ lmask,
                                                     const int* __restrict__ count, int64_t list_cap, Table t,
@@ -341,39 +370,20 @@ __global__ __launch_bounds__(NT) void k_integrate_t(const int32_t* __restrict__ 
                                                     float depth_max, float sdf_trunc, int first_new) {
     constexpr int R2 = R * R;
     constexpr int R3 = R2 * R;
-    constexpr int ZPER = R3 / NT;   // voxels per thread
-    constexpr int ZSTEP = NT / R2;  // z stride between a thread's voxels
     static_assert(R3 % NT == 0 && NT % R2 == 0, "NT must divide R^3 and be a multiple of R^2");
-    static_assert(ZPER % G == 0, "group size must divide the voxels per thread");
-    const bool unit_scale = depth_scale == 1.0f;  // d / 1 == d exactly: skip the division
+    static_assert((R3 / NT) % G == 0, "group size must divide the voxels per thread");
     const int64_t n = min((int64_t)*count, list_cap);
     const float hm1 = (float)H - 1.0f, wm1 = (float)W - 1.0f;
     const int tid = threadIdx.x;
-    const int xv = tid % R, yv = (tid / R) % R, z0 = tid / R2;
     for (int64_t i = blockIdx.x; i < n; i += gridDim.x) {
         const int32_t slot = list[i];
         const int buf = t.vals[slot];
         const bmask_t mask = readfirstlane_u64(lmask ? lmask[i] : t.mask[slot]);
         int xb, yb, zb;
         unpack_key(t.keys[slot], xb, yb, zb);
-        if (buf >= 0) {
-            float2* vox = pool + (int64_t)buf * R3;
-            float2 tw[ZPER];
-            float zs[ZPER];
-#pragma unroll
-            for (int k = 0; k < ZPER; ++k) {
-                tw[k] = buf >= first_new ? make_float2(0.f, 0.f) : vox[k * NT + tid];
-                zs[k] = (float)(zb * R + z0 + k * ZSTEP) * voxel_size;
-            }
-            const float xs = (float)(xb * R + xv) * voxel_size;
-            const float ys = (float)(yb * R + yv) * voxel_size;
-            uint32_t dirty = buf >= first_new ? 0xffffffffu : 0u;  // a fresh block is written whole
-            integrate_column<ZPER, G>(tw, dirty, mask, zs, xs, ys, depths, HW, W, hm1, wm1, fps, depth_frame,
-                                      depth_scale, unit_scale, depth_max, sdf_trunc);
-#pragma unroll
-            for (int k = 0; k < ZPER; ++k)
-                if (dirty & (1u << k)) vox[k * NT + tid] = tw[k];
-        }
+        if (buf >= 0)
+            exact_block<R, G, NT>(pool + (int64_t)buf * R3, buf >= first_new, mask, xb, yb, zb, tid, voxel_size,
+                                  depths, HW, W, hm1, wm1, fps, depth_frame, depth_scale, depth_max, sdf_trunc);
         __syncthreads();
         if (tid == 0) t.mask[slot] = 0;
     }

@@ -89,26 +89,71 @@ def _try_open3d():
 
 
 def _write_ply(path, verts, normals=None, tris=None):
-    verts = np.asarray(verts, np.float32)
+    """Binary little-endian PLY in the layout Open3D's legacy writers use (``write_point_cloud`` /
+    ``write_triangle_mesh`` with ``write_ascii=False``, reference ``reconstruction_data_io.py:57-94``;
+    upstream FilePLY.cpp as recalled -- VERIFY): a ``comment Created by Open3D`` line, vertex
+    coordinates and normals as ``double`` (the legacy geometry holds float64), faces as a ``uchar``
+    count followed by ``uint`` indices.  The float32 device values widen to float64 exactly."""
+    verts = np.asarray(verts, np.float64).reshape(-1, 3)
     n = len(verts)
-    props = ["property float x", "property float y", "property float z"]
+    props = ["property double x", "property double y", "property double z"]
     cols = [verts]
     if normals is not None and len(normals) == n:
-        props += ["property float nx", "property float ny", "property float nz"]
-        cols.append(np.asarray(normals, np.float32))
-    header = ["ply", "format binary_little_endian 1.0", f"element vertex {n}"] + props
+        props += ["property double nx", "property double ny", "property double nz"]
+        cols.append(np.asarray(normals, np.float64).reshape(-1, 3))
+    header = ["ply", "format binary_little_endian 1.0", "comment Created by Open3D", f"element vertex {n}"] + props
     if tris is not None:
-        header += [f"element face {len(tris)}", "property list uchar int vertex_indices"]
+        header += [f"element face {len(tris)}", "property list uchar uint vertex_indices"]
     header.append("end_header")
     with open(path, "wb") as f:
         f.write(("\n".join(header) + "\n").encode())
-        f.write(np.ascontiguousarray(np.concatenate(cols, axis=1), dtype="<f4").tobytes())
+        f.write(np.ascontiguousarray(np.concatenate(cols, axis=1), dtype="<f8").tobytes())
         if tris is not None:
-            t = np.asarray(tris, np.int32)
-            rec = np.empty(len(t), dtype=[("c", "u1"), ("i", "<i4", (3,))])
+            t = np.asarray(tris).reshape(-1, 3)
+            if len(t) and (t.min() < 0 or t.max() >= max(n, 1)):
+                raise ValueError("triangle index out of range")
+            rec = np.empty(len(t), dtype=[("c", "u1"), ("i", "<u4", (3,))])
             rec["c"] = 3
-            rec["i"] = t
+            rec["i"] = t.astype(np.uint32)
             f.write(rec.tobytes())
+
+
+def read_ply(path):
+    """Minimal reader for binary little-endian PLY files with vertex (float / double properties)
+    and optional face (list uchar int / uint) elements: returns (properties dict, faces or None)."""
+    sizes = {"char": "i1", "uchar": "u1", "short": "<i2", "ushort": "<u2", "int": "<i4", "uint": "<u4",
+             "float": "<f4", "double": "<f8", "int8": "i1", "uint8": "u1", "int32": "<i4", "uint32": "<u4",
+             "float32": "<f4", "float64": "<f8"}
+    with open(path, "rb") as f:
+        data = f.read()
+    end = data.index(b"end_header\n") + len(b"end_header\n")
+    lines = data[:end].decode().splitlines()
+    if lines[0] != "ply" or lines[1] != "format binary_little_endian 1.0":
+        raise ValueError("not a binary little-endian PLY")
+    elems = []
+    for ln in lines[2:]:
+        tok = ln.split()
+        if tok[0] == "element":
+            elems.append((tok[1], int(tok[2]), []))
+        elif tok[0] == "property":
+            elems[-1][2].append(tok[1:])
+    off = end
+    props, faces = {}, None
+    for name, count, plist in elems:
+        if name == "vertex":
+            dt = np.dtype([(p[1], sizes[p[0]]) for p in plist])
+            arr = np.frombuffer(data, dt, count, off)
+            off += dt.itemsize * count
+            props = {k: arr[k] for k in dt.names}
+        elif name == "face":
+            (_, cnt_t, idx_t, _), = plist
+            dt = np.dtype([("c", sizes[cnt_t]), ("i", sizes[idx_t], (3,))])
+            arr = np.frombuffer(data, dt, count, off)
+            if count and (arr["c"] != 3).any():
+                raise ValueError("non-triangle face")
+            off += dt.itemsize * count
+            faces = arr["i"].astype(np.int64)
+    return props, faces
 
 
 class PointCloud:
@@ -181,3 +226,39 @@ class TriangleMesh:
 
     def write_ply(self, path):
         _write_ply(path, self.vertices, self.vertex_normals, self.triangles)
+
+
+# ---- o3d.io mirror for the reference's writers (reconstruction_data_io.py:57-94) -------------------
+def write_point_cloud(filename, pointcloud, write_ascii=False, compressed=False, print_progress=False):
+    """``o3d.io.write_point_cloud`` for ``.ply`` (binary; ``compressed`` has no effect on PLY in
+    Open3D either).  Returns True like Open3D."""
+    if write_ascii:
+        raise NotImplementedError("ASCII PLY is not written by the reference pipeline")
+    if not str(filename).lower().endswith(".ply"):
+        raise ValueError("only .ply is supported")
+    _write_ply(filename, pointcloud.points, pointcloud.normals)
+    return True
+
+
+def write_triangle_mesh(filename, mesh, write_ascii=False, compressed=False, write_vertex_normals=True,
+                        write_vertex_colors=True, write_triangle_uvs=True, print_progress=False):
+    """``o3d.io.write_triangle_mesh`` for ``.ply`` meshes without colours (the colorless raw and
+    clean meshes, ``reconstruction_data_io.py:68-78``).  Returns True like Open3D."""
+    if write_ascii:
+        raise NotImplementedError("ASCII PLY is not written by the reference pipeline")
+    if not str(filename).lower().endswith(".ply"):
+        raise ValueError("only .ply is supported")
+    normals = mesh.vertex_normals if write_vertex_normals else None
+    _write_ply(filename, mesh.vertices, normals, mesh.triangles)
+    return True
+
+
+def read_triangle_mesh(filename):
+    """Read a PLY mesh written by ``write_triangle_mesh`` (or any binary PLY with x/y/z[, nx/ny/nz]
+    and triangle faces) back as a :class:`TriangleMesh` (float32 positions, int32 triangles)."""
+    props, faces = read_ply(filename)
+    v = np.stack([props["x"], props["y"], props["z"]], 1).astype(np.float32)
+    nrm = (np.stack([props["nx"], props["ny"], props["nz"]], 1).astype(np.float32) if "nx" in props
+           else np.zeros_like(v))
+    tris = (faces if faces is not None else np.zeros((0, 3))).astype(np.int32)
+    return TriangleMesh(v, nrm, tris)

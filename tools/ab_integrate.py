@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--frames", type=int, default=500)
     ap.add_argument("--batch", type=int, default=0, help="frames per integrate_frames call (0 = all)")
+    ap.add_argument("--no-profile", action="store_true", help="no per-launch timing events (step time only)")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -40,7 +41,7 @@ def main():
             _lib.call("mqr_vbg_set_variant", vbg.handle, v)
             vbg.reset()
             vbg.stats(reset=True)
-            vbg.profile(True)
+            vbg.profile(not a.no_profile)
             t0 = time.perf_counter()
             vbg.integrate_frames((_DevPtr(d.data_ptr()), B, H, W), K, T, depth_scale=1.0, depth_max=4.0,
                                  trunc_voxel_multiplier=10.0)
