@@ -21,6 +21,7 @@ from typing import Optional
 import numpy as np
 
 from . import _lib
+from ._io import io_pool
 from ._lib import MQR_HOST, call, ptr
 from .models import ConfidenceMap, CoordinateSystem, Side
 from .o3d_utils import compute_o3d_intrinsic_matrices
@@ -116,14 +117,25 @@ def estimate_depth_confidences(depth_data_io, config: DepthConfidenceEstimationC
         todo = [i for i in range(n) if depth_data_io.load_confidence_map(side=side, timestamp=dataset.timestamps[i])
                 is None]
         cache = {}  # index -> decoded frame (None: missing / invalid), frames of the current window only
+        pool = io_pool()
+        writes = []  # npz writes in flight (the I/O threads), awaited before the next side
 
         def frame(i):
             if i not in cache:
                 cache[i] = depth_data_io.load_depth_map_by_index(side=side, dataset=dataset, index=i)
             return cache[i]
 
+        def prefetch(lo, hi):  # decode the frames of [lo, hi) not cached yet on the I/O threads
+            need = [i for i in range(max(0, lo), min(n, hi)) if i not in cache]
+            for i, d in zip(need, pool.map(lambda k: depth_data_io.load_depth_map_by_index(
+                    side=side, dataset=dataset, index=k), need)):
+                cache[i] = d
+
         for c0 in range(0, len(todo), REF_CHUNK):
-            chunk = [i for i in todo[c0:c0 + REF_CHUNK] if frame(i) is not None]  # invalid refs: no output
+            part = todo[c0:c0 + REF_CHUNK]
+            if part:
+                prefetch(part[0] - r, part[-1] + r + 1)
+            chunk = [i for i in part if frame(i) is not None]  # invalid refs: no output
             for i in [k for k in cache if chunk and k < chunk[0] - r]:
                 del cache[i]
             # runs of one frame size spanning < REF_CHUNK indices (sparse resumes keep windows small); a
@@ -146,6 +158,13 @@ def estimate_depth_confidences(depth_data_io, config: DepthConfidenceEstimationC
                                               config.depth_max, config.error_threshold, ok,
                                               device=getattr(config, "device", 0))
                 for i in refs:
-                    depth_data_io.save_confidence_map(side=side, timestamp=dataset.timestamps[i],
-                                                      confidence_map=ConfidenceMap(conf[i - a], valid[i - a]))
+                    writes.append(pool.submit(depth_data_io.save_confidence_map, side=side,
+                                              timestamp=dataset.timestamps[i],
+                                              confidence_map=ConfidenceMap(conf[i - a], valid[i - a])))
+                if len(writes) > 2 * REF_CHUNK:  # bound the maps held for writing
+                    for w in writes[:-REF_CHUNK]:
+                        w.result()
+                    writes = writes[-REF_CHUNK:]
                 j = k
+        for w in writes:  # raises the first write error, as the sequential loop would
+            w.result()

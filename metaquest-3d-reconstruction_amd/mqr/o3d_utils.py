@@ -20,6 +20,7 @@ from typing import Optional
 
 import numpy as np
 
+from ._io import io_pool
 from .geometry import Image
 from .meshfilter import filter_mesh_components  # noqa: F401  (re-exported: o3d_utils.py:241-321)
 from .raycasting import raycast_in_color_view  # noqa: F401  (re-exported: o3d_utils.py:324-341)
@@ -88,28 +89,27 @@ def integrate(dataset, depth_data_io, side, use_confidence_filtered_depth: bool,
     intrinsics = compute_o3d_intrinsic_matrices(dataset)
     read_raw = _raw_reader(depth_data_io, side)
 
+    def load_one(i):
+        if read_raw is None:
+            d = _masked_depth(depth_data_io, side, i, dataset, use_confidence_filtered_depth,
+                              confidence_threshold, valid_count_threshold)
+            return None if d is None else (i, d, None)
+        raw = read_raw(dataset.timestamps[i], dataset.widths[i], dataset.heights[i])
+        if raw is None:
+            return None
+        cm = None
+        if use_confidence_filtered_depth:
+            cm = depth_data_io.load_confidence_map(side=side, timestamp=dataset.timestamps[i])
+            if cm is None:
+                print(f"[Warning] Confidence map not found for timestamp {dataset.timestamps[i]}")
+        return i, raw, cm
+
     def load_chunk(lo):
         """Host side of one chunk: file reads only (decode + mask run on the device), or the
-        caller's own DataIO decode when it exposes no raw-buffer access."""
+        caller's own DataIO decode when it exposes no raw-buffer access; frames read by the I/O
+        threads, results in frame order."""
         hi = min(n, lo + CHUNK)
-        items = []
-        for i in range(lo, hi):
-            if read_raw is None:
-                d = _masked_depth(depth_data_io, side, i, dataset, use_confidence_filtered_depth,
-                                  confidence_threshold, valid_count_threshold)
-                if d is not None:
-                    items.append((i, d, None))
-                continue
-            raw = read_raw(dataset.timestamps[i], dataset.widths[i], dataset.heights[i])
-            if raw is None:
-                continue
-            cm = None
-            if use_confidence_filtered_depth:
-                cm = depth_data_io.load_confidence_map(side=side, timestamp=dataset.timestamps[i])
-                if cm is None:
-                    print(f"[Warning] Confidence map not found for timestamp {dataset.timestamps[i]}")
-            items.append((i, raw, cm))
-        return lo, hi, items
+        return lo, hi, [it for it in io_pool().map(load_one, range(lo, hi)) if it is not None]
 
     stage = {}  # (H, W) -> DeviceBuffer of CHUNK decoded frames
 
