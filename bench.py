@@ -618,8 +618,23 @@ def main():
 
     merge_times = []
     shard = {"out": None, "owned": 0}
+    transport = None
     if world > 1:
-        comm = make_comm(local)
+        # RCCL inside libmqr; if it cannot start on every rank (the decision is agreed over gloo), the
+        # merge falls back to mqr.distributed.merge_to_root over the gloo group -- slower, but the
+        # scaling run still measures something, and the JSON says which transport ran
+        err = None
+        try:
+            comm = make_comm(local)
+        except Exception as e:  # noqa: BLE001 -- reported in the JSON line
+            comm, err = None, f"{type(e).__name__}: {e}"
+        ok = torch.tensor([0 if comm is None else 1], dtype=torch.int32)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if not int(ok.item()) and comm is not None:
+            comm.close()
+            comm = None
+        transport = "rccl (mqr_reduce_rccl)" if comm is not None else f"gloo fallback (merge_to_root): {err}"
+        log(f"rank {rank}: merge transport {transport}")
         shard["out"] = VoxelBlockGrid(voxel_size=args.voxel, block_resolution=args.block_resolution,
                                       block_count=args.block_count, device=local)
 
@@ -632,7 +647,12 @@ def main():
         step_integrate()
         if world > 1:
             t = time.perf_counter()
-            shard["out"], shard["owned"] = merge_rccl(vbg, comm, mode=args.merge, out=shard["out"])
+            if comm is not None:
+                shard["out"], shard["owned"] = merge_rccl(vbg, comm, mode=args.merge, out=shard["out"])
+            else:
+                from mqr.distributed import merge_to_root
+                merge_to_root(vbg, root=0)
+                shard["out"], shard["owned"] = vbg, (vbg.size() if rank == 0 else 0)
             torch.cuda.synchronize()
             merge_times.append(time.perf_counter() - t)
 
@@ -763,9 +783,11 @@ def main():
                        "block_resolution": args.block_resolution, "depth_max": args.depth_max,
                        "trunc_voxel_multiplier": args.trunc, "frame_batch": 64,
                        "parallelism": f"frame-shard x{world}" + (
-                           f" + libmqr RCCL merge ({args.merge})" if world > 1 else "")},
+                           (f" + libmqr RCCL merge ({args.merge})" if transport and transport.startswith("rccl")
+                            else " + gloo merge to rank 0 (fallback)") if world > 1 else "")},
             "sharded_extract": sharded,
             "merge_ms": (sum(merge_times) / len(merge_times) * 1e3) if merge_times else None,
+            "merge_transport": transport,
             "union_blocks": blocks if world > 1 else None,
             "extract_ms": ext_ms,
             "extract": {"weight_threshold": args.extract_threshold, "vertices": nv, "triangles": nt,

@@ -87,6 +87,20 @@ def test_c2_room_500_frames_5mm(vbg_mod, c2_seq):
     assert n15 >= n30 > 1_000_000
 
 
+def test_c2_room_320x320(vbg_mod):
+    """C2's second frame size (the Quest depth size is not recorded in the reference,
+    so C2 also runs at 320 x 320): 500 frames, 5 mm, against the oracle."""
+    from mqr import synthetic
+    seq = synthetic.make_sequence_fast("room", n=500, height=320, width=320, f=262.5, seed=1, device="cuda:0")
+    depth = seq.pop("depth_t").cpu().numpy()
+    vbg = vbg_mod.VoxelBlockGrid(voxel_size=0.005, block_resolution=16, block_count=4096)
+    vbg.integrate_frames(depth, seq["K"], seq["T_wc"], depth_scale=1.0, depth_max=4.0, trunc_voxel_multiplier=10.0)
+    ref = _oracle_volume(depth, seq["K"], seq["T_wc"], 0.005, 16, 4.0, 10.0, 8192)
+    assert ref.size() > 3000
+    assert compare_volumes(vbg.export(), ref.export(), TOL) == 0.0
+    _check_mesh(vbg, ref, 1.5)
+
+
 def test_c3_confidence_mask_integrate(vbg_mod, c2_seq):
     """C3: confidence of every frame (r = 10) on the GPU, checked against the oracle on reference
     frames at both window edges and in the middle; then the masked sequence integrates
