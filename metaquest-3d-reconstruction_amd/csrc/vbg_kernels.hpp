@@ -523,7 +523,7 @@ __device__ __forceinline__ void lean_update(float2 (&tw)[ZPER], const float (&dv
         const float sdf = d - zc;
         // zc > 0 holds in every block that is not handed to the fix-up launch
         const bool up = !(d <= 0) && !(d > depth_max) && !(sdf < -sdf_trunc);
-        const float s = sdf < sdf_trunc ? sdf : sdf_trunc;
+        const float s = __builtin_fminf(sdf, sdf_trunc);  // = (sdf < trunc ? sdf : trunc), NaN -> trunc
         const float q0 = s * y1t;  // s / sdf_trunc: div_rn_core with the reciprocal refinement hoisted
         const float q1 = __builtin_fmaf(__builtin_fmaf(-sdf_trunc, q0, s), y1t, q0);
         const float sn = __builtin_fmaf(__builtin_fmaf(-sdf_trunc, q1, s), y1t, q1);
