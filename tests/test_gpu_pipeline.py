@@ -70,3 +70,40 @@ def test_integrate_dropin_chains_volumes(tmp_path):
     a = integrate(ds[list(range(5, 10))], io, Side.LEFT, vbg_opt=a, **kw)
     b = integrate(ds, io, Side.LEFT, **kw)
     assert compare_volumes(a.export(), b.export(), 0.0) == 0.0
+
+
+def test_integrate_dropin_ragged_frame_sizes(tmp_path):
+    """Frames of different sizes in one capture (the descriptor CSV gives each frame's width and
+    height, depth_data_io.py:187-188): runs of one size go to the device in dataset order, and the
+    volume equals frame-by-frame integration."""
+    import pandas as pd
+    from gpu_helpers import compare_volumes
+    from mqr import synthetic
+    from mqr.dataio import DepthDataIO
+    from mqr.models import Side
+    from mqr.o3d_utils import _masked_depth, compute_o3d_intrinsic_matrices, integrate
+    parts = [("a", 240, 320, 262.5, 1_000_000, 5), ("b", 120, 160, 131.25, 2_000_000, 4),
+             ("c", 240, 320, 262.5, 3_000_000, 3)]
+    frames = []
+    for name, h, w, f, t0, n in parts:
+        seq = synthetic.make_sequence("room", n=n, height=h, width=w, f=f, noise=True, seed=len(frames) + 3)
+        synthetic.write_capture(tmp_path / name, seq, t0=t0)
+        frames.append(pd.read_csv(tmp_path / name / "left_depth_descriptors.csv"))
+        (tmp_path / "left_depth").mkdir(exist_ok=True)
+        for raw in (tmp_path / name / "left_depth").glob("*.raw"):
+            raw.rename(tmp_path / "left_depth" / raw.name)
+    pd.concat(frames).to_csv(tmp_path / "left_depth_descriptors.csv", index=False)
+    io = DepthDataIO(tmp_path)
+    ds = io.build_depth_dataset(Side.LEFT)
+    assert len(ds) == 12 and len(set(zip(ds.widths, ds.heights))) == 2
+    kw = dict(use_confidence_filtered_depth=False, confidence_threshold=0.0, valid_count_threshold=0)
+    vbg = integrate(ds, io, Side.LEFT, voxel_size=0.01, block_resolution=16, block_count=300, depth_max=4.0,
+                    trunc_voxel_multiplier=10.0, device="CUDA:0", **kw)
+    ref = oracle.OracleVBG(0.01, 16, 256)
+    K = compute_o3d_intrinsic_matrices(ds).astype(np.float64)
+    T = ds.transforms.extrinsics_wc.astype(np.float64)
+    for i in range(len(ds)):
+        d = _masked_depth(io, Side.LEFT, i, ds, **kw)
+        assert d is not None and d.shape == (ds.heights[i], ds.widths[i])
+        ref.integrate_frame(d, K[i], T[i], 1.0, 4.0, 10.0)
+    assert compare_volumes(vbg.export(), ref.export(), 0.0) == 0.0
