@@ -77,7 +77,7 @@ enum Counter : int {
     kListCount = 1,   // slots appended to the batch list
     kOverflow = 2,    // bit0 pool overflow, bit1 table full, bit2 list overflow, bit3 key range
     kTouched = 3,     // raw (pre-dedup) touched samples
-    kFrameBlocks = 4, // sum over frames of touched blocks (per-frame unique)
+    kFrameBlocks = 4, // (unused: per-frame new marks live at kFreshBase + f)
     kBadCount = 5,    // blocks the fast integrate kernel handed to the exact fix-up launch
     kNumCounters = 8
 };
@@ -94,7 +94,8 @@ void make_frame_params(const double* K, const double* T_wc, FrameParams* fp);
 
 constexpr int kMaxBatch = 64;         // frames per device batch (one bit each in the slot mask)
 constexpr int kFrameCounterBase = 8;  // per-frame raw touch counts live at counters[8 + f]
-constexpr int kCountersTotal = kFrameCounterBase + kMaxBatch;
+constexpr int kFreshBase = kFrameCounterBase + kMaxBatch;  // per-frame new (block, frame) marks
+constexpr int kCountersTotal = kFreshBase + kMaxBatch;
 
 // ---------------------------------------------------------------- volume
 }  // namespace mqr

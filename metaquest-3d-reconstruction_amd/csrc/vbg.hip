@@ -340,7 +340,7 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
         v->int_events.emplace_back(e0, e1);
         v->stats.integrate_launches += 1;
         v->stats.union_blocks += n;
-        v->stats.frame_blocks += v->hctr(p)[kFrameBlocks];
+        for (int f = 0; f < kMaxBatch; ++f) v->stats.frame_blocks += v->hctr(p)[kFreshBase + f];
         v->stats.frames += nframes;
     }
     MQR_CHECK_HIP(hipEventRecord(v->int_ev(p), s));

@@ -77,6 +77,82 @@ __device__ inline bool mark_slot(Table t, int64_t slot, int f, int* counters, in
     return !(old & bit);
 }
 
+// ---- wave-aggregated table updates of k_touch (call with the whole wave converged) ----------------
+// Same-address device atomics serialise (a few ns each at the home agent): per-lane list appends and
+// pool allocations of a batch's ~3 000 new blocks, one per workgroup on a shared counter, cost tens
+// of microseconds of the touch launch.  One atomic per wave per counter instead.
+
+// Insert-or-find without allocation: `won` is set for the lane whose CAS created the entry.
+__device__ inline int64_t table_claim(Table t, uint64_t k, int* counters, bool& won) {
+    const uint64_t m = (uint64_t)t.cap - 1;
+    uint64_t h = mix64(k) & m;
+    for (int64_t p = 0; p < t.cap; ++p) {
+        const uint64_t cur = t.keys[h];
+        if (cur == k) return (int64_t)h;
+        if (cur == kEmpty) {
+            const uint64_t old = atomicCAS((unsigned long long*)&t.keys[h], (unsigned long long)kEmpty,
+                                           (unsigned long long)k);
+            if (old == kEmpty) {
+                won = true;
+                return (int64_t)h;
+            }
+            if (old == k) return (int64_t)h;
+        }
+        h = (h + 1) & m;
+    }
+    atomicOr(&counters[kOverflow], 2);
+    return -1;
+}
+
+// Rank of this lane among the lanes of mask m below it, and the base one lane reserved for all of
+// them with a single atomicAdd(ctr, popcount(m)).
+__device__ inline int wave_reserve(uint64_t m, int* ctr) {
+    const int lane = threadIdx.x & 63, leader = __builtin_ctzll(m);
+    int base = 0;
+    if (lane == leader) base = atomicAdd(ctr, __popcll(m));
+    base = __shfl(base, leader, 64);
+    return base + __popcll(m & ((1ull << lane) - 1));
+}
+
+// Pool buffers for the entries this wave's lanes created (won).
+__device__ inline void wave_alloc(bool won, int64_t slot, uint64_t k, Table t, int* counters, int* pool_ctr,
+                                  int64_t pool_cap, uint64_t* bkeys) {
+    const uint64_t m = __ballot(won);
+    if (!m) return;  // wave-uniform
+    const int b = wave_reserve(m, pool_ctr);
+    if (won) {
+        if (b < pool_cap) {
+            t.vals[slot] = b;
+            bkeys[b] = k;
+        } else {
+            t.vals[slot] = -2;
+            atomicOr(&counters[kOverflow], 1);
+        }
+    }
+}
+
+// Frame bit f of the slot; `first` when the slot's batch mask was empty (the slot joins the list).
+__device__ inline bool mark_slot_bit(Table t, int64_t slot, int f, bool& first) {
+    const bmask_t bit = (bmask_t)1 << f;
+    if (__hip_atomic_load(&t.mask[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & bit) return false;
+    const bmask_t old = atomicOr((unsigned long long*)&t.mask[slot], (unsigned long long)bit);
+    first = old == 0;
+    return !(old & bit);
+}
+
+// Batch-list appends of this wave's first-marked slots.
+__device__ inline void wave_append(bool app, int64_t slot, int* counters, int32_t* list, int64_t list_cap) {
+    const uint64_t m = __ballot(app);
+    if (!m) return;  // wave-uniform
+    const int pos = wave_reserve(m, &counters[kListCount]);
+    if (app) {
+        if (pos < list_cap)
+            list[pos] = (int32_t)slot;
+        else
+            atomicOr(&counters[kOverflow], 4);
+    }
+}
+
 // Sum of a per-lane count over the wave, added to *ctr by one lane (an LDS word of the workgroup
 // here; per-thread global atomics on the batch counters serialised on a handful of addresses).
 __device__ inline void wave_add(int* ctr, int v) {
@@ -140,27 +216,30 @@ __global__ __launch_bounds__(256) void k_touch(const float* __restrict__ depths,
     }
     wave_add(&wg_count[0], valid);
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
+    for (int s = 0; s < 4; ++s) {  // every lane runs every iteration: the wave_* calls need the whole wave
         const uint64_t k = key[s];
-        if (k == kEmpty || (s > 0 && key[s - 1] == k)) continue;
         bool first = false;
-        uint32_t h = (uint32_t)mix64(k) & (kSeen - 1);
-        for (int p = 0; p < kSeen; ++p) {  // <= 1024 keys per workgroup: at most half full
-            const unsigned long long old = atomicCAS(&seen[h], (unsigned long long)kEmpty, (unsigned long long)k);
-            if (old == kEmpty) first = true;
-            if (old == kEmpty || old == k) break;
-            h = (h + 1) & (kSeen - 1);
+        if (k != kEmpty && !(s > 0 && key[s - 1] == k)) {
+            uint32_t h = (uint32_t)mix64(k) & (kSeen - 1);
+            for (int p = 0; p < kSeen; ++p) {  // <= 1024 keys per workgroup: at most half full
+                const unsigned long long old = atomicCAS(&seen[h], (unsigned long long)kEmpty, (unsigned long long)k);
+                if (old == kEmpty) first = true;
+                if (old == kEmpty || old == k) break;
+                h = (h + 1) & (kSeen - 1);
+            }
         }
-        if (first) {
-            const int64_t slot = table_insert(t, k, alloc != 0, counters, pool_ctr, pool_cap, bkeys);
-            if (slot >= 0) fresh += mark_slot(t, slot, f, counters, list, list_cap);
-        }
+        int64_t slot = -1;
+        bool won = false, app = false;
+        if (first) slot = table_claim(t, k, counters, won);
+        if (alloc) wave_alloc(won, slot, k, t, counters, pool_ctr, pool_cap, bkeys);
+        if (slot >= 0) fresh += mark_slot_bit(t, slot, f, app);
+        wave_append(app, slot, counters, list, list_cap);
     }
     wave_add(&wg_count[1], fresh);
     __syncthreads();
     if (threadIdx.x == 0) {
         if (wg_count[0]) atomicAdd(&counters[kFrameCounterBase + f], wg_count[0]);
-        if (wg_count[1]) atomicAdd(&counters[kFrameBlocks], wg_count[1]);
+        if (wg_count[1]) atomicAdd(&counters[kFreshBase + f], wg_count[1]);  // spread: one word per frame
     }
 }
 
@@ -175,7 +254,7 @@ __global__ void k_activate(const int32_t* __restrict__ keys, int64_t n, Table t,
         return;
     }
     const int64_t slot = table_insert(t, pack_key(x, y, z), true, counters, pool_ctr, pool_cap, bkeys);
-    if (slot >= 0 && mark && mark_slot(t, slot, 0, counters, list, list_cap)) atomicAdd(&counters[kFrameBlocks], 1);
+    if (slot >= 0 && mark && mark_slot(t, slot, 0, counters, list, list_cap)) atomicAdd(&counters[kFreshBase], 1);
 }
 
 // Projective TSDF update of every voxel of every listed block, frames applied in bit order.
