@@ -24,7 +24,6 @@
 #include <climits>
 #include <cstring>
 #include <mutex>
-#include <unordered_map>
 #include <vector>
 
 #include "mqr_common.hpp"
@@ -140,12 +139,19 @@ __global__ void k_merge_blocks(const int32_t* __restrict__ dst, int64_t n, const
 // ------------------------------------------------------------------ host plan
 struct MergePlan {
     int world = 1;
-    std::vector<uint64_t> uni;                 // sorted union
-    std::unordered_map<uint64_t, int64_t> idx; // key -> union index
-    std::vector<int64_t> bounds;               // owner slices, world + 1
-    std::vector<uint64_t> dmask;               // destination ranks of each union block
+    std::vector<uint64_t> uni;     // sorted union
+    std::vector<int64_t> bounds;   // owner slices of the union (indices), world + 1
+    std::vector<uint64_t> lokey;   // first key of each slice (world entries)
+    std::vector<uint64_t> dmask;   // destination ranks of each union block
     int owner(int64_t u) const {
         return (int)(std::upper_bound(bounds.begin(), bounds.end(), u) - bounds.begin()) - 1;
+    }
+    int owner_of_key(uint64_t k) const {  // the slice whose key range holds k (k in the union)
+        return std::max(0, (int)(std::upper_bound(lokey.begin(), lokey.end(), k) - lokey.begin()) - 1);
+    }
+    int64_t index(uint64_t k) const {  // union index of k, -1 if absent
+        const auto it = std::lower_bound(uni.begin(), uni.end(), k);
+        return it != uni.end() && *it == k ? (int64_t)(it - uni.begin()) : -1;
     }
 };
 
@@ -160,25 +166,32 @@ static int build_plan(const std::vector<std::vector<uint64_t>>& keys, int mode, 
     std::sort(P.uni.begin(), P.uni.end());
     P.uni.erase(std::unique(P.uni.begin(), P.uni.end()), P.uni.end());
     const int64_t U = (int64_t)P.uni.size();
-    P.idx.clear();
-    P.idx.reserve(U * 2);
-    for (int64_t u = 0; u < U; ++u) P.idx.emplace(P.uni[u], u);
     P.bounds.resize(W + 1);
     for (int r = 0; r <= W; ++r) P.bounds[r] = U * r / W;
+    P.lokey.resize(W);
+    for (int r = 0; r < W; ++r) P.lokey[r] = P.bounds[r] < U ? P.uni[P.bounds[r]] : kEmpty;
     P.dmask.assign(U, 0);
     for (int64_t u = 0; u < U; ++u) {
         if (mode == MQR_MERGE_ROOT) {
             P.dmask[u] = 1ull << root;
             continue;
         }
-        uint64_t m = 1ull << P.owner(u);
+        const int own = P.owner(u);
+        uint64_t m = 1ull << own;
         int x, y, z;
         unpack_key(P.uni[u], x, y, z);
-        for (int k = 0; k < 27; ++k) {
-            const int nx = x + k % 3 - 1, ny = y + (k / 3) % 3 - 1, nz = z + k / 9 - 1;
-            if (k == 13 || !key_in_range(nx, ny, nz)) continue;
-            auto it = P.idx.find(pack_key(nx, ny, nz));
-            if (it != P.idx.end()) m |= 1ull << P.owner(it->second);  // n's owner needs u as halo
+        // keys pack x-major, so every neighbour key lies in [pack(x-1,y-1,z-1), pack(x+1,y+1,z+1)]:
+        // a block whose neighbourhood range sits inside its own slice's key range needs no lookup
+        const bool inside = key_in_range(x - 1, y - 1, z - 1) && key_in_range(x + 1, y + 1, z + 1) &&
+                            pack_key(x - 1, y - 1, z - 1) >= P.lokey[own] &&
+                            (own + 1 == W || pack_key(x + 1, y + 1, z + 1) < P.lokey[own + 1]);
+        if (!inside) {
+            for (int k = 0; k < 27; ++k) {
+                const int nx = x + k % 3 - 1, ny = y + (k / 3) % 3 - 1, nz = z + k / 9 - 1;
+                if (k == 13 || !key_in_range(nx, ny, nz)) continue;
+                const uint64_t nk = pack_key(nx, ny, nz);
+                if (P.index(nk) >= 0) m |= 1ull << P.owner_of_key(nk);  // n's owner needs u as halo
+            }
         }
         P.dmask[u] = m;
     }
@@ -217,7 +230,7 @@ static void rank_lists(const MergePlan& P, const std::vector<std::vector<uint64_
     // sends: my blocks by union index
     const auto& mine = keys[me];
     std::vector<std::pair<int64_t, int32_t>> ub(mine.size());
-    for (size_t b = 0; b < mine.size(); ++b) ub[b] = {P.idx.at(mine[b]), (int32_t)b};
+    for (size_t b = 0; b < mine.size(); ++b) ub[b] = {P.index(mine[b]), (int32_t)b};
     std::sort(ub.begin(), ub.end());
     L.send.assign(W, {});
     for (auto& e : ub)
@@ -228,7 +241,7 @@ static void rank_lists(const MergePlan& P, const std::vector<std::vector<uint64_
     for (int s = 0; s < W; ++s) {
         std::vector<int64_t> us;
         for (uint64_t k : keys[s]) {
-            const int64_t u = P.idx.at(k);
+            const int64_t u = P.index(k);
             if (P.dmask[u] & bit) us.push_back(u);
         }
         std::sort(us.begin(), us.end());
