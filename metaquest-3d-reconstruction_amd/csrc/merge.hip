@@ -98,8 +98,10 @@ struct mqr_comm {
     size_t send_cap = 0;
     void* recvbuf = nullptr;
     size_t recv_cap = 0;
-    void* small = nullptr;  // counts, padded keys, index lists
+    void* small = nullptr;  // counts, padded keys
     size_t small_cap = 0;
+    void* lists = nullptr;  // send / receive index lists, output keys (no allocation per merge:
+    size_t lists_cap = 0;   // hipFree synchronises the device)
 };
 
 namespace mqr {
@@ -280,16 +282,20 @@ static size_t total(const std::vector<std::vector<int32_t>>& l) {
     return n;
 }
 
-// Output volume of one rank: empty it, activate its keys in order (owned first).
-static int prepare_out(mqr_vbg* out, const RankLists& L, hipStream_t s) {
+// Output volume of one rank: empty it, activate its keys in order (owned first).  `dk`: device
+// scratch for the keys (>= out_keys.size() entries), or null to allocate one here.
+static int prepare_out(mqr_vbg* out, const RankLists& L, uint64_t* dk) {
     if (mqr_vbg_reset(out)) return 1;
     if (L.out_keys.empty()) return 0;
-    uint64_t* dk = nullptr;
-    MQR_CHECK_HIP(hipMalloc(&dk, sizeof(uint64_t) * L.out_keys.size()));
-    MQR_CHECK_HIP(hipMemcpy(dk, L.out_keys.data(), sizeof(uint64_t) * L.out_keys.size(), hipMemcpyHostToDevice));
+    uint64_t* own = nullptr;
+    if (!dk) {
+        MQR_CHECK_HIP(hipMalloc(&own, sizeof(uint64_t) * L.out_keys.size()));
+        dk = own;
+    }
+    MQR_CHECK_HIP(hipMemcpyAsync(dk, L.out_keys.data(), sizeof(uint64_t) * L.out_keys.size(), hipMemcpyHostToDevice,
+                                 out->stream));
     const int rc = activate_ordered(out, dk, (int64_t)L.out_keys.size());
-    (void)hipFree(dk);
-    (void)s;
+    if (own) (void)hipFree(own);
     return rc;
 }
 
@@ -346,6 +352,7 @@ int mqr_comm_destroy(mqr_comm* c) {
     if (c->sendbuf) (void)hipFree(c->sendbuf);
     if (c->recvbuf) (void)hipFree(c->recvbuf);
     if (c->small) (void)hipFree(c->small);
+    if (c->lists) (void)hipFree(c->lists);
     if (c->s) (void)hipStreamDestroy(c->s);
     delete c;
     return 0;
@@ -390,9 +397,13 @@ int mqr_reduce_rccl(mqr_vbg* local, mqr_comm* c, int mode, int root, mqr_vbg* ou
     build_plan(keys, mode, root, P);
     RankLists L;
     rank_lists(P, keys, me, mode, L);
-    if (prepare_out(out, L, c->s)) return 1;
-    // 3. gather my outgoing blocks (segments by destination), post the sparse all-to-all
     const size_t ns = total(L.send), nr = total(L.recv);
+    // index lists, then (8-byte aligned) the output keys
+    const size_t lbytes = (sizeof(int32_t) * (ns + nr) + 7) & ~size_t(7);
+    if (grow(&c->lists, &c->lists_cap, std::max<size_t>(lbytes + sizeof(uint64_t) * L.out_keys.size(), 8))) return 1;
+    int32_t* dlists = static_cast<int32_t*>(c->lists);
+    if (prepare_out(out, L, reinterpret_cast<uint64_t*>(static_cast<char*>(c->lists) + lbytes))) return 1;
+    // 3. gather my outgoing blocks (segments by destination), post the sparse all-to-all
     const size_t eb = sizeof(float2) * R3;
     if (grow(&c->sendbuf, &c->send_cap, std::max<size_t>(ns, 1) * eb) ||
         grow(&c->recvbuf, &c->recv_cap, std::max<size_t>(nr, 1) * eb))
@@ -400,8 +411,6 @@ int mqr_reduce_rccl(mqr_vbg* local, mqr_comm* c, int mode, int root, mqr_vbg* ou
     std::vector<int32_t> sidx, ridx;
     for (auto& l : L.send) sidx.insert(sidx.end(), l.begin(), l.end());
     for (auto& l : L.recv) ridx.insert(ridx.end(), l.begin(), l.end());
-    int32_t* dlists = nullptr;
-    MQR_CHECK_HIP(hipMalloc(&dlists, sizeof(int32_t) * std::max<size_t>(ns + nr, 1)));
     int rc = upload(sidx, dlists, c->s) || upload(ridx, dlists + ns, c->s);
     if (!rc && ns)
         hipLaunchKernelGGL(k_gather_blocks, dim3((unsigned)ns), dim3(256), 0, c->s, dlists, (int64_t)ns, local->pool,
@@ -440,7 +449,6 @@ int mqr_reduce_rccl(mqr_vbg* local, mqr_comm* c, int mode, int root, mqr_vbg* ou
         set_error("mqr_reduce_rccl: merge kernels failed");
         rc = 1;
     }
-    (void)hipFree(dlists);
     *n_owned = rc ? 0 : L.n_owned;
     return rc;
 }
@@ -484,7 +492,7 @@ int mqr_merge_local(mqr_vbg** locals, int n, int mode, int root, mqr_vbg** outs,
     for (int d = 0; d < n && !rc; ++d) {
         mqr_vbg* o = outs[d];
         MQR_CHECK_HIP(hipSetDevice(o->device));
-        if (prepare_out(o, L[d], o->stream)) {
+        if (prepare_out(o, L[d], nullptr)) {
             rc = 1;
             break;
         }

@@ -45,6 +45,23 @@ def main():
             ts.append(time.perf_counter() - t0)
             outs = [o for o, _ in got]
         res[mode] = {"ms": sorted(ts[1:])[len(ts[1:]) // 2] * 1e3, "owned": [n for _, n in got]}
+    # the RCCL path at world size 1 (plan, output volume, gather, merge kernels; no peers)
+    import torch.distributed as dist
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29541")
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    from mqr.distributed import make_comm, merge_rccl
+    comm = make_comm(0)
+    for mode in ("sharded", "root"):
+        out, ts = None, []
+        for _ in range(a.reps + 1):
+            t0 = time.perf_counter()
+            out, owned = merge_rccl(vols[0], comm, mode=mode, out=out)
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        res["rccl_world1_" + mode] = {"ms": sorted(ts[1:])[len(ts[1:]) // 2] * 1e3, "owned": owned}
+    comm.close()
+    dist.destroy_process_group()
     print(json.dumps(res), flush=True)
 
 
