@@ -33,6 +33,27 @@ def shard_range(n_frames: int, rank: int, world: int):
     return lo, lo + base + (1 if rank < extra else 0)
 
 
+def confidence_shard(depths, intrinsics, T_cw, T_cw_inv, rank: int, world: int, target_frame_range=10,
+                     depth_max=3.0, error_threshold=0.05, frame_ok=None, device=0):
+    """This rank's share of the confidence maps (reference frames are independent):
+    reference frames shard_range(n, rank, world), read with a +-r halo of neighbour frames; no
+    collective.  The shards of all ranks concatenate, in rank order, to the single-GPU result.
+    Returns (lo, hi, conf (hi-lo,H,W) f64, valid (hi-lo,H,W) i32)."""
+    from .confidence import confidence_maps
+    n = len(depths)
+    lo, hi = shard_range(n, rank, world)
+    if hi <= lo:
+        H, W = np.shape(depths)[1:]
+        return lo, hi, np.empty((0, H, W), np.float64), np.empty((0, H, W), np.int32)
+    r = int(target_frame_range)
+    a, b = max(0, lo - r), min(n, hi + r)  # the window the kernel reads; indices stay global through lo - a
+    ok = None if frame_ok is None else np.asarray(frame_ok)[a:b]
+    conf, valid = confidence_maps(np.asarray(depths)[a:b], np.asarray(intrinsics)[a:b], np.asarray(T_cw)[a:b],
+                                  np.asarray(T_cw_inv)[a:b], lo - a, hi - a, r, depth_max, error_threshold, ok,
+                                  device=device)
+    return lo, hi, conf, valid
+
+
 def union_keys(local_keys: np.ndarray, group=None, device=None) -> np.ndarray:
     """All-gather every rank's block keys; return the sorted (lexicographic) union, int32 (U,3)."""
     import torch

@@ -63,3 +63,25 @@ def test_multi_rank_merge_on_gpu(world, method):
     _, U, k, t, w = res[0]
     assert all(res[r][1] == U for r in range(world)) and U == ref.size()
     assert compare_volumes((k, t, w), ref.export(), 1e-4) < 1e-5
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_confidence_shards_concatenate_to_single_pass(world):
+    """§8(e) confidence: each rank computes its reference-frame range with a +-r halo, no collective;
+    the shards in rank order equal the single-GPU maps bit for bit (an invalid frame included)."""
+    import numpy as np
+    import torch
+    assert torch.cuda.is_available()
+    from mqr import synthetic
+    from mqr.confidence import confidence_maps
+    from mqr.distributed import confidence_shard
+    seq = synthetic.make_sequence("room", n=23, height=120, width=160, f=131.25, noise=True, seed=4)
+    d, K, Tcw = seq["depth"], seq["K"], seq["T_cw"]
+    Ti = np.linalg.inv(Tcw)
+    ok = np.ones(len(d), np.uint8)
+    ok[7] = 0
+    full_c, full_v = confidence_maps(d, K, Tcw, Ti, 0, len(d), 4, 4.0, 0.08, ok)
+    parts = [confidence_shard(d, K, Tcw, Ti, r, world, 4, 4.0, 0.08, ok) for r in range(world)]
+    assert [p[0] for p in parts] == sorted(p[0] for p in parts) and parts[-1][1] == len(d)
+    assert np.array_equal(np.concatenate([p[2] for p in parts]), full_c)
+    assert np.array_equal(np.concatenate([p[3] for p in parts]), full_v)
