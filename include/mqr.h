@@ -161,13 +161,16 @@ typedef struct mqr_stats {
     int64_t touch_launches;
     double touch_ms;
     int64_t pixels;
+    int64_t table_retries; /* batches touched again after the probe-limited table filled up */
 } mqr_stats;
 int mqr_vbg_profile(mqr_vbg* v, int enable);
 
 /* Test / tuning hooks.  mqr_vbg_set_variant: low byte = integrate kernel (0 default = lean kernel
  * where its preconditions hold, 1 generic, 2-59 specialised / A/B configurations, all bit-identical,
  * see launch_integrate in csrc/vbg.hip); bit 8 serialises touch and integrate, bit 9 keeps touch
- * order instead of longest-first, bit 10 uses 32-frame batches instead of 64.
+ * order instead of longest-first, bit 10 uses 32-frame batches instead of 64, bit 11 records
+ * system-scope ordering events, bit 12 probes one table slot per new key in the batch touch (forces
+ * the full-table undo-and-retry path; test hook), bit 13 sizes the table for the worst case (A/B).
  * mqr_check_division: exhaustive bit-pattern check of the division shortcuts used on device against
  * IEEE division (which=0: 1/b via rcp_rn, 1: a/b via div_rn, 2: a/b via the bare core, 3: 1/b via
  * rcp_nm, 4: 1/b via rcp_m, over float bit patterns [lo_bits, lo_bits+count) as b or a); returns

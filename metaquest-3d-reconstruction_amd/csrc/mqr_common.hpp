@@ -123,6 +123,7 @@ struct mqr_vbg {
     hipEvent_t ev_host[2] = {nullptr, nullptr};
     bool sys_fence = false;
     bool int_pending[2] = {false, false};
+    bool lpt_ready[2] = {false, false};  // k_lpt_order already enqueued behind this parity's touch
     hipEvent_t touch_ev(int p) const { return sys_fence ? ev_touch_sys[p] : ev_touch[p]; }
     hipEvent_t int_ev(int p) const { return sys_fence ? ev_int_sys[p] : ev_int[p]; }
 
@@ -133,6 +134,7 @@ struct mqr_vbg {
     uint64_t* bkeys = nullptr; // [pool_cap] packed key of each buffer
     int64_t pool_cap = 0;
     int64_t pool_count = 0;    // host mirror (valid after each batch)
+    int64_t batch_new_max = 0; // most blocks one integrate batch has allocated (sizes the table headroom)
 
     int32_t* lists[2] = {nullptr, nullptr};  // batch slot lists, capacity list_cap each
     int32_t* lpt[2] = {nullptr, nullptr};    // the same lists in longest-first order (k_lpt_order)
@@ -153,6 +155,8 @@ struct mqr_vbg {
     int kernel_variant = 0;    // integrate kernel configuration (launch_integrate in vbg.hip), 1 = generic
     bool pipelined = true;     // overlap touch(b+1) with integrate(b)
     bool lpt_order = true;     // integrate blocks in longest-first order
+    bool table_worst = false;  // table sized for every sample a new block (variant bit 0x2000, A/B)
+    bool probe_one = false;    // batch touch probes one slot per new key (variant bit 0x1000, test hook)
     int batch_frames = mqr::kMaxBatch;  // frames per device batch (A/B: 32, variant bit 0x400)
     // profiling
     bool profile = false;

@@ -191,6 +191,7 @@ static int upload_frames(mqr_vbg* v, int p, const double* K, const double* T, co
 
 // Counters of parity p: zero (pool counter untouched).
 static int reset_batch_counters(mqr_vbg* v, int p) {
+    v->lpt_ready[p] = false;
     MQR_CHECK_HIP(hipMemsetAsync(v->ctr(p), 0, sizeof(int) * kCountersTotal, v->stream));
     return 0;
 }
@@ -207,10 +208,16 @@ static int read_counters(mqr_vbg* v, int p) {
 }
 
 // After a touch/activate of parity p: allocate pool buffers that did not fit, if any.
-static int resolve_pool_overflow(mqr_vbg* v, int p) {
+// table_full: when given, a full table is reported there (the caller undoes the touch and retries on
+// a grown table) instead of as an error.
+static int resolve_pool_overflow(mqr_vbg* v, int p, bool* table_full = nullptr) {
     if (read_counters(v, p)) return 1;
     int* c = v->hctr(p);
     if (c[kOverflow] & 2) {
+        if (table_full) {
+            *table_full = true;
+            return 0;
+        }
         set_error("internal: block table full");
         return 1;
     }
@@ -244,6 +251,16 @@ static int resolve_pool_overflow(mqr_vbg* v, int p) {
     return 0;
 }
 
+// Longest-first order of parity p's batch list (k_lpt_order reads the list length on the device, so
+// the batch touch enqueues it before the host has read the counters).
+static int enqueue_lpt(mqr_vbg* v, int p) {
+    hipLaunchKernelGGL(k_lpt_order, dim3(1), dim3(1024), 0, v->stream, v->lists[p], v->ctr(p), v->list_cap,
+                       v->table(p).mask, v->lpt[p], reinterpret_cast<bmask_t*>(v->lpt[p] + v->list_cap));
+    MQR_CHECK_HIP(hipGetLastError());
+    v->lpt_ready[p] = true;
+    return 0;
+}
+
 // Launch the integrate kernel for parity p on `stream2`, after touch(p) (event) completed.
 // first_new: the pool size before this batch's allocations (its blocks start at (0, 0)).
 static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, int H, int W, int nframes,
@@ -258,14 +275,12 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
     const int32_t* list = v->lists[p];
     const bmask_t* lmask = nullptr;
     if (v->lpt_order && n > 1) {  // on the touch stream: overlaps the previous integrate
-        bmask_t* om = reinterpret_cast<bmask_t*>(v->lpt[p] + v->list_cap);
-        hipLaunchKernelGGL(k_lpt_order, dim3(1), dim3(1024), 0, v->stream, list, counters, v->list_cap, t.mask,
-                           v->lpt[p], om);
-        MQR_CHECK_HIP(hipGetLastError());
+        if (!v->lpt_ready[p] && enqueue_lpt(v, p)) return 1;
         if (v->pipelined) MQR_CHECK_HIP(hipEventRecord(v->touch_ev(p), v->stream));
         list = v->lpt[p];
-        lmask = om;
+        lmask = reinterpret_cast<bmask_t*>(v->lpt[p] + v->list_cap);
     }
+    v->lpt_ready[p] = false;
     if (v->pipelined) MQR_CHECK_HIP(hipStreamWaitEvent(s, v->touch_ev(p), 0));
     const FrameParams* fp = v->d_fp[p];
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -396,8 +411,10 @@ int activate_ordered(mqr_vbg* v, const uint64_t* dkeys, int64_t n) {
     return 0;
 }
 
+// max_probe: slots a new key may probe before the touch reports a full table (Table.cap = no limit).
 static int touch_launch(mqr_vbg* v, int p, const float* dbase, int64_t HW, int H, int W, int b, float depth_scale,
-                        float depth_max, float sdf_trunc, float block_size, const Table& t, int alloc) {
+                        float depth_max, float sdf_trunc, float block_size, const Table& t, int alloc,
+                        int64_t max_probe) {
     const int n = (H / 4) * (W / 4);
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (v->profile) {
@@ -408,7 +425,7 @@ static int touch_launch(mqr_vbg* v, int p, const float* dbase, int64_t HW, int H
     }
     if (n > 0)
         hipLaunchKernelGGL(k_touch, dim3((n + 255) / 256, b), dim3(256), 0, v->stream, dbase, HW, H, W, v->d_fp[p],
-                           dframe_dev(v, p), depth_scale, depth_max, sdf_trunc, block_size, t, alloc, v->ctr(p),
+                           dframe_dev(v, p), depth_scale, depth_max, sdf_trunc, block_size, t, max_probe, alloc, v->ctr(p),
                            v->pool_ctr(), v->pool_cap, v->bkeys, v->lists[p], v->list_cap);
     MQR_CHECK_HIP(hipGetLastError());
     if (v->profile) {
@@ -417,6 +434,66 @@ static int touch_launch(mqr_vbg* v, int p, const float* dbase, int64_t HW, int H
         v->stats.touch_launches += 1;
         v->stats.pixels += (int64_t)b * HW;
     }
+    return 0;
+}
+
+// Undo the touch of parity p: clear its slot marks, remove the keys it inserted (buffer index >=
+// pool_before, or -2 when the pool overflowed) and give their pool buffers back.
+static int undo_touch(mqr_vbg* v, int p, int64_t pool_before) {
+    const int64_t n = std::min<int64_t>(v->hctr(p)[kListCount], v->list_cap);
+    if (n > 0)
+        hipLaunchKernelGGL(k_clear_slots, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, v->stream, v->lists[p], n,
+                           v->table(p), 0);
+    hipLaunchKernelGGL(k_rollback, dim3((unsigned)((v->tab.cap + 255) / 256)), dim3(256), 0, v->stream, v->table(p),
+                       (int)pool_before);
+    hipLaunchKernelGGL(k_set_counter, dim3(1), dim3(1), 0, v->stream, v->pool_ctr(), (int)pool_before);
+    MQR_CHECK_HIP(hipGetLastError());
+    v->pool_count = pool_before;
+    v->lpt_ready[p] = false;
+    return 0;
+}
+
+// Table keys the touch of a batch may need room for.  The worst case (every sample of every frame a
+// new block: 4 * (H/4) * (W/4) keys per frame) would size the table at ~2^24 slots for 64 VGA frames
+// -- 470 MB that every reset clears and that the touch probes far outside the L2s -- while a batch of
+// the C2 sequence allocates ~3 000 blocks.  The table is sized for the live blocks plus a headroom of
+// 4x the largest batch seen (at least 32768), the touch probes at most kProbeLimit slots per key, and
+// a batch that overflows that is undone and touched again on a table grown to the worst case.
+// The table keeps >= 2^20 slots: the touch's mask atomics serialise per cache line, and a table of
+// 2^17 slots (16 masks per 128-byte line, ~3 of them active in a batch) made the touch 10 % and the
+// overlapped integrate 4 % slower than sparse lines did (profiles/r02_table_sizing.json).
+constexpr int64_t kMinHeadroom = 1 << 15;
+constexpr int64_t kMinTableLive = 1 << 19;  // ensure_table sizes for 2x live keys: 2^20 slots
+constexpr int64_t kProbeLimit = 128;
+
+// Touch (and allocate) frames [0, b) of the staged parity-p batch; pool overflow resolved.
+static int touch_batch(mqr_vbg* v, int p, const float* dbase, int64_t HW, int H, int W, int b, float depth_scale,
+                       float depth_max, float sdf_trunc, float block_size, int64_t max_touch) {
+    const int64_t worst = v->pool_count + b * max_touch;
+    const int64_t headroom = v->table_worst ? b * max_touch
+                                            : std::min<int64_t>(b * max_touch,
+                                                                std::max<int64_t>(kMinHeadroom, 4 * v->batch_new_max));
+    if (ensure_table(v, std::max(kMinTableLive, v->pool_count + headroom))) return 1;
+    const bool limited = v->tab.cap < next_pow2(2 * worst);
+    const int64_t pool_before = v->pool_count;
+    if (touch_launch(v, p, dbase, HW, H, W, b, depth_scale, depth_max, sdf_trunc, block_size, v->table(p), 1,
+                     limited ? (v->probe_one ? 1 : std::min(kProbeLimit, v->tab.cap)) : v->tab.cap))
+        return 1;
+    // the batch order is computed while the host waits for the counters (pool growth below only
+    // rewrites buffer indices, which the order does not read)
+    if (v->lpt_order && enqueue_lpt(v, p)) return 1;
+    bool full = false;
+    if (resolve_pool_overflow(v, p, limited ? &full : nullptr)) return 1;
+    if (full) {
+        if (undo_touch(v, p, pool_before) || ensure_table(v, worst) || reset_batch_counters(v, p)) return 1;
+        if (touch_launch(v, p, dbase, HW, H, W, b, depth_scale, depth_max, sdf_trunc, block_size, v->table(p), 1,
+                         v->tab.cap))
+            return 1;
+        if (v->lpt_order && enqueue_lpt(v, p)) return 1;
+        if (resolve_pool_overflow(v, p)) return 1;
+        v->stats.table_retries += 1;
+    }
+    v->batch_new_max = std::max(v->batch_new_max, v->pool_count - pool_before);
     return 0;
 }
 
@@ -598,8 +675,7 @@ int mqr_integrate_frames(mqr_vbg* v, const float* depths, int depth_loc, int B, 
         const int p = v->pipelined ? (batch & 1) : 0;
         const int b = (int)std::min<size_t>(nb, valid.size() - s);
         const int* idx = valid.data() + s;
-        // table headroom for every key this batch could add (a rehash waits for in-flight work)
-        if (ensure_table(v, v->pool_count + b * max_touch) || ensure_fp(v, b)) return 1;
+        if (ensure_fp(v, b)) return 1;
         if (depth_loc != MQR_DEVICE && ensure_depth(v, b * HW)) return 1;
         if (wait_parity_free(v, p)) return 1;
         const float* dbase = depths;
@@ -616,9 +692,7 @@ int mqr_integrate_frames(mqr_vbg* v, const float* depths, int depth_loc, int B, 
         }
         const int64_t pool_before = v->pool_count;
         if (upload_frames(v, p, K, T_wc, idx, b, dframe) || reset_batch_counters(v, p)) return 1;
-        if (touch_launch(v, p, dbase, HW, H, W, b, depth_scale, depth_max, sdf_trunc, block_size, v->table(p), 1))
-            return 1;
-        if (resolve_pool_overflow(v, p)) return 1;
+        if (touch_batch(v, p, dbase, HW, H, W, b, depth_scale, depth_max, sdf_trunc, block_size, max_touch)) return 1;
         int empty = -1;  // first frame of the batch that touched no block
         for (int f = 0; f < b && empty < 0; ++f)
             if (v->hctr(p)[kFrameCounterBase + f] == 0) empty = f;
@@ -628,21 +702,12 @@ int mqr_integrate_frames(mqr_vbg* v, const float* depths, int depth_loc, int B, 
             // blocks it allocated), then integrate the prefix [0, empty) as a batch of its own.
             set_error(kNoBlock);
             rc = 3;
-            const int64_t n = std::min<int64_t>(v->hctr(p)[kListCount], v->list_cap);
-            if (n > 0)
-                hipLaunchKernelGGL(k_clear_slots, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, v->stream,
-                                   v->lists[p], n, v->table(p), 0);
-            hipLaunchKernelGGL(k_rollback, dim3((unsigned)((v->tab.cap + 255) / 256)), dim3(256), 0, v->stream,
-                               v->table(p), (int)pool_before);
-            hipLaunchKernelGGL(k_set_counter, dim3(1), dim3(1), 0, v->stream, v->pool_ctr(), (int)pool_before);
-            MQR_CHECK_HIP(hipGetLastError());
-            v->pool_count = pool_before;
+            if (undo_touch(v, p, pool_before)) return 1;
             if (empty > 0) {
                 if (upload_frames(v, p, K, T_wc, idx, empty, dframe) || reset_batch_counters(v, p)) return 1;
-                if (touch_launch(v, p, dbase, HW, H, W, empty, depth_scale, depth_max, sdf_trunc, block_size,
-                                 v->table(p), 1))
+                if (touch_batch(v, p, dbase, HW, H, W, empty, depth_scale, depth_max, sdf_trunc, block_size,
+                                max_touch))
                     return 1;
-                if (resolve_pool_overflow(v, p)) return 1;
                 if (launch_integrate(v, p, dbase, HW, H, W, empty, depth_scale, depth_max, sdf_trunc, (int)pool_before))
                     return 1;
             }
@@ -678,7 +743,7 @@ int mqr_touch(mqr_vbg* v, const float* depth, int depth_loc, int H, int W, const
     const int64_t dframe = 0;
     if (upload_frames(v, 0, K, T_wc, &idx, 1, &dframe) || reset_batch_counters(v, 0)) return 1;
     if (touch_launch(v, 0, dptr, HW, H, W, 1, depth_scale, depth_max, v->voxel_size * trunc_mult,
-                     v->voxel_size * v->R, v->ftab, 0))
+                     v->voxel_size * v->R, v->ftab, 0, v->ftab.cap))
         return 1;
     if (read_counters(v, 0)) return 1;
     const int64_t cnt = v->hctr(0)[kListCount];
@@ -848,6 +913,8 @@ int mqr_vbg_set_variant(mqr_vbg* v, int variant) {
     v->lpt_order = (variant & 0x200) == 0;  // bit 9: integrate in touch order instead of longest-first
     v->batch_frames = (variant & 0x400) ? 32 : kMaxBatch;  // bit 10: 32-frame batches (A/B)
     v->sys_fence = (variant & 0x800) != 0;  // bit 11: system-scope ordering / timing events (A/B)
+    v->probe_one = (variant & 0x1000) != 0; // bit 12: force the full-table retry path (test hook)
+    v->table_worst = (variant & 0x2000) != 0; // bit 13: size the table for the worst case (round-2 A/B)
     return 0;
 }
 

@@ -82,11 +82,13 @@ __device__ inline bool mark_slot(Table t, int64_t slot, int f, int* counters, in
 // pool allocations of a batch's ~3 000 new blocks, one per workgroup on a shared counter, cost tens
 // of microseconds of the touch launch.  One atomic per wave per counter instead.
 
-// Insert-or-find without allocation: `won` is set for the lane whose CAS created the entry.
-__device__ inline int64_t table_claim(Table t, uint64_t k, int* counters, bool& won) {
+// Insert-or-find without allocation: `won` is set for the lane whose CAS created the entry.  A key
+// that finds no free slot within `max_probe` slots sets the table-full bit (the host then undoes the
+// batch's touch, grows the table to the worst case and touches again with max_probe = cap).
+__device__ inline int64_t table_claim(Table t, uint64_t k, int* counters, bool& won, int64_t max_probe) {
     const uint64_t m = (uint64_t)t.cap - 1;
     uint64_t h = mix64(k) & m;
-    for (int64_t p = 0; p < t.cap; ++p) {
+    for (int64_t p = 0; p < max_probe; ++p) {
         const uint64_t cur = t.keys[h];
         if (cur == k) return (int64_t)h;
         if (cur == kEmpty) {
@@ -168,8 +170,8 @@ __global__ __launch_bounds__(256) void k_touch(const float* __restrict__ depths,
                                                const FrameParams* __restrict__ fps,
                                                const int64_t* __restrict__ depth_frame, float depth_scale,
                                                float depth_max, float sdf_trunc, float block_size, Table t,
-                                               int alloc, int* counters, int* pool_ctr, int64_t pool_cap,
-                                               uint64_t* bkeys, int32_t* list, int64_t list_cap) {
+                                               int64_t max_probe, int alloc, int* counters, int* pool_ctr,
+                                               int64_t pool_cap, uint64_t* bkeys, int32_t* list, int64_t list_cap) {
     // keys already inserted by this workgroup (a 256-pixel strip of one frame shares most of its
     // blocks): only a key's first occurrence probes the global table and sets the frame bit
     constexpr int kSeen = 2048;
@@ -230,7 +232,7 @@ __global__ __launch_bounds__(256) void k_touch(const float* __restrict__ depths,
         }
         int64_t slot = -1;
         bool won = false, app = false;
-        if (first) slot = table_claim(t, k, counters, won);
+        if (first) slot = table_claim(t, k, counters, won, max_probe);
         if (alloc) wave_alloc(won, slot, k, t, counters, pool_ctr, pool_cap, bkeys);
         if (slot >= 0) fresh += mark_slot_bit(t, slot, f, app);
         wave_append(app, slot, counters, list, list_cap);

@@ -27,7 +27,8 @@ _vp = ctypes.c_void_p
 class MqrStats(ctypes.Structure):
     _fields_ = [("integrate_launches", ctypes.c_int64), ("integrate_ms", ctypes.c_double),
                 ("union_blocks", ctypes.c_int64), ("frame_blocks", ctypes.c_int64), ("frames", ctypes.c_int64),
-                ("touch_launches", ctypes.c_int64), ("touch_ms", ctypes.c_double), ("pixels", ctypes.c_int64)]
+                ("touch_launches", ctypes.c_int64), ("touch_ms", ctypes.c_double), ("pixels", ctypes.c_int64),
+                ("table_retries", ctypes.c_int64)]
 
 
 # name -> (restype, argtypes); every function returns int status

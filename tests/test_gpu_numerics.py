@@ -67,6 +67,34 @@ def test_specialised_integrate_equals_generic():
             assert compare_volumes(out[1], out[variant], 0.0) == 0.0, (R, variant)
 
 
+def test_table_full_retry_equals_default():
+    """The batch touch probes a bounded number of table slots per new key; a batch that fills the
+    table is undone and touched again on a table grown to the worst case.  Variant bit 0x1000 probes
+    one slot, so nearly every fresh volume takes that path -- on an empty volume and on one that
+    already holds blocks (the undo must keep those): results equal the default path bit for bit."""
+    from gpu_helpers import compare_volumes
+    from mqr import _lib, synthetic
+    from mqr.vbg import VoxelBlockGrid
+    seq = synthetic.make_sequence("room", n=20, height=240, width=320, f=262.5, noise=True, seed=33)
+    args = dict(depth_scale=1.0, depth_max=4.0, trunc_voxel_multiplier=10.0)
+    ref = VoxelBlockGrid(voxel_size=0.01, block_resolution=16, block_count=64)
+    ref.integrate_frames(seq["depth"], seq["K"], seq["T_wc"], **args)
+    ref_out = ref.export()
+    a = VoxelBlockGrid(voxel_size=0.01, block_resolution=16, block_count=64)
+    _lib.call("mqr_vbg_set_variant", a.handle, 0x1000)
+    a.stats(reset=True)
+    a.integrate_frames(seq["depth"], seq["K"], seq["T_wc"], **args)
+    assert a.stats()["table_retries"] >= 1
+    assert compare_volumes(ref_out, a.export(), 0.0) == 0.0
+    b = VoxelBlockGrid(voxel_size=0.01, block_resolution=16, block_count=64)
+    b.integrate_frames(seq["depth"][:10], seq["K"][:10], seq["T_wc"][:10], **args)
+    _lib.call("mqr_vbg_set_variant", b.handle, 0x1000)
+    b.stats(reset=True)
+    b.integrate_frames(seq["depth"][10:], seq["K"][10:], seq["T_wc"][10:], **args)
+    assert b.stats()["table_retries"] >= 1
+    assert compare_volumes(ref_out, b.export(), 0.0) == 0.0
+
+
 def test_fast_integrate_exact_fallback():
     """Depth in millimetres (depth_scale 1000: the exact kernel runs alone) with tiny non-zero
     depths, and weights near 2^61 from an imported volume: every variant equals the generic kernel."""

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--frames", type=int, default=500)
     ap.add_argument("--batch", type=int, default=0, help="frames per integrate_frames call (0 = all)")
     ap.add_argument("--no-profile", action="store_true", help="no per-launch timing events (step time only)")
+    ap.add_argument("--separate", action="store_true", help="one volume per variant (variants that size the table)")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -33,11 +34,14 @@ def main():
     B, H, W = d.shape
     K, T = seq["K"].astype(np.float64), seq["T_wc"].astype(np.float64)
     torch.cuda.synchronize()
-    vbg = VoxelBlockGrid(voxel_size=0.005, block_resolution=16, block_count=40000, device=0)
     variants = [int(x) for x in a.variants.split(",")]
+    shared = VoxelBlockGrid(voxel_size=0.005, block_resolution=16, block_count=40000, device=0)
+    vols = {v: (VoxelBlockGrid(voxel_size=0.005, block_resolution=16, block_count=40000, device=0)
+                if a.separate else shared) for v in variants}
     res = {v: {"int": [], "touch": [], "step": []} for v in variants}
     for r in range(a.rounds + 1):
         for v in variants:
+            vbg = vols[v]
             _lib.call("mqr_vbg_set_variant", vbg.handle, v)
             vbg.reset()
             vbg.stats(reset=True)
@@ -54,7 +58,7 @@ def main():
             res[v]["touch"].append(st["touch_ms"] / max(st["touch_launches"], 1))
             res[v]["step"].append(dt * 1e3)
     out = {v: {k: float(np.median(x)) for k, x in r.items()} for v, r in res.items()}
-    print(json.dumps({"variants": out, "blocks": vbg.size()}))
+    print(json.dumps({"variants": out, "blocks": shared.size() if not a.separate else vols[variants[0]].size()}))
 
 
 if __name__ == "__main__":
