@@ -155,6 +155,7 @@ struct mqr_vbg {
     int kernel_variant = 0;    // integrate kernel configuration (launch_integrate in vbg.hip), 1 = generic
     bool pipelined = true;     // overlap touch(b+1) with integrate(b)
     bool lpt_order = true;     // integrate blocks in longest-first order
+    bool touch_wait = false;   // integrate waits on a touch-stream event every batch (variant bit 0x4000, A/B)
     bool table_worst = false;  // table sized for every sample a new block (variant bit 0x2000, A/B)
     bool probe_one = false;    // batch touch probes one slot per new key (variant bit 0x1000, test hook)
     int batch_frames = mqr::kMaxBatch;  // frames per device batch (A/B: 32, variant bit 0x400)

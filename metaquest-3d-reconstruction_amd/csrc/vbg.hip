@@ -274,14 +274,23 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
     int* counters = v->ctr(p);
     const int32_t* list = v->lists[p];
     const bmask_t* lmask = nullptr;
+    // The host has just read this batch's counters (resolve_pool_overflow waits for them), so the
+    // touch -- and an order enqueued behind it -- completed: integrate needs no device-side wait on
+    // the touch stream, only for an order enqueued here, after that read.
+    bool touch_wait = v->touch_wait;
     if (v->lpt_order && n > 1) {  // on the touch stream: overlaps the previous integrate
-        if (!v->lpt_ready[p] && enqueue_lpt(v, p)) return 1;
-        if (v->pipelined) MQR_CHECK_HIP(hipEventRecord(v->touch_ev(p), v->stream));
+        if (!v->lpt_ready[p]) {
+            if (enqueue_lpt(v, p)) return 1;
+            touch_wait = true;
+        }
         list = v->lpt[p];
         lmask = reinterpret_cast<bmask_t*>(v->lpt[p] + v->list_cap);
     }
     v->lpt_ready[p] = false;
-    if (v->pipelined) MQR_CHECK_HIP(hipStreamWaitEvent(s, v->touch_ev(p), 0));
+    if (v->pipelined && touch_wait) {
+        MQR_CHECK_HIP(hipEventRecord(v->touch_ev(p), v->stream));
+        MQR_CHECK_HIP(hipStreamWaitEvent(s, v->touch_ev(p), 0));
+    }
     const FrameParams* fp = v->d_fp[p];
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (v->profile) {
@@ -474,7 +483,7 @@ static int touch_batch(mqr_vbg* v, int p, const float* dbase, int64_t HW, int H,
                                             : std::min<int64_t>(b * max_touch,
                                                                 std::max<int64_t>(kMinHeadroom, 4 * v->batch_new_max));
     if (ensure_table(v, std::max(kMinTableLive, v->pool_count + headroom))) return 1;
-    const bool limited = v->tab.cap < next_pow2(2 * worst);
+    const bool limited = v->probe_one || v->tab.cap < next_pow2(2 * worst);
     const int64_t pool_before = v->pool_count;
     if (touch_launch(v, p, dbase, HW, H, W, b, depth_scale, depth_max, sdf_trunc, block_size, v->table(p), 1,
                      limited ? (v->probe_one ? 1 : std::min(kProbeLimit, v->tab.cap)) : v->tab.cap))
@@ -915,6 +924,7 @@ int mqr_vbg_set_variant(mqr_vbg* v, int variant) {
     v->sys_fence = (variant & 0x800) != 0;  // bit 11: system-scope ordering / timing events (A/B)
     v->probe_one = (variant & 0x1000) != 0; // bit 12: force the full-table retry path (test hook)
     v->table_worst = (variant & 0x2000) != 0; // bit 13: size the table for the worst case (round-2 A/B)
+    v->touch_wait = (variant & 0x4000) != 0;  // bit 14: integrate always waits on a touch-stream event (A/B)
     return 0;
 }
 
