@@ -95,7 +95,9 @@ void make_frame_params(const double* K, const double* T_wc, FrameParams* fp);
 constexpr int kMaxBatch = 64;         // frames per device batch (one bit each in the slot mask)
 constexpr int kFrameCounterBase = 8;  // per-frame raw touch counts live at counters[8 + f]
 constexpr int kFreshBase = kFrameCounterBase + kMaxBatch;  // per-frame new (block, frame) marks
-constexpr int kCountersTotal = kFreshBase + kMaxBatch;
+constexpr int kNumGroups = 8;                               // workgroup groups that share an XCD
+constexpr int kGroupBase = kFreshBase + kMaxBatch;          // k_xcd_order: group g = [off[g], off[g+1])
+constexpr int kCountersTotal = kGroupBase + kNumGroups + 1;
 
 // ---------------------------------------------------------------- volume
 }  // namespace mqr
@@ -137,7 +139,8 @@ struct mqr_vbg {
     int64_t batch_new_max = 0; // most blocks one integrate batch has allocated (sizes the table headroom)
 
     int32_t* lists[2] = {nullptr, nullptr};  // batch slot lists, capacity list_cap each
-    int32_t* lpt[2] = {nullptr, nullptr};    // the same lists in longest-first order (k_lpt_order)
+    int32_t* lpt[2] = {nullptr, nullptr};    // the same lists reordered (k_lpt_order / k_xcd_order): slots,
+                                             // then their masks, then a group byte per entry (scratch)
     int32_t* bad[2] = {nullptr, nullptr};    // fast-kernel fix-up list: slots, then their masks
     int64_t list_cap = 0;
     int* counters = nullptr;   // device: 2 x kCountersTotal per-parity sets, then the pool counter
@@ -155,6 +158,7 @@ struct mqr_vbg {
     int kernel_variant = 0;    // integrate kernel configuration (launch_integrate in vbg.hip), 1 = generic
     bool pipelined = true;     // overlap touch(b+1) with integrate(b)
     bool lpt_order = true;     // integrate blocks in longest-first order
+    bool xcd_order = false;    // spatial groups per XCD (k_xcd_order; variant bit 0x8000, A/B)
     bool touch_wait = false;   // integrate waits on a touch-stream event every batch (variant bit 0x4000, A/B)
     bool table_worst = false;  // table sized for every sample a new block (variant bit 0x2000, A/B)
     bool probe_one = false;    // batch touch probes one slot per new key (variant bit 0x1000, test hook)

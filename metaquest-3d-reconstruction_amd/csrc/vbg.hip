@@ -82,7 +82,8 @@ static int ensure_lists(mqr_vbg* v, int64_t cap) {
         if (v->lpt[p]) MQR_CHECK_HIP(hipFree(v->lpt[p]));
         v->lists[p] = v->lpt[p] = nullptr;
         MQR_CHECK_HIP(hipMalloc(&v->lists[p], sizeof(int32_t) * cap));
-        MQR_CHECK_HIP(hipMalloc(&v->lpt[p], (sizeof(int32_t) + sizeof(bmask_t)) * cap));  // slots, then their masks
+        // slots, then their masks, then k_xcd_order's group byte per entry
+        MQR_CHECK_HIP(hipMalloc(&v->lpt[p], (sizeof(int32_t) + sizeof(bmask_t) + 1) * cap));
         if (v->bad[p]) MQR_CHECK_HIP(hipFree(v->bad[p]));
         v->bad[p] = nullptr;
         MQR_CHECK_HIP(hipMalloc(&v->bad[p], (sizeof(int32_t) + sizeof(bmask_t)) * cap));  // slots, then masks
@@ -254,8 +255,13 @@ static int resolve_pool_overflow(mqr_vbg* v, int p, bool* table_full = nullptr) 
 // Longest-first order of parity p's batch list (k_lpt_order reads the list length on the device, so
 // the batch touch enqueues it before the host has read the counters).
 static int enqueue_lpt(mqr_vbg* v, int p) {
-    hipLaunchKernelGGL(k_lpt_order, dim3(1), dim3(1024), 0, v->stream, v->lists[p], v->ctr(p), v->list_cap,
-                       v->table(p).mask, v->lpt[p], reinterpret_cast<bmask_t*>(v->lpt[p] + v->list_cap));
+    bmask_t* om = reinterpret_cast<bmask_t*>(v->lpt[p] + v->list_cap);
+    if (v->xcd_order)
+        hipLaunchKernelGGL(k_xcd_order, dim3(1), dim3(1024), 0, v->stream, v->lists[p], v->ctr(p), v->list_cap,
+                           v->table(p), v->lpt[p], om, reinterpret_cast<uint8_t*>(om + v->list_cap));
+    else
+        hipLaunchKernelGGL(k_lpt_order, dim3(1), dim3(1024), 0, v->stream, v->lists[p], v->ctr(p), v->list_cap,
+                           v->table(p).mask, v->lpt[p], om);
     MQR_CHECK_HIP(hipGetLastError());
     v->lpt_ready[p] = true;
     return 0;
@@ -287,6 +293,10 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
         lmask = reinterpret_cast<bmask_t*>(v->lpt[p] + v->list_cap);
     }
     v->lpt_ready[p] = false;
+    // the lean kernels run k_xcd_order's groups on the workgroups that share an XCD
+    const int grouped = (v->xcd_order && lmask) ? 1 : 0;
+    const unsigned lean_grid =
+        grouped ? (unsigned)(kNumGroups * std::min<int64_t>((3 * n / 2 + kNumGroups - 1) / kNumGroups, 1024)) : grid;
     if (v->pipelined && touch_wait) {
         MQR_CHECK_HIP(hipEventRecord(v->touch_ev(p), v->stream));
         MQR_CHECK_HIP(hipStreamWaitEvent(s, v->touch_ev(p), 0));
@@ -331,13 +341,13 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
                                    v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp, depth_frame,
                                    depth_max, sdf_trunc, first_new);
             else if (var == 3)
-                hipLaunchKernelGGL((k_integrate_lean<16, 512>), dim3(grid), dim3(512), 0, s, list, lmask, v->bad[p],
-                                   counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp,
-                                   depth_frame, depth_max, sdf_trunc, first_new);
-            else
-                hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 8, 2>), dim3(grid), dim3(512), 0, s, list, lmask,
+                hipLaunchKernelGGL((k_integrate_lean<16, 512>), dim3(lean_grid), dim3(512), 0, s, list, lmask,
                                    v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp,
-                                   depth_frame, depth_max, sdf_trunc, first_new);
+                                   depth_frame, depth_max, sdf_trunc, first_new, grouped);
+            else
+                hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 8, 2>), dim3(lean_grid), dim3(512), 0, s, list,
+                                   lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H,
+                                   W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
             // exact fix-up of the blocks the fast kernel handed back (usually none: reads a zero count;
             // redoing them inside the fast kernel costs it registers in the hot loop)
             hipLaunchKernelGGL((k_integrate_t<16, 4, 512>), dim3(8), dim3(512), 0, s, bad_list, bad_mask, bad_count,
@@ -350,9 +360,9 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
                                counters + kListCount, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp,
                                depth_frame, depth_scale, depth_max, sdf_trunc, first_new);
         } else {
-            hipLaunchKernelGGL((k_integrate_lean<8, 256>), dim3(grid), dim3(256), 0, s, list, lmask, v->bad[p],
+            hipLaunchKernelGGL((k_integrate_lean<8, 256>), dim3(lean_grid), dim3(256), 0, s, list, lmask, v->bad[p],
                                counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp, depth_frame,
-                               depth_max, sdf_trunc, first_new);
+                               depth_max, sdf_trunc, first_new, grouped);
             hipLaunchKernelGGL((k_integrate_t<8, 2, 256>), dim3(8), dim3(256), 0, s, bad_list, bad_mask, bad_count,
                                v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp, depth_frame, depth_scale,
                                depth_max, sdf_trunc, first_new);
@@ -925,6 +935,7 @@ int mqr_vbg_set_variant(mqr_vbg* v, int variant) {
     v->probe_one = (variant & 0x1000) != 0; // bit 12: force the full-table retry path (test hook)
     v->table_worst = (variant & 0x2000) != 0; // bit 13: size the table for the worst case (round-2 A/B)
     v->touch_wait = (variant & 0x4000) != 0;  // bit 14: integrate always waits on a touch-stream event (A/B)
+    v->xcd_order = (variant & 0x8000) != 0;   // bit 15: spatial per-XCD groups (k_xcd_order, A/B)
     return 0;
 }
 

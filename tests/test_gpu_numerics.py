@@ -44,7 +44,7 @@ def test_shortened_reciprocals_exact(which, lo, hi):
     assert mm == 0, f"mode {which}: {mm} mismatches, first bit pattern {first:#x}"
 
 
-INTEGRATE_VARIANTS = {16: (0, 2, 3, 5, 0x100, 0x200, 0x400, 0x105, 0x605, 0x800), 8: (0, 2, 0x100)}
+INTEGRATE_VARIANTS = {16: (0, 2, 3, 5, 0x100, 0x200, 0x400, 0x105, 0x605, 0x800, 0x8000, 0x8003), 8: (0, 2, 0x100, 0x8000)}
 
 
 def test_specialised_integrate_equals_generic():
