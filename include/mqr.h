@@ -166,8 +166,8 @@ typedef struct mqr_stats {
 int mqr_vbg_profile(mqr_vbg* v, int enable);
 
 /* Test / tuning hooks.  mqr_vbg_set_variant: low byte = integrate kernel (0 default = lean kernel
- * where its preconditions hold, 1 generic, 2-59 specialised / A/B configurations, all bit-identical,
- * see launch_integrate in csrc/vbg.hip); bit 8 serialises touch and integrate, bit 9 keeps touch
+ * where its preconditions hold, 1 generic, 2 exact R-specialised, 3 lean with the plate map, 5 depth
+ * from LDS tiles; all bit-identical, see launch_integrate in csrc/vbg.hip); bit 8 serialises touch and integrate, bit 9 keeps touch
  * order instead of longest-first, bit 10 uses 32-frame batches instead of 64, bit 11 records
  * system-scope ordering events, bit 12 probes one table slot per new key in the batch touch (forces
  * the full-table undo-and-retry path; test hook), bit 13 sizes the table for the worst case, bit 14 makes

@@ -309,7 +309,7 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
         MQR_REQUIRE(e0 && e1, "profiling: event creation failed");
         MQR_CHECK_HIP(hipEventRecord(e0, s));
     }
-    // The fast kernels (k_integrate_lean, k_integrate_tb) evaluate s / sdf_trunc through the division
+    // The fast kernels (k_integrate_lean, k_integrate_lt) evaluate s / sdf_trunc through the division
     // core (div_rn_core: exact while the denominator is in [2^-60, 2^60]), take depth in metres
     // (depth_scale 1: Open3D's d / 1 is d), and address the frame with 32-bit byte offsets that
     // must stay past 4HW for out-of-image voxels.  Otherwise the exact k_integrate_t runs alone.
@@ -317,8 +317,8 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
     // Variants (mqr_vbg_set_variant, low byte; all bit-identical, tests/test_gpu_numerics.py):
     //   0 default: k_integrate_lean -- R = 16: brick map, >= 8 waves per SIMD, 2 interleaved voxel
     //     chains; R = 8: plate map;  1 generic k_integrate (runtime R);  2 exact k_integrate_t;
-    //   3 k_integrate_lean with the plate map (round-1 default, A/B);  5 k_integrate_tb (R = 16:
-    //     block depth tile in LDS, A/B).  DESIGN.md §4 has the measurements behind the choice.
+    //   3 k_integrate_lean with the plate map (round-1 default, A/B);  5 k_integrate_lt (R = 16: depth
+    //     from packed LDS tiles, A/B).  DESIGN.md §4 has the measurements behind the choice.
     int var = v->kernel_variant;
     if (var != 1 && var != 2 && var != 3 && var != 5) var = 0;
     if (var != 1 && var != 2 && !lean_ok) var = 2;
@@ -337,7 +337,7 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
                                depth_frame, depth_scale, depth_max, sdf_trunc, first_new);
         } else {
             if (var == 5)
-                hipLaunchKernelGGL(k_integrate_tb, dim3(grid), dim3(512), 0, s, list, lmask, v->bad[p], counters,
+                hipLaunchKernelGGL((k_integrate_lt<1>), dim3(grid), dim3(512), 0, s, list, lmask, v->bad[p], counters,
                                    v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp, depth_frame,
                                    depth_max, sdf_trunc, first_new);
             else if (var == 3)

@@ -2,7 +2,7 @@
 // Open3D 0.19 VoxelBlockGrid semantics; float32 with no FMA contraction.
 #pragma once
 #ifndef MQR_DIAG
-#define MQR_DIAG 0  // 1 / 2: timing-only builds of the lean kernel (wrong results; never shipped)
+#define MQR_DIAG 0  // 1 / 2: timing-only builds of the lean kernel, 3 / 4 / 5 of the tile kernels (wrong results; never shipped)
 #endif
 #include <climits>
 
@@ -744,19 +744,9 @@ __device__ __forceinline__ void hand_off(int32_t* bad_out, int* counters, int64_
     reinterpret_cast<bmask_t*>(bad_out + list_cap)[j] = mask;
 }
 
-// ---- helpers of the packed / tiled kernels ---------------------------------------------------------
+// ---- helpers of the tiled kernel ------------------------------------------------------------------
 typedef __attribute__((address_space(1))) void gvoid_t;
 typedef __attribute__((address_space(3))) void lvoid_t;
-
-typedef float f2v __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ f2v fma2(f2v a, f2v b, f2v c) { return __builtin_elementwise_fma(a, b, c); }
-__device__ __forceinline__ f2v splat2(float x) { return f2v{x, x}; }
-// rcp_m of both elements: v_rcp each, the Markstein correction packed
-__device__ __forceinline__ f2v rcp_m2(f2v b) {
-    const f2v one = splat2(1.0f);
-    const f2v y0 = {__builtin_amdgcn_rcpf(b.x), __builtin_amdgcn_rcpf(b.y)};
-    return fma2(fma2(-b, y0, one), y0, y0);
-}
 
 // Index of the j-th (from 0) set bit of m (m has more than j set bits).
 __device__ __forceinline__ int nth_bit(bmask_t m, int j) {
@@ -778,72 +768,6 @@ __device__ __forceinline__ int nth_bit(bmask_t m, int j) {
         }
     }
     return base;
-}
-
-// ---- packed lean integrate ------------------------------------------------------------------------
-// The lean kernel with its arithmetic on voxel pairs (v_pk_mul / v_pk_add / v_pk_fma_f32: two
-// voxels of a thread's column per VALU instruction), the voxels' camera z kept from the projection
-// for the update, and s = min(sdf, trunc) as one v_min (minNum(NaN, t) = t, as the ternary).  Same
-// float operations in the same order per voxel as lean_gather / lean_update: bit-identical.
-template <int ZPER>
-__device__ __forceinline__ void lean_gather_pk(float (&dv)[ZPER], f2v (&zc2)[ZPER / 2], bool& bad,
-                                               const FrameParams& fp, __amdgpu_buffer_rsrc_t rs, float xs,
-                                               const float (&ys2)[ZPER / 2], const f2v (&zs2)[ZPER / 2], uint32_t W4,
-                                               float hf, float hm1, float wm1) {
-    float e[12];
-#pragma unroll
-    for (int j = 0; j < 12; ++j) e[j] = fp.ext[j];
-    const f2v FX = splat2(fp.fx), FY = splat2(fp.fy), CX = splat2(fp.cx), CY = splat2(fp.cy);
-#pragma unroll
-    for (int q = 0; q < ZPER / 2; ++q) {
-        const float ys = ys2[q];  // equal operands across q are merged
-        const f2v AX = splat2(xs * e[0] + ys * e[1]), AY = splat2(xs * e[4] + ys * e[5]);
-        const f2v AZ = splat2(xs * e[8] + ys * e[9]);
-        const f2v Z = zs2[q];
-        const f2v xc = (AX + Z * splat2(e[2])) + splat2(e[3]);
-        const f2v yc = (AY + Z * splat2(e[6])) + splat2(e[7]);
-        const f2v zc = (AZ + Z * splat2(e[10])) + splat2(e[11]);
-        bad |= (__float_as_uint(zc.x) - 0x2D800000u) > 0x30000000u;  // not 2^-36 <= zc <= 2^60
-        bad |= (__float_as_uint(zc.y) - 0x2D800000u) > 0x30000000u;
-        const f2v inv = rcp_m2(zc);
-        const f2v u = (FX * xc) * inv + CX;
-        const f2v v = (FY * yc) * inv + CY;
-        zc2[q] = zc;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const float uu = u[h], vv = v[h];
-            const bool in = (vv >= 0) & (uu >= 0) & (vv <= hm1) & (uu <= wm1);
-            const int ui = (int)(in ? uu : 0.f), vi = (int)(in ? vv : hf);
-            const uint32_t off = __umul24((uint32_t)vi, W4) + ((uint32_t)ui << 2);
-            dv[2 * q + h] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
-        }
-        __builtin_amdgcn_sched_barrier(0);
-    }
-}
-
-template <int ZPER>
-__device__ __forceinline__ void lean_update_pk(f2v (&T)[ZPER / 2], f2v (&Wt)[ZPER / 2], const float (&dv)[ZPER],
-                                               const f2v (&zc2)[ZPER / 2], float depth_max, float sdf_trunc,
-                                               float y1t) {
-    const f2v ONE = splat2(1.0f), Y1T = splat2(y1t), NTR = splat2(-sdf_trunc);
-#pragma unroll
-    for (int q = 0; q < ZPER / 2; ++q) {
-        const f2v d = {dv[2 * q], dv[2 * q + 1]};
-        const f2v sdf = d - zc2[q];
-        const bool up0 = !(d.x <= 0) && !(d.x > depth_max) && !(sdf.x < -sdf_trunc);
-        const bool up1 = !(d.y <= 0) && !(d.y > depth_max) && !(sdf.y < -sdf_trunc);
-        const f2v s = {__builtin_fminf(sdf.x, sdf_trunc), __builtin_fminf(sdf.y, sdf_trunc)};
-        const f2v q0 = s * Y1T;
-        const f2v q1 = fma2(fma2(NTR, q0, s), Y1T, q0);
-        const f2v sn = fma2(fma2(NTR, q1, s), Y1T, q1);
-        const f2v wp = Wt[q] + ONE;
-        const f2v nt = (Wt[q] * T[q] + sn) * rcp_m2(wp);
-        T[q].x = up0 ? nt.x : T[q].x;
-        T[q].y = up1 ? nt.y : T[q].y;
-        Wt[q].x = up0 ? wp.x : Wt[q].x;
-        Wt[q].y = up1 ? wp.y : Wt[q].y;
-        __builtin_amdgcn_sched_barrier(0);
-    }
 }
 
 // Thread -> voxels of the lean kernel.
@@ -936,8 +860,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
                 const int f = __builtin_ctzll(m);
                 m &= m - 1;
                 float dv[ZPER];
-                lean_gather<ZPER, ILP>(dv, bad, fps[f], frame_rsrc(depths + depth_frame[f] * HW, bytes), xs, ys, zs,
-                                       W4, hf, hm1, wm1);
+                lean_gather<ZPER, ILP>(dv, bad, fps[f], frame_rsrc(depths + depth_frame[f] * HW, bytes), xs, ys,
+                                       zs, W4, hf, hm1, wm1);
                 lean_update<ZPER, ILP>(tw, dv, fps[f], xs, ys, zs, depth_max, sdf_trunc, y1t);
             }
             if (__syncthreads_or(bad)) {  // block-uniform: the exact fix-up launch redoes it from the pool
@@ -954,90 +878,215 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
     }
 }
 
-// ---- block-tiled integrate: one LDS depth tile per (block, frame), shared by the workgroup ----------
-// Counters of the lean kernel (tools/pmc_ab.sh) show it bound by the vector-memory address path:
-// every 64-lane depth gather costs ~33 TA cycles and no VMEM instruction costs much under ~16-20,
-// coalesced or not, while VALU has slack (halving VALU with packed math did not move the time).
-// So the lever is VMEM instructions per voxel-frame pair: lean issues one per 64 pairs.  Here the
-// pixel rectangle a whole 16^3 block projects to (<= 68 x 64 px) is copied into LDS with 16-byte
-// LDS-DMA loads (global_load_lds_dwordx4: 17 lanes per 68-px row, ~ceil(17 h / 64) instructions per
-// block and frame, shared by 4096 pairs), double-buffered across the batch's frames with one
-// workgroup barrier per frame, and the voxels read their depth from LDS.  Row pitch 68 floats: rows
-// land 4 banks apart.  Column thread mapping, projection and update arithmetic of the lean kernel
-// (bit-identical).  Rectangles come from the block's 8 corners projected with the kernel's own
-// operations (all voxels lie in their hull when every corner is in front of the camera), padded by
-// 2 px, clamped to the image, the left edge aligned down to 4 px; a frame whose rectangle is too big
-// or whose corners leave [2^-30, 2^50] in z uses direct gathers, one outside the image is skipped.
-constexpr int kTBP = 68;  // tile row pitch in floats (17 chunks of 4 px)
-constexpr int kTBH = 64;  // tile rows
+// ---- tiled integrate (A/B, variant 5): depth read from LDS tiles instead of gathered from HBM ---------
+// The lean kernel is co-limited by the vector-memory address path (TA busy ~0.74 of the launch,
+// ~45 TCP tag lookups per 64-lane dword gather) and by VALU issue (~0.57).  Here the pixel rectangle
+// a block projects to in each frame -- its 8 corners projected with the kernel's own operations
+// (all voxels lie in their hull when every corner is in front of the camera), padded by 2 px,
+// clamped to the image, the left edge aligned down to 4 px -- is copied into LDS with 16-byte
+// LDS-DMA loads and the voxels read their depth from there.  Each rectangle gets only the LDS it
+// needs (pitch = its width rounded up to 4 px, size rounded up to one 64-lane copy instruction =
+// 256 floats; a 16^3 block of 5 mm voxels at 2 m covers ~22 x 22 px), and consecutive frames (bit
+// order) are packed into one half of a double buffer until it is full: one workgroup barrier per
+// group of frames, group g + 1 copied while group g is integrated.  Rectangles come from 8 waves at
+// once (frame j: wave j / 8, lanes (j % 8, corner)); the grouping is a greedy scan over a wave-wide
+// prefix sum of the tile sizes.  A frame whose rectangle exceeds 68 x 64 px, or whose corners leave
+// 2^-30 <= zc <= 2^50, uses the lean kernel's direct gathers; one outside the image is skipped.
+// Measured: TA busy 0.74 -> 0.12, but VALU +15 % (rectangles, the in-image test
+// where a rectangle touches the border) and 0.39 vs 0.34 ms per launch.  Earlier forms -- one tile
+// per frame with a barrier each (k_integrate_tb), packed f32 math at 6 waves / SIMD (k_integrate_tg)
+// -- were 0.40 ms and are gone.
+constexpr int kTBP = 68;                 // widest rectangle (px; 17 chunks of 4 px)
+constexpr int kTBH = 64;                 // tallest rectangle (rows)
+constexpr int kTGHalf = kTBP * kTBH;     // floats per half of the double buffer (17 KB): one worst-case tile
+constexpr int kTGSlots = kTGHalf / 256;  // 64-lane copy instructions per half
 
-// Projection of a thread's voxel pairs and their depth read from the frame's LDS tile.  INNER: the
-// rectangle keeps 1 px off every image edge, so a voxel inside it is inside the image (no bound
-// test).  A voxel in the image but outside the rectangle sets `bad` (the block is redone exactly;
-// its dv is then irrelevant), so dv needs no select beyond the out-of-image zero.
-template <int NP, bool INNER>
-__device__ __forceinline__ void tb_gather(float (&dv)[2 * NP], f2v (&zc2)[NP], bool& bad, const FrameParams& fp,
-                                          float xs, float ys, const f2v (&zs2)[NP], const float* tile, int rx,
-                                          int ry, uint32_t tw, uint32_t th, float hm1, float wm1) {
-    float e[12];
+struct TileShared {
+    __attribute__((aligned(16))) float tile[2][kTGHalf];
+    int4 rect[kMaxBatch];  // frame j of the block (bit order): u0, v0, width (0: outside the image,
+                           // -1: direct gathers), height | inner << 16 (1 px off every image edge)
+    int off[kMaxBatch];    // its tile's offset in its group's half (floats)
+    int fidx[kMaxBatch];   // its bit (batch frame)
+    int gstart[kMaxBatch + 1], gq[kMaxBatch];  // group g: first frame, copy instructions
+    uint8_t qf[kMaxBatch * kTGSlots];          // group g, instruction q -> frame
+    int ng;
+};
+
+// Rectangles and groups of one block's frames (call with the whole workgroup; ends on a barrier).
+__device__ __forceinline__ void tile_plan(TileShared& sh, bmask_t mask, int nf, int xb, int yb, int zb, int R,
+                                          float voxel_size, const FrameParams* __restrict__ fps, int H, int W) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    {
+        const int c = lane & 7, j = 8 * wave + (lane >> 3);
+        if (8 * wave < nf) {  // wave-uniform
+            const bool have = j < nf;
+            const int fb = have ? nth_bit(mask, j) : 0;
+            const FrameParams& fp = fps[fb];
+            const float cxs = (float)(xb * R + (c & 1) * (R - 1)) * voxel_size;
+            const float cys = (float)(yb * R + ((c >> 1) & 1) * (R - 1)) * voxel_size;
+            const float czs = (float)(zb * R + (c >> 2) * (R - 1)) * voxel_size;
+            const float xc = ((cxs * fp.ext[0] + cys * fp.ext[1]) + czs * fp.ext[2]) + fp.ext[3];
+            const float yc = ((cxs * fp.ext[4] + cys * fp.ext[5]) + czs * fp.ext[6]) + fp.ext[7];
+            const float zc = ((cxs * fp.ext[8] + cys * fp.ext[9]) + czs * fp.ext[10]) + fp.ext[11];
+            const float inv = rcp_m(zc);
+            const float u = fp.fx * xc * inv + fp.cx;
+            const float v = fp.fy * yc * inv + fp.cy;
+            int ok = zc >= 0x1p-30f && zc <= 0x1p50f && fabsf(u) < 1e6f && fabsf(v) < 1e6f;
+            float umin = u, umax = u, vmin = v, vmax = v;
 #pragma unroll
-    for (int q = 0; q < 12; ++q) e[q] = fp.ext[q];
-    const f2v AX = splat2(xs * e[0] + ys * e[1]), AY = splat2(xs * e[4] + ys * e[5]);
-    const f2v AZ = splat2(xs * e[8] + ys * e[9]);
-    const f2v FX = splat2(fp.fx), FY = splat2(fp.fy), CX = splat2(fp.cx), CY = splat2(fp.cy);
-#pragma unroll
-    for (int q = 0; q < NP; ++q) {
-        const f2v Z = zs2[q];
-        const f2v xc = (AX + Z * splat2(e[2])) + splat2(e[3]);
-        const f2v yc = (AY + Z * splat2(e[6])) + splat2(e[7]);
-        zc2[q] = (AZ + Z * splat2(e[10])) + splat2(e[11]);
-        const f2v inv = rcp_m2(zc2[q]);
-        const f2v u2 = (FX * xc) * inv + CX;
-        const f2v v2 = (FY * yc) * inv + CY;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const float u = u2[h], v = v2[h];
-            const uint32_t tu = (uint32_t)((int)u - rx), tv = (uint32_t)((int)v - ry);
-            const bool hit = (tu < tw) & (tv < th);
-            const float d = tile[hit ? __umul24(tv, (uint32_t)kTBP) + tu : 0];
-            if (INNER) {
-                bad |= !hit;
-                dv[2 * q + h] = d;
-            } else {
-                const bool in = (v >= 0) & (u >= 0) & (v <= hm1) & (u <= wm1);
-                bad |= in & !hit;
-                dv[2 * q + h] = in ? d : 0.f;
+            for (int o = 1; o <= 4; o <<= 1) {
+                umin = fminf(umin, __shfl_xor(umin, o, 64));
+                umax = fmaxf(umax, __shfl_xor(umax, o, 64));
+                vmin = fminf(vmin, __shfl_xor(vmin, o, 64));
+                vmax = fmaxf(vmax, __shfl_xor(vmax, o, 64));
+                ok &= __shfl_xor(ok, o, 64);
+            }
+            if (have && c == 0) {
+                int4 r = make_int4(0, 0, -1, 0);
+                if (ok) {
+                    const int u0 = max(0, (int)floorf(umin) - 2) & ~3, u1 = min(W - 1, (int)floorf(umax) + 2);
+                    const int v0 = max(0, (int)floorf(vmin) - 2), v1 = min(H - 1, (int)floorf(vmax) + 2);
+                    const int w = u1 - u0 + 1, h = v1 - v0 + 1;
+                    const bool inner = u0 >= 1 && u1 <= W - 2 && v0 >= 1 && v1 <= H - 2;
+                    if (w <= 0 || h <= 0)
+                        r = make_int4(0, 0, 0, 0);
+                    else if (w <= kTBP && h <= kTBH)
+                        r = make_int4(u0, v0, w, h | (inner ? 0x10000 : 0));
+                }
+                sh.rect[j] = r;
+                sh.fidx[j] = fb;
             }
         }
-        __builtin_amdgcn_sched_barrier(0);
+    }
+    __syncthreads();
+    if (wave == 0) {  // lane = frame; greedy groups over the prefix sum of tile sizes
+        const int4 r = lane < nf ? sh.rect[lane] : make_int4(0, 0, 0, 0);
+        const int A = r.z > 0 ? ((((r.w & 0xffff) * ((r.z + 3) >> 2)) + 63) >> 6) << 8 : 0;  // <= kTGHalf
+        int P = A;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int u = __shfl_up(P, o, 64);
+            if (lane >= o) P += u;
+        }
+        int s = 0, base = 0, g = 0, grp = 0, off = 0;
+        while (s < nf) {  // wave-uniform; every group takes at least frame s (A_s <= kTGHalf)
+            const uint64_t b = __ballot(lane >= s && lane < nf && P - base <= kTGHalf);
+            const int e = 64 - __builtin_clzll(b);
+            if (lane >= s && lane < e) {
+                grp = g;
+                off = P - A - base;
+            }
+            const int end = __shfl(P, e - 1, 64);
+            if (lane == 0) {
+                sh.gstart[g] = s;
+                sh.gq[g] = (end - base) >> 8;
+            }
+            base = end;
+            s = e;
+            ++g;
+        }
+        if (lane == 0) {
+            sh.gstart[g] = nf;
+            sh.ng = g;
+        }
+        if (lane < nf) {
+            sh.off[lane] = off;
+            for (int q = 0; q < (A >> 8); ++q) sh.qf[grp * kTGSlots + (off >> 8) + q] = (uint8_t)lane;
+        }
+    }
+    __syncthreads();
+}
+
+// Copy of group g into half g & 1: instruction q (wave-uniform) covers 64 consecutive 4-px chunks of
+// one frame's tile; chunks past the tile's last row re-read its row 0 into the unused tail.
+__device__ __forceinline__ void tile_stage(TileShared& sh, int g, const float* __restrict__ depths, int64_t HW, int W,
+                                           const int64_t* __restrict__ depth_frame) {
+#if MQR_DIAG == 4 || MQR_DIAG == 5  // timing diagnostics only: no tile copies
+    return;
+#endif
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, nwaves = blockDim.x >> 6;
+    const int Q = __builtin_amdgcn_readfirstlane(sh.gq[g]);
+    float* half = sh.tile[g & 1];
+    for (int q = wave; q < Q; q += nwaves) {
+        const int j = __builtin_amdgcn_readfirstlane(sh.qf[g * kTGSlots + q]);
+        const int4 r = sh.rect[j];
+        const int u0 = __builtin_amdgcn_readfirstlane(r.x), v0 = __builtin_amdgcn_readfirstlane(r.y);
+        const int pq = (__builtin_amdgcn_readfirstlane(r.z) + 3) >> 2;
+        const int h = __builtin_amdgcn_readfirstlane(r.w) & 0xffff;
+        const int fb = __builtin_amdgcn_readfirstlane(sh.fidx[j]);
+        const int c = (q - (__builtin_amdgcn_readfirstlane(sh.off[j]) >> 8)) * 64 + lane;
+        int row = (int)(((float)c + 0.5f) * __builtin_amdgcn_rcpf((float)pq));  // c / pq (c < 1088)
+        const int col = c - row * pq;
+        row = row < h ? row : 0;
+        const float* dep = depths + depth_frame[fb] * HW;
+        const int gc = min(u0 + 4 * col, W - 4);
+        __builtin_amdgcn_global_load_lds((gvoid_t*)(dep + (int64_t)(v0 + row) * W + gc), (lvoid_t*)(half + 256 * q),
+                                         16, 0, 0);
     }
 }
 
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_integrate_tb(const int32_t* __restrict__ list,
-                                                      const bmask_t* __restrict__ lmask,
-                                                      int32_t* __restrict__ bad_out, int* __restrict__ counters,
-                                                      int64_t list_cap, Table t, float2* __restrict__ pool,
-                                                      float voxel_size, const float* __restrict__ depths,
-                                                      int64_t HW, int H, int W, const FrameParams* __restrict__ fps,
-                                                      const int64_t* __restrict__ depth_frame, float depth_max,
-                                                      float sdf_trunc, int first_new) {
-    constexpr int R = 16, R2 = R * R, R3 = R2 * R, NT = 512, ZPER = R3 / NT, NP = ZPER / 2;
-    __shared__ __attribute__((aligned(16))) float s_tile[2][kTBH * kTBP];
-    __shared__ int4 s_rect[kMaxBatch];
+// Per voxel: Open3D's projection (the same operations as lean_gather), then the tile read; a voxel
+// in the image but outside its frame's rectangle sets `bad` (the block is redone exactly), one
+// outside the image reads 0 (as lean_gather's past-the-end read).  Every corner of the block has
+// 2^-30 <= zc <= 2^50 when a frame has a rectangle, so the voxels' 1 / zc by rcp_m is exact without
+// lean_gather's per-voxel range check.  INNER: the rectangle keeps 1 px off every image edge, so a
+// voxel inside it is inside the image (no bound test).
+template <int ZPER, int ILP, bool INNER>
+__device__ __forceinline__ void lean_gather_tile(float (&dv)[ZPER], bool& bad, const FrameParams& fp,
+                                                 const float* tile, int rx, int ry, uint32_t tw, uint32_t th,
+                                                 uint32_t pitch, const float (&xs)[ZPER], const float (&ys)[ZPER],
+                                                 const float (&zs)[ZPER], float hm1, float wm1) {
+    float e[12];
+#pragma unroll
+    for (int j = 0; j < 12; ++j) e[j] = fp.ext[j];
+    const float fx = fp.fx, fy = fp.fy, cx = fp.cx, cy = fp.cy;
+#pragma unroll
+    for (int k = 0; k < ZPER; ++k) {
+        const float ax = xs[k] * e[0] + ys[k] * e[1];
+        const float ay = xs[k] * e[4] + ys[k] * e[5];
+        const float az = xs[k] * e[8] + ys[k] * e[9];
+        const float xc = (ax + zs[k] * e[2]) + e[3];
+        const float yc = (ay + zs[k] * e[6]) + e[7];
+        const float zc = (az + zs[k] * e[10]) + e[11];
+        const float inv_z = rcp_m(zc);
+        const float u = fx * xc * inv_z + cx;
+        const float v = fy * yc * inv_z + cy;
+        const uint32_t tu = (uint32_t)((int)u - rx), tv = (uint32_t)((int)v - ry);
+        const bool hit = (tu < tw) & (tv < th);
+#if MQR_DIAG == 3 || MQR_DIAG == 5
+        const float d = zc + (float)((hit ? __umul24(tv, pitch) + tu : 0) & 1u) * 1e-30f;
+#else
+        const float d = tile[hit ? __umul24(tv, pitch) + tu : 0];
+#endif
+        if (INNER) {
+            bad |= !hit;
+            dv[k] = d;
+        } else {
+            const bool in = (v >= 0) & (u >= 0) & (v <= hm1) & (u <= wm1);
+            bad |= in & !hit;
+            dv[k] = in ? d : 0.f;
+        }
+        if ((k + 1) % ILP == 0) __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+template <int ILP>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_integrate_lt(
+    const int32_t* __restrict__ list, const bmask_t* __restrict__ lmask, int32_t* __restrict__ bad_out,
+    int* __restrict__ counters, int64_t list_cap, Table t, float2* __restrict__ pool, float voxel_size,
+    const float* __restrict__ depths, int64_t HW, int H, int W, const FrameParams* __restrict__ fps,
+    const int64_t* __restrict__ depth_frame, float depth_max, float sdf_trunc, int first_new) {
+    constexpr int R = 16, R2 = R * R, R3 = R2 * R, NT = 512, ZPER = R3 / NT, MAP = 1;
+    __shared__ TileShared sh;
     const int64_t n = min((int64_t)counters[kListCount], list_cap);
-    const float hm1 = (float)H - 1.0f, wm1 = (float)W - 1.0f;
+    const float hf = (float)H, hm1 = (float)H - 1.0f, wm1 = (float)W - 1.0f;
+    const uint32_t W4 = 4u * (uint32_t)W, bytes = 4u * (uint32_t)HW;
     const float y0t = __builtin_amdgcn_rcpf(sdf_trunc);
     const float y1t = __builtin_fmaf(__builtin_fmaf(-sdf_trunc, y0t, 1.0f), y0t, y0t);
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    // this lane's part of a tile copy: 64-lane instructions k = wave + 8 i (i < 3) over the tile's
-    // linear 4-px chunks, 17 per row: (row, chunk) of chunk 64 k + lane, fixed for the kernel
-    int crow[3], cchunk[3];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        const int q = 64 * (wave + 8 * i) + lane;
-        crow[i] = q / 17;
-        cchunk[i] = q - 17 * crow[i];
-    }
+    const int tid = threadIdx.x;
+    int vx, vy, vz;
+    lean_map<R, NT, MAP>(tid, vx, vy, vz);
+    const uint32_t voff = 8u * (uint32_t)(vx + R * vy + R2 * vz);
     for (int64_t i = blockIdx.x; i < n; i += gridDim.x) {
         const int32_t slot = list[i];
         const int buf = __builtin_amdgcn_readfirstlane(t.vals[slot]);
@@ -1051,131 +1100,62 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
         }
         const __amdgpu_buffer_rsrc_t vox = __builtin_amdgcn_make_buffer_rsrc(
             pool + (int64_t)buf * R3, (short)0, (int)(R3 * sizeof(float2)), 0x00020000);
-        f2v T[NP], Wt[NP], zs2[NP];
+        float2 tw[ZPER];
+        float xs[ZPER], ys[ZPER], zs[ZPER];
         bool bad = false;
-        const float xs = (float)(xb * R + tid % R) * voxel_size;
-        const float ys = (float)(yb * R + (tid / R) % R) * voxel_size;
+        const float xs0 = (float)(xb * R + vx) * voxel_size;
 #pragma unroll
         for (int k = 0; k < ZPER; ++k) {
-            const float2 a = buf >= first_new ? make_float2(0.f, 0.f)
-                                              : pool_load(vox, 8u * (uint32_t)tid, k * NT * (int)sizeof(float2));
-            T[k >> 1][k & 1] = a.x;
-            Wt[k >> 1][k & 1] = a.y;
-            zs2[k >> 1][k & 1] = (float)(zb * R + tid / R2 + k * (NT / R2)) * voxel_size;
-            bad |= !(a.y >= 0.0f && a.y <= 0x1p23f && a.y == __builtin_truncf(a.y));  // rcp_m(w + 1) exact
+            const int dy = lean_dy<R, NT, MAP>(k), dz = lean_dz<R, NT, MAP>(k);
+            tw[k] = buf >= first_new ? make_float2(0.f, 0.f)
+                                     : pool_load(vox, voff, (R * dy + R2 * dz) * (int)sizeof(float2));
+            xs[k] = xs0;
+            ys[k] = (float)(yb * R + vy + dy) * voxel_size;
+            zs[k] = (float)(zb * R + vz + dz) * voxel_size;
+            const float w = tw[k].y;  // rcp_m(w + 1) needs integer weights (a batch adds <= 64)
+            bad |= !(w >= 0.0f && w <= 0x1p23f && w == __builtin_truncf(w));
         }
-        const int nf = __popcll(mask);
-        if (wave == 0) {  // rectangles of every frame of the batch: lane = (frame in pass, corner)
-            const int c = lane & 7, jj = lane >> 3;
-            const float cxs = (float)(xb * R + (c & 1) * (R - 1)) * voxel_size;
-            const float cys = (float)(yb * R + ((c >> 1) & 1) * (R - 1)) * voxel_size;
-            const float czs = (float)(zb * R + (c >> 2) * (R - 1)) * voxel_size;
-            for (int g = 0; g * 8 < nf; ++g) {
-                const int j = g * 8 + jj;
-                const bool have = j < nf;
-                const FrameParams& fp = fps[have ? nth_bit(mask, j) : 0];
-                const float xc = ((cxs * fp.ext[0] + cys * fp.ext[1]) + czs * fp.ext[2]) + fp.ext[3];
-                const float yc = ((cxs * fp.ext[4] + cys * fp.ext[5]) + czs * fp.ext[6]) + fp.ext[7];
-                const float zc = ((cxs * fp.ext[8] + cys * fp.ext[9]) + czs * fp.ext[10]) + fp.ext[11];
-                const float inv = rcp_m(zc);
-                const float u = fp.fx * xc * inv + fp.cx;
-                const float v = fp.fy * yc * inv + fp.cy;
-                int ok = zc >= 0x1p-30f && zc <= 0x1p50f && fabsf(u) < 1e6f && fabsf(v) < 1e6f;
-                float umin = u, umax = u, vmin = v, vmax = v;
-#pragma unroll
-                for (int o = 1; o <= 4; o <<= 1) {
-                    umin = fminf(umin, __shfl_xor(umin, o, 64));
-                    umax = fmaxf(umax, __shfl_xor(umax, o, 64));
-                    vmin = fminf(vmin, __shfl_xor(vmin, o, 64));
-                    vmax = fmaxf(vmax, __shfl_xor(vmax, o, 64));
-                    ok &= __shfl_xor(ok, o, 64);
-                }
-                if (have && c == 0) {
-                    // x = left column (aligned to 4 px), y = top row, z = width (0: outside the image,
-                    // -1: direct gathers), w = height | 0x10000 when the rectangle keeps 1 px off every
-                    // image edge (then a voxel inside it is inside the image: no per-voxel bound test)
-                    int4 r = make_int4(0, 0, -1, 0);
-                    if (ok) {
-                        const int u0 = max(0, (int)floorf(umin) - 2) & ~3, u1 = min(W - 1, (int)floorf(umax) + 2);
-                        const int v0 = max(0, (int)floorf(vmin) - 2), v1 = min(H - 1, (int)floorf(vmax) + 2);
-                        const int w = u1 - u0 + 1, h = v1 - v0 + 1;
-                        const bool inner = u0 >= 1 && u1 <= W - 2 && v0 >= 1 && v1 <= H - 2;
-                        if (w <= 0 || h <= 0)
-                            r = make_int4(0, 0, 0, 0);
-                        else if (w <= kTBP && h <= kTBH)
-                            r = make_int4(u0, v0, w, h | (inner ? 0x10000 : 0));
-                    }
-                    s_rect[j] = r;
-                }
-            }
-        }
-        __syncthreads();
+        tile_plan(sh, mask, __popcll(mask), xb, yb, zb, R, voxel_size, fps, H, W);
+        const int ng = __builtin_amdgcn_readfirstlane(sh.ng);
+        tile_stage(sh, 0, depths, HW, W, depth_frame);
         bmask_t m = mask;
-        int f = __builtin_ctzll(m);
-        m &= m - 1;
-        int4 r = s_rect[0];
-        r = make_int4(__builtin_amdgcn_readfirstlane(r.x), __builtin_amdgcn_readfirstlane(r.y),
-                      __builtin_amdgcn_readfirstlane(r.z), __builtin_amdgcn_readfirstlane(r.w));
-        auto stage = [&](int fr, int4 rr, float* tile) {  // lanes past the last row re-read row 0 (never hit)
-            asm volatile("" ::: "memory");
-            const int h = rr.w & 0xffff;
-            const float* dep = depths + depth_frame[fr] * HW;
-#pragma unroll
-            for (int c = 0; c < 3; ++c) {
-                const int k = wave + 8 * c;
-                if (64 * k < 17 * h) {
-                    const int gr = rr.y + (crow[c] < h ? crow[c] : 0);
-                    const int gc = min(rr.x + 4 * cchunk[c], W - 4);
-                    __builtin_amdgcn_global_load_lds((gvoid_t*)(dep + (int64_t)gr * W + gc), (lvoid_t*)(tile + 256 * k),
-                                                     16, 0, 0);
-                }
-            }
-        };
-        if (r.z > 0) stage(f, r, s_tile[0]);
-        for (int j = 0; j < nf; ++j) {
-            const bool more = j + 1 < nf;  // block-uniform
-            const int g = more ? __builtin_ctzll(m) : 0;
-            m &= m - 1;
-            int4 rn = make_int4(0, 0, 0, 0);
-            if (more) {
-                rn = s_rect[j + 1];
-                rn = make_int4(__builtin_amdgcn_readfirstlane(rn.x), __builtin_amdgcn_readfirstlane(rn.y),
-                               __builtin_amdgcn_readfirstlane(rn.z), __builtin_amdgcn_readfirstlane(rn.w));
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's part of frame j's tile has landed
-            __syncthreads();  // ... every wave's part; and every wave is done reading frame j-1's buffer
-            if (rn.z > 0) stage(g, rn, s_tile[(j + 1) & 1]);
-            if (r.z != 0) {
+        for (int g = 0; g < ng; ++g) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's copies of group g have landed
+            __syncthreads();  // ... every wave's; and every wave is done with group g - 1's half
+            if (g + 1 < ng) tile_stage(sh, g + 1, depths, HW, W, depth_frame);
+            const float* half = sh.tile[g & 1];
+            const int j1 = __builtin_amdgcn_readfirstlane(sh.gstart[g + 1]);
+            for (int j = __builtin_amdgcn_readfirstlane(sh.gstart[g]); j < j1; ++j) {
+                const int f = __builtin_ctzll(m);
+                m &= m - 1;
+                int4 r = sh.rect[j];
+                r = make_int4(__builtin_amdgcn_readfirstlane(r.x), __builtin_amdgcn_readfirstlane(r.y),
+                              __builtin_amdgcn_readfirstlane(r.z), __builtin_amdgcn_readfirstlane(r.w));
+                if (r.z == 0) continue;  // the block is outside this frame's image
                 float dv[ZPER];
-                f2v zc2[NP];
                 if (r.z > 0) {
-                    const float* tile = s_tile[j & 1];
+                    const float* tile = half + __builtin_amdgcn_readfirstlane(sh.off[j]);
+                    const uint32_t pitch = (uint32_t)((r.z + 3) & ~3);
                     if (r.w >> 16)
-                        tb_gather<NP, true>(dv, zc2, bad, fps[f], xs, ys, zs2, tile, r.x, r.y, (uint32_t)r.z,
-                                            (uint32_t)(r.w & 0xffff), hm1, wm1);
+                        lean_gather_tile<ZPER, ILP, true>(dv, bad, fps[f], tile, r.x, r.y, (uint32_t)r.z,
+                                                          (uint32_t)(r.w & 0xffff), pitch, xs, ys, zs, hm1, wm1);
                     else
-                        tb_gather<NP, false>(dv, zc2, bad, fps[f], xs, ys, zs2, tile, r.x, r.y, (uint32_t)r.z,
-                                             (uint32_t)(r.w & 0xffff), hm1, wm1);
-                } else {  // direct gathers (the lean kernel's, with its per-voxel zc check)
-                    float ys2[NP];
-#pragma unroll
-                    for (int q = 0; q < NP; ++q) ys2[q] = ys;
-                    lean_gather_pk<ZPER>(dv, zc2, bad, fps[f], frame_rsrc(depths + depth_frame[f] * HW,
-                                                                           4u * (uint32_t)HW),
-                                         xs, ys2, zs2, 4u * (uint32_t)W, (float)H, hm1, wm1);
+                        lean_gather_tile<ZPER, ILP, false>(dv, bad, fps[f], tile, r.x, r.y, (uint32_t)r.z,
+                                                           (uint32_t)(r.w & 0xffff), pitch, xs, ys, zs, hm1, wm1);
+                } else {
+                    lean_gather<ZPER, ILP>(dv, bad, fps[f], frame_rsrc(depths + depth_frame[f] * HW, bytes), xs, ys,
+                                           zs, W4, hf, hm1, wm1);
                 }
-                lean_update_pk<ZPER>(T, Wt, dv, zc2, depth_max, sdf_trunc, y1t);
+                lean_update<ZPER, ILP>(tw, dv, fps[f], xs, ys, zs, depth_max, sdf_trunc, y1t);
             }
-            f = g;
-            r = rn;
         }
         if (__syncthreads_or(bad)) {  // block-uniform: the exact fix-up launch redoes it from the pool
             if (tid == 0) hand_off(bad_out, counters, list_cap, slot, mask);
         } else {
 #pragma unroll
             for (int k = 0; k < ZPER; ++k)
-                pool_store(vox, 8u * (uint32_t)tid, k * NT * (int)sizeof(float2),
-                           make_float2(T[k >> 1][k & 1], Wt[k >> 1][k & 1]));
+                pool_store(vox, voff, (R * lean_dy<R, NT, MAP>(k) + R2 * lean_dz<R, NT, MAP>(k)) * (int)sizeof(float2),
+                           tw[k]);
         }
         __syncthreads();
         if (tid == 0) t.mask[slot] = 0;

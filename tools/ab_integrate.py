@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--batch", type=int, default=0, help="frames per integrate_frames call (0 = all)")
     ap.add_argument("--no-profile", action="store_true", help="no per-launch timing events (step time only)")
     ap.add_argument("--separate", action="store_true", help="one volume per variant (variants that size the table)")
+    ap.add_argument("--check", action="store_true", help="compare every variant's volume with the first's, bit for bit")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -39,6 +40,7 @@ def main():
     vols = {v: (VoxelBlockGrid(voxel_size=0.005, block_resolution=16, block_count=40000, device=0)
                 if a.separate else shared) for v in variants}
     res = {v: {"int": [], "touch": [], "step": []} for v in variants}
+    check = {}
     for r in range(a.rounds + 1):
         for v in variants:
             vbg = vols[v]
@@ -57,7 +59,18 @@ def main():
             res[v]["int"].append(st["integrate_ms"] / max(st["integrate_launches"], 1))
             res[v]["touch"].append(st["touch_ms"] / max(st["touch_launches"], 1))
             res[v]["step"].append(dt * 1e3)
+            if a.check and r == a.rounds:
+                keys, tsdf, wgt = vbg.export()
+                order = np.lexsort(keys.T[::-1])
+                check[v] = (keys[order], tsdf[order], wgt[order])
     out = {v: {k: float(np.median(x)) for k, x in r.items()} for v, r in res.items()}
+    if a.check:
+        k0, t0_, w0 = check[variants[0]]
+        for v in variants[1:]:
+            k1, t1, w1 = check[v]
+            same = k0.shape == k1.shape and (k0 == k1).all() and (w0 == w1).all() and \
+                (t0_.view(np.uint32) == t1.view(np.uint32)).all()
+            out[v]["bit_identical_to_first"] = bool(same)
     print(json.dumps({"variants": out, "blocks": shared.size() if not a.separate else vols[variants[0]].size()}))
 
 

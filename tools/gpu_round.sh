@@ -24,6 +24,6 @@ grep "mqr" gpurun_out/kernel_stats.csv | cut -c1-60,300-420 | head -12
 ROUND=$ROUND bash tools/pmc_traffic.sh > gpurun_out/pmc_traffic.log 2>&1 || { tail -20 gpurun_out/pmc_traffic.log; exit 1; }
 grep -E "traffic_bytes_per_launch|alg_bytes_per_launch|traffic_over_alg|\"kernel\"" profiles/${ROUND}_pmc_traffic.json
 mkdir -p gpurun_out/profiles_new && cp profiles/${ROUND}_pmc_traffic.json profiles/${ROUND}_pmc_fetch.csv profiles/${ROUND}_pmc_write.csv gpurun_out/profiles_new/
-KRE="k_integrate_(lean|tb)" VARIANTS="0 3 5" timeout -k 10 700 bash tools/pmc_ab.sh > gpurun_out/pmc_ab_round.log 2>&1 || { tail -20 gpurun_out/pmc_ab_round.log; exit 1; }
+KRE="k_integrate_(lean|lt)" VARIANTS="0 3 5" timeout -k 10 700 bash tools/pmc_ab.sh > gpurun_out/pmc_ab_round.log 2>&1 || { tail -20 gpurun_out/pmc_ab_round.log; exit 1; }
 cp gpurun_out/pmc_ab.json gpurun_out/profiles_new/${ROUND}_pmc_integrate_counters.json
 echo round evidence done
