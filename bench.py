@@ -36,7 +36,7 @@ class _DevPtr:
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--frames", type=int, default=500)
     ap.add_argument("--height", type=int, default=480)

@@ -691,8 +691,8 @@ __device__ __forceinline__ void lean_gather(float (&dv)[ZPER], bool& bad, const 
         const float u = fx * xc * inv_z + cx;
         const float v = fy * yc * inv_z + cy;
         const bool in = (v >= 0) & (u >= 0) & (v <= hm1) & (u <= wm1);
-        const int ui = (int)(in ? u : 0.f), vi = (int)(in ? v : hf);
-        const uint32_t off = __umul24((uint32_t)vi, W4) + ((uint32_t)ui << 2);
+        // out of the image: row H (byte offset H W4 = 4HW, past the end of the frame)
+        const uint32_t off = in ? __umul24((uint32_t)(int)v, W4) + ((uint32_t)(int)u << 2) : __umul24((uint32_t)hf, W4);
 #if MQR_DIAG == 1  // timing diagnostics only (tools/diag_integrate.sh): projection without the gather
         dv[k] = zc + (float)(off & 1u) * 1e-30f;
 #else
