@@ -808,7 +808,7 @@ def main():
                          "launches": st["integrate_launches"], "union_blocks_per_launch":
                              st["union_blocks"] / launches, "frame_blocks_per_frame":
                              st["frame_blocks"] / max(st["frames"], 1),
-                         "touch_ms_per_launch": st["touch_ms"] / max(st["touch_launches"], 1)},
+                         "touch_ms_per_launch": (st["touch_ms"] / st["touch_launches"]) if st["touch_launches"] else None},
             "cpu_baseline": cpu,
             "parity": parity,
             "c3": extras.get("c3"),

@@ -163,6 +163,8 @@ typedef struct mqr_stats {
     int64_t pixels;
     int64_t table_retries; /* batches touched again after the probe-limited table filled up */
 } mqr_stats;
+/* enable: 0 off, 1 time every integrate launch (two events per batch on the integrate stream), 2 also
+ * every touch launch (two more on the touch stream); results in mqr_vbg_stats. */
 int mqr_vbg_profile(mqr_vbg* v, int enable);
 
 /* Test / tuning hooks.  mqr_vbg_set_variant: low byte = integrate kernel (0 default = lean kernel

@@ -128,6 +128,9 @@ struct mqr_vbg {
     bool lpt_ready[2] = {false, false};  // k_lpt_order already enqueued behind this parity's touch
     hipEvent_t touch_ev(int p) const { return sys_fence ? ev_touch_sys[p] : ev_touch[p]; }
     hipEvent_t int_ev(int p) const { return sys_fence ? ev_int_sys[p] : ev_int[p]; }
+    // the event that last closed parity p's integrate on its stream: int_ev(p), or, while profiling,
+    // that launch's timing end event (one event record between launches instead of two)
+    hipEvent_t int_done[2] = {nullptr, nullptr};
 
     mqr::Table tab{};          // main block table (tab.mask == mask[0])
     mqr::bmask_t* mask1 = nullptr; // parity-1 slot masks
@@ -165,6 +168,7 @@ struct mqr_vbg {
     int batch_frames = mqr::kMaxBatch;  // frames per device batch (A/B: 32, variant bit 0x400)
     // profiling
     bool profile = false;
+    bool profile_touch = false;  // mqr_vbg_profile level 2: also time the touch launches
     std::vector<std::pair<hipEvent_t, hipEvent_t>> int_events, touch_events;
     std::vector<hipEvent_t> ev_pool;  // timing events, created once and reused (hipEventCreate per
     size_t ev_used = 0;               // launch added ~0.1 ms to a 500-frame step); device-scope

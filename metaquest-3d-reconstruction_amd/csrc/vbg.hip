@@ -371,13 +371,17 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
     MQR_CHECK_HIP(hipGetLastError());
     if (v->profile) {
         MQR_CHECK_HIP(hipEventRecord(e1, s));
+        v->int_done[p] = e1;
         v->int_events.emplace_back(e0, e1);
         v->stats.integrate_launches += 1;
         v->stats.union_blocks += n;
         for (int f = 0; f < kMaxBatch; ++f) v->stats.frame_blocks += v->hctr(p)[kFreshBase + f];
         v->stats.frames += nframes;
     }
-    MQR_CHECK_HIP(hipEventRecord(v->int_ev(p), s));
+    if (!v->profile) {
+        MQR_CHECK_HIP(hipEventRecord(v->int_ev(p), s));
+        v->int_done[p] = v->int_ev(p);
+    }
     v->int_pending[p] = true;
     return 0;
 }
@@ -385,7 +389,7 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
 // Before reusing parity p's batch state on `stream`: the integrate that last used it must be done.
 static int wait_parity_free(mqr_vbg* v, int p) {
     if (v->int_pending[p]) {
-        MQR_CHECK_HIP(hipStreamWaitEvent(v->stream, v->int_ev(p), 0));
+        MQR_CHECK_HIP(hipStreamWaitEvent(v->stream, v->int_done[p], 0));
         v->int_pending[p] = false;  // ordered behind it on `stream` from here on
     }
     return 0;
@@ -436,7 +440,7 @@ static int touch_launch(mqr_vbg* v, int p, const float* dbase, int64_t HW, int H
                         int64_t max_probe) {
     const int n = (H / 4) * (W / 4);
     hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (v->profile) {
+    if (v->profile_touch) {
         e0 = v->pooled_event();
         e1 = v->pooled_event();
         MQR_REQUIRE(e0 && e1, "profiling: event creation failed");
@@ -447,7 +451,7 @@ static int touch_launch(mqr_vbg* v, int p, const float* dbase, int64_t HW, int H
                            dframe_dev(v, p), depth_scale, depth_max, sdf_trunc, block_size, t, max_probe, alloc, v->ctr(p),
                            v->pool_ctr(), v->pool_cap, v->bkeys, v->lists[p], v->list_cap);
     MQR_CHECK_HIP(hipGetLastError());
-    if (v->profile) {
+    if (v->profile_touch) {
         MQR_CHECK_HIP(hipEventRecord(e1, v->stream));
         v->touch_events.emplace_back(e0, e1);
         v->stats.touch_launches += 1;
@@ -969,9 +973,11 @@ int mqr_check_division(int device, int which, float b, uint32_t lo_bits, uint64_
 
 int mqr_vbg_profile(mqr_vbg* v, int enable) {
     MQR_REQUIRE(v, "null volume");
+    // enable: 1 = integrate launches (2 events per batch), 2 = also the touch launches (4)
     v->profile = enable != 0;
-    // create the timing events now, outside any timed region (4 per batch; more are created on
-    // demand until the next stats read recycles them)
+    v->profile_touch = enable >= 2;
+    // create the timing events now, outside any timed region (more are created on demand until the
+    // next stats read recycles them)
     MQR_CHECK_HIP(hipSetDevice(v->device));
     if (v->profile && v->ev_pool_sys != v->sys_fence) {  // the fence scope changed: rebuild the pool
         if (sync_all(v)) return 1;

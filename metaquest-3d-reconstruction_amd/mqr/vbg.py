@@ -254,8 +254,9 @@ class VoxelBlockGrid:
         return vbg
 
     # -- profiling ---------------------------------------------------------------------------------
-    def profile(self, enable=True):
-        call("mqr_vbg_profile", self._h, 1 if enable else 0)
+    def profile(self, enable=True, touch=False):
+        """Per-launch timing events (stats()['integrate_ms']); touch=True also times the touch launches."""
+        call("mqr_vbg_profile", self._h, (2 if touch else 1) if enable else 0)
 
     def stats(self, reset=False) -> dict:
         s = MqrStats()

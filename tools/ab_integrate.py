@@ -47,7 +47,7 @@ def main():
             _lib.call("mqr_vbg_set_variant", vbg.handle, v)
             vbg.reset()
             vbg.stats(reset=True)
-            vbg.profile(not a.no_profile)
+            vbg.profile(not a.no_profile, touch=True)
             t0 = time.perf_counter()
             vbg.integrate_frames((_DevPtr(d.data_ptr()), B, H, W), K, T, depth_scale=1.0, depth_max=4.0,
                                  trunc_voxel_multiplier=10.0)

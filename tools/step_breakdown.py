@@ -27,7 +27,7 @@ def main():
         vbg.reset()
         t1 = time.perf_counter()
         prof = r % 2 == 1
-        vbg.profile(prof)
+        vbg.profile(prof, touch=True)
         vbg.integrate_frames((_DevPtr(d.data_ptr()), B, H, W), K, T, depth_scale=1.0, depth_max=4.0,
                              trunc_voxel_multiplier=10.0)
         t2 = time.perf_counter()
