@@ -447,9 +447,16 @@ static int touch_launch(mqr_vbg* v, int p, const float* dbase, int64_t HW, int H
         MQR_CHECK_HIP(hipEventRecord(e0, v->stream));
     }
     if (n > 0)
-        hipLaunchKernelGGL(k_touch, dim3((n + 255) / 256, b), dim3(256), 0, v->stream, dbase, HW, H, W, v->d_fp[p],
-                           dframe_dev(v, p), depth_scale, depth_max, sdf_trunc, block_size, t, max_probe, alloc, v->ctr(p),
-                           v->pool_ctr(), v->pool_cap, v->bkeys, v->lists[p], v->list_cap);
+    {
+        if (v->touch_ppt == 1)
+            hipLaunchKernelGGL(k_touch<1>, dim3((n + 255) / 256, b), dim3(256), 0, v->stream, dbase, HW, H, W,
+                               v->d_fp[p], dframe_dev(v, p), depth_scale, depth_max, sdf_trunc, block_size, t, max_probe,
+                               alloc, v->ctr(p), v->pool_ctr(), v->pool_cap, v->bkeys, v->lists[p], v->list_cap);
+        else
+            hipLaunchKernelGGL(k_touch<2>, dim3((n + 511) / 512, b), dim3(256), 0, v->stream, dbase, HW, H, W,
+                               v->d_fp[p], dframe_dev(v, p), depth_scale, depth_max, sdf_trunc, block_size, t, max_probe,
+                               alloc, v->ctr(p), v->pool_ctr(), v->pool_cap, v->bkeys, v->lists[p], v->list_cap);
+    }
     MQR_CHECK_HIP(hipGetLastError());
     if (v->profile_touch) {
         MQR_CHECK_HIP(hipEventRecord(e1, v->stream));
@@ -940,6 +947,7 @@ int mqr_vbg_set_variant(mqr_vbg* v, int variant) {
     v->table_worst = (variant & 0x2000) != 0; // bit 13: size the table for the worst case (round-2 A/B)
     v->touch_wait = (variant & 0x4000) != 0;  // bit 14: integrate always waits on a touch-stream event (A/B)
     v->xcd_order = (variant & 0x8000) != 0;   // bit 15: spatial per-XCD groups (k_xcd_order, A/B)
+    v->touch_ppt = (variant & 0x10000) ? 1 : 2;  // bit 16: one stride-4 pixel per touch thread (A/B)
     return 0;
 }
 

@@ -166,20 +166,25 @@ __device__ inline void wave_add(int* ctr, int v) {
 }
 
 // ------------------------------------------------------------------ kernels
-// compute_unique_block_coordinates for a batch: blockIdx.y = batch frame (bit), one thread per
-// stride-4 pixel, 4 samples over [max(d - trunc, 0), min(d + trunc, depth_max)] (Appendix A.2).
+// compute_unique_block_coordinates for a batch: blockIdx.y = batch frame (bit), PPT stride-4 pixels
+// per thread (a workgroup covers 256 PPT consecutive ones), 4 samples each over
+// [max(d - trunc, 0), min(d + trunc, depth_max)] (Appendix A.2).
+template <int PPT>
 __global__ __launch_bounds__(256) void k_touch(const float* __restrict__ depths, int64_t HW, int H, int W,
                                                const FrameParams* __restrict__ fps,
                                                const int64_t* __restrict__ depth_frame, float depth_scale,
                                                float depth_max, float sdf_trunc, float block_size, Table t,
                                                int64_t max_probe, int alloc, int* counters, int* pool_ctr,
                                                int64_t pool_cap, uint64_t* bkeys, int32_t* list, int64_t list_cap) {
-    // keys already inserted by this workgroup (a 256-pixel strip of one frame shares most of its
-    // blocks): only a key's first occurrence probes the global table and sets the frame bit.  The
-    // first occurrences are collected in LDS and then claimed all at once, one per thread: each claim
-    // is a chain of device-coherent round trips (probe, mask read, atomicOr, list append; ~2 200 cycles
-    // per L2 read in this kernel), and claiming per sample left four such chains in sequence.
-    constexpr int kSeen = 1024;  // >= the 4 x 256 keys a workgroup can produce
+    // keys already inserted by this workgroup (a strip of one frame shares most of its blocks): only
+    // a key's first occurrence probes the global table and sets the frame bit.  The first
+    // occurrences are collected in LDS and then claimed all at once, one per thread: each claim is a
+    // chain of device-coherent round trips (probe, mask read, atomicOr, list append; ~2 200 cycles
+    // per L2 read in this kernel), and claiming per sample left four such chains in sequence.  With
+    // PPT > 1 a workgroup covers a longer strip: the touch is latency-bound and holds its wave slots
+    // (taken from the overlapped integrate) for about one claim round, so fewer, longer-lived
+    // workgroups with better deduplication hold fewer slot-microseconds.
+    constexpr int kSeen = 1024 * PPT;  // >= the 4 x 256 x PPT keys a workgroup can produce
     __shared__ unsigned long long seen[kSeen];
     __shared__ unsigned long long uniq[kSeen];
     __shared__ int wg_count[3];  // valid samples, new frame bits (one global atomic each), first keys
@@ -189,54 +194,66 @@ __global__ __launch_bounds__(256) void k_touch(const float* __restrict__ depths,
     const int f = blockIdx.y;
     const FrameParams& fp = fps[f];
     const int cols = W / 4, rows = H / 4, n = rows * cols;
-    const int w = blockIdx.x * blockDim.x + threadIdx.x;
-    uint64_t key[4] = {kEmpty, kEmpty, kEmpty, kEmpty};
-    int valid = 0, fresh = 0;
-    if (w < n) {
-        const int y = (w / cols) * 4, x = (w % cols) * 4;
-        const float d = depths[depth_frame[f] * HW + (int64_t)y * W + x] / depth_scale;
-        if (d > 0 && d < depth_max) {
-            const float xc = ((float)x - fp.cx) * 1.0f / fp.fx;
-            const float yc = ((float)y - fp.cy) * 1.0f / fp.fy;
-            const float zc = 1.0f;
-            const float xg = xc * fp.pose[0] + yc * fp.pose[1] + zc * fp.pose[2] + fp.pose[3];
-            const float yg = xc * fp.pose[4] + yc * fp.pose[5] + zc * fp.pose[6] + fp.pose[7];
-            const float zg = xc * fp.pose[8] + yc * fp.pose[9] + zc * fp.pose[10] + fp.pose[11];
-            const float xo = fp.pose[3], yo = fp.pose[7], zo = fp.pose[11];
-            const float xd = xg - xo, yd = yg - yo, zd = zg - zo;
-            const float t_min = fmaxf(d - sdf_trunc, 0.0f);
-            const float t_max = fminf(d + sdf_trunc, depth_max);
-            const float t_step = (t_max - t_min) / 3;
-            float tt = t_min;
+    const float* __restrict__ dep = depths + depth_frame[f] * HW;
+    int wpx[PPT];
+    float dd[PPT];
 #pragma unroll
-            for (int s = 0; s < 4; ++s) {
-                const int xb = (int)floorf((xo + tt * xd) / block_size);
-                const int yb = (int)floorf((yo + tt * yd) / block_size);
-                const int zb = (int)floorf((zo + tt * zd) / block_size);
-                if (key_in_range(xb, yb, zb))
-                    key[s] = pack_key(xb, yb, zb);
-                else
-                    atomicOr(&counters[kOverflow], 8);
-                tt += t_step;
+    for (int jp = 0; jp < PPT; ++jp) {  // all of the thread's depth reads in flight together
+        const int w = (blockIdx.x * PPT + jp) * blockDim.x + threadIdx.x;
+        wpx[jp] = w;
+        dd[jp] = w < n ? dep[(int64_t)((w / cols) * 4) * W + (w % cols) * 4] : 0.f;
+    }
+    int valid = 0, fresh = 0;
+#pragma unroll
+    for (int jp = 0; jp < PPT; ++jp) {
+        const int w = wpx[jp];
+        uint64_t key[4] = {kEmpty, kEmpty, kEmpty, kEmpty};
+        if (w < n) {
+            const int y = (w / cols) * 4, x = (w % cols) * 4;
+            const float d = dd[jp] / depth_scale;
+            if (d > 0 && d < depth_max) {
+                const float xc = ((float)x - fp.cx) * 1.0f / fp.fx;
+                const float yc = ((float)y - fp.cy) * 1.0f / fp.fy;
+                const float zc = 1.0f;
+                const float xg = xc * fp.pose[0] + yc * fp.pose[1] + zc * fp.pose[2] + fp.pose[3];
+                const float yg = xc * fp.pose[4] + yc * fp.pose[5] + zc * fp.pose[6] + fp.pose[7];
+                const float zg = xc * fp.pose[8] + yc * fp.pose[9] + zc * fp.pose[10] + fp.pose[11];
+                const float xo = fp.pose[3], yo = fp.pose[7], zo = fp.pose[11];
+                const float xd = xg - xo, yd = yg - yo, zd = zg - zo;
+                const float t_min = fmaxf(d - sdf_trunc, 0.0f);
+                const float t_max = fminf(d + sdf_trunc, depth_max);
+                const float t_step = (t_max - t_min) / 3;
+                float tt = t_min;
+#pragma unroll
+                for (int s = 0; s < 4; ++s) {
+                    const int xb = (int)floorf((xo + tt * xd) / block_size);
+                    const int yb = (int)floorf((yo + tt * yd) / block_size);
+                    const int zb = (int)floorf((zo + tt * zd) / block_size);
+                    if (key_in_range(xb, yb, zb))
+                        key[s] = pack_key(xb, yb, zb);
+                    else
+                        atomicOr(&counters[kOverflow], 8);
+                    tt += t_step;
+                }
+                valid += 4;
             }
-            valid = 4;
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const uint64_t k = key[s];
+            if (k == kEmpty || (s > 0 && key[s - 1] == k)) continue;
+            uint32_t h = (uint32_t)mix64(k) & (kSeen - 1);
+            bool first = true;  // (a probe that found no room would also claim: a repeated claim is harmless)
+            for (int p = 0; p < kSeen; ++p) {
+                const unsigned long long old = atomicCAS(&seen[h], (unsigned long long)kEmpty, (unsigned long long)k);
+                if (old == k) first = false;
+                if (old == kEmpty || old == k) break;
+                h = (h + 1) & (kSeen - 1);
+            }
+            if (first) uniq[atomicAdd(&wg_count[2], 1)] = k;
         }
     }
     wave_add(&wg_count[0], valid);
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-        const uint64_t k = key[s];
-        if (k == kEmpty || (s > 0 && key[s - 1] == k)) continue;
-        uint32_t h = (uint32_t)mix64(k) & (kSeen - 1);
-        bool first = true;  // (a probe that found no room would also claim: a repeated claim is harmless)
-        for (int p = 0; p < kSeen; ++p) {
-            const unsigned long long old = atomicCAS(&seen[h], (unsigned long long)kEmpty, (unsigned long long)k);
-            if (old == k) first = false;
-            if (old == kEmpty || old == k) break;
-            h = (h + 1) & (kSeen - 1);
-        }
-        if (first) uniq[atomicAdd(&wg_count[2], 1)] = k;
-    }
     __syncthreads();
     const int nu = wg_count[2];
     for (int base = 0; base < nu; base += blockDim.x) {  // uniform trip count: the wave_* calls need whole waves
