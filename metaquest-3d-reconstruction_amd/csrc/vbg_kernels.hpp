@@ -184,9 +184,9 @@ __global__ __launch_bounds__(256) void k_touch(const float* __restrict__ depths,
     // PPT > 1 a workgroup covers a longer strip: the touch is latency-bound and holds its wave slots
     // (taken from the overlapped integrate) for about one claim round, so fewer, longer-lived
     // workgroups with better deduplication hold fewer slot-microseconds.
-    constexpr int kSeen = 1024 * PPT;  // >= the 4 x 256 x PPT keys a workgroup can produce
+    constexpr int kSeen = 1024 * PPT;  // >= the 4 x 256 x PPT keys a workgroup can produce: never full
     __shared__ unsigned long long seen[kSeen];
-    __shared__ unsigned long long uniq[kSeen];
+    __shared__ uint16_t uniq[kSeen];  // seen-slots of the first occurrences (LDS: workgroups per CU)
     __shared__ int wg_count[3];  // valid samples, new frame bits (one global atomic each), first keys
     for (int i = threadIdx.x; i < kSeen; i += blockDim.x) seen[i] = kEmpty;
     if (threadIdx.x < 3) wg_count[threadIdx.x] = 0;
@@ -243,14 +243,14 @@ __global__ __launch_bounds__(256) void k_touch(const float* __restrict__ depths,
             const uint64_t k = key[s];
             if (k == kEmpty || (s > 0 && key[s - 1] == k)) continue;
             uint32_t h = (uint32_t)mix64(k) & (kSeen - 1);
-            bool first = true;  // (a probe that found no room would also claim: a repeated claim is harmless)
-            for (int p = 0; p < kSeen; ++p) {
+            bool first = false;
+            for (;;) {  // terminates: the set has room for every key of the workgroup
                 const unsigned long long old = atomicCAS(&seen[h], (unsigned long long)kEmpty, (unsigned long long)k);
-                if (old == k) first = false;
+                first = old == kEmpty;
                 if (old == kEmpty || old == k) break;
                 h = (h + 1) & (kSeen - 1);
             }
-            if (first) uniq[atomicAdd(&wg_count[2], 1)] = k;
+            if (first) uniq[atomicAdd(&wg_count[2], 1)] = (uint16_t)h;
         }
     }
     wave_add(&wg_count[0], valid);
@@ -258,7 +258,7 @@ __global__ __launch_bounds__(256) void k_touch(const float* __restrict__ depths,
     const int nu = wg_count[2];
     for (int base = 0; base < nu; base += blockDim.x) {  // uniform trip count: the wave_* calls need whole waves
         const int idx = base + (int)threadIdx.x;
-        const uint64_t k = idx < nu ? uniq[idx] : kEmpty;
+        const uint64_t k = idx < nu ? seen[uniq[idx]] : kEmpty;
         int64_t slot = -1;
         bool won = false, app = false;
         if (k != kEmpty) slot = table_claim(t, k, counters, won, max_probe);
