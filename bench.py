@@ -701,7 +701,7 @@ def main():
                    "note": "per-rank owned-cube extraction of the merged shard (host copy of the shard mesh "
                            "included); triangles add up to the single-volume mesh"}
         blocks = sharded["union_blocks"]
-        nt = sharded["triangles"]
+        nv, nt = sharded["vertices_with_boundary_copies"], sharded["triangles"]
     elif rank == 0:
         ext_ms, (nv, nt) = extract_ms(vbg, args.extract_threshold, args.extract_reps)
 
