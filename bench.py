@@ -10,7 +10,9 @@ and the step ends with the single RCCL merge of the partial volumes into rank 0.
 Prints ONE JSON line (rank 0): value = frames integrated per second over all ranks, the mesh
 extraction time (weight_threshold 1.5, the pipeline's setting), the integrate kernel's roofline
 (algorithmic bytes per launch / its average HIP-event duration), the CPU-oracle baseline and the
-parity of the last timed step's volume and mesh against the oracle's.
+parity of the last timed step's volume, mesh and point cloud against the oracle's (checked before
+any other leg touches the volume).  The C4 (2000 frames L+R chained) and C5 (4000 frames @ 3 mm +
+colour) legs carry parity blocks of their own, on the volumes they timed.
 """
 from __future__ import annotations
 
@@ -66,6 +68,7 @@ def parse():
                          "split over the ranks (strong scaling) instead of 500 frames per rank")
     ap.add_argument("--strong-frames", type=int, default=1000, help="frames per side in --strong mode")
     ap.add_argument("--no-c5", action="store_true", help="skip the 1-GPU C5 leg (4000 frames @ 3 mm + colour)")
+    ap.add_argument("--no-c4", action="store_true", help="skip the 1-GPU C4 leg (1000 + 1000 frames chained)")
     return ap.parse_args()
 
 
@@ -274,7 +277,7 @@ def dropin_e2e_leg(seq, frames, device):
                     "o3d_utils.integrate with confidence masking; host file I/O + PCIe included"}
 
 
-def c5_leg(args, device, frames_per_side=2000, voxel=0.003, key_every=40):
+def c5_leg(args, device, frames_per_side=2000, voxel=0.003, key_every=40, parity=True):
     """C5 on one GPU (BASELINE.json configs[4] minus the 8-GPU split): a 2000 + 2000
     frame LEFT+RIGHT walk through an 8 x 8 x 3 m hall, 3 mm voxels (R = 16), integrated in
     reconstruct_scene.py's order (all LEFT, then all RIGHT) into one volume grown from a small
@@ -315,6 +318,7 @@ def c5_leg(args, device, frames_per_side=2000, voxel=0.003, key_every=40):
     t_int = min(times)
     blocks = vbg.size()
     pool_gb = vbg.capacity() * 16 ** 3 * 8 / 1e9
+    host = depth.cpu().numpy() if parity else None
     del depth, seq
     torch.cuda.empty_cache()
     ext = []
@@ -348,7 +352,87 @@ def c5_leg(args, device, frames_per_side=2000, voxel=0.003, key_every=40):
            "note": "integrate: device-resident depth, best of 2 passes from an emptied volume (capacity grows "
                    "from 16384 blocks); extract: host copy included, median of 3; colour: host arrays in/out "
                    "(PCIe included), error vs the analytic texture the colour frames were rendered with"}
+    if parity:
+        # the volume of the last timed pass, its mesh (the one coloured above) and point cloud, and the
+        # per-vertex colours, against the oracle on the same 4000 frames (LEFT then RIGHT)
+        del scene
+        log("C5 parity: oracle volume of the same frames")
+        t0 = time.perf_counter()
+        ref = oracle_volume(host, K, T, voxel, args, block_count=16384)
+        out["oracle_s"] = time.perf_counter() - t0
+        del host
+        out["parity"] = parity_check(vbg, ref, 1.5, mesh=mesh, points_thr=3.0)
+        del ref
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+        from mqr.color import MARGIN, MAX_DEPTH, VISIBILITY_THRESHOLD
+        oc, on = oracle.color_vertices(mesh.vertices, imgs, cad, K[key], T[key], MAX_DEPTH, VISIBILITY_THRESHOLD,
+                                       MARGIN)
+        out["parity"]["colour_counts_equal"] = bool(np.array_equal(cnt, on))
+        out["parity"]["colours_equal"] = bool(np.array_equal(col, oc))
+        out["parity"]["all_ok"] = bool(out["parity"]["all_ok"] and out["parity"]["colour_counts_equal"]
+                                       and out["parity"]["colours_equal"])
+        scene = None
     del vbg, mesh, scene
+    torch.cuda.empty_cache()
+    return out
+
+
+def c4_leg(args, device, frames_per_side=1000, reps=3, parity=True):
+    """C4 on one GPU (BASELINE.json configs[3], the N = 1 point): 1000 LEFT + 1000 RIGHT frames of
+    the room walk (0.064 m stereo baseline), 640x480, 5 mm, integrated as reconstruct_scene.py:64-81
+    does -- one integrate call per side into ONE volume (vbg_opt threaded through).  Inputs
+    resident in HBM; best of `reps` passes from an emptied volume; the last pass's volume, its mesh
+    at 1.5 and its point cloud at 3.0 are checked against the oracle's volume of the same frames."""
+    import numpy as np
+    import torch
+    from mqr import synthetic
+    from mqr.vbg import VoxelBlockGrid
+    dev = int(device.index or 0)
+    left = synthetic.room_loop_poses(frames_per_side)
+    right = [(R_, t_ + R_[:, 0] * 0.064) for R_, t_ in left]
+    seq = synthetic.make_sequence_fast("room", poses=left + right, height=args.height, width=args.width, seed=4,
+                                       device=f"cuda:{dev}")
+    depth = seq["depth_t"].contiguous()
+    B, H, W = depth.shape
+    K = seq["K"].astype(np.float64)
+    T = seq["T_wc"].astype(np.float64)
+    n = frames_per_side
+
+    class _L:
+        ptr = ctypes.c_void_p(depth.data_ptr())
+
+    class _R:
+        ptr = ctypes.c_void_p(depth[n:].data_ptr())
+
+    vbg = VoxelBlockGrid(voxel_size=args.voxel, block_resolution=args.block_resolution, block_count=args.block_count,
+                         device=dev)
+    times = []
+    for _ in range(reps + 1):
+        vbg.reset()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        vbg.integrate_frames((_L, n, H, W), K[:n], T[:n], depth_scale=1.0, depth_max=args.depth_max,
+                             trunc_voxel_multiplier=args.trunc)
+        vbg.integrate_frames((_R, B - n, H, W), K[n:], T[n:], depth_scale=1.0, depth_max=args.depth_max,
+                             trunc_voxel_multiplier=args.trunc)
+        torch.cuda.synchronize()
+        times.append(time.perf_counter() - t0)
+    t = min(times[1:])
+    mesh = vbg.extract_triangle_mesh(weight_threshold=args.extract_threshold)
+    out = {"frames": B, "sides": [n, B - n], "ms": t * 1e3, "frames_per_s": B / t, "blocks": vbg.size(),
+           "triangles": int(len(mesh.triangles)),
+           "note": "2 integrate_frames calls (LEFT, RIGHT) into one volume, device-resident depth, best of "
+                   f"{reps} passes after a warm-up pass"}
+    if parity:
+        host = depth.cpu().numpy()
+        del depth, seq
+        t0 = time.perf_counter()
+        ref = oracle_volume(host, K, T, args.voxel, args)
+        out["oracle_s"] = time.perf_counter() - t0
+        out["parity"] = parity_check(vbg, ref, args.extract_threshold, mesh=mesh, points_thr=3.0)
+        del ref
+    del vbg, mesh
     torch.cuda.empty_cache()
     return out
 
@@ -515,34 +599,71 @@ def cpu_baseline(seq_host, K, T, args):
     return out, last
 
 
-def parity_check(vbg, ref, thr):
-    """The last timed step's GPU volume and mesh vs the oracle's volume of the same 500 frames."""
+def parity_check(vbg, ref, thr, mesh=None, points_thr=None):
+    """A GPU volume (and its mesh at `thr`, and optionally its point cloud at `points_thr`) vs the
+    oracle's volume of the same frames: identical block keys and weights, |dtsdf| <= 1e-4 on w > 0,
+    identical vertex-position and oriented-triangle multisets (tests/gpu_helpers.py)."""
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "tests"))
-    from gpu_helpers import canon_blocks, canon_triangles, canon_vertices
-    gk, gt, gw = canon_blocks(*vbg.export())
-    ok_, ot, ow = canon_blocks(*ref.export())
-    keys_equal = gk.shape == ok_.shape and bool(np.array_equal(gk, ok_))
-    out = {"blocks": int(len(gk)), "keys_equal": keys_equal}
+    from gpu_helpers import _key_order, mesh_signature, position_hashes
+    gk, gt, gw = vbg.export()
+    ok_, ot, ow = ref.export()
+    out = {"blocks": int(len(gk))}
+    ga, oa = _key_order(gk), _key_order(ok_)
+    keys_equal = gk.shape == ok_.shape and bool(np.array_equal(gk[ga], ok_[oa]))
+    out["keys_equal"] = keys_equal
     if keys_equal:
-        out["weights_equal"] = bool(np.array_equal(gw, ow))
-        m = gw > 0
-        out["max_dtsdf"] = float(np.abs(gt[m] - ot[m]).max()) if m.any() else 0.0
+        weq, err = True, 0.0
+        for c in range(0, len(ga), 4096):
+            i, j = ga[c:c + 4096], oa[c:c + 4096]
+            w1, w2 = gw[i], ow[j]
+            weq = weq and bool(np.array_equal(w1, w2))
+            m = w1 > 0
+            if m.any():
+                err = max(err, float(np.abs(gt[i][m] - ot[j][m]).max()))
+        out["weights_equal"], out["max_dtsdf"] = weq, err
     del gt, gw, ot, ow
-    mesh = vbg.extract_triangle_mesh(weight_threshold=thr)
+    if mesh is None:
+        mesh = vbg.extract_triangle_mesh(weight_threshold=thr)
     ov, _, otri = ref.extract_mesh(thr)
     out["mesh_threshold"] = thr
     out["triangles"] = int(len(mesh.triangles))
     out["triangle_count_equal"] = len(mesh.triangles) == len(otri)
     out["vertex_count_equal"] = len(mesh.vertices) == len(ov)
     if out["triangle_count_equal"] and out["vertex_count_equal"]:
-        out["vertices_equal"] = bool(np.array_equal(canon_vertices(mesh.vertices)[0], canon_vertices(ov)[0]))
-        out["triangles_equal"] = bool(np.array_equal(canon_triangles(mesh.vertices, mesh.triangles),
-                                                     canon_triangles(ov, otri)))
+        gs, os_ = mesh_signature(mesh.vertices, mesh.triangles), mesh_signature(ov, otri)
+        out["vertices_equal"] = bool(np.array_equal(gs[0], os_[0]))
+        out["triangles_equal"] = bool(np.array_equal(gs[1], os_[1]))
+    del ov, otri
+    ok_pts = True
+    if points_thr is not None:
+        pcd = vbg.extract_point_cloud(weight_threshold=points_thr)
+        op, on = ref.extract_points(points_thr)
+        hg, ho = position_hashes(pcd.points), position_hashes(op)
+        out["points"] = {"weight_threshold": points_thr, "count": int(len(op)),
+                         "count_equal": len(op) == len(pcd.points)}
+        if out["points"]["count_equal"]:
+            og, oo = np.argsort(hg, kind="stable"), np.argsort(ho, kind="stable")
+            out["points"]["positions_equal"] = bool(np.array_equal(hg[og], ho[oo]))
+        ok_pts = bool(out["points"].get("positions_equal"))
     out["tolerance"] = 1e-4
+    out["comparison"] = ("keys/weights exact, tsdf within tolerance, mesh and points as exact multisets of 64-bit "
+                         "position hashes (order-independent)")
     out["all_ok"] = bool(out.get("keys_equal") and out.get("weights_equal") and out.get("max_dtsdf", 1) <= 1e-4
-                         and out.get("triangles_equal") and out.get("vertices_equal"))
+                         and out.get("triangles_equal") and out.get("vertices_equal") and ok_pts)
     return out
+
+
+def oracle_volume(depth_host, K, T, args_voxel, args, block_count=4096):
+    """The oracle's volume of the same frames, one by one (touch + integrate per frame)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # the checker only
+    cores, _ = host_cores()
+    oracle.set_threads(cores)
+    ref = oracle.OracleVBG(args_voxel, args.block_resolution, block_count)
+    for i in range(len(depth_host)):
+        ref.integrate_frame(depth_host[i], K[i], T[i], 1.0, args.depth_max, args.trunc)
+    return ref
 
 
 def confidence_cpu(depth_host, K, T_wc, args, budget_s):
@@ -617,6 +738,7 @@ def main():
                          block_count=args.block_count, device=local)
 
     merge_times = []
+    merge_phases = []
     shard = {"out": None, "owned": 0}
     transport = None
     if world > 1:
@@ -649,6 +771,7 @@ def main():
             t = time.perf_counter()
             if comm is not None:
                 shard["out"], shard["owned"] = merge_rccl(vbg, comm, mode=args.merge, out=shard["out"])
+                merge_phases.append(comm.timing())
             else:
                 from mqr.distributed import merge_to_root
                 merge_to_root(vbg, root=0)
@@ -660,6 +783,7 @@ def main():
     for _ in range(args.warmup):
         step()
     merge_times.clear()
+    merge_phases.clear()
     vbg.stats(reset=True)
     vbg.profile(True)
     if dist:
@@ -711,6 +835,18 @@ def main():
     avg_ms = st["integrate_ms"] / launches
     achieved = alg_bytes / launches / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
 
+    cpu = parity = None
+    host_depth = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        # CPU baseline and parity FIRST: the volume checked is the one the last timed step left
+        host_depth = depth_t.cpu().numpy()
+        log("CPU baseline (oracle)")
+        cpu, ref_vol = cpu_baseline(host_depth, K, T, args)
+        if not args.no_parity:
+            log("parity check of the timed volume")
+            parity = parity_check(vbg, ref_vol, args.extract_threshold, points_thr=3.0)
+        del ref_vol
+
     extras = {}
     if rank == 0 and world == 1 and not args.no_extras:
         dev = torch.device("cuda", local)
@@ -721,9 +857,12 @@ def main():
         extras["raycast"] = raycast_leg(vbg, K, T, H, W, args.extract_threshold)
         extras["meshfilter"] = meshfilter_leg(vbg, args.extract_threshold)
         extras["c3"] = c3_leg(seq, vbg, args, dev)
-        log("C5 leg (4000 frames @ 3 mm, extract, colour)")
+        if not args.strong and not args.no_c4:
+            log("C4 leg (1000 + 1000 frames chained, parity)")
+            extras["c4"] = c4_leg(args, dev, parity=not (args.no_cpu or args.no_parity))
         if not args.no_c5:
-            extras["c5"] = c5_leg(args, dev)
+            log("C5 leg (4000 frames @ 3 mm, extract, colour, parity)")
+            extras["c5"] = c5_leg(args, dev, parity=not (args.no_cpu or args.no_parity))
         log("C3 / C5 legs done; drop-in leg (on-disk capture)")
         if args.e2e_frames > 0:
             extras["dropin_e2e"] = dropin_e2e_leg(seq, min(args.e2e_frames, B), dev)
@@ -740,19 +879,7 @@ def main():
     if ext_ms:
         ext_alg = (8 * R3_ * blocks + 4 * 27 * blocks + 24 * nv + 12 * nt) / (ext_ms * 1e-3) / 1e9
 
-    cpu = parity = None
-    if rank == 0 and world == 1 and not args.no_cpu:
-        host_depth = depth_t.cpu().numpy()
-        log("CPU baseline (oracle)")
-        cpu, ref_vol = cpu_baseline(host_depth, K, T, args)
-        log("parity check of the timed volume")
-        if not args.no_parity:
-            # the volume of the last timed step is still in vbg unless an extra leg reset it: rebuild
-            # it exactly as a step does (reset + integrate_frames) when the legs ran
-            if extras:
-                step_integrate()
-            parity = parity_check(vbg, ref_vol, args.extract_threshold)
-        del ref_vol
+    if host_depth is not None:
         if extras.get("confidence") is not None and args.conf_cpu_seconds > 0:
             extras["confidence"]["cpu_baseline"] = confidence_cpu(host_depth, K, T, args, args.conf_cpu_seconds)
 
@@ -787,6 +914,8 @@ def main():
                             else " + gloo merge to rank 0 (fallback)") if world > 1 else "")},
             "sharded_extract": sharded,
             "merge_ms": (sum(merge_times) / len(merge_times) * 1e3) if merge_times else None,
+            "merge_phases_ms": ({k: sum(p[k] for p in merge_phases) / len(merge_phases) for k in merge_phases[0]}
+                                if merge_phases else None),
             "merge_transport": transport,
             "union_blocks": blocks if world > 1 else None,
             "extract_ms": ext_ms,
@@ -812,6 +941,7 @@ def main():
             "cpu_baseline": cpu,
             "parity": parity,
             "c3": extras.get("c3"),
+            "c4": extras.get("c4"),
             "c5": extras.get("c5"),
             "dropin_e2e": extras.get("dropin_e2e"),
         }

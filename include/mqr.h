@@ -97,9 +97,13 @@ int mqr_vbg_unpack_weighted(mqr_vbg* v, const int32_t* union_keys, int64_t U, co
  *                      mqr_extract_mesh_owned(out, thr, *n_owned): shard meshes concatenate to the
  *                      single-volume mesh (triangle counts add exactly).
  * Voxels seen by one rank keep its (tsdf, weight) bit for bit; others merge in rank order:
- * tsdf = (w_a tsdf_a + w_b tsdf_b) / (w_a + w_b), weight = w_a + w_b.
- * mqr_merge_local: the same plan and arithmetic for n volumes of one process (device copies
- * instead of RCCL; tests and single-node fallbacks). */
+ * tsdf = (w_a tsdf_a + w_b tsdf_b) / (w_a + w_b), weight = w_a + w_b.  `out` must not be `local`.
+ * The plan (sorted block union, owner slices, halo sets, send / receive lists) is computed on the
+ * device; the host reads only block counts and list lengths.
+ * mqr_comm_timing: the last merge's phases in ms -- [0] count + key all-gathers and the plan,
+ * [1] output volume + gather of the outgoing blocks, [2] the RCCL exchange, [3] the merge kernels.
+ * mqr_merge_local: the same plan and arithmetic for n volumes of one process on one device (the
+ * merge reads each source's pool directly instead of receiving over RCCL; tests and timing). */
 #define MQR_MERGE_ROOT 0
 #define MQR_MERGE_SHARDED 1
 int mqr_comm_unique_id(uint8_t* id_out /* 128 bytes */);
@@ -107,6 +111,7 @@ int mqr_comm_init(int device, int rank, int world, const uint8_t* id /* 128 byte
 int mqr_comm_destroy(mqr_comm* comm);
 int mqr_reduce_rccl(mqr_vbg* local, mqr_comm* comm, int mode, int root, mqr_vbg* out, int64_t* n_owned);
 int mqr_merge_local(mqr_vbg** locals, int n, int mode, int root, mqr_vbg** outs, int64_t* n_owned);
+int mqr_comm_timing(mqr_comm* comm, float* ms4);
 
 /* vbg.extract_point_cloud(weight_threshold=3.0)   -- reconstruct_scene.py:90, refine_fragment_poses.py:39
  * vbg.extract_triangle_mesh(weight_threshold)       -- reconstruct_scene.py:105-108, 186-189 */

@@ -11,7 +11,8 @@
 //   visible in keyframe c iff d >= 0, (ui, vi) inside the image, depth_c(ui, vi) <= max_depth and
 //   |d - depth_c(ui, vi)| < visibility_threshold (float difference, compared in float64);
 //   sampled iff also margin <= u < W - margin and margin <= v < H - margin: the colour is the
-//   average over the sampled keyframes of image_c(ui, vi) / 255 (float64 sums in keyframe order).
+//   average over the sampled keyframes of (float)image_c(ui, vi) / 255.0f, summed in float64 in
+//   keyframe order.
 // Not restated: the depth-discontinuity mask and the k-nearest-neighbour fill of vertices no
 // keyframe sees (their colour stays 0, count 0), and the pose optimisation itself (OUT of scope).
 //
@@ -58,9 +59,10 @@ __global__ __launch_bounds__(256) void k_color_vertices(const float* __restrict_
         if (!((double)fabsf(d - ds) < vis_thr)) continue;
         if (!(u >= margin && u < W - margin && v >= margin && v < H - margin)) continue;
         const uint8_t* p = images + 3 * px;
-        sr += p[0] / 255.0;
-        sg += p[1] / 255.0;
-        sb += p[2] / 255.0;
+        // upstream: float r = (float)r_temp / 255.0f, summed into a double vector
+        sr += (double)((float)p[0] / 255.0f);
+        sg += (double)((float)p[1] / 255.0f);
+        sb += (double)((float)p[2] / 255.0f);
         ++cnt;
     }
     out[3 * i] = cnt ? (float)(sr / cnt) : 0.f;

@@ -7,18 +7,26 @@
 // applied source by source in rank order (deterministic); a voxel that only one rank saw keeps
 // that rank's (tsdf, weight) bit for bit.
 //
-// Plan (identical on every rank, computed on the host from the all-gathered block keys):
-//   union U = sorted distinct keys (packed order = lexicographic x, y, z); owner slices =
-//   [U r / N, U (r+1) / N); each union block goes to a destination set:
+// Plan (identical on every rank, computed ON THE DEVICE from the all-gathered block keys):
+//   union U = sorted distinct keys (packed order = lexicographic x, y, z; a radix sort of the W
+//   ranks' padded key arrays); owner slices = [U r / W, U (r+1) / W); each union block goes to a
+//   destination set:
 //     MQR_MERGE_ROOT     the root only (the root's output holds the whole volume)
-//     MQR_MERGE_SHARDED  its owner and the owners of its 26 neighbours -- so every rank holds its
-//                        owned blocks plus a one-block halo, and extracts exactly the cubes whose
-//                        origin lies in an owned block (mqr_extract_mesh_owned): triangle counts of
-//                        the shards add up to the single-volume count.
+//     MQR_MERGE_SHARDED  its owner and the owners of its 26 neighbours (binary search in the
+//                        sorted union) -- so every rank holds its owned blocks plus a one-block
+//                        halo, and extracts exactly the cubes whose origin lies in an owned block
+//                        (mqr_extract_mesh_owned): triangle counts of the shards add up to the
+//                        single-volume count.
 //   Every rank sends each of its blocks once per destination (grouped ncclSend / ncclRecv: a
-//   sparse all-to-all, per-link traffic ~ own blocks + halo instead of the dense union).
+//   sparse all-to-all, per-link traffic ~ own blocks + halo instead of the dense union).  The
+//   send and receive lists of one rank are the segments of one sorted record array (kind, peer,
+//   entry), so a sender's segment for d and d's segment from that sender list the same blocks in
+//   the same (union) order.  The host reads two small count arrays per merge (block counts after
+//   the first all-gather, list lengths after the plan); nothing else leaves the device.
 #include <dlfcn.h>
 #include <rccl/rccl.h>
+
+#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <climits>
@@ -89,6 +97,20 @@ RcclApi* rccl() {
         }                                                                                          \
     } while (0)
 
+namespace mqr {
+// Grow-only device scratch of the merge plan (hipFree synchronises the device: no allocation per
+// merge once the block counts stop growing) and the pinned summary the host reads.
+struct PlanScratch {
+    void* buf = nullptr;
+    size_t cap = 0;
+    void* h_sum = nullptr;  // pinned PlanSummary
+    ~PlanScratch() {
+        if (buf) (void)hipFree(buf);
+        if (h_sum) (void)hipHostFree(h_sum);
+    }
+};
+}  // namespace mqr
+
 struct mqr_comm {
     int device = 0, rank = 0, world = 1;
     ncclComm_t nc = nullptr;
@@ -100,8 +122,10 @@ struct mqr_comm {
     size_t recv_cap = 0;
     void* small = nullptr;  // counts, padded keys
     size_t small_cap = 0;
-    void* lists = nullptr;  // send / receive index lists, output keys (no allocation per merge:
-    size_t lists_cap = 0;   // hipFree synchronises the device)
+    mqr::PlanScratch plan;
+    // phase timing of the last merge (mqr_comm_timing): start, plan done, gathered, exchanged, merged
+    hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    float last_ms[4] = {0.f, 0.f, 0.f, 0.f};
 };
 
 namespace mqr {
@@ -138,165 +162,303 @@ __global__ void k_merge_blocks(const int32_t* __restrict__ dst, int64_t n, const
     }
 }
 
-// ------------------------------------------------------------------ host plan
-struct MergePlan {
-    int world = 1;
-    std::vector<uint64_t> uni;     // sorted union
-    std::vector<int64_t> bounds;   // owner slices of the union (indices), world + 1
-    std::vector<uint64_t> lokey;   // first key of each slice (world entries)
-    std::vector<uint64_t> dmask;   // destination ranks of each union block
-    int owner(int64_t u) const {
-        return (int)(std::upper_bound(bounds.begin(), bounds.end(), u) - bounds.begin()) - 1;
-    }
-    int owner_of_key(uint64_t k) const {  // the slice whose key range holds k (k in the union)
-        return std::max(0, (int)(std::upper_bound(lokey.begin(), lokey.end(), k) - lokey.begin()) - 1);
-    }
-    int64_t index(uint64_t k) const {  // union index of k, -1 if absent
-        const auto it = std::lower_bound(uni.begin(), uni.end(), k);
-        return it != uni.end() && *it == k ? (int64_t)(it - uni.begin()) : -1;
-    }
-};
-
-static int build_plan(const std::vector<std::vector<uint64_t>>& keys, int mode, int root, MergePlan& P) {
-    const int W = (int)keys.size();
-    P.world = W;
-    size_t tot = 0;
-    for (auto& k : keys) tot += k.size();
-    P.uni.clear();
-    P.uni.reserve(tot);
-    for (auto& k : keys) P.uni.insert(P.uni.end(), k.begin(), k.end());
-    std::sort(P.uni.begin(), P.uni.end());
-    P.uni.erase(std::unique(P.uni.begin(), P.uni.end()), P.uni.end());
-    const int64_t U = (int64_t)P.uni.size();
-    P.bounds.resize(W + 1);
-    for (int r = 0; r <= W; ++r) P.bounds[r] = U * r / W;
-    P.lokey.resize(W);
-    for (int r = 0; r < W; ++r) P.lokey[r] = P.bounds[r] < U ? P.uni[P.bounds[r]] : kEmpty;
-    P.dmask.assign(U, 0);
-    for (int64_t u = 0; u < U; ++u) {
-        if (mode == MQR_MERGE_ROOT) {
-            P.dmask[u] = 1ull << root;
-            continue;
+// Merge received entries straight from a source volume's pool (the one-process twin): entry j takes
+// source buffer src[j] into destination buffer dst[j], same arithmetic as k_merge_blocks.
+__global__ void k_merge_direct(const int32_t* __restrict__ src, const int32_t* __restrict__ dst, int64_t n,
+                               const float2* __restrict__ spool, int R3, float2* __restrict__ pool) {
+    const int64_t j = blockIdx.x;
+    if (j >= n) return;
+    const float2* in = spool + (int64_t)src[j] * R3;
+    float2* out = pool + (int64_t)dst[j] * R3;
+    for (int p = threadIdx.x; p < R3; p += blockDim.x) {
+        const float2 a = out[p], b = in[p];
+        if (b.y == 0.f) continue;
+        if (a.y == 0.f) {
+            out[p] = b;
+        } else {
+            const float w = a.y + b.y;
+            out[p] = make_float2((a.y * a.x + b.y * b.x) / w, w);
         }
-        const int own = P.owner(u);
-        uint64_t m = 1ull << own;
-        int x, y, z;
-        unpack_key(P.uni[u], x, y, z);
-        // keys pack x-major, so every neighbour key lies in [pack(x-1,y-1,z-1), pack(x+1,y+1,z+1)]:
-        // a block whose neighbourhood range sits inside its own slice's key range needs no lookup
-        const bool inside = key_in_range(x - 1, y - 1, z - 1) && key_in_range(x + 1, y + 1, z + 1) &&
-                            pack_key(x - 1, y - 1, z - 1) >= P.lokey[own] &&
-                            (own + 1 == W || pack_key(x + 1, y + 1, z + 1) < P.lokey[own + 1]);
-        if (!inside) {
-            for (int k = 0; k < 27; ++k) {
-                const int nx = x + k % 3 - 1, ny = y + (k / 3) % 3 - 1, nz = z + k / 9 - 1;
-                if (k == 13 || !key_in_range(nx, ny, nz)) continue;
-                const uint64_t nk = pack_key(nx, ny, nz);
-                if (P.index(nk) >= 0) m |= 1ull << P.owner_of_key(nk);  // n's owner needs u as halo
-            }
-        }
-        P.dmask[u] = m;
     }
-    return 0;
 }
 
-// What rank `me` sends to each destination (local buffer indices, by union index) and receives
-// from each source (destination buffer of each entry), and the keys of its output volume (owned
-// union blocks first, then halo, each by union index).
-struct RankLists {
-    std::vector<std::vector<int32_t>> send;  // [dest] local buffers
-    std::vector<std::vector<int32_t>> recv;  // [source] output buffers
-    std::vector<uint64_t> out_keys;
-    int64_t n_owned = 0;
+// ------------------------------------------------------------------ device plan
+// Entries: the W x mx all-gathered keys (rank r's block b at r mx + b, padding = kEmpty).
+// After the sort, entry p of the sorted order has key ks[p] and origin vs[p] = r mx + b.
+constexpr int kMaxRanks = 64;  // destination sets are 64-bit masks
+
+struct PlanSummary {
+    int64_t U;          // union blocks
+    int64_t n_owned;    // this rank's owned blocks (the first n_owned output buffers)
+    int64_t n_out;      // owned + halo output blocks
+    int64_t total;      // send + receive records
+    int64_t cnt[2][kMaxRanks];  // [0][d] blocks sent to d, [1][s] blocks received from s
 };
 
-static void rank_lists(const MergePlan& P, const std::vector<std::vector<uint64_t>>& keys, int me, int mode,
-                       RankLists& L) {
-    const int W = P.world;
-    const int64_t U = (int64_t)P.uni.size();
-    const uint64_t bit = 1ull << me;
-    std::vector<int64_t> outpos(U, -1);
-    L.out_keys.clear();
-    const int64_t lo = mode == MQR_MERGE_ROOT ? 0 : P.bounds[me], hi = mode == MQR_MERGE_ROOT ? U : P.bounds[me + 1];
-    for (int64_t u = lo; u < hi; ++u)
-        if (P.dmask[u] & bit) {
-            outpos[u] = (int64_t)L.out_keys.size();
-            L.out_keys.push_back(P.uni[u]);
-        }
-    L.n_owned = (int64_t)L.out_keys.size();
-    for (int64_t u = 0; u < U; ++u)
-        if ((P.dmask[u] & bit) && outpos[u] < 0) {
-            outpos[u] = (int64_t)L.out_keys.size();
-            L.out_keys.push_back(P.uni[u]);
-        }
-    // sends: my blocks by union index
-    const auto& mine = keys[me];
-    std::vector<std::pair<int64_t, int32_t>> ub(mine.size());
-    for (size_t b = 0; b < mine.size(); ++b) ub[b] = {P.index(mine[b]), (int32_t)b};
-    std::sort(ub.begin(), ub.end());
-    L.send.assign(W, {});
-    for (auto& e : ub)
-        for (int d = 0; d < W; ++d)
-            if (P.dmask[e.first] & (1ull << d)) L.send[d].push_back(e.second);
-    // receives: each source's blocks that come to me, in the order that source sends them
-    L.recv.assign(W, {});
-    for (int s = 0; s < W; ++s) {
-        std::vector<int64_t> us;
-        for (uint64_t k : keys[s]) {
-            const int64_t u = P.index(k);
-            if (P.dmask[u] & bit) us.push_back(u);
-        }
-        std::sort(us.begin(), us.end());
-        for (int64_t u : us) L.recv[s].push_back((int32_t)outpos[u]);
+__device__ __forceinline__ int64_t slice_lo(int64_t U, int W, int r) { return U * r / W; }
+// rank owning union index u (the r with U r / W <= u < U (r + 1) / W)
+__device__ __forceinline__ int owner_of(int64_t u, int64_t U, int W) {
+    int r = (int)((u * W) / (U > 0 ? U : 1));
+    while (r > 0 && slice_lo(U, W, r) > u) --r;
+    while (r + 1 < W && slice_lo(U, W, r + 1) <= u) ++r;
+    return r;
+}
+
+__global__ void k_plan_iota(int32_t* __restrict__ v, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) v[i] = (int32_t)i;
+}
+
+// head[p] = 1 at the first entry of each distinct key
+__global__ void k_plan_heads(const uint64_t* __restrict__ ks, int64_t n, int32_t* __restrict__ head) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    const uint64_t k = ks[p];
+    head[p] = (k != kEmpty && (p == 0 || ks[p - 1] != k)) ? 1 : 0;
+}
+
+// uidx (inclusive head scan) - 1 = union index of entry p; the union keys; U
+__global__ void k_plan_union(const uint64_t* __restrict__ ks, const int32_t* __restrict__ incl, int64_t n,
+                             uint64_t* __restrict__ uni, PlanSummary* __restrict__ sum) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    const uint64_t k = ks[p];
+    if (k != kEmpty && (p == 0 || ks[p - 1] != k)) uni[incl[p] - 1] = k;
+    if (p == n - 1) sum->U = incl[p];
+}
+
+__device__ __forceinline__ int64_t find_union(const uint64_t* __restrict__ uni, int64_t U, uint64_t k) {
+    int64_t lo = 0, hi = U;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (uni[mid] < k) lo = mid + 1;
+        else hi = mid;
     }
+    return lo < U && uni[lo] == k ? lo : -1;
+}
+
+// Destination ranks of each union block; halo flag of this rank (receives u without owning it).
+__global__ void k_plan_dmask(const uint64_t* __restrict__ uni, const PlanSummary* __restrict__ sum, int W, int mode,
+                             int root, int me, uint64_t* __restrict__ dmask, int32_t* __restrict__ halo) {
+    const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t U = sum->U;
+    if (u >= U) return;
+    uint64_t m;
+    if (mode == MQR_MERGE_ROOT) {
+        m = 1ull << root;
+    } else {
+        m = 1ull << owner_of(u, U, W);
+        int x, y, z;
+        unpack_key(uni[u], x, y, z);
+        for (int k = 0; k < 27; ++k) {
+            const int nx = x + k % 3 - 1, ny = y + (k / 3) % 3 - 1, nz = z + k / 9 - 1;
+            if (k == 13 || !key_in_range(nx, ny, nz)) continue;
+            const int64_t j = find_union(uni, U, pack_key(nx, ny, nz));
+            if (j >= 0) m |= 1ull << owner_of(j, U, W);  // the neighbour's owner needs u as halo
+        }
+    }
+    dmask[u] = m;
+    const bool owned = mode == MQR_MERGE_ROOT ? me == root : owner_of(u, U, W) == me;
+    halo[u] = ((m >> me) & 1) && !owned ? 1 : 0;
+}
+
+// Output position of each union block this rank receives (owned slice first, then halo, both in
+// union order), and the output keys.
+__global__ void k_plan_outpos(const uint64_t* __restrict__ uni, const uint64_t* __restrict__ dmask,
+                              const int32_t* __restrict__ halo, const int32_t* __restrict__ hpos,
+                              PlanSummary* __restrict__ sum, int W, int mode,
+                              int root, int me, int32_t* __restrict__ outpos, uint64_t* __restrict__ out_keys) {
+    const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t U = sum->U;
+    int64_t lo, hi;
+    if (mode == MQR_MERGE_ROOT) {
+        lo = 0;
+        hi = me == root ? U : 0;
+    } else {
+        lo = slice_lo(U, W, me);
+        hi = slice_lo(U, W, me + 1);
+    }
+    if (u == 0) {
+        sum->n_owned = hi - lo;
+        sum->n_out = (hi - lo) + (U > 0 ? hpos[U - 1] + halo[U - 1] : 0);
+    }
+    if (u >= U) return;
+    int32_t o = -1;
+    if (u >= lo && u < hi) o = (int32_t)(u - lo);
+    else if ((dmask[u] >> me) & 1) o = (int32_t)((hi - lo) + hpos[u]);
+    outpos[u] = o;
+    if (o >= 0) out_keys[o] = uni[u];
+}
+
+// Records per sorted entry: one per destination if this rank holds the block (send), one if this
+// rank receives it (from the entry's origin rank).
+__global__ void k_plan_rec_count(const uint64_t* __restrict__ ks, const int32_t* __restrict__ vs,
+                                 const int32_t* __restrict__ incl, const uint64_t* __restrict__ dmask, int64_t n,
+                                 int64_t mx, int me, int32_t* __restrict__ rc) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    int c = 0;
+    if (ks[p] != kEmpty) {
+        const uint64_t m = dmask[incl[p] - 1];
+        if (vs[p] / mx == me) c += __popcll(m);
+        c += (int)((m >> me) & 1);
+    }
+    rc[p] = c;
+}
+
+// record key: kind (bit 40: 0 send, 1 receive) | peer (bits 32..37) | entry p (bits 0..31)
+__global__ void k_plan_rec_emit(const uint64_t* __restrict__ ks, const int32_t* __restrict__ vs,
+                                const int32_t* __restrict__ incl, const uint64_t* __restrict__ dmask,
+                                const int32_t* __restrict__ roff, int64_t n, int64_t mx, int me,
+                                uint64_t* __restrict__ rec, PlanSummary* __restrict__ sum) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n || ks[p] == kEmpty) return;
+    const uint64_t m = dmask[incl[p] - 1];
+    const int src = (int)(vs[p] / mx);
+    int64_t o = roff[p];
+    if (src == me) {
+        uint64_t mm = m;
+        while (mm) {
+            const int d = __builtin_ctzll(mm);
+            mm &= mm - 1;
+            rec[o++] = ((uint64_t)d << 32) | (uint64_t)p;
+            atomicAdd((unsigned long long*)&sum->cnt[0][d], 1ull);
+        }
+    }
+    if ((m >> me) & 1) {
+        rec[o] = (1ull << 40) | ((uint64_t)src << 32) | (uint64_t)p;
+        atomicAdd((unsigned long long*)&sum->cnt[1][src], 1ull);
+    }
+}
+
+// Sorted records -> lists: sends: origin buffer; receives: output buffer and origin buffer.
+__global__ void k_plan_lists(const uint64_t* __restrict__ rec, int64_t R, const int32_t* __restrict__ vs,
+                             const int32_t* __restrict__ incl, const int32_t* __restrict__ outpos, int64_t mx,
+                             const PlanSummary* __restrict__ sum, int W, int32_t* __restrict__ send_idx,
+                             int32_t* __restrict__ recv_dst, int32_t* __restrict__ recv_src) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= R) return;
+    const uint64_t r = rec[i];
+    if (r == kEmpty) return;
+    const int64_t p = (int64_t)(r & 0xffffffffull);
+    const int32_t b = (int32_t)(vs[p] % mx);
+    if (!((r >> 40) & 1)) {
+        send_idx[i] = b;
+    } else {
+        int64_t ns = 0;
+        for (int d = 0; d < W; ++d) ns += sum->cnt[0][d];
+        recv_dst[i - ns] = outpos[incl[p] - 1];
+        recv_src[i - ns] = b;
+    }
+}
+
+// One rank's plan over the gathered keys dkeys[W * mx] (device).  Host results in `H` (pinned
+// summary, read after one stream sync); device lists in the scratch: send_idx (segments by
+// destination), recv_dst / recv_src (segments by source), out_keys.
+struct PlanView {
+    const PlanSummary* H = nullptr;
+    int32_t* send_idx = nullptr;
+    int32_t* recv_dst = nullptr;
+    int32_t* recv_src = nullptr;
+    uint64_t* out_keys = nullptr;
+};
+
+static size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
+
+static int device_plan(PlanScratch& S, hipStream_t st, const uint64_t* dkeys, int W, int64_t mx, int me, int mode,
+                       int root, PlanView& out) {
+    const int64_t n = (int64_t)W * mx;
+    MQR_REQUIRE(n < (int64_t{1} << 31), "merge plan: too many blocks");
+    const int64_t rmax = n * (int64_t)(std::min(W, 27) + 1);  // records: <= 27 destinations + 1 receive per entry
+    size_t tb_sort = 0, tb_scan = 0, tb_rsort = 0;
+    MQR_CHECK_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb_sort, (const uint64_t*)nullptr, (uint64_t*)nullptr,
+                                                     (const int32_t*)nullptr, (int32_t*)nullptr, (int)n, 0, 64, st));
+    MQR_CHECK_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, tb_scan, (const int32_t*)nullptr, (int32_t*)nullptr,
+                                                   (int)n, st));
+    MQR_CHECK_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tb_rsort, (const uint64_t*)nullptr, (uint64_t*)nullptr,
+                                                    (int)rmax, 0, 41, st));
+    const size_t tb = std::max(tb_sort, std::max(tb_scan, tb_rsort));
+    // carve the scratch
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        const size_t o = off;
+        off += align_up(bytes);
+        return o;
+    };
+    const size_t o_ks = take(8 * n), o_vi = take(4 * n), o_vs = take(4 * n), o_head = take(4 * n),
+                 o_incl = take(4 * n), o_uni = take(8 * n), o_dm = take(8 * n), o_halo = take(4 * n),
+                 o_hpos = take(4 * n), o_outpos = take(4 * n), o_rc = take(4 * (n + 1)), o_roff = take(4 * (n + 1)),
+                 o_rec = take(8 * rmax), o_recs = take(8 * rmax), o_send = take(4 * rmax), o_rdst = take(4 * rmax),
+                 o_rsrc = take(4 * rmax), o_okeys = take(8 * n), o_sum = take(sizeof(PlanSummary)), o_tmp = take(tb);
+    if (S.cap < off) {
+        const size_t want = std::max(off, S.cap + S.cap / 2);
+        if (S.buf) MQR_CHECK_HIP(hipFree(S.buf));
+        S.buf = nullptr;
+        S.cap = 0;
+        MQR_CHECK_HIP(hipMalloc(&S.buf, want));
+        S.cap = want;
+    }
+    if (!S.h_sum) MQR_CHECK_HIP(hipHostMalloc(&S.h_sum, sizeof(PlanSummary), hipHostMallocDefault));
+    char* b = static_cast<char*>(S.buf);
+    auto U64 = [&](size_t o) { return reinterpret_cast<uint64_t*>(b + o); };
+    auto I32 = [&](size_t o) { return reinterpret_cast<int32_t*>(b + o); };
+    PlanSummary* dsum = reinterpret_cast<PlanSummary*>(b + o_sum);
+    void* tmp = b + o_tmp;
+    const unsigned g = (unsigned)((n + 255) / 256);
+    MQR_CHECK_HIP(hipMemsetAsync(dsum, 0, sizeof(PlanSummary), st));
+    hipLaunchKernelGGL(k_plan_iota, dim3(g), dim3(256), 0, st, I32(o_vi), n);
+    size_t t = tb;
+    MQR_CHECK_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, t, dkeys, U64(o_ks), I32(o_vi), I32(o_vs), (int)n, 0, 64, st));
+    hipLaunchKernelGGL(k_plan_heads, dim3(g), dim3(256), 0, st, U64(o_ks), n, I32(o_head));
+    t = tb;
+    MQR_CHECK_HIP(hipcub::DeviceScan::InclusiveSum(tmp, t, I32(o_head), I32(o_incl), (int)n, st));
+    hipLaunchKernelGGL(k_plan_union, dim3(g), dim3(256), 0, st, U64(o_ks), I32(o_incl), n, U64(o_uni), dsum);
+    MQR_CHECK_HIP(hipMemsetAsync(I32(o_halo), 0, 4 * n, st));
+    hipLaunchKernelGGL(k_plan_dmask, dim3(g), dim3(256), 0, st, U64(o_uni), dsum, W, mode, root, me, U64(o_dm),
+                       I32(o_halo));
+    t = tb;
+    MQR_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, t, I32(o_halo), I32(o_hpos), (int)n, st));
+    hipLaunchKernelGGL(k_plan_outpos, dim3(g), dim3(256), 0, st, U64(o_uni), U64(o_dm), I32(o_halo), I32(o_hpos),
+                       dsum, W, mode,
+                       root, me, I32(o_outpos), U64(o_okeys));
+    hipLaunchKernelGGL(k_plan_rec_count, dim3(g), dim3(256), 0, st, U64(o_ks), I32(o_vs), I32(o_incl), U64(o_dm), n,
+                       mx, me, I32(o_rc));
+    MQR_CHECK_HIP(hipMemsetAsync(I32(o_rc) + n, 0, 4, st));
+    t = tb;
+    MQR_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, t, I32(o_rc), I32(o_roff), (int)(n + 1), st));
+    MQR_CHECK_HIP(hipMemsetAsync(U64(o_rec), 0xff, 8 * rmax, st));
+    hipLaunchKernelGGL(k_plan_rec_emit, dim3(g), dim3(256), 0, st, U64(o_ks), I32(o_vs), I32(o_incl), U64(o_dm),
+                       I32(o_roff), n, mx, me, U64(o_rec), dsum);
+    t = tb;
+    MQR_CHECK_HIP(hipcub::DeviceRadixSort::SortKeys(tmp, t, U64(o_rec), U64(o_recs), (int)rmax, 0, 41, st));
+    hipLaunchKernelGGL(k_plan_lists, dim3((unsigned)((rmax + 255) / 256)), dim3(256), 0, st, U64(o_recs), rmax,
+                       I32(o_vs), I32(o_incl), I32(o_outpos), mx, dsum, W, I32(o_send), I32(o_rdst), I32(o_rsrc));
+    MQR_CHECK_HIP(hipGetLastError());
+    MQR_CHECK_HIP(hipMemcpyAsync(S.h_sum, dsum, sizeof(PlanSummary), hipMemcpyDeviceToHost, st));
+    MQR_CHECK_HIP(hipStreamSynchronize(st));
+    out.H = static_cast<const PlanSummary*>(S.h_sum);
+    out.send_idx = I32(o_send);
+    out.recv_dst = I32(o_rdst);
+    out.recv_src = I32(o_rsrc);
+    out.out_keys = U64(o_okeys);
+    return 0;
 }
 
 static int grow(void** p, size_t* cap, size_t need) {
     if (*cap >= need) return 0;
+    const size_t want = std::max(need, *cap + *cap / 2);  // 1.5x: few reallocations as counts vary
     if (*p) MQR_CHECK_HIP(hipFree(*p));
     *p = nullptr;
     *cap = 0;
-    const size_t want = std::max(need, *cap + *cap / 2);
     MQR_CHECK_HIP(hipMalloc(p, want));
     *cap = want;
     return 0;
 }
 
-static int local_keys(mqr_vbg* v, std::vector<uint64_t>& out) {
-    if (sync_all(v)) return 1;
-    out.resize(v->pool_count);
-    if (v->pool_count)
-        MQR_CHECK_HIP(hipMemcpy(out.data(), v->bkeys, sizeof(uint64_t) * v->pool_count, hipMemcpyDeviceToHost));
-    return 0;
-}
-
-// Upload an int32 list to `dst` (device) on stream s.
-static int upload(const std::vector<int32_t>& h, int32_t* dst, hipStream_t s) {
-    if (!h.empty()) MQR_CHECK_HIP(hipMemcpyAsync(dst, h.data(), sizeof(int32_t) * h.size(), hipMemcpyHostToDevice, s));
-    return 0;
-}
-
-static size_t total(const std::vector<std::vector<int32_t>>& l) {
-    size_t n = 0;
-    for (auto& x : l) n += x.size();
-    return n;
-}
-
-// Output volume of one rank: empty it, activate its keys in order (owned first).  `dk`: device
-// scratch for the keys (>= out_keys.size() entries), or null to allocate one here.
-static int prepare_out(mqr_vbg* out, const RankLists& L, uint64_t* dk) {
+// Output volume of one rank: empty it, activate its keys in order (owned first).
+static int prepare_out(mqr_vbg* out, const uint64_t* dk, int64_t n) {
     if (mqr_vbg_reset(out)) return 1;
-    if (L.out_keys.empty()) return 0;
-    uint64_t* own = nullptr;
-    if (!dk) {
-        MQR_CHECK_HIP(hipMalloc(&own, sizeof(uint64_t) * L.out_keys.size()));
-        dk = own;
-    }
-    MQR_CHECK_HIP(hipMemcpyAsync(dk, L.out_keys.data(), sizeof(uint64_t) * L.out_keys.size(), hipMemcpyHostToDevice,
-                                 out->stream));
-    const int rc = activate_ordered(out, dk, (int64_t)L.out_keys.size());
-    if (own) (void)hipFree(own);
-    return rc;
+    return n > 0 ? activate_ordered(out, dk, n) : 0;
 }
 
 }  // namespace mqr
@@ -317,7 +479,8 @@ int mqr_comm_unique_id(uint8_t* id_out) {
 
 int mqr_comm_init(int device, int rank, int world, const uint8_t* id, mqr_comm** out) {
     MQR_REQUIRE(id && out, "null argument");
-    MQR_REQUIRE(world >= 1 && world <= 64 && rank >= 0 && rank < world, "rank / world out of range (world <= 64)");
+    MQR_REQUIRE(world >= 1 && world <= kMaxRanks && rank >= 0 && rank < world,
+                "rank / world out of range (world <= 64)");
     RcclApi* api = rccl();
     MQR_REQUIRE(api, g_rccl.err.c_str());
     MQR_CHECK_HIP(hipSetDevice(device));
@@ -333,10 +496,11 @@ int mqr_comm_init(int device, int rank, int world, const uint8_t* id, mqr_comm**
         delete c;
         return 1;
     }
-    if (hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking) != hipSuccess) {
-        set_error("mqr_comm_init: stream creation failed");
-        api->CommDestroy(c->nc);
-        delete c;
+    bool ok = hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking) == hipSuccess;
+    for (int i = 0; i < 5 && ok; ++i) ok = hipEventCreate(&c->ev[i]) == hipSuccess;
+    if (!ok) {
+        set_error("mqr_comm_init: stream / event creation failed");
+        mqr_comm_destroy(c);
         return 1;
     }
     *out = c;
@@ -352,14 +516,31 @@ int mqr_comm_destroy(mqr_comm* c) {
     if (c->sendbuf) (void)hipFree(c->sendbuf);
     if (c->recvbuf) (void)hipFree(c->recvbuf);
     if (c->small) (void)hipFree(c->small);
-    if (c->lists) (void)hipFree(c->lists);
+    for (hipEvent_t e : c->ev)
+        if (e) (void)hipEventDestroy(e);
     if (c->s) (void)hipStreamDestroy(c->s);
     delete c;
     return 0;
 }
 
+int mqr_comm_timing(mqr_comm* c, float* ms4) {
+    MQR_REQUIRE(c && ms4, "null argument");
+    for (int i = 0; i < 4; ++i) ms4[i] = c->last_ms[i];
+    return 0;
+}
+
+namespace {
+// Every exit of mqr_reduce_rccl waits for its stream first: async copies read host memory of the
+// call (counts, the pinned plan summary) and a failing rank must not leave kernels in flight.
+struct StreamDrain {
+    hipStream_t s;
+    ~StreamDrain() { (void)hipStreamSynchronize(s); }
+};
+}  // namespace
+
 int mqr_reduce_rccl(mqr_vbg* local, mqr_comm* c, int mode, int root, mqr_vbg* out, int64_t* n_owned) {
     MQR_REQUIRE(local && c && out && n_owned, "null argument");
+    MQR_REQUIRE(local != out, "mqr_reduce_rccl: `out` must be a different volume than `local` (it is emptied first)");
     MQR_REQUIRE(mode == MQR_MERGE_ROOT || mode == MQR_MERGE_SHARDED, "unknown merge mode");
     MQR_REQUIRE(root >= 0 && root < c->world, "root out of range");
     MQR_REQUIRE(local->device == c->device && out->device == c->device, "volumes and communicator on one device");
@@ -367,17 +548,22 @@ int mqr_reduce_rccl(mqr_vbg* local, mqr_comm* c, int mode, int root, mqr_vbg* ou
     RcclApi* api = rccl();
     MQR_REQUIRE(api, g_rccl.err.c_str());
     MQR_CHECK_HIP(hipSetDevice(c->device));
+    *n_owned = 0;
     const int W = c->world, me = c->rank;
     const int R3 = (int)local->R3;
-    // 1. all-gather block counts, then the padded packed keys
-    std::vector<uint64_t> mine;
-    if (local_keys(local, mine)) return 1;
-    const int64_t n_me = (int64_t)mine.size();
+    const size_t eb = sizeof(float2) * R3;
+    // host state the stream's async copies read: declared before the drain guard, so it outlives it
+    int64_t n_me = 0;
+    std::vector<int64_t> cnt(W);
+    StreamDrain drain{c->s};
+    if (sync_all(local)) return 1;  // the local volume's integration is complete
+    n_me = local->pool_count;
+    MQR_CHECK_HIP(hipEventRecord(c->ev[0], c->s));
+    // 1. all-gather block counts (host: the padding), then the padded packed keys
     if (grow(&c->small, &c->small_cap, sizeof(int64_t) * 2 * W)) return 1;
     int64_t* dcnt = static_cast<int64_t*>(c->small);
     MQR_CHECK_HIP(hipMemcpyAsync(dcnt + W, &n_me, sizeof(int64_t), hipMemcpyHostToDevice, c->s));
     MQR_CHECK_NCCL(api, api->AllGather(dcnt + W, dcnt, 1, ncclInt64, c->nc, c->s));
-    std::vector<int64_t> cnt(W);
     MQR_CHECK_HIP(hipMemcpyAsync(cnt.data(), dcnt, sizeof(int64_t) * W, hipMemcpyDeviceToHost, c->s));
     MQR_CHECK_HIP(hipStreamSynchronize(c->s));
     const int64_t mx = std::max<int64_t>(1, *std::max_element(cnt.begin(), cnt.end()));
@@ -385,141 +571,125 @@ int mqr_reduce_rccl(mqr_vbg* local, mqr_comm* c, int mode, int root, mqr_vbg* ou
     uint64_t* dkeys = static_cast<uint64_t*>(c->small);
     uint64_t* dmine = dkeys + mx * W;
     MQR_CHECK_HIP(hipMemsetAsync(dmine, 0xff, sizeof(uint64_t) * mx, c->s));
-    if (n_me) MQR_CHECK_HIP(hipMemcpyAsync(dmine, mine.data(), sizeof(uint64_t) * n_me, hipMemcpyHostToDevice, c->s));
+    if (n_me)
+        MQR_CHECK_HIP(hipMemcpyAsync(dmine, local->bkeys, sizeof(uint64_t) * n_me, hipMemcpyDeviceToDevice, c->s));
     MQR_CHECK_NCCL(api, api->AllGather(dmine, dkeys, mx, ncclUint64, c->nc, c->s));
-    std::vector<uint64_t> flat(mx * W);
-    MQR_CHECK_HIP(hipMemcpyAsync(flat.data(), dkeys, sizeof(uint64_t) * mx * W, hipMemcpyDeviceToHost, c->s));
-    MQR_CHECK_HIP(hipStreamSynchronize(c->s));
-    std::vector<std::vector<uint64_t>> keys(W);
-    for (int r = 0; r < W; ++r) keys[r].assign(flat.begin() + r * mx, flat.begin() + r * mx + cnt[r]);
-    // 2. plan (identical everywhere) and this rank's lists
-    MergePlan P;
-    build_plan(keys, mode, root, P);
-    RankLists L;
-    rank_lists(P, keys, me, mode, L);
-    const size_t ns = total(L.send), nr = total(L.recv);
-    // index lists, then (8-byte aligned) the output keys
-    const size_t lbytes = (sizeof(int32_t) * (ns + nr) + 7) & ~size_t(7);
-    if (grow(&c->lists, &c->lists_cap, std::max<size_t>(lbytes + sizeof(uint64_t) * L.out_keys.size(), 8))) return 1;
-    int32_t* dlists = static_cast<int32_t*>(c->lists);
-    if (prepare_out(out, L, reinterpret_cast<uint64_t*>(static_cast<char*>(c->lists) + lbytes))) return 1;
+    // 2. the plan on the device (identical on every rank); the host reads the list lengths
+    PlanView pv;
+    if (device_plan(c->plan, c->s, dkeys, W, mx, me, mode, root, pv)) return 1;
+    MQR_CHECK_HIP(hipEventRecord(c->ev[1], c->s));
+    const PlanSummary H = *pv.H;
+    std::vector<size_t> soff(W + 1, 0), roff(W + 1, 0);
+    for (int r = 0; r < W; ++r) {
+        soff[r + 1] = soff[r] + (size_t)H.cnt[0][r];
+        roff[r + 1] = roff[r] + (size_t)H.cnt[1][r];
+    }
+    const size_t ns = soff[W], nr = roff[W];
+    if (prepare_out(out, pv.out_keys, H.n_out)) return 1;  // synchronous (out's stream)
     // 3. gather my outgoing blocks (segments by destination), post the sparse all-to-all
-    const size_t eb = sizeof(float2) * R3;
     if (grow(&c->sendbuf, &c->send_cap, std::max<size_t>(ns, 1) * eb) ||
         grow(&c->recvbuf, &c->recv_cap, std::max<size_t>(nr, 1) * eb))
         return 1;
-    std::vector<int32_t> sidx, ridx;
-    for (auto& l : L.send) sidx.insert(sidx.end(), l.begin(), l.end());
-    for (auto& l : L.recv) ridx.insert(ridx.end(), l.begin(), l.end());
-    int rc = upload(sidx, dlists, c->s) || upload(ridx, dlists + ns, c->s);
-    if (!rc && ns)
-        hipLaunchKernelGGL(k_gather_blocks, dim3((unsigned)ns), dim3(256), 0, c->s, dlists, (int64_t)ns, local->pool,
-                           R3, static_cast<float2*>(c->sendbuf));
     float2* sb = static_cast<float2*>(c->sendbuf);
     float2* rb = static_cast<float2*>(c->recvbuf);
-    std::vector<size_t> soff(W + 1, 0), roff(W + 1, 0);
-    for (int r = 0; r < W; ++r) {
-        soff[r + 1] = soff[r] + L.send[r].size();
-        roff[r + 1] = roff[r] + L.recv[r].size();
-    }
-    if (!rc) {
-        if (L.send[me].size())
-            rc = hipMemcpyAsync(rb + roff[me] * R3, sb + soff[me] * R3, eb * L.send[me].size(),
-                                hipMemcpyDeviceToDevice, c->s) != hipSuccess;
+    if (ns)
+        hipLaunchKernelGGL(k_gather_blocks, dim3((unsigned)ns), dim3(256), 0, c->s, pv.send_idx, (int64_t)ns,
+                           local->pool, R3, sb);
+    MQR_CHECK_HIP(hipGetLastError());
+    MQR_CHECK_HIP(hipEventRecord(c->ev[2], c->s));
+    const size_t nself = soff[me + 1] - soff[me];
+    if (nself)
+        MQR_CHECK_HIP(hipMemcpyAsync(rb + roff[me] * R3, sb + soff[me] * R3, eb * nself, hipMemcpyDeviceToDevice, c->s));
+    {
         ncclResult_t r = api->GroupStart();
         for (int p = 0; p < W && r == ncclSuccess; ++p) {
             if (p == me) continue;
-            if (L.send[p].size())
-                r = api->Send(sb + soff[p] * R3, L.send[p].size() * R3 * 2, ncclFloat32, p, c->nc, c->s);
-            if (r == ncclSuccess && L.recv[p].size())
-                r = api->Recv(rb + roff[p] * R3, L.recv[p].size() * R3 * 2, ncclFloat32, p, c->nc, c->s);
+            if (soff[p + 1] > soff[p])
+                r = api->Send(sb + soff[p] * R3, (soff[p + 1] - soff[p]) * R3 * 2, ncclFloat32, p, c->nc, c->s);
+            if (r == ncclSuccess && roff[p + 1] > roff[p])
+                r = api->Recv(rb + roff[p] * R3, (roff[p + 1] - roff[p]) * R3 * 2, ncclFloat32, p, c->nc, c->s);
         }
         const ncclResult_t r2 = api->GroupEnd();
         if (r != ncclSuccess || r2 != ncclSuccess) {
             set_error(std::string("RCCL exchange: ") + api->GetErrorString(r != ncclSuccess ? r : r2));
-            rc = 1;
+            return 1;
         }
     }
+    MQR_CHECK_HIP(hipEventRecord(c->ev[3], c->s));
     // 4. merge the received entries source by source (rank order)
-    for (int s = 0; s < W && !rc; ++s)
-        if (L.recv[s].size())
-            hipLaunchKernelGGL(k_merge_blocks, dim3((unsigned)L.recv[s].size()), dim3(256), 0, c->s,
-                               dlists + ns + roff[s], (int64_t)L.recv[s].size(), rb + roff[s] * R3, R3, out->pool);
-    if (!rc && (hipGetLastError() != hipSuccess || hipStreamSynchronize(c->s) != hipSuccess)) {
+    for (int src = 0; src < W; ++src)
+        if (roff[src + 1] > roff[src])
+            hipLaunchKernelGGL(k_merge_blocks, dim3((unsigned)(roff[src + 1] - roff[src])), dim3(256), 0, c->s,
+                               pv.recv_dst + roff[src], (int64_t)(roff[src + 1] - roff[src]), rb + roff[src] * R3, R3,
+                               out->pool);
+    MQR_CHECK_HIP(hipGetLastError());
+    MQR_CHECK_HIP(hipEventRecord(c->ev[4], c->s));
+    if (hipStreamSynchronize(c->s) != hipSuccess) {
         set_error("mqr_reduce_rccl: merge kernels failed");
-        rc = 1;
+        return 1;
     }
-    *n_owned = rc ? 0 : L.n_owned;
-    return rc;
+    for (int i = 0; i < 4; ++i)
+        if (hipEventElapsedTime(&c->last_ms[i], c->ev[i], c->ev[i + 1]) != hipSuccess) c->last_ms[i] = -1.f;
+    *n_owned = H.n_owned;
+    return 0;
 }
 
 int mqr_merge_local(mqr_vbg** locals, int n, int mode, int root, mqr_vbg** outs, int64_t* n_owned) {
-    MQR_REQUIRE(locals && outs && n_owned && n >= 1 && n <= 64, "bad arguments");
+    MQR_REQUIRE(locals && outs && n_owned && n >= 1 && n <= kMaxRanks, "bad arguments");
     MQR_REQUIRE(mode == MQR_MERGE_ROOT || mode == MQR_MERGE_SHARDED, "unknown merge mode");
     MQR_REQUIRE(root >= 0 && root < n, "root out of range");
-    for (int r = 0; r < n; ++r) MQR_REQUIRE(locals[r] && outs[r], "null volume");
+    for (int r = 0; r < n; ++r) {
+        MQR_REQUIRE(locals[r] && outs[r], "null volume");
+        MQR_REQUIRE(locals[r]->device == locals[0]->device && outs[r]->device == locals[0]->device,
+                    "mqr_merge_local: all volumes on one device");
+        for (int q = 0; q < n; ++q) MQR_REQUIRE(outs[r] != locals[q], "mqr_merge_local: an output aliases an input");
+    }
+    MQR_CHECK_HIP(hipSetDevice(locals[0]->device));
     const int R3 = (int)locals[0]->R3;
-    std::vector<std::vector<uint64_t>> keys(n);
+    int64_t mx = 1;
+    for (int r = 0; r < n; ++r) {
+        if (sync_all(locals[r])) return 1;
+        mx = std::max<int64_t>(mx, locals[r]->pool_count);
+    }
+    hipStream_t st = nullptr;
+    MQR_CHECK_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    StreamDrain drain{st};
+    struct StreamFree {
+        hipStream_t s;
+        ~StreamFree() { (void)hipStreamDestroy(s); }
+    } sfree{st};
+    // the all-gather, as device copies: rank r's keys at r mx, padded with kEmpty
+    uint64_t* dkeys = nullptr;
+    MQR_CHECK_HIP(hipMalloc(&dkeys, sizeof(uint64_t) * mx * n));
+    struct DevFree {
+        void* p;
+        ~DevFree() { if (p) (void)hipFree(p); }
+    } kfree{dkeys};
+    MQR_CHECK_HIP(hipMemsetAsync(dkeys, 0xff, sizeof(uint64_t) * mx * n, st));
     for (int r = 0; r < n; ++r)
-        if (local_keys(locals[r], keys[r])) return 1;
-    MergePlan P;
-    build_plan(keys, mode, root, P);
-    std::vector<RankLists> L(n);
-    for (int r = 0; r < n; ++r) rank_lists(P, keys, r, mode, L[r]);
-    const size_t eb = sizeof(float2) * R3;
-    // every source gathers its outgoing segments; every destination merges them in source order
-    std::vector<float2*> send(n, nullptr);
-    std::vector<std::vector<size_t>> soff(n, std::vector<size_t>(n + 1, 0));
-    int rc = 0;
-    for (int s = 0; s < n && !rc; ++s) {
-        MQR_CHECK_HIP(hipSetDevice(locals[s]->device));
-        const size_t ns = total(L[s].send);
-        for (int d = 0; d < n; ++d) soff[s][d + 1] = soff[s][d] + L[s].send[d].size();
-        std::vector<int32_t> sidx;
-        for (auto& l : L[s].send) sidx.insert(sidx.end(), l.begin(), l.end());
-        int32_t* di = nullptr;
-        rc = hipMalloc(&send[s], std::max<size_t>(ns, 1) * eb) != hipSuccess ||
-             hipMalloc(&di, sizeof(int32_t) * std::max<size_t>(ns, 1)) != hipSuccess;
-        if (!rc && ns) {
-            rc = upload(sidx, di, locals[s]->stream);
-            hipLaunchKernelGGL(k_gather_blocks, dim3((unsigned)ns), dim3(256), 0, locals[s]->stream, di, (int64_t)ns,
-                               locals[s]->pool, R3, send[s]);
-            rc = rc || hipStreamSynchronize(locals[s]->stream) != hipSuccess;
+        if (locals[r]->pool_count)
+            MQR_CHECK_HIP(hipMemcpyAsync(dkeys + r * mx, locals[r]->bkeys, sizeof(uint64_t) * locals[r]->pool_count,
+                                         hipMemcpyDeviceToDevice, st));
+    PlanScratch S;
+    for (int d = 0; d < n; ++d) {
+        // destination d's plan: its receive segments name, per source, the source's buffers
+        PlanView pv;
+        if (device_plan(S, st, dkeys, n, mx, d, mode, root, pv)) return 1;
+        const PlanSummary H = *pv.H;
+        if (prepare_out(outs[d], pv.out_keys, H.n_out)) return 1;
+        int64_t o = 0;
+        for (int src = 0; src < n; ++src) {
+            const int64_t m = H.cnt[1][src];
+            if (m)
+                hipLaunchKernelGGL(k_merge_direct, dim3((unsigned)m), dim3(256), 0, st, pv.recv_src + o,
+                                   pv.recv_dst + o, m, locals[src]->pool, R3, outs[d]->pool);
+            o += m;
         }
-        if (di) (void)hipFree(di);
-        if (rc) set_error("mqr_merge_local: gather failed");
+        MQR_CHECK_HIP(hipGetLastError());
+        MQR_CHECK_HIP(hipStreamSynchronize(st));  // the plan scratch is reused for the next destination
+        n_owned[d] = H.n_owned;
     }
-    for (int d = 0; d < n && !rc; ++d) {
-        mqr_vbg* o = outs[d];
-        MQR_CHECK_HIP(hipSetDevice(o->device));
-        if (prepare_out(o, L[d], nullptr)) {
-            rc = 1;
-            break;
-        }
-        for (int s = 0; s < n && !rc; ++s) {
-            const size_t m = L[d].recv[s].size();
-            if (!m) continue;
-            float2* rb = nullptr;
-            int32_t* di = nullptr;
-            rc = hipMalloc(&rb, m * eb) != hipSuccess || hipMalloc(&di, sizeof(int32_t) * m) != hipSuccess ||
-                 // on the merge's stream: a plain device-to-device hipMemcpy is not ordered before
-                 // work on a non-blocking stream
-                 hipMemcpyAsync(rb, send[s] + soff[s][d] * R3, m * eb, hipMemcpyDefault, o->stream) != hipSuccess ||
-                 upload(L[d].recv[s], di, o->stream);
-            if (!rc) {
-                hipLaunchKernelGGL(k_merge_blocks, dim3((unsigned)m), dim3(256), 0, o->stream, di, (int64_t)m, rb, R3,
-                                   o->pool);
-                rc = hipGetLastError() != hipSuccess || hipStreamSynchronize(o->stream) != hipSuccess;
-            }
-            if (rb) (void)hipFree(rb);
-            if (di) (void)hipFree(di);
-            if (rc) set_error("mqr_merge_local: merge failed");
-        }
-        n_owned[d] = L[d].n_owned;
-    }
-    for (int s = 0; s < n; ++s)
-        if (send[s]) (void)hipFree(send[s]);
-    return rc;
+    return 0;
 }
 
 }  // extern "C"

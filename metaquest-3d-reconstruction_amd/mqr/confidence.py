@@ -76,6 +76,22 @@ def compute_pixel_error_map(intrinsic_matrices, extrinsic_matrices, extrinsic_ma
     return out
 
 
+def _canvas_stack(frames):
+    """Stack a window of frames of possibly different sizes (None = failed load) on a zero canvas of
+    the largest height and width.  Exact for the reference's arithmetic: bilinear_interpolate_depth
+    bounds-checks against the target's own (h, w) (compute_pixel_error_map.py:4-60), and a tap in
+    the zero padding fails the same tap test (`0 < depth`) that the reference's `u1 < w` / `v1 < h`
+    check rejects; coordinates beyond 10 max(w, h) fail the bounds check either way."""
+    shapes = [f.shape for f in frames if f is not None]
+    H = max(h for h, _ in shapes)
+    W = max(w for _, w in shapes)
+    out = np.zeros((len(frames), H, W), np.float32)
+    for i, f in enumerate(frames):
+        if f is not None:
+            out[i, :f.shape[0], :f.shape[1]] = f
+    return out
+
+
 def build_confidence_map(depth_data_io, dataset, intrinsic_matrices, extrinsic_matrices, extrinsic_matrices_inv,
                          side, ref_frame_idx, target_frame_range=10, depth_max=3.0,
                          error_threshold=0.05) -> Optional[ConfidenceMap]:
@@ -84,22 +100,32 @@ def build_confidence_map(depth_data_io, dataset, intrinsic_matrices, extrinsic_m
         return None
     lo = max(0, ref_frame_idx - target_frame_range)
     hi = min(len(dataset), ref_frame_idx + target_frame_range + 1)
-    frames, ok = [], []
-    for i in range(lo, hi):
-        d = ref if i == ref_frame_idx else depth_data_io.load_depth_map_by_index(side=side, dataset=dataset, index=i)
-        ok.append(d is not None and d.shape == ref.shape)
-        frames.append(d if ok[-1] else np.zeros_like(ref))
-    conf, valid = confidence_maps(np.stack(frames), np.asarray(intrinsic_matrices)[lo:hi],
+    frames = [ref if i == ref_frame_idx else depth_data_io.load_depth_map_by_index(side=side, dataset=dataset,
+                                                                                     index=i)
+              for i in range(lo, hi)]
+    ok = np.array([f is not None for f in frames])
+    conf, valid = confidence_maps(_canvas_stack(frames), np.asarray(intrinsic_matrices)[lo:hi],
                                   np.asarray(extrinsic_matrices)[lo:hi], np.asarray(extrinsic_matrices_inv)[lo:hi],
                                   ref_frame_idx - lo, ref_frame_idx - lo + 1, target_frame_range, depth_max,
-                                  error_threshold, np.array(ok))
-    return ConfidenceMap(confidence_map=conf[0], valid_count=valid[0])
+                                  error_threshold, ok)
+    h, w = ref.shape
+    return ConfidenceMap(confidence_map=np.ascontiguousarray(conf[0, :h, :w]),
+                         valid_count=np.ascontiguousarray(valid[0, :h, :w]))
+
+
+def _report(side, idx, timestamp, e):
+    """estimate_depth_confidences.py:114-117: a failing reference frame is reported and skipped."""
+    import traceback
+    print(f"[Error] build_and_save_confidence_map failed for {side.name} frame {idx} (timestamp {timestamp}): {e}")
+    traceback.print_exception(type(e), e, e.__traceback__)
 
 
 def estimate_depth_confidences(depth_data_io, config: DepthConfidenceEstimationConfig, sides=None):
     """Per side: skip if the output directory exists (``skip_if_output_dir_exists``), keep existing
     per-frame files, compute the rest in chunks of REF_CHUNK reference frames.  Frames are decoded
-    once each and held only while a chunk's window [first - r, last + r] needs them."""
+    once each and held only while a chunk's window [first - r, last + r] needs them.  As in the
+    reference (estimate_depth_confidences.py:98-117), an error while building or saving one
+    reference frame's map is printed and that frame is skipped; the other frames go on."""
     for side in (sides or list(Side)):
         if config.skip_if_output_dir_exists and depth_data_io.exists_depth_confidence_map_dir(side=side):
             print(f"[{side.name}] Skipping confidence map estimation: output directory already exists. "
@@ -118,7 +144,7 @@ def estimate_depth_confidences(depth_data_io, config: DepthConfidenceEstimationC
                 is None]
         cache = {}  # index -> decoded frame (None: missing / invalid), frames of the current window only
         pool = io_pool()
-        writes = []  # npz writes in flight (the I/O threads), awaited before the next side
+        writes = []  # (frame index, npz write in flight on the I/O threads)
 
         def frame(i):
             if i not in cache:
@@ -131,40 +157,47 @@ def estimate_depth_confidences(depth_data_io, config: DepthConfidenceEstimationC
                     side=side, dataset=dataset, index=k), need)):
                 cache[i] = d
 
+        def settle(keep):  # wait for all but the last `keep` writes, reporting failures per frame
+            nonlocal writes
+            cut = max(0, len(writes) - keep)
+            for i, w in writes[:cut]:
+                try:
+                    w.result()
+                except Exception as e:  # noqa: BLE001 -- the reference catches everything per frame
+                    _report(side, i, dataset.timestamps[i], e)
+            writes = writes[cut:]
+
         for c0 in range(0, len(todo), REF_CHUNK):
             part = todo[c0:c0 + REF_CHUNK]
-            if part:
-                prefetch(part[0] - r, part[-1] + r + 1)
+            prefetch(part[0] - r, part[-1] + r + 1)
             chunk = [i for i in part if frame(i) is not None]  # invalid refs: no output
             for i in [k for k in cache if chunk and k < chunk[0] - r]:
                 del cache[i]
-            # runs of one frame size spanning < REF_CHUNK indices (sparse resumes keep windows small); a
-            # neighbour of another size counts as a failed load
             j = 0
-            while j < len(chunk):
-                shape = frame(chunk[j]).shape
+            while j < len(chunk):  # runs spanning < REF_CHUNK indices (sparse resumes keep windows small)
                 k = j + 1
-                while k < len(chunk) and frame(chunk[k]).shape == shape and chunk[k] - chunk[j] < REF_CHUNK:
+                while k < len(chunk) and chunk[k] - chunk[j] < REF_CHUNK:
                     k += 1
                 refs = chunk[j:k]
+                j = k
                 a, b = refs[0], refs[-1] + 1
                 lo, hi = max(0, a - r), min(n, b + r)
                 win = [frame(i) for i in range(lo, hi)]
-                ok = np.array([f is not None and f.shape == shape for f in win])
-                if (~ok & np.array([f is not None for f in win])).any():
-                    print(f"[Warning] {side.name}: neighbour frames of a size other than {shape} are skipped")
-                depths = np.stack([f if o else np.zeros(shape, np.float32) for f, o in zip(win, ok)])
-                conf, valid = confidence_maps(depths, K[lo:hi], T_cw[lo:hi], T_inv[lo:hi], a - lo, b - lo, r,
-                                              config.depth_max, config.error_threshold, ok,
-                                              device=getattr(config, "device", 0))
+                ok = np.array([f is not None for f in win])
+                try:
+                    conf, valid = confidence_maps(_canvas_stack(win), K[lo:hi], T_cw[lo:hi], T_inv[lo:hi], a - lo,
+                                                  b - lo, r, config.depth_max, config.error_threshold, ok,
+                                                  device=getattr(config, "device", 0))
+                except Exception as e:  # noqa: BLE001 -- every reference frame of the run failed
+                    for i in refs:
+                        _report(side, i, dataset.timestamps[i], e)
+                    continue
                 for i in refs:
-                    writes.append(pool.submit(depth_data_io.save_confidence_map, side=side,
-                                              timestamp=dataset.timestamps[i],
-                                              confidence_map=ConfidenceMap(conf[i - a], valid[i - a])))
+                    h, w = frame(i).shape
+                    cm = ConfidenceMap(np.ascontiguousarray(conf[i - a, :h, :w]),
+                                       np.ascontiguousarray(valid[i - a, :h, :w]))
+                    writes.append((i, pool.submit(depth_data_io.save_confidence_map, side=side,
+                                                  timestamp=dataset.timestamps[i], confidence_map=cm)))
                 if len(writes) > 2 * REF_CHUNK:  # bound the maps held for writing
-                    for w in writes[:-REF_CHUNK]:
-                        w.result()
-                    writes = writes[-REF_CHUNK:]
-                j = k
-        for w in writes:  # raises the first write error, as the sequential loop would
-            w.result()
+                    settle(REF_CHUNK)
+        settle(0)

@@ -221,6 +221,14 @@ class RcclComm:
         _lib.call("mqr_comm_unique_id", buf)
         return bytes(buf)
 
+    def timing(self) -> dict:
+        """Phases of the last merge (ms, HIP events on the merge stream)."""
+        import ctypes
+        from . import _lib
+        ms = (ctypes.c_float * 4)()
+        _lib.call("mqr_comm_timing", self._h, ms)
+        return {"plan_ms": ms[0], "out_and_gather_ms": ms[1], "exchange_ms": ms[2], "merge_kernels_ms": ms[3]}
+
     def close(self):
         from . import _lib
         if getattr(self, "_h", None) is not None and self._h.value and _lib._lib is not None:
@@ -261,8 +269,9 @@ def merge_rccl(vbg, comm: RcclComm, mode: str = "sharded", root: int = 0, out=No
 
 
 def merge_local(vbgs, mode: str = "sharded", root: int = 0, outs=None):
-    """The merge of several volumes of one process (same plan and kernels, device copies instead
-    of RCCL).  Returns [(out volume, owned block count)] per input."""
+    """The merge of several volumes of one process on one device (the same device plan and merge
+    arithmetic; each destination reads the sources' pools directly instead of receiving over RCCL).
+    Returns [(out volume, owned block count)] per input; outputs must not alias inputs."""
     import ctypes
     from . import _lib
     n = len(vbgs)

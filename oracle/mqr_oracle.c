@@ -102,7 +102,8 @@ static int h_grow(orc_vbg* v) {
     return 0;
 }
 
-/* Activate: return the buffer index of key, allocating a zero-initialised block if new. */
+/* Activate: return the buffer index of key, allocating a zero-initialised block if new (with
+ * `created` given, the caller zeroes the new block itself: orc_integrate does it in parallel). */
 static int64_t activate(orc_vbg* v, int32_t x, int32_t y, int32_t z, int* created) {
     uint64_t k = pack_key(x, y, z);
     int64_t idx = h_find(v, k);
@@ -126,8 +127,10 @@ static int64_t activate(orc_vbg* v, int32_t x, int32_t y, int32_t z, int* create
     v->keys[3 * idx + 0] = x;
     v->keys[3 * idx + 1] = y;
     v->keys[3 * idx + 2] = z;
-    memset(v->tsdf + idx * v->R3, 0, sizeof(float) * v->R3);
-    memset(v->weight + idx * v->R3, 0, sizeof(float) * v->R3);
+    if (!created) {
+        memset(v->tsdf + idx * v->R3, 0, sizeof(float) * v->R3);
+        memset(v->weight + idx * v->R3, 0, sizeof(float) * v->R3);
+    }
     h_insert_raw(v->hkeys, v->hvals, v->hcap, k, idx);
     if (created) *created = 1;
     return idx;
@@ -282,10 +285,14 @@ int orc_touch(const float* depth, int H, int W, const double* K, const double* T
 int orc_integrate(orc_vbg* v, const int32_t* keys, int64_t n, const float* depth, int H, int W, const double* K,
                   const double* T, float depth_scale, float depth_max, float trunc_mult) {
     int64_t* idx = (int64_t*)malloc(sizeof(int64_t) * (n > 0 ? n : 1));
+    uint8_t* fresh = (uint8_t*)malloc(n > 0 ? n : 1);
     for (int64_t b = 0; b < n; ++b) {
-        idx[b] = activate(v, keys[3 * b], keys[3 * b + 1], keys[3 * b + 2], NULL);
+        int created = 0;
+        idx[b] = activate(v, keys[3 * b], keys[3 * b + 1], keys[3 * b + 2], &created);
+        fresh[b] = (uint8_t)created;
         if (idx[b] < 0) {
             free(idx);
+            free(fresh);
             return 2;
         }
     }
@@ -295,35 +302,44 @@ int orc_integrate(orc_vbg* v, const int32_t* keys, int64_t n, const float* depth
     const int64_t R3 = v->R3;
     const float sdf_trunc = v->voxel_size * trunc_mult;
     const float hm1 = (float)H - 1.0f, wm1 = (float)W - 1.0f;
-    /* Duplicate keys in one call would update a block twice; the reference passes unique keys. */
-#pragma omp parallel for schedule(static)
+    /* Duplicate keys in one call would update a block twice; the reference passes unique keys.
+     * Voxel loops nested z, y, x (linear index (z R + y) R + x): the per-voxel arithmetic is the
+     * upstream kernel's, evaluated in the same order; only the index decode is hoisted. */
+#pragma omp parallel for schedule(dynamic, 8)
     for (int64_t b = 0; b < n; ++b) {
         int64_t bi = idx[b];
         int32_t xb = keys[3 * b], yb = keys[3 * b + 1], zb = keys[3 * b + 2];
         float* tsdf = v->tsdf + bi * R3;
         float* wgt = v->weight + bi * R3;
-        for (int64_t vi = 0; vi < R3; ++vi) {
-            int xv = (int)(vi % R), yv = (int)((vi / R) % R), zv = (int)(vi / (R * R));
-            int32_t x = xb * R + xv, y = yb * R + yv, z = zb * R + zv;
-            float xc, yc, zc;
-            ti_rigid(&ti, (float)x, (float)y, (float)z, &xc, &yc, &zc);
-            float inv_z = 1.0f / zc;
-            float u = ti.fx * xc * inv_z + ti.cx;
-            float vv = ti.fy * yc * inv_z + ti.cy;
-            if (!(vv >= 0 && u >= 0 && vv <= hm1 && u <= wm1)) continue;
-            int ui = (int)u, vi2 = (int)vv;
-            float d = depth[(int64_t)vi2 * W + ui] / depth_scale;
-            float sdf = d - zc;
-            if (d <= 0 || d > depth_max || zc <= 0 || sdf < -sdf_trunc) continue;
-            sdf = sdf < sdf_trunc ? sdf : sdf_trunc;
-            sdf /= sdf_trunc;
-            float inv_wsum = 1.0f / (wgt[vi] + 1);
-            float w = wgt[vi];
-            tsdf[vi] = (w * tsdf[vi] + sdf) * inv_wsum;
-            wgt[vi] = w + 1;
+        if (fresh[b]) { /* new blocks start at zero (App. A.1) */
+            memset(tsdf, 0, sizeof(float) * R3);
+            memset(wgt, 0, sizeof(float) * R3);
         }
+        int64_t vi = 0;
+        for (int zv = 0; zv < R; ++zv)
+            for (int yv = 0; yv < R; ++yv)
+                for (int xv = 0; xv < R; ++xv, ++vi) {
+                    int32_t x = xb * R + xv, y = yb * R + yv, z = zb * R + zv;
+                    float xc, yc, zc;
+                    ti_rigid(&ti, (float)x, (float)y, (float)z, &xc, &yc, &zc);
+                    float inv_z = 1.0f / zc;
+                    float u = ti.fx * xc * inv_z + ti.cx;
+                    float vv = ti.fy * yc * inv_z + ti.cy;
+                    if (!(vv >= 0 && u >= 0 && vv <= hm1 && u <= wm1)) continue;
+                    int ui = (int)u, vi2 = (int)vv;
+                    float d = depth[(int64_t)vi2 * W + ui] / depth_scale;
+                    float sdf = d - zc;
+                    if (d <= 0 || d > depth_max || zc <= 0 || sdf < -sdf_trunc) continue;
+                    sdf = sdf < sdf_trunc ? sdf : sdf_trunc;
+                    sdf /= sdf_trunc;
+                    float inv_wsum = 1.0f / (wgt[vi] + 1);
+                    float w = wgt[vi];
+                    tsdf[vi] = (w * tsdf[vi] + sdf) * inv_wsum;
+                    wgt[vi] = w + 1;
+                }
     }
     free(idx);
+    free(fresh);
     return 0;
 }
 
@@ -349,6 +365,7 @@ int orc_import(orc_vbg* v, const int32_t* keys, const float* tsdf, const float* 
 /* 27-neighbour block table for the active blocks: nb[b*27 + k] = buffer index or -1. */
 static int64_t* build_nb(const orc_vbg* v) {
     int64_t* nb = (int64_t*)malloc(sizeof(int64_t) * 27 * (v->n > 0 ? v->n : 1));
+#pragma omp parallel for schedule(static)
     for (int64_t b = 0; b < v->n; ++b)
         for (int k = 0; k < 27; ++k) {
             int dx = k % 3 - 1, dy = (k % 9) / 3 - 1, dz = k / 9 - 1;
@@ -387,34 +404,44 @@ static void normalize_into(float nx, float ny, float nz, float* out) {
     out[2] = nz / norm;
 }
 
-int64_t orc_extract_points(const orc_vbg* v, float thr, float** pos_out, float** nrm_out) {
-    int64_t* nb = build_nb(v);
+/* Exclusive prefix sum of per-block counts (in place); returns the total. */
+static int64_t excl_scan(int64_t* c, int64_t n) {
+    int64_t acc = 0;
+    for (int64_t b = 0; b < n; ++b) {
+        int64_t t = c[b];
+        c[b] = acc;
+        acc += t;
+    }
+    return acc;
+}
+
+/* Points of block b (upstream ExtractPointCloud, per voxel, axes x, y, z).  With pos == NULL only
+ * counts.  Output order = block order, voxel order, axis: the sequential loop's order; the
+ * parallel extraction counts per block, scans, then fills. */
+static int64_t points_of_block(const orc_vbg* v, const int64_t* nb, int64_t b, float thr, float* pos, float* nrm) {
     const int R = v->R;
     const int64_t R3 = v->R3;
-    int64_t cap = 1024, cnt = 0;
-    float* pos = (float*)malloc(sizeof(float) * 3 * cap);
-    float* nrm = (float*)malloc(sizeof(float) * 3 * cap);
-    for (int64_t b = 0; b < v->n; ++b) {
-        int32_t xb = v->keys[3 * b], yb = v->keys[3 * b + 1], zb = v->keys[3 * b + 2];
-        for (int64_t vi = 0; vi < R3; ++vi) {
-            int xv = (int)(vi % R), yv = (int)((vi / R) % R), zv = (int)(vi / (R * R));
-            int64_t li = b * R3 + vi;
-            float tsdf_o = v->tsdf[li], weight_o = v->weight[li];
-            if (weight_o <= thr) continue;
-            int32_t x = xb * R + xv, y = yb * R + yv, z = zb * R + zv;
-            float no[3] = {0, 0, 0}, ni[3] = {0, 0, 0};
-            get_normal(v, nb, b, xv, yv, zv, no);
-            for (int i = 0; i < 3; ++i) {
-                int64_t lii = lin_idx(v, nb, b, xv + (i == 0), yv + (i == 1), zv + (i == 2));
-                if (lii < 0) continue;
-                float tsdf_i = v->tsdf[lii], weight_i = v->weight[lii];
-                if (weight_i > thr && tsdf_i * tsdf_o < 0) {
-                    float ratio = (0 - tsdf_o) / (tsdf_i - tsdf_o);
-                    if (cnt == cap) {
-                        cap *= 2;
-                        pos = (float*)realloc(pos, sizeof(float) * 3 * cap);
-                        nrm = (float*)realloc(nrm, sizeof(float) * 3 * cap);
+    int64_t cnt = 0;
+    int32_t xb = v->keys[3 * b], yb = v->keys[3 * b + 1], zb = v->keys[3 * b + 2];
+    for (int64_t vi = 0; vi < R3; ++vi) {
+        int xv = (int)(vi % R), yv = (int)((vi / R) % R), zv = (int)(vi / (R * R));
+        int64_t li = b * R3 + vi;
+        float tsdf_o = v->tsdf[li], weight_o = v->weight[li];
+        if (weight_o <= thr) continue;
+        int32_t x = xb * R + xv, y = yb * R + yv, z = zb * R + zv;
+        float no[3] = {0, 0, 0}, ni[3] = {0, 0, 0};
+        int have_no = 0;
+        for (int i = 0; i < 3; ++i) {
+            int64_t lii = lin_idx(v, nb, b, xv + (i == 0), yv + (i == 1), zv + (i == 2));
+            if (lii < 0) continue;
+            float tsdf_i = v->tsdf[lii], weight_i = v->weight[lii];
+            if (weight_i > thr && tsdf_i * tsdf_o < 0) {
+                if (pos) {
+                    if (!have_no) {
+                        get_normal(v, nb, b, xv, yv, zv, no);
+                        have_no = 1;
                     }
+                    float ratio = (0 - tsdf_o) / (tsdf_i - tsdf_o);
                     pos[3 * cnt + 0] = v->voxel_size * (x + ratio * (int)(i == 0));
                     pos[3 * cnt + 1] = v->voxel_size * (y + ratio * (int)(i == 1));
                     pos[3 * cnt + 2] = v->voxel_size * (z + ratio * (int)(i == 2));
@@ -423,11 +450,26 @@ int64_t orc_extract_points(const orc_vbg* v, float thr, float** pos_out, float**
                     float ny = (1 - ratio) * no[1] + ratio * ni[1];
                     float nz = (1 - ratio) * no[2] + ratio * ni[2];
                     normalize_into(nx, ny, nz, nrm + 3 * cnt);
-                    ++cnt;
                 }
+                ++cnt;
             }
         }
     }
+    return cnt;
+}
+
+int64_t orc_extract_points(const orc_vbg* v, float thr, float** pos_out, float** nrm_out) {
+    int64_t* nb = build_nb(v);
+    const int64_t nblk = v->n;
+    int64_t* off = (int64_t*)malloc(sizeof(int64_t) * (nblk > 0 ? nblk : 1));
+#pragma omp parallel for schedule(dynamic, 16)
+    for (int64_t b = 0; b < nblk; ++b) off[b] = points_of_block(v, nb, b, thr, NULL, NULL);
+    const int64_t cnt = excl_scan(off, nblk);
+    float* pos = (float*)malloc(sizeof(float) * 3 * (cnt > 0 ? cnt : 1));
+    float* nrm = (float*)malloc(sizeof(float) * 3 * (cnt > 0 ? cnt : 1));
+#pragma omp parallel for schedule(dynamic, 16)
+    for (int64_t b = 0; b < nblk; ++b) points_of_block(v, nb, b, thr, pos + 3 * off[b], nrm + 3 * off[b]);
+    free(off);
     free(nb);
     *pos_out = pos;
     *nrm_out = nrm;
@@ -441,7 +483,9 @@ int64_t orc_extract_mesh(const orc_vbg* v, float thr, float** vtx_out, float** n
     const int64_t R3 = v->R3, nblk = v->n;
     /* mesh structure: per voxel {vertex idx on +x, +y, +z edge, table index} */
     int32_t* ms = (int32_t*)calloc((size_t)(nblk > 0 ? nblk : 1) * R3 * 4, sizeof(int32_t));
-    /* pass 0: cube classification and edge marking */
+    /* pass 0: cube classification and edge marking (an edge may belong to a neighbour block's
+     * voxel: every writer stores the same -1) */
+#pragma omp parallel for schedule(dynamic, 16)
     for (int64_t b = 0; b < nblk; ++b)
         for (int64_t vi = 0; vi < R3; ++vi) {
             int xv = (int)(vi % R), yv = (int)((vi / R) % R), zv = (int)(vi / (R * R));
@@ -471,14 +515,27 @@ int64_t orc_extract_mesh(const orc_vbg* v, float thr, float** vtx_out, float** n
                 int64_t bi = nb[b * 27 + k];
                 /* inverse index == buffer index here (blocks are enumerated in buffer order) */
                 int64_t vi2 = ((int64_t)(zi - dzb * R) * R + (yi - dyb * R)) * R + (xi - dxb * R);
+#pragma omp atomic write
                 ms[(bi * R3 + vi2) * 4 + mqr_edge_shifts[i][3]] = -1;
             }
         }
-    /* pass 1+2: vertices */
-    int64_t vcap = 1024, vcnt = 0;
-    float* vtx = (float*)malloc(sizeof(float) * 3 * vcap);
-    float* nrm = (float*)malloc(sizeof(float) * 3 * vcap);
+    /* pass 1+2: vertices, numbered in block / voxel / edge order (count, scan, fill) */
+    int64_t* off = (int64_t*)malloc(sizeof(int64_t) * (nblk > 0 ? nblk : 1));
+#pragma omp parallel for schedule(static)
     for (int64_t b = 0; b < nblk; ++b) {
+        int64_t c = 0;
+        for (int64_t vi = 0; vi < R3; ++vi) {
+            const int32_t* m = ms + (b * R3 + vi) * 4;
+            c += (m[0] == -1) + (m[1] == -1) + (m[2] == -1);
+        }
+        off[b] = c;
+    }
+    const int64_t vcnt = excl_scan(off, nblk);
+    float* vtx = (float*)malloc(sizeof(float) * 3 * (vcnt > 0 ? vcnt : 1));
+    float* nrm = (float*)malloc(sizeof(float) * 3 * (vcnt > 0 ? vcnt : 1));
+#pragma omp parallel for schedule(dynamic, 16)
+    for (int64_t b = 0; b < nblk; ++b) {
+        int64_t vc = off[b];
         int32_t xb = v->keys[3 * b], yb = v->keys[3 * b + 1], zb = v->keys[3 * b + 2];
         for (int64_t vi = 0; vi < R3; ++vi) {
             int32_t* m = ms + (b * R3 + vi) * 4;
@@ -493,39 +550,38 @@ int64_t orc_extract_mesh(const orc_vbg* v, float thr, float** vtx_out, float** n
                 int64_t lie = lin_idx(v, nb, b, xv + (e == 0), yv + (e == 1), zv + (e == 2));
                 float tsdf_e = v->tsdf[lie];
                 float ratio = (0 - tsdf_o) / (tsdf_e - tsdf_o);
-                if (vcnt == vcap) {
-                    vcap *= 2;
-                    vtx = (float*)realloc(vtx, sizeof(float) * 3 * vcap);
-                    nrm = (float*)realloc(nrm, sizeof(float) * 3 * vcap);
-                }
-                m[e] = (int32_t)vcnt;
+                m[e] = (int32_t)vc;
                 float rx = ratio * (int)(e == 0), ry = ratio * (int)(e == 1), rz = ratio * (int)(e == 2);
-                vtx[3 * vcnt + 0] = v->voxel_size * (x + rx);
-                vtx[3 * vcnt + 1] = v->voxel_size * (y + ry);
-                vtx[3 * vcnt + 2] = v->voxel_size * (z + rz);
+                vtx[3 * vc + 0] = v->voxel_size * (x + rx);
+                vtx[3 * vc + 1] = v->voxel_size * (y + ry);
+                vtx[3 * vc + 2] = v->voxel_size * (z + rz);
                 get_normal(v, nb, b, xv + (e == 0), yv + (e == 1), zv + (e == 2), ne);
                 float nx = (1 - ratio) * no[0] + ratio * ne[0];
                 float ny = (1 - ratio) * no[1] + ratio * ne[1];
                 float nz = (1 - ratio) * no[2] + ratio * ne[2];
-                normalize_into(nx, ny, nz, nrm + 3 * vcnt);
-                ++vcnt;
+                normalize_into(nx, ny, nz, nrm + 3 * vc);
+                ++vc;
             }
         }
     }
-    /* pass 3: triangles (vertex order reversed, tri[2 - k]) */
-    int64_t tcap = 1024, tcnt = 0;
-    int32_t* tri = (int32_t*)malloc(sizeof(int32_t) * 3 * tcap);
-    for (int64_t b = 0; b < nblk; ++b)
+    /* pass 3: triangles (vertex order reversed, tri[2 - k]), block / voxel order */
+#pragma omp parallel for schedule(static)
+    for (int64_t b = 0; b < nblk; ++b) {
+        int64_t c = 0;
+        for (int64_t vi = 0; vi < R3; ++vi) c += mqr_tri_count[ms[(b * R3 + vi) * 4 + 3]];
+        off[b] = c;
+    }
+    const int64_t tcnt = excl_scan(off, nblk);
+    int32_t* tri = (int32_t*)malloc(sizeof(int32_t) * 3 * (tcnt > 0 ? tcnt : 1));
+#pragma omp parallel for schedule(dynamic, 16)
+    for (int64_t b = 0; b < nblk; ++b) {
+        int64_t tc = off[b];
         for (int64_t vi = 0; vi < R3; ++vi) {
             int table_idx = ms[(b * R3 + vi) * 4 + 3];
             if (mqr_tri_count[table_idx] == 0) continue;
             int xv = (int)(vi % R), yv = (int)((vi / R) % R), zv = (int)(vi / (R * R));
             for (int t = 0; t < 16; t += 3) {
                 if (mqr_tri_table[table_idx][t] == -1) break;
-                if (tcnt == tcap) {
-                    tcap *= 2;
-                    tri = (int32_t*)realloc(tri, sizeof(int32_t) * 3 * tcap);
-                }
                 for (int k = 0; k < 3; ++k) {
                     int edge = mqr_tri_table[table_idx][t + k];
                     int xi = xv + mqr_edge_shifts[edge][0], yi = yv + mqr_edge_shifts[edge][1],
@@ -534,11 +590,13 @@ int64_t orc_extract_mesh(const orc_vbg* v, float thr, float** vtx_out, float** n
                     int kk = (dxb + 1) + (dyb + 1) * 3 + (dzb + 1) * 9;
                     int64_t bi = nb[b * 27 + kk];
                     int64_t vi2 = ((int64_t)(zi - dzb * R) * R + (yi - dyb * R)) * R + (xi - dxb * R);
-                    tri[3 * tcnt + (2 - k)] = ms[(bi * R3 + vi2) * 4 + mqr_edge_shifts[edge][3]];
+                    tri[3 * tc + (2 - k)] = ms[(bi * R3 + vi2) * 4 + mqr_edge_shifts[edge][3]];
                 }
-                ++tcnt;
+                ++tc;
             }
         }
+    }
+    free(off);
     free(ms);
     free(nb);
     *vtx_out = vtx;
@@ -700,7 +758,7 @@ int orc_raycast(const float* V, int64_t nv, const int32_t* T, int64_t nt, const 
  * Float64 projection Vt = T [X 1], u = float(Vt.x fx / Vt.z + cx), v likewise, d = float(Vt.z);
  * visible iff d >= 0, (round u, round v) in the image, depth there <= max_depth and
  * |d - depth| < thr; sampled iff also margin <= u < W - margin, margin <= v < H - margin;
- * colour = mean of rgb / 255 over sampled keyframes (float64 sums in keyframe order), 0 if none.
+ * colour = mean of (float)rgb / 255.0f over sampled keyframes (float64 sums in keyframe order), 0 if none.
  * The depth-discontinuity mask and the knn fill of unseen vertices are not restated. */
 int orc_color_vertices(const float* V, int64_t nv, const uint8_t* images, const float* depths, int N, int H, int W,
                        const double* K, const double* T, double max_depth, double thr, int margin, float* out,
@@ -727,9 +785,9 @@ int orc_color_vertices(const float* V, int64_t nv, const uint8_t* images, const 
             if (!((double)fabsf(d - ds) < thr)) continue;
             if (!(u >= margin && u < W - margin && v >= margin && v < H - margin)) continue;
             const uint8_t* p = images + 3 * px;
-            sr += p[0] / 255.0;
-            sg += p[1] / 255.0;
-            sb += p[2] / 255.0;
+            sr += (double)((float)p[0] / 255.0f);
+            sg += (double)((float)p[1] / 255.0f);
+            sb += (double)((float)p[2] / 255.0f);
             ++cnt;
         }
         out[3 * i] = cnt ? (float)(sr / cnt) : 0.f;

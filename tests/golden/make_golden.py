@@ -1,6 +1,6 @@
 """Generate the golden fixtures in tests/golden/ by running the REFERENCE's own Python code.
 
-Run here (this container) only:  python tests/golden/make_golden.py [decode]
+Run here (this container) only:  python tests/golden/make_golden.py [decode | ragged]
 It imports /root/reference/scripts (read-only) with ``open3d`` and ``cv2`` stubbed by
 MagicMock (neither is installed; the functions exercised never touch them), feeds it synthetic
 captures, and stores inputs + reference outputs as .npz data.  Nothing from the reference is
@@ -16,6 +16,8 @@ Fixtures:
                          build_confidence_map (estimate_depth_confidences.py:15-79) for every ref frame
                          under two parameter sets (_conf_a/_valid_a, _conf_b/_valid_b) and
                          compute_pixel_error_map (compute_pixel_error_map.py:120-220) for frame pairs
+  confidence_ragged_golden.npz  a capture with frames of two sizes (per-row width / height in the
+                         descriptor CSV), build_confidence_map for every ref frame, two parameter sets
 """
 from __future__ import annotations
 
@@ -127,10 +129,66 @@ def make_dataset_and_confidence(ref):
     np.savez_compressed(HERE / "confidence_golden.npz", **out)
 
 
+def make_ragged_confidence(ref):
+    """confidence_ragged_golden.npz: one capture whose frames have two sizes (the descriptor CSV
+    gives each frame's width / height, depth_data_io.py:187-188) along one room walk; the
+    reference's build_confidence_map for every reference frame (windows mixing both sizes: its
+    bilinear_interpolate_depth bounds-checks against the target's own h, w).  Per-frame arrays are
+    stored under indexed keys (raw_<i>, conf_<tag>_<i>, valid_<tag>_<i>)."""
+    sys.path.insert(0, str(REPO / "metaquest-3d-reconstruction_amd"))
+    import pandas as pd
+    from mqr import synthetic
+    poses = synthetic.room_loop_poses(40)[::3][:12]
+    parts = [(0, 5, 120, 160, 131.25), (5, 9, 96, 128, 105.0), (9, 12, 120, 160, 131.25)]
+    out = {}
+    with tempfile.TemporaryDirectory() as td:
+        td = Path(td)
+        (td / "left_depth").mkdir()
+        rows = []
+        raws = []
+        for k, (a, b, h, w, f) in enumerate(parts):
+            seq = synthetic.make_sequence("room", poses=poses[a:b], height=h, width=w, f=f, noise=True, seed=30 + k)
+            sub = td / f"part{k}"
+            synthetic.write_capture(sub, seq, t0=1_000_000 + 33 * a)
+            rows.append(pd.read_csv(sub / "left_depth_descriptors.csv"))
+            for raw in sorted((sub / "left_depth").glob("*.raw")):
+                raw.rename(td / "left_depth" / raw.name)
+            raws.extend(seq["raw"])
+        csv = pd.concat(rows)
+        csv.to_csv(td / "left_depth_descriptors.csv", index=False)
+        io, ds, K, T_cw, T_wc, T_cw_inv, _ = capture_to_reference_ragged(ref, td)
+        out["descriptor"] = csv.to_numpy(dtype=np.float64)
+        out["descriptor_cols"] = np.array(list(csv.columns))
+        out["n"] = np.array(len(ds))
+        out["K"], out["T_cw"], out["T_cw_inv"] = K, T_cw, T_cw_inv
+        for i, r in enumerate(raws):
+            out[f"raw_{i}"] = r
+        for tag, (r, dmax, thr) in {"a": (3, 3.0, 0.05), "b": (10, 4.0, 0.08)}.items():
+            for i in range(len(ds)):
+                cm = ref["build_confidence_map"](io, ds, K, T_cw, T_cw_inv, ref["Side"].LEFT, i, target_frame_range=r,
+                                                 depth_max=dmax, error_threshold=thr)
+                out[f"conf_{tag}_{i}"] = cm.confidence_map
+                out[f"valid_{tag}_{i}"] = cm.valid_count
+    np.savez_compressed(HERE / "confidence_ragged_golden.npz", **out)
+
+
+def capture_to_reference_ragged(ref, project_dir):
+    io = ref["DepthDataIO"](depth_path_config=ref["DepthPathConfig"](project_dir=Path(project_dir)))
+    ds = io.build_depth_dataset(side=ref["Side"].LEFT)
+    K = ref["compute_o3d_intrinsic_matrices"](dataset=ds)
+    o3d = ds.transforms.convert_coordinate_system(target_coordinate_system=ref["CoordinateSystem"].OPEN3D,
+                                                  is_camera=True)
+    return io, ds, K, o3d.extrinsics_cw, o3d.extrinsics_wc, np.linalg.inv(o3d.extrinsics_cw), None
+
+
 if __name__ == "__main__":
     ref = import_reference()
-    make_decode(ref)
-    if "decode" not in sys.argv[1:]:
-        make_dataset_and_confidence(ref)
+    if "ragged" in sys.argv[1:]:
+        make_ragged_confidence(ref)
+    else:
+        make_decode(ref)
+        if "decode" not in sys.argv[1:]:
+            make_dataset_and_confidence(ref)
+            make_ragged_confidence(ref)
     for f in sorted(HERE.glob("*.npz")):
         print(f.name, os.path.getsize(f))

@@ -108,3 +108,72 @@ def test_build_confidence_map_wrapper(capture):
         oc, ov = oracle.confidence(depth, K, Tcw, Ti, i, R_WIN, DMAX, ERR)
         assert np.array_equal(cm.valid_count, ov)
         assert np.array_equal(cm.confidence_map, oc)
+
+
+def _ragged_capture(tmp, g):
+    """The reference-generated ragged capture (two frame sizes) written back to disk."""
+    import pandas as pd
+    cols = [str(c) for c in g["descriptor_cols"]]
+    df = pd.DataFrame(g["descriptor"], columns=cols)
+    for c in ("timestamp_ms", "width", "height"):
+        df[c] = df[c].astype(np.int64)
+    (tmp / "left_depth").mkdir(parents=True)
+    for i, ts in enumerate(df["timestamp_ms"]):
+        g[f"raw_{i}"].astype("<f4").tofile(tmp / "left_depth" / f"{ts}.raw")
+    df.to_csv(tmp / "left_depth_descriptors.csv", index=False)
+
+
+@pytest.mark.parametrize("tag,params", [("a", (3, 3.0, 0.05)), ("b", (10, 4.0, 0.08))])
+def test_driver_mixed_frame_sizes_match_reference_golden(tmp_path, golden_dir, tag, params):
+    """Windows that mix two frame sizes: the reference interpolates each neighbour within its own
+    (h, w) (compute_pixel_error_map.py:4-60), so such a neighbour counts; the driver and the
+    build_confidence_map wrapper reproduce the reference's maps bit for bit
+    (tests/golden/confidence_ragged_golden.npz, generated by the reference itself)."""
+    import os
+    from mqr import _lib
+    from mqr.confidence import DepthConfidenceEstimationConfig, build_confidence_map, estimate_depth_confidences
+    from mqr.dataio import DepthDataIO
+    from mqr.models import Side
+    _lib.load()
+    g = np.load(os.path.join(golden_dir, "confidence_ragged_golden.npz"))
+    r, dmax, thr = params
+    _ragged_capture(tmp_path, g)
+    io = DepthDataIO(tmp_path)
+    estimate_depth_confidences(io, DepthConfidenceEstimationConfig(target_frame_range=r, depth_max=dmax,
+                                                                   error_threshold=thr,
+                                                                   skip_if_output_dir_exists=False),
+                               sides=[Side.LEFT])
+    ds = io.load_depth_dataset(Side.LEFT)
+    n = int(g["n"])
+    assert len(ds) == n and len(set(zip(ds.widths, ds.heights))) == 2
+    for i, ts in enumerate(ds.timestamps):
+        cm = io.load_confidence_map(Side.LEFT, int(ts))
+        assert cm is not None and cm.confidence_map.shape == g[f"conf_{tag}_{i}"].shape, i
+        assert np.array_equal(cm.valid_count, g[f"valid_{tag}_{i}"]), i
+        assert np.array_equal(cm.confidence_map, g[f"conf_{tag}_{i}"]), i
+    for i in (0, 5, 8, n - 1):
+        cm = build_confidence_map(io, ds, g["K"], g["T_cw"], g["T_cw_inv"], Side.LEFT, i, r, dmax, thr)
+        assert np.array_equal(cm.valid_count, g[f"valid_{tag}_{i}"]), i
+        assert np.array_equal(cm.confidence_map, g[f"conf_{tag}_{i}"]), i
+
+
+def test_driver_reports_a_failing_frame_and_goes_on(capture, capsys, monkeypatch):
+    """estimate_depth_confidences.py:98-117: an error while saving one reference frame's map is
+    printed with the reference's message and that frame is skipped; every other frame is written."""
+    from mqr.confidence import estimate_depth_confidences
+    path, seq, io, ds, Side = capture
+    bad = int(ds.timestamps[7])
+    orig = io.save_confidence_map
+
+    def flaky(side, timestamp, confidence_map):
+        if int(timestamp) == bad:
+            raise OSError("disk full")
+        return orig(side=side, timestamp=timestamp, confidence_map=confidence_map)
+
+    monkeypatch.setattr(io, "save_confidence_map", flaky)
+    estimate_depth_confidences(io, _config(skip=False), sides=[Side.LEFT])
+    out = capsys.readouterr().out
+    assert f"[Error] build_and_save_confidence_map failed for LEFT frame 7 (timestamp {bad}): disk full" in out
+    conf_dir = path / "left_depth_confidence"
+    assert len(list(conf_dir.glob("*.npz"))) == N - 1
+    assert io.load_confidence_map(Side.LEFT, bad) is None

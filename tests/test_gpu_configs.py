@@ -4,7 +4,15 @@ oracle on the same inputs:
 * C1: 32 x 640x480 procedural sphere, 2 cm voxels, R = 16, the 128^3 region (o3d_utils.py:153-238);
 * C2: 500 x 640x480 procedural room walk, 5 mm voxels, R = 16, trunc 10, depth_max 4 m;
 * C3: C2 + estimate_depth_confidences (r = 10, depth_max 4, err 0.08) -> mask (0.02 / 2) -> integrate
-  (estimate_depth_confidences.py:15-79, o3d_utils.py:109-150).
+  (estimate_depth_confidences.py:15-79, o3d_utils.py:109-150);
+* C4: 1000 LEFT + 1000 RIGHT frames (stereo baseline 0.064 m) chained into ONE volume, LEFT then
+  RIGHT as two integrate calls (reconstruct_scene.py:64-81, vbg_opt threaded through);
+* C5: 1000 + 1000 frames of the 8 x 8 x 3 m hall at 3 mm, 640x480, the volume grown from 4096
+  blocks to ~10^5 (multi-GB pool growth), mesh at 1.5 and point cloud at 3.0.
+
+Point clouds (extract_point_cloud, reconstruct_scene.py:90 / refine_fragment_poses.py:39, default
+weight_threshold 3.0) are compared at C2, C4 and C5 sizes.  Config-size meshes and point clouds are
+compared as exact multisets through 64-bit position hashes (gpu_helpers.compare_meshes_fast).
 
 Bar (north_star): identical touched-block sets and weights, |dtsdf| <= 1e-4 on w > 0 voxels
 (bit-exact in practice), identical marching-cubes vertex and triangle sets at the pipeline's mesh
@@ -15,7 +23,7 @@ import numpy as np
 import pytest
 
 import oracle
-from gpu_helpers import compare_meshes, compare_volumes
+from gpu_helpers import compare_meshes, compare_meshes_fast, compare_points_fast, compare_volumes
 
 pytestmark = pytest.mark.gpu
 
@@ -41,12 +49,35 @@ def _oracle_volume(depth, K, T, vs, R, dmax, tm, block_count=4096):
     return ref
 
 
-def _check_mesh(vbg, ref, thr):
+def _check_mesh(vbg, ref, thr, fast=False):
     mesh = vbg.extract_triangle_mesh(weight_threshold=thr)
     ov, _, ot = ref.extract_mesh(thr)
     assert len(ot) > 1000
-    compare_meshes(mesh.vertices, mesh.triangles, ov, ot, pos_tol=0.0)
+    if fast:
+        compare_meshes_fast(mesh.vertices, mesh.triangles, ov, ot)
+    else:
+        compare_meshes(mesh.vertices, mesh.triangles, ov, ot, pos_tol=0.0)
     return len(ot)
+
+
+def _check_points(vbg, ref, thr=3.0):
+    """extract_point_cloud() at the reference's default threshold (reconstruct_scene.py:90)."""
+    pcd = vbg.extract_point_cloud(weight_threshold=thr)
+    op, on = ref.extract_points(thr)
+    assert len(op) > 1000
+    compare_points_fast(pcd.points, pcd.normals, op, on, tol=1e-6)
+    return len(op)
+
+
+def _integrate_sides(vbg, ref, sides, vs, dmax=4.0, tm=10.0):
+    """reconstruct_scene.py:64-81: one integrate call per side into the same volume (vbg_opt),
+    LEFT first; the oracle runs the same frames one by one."""
+    for depth, K, T in sides:
+        vbg.integrate_frames(depth, K, T, depth_scale=1.0, depth_max=dmax, trunc_voxel_multiplier=tm)
+        K = np.asarray(K, np.float64)
+        T = np.asarray(T, np.float64)
+        for i in range(len(depth)):
+            ref.integrate_frame(depth[i], K[i], T[i], 1.0, dmax, tm)
 
 
 def test_c1_sphere_32_frames_2cm(vbg_mod):
@@ -74,17 +105,30 @@ def c2_seq(vbg_mod):
     return seq
 
 
-def test_c2_room_500_frames_5mm(vbg_mod, c2_seq):
+@pytest.fixture(scope="module")
+def c2_pair(vbg_mod, c2_seq):
     seq = c2_seq
     vbg = vbg_mod.VoxelBlockGrid(voxel_size=0.005, block_resolution=16, block_count=4096)  # grows
     vbg.integrate_frames(seq["depth"], seq["K"], seq["T_wc"], depth_scale=1.0, depth_max=4.0,
                          trunc_voxel_multiplier=10.0)
     ref = _oracle_volume(seq["depth"], seq["K"], seq["T_wc"], 0.005, 16, 4.0, 10.0, 8192)
+    return vbg, ref
+
+
+def test_c2_room_500_frames_5mm(c2_pair):
+    vbg, ref = c2_pair
     assert ref.size() > 5000
     assert compare_volumes(vbg.export(), ref.export(), TOL) == 0.0
     n15 = _check_mesh(vbg, ref, 1.5)
     n30 = _check_mesh(vbg, ref, 3.0)
     assert n15 >= n30 > 1_000_000
+
+
+def test_c2_point_cloud_threshold_3(c2_pair):
+    """extract_point_cloud() with its default weight_threshold 3.0 on the C2 volume: the file
+    reconstruct_scene.py:90-91 persists, and what the fragment path extracts."""
+    vbg, ref = c2_pair
+    assert _check_points(vbg, ref, 3.0) > 1_000_000
 
 
 def test_c2_room_320x320(vbg_mod):
@@ -176,7 +220,7 @@ def test_c5_structure_hall_3mm(vbg_mod):
     ref = _oracle_volume(seq["depth"], seq["K"], seq["T_wc"], 0.003, 16, 4.0, 10.0, 256)
     assert ref.size() > 4 * 256  # grew several times
     assert compare_volumes(vbg.export(), ref.export(), TOL) == 0.0
-    _check_mesh(vbg, ref, 1.5)
+    _check_mesh(vbg, ref, 1.5, fast=True)
     mesh = vbg.extract_triangle_mesh(weight_threshold=1.5)
     key = list(range(0, 48, 4))
     K = seq["K"][key].astype(np.float64)
@@ -191,3 +235,47 @@ def test_c5_structure_hall_3mm(vbg_mod):
     assert np.array_equal(gn, on) and np.array_equal(gc, oc)
     # colour max depth 2.5 m in an 8 x 8 m hall: only the near walls and floor are coloured
     assert (gn > 0).mean() > 0.02
+
+
+def _device_sides(seq, n_left):
+    """The generated (GPU) sequence split into its LEFT and RIGHT halves as host arrays."""
+    depth = seq.pop("depth_t").cpu().numpy()
+    K, T = seq["K"], seq["T_wc"]
+    return [(depth[:n_left], K[:n_left], T[:n_left]), (depth[n_left:], K[n_left:], T[n_left:])]
+
+
+def test_c4_left_right_2000_frames_chained(vbg_mod):
+    """C4 on one GPU: 1000 LEFT + 1000 RIGHT frames (0.064 m stereo baseline) of the room walk at
+    5 mm, chained into one volume LEFT then RIGHT (reconstruct_scene.py:64-81)."""
+    from mqr import synthetic
+    left = synthetic.room_loop_poses(1000)
+    right = [(R_, t_ + R_[:, 0] * 0.064) for R_, t_ in left]
+    seq = synthetic.make_sequence_fast("room", poses=left + right, height=480, width=640, seed=4, device="cuda:0")
+    sides = _device_sides(seq, 1000)
+    vbg = vbg_mod.VoxelBlockGrid(voxel_size=0.005, block_resolution=16, block_count=4096)
+    ref = oracle.OracleVBG(0.005, 16, 8192)
+    _integrate_sides(vbg, ref, sides, 0.005)
+    del sides
+    assert ref.size() > 6000
+    assert compare_volumes(vbg.export(), ref.export(), TOL) == 0.0
+    assert _check_mesh(vbg, ref, 1.5, fast=True) > 1_500_000
+    _check_points(vbg, ref, 3.0)
+
+
+def test_c5_hall_1000_plus_1000_3mm(vbg_mod):
+    """C5 at 1000 + 1000 frames of 640x480 through the 8 x 8 x 3 m hall at 3 mm voxels (R = 16),
+    LEFT then RIGHT into one volume grown from 4096 blocks; volume, mesh at 1.5 and point cloud at
+    3.0 against the oracle (the 4000-frame bench leg carries the same comparison)."""
+    from mqr import synthetic
+    left = synthetic.hall_loop_poses(1000)
+    right = [(R_, t_ + R_[:, 0] * 0.064) for R_, t_ in left]
+    seq = synthetic.make_sequence_fast("hall", poses=left + right, height=480, width=640, seed=5, device="cuda:0")
+    sides = _device_sides(seq, 1000)
+    vbg = vbg_mod.VoxelBlockGrid(voxel_size=0.003, block_resolution=16, block_count=4096)
+    ref = oracle.OracleVBG(0.003, 16, 4096)
+    _integrate_sides(vbg, ref, sides, 0.003)
+    del sides
+    assert ref.size() > 20 * 4096  # the pool grew many times over
+    assert compare_volumes(vbg.export(), ref.export(), TOL) == 0.0
+    assert _check_mesh(vbg, ref, 1.5, fast=True) > 10_000_000
+    _check_points(vbg, ref, 3.0)

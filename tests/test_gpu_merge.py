@@ -122,6 +122,13 @@ def test_rccl_world_one(seq):
         from mqr.distributed import extract_mesh_owned
         b = extract_mesh_owned(out2, n2, 1.5)
         compare_meshes(b.vertices, b.triangles, a.vertices, a.triangles)
+        ph = comm.timing()
+        assert all(v >= 0.0 for v in ph.values()), ph
+        # `out` aliasing `local` would empty the volume before it is sent: refused, volume intact
+        before = vol.export()
+        with pytest.raises(RuntimeError, match="different volume"):
+            merge_rccl(vol, comm, mode="root", out=vol)
+        assert compare_volumes(vol.export(), before, 0.0) == 0.0
     finally:
         comm.close()
 

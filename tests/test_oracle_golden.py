@@ -52,3 +52,29 @@ def test_oracle_confidence_skips_failed_frames(golden):
     with np.errstate(invalid="ignore", divide="ignore"):
         want = np.where(valid == 0, 0.0, cons / np.maximum(valid, 1))
     assert np.array_equal(c, want)
+
+
+@pytest.mark.parametrize("tag,params", [("a", (3, 3.0, 0.05)), ("b", (10, 4.0, 0.08))])
+def test_zero_canvas_reproduces_reference_on_mixed_frame_sizes(tmp_path, golden_dir, tag, params):
+    """The confidence driver stacks a window of differently sized frames on a zero canvas
+    (mqr.confidence._canvas_stack).  The oracle run on that canvas, cropped to the reference frame,
+    equals the reference's own build_confidence_map on the ragged capture bit for bit
+    (confidence_ragged_golden.npz; the reference interpolates each neighbour within its own h, w)."""
+    from test_gpu_confidence_driver import _ragged_capture
+    from mqr.confidence import _canvas_stack
+    from mqr.dataio import DepthDataIO
+    from mqr.models import Side
+    g = np.load(os.path.join(golden_dir, "confidence_ragged_golden.npz"))
+    r, dmax, thr = params
+    _ragged_capture(tmp_path, g)
+    io = DepthDataIO(tmp_path)
+    ds = io.build_depth_dataset(Side.LEFT)
+    n = int(g["n"])
+    frames = [io.load_depth_map_by_index(Side.LEFT, ds, i) for i in range(n)]
+    for i in range(n):
+        lo, hi = max(0, i - r), min(n, i + r + 1)
+        canvas = _canvas_stack(frames[lo:hi])
+        c, v = oracle.confidence(canvas, g["K"][lo:hi], g["T_cw"][lo:hi], g["T_cw_inv"][lo:hi], i - lo, r, dmax, thr)
+        h, w = frames[i].shape
+        assert np.array_equal(v[:h, :w], g[f"valid_{tag}_{i}"]), i
+        assert np.array_equal(c[:h, :w], g[f"conf_{tag}_{i}"]), i

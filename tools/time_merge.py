@@ -59,7 +59,8 @@ def main():
             out, owned = merge_rccl(vols[0], comm, mode=mode, out=out)
             torch.cuda.synchronize()
             ts.append(time.perf_counter() - t0)
-        res["rccl_world1_" + mode] = {"ms": sorted(ts[1:])[len(ts[1:]) // 2] * 1e3, "owned": owned}
+        res["rccl_world1_" + mode] = {"ms": sorted(ts[1:])[len(ts[1:]) // 2] * 1e3, "owned": owned,
+                                      "phases_ms": comm.timing()}
     comm.close()
     dist.destroy_process_group()
     print(json.dumps(res), flush=True)
