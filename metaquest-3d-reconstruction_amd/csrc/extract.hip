@@ -11,12 +11,16 @@
 //
 // GPU structure (no atomics on the output, deterministic order = (block, voxel, edge)):
 //   k_nb        27-neighbour buffer table per active block (hash lookups)
-//   k_*_count   one 256-thread workgroup per block: stage the (R+3)^3 tile [-1, R+1]^3 of
-//               (tsdf, flags) in LDS from up to 27 blocks, classify cubes, count vertices /
-//               triangles / points, block-local prefix by wave64 scan; the mesh pass also
-//               publishes the local vertex ids of the block's three low faces
-//   hipcub      exclusive scans of the per-block counts
-//   k_*_emit    re-stage the tile, write vertices + normals + triangles at their global offsets
+//   R = 8 / 16 (k_mc_*):
+//   k_mc_bits   the volume read once, coalesced: per block three bit planes (weight > thr,
+//               tsdf < 0, tsdf > 0) of R^2 rows
+//   k_mc_count  one workgroup per block: halo rows [-1, R]^3 rebuilt from the block's and its
+//               neighbours' bit planes, cube classification, vertex / triangle counts, per-row
+//               records (bases, owned edges / cubes) and sign rows for the emission pass
+//   k_scan_counts  exclusive scans of the per-block counts (one workgroup)
+//   k_mc_emit   blocks with output only: vertices with tsdf values gathered from the pool,
+//               triangles at their global offsets (latency: ~4 dependent load phases per block)
+//   other R: the byte-tile kernels (k_mesh_count / k_mesh_emit) stage (tsdf, flags) tiles.
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
@@ -32,6 +36,9 @@ namespace mqr {
 
 constexpr int kMaxR = 16;
 constexpr int kThreads = 512;  // 8 waves per workgroup: two LDS-resident blocks per CU keep 16 waves busy
+// The bit-row kernels (R = 8 / 16) are latency-bound chains of small dependent loads per block:
+// 256-thread workgroups (one per voxel row at R = 16) double the blocks in flight per CU.
+constexpr int kMcThreads = 256;
 
 __device__ inline int64_t dev_find(const Table t, uint64_t k) {
     const uint64_t m = (uint64_t)t.cap - 1;
@@ -436,20 +443,18 @@ __global__ __launch_bounds__(kThreads) void k_mesh_emit(const int32_t* __restric
 // per-voxel kernels above: SQ_LDS_IDX_ACTIVE ~ 80 % of k_mesh_count's time).  Vertices and
 // triangles are emitted by a balanced thread-per-output loop (binary search over the per-row
 // prefix), in the same (block, voxel, edge) / (block, cube, triangle) order as the kernels above.
-// HI = 1: tile [-1, R]^3 (classification only, count pass); HI = 2: [-1, R + 1]^3 (normals, emit pass).
+// HI = 1: tile [-1, R]^3 (classification; both passes -- the emit pass reads its tsdf values from the pool).
 template <int R, int HI>
 struct Mc {
     static constexpr int S = R + 1 + HI, S2 = S * S, C = R + 1, C2 = C * C, R2 = R * R, R3 = R * R * R;
     static constexpr int NH = 1 + HI;                  // halo columns x = -1 and x = R .. R + HI - 1
     static constexpr int RPW = 64 / R;                 // tile rows per wave-wide ballot
     static constexpr int NG = (S2 + RPW - 1) / RPW;    // ballot groups
-    static constexpr int NW = kThreads / 64;
-    static constexpr int NIT = (NG + NW - 1) / NW;     // ballot groups per wave
     static constexpr uint32_t RMASK = (1u << R) - 1;
     static constexpr uint32_t CMASK = (1u << C) - 1;
     static_assert(R == 8 || R == 16, "bit-row kernels: R = 8 or 16");
     static_assert(HI == 1 || HI == 2, "tile upper halo: 1 or 2");
-    static_assert(R2 <= kThreads, "one thread per voxel row");
+    static_assert(R2 <= kMcThreads, "one thread per voxel row");
     __device__ static int q(int y, int z) { return (z + 1) * S + (y + 1); }
     __device__ static int c(int y, int z) { return (z + 1) * C + (y + 1); }
     __device__ static int t(int x, int y, int z) { return q(y, z) * S + (x + 1); }
@@ -457,80 +462,87 @@ struct Mc {
     __device__ static int k27(int x, int y, int z) { return (blk(x) + 1) + 3 * (blk(y) + 1) + 9 * (blk(z) + 1); }
 };
 
-// Stage the bit rows (and, for the emit pass, the tsdf tile [-1, R+1]^3).  Columns x in [0, R) come
-// from row-contiguous loads combined by wave ballots; the halo columns x = -1, R, R+1 are loaded by
-// one thread per tile row.  All loads of a thread are issued before any LDS write.
-template <class M, bool TSDF>
-__device__ void mc_stage(const int32_t* __restrict__ nbrow, const float2* __restrict__ pool, float thr,
-                         uint32_t* rowV, uint32_t* rowN, float* tile) {
-    constexpr int R = M::C - 1;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    float2 h[3] = {make_float2(0.f, 0.f), make_float2(0.f, 0.f), make_float2(0.f, 0.f)};
-    uint32_t hp = 0;
-    if (tid < M::S2) {
-        const int ty = tid % M::S - 1, tz = tid / M::S - 1;
+// ---- bits pass: every voxel read once, fully coalesced -------------------------------------------
+// Per block three bit planes of R^2 rows of R bits (u16, row = z R + y, bit = x): weight > thr
+// (V), tsdf < 0 (N), tsdf > 0 (P).  NaN sets neither N nor P, like the upstream comparisons.  The
+// classification and emission passes rebuild their halo rows from these (~3 KB per block instead
+// of re-reading the (R+2)^3 neighbourhood of float2 voxels, 2.6x the volume over two passes).
+// The same launch also fills the block's row of the 27-neighbour table (hash lookups, k_nb).
+template <int R>
+__global__ __launch_bounds__(kMcThreads) void k_mc_bits(const float2* __restrict__ pool, float thr,
+                                                        uint16_t* __restrict__ bits, const uint64_t* __restrict__ bkeys,
+                                                        const Table t, int32_t* __restrict__ nb) {
+    constexpr int R2 = R * R, R3 = R2 * R, NIT = (R3 + kMcThreads - 1) / kMcThreads, RPB = 64 / R;
+    constexpr uint64_t RM = (1ull << R) - 1;
+    const int64_t b = blockIdx.x;
+    const float2* __restrict__ src = pool + b * R3;
+    const int tid = threadIdx.x, lane = tid & 63;
+    float2 v[NIT];
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {  // all loads in flight before the ballots
+        const int i = it * kMcThreads + tid;
+        v[it] = i < R3 ? src[i] : make_float2(0.f, 0.f);
+    }
+    if (tid < 27) {
+        int x, y, z;
+        unpack_key(bkeys[b], x, y, z);
+        x += tid % 3 - 1;
+        y += (tid % 9) / 3 - 1;
+        z += tid / 9 - 1;
+        int32_t r = -1;
+        if (key_in_range(x, y, z)) {
+            const int64_t sl = dev_find(t, pack_key(x, y, z));
+            if (sl >= 0) r = t.vals[sl];
+        }
+        nb[b * 27 + tid] = r;
+    }
+    uint16_t* __restrict__ out = bits + b * 3 * R2;
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+        const int i = it * kMcThreads + tid;
+        const bool in = i < R3;
+        const uint64_t mv = __ballot(in && v[it].y > thr);
+        const uint64_t mn = __ballot(in && v[it].x < 0.f);
+        const uint64_t mp = __ballot(in && v[it].x > 0.f);
+        const int i0 = i - lane;  // the wave's first voxel
+        if (lane < RPB && i0 + lane * R < R3) {
+            const int row = i0 / R + lane;
+            out[row] = (uint16_t)((mv >> (lane * R)) & RM);
+            out[R2 + row] = (uint16_t)((mn >> (lane * R)) & RM);
+            out[2 * R2 + row] = (uint16_t)((mp >> (lane * R)) & RM);
+        }
+    }
+}
+
+// Tile rows of the block's [-1, R + HI - 1] neighbourhood from the bit planes: bit (x + 1) of
+// rowV[q] / rowN[q] (/ rowP[q]) for tile row q = (z + 1) S + (y + 1); absent blocks give 0 bits.
+template <class M>
+__device__ void mc_stage_bits(const int32_t* __restrict__ nbrow, const uint16_t* __restrict__ bits, uint32_t* rowV,
+                              uint32_t* rowN, uint32_t* rowP) {
+    constexpr int R = M::C - 1, R2 = R * R;
+    for (int q = threadIdx.x; q < M::S2; q += blockDim.x) {
+        const int ty = q % M::S - 1, tz = q / M::S - 1;
         const int dy = M::blk(ty), dz = M::blk(tz);
+        const int row = (tz - dz * R) * R + (ty - dy * R);
+        const int k0 = 3 * (dy + 1) + 9 * (dz + 1);
+        const int32_t bm = nbrow[k0], bc = nbrow[k0 + 1], bp = nbrow[k0 + 2];
+        uint32_t w[3];
 #pragma unroll
-        for (int s = 0; s < M::NH; ++s) {
-            const int x = s == 0 ? -1 : R + s - 1, dx = s == 0 ? -1 : 1;
-            const int nbuf = nbrow[(dx + 1) + 3 * (dy + 1) + 9 * (dz + 1)];
-            if (nbuf >= 0) {
-                h[s] = pool[(int64_t)nbuf * M::R3 + ((tz - dz * R) * R + (ty - dy * R)) * R + (x - dx * R)];
-                hp |= 1u << s;
+        for (int a = 0; a < 3; ++a) {
+            if (a == 2 && !rowP) break;
+            uint32_t x = 0;
+            if (bc >= 0) x = (uint32_t)bits[((int64_t)bc * 3 + a) * R2 + row] << 1;
+            if (bm >= 0) x |= ((uint32_t)bits[((int64_t)bm * 3 + a) * R2 + row] >> (R - 1)) & 1u;
+            if (bp >= 0) {
+                const uint32_t pb = bits[((int64_t)bp * 3 + a) * R2 + row];
+#pragma unroll
+                for (int h = 0; h < M::NH - 1; ++h) x |= ((pb >> h) & 1u) << (R + 1 + h);
             }
+            w[a] = x;
         }
-    }
-    float2 mv[M::NIT];
-    uint32_t mp = 0;
-#pragma unroll
-    for (int it = 0; it < M::NIT; ++it) {
-        const int g = wave + it * M::NW;
-        const int qq = g * M::RPW + lane / R;
-        mv[it] = make_float2(0.f, 0.f);
-        if (g < M::NG && qq < M::S2) {
-            const int ty = qq % M::S - 1, tz = qq / M::S - 1;
-            const int dy = M::blk(ty), dz = M::blk(tz);
-            const int nbuf = nbrow[1 + 3 * (dy + 1) + 9 * (dz + 1)];
-            if (nbuf >= 0) {
-                mv[it] = pool[(int64_t)nbuf * M::R3 + ((tz - dz * R) * R + (ty - dy * R)) * R + lane % R];
-                mp |= 1u << it;
-            }
-        }
-    }
-#pragma unroll
-    for (int it = 0; it < M::NIT; ++it) {
-        const int g = wave + it * M::NW;
-        if (g >= M::NG) break;  // wave-uniform
-        const int qq = g * M::RPW + lane / R;
-        const bool p = (mp >> it) & 1u;
-        const uint64_t bv = __ballot(p && mv[it].y > thr);
-        const uint64_t bn = __ballot(p && mv[it].x < 0.f);
-        if (qq < M::S2) {
-            if (lane % R == 0) {
-                rowV[qq] = (uint32_t)((bv >> lane) & M::RMASK) << 1;
-                rowN[qq] = (uint32_t)((bn >> lane) & M::RMASK) << 1;
-            }
-            if (TSDF) tile[qq * M::S + lane % R + 1] = mv[it].x;
-        }
-    }
-    __syncthreads();
-    if (tid < M::S2) {
-        uint32_t v = 0, n = 0;
-#pragma unroll
-        for (int s = 0; s < M::NH; ++s) {
-            const int bit = s == 0 ? 0 : R + s;
-            if ((hp >> s) & 1u) {
-                v |= (uint32_t)(h[s].y > thr) << bit;
-                n |= (uint32_t)(h[s].x < 0.f) << bit;
-            }
-        }
-        rowV[tid] |= v;
-        rowN[tid] |= n;
-        if (TSDF) {
-            tile[tid * M::S] = h[0].x;
-#pragma unroll
-            for (int s = 1; s < M::NH; ++s) tile[tid * M::S + R + s] = h[s].x;
-        }
+        rowV[q] = w[0];
+        rowN[q] = w[1];
+        if (rowP) rowP[q] = w[2];
     }
     __syncthreads();
 }
@@ -591,12 +603,15 @@ __device__ inline int mc_row_tris(const uint32_t* rowN, uint32_t oc, int y, int 
     return n;
 }
 
-// Per-block counts + per-row vertex base and edge masks (rowinfo: {vbase | ez << 16, ex | ey << 16}),
-// which the emit pass of this block and of its -x / -y / -z neighbours read.
+// Per-block counts and, per voxel row, the record the emission pass works from:
+//   rows4[b][row] = {vertex base in the block, triangle base in the block, ex | ey << 16, ez | oc << 16}
+// (owned crossing edges and owned surface cubes of the row) and the sign rows rowNt[b][q] of the
+// block's [-1, R]^3 tile (cube indices).  Emission of this block and of its -x / -y / -z
+// neighbours (triangles referencing vertices this block owns) read these instead of rebuilding them.
 template <int R>
-__global__ __launch_bounds__(kThreads) void k_mc_count(const int32_t* __restrict__ nb, const float2* __restrict__ pool,
-                                                       float thr, int64_t tri_blocks, int32_t* vcount,
-                                                       int32_t* tcount, uint2* rowinfo) {
+__global__ __launch_bounds__(kMcThreads) void k_mc_count(const int32_t* __restrict__ nb, const uint16_t* __restrict__ bits,
+                                                         int64_t tri_blocks, int32_t* vcount, int32_t* tcount,
+                                                         uint4* __restrict__ rows4, uint32_t* __restrict__ rowNt) {
     using M = Mc<R, 1>;
     __shared__ uint32_t rowV[M::S2], rowN[M::S2], cs[M::C2];
     __shared__ int32_t nbrow[27];
@@ -604,7 +619,7 @@ __global__ __launch_bounds__(kThreads) void k_mc_count(const int32_t* __restrict
     const int64_t b = blockIdx.x;
     if (threadIdx.x < 27) nbrow[threadIdx.x] = nb[b * 27 + threadIdx.x];
     __syncthreads();
-    mc_stage<M, false>(nbrow, pool, thr, rowV, rowN, nullptr);
+    mc_stage_bits<M>(nbrow, bits, rowV, rowN, nullptr);
     mc_cubes<M>(rowV, rowN, cs);
     __syncthreads();
     const int r = threadIdx.x;
@@ -618,22 +633,37 @@ __global__ __launch_bounds__(kThreads) void k_mc_count(const int32_t* __restrict
     }
     int vtot, ttot;
     const int vb = block_exclusive_scan(nv, scratch, vtot);
-    block_exclusive_scan(nt, scratch + 8, ttot);
-    if (r < M::R2) rowinfo[b * M::R2 + r] = make_uint2((uint32_t)vb | (e.ez << 16), e.ex | (e.ey << 16));
+    const int tb = block_exclusive_scan(nt, scratch + 8, ttot);
+    if (r < M::R2) rows4[b * M::R2 + r] = make_uint4((uint32_t)vb, (uint32_t)tb, e.ex | (e.ey << 16), e.ez | (e.oc << 16));
+    for (int q = threadIdx.x; q < M::S2; q += blockDim.x) rowNt[b * M::S2 + q] = rowN[q];
     if (threadIdx.x == 0) {
         vcount[b] = vtot;
         tcount[b] = ttot;
     }
 }
 
+// tsdf of tile point (x, y, z) in [-1, R + 1]^3 (its block present), read from the pool.
+template <class M>
+__device__ inline float mc_tsdf(const int32_t* __restrict__ nbrow, const float2* __restrict__ pool, int x, int y,
+                                int z) {
+    constexpr int R = M::C - 1;
+    const int dx = M::blk(x), dy = M::blk(y), dz = M::blk(z);
+    const int32_t nbuf = nbrow[(dx + 1) + 3 * (dy + 1) + 9 * (dz + 1)];
+    return pool[(int64_t)nbuf * M::R3 + ((z - dz * R) * R + (y - dy * R)) * R + (x - dx * R)].x;
+}
+
 // Central-difference normal at tile point (x, y, z), components left untouched where a side's
 // block is absent (upstream DeviceGetNormal; presence is per block: bit k27 of pres).
 template <class M>
-__device__ inline void mc_normal(const float* tile, uint32_t pres, int x, int y, int z, float* n) {
+__device__ inline void mc_normal(const int32_t* __restrict__ nbrow, const float2* __restrict__ pool, uint32_t pres,
+                                 int x, int y, int z, float* n) {
     auto present = [&](int a, int b, int c) { return (pres >> M::k27(a, b, c)) & 1u; };
-    if (present(x + 1, y, z) && present(x - 1, y, z)) n[0] = tile[M::t(x + 1, y, z)] - tile[M::t(x - 1, y, z)];
-    if (present(x, y + 1, z) && present(x, y - 1, z)) n[1] = tile[M::t(x, y + 1, z)] - tile[M::t(x, y - 1, z)];
-    if (present(x, y, z + 1) && present(x, y, z - 1)) n[2] = tile[M::t(x, y, z + 1)] - tile[M::t(x, y, z - 1)];
+    if (present(x + 1, y, z) && present(x - 1, y, z))
+        n[0] = mc_tsdf<M>(nbrow, pool, x + 1, y, z) - mc_tsdf<M>(nbrow, pool, x - 1, y, z);
+    if (present(x, y + 1, z) && present(x, y - 1, z))
+        n[1] = mc_tsdf<M>(nbrow, pool, x, y + 1, z) - mc_tsdf<M>(nbrow, pool, x, y - 1, z);
+    if (present(x, y, z + 1) && present(x, y, z - 1))
+        n[2] = mc_tsdf<M>(nbrow, pool, x, y, z + 1) - mc_tsdf<M>(nbrow, pool, x, y, z - 1);
 }
 
 // Global vertex id of the edge owned by voxel (ox, oy, oz) (may lie in a +x/+y/+z neighbour) along axis.
@@ -643,54 +673,43 @@ __device__ inline int32_t mc_vid(uint32_t vbase, uint32_t ex, uint32_t ey, uint3
                      (axis > 0 ? (ex >> x) & 1u : 0u) + (axis > 1 ? (ey >> x) & 1u : 0u));
 }
 
+// Emission of a block with vertices or triangles, from the count pass's row records: vertices
+// (positions and normals from tsdf values gathered from the pool) and triangles at the offsets of
+// the scan, in (block, voxel, edge) / (block, cube, triangle) order.
 template <int R>
-__global__ __launch_bounds__(kThreads) void k_mc_emit(const int32_t* __restrict__ nb, const uint64_t* __restrict__ bkeys,
-                                                      const float2* __restrict__ pool, float voxel_size, float thr,
-                                                      int64_t tri_blocks, const int32_t* __restrict__ vcount,
-                                                      const int32_t* __restrict__ tcount,
-                                                      const int32_t* __restrict__ voff,
-                                                      const int32_t* __restrict__ toff,
-                                                      const uint2* __restrict__ rowinfo, float* pos, float* nrm,
-                                                      int32_t* tri) {
-    using M = Mc<R, 2>;
-    __shared__ float tile[M::S2 * M::S];
-    __shared__ uint32_t rowV[M::S2], rowN[M::S2], cs[M::C2];
+__global__ __launch_bounds__(kMcThreads) void k_mc_emit(const int32_t* __restrict__ nb, const uint64_t* __restrict__ bkeys,
+                                                        const float2* __restrict__ pool, float voxel_size,
+                                                        const int32_t* __restrict__ vcount,
+                                                        const int32_t* __restrict__ tcount,
+                                                        const int32_t* __restrict__ voff,
+                                                        const int32_t* __restrict__ toff,
+                                                        const uint4* __restrict__ rows4,
+                                                        const uint32_t* __restrict__ rowNt, float* pos, float* nrm,
+                                                        int32_t* tri) {
+    using M = Mc<R, 1>;
+    __shared__ uint32_t rowN[M::S2];
     __shared__ uint4 rows[M::R2];  // vbase, tbase, ex | ey << 16, ez | oc << 16
     __shared__ int32_t nbrow[27], nbvoff[27];
-    __shared__ int scratch[16];
     const int64_t b = blockIdx.x;
     const int nvb = vcount[b], ntb = tcount[b];
     if (nvb == 0 && ntb == 0) return;  // block-uniform: nothing to write
-    if (threadIdx.x < 27) {
-        const int32_t q = nb[b * 27 + threadIdx.x];
-        nbrow[threadIdx.x] = q;
-        nbvoff[threadIdx.x] = q >= 0 ? voff[q] : 0;
+    const int tid = threadIdx.x;
+    if (tid < 27) {
+        const int32_t q = nb[b * 27 + tid];
+        nbrow[tid] = q;
+        nbvoff[tid] = q >= 0 ? voff[q] : 0;
     }
+    for (int r = tid; r < M::R2; r += blockDim.x) rows[r] = rows4[b * M::R2 + r];
+    if (ntb)
+        for (int q = tid; q < M::S2; q += blockDim.x) rowN[q] = rowNt[b * M::S2 + q];
     __syncthreads();
-    const int lane = threadIdx.x & 63;
+    const int lane = tid & 63;
     const uint32_t pres = (uint32_t)__ballot(lane < 27 && nbrow[lane < 27 ? lane : 0] >= 0);
-    mc_stage<M, true>(nbrow, pool, thr, rowV, rowN, tile);
-    mc_cubes<M>(rowV, rowN, cs);
-    __syncthreads();
-    const int r = threadIdx.x;
-    RowEdges e{0, 0, 0, 0};
-    int nt = 0;
-    uint32_t vbase = 0;
-    if (r < M::R2) {
-        e = mc_row<M>(rowN, cs, r % R, r / R);
-        if (b >= tri_blocks) e.oc = 0;
-        nt = mc_row_tris<M>(rowN, e.oc, r % R, r / R);
-        vbase = rowinfo[b * M::R2 + r].x & 0xffffu;
-    }
-    int ttot;
-    const int tb = block_exclusive_scan(nt, scratch, ttot);
-    if (r < M::R2) rows[r] = make_uint4(vbase, (uint32_t)tb, e.ex | (e.ey << 16), e.ez | (e.oc << 16));
-    __syncthreads();
 
     int xb, yb, zb;
     unpack_key(bkeys[b], xb, yb, zb);
     const int32_t vb0 = voff[b], tb0 = toff[b];
-    for (int i = threadIdx.x; i < nvb; i += blockDim.x) {
+    for (int i = tid; i < nvb; i += blockDim.x) {
         int lo = 0, hi = M::R2 - 1;  // last row whose vertex base is <= i (non-empty)
         while (lo < hi) {
             const int mid = (lo + hi + 1) >> 1;
@@ -706,20 +725,19 @@ __global__ __launch_bounds__(kThreads) void k_mc_emit(const int32_t* __restrict_
         }
         const uint32_t m3 = ((ex >> x) & 1u) | (((ey >> x) & 1u) << 1) | (((ez >> x) & 1u) << 2);
         const int y = lo % R, z = lo / R;
-        const float tsdf_o = tile[M::t(x, y, z)];
+        const float tsdf_o = mc_tsdf<M>(nbrow, pool, x, y, z);
         float no[3] = {0.f, 0.f, 0.f}, ne[3] = {0.f, 0.f, 0.f};
-        mc_normal<M>(tile, pres, x, y, z, no);
+        mc_normal<M>(nbrow, pool, pres, x, y, z, no);
         // upstream keeps one per-voxel normal scratch across the voxel's edges: replay the earlier ones
         uint32_t mm = m3;
         int axis = 0;
         for (int j = 0;; ++j) {
             axis = __builtin_ctz(mm);
-            mc_normal<M>(tile, pres, x + (axis == 0), y + (axis == 1), z + (axis == 2), ne);
+            mc_normal<M>(nbrow, pool, pres, x + (axis == 0), y + (axis == 1), z + (axis == 2), ne);
             if (j == k) break;
             mm &= mm - 1;
         }
-        const int ex_ = x + (axis == 0), ey_ = y + (axis == 1), ez_ = z + (axis == 2);
-        const float tsdf_e = tile[M::t(ex_, ey_, ez_)];
+        const float tsdf_e = mc_tsdf<M>(nbrow, pool, x + (axis == 0), y + (axis == 1), z + (axis == 2));
         const float ratio = (0 - tsdf_o) / (tsdf_e - tsdf_o);
         const float rx = ratio * (int)(axis == 0), ry = ratio * (int)(axis == 1), rz = ratio * (int)(axis == 2);
         const int gx = xb * R + x, gy = yb * R + y, gz = zb * R + z;
@@ -732,7 +750,7 @@ __global__ __launch_bounds__(kThreads) void k_mc_emit(const int32_t* __restrict_
         const float nz = (1 - ratio) * no[2] + ratio * ne[2];
         write_normal(nx, ny, nz, nrm + 3 * id);
     }
-    for (int i = threadIdx.x; i < ntb; i += blockDim.x) {
+    for (int i = tid; i < ntb; i += blockDim.x) {
         int lo = 0, hi = M::R2 - 1;
         while (lo < hi) {
             const int mid = (lo + hi + 1) >> 1;
@@ -772,8 +790,8 @@ __global__ __launch_bounds__(kThreads) void k_mc_emit(const int32_t* __restrict_
                     vid = -1;  // cannot happen for a valid cube (all corners exist); stay in bounds
                 } else {
                     const int lx = ox - dx * R, ly = oy - dy * R, lz = oz - dz * R;
-                    const uint2 ri = rowinfo[(int64_t)nbuf * M::R2 + lz * R + ly];
-                    vid = nbvoff[k27] + mc_vid(ri.x & 0xffffu, ri.y & 0xffffu, ri.y >> 16, ri.x >> 16, lx, axis);
+                    const uint4 ow = rows4[(int64_t)nbuf * M::R2 + lz * R + ly];
+                    vid = nbvoff[k27] + mc_vid(ow.x, ow.z & 0xffffu, ow.z >> 16, ow.w & 0xffffu, lx, axis);
                 }
             }
             tri[3 * t + (2 - j)] = vid;
@@ -781,7 +799,120 @@ __global__ __launch_bounds__(kThreads) void k_mc_emit(const int32_t* __restrict_
     }
 }
 
-// ---------------------------------------------------------------- point cloud
+// ---------------------------------------------------------------- point cloud (R = 8 / 16)
+// Candidates from the bit planes: voxel o (weight > thr) and its +x / +y / +z neighbour q (weight >
+// thr, block present) with opposite strict signs; each candidate is then confirmed by upstream's own
+// test tsdf_o * tsdf_q < 0 on the two tsdf values (a product that underflows to -0 is not a point),
+// so the counts are exact.  Per row: {point base in the block, ex | ey << 16, ez}.
+template <int R>
+__global__ __launch_bounds__(kMcThreads) void k_pt_count(const int32_t* __restrict__ nb, const uint16_t* __restrict__ bits,
+                                                         const float2* __restrict__ pool, int32_t* __restrict__ count,
+                                                         uint4* __restrict__ rows4) {
+    using M = Mc<R, 1>;
+    __shared__ uint32_t rowV[M::S2], rowN[M::S2], rowP[M::S2];
+    __shared__ int32_t nbrow[27];
+    __shared__ int scratch[16];
+    const int64_t b = blockIdx.x;
+    if (threadIdx.x < 27) nbrow[threadIdx.x] = nb[b * 27 + threadIdx.x];
+    __syncthreads();
+    mc_stage_bits<M>(nbrow, bits, rowV, rowN, rowP);
+    const int r = threadIdx.x;
+    uint32_t m[3] = {0, 0, 0};
+    if (r < M::R2) {
+        const int y = r % R, z = r / R;
+        const int q0 = M::q(y, z);
+        const uint32_t v0 = rowV[q0], n0 = rowN[q0], p0 = rowP[q0];
+        const int qn[3] = {q0, M::q(y + 1, z), M::q(y, z + 1)};
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            // neighbour bits aligned onto the voxel's bit (x + 1): +x is the same row shifted right
+            const uint32_t va = a == 0 ? v0 >> 1 : rowV[qn[a]], na = a == 0 ? n0 >> 1 : rowN[qn[a]];
+            const uint32_t pa = a == 0 ? p0 >> 1 : rowP[qn[a]];
+            uint32_t c = ((v0 & va & ((n0 & pa) | (p0 & na))) >> 1) & M::RMASK;
+            uint32_t ok = 0;
+            while (c) {  // confirm with the product (few candidates per row)
+                const int x = __builtin_ctz(c);
+                c &= c - 1;
+                const float t_o = mc_tsdf<M>(nbrow, pool, x, y, z);
+                const float t_q = mc_tsdf<M>(nbrow, pool, x + (a == 0), y + (a == 1), z + (a == 2));
+                if (t_q * t_o < 0) ok |= 1u << x;
+            }
+            m[a] = ok;
+        }
+    }
+    const int np = __popc(m[0]) + __popc(m[1]) + __popc(m[2]);
+    int tot;
+    const int base = block_exclusive_scan(np, scratch, tot);
+    if (r < M::R2) rows4[b * M::R2 + r] = make_uint4((uint32_t)base, m[0] | (m[1] << 16), m[2], 0u);
+    if (threadIdx.x == 0) count[b] = tot;
+}
+
+// Points in (block, voxel, axis) order: position voxel_size (X + ratio e), normal interpolated
+// between the central-difference normals at o and q (the q-normal scratch carried across the
+// voxel's point axes, as upstream's per-voxel ni).
+template <int R>
+__global__ __launch_bounds__(kMcThreads) void k_pt_emit(const int32_t* __restrict__ nb, const uint64_t* __restrict__ bkeys,
+                                                        const float2* __restrict__ pool, float voxel_size,
+                                                        const int32_t* __restrict__ count,
+                                                        const int32_t* __restrict__ off,
+                                                        const uint4* __restrict__ rows4, float* pos, float* nrm) {
+    using M = Mc<R, 1>;
+    __shared__ uint4 rows[M::R2];
+    __shared__ int32_t nbrow[27];
+    const int64_t b = blockIdx.x;
+    const int npb = count[b];
+    if (npb == 0) return;  // block-uniform
+    const int tid = threadIdx.x;
+    if (tid < 27) nbrow[tid] = nb[b * 27 + tid];
+    for (int r = tid; r < M::R2; r += blockDim.x) rows[r] = rows4[b * M::R2 + r];
+    __syncthreads();
+    const int lane = tid & 63;
+    const uint32_t pres = (uint32_t)__ballot(lane < 27 && nbrow[lane < 27 ? lane : 0] >= 0);
+    int xb, yb, zb;
+    unpack_key(bkeys[b], xb, yb, zb);
+    const int64_t p0 = off[b];
+    for (int i = tid; i < npb; i += blockDim.x) {
+        int lo = 0, hi = M::R2 - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if ((int)rows[mid].x <= i) lo = mid; else hi = mid - 1;
+        }
+        const uint4 rw = rows[lo];
+        const uint32_t ex = rw.y & 0xffffu, ey = rw.y >> 16, ez = rw.z;
+        int k = i - (int)rw.x, x = 0;
+        for (; x < R; ++x) {
+            const int c = (int)(((ex >> x) & 1u) + ((ey >> x) & 1u) + ((ez >> x) & 1u));
+            if (k < c) break;
+            k -= c;
+        }
+        const uint32_t m3 = ((ex >> x) & 1u) | (((ey >> x) & 1u) << 1) | (((ez >> x) & 1u) << 2);
+        const int y = lo % R, z = lo / R;
+        const float t_o = mc_tsdf<M>(nbrow, pool, x, y, z);
+        float no[3] = {0.f, 0.f, 0.f}, ni[3] = {0.f, 0.f, 0.f};
+        mc_normal<M>(nbrow, pool, pres, x, y, z, no);
+        uint32_t mm = m3;
+        int axis = 0;
+        for (int j = 0;; ++j) {
+            axis = __builtin_ctz(mm);
+            mc_normal<M>(nbrow, pool, pres, x + (axis == 0), y + (axis == 1), z + (axis == 2), ni);
+            if (j == k) break;
+            mm &= mm - 1;
+        }
+        const float t_i = mc_tsdf<M>(nbrow, pool, x + (axis == 0), y + (axis == 1), z + (axis == 2));
+        const float ratio = (0 - t_o) / (t_i - t_o);
+        const int gx = xb * R + x, gy = yb * R + y, gz = zb * R + z;
+        const int64_t id = p0 + i;
+        pos[3 * id + 0] = voxel_size * (gx + ratio * (int)(axis == 0));
+        pos[3 * id + 1] = voxel_size * (gy + ratio * (int)(axis == 1));
+        pos[3 * id + 2] = voxel_size * (gz + ratio * (int)(axis == 2));
+        const float nx = (1 - ratio) * no[0] + ratio * ni[0];
+        const float ny = (1 - ratio) * no[1] + ratio * ni[1];
+        const float nz = (1 - ratio) * no[2] + ratio * ni[2];
+        write_normal(nx, ny, nz, nrm + 3 * id);
+    }
+}
+
+// ---------------------------------------------------------------- point cloud (other R: byte tiles)
 template <int RT>
 __device__ inline int point_mask(const Tile<RT>& tl, const Dims<RT>& d, int x, int y, int z) {
     const int o = d.tidx(x, y, z);
@@ -852,6 +983,60 @@ __global__ __launch_bounds__(kThreads) void k_points(const int32_t* __restrict__
     }
 }
 
+// Exclusive scans of the two per-block count arrays (vertices, triangles) in one workgroup of
+// kScanThreads; totals[0..1] = the sums.  (Two hipcub scans cost ~20 us of launches at these sizes.)
+constexpr int kScanThreads = 1024;
+__global__ __launch_bounds__(kScanThreads) void k_scan_counts(const int32_t* __restrict__ c0,
+                                                              const int32_t* __restrict__ c1, int64_t n,
+                                                              int32_t* __restrict__ o0, int32_t* __restrict__ o1,
+                                                              int64_t* __restrict__ totals) {
+    __shared__ int64_t ws0[kScanThreads / 64], ws1[kScanThreads / 64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t chunk = (n + kScanThreads - 1) / kScanThreads;
+    const int64_t lo = min(n, tid * chunk), hi = min(n, lo + chunk);
+    int64_t s0 = 0, s1 = 0;
+    for (int64_t i = lo; i < hi; ++i) {
+        s0 += c0[i];
+        if (c1) s1 += c1[i];
+    }
+    int64_t i0 = s0, i1 = s1;  // inclusive wave scans
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int64_t a = __shfl_up(i0, d, 64), b = __shfl_up(i1, d, 64);
+        if (lane >= d) {
+            i0 += a;
+            i1 += b;
+        }
+    }
+    if (lane == 63) {
+        ws0[wave] = i0;
+        ws1[wave] = i1;
+    }
+    __syncthreads();
+    int64_t b0 = 0, b1 = 0, t0 = 0, t1 = 0;
+    for (int w = 0; w < kScanThreads / 64; ++w) {
+        if (w < wave) {
+            b0 += ws0[w];
+            b1 += ws1[w];
+        }
+        t0 += ws0[w];
+        t1 += ws1[w];
+    }
+    int64_t r0 = b0 + i0 - s0, r1 = b1 + i1 - s1;  // exclusive prefix of this thread's chunk
+    for (int64_t i = lo; i < hi; ++i) {
+        o0[i] = (int32_t)r0;
+        r0 += c0[i];
+        if (c1) {
+            o1[i] = (int32_t)r1;
+            r1 += c1[i];
+        }
+    }
+    if (tid == 0) {
+        totals[0] = t0;
+        totals[1] = t1;
+    }
+}
+
 // ---------------------------------------------------------------- host side
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
@@ -859,6 +1044,7 @@ static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 struct ExScratch {
     int32_t *nb, *c0, *c1, *o0, *o1;
     uint32_t* faces;
+    uint16_t* bits;  // k_mc_bits planes, 3 R^2 u16 per block (R = 8 / 16)
     void* tmp;
     size_t tmp_bytes;
 };
@@ -868,8 +1054,15 @@ static int ex_scratch(mqr_vbg* v, int64_t n, bool mesh, ExScratch& e) {
     MQR_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, (const int32_t*)nullptr, (int32_t*)nullptr,
                                                    (int)n, v->stream));
     const size_t sz_nb = align256(sizeof(int32_t) * 27 * n), sz_c = align256(sizeof(int32_t) * n);
-    const size_t sz_f = mesh ? align256(sizeof(uint32_t) * 3 * v->R * v->R * n) : 0;
-    const size_t need = sz_nb + 4 * sz_c + sz_f + align256(tmp_bytes);
+    // mesh: the byte-tile path's face tables (3 R^2 u32 per block), or the bit-row path's row records
+    // (R^2 uint4) and sign rows ((R + 2)^2 u32) per block, whichever is larger
+    const size_t sz_f = mesh ? align256(std::max(sizeof(uint32_t) * 3 * v->R * v->R,
+                                                 sizeof(uint32_t) * (4 * v->R * v->R + (v->R + 2) * (v->R + 2))) *
+                                        n)
+                             : 0;
+    const size_t sz_b = align256(sizeof(uint16_t) * 3 * v->R * v->R * n);
+    tmp_bytes = std::max<size_t>(tmp_bytes, 2 * sizeof(int64_t));
+    const size_t need = sz_nb + 4 * sz_c + sz_f + sz_b + align256(tmp_bytes);
     if (v->ex_scratch_bytes < need) {
         MQR_CHECK_HIP(hipStreamSynchronize(v->stream));
         if (v->ex_scratch) MQR_CHECK_HIP(hipFree(v->ex_scratch));
@@ -890,6 +1083,8 @@ static int ex_scratch(mqr_vbg* v, int64_t n, bool mesh, ExScratch& e) {
     p += 4 * sz_c;
     e.faces = reinterpret_cast<uint32_t*>(p);
     p += sz_f;
+    e.bits = reinterpret_cast<uint16_t*>(p);
+    p += sz_b;
     e.tmp = p;
     e.tmp_bytes = tmp_bytes;
     return 0;
@@ -977,23 +1172,36 @@ static int build_nb(mqr_vbg* v, int32_t* nb) {
 template <int RT>
 static int mesh_passes(mqr_vbg* v, float thr, const ExScratch& e, mqr_geom* g, int64_t tri_blocks) {
     const int64_t n = v->pool_count;
-    uint2* rowinfo = reinterpret_cast<uint2*>(e.faces);  // R^2 uint2 per block fit in the 3 R^2 u32 faces slot
-    if constexpr (RT > 0)
-        hipLaunchKernelGGL(k_mc_count<RT>, dim3((unsigned)n), dim3(kThreads), 0, v->stream, e.nb, v->pool, thr,
-                           tri_blocks, e.c0, e.c1, rowinfo);
-    else
+    constexpr int RR = RT > 0 ? RT : 16;
+    uint4* rows4 = reinterpret_cast<uint4*>(e.faces);
+    uint32_t* rowNt = reinterpret_cast<uint32_t*>(rows4 + n * RR * RR);
+    int64_t nv = 0, nt = 0;
+    if constexpr (RT > 0) {
+        hipLaunchKernelGGL(k_mc_bits<RT>, dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, v->pool, thr, e.bits,
+                           v->bkeys, v->tab, e.nb);
+        hipLaunchKernelGGL(k_mc_count<RT>, dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, e.nb, e.bits, tri_blocks,
+                           e.c0, e.c1, rows4, rowNt);
+        int64_t* tot = reinterpret_cast<int64_t*>(e.tmp);
+        hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(kScanThreads), 0, v->stream, e.c0, e.c1, n, e.o0, e.o1, tot);
+        MQR_CHECK_HIP(hipGetLastError());
+        MQR_CHECK_HIP(hipMemcpyAsync(v->h_ex, tot, 2 * sizeof(int64_t), hipMemcpyDeviceToHost, v->stream));
+        MQR_CHECK_HIP(hipStreamSynchronize(v->stream));
+        nv = v->h_ex[0];
+        nt = v->h_ex[1];
+    } else {
+        if (build_nb(v, e.nb)) return 1;
         hipLaunchKernelGGL(k_mesh_count<RT>, dim3((unsigned)n), dim3(kThreads), 0, v->stream, e.nb, n, v->pool, v->R,
                            thr, e.c0, e.c1, e.faces);
-    MQR_CHECK_HIP(hipGetLastError());
-    int64_t nv = 0, nt = 0;
-    if (scan_totals(v, e, n, 2, &nv, &nt)) return 1;
+        MQR_CHECK_HIP(hipGetLastError());
+        if (scan_totals(v, e, n, 2, &nv, &nt)) return 1;
+    }
     MQR_REQUIRE(nv < (int64_t)1 << 31 && nt < (int64_t)1 << 31, "mesh exceeds int32 vertex / triangle ids");
     g->nv = nv;
     g->nt = nt;
     if (alloc_geom(g, nv, nt)) return 1;
     if constexpr (RT > 0)
-        hipLaunchKernelGGL(k_mc_emit<RT>, dim3((unsigned)n), dim3(kThreads), 0, v->stream, e.nb, v->bkeys, v->pool,
-                           v->voxel_size, thr, tri_blocks, e.c0, e.c1, e.o0, e.o1, rowinfo, g->pos, g->nrm, g->tri);
+        hipLaunchKernelGGL(k_mc_emit<RT>, dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, e.nb, v->bkeys, v->pool,
+                           v->voxel_size, e.c0, e.c1, e.o0, e.o1, rows4, rowNt, g->pos, g->nrm, g->tri);
     else
         hipLaunchKernelGGL(k_mesh_emit<RT>, dim3((unsigned)n), dim3(kThreads), 0, v->stream, e.nb, n, v->bkeys,
                            v->pool, v->R, v->voxel_size, thr, e.c0, e.c1, e.o0, e.o1, e.faces, g->pos, g->nrm, g->tri);
@@ -1005,16 +1213,35 @@ static int mesh_passes(mqr_vbg* v, float thr, const ExScratch& e, mqr_geom* g, i
 template <int RT>
 static int point_passes(mqr_vbg* v, float thr, const ExScratch& e, mqr_geom* g) {
     const int64_t n = v->pool_count;
-    hipLaunchKernelGGL(k_points<RT>, dim3((unsigned)n), dim3(kThreads), 0, v->stream, e.nb, n, v->bkeys, v->pool,
-                       v->R, v->voxel_size, thr, e.c0, (const int32_t*)nullptr, (float*)nullptr, (float*)nullptr);
-    MQR_CHECK_HIP(hipGetLastError());
     int64_t np = 0;
-    if (scan_totals(v, e, n, 1, &np, nullptr)) return 1;
+    if constexpr (RT > 0) {
+        uint4* rows4 = reinterpret_cast<uint4*>(e.faces);
+        hipLaunchKernelGGL(k_mc_bits<RT>, dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, v->pool, thr, e.bits,
+                           v->bkeys, v->tab, e.nb);
+        hipLaunchKernelGGL(k_pt_count<RT>, dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, e.nb, e.bits, v->pool,
+                           e.c0, rows4);
+        int64_t* tot = reinterpret_cast<int64_t*>(e.tmp);
+        hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(kScanThreads), 0, v->stream, e.c0, (const int32_t*)nullptr, n,
+                           e.o0, (int32_t*)nullptr, tot);
+        MQR_CHECK_HIP(hipGetLastError());
+        MQR_CHECK_HIP(hipMemcpyAsync(v->h_ex, tot, sizeof(int64_t), hipMemcpyDeviceToHost, v->stream));
+        MQR_CHECK_HIP(hipStreamSynchronize(v->stream));
+        np = v->h_ex[0];
+    } else {
+        if (build_nb(v, e.nb)) return 1;
+        hipLaunchKernelGGL(k_points<RT>, dim3((unsigned)n), dim3(kThreads), 0, v->stream, e.nb, n, v->bkeys, v->pool,
+                           v->R, v->voxel_size, thr, e.c0, (const int32_t*)nullptr, (float*)nullptr, (float*)nullptr);
+        MQR_CHECK_HIP(hipGetLastError());
+        if (scan_totals(v, e, n, 1, &np, nullptr)) return 1;
+    }
     g->nv = np;
-    MQR_CHECK_HIP(hipMalloc(&g->pos, sizeof(float) * 3 * std::max<int64_t>(np, 1)));
-    MQR_CHECK_HIP(hipMalloc(&g->nrm, sizeof(float) * 3 * std::max<int64_t>(np, 1)));
-    hipLaunchKernelGGL(k_points<RT>, dim3((unsigned)n), dim3(kThreads), 0, v->stream, e.nb, n, v->bkeys, v->pool,
-                       v->R, v->voxel_size, thr, e.c0, e.o0, g->pos, g->nrm);
+    if (alloc_geom(g, np, 0)) return 1;
+    if constexpr (RT > 0)
+        hipLaunchKernelGGL(k_pt_emit<RT>, dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, e.nb, v->bkeys, v->pool,
+                           v->voxel_size, e.c0, e.o0, reinterpret_cast<const uint4*>(e.faces), g->pos, g->nrm);
+    else
+        hipLaunchKernelGGL(k_points<RT>, dim3((unsigned)n), dim3(kThreads), 0, v->stream, e.nb, n, v->bkeys, v->pool,
+                           v->R, v->voxel_size, thr, e.c0, e.o0, g->pos, g->nrm);
     MQR_CHECK_HIP(hipGetLastError());
     MQR_CHECK_HIP(hipStreamSynchronize(v->stream));
     return 0;
@@ -1042,7 +1269,7 @@ int mqr_extract_mesh_owned(mqr_vbg* v, float thr, int64_t n_owned, mqr_geom** ou
     int rc = 0;
     if (n > 0) {
         ExScratch e{};
-        rc = ex_scratch(v, n, true, e) || build_nb(v, e.nb);
+        rc = ex_scratch(v, n, true, e);
         if (!rc) rc = v->R == 16 ? mesh_passes<16>(v, thr, e, g, tri_blocks)
                       : v->R == 8 ? mesh_passes<8>(v, thr, e, g, tri_blocks)
                                   : mesh_passes<0>(v, thr, e, g, tri_blocks);
@@ -1069,7 +1296,7 @@ int mqr_extract_points(mqr_vbg* v, float thr, mqr_geom** out) {
     int rc = 0;
     if (n > 0) {
         ExScratch e{};
-        rc = ex_scratch(v, n, false, e) || build_nb(v, e.nb);
+        rc = ex_scratch(v, n, true, e);  // the row records use the mesh path's slot
         if (!rc) rc = v->R == 16 ? point_passes<16>(v, thr, e, g) : v->R == 8 ? point_passes<8>(v, thr, e, g)
                                                                            : point_passes<0>(v, thr, e, g);
     }
