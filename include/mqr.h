@@ -187,6 +187,12 @@ int mqr_vbg_profile(mqr_vbg* v, int enable);
 int mqr_vbg_set_variant(mqr_vbg* v, int variant);
 int mqr_check_division(int device, int which, float b, uint32_t lo_bits, uint64_t count, uint32_t* mismatches,
                        uint32_t* first_bad);
+/* mqr_check_div64: the confidence kernel's float64 quotients against IEEE division on `count`
+ * hashed pairs (a in [-a_max, a_max], b log-uniform in [b_lo, b_hi]); mode 0 = shared refined
+ * reciprocal (quotients by Z), 1 = host-rounded reciprocal + Markstein correction (by fx / fy).
+ * first_bad: 2 doubles (a, b) of a mismatch. */
+int mqr_check_div64(int device, int mode, uint64_t seed, uint64_t count, double a_max, double b_lo, double b_hi,
+                    uint64_t* mismatches, double* first_bad);
 int mqr_vbg_stats(mqr_vbg* v, mqr_stats* out, int reset);
 
 /* Ray casting: replaces o3d.t.geometry.RaycastingScene as used for colour-aligned

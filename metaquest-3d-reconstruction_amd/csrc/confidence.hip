@@ -6,36 +6,87 @@
 // sequence resident in HBM (the reference re-reads and re-decodes each frame ~21x from disk).
 // Arithmetic is float64 in numpy's order with the two float32 roundings numpy performs
 // (interpolated target depth, error), so valid_count / confidence match the reference exactly
-// (pinned by tests/golden/confidence_golden.npz).  FP64 VALU + L2-resident gathers: bounded by
-// the neighbour-frame gathers, not by HBM streaming.
+// (pinned by tests/golden/confidence_golden.npz).  The kernel is FP64-VALU bound; the per-(pixel,
+// neighbour) instruction count is cut without changing a result bit: frame parameters widened
+// once on the host, the float32 error's threshold test as one float64 compare of the squared
+// distance, the quotients by Z sharing one refined reciprocal and those by fx / fy using a
+// host-rounded reciprocal (Markstein correction), all checked against IEEE division
+// (mqr_check_div64, tests/test_gpu_numerics.py).
 #include <algorithm>
 #include <cmath>
+#include <cstring>
 #include <vector>
 
 #include "mqr_common.hpp"
 
 namespace mqr {
 
+// Per-frame parameters, widened to double on the host (numpy promotes the float32 K / T entries to
+// float64 in every product; widening is exact, so doing it once per frame changes no bit), plus the
+// correctly rounded reciprocals of fx and fy for the quotient below.
 struct ConfFrame {
-    float K[9];
-    float Tcw[16];
-    float Tinv[16];
+    double fx, fy, cx, cy;
+    double rfx, rfy;  // RN(1 / fx), RN(1 / fy)
+    double Tcw[12];   // camera -> world, rows 0..2
+    double Tinv[12];  // world -> camera (float32 np.linalg.inv of Tcw, widened)
 };
 
-// Returns 1 and the float32 error when (ref pixel -> target frame) yields a finite error.
-__device__ inline int pixel_error(const float* __restrict__ tgt, int H, int W, const ConfFrame& ft,
-                                  const double pw[3], double depth_max, float* err) {
+// ---- correctly rounded float64 quotients without the v_div_scale / v_div_fixup wrapper ----------
+// (i) a / d with d's reciprocal refined once and shared by several numerators: the compiler's own
+// division sequence (v_rcp_f64, two Newton steps, quotient, one residual correction) minus
+// v_div_scale / v_div_fmas scaling and v_div_fixup, which leave operands and result unchanged while
+// |a|, |d| and the quotient stay within [2^-500, 2^500] (callers check; zero numerators are exact).
+struct Rcp64 {
+    double d, r;
+};
+__device__ __forceinline__ Rcp64 rcp64_refine(double d) {
+    const double r0 = __builtin_amdgcn_rcp(d);
+    const double e0 = __builtin_fma(-d, r0, 1.0);
+    const double r1 = __builtin_fma(r0, e0, r0);
+    const double e1 = __builtin_fma(-d, r1, 1.0);
+    return {d, __builtin_fma(r1, e1, r1)};
+}
+__device__ __forceinline__ double div64_core(double a, const Rcp64& rd) {
+    const double q = a * rd.r;
+    const double rem = __builtin_fma(-rd.d, q, a);
+    return __builtin_fma(rem, rd.r, q);
+}
+__device__ __forceinline__ bool div64_safe(double x) {
+    const double m = fabs(x);
+    return m == 0.0 || (m >= 0x1p-500 && m <= 0x1p500);
+}
+// (ii) a / b with y = RN(1 / b) computed on the host: q = RN(a y) is within one ulp of a / b, and
+// RN(q + (a - b q) y) is then RN(a / b) (Markstein's theorem; radix 2, round to nearest).
+__device__ __forceinline__ double div64_by_rn_rcp(double a, double b, double y) {
+    const double q = a * y;
+    const double rem = __builtin_fma(-b, q, a);
+    return __builtin_fma(rem, y, q);
+}
+
+// One (ref pixel, target frame) evaluation of compute_pixel_error_map.py:120-220 in numpy's float64
+// order with its two float32 roundings.  Returns 1 when the pixel gets a finite-input error; `d2`
+// = the squared distance whose sqrt, rounded to float32, is the reference's error.
+__device__ inline int pixel_error_d2(const float* __restrict__ tgt, int H, int W, const ConfFrame& ft,
+                                     const double pw[3], double depth_max, double* d2) {
     const float dmf = (float)depth_max;
     double pt[3];
 #pragma unroll
-    for (int i = 0; i < 3; ++i)
-        pt[i] = (double)ft.Tinv[i * 4 + 0] * pw[0] + (double)ft.Tinv[i * 4 + 1] * pw[1] +
-                (double)ft.Tinv[i * 4 + 2] * pw[2] + (double)ft.Tinv[i * 4 + 3] * 1.0;
+    for (int i = 0; i < 3; ++i)  // (... + T3 * 1.0): the product with 1.0 is exact
+        pt[i] = ft.Tinv[i * 4 + 0] * pw[0] + ft.Tinv[i * 4 + 1] * pw[1] + ft.Tinv[i * 4 + 2] * pw[2] + ft.Tinv[i * 4 + 3];
     const double X = pt[0], Y = pt[1], Z = pt[2];
     if (!(Z > 0 && isfinite(Z) && Z <= depth_max && isfinite(X) && isfinite(Y))) return 0;
-    const double fx = (double)ft.K[0], fy = (double)ft.K[4], cx = (double)ft.K[2], cy = (double)ft.K[5];
-    const double uu = ((X * fx) / Z) + cx;
-    const double vv = ((Y * fy) / Z) + cy;
+    const double ax = X * ft.fx, ay = Y * ft.fy;
+    double qx, qy;
+    if (div64_safe(Z) && div64_safe(ax) && div64_safe(ay) && fabs(ax) <= 0x1p400 * Z && fabs(ay) <= 0x1p400 * Z) {
+        const Rcp64 rz = rcp64_refine(Z);  // shared by both quotients
+        qx = div64_core(ax, rz);
+        qy = div64_core(ay, rz);
+    } else {
+        qx = ax / Z;
+        qy = ay / Z;
+    }
+    const double uu = qx + ft.cx;
+    const double vv = qy + ft.cy;
     if (!(isfinite(uu) && isfinite(vv))) return 0;
     const double max_coord = (double)((W > H ? W : H) * 10);
     if (!(uu >= -max_coord && uu < max_coord && vv >= -max_coord && vv < max_coord)) return 0;
@@ -54,15 +105,14 @@ __device__ inline int pixel_error(const float* __restrict__ tgt, int H, int W, c
     const float zt = (float)(wa * Ia + wb * Ib + wc * Ic + wd * Id);
     if (!(zt > 0 && isfinite(zt))) return 0;
     const double ztd = (double)zt;
-    const double xt = ((uu - cx) * ztd) / fx;
-    const double yt = ((vv - cy) * ztd) / fy;
+    const double xt = div64_by_rn_rcp((uu - ft.cx) * ztd, ft.fx, ft.rfx);
+    const double yt = div64_by_rn_rcp((vv - ft.cy) * ztd, ft.fy, ft.rfy);
     double q[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i)
-        q[i] = (double)ft.Tcw[i * 4 + 0] * xt + (double)ft.Tcw[i * 4 + 1] * yt + (double)ft.Tcw[i * 4 + 2] * ztd +
-               (double)ft.Tcw[i * 4 + 3] * 1.0;
+        q[i] = ft.Tcw[i * 4 + 0] * xt + ft.Tcw[i * 4 + 1] * yt + ft.Tcw[i * 4 + 2] * ztd + ft.Tcw[i * 4 + 3];
     const double dx = pw[0] - q[0], dy = pw[1] - q[1], dz = pw[2] - q[2];
-    *err = (float)sqrt(dx * dx + dy * dy + dz * dz);
+    *d2 = dx * dx + dy * dy + dz * dz;
     return 1;
 }
 
@@ -70,18 +120,19 @@ __device__ inline int pixel_error(const float* __restrict__ tgt, int H, int W, c
 __device__ inline int ref_point(const ConfFrame& fr, int u, int v, float dref, double depth_max, double pw[3]) {
     if (!(dref > 0 && dref <= (float)depth_max)) return 0;
     const double z = (double)dref;
-    const double x = (((double)u - (double)fr.K[2]) * z) / (double)fr.K[0];
-    const double y = (((double)v - (double)fr.K[5]) * z) / (double)fr.K[4];
+    const double x = div64_by_rn_rcp(((double)u - fr.cx) * z, fr.fx, fr.rfx);
+    const double y = div64_by_rn_rcp(((double)v - fr.cy) * z, fr.fy, fr.rfy);
 #pragma unroll
     for (int i = 0; i < 3; ++i)
-        pw[i] = (double)fr.Tcw[i * 4 + 0] * x + (double)fr.Tcw[i * 4 + 1] * y + (double)fr.Tcw[i * 4 + 2] * z +
-                (double)fr.Tcw[i * 4 + 3] * 1.0;
+        pw[i] = fr.Tcw[i * 4 + 0] * x + fr.Tcw[i * 4 + 1] * y + fr.Tcw[i * 4 + 2] * z + fr.Tcw[i * 4 + 3];
     return 1;
 }
 
+// d2_max: the largest double d2 with (float)sqrt(d2) <= threshold (host, exact); the reference's
+// `err <= threshold` on the float32 error map is d2 <= d2_max (sqrt and both roundings monotone).
 __global__ __launch_bounds__(256) void k_confidence(const float* __restrict__ depths, int N, int H, int W,
                                                     const ConfFrame* __restrict__ fr, const uint8_t* __restrict__ ok,
-                                                    int ref_begin, int r, double depth_max, float thr,
+                                                    int ref_begin, int r, double depth_max, double d2_max,
                                                     double* __restrict__ conf, int32_t* __restrict__ valid) {
     const int64_t HW = (int64_t)H * W;
     const int ref = ref_begin + blockIdx.y;
@@ -94,10 +145,10 @@ __global__ __launch_bounds__(256) void k_confidence(const float* __restrict__ de
         const int lo = max(0, ref - r), hi = min(N, ref + r + 1);
         for (int t = lo; t < hi; ++t) {
             if (t == ref || !ok[t]) continue;
-            float e;
-            if (pixel_error(depths + (int64_t)t * HW, H, W, fr[t], pw, depth_max, &e)) {
+            double d2;
+            if (pixel_error_d2(depths + (int64_t)t * HW, H, W, fr[t], pw, depth_max, &d2)) {
                 ++nv;
-                if (e <= thr) ++nc;
+                if (d2 <= d2_max) ++nc;
             }
         }
     }
@@ -111,18 +162,77 @@ __global__ void k_error_map(const float* __restrict__ refd, const float* __restr
     const int64_t HW = (int64_t)H * W;
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= HW) return;
-    double pw[3];
+    double pw[3], d2;
     float e = NAN;
-    float ev;
     if (ref_point(fr[0], (int)(p % W), (int)(p / W), refd[p], depth_max, pw) &&
-        pixel_error(tgtd, H, W, fr[1], pw, depth_max, &ev))
-        e = ev;
+        pixel_error_d2(tgtd, H, W, fr[1], pw, depth_max, &d2))
+        e = (float)sqrt(d2);
     out[p] = e;
+}
+
+// Self-test of the two quotient paths against IEEE division: mode 0 = div64_core (shared refined
+// reciprocal), 1 = div64_by_rn_rcp with y = RN(1/b) computed here by IEEE division.  Pairs from a
+// counter-based hash: a uniform in [-a_max, a_max] and b in [b_lo, b_hi] (log-uniform), plus the
+// bit-neighbourhood of exact halfway-prone values.  Counts mismatches.
+__global__ void k_check_div64(int mode, uint64_t seed, uint64_t count, double a_max, double b_lo, double b_hi,
+                              unsigned long long* mismatches, double* first_bad) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    uint64_t h1 = mix64(seed ^ (2 * i + 1)), h2 = mix64(seed + 0x9e3779b97f4a7c15ull * (i + 7));
+    const double ua = (double)(h1 >> 11) * 0x1p-53, ub = (double)(h2 >> 11) * 0x1p-53;
+    double a = (2.0 * ua - 1.0) * a_max;
+    if (h1 & 1) a = __longlong_as_double(__double_as_longlong(a) ^ (h2 & 0xff));  // low-bit perturbation
+    const double b = exp2(log2(b_lo) + ub * (log2(b_hi) - log2(b_lo)));
+    const double want = a / b;
+    double got;
+    if (mode == 0) got = div64_core(a, rcp64_refine(b));
+    else got = div64_by_rn_rcp(a, b, 1.0 / b);
+    if (__double_as_longlong(got) != __double_as_longlong(want)) {
+        atomicAdd(mismatches, 1ull);
+        first_bad[0] = a;
+        first_bad[1] = b;
+    }
 }
 
 }  // namespace mqr
 
 using namespace mqr;
+
+namespace {
+void fill_frame(const float* K, const float* Tcw, const float* Tinv, ConfFrame& f) {
+    f.fx = (double)K[0];
+    f.fy = (double)K[4];
+    f.cx = (double)K[2];
+    f.cy = (double)K[5];
+    f.rfx = 1.0 / f.fx;  // correctly rounded (IEEE host division)
+    f.rfy = 1.0 / f.fy;
+    for (int k = 0; k < 12; ++k) {
+        f.Tcw[k] = (double)Tcw[k];
+        f.Tinv[k] = Tinv ? (double)Tinv[k] : 0.0;
+    }
+}
+
+// Largest double d2 >= 0 with (float)sqrt(d2) <= thr (binary search over the ordered bit patterns
+// of non-negative doubles; the host's sqrt and float conversion are IEEE, like the device's).
+double d2_threshold(float thr) {
+    auto ok = [&](uint64_t bits) {
+        double d;
+        std::memcpy(&d, &bits, sizeof d);
+        return (float)std::sqrt(d) <= thr;
+    };
+    if (!ok(0)) return -1.0;  // thr < 0 (or NaN): nothing is consistent
+    uint64_t lo = 0, hi = 0x7ff0000000000000ull;  // ok(lo); +inf
+    if (ok(hi)) return INFINITY;
+    while (hi - lo > 1) {
+        const uint64_t mid = lo + (hi - lo) / 2;
+        if (ok(mid)) lo = mid;
+        else hi = mid;
+    }
+    double d;
+    std::memcpy(&d, &lo, sizeof d);
+    return d;
+}
+}  // namespace
 
 extern "C" {
 
@@ -142,9 +252,7 @@ int mqr_confidence(int device, const float* depths, int depth_loc, int N, int H,
     std::vector<ConfFrame> fr(N);
     std::vector<uint8_t> okv(N, 1);
     for (int i = 0; i < N; ++i) {
-        std::copy(K + 9 * i, K + 9 * i + 9, fr[i].K);
-        std::copy(T_cw + 16 * i, T_cw + 16 * i + 16, fr[i].Tcw);
-        std::copy(T_cw_inv + 16 * i, T_cw_inv + 16 * i + 16, fr[i].Tinv);
+        fill_frame(K + 9 * i, T_cw + 16 * i, T_cw_inv + 16 * i, fr[i]);
         if (frame_ok) okv[i] = frame_ok[i] ? 1 : 0;
     }
     ConfFrame* dfr = nullptr;
@@ -168,7 +276,7 @@ int mqr_confidence(int device, const float* depths, int depth_loc, int N, int H,
     }
     // (float) threshold: numpy compares the float32 error map against a weak Python float.
     hipLaunchKernelGGL(k_confidence, dim3((unsigned)((HW + 255) / 256), nref), dim3(256), 0, s, dsrc, N, H, W, dfr,
-                       dok, ref_begin, frame_range, depth_max, (float)error_threshold, dconf, dvalid);
+                       dok, ref_begin, frame_range, depth_max, d2_threshold((float)error_threshold), dconf, dvalid);
     MQR_CHECK_HIP(hipGetLastError());
     if (out_loc != MQR_DEVICE) {
         MQR_CHECK_HIP(hipMemcpyAsync(conf, dconf, sizeof(double) * nref * HW, hipMemcpyDeviceToHost, s));
@@ -186,6 +294,32 @@ int mqr_confidence(int device, const float* depths, int depth_loc, int N, int H,
     return 0;
 }
 
+int mqr_check_div64(int device, int mode, uint64_t seed, uint64_t count, double a_max, double b_lo, double b_hi,
+                    uint64_t* mismatches, double* first_bad) {
+    MQR_REQUIRE(mismatches && first_bad && (mode == 0 || mode == 1) && b_lo > 0 && b_hi >= b_lo, "bad arguments");
+    MQR_CHECK_HIP(hipSetDevice(device));
+    unsigned long long* dm = nullptr;
+    double* db = nullptr;
+    MQR_CHECK_HIP(hipMalloc(&dm, sizeof(unsigned long long)));
+    MQR_CHECK_HIP(hipMalloc(&db, 2 * sizeof(double)));
+    MQR_CHECK_HIP(hipMemset(dm, 0, sizeof(unsigned long long)));
+    MQR_CHECK_HIP(hipMemset(db, 0, 2 * sizeof(double)));
+    const uint64_t chunk = 1ull << 28;
+    for (uint64_t off = 0; off < count; off += chunk) {
+        const uint64_t c = std::min<uint64_t>(chunk, count - off);
+        hipLaunchKernelGGL(k_check_div64, dim3((unsigned)((c + 255) / 256)), dim3(256), 0, 0, mode, seed + off, c, a_max,
+                           b_lo, b_hi, dm, db);
+        MQR_CHECK_HIP(hipGetLastError());
+    }
+    unsigned long long m = 0;
+    MQR_CHECK_HIP(hipMemcpy(&m, dm, sizeof m, hipMemcpyDeviceToHost));
+    MQR_CHECK_HIP(hipMemcpy(first_bad, db, 2 * sizeof(double), hipMemcpyDeviceToHost));
+    (void)hipFree(dm);
+    (void)hipFree(db);
+    *mismatches = m;
+    return 0;
+}
+
 int mqr_pixel_error_map(int device, const float* ref_depth, const float* tgt_depth, int H, int W, const float* K_ref,
                         const float* K_tgt, const float* T_cw_ref, const float* T_cw_inv_tgt, const float* T_cw_tgt,
                         double depth_max, float* err_out) {
@@ -194,11 +328,8 @@ int mqr_pixel_error_map(int device, const float* ref_depth, const float* tgt_dep
     MQR_CHECK_HIP(hipSetDevice(device));
     const int64_t HW = (int64_t)H * W;
     ConfFrame fr[2] = {};
-    std::copy(K_ref, K_ref + 9, fr[0].K);
-    std::copy(T_cw_ref, T_cw_ref + 16, fr[0].Tcw);
-    std::copy(K_tgt, K_tgt + 9, fr[1].K);
-    std::copy(T_cw_tgt, T_cw_tgt + 16, fr[1].Tcw);
-    std::copy(T_cw_inv_tgt, T_cw_inv_tgt + 16, fr[1].Tinv);
+    fill_frame(K_ref, T_cw_ref, nullptr, fr[0]);
+    fill_frame(K_tgt, T_cw_tgt, T_cw_inv_tgt, fr[1]);
     ConfFrame* dfr = nullptr;
     float *dr = nullptr, *dt = nullptr, *de = nullptr;
     MQR_CHECK_HIP(hipMalloc(&dfr, sizeof(fr)));

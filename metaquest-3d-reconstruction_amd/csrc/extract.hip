@@ -39,6 +39,7 @@ constexpr int kThreads = 512;  // 8 waves per workgroup: two LDS-resident blocks
 // The bit-row kernels (R = 8 / 16) are latency-bound chains of small dependent loads per block:
 // 256-thread workgroups (one per voxel row at R = 16) double the blocks in flight per CU.
 constexpr int kMcThreads = 256;
+constexpr uint32_t kAll27 = (1u << 27) - 1;  // presence mask of a block whose 26 neighbours all exist
 
 __device__ inline int64_t dev_find(const Table t, uint64_t k) {
     const uint64_t m = (uint64_t)t.cap - 1;
@@ -666,6 +667,30 @@ __device__ inline void mc_normal(const int32_t* __restrict__ nbrow, const float2
         n[2] = mc_tsdf<M>(nbrow, pool, x, y, z + 1) - mc_tsdf<M>(nbrow, pool, x, y, z - 1);
 }
 
+// Everything a vertex / point on the edge (o, o + axis) needs when all 27 blocks of the neighbourhood
+// are present (then every normal component is written, so upstream's per-voxel normal scratch
+// carries nothing across the voxel's edges and only this edge's normals matter): the 13 tsdf taps
+// -- o, o +- x/y/z, e = o + axis, e +- x/y/z -- issued as one batch of loads.
+template <class M>
+__device__ inline void mc_edge_full(const int32_t* __restrict__ nbrow, const float2* __restrict__ pool, int x, int y,
+                                    int z, int axis, float& t_o, float& t_e, float* no, float* ne) {
+    const int ex = x + (axis == 0), ey = y + (axis == 1), ez = z + (axis == 2);
+    const int px[13] = {x, x + 1, x - 1, x, x, x, x, ex + 1, ex - 1, ex, ex, ex, ex};
+    const int py[13] = {y, y, y, y + 1, y - 1, y, y, ey, ey, ey + 1, ey - 1, ey, ey};
+    const int pz[13] = {z, z, z, z, z, z + 1, z - 1, ez, ez, ez, ez, ez + 1, ez - 1};
+    float v[13];
+#pragma unroll
+    for (int j = 0; j < 13; ++j) v[j] = mc_tsdf<M>(nbrow, pool, px[j], py[j], pz[j]);
+    t_o = v[0];
+    t_e = axis == 0 ? v[1] : axis == 1 ? v[3] : v[5];
+    no[0] = v[1] - v[2];
+    no[1] = v[3] - v[4];
+    no[2] = v[5] - v[6];
+    ne[0] = v[7] - v[8];
+    ne[1] = v[9] - v[10];
+    ne[2] = v[11] - v[12];
+}
+
 // Global vertex id of the edge owned by voxel (ox, oy, oz) (may lie in a +x/+y/+z neighbour) along axis.
 __device__ inline int32_t mc_vid(uint32_t vbase, uint32_t ex, uint32_t ey, uint32_t ez, int x, int axis) {
     const uint32_t low = (1u << x) - 1;
@@ -725,19 +750,27 @@ __global__ __launch_bounds__(kMcThreads) void k_mc_emit(const int32_t* __restric
         }
         const uint32_t m3 = ((ex >> x) & 1u) | (((ey >> x) & 1u) << 1) | (((ez >> x) & 1u) << 2);
         const int y = lo % R, z = lo / R;
-        const float tsdf_o = mc_tsdf<M>(nbrow, pool, x, y, z);
+        float tsdf_o, tsdf_e;
         float no[3] = {0.f, 0.f, 0.f}, ne[3] = {0.f, 0.f, 0.f};
-        mc_normal<M>(nbrow, pool, pres, x, y, z, no);
-        // upstream keeps one per-voxel normal scratch across the voxel's edges: replay the earlier ones
-        uint32_t mm = m3;
         int axis = 0;
-        for (int j = 0;; ++j) {
+        if (pres == kAll27) {  // block-uniform
+            uint32_t mm = m3;
+            for (int j = 0; j < k; ++j) mm &= mm - 1;
             axis = __builtin_ctz(mm);
-            mc_normal<M>(nbrow, pool, pres, x + (axis == 0), y + (axis == 1), z + (axis == 2), ne);
-            if (j == k) break;
-            mm &= mm - 1;
+            mc_edge_full<M>(nbrow, pool, x, y, z, axis, tsdf_o, tsdf_e, no, ne);
+        } else {
+            tsdf_o = mc_tsdf<M>(nbrow, pool, x, y, z);
+            mc_normal<M>(nbrow, pool, pres, x, y, z, no);
+            // upstream keeps one per-voxel normal scratch across the voxel's edges: replay the earlier ones
+            uint32_t mm = m3;
+            for (int j = 0;; ++j) {
+                axis = __builtin_ctz(mm);
+                mc_normal<M>(nbrow, pool, pres, x + (axis == 0), y + (axis == 1), z + (axis == 2), ne);
+                if (j == k) break;
+                mm &= mm - 1;
+            }
+            tsdf_e = mc_tsdf<M>(nbrow, pool, x + (axis == 0), y + (axis == 1), z + (axis == 2));
         }
-        const float tsdf_e = mc_tsdf<M>(nbrow, pool, x + (axis == 0), y + (axis == 1), z + (axis == 2));
         const float ratio = (0 - tsdf_o) / (tsdf_e - tsdf_o);
         const float rx = ratio * (int)(axis == 0), ry = ratio * (int)(axis == 1), rz = ratio * (int)(axis == 2);
         const int gx = xb * R + x, gy = yb * R + y, gz = zb * R + z;
@@ -887,18 +920,26 @@ __global__ __launch_bounds__(kMcThreads) void k_pt_emit(const int32_t* __restric
         }
         const uint32_t m3 = ((ex >> x) & 1u) | (((ey >> x) & 1u) << 1) | (((ez >> x) & 1u) << 2);
         const int y = lo % R, z = lo / R;
-        const float t_o = mc_tsdf<M>(nbrow, pool, x, y, z);
+        float t_o, t_i;
         float no[3] = {0.f, 0.f, 0.f}, ni[3] = {0.f, 0.f, 0.f};
-        mc_normal<M>(nbrow, pool, pres, x, y, z, no);
-        uint32_t mm = m3;
         int axis = 0;
-        for (int j = 0;; ++j) {
+        if (pres == kAll27) {  // block-uniform
+            uint32_t mm = m3;
+            for (int j = 0; j < k; ++j) mm &= mm - 1;
             axis = __builtin_ctz(mm);
-            mc_normal<M>(nbrow, pool, pres, x + (axis == 0), y + (axis == 1), z + (axis == 2), ni);
-            if (j == k) break;
-            mm &= mm - 1;
+            mc_edge_full<M>(nbrow, pool, x, y, z, axis, t_o, t_i, no, ni);
+        } else {
+            t_o = mc_tsdf<M>(nbrow, pool, x, y, z);
+            mc_normal<M>(nbrow, pool, pres, x, y, z, no);
+            uint32_t mm = m3;
+            for (int j = 0;; ++j) {
+                axis = __builtin_ctz(mm);
+                mc_normal<M>(nbrow, pool, pres, x + (axis == 0), y + (axis == 1), z + (axis == 2), ni);
+                if (j == k) break;
+                mm &= mm - 1;
+            }
+            t_i = mc_tsdf<M>(nbrow, pool, x + (axis == 0), y + (axis == 1), z + (axis == 2));
         }
-        const float t_i = mc_tsdf<M>(nbrow, pool, x + (axis == 0), y + (axis == 1), z + (axis == 2));
         const float ratio = (0 - t_o) / (t_i - t_o);
         const int gx = xb * R + x, gy = yb * R + y, gz = zb * R + z;
         const int64_t id = p0 + i;

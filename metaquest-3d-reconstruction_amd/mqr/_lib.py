@@ -94,6 +94,8 @@ SIGNATURES = {
                                                   ctypes.c_int, ctypes.c_int64, ctypes.POINTER(_vp), _i64p]),
     "mqr_vbg_profile": (ctypes.c_int, [_vp, ctypes.c_int]),
     "mqr_vbg_set_variant": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "mqr_check_div64": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_double,
+                                       ctypes.c_double, ctypes.c_double, ctypes.POINTER(ctypes.c_uint64), _f64p]),
     "mqr_check_division": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_uint32, ctypes.c_uint64,
                                           ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]),
     "mqr_vbg_stats": (ctypes.c_int, [_vp, ctypes.POINTER(MqrStats), ctypes.c_int]),

@@ -166,3 +166,21 @@ def test_lean_integrate_exact_fallback():
         assert compare_volumes(out[0], out[i], 0.0) == 0.0, cases[i]
     for i in (6, 7):
         assert compare_volumes(out[5], out[i], 0.0) == 0.0, cases[i]
+
+
+@pytest.mark.parametrize("mode,a_max,b_lo,b_hi", [
+    (0, 2.0e3 * 700.0, 1e-3, 8.0),        # (X fx) / Z: pixel-scale numerators, depths up to 8 m
+    (0, 1.0e12, 2.0 ** -480, 2.0 ** 60),  # the guarded range edges
+    (1, 4.0e3, 50.0, 2000.0),             # ((u - cx) z) / fx: focal lengths of real and synthetic cameras
+    (1, 1.0e9, 1e-3, 1e6),
+])
+def test_confidence_float64_quotients_match_ieee(mode, a_max, b_lo, b_hi):
+    """The confidence kernel's float64 quotients (shared refined reciprocal; host-rounded reciprocal
+    with a Markstein correction) equal IEEE division on 2^31 hashed operand pairs per case."""
+    import ctypes
+    from mqr import _lib
+    mm = ctypes.c_uint64()
+    bad = np.zeros(2, np.float64)
+    _lib.call("mqr_check_div64", 0, mode, 12345 + mode, 1 << 31, a_max, b_lo, b_hi, ctypes.byref(mm),
+              _lib.ptr(bad, _lib._f64p))
+    assert mm.value == 0, f"{mm.value} mismatches, e.g. a={bad[0]!r} b={bad[1]!r}"

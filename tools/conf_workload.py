@@ -1,0 +1,38 @@
+#!/usr/bin/env python3
+"""Workload for rocprofv3 passes over the confidence kernel: the bench's C3 confidence leg (every
+one of the C2 sequence's 500 frames as a reference frame, r = 10, depth_max 4, error 0.08),
+device-resident depth in and maps out, one warm-up call then `--reps` calls."""
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "metaquest-3d-reconstruction_amd"))
+
+
+def main():
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=2)
+    a = ap.parse_args()
+    import numpy as np
+    import torch
+    from mqr import _lib, synthetic
+    seq = synthetic.make_sequence_fast("room", poses=synthetic.room_loop_poses(500), device="cuda:0")
+    d = seq["depth_t"].contiguous()
+    B, H, W = d.shape
+    T_cw = np.ascontiguousarray(seq["T_cw"], dtype=np.float32).reshape(B, 16)
+    T_ci = np.ascontiguousarray(np.linalg.inv(seq["T_cw"]), dtype=np.float32).reshape(B, 16)
+    K32 = np.ascontiguousarray(seq["K"], dtype=np.float32).reshape(B, 9)
+    conf = torch.empty((B, H, W), dtype=torch.float64, device="cuda:0")
+    valid = torch.empty((B, H, W), dtype=torch.int32, device="cuda:0")
+    for _ in range(a.reps + 1):
+        _lib.call("mqr_confidence", 0, ctypes.c_void_p(d.data_ptr()), 1, B, H, W, _lib.ptr(K32, _lib._f32p),
+                  _lib.ptr(T_cw, _lib._f32p), _lib.ptr(T_ci, _lib._f32p), None, 0, B, 10, 4.0, 0.08,
+                  ctypes.c_void_p(conf.data_ptr()), ctypes.c_void_p(valid.data_ptr()), 1)
+    torch.cuda.synchronize()
+    print("valid mean", float(valid.float().mean()), "conf mean", float(conf.mean()))
+
+
+if __name__ == "__main__":
+    main()
