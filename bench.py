@@ -286,7 +286,7 @@ def c5_leg(args, device, frames_per_side=2000, voxel=0.003, key_every=40, parity
     import numpy as np
     import torch
     from mqr import synthetic
-    from mqr.color import color_vertices
+    from mqr.color import color_map
     from mqr.raycasting import RaycastingScene
     from mqr.vbg import VoxelBlockGrid
     dev = int(device.index or 0)
@@ -339,19 +339,23 @@ def c5_leg(args, device, frames_per_side=2000, voxel=0.003, key_every=40, parity
     cad = scene.cast_pinhole(K[key], T[key], W, H)["t_hit"].numpy()
     cast_s = time.perf_counter() - t0
     t0 = time.perf_counter()
-    col, cnt = color_vertices(mesh.vertices, imgs, cad, K[key], T[key], device=dev)
+    col, cnt = color_map(mesh.vertices, imgs, cad, K[key], T[key], device=dev)
     col_s = time.perf_counter() - t0
     seen = cnt > 0
     err = float(np.abs(col[seen] - synthetic.texture(mesh.vertices[seen])).mean()) if seen.any() else None
+    err_fill = (float(np.abs(col[~seen] - synthetic.texture(mesh.vertices[~seen])).mean()) if (~seen).any()
+                else None)
     out = {"frames": B, "voxel_size": voxel, "integrate_ms": t_int * 1e3, "frames_per_s": B / t_int,
            "blocks": blocks, "pool_gb": pool_gb, "extract_ms": sorted(ext)[1] * 1e3,
            "vertices": int(len(mesh.vertices)), "triangles": int(len(mesh.triangles)),
            "keyframes": len(key), "bvh_build_ms": bvh_s * 1e3, "colour_depth_cast_ms": cast_s * 1e3,
            "colour_ms": col_s * 1e3, "coloured_fraction": float(seen.mean()), "colour_mean_abs_err": err,
+           "colour_mean_abs_err_knn_filled": err_fill,
            "generation_s": gen_s,
            "note": "integrate: device-resident depth, best of 2 passes from an emptied volume (capacity grows "
-                   "from 16384 blocks); extract: host copy included, median of 3; colour: host arrays in/out "
-                   "(PCIe included), error vs the analytic texture the colour frames were rendered with"}
+                   "from 16384 blocks); extract: host copy included, median of 3; colour: mqr_color_map (boundary "
+                   "masks, float64 means, 3-NN fill of unseen vertices), host arrays in/out (PCIe included), error vs "
+                   "the analytic texture the colour frames were rendered with"}
     if parity:
         # the volume of the last timed pass, its mesh (the one coloured above) and point cloud, and the
         # per-vertex colours, against the oracle on the same 4000 frames (LEFT then RIGHT)
@@ -365,9 +369,7 @@ def c5_leg(args, device, frames_per_side=2000, voxel=0.003, key_every=40, parity
         del ref
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle
-        from mqr.color import MARGIN, MAX_DEPTH, VISIBILITY_THRESHOLD
-        oc, on = oracle.color_vertices(mesh.vertices, imgs, cad, K[key], T[key], MAX_DEPTH, VISIBILITY_THRESHOLD,
-                                       MARGIN)
+        oc, on = oracle.color_map(mesh.vertices, imgs, cad, K[key], T[key])
         out["parity"]["colour_counts_equal"] = bool(np.array_equal(cnt, on))
         out["parity"]["colours_equal"] = bool(np.array_equal(col, oc))
         out["parity"]["all_ok"] = bool(out["parity"]["all_ok"] and out["parity"]["colour_counts_equal"]

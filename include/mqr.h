@@ -215,6 +215,16 @@ int mqr_color_vertices(int device, const float* vertices, int64_t nv, int vertic
                        const float* depths, int images_loc, int N, int H, int W, const double* K, const double* T_wc,
                        double max_depth, double visibility_threshold, int margin, float* colors_out,
                        int32_t* counts_out, int out_loc);
+/* mqr_color_map: the complete vertex colouring of run_rigid_optimizer with the keyframe poses as
+ * given (optimize_color_pose.py:70-73; pose refinement OUT of scope): t_hit = raycast_in_color_view
+ * depth (o3d_utils.py:324-341), RGBD depth truncated at depth_trunc (3.0), depth-discontinuity
+ * masks (Sobel magnitude > disc_threshold 0.1, dilated by half_dilation 3), visibility, float64
+ * colour means, and vertices no keyframe samples filled with the mean of their knn (3) nearest
+ * sampled vertices.  counts: keyframes averaged (0 for filled vertices). */
+int mqr_color_map(int device, const float* vertices, int64_t nv, int vloc, const uint8_t* images, const float* t_hit,
+                  int img_loc, int N, int H, int W, const double* K, const double* T_wc, double max_depth,
+                  double visibility_threshold, int margin, double disc_threshold, int half_dilation, double depth_trunc,
+                  int knn, float* colors_out, int32_t* counts_out, int out_loc);
 
 int mqr_scene_create(int device, mqr_scene** out);
 int mqr_scene_destroy(mqr_scene* s);

@@ -13,11 +13,14 @@
 //   sampled iff also margin <= u < W - margin and margin <= v < H - margin: the colour is the
 //   average over the sampled keyframes of (float)image_c(ui, vi) / 255.0f, summed in float64 in
 //   keyframe order.
-// Not restated: the depth-discontinuity mask and the k-nearest-neighbour fill of vertices no
-// keyframe sees (their colour stays 0, count 0), and the pose optimisation itself (OUT of scope).
+// mqr_color_vertices is that visibility-and-average primitive; mqr_color_map (below) is the complete
+// assignment -- RGBD depth truncation, depth-discontinuity masks, float64 averages and the
+// k-nearest-neighbour fill of vertices no keyframe sees.  The pose optimisation stays OUT of scope.
 //
 // One thread per vertex, keyframe loop in registers; the keyframe parameters sit in constant-
 // cached global memory.  Colour images are RGB uint8 [N][H][W][3], depth float32 [N][H][W].
+#include <hipcub/hipcub.hpp>
+
 #include <cmath>
 #include <mutex>
 #include <vector>
@@ -69,6 +72,294 @@ __global__ __launch_bounds__(256) void k_color_vertices(const float* __restrict_
     out[3 * i + 1] = cnt ? (float)(sg / cnt) : 0.f;
     out[3 * i + 2] = cnt ? (float)(sb / cnt) : 0.f;
     if (counts) counts[i] = cnt;
+}
+
+// ================================================================== complete colour map (mqr_color_map)
+// run_rigid_optimizer's vertex colours with the keyframe poses as given (the pose refinement stays
+// OUT of scope; = maximum_iteration 0), upstream ColorMapUtils / Image.cpp as recalled -- VERIFY:
+//   RGBD depth d = t_hit / 1.0, d >= depth_trunc (3.0, create_from_color_and_depth's default) -> 0;
+//   depth-boundary mask: Sobel dx = (Sobel31 along x, then Sobel32 along y), dy = (Sobel32, Sobel31),
+//     every pass a float32 image of double sums of float products over the clamped 3-tap window;
+//     sqrt(dx^2 + dy^2) > 0.1 -> 255, dilated over the (2 half + 1)^2 window (half = 3);
+//   visibility as k_color_vertices plus mask != 255; float64 averages; vertices no keyframe samples
+//   take the float64 mean of their knn (3) nearest sampled vertices' colours (squared-distance ties
+//   broken by the lower vertex index).
+
+// horizontal pass of both filters from the truncated depth: hx = Sobel31 along x, hy = Sobel32 along x
+__global__ void k_cm_filter_h(const float* __restrict__ t_hit, int64_t total, int H, int W, float depth_trunc,
+                              float* __restrict__ hx, float* __restrict__ hy) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    const int x = (int)(i % W);
+    const int64_t row = i - x;
+    float d[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const int xs = min(max(x + k - 1, 0), W - 1);
+        const float v = t_hit[row + xs] / 1.0f;
+        d[k] = v >= depth_trunc ? 0.0f : v;
+    }
+    double a = 0, b = 0;
+    a += (double)(d[0] * -1.0f);
+    a += (double)(d[1] * 0.0f);
+    a += (double)(d[2] * 1.0f);
+    b += (double)(d[0] * 1.0f);
+    b += (double)(d[1] * 2.0f);
+    b += (double)(d[2] * 1.0f);
+    hx[i] = (float)a;
+    hy[i] = (float)b;
+    (void)H;
+}
+
+// vertical passes (dx = Sobel32 along y of hx, dy = Sobel31 along y of hy) and the threshold
+__global__ void k_cm_filter_v(const float* __restrict__ hx, const float* __restrict__ hy, int64_t total, int H, int W,
+                              double disc_thr, uint8_t* __restrict__ m0) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    const int64_t HW = (int64_t)H * W;
+    const int64_t f = i / HW;
+    const int p = (int)(i - f * HW), y = p / W, x = p % W;
+    double a = 0, b = 0;
+    const float ka[3] = {1.0f, 2.0f, 1.0f}, kb[3] = {-1.0f, 0.0f, 1.0f};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const int ys = min(max(y + k - 1, 0), H - 1);
+        const int64_t q = f * HW + (int64_t)ys * W + x;
+        a += (double)(hx[q] * ka[k]);
+        b += (double)(hy[q] * kb[k]);
+    }
+    const double dx = (double)(float)a, dy = (double)(float)b;
+    m0[i] = sqrt(dx * dx + dy * dy) > disc_thr ? 255 : 0;
+}
+
+__global__ void k_cm_dilate(const uint8_t* __restrict__ m0, int64_t total, int H, int W, int half,
+                            uint8_t* __restrict__ mask) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    const int64_t HW = (int64_t)H * W;
+    const int64_t f = i / HW;
+    const int p = (int)(i - f * HW), y = p / W, x = p % W;
+    uint8_t o = 0;
+    for (int yy = max(y - half, 0); yy <= min(y + half, H - 1) && !o; ++yy)
+        for (int xx = max(x - half, 0); xx <= min(x + half, W - 1); ++xx)
+            if (m0[f * HW + (int64_t)yy * W + xx] == 255) {
+                o = 255;
+                break;
+            }
+    mask[i] = o;
+}
+
+__global__ __launch_bounds__(256) void k_cm_vertices(const float* __restrict__ V, int64_t nv,
+                                                     const uint8_t* __restrict__ images,
+                                                     const float* __restrict__ t_hit, const uint8_t* __restrict__ mask,
+                                                     const ColorCam* __restrict__ cams, int N, int H, int W,
+                                                     double max_depth, double vis_thr, int margin, float depth_trunc,
+                                                     double* __restrict__ avg, int32_t* __restrict__ counts) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nv) return;
+    const double X = V[3 * i], Y = V[3 * i + 1], Z = V[3 * i + 2];
+    double sr = 0.0, sg = 0.0, sb = 0.0;
+    int cnt = 0;
+    const int64_t HW = (int64_t)H * W;
+    for (int c = 0; c < N; ++c) {
+        const ColorCam& cm = cams[c];
+        const double vx = cm.E[0] * X + cm.E[1] * Y + cm.E[2] * Z + cm.E[3];
+        const double vy = cm.E[4] * X + cm.E[5] * Y + cm.E[6] * Z + cm.E[7];
+        const double vz = cm.E[8] * X + cm.E[9] * Y + cm.E[10] * Z + cm.E[11];
+        const float u = (float)((vx * cm.fx) / vz + cm.cx);
+        const float v = (float)((vy * cm.fy) / vz + cm.cy);
+        const float d = (float)vz;
+        const int ui = (int)roundf(u), vi = (int)roundf(v);
+        if (d < 0.0f || ui < 0 || ui >= W || vi < 0 || vi >= H) continue;
+        const int64_t px = (int64_t)c * HW + (int64_t)vi * W + ui;
+        const float th = t_hit[px] / 1.0f;
+        const float ds = th >= depth_trunc ? 0.0f : th;
+        if (ds > max_depth) continue;
+        if (mask[px] == 255) continue;
+        if (!((double)fabsf(d - ds) < vis_thr)) continue;
+        if (!(u >= margin && u < W - margin && v >= margin && v < H - margin)) continue;
+        const uint8_t* p = images + 3 * px;
+        sr += (double)((float)p[0] / 255.0f);
+        sg += (double)((float)p[1] / 255.0f);
+        sb += (double)((float)p[2] / 255.0f);
+        ++cnt;
+    }
+    avg[3 * i] = cnt ? sr / cnt : 0.0;
+    avg[3 * i + 1] = cnt ? sg / cnt : 0.0;
+    avg[3 * i + 2] = cnt ? sb / cnt : 0.0;
+    counts[i] = cnt;
+}
+
+// ---- knn over the sampled vertices: Morton-sorted buckets of kBucket points under an implicit
+// complete binary tree of bucket boxes (heap order, leaves at P + b); exact search in float64.
+constexpr int kBucket = 16;
+
+__device__ inline uint32_t ordered_u32(float f) {
+    const uint32_t u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ inline float from_ordered(uint32_t u) {
+    return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
+}
+
+__global__ void k_cm_bounds(const float* __restrict__ V, const int32_t* __restrict__ ids, int64_t n,
+                            uint32_t* __restrict__ bb /* min x y z (ordered), max x y z */) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t lo[3] = {~0u, ~0u, ~0u}, hi[3] = {0u, 0u, 0u};
+    if (i < n) {
+        const int32_t v = ids[i];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) lo[a] = hi[a] = ordered_u32(V[3 * (int64_t)v + a]);
+    }
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        uint32_t l = lo[a], h = hi[a];
+        for (int o = 32; o >= 1; o >>= 1) {
+            l = min(l, (uint32_t)__shfl_xor((int)l, o, 64));
+            h = max(h, (uint32_t)__shfl_xor((int)h, o, 64));
+        }
+        if ((threadIdx.x & 63) == 0) {
+            atomicMin(&bb[a], l);
+            atomicMax(&bb[3 + a], h);
+        }
+    }
+}
+
+__device__ inline uint64_t spread21(uint32_t v) {
+    uint64_t x = v & 0x1fffff;
+    x = (x | x << 32) & 0x1f00000000ffffull;
+    x = (x | x << 16) & 0x1f0000ff0000ffull;
+    x = (x | x << 8) & 0x100f00f00f00f00full;
+    x = (x | x << 4) & 0x10c30c30c30c30c3ull;
+    x = (x | x << 2) & 0x1249249249249249ull;
+    return x;
+}
+
+__global__ void k_cm_morton(const float* __restrict__ V, const int32_t* __restrict__ ids, int64_t n,
+                            const uint32_t* __restrict__ bb, uint64_t* __restrict__ keys) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int32_t v = ids[i];
+    uint32_t c[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const float lo = from_ordered(bb[a]), hi = from_ordered(bb[3 + a]);
+        const float t = hi > lo ? (V[3 * (int64_t)v + a] - lo) / (hi - lo) : 0.f;
+        c[a] = (uint32_t)fminf(fmaxf(t * 2097151.0f, 0.f), 2097151.f);
+    }
+    keys[i] = spread21(c[0]) | spread21(c[1]) << 1 | spread21(c[2]) << 2;
+}
+
+// leaf boxes (bucket b = sorted points [kBucket b, kBucket (b + 1)) ); empty leaves get an inverted box
+__global__ void k_cm_leaf_boxes(const float* __restrict__ V, const int32_t* __restrict__ sorted, int64_t n, int64_t P,
+                                float4* __restrict__ lo, float4* __restrict__ hi) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= P) return;
+    float l[3] = {INFINITY, INFINITY, INFINITY}, h[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int64_t j = b * kBucket; j < min(n, (b + 1) * kBucket); ++j) {
+        const int32_t v = sorted[j];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            l[a] = fminf(l[a], V[3 * (int64_t)v + a]);
+            h[a] = fmaxf(h[a], V[3 * (int64_t)v + a]);
+        }
+    }
+    lo[P + b] = make_float4(l[0], l[1], l[2], 0.f);
+    hi[P + b] = make_float4(h[0], h[1], h[2], 0.f);
+}
+
+__global__ void k_cm_level(int64_t first, int64_t count, float4* __restrict__ lo, float4* __restrict__ hi) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    const int64_t n = first + i, a = 2 * n, b = a + 1;
+    lo[n] = make_float4(fminf(lo[a].x, lo[b].x), fminf(lo[a].y, lo[b].y), fminf(lo[a].z, lo[b].z), 0.f);
+    hi[n] = make_float4(fmaxf(hi[a].x, hi[b].x), fmaxf(hi[a].y, hi[b].y), fmaxf(hi[a].z, hi[b].z), 0.f);
+}
+
+__device__ inline double box_d2(const double q[3], float4 lo, float4 hi) {
+    const double l[3] = {lo.x, lo.y, lo.z}, h[3] = {hi.x, hi.y, hi.z};
+    double s = 0.0;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const double t = fmax(fmax(l[a] - q[a], q[a] - h[a]), 0.0);
+        s += t * t;
+    }
+    return s;
+}
+
+template <int KMAX>
+__global__ __launch_bounds__(256) void k_cm_knn_fill(const float* __restrict__ V, const int32_t* __restrict__ qids,
+                                                     int64_t nq, const int32_t* __restrict__ sorted, int64_t n,
+                                                     int64_t P, const float4* __restrict__ lo,
+                                                     const float4* __restrict__ hi, const double* __restrict__ avg,
+                                                     int knn, float* __restrict__ out) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nq) return;
+    const int32_t qv = qids[t];
+    const double q[3] = {V[3 * (int64_t)qv], V[3 * (int64_t)qv + 1], V[3 * (int64_t)qv + 2]};
+    double bd[KMAX];
+    int32_t bi[KMAX];
+    int nb = 0;
+    int64_t stack[64];
+    int sp = 0;
+    stack[sp++] = 1;
+    while (sp) {
+        const int64_t node = stack[--sp];
+        if (nb == knn && box_d2(q, lo[node], hi[node]) > bd[nb - 1]) continue;
+        if (node >= P) {  // bucket
+            const int64_t b = node - P;
+            for (int64_t j = b * kBucket; j < min(n, (b + 1) * kBucket); ++j) {
+                const int32_t v = sorted[j];
+                const double dx = q[0] - (double)V[3 * (int64_t)v], dy = q[1] - (double)V[3 * (int64_t)v + 1];
+                const double dz = q[2] - (double)V[3 * (int64_t)v + 2];
+                const double d2 = dx * dx + dy * dy + dz * dz;
+                if (nb == knn && !(d2 < bd[nb - 1] || (d2 == bd[nb - 1] && v < bi[nb - 1]))) continue;
+                int k = nb < knn ? nb++ : nb - 1;
+                while (k > 0 && (d2 < bd[k - 1] || (d2 == bd[k - 1] && v < bi[k - 1]))) {
+                    bd[k] = bd[k - 1];
+                    bi[k] = bi[k - 1];
+                    --k;
+                }
+                bd[k] = d2;
+                bi[k] = v;
+            }
+        } else {  // nearer child popped first
+            const int64_t a = 2 * node, c = a + 1;
+            const double da = box_d2(q, lo[a], hi[a]), dc = box_d2(q, lo[c], hi[c]);
+            if (da <= dc) {
+                stack[sp++] = c;
+                stack[sp++] = a;
+            } else {
+                stack[sp++] = a;
+                stack[sp++] = c;
+            }
+        }
+    }
+    double c[3] = {0.0, 0.0, 0.0};
+    for (int k = 0; k < nb; ++k)
+#pragma unroll
+        for (int a = 0; a < 3; ++a) c[a] += avg[3 * (int64_t)bi[k] + a];
+    if (nb > 0)
+#pragma unroll
+        for (int a = 0; a < 3; ++a) c[a] /= (double)nb;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) out[3 * (int64_t)qv + a] = (float)c[a];
+}
+
+__global__ void k_cm_out_seen(const double* __restrict__ avg, const int32_t* __restrict__ counts, int64_t nv,
+                              float* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nv || counts[i] == 0) return;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) out[3 * i + a] = (float)avg[3 * i + a];
+}
+
+__global__ void k_cm_flags(const int32_t* __restrict__ counts, int64_t nv, uint8_t* __restrict__ seen,
+                           uint8_t* __restrict__ unseen) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nv) return;
+    seen[i] = counts[i] > 0;
+    unseen[i] = counts[i] == 0;
 }
 
 }  // namespace mqr
@@ -140,6 +431,140 @@ int mqr_color_vertices(int device, const float* vertices, int64_t nv, int vloc, 
         set_error("mqr_color_vertices: kernel failed");
         rc = 1;
     }
+    for (void* p : owned) (void)hipFree(p);
+    (void)hipStreamDestroy(s);
+    return rc;
+}
+
+int mqr_color_map(int device, const float* vertices, int64_t nv, int vloc, const uint8_t* images, const float* t_hit,
+                  int img_loc, int N, int H, int W, const double* K, const double* T_wc, double max_depth,
+                  double visibility_threshold, int margin, double disc_threshold, int half_dilation, double depth_trunc,
+                  int knn, float* colors_out, int32_t* counts_out, int out_loc) {
+    MQR_REQUIRE(vertices && images && t_hit && K && T_wc && colors_out, "null argument");
+    MQR_REQUIRE(nv >= 0 && N >= 0 && H > 0 && W > 0 && knn >= 0 && knn <= 8 && half_dilation >= 0, "bad sizes");
+    MQR_REQUIRE(nv < (int64_t{1} << 31), "mqr_color_map: vertex ids are int32");
+    if (nv == 0) return 0;
+    MQR_CHECK_HIP(hipSetDevice(device));
+    std::vector<ColorCam> cams(N);
+    for (int c = 0; c < N; ++c) {
+        for (int k = 0; k < 12; ++k) cams[c].E[k] = T_wc[16 * c + k];
+        cams[c].fx = K[9 * c + 0];
+        cams[c].fy = K[9 * c + 4];
+        cams[c].cx = K[9 * c + 2];
+        cams[c].cy = K[9 * c + 5];
+    }
+    hipStream_t s = nullptr;
+    MQR_CHECK_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    std::vector<void*> owned;
+    auto alloc = [&](size_t bytes) -> void* {
+        void* p = nullptr;
+        if (hipMalloc(&p, std::max<size_t>(bytes, 16)) != hipSuccess) return nullptr;
+        owned.push_back(p);
+        return p;
+    };
+    auto dev = [&](const void* h, size_t bytes, bool host) -> const void* {
+        if (!host) return h;
+        void* p = alloc(bytes);
+        if (!p || hipMemcpyAsync(p, h, bytes, hipMemcpyHostToDevice, s) != hipSuccess) return nullptr;
+        return p;
+    };
+    int rc = 0;
+    auto fail = [&](const char* msg) {
+        set_error(msg);
+        rc = 1;
+    };
+    const int64_t HW = (int64_t)H * W, NHW = HW * N;
+    const float* dV = static_cast<const float*>(dev(vertices, sizeof(float) * 3 * nv, vloc != MQR_DEVICE));
+    const uint8_t* dI = static_cast<const uint8_t*>(dev(images, (size_t)3 * NHW, img_loc != MQR_DEVICE));
+    const float* dT = static_cast<const float*>(dev(t_hit, sizeof(float) * NHW, img_loc != MQR_DEVICE));
+    const ColorCam* dC = static_cast<const ColorCam*>(dev(cams.data(), sizeof(ColorCam) * std::max(N, 1), true));
+    float* hx = static_cast<float*>(alloc(sizeof(float) * NHW));
+    float* hy = static_cast<float*>(alloc(sizeof(float) * NHW));
+    uint8_t* m0 = static_cast<uint8_t*>(alloc(NHW));
+    uint8_t* mask = static_cast<uint8_t*>(alloc(NHW));
+    double* avg = static_cast<double*>(alloc(sizeof(double) * 3 * nv));
+    int32_t* cnt = static_cast<int32_t*>(alloc(sizeof(int32_t) * nv));
+    float* dO = out_loc == MQR_DEVICE ? colors_out : static_cast<float*>(alloc(sizeof(float) * 3 * nv));
+    uint8_t* fseen = static_cast<uint8_t*>(alloc(nv));
+    uint8_t* funseen = static_cast<uint8_t*>(alloc(nv));
+    int32_t* ids = static_cast<int32_t*>(alloc(sizeof(int32_t) * 2 * nv));  // seen, then unseen
+    int64_t* nsel = static_cast<int64_t*>(alloc(2 * sizeof(int64_t)));
+    if (!dV || !dI || !dT || !dC || !hx || !hy || !m0 || !mask || !avg || !cnt || !dO || !fseen || !funseen || !ids ||
+        !nsel) {
+        fail("mqr_color_map: device allocation or upload failed");
+    }
+    int64_t nseen = 0, nunseen = 0;
+    if (!rc) {
+        const unsigned gi = (unsigned)((NHW + 255) / 256), gv = (unsigned)((nv + 255) / 256);
+        if (NHW > 0) {
+            hipLaunchKernelGGL(k_cm_filter_h, dim3(gi), dim3(256), 0, s, dT, NHW, H, W, (float)depth_trunc, hx, hy);
+            hipLaunchKernelGGL(k_cm_filter_v, dim3(gi), dim3(256), 0, s, hx, hy, NHW, H, W, disc_threshold, m0);
+            hipLaunchKernelGGL(k_cm_dilate, dim3(gi), dim3(256), 0, s, m0, NHW, H, W, half_dilation, mask);
+        }
+        hipLaunchKernelGGL(k_cm_vertices, dim3(gv), dim3(256), 0, s, dV, nv, dI, dT, mask, dC, N, H, W, max_depth,
+                           visibility_threshold, margin, (float)depth_trunc, avg, cnt);
+        hipLaunchKernelGGL(k_cm_flags, dim3(gv), dim3(256), 0, s, cnt, nv, fseen, funseen);
+        size_t tb = 0;
+        hipcub::CountingInputIterator<int32_t> it(0);
+        if (hipcub::DeviceSelect::Flagged(nullptr, tb, it, fseen, ids, nsel, (int)nv, s) != hipSuccess)
+            fail("mqr_color_map: select sizing failed");
+        void* tmp = rc ? nullptr : alloc(tb);
+        if (!rc && (!tmp || hipcub::DeviceSelect::Flagged(tmp, tb, it, fseen, ids, nsel, (int)nv, s) != hipSuccess ||
+                    hipcub::DeviceSelect::Flagged(tmp, tb, it, funseen, ids + nv, nsel + 1, (int)nv, s) != hipSuccess))
+            fail("mqr_color_map: select failed");
+        int64_t h[2] = {0, 0};
+        if (!rc && (hipMemcpyAsync(h, nsel, sizeof h, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                    hipStreamSynchronize(s) != hipSuccess))
+            fail("mqr_color_map: visibility pass failed");
+        nseen = h[0];
+        nunseen = h[1];
+        if (!rc && hipMemsetAsync(dO, 0, sizeof(float) * 3 * nv, s) != hipSuccess) fail("mqr_color_map: memset failed");
+        if (!rc && nseen > 0)
+            hipLaunchKernelGGL(k_cm_out_seen, dim3(gv), dim3(256), 0, s, avg, cnt, nv, dO);
+        if (!rc && knn > 0 && nseen > 0 && nunseen > 0) {
+            const int64_t nb = (nseen + kBucket - 1) / kBucket;
+            int64_t P = 1;
+            while (P < nb) P <<= 1;
+            uint32_t* bb = static_cast<uint32_t*>(alloc(6 * sizeof(uint32_t)));
+            uint64_t* keys = static_cast<uint64_t*>(alloc(sizeof(uint64_t) * 2 * nseen));
+            int32_t* sorted = static_cast<int32_t*>(alloc(sizeof(int32_t) * nseen));
+            float4* blo = static_cast<float4*>(alloc(sizeof(float4) * 2 * P));
+            float4* bhi = static_cast<float4*>(alloc(sizeof(float4) * 2 * P));
+            size_t tbs = 0;
+            if (!bb || !keys || !sorted || !blo || !bhi ||
+                hipcub::DeviceRadixSort::SortPairs(nullptr, tbs, keys, keys + nseen, ids, sorted, (int)nseen, 0, 63, s) !=
+                    hipSuccess)
+                fail("mqr_color_map: knn allocation failed");
+            void* tmps = rc ? nullptr : alloc(tbs);
+            if (!rc && !tmps) fail("mqr_color_map: knn allocation failed");
+            if (!rc) {
+                const uint32_t init[6] = {~0u, ~0u, ~0u, 0u, 0u, 0u};
+                const unsigned gs = (unsigned)((nseen + 255) / 256);
+                if (hipMemcpyAsync(bb, init, sizeof init, hipMemcpyHostToDevice, s) != hipSuccess) fail("mqr_color_map: copy");
+                hipLaunchKernelGGL(k_cm_bounds, dim3(gs), dim3(256), 0, s, dV, ids, nseen, bb);
+                hipLaunchKernelGGL(k_cm_morton, dim3(gs), dim3(256), 0, s, dV, ids, nseen, bb, keys);
+                if (hipcub::DeviceRadixSort::SortPairs(tmps, tbs, keys, keys + nseen, ids, sorted, (int)nseen, 0, 63, s) !=
+                    hipSuccess)
+                    fail("mqr_color_map: sort failed");
+                hipLaunchKernelGGL(k_cm_leaf_boxes, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, dV, sorted, nseen,
+                                   P, blo, bhi);
+                for (int64_t first = P / 2; first >= 1; first /= 2)
+                    hipLaunchKernelGGL(k_cm_level, dim3((unsigned)((first + 255) / 256)), dim3(256), 0, s, first, first,
+                                       blo, bhi);
+                hipLaunchKernelGGL(k_cm_knn_fill<8>, dim3((unsigned)((nunseen + 255) / 256)), dim3(256), 0, s, dV,
+                                   ids + nv, nunseen, sorted, nseen, P, blo, bhi, avg, knn, dO);
+            }
+        }
+        if (!rc && hipGetLastError() != hipSuccess) fail("mqr_color_map: kernel launch failed");
+        if (!rc && out_loc != MQR_DEVICE &&
+            (hipMemcpyAsync(colors_out, dO, sizeof(float) * 3 * nv, hipMemcpyDeviceToHost, s) != hipSuccess ||
+             (counts_out && hipMemcpyAsync(counts_out, cnt, sizeof(int32_t) * nv, hipMemcpyDeviceToHost, s) != hipSuccess)))
+            fail("mqr_color_map: copy back failed");
+        if (!rc && out_loc == MQR_DEVICE && counts_out &&
+            hipMemcpyAsync(counts_out, cnt, sizeof(int32_t) * nv, hipMemcpyDeviceToDevice, s) != hipSuccess)
+            fail("mqr_color_map: copy failed");
+    }
+    if (hipStreamSynchronize(s) != hipSuccess && !rc) fail("mqr_color_map: kernel failed");
     for (void* p : owned) (void)hipFree(p);
     (void)hipStreamDestroy(s);
     return rc;

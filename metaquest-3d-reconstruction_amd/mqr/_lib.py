@@ -80,6 +80,10 @@ SIGNATURES = {
     "mqr_color_vertices": (ctypes.c_int, [ctypes.c_int, _vp, ctypes.c_int64, ctypes.c_int, _vp, _vp, ctypes.c_int,
                                           ctypes.c_int, ctypes.c_int, ctypes.c_int, _f64p, _f64p, ctypes.c_double,
                                           ctypes.c_double, ctypes.c_int, _vp, _vp, ctypes.c_int]),
+    "mqr_color_map": (ctypes.c_int, [ctypes.c_int, _vp, ctypes.c_int64, ctypes.c_int, _vp, _vp, ctypes.c_int,
+                                     ctypes.c_int, ctypes.c_int, ctypes.c_int, _f64p, _f64p, ctypes.c_double,
+                                     ctypes.c_double, ctypes.c_int, ctypes.c_double, ctypes.c_int, ctypes.c_double,
+                                     ctypes.c_int, _vp, _vp, ctypes.c_int]),
     "mqr_scene_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(_vp)]),
     "mqr_scene_destroy": (ctypes.c_int, [_vp]),
     "mqr_scene_add_triangles": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp, ctypes.c_int64, ctypes.c_int,

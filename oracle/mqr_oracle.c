@@ -797,3 +797,259 @@ int orc_color_vertices(const float* V, int64_t nv, const uint8_t* images, const 
     }
     return 0;
 }
+
+/* ------------------------------------------------------------------ colour map (row f1, complete)
+ * What run_rigid_optimizer (optimize_color_pose.py:70-73) does to the vertex colours with the
+ * keyframe poses as given (its pose refinement is OUT of scope, i.e. maximum_iteration = 0), from
+ * upstream Open3D 0.19 ColorMapUtils.cpp / RigidOptimizer.cpp / Image.cpp as recalled (Open3D is not
+ * installed here: parity unpinned, every rule VERIFY):
+ *   RGBD depth: RGBDImage.create_from_color_and_depth(depth_scale = 1.0) -> d = t_hit / 1.0,
+ *     d >= depth_trunc (3.0) -> 0 (misses, t_hit = inf, too);
+ *   boundary mask (CreateDepthBoundaryMasks): dx = Filter(Sobel31 horizontal, Sobel32 vertical),
+ *     dy = Filter(Sobel32, Sobel31) -- each pass per pixel temp (double) += (float)(d * (float)k)
+ *     over the clamped 3-tap window, stored as float -- mask = sqrt(dx^2 + dy^2) > disc_thr (0.1),
+ *     then Dilate(half = 3): 255 where any pixel of the (2 half + 1)^2 window inside the image is;
+ *   visibility (CreateVertexAndImageVisibility): as orc_color_vertices plus mask(ui, vi) != 255;
+ *   colour (SetGeometryColorAverage): the float64 mean over sampled keyframes of (float)rgb / 255.0f;
+ *     a vertex no keyframe samples gets the float64 mean of the colours of its knn (3) nearest
+ *     sampled vertices (KDTreeFlann over the sampled vertices; ties of the squared distance broken
+ *     here by the lower vertex index -- VERIFY against nanoflann's visiting order).
+ * Output colours float32 of the float64 values; counts = keyframes averaged (0 for filled ones). */
+
+static void sobel_pass(const float* in, float* out, int H, int W, const float* k, int vertical) {
+    for (int y = 0; y < H; ++y)
+        for (int x = 0; x < W; ++x) {
+            double temp = 0;
+            for (int i = -1; i <= 1; ++i) {
+                int xs = x, ys = y;
+                if (vertical) {
+                    ys = y + i;
+                    if (ys < 0) ys = 0;
+                    if (ys > H - 1) ys = H - 1;
+                } else {
+                    xs = x + i;
+                    if (xs < 0) xs = 0;
+                    if (xs > W - 1) xs = W - 1;
+                }
+                temp += (in[(int64_t)ys * W + xs] * k[i + 1]);
+            }
+            out[(int64_t)y * W + x] = (float)temp;
+        }
+}
+
+int orc_depth_boundary_mask(const float* t_hit, int H, int W, double depth_trunc, double disc_thr, int half,
+                            float* depth_out, uint8_t* mask_out) {
+    const int64_t HW = (int64_t)H * W;
+    static const float s31[3] = {-1.0f, 0.0f, 1.0f}, s32[3] = {1.0f, 2.0f, 1.0f};
+    float* d = depth_out;
+    float* a = (float*)malloc(sizeof(float) * HW);
+    float* b = (float*)malloc(sizeof(float) * HW);
+    float* gx = (float*)malloc(sizeof(float) * HW);
+    uint8_t* m0 = (uint8_t*)malloc(HW);
+    for (int64_t p = 0; p < HW; ++p) {
+        float v = t_hit[p] / (float)1.0;
+        d[p] = v >= depth_trunc ? 0.0f : v;
+    }
+    sobel_pass(d, a, H, W, s31, 0);  /* dx: Sobel31 along x, then Sobel32 along y */
+    sobel_pass(a, gx, H, W, s32, 1);
+    sobel_pass(d, a, H, W, s32, 0);  /* dy: Sobel32 along x, then Sobel31 along y */
+    sobel_pass(a, b, H, W, s31, 1);
+    for (int64_t p = 0; p < HW; ++p) {
+        double dx = gx[p], dy = b[p];
+        m0[p] = sqrt(dx * dx + dy * dy) > disc_thr ? 255 : 0;
+    }
+    for (int y = 0; y < H; ++y)
+        for (int x = 0; x < W; ++x) {
+            uint8_t o = 0;
+            for (int yy = -half; yy <= half && !o; ++yy)
+                for (int xx = -half; xx <= half; ++xx) {
+                    int u = x + xx, v = y + yy;
+                    if (u >= 0 && u < W && v >= 0 && v < H && m0[(int64_t)v * W + u] == 255) {
+                        o = 255;
+                        break;
+                    }
+                }
+            mask_out[(int64_t)y * W + x] = o;
+        }
+    free(a);
+    free(b);
+    free(gx);
+    free(m0);
+    return 0;
+}
+
+/* ---- exact knn over the sampled vertices: implicit k-d tree (node = index range, split at the
+ * middle element along the widest axis), best list ordered by (squared distance, vertex index) */
+typedef struct {
+    const double* P; /* 3 per point */
+    int32_t* idx;    /* point ids, reordered */
+    uint8_t* axis;   /* split axis of the node whose middle element is this position */
+} kdtree;
+
+/* (value on axis, point id) order */
+static int kd_less(const double* P, int32_t i, int32_t j, int ax) {
+    const double x = P[3 * i + ax], y = P[3 * j + ax];
+    return x < y || (x == y && i < j);
+}
+
+/* Quickselect: idx[mid] gets the element of rank mid - lo in [lo, hi), smaller ones before it,
+ * larger after (O(n) expected per call; the tree build is O(n log n)). */
+static void kd_select(const double* P, int32_t* idx, int64_t lo, int64_t hi, int64_t mid, int ax) {
+    uint64_t seed = 0x9e3779b97f4a7c15ull ^ (uint64_t)lo ^ ((uint64_t)hi << 20);
+    while (hi - lo > 1) {
+        seed = seed * 6364136223846793005ull + 1442695040888963407ull;
+        const int64_t pv = lo + (int64_t)((seed >> 33) % (uint64_t)(hi - lo));
+        int32_t tmp = idx[pv];
+        idx[pv] = idx[hi - 1];
+        idx[hi - 1] = tmp;
+        const int32_t piv = idx[hi - 1];
+        int64_t st = lo;
+        for (int64_t i = lo; i < hi - 1; ++i)
+            if (kd_less(P, idx[i], piv, ax)) {
+                tmp = idx[i];
+                idx[i] = idx[st];
+                idx[st] = tmp;
+                ++st;
+            }
+        idx[hi - 1] = idx[st];
+        idx[st] = piv;
+        if (st == mid) return;
+        if (st < mid) lo = st + 1;
+        else hi = st;
+    }
+}
+
+static void kd_build(kdtree* t, int64_t lo, int64_t hi) {
+    if (hi - lo <= 8) return;
+    double mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int64_t i = lo; i < hi; ++i)
+        for (int a = 0; a < 3; ++a) {
+            double v = t->P[3 * t->idx[i] + a];
+            if (v < mn[a]) mn[a] = v;
+            if (v > mx[a]) mx[a] = v;
+        }
+    int ax = 0;
+    for (int a = 1; a < 3; ++a)
+        if (mx[a] - mn[a] > mx[ax] - mn[ax]) ax = a;
+    const int64_t mid = (lo + hi) / 2;
+    kd_select(t->P, t->idx, lo, hi, mid, ax);
+    t->axis[mid] = (uint8_t)ax;
+    kd_build(t, lo, mid);
+    kd_build(t, mid, hi);
+}
+
+typedef struct {
+    double d2[8];
+    int32_t id[8];
+    int n, k;
+} kbest;
+
+static void kb_push(kbest* b, double d2, int32_t id) {
+    if (b->n == b->k && !(d2 < b->d2[b->n - 1] || (d2 == b->d2[b->n - 1] && id < b->id[b->n - 1]))) return;
+    int j = b->n < b->k ? b->n++ : b->n - 1;
+    while (j > 0 && (d2 < b->d2[j - 1] || (d2 == b->d2[j - 1] && id < b->id[j - 1]))) {
+        b->d2[j] = b->d2[j - 1];
+        b->id[j] = b->id[j - 1];
+        --j;
+    }
+    b->d2[j] = d2;
+    b->id[j] = id;
+}
+
+static double sq3(const double* q, const double* p) {
+    double dx = q[0] - p[0], dy = q[1] - p[1], dz = q[2] - p[2];
+    return dx * dx + dy * dy + dz * dz;
+}
+
+static void kd_search(const kdtree* t, int64_t lo, int64_t hi, const double* q, kbest* b) {
+    if (hi - lo <= 8) {
+        for (int64_t i = lo; i < hi; ++i) kb_push(b, sq3(q, t->P + 3 * t->idx[i]), t->idx[i]);
+        return;
+    }
+    const int64_t mid = (lo + hi) / 2;
+    const int ax = t->axis[mid];
+    const double s = t->P[3 * t->idx[mid] + ax], diff = q[ax] - s;
+    /* left range [lo, mid) holds values <= s, right [mid, hi) values >= s */
+    if (diff < 0) {
+        kd_search(t, lo, mid, q, b);
+        if (b->n < b->k || diff * diff <= b->d2[b->n - 1]) kd_search(t, mid, hi, q, b);
+    } else {
+        kd_search(t, mid, hi, q, b);
+        if (b->n < b->k || diff * diff <= b->d2[b->n - 1]) kd_search(t, lo, mid, q, b);
+    }
+}
+
+int orc_color_map(const float* V, int64_t nv, const uint8_t* images, const float* t_hit, int N, int H, int W,
+                  const double* K, const double* T, double max_depth, double thr, int margin, double disc_thr,
+                  int half, double depth_trunc, int knn, float* out, int32_t* counts) {
+    const int64_t HW = (int64_t)H * W;
+    float* depth = (float*)malloc(sizeof(float) * HW * (N > 0 ? N : 1));
+    uint8_t* mask = (uint8_t*)malloc(HW * (N > 0 ? N : 1));
+    for (int c = 0; c < N; ++c)
+        orc_depth_boundary_mask(t_hit + c * HW, H, W, depth_trunc, disc_thr, half, depth + c * HW, mask + c * HW);
+    double* avg = (double*)malloc(sizeof(double) * 3 * (nv > 0 ? nv : 1));
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < nv; ++i) {
+        const double X = V[3 * i], Y = V[3 * i + 1], Z = V[3 * i + 2];
+        double sr = 0.0, sg = 0.0, sb = 0.0;
+        int cnt = 0;
+        for (int c = 0; c < N; ++c) {
+            const double* E = T + 16 * c;
+            const double vx = E[0] * X + E[1] * Y + E[2] * Z + E[3];
+            const double vy = E[4] * X + E[5] * Y + E[6] * Z + E[7];
+            const double vz = E[8] * X + E[9] * Y + E[10] * Z + E[11];
+            const float u = (float)((vx * K[9 * c]) / vz + K[9 * c + 2]);
+            const float v = (float)((vy * K[9 * c + 4]) / vz + K[9 * c + 5]);
+            const float d = (float)vz;
+            const int ui = (int)roundf(u), vi = (int)roundf(v);
+            if (d < 0.0f || ui < 0 || ui >= W || vi < 0 || vi >= H) continue;
+            const int64_t px = (int64_t)c * HW + (int64_t)vi * W + ui;
+            const float ds = depth[px];
+            if (ds > max_depth) continue;
+            if (mask[px] == 255) continue;
+            if (!((double)fabsf(d - ds) < thr)) continue;
+            if (!(u >= margin && u < W - margin && v >= margin && v < H - margin)) continue;
+            const uint8_t* p = images + 3 * px;
+            sr += (double)((float)p[0] / 255.0f);
+            sg += (double)((float)p[1] / 255.0f);
+            sb += (double)((float)p[2] / 255.0f);
+            ++cnt;
+        }
+        avg[3 * i] = cnt ? sr / cnt : 0.0;
+        avg[3 * i + 1] = cnt ? sg / cnt : 0.0;
+        avg[3 * i + 2] = cnt ? sb / cnt : 0.0;
+        counts[i] = cnt;
+    }
+    int64_t nvalid = 0;
+    for (int64_t i = 0; i < nv; ++i) nvalid += counts[i] > 0;
+    double* P = (double*)malloc(sizeof(double) * 3 * (nv > 0 ? nv : 1));
+    for (int64_t i = 0; i < 3 * nv; ++i) P[i] = V[i];
+    kdtree t = {P, (int32_t*)malloc(sizeof(int32_t) * (nvalid > 0 ? nvalid : 1)), (uint8_t*)calloc(nvalid + 1, 1)};
+    int64_t j = 0;
+    for (int64_t i = 0; i < nv; ++i)
+        if (counts[i] > 0) t.idx[j++] = (int32_t)i;
+    kd_build(&t, 0, nvalid);
+    if (knn > 8) knn = 8;
+#pragma omp parallel for schedule(dynamic, 256)
+    for (int64_t i = 0; i < nv; ++i) {
+        double c[3] = {avg[3 * i], avg[3 * i + 1], avg[3 * i + 2]};
+        if (counts[i] == 0 && knn > 0 && nvalid > 0) {
+            kbest b;
+            b.n = 0;
+            b.k = knn;
+            kd_search(&t, 0, nvalid, P + 3 * i, &b);
+            c[0] = c[1] = c[2] = 0.0;
+            for (int q = 0; q < b.n; ++q)
+                for (int a = 0; a < 3; ++a) c[a] += avg[3 * b.id[q] + a];
+            for (int a = 0; a < 3; ++a) c[a] /= (double)b.n;
+        }
+        for (int a = 0; a < 3; ++a) out[3 * i + a] = (float)c[a];
+    }
+    free(t.idx);
+    free(t.axis);
+    free(P);
+    free(avg);
+    free(depth);
+    free(mask);
+    return 0;
+}

@@ -68,6 +68,13 @@ def lib():
                                      ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_double, _f64p, _i32p]
         L.orc_raycast.restype = ctypes.c_int
         L.orc_raycast.argtypes = [_f32p, ctypes.c_int64, _i32p, ctypes.c_int64, _f32p, ctypes.c_int64, _f32p, _i32p]
+        L.orc_depth_boundary_mask.restype = ctypes.c_int
+        L.orc_depth_boundary_mask.argtypes = [_f32p, ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_double,
+                                              ctypes.c_int, _f32p, _u8p]
+        L.orc_color_map.restype = ctypes.c_int
+        L.orc_color_map.argtypes = [_f32p, ctypes.c_int64, _u8p, _f32p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                    _f64p, _f64p, ctypes.c_double, ctypes.c_double, ctypes.c_int, ctypes.c_double,
+                                    ctypes.c_int, ctypes.c_double, ctypes.c_int, _f32p, _i32p]
         L.orc_color_vertices.restype = ctypes.c_int
         L.orc_color_vertices.argtypes = [_f32p, ctypes.c_int64, _u8p, _f32p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                          _f64p, _f64p, ctypes.c_double, ctypes.c_double, ctypes.c_int, _f32p, _i32p]
@@ -237,4 +244,33 @@ def color_vertices(vertices, images, depths, K, T_wc, max_depth=2.5, visibility_
     lib().orc_color_vertices(_p(V, _f32p), len(V), _p(im, _u8p), _p(d, _f32p), N, H, W, _p(K, _f64p), _p(T, _f64p),
                              float(max_depth), float(visibility_threshold), int(margin), _p(out, _f32p),
                              _p(cnt, _i32p))
+    return out, cnt
+
+
+def depth_boundary_mask(t_hit, depth_trunc=3.0, disc_thr=0.1, half=3):
+    """(truncated RGBD depth (H,W) f32, boundary mask (H,W) u8) of one colour-aligned depth map."""
+    t = np.ascontiguousarray(t_hit, dtype=np.float32)
+    H, W = t.shape
+    d = np.empty((H, W), np.float32)
+    m = np.empty((H, W), np.uint8)
+    lib().orc_depth_boundary_mask(_p(t, _f32p), H, W, float(depth_trunc), float(disc_thr), int(half), _p(d, _f32p),
+                                  _p(m, _u8p))
+    return d, m
+
+
+def color_map(vertices, images, t_hit, K, T_wc, max_depth=2.5, visibility_threshold=0.03, margin=10, disc_thr=0.1,
+              half=3, depth_trunc=3.0, knn=3):
+    """run_rigid_optimizer's vertex colours with the poses as given (see orc_color_map) ->
+    (colours (V,3) float32, counts (V,) int32; 0 for vertices filled from their knn sampled ones)."""
+    V = np.ascontiguousarray(vertices, dtype=np.float32).reshape(-1, 3)
+    im = np.ascontiguousarray(images, dtype=np.uint8)
+    N, H, W = im.shape[:3]
+    d = np.ascontiguousarray(t_hit, dtype=np.float32).reshape(N, H, W)
+    K = np.ascontiguousarray(K, dtype=np.float64).reshape(N, 9)
+    T = np.ascontiguousarray(T_wc, dtype=np.float64).reshape(N, 16)
+    out = np.empty((len(V), 3), np.float32)
+    cnt = np.empty(len(V), np.int32)
+    lib().orc_color_map(_p(V, _f32p), len(V), _p(im, _u8p), _p(d, _f32p), N, H, W, _p(K, _f64p), _p(T, _f64p),
+                        float(max_depth), float(visibility_threshold), int(margin), float(disc_thr), int(half),
+                        float(depth_trunc), int(knn), _p(out, _f32p), _p(cnt, _i32p))
     return out, cnt

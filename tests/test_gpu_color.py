@@ -1,9 +1,15 @@
-"""Row f1 / C5: per-vertex colour projection (mqr_color_vertices) vs the CPU oracle
-(oracle.color_vertices, a restatement of Open3D's colour-map averaging -- parity unpinned against
-Open3D itself, which is not installed), on a mesh extracted from a fused room capture, with the
-colour-aligned depth ray-cast from that mesh as the reference does (raycast_in_color_view).
-Bit-identical colours and counts; colours close to the analytic texture the frames were rendered
-with wherever a keyframe sees the vertex."""
+"""Row f1 / C5: per-vertex colour projection vs the CPU oracle, on a mesh extracted from a fused
+room capture, with the colour-aligned depth ray-cast from that mesh as the reference does
+(raycast_in_color_view):
+
+* mqr_color_vertices (visibility + average) vs oracle.color_vertices;
+* mqr_color_map (run_rigid_optimizer's complete colouring with the poses as given: RGBD depth
+  truncation, depth-discontinuity masks, float64 means, 3-NN fill of unseen vertices) vs
+  oracle.color_map -- with keyframes that see only part of the room, so masks and the fill act.
+
+Both restate Open3D's colour-map code as recalled (parity unpinned against Open3D itself, which is
+not installed).  Bit-identical colours and counts; colours close to the analytic texture the
+frames were rendered with wherever a keyframe sees the vertex."""
 import numpy as np
 import pytest
 
@@ -36,7 +42,7 @@ def test_color_matches_oracle(scene):
     from mqr.raycasting import RaycastingScene
     from mqr import synthetic
     mesh, imgs, K, T = scene
-    gc, gn = project_vertex_colors(mesh, imgs, K, T)
+    gc, gn = project_vertex_colors(mesh, imgs, K, T, complete=False)
     rs = RaycastingScene()
     rs.add_triangles(mesh.vertices, mesh.triangles)
     depth = rs.cast_pinhole(K, T, 320, 240)["t_hit"].numpy()
@@ -58,3 +64,29 @@ def test_color_thresholds_and_empty(scene):
     assert (n == 0).all() and (c == 0).all()
     c, n = color_vertices(np.zeros((0, 3), np.float32), imgs, far, K, T)
     assert c.shape == (0, 3)
+
+
+def test_color_map_masks_and_fill_match_oracle(scene):
+    """The complete colouring with 3 of the 8 keyframes: the depth-boundary masks drop samples at
+    silhouettes (counts below the unmasked average's), and the vertices no keyframe samples take
+    the mean of their 3 nearest sampled vertices -- all bit-identical to the oracle."""
+    from mqr.color import MARGIN, MAX_DEPTH, VISIBILITY_THRESHOLD, color_map, color_vertices
+    from mqr.raycasting import RaycastingScene
+    from mqr import synthetic
+    mesh, imgs, K, T = scene
+    sel = [0, 3, 6]
+    imgs, K, T = imgs[sel], K[sel], T[sel]
+    rs = RaycastingScene()
+    rs.add_triangles(mesh.vertices, mesh.triangles)
+    t_hit = rs.cast_pinhole(K, T, 320, 240)["t_hit"].numpy()
+    gc, gn = color_map(mesh.vertices, imgs, t_hit, K, T)
+    oc, on = oracle.color_map(mesh.vertices, imgs, t_hit, K, T)
+    assert np.array_equal(gn, on)
+    assert np.array_equal(gc, oc)
+    _, n_plain = color_vertices(mesh.vertices, imgs, t_hit, K, T)
+    assert (gn <= n_plain).all() and (gn < n_plain).sum() > 100, "masks drop silhouette samples"
+    unseen = gn == 0
+    assert 0.2 < unseen.mean() < 0.95
+    assert (np.abs(gc[unseen]).sum(1) > 0).mean() > 0.99, "unseen vertices are filled from their neighbours"
+    seen = ~unseen
+    assert np.abs(gc[seen] - synthetic.texture(mesh.vertices[seen])).mean() < 0.05

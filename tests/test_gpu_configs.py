@@ -209,7 +209,7 @@ def test_c5_structure_hall_3mm(vbg_mod):
     hall at 3 mm voxels, volume grown from a small capacity, mesh at 1.5 and per-vertex colour from
     keyframes with ray-cast colour-aligned depth -- all against the oracle."""
     from mqr import synthetic
-    from mqr.color import MARGIN, MAX_DEPTH, VISIBILITY_THRESHOLD, color_vertices
+    from mqr.color import color_map
     from mqr.raycasting import RaycastingScene
     left = synthetic.hall_loop_poses(24)
     right = [(R, t + R[:, 0] * 0.064) for R, t in left]
@@ -230,8 +230,8 @@ def test_c5_structure_hall_3mm(vbg_mod):
     rs = RaycastingScene()
     rs.add_triangles(mesh.vertices, mesh.triangles)
     depth = rs.cast_pinhole(K, T, 320, 240)["t_hit"].numpy()
-    gc, gn = color_vertices(mesh.vertices, imgs, depth, K, T)
-    oc, on = oracle.color_vertices(mesh.vertices, imgs, depth, K, T, MAX_DEPTH, VISIBILITY_THRESHOLD, MARGIN)
+    gc, gn = color_map(mesh.vertices, imgs, depth, K, T)
+    oc, on = oracle.color_map(mesh.vertices, imgs, depth, K, T)
     assert np.array_equal(gn, on) and np.array_equal(gc, oc)
     # colour max depth 2.5 m in an 8 x 8 m hall: only the near walls and floor are coloured
     assert (gn > 0).mean() > 0.02
