@@ -230,7 +230,7 @@ def c3_leg(seq, vbg, args, device, reps=3):
                     "wall time, median of 3"}
 
 
-def dropin_e2e_leg(seq, frames, device):
+def dropin_e2e_leg(seq, frames, device, fragment_workers=4):
     """The reference's own loop on disk: a C3 capture (raw NDC files + descriptor CSV) in a temp dir,
     mqr.confidence.estimate_depth_confidences writing the per-frame npz, then
     mqr.o3d_utils.integrate(use_confidence_filtered_depth=True) reading raw + npz back
@@ -269,12 +269,75 @@ def dropin_e2e_leg(seq, frames, device):
         t_int = time.perf_counter() - t0
         blocks = vbg.size()
         del vbg
+        frag = fragments_leg(io, ds, fragment_workers) if fragment_workers > 0 else None
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
     return {"frames": n, "confidence_s": t_conf, "confidence_frames_per_s": n / t_conf, "integrate_s": t_int,
             "integrate_frames_per_s": n / t_int, "frames_per_s": n / (t_conf + t_int), "blocks": blocks,
+            "fragments": frag,
             "note": "on-disk capture (raw + descriptor CSV), estimate_depth_confidences (writes npz) then "
                     "o3d_utils.integrate with confidence masking; host file I/O + PCIe included"}
+
+
+def fragments_leg(io, ds, workers, fragment_size=100):
+    """The fragment path (refine_fragment_poses.py:14-58, 81-90) on the same on-disk capture: 100-frame
+    fragments, each into a FRESH volume (pipeline_config.yml:50-58: 1 cm, R 16, block_count 50 000,
+    depth_max 4, trunc 10, confidence mask 0.02 / 2), then extract_point_cloud(); on a spawn Pool of
+    `workers` processes sharing the GPU (warmed up before the timed run) and in-process; every
+    fragment's points checked against the oracle's volume of the same masked frames."""
+    import multiprocessing
+    import numpy as np
+    from mqr.fragments import (FragmentPoseRefinementConfig, _warm, fragment_datasets,
+                               integrate_fragment_point_clouds)
+    from mqr.models import Side
+    from mqr.o3d_utils import _masked_depth, compute_o3d_intrinsic_matrices
+    frags = fragment_datasets(ds, fragment_size)
+    cfg = FragmentPoseRefinementConfig(device="CUDA:0", confidence_threshold=0.02, valid_count_threshold=2,
+                                       voxel_size=0.01, block_count=50_000, depth_max=4.0, trunc_voxel_multiplier=10.0,
+                                       use_multi_threading=True)
+    os.environ["OMP_NUM_THREADS"] = "1"
+    ctx = multiprocessing.get_context("spawn")
+    t0 = time.perf_counter()
+    with ctx.Pool(processes=workers) as pool:
+        pool.map(_warm, range(workers))  # spawn, import, HIP context per worker
+        t_spawn = time.perf_counter() - t0
+        integrate_fragment_point_clouds(io, {Side.LEFT: frags}, cfg, pool=pool)  # warm-up (first allocations)
+        t0 = time.perf_counter()
+        pooled = integrate_fragment_point_clouds(io, {Side.LEFT: frags}, cfg, pool=pool)
+        t_pool = time.perf_counter() - t0
+    cfg.use_multi_threading = False
+    t0 = time.perf_counter()
+    integrate_fragment_point_clouds(io, {Side.LEFT: frags}, cfg)
+    t_seq = time.perf_counter() - t0
+    out = {"fragments": len(frags), "fragment_frames": fragment_size, "workers": workers,
+           "pool_spawn_s": t_spawn, "pool_s": t_pool, "fragments_per_s": len(frags) / t_pool,
+           "sequential_s": t_seq, "sequential_fragments_per_s": len(frags) / t_seq,
+           "points": [int(len(r[1])) if r else 0 for r in pooled],
+           "note": "integrate_fragment_point_cloud on a spawn Pool sharing one GPU (one HIP context per worker), "
+                   "from disk (raw + npz reads, device decode / mask), fresh 50 000-block volume per fragment, "
+                   "extract_point_cloud(3.0) copied to the host"}
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle
+    from gpu_helpers import position_hashes
+    cores, _ = host_cores()
+    oracle.set_threads(cores)
+    ok = True
+    kw = dict(use_confidence_filtered_depth=True, confidence_threshold=0.02, valid_count_threshold=2)
+    for fd, r in zip(frags, pooled):
+        ref = oracle.OracleVBG(0.01, 16, 4096)
+        K = compute_o3d_intrinsic_matrices(fd).astype(np.float64)
+        T = fd.transforms.extrinsics_wc.astype(np.float64)
+        for i in range(len(fd)):
+            d = _masked_depth(io, Side.LEFT, i, fd, **kw)
+            if d is not None:
+                ref.integrate_frame(d, K[i], T[i], 1.0, 4.0, 10.0)
+        op, _ = ref.extract_points(3.0)
+        ok = ok and r is not None and len(r[1]) == len(op) and bool(
+            np.array_equal(np.sort(position_hashes(r[1])), np.sort(position_hashes(op))))
+    out["parity"] = {"all_ok": ok, "comparison": "per fragment: point positions as exact multisets (64-bit "
+                                                 "position hashes) vs the oracle at weight 3.0"}
+    return out
 
 
 def c5_leg(args, device, frames_per_side=2000, voxel=0.003, key_every=40, parity=True):
