@@ -884,6 +884,7 @@ typedef struct {
     const double* P; /* 3 per point */
     int32_t* idx;    /* point ids, reordered */
     uint8_t* axis;   /* split axis of the node whose middle element is this position */
+    double* split;   /* its split value, recorded at build time (the children's builds reorder idx) */
 } kdtree;
 
 /* (value on axis, point id) order */
@@ -934,6 +935,7 @@ static void kd_build(kdtree* t, int64_t lo, int64_t hi) {
     const int64_t mid = (lo + hi) / 2;
     kd_select(t->P, t->idx, lo, hi, mid, ax);
     t->axis[mid] = (uint8_t)ax;
+    t->split[mid] = t->P[3 * t->idx[mid] + ax];
     kd_build(t, lo, mid);
     kd_build(t, mid, hi);
 }
@@ -968,7 +970,7 @@ static void kd_search(const kdtree* t, int64_t lo, int64_t hi, const double* q, 
     }
     const int64_t mid = (lo + hi) / 2;
     const int ax = t->axis[mid];
-    const double s = t->P[3 * t->idx[mid] + ax], diff = q[ax] - s;
+    const double s = t->split[mid], diff = q[ax] - s;
     /* left range [lo, mid) holds values <= s, right [mid, hi) values >= s */
     if (diff < 0) {
         kd_search(t, lo, mid, q, b);
@@ -1024,7 +1026,8 @@ int orc_color_map(const float* V, int64_t nv, const uint8_t* images, const float
     for (int64_t i = 0; i < nv; ++i) nvalid += counts[i] > 0;
     double* P = (double*)malloc(sizeof(double) * 3 * (nv > 0 ? nv : 1));
     for (int64_t i = 0; i < 3 * nv; ++i) P[i] = V[i];
-    kdtree t = {P, (int32_t*)malloc(sizeof(int32_t) * (nvalid > 0 ? nvalid : 1)), (uint8_t*)calloc(nvalid + 1, 1)};
+    kdtree t = {P, (int32_t*)malloc(sizeof(int32_t) * (nvalid > 0 ? nvalid : 1)), (uint8_t*)calloc(nvalid + 1, 1),
+                (double*)calloc(nvalid + 1, sizeof(double))};
     int64_t j = 0;
     for (int64_t i = 0; i < nv; ++i)
         if (counts[i] > 0) t.idx[j++] = (int32_t)i;
@@ -1047,6 +1050,7 @@ int orc_color_map(const float* V, int64_t nv, const uint8_t* images, const float
     }
     free(t.idx);
     free(t.axis);
+    free(t.split);
     free(P);
     free(avg);
     free(depth);

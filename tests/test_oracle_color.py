@@ -44,3 +44,32 @@ def test_knn_fill_equals_brute_force():
         o = np.lexsort((seen, d2))[:3]
         want = c[seen[o]].astype(np.float64).mean(0)
         assert np.abs(want - c[q]).max() <= 1e-6, q
+
+
+def test_knn_fill_equals_brute_force_on_a_surface():
+    """Surface-like points (a noisy sphere shell, many near-equal distances): the k-d tree's pruning
+    planes must be the values recorded at build time."""
+    rng = np.random.default_rng(7)
+    n = 20000
+    d = rng.normal(size=(n, 3))
+    V = (d / np.linalg.norm(d, axis=1, keepdims=True) * 0.5 + np.array([0, 0, 2.0])).astype(np.float32)
+    V = np.round(V / 0.002) * 0.002  # lattice-like coordinates: exact ties
+    V = V.astype(np.float32)
+    H = W = 96
+    K = np.array([[[60.0, 0, 48], [0, 60.0, 48], [0, 0, 1]]])
+    T = np.eye(4)[None]
+    t = np.full((1, H, W), np.inf, np.float32)
+    front = V[:, 2] < 2.0
+    u = np.round(V[front, 0] * 60 / V[front, 2] + 48).astype(int)
+    v = np.round(V[front, 1] * 60 / V[front, 2] + 48).astype(int)
+    t[0, v.clip(0, H - 1), u.clip(0, W - 1)] = V[front, 2]
+    im = rng.integers(0, 255, (1, H, W, 3)).astype(np.uint8)
+    c, cnt = oracle.color_map(V, im, t, K, T, disc_thr=1e9)
+    seen, unseen = np.nonzero(cnt > 0)[0], np.nonzero(cnt == 0)[0]
+    assert len(seen) > 200 and len(unseen) > 1000
+    P = V.astype(np.float64)
+    for q in unseen[::37]:
+        d2 = ((P[seen] - P[q]) ** 2).sum(1)
+        o = np.lexsort((seen, d2))[:3]
+        want = c[seen[o]].astype(np.float64).mean(0)
+        assert np.abs(want - c[q]).max() <= 1e-6, q
