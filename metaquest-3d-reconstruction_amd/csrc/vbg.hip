@@ -19,6 +19,9 @@
 
 #include "mqr_common.hpp"
 #include "vbg_kernels.hpp"
+#if MQR_AB
+#include "vbg_ab.hpp"
+#endif
 
 namespace mqr {
 
@@ -256,10 +259,12 @@ static int resolve_pool_overflow(mqr_vbg* v, int p, bool* table_full = nullptr) 
 // the batch touch enqueues it before the host has read the counters).
 static int enqueue_lpt(mqr_vbg* v, int p) {
     bmask_t* om = reinterpret_cast<bmask_t*>(v->lpt[p] + v->list_cap);
+#if MQR_AB
     if (v->xcd_order)
         hipLaunchKernelGGL(k_xcd_order, dim3(1), dim3(1024), 0, v->stream, v->lists[p], v->ctr(p), v->list_cap,
                            v->table(p), v->lpt[p], om, reinterpret_cast<uint8_t*>(om + v->list_cap));
     else
+#endif
         hipLaunchKernelGGL(k_lpt_order, dim3(1), dim3(1024), 0, v->stream, v->lists[p], v->ctr(p), v->list_cap,
                            v->table(p).mask, v->lpt[p], om);
     MQR_CHECK_HIP(hipGetLastError());
@@ -318,7 +323,8 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
     //   0 default: k_integrate_lean -- R = 16: brick map, >= 8 waves per SIMD, 2 interleaved voxel
     //     chains; R = 8: plate map;  1 generic k_integrate (runtime R);  2 exact k_integrate_t;
     //   3 k_integrate_lean with the plate map (round-1 default, A/B);  5 k_integrate_lt (R = 16: depth
-    //     from packed LDS tiles, A/B).  DESIGN.md §4 has the measurements behind the choice.
+    //     from packed LDS tiles, A/B).  3 and 5 exist only in the A/B library (MQR_AB, vbg_ab.hpp).
+    //     DESIGN.md §4 has the measurements behind the choice.
     int var = v->kernel_variant;
     if (var != 1 && var != 2 && var != 3 && var != 5) var = 0;
     if (var != 1 && var != 2 && !lean_ok) var = 2;
@@ -336,6 +342,7 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
                                counters + kListCount, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp,
                                depth_frame, depth_scale, depth_max, sdf_trunc, first_new);
         } else {
+#if MQR_AB
             if (var == 5)
                 hipLaunchKernelGGL((k_integrate_lt<1>), dim3(grid), dim3(512), 0, s, list, lmask, v->bad[p], counters,
                                    v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp, depth_frame,
@@ -345,6 +352,7 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
                                    v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp,
                                    depth_frame, depth_max, sdf_trunc, first_new, grouped);
             else
+#endif
                 hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 8, 2>), dim3(lean_grid), dim3(512), 0, s, list,
                                    lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H,
                                    W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
@@ -938,6 +946,10 @@ int mqr_vbg_unpack_weighted(mqr_vbg* v, const int32_t* union_keys, int64_t U, co
 int mqr_vbg_set_variant(mqr_vbg* v, int variant) {
     MQR_REQUIRE(v, "null volume");
     if (sync_all(v)) return 1;
+    if (!MQR_AB && ((variant & 0xff) == 3 || (variant & 0xff) == 5 || (variant & 0x8000))) {
+        set_error("integrate variant " + std::to_string(variant) + " is an A/B kernel: only in tools/_ab/libmqr_ab.so (make ab)");
+        return 1;
+    }
     v->kernel_variant = variant & 0xff;
     v->pipelined = (variant & 0x100) == 0;  // bit 8: serialise touch and integrate (A/B of the overlap)
     v->lpt_order = (variant & 0x200) == 0;  // bit 9: integrate in touch order instead of longest-first

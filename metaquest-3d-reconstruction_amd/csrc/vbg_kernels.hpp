@@ -4,6 +4,9 @@
 #ifndef MQR_DIAG
 #define MQR_DIAG 0  // 1 / 2: timing-only builds of the lean kernel, 3 / 4 / 5 of the tile kernels (wrong results; never shipped)
 #endif
+#ifndef MQR_AB
+#define MQR_AB 0  // 1: the A/B kernels of vbg_ab.hpp (tools/_ab/libmqr_ab.so only)
+#endif
 #include <climits>
 
 #include "mqr_common.hpp"
@@ -529,113 +532,6 @@ __global__ __launch_bounds__(1024) void k_lpt_order(const int32_t* __restrict__ 
         out_mask[pos] = m;
     }
 }
-// XCD-grouped longest-first order (variant bit 0x8000, A/B; not the default).  Workgroups are
-// dispatched round-robin over the 8 XCDs (blockIdx % 8 labels the workgroups that share an XCD and
-// its L2; cdna_hip_programming.md T1), so a list in plain LPT order hands every XCD blocks from the
-// whole volume and each XCD's L2 fetches nearly every depth line of every frame of the batch
-// (traffic 2.7x the algorithmic bytes).  Here the batch's blocks are cut into 8 spatially compact
-// groups of equal work (popcount of the frame mask): Morton order of a 16^3 grid of cells over the
-// batch's bounding box, cut at the work octiles (a cell on a cut is split by arrival order).  Group
-// g is written to [off[g], off[g+1]) of `out` in longest-first order, and the integrate kernel runs
-// group g on the workgroups with blockIdx % 8 == g.  Traffic falls to 1.35x, but the launch is 13 %
-// slower: the kernel is bound by the gather address path, not by HBM, and the XCDs' shares of the
-// time do not balance.  One workgroup; `gbyte` is n bytes of scratch.
-__global__ __launch_bounds__(1024) void k_xcd_order(const int32_t* __restrict__ list, int* __restrict__ counters,
-                                                    int64_t list_cap, Table t, int32_t* __restrict__ out,
-                                                    bmask_t* __restrict__ out_mask, uint8_t* __restrict__ gbyte) {
-    constexpr int kCells = 4096;
-    __shared__ int cellw[kCells];   // work per cell, then the work before the cell in Morton order
-    __shared__ int cellrun[kCells]; // work of the cell's blocks placed so far
-    __shared__ int ghist[kNumGroups][kMaxBatch + 1];
-    __shared__ int bb[6];
-    __shared__ int wsum[1024 / 64];
-    const int n = (int)min((int64_t)counters[kListCount], list_cap);
-    const int tid = threadIdx.x;
-    for (int c = tid; c < kCells; c += blockDim.x) cellw[c] = cellrun[c] = 0;
-    for (int c = tid; c < kNumGroups * (kMaxBatch + 1); c += blockDim.x) (&ghist[0][0])[c] = 0;
-    if (tid < 3) bb[tid] = INT_MAX;
-    else if (tid < 6) bb[tid] = INT_MIN;
-    __syncthreads();
-    for (int i = tid; i < n; i += blockDim.x) {
-        int x, y, z;
-        unpack_key(t.keys[list[i]], x, y, z);
-        atomicMin(&bb[0], x), atomicMin(&bb[1], y), atomicMin(&bb[2], z);
-        atomicMax(&bb[3], x), atomicMax(&bb[4], y), atomicMax(&bb[5], z);
-    }
-    __syncthreads();
-    auto cell_of = [&](uint64_t key) {
-        int x, y, z;
-        unpack_key(key, x, y, z);
-        const int c[3] = {((x - bb[0]) * 16) / (bb[3] - bb[0] + 1), ((y - bb[1]) * 16) / (bb[4] - bb[1] + 1),
-                          ((z - bb[2]) * 16) / (bb[5] - bb[2] + 1)};
-        int code = 0;
-#pragma unroll
-        for (int b = 0; b < 4; ++b)
-#pragma unroll
-            for (int a = 0; a < 3; ++a) code |= ((c[a] >> b) & 1) << (3 * b + a);
-        return code;
-    };
-    for (int i = tid; i < n; i += blockDim.x) {
-        const int32_t s = list[i];
-        atomicAdd(&cellw[cell_of(t.keys[s])], __popcll(t.mask[s]));
-    }
-    __syncthreads();
-    // exclusive scan of the 4096 cell weights: 4 per thread, wave shuffles, then the 16 wave totals
-    int v4[4], acc = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        v4[k] = cellw[4 * tid + k];
-        acc += v4[k];
-    }
-    int incl = acc;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int u = __shfl_up(incl, o, 64);
-        if ((tid & 63) >= o) incl += u;
-    }
-    if ((tid & 63) == 63) wsum[tid >> 6] = incl;
-    __syncthreads();
-    int before = incl - acc;
-    for (int w = 0; w < (tid >> 6); ++w) before += wsum[w];
-    int total = 0;
-    for (int w = 0; w < 1024 / 64; ++w) total += wsum[w];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        cellw[4 * tid + k] = before;
-        before += v4[k];
-    }
-    __syncthreads();
-    for (int i = tid; i < n; i += blockDim.x) {
-        const int32_t s = list[i];
-        const int w = __popcll(t.mask[s]);
-        const int c = cell_of(t.keys[s]);
-        const int64_t start = (int64_t)cellw[c] + atomicAdd(&cellrun[c], w);
-        const int g = total > 0 ? (int)min<int64_t>(kNumGroups - 1, ((2 * start + w) * kNumGroups) / (2 * (int64_t)total)) : 0;
-        gbyte[i] = (uint8_t)g;
-        atomicAdd(&ghist[g][w], 1);
-    }
-    __syncthreads();
-    if (tid == 0) {  // group offsets, and within each group the longest-first positions
-        int pos = 0;
-        for (int g = 0; g < kNumGroups; ++g) {
-            counters[kGroupBase + g] = pos;
-            for (int c = kMaxBatch; c >= 0; --c) {
-                const int h = ghist[g][c];
-                ghist[g][c] = pos;
-                pos += h;
-            }
-        }
-        counters[kGroupBase + kNumGroups] = pos;
-    }
-    __syncthreads();
-    for (int i = tid; i < n; i += blockDim.x) {
-        const int32_t s = list[i];
-        const bmask_t m = t.mask[s];
-        const int pos = atomicAdd(&ghist[gbyte[i]][__popcll(m)], 1);
-        out[pos] = s;
-        out_mask[pos] = m;
-    }
-}
 
 // ---- lean integrate ------------------------------------------------------------------------------
 // The exact kernel's arithmetic with (i) shortened reciprocals, (ii) gathers through a raw buffer
@@ -761,32 +657,6 @@ __device__ __forceinline__ void hand_off(int32_t* bad_out, int* counters, int64_
     reinterpret_cast<bmask_t*>(bad_out + list_cap)[j] = mask;
 }
 
-// ---- helpers of the tiled kernel ------------------------------------------------------------------
-typedef __attribute__((address_space(1))) void gvoid_t;
-typedef __attribute__((address_space(3))) void lvoid_t;
-
-// Index of the j-th (from 0) set bit of m (m has more than j set bits).
-__device__ __forceinline__ int nth_bit(bmask_t m, int j) {
-    uint32_t w = (uint32_t)m;
-    int base = 0;
-    const int c = __popc(w);
-    if (j >= c) {
-        j -= c;
-        base = 32;
-        w = (uint32_t)(m >> 32);
-    }
-#pragma unroll
-    for (int s = 16; s >= 1; s >>= 1) {
-        const int cl = __popc(w & ((1u << s) - 1));
-        if (j >= cl) {
-            j -= cl;
-            w >>= s;
-            base += s;
-        }
-    }
-    return base;
-}
-
 // Thread -> voxels of the lean kernel.
 // MAP 0 (plate): thread t owns column (x, y) = (t % R, t / R % R), voxels z = t / R^2 + k NT / R^2;
 //   a wave's k-th voxels form a 16 x 4 x 1 plate (R = 16).
@@ -889,290 +759,6 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
                     pool_store(vox, voff, (R * lean_dy<R, NT, MAP>(k) + R2 * lean_dz<R, NT, MAP>(k)) * (int)sizeof(float2),
                                tw[k]);
             }
-        }
-        __syncthreads();
-        if (tid == 0) t.mask[slot] = 0;
-    }
-}
-
-// ---- tiled integrate (A/B, variant 5): depth read from LDS tiles instead of gathered from HBM ---------
-// The lean kernel is co-limited by the vector-memory address path (TA busy ~0.74 of the launch,
-// ~45 TCP tag lookups per 64-lane dword gather) and by VALU issue (~0.57).  Here the pixel rectangle
-// a block projects to in each frame -- its 8 corners projected with the kernel's own operations
-// (all voxels lie in their hull when every corner is in front of the camera), padded by 2 px,
-// clamped to the image, the left edge aligned down to 4 px -- is copied into LDS with 16-byte
-// LDS-DMA loads and the voxels read their depth from there.  Each rectangle gets only the LDS it
-// needs (pitch = its width rounded up to 4 px, size rounded up to one 64-lane copy instruction =
-// 256 floats; a 16^3 block of 5 mm voxels at 2 m covers ~22 x 22 px), and consecutive frames (bit
-// order) are packed into one half of a double buffer until it is full: one workgroup barrier per
-// group of frames, group g + 1 copied while group g is integrated.  Rectangles come from 8 waves at
-// once (frame j: wave j / 8, lanes (j % 8, corner)); the grouping is a greedy scan over a wave-wide
-// prefix sum of the tile sizes.  A frame whose rectangle exceeds 68 x 64 px, or whose corners leave
-// 2^-30 <= zc <= 2^50, uses the lean kernel's direct gathers; one outside the image is skipped.
-// Measured: TA busy 0.74 -> 0.12, but VALU +15 % (rectangles, the in-image test
-// where a rectangle touches the border) and 0.39 vs 0.34 ms per launch.  Earlier forms -- one tile
-// per frame with a barrier each (k_integrate_tb), packed f32 math at 6 waves / SIMD (k_integrate_tg)
-// -- were 0.40 ms and are gone.
-constexpr int kTBP = 68;                 // widest rectangle (px; 17 chunks of 4 px)
-constexpr int kTBH = 64;                 // tallest rectangle (rows)
-constexpr int kTGHalf = kTBP * kTBH;     // floats per half of the double buffer (17 KB): one worst-case tile
-constexpr int kTGSlots = kTGHalf / 256;  // 64-lane copy instructions per half
-
-struct TileShared {
-    __attribute__((aligned(16))) float tile[2][kTGHalf];
-    int4 rect[kMaxBatch];  // frame j of the block (bit order): u0, v0, width (0: outside the image,
-                           // -1: direct gathers), height | inner << 16 (1 px off every image edge)
-    int off[kMaxBatch];    // its tile's offset in its group's half (floats)
-    int fidx[kMaxBatch];   // its bit (batch frame)
-    int gstart[kMaxBatch + 1], gq[kMaxBatch];  // group g: first frame, copy instructions
-    uint8_t qf[kMaxBatch * kTGSlots];          // group g, instruction q -> frame
-    int ng;
-};
-
-// Rectangles and groups of one block's frames (call with the whole workgroup; ends on a barrier).
-__device__ __forceinline__ void tile_plan(TileShared& sh, bmask_t mask, int nf, int xb, int yb, int zb, int R,
-                                          float voxel_size, const FrameParams* __restrict__ fps, int H, int W) {
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    {
-        const int c = lane & 7, j = 8 * wave + (lane >> 3);
-        if (8 * wave < nf) {  // wave-uniform
-            const bool have = j < nf;
-            const int fb = have ? nth_bit(mask, j) : 0;
-            const FrameParams& fp = fps[fb];
-            const float cxs = (float)(xb * R + (c & 1) * (R - 1)) * voxel_size;
-            const float cys = (float)(yb * R + ((c >> 1) & 1) * (R - 1)) * voxel_size;
-            const float czs = (float)(zb * R + (c >> 2) * (R - 1)) * voxel_size;
-            const float xc = ((cxs * fp.ext[0] + cys * fp.ext[1]) + czs * fp.ext[2]) + fp.ext[3];
-            const float yc = ((cxs * fp.ext[4] + cys * fp.ext[5]) + czs * fp.ext[6]) + fp.ext[7];
-            const float zc = ((cxs * fp.ext[8] + cys * fp.ext[9]) + czs * fp.ext[10]) + fp.ext[11];
-            const float inv = rcp_m(zc);
-            const float u = fp.fx * xc * inv + fp.cx;
-            const float v = fp.fy * yc * inv + fp.cy;
-            int ok = zc >= 0x1p-30f && zc <= 0x1p50f && fabsf(u) < 1e6f && fabsf(v) < 1e6f;
-            float umin = u, umax = u, vmin = v, vmax = v;
-#pragma unroll
-            for (int o = 1; o <= 4; o <<= 1) {
-                umin = fminf(umin, __shfl_xor(umin, o, 64));
-                umax = fmaxf(umax, __shfl_xor(umax, o, 64));
-                vmin = fminf(vmin, __shfl_xor(vmin, o, 64));
-                vmax = fmaxf(vmax, __shfl_xor(vmax, o, 64));
-                ok &= __shfl_xor(ok, o, 64);
-            }
-            if (have && c == 0) {
-                int4 r = make_int4(0, 0, -1, 0);
-                if (ok) {
-                    const int u0 = max(0, (int)floorf(umin) - 2) & ~3, u1 = min(W - 1, (int)floorf(umax) + 2);
-                    const int v0 = max(0, (int)floorf(vmin) - 2), v1 = min(H - 1, (int)floorf(vmax) + 2);
-                    const int w = u1 - u0 + 1, h = v1 - v0 + 1;
-                    const bool inner = u0 >= 1 && u1 <= W - 2 && v0 >= 1 && v1 <= H - 2;
-                    if (w <= 0 || h <= 0)
-                        r = make_int4(0, 0, 0, 0);
-                    else if (w <= kTBP && h <= kTBH)
-                        r = make_int4(u0, v0, w, h | (inner ? 0x10000 : 0));
-                }
-                sh.rect[j] = r;
-                sh.fidx[j] = fb;
-            }
-        }
-    }
-    __syncthreads();
-    if (wave == 0) {  // lane = frame; greedy groups over the prefix sum of tile sizes
-        const int4 r = lane < nf ? sh.rect[lane] : make_int4(0, 0, 0, 0);
-        const int A = r.z > 0 ? ((((r.w & 0xffff) * ((r.z + 3) >> 2)) + 63) >> 6) << 8 : 0;  // <= kTGHalf
-        int P = A;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int u = __shfl_up(P, o, 64);
-            if (lane >= o) P += u;
-        }
-        int s = 0, base = 0, g = 0, grp = 0, off = 0;
-        while (s < nf) {  // wave-uniform; every group takes at least frame s (A_s <= kTGHalf)
-            const uint64_t b = __ballot(lane >= s && lane < nf && P - base <= kTGHalf);
-            const int e = 64 - __builtin_clzll(b);
-            if (lane >= s && lane < e) {
-                grp = g;
-                off = P - A - base;
-            }
-            const int end = __shfl(P, e - 1, 64);
-            if (lane == 0) {
-                sh.gstart[g] = s;
-                sh.gq[g] = (end - base) >> 8;
-            }
-            base = end;
-            s = e;
-            ++g;
-        }
-        if (lane == 0) {
-            sh.gstart[g] = nf;
-            sh.ng = g;
-        }
-        if (lane < nf) {
-            sh.off[lane] = off;
-            for (int q = 0; q < (A >> 8); ++q) sh.qf[grp * kTGSlots + (off >> 8) + q] = (uint8_t)lane;
-        }
-    }
-    __syncthreads();
-}
-
-// Copy of group g into half g & 1: instruction q (wave-uniform) covers 64 consecutive 4-px chunks of
-// one frame's tile; chunks past the tile's last row re-read its row 0 into the unused tail.
-__device__ __forceinline__ void tile_stage(TileShared& sh, int g, const float* __restrict__ depths, int64_t HW, int W,
-                                           const int64_t* __restrict__ depth_frame) {
-#if MQR_DIAG == 4 || MQR_DIAG == 5  // timing diagnostics only: no tile copies
-    return;
-#endif
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, nwaves = blockDim.x >> 6;
-    const int Q = __builtin_amdgcn_readfirstlane(sh.gq[g]);
-    float* half = sh.tile[g & 1];
-    for (int q = wave; q < Q; q += nwaves) {
-        const int j = __builtin_amdgcn_readfirstlane(sh.qf[g * kTGSlots + q]);
-        const int4 r = sh.rect[j];
-        const int u0 = __builtin_amdgcn_readfirstlane(r.x), v0 = __builtin_amdgcn_readfirstlane(r.y);
-        const int pq = (__builtin_amdgcn_readfirstlane(r.z) + 3) >> 2;
-        const int h = __builtin_amdgcn_readfirstlane(r.w) & 0xffff;
-        const int fb = __builtin_amdgcn_readfirstlane(sh.fidx[j]);
-        const int c = (q - (__builtin_amdgcn_readfirstlane(sh.off[j]) >> 8)) * 64 + lane;
-        int row = (int)(((float)c + 0.5f) * __builtin_amdgcn_rcpf((float)pq));  // c / pq (c < 1088)
-        const int col = c - row * pq;
-        row = row < h ? row : 0;
-        const float* dep = depths + depth_frame[fb] * HW;
-        const int gc = min(u0 + 4 * col, W - 4);
-        __builtin_amdgcn_global_load_lds((gvoid_t*)(dep + (int64_t)(v0 + row) * W + gc), (lvoid_t*)(half + 256 * q),
-                                         16, 0, 0);
-    }
-}
-
-// Per voxel: Open3D's projection (the same operations as lean_gather), then the tile read; a voxel
-// in the image but outside its frame's rectangle sets `bad` (the block is redone exactly), one
-// outside the image reads 0 (as lean_gather's past-the-end read).  Every corner of the block has
-// 2^-30 <= zc <= 2^50 when a frame has a rectangle, so the voxels' 1 / zc by rcp_m is exact without
-// lean_gather's per-voxel range check.  INNER: the rectangle keeps 1 px off every image edge, so a
-// voxel inside it is inside the image (no bound test).
-template <int ZPER, int ILP, bool INNER>
-__device__ __forceinline__ void lean_gather_tile(float (&dv)[ZPER], bool& bad, const FrameParams& fp,
-                                                 const float* tile, int rx, int ry, uint32_t tw, uint32_t th,
-                                                 uint32_t pitch, const float (&xs)[ZPER], const float (&ys)[ZPER],
-                                                 const float (&zs)[ZPER], float hm1, float wm1) {
-    float e[12];
-#pragma unroll
-    for (int j = 0; j < 12; ++j) e[j] = fp.ext[j];
-    const float fx = fp.fx, fy = fp.fy, cx = fp.cx, cy = fp.cy;
-#pragma unroll
-    for (int k = 0; k < ZPER; ++k) {
-        const float ax = xs[k] * e[0] + ys[k] * e[1];
-        const float ay = xs[k] * e[4] + ys[k] * e[5];
-        const float az = xs[k] * e[8] + ys[k] * e[9];
-        const float xc = (ax + zs[k] * e[2]) + e[3];
-        const float yc = (ay + zs[k] * e[6]) + e[7];
-        const float zc = (az + zs[k] * e[10]) + e[11];
-        const float inv_z = rcp_m(zc);
-        const float u = fx * xc * inv_z + cx;
-        const float v = fy * yc * inv_z + cy;
-        const uint32_t tu = (uint32_t)((int)u - rx), tv = (uint32_t)((int)v - ry);
-        const bool hit = (tu < tw) & (tv < th);
-#if MQR_DIAG == 3 || MQR_DIAG == 5
-        const float d = zc + (float)((hit ? __umul24(tv, pitch) + tu : 0) & 1u) * 1e-30f;
-#else
-        const float d = tile[hit ? __umul24(tv, pitch) + tu : 0];
-#endif
-        if (INNER) {
-            bad |= !hit;
-            dv[k] = d;
-        } else {
-            const bool in = (v >= 0) & (u >= 0) & (v <= hm1) & (u <= wm1);
-            bad |= in & !hit;
-            dv[k] = in ? d : 0.f;
-        }
-        if ((k + 1) % ILP == 0) __builtin_amdgcn_sched_barrier(0);
-    }
-}
-
-template <int ILP>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_integrate_lt(
-    const int32_t* __restrict__ list, const bmask_t* __restrict__ lmask, int32_t* __restrict__ bad_out,
-    int* __restrict__ counters, int64_t list_cap, Table t, float2* __restrict__ pool, float voxel_size,
-    const float* __restrict__ depths, int64_t HW, int H, int W, const FrameParams* __restrict__ fps,
-    const int64_t* __restrict__ depth_frame, float depth_max, float sdf_trunc, int first_new) {
-    constexpr int R = 16, R2 = R * R, R3 = R2 * R, NT = 512, ZPER = R3 / NT, MAP = 1;
-    __shared__ TileShared sh;
-    const int64_t n = min((int64_t)counters[kListCount], list_cap);
-    const float hf = (float)H, hm1 = (float)H - 1.0f, wm1 = (float)W - 1.0f;
-    const uint32_t W4 = 4u * (uint32_t)W, bytes = 4u * (uint32_t)HW;
-    const float y0t = __builtin_amdgcn_rcpf(sdf_trunc);
-    const float y1t = __builtin_fmaf(__builtin_fmaf(-sdf_trunc, y0t, 1.0f), y0t, y0t);
-    const int tid = threadIdx.x;
-    int vx, vy, vz;
-    lean_map<R, NT, MAP>(tid, vx, vy, vz);
-    const uint32_t voff = 8u * (uint32_t)(vx + R * vy + R2 * vz);
-    for (int64_t i = blockIdx.x; i < n; i += gridDim.x) {
-        const int32_t slot = list[i];
-        const int buf = __builtin_amdgcn_readfirstlane(t.vals[slot]);
-        const bmask_t mask = readfirstlane_u64(lmask ? lmask[i] : t.mask[slot]);
-        int xb, yb, zb;
-        unpack_key(t.keys[slot], xb, yb, zb);
-        if (buf < 0 || !mask) {  // block-uniform
-            __syncthreads();
-            if (tid == 0) t.mask[slot] = 0;
-            continue;
-        }
-        const __amdgpu_buffer_rsrc_t vox = __builtin_amdgcn_make_buffer_rsrc(
-            pool + (int64_t)buf * R3, (short)0, (int)(R3 * sizeof(float2)), 0x00020000);
-        float2 tw[ZPER];
-        float xs[ZPER], ys[ZPER], zs[ZPER];
-        bool bad = false;
-        const float xs0 = (float)(xb * R + vx) * voxel_size;
-#pragma unroll
-        for (int k = 0; k < ZPER; ++k) {
-            const int dy = lean_dy<R, NT, MAP>(k), dz = lean_dz<R, NT, MAP>(k);
-            tw[k] = buf >= first_new ? make_float2(0.f, 0.f)
-                                     : pool_load(vox, voff, (R * dy + R2 * dz) * (int)sizeof(float2));
-            xs[k] = xs0;
-            ys[k] = (float)(yb * R + vy + dy) * voxel_size;
-            zs[k] = (float)(zb * R + vz + dz) * voxel_size;
-            const float w = tw[k].y;  // rcp_m(w + 1) needs integer weights (a batch adds <= 64)
-            bad |= !(w >= 0.0f && w <= 0x1p23f && w == __builtin_truncf(w));
-        }
-        tile_plan(sh, mask, __popcll(mask), xb, yb, zb, R, voxel_size, fps, H, W);
-        const int ng = __builtin_amdgcn_readfirstlane(sh.ng);
-        tile_stage(sh, 0, depths, HW, W, depth_frame);
-        bmask_t m = mask;
-        for (int g = 0; g < ng; ++g) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's copies of group g have landed
-            __syncthreads();  // ... every wave's; and every wave is done with group g - 1's half
-            if (g + 1 < ng) tile_stage(sh, g + 1, depths, HW, W, depth_frame);
-            const float* half = sh.tile[g & 1];
-            const int j1 = __builtin_amdgcn_readfirstlane(sh.gstart[g + 1]);
-            for (int j = __builtin_amdgcn_readfirstlane(sh.gstart[g]); j < j1; ++j) {
-                const int f = __builtin_ctzll(m);
-                m &= m - 1;
-                int4 r = sh.rect[j];
-                r = make_int4(__builtin_amdgcn_readfirstlane(r.x), __builtin_amdgcn_readfirstlane(r.y),
-                              __builtin_amdgcn_readfirstlane(r.z), __builtin_amdgcn_readfirstlane(r.w));
-                if (r.z == 0) continue;  // the block is outside this frame's image
-                float dv[ZPER];
-                if (r.z > 0) {
-                    const float* tile = half + __builtin_amdgcn_readfirstlane(sh.off[j]);
-                    const uint32_t pitch = (uint32_t)((r.z + 3) & ~3);
-                    if (r.w >> 16)
-                        lean_gather_tile<ZPER, ILP, true>(dv, bad, fps[f], tile, r.x, r.y, (uint32_t)r.z,
-                                                          (uint32_t)(r.w & 0xffff), pitch, xs, ys, zs, hm1, wm1);
-                    else
-                        lean_gather_tile<ZPER, ILP, false>(dv, bad, fps[f], tile, r.x, r.y, (uint32_t)r.z,
-                                                           (uint32_t)(r.w & 0xffff), pitch, xs, ys, zs, hm1, wm1);
-                } else {
-                    lean_gather<ZPER, ILP>(dv, bad, fps[f], frame_rsrc(depths + depth_frame[f] * HW, bytes), xs, ys,
-                                           zs, W4, hf, hm1, wm1);
-                }
-                lean_update<ZPER, ILP>(tw, dv, fps[f], xs, ys, zs, depth_max, sdf_trunc, y1t);
-            }
-        }
-        if (__syncthreads_or(bad)) {  // block-uniform: the exact fix-up launch redoes it from the pool
-            if (tid == 0) hand_off(bad_out, counters, list_cap, slot, mask);
-        } else {
-#pragma unroll
-            for (int k = 0; k < ZPER; ++k)
-                pool_store(vox, voff, (R * lean_dy<R, NT, MAP>(k) + R2 * lean_dz<R, NT, MAP>(k)) * (int)sizeof(float2),
-                           tw[k]);
         }
         __syncthreads();
         if (tid == 0) t.mask[slot] = 0;

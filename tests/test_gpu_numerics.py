@@ -1,6 +1,7 @@
 """Exhaustive check that the device's division shortcut is bit-identical to IEEE float division,
 and that the R-specialised integrate kernel equals the generic one bit for bit."""
 import ctypes
+import os
 
 import numpy as np
 import pytest
@@ -44,7 +45,12 @@ def test_shortened_reciprocals_exact(which, lo, hi):
     assert mm == 0, f"mode {which}: {mm} mismatches, first bit pattern {first:#x}"
 
 
-INTEGRATE_VARIANTS = {16: (0, 2, 3, 5, 0x100, 0x200, 0x400, 0x105, 0x605, 0x800, 0x8000, 0x8003), 8: (0, 2, 0x100, 0x8000)}
+# MQR_AB_TEST=1 (tests/test_gpu_ab_variants.py, with MQR_HIP_LIB = tools/_ab/libmqr_ab.so): the integrate
+# tests below also cover the A/B kernels the shipped library leaves out (variants 3 and 5, bit 0x8000)
+AB = os.environ.get("MQR_AB_TEST") == "1"
+INTEGRATE_VARIANTS = {16: (0, 2, 0x100, 0x200, 0x400, 0x800), 8: (0, 2, 0x100)}
+if AB:
+    INTEGRATE_VARIANTS = {16: (0, 3, 5, 0x105, 0x605, 0x8000, 0x8003), 8: (0, 0x8000)}
 
 
 def test_specialised_integrate_equals_generic():
@@ -106,7 +112,7 @@ def test_fast_integrate_exact_fallback():
     for d in depth_mm:
         d[::7, ::5] = np.float32(1e-30)   # in-image, > 0, below 2^-60: exact division path
     out = []
-    cases = ((16, 1), (16, 0), (16, 2), (16, 5), (8, 1), (8, 0), (8, 2))
+    cases = ((16, 1), (16, 0), (16, 2), (16, 5 if AB else 0x100), (8, 1), (8, 0), (8, 2))
     for R, variant in cases:
         v = VoxelBlockGrid(voxel_size=0.01, block_resolution=R, block_count=64)
         _lib.call("mqr_vbg_set_variant", v.handle, variant)
@@ -146,7 +152,7 @@ def test_lean_integrate_exact_fallback():
     depths = [near] + [np.asarray(d, np.float32) for d in seq["depth"]]
     Ks = np.concatenate([seq["K"][:1], seq["K"]])
     Ts = np.concatenate([np.eye(4)[None], seq["T_wc"]])
-    cases = ((16, 1), (16, 0), (16, 5), (16, 2), (16, 0x100), (8, 1), (8, 0), (8, 2))
+    cases = ((16, 1), (16, 0), (16, 5 if AB else 0x200), (16, 2), (16, 0x100), (8, 1), (8, 0), (8, 2))
     out = []
     for R, variant in cases:
         v = VoxelBlockGrid(voxel_size=0.005, block_resolution=R, block_count=64)

@@ -2,6 +2,7 @@
 """Interleaved A/B of integrate-kernel variants on the bench workload (one process, same data).
 
 python tools/ab_integrate.py --variants 0,5 --rounds 5
+(variants 3 and 5 and bit 0x8000 need the A/B library: MQR_HIP_LIB=tools/_ab/libmqr_ab.so)
 Prints per-variant median integrate-kernel ms per launch, touch ms, and step ms.
 """
 import argparse

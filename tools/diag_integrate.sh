@@ -14,7 +14,7 @@ if [ "$1" = build ]; then
   for d in ${DIAGS:-1 2}; do
     tmp=$(mktemp -d)
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -fPIC -std=c++17 -I"$ROOT/include" \
-      -fno-slp-vectorize -DMQR_DIAG=$d -c "$CSRC/vbg.hip" -o "$tmp/vbg.o" || exit 1
+      -fno-slp-vectorize -DMQR_AB=1 -DMQR_DIAG=$d -c "$CSRC/vbg.hip" -o "$tmp/vbg.o" || exit 1
     objs=$(ls "$CSRC"/build/*.o | grep -v "/vbg.o$")
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$ROOT/tools/_diag/libmqr_diag$d.so" "$tmp/vbg.o" $objs \
       -Wl,-rpath,/opt/rocm/lib -ldl || exit 1
