@@ -691,6 +691,22 @@ __device__ inline void mc_edge_full(const int32_t* __restrict__ nbrow, const flo
     ne[2] = v[11] - v[12];
 }
 
+// The k-th output of a row whose outputs are ordered by (x, axis) with per-axis bit rows ex / ey /
+// ez: x = the largest x with (outputs below x) <= k, by binary search on prefix popcounts; k becomes
+// the rank of the output among voxel x's axes.
+template <int R>
+__device__ __forceinline__ void row_select(uint32_t ex, uint32_t ey, uint32_t ez, int& k, int& x) {
+    auto below = [&](int c) {
+        const uint32_t low = (1u << c) - 1;
+        return __popc(ex & low) + __popc(ey & low) + __popc(ez & low);
+    };
+    x = 0;
+#pragma unroll
+    for (int st = R / 2; st >= 1; st >>= 1)
+        if (below(x + st) <= k) x += st;
+    k -= below(x);
+}
+
 // Global vertex id of the edge owned by voxel (ox, oy, oz) (may lie in a +x/+y/+z neighbour) along axis.
 __device__ inline int32_t mc_vid(uint32_t vbase, uint32_t ex, uint32_t ey, uint32_t ez, int x, int axis) {
     const uint32_t low = (1u << x) - 1;
@@ -710,15 +726,23 @@ __global__ __launch_bounds__(kMcThreads) void k_mc_emit(const int32_t* __restric
                                                         const int32_t* __restrict__ toff,
                                                         const uint4* __restrict__ rows4,
                                                         const uint32_t* __restrict__ rowNt, float* pos, float* nrm,
-                                                        int32_t* tri) {
+                                                        int32_t* tri, int64_t cap_v, int64_t cap_t) {
     using M = Mc<R, 1>;
+    static_assert(kMcThreads >= 256, "one thread per triangle-table row");
     __shared__ uint32_t rowN[M::S2];
     __shared__ uint4 rows[M::R2];  // vbase, tbase, ex | ey << 16, ez | oc << 16
     __shared__ int32_t nbrow[27], nbvoff[27];
+    __shared__ uint64_t triP[256];  // the triangle tables: lane-divergent lookups in a dependent loop
+    __shared__ uint32_t triC[32];
     const int64_t b = blockIdx.x;
     const int nvb = vcount[b], ntb = tcount[b];
     if (nvb == 0 && ntb == 0) return;  // block-uniform: nothing to write
+    const int32_t vb0 = voff[b], tb0 = toff[b];
+    // outputs past the speculative capacity: the host re-runs this pass into exact buffers
+    if ((int64_t)vb0 + nvb > cap_v || (int64_t)tb0 + ntb > cap_t) return;
     const int tid = threadIdx.x;
+    triP[tid] = mqr_tri_packed[tid];
+    if (tid < 32) triC[tid] = mqr_tri_count_packed[tid];
     if (tid < 27) {
         const int32_t q = nb[b * 27 + tid];
         nbrow[tid] = q;
@@ -733,7 +757,6 @@ __global__ __launch_bounds__(kMcThreads) void k_mc_emit(const int32_t* __restric
 
     int xb, yb, zb;
     unpack_key(bkeys[b], xb, yb, zb);
-    const int32_t vb0 = voff[b], tb0 = toff[b];
     for (int i = tid; i < nvb; i += blockDim.x) {
         int lo = 0, hi = M::R2 - 1;  // last row whose vertex base is <= i (non-empty)
         while (lo < hi) {
@@ -742,12 +765,8 @@ __global__ __launch_bounds__(kMcThreads) void k_mc_emit(const int32_t* __restric
         }
         const uint4 rw = rows[lo];
         const uint32_t ex = rw.z & 0xffffu, ey = rw.z >> 16, ez = rw.w & 0xffffu;
-        int k = i - (int)rw.x, x = 0;
-        for (; x < R; ++x) {
-            const int c = (int)(((ex >> x) & 1u) + ((ey >> x) & 1u) + ((ez >> x) & 1u));
-            if (k < c) break;
-            k -= c;
-        }
+        int k = i - (int)rw.x, x;
+        row_select<R>(ex, ey, ez, k, x);
         const uint32_t m3 = ((ex >> x) & 1u) | (((ey >> x) & 1u) << 1) | (((ez >> x) & 1u) << 2);
         const int y = lo % R, z = lo / R;
         float tsdf_o, tsdf_e;
@@ -798,12 +817,12 @@ __global__ __launch_bounds__(kMcThreads) void k_mc_emit(const int32_t* __restric
         while (oc) {
             x = __builtin_ctz(oc);
             ci = mc_index(a >> (x + 1), bb >> (x + 1), c >> (x + 1), d >> (x + 1));
-            const int n = mc_tri_count(ci);
+            const int n = (int)((triC[ci >> 3] >> ((ci & 7) * 4)) & 0xFu);
             if (k < n) break;
             k -= n;
             oc &= oc - 1;
         }
-        const uint64_t te = mqr_tri_packed[ci] >> (12 * k);
+        const uint64_t te = triP[ci] >> (12 * k);
         const int64_t t = (int64_t)tb0 + i;
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
@@ -888,13 +907,15 @@ __global__ __launch_bounds__(kMcThreads) void k_pt_emit(const int32_t* __restric
                                                         const float2* __restrict__ pool, float voxel_size,
                                                         const int32_t* __restrict__ count,
                                                         const int32_t* __restrict__ off,
-                                                        const uint4* __restrict__ rows4, float* pos, float* nrm) {
+                                                        const uint4* __restrict__ rows4, float* pos, float* nrm,
+                                                        int64_t cap) {
     using M = Mc<R, 1>;
     __shared__ uint4 rows[M::R2];
     __shared__ int32_t nbrow[27];
     const int64_t b = blockIdx.x;
     const int npb = count[b];
     if (npb == 0) return;  // block-uniform
+    if ((int64_t)off[b] + npb > cap) return;  // past the speculative capacity (the host re-runs)
     const int tid = threadIdx.x;
     if (tid < 27) nbrow[tid] = nb[b * 27 + tid];
     for (int r = tid; r < M::R2; r += blockDim.x) rows[r] = rows4[b * M::R2 + r];
@@ -912,12 +933,8 @@ __global__ __launch_bounds__(kMcThreads) void k_pt_emit(const int32_t* __restric
         }
         const uint4 rw = rows[lo];
         const uint32_t ex = rw.y & 0xffffu, ey = rw.y >> 16, ez = rw.z;
-        int k = i - (int)rw.x, x = 0;
-        for (; x < R; ++x) {
-            const int c = (int)(((ex >> x) & 1u) + ((ey >> x) & 1u) + ((ez >> x) & 1u));
-            if (k < c) break;
-            k -= c;
-        }
+        int k = i - (int)rw.x, x;
+        row_select<R>(ex, ey, ez, k, x);
         const uint32_t m3 = ((ex >> x) & 1u) | (((ey >> x) & 1u) << 1) | (((ez >> x) & 1u) << 2);
         const int y = lo % R, z = lo / R;
         float t_o, t_i;
@@ -1026,55 +1043,87 @@ __global__ __launch_bounds__(kThreads) void k_points(const int32_t* __restrict__
 
 // Exclusive scans of the two per-block count arrays (vertices, triangles) in one workgroup of
 // kScanThreads; totals[0..1] = the sums.  (Two hipcub scans cost ~20 us of launches at these sizes.)
-constexpr int kScanThreads = 1024;
+// Tiles of kScanTile counts: coalesced loads, all of a thread's in flight, staged in LDS; each
+// thread scans kScanPer consecutive counts, wave and workgroup scans of the thread sums; results
+// back through LDS to coalesced stores; a running carry between tiles.
+constexpr int kScanThreads = 1024, kScanPer = 8, kScanTile = kScanThreads * kScanPer;
 __global__ __launch_bounds__(kScanThreads) void k_scan_counts(const int32_t* __restrict__ c0,
                                                               const int32_t* __restrict__ c1, int64_t n,
                                                               int32_t* __restrict__ o0, int32_t* __restrict__ o1,
                                                               int64_t* __restrict__ totals) {
+    __shared__ int32_t t0[kScanTile], t1[kScanTile];
     __shared__ int64_t ws0[kScanThreads / 64], ws1[kScanThreads / 64];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int64_t chunk = (n + kScanThreads - 1) / kScanThreads;
-    const int64_t lo = min(n, tid * chunk), hi = min(n, lo + chunk);
-    int64_t s0 = 0, s1 = 0;
-    for (int64_t i = lo; i < hi; ++i) {
-        s0 += c0[i];
-        if (c1) s1 += c1[i];
-    }
-    int64_t i0 = s0, i1 = s1;  // inclusive wave scans
+    const bool two = c1 != nullptr;
+    int64_t carry0 = 0, carry1 = 0;
+    for (int64_t base = 0; base < n; base += kScanTile) {
+        int32_t v0[kScanPer], v1[kScanPer];
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const int64_t a = __shfl_up(i0, d, 64), b = __shfl_up(i1, d, 64);
-        if (lane >= d) {
-            i0 += a;
-            i1 += b;
+        for (int k = 0; k < kScanPer; ++k) {
+            const int64_t i = base + k * kScanThreads + tid;
+            v0[k] = i < n ? c0[i] : 0;
+            v1[k] = two && i < n ? c1[i] : 0;
         }
-    }
-    if (lane == 63) {
-        ws0[wave] = i0;
-        ws1[wave] = i1;
-    }
-    __syncthreads();
-    int64_t b0 = 0, b1 = 0, t0 = 0, t1 = 0;
-    for (int w = 0; w < kScanThreads / 64; ++w) {
-        if (w < wave) {
-            b0 += ws0[w];
-            b1 += ws1[w];
+#pragma unroll
+        for (int k = 0; k < kScanPer; ++k) {
+            t0[k * kScanThreads + tid] = v0[k];
+            t1[k * kScanThreads + tid] = v1[k];
         }
-        t0 += ws0[w];
-        t1 += ws1[w];
-    }
-    int64_t r0 = b0 + i0 - s0, r1 = b1 + i1 - s1;  // exclusive prefix of this thread's chunk
-    for (int64_t i = lo; i < hi; ++i) {
-        o0[i] = (int32_t)r0;
-        r0 += c0[i];
-        if (c1) {
-            o1[i] = (int32_t)r1;
-            r1 += c1[i];
+        __syncthreads();
+        int64_t s0 = 0, s1 = 0;
+#pragma unroll
+        for (int k = 0; k < kScanPer; ++k) {
+            s0 += t0[tid * kScanPer + k];
+            s1 += t1[tid * kScanPer + k];
         }
+        int64_t i0 = s0, i1 = s1;  // inclusive wave scans of the thread sums
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int64_t a = __shfl_up(i0, d, 64), b = __shfl_up(i1, d, 64);
+            if (lane >= d) {
+                i0 += a;
+                i1 += b;
+            }
+        }
+        if (lane == 63) {
+            ws0[wave] = i0;
+            ws1[wave] = i1;
+        }
+        __syncthreads();
+        int64_t b0 = carry0, b1 = carry1, tot0 = 0, tot1 = 0;
+        for (int w = 0; w < kScanThreads / 64; ++w) {
+            if (w < wave) {
+                b0 += ws0[w];
+                b1 += ws1[w];
+            }
+            tot0 += ws0[w];
+            tot1 += ws1[w];
+        }
+        int64_t r0 = b0 + i0 - s0, r1 = b1 + i1 - s1;  // exclusive prefix of this thread's counts
+#pragma unroll
+        for (int k = 0; k < kScanPer; ++k) {
+            const int32_t a = t0[tid * kScanPer + k], b = t1[tid * kScanPer + k];
+            t0[tid * kScanPer + k] = (int32_t)r0;
+            t1[tid * kScanPer + k] = (int32_t)r1;
+            r0 += a;
+            r1 += b;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kScanPer; ++k) {
+            const int64_t i = base + k * kScanThreads + tid;
+            if (i < n) {
+                o0[i] = t0[k * kScanThreads + tid];
+                if (two) o1[i] = t1[k * kScanThreads + tid];
+            }
+        }
+        carry0 += tot0;
+        carry1 += tot1;
+        __syncthreads();  // the tile buffers and wave sums are reused
     }
     if (tid == 0) {
-        totals[0] = t0;
-        totals[1] = t1;
+        totals[0] = carry0;
+        totals[1] = carry1;
     }
 }
 
@@ -1210,6 +1259,11 @@ static int build_nb(mqr_vbg* v, int32_t* nb) {
     return 0;
 }
 
+// Speculative output capacity from the volume's previous extraction (0 = none yet: the host waits
+// for the totals before emitting).  The margin absorbs the growth between two extractions of a
+// volume that is still being integrated.
+static int64_t spec_cap(int64_t hint) { return hint > 0 ? hint + hint / 4 + 4096 : 0; }
+
 template <int RT>
 static int mesh_passes(mqr_vbg* v, float thr, const ExScratch& e, mqr_geom* g, int64_t tri_blocks) {
     const int64_t n = v->pool_count;
@@ -1226,26 +1280,48 @@ static int mesh_passes(mqr_vbg* v, float thr, const ExScratch& e, mqr_geom* g, i
         hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(kScanThreads), 0, v->stream, e.c0, e.c1, n, e.o0, e.o1, tot);
         MQR_CHECK_HIP(hipGetLastError());
         MQR_CHECK_HIP(hipMemcpyAsync(v->h_ex, tot, 2 * sizeof(int64_t), hipMemcpyDeviceToHost, v->stream));
+        // With a previous extraction's counts, emit into buffers of that size (+ margin) without
+        // waiting for this one's totals; blocks past the capacity write nothing and the pass is re-run
+        // into exact buffers if the totals exceed it.  Without, wait for the totals first.
+        int64_t cv = spec_cap(v->ex_hint[0]), ct = spec_cap(v->ex_hint[1]);
+        bool emitted = false;
+        if (cv > 0 && ct > 0) {
+            if (alloc_geom(g, cv, ct)) return 1;
+            hipLaunchKernelGGL(k_mc_emit<RT>, dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, e.nb, v->bkeys,
+                               v->pool, v->voxel_size, e.c0, e.c1, e.o0, e.o1, rows4, rowNt, g->pos, g->nrm, g->tri, cv,
+                               ct);
+            MQR_CHECK_HIP(hipGetLastError());
+            emitted = true;
+        }
         MQR_CHECK_HIP(hipStreamSynchronize(v->stream));
         nv = v->h_ex[0];
         nt = v->h_ex[1];
+        MQR_REQUIRE(nv < (int64_t)1 << 31 && nt < (int64_t)1 << 31, "mesh exceeds int32 vertex / triangle ids");
+        v->ex_hint[0] = nv;
+        v->ex_hint[1] = nt;
+        g->nv = nv;
+        g->nt = nt;
+        if (emitted && nv <= cv && nt <= ct) return 0;
+        if (g->blk) {
+            geom_block_release(g->device, g->blk, g->blk_cap);
+            g->blk = nullptr;
+        }
+        if (alloc_geom(g, nv, nt)) return 1;
+        hipLaunchKernelGGL(k_mc_emit<RT>, dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, e.nb, v->bkeys, v->pool,
+                           v->voxel_size, e.c0, e.c1, e.o0, e.o1, rows4, rowNt, g->pos, g->nrm, g->tri, nv, nt);
     } else {
         if (build_nb(v, e.nb)) return 1;
         hipLaunchKernelGGL(k_mesh_count<RT>, dim3((unsigned)n), dim3(kThreads), 0, v->stream, e.nb, n, v->pool, v->R,
                            thr, e.c0, e.c1, e.faces);
         MQR_CHECK_HIP(hipGetLastError());
         if (scan_totals(v, e, n, 2, &nv, &nt)) return 1;
-    }
-    MQR_REQUIRE(nv < (int64_t)1 << 31 && nt < (int64_t)1 << 31, "mesh exceeds int32 vertex / triangle ids");
-    g->nv = nv;
-    g->nt = nt;
-    if (alloc_geom(g, nv, nt)) return 1;
-    if constexpr (RT > 0)
-        hipLaunchKernelGGL(k_mc_emit<RT>, dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, e.nb, v->bkeys, v->pool,
-                           v->voxel_size, e.c0, e.c1, e.o0, e.o1, rows4, rowNt, g->pos, g->nrm, g->tri);
-    else
+        MQR_REQUIRE(nv < (int64_t)1 << 31 && nt < (int64_t)1 << 31, "mesh exceeds int32 vertex / triangle ids");
+        g->nv = nv;
+        g->nt = nt;
+        if (alloc_geom(g, nv, nt)) return 1;
         hipLaunchKernelGGL(k_mesh_emit<RT>, dim3((unsigned)n), dim3(kThreads), 0, v->stream, e.nb, n, v->bkeys,
                            v->pool, v->R, v->voxel_size, thr, e.c0, e.c1, e.o0, e.o1, e.faces, g->pos, g->nrm, g->tri);
+    }
     MQR_CHECK_HIP(hipGetLastError());
     MQR_CHECK_HIP(hipStreamSynchronize(v->stream));
     return 0;
@@ -1266,23 +1342,38 @@ static int point_passes(mqr_vbg* v, float thr, const ExScratch& e, mqr_geom* g) 
                            e.o0, (int32_t*)nullptr, tot);
         MQR_CHECK_HIP(hipGetLastError());
         MQR_CHECK_HIP(hipMemcpyAsync(v->h_ex, tot, sizeof(int64_t), hipMemcpyDeviceToHost, v->stream));
+        const int64_t cp = spec_cap(v->ex_hint[2]);  // speculative capacity, as in mesh_passes
+        if (cp > 0) {
+            if (alloc_geom(g, cp, 0)) return 1;
+            hipLaunchKernelGGL(k_pt_emit<RT>, dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, e.nb, v->bkeys,
+                               v->pool, v->voxel_size, e.c0, e.o0, reinterpret_cast<const uint4*>(e.faces), g->pos,
+                               g->nrm, cp);
+            MQR_CHECK_HIP(hipGetLastError());
+        }
         MQR_CHECK_HIP(hipStreamSynchronize(v->stream));
         np = v->h_ex[0];
+        MQR_REQUIRE(np < (int64_t)1 << 31, "point cloud exceeds int32 offsets");
+        v->ex_hint[2] = np;
+        g->nv = np;
+        if (cp > 0 && np <= cp) return 0;
+        if (g->blk) {
+            geom_block_release(g->device, g->blk, g->blk_cap);
+            g->blk = nullptr;
+        }
+        if (alloc_geom(g, np, 0)) return 1;
+        hipLaunchKernelGGL(k_pt_emit<RT>, dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, e.nb, v->bkeys, v->pool,
+                           v->voxel_size, e.c0, e.o0, reinterpret_cast<const uint4*>(e.faces), g->pos, g->nrm, np);
     } else {
         if (build_nb(v, e.nb)) return 1;
         hipLaunchKernelGGL(k_points<RT>, dim3((unsigned)n), dim3(kThreads), 0, v->stream, e.nb, n, v->bkeys, v->pool,
                            v->R, v->voxel_size, thr, e.c0, (const int32_t*)nullptr, (float*)nullptr, (float*)nullptr);
         MQR_CHECK_HIP(hipGetLastError());
         if (scan_totals(v, e, n, 1, &np, nullptr)) return 1;
-    }
-    g->nv = np;
-    if (alloc_geom(g, np, 0)) return 1;
-    if constexpr (RT > 0)
-        hipLaunchKernelGGL(k_pt_emit<RT>, dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, e.nb, v->bkeys, v->pool,
-                           v->voxel_size, e.c0, e.o0, reinterpret_cast<const uint4*>(e.faces), g->pos, g->nrm);
-    else
+        g->nv = np;
+        if (alloc_geom(g, np, 0)) return 1;
         hipLaunchKernelGGL(k_points<RT>, dim3((unsigned)n), dim3(kThreads), 0, v->stream, e.nb, n, v->bkeys, v->pool,
                            v->R, v->voxel_size, thr, e.c0, e.o0, g->pos, g->nrm);
+    }
     MQR_CHECK_HIP(hipGetLastError());
     MQR_CHECK_HIP(hipStreamSynchronize(v->stream));
     return 0;

@@ -157,6 +157,7 @@ struct mqr_vbg {
     void* ex_scratch = nullptr;                      // extraction scratch (grow-only, extract.hip)
     size_t ex_scratch_bytes = 0;
     int64_t* h_ex = nullptr;                         // pinned totals of the extraction scans
+    int64_t ex_hint[3] = {0, 0, 0};  // last extraction's vertex / triangle / point counts (speculative capacity)
 
     int kernel_variant = 0;    // integrate kernel configuration (launch_integrate in vbg.hip), 1 = generic
     bool pipelined = true;     // overlap touch(b+1) with integrate(b)

@@ -123,6 +123,33 @@ def test_points_match_oracle(mqr_mod, room_seq, thr):
     compare_points_normals(pcd.points, pcd.normals, op, on, 1e-6)
 
 
+def test_repeated_extraction_speculative_capacity(mqr_mod, room_seq):
+    """The second and later extractions of a volume emit into buffers sized from the previous
+    extraction's counts without waiting for the totals: a mesh / point cloud that grew past that
+    capacity (2 frames, then 40) is re-emitted into exact buffers, one that fits (same volume again,
+    a higher threshold) is kept.  Every result equals the oracle."""
+    vbg = mqr_mod.VoxelBlockGrid(voxel_size=0.01, block_resolution=16, block_count=512)
+    args = dict(depth_scale=1.0, depth_max=4.0, trunc_voxel_multiplier=10.0)
+    vbg.integrate_frames(room_seq["depth"][:1], room_seq["K"][:1], room_seq["T_wc"][:1], **args)
+    small = vbg.extract_triangle_mesh(weight_threshold=0.0)
+    small_p = vbg.extract_point_cloud(weight_threshold=0.0)
+    vbg.integrate_frames(room_seq["depth"][1:], room_seq["K"][1:], room_seq["T_wc"][1:], **args)
+    cap = lambda n: n + n // 4 + 4096  # extract.hip spec_cap
+    ref = _oracle_run(room_seq, 0.01, 16, 4.0, 10.0)
+    for i, thr in enumerate((0.0, 0.0, 3.0)):  # grown past the hint, then equal, then smaller
+        mesh = vbg.extract_triangle_mesh(weight_threshold=thr)
+        ov, on, ot = ref.extract_mesh(thr)
+        if i == 0:
+            assert len(ot) > cap(len(small.triangles)), "the re-emission path is not exercised"
+        compare_meshes(mesh.vertices, mesh.triangles, ov, ot, pos_tol=0.0)
+        compare_points_normals(mesh.vertices, mesh.vertex_normals, ov, on, 1e-6)
+        pcd = vbg.extract_point_cloud(weight_threshold=thr)
+        op, onn = ref.extract_points(thr)
+        if i == 0:
+            assert op.shape[0] > cap(small_p.point.positions.shape[0]), "the re-emission path is not exercised"
+        compare_points_normals(pcd.points, pcd.normals, op, onn, 1e-6)
+
+
 def test_save_load_roundtrip(mqr_mod, sphere_seq, tmp_path):
     vbg = mqr_mod.VoxelBlockGrid(voxel_size=0.02, block_resolution=16, block_count=64)
     vbg.integrate_frames(sphere_seq["depth"], sphere_seq["K"], sphere_seq["T_wc"], depth_scale=1.0, depth_max=3.0,

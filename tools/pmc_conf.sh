@@ -41,4 +41,4 @@ if cyc:
 json.dump(res, open("gpurun_out/pmc_conf.json", "w"), indent=1)
 print(json.dumps(res, indent=1))
 PY
-grep -i "f64\|FP64" gpurun_out/pmc_avail.txt | head -20
+grep -i "f64\|FP64" gpurun_out/pmc_avail.txt | head -20 || true
