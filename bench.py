@@ -137,7 +137,33 @@ def confidence_leg(depth_t, K, T_wc, args, device):
     alg = 4 * H * W * (B + n_nb) + 12 * H * W * B
     return {"ref_frames": B, "window_r": args.conf_range, "ms": t * 1e3, "ref_frames_per_s": B / t,
             "alg_gbs": alg / t / 1e9, "depth_max": args.conf_depth_max, "error_threshold": args.conf_error,
+            "binding": conf_binding(),
             "note": "mqr_confidence over all frames, device-resident depth in/out, wall time of the call"}
+
+
+def conf_binding():
+    """k_confidence's binding resource from the committed counter passes (tools/pmc_conf.sh over
+    tools/conf_workload.py -> profiles/*_pmc_confidence.json): VALU issue share of the launch's
+    cycles (fp64 instructions weighted at half rate), texture-addresser busy share, occupancy."""
+    import glob
+    for path in reversed(sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_confidence.json")))):
+        try:
+            rec = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        d = rec.get("derived")
+        if not d:
+            continue
+        valu, ta = d.get("valu_issue_frac_f64_at_half_rate"), d.get("ta_busy_frac")
+        bound = ("VALU issue (fp64 at half rate)" if valu is not None and (ta is None or valu >= ta)
+                 else "vector-memory gather path (TA)")
+        return {"bound": bound, "source": os.path.relpath(path, ROOT), "valu_issue_frac_f64_weighted": valu,
+                "valu_issue_frac_f32_rate": d.get("valu_issue_frac_f32_rate"), "ta_busy_frac": ta,
+                "f64_share_of_valu": d.get("f64_share_of_valu"),
+                "waves_per_simd": d.get("waves_per_simd"),
+                "note": "fractions of the k_confidence launch's GPU cycles (GRBM_GUI_ACTIVE / 8 XCDs) in the "
+                        "counter run of the C3 workload"}
+    return None
 
 
 def ingest_leg(B, H, W, device):

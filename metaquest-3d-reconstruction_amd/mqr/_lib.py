@@ -171,7 +171,11 @@ def load(path: str = LIB_PATH):
     if rt:
         ctypes.CDLL(rt, mode=ctypes.RTLD_GLOBAL)
     L = ctypes.CDLL(path)
+    partial = os.path.abspath(path) != os.path.abspath(os.path.join(_HERE, "libmqr_hip.so"))
     for name, (res, args) in SIGNATURES.items():
+        fn = getattr(L, name, None)
+        if fn is None and partial:  # the A/B library (tools/_ab) carries the volume entry points only
+            continue
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args

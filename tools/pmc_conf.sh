@@ -37,7 +37,10 @@ if cyc:
                       "valu_issue_frac_f32_rate": 2.0 * v / 1024 / cyc,
                       "valu_issue_frac_f64_at_half_rate": (2.0 * (v - f64) + 4.0 * f64) / 1024 / cyc,
                       "f64_share_of_valu": f64 / v if v else None,
-                      "ta_busy_frac": res.get("TA_BUSY_avr", 0) / cyc if "TA_BUSY_avr" in res else None}
+                      "ta_busy_frac": res.get("TA_BUSY_avr", 0) / cyc if "TA_BUSY_avr" in res else None,
+                      # resident waves per SIMD over the launch: SQ_WAVE_CYCLES counts quad-cycles
+                      # (MI355X_MICROARCH.md), / (1024 SIMDs x cycles)
+                      "waves_per_simd": 4.0 * res.get("SQ_WAVE_CYCLES", 0.0) / 1024 / cyc if "SQ_WAVE_CYCLES" in res else None}
 json.dump(res, open("gpurun_out/pmc_conf.json", "w"), indent=1)
 print(json.dumps(res, indent=1))
 PY
