@@ -217,13 +217,17 @@ __global__ void k_plan_heads(const uint64_t* __restrict__ ks, int64_t n, int32_t
     head[p] = (k != kEmpty && (p == 0 || ks[p - 1] != k)) ? 1 : 0;
 }
 
-// uidx (inclusive head scan) - 1 = union index of entry p; the union keys; U
+// uidx (inclusive head scan) - 1 = union index of entry p; the union keys, the sorted position of
+// each union block's first entry; U
 __global__ void k_plan_union(const uint64_t* __restrict__ ks, const int32_t* __restrict__ incl, int64_t n,
-                             uint64_t* __restrict__ uni, PlanSummary* __restrict__ sum) {
+                             uint64_t* __restrict__ uni, int32_t* __restrict__ first, PlanSummary* __restrict__ sum) {
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= n) return;
     const uint64_t k = ks[p];
-    if (k != kEmpty && (p == 0 || ks[p - 1] != k)) uni[incl[p] - 1] = k;
+    if (k != kEmpty && (p == 0 || ks[p - 1] != k)) {
+        uni[incl[p] - 1] = k;
+        first[incl[p] - 1] = (int32_t)p;
+    }
     if (p == n - 1) sum->U = incl[p];
 }
 
@@ -237,39 +241,112 @@ __device__ __forceinline__ int64_t find_union(const uint64_t* __restrict__ uni, 
     return lo < U && uni[lo] == k ? lo : -1;
 }
 
-// Destination ranks of each union block; halo flag of this rank (receives u without owning it).
-__global__ void k_plan_dmask(const uint64_t* __restrict__ uni, const PlanSummary* __restrict__ sum, int W, int mode,
-                             int root, int me, uint64_t* __restrict__ dmask, int32_t* __restrict__ halo) {
-    const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t U = sum->U;
-    if (u >= U) return;
-    uint64_t m;
-    if (mode == MQR_MERGE_ROOT) {
-        m = 1ull << root;
-    } else {
-        m = 1ull << owner_of(u, U, W);
-        int x, y, z;
-        unpack_key(uni[u], x, y, z);
-        for (int k = 0; k < 27; ++k) {
-            const int nx = x + k % 3 - 1, ny = y + (k / 3) % 3 - 1, nz = z + k / 9 - 1;
-            if (k == 13 || !key_in_range(nx, ny, nz)) continue;
-            const int64_t j = find_union(uni, U, pack_key(nx, ny, nz));
-            if (j >= 0) m |= 1ull << owner_of(j, U, W);  // the neighbour's owner needs u as halo
-        }
-    }
-    dmask[u] = m;
-    const bool owned = mode == MQR_MERGE_ROOT ? me == root : owner_of(u, U, W) == me;
-    halo[u] = ((m >> me) & 1) && !owned ? 1 : 0;
+// The plan's lists come from per-union-block flags on 2W + 1 channels, in union order within each:
+//   channel d < W        send u to rank d       (I hold u, d in dmask[u])
+//   channel W + s        receive u from rank s  (s holds u, I am in dmask[u])
+//   channel 2W           u is halo for me       (I am in dmask[u], u outside my owned slice)
+// Sender and receiver both list a block pair in union order, so their segments match.  Positions:
+// one exclusive scan over the per-workgroup channel counts laid out channel-major, so channel c's
+// entries start at the sum of the earlier channels' totals: sends [0, ns), receives [ns, ns + nr),
+// halo [ns + nr, ...).
+constexpr int kPlanThreads = 256;
+constexpr int kPlanChannels = 2 * kMaxRanks + 1;
+
+__device__ __forceinline__ bool plan_flag(int c, int W, int me, uint64_t dm, uint64_t hm, bool owned) {
+    if (c < W) return ((hm >> me) & 1) && ((dm >> c) & 1);
+    if (c < 2 * W) return ((hm >> (c - W)) & 1) && ((dm >> me) & 1);
+    return ((dm >> me) & 1) && !owned;
 }
 
-// Output position of each union block this rank receives (owned slice first, then halo, both in
-// union order), and the output keys.
-__global__ void k_plan_outpos(const uint64_t* __restrict__ uni, const uint64_t* __restrict__ dmask,
-                              const int32_t* __restrict__ halo, const int32_t* __restrict__ hpos,
-                              PlanSummary* __restrict__ sum, int W, int mode,
-                              int root, int me, int32_t* __restrict__ outpos, uint64_t* __restrict__ out_keys) {
+__device__ __forceinline__ bool plan_owned(int64_t u, int64_t U, int W, int mode, int root, int me) {
+    return mode == MQR_MERGE_ROOT ? me == root : owner_of(u, U, W) == me;
+}
+
+// Destination ranks (owner + owners of the 26 neighbours, or the root), holder ranks (the union
+// block's run of sorted entries; the sort is stable, so the run is in rank order) and the
+// workgroup's channel counts wcnt[c * gridDim.x + blockIdx.x].
+__global__ __launch_bounds__(kPlanThreads) void k_plan_masks(const uint64_t* __restrict__ uni,
+                                                             const int32_t* __restrict__ first,
+                                                             const uint64_t* __restrict__ ks,
+                                                             const int32_t* __restrict__ vs, int64_t n, int64_t mx,
+                                                             const PlanSummary* __restrict__ sum, int W, int mode,
+                                                             int root, int me, uint64_t* __restrict__ dmask,
+                                                             uint64_t* __restrict__ hmask, int32_t* __restrict__ wcnt) {
+    __shared__ int cnt[kPlanChannels];
+    const int NC = 2 * W + 1;
+    for (int c = threadIdx.x; c < NC; c += blockDim.x) cnt[c] = 0;
+    __syncthreads();
     const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t U = sum->U;
+    const bool act = u < U;
+    uint64_t dm = 0, hm = 0;
+    bool owned = false;
+    if (act) {
+        const uint64_t k = uni[u];
+        if (mode == MQR_MERGE_ROOT) {
+            dm = 1ull << root;
+        } else {
+            dm = 1ull << owner_of(u, U, W);
+            int x, y, z;
+            unpack_key(k, x, y, z);
+            for (int q = 0; q < 27; ++q) {
+                const int nx = x + q % 3 - 1, ny = y + (q / 3) % 3 - 1, nz = z + q / 9 - 1;
+                if (q == 13 || !key_in_range(nx, ny, nz)) continue;
+                const int64_t j = find_union(uni, U, pack_key(nx, ny, nz));
+                if (j >= 0) dm |= 1ull << owner_of(j, U, W);  // the neighbour's owner needs u as halo
+            }
+        }
+        for (int64_t p = first[u]; p < n && ks[p] == k; ++p) hm |= 1ull << (vs[p] / mx);
+        dmask[u] = dm;
+        hmask[u] = hm;
+        owned = plan_owned(u, U, W, mode, root, me);
+    }
+    const int lane = threadIdx.x & 63;
+    for (int c = 0; c < NC; ++c) {
+        const uint64_t bl = __ballot(act && plan_flag(c, W, me, dm, hm, owned));
+        if (lane == 0 && bl) atomicAdd(&cnt[c], __popcll(bl));
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < NC; c += blockDim.x) wcnt[(int64_t)c * gridDim.x + blockIdx.x] = cnt[c];
+}
+
+// Lists at the scanned positions (wbase = exclusive scan of wcnt): send_idx (my buffer of u, by
+// destination), recv_dst / recv_src (output position of u and the source's buffer of u, by source),
+// output positions (owned slice first, then halo, both in union order), output keys, the summary.
+__global__ __launch_bounds__(kPlanThreads) void k_plan_lists(
+    const uint64_t* __restrict__ uni, const int32_t* __restrict__ first, const int32_t* __restrict__ vs, int64_t mx,
+    const uint64_t* __restrict__ dmask, const uint64_t* __restrict__ hmask, const int32_t* __restrict__ wcnt,
+    const int32_t* __restrict__ wbase, PlanSummary* __restrict__ sum, int W, int mode, int root, int me,
+    int32_t* __restrict__ send_idx, int32_t* __restrict__ recv_dst, int32_t* __restrict__ recv_src,
+    uint64_t* __restrict__ out_keys) {
+    constexpr int NW = kPlanThreads / 64;
+    __shared__ int wc[NW][kPlanChannels];  // per-wave channel counts, then their prefix over waves
+    const int NC = 2 * W + 1;
+    const int64_t nwg = gridDim.x, U = sum->U;
+    const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool act = u < U;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t below = (1ull << lane) - 1;
+    const uint64_t dm = act ? dmask[u] : 0, hm = act ? hmask[u] : 0;
+    const bool owned = act && plan_owned(u, U, W, mode, root, me);
+    for (int c = 0; c < NC; ++c) {
+        const uint64_t bl = __ballot(act && plan_flag(c, W, me, dm, hm, owned));
+        if (lane == 0) wc[wave][c] = __popcll(bl);
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < NC; c += blockDim.x) {
+        int run = 0;
+        for (int w = 0; w < NW; ++w) {
+            const int t = wc[w][c];
+            wc[w][c] = run;
+            run += t;
+        }
+    }
+    __syncthreads();
+    const int64_t ns = wbase[(int64_t)W * nwg], nsr = wbase[(int64_t)2 * W * nwg];
+    auto pos_of = [&](int c, uint64_t bl) {
+        return (int64_t)wbase[(int64_t)c * nwg + blockIdx.x] + wc[wave][c] + __popcll(bl & below);
+    };
     int64_t lo, hi;
     if (mode == MQR_MERGE_ROOT) {
         lo = 0;
@@ -278,78 +355,42 @@ __global__ void k_plan_outpos(const uint64_t* __restrict__ uni, const uint64_t* 
         lo = slice_lo(U, W, me);
         hi = slice_lo(U, W, me + 1);
     }
-    if (u == 0) {
-        sum->n_owned = hi - lo;
-        sum->n_out = (hi - lo) + (U > 0 ? hpos[U - 1] + halo[U - 1] : 0);
+    int32_t op = -1;  // output position of u
+    {
+        const bool f = act && plan_flag(2 * W, W, me, dm, hm, owned);
+        const uint64_t bl = __ballot(f);
+        if (act && u >= lo && u < hi) op = (int32_t)(u - lo);
+        else if (f) op = (int32_t)((hi - lo) + (pos_of(2 * W, bl) - nsr));
     }
-    if (u >= U) return;
-    int32_t o = -1;
-    if (u >= lo && u < hi) o = (int32_t)(u - lo);
-    else if ((dmask[u] >> me) & 1) o = (int32_t)((hi - lo) + hpos[u]);
-    outpos[u] = o;
-    if (o >= 0) out_keys[o] = uni[u];
-}
-
-// Records per sorted entry: one per destination if this rank holds the block (send), one if this
-// rank receives it (from the entry's origin rank).
-__global__ void k_plan_rec_count(const uint64_t* __restrict__ ks, const int32_t* __restrict__ vs,
-                                 const int32_t* __restrict__ incl, const uint64_t* __restrict__ dmask, int64_t n,
-                                 int64_t mx, int me, int32_t* __restrict__ rc) {
-    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= n) return;
-    int c = 0;
-    if (ks[p] != kEmpty) {
-        const uint64_t m = dmask[incl[p] - 1];
-        if (vs[p] / mx == me) c += __popcll(m);
-        c += (int)((m >> me) & 1);
+    if (op >= 0) out_keys[op] = uni[u];
+    const int64_t f0 = act ? first[u] : 0;
+    for (int d = 0; d < W; ++d) {
+        const bool f = act && plan_flag(d, W, me, dm, hm, owned);
+        const uint64_t bl = __ballot(f);
+        if (f) send_idx[pos_of(d, bl)] = (int32_t)(vs[f0 + __popcll(hm & ((1ull << me) - 1))] % mx);
     }
-    rc[p] = c;
-}
-
-// record key: kind (bit 40: 0 send, 1 receive) | peer (bits 32..37) | entry p (bits 0..31)
-__global__ void k_plan_rec_emit(const uint64_t* __restrict__ ks, const int32_t* __restrict__ vs,
-                                const int32_t* __restrict__ incl, const uint64_t* __restrict__ dmask,
-                                const int32_t* __restrict__ roff, int64_t n, int64_t mx, int me,
-                                uint64_t* __restrict__ rec, PlanSummary* __restrict__ sum) {
-    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= n || ks[p] == kEmpty) return;
-    const uint64_t m = dmask[incl[p] - 1];
-    const int src = (int)(vs[p] / mx);
-    int64_t o = roff[p];
-    if (src == me) {
-        uint64_t mm = m;
-        while (mm) {
-            const int d = __builtin_ctzll(mm);
-            mm &= mm - 1;
-            rec[o++] = ((uint64_t)d << 32) | (uint64_t)p;
-            atomicAdd((unsigned long long*)&sum->cnt[0][d], 1ull);
+    for (int s = 0; s < W; ++s) {
+        const bool f = act && plan_flag(W + s, W, me, dm, hm, owned);
+        const uint64_t bl = __ballot(f);
+        if (f) {
+            const int64_t j = pos_of(W + s, bl) - ns;
+            recv_dst[j] = op;
+            recv_src[j] = (int32_t)(vs[f0 + __popcll(hm & ((1ull << s) - 1))] % mx);
         }
     }
-    if ((m >> me) & 1) {
-        rec[o] = (1ull << 40) | ((uint64_t)src << 32) | (uint64_t)p;
-        atomicAdd((unsigned long long*)&sum->cnt[1][src], 1ull);
-    }
-}
-
-// Sorted records -> lists: sends: origin buffer; receives: output buffer and origin buffer.
-__global__ void k_plan_lists(const uint64_t* __restrict__ rec, int64_t R, const int32_t* __restrict__ vs,
-                             const int32_t* __restrict__ incl, const int32_t* __restrict__ outpos, int64_t mx,
-                             const PlanSummary* __restrict__ sum, int W, int32_t* __restrict__ send_idx,
-                             int32_t* __restrict__ recv_dst, int32_t* __restrict__ recv_src) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= R) return;
-    const uint64_t r = rec[i];
-    if (r == kEmpty) return;
-    const int64_t p = (int64_t)(r & 0xffffffffull);
-    const int32_t b = (int32_t)(vs[p] % mx);
-    if (!((r >> 40) & 1)) {
-        send_idx[i] = b;
-    } else {
-        int64_t ns = 0;
-        for (int d = 0; d < W; ++d) ns += sum->cnt[0][d];
-        recv_dst[i - ns] = outpos[incl[p] - 1];
-        recv_src[i - ns] = b;
-    }
+    if (blockIdx.x == 0)
+        for (int c = threadIdx.x; c < NC; c += blockDim.x) {
+            const int64_t last = (int64_t)NC * nwg - 1;
+            const int64_t start = wbase[(int64_t)c * nwg];
+            const int64_t end = c + 1 < NC ? wbase[(int64_t)(c + 1) * nwg] : wbase[last] + wcnt[last];
+            if (c < W) sum->cnt[0][c] = end - start;
+            else if (c < 2 * W) sum->cnt[1][c - W] = end - start;
+            else {
+                sum->n_owned = hi - lo;
+                sum->n_out = (hi - lo) + (end - start);
+                sum->total = start;  // send + receive records
+            }
+        }
 }
 
 // One rank's plan over the gathered keys dkeys[W * mx] (device).  Host results in `H` (pinned
@@ -369,15 +410,17 @@ static int device_plan(PlanScratch& S, hipStream_t st, const uint64_t* dkeys, in
                        int root, PlanView& out) {
     const int64_t n = (int64_t)W * mx;
     MQR_REQUIRE(n < (int64_t{1} << 31), "merge plan: too many blocks");
-    const int64_t rmax = n * (int64_t)(std::min(W, 27) + 1);  // records: <= 27 destinations + 1 receive per entry
-    size_t tb_sort = 0, tb_scan = 0, tb_rsort = 0;
+    const int NC = 2 * W + 1;
+    const int64_t nwg = (n + kPlanThreads - 1) / kPlanThreads;  // over union indices (U <= n)
+    const int64_t nsend = n * (int64_t)std::min(W, 27);         // each union block goes to <= 27 ranks
+    size_t tb_sort = 0, tb_scan = 0, tb_wscan = 0;
     MQR_CHECK_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb_sort, (const uint64_t*)nullptr, (uint64_t*)nullptr,
                                                      (const int32_t*)nullptr, (int32_t*)nullptr, (int)n, 0, 64, st));
     MQR_CHECK_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, tb_scan, (const int32_t*)nullptr, (int32_t*)nullptr,
                                                    (int)n, st));
-    MQR_CHECK_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tb_rsort, (const uint64_t*)nullptr, (uint64_t*)nullptr,
-                                                    (int)rmax, 0, 41, st));
-    const size_t tb = std::max(tb_sort, std::max(tb_scan, tb_rsort));
+    MQR_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb_wscan, (const int32_t*)nullptr, (int32_t*)nullptr,
+                                                   (int)(NC * nwg), st));
+    const size_t tb = std::max(tb_sort, std::max(tb_scan, tb_wscan));
     // carve the scratch
     size_t off = 0;
     auto take = [&](size_t bytes) {
@@ -386,10 +429,10 @@ static int device_plan(PlanScratch& S, hipStream_t st, const uint64_t* dkeys, in
         return o;
     };
     const size_t o_ks = take(8 * n), o_vi = take(4 * n), o_vs = take(4 * n), o_head = take(4 * n),
-                 o_incl = take(4 * n), o_uni = take(8 * n), o_dm = take(8 * n), o_halo = take(4 * n),
-                 o_hpos = take(4 * n), o_outpos = take(4 * n), o_rc = take(4 * (n + 1)), o_roff = take(4 * (n + 1)),
-                 o_rec = take(8 * rmax), o_recs = take(8 * rmax), o_send = take(4 * rmax), o_rdst = take(4 * rmax),
-                 o_rsrc = take(4 * rmax), o_okeys = take(8 * n), o_sum = take(sizeof(PlanSummary)), o_tmp = take(tb);
+                 o_incl = take(4 * n), o_uni = take(8 * n), o_first = take(4 * n), o_dm = take(8 * n),
+                 o_hm = take(8 * n), o_wcnt = take(4 * NC * nwg), o_wbase = take(4 * NC * nwg),
+                 o_send = take(4 * nsend), o_rdst = take(4 * n), o_rsrc = take(4 * n), o_okeys = take(8 * n),
+                 o_sum = take(sizeof(PlanSummary)), o_tmp = take(tb);
     if (S.cap < off) {
         const size_t want = std::max(off, S.cap + S.cap / 2);
         if (S.buf) MQR_CHECK_HIP(hipFree(S.buf));
@@ -412,27 +455,15 @@ static int device_plan(PlanScratch& S, hipStream_t st, const uint64_t* dkeys, in
     hipLaunchKernelGGL(k_plan_heads, dim3(g), dim3(256), 0, st, U64(o_ks), n, I32(o_head));
     t = tb;
     MQR_CHECK_HIP(hipcub::DeviceScan::InclusiveSum(tmp, t, I32(o_head), I32(o_incl), (int)n, st));
-    hipLaunchKernelGGL(k_plan_union, dim3(g), dim3(256), 0, st, U64(o_ks), I32(o_incl), n, U64(o_uni), dsum);
-    MQR_CHECK_HIP(hipMemsetAsync(I32(o_halo), 0, 4 * n, st));
-    hipLaunchKernelGGL(k_plan_dmask, dim3(g), dim3(256), 0, st, U64(o_uni), dsum, W, mode, root, me, U64(o_dm),
-                       I32(o_halo));
+    hipLaunchKernelGGL(k_plan_union, dim3(g), dim3(256), 0, st, U64(o_ks), I32(o_incl), n, U64(o_uni), I32(o_first),
+                       dsum);
+    hipLaunchKernelGGL(k_plan_masks, dim3((unsigned)nwg), dim3(kPlanThreads), 0, st, U64(o_uni), I32(o_first),
+                       U64(o_ks), I32(o_vs), n, mx, dsum, W, mode, root, me, U64(o_dm), U64(o_hm), I32(o_wcnt));
     t = tb;
-    MQR_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, t, I32(o_halo), I32(o_hpos), (int)n, st));
-    hipLaunchKernelGGL(k_plan_outpos, dim3(g), dim3(256), 0, st, U64(o_uni), U64(o_dm), I32(o_halo), I32(o_hpos),
-                       dsum, W, mode,
-                       root, me, I32(o_outpos), U64(o_okeys));
-    hipLaunchKernelGGL(k_plan_rec_count, dim3(g), dim3(256), 0, st, U64(o_ks), I32(o_vs), I32(o_incl), U64(o_dm), n,
-                       mx, me, I32(o_rc));
-    MQR_CHECK_HIP(hipMemsetAsync(I32(o_rc) + n, 0, 4, st));
-    t = tb;
-    MQR_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, t, I32(o_rc), I32(o_roff), (int)(n + 1), st));
-    MQR_CHECK_HIP(hipMemsetAsync(U64(o_rec), 0xff, 8 * rmax, st));
-    hipLaunchKernelGGL(k_plan_rec_emit, dim3(g), dim3(256), 0, st, U64(o_ks), I32(o_vs), I32(o_incl), U64(o_dm),
-                       I32(o_roff), n, mx, me, U64(o_rec), dsum);
-    t = tb;
-    MQR_CHECK_HIP(hipcub::DeviceRadixSort::SortKeys(tmp, t, U64(o_rec), U64(o_recs), (int)rmax, 0, 41, st));
-    hipLaunchKernelGGL(k_plan_lists, dim3((unsigned)((rmax + 255) / 256)), dim3(256), 0, st, U64(o_recs), rmax,
-                       I32(o_vs), I32(o_incl), I32(o_outpos), mx, dsum, W, I32(o_send), I32(o_rdst), I32(o_rsrc));
+    MQR_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, t, I32(o_wcnt), I32(o_wbase), (int)(NC * nwg), st));
+    hipLaunchKernelGGL(k_plan_lists, dim3((unsigned)nwg), dim3(kPlanThreads), 0, st, U64(o_uni), I32(o_first),
+                       I32(o_vs), mx, U64(o_dm), U64(o_hm), I32(o_wcnt), I32(o_wbase), dsum, W, mode, root, me,
+                       I32(o_send), I32(o_rdst), I32(o_rsrc), U64(o_okeys));
     MQR_CHECK_HIP(hipGetLastError());
     MQR_CHECK_HIP(hipMemcpyAsync(S.h_sum, dsum, sizeof(PlanSummary), hipMemcpyDeviceToHost, st));
     MQR_CHECK_HIP(hipStreamSynchronize(st));
