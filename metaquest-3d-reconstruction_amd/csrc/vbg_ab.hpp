@@ -425,4 +425,56 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
     }
 }
 
+// ---- paired-lane gather (A/B, variant 6) ----------------------------------------------------------
+// Lanes l and l ^ 1 of the brick map hold x-adjacent voxels, which mostly project into the same
+// image row within 4 pixels (80 % of pairs on the C2 walk, tools/integrate_work_stats.py).  The even
+// lane loads 16 bytes at its own pixel and hands the odd lane its dword (DPP quad swap) when that
+// dword lies inside them; every other lane issues its own dword gather.  Two gather instructions per
+// voxel (x4 by even lanes, x1 by the rest) in place of one x1 by all 64 lanes: fewer addresses for
+// the texture addresser and the L1 tag lookups, ~10 more VALU per voxel-frame.  Same values as
+// lean_gather: a served lane reads the same dword; a 16-byte load that would leave the frame is not
+// used (out-of-range dwords read as 0).
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+template <int ZPER, int ILP>
+__device__ void lean_gather_pair(float (&dv)[ZPER], bool& bad, const FrameParams& fp, __amdgpu_buffer_rsrc_t rs,
+                                 const float (&xs)[ZPER], const float (&ys)[ZPER], const float (&zs)[ZPER], uint32_t W4,
+                                 float hf, float hm1, float wm1, uint32_t bytes) {
+    constexpr int kSwap = 0xB1;  // DPP quad_perm [1, 0, 3, 2]: the partner lane
+    float e[12];
+#pragma unroll
+    for (int j = 0; j < 12; ++j) e[j] = fp.ext[j];
+    const float fx = fp.fx, fy = fp.fy, cx = fp.cx, cy = fp.cy;
+    const bool odd = threadIdx.x & 1;
+#pragma unroll
+    for (int k = 0; k < ZPER; ++k) {
+        const float ax = xs[k] * e[0] + ys[k] * e[1];
+        const float ay = xs[k] * e[4] + ys[k] * e[5];
+        const float az = xs[k] * e[8] + ys[k] * e[9];
+        const float xc = (ax + zs[k] * e[2]) + e[3];
+        const float yc = (ay + zs[k] * e[6]) + e[7];
+        const float zc = (az + zs[k] * e[10]) + e[11];
+        bad |= (__float_as_uint(zc) - 0x2D800000u) > 0x30000000u;
+        const float inv_z = rcp_m(zc);
+        const float u = fx * xc * inv_z + cx;
+        const float v = fy * yc * inv_z + cy;
+        const bool in = (v >= 0) & (u >= 0) & (v <= hm1) & (u <= wm1);
+        const uint32_t off = in ? __umul24((uint32_t)(int)v, W4) + ((uint32_t)(int)u << 2) : __umul24((uint32_t)hf, W4);
+        const uint32_t poff = (uint32_t)__builtin_amdgcn_mov_dpp((int)off, kSwap, 0xF, 0xF, false);
+        const uint32_t delta = poff - off;  // even lane: the odd partner's byte offset past mine
+        const bool wide = !odd && off + 16u <= bytes;
+        const bool serves = wide && delta <= 12u;
+        const bool served = odd && __builtin_amdgcn_mov_dpp((int)serves, kSwap, 0xF, 0xF, false);
+        float mine = 0.f, partner = 0.f;
+        if (wide) {
+            const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+            mine = __uint_as_float(q.x);
+            partner = __uint_as_float(delta == 0 ? q.x : delta == 4 ? q.y : delta == 8 ? q.z : q.w);
+        }
+        const float got = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(partner), kSwap, 0xF, 0xF, false));
+        if (!wide && !served) mine = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
+        dv[k] = served ? got : mine;
+        if ((k + 1) % ILP == 0) __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
 }  // namespace mqr

@@ -688,7 +688,15 @@ __host__ __device__ constexpr int lean_dz(int k) { return MAP == 1 ? 4 * (k & 3)
 // workgroup, voxels per lean_map<MAP>; every voxel of a block not handed off is written back.
 // WPE: minimum waves per SIMD the register allocation must allow; ILP: voxel chains the scheduler
 // may interleave (lean_gather / lean_update).
-template <int R, int NT, int MAP = 0, int WPE = 1, int ILP = 1>
+#if MQR_AB
+template <int ZPER, int ILP>
+__device__ void lean_gather_pair(float (&dv)[ZPER], bool& bad, const FrameParams& fp, __amdgpu_buffer_rsrc_t rs,
+                                 const float (&xs)[ZPER], const float (&ys)[ZPER], const float (&zs)[ZPER], uint32_t W4,
+                                 float hf, float hm1, float wm1, uint32_t bytes);  // vbg_ab.hpp (variant 6)
+#endif
+
+// PAIR (A/B library only, variant 6): the paired-lane gather of vbg_ab.hpp.
+template <int R, int NT, int MAP = 0, int WPE = 1, int ILP = 1, int PAIR = 0>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void k_integrate_lean(
     const int32_t* __restrict__ list, const bmask_t* __restrict__ lmask, int32_t* __restrict__ bad_out,
     int* __restrict__ counters, int64_t list_cap, Table t, float2* __restrict__ pool, float voxel_size,
@@ -747,8 +755,16 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
                 const int f = __builtin_ctzll(m);
                 m &= m - 1;
                 float dv[ZPER];
-                lean_gather<ZPER, ILP>(dv, bad, fps[f], frame_rsrc(depths + depth_frame[f] * HW, bytes), xs, ys,
-                                       zs, W4, hf, hm1, wm1);
+                if constexpr (PAIR) {
+#if MQR_AB
+                    static_assert(MAP == 1, "pairs are the x-adjacent lanes of the brick map");
+                    lean_gather_pair<ZPER, ILP>(dv, bad, fps[f], frame_rsrc(depths + depth_frame[f] * HW, bytes), xs,
+                                                ys, zs, W4, hf, hm1, wm1, bytes);
+#endif
+                } else {
+                    lean_gather<ZPER, ILP>(dv, bad, fps[f], frame_rsrc(depths + depth_frame[f] * HW, bytes), xs, ys,
+                                           zs, W4, hf, hm1, wm1);
+                }
                 lean_update<ZPER, ILP>(tw, dv, fps[f], xs, ys, zs, depth_max, sdf_trunc, y1t);
             }
             if (__syncthreads_or(bad)) {  // block-uniform: the exact fix-up launch redoes it from the pool

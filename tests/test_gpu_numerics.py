@@ -50,7 +50,7 @@ def test_shortened_reciprocals_exact(which, lo, hi):
 AB = os.environ.get("MQR_AB_TEST") == "1"
 INTEGRATE_VARIANTS = {16: (0, 2, 0x100, 0x200, 0x400, 0x800), 8: (0, 2, 0x100)}
 if AB:
-    INTEGRATE_VARIANTS = {16: (0, 3, 5, 0x105, 0x605, 0x8000, 0x8003), 8: (0, 0x8000)}
+    INTEGRATE_VARIANTS = {16: (0, 3, 5, 6, 7, 0x105, 0x605, 0x106, 0x8000, 0x8003), 8: (0, 0x8000)}
 
 
 def test_specialised_integrate_equals_generic():
@@ -112,7 +112,7 @@ def test_fast_integrate_exact_fallback():
     for d in depth_mm:
         d[::7, ::5] = np.float32(1e-30)   # in-image, > 0, below 2^-60: exact division path
     out = []
-    cases = ((16, 1), (16, 0), (16, 2), (16, 5 if AB else 0x100), (8, 1), (8, 0), (8, 2))
+    cases = ((16, 1), (16, 0), (16, 2), (16, 6 if AB else 0x100), (8, 1), (8, 0), (8, 2))
     for R, variant in cases:
         v = VoxelBlockGrid(voxel_size=0.01, block_resolution=R, block_count=64)
         _lib.call("mqr_vbg_set_variant", v.handle, variant)
