@@ -103,7 +103,9 @@ int mqr_vbg_unpack_weighted(mqr_vbg* v, const int32_t* union_keys, int64_t U, co
  * mqr_comm_timing: the last merge's phases in ms -- [0] count + key all-gathers and the plan,
  * [1] output volume + gather of the outgoing blocks, [2] the RCCL exchange, [3] the merge kernels.
  * mqr_merge_local: the same plan and arithmetic for n volumes of one process on one device (the
- * merge reads each source's pool directly instead of receiving over RCCL; tests and timing). */
+ * merge reads each source's pool directly instead of receiving over RCCL; tests and timing).
+ * mqr_merge_local_timing: the last mqr_merge_local's wall time per destination in ms (its plan,
+ * output volume and merge kernels: one rank's share of a merge, without the transfer). */
 #define MQR_MERGE_ROOT 0
 #define MQR_MERGE_SHARDED 1
 int mqr_comm_unique_id(uint8_t* id_out /* 128 bytes */);
@@ -112,6 +114,7 @@ int mqr_comm_destroy(mqr_comm* comm);
 int mqr_reduce_rccl(mqr_vbg* local, mqr_comm* comm, int mode, int root, mqr_vbg* out, int64_t* n_owned);
 int mqr_merge_local(mqr_vbg** locals, int n, int mode, int root, mqr_vbg** outs, int64_t* n_owned);
 int mqr_comm_timing(mqr_comm* comm, float* ms4);
+int mqr_merge_local_timing(float* ms, int n);
 
 /* vbg.extract_point_cloud(weight_threshold=3.0)   -- reconstruct_scene.py:90, refine_fragment_poses.py:39
  * vbg.extract_triangle_mesh(weight_threshold)       -- reconstruct_scene.py:105-108, 186-189 */

@@ -29,6 +29,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <chrono>
 #include <climits>
 #include <cstring>
 #include <mutex>
@@ -665,6 +666,8 @@ int mqr_reduce_rccl(mqr_vbg* local, mqr_comm* c, int mode, int root, mqr_vbg* ou
     return 0;
 }
 
+static thread_local std::vector<float> t_local_ms;  // mqr_merge_local_timing
+
 int mqr_merge_local(mqr_vbg** locals, int n, int mode, int root, mqr_vbg** outs, int64_t* n_owned) {
     MQR_REQUIRE(locals && outs && n_owned && n >= 1 && n <= kMaxRanks, "bad arguments");
     MQR_REQUIRE(mode == MQR_MERGE_ROOT || mode == MQR_MERGE_SHARDED, "unknown merge mode");
@@ -702,7 +705,10 @@ int mqr_merge_local(mqr_vbg** locals, int n, int mode, int root, mqr_vbg** outs,
             MQR_CHECK_HIP(hipMemcpyAsync(dkeys + r * mx, locals[r]->bkeys, sizeof(uint64_t) * locals[r]->pool_count,
                                          hipMemcpyDeviceToDevice, st));
     PlanScratch S;
+    t_local_ms.assign(n, 0.f);
+    MQR_CHECK_HIP(hipStreamSynchronize(st));  // the key copies are the all-gather's, not a destination's
     for (int d = 0; d < n; ++d) {
+        const auto t0 = std::chrono::steady_clock::now();
         // destination d's plan: its receive segments name, per source, the source's buffers
         PlanView pv;
         if (device_plan(S, st, dkeys, n, mx, d, mode, root, pv)) return 1;
@@ -719,7 +725,15 @@ int mqr_merge_local(mqr_vbg** locals, int n, int mode, int root, mqr_vbg** outs,
         MQR_CHECK_HIP(hipGetLastError());
         MQR_CHECK_HIP(hipStreamSynchronize(st));  // the plan scratch is reused for the next destination
         n_owned[d] = H.n_owned;
+        t_local_ms[d] = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }
+    return 0;
+}
+
+int mqr_merge_local_timing(float* ms, int n) {
+    MQR_REQUIRE(ms && n >= 0, "bad arguments");
+    MQR_REQUIRE((size_t)n <= t_local_ms.size(), "fewer destinations in the last mqr_merge_local");
+    for (int i = 0; i < n; ++i) ms[i] = t_local_ms[i];
     return 0;
 }
 

@@ -283,6 +283,15 @@ def merge_local(vbgs, mode: str = "sharded", root: int = 0, outs=None):
     return list(zip(outs, owned.tolist()))
 
 
+def merge_local_timing(n: int):
+    """Per-destination wall ms of the last merge_local (one rank's plan, output volume and merge
+    kernels, without the transfer)."""
+    from . import _lib
+    ms = np.zeros(n, np.float32)
+    _lib.call("mqr_merge_local_timing", _lib.ptr(ms, _lib._f32p), int(n))
+    return ms.tolist()
+
+
 def extract_mesh_owned(vbg, n_owned: int, weight_threshold: float = 1.5):
     """A shard's mesh: triangles of the cubes whose origin lies in its owned blocks, the vertices
     they reference (re-indexed; vertices on the shard boundary also appear in the neighbour's mesh)."""

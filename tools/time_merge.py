@@ -22,7 +22,7 @@ def main():
     a = ap.parse_args()
     from bench import _DevPtr
     from mqr import synthetic
-    from mqr.distributed import merge_local
+    from mqr.distributed import merge_local, merge_local_timing
     from mqr.vbg import VoxelBlockGrid
     poses = synthetic.room_loop_poses(a.frames * a.ranks)
     vols = []
@@ -44,7 +44,9 @@ def main():
             torch.cuda.synchronize()
             ts.append(time.perf_counter() - t0)
             outs = [o for o, _ in got]
-        res[mode] = {"ms": sorted(ts[1:])[len(ts[1:]) // 2] * 1e3, "owned": [n for _, n in got]}
+        per = merge_local_timing(a.ranks)
+        res[mode] = {"ms": sorted(ts[1:])[len(ts[1:]) // 2] * 1e3, "owned": [n for _, n in got],
+                     "per_destination_ms": per, "max_per_destination_ms": max(per)}
     # the RCCL path at world size 1 (plan, output volume, gather, merge kernels; no peers)
     import torch.distributed as dist
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
