@@ -428,8 +428,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
 // ---- paired-lane gather (A/B, variant 6) ----------------------------------------------------------
 // Lanes l and l ^ 1 of the brick map hold x-adjacent voxels, which mostly project into the same
 // image row within 4 pixels (80 % of pairs on the C2 walk, tools/integrate_work_stats.py).  The even
-// lane loads 16 bytes at its own pixel and hands the odd lane its dword (DPP quad swap) when that
-// dword lies inside them; every other lane issues its own dword gather.  Two gather instructions per
+// lane loads the 16-byte-aligned window holding its own pixel and hands the odd lane its dword (DPP
+// quad swap) when that dword lies in the window; every other lane issues its own dword gather.  Two gather instructions per
 // voxel (x4 by even lanes, x1 by the rest) in place of one x1 by all 64 lanes: fewer addresses for
 // the texture addresser and the L1 tag lookups, ~10 more VALU per voxel-frame.  Same values as
 // lean_gather: a served lane reads the same dword; a 16-byte load that would leave the frame is not
@@ -460,15 +460,21 @@ __device__ void lean_gather_pair(float (&dv)[ZPER], bool& bad, const FrameParams
         const bool in = (v >= 0) & (u >= 0) & (v <= hm1) & (u <= wm1);
         const uint32_t off = in ? __umul24((uint32_t)(int)v, W4) + ((uint32_t)(int)u << 2) : __umul24((uint32_t)hf, W4);
         const uint32_t poff = (uint32_t)__builtin_amdgcn_mov_dpp((int)off, kSwap, 0xF, 0xF, false);
-        const uint32_t delta = poff - off;  // even lane: the odd partner's byte offset past mine
-        const bool wide = !odd && off + 16u <= bytes;
-        const bool serves = wide && delta <= 12u;
-        const bool served = odd && __builtin_amdgcn_mov_dpp((int)serves, kSwap, 0xF, 0xF, false);
+        // even lane: the 16-byte-aligned window holding its own dword; it serves the odd partner when
+        // the partner's dword lies in the same window
+        const uint32_t a = off & ~15u;
+        const uint32_t pd = poff - a, od = off - a;
+        const bool wide = !odd && a + 16u <= bytes;
+        const bool serves = wide && pd < 16u;
+        // the DPP reads run with every lane active (under `odd && ...` they would run for the odd
+        // lanes only, reading disabled even lanes)
+        const int pserves = __builtin_amdgcn_mov_dpp((int)serves, kSwap, 0xF, 0xF, false);
+        const bool served = odd && pserves;
         float mine = 0.f, partner = 0.f;
         if (wide) {
-            const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
-            mine = __uint_as_float(q.x);
-            partner = __uint_as_float(delta == 0 ? q.x : delta == 4 ? q.y : delta == 8 ? q.z : q.w);
+            const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(rs, a, 0, 0);
+            mine = __uint_as_float(od == 0 ? q.x : od == 4 ? q.y : od == 8 ? q.z : q.w);
+            partner = __uint_as_float(pd == 0 ? q.x : pd == 4 ? q.y : pd == 8 ? q.z : q.w);
         }
         const float got = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(partner), kSwap, 0xF, 0xF, false));
         if (!wide && !served) mine = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
