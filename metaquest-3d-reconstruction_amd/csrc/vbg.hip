@@ -34,6 +34,10 @@ void make_frame_params(const double* K, const double* T, FrameParams* fp) {
     fp->fy = (float)K[4];
     fp->cx = (float)K[2];
     fp->cy = (float)K[5];
+    // a -0.0 principal point becomes +0.0: u = p + c is the same for both unless p = -0, where it is
+    // -0 or +0, the same pixel; then no u or v is -0.0 (lean_gather_v's in-image test on float bits)
+    if (fp->cx == 0.0f) fp->cx = 0.0f;
+    if (fp->cy == 0.0f) fp->cy = 0.0f;
     for (int i = 0; i < 3; ++i)
         for (int j = 0; j < 4; ++j) fp->ext[i * 4 + j] = (float)T[i * 4 + j];
     // Rigid inverse in float64 (upstream t::geometry::InverseTransformation), then float32.
@@ -323,14 +327,14 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
     //   0 default: k_integrate_lean -- R = 16: brick map, >= 8 waves per SIMD, 2 interleaved voxel
     //     chains; R = 8: plate map;  1 generic k_integrate (runtime R);  2 exact k_integrate_t;
     //   3 k_integrate_lean with the plate map (round-1 default, A/B);  5 k_integrate_lt (R = 16: depth
-    //     from packed LDS tiles, A/B);  6 / 7 the lean kernel with the paired-lane gather (A/B).  3, 5-7
+    //     from packed LDS tiles, A/B);  6 / 7 the lean kernel with the paired-lane gather (A/B);  8 VALU-lean projection / update (A/B).  3, 5-8
     //     exist only in the A/B library (MQR_AB, vbg_ab.hpp).
     //     DESIGN.md §4 has the measurements behind the choice.
     int var = v->kernel_variant;
-    if (var != 1 && var != 2 && var != 3 && var != 5 && var != 6 && var != 7) var = 0;
+    if (var != 1 && var != 2 && var != 3 && var != 5 && var != 6 && var != 7 && var != 8) var = 0;
     if (var != 1 && var != 2 && !lean_ok) var = 2;
     if (var == 5 && (v->R != 16 || W % 4 != 0 || W < 4 || (reinterpret_cast<uintptr_t>(depths) & 15))) var = 0;
-    if ((var == 6 || var == 7) && v->R != 16) var = 0;
+    if ((var == 6 || var == 7 || var == 8) && v->R != 16) var = 0;
     if (v->R != 16 && v->R != 8) var = 1;
     const int32_t* bad_list = v->bad[p];
     const bmask_t* bad_mask = reinterpret_cast<const bmask_t*>(v->bad[p] + v->list_cap);
@@ -345,7 +349,11 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
                                depth_frame, depth_scale, depth_max, sdf_trunc, first_new);
         } else {
 #if MQR_AB
-            if (var == 6)  // paired gather at 8 waves / SIMD (spills) or 6 (variant 7)
+            if (var == 8)  // VALU-lean projection / update (lean_gather_v)
+                hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 8, 2, 2>), dim3(lean_grid), dim3(512), 0, s, list,
+                                   lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H,
+                                   W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
+            else if (var == 6)  // paired gather at 8 waves / SIMD (spills) or 6 (variant 7)
                 hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 8, 1, 1>), dim3(lean_grid), dim3(512), 0, s, list,
                                    lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H,
                                    W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
@@ -956,7 +964,7 @@ int mqr_vbg_unpack_weighted(mqr_vbg* v, const int32_t* union_keys, int64_t U, co
 int mqr_vbg_set_variant(mqr_vbg* v, int variant) {
     MQR_REQUIRE(v, "null volume");
     if (sync_all(v)) return 1;
-    if (!MQR_AB && ((variant & 0xff) == 3 || (variant & 0xff) == 5 || (variant & 0xff) == 6 || (variant & 0xff) == 7 || (variant & 0x8000))) {
+    if (!MQR_AB && ((variant & 0xff) == 3 || (variant & 0xff) == 5 || (variant & 0xff) == 6 || (variant & 0xff) == 7 || (variant & 0xff) == 8 || (variant & 0x8000))) {
         set_error("integrate variant " + std::to_string(variant) + " is an A/B kernel: only in tools/_ab/libmqr_ab.so (make ab)");
         return 1;
     }

@@ -649,6 +649,79 @@ __device__ __forceinline__ void lean_update(float2 (&tw)[ZPER], const float (&dv
     }
 }
 
+// ---- VALU-lean projection / update (PAIR = 2) ------------------------------------------------------
+// The same float operations as lean_gather / lean_update with fewer instructions around them:
+//  * in-image test as two unsigned compares of the float bits: 0 <= u <= W - 1 holds exactly when
+//    bits(u) <= bits(W - 1) for every u but -0.0 (sign bit) -- the host replaces a -0.0 principal
+//    point by +0.0, which changes no u and no pixel (x + -0 = x + +0 unless x = -0, and (int)-0 =
+//    (int)+0), so u = -0.0 cannot occur; NaN and negative values compare above the bound;
+//  * the depth read only by in-image lanes (exec mask), addressed as element (row W + col) of a
+//    stride-4 structured buffer view: no shift, no out-of-image select, and the in-image mask is
+//    kept as a lane mask for the update (no zero fill of the out-of-image lanes);
+//  * min(sdf, trunc) as one v_min_f32: sdf comes out of a subtraction, so it is never a signalling
+//    NaN and IEEE-mode v_min_f32 returns trunc for a NaN sdf, as fminf does (the compiler's fminf adds
+//    a canonicalising v_max_f32 in front).
+__device__ float mqr_struct_load_f32(__amdgpu_buffer_rsrc_t rsrc, int vindex, int voffset, int soffset,
+                                     int aux) __asm("llvm.amdgcn.struct.ptr.buffer.load.f32");
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t frame_rsrc_elems(const float* base, uint32_t n) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)4, (int)n, 0x00020000);
+}
+
+template <int ZPER, int ILP = 1>
+__device__ __forceinline__ void lean_gather_v(float (&dv)[ZPER], bool (&in)[ZPER], bool& bad, const FrameParams& fp,
+                                              __amdgpu_buffer_rsrc_t rs, const float (&xs)[ZPER],
+                                              const float (&ys)[ZPER], const float (&zs)[ZPER], uint32_t W,
+                                              uint32_t hm1_bits, uint32_t wm1_bits) {
+    float e[12];
+#pragma unroll
+    for (int j = 0; j < 12; ++j) e[j] = fp.ext[j];
+    const float fx = fp.fx, fy = fp.fy, cx = fp.cx, cy = fp.cy;
+#pragma unroll
+    for (int k = 0; k < ZPER; ++k) {
+        const float ax = xs[k] * e[0] + ys[k] * e[1];
+        const float ay = xs[k] * e[4] + ys[k] * e[5];
+        const float az = xs[k] * e[8] + ys[k] * e[9];
+        const float xc = (ax + zs[k] * e[2]) + e[3];
+        const float yc = (ay + zs[k] * e[6]) + e[7];
+        const float zc = (az + zs[k] * e[10]) + e[11];
+        bad |= (__float_as_uint(zc) - 0x2D800000u) > 0x30000000u;  // not 2^-36 <= zc <= 2^60
+        const float inv_z = rcp_m(zc);
+        const float u = fx * xc * inv_z + cx;
+        const float v = fy * yc * inv_z + cy;
+        in[k] = (__float_as_uint(v) <= hm1_bits) && (__float_as_uint(u) <= wm1_bits);
+        if (in[k]) dv[k] = mqr_struct_load_f32(rs, (int)__umul24((uint32_t)(int)v, W) + (int)u, 0, 0, 0);
+        if ((k + 1) % ILP == 0) __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+template <int ZPER, int ILP = 1>
+__device__ __forceinline__ void lean_update_v(float2 (&tw)[ZPER], const float (&dv)[ZPER], const bool (&in)[ZPER],
+                                              const FrameParams& fp, const float (&xs)[ZPER], const float (&ys)[ZPER],
+                                              const float (&zs)[ZPER], float depth_max, float sdf_trunc, float y1t) {
+    const float e8 = fp.ext[8], e9 = fp.ext[9], e10 = fp.ext[10], e11 = fp.ext[11];
+#pragma unroll
+    for (int k = 0; k < ZPER; ++k) {
+        if (in[k]) {  // an out-of-image voxel reads depth 0 in lean_update: no update
+            const float az = xs[k] * e8 + ys[k] * e9;
+            const float zc = (az + zs[k] * e10) + e11;
+            const float d = dv[k];
+            const float sdf = d - zc;
+            if (!(d <= 0) && !(d > depth_max) && !(sdf < -sdf_trunc)) {
+                float s;
+                asm("v_min_f32 %0, %1, %2" : "=v"(s) : "s"(sdf_trunc), "v"(sdf));
+                const float q0 = s * y1t;
+                const float q1 = __builtin_fmaf(__builtin_fmaf(-sdf_trunc, q0, s), y1t, q0);
+                const float sn = __builtin_fmaf(__builtin_fmaf(-sdf_trunc, q1, s), y1t, q1);
+                const float wgt = tw[k].y, wp = wgt + 1;
+                tw[k].x = (wgt * tw[k].x + sn) * rcp_m(wp);
+                tw[k].y = wp;
+            }
+        }
+        if ((k + 1) % ILP == 0) __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
 // Hand a block to the exact fix-up launch (its (slot, batch mask) appended to bad_out).
 __device__ __forceinline__ void hand_off(int32_t* bad_out, int* counters, int64_t list_cap, int32_t slot,
                                          bmask_t mask) {
@@ -755,7 +828,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
                 const int f = __builtin_ctzll(m);
                 m &= m - 1;
                 float dv[ZPER];
-                if constexpr (PAIR) {
+                if constexpr (PAIR == 2) {
+                    bool in[ZPER];
+                    lean_gather_v<ZPER, ILP>(dv, in, bad, fps[f], frame_rsrc_elems(depths + depth_frame[f] * HW, (uint32_t)HW),
+                                             xs, ys, zs, (uint32_t)W, __float_as_uint(hm1), __float_as_uint(wm1));
+                    lean_update_v<ZPER, ILP>(tw, dv, in, fps[f], xs, ys, zs, depth_max, sdf_trunc, y1t);
+                    continue;
+                } else if constexpr (PAIR) {
 #if MQR_AB
                     static_assert(MAP == 1, "pairs are the x-adjacent lanes of the brick map");
                     lean_gather_pair<ZPER, ILP>(dv, bad, fps[f], frame_rsrc(depths + depth_frame[f] * HW, bytes), xs,

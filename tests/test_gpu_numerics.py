@@ -50,7 +50,7 @@ def test_shortened_reciprocals_exact(which, lo, hi):
 AB = os.environ.get("MQR_AB_TEST") == "1"
 INTEGRATE_VARIANTS = {16: (0, 2, 0x100, 0x200, 0x400, 0x800), 8: (0, 2, 0x100)}
 if AB:
-    INTEGRATE_VARIANTS = {16: (0, 3, 5, 6, 7, 0x105, 0x605, 0x106, 0x8000, 0x8003), 8: (0, 0x8000)}
+    INTEGRATE_VARIANTS = {16: (0, 3, 5, 6, 7, 8, 0x105, 0x605, 0x106, 0x108, 0x8000, 0x8003, 0x8008), 8: (0, 0x8000)}
 
 
 def test_specialised_integrate_equals_generic():
@@ -71,6 +71,53 @@ def test_specialised_integrate_equals_generic():
             out[variant] = v.export()
         bad = []
         for variant in variants:  # every variant checked, the failures reported together
+            try:
+                compare_volumes(out[1], out[variant], 0.0)
+            except AssertionError as e:
+                bad.append((R, hex(variant), str(e)[:120]))
+        assert not bad, bad
+
+
+def test_special_depth_values_equal_generic():
+    """Depth frames holding NaN (both signs), +-inf, -0.0, negative depths, values at and just past
+    depth_max and denormals, seen by a camera whose principal point is -0.0 in one frame: every
+    integrate variant equals the generic kernel bit for bit, and the generic kernel equals the oracle
+    (Open3D's strict `d > 0`, `d <= depth_max` tests: a NaN depth passes both and updates with
+    sdf clamped to the truncation, as the oracle restates it)."""
+    import sys
+    from gpu_helpers import compare_volumes
+    from mqr import _lib, synthetic
+    from mqr.vbg import VoxelBlockGrid
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+    import oracle
+    seq = synthetic.make_sequence("room", n=8, height=240, width=320, f=262.5, noise=True, seed=77)
+    rng = np.random.default_rng(77)
+    specials = np.array([np.nan, -np.nan, np.inf, -np.inf, -0.0, 0.0, -1.0, 4.0, np.nextafter(np.float32(4.0), np.float32(5)),
+                         1e-40, np.float32(-1e-40)], np.float32)
+    depths = []
+    for d in seq["depth"]:
+        d = np.array(d, np.float32)
+        m = rng.random(d.shape) < 0.05
+        d[m] = specials[rng.integers(0, len(specials), int(m.sum()))]
+        depths.append(d)
+    K = np.array(seq["K"], np.float64)
+    K[2, 0, 2] = -0.0
+    K[2, 1, 2] = -0.0
+    args = dict(depth_scale=1.0, depth_max=4.0, trunc_voxel_multiplier=10.0)
+    ref = oracle.OracleVBG(0.01, 16, 64)
+    for i in range(len(depths)):
+        ref.integrate_frame(depths[i], K[i], seq["T_wc"][i], 1.0, 4.0, 10.0)
+    for R, variants in INTEGRATE_VARIANTS.items():
+        out = {}
+        for variant in (1,) + variants:
+            v = VoxelBlockGrid(voxel_size=0.01, block_resolution=R, block_count=64)
+            _lib.call("mqr_vbg_set_variant", v.handle, variant)
+            v.integrate_frames(depths, K, seq["T_wc"], **args)
+            out[variant] = v.export()
+        if R == 16:
+            compare_volumes(ref.export(), out[1], 0.0)
+        bad = []
+        for variant in variants:
             try:
                 compare_volumes(out[1], out[variant], 0.0)
             except AssertionError as e:
