@@ -16,6 +16,8 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <mutex>
+#include <unordered_map>
 
 #include "mqr_common.hpp"
 #include "vbg_kernels.hpp"
@@ -170,6 +172,39 @@ static int ensure_depth(mqr_vbg* v, int64_t floats) {
     }
     v->depth_cap = floats;
     return 0;
+}
+
+// Whether one Markstein correction gives IEEE s / t for every s in [-t, t] (lean_update_v<DIV1>):
+// k_check_strunc over the ~1e9 floats of [+0, t] once per t per process (a few ms; the sequence is
+// odd in s).  Cached; on any error the answer is false (two corrections stay).
+[[maybe_unused]] static bool strunc_one_correction_ok(float t) {
+    static std::mutex mu;
+    static std::unordered_map<uint32_t, bool> cache;
+    const uint32_t tb = __builtin_bit_cast(uint32_t, t);
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache.find(tb);
+    if (it != cache.end()) return it->second;
+    bool ok = false;
+    uint32_t* d = nullptr;
+    if (t > 0.0f && std::isfinite(t) && hipMalloc(&d, sizeof(uint32_t)) == hipSuccess) {
+        hipStream_t s = nullptr;
+        bool run = hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess &&
+                   hipMemsetAsync(d, 0, sizeof(uint32_t), s) == hipSuccess;
+        const uint64_t count = (uint64_t)tb + 1, chunk = 1ull << 28;
+        for (uint64_t off = 0; run && off < count; off += chunk) {
+            const uint64_t c = std::min<uint64_t>(chunk, count - off);
+            hipLaunchKernelGGL(k_check_strunc, dim3((unsigned)((c + 255) / 256)), dim3(256), 0, s, t, (uint32_t)off, c, d);
+            run = hipGetLastError() == hipSuccess;
+        }
+        uint32_t mism = 1;
+        if (run && hipMemcpyAsync(&mism, d, sizeof(uint32_t), hipMemcpyDeviceToHost, s) == hipSuccess &&
+            hipStreamSynchronize(s) == hipSuccess)
+            ok = mism == 0;
+        if (s) (void)hipStreamDestroy(s);
+        (void)hipFree(d);
+    }
+    cache[tb] = ok;
+    return ok;
 }
 
 // Host twin of den_unsafe(): true unless 2^-60 <= |x| <= 2^60.
@@ -327,14 +362,14 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
     //   0 default: k_integrate_lean -- R = 16: brick map, >= 8 waves per SIMD, 2 interleaved voxel
     //     chains; R = 8: plate map;  1 generic k_integrate (runtime R);  2 exact k_integrate_t;
     //   3 k_integrate_lean with the plate map (round-1 default, A/B);  5 k_integrate_lt (R = 16: depth
-    //     from packed LDS tiles, A/B);  6 / 7 the lean kernel with the paired-lane gather (A/B);  8 VALU-lean projection / update (A/B).  3, 5-8
+    //     from packed LDS tiles, A/B);  6 / 7 the lean kernel with the paired-lane gather (A/B);  8 VALU-lean projection / update, 9 the same with the zc check per block, 10 9 with one division correction (A/B).  3, 5-10
     //     exist only in the A/B library (MQR_AB, vbg_ab.hpp).
     //     DESIGN.md §4 has the measurements behind the choice.
     int var = v->kernel_variant;
-    if (var != 1 && var != 2 && var != 3 && var != 5 && var != 6 && var != 7 && var != 8) var = 0;
+    if (var != 1 && var != 2 && var != 3 && var != 5 && var != 6 && var != 7 && var != 8 && var != 9 && var != 10) var = 0;
     if (var != 1 && var != 2 && !lean_ok) var = 2;
     if (var == 5 && (v->R != 16 || W % 4 != 0 || W < 4 || (reinterpret_cast<uintptr_t>(depths) & 15))) var = 0;
-    if ((var == 6 || var == 7 || var == 8) && v->R != 16) var = 0;
+    if (var >= 6 && v->R != 16) var = 0;
     if (v->R != 16 && v->R != 8) var = 1;
     const int32_t* bad_list = v->bad[p];
     const bmask_t* bad_mask = reinterpret_cast<const bmask_t*>(v->bad[p] + v->list_cap);
@@ -351,6 +386,15 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
 #if MQR_AB
             if (var == 8)  // VALU-lean projection / update (lean_gather_v)
                 hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 8, 2, 2>), dim3(lean_grid), dim3(512), 0, s, list,
+                                   lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H,
+                                   W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
+            else if (var == 9 || (var == 10 && !strunc_one_correction_ok(sdf_trunc)))
+                // variant 8 with the zc range checked once per block (block_zc_unsafe)
+                hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 8, 2, 3>), dim3(lean_grid), dim3(512), 0, s, list,
+                                   lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H,
+                                   W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
+            else if (var == 10)  // variant 9 with s / sdf_trunc in one correction (verified for this sdf_trunc)
+                hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 8, 2, 3, 1>), dim3(lean_grid), dim3(512), 0, s, list,
                                    lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H,
                                    W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
             else if (var == 6)  // paired gather at 8 waves / SIMD (spills) or 6 (variant 7)
@@ -964,7 +1008,7 @@ int mqr_vbg_unpack_weighted(mqr_vbg* v, const int32_t* union_keys, int64_t U, co
 int mqr_vbg_set_variant(mqr_vbg* v, int variant) {
     MQR_REQUIRE(v, "null volume");
     if (sync_all(v)) return 1;
-    if (!MQR_AB && ((variant & 0xff) == 3 || (variant & 0xff) == 5 || (variant & 0xff) == 6 || (variant & 0xff) == 7 || (variant & 0xff) == 8 || (variant & 0x8000))) {
+    if (!MQR_AB && ((variant & 0xff) == 3 || (variant & 0xff) == 5 || (variant & 0xff) == 6 || (variant & 0xff) == 7 || (variant & 0xff) == 8 || (variant & 0xff) == 9 || (variant & 0xff) == 10 || (variant & 0x8000))) {
         set_error("integrate variant " + std::to_string(variant) + " is an A/B kernel: only in tools/_ab/libmqr_ab.so (make ab)");
         return 1;
     }

@@ -649,30 +649,25 @@ __device__ __forceinline__ void lean_update(float2 (&tw)[ZPER], const float (&dv
     }
 }
 
-// ---- VALU-lean projection / update (PAIR = 2) ------------------------------------------------------
+// ---- VALU-lean projection / update (PAIR = 2, 3) ---------------------------------------------------
 // The same float operations as lean_gather / lean_update with fewer instructions around them:
 //  * in-image test as two unsigned compares of the float bits: 0 <= u <= W - 1 holds exactly when
 //    bits(u) <= bits(W - 1) for every u but -0.0 (sign bit) -- the host replaces a -0.0 principal
 //    point by +0.0, which changes no u and no pixel (x + -0 = x + +0 unless x = -0, and (int)-0 =
 //    (int)+0), so u = -0.0 cannot occur; NaN and negative values compare above the bound;
-//  * the depth read only by in-image lanes (exec mask), addressed as element (row W + col) of a
-//    stride-4 structured buffer view: no shift, no out-of-image select, and the in-image mask is
-//    kept as a lane mask for the update (no zero fill of the out-of-image lanes);
 //  * min(sdf, trunc) as one v_min_f32: sdf comes out of a subtraction, so it is never a signalling
 //    NaN and IEEE-mode v_min_f32 returns trunc for a NaN sdf, as fminf does (the compiler's fminf adds
-//    a canonicalising v_max_f32 in front).
-__device__ float mqr_struct_load_f32(__amdgpu_buffer_rsrc_t rsrc, int vindex, int voffset, int soffset,
-                                     int aux) __asm("llvm.amdgcn.struct.ptr.buffer.load.f32");
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t frame_rsrc_elems(const float* base, uint32_t n) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)4, (int)n, 0x00020000);
-}
-
-template <int ZPER, int ILP = 1>
-__device__ __forceinline__ void lean_gather_v(float (&dv)[ZPER], bool (&in)[ZPER], bool& bad, const FrameParams& fp,
+//    a canonicalising v_max_f32 in front);
+//  * (PAIR = 3) the zc range checked once per block and batch (block_zc_unsafe), not per voxel-frame.
+// The depth read stays a gather by every lane through the raw view (out-of-image lanes read 0 past
+// the end): reading under the in-image exec mask kept 8 lane masks live across the gathers, which
+// the compiler spilled to VGPR booleans (3 VALU per voxel-frame) and made the update wait for all 8
+// gathers.
+template <int ZPER, int ILP = 1, bool ZCHK = true>
+__device__ __forceinline__ void lean_gather_v(float (&dv)[ZPER], bool& bad, const FrameParams& fp,
                                               __amdgpu_buffer_rsrc_t rs, const float (&xs)[ZPER],
-                                              const float (&ys)[ZPER], const float (&zs)[ZPER], uint32_t W,
-                                              uint32_t hm1_bits, uint32_t wm1_bits) {
+                                              const float (&ys)[ZPER], const float (&zs)[ZPER], uint32_t W4,
+                                              uint32_t past_end, uint32_t hm1_bits, uint32_t wm1_bits) {
     float e[12];
 #pragma unroll
     for (int j = 0; j < 12; ++j) e[j] = fp.ext[j];
@@ -685,41 +680,70 @@ __device__ __forceinline__ void lean_gather_v(float (&dv)[ZPER], bool (&in)[ZPER
         const float xc = (ax + zs[k] * e[2]) + e[3];
         const float yc = (ay + zs[k] * e[6]) + e[7];
         const float zc = (az + zs[k] * e[10]) + e[11];
-        bad |= (__float_as_uint(zc) - 0x2D800000u) > 0x30000000u;  // not 2^-36 <= zc <= 2^60
+        if (ZCHK) bad |= (__float_as_uint(zc) - 0x2D800000u) > 0x30000000u;  // not 2^-36 <= zc <= 2^60
         const float inv_z = rcp_m(zc);
         const float u = fx * xc * inv_z + cx;
         const float v = fy * yc * inv_z + cy;
-        in[k] = (__float_as_uint(v) <= hm1_bits) && (__float_as_uint(u) <= wm1_bits);
-        if (in[k]) dv[k] = mqr_struct_load_f32(rs, (int)__umul24((uint32_t)(int)v, W) + (int)u, 0, 0, 0);
+        const bool in = (__float_as_uint(v) <= hm1_bits) && (__float_as_uint(u) <= wm1_bits);
+        const uint32_t off = in ? __umul24((uint32_t)(int)v, W4) + ((uint32_t)(int)u << 2) : past_end;
+        dv[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
         if ((k + 1) % ILP == 0) __builtin_amdgcn_sched_barrier(0);
     }
 }
 
-template <int ZPER, int ILP = 1>
-__device__ __forceinline__ void lean_update_v(float2 (&tw)[ZPER], const float (&dv)[ZPER], const bool (&in)[ZPER],
-                                              const FrameParams& fp, const float (&xs)[ZPER], const float (&ys)[ZPER],
+// DIV1: s / sdf_trunc with one Markstein correction (the host enables it only for an sdf_trunc whose
+// every s in [0, sdf_trunc] it verified against IEEE division, strunc_one_correction_ok; the
+// sequence is odd in s, so negative s follow).
+template <int ZPER, int ILP = 1, int DIV1 = 0>
+__device__ __forceinline__ void lean_update_v(float2 (&tw)[ZPER], const float (&dv)[ZPER], const FrameParams& fp,
+                                              const float (&xs)[ZPER], const float (&ys)[ZPER],
                                               const float (&zs)[ZPER], float depth_max, float sdf_trunc, float y1t) {
     const float e8 = fp.ext[8], e9 = fp.ext[9], e10 = fp.ext[10], e11 = fp.ext[11];
 #pragma unroll
     for (int k = 0; k < ZPER; ++k) {
-        if (in[k]) {  // an out-of-image voxel reads depth 0 in lean_update: no update
-            const float az = xs[k] * e8 + ys[k] * e9;
-            const float zc = (az + zs[k] * e10) + e11;
-            const float d = dv[k];
-            const float sdf = d - zc;
-            if (!(d <= 0) && !(d > depth_max) && !(sdf < -sdf_trunc)) {
-                float s;
-                asm("v_min_f32 %0, %1, %2" : "=v"(s) : "s"(sdf_trunc), "v"(sdf));
-                const float q0 = s * y1t;
-                const float q1 = __builtin_fmaf(__builtin_fmaf(-sdf_trunc, q0, s), y1t, q0);
-                const float sn = __builtin_fmaf(__builtin_fmaf(-sdf_trunc, q1, s), y1t, q1);
-                const float wgt = tw[k].y, wp = wgt + 1;
-                tw[k].x = (wgt * tw[k].x + sn) * rcp_m(wp);
-                tw[k].y = wp;
-            }
+        const float az = xs[k] * e8 + ys[k] * e9;
+        const float zc = (az + zs[k] * e10) + e11;
+        const float d = dv[k];
+        const float sdf = d - zc;
+        if (!(d <= 0) && !(d > depth_max) && !(sdf < -sdf_trunc)) {
+            float s;
+            asm("v_min_f32 %0, %1, %2" : "=v"(s) : "s"(sdf_trunc), "v"(sdf));
+            const float q0 = s * y1t;
+            const float q1 = __builtin_fmaf(__builtin_fmaf(-sdf_trunc, q0, s), y1t, q0);
+            const float sn = DIV1 ? q1 : __builtin_fmaf(__builtin_fmaf(-sdf_trunc, q1, s), y1t, q1);
+            const float wgt = tw[k].y, wp = wgt + 1;
+            tw[k].x = (wgt * tw[k].x + sn) * rcp_m(wp);
+            tw[k].y = wp;
         }
         if ((k + 1) % ILP == 0) __builtin_amdgcn_sched_barrier(0);
     }
+}
+
+// The zc range check of lean_gather (2^-36 <= zc <= 2^60, where rcp_m is exact) once per block and
+// batch instead of per voxel-frame (PAIR = 3): thread (frame j = tid / 8, corner c = tid % 8) bounds
+// zc at one corner of the block's voxel-coordinate box.  The voxel coordinates are the float values
+// fl((float)i * voxel_size), monotone in i, so every voxel lies in the box of the corner values; the
+// exact affine Z = x e8 + y e9 + z e10 + e11 takes its extremes over the box at the corners; the
+// float32 evaluation (three products, three sums) differs from Z by at most gamma_4 A < 2^-21 A,
+// A = max|x| |e8| + max|y| |e9| + max|z| |e10| + |e11| over the box.  A corner with Z - 2^-20 A <
+// 2^-36 or Z + 2^-20 A > 2^60 (or NaN) marks the block bad: the exact fix-up launch redoes it.
+template <int R>
+__device__ __forceinline__ bool block_zc_unsafe(int tid, bmask_t mask, const FrameParams* __restrict__ fps, int xb,
+                                                int yb, int zb, float voxel_size) {
+    const int j = tid >> 3, c = tid & 7;
+    if (j >= 64 || !((mask >> j) & 1)) return false;
+    const FrameParams& fp = fps[j];
+    const float xl = (float)(xb * R) * voxel_size, xh = (float)(xb * R + R - 1) * voxel_size;
+    const float yl = (float)(yb * R) * voxel_size, yh = (float)(yb * R + R - 1) * voxel_size;
+    const float zl = (float)(zb * R) * voxel_size, zh = (float)(zb * R + R - 1) * voxel_size;
+    const double e8 = fp.ext[8], e9 = fp.ext[9], e10 = fp.ext[10], e11 = fp.ext[11];
+    const double x = (c & 1) ? xh : xl, y = (c & 2) ? yh : yl, z = (c & 4) ? zh : zl;
+    const double Z = x * e8 + y * e9 + z * e10 + e11;
+    const double A = fmax(fabs((double)xl), fabs((double)xh)) * fabs(e8) +
+                     fmax(fabs((double)yl), fabs((double)yh)) * fabs(e9) +
+                     fmax(fabs((double)zl), fabs((double)zh)) * fabs(e10) + fabs(e11);
+    const double err = A * 0x1p-20;
+    return !(Z - err >= 0x1p-36 && Z + err <= 0x1p60);
 }
 
 // Hand a block to the exact fix-up launch (its (slot, batch mask) appended to bad_out).
@@ -769,7 +793,7 @@ __device__ void lean_gather_pair(float (&dv)[ZPER], bool& bad, const FrameParams
 #endif
 
 // PAIR (A/B library only, variant 6): the paired-lane gather of vbg_ab.hpp.
-template <int R, int NT, int MAP = 0, int WPE = 1, int ILP = 1, int PAIR = 0>
+template <int R, int NT, int MAP = 0, int WPE = 1, int ILP = 1, int PAIR = 0, int DIV1 = 0>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void k_integrate_lean(
     const int32_t* __restrict__ list, const bmask_t* __restrict__ lmask, int32_t* __restrict__ bad_out,
     int* __restrict__ counters, int64_t list_cap, Table t, float2* __restrict__ pool, float voxel_size,
@@ -824,15 +848,18 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
                 bad |= !(w >= 0.0f && w <= 0x1p23f && w == __builtin_truncf(w));
             }
             bmask_t m = mask;
+            if constexpr (PAIR == 3) {  // block-level zc range check (block_zc_unsafe): skip the frame loop
+                static_assert(NT == 512, "one (frame, corner) per thread");
+                if (__syncthreads_or(block_zc_unsafe<R>(tid, mask, fps, xb, yb, zb, voxel_size))) bad = true, m = 0;
+            }
             while (m) {
                 const int f = __builtin_ctzll(m);
                 m &= m - 1;
                 float dv[ZPER];
-                if constexpr (PAIR == 2) {
-                    bool in[ZPER];
-                    lean_gather_v<ZPER, ILP>(dv, in, bad, fps[f], frame_rsrc_elems(depths + depth_frame[f] * HW, (uint32_t)HW),
-                                             xs, ys, zs, (uint32_t)W, __float_as_uint(hm1), __float_as_uint(wm1));
-                    lean_update_v<ZPER, ILP>(tw, dv, in, fps[f], xs, ys, zs, depth_max, sdf_trunc, y1t);
+                if constexpr (PAIR == 2 || PAIR == 3) {
+                    lean_gather_v<ZPER, ILP, PAIR == 2>(dv, bad, fps[f], frame_rsrc(depths + depth_frame[f] * HW, bytes),
+                                                         xs, ys, zs, W4, bytes, __float_as_uint(hm1), __float_as_uint(wm1));
+                    lean_update_v<ZPER, ILP, DIV1>(tw, dv, fps[f], xs, ys, zs, depth_max, sdf_trunc, y1t);
                     continue;
                 } else if constexpr (PAIR) {
 #if MQR_AB
@@ -872,6 +899,19 @@ __global__ void k_check_rcp(int mode, uint32_t lo_bits, uint64_t count, uint32_t
         atomicAdd(mismatches, 1u);
         atomicMin(first_bad, bits);
     }
+}
+
+// One-correction quotient s / t of lean_update_v<DIV1 = 1> against IEEE division for every float s
+// with bits in [lo_bits, lo_bits + count) (the host passes [+0, t]).
+__global__ void k_check_strunc(float t, uint32_t lo_bits, uint64_t count, uint32_t* mismatches) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    const float s = __uint_as_float(lo_bits + (uint32_t)i);
+    const float y0t = __builtin_amdgcn_rcpf(t);
+    const float y1t = __builtin_fmaf(__builtin_fmaf(-t, y0t, 1.0f), y0t, y0t);
+    const float q0 = s * y1t;
+    const float q1 = __builtin_fmaf(__builtin_fmaf(-t, q0, s), y1t, q0);
+    if (__float_as_uint(q1) != __float_as_uint(s / t)) atomicAdd(mismatches, 1u);
 }
 
 __global__ void k_check_div(int which_core, float b, uint32_t lo_bits, uint64_t count, uint32_t* mismatches, uint32_t* first_bad) {

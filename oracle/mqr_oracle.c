@@ -883,9 +883,33 @@ int orc_depth_boundary_mask(const float* t_hit, int H, int W, double depth_trunc
 typedef struct {
     const double* P; /* 3 per point */
     int32_t* idx;    /* point ids, reordered */
-    uint8_t* axis;   /* split axis of the node whose middle element is this position */
+    uint8_t* axis;   /* split axis of the node whose middle element is this position (unused by the search) */
     double* split;   /* its split value, recorded at build time (the children's builds reorder idx) */
+    double* box;     /* 12 per node position: tight boxes (min xyz, max xyz) of [lo, mid) and [mid, hi) --
+                      * the search prunes a child by its box distance: with the split plane alone a
+                      * query far from a compact point set visits every node */
 } kdtree;
+
+static void kd_bounds(const kdtree* t, int64_t lo, int64_t hi, double* b) {
+    b[0] = b[1] = b[2] = INFINITY;
+    b[3] = b[4] = b[5] = -INFINITY;
+    for (int64_t i = lo; i < hi; ++i)
+        for (int a = 0; a < 3; ++a) {
+            const double v = t->P[3 * t->idx[i] + a];
+            if (v < b[a]) b[a] = v;
+            if (v > b[3 + a]) b[3 + a] = v;
+        }
+}
+
+/* squared distance from q to the box b (0 inside) */
+static double box_d2(const double* q, const double* b) {
+    double s = 0.0;
+    for (int a = 0; a < 3; ++a) {
+        const double d = q[a] < b[a] ? b[a] - q[a] : (q[a] > b[3 + a] ? q[a] - b[3 + a] : 0.0);
+        s += d * d;
+    }
+    return s;
+}
 
 /* (value on axis, point id) order */
 static int kd_less(const double* P, int32_t i, int32_t j, int ax) {
@@ -936,6 +960,8 @@ static void kd_build(kdtree* t, int64_t lo, int64_t hi) {
     kd_select(t->P, t->idx, lo, hi, mid, ax);
     t->axis[mid] = (uint8_t)ax;
     t->split[mid] = t->P[3 * t->idx[mid] + ax];
+    kd_bounds(t, lo, mid, t->box + 12 * mid);
+    kd_bounds(t, mid, hi, t->box + 12 * mid + 6);
     kd_build(t, lo, mid);
     kd_build(t, mid, hi);
 }
@@ -969,15 +995,17 @@ static void kd_search(const kdtree* t, int64_t lo, int64_t hi, const double* q, 
         return;
     }
     const int64_t mid = (lo + hi) / 2;
-    const int ax = t->axis[mid];
-    const double s = t->split[mid], diff = q[ax] - s;
-    /* left range [lo, mid) holds values <= s, right [mid, hi) values >= s */
-    if (diff < 0) {
-        kd_search(t, lo, mid, q, b);
-        if (b->n < b->k || diff * diff <= b->d2[b->n - 1]) kd_search(t, mid, hi, q, b);
-    } else {
-        kd_search(t, mid, hi, q, b);
-        if (b->n < b->k || diff * diff <= b->d2[b->n - 1]) kd_search(t, lo, mid, q, b);
+    /* nearer child (by box distance) first; a child is visited while its box is not farther than the
+     * current k-th distance (<=: equal distances still compete by vertex index) */
+    const double dl = box_d2(q, t->box + 12 * mid), dr = box_d2(q, t->box + 12 * mid + 6);
+    const int left_first = dl <= dr;
+    for (int pass = 0; pass < 2; ++pass) {
+        const int left = pass == 0 ? left_first : !left_first;
+        const double dc = left ? dl : dr;
+        if (b->n < b->k || dc <= b->d2[b->n - 1]) {
+            if (left) kd_search(t, lo, mid, q, b);
+            else kd_search(t, mid, hi, q, b);
+        }
     }
 }
 
@@ -1027,7 +1055,7 @@ int orc_color_map(const float* V, int64_t nv, const uint8_t* images, const float
     double* P = (double*)malloc(sizeof(double) * 3 * (nv > 0 ? nv : 1));
     for (int64_t i = 0; i < 3 * nv; ++i) P[i] = V[i];
     kdtree t = {P, (int32_t*)malloc(sizeof(int32_t) * (nvalid > 0 ? nvalid : 1)), (uint8_t*)calloc(nvalid + 1, 1),
-                (double*)calloc(nvalid + 1, sizeof(double))};
+                (double*)calloc(nvalid + 1, sizeof(double)), (double*)calloc(12 * (nvalid + 1), sizeof(double))};
     int64_t j = 0;
     for (int64_t i = 0; i < nv; ++i)
         if (counts[i] > 0) t.idx[j++] = (int32_t)i;
@@ -1051,6 +1079,7 @@ int orc_color_map(const float* V, int64_t nv, const uint8_t* images, const float
     free(t.idx);
     free(t.axis);
     free(t.split);
+    free(t.box);
     free(P);
     free(avg);
     free(depth);

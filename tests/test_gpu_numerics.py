@@ -50,7 +50,7 @@ def test_shortened_reciprocals_exact(which, lo, hi):
 AB = os.environ.get("MQR_AB_TEST") == "1"
 INTEGRATE_VARIANTS = {16: (0, 2, 0x100, 0x200, 0x400, 0x800), 8: (0, 2, 0x100)}
 if AB:
-    INTEGRATE_VARIANTS = {16: (0, 3, 5, 6, 7, 8, 0x105, 0x605, 0x106, 0x108, 0x8000, 0x8003, 0x8008), 8: (0, 0x8000)}
+    INTEGRATE_VARIANTS = {16: (0, 3, 5, 6, 7, 8, 9, 10, 0x105, 0x605, 0x106, 0x108, 0x109, 0x10a, 0x8000, 0x8003, 0x8008, 0x8009, 0x800a), 8: (0, 0x8000)}
 
 
 def test_specialised_integrate_equals_generic():
@@ -204,7 +204,8 @@ def test_lean_integrate_exact_fallback():
     depths = [near] + [np.asarray(d, np.float32) for d in seq["depth"]]
     Ks = np.concatenate([seq["K"][:1], seq["K"]])
     Ts = np.concatenate([np.eye(4)[None], seq["T_wc"]])
-    cases = ((16, 1), (16, 0), (16, 5 if AB else 0x200), (16, 2), (16, 0x100), (8, 1), (8, 0), (8, 2))
+    cases = ((16, 1), (16, 0), (16, 5 if AB else 0x200), (16, 2), (16, 0x100), (16, 9 if AB else 0x400),
+             (16, 8 if AB else 0x800), (8, 1), (8, 0), (8, 2))
     out = []
     for R, variant in cases:
         v = VoxelBlockGrid(voxel_size=0.005, block_resolution=R, block_count=64)
@@ -220,10 +221,10 @@ def test_lean_integrate_exact_fallback():
         v.import_blocks(keys, tsdf, wgt)
         v.integrate_frames(depths[3:], Ks[3:], Ts[3:], depth_scale=1.0, depth_max=4.0, trunc_voxel_multiplier=10.0)
         out.append(v.export())
-    for i in range(1, 5):
+    for i in range(1, 7):
         assert compare_volumes(out[0], out[i], 0.0) == 0.0, cases[i]
-    for i in (6, 7):
-        assert compare_volumes(out[5], out[i], 0.0) == 0.0, cases[i]
+    for i in (8, 9):
+        assert compare_volumes(out[7], out[i], 0.0) == 0.0, cases[i]
 
 
 @pytest.mark.parametrize("mode,a_max,b_lo,b_hi", [
