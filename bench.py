@@ -601,6 +601,26 @@ def pmc_traffic(H, W, frames):
     return None, None
 
 
+def gather_ceiling(avg_launch_ms, gathers_per_launch, cus):
+    """The integrate launch against the measured gather-instruction ceiling (tools/gather_ceiling.hip ->
+    profiles/*_gather_ceiling.jsonl, pattern "brick": the kernel's lane map gathering 4-byte depths
+    from an L2-resident frame with no other work).  One depth gather instruction per 64 voxel-frames."""
+    import glob
+    for path in reversed(sorted(glob.glob(os.path.join(ROOT, "profiles", "*_gather_ceiling.jsonl")))):
+        try:
+            rows = [json.loads(x) for x in open(path) if x.strip()]
+        except (OSError, ValueError):
+            continue
+        ceil = {r["pattern"]: r["ns_per_gather_instr_per_cu"] for r in rows}
+        if "brick" not in ceil or not avg_launch_ms or not gathers_per_launch:
+            continue
+        achieved = avg_launch_ms * 1e6 / (gathers_per_launch / cus)
+        return {"unit": "ns per gather instruction per CU", "achieved": achieved, "ceiling": ceil["brick"],
+                "frac": ceil["brick"] / achieved, "gathers_per_launch": gathers_per_launch,
+                "ceiling_16B_windows": ceil.get("brick_x4"), "source": os.path.relpath(path, ROOT)}
+    return None
+
+
 def pmc_binding(avg_launch_ms):
     """The integrate kernel's binding resource from the committed rocprofv3 counter passes of the
     default kernel (tools/pmc_ab.sh -> profiles/*_pmc_integrate_counters.json, entry "v0:..."):
@@ -1019,7 +1039,9 @@ def main():
             "raycast": extras.get("raycast"),
             "meshfilter": extras.get("meshfilter"),
             "host_input_frames_per_s": extras.get("host_input_frames_per_s"),
-            "roofline_binding": pmc_binding(avg_ms),
+            "roofline_binding": dict(pmc_binding(avg_ms) or {}, gather_ceiling=gather_ceiling(
+                avg_ms, st["frame_blocks"] * args.block_resolution ** 3 / 64 / launches,
+                torch.cuda.get_device_properties(local).multi_processor_count)),
             "roofline": {"bound": "hbm", "kernel": "k_integrate_lean", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "peak_measured_copy": extras.get("hbm_copy_gbs"),
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

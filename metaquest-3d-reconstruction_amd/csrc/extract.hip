@@ -714,11 +714,121 @@ __device__ inline int32_t mc_vid(uint32_t vbase, uint32_t ex, uint32_t ey, uint3
                      (axis > 0 ? (ex >> x) & 1u : 0u) + (axis > 1 ? (ey >> x) & 1u : 0u));
 }
 
+// Vertex i of a block (emission pass): its row by binary search over the row vertex bases, its voxel
+// and edge by row_select, position and normal from the tsdf taps of the pool.
+template <class M>
+__device__ __forceinline__ void mc_emit_vertex(int i, const uint4* rows, const int32_t* nbrow,
+                                               const float2* __restrict__ pool, uint32_t pres, int xb, int yb, int zb,
+                                               float voxel_size, int32_t vb0, float* pos, float* nrm) {
+    constexpr int R = M::C - 1;
+    int lo = 0, hi = M::R2 - 1;  // last row whose vertex base is <= i (non-empty)
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if ((int)rows[mid].x <= i) lo = mid; else hi = mid - 1;
+    }
+    const uint4 rw = rows[lo];
+    const uint32_t ex = rw.z & 0xffffu, ey = rw.z >> 16, ez = rw.w & 0xffffu;
+    int k = i - (int)rw.x, x;
+    row_select<R>(ex, ey, ez, k, x);
+    const uint32_t m3 = ((ex >> x) & 1u) | (((ey >> x) & 1u) << 1) | (((ez >> x) & 1u) << 2);
+    const int y = lo % R, z = lo / R;
+    float tsdf_o, tsdf_e;
+    float no[3] = {0.f, 0.f, 0.f}, ne[3] = {0.f, 0.f, 0.f};
+    int axis = 0;
+    if (pres == kAll27) {  // block-uniform
+        uint32_t mm = m3;
+        for (int j = 0; j < k; ++j) mm &= mm - 1;
+        axis = __builtin_ctz(mm);
+        mc_edge_full<M>(nbrow, pool, x, y, z, axis, tsdf_o, tsdf_e, no, ne);
+    } else {
+        tsdf_o = mc_tsdf<M>(nbrow, pool, x, y, z);
+        mc_normal<M>(nbrow, pool, pres, x, y, z, no);
+        // upstream keeps one per-voxel normal scratch across the voxel's edges: replay the earlier ones
+        uint32_t mm = m3;
+        for (int j = 0;; ++j) {
+            axis = __builtin_ctz(mm);
+            mc_normal<M>(nbrow, pool, pres, x + (axis == 0), y + (axis == 1), z + (axis == 2), ne);
+            if (j == k) break;
+            mm &= mm - 1;
+        }
+        tsdf_e = mc_tsdf<M>(nbrow, pool, x + (axis == 0), y + (axis == 1), z + (axis == 2));
+    }
+    const float ratio = (0 - tsdf_o) / (tsdf_e - tsdf_o);
+    const float rx = ratio * (int)(axis == 0), ry = ratio * (int)(axis == 1), rz = ratio * (int)(axis == 2);
+    const int gx = xb * R + x, gy = yb * R + y, gz = zb * R + z;
+    const int64_t id = (int64_t)vb0 + i;
+    pos[3 * id + 0] = voxel_size * (gx + rx);
+    pos[3 * id + 1] = voxel_size * (gy + ry);
+    pos[3 * id + 2] = voxel_size * (gz + rz);
+    const float nx = (1 - ratio) * no[0] + ratio * ne[0];
+    const float ny = (1 - ratio) * no[1] + ratio * ne[1];
+    const float nz = (1 - ratio) * no[2] + ratio * ne[2];
+    write_normal(nx, ny, nz, nrm + 3 * id);
+}
+
+// Triangle i of a block (emission pass): its cube by binary search over the row triangle bases and a
+// walk over the row's owned cubes, its three vertex ids from the row records (this block's in LDS,
+// a +x / +y / +z neighbour's from rows4).
+template <class M>
+__device__ __forceinline__ void mc_emit_tri(int i, const uint4* rows, const uint32_t* rowN, const uint32_t* triC,
+                                            const uint64_t* triP, const int32_t* nbrow, const int32_t* nbvoff,
+                                            const uint4* __restrict__ rows4, int32_t vb0, int32_t tb0, int32_t* tri) {
+    constexpr int R = M::C - 1;
+    int lo = 0, hi = M::R2 - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if ((int)rows[mid].y <= i) lo = mid; else hi = mid - 1;
+    }
+    const uint4 rw = rows[lo];
+    const int y = lo % R, z = lo / R;
+    const uint32_t a = rowN[M::q(y, z)], bb = rowN[M::q(y + 1, z)], c = rowN[M::q(y, z + 1)];
+    const uint32_t d = rowN[M::q(y + 1, z + 1)];
+    uint32_t oc = rw.w >> 16;
+    int k = i - (int)rw.y, x = 0, ci = 0;
+    while (oc) {
+        x = __builtin_ctz(oc);
+        ci = mc_index(a >> (x + 1), bb >> (x + 1), c >> (x + 1), d >> (x + 1));
+        const int n = (int)((triC[ci >> 3] >> ((ci & 7) * 4)) & 0xFu);
+        if (k < n) break;
+        k -= n;
+        oc &= oc - 1;
+    }
+    const uint64_t te = triP[ci] >> (12 * k);
+    const int64_t t = (int64_t)tb0 + i;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        const int edge = (int)((te >> (4 * j)) & 0xFu);
+        const uint32_t es = (uint32_t)(kEdgeShifts >> (5 * edge));
+        const int ox = x + (int)(es & 1u), oy = y + (int)((es >> 1) & 1u), oz = z + (int)((es >> 2) & 1u);
+        const int axis = (int)((es >> 3) & 3u);
+        int32_t vid;
+        if (ox < R && oy < R && oz < R) {
+            const uint4 ow = rows[oz * R + oy];
+            vid = vb0 + mc_vid(ow.x, ow.z & 0xffffu, ow.z >> 16, ow.w & 0xffffu, ox, axis);
+        } else {
+            const int dx = ox >= R, dy = oy >= R, dz = oz >= R;
+            const int k27 = (dx + 1) + 3 * (dy + 1) + 9 * (dz + 1);
+            const int32_t nbuf = nbrow[k27];
+            if (nbuf < 0) {
+                vid = -1;  // cannot happen for a valid cube (all corners exist); stay in bounds
+            } else {
+                const int lx = ox - dx * R, ly = oy - dy * R, lz = oz - dz * R;
+                const uint4 ow = rows4[(int64_t)nbuf * M::R2 + lz * R + ly];
+                vid = nbvoff[k27] + mc_vid(ow.x, ow.z & 0xffffu, ow.z >> 16, ow.w & 0xffffu, lx, axis);
+            }
+        }
+        tri[3 * t + (2 - j)] = vid;
+    }
+}
+
 // Emission of a block with vertices or triangles, from the count pass's row records: vertices
 // (positions and normals from tsdf values gathered from the pool) and triangles at the offsets of
 // the scan, in (block, voxel, edge) / (block, cube, triangle) order.
-template <int R>
-__global__ __launch_bounds__(kMcThreads) void k_mc_emit(const int32_t* __restrict__ nb, const uint64_t* __restrict__ bkeys,
+// NT threads per block; MERGED: vertices and triangles as one strided item loop (items [0, nv) are
+// vertices, [nv, nv + nt) triangles), so a block's dependent load rounds are ceil((nv + nt) / NT)
+// instead of ceil(nv / NT) + ceil(nt / NT).
+template <int R, int NT = kMcThreads, bool MERGED = false>
+__global__ __launch_bounds__(NT) void k_mc_emit(const int32_t* __restrict__ nb, const uint64_t* __restrict__ bkeys,
                                                         const float2* __restrict__ pool, float voxel_size,
                                                         const int32_t* __restrict__ vcount,
                                                         const int32_t* __restrict__ tcount,
@@ -728,7 +838,7 @@ __global__ __launch_bounds__(kMcThreads) void k_mc_emit(const int32_t* __restric
                                                         const uint32_t* __restrict__ rowNt, float* pos, float* nrm,
                                                         int32_t* tri, int64_t cap_v, int64_t cap_t) {
     using M = Mc<R, 1>;
-    static_assert(kMcThreads >= 256, "one thread per triangle-table row");
+    static_assert(NT >= 256, "one thread per triangle-table row");
     __shared__ uint32_t rowN[M::S2];
     __shared__ uint4 rows[M::R2];  // vbase, tbase, ex | ey << 16, ez | oc << 16
     __shared__ int32_t nbrow[27], nbvoff[27];
@@ -741,114 +851,33 @@ __global__ __launch_bounds__(kMcThreads) void k_mc_emit(const int32_t* __restric
     // outputs past the speculative capacity: the host re-runs this pass into exact buffers
     if ((int64_t)vb0 + nvb > cap_v || (int64_t)tb0 + ntb > cap_t) return;
     const int tid = threadIdx.x;
-    triP[tid] = mqr_tri_packed[tid];
+    if (tid < 256) triP[tid] = mqr_tri_packed[tid];
     if (tid < 32) triC[tid] = mqr_tri_count_packed[tid];
     if (tid < 27) {
         const int32_t q = nb[b * 27 + tid];
         nbrow[tid] = q;
         nbvoff[tid] = q >= 0 ? voff[q] : 0;
     }
-    for (int r = tid; r < M::R2; r += blockDim.x) rows[r] = rows4[b * M::R2 + r];
+    for (int r = tid; r < M::R2; r += NT) rows[r] = rows4[b * M::R2 + r];
     if (ntb)
-        for (int q = tid; q < M::S2; q += blockDim.x) rowN[q] = rowNt[b * M::S2 + q];
+        for (int q = tid; q < M::S2; q += NT) rowN[q] = rowNt[b * M::S2 + q];
     __syncthreads();
     const int lane = tid & 63;
     const uint32_t pres = (uint32_t)__ballot(lane < 27 && nbrow[lane < 27 ? lane : 0] >= 0);
 
     int xb, yb, zb;
     unpack_key(bkeys[b], xb, yb, zb);
-    for (int i = tid; i < nvb; i += blockDim.x) {
-        int lo = 0, hi = M::R2 - 1;  // last row whose vertex base is <= i (non-empty)
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if ((int)rows[mid].x <= i) lo = mid; else hi = mid - 1;
+    if (MERGED) {
+        for (int i = tid; i < nvb + ntb; i += NT) {
+            if (i < nvb)
+                mc_emit_vertex<M>(i, rows, nbrow, pool, pres, xb, yb, zb, voxel_size, vb0, pos, nrm);
+            else
+                mc_emit_tri<M>(i - nvb, rows, rowN, triC, triP, nbrow, nbvoff, rows4, vb0, tb0, tri);
         }
-        const uint4 rw = rows[lo];
-        const uint32_t ex = rw.z & 0xffffu, ey = rw.z >> 16, ez = rw.w & 0xffffu;
-        int k = i - (int)rw.x, x;
-        row_select<R>(ex, ey, ez, k, x);
-        const uint32_t m3 = ((ex >> x) & 1u) | (((ey >> x) & 1u) << 1) | (((ez >> x) & 1u) << 2);
-        const int y = lo % R, z = lo / R;
-        float tsdf_o, tsdf_e;
-        float no[3] = {0.f, 0.f, 0.f}, ne[3] = {0.f, 0.f, 0.f};
-        int axis = 0;
-        if (pres == kAll27) {  // block-uniform
-            uint32_t mm = m3;
-            for (int j = 0; j < k; ++j) mm &= mm - 1;
-            axis = __builtin_ctz(mm);
-            mc_edge_full<M>(nbrow, pool, x, y, z, axis, tsdf_o, tsdf_e, no, ne);
-        } else {
-            tsdf_o = mc_tsdf<M>(nbrow, pool, x, y, z);
-            mc_normal<M>(nbrow, pool, pres, x, y, z, no);
-            // upstream keeps one per-voxel normal scratch across the voxel's edges: replay the earlier ones
-            uint32_t mm = m3;
-            for (int j = 0;; ++j) {
-                axis = __builtin_ctz(mm);
-                mc_normal<M>(nbrow, pool, pres, x + (axis == 0), y + (axis == 1), z + (axis == 2), ne);
-                if (j == k) break;
-                mm &= mm - 1;
-            }
-            tsdf_e = mc_tsdf<M>(nbrow, pool, x + (axis == 0), y + (axis == 1), z + (axis == 2));
-        }
-        const float ratio = (0 - tsdf_o) / (tsdf_e - tsdf_o);
-        const float rx = ratio * (int)(axis == 0), ry = ratio * (int)(axis == 1), rz = ratio * (int)(axis == 2);
-        const int gx = xb * R + x, gy = yb * R + y, gz = zb * R + z;
-        const int64_t id = (int64_t)vb0 + i;
-        pos[3 * id + 0] = voxel_size * (gx + rx);
-        pos[3 * id + 1] = voxel_size * (gy + ry);
-        pos[3 * id + 2] = voxel_size * (gz + rz);
-        const float nx = (1 - ratio) * no[0] + ratio * ne[0];
-        const float ny = (1 - ratio) * no[1] + ratio * ne[1];
-        const float nz = (1 - ratio) * no[2] + ratio * ne[2];
-        write_normal(nx, ny, nz, nrm + 3 * id);
+        return;
     }
-    for (int i = tid; i < ntb; i += blockDim.x) {
-        int lo = 0, hi = M::R2 - 1;
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if ((int)rows[mid].y <= i) lo = mid; else hi = mid - 1;
-        }
-        const uint4 rw = rows[lo];
-        const int y = lo % R, z = lo / R;
-        const uint32_t a = rowN[M::q(y, z)], bb = rowN[M::q(y + 1, z)], c = rowN[M::q(y, z + 1)];
-        const uint32_t d = rowN[M::q(y + 1, z + 1)];
-        uint32_t oc = rw.w >> 16;
-        int k = i - (int)rw.y, x = 0, ci = 0;
-        while (oc) {
-            x = __builtin_ctz(oc);
-            ci = mc_index(a >> (x + 1), bb >> (x + 1), c >> (x + 1), d >> (x + 1));
-            const int n = (int)((triC[ci >> 3] >> ((ci & 7) * 4)) & 0xFu);
-            if (k < n) break;
-            k -= n;
-            oc &= oc - 1;
-        }
-        const uint64_t te = triP[ci] >> (12 * k);
-        const int64_t t = (int64_t)tb0 + i;
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-            const int edge = (int)((te >> (4 * j)) & 0xFu);
-            const uint32_t es = (uint32_t)(kEdgeShifts >> (5 * edge));
-            const int ox = x + (int)(es & 1u), oy = y + (int)((es >> 1) & 1u), oz = z + (int)((es >> 2) & 1u);
-            const int axis = (int)((es >> 3) & 3u);
-            int32_t vid;
-            if (ox < R && oy < R && oz < R) {
-                const uint4 ow = rows[oz * R + oy];
-                vid = vb0 + mc_vid(ow.x, ow.z & 0xffffu, ow.z >> 16, ow.w & 0xffffu, ox, axis);
-            } else {
-                const int dx = ox >= R, dy = oy >= R, dz = oz >= R;
-                const int k27 = (dx + 1) + 3 * (dy + 1) + 9 * (dz + 1);
-                const int32_t nbuf = nbrow[k27];
-                if (nbuf < 0) {
-                    vid = -1;  // cannot happen for a valid cube (all corners exist); stay in bounds
-                } else {
-                    const int lx = ox - dx * R, ly = oy - dy * R, lz = oz - dz * R;
-                    const uint4 ow = rows4[(int64_t)nbuf * M::R2 + lz * R + ly];
-                    vid = nbvoff[k27] + mc_vid(ow.x, ow.z & 0xffffu, ow.z >> 16, ow.w & 0xffffu, lx, axis);
-                }
-            }
-            tri[3 * t + (2 - j)] = vid;
-        }
-    }
+    for (int i = tid; i < nvb; i += NT) mc_emit_vertex<M>(i, rows, nbrow, pool, pres, xb, yb, zb, voxel_size, vb0, pos, nrm);
+    for (int i = tid; i < ntb; i += NT) mc_emit_tri<M>(i, rows, rowN, triC, triP, nbrow, nbvoff, rows4, vb0, tb0, tri);
 }
 
 // ---------------------------------------------------------------- point cloud (R = 8 / 16)
@@ -1264,6 +1293,17 @@ static int build_nb(mqr_vbg* v, int32_t* nb) {
 // volume that is still being integrated.
 static int64_t spec_cap(int64_t hint) { return hint > 0 ? hint + hint / 4 + 4096 : 0; }
 
+// k_mc_emit in the configuration v->emit_mode selects (bit 0: merged item loop, bit 1: 512 threads).
+template <int RT, class... A>
+static void launch_mc_emit(const mqr_vbg* v, int64_t n, A... args) {
+    switch (v->emit_mode & 3) {
+        case 1: hipLaunchKernelGGL((k_mc_emit<RT, 256, true>), dim3((unsigned)n), dim3(256), 0, v->stream, args...); break;
+        case 2: hipLaunchKernelGGL((k_mc_emit<RT, 512, false>), dim3((unsigned)n), dim3(512), 0, v->stream, args...); break;
+        case 3: hipLaunchKernelGGL((k_mc_emit<RT, 512, true>), dim3((unsigned)n), dim3(512), 0, v->stream, args...); break;
+        default: hipLaunchKernelGGL((k_mc_emit<RT, 256, false>), dim3((unsigned)n), dim3(256), 0, v->stream, args...);
+    }
+}
+
 template <int RT>
 static int mesh_passes(mqr_vbg* v, float thr, const ExScratch& e, mqr_geom* g, int64_t tri_blocks) {
     const int64_t n = v->pool_count;
@@ -1287,9 +1327,10 @@ static int mesh_passes(mqr_vbg* v, float thr, const ExScratch& e, mqr_geom* g, i
         bool emitted = false;
         if (cv > 0 && ct > 0) {
             if (alloc_geom(g, cv, ct)) return 1;
-            hipLaunchKernelGGL(k_mc_emit<RT>, dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, e.nb, v->bkeys,
-                               v->pool, v->voxel_size, e.c0, e.c1, e.o0, e.o1, rows4, rowNt, g->pos, g->nrm, g->tri, cv,
-                               ct);
+            launch_mc_emit<RT>(v, n, (const int32_t*)e.nb, (const uint64_t*)v->bkeys, (const float2*)v->pool,
+                               v->voxel_size, (const int32_t*)e.c0, (const int32_t*)e.c1, (const int32_t*)e.o0,
+                               (const int32_t*)e.o1, (const uint4*)rows4, (const uint32_t*)rowNt, g->pos, g->nrm,
+                               g->tri, cv, ct);
             MQR_CHECK_HIP(hipGetLastError());
             emitted = true;
         }
@@ -1307,8 +1348,9 @@ static int mesh_passes(mqr_vbg* v, float thr, const ExScratch& e, mqr_geom* g, i
             g->blk = nullptr;
         }
         if (alloc_geom(g, nv, nt)) return 1;
-        hipLaunchKernelGGL(k_mc_emit<RT>, dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, e.nb, v->bkeys, v->pool,
-                           v->voxel_size, e.c0, e.c1, e.o0, e.o1, rows4, rowNt, g->pos, g->nrm, g->tri, nv, nt);
+        launch_mc_emit<RT>(v, n, (const int32_t*)e.nb, (const uint64_t*)v->bkeys, (const float2*)v->pool, v->voxel_size,
+                           (const int32_t*)e.c0, (const int32_t*)e.c1, (const int32_t*)e.o0, (const int32_t*)e.o1,
+                           (const uint4*)rows4, (const uint32_t*)rowNt, g->pos, g->nrm, g->tri, nv, nt);
     } else {
         if (build_nb(v, e.nb)) return 1;
         hipLaunchKernelGGL(k_mesh_count<RT>, dim3((unsigned)n), dim3(kThreads), 0, v->stream, e.nb, n, v->pool, v->R,
