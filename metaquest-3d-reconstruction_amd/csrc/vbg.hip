@@ -366,12 +366,12 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
     //     exist only in the A/B library (MQR_AB, vbg_ab.hpp).
     //     DESIGN.md §4 has the measurements behind the choice.
     int var = v->kernel_variant;
-    if (var != 1 && var != 2 && var != 3 && var != 5 && var != 6 && var != 7 && var != 8 && var != 9 && var != 10 && (var < 11 || var > 14)) var = 0;
+    if (var != 1 && var != 2 && var != 3 && var != 5 && var != 6 && var != 7 && var != 8 && var != 9 && var != 10 && (var < 11 || var > 18)) var = 0;
     if (var != 1 && var != 2 && !lean_ok) var = 2;
     if (var == 5 && (v->R != 16 || W % 4 != 0 || W < 4 || (reinterpret_cast<uintptr_t>(depths) & 15))) var = 0;
     if (var >= 6 && v->R != 16) var = 0;
     // window gathers: 16-byte aligned frame bases and 4HW a multiple of 16 (lean_gather_w)
-    if (var >= 11 && var <= 14 && ((HW % 4) != 0 || (reinterpret_cast<uintptr_t>(depths) & 15))) var = 0;
+    if (var >= 11 && var <= 18 && ((HW % 4) != 0 || (reinterpret_cast<uintptr_t>(depths) & 15))) var = 0;
     if (v->R != 16 && v->R != 8) var = 1;
     const int32_t* bad_list = v->bad[p];
     const bmask_t* bad_mask = reinterpret_cast<const bmask_t*>(v->bad[p] + v->list_cap);
@@ -409,6 +409,23 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
                                    W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
             else if (var == 14)  // 16-byte window gathers, ILP 1, >= 5 waves / SIMD
                 hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 5, 1, 4>), dim3(lean_grid), dim3(512), 0, s, list,
+                                   lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H,
+                                   W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
+            else if (var == 15)  // 8-byte window gathers, >= 7 waves / SIMD
+                hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 7, 2, 5>), dim3(lean_grid), dim3(512), 0, s, list,
+                                   lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H,
+                                   W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
+            else if (var == 16 || (var == 17 && !strunc_one_correction_ok(sdf_trunc)))
+                // 8-byte windows, zc checked per block
+                hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 6, 2, 5, 0, true>), dim3(lean_grid), dim3(512), 0, s,
+                                   list, lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW,
+                                   H, W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
+            else if (var == 17)  // 16 + one-correction s / sdf_trunc
+                hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 6, 2, 5, 1, true>), dim3(lean_grid), dim3(512), 0, s,
+                                   list, lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW,
+                                   H, W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
+            else if (var == 18)  // 8-byte windows, 4 interleaved voxel chains
+                hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 6, 4, 5>), dim3(lean_grid), dim3(512), 0, s, list,
                                    lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H,
                                    W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
             else if (var == 10)  // variant 9 with s / sdf_trunc in one correction (verified for this sdf_trunc)
@@ -1026,7 +1043,7 @@ int mqr_vbg_unpack_weighted(mqr_vbg* v, const int32_t* union_keys, int64_t U, co
 int mqr_vbg_set_variant(mqr_vbg* v, int variant) {
     MQR_REQUIRE(v, "null volume");
     if (sync_all(v)) return 1;
-    if (!MQR_AB && ((variant & 0xff) == 3 || (variant & 0xff) == 5 || (variant & 0xff) == 6 || (variant & 0xff) == 7 || (variant & 0xff) == 8 || (variant & 0xff) == 9 || (variant & 0xff) == 10 || ((variant & 0xff) >= 11 && (variant & 0xff) <= 14) || (variant & 0x8000))) {
+    if (!MQR_AB && ((variant & 0xff) == 3 || (variant & 0xff) == 5 || (variant & 0xff) == 6 || (variant & 0xff) == 7 || (variant & 0xff) == 8 || (variant & 0xff) == 9 || (variant & 0xff) == 10 || ((variant & 0xff) >= 11 && (variant & 0xff) <= 18) || (variant & 0x8000))) {
         set_error("integrate variant " + std::to_string(variant) + " is an A/B kernel: only in tools/_ab/libmqr_ab.so (make ab)");
         return 1;
     }

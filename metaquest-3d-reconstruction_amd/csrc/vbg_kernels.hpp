@@ -699,7 +699,7 @@ __device__ __forceinline__ void lean_gather_v(float (&dv)[ZPER], bool& bad, cons
 // multiple of the window (host): then an in-image window never crosses the end of the frame, and an
 // out-of-image lane's window at 4HW is wholly past the end (reads 0).
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-template <int ZPER, int ILP = 1, int WIN = 16>
+template <int ZPER, int ILP = 1, int WIN = 16, bool ZCHK = true>
 __device__ __forceinline__ void lean_gather_w(float (&dv)[ZPER], bool& bad, const FrameParams& fp,
                                               __amdgpu_buffer_rsrc_t rs, const float (&xs)[ZPER],
                                               const float (&ys)[ZPER], const float (&zs)[ZPER], uint32_t W4,
@@ -716,7 +716,7 @@ __device__ __forceinline__ void lean_gather_w(float (&dv)[ZPER], bool& bad, cons
         const float xc = (ax + zs[k] * e[2]) + e[3];
         const float yc = (ay + zs[k] * e[6]) + e[7];
         const float zc = (az + zs[k] * e[10]) + e[11];
-        bad |= (__float_as_uint(zc) - 0x2D800000u) > 0x30000000u;  // not 2^-36 <= zc <= 2^60
+        if (ZCHK) bad |= (__float_as_uint(zc) - 0x2D800000u) > 0x30000000u;  // not 2^-36 <= zc <= 2^60
         const float inv_z = rcp_m(zc);
         const float u = fx * xc * inv_z + cx;
         const float v = fy * yc * inv_z + cy;
@@ -836,7 +836,7 @@ __device__ void lean_gather_pair(float (&dv)[ZPER], bool& bad, const FrameParams
 #endif
 
 // PAIR (A/B library only, variant 6): the paired-lane gather of vbg_ab.hpp.
-template <int R, int NT, int MAP = 0, int WPE = 1, int ILP = 1, int PAIR = 0, int DIV1 = 0>
+template <int R, int NT, int MAP = 0, int WPE = 1, int ILP = 1, int PAIR = 0, int DIV1 = 0, bool ZBLK = false>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void k_integrate_lean(
     const int32_t* __restrict__ list, const bmask_t* __restrict__ lmask, int32_t* __restrict__ bad_out,
     int* __restrict__ counters, int64_t list_cap, Table t, float2* __restrict__ pool, float voxel_size,
@@ -891,7 +891,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
                 bad |= !(w >= 0.0f && w <= 0x1p23f && w == __builtin_truncf(w));
             }
             bmask_t m = mask;
-            if constexpr (PAIR == 3) {  // block-level zc range check (block_zc_unsafe): skip the frame loop
+            if constexpr (PAIR == 3 || ZBLK) {  // block-level zc range check (block_zc_unsafe): skip the frame loop
                 static_assert(NT == 512, "one (frame, corner) per thread");
                 if (__syncthreads_or(block_zc_unsafe<R>(tid, mask, fps, xb, yb, zb, voxel_size))) bad = true, m = 0;
             }
@@ -900,7 +900,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
                 m &= m - 1;
                 float dv[ZPER];
                 if constexpr (PAIR == 4 || PAIR == 5) {
-                    lean_gather_w<ZPER, ILP, PAIR == 4 ? 16 : 8>(dv, bad, fps[f], frame_rsrc(depths + depth_frame[f] * HW, bytes),
+                    lean_gather_w<ZPER, ILP, PAIR == 4 ? 16 : 8, !ZBLK>(dv, bad, fps[f], frame_rsrc(depths + depth_frame[f] * HW, bytes),
                                                                   xs, ys, zs, W4, bytes, __float_as_uint(hm1),
                                                                   __float_as_uint(wm1));
                     lean_update_v<ZPER, ILP, DIV1>(tw, dv, fps[f], xs, ys, zs, depth_max, sdf_trunc, y1t);

@@ -50,7 +50,7 @@ def test_shortened_reciprocals_exact(which, lo, hi):
 AB = os.environ.get("MQR_AB_TEST") == "1"
 INTEGRATE_VARIANTS = {16: (0, 2, 0x100, 0x200, 0x400, 0x800), 8: (0, 2, 0x100)}
 if AB:
-    INTEGRATE_VARIANTS = {16: (0, 3, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 0x105, 0x605, 0x106, 0x108, 0x10b, 0x10d, 0x8000, 0x8003, 0x8008, 0x800a, 0x800b, 0x800d), 8: (0, 0x8000)}
+    INTEGRATE_VARIANTS = {16: (0, 3, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 0x105, 0x605, 0x106, 0x108, 0x10b, 0x10d, 0x111, 0x8000, 0x8003, 0x8008, 0x800a, 0x800b, 0x800d, 0x8011), 8: (0, 0x8000)}
 
 
 def test_specialised_integrate_equals_generic():
@@ -205,7 +205,7 @@ def test_lean_integrate_exact_fallback():
     Ks = np.concatenate([seq["K"][:1], seq["K"]])
     Ts = np.concatenate([np.eye(4)[None], seq["T_wc"]])
     cases = ((16, 1), (16, 0), (16, 5 if AB else 0x200), (16, 2), (16, 0x100), (16, 9 if AB else 0x400),
-             (16, 8 if AB else 0x800), (8, 1), (8, 0), (8, 2))
+             (16, 8 if AB else 0x800), (16, 13 if AB else 0x100), (16, 17 if AB else 0x200), (8, 1), (8, 0), (8, 2))
     out = []
     for R, variant in cases:
         v = VoxelBlockGrid(voxel_size=0.005, block_resolution=R, block_count=64)
@@ -221,10 +221,10 @@ def test_lean_integrate_exact_fallback():
         v.import_blocks(keys, tsdf, wgt)
         v.integrate_frames(depths[3:], Ks[3:], Ts[3:], depth_scale=1.0, depth_max=4.0, trunc_voxel_multiplier=10.0)
         out.append(v.export())
-    for i in range(1, 7):
+    for i in range(1, 9):
         assert compare_volumes(out[0], out[i], 0.0) == 0.0, cases[i]
-    for i in (8, 9):
-        assert compare_volumes(out[7], out[i], 0.0) == 0.0, cases[i]
+    for i in (10, 11):
+        assert compare_volumes(out[9], out[i], 0.0) == 0.0, cases[i]
 
 
 @pytest.mark.parametrize("mode,a_max,b_lo,b_hi", [
