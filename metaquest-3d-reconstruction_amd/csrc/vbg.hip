@@ -359,19 +359,29 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
     // must stay past 4HW for out-of-image voxels.  Otherwise the exact k_integrate_t runs alone.
     const bool lean_ok = !div_unsafe_host(sdf_trunc) && depth_scale == 1.0f && 4 * (HW + W) <= (int64_t{1} << 31);
     // Variants (mqr_vbg_set_variant, low byte; all bit-identical, tests/test_gpu_numerics.py):
-    //   0 default: k_integrate_lean -- R = 16: brick map, >= 8 waves per SIMD, 2 interleaved voxel
-    //     chains; R = 8: plate map;  1 generic k_integrate (runtime R);  2 exact k_integrate_t;
-    //   3 k_integrate_lean with the plate map (round-1 default, A/B);  5 k_integrate_lt (R = 16: depth
-    //     from packed LDS tiles, A/B);  6 / 7 the lean kernel with the paired-lane gather (A/B);  8 VALU-lean projection / update, 9 the same with the zc check per block, 10 9 with one division correction (A/B).  3, 5-10
-    //     exist only in the A/B library (MQR_AB, vbg_ab.hpp).
-    //     DESIGN.md §4 has the measurements behind the choice.
+    //   0 default: k_integrate_lean -- R = 16: brick map, 8-byte window depth reads (lean_gather_w,
+    //     >= 6 waves per SIMD, 2 interleaved voxel chains) when the frames allow them (even H W,
+    //     8-byte aligned stack), else variant 4;  R = 8: plate map, dword gathers;
+    //   1 generic k_integrate (runtime R);  2 exact k_integrate_t;  4 k_integrate_lean with dword
+    //     gathers at >= 8 waves per SIMD (the round-2 default);
+    //   A/B library only (MQR_AB, vbg_ab.hpp): 3 plate map;  5 packed LDS tiles (k_integrate_lt);
+    //     6 / 7 paired-lane gathers;  8 VALU-lean projection / update, 9 + zc checked per block, 10 +
+    //     one-correction s / trunc;  11 / 12 / 14 16-byte windows;  13 / 15 / 16 / 17 / 18 8-byte
+    //     windows at other occupancies, with the block zc check, one-correction division, ILP 4.
+    //     DESIGN.md §4.1 has the measurements behind the choice.
     int var = v->kernel_variant;
-    if (var != 1 && var != 2 && var != 3 && var != 5 && var != 6 && var != 7 && var != 8 && var != 9 && var != 10 && (var < 11 || var > 18)) var = 0;
+    if (var < 0 || var > 18) var = 0;
+    if (!MQR_AB && var != 1 && var != 2 && var != 4) var = 0;
     if (var != 1 && var != 2 && !lean_ok) var = 2;
     if (var == 5 && (v->R != 16 || W % 4 != 0 || W < 4 || (reinterpret_cast<uintptr_t>(depths) & 15))) var = 0;
-    if (var >= 6 && v->R != 16) var = 0;
-    // window gathers: 16-byte aligned frame bases and 4HW a multiple of 16 (lean_gather_w)
-    if (var >= 11 && var <= 18 && ((HW % 4) != 0 || (reinterpret_cast<uintptr_t>(depths) & 15))) var = 0;
+    if (var >= 5 && v->R != 16) var = 0;
+    // window reads: 4HW a multiple of the window and a frame base aligned to it, so an in-image
+    // window never crosses the end of a frame and an out-of-image one (at 4HW) lies wholly past it
+    const bool win8_ok = (HW % 2) == 0 && (reinterpret_cast<uintptr_t>(depths) & 7) == 0;
+    const bool win16_ok = (HW % 4) == 0 && (reinterpret_cast<uintptr_t>(depths) & 15) == 0;
+    if ((var == 11 || var == 12 || var == 14) && !win16_ok) var = 0;
+    if (var == 0 && !(v->R == 16 && win8_ok)) var = 4;
+    if (var >= 13 && !win8_ok) var = 4;
     if (v->R != 16 && v->R != 8) var = 1;
     const int32_t* bad_list = v->bad[p];
     const bmask_t* bad_mask = reinterpret_cast<const bmask_t*>(v->bad[p] + v->list_cap);
@@ -401,10 +411,6 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
                                    W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
             else if (var == 12)  // 16-byte window gathers, >= 4 waves / SIMD
                 hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 4, 2, 4>), dim3(lean_grid), dim3(512), 0, s, list,
-                                   lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H,
-                                   W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
-            else if (var == 13)  // 8-byte window gathers, >= 6 waves / SIMD
-                hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 6, 2, 5>), dim3(lean_grid), dim3(512), 0, s, list,
                                    lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H,
                                    W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
             else if (var == 14)  // 16-byte window gathers, ILP 1, >= 5 waves / SIMD
@@ -450,7 +456,12 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
                                    depth_frame, depth_max, sdf_trunc, first_new, grouped);
             else
 #endif
+            if (var == 4)  // dword gathers (round-2 default; frames the window reads cannot take)
                 hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 8, 2>), dim3(lean_grid), dim3(512), 0, s, list,
+                                   lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H,
+                                   W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
+            else  // default: 8-byte window reads
+                hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 6, 2, 5>), dim3(lean_grid), dim3(512), 0, s, list,
                                    lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H,
                                    W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
             // exact fix-up of the blocks the fast kernel handed back (usually none: reads a zero count;
@@ -1043,7 +1054,7 @@ int mqr_vbg_unpack_weighted(mqr_vbg* v, const int32_t* union_keys, int64_t U, co
 int mqr_vbg_set_variant(mqr_vbg* v, int variant) {
     MQR_REQUIRE(v, "null volume");
     if (sync_all(v)) return 1;
-    if (!MQR_AB && ((variant & 0xff) == 3 || (variant & 0xff) == 5 || (variant & 0xff) == 6 || (variant & 0xff) == 7 || (variant & 0xff) == 8 || (variant & 0xff) == 9 || (variant & 0xff) == 10 || ((variant & 0xff) >= 11 && (variant & 0xff) <= 18) || (variant & 0x8000))) {
+    if (!MQR_AB && (((variant & 0xff) != 0 && (variant & 0xff) != 1 && (variant & 0xff) != 2 && (variant & 0xff) != 4) || (variant & 0x8000))) {
         set_error("integrate variant " + std::to_string(variant) + " is an A/B kernel: only in tools/_ab/libmqr_ab.so (make ab)");
         return 1;
     }

@@ -48,7 +48,7 @@ def test_shortened_reciprocals_exact(which, lo, hi):
 # MQR_AB_TEST=1 (tests/test_gpu_ab_variants.py, with MQR_HIP_LIB = tools/_ab/libmqr_ab.so): the integrate
 # tests below also cover the A/B kernels the shipped library leaves out (variants 3 and 5, bit 0x8000)
 AB = os.environ.get("MQR_AB_TEST") == "1"
-INTEGRATE_VARIANTS = {16: (0, 2, 0x100, 0x200, 0x400, 0x800), 8: (0, 2, 0x100)}
+INTEGRATE_VARIANTS = {16: (0, 2, 4, 0x100, 0x104, 0x200, 0x400, 0x800), 8: (0, 2, 0x100)}
 if AB:
     INTEGRATE_VARIANTS = {16: (0, 3, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 0x105, 0x605, 0x106, 0x108, 0x10b, 0x10d, 0x111, 0x8000, 0x8003, 0x8008, 0x800a, 0x800b, 0x800d, 0x8011), 8: (0, 0x8000)}
 
@@ -123,6 +123,44 @@ def test_special_depth_values_equal_generic():
             except AssertionError as e:
                 bad.append((R, hex(variant), str(e)[:120]))
         assert not bad, bad
+
+
+def test_window_reads_fallback_frames():
+    """The default kernel reads 8-byte depth windows only from frame stacks with an even pixel count
+    and an 8-byte aligned base; odd-sized frames and a device stack starting 4 bytes into its
+    allocation take the dword-gather kernel (variant 4).  Every case equals the generic kernel."""
+    import ctypes
+    import torch
+    from gpu_helpers import compare_volumes
+    from mqr import synthetic
+    from mqr import _lib
+    from mqr.vbg import VoxelBlockGrid
+    args = dict(depth_scale=1.0, depth_max=4.0, trunc_voxel_multiplier=10.0)
+
+    def run(variant, depths, K, T):
+        v = VoxelBlockGrid(voxel_size=0.01, block_resolution=16, block_count=64)
+        _lib.call("mqr_vbg_set_variant", v.handle, variant)
+        v.integrate_frames(depths, K, T, **args)
+        return v.export()
+
+    odd = synthetic.make_sequence("room", n=10, height=241, width=321, f=262.5, noise=True, seed=44)
+    ref = run(1, odd["depth"], odd["K"], odd["T_wc"])
+    for variant in (0, 4):
+        compare_volumes(ref, run(variant, odd["depth"], odd["K"], odd["T_wc"]), 0.0)
+    even = synthetic.make_sequence("room", n=10, height=240, width=320, f=262.5, noise=True, seed=45)
+    d = np.ascontiguousarray(np.stack(even["depth"]), np.float32)
+    B, H, W = d.shape
+    flat = torch.zeros(B * H * W + 1, dtype=torch.float32, device="cuda:0")
+    flat[1:] = torch.from_numpy(d.reshape(-1)).to("cuda:0")
+    torch.cuda.synchronize()
+
+    class Shifted:  # the stack 4 bytes into the allocation
+        ptr = ctypes.c_void_p(flat.data_ptr() + 4)
+
+    ref = run(1, even["depth"], even["K"], even["T_wc"])
+    for variant in (0, 4):
+        compare_volumes(ref, run(variant, (Shifted, B, H, W), even["K"], even["T_wc"]), 0.0)
+        compare_volumes(ref, run(variant, even["depth"], even["K"], even["T_wc"]), 0.0)
 
 
 def test_table_full_retry_equals_default():
