@@ -824,10 +824,8 @@ __device__ __forceinline__ void mc_emit_tri(int i, const uint4* rows, const uint
 // Emission of a block with vertices or triangles, from the count pass's row records: vertices
 // (positions and normals from tsdf values gathered from the pool) and triangles at the offsets of
 // the scan, in (block, voxel, edge) / (block, cube, triangle) order.
-// NT threads per block; MERGED: vertices and triangles as one strided item loop (items [0, nv) are
-// vertices, [nv, nv + nt) triangles), so a block's dependent load rounds are ceil((nv + nt) / NT)
-// instead of ceil(nv / NT) + ceil(nt / NT).
-template <int R, int NT = kMcThreads, bool MERGED = false>
+// (A merged vertex / triangle item loop and 512-thread blocks were measured: no change)
+template <int R, int NT = kMcThreads>
 __global__ __launch_bounds__(NT) void k_mc_emit(const int32_t* __restrict__ nb, const uint64_t* __restrict__ bkeys,
                                                         const float2* __restrict__ pool, float voxel_size,
                                                         const int32_t* __restrict__ vcount,
@@ -867,15 +865,6 @@ __global__ __launch_bounds__(NT) void k_mc_emit(const int32_t* __restrict__ nb, 
 
     int xb, yb, zb;
     unpack_key(bkeys[b], xb, yb, zb);
-    if (MERGED) {
-        for (int i = tid; i < nvb + ntb; i += NT) {
-            if (i < nvb)
-                mc_emit_vertex<M>(i, rows, nbrow, pool, pres, xb, yb, zb, voxel_size, vb0, pos, nrm);
-            else
-                mc_emit_tri<M>(i - nvb, rows, rowN, triC, triP, nbrow, nbvoff, rows4, vb0, tb0, tri);
-        }
-        return;
-    }
     for (int i = tid; i < nvb; i += NT) mc_emit_vertex<M>(i, rows, nbrow, pool, pres, xb, yb, zb, voxel_size, vb0, pos, nrm);
     for (int i = tid; i < ntb; i += NT) mc_emit_tri<M>(i, rows, rowN, triC, triP, nbrow, nbvoff, rows4, vb0, tb0, tri);
 }
@@ -1293,15 +1282,9 @@ static int build_nb(mqr_vbg* v, int32_t* nb) {
 // volume that is still being integrated.
 static int64_t spec_cap(int64_t hint) { return hint > 0 ? hint + hint / 4 + 4096 : 0; }
 
-// k_mc_emit in the configuration v->emit_mode selects (bit 0: merged item loop, bit 1: 512 threads).
 template <int RT, class... A>
 static void launch_mc_emit(const mqr_vbg* v, int64_t n, A... args) {
-    switch (v->emit_mode & 3) {
-        case 1: hipLaunchKernelGGL((k_mc_emit<RT, 256, true>), dim3((unsigned)n), dim3(256), 0, v->stream, args...); break;
-        case 2: hipLaunchKernelGGL((k_mc_emit<RT, 512, false>), dim3((unsigned)n), dim3(512), 0, v->stream, args...); break;
-        case 3: hipLaunchKernelGGL((k_mc_emit<RT, 512, true>), dim3((unsigned)n), dim3(512), 0, v->stream, args...); break;
-        default: hipLaunchKernelGGL((k_mc_emit<RT, 256, false>), dim3((unsigned)n), dim3(256), 0, v->stream, args...);
-    }
+    hipLaunchKernelGGL((k_mc_emit<RT>), dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, args...);
 }
 
 template <int RT>

@@ -1068,7 +1068,6 @@ int mqr_vbg_set_variant(mqr_vbg* v, int variant) {
     v->touch_wait = (variant & 0x4000) != 0;  // bit 14: integrate always waits on a touch-stream event (A/B)
     v->xcd_order = (variant & 0x8000) != 0;   // bit 15: spatial per-XCD groups (k_xcd_order, A/B)
     v->touch_ppt = (variant & 0x10000) ? 1 : 2;  // bit 16: one stride-4 pixel per touch thread (A/B)
-    v->emit_mode = (variant >> 17) & 3;       // bits 17-18: k_mc_emit item loop / width (A/B)
     return 0;
 }
 

@@ -1,10 +1,12 @@
 #!/usr/bin/env python3
 """Interleaved A/B of extract_triangle_mesh configurations on the bench volume (C2, one process).
 
-python tools/ab_extract.py --modes 0,1,2,3 --reps 15
-mode = k_mc_emit configuration (mqr_vbg_set_variant bits 17-18: bit 0 merged vertex / triangle item
-loop, bit 1 512 threads).  Prints per-mode median wall ms of mqr_extract_mesh (device-resident,
-the bench's extract_ms) and whether positions / normals / triangles equal mode 0's bit for bit.
+python tools/ab_extract.py --modes 0 --reps 15
+mode = value of mqr_vbg_set_variant bits 17+ for an extraction configuration under test (round 3
+measured a merged vertex / triangle item loop and 512-thread emission blocks this way: no change,
+profiles/r03_ab_integrate_windows.json; neither is in the library now, so mode 0 is the library).
+Prints per-mode median wall ms of mqr_extract_mesh (device-resident, the bench's extract_ms) and
+whether positions / normals / triangles equal the first mode's bit for bit.
 """
 import argparse
 import ctypes
@@ -20,7 +22,7 @@ sys.path.insert(0, ROOT)
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--modes", default="0,1,2,3")
+    ap.add_argument("--modes", default="0")
     ap.add_argument("--reps", type=int, default=15)
     ap.add_argument("--threshold", type=float, default=1.5)
     a = ap.parse_args()
