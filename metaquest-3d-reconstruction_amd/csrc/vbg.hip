@@ -370,7 +370,7 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
     //     windows at other occupancies, with the block zc check, one-correction division, ILP 4.
     //     DESIGN.md §4.1 has the measurements behind the choice.
     int var = v->kernel_variant;
-    if (var < 0 || var > 18) var = 0;
+    if (var < 0 || var > 20) var = 0;
     if (!MQR_AB && var != 1 && var != 2 && var != 4) var = 0;
     if (var != 1 && var != 2 && !lean_ok) var = 2;
     if (var == 5 && (v->R != 16 || W % 4 != 0 || W < 4 || (reinterpret_cast<uintptr_t>(depths) & 15))) var = 0;
@@ -379,7 +379,7 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
     // window never crosses the end of a frame and an out-of-image one (at 4HW) lies wholly past it
     const bool win8_ok = (HW % 2) == 0 && (reinterpret_cast<uintptr_t>(depths) & 7) == 0;
     const bool win16_ok = (HW % 4) == 0 && (reinterpret_cast<uintptr_t>(depths) & 15) == 0;
-    if ((var == 11 || var == 12 || var == 14) && !win16_ok) var = 0;
+    if ((var == 11 || var == 12 || var == 14 || var == 19) && !win16_ok) var = 0;
     if (var == 0 && !(v->R == 16 && win8_ok)) var = 4;
     if (var >= 13 && !win8_ok) var = 4;
     if (v->R != 16 && v->R != 8) var = 1;
@@ -432,6 +432,14 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
                                    H, W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
             else if (var == 18)  // 8-byte windows, 4 interleaved voxel chains
                 hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 6, 4, 5>), dim3(lean_grid), dim3(512), 0, s, list,
+                                   lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H,
+                                   W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
+            else if (var == 19)  // 16-byte windows in two halves (<= 4 window loads in flight), >= 6 waves / SIMD
+                hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 6, 2, 6>), dim3(lean_grid), dim3(512), 0, s, list,
+                                   lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H,
+                                   W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
+            else if (var == 20)  // 8-byte windows in two halves, >= 7 waves / SIMD
+                hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 7, 2, 7>), dim3(lean_grid), dim3(512), 0, s, list,
                                    lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H,
                                    W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
             else if (var == 10)  // variant 9 with s / sdf_trunc in one correction (verified for this sdf_trunc)

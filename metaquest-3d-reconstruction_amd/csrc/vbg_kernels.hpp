@@ -699,7 +699,7 @@ __device__ __forceinline__ void lean_gather_v(float (&dv)[ZPER], bool& bad, cons
 // multiple of the window (host): then an in-image window never crosses the end of the frame, and an
 // out-of-image lane's window at 4HW is wholly past the end (reads 0).
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-template <int ZPER, int ILP = 1, int WIN = 16, bool ZCHK = true>
+template <int ZPER, int ILP = 1, int WIN = 16, bool ZCHK = true, int K0 = 0, int K1 = ZPER>
 __device__ __forceinline__ void lean_gather_w(float (&dv)[ZPER], bool& bad, const FrameParams& fp,
                                               __amdgpu_buffer_rsrc_t rs, const float (&xs)[ZPER],
                                               const float (&ys)[ZPER], const float (&zs)[ZPER], uint32_t W4,
@@ -709,7 +709,7 @@ __device__ __forceinline__ void lean_gather_w(float (&dv)[ZPER], bool& bad, cons
     for (int j = 0; j < 12; ++j) e[j] = fp.ext[j];
     const float fx = fp.fx, fy = fp.fy, cx = fp.cx, cy = fp.cy;
 #pragma unroll
-    for (int k = 0; k < ZPER; ++k) {
+    for (int k = K0; k < K1; ++k) {
         const float ax = xs[k] * e[0] + ys[k] * e[1];
         const float ay = xs[k] * e[4] + ys[k] * e[5];
         const float az = xs[k] * e[8] + ys[k] * e[9];
@@ -737,13 +737,13 @@ __device__ __forceinline__ void lean_gather_w(float (&dv)[ZPER], bool& bad, cons
 // DIV1: s / sdf_trunc with one Markstein correction (the host enables it only for an sdf_trunc whose
 // every s in [0, sdf_trunc] it verified against IEEE division, strunc_one_correction_ok; the
 // sequence is odd in s, so negative s follow).
-template <int ZPER, int ILP = 1, int DIV1 = 0>
+template <int ZPER, int ILP = 1, int DIV1 = 0, int K0 = 0, int K1 = ZPER>
 __device__ __forceinline__ void lean_update_v(float2 (&tw)[ZPER], const float (&dv)[ZPER], const FrameParams& fp,
                                               const float (&xs)[ZPER], const float (&ys)[ZPER],
                                               const float (&zs)[ZPER], float depth_max, float sdf_trunc, float y1t) {
     const float e8 = fp.ext[8], e9 = fp.ext[9], e10 = fp.ext[10], e11 = fp.ext[11];
 #pragma unroll
-    for (int k = 0; k < ZPER; ++k) {
+    for (int k = K0; k < K1; ++k) {
         const float az = xs[k] * e8 + ys[k] * e9;
         const float zc = (az + zs[k] * e10) + e11;
         const float d = dv[k];
@@ -899,7 +899,21 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
                 const int f = __builtin_ctzll(m);
                 m &= m - 1;
                 float dv[ZPER];
-                if constexpr (PAIR == 4 || PAIR == 5) {
+                if constexpr (PAIR == 6 || PAIR == 7) {  // windows in two halves: <= 4 window loads in flight
+                    constexpr int H2 = ZPER / 2;
+                    const __amdgpu_buffer_rsrc_t rsf = frame_rsrc(depths + depth_frame[f] * HW, bytes);
+                    constexpr int WB = PAIR == 6 ? 16 : 8;
+                    lean_gather_w<ZPER, ILP, WB, true, 0, H2>(dv, bad, fps[f], rsf, xs, ys, zs, W4, bytes,
+                                                              __float_as_uint(hm1), __float_as_uint(wm1));
+                    __builtin_amdgcn_sched_barrier(0);
+                    lean_update_v<ZPER, ILP, DIV1, 0, H2>(tw, dv, fps[f], xs, ys, zs, depth_max, sdf_trunc, y1t);
+                    __builtin_amdgcn_sched_barrier(0);
+                    lean_gather_w<ZPER, ILP, WB, true, H2, ZPER>(dv, bad, fps[f], rsf, xs, ys, zs, W4, bytes,
+                                                                 __float_as_uint(hm1), __float_as_uint(wm1));
+                    __builtin_amdgcn_sched_barrier(0);
+                    lean_update_v<ZPER, ILP, DIV1, H2, ZPER>(tw, dv, fps[f], xs, ys, zs, depth_max, sdf_trunc, y1t);
+                    continue;
+                } else if constexpr (PAIR == 4 || PAIR == 5) {
                     lean_gather_w<ZPER, ILP, PAIR == 4 ? 16 : 8, !ZBLK>(dv, bad, fps[f], frame_rsrc(depths + depth_frame[f] * HW, bytes),
                                                                   xs, ys, zs, W4, bytes, __float_as_uint(hm1),
                                                                   __float_as_uint(wm1));
