@@ -169,7 +169,6 @@ struct mqr_vbg {
     int batch_frames = mqr::kMaxBatch;  // frames per device batch (A/B: 32, variant bit 0x400)
     // profiling
     int touch_ppt = 2;  // stride-4 pixels per k_touch thread
-    int first_batch = 0;  // frames in a call's first batch (0: batch_frames)
     bool profile = false;
     bool profile_touch = false;  // mqr_vbg_profile level 2: also time the touch launches
     std::vector<std::pair<hipEvent_t, hipEvent_t>> int_events, touch_events;

@@ -825,12 +825,9 @@ int mqr_integrate_frames(mqr_vbg* v, const float* depths, int depth_loc, int B, 
     int rc = 0;
     int batch = 0;
     const size_t nb = (size_t)std::max(1, std::min(v->batch_frames, kMaxBatch));
-    int b = 0;
-    for (size_t s = 0; s < valid.size(); s += (size_t)b, ++batch) {
+    for (size_t s = 0; s < valid.size(); s += nb, ++batch) {
         const int p = v->pipelined ? (batch & 1) : 0;
-        // a shorter first batch starts the first integrate launch sooner (its touch runs alone)
-        const size_t first = v->first_batch > 0 ? std::min<size_t>(nb, (size_t)v->first_batch) : nb;
-        b = (int)std::min<size_t>(batch == 0 ? first : nb, valid.size() - s);
+        const int b = (int)std::min<size_t>(nb, valid.size() - s);
         const int* idx = valid.data() + s;
         if (ensure_fp(v, b)) return 1;
         if (depth_loc != MQR_DEVICE && ensure_depth(v, b * HW)) return 1;
@@ -1073,7 +1070,6 @@ int mqr_vbg_set_variant(mqr_vbg* v, int variant) {
     v->pipelined = (variant & 0x100) == 0;  // bit 8: serialise touch and integrate (A/B of the overlap)
     v->lpt_order = (variant & 0x200) == 0;  // bit 9: integrate in touch order instead of longest-first
     v->batch_frames = (variant & 0x400) ? 32 : kMaxBatch;  // bit 10: 32-frame batches (A/B)
-    v->first_batch = (variant & 0x20000) ? 16 : (variant & 0x40000) ? 32 : 0;  // bits 17 / 18: first batch 16 / 32 frames (A/B)
     v->sys_fence = (variant & 0x800) != 0;  // bit 11: system-scope ordering / timing events (A/B)
     v->probe_one = (variant & 0x1000) != 0; // bit 12: force the full-table retry path (test hook)
     v->table_worst = (variant & 0x2000) != 0; // bit 13: size the table for the worst case (round-2 A/B)
