@@ -26,12 +26,23 @@ def main():
     K32 = np.ascontiguousarray(seq["K"], dtype=np.float32).reshape(B, 9)
     conf = torch.empty((B, H, W), dtype=torch.float64, device="cuda:0")
     valid = torch.empty((B, H, W), dtype=torch.int32, device="cuda:0")
-    for _ in range(a.reps + 1):
+    import hashlib
+    import json
+    import time
+    times = []
+    for i in range(a.reps + 1):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
         _lib.call("mqr_confidence", 0, ctypes.c_void_p(d.data_ptr()), 1, B, H, W, _lib.ptr(K32, _lib._f32p),
                   _lib.ptr(T_cw, _lib._f32p), _lib.ptr(T_ci, _lib._f32p), None, 0, B, 10, 4.0, 0.08,
                   ctypes.c_void_p(conf.data_ptr()), ctypes.c_void_p(valid.data_ptr()), 1)
-    torch.cuda.synchronize()
-    print("valid mean", float(valid.float().mean()), "conf mean", float(conf.mean()))
+        torch.cuda.synchronize()
+        if i:
+            times.append((time.perf_counter() - t0) * 1e3)
+    digest = hashlib.sha256(conf.cpu().numpy().tobytes() + valid.cpu().numpy().tobytes()).hexdigest()[:16]
+    print(json.dumps({"ms_median": sorted(times)[len(times) // 2], "reps": a.reps, "valid_mean": float(valid.float().mean()),
+                      "conf_mean": float(conf.mean()), "digest": digest,
+                      "single": os.environ.get("MQR_CONF_SINGLE") is not None}))
 
 
 if __name__ == "__main__":
