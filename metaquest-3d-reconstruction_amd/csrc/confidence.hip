@@ -14,7 +14,6 @@
 // (mqr_check_div64, tests/test_gpu_numerics.py).
 #include <algorithm>
 #include <cmath>
-#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -117,74 +116,6 @@ __device__ inline int pixel_error_d2(const float* __restrict__ tgt, int H, int W
     return 1;
 }
 
-// pixel_error_d2 in two stages, so that a thread can have two neighbours' depth reads in flight:
-// stage 1 projects the world point into the target frame and yields the two row addresses of its
-// bilinear taps (or ok = 0 for every early return of pixel_error_d2 before the reads), stage 2
-// finishes from the four taps.  Same operations in the same order as pixel_error_d2.
-struct ErrStage {
-    double uu, vv;
-    int64_t row0;  // element offset of tap (u0, v0) in the frame
-    int u0, v0;
-    int ok;
-};
-__device__ inline ErrStage err_stage1(int H, int W, const ConfFrame& ft, const double pw[3], double depth_max) {
-    ErrStage st{0.0, 0.0, 0, 0, 0, 0};
-    double pt[3];
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-        pt[i] = ft.Tinv[i * 4 + 0] * pw[0] + ft.Tinv[i * 4 + 1] * pw[1] + ft.Tinv[i * 4 + 2] * pw[2] + ft.Tinv[i * 4 + 3];
-    const double X = pt[0], Y = pt[1], Z = pt[2];
-    if (!(Z > 0 && isfinite(Z) && Z <= depth_max && isfinite(X) && isfinite(Y))) return st;
-    const double ax = X * ft.fx, ay = Y * ft.fy;
-    double qx, qy;
-    if (div64_safe(Z) && div64_safe(ax) && div64_safe(ay) && fabs(ax) <= 0x1p400 * Z && fabs(ay) <= 0x1p400 * Z) {
-        const Rcp64 rz = rcp64_refine(Z);
-        qx = div64_core(ax, rz);
-        qy = div64_core(ay, rz);
-    } else {
-        qx = ax / Z;
-        qy = ay / Z;
-    }
-    const double uu = qx + ft.cx;
-    const double vv = qy + ft.cy;
-    if (!(isfinite(uu) && isfinite(vv))) return st;
-    const double max_coord = (double)((W > H ? W : H) * 10);
-    if (!(uu >= -max_coord && uu < max_coord && vv >= -max_coord && vv < max_coord)) return st;
-    const int u0 = (int)floor(uu), v0 = (int)floor(vv);
-    if (!(u0 >= 0 && u0 + 1 < W && v0 >= 0 && v0 + 1 < H)) return st;
-    st.uu = uu;
-    st.vv = vv;
-    st.u0 = u0;
-    st.v0 = v0;
-    st.row0 = (int64_t)v0 * W + u0;
-    st.ok = 1;
-    return st;
-}
-__device__ inline int err_stage2(const ErrStage& st, float2 ab, float2 cd, const ConfFrame& ft, const double pw[3],
-                                 double depth_max, double* d2) {
-    const float dmf = (float)depth_max;
-    const float Ia = ab.x, Ib = ab.y, Ic = cd.x, Id = cd.y;
-    if (!(Ib > 0 && Ib <= dmf && Ia > 0 && Ia <= dmf && Ic > 0 && Ic <= dmf && Id > 0 && Id <= dmf)) return 0;
-    const double uu = st.uu, vv = st.vv;
-    const int u1 = st.u0 + 1, v1 = st.v0 + 1;
-    const double wa = ((double)u1 - uu) * ((double)v1 - vv);
-    const double wb = (uu - (double)st.u0) * ((double)v1 - vv);
-    const double wc = ((double)u1 - uu) * (vv - (double)st.v0);
-    const double wd = (uu - (double)st.u0) * (vv - (double)st.v0);
-    const float zt = (float)(wa * Ia + wb * Ib + wc * Ic + wd * Id);
-    if (!(zt > 0 && isfinite(zt))) return 0;
-    const double ztd = (double)zt;
-    const double xt = div64_by_rn_rcp((uu - ft.cx) * ztd, ft.fx, ft.rfx);
-    const double yt = div64_by_rn_rcp((vv - ft.cy) * ztd, ft.fy, ft.rfy);
-    double q[3];
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-        q[i] = ft.Tcw[i * 4 + 0] * xt + ft.Tcw[i * 4 + 1] * yt + ft.Tcw[i * 4 + 2] * ztd + ft.Tcw[i * 4 + 3];
-    const double dx = pw[0] - q[0], dy = pw[1] - q[1], dz = pw[2] - q[2];
-    *d2 = dx * dx + dy * dy + dz * dz;
-    return 1;
-}
-
 // depth_to_pointcloud_numpy for one pixel: returns 0 when the ref pixel is not in (0, depth_max].
 __device__ inline int ref_point(const ConfFrame& fr, int u, int v, float dref, double depth_max, double pw[3]) {
     if (!(dref > 0 && dref <= (float)depth_max)) return 0;
@@ -199,8 +130,6 @@ __device__ inline int ref_point(const ConfFrame& fr, int u, int v, float dref, d
 
 // d2_max: the largest double d2 with (float)sqrt(d2) <= threshold (host, exact); the reference's
 // `err <= threshold` on the float32 error map is d2 <= d2_max (sqrt and both roundings monotone).
-// PAIRS: two neighbours' depth reads in flight per thread (err_stage1 / err_stage2).
-template <bool PAIRS>
 __global__ __launch_bounds__(256) void k_confidence(const float* __restrict__ depths, int N, int H, int W,
                                                     const ConfFrame* __restrict__ fr, const uint8_t* __restrict__ ok,
                                                     int ref_begin, int r, double depth_max, double d2_max,
@@ -214,50 +143,12 @@ __global__ __launch_bounds__(256) void k_confidence(const float* __restrict__ de
     int nv = 0, nc = 0;
     if (ref_point(fr[ref], u, v, depths[(int64_t)ref * HW + p], depth_max, pw)) {
         const int lo = max(0, ref - r), hi = min(N, ref + r + 1);
-        if (PAIRS) {
-            // two neighbours per step, their tap reads issued together (neighbour order is free:
-            // the counts are sums)
-            int t = lo;
-            auto next = [&](int from) {
-                while (from < hi && (from == ref || !ok[from])) ++from;
-                return from;
-            };
-            t = next(t);
-            while (t < hi) {
-                const int t2 = next(t + 1);
-                const bool two = t2 < hi;
-                const ErrStage s1 = err_stage1(H, W, fr[t], pw, depth_max);
-                const ErrStage s2 = two ? err_stage1(H, W, fr[t2], pw, depth_max) : ErrStage{0.0, 0.0, 0, 0, 0, 0};
-                float2 ab1 = make_float2(0.f, 0.f), cd1 = ab1, ab2 = ab1, cd2 = ab1;
-                if (s1.ok) {
-                    const float* f1 = depths + (int64_t)t * HW + s1.row0;
-                    __builtin_memcpy(&ab1, f1, sizeof(float2));
-                    __builtin_memcpy(&cd1, f1 + W, sizeof(float2));
-                }
-                if (s2.ok) {
-                    const float* f2 = depths + (int64_t)t2 * HW + s2.row0;
-                    __builtin_memcpy(&ab2, f2, sizeof(float2));
-                    __builtin_memcpy(&cd2, f2 + W, sizeof(float2));
-                }
-                double d2;
-                if (s1.ok && err_stage2(s1, ab1, cd1, fr[t], pw, depth_max, &d2)) {
-                    ++nv;
-                    if (d2 <= d2_max) ++nc;
-                }
-                if (s2.ok && err_stage2(s2, ab2, cd2, fr[t2], pw, depth_max, &d2)) {
-                    ++nv;
-                    if (d2 <= d2_max) ++nc;
-                }
-                t = two ? next(t2 + 1) : hi;
-            }
-        } else {
-            for (int t = lo; t < hi; ++t) {
-                if (t == ref || !ok[t]) continue;
-                double d2;
-                if (pixel_error_d2(depths + (int64_t)t * HW, H, W, fr[t], pw, depth_max, &d2)) {
-                    ++nv;
-                    if (d2 <= d2_max) ++nc;
-                }
+        for (int t = lo; t < hi; ++t) {
+            if (t == ref || !ok[t]) continue;
+            double d2;
+            if (pixel_error_d2(depths + (int64_t)t * HW, H, W, fr[t], pw, depth_max, &d2)) {
+                ++nv;
+                if (d2 <= d2_max) ++nc;
             }
         }
     }
@@ -384,14 +275,8 @@ int mqr_confidence(int device, const float* depths, int depth_loc, int N, int H,
         MQR_CHECK_HIP(hipMalloc(&dvalid, sizeof(int32_t) * nref * HW));
     }
     // (float) threshold: numpy compares the float32 error map against a weak Python float.
-    static const bool pairs = getenv("MQR_CONF_SINGLE") == nullptr;  // A/B switch: one neighbour at a time
-    const double d2max = d2_threshold((float)error_threshold);
-    if (pairs)
-        hipLaunchKernelGGL(k_confidence<true>, dim3((unsigned)((HW + 255) / 256), nref), dim3(256), 0, s, dsrc, N, H,
-                           W, dfr, dok, ref_begin, frame_range, depth_max, d2max, dconf, dvalid);
-    else
-        hipLaunchKernelGGL(k_confidence<false>, dim3((unsigned)((HW + 255) / 256), nref), dim3(256), 0, s, dsrc, N, H,
-                           W, dfr, dok, ref_begin, frame_range, depth_max, d2max, dconf, dvalid);
+    hipLaunchKernelGGL(k_confidence, dim3((unsigned)((HW + 255) / 256), nref), dim3(256), 0, s, dsrc, N, H, W, dfr,
+                       dok, ref_begin, frame_range, depth_max, d2_threshold((float)error_threshold), dconf, dvalid);
     MQR_CHECK_HIP(hipGetLastError());
     if (out_loc != MQR_DEVICE) {
         MQR_CHECK_HIP(hipMemcpyAsync(conf, dconf, sizeof(double) * nref * HW, hipMemcpyDeviceToHost, s));
