@@ -601,10 +601,11 @@ def pmc_traffic(H, W, frames):
     return None, None
 
 
-def gather_ceiling(avg_launch_ms, gathers_per_launch, cus):
-    """The integrate launch against the measured gather-instruction ceiling (tools/gather_ceiling.hip ->
-    profiles/*_gather_ceiling.jsonl, pattern "brick": the kernel's lane map gathering 4-byte depths
-    from an L2-resident frame with no other work).  One depth gather instruction per 64 voxel-frames."""
+def gather_ceiling(avg_launch_ms, gathers_per_launch, cus, pattern="brick_x2"):
+    """The integrate launch against the measured depth-read ceiling (tools/gather_ceiling.hip ->
+    profiles/*_gather_ceiling.jsonl): `pattern` is the kernel's lane map reading what the default
+    kernel reads ("brick_x2": each lane the aligned 8-byte window of its pixel; "brick": dword
+    gathers) from an L2-resident frame with no other work.  One read instruction per 64 voxel-frames."""
     import glob
     for path in reversed(sorted(glob.glob(os.path.join(ROOT, "profiles", "*_gather_ceiling.jsonl")))):
         try:
@@ -612,12 +613,13 @@ def gather_ceiling(avg_launch_ms, gathers_per_launch, cus):
         except (OSError, ValueError):
             continue
         ceil = {r["pattern"]: r["ns_per_gather_instr_per_cu"] for r in rows}
-        if "brick" not in ceil or not avg_launch_ms or not gathers_per_launch:
+        if pattern not in ceil or not avg_launch_ms or not gathers_per_launch:
             continue
         achieved = avg_launch_ms * 1e6 / (gathers_per_launch / cus)
-        return {"unit": "ns per gather instruction per CU", "achieved": achieved, "ceiling": ceil["brick"],
-                "frac": ceil["brick"] / achieved, "gathers_per_launch": gathers_per_launch,
-                "ceiling_16B_windows": ceil.get("brick_x4"), "source": os.path.relpath(path, ROOT)}
+        return {"unit": "ns per depth-read instruction per CU", "achieved": achieved, "ceiling": ceil[pattern],
+                "frac": ceil[pattern] / achieved, "pattern": pattern, "gathers_per_launch": gathers_per_launch,
+                "ceiling_dword_gathers": ceil.get("brick"), "ceiling_16B_windows": ceil.get("brick_x4"),
+                "source": os.path.relpath(path, ROOT)}
     return None
 
 

@@ -8,6 +8,9 @@
 //                pixel (c + 1.3 x + 0.4 z, r + 1.3 y + 0.3 z) -- ~6 distinct 128-byte lines per load
 //   brick_even   brick, odd lanes masked off (exec): does the cost follow lanes or instructions?
 //   brick_x4     brick lanes, 16-byte loads (each lane reads its pixel's aligned 16-byte window)
+//   brick_x2     brick lanes, 8-byte loads (each lane reads its pixel's aligned 8-byte window)
+//   brick_x4_lds brick lanes, 16-byte windows by LDS-DMA (global_load_lds_dwordx4: lane i's window
+//                lands at the wave's LDS base + 16 i), then each lane reads its dword from LDS
 //   window       random pixels of a 64 x 16 window
 //   frame        random pixels of the whole frame
 // The window origin moves every iteration, so L1 reuse stays what the integrate kernel sees.
@@ -43,6 +46,7 @@ __device__ __forceinline__ uint32_t hash32(uint32_t x) {
 
 template <int P>
 __global__ __launch_bounds__(NT) void k_gather(const float* __restrict__ frame, float* __restrict__ out) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[P == 8 ? NT / 64 * 8 * 256 : 1];  // 8 KB per wave
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(frame), (short)0, W * H * 4, 0x00020000);
     const int l = threadIdx.x & 63;
@@ -54,7 +58,7 @@ __global__ __launch_bounds__(NT) void k_gather(const float* __restrict__ frame, 
         switch (P) {
             case 0: dx[k] = 0; dy[k] = 2 * k; break;
             case 1: dx[k] = l; dy[k] = 2 * k; break;
-            case 2: case 3: case 4:
+            case 2: case 3: case 4: case 7: case 8:
                 dx[k] = (13 * x + 4 * z) / 10 + 3 * (k & 3);
                 dy[k] = (13 * y + 3 * z) / 10 + 11 * (k >> 2);
                 break;
@@ -75,7 +79,7 @@ __global__ __launch_bounds__(NT) void k_gather(const float* __restrict__ frame, 
     if (P == 3 && (l & 1)) return;
     for (int it = 0; it < ITERS; ++it) {
         const uint32_t h = hash32(wave * 131 + it);
-        const int c = P >= 6 ? (int)(h % 80) : (int)(h % (W - 80)), r = P >= 6 ? (int)((h >> 10) % 80) : (int)((h >> 10) % (H - 48));
+        const int c = P == 6 ? (int)(h % 80) : (int)(h % (W - 80)), r = P == 6 ? (int)((h >> 10) % 80) : (int)((h >> 10) % (H - 48));
         float v[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
@@ -83,8 +87,23 @@ __global__ __launch_bounds__(NT) void k_gather(const float* __restrict__ frame, 
             if (P == 4) {
                 const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(rs, off & ~15u, 0, 0);
                 v[k] = __uint_as_float(q.x) + __uint_as_float(q.w);
+            } else if (P == 7) {
+                const uint2 q = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rs, off & ~7u, 0, 0));
+                v[k] = __uint_as_float((off & 4u) ? q.y : q.x);
+            } else if (P == 8) {
+                uint32_t* base = lds + (threadIdx.x >> 6) * 8 * 256 + k * 256;  // wave-uniform
+                __builtin_amdgcn_global_load_lds(reinterpret_cast<const char*>(frame) + (off & ~15u), base, 16, 0, 0);
+                v[k] = 0.f;
             } else {
                 v[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
+            }
+        }
+        if (P == 8) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const uint32_t off = 4u * (uint32_t)((r + dy[k]) * W + c + dx[k]);
+                v[k] = __uint_as_float(lds[(threadIdx.x >> 6) * 8 * 256 + k * 256 + l * 4 + ((off >> 2) & 3u)]);
             }
         }
 #pragma unroll
@@ -118,7 +137,7 @@ static void run(const char* name, const float* d_frame, float* d_out, int grid, 
     const double lanes = (P == 3 ? 32.0 : 64.0);
     printf("{\"pattern\": \"%s\", \"ms\": %.4f, \"ns_per_gather_instr_per_cu\": %.3f, \"lanes_per_ns_per_cu\": %.3f, "
            "\"bytes_per_lane\": %d}\n",
-           name, t, t * 1e6 / instr_per_cu, instr_per_cu * lanes / (t * 1e6), P == 4 ? 16 : 4);
+           name, t, t * 1e6 / instr_per_cu, instr_per_cu * lanes / (t * 1e6), (P == 4 || P == 8) ? 16 : P == 7 ? 8 : 4);
     CK(hipEventDestroy(a));
     CK(hipEventDestroy(b));
 }
@@ -139,6 +158,8 @@ int main() {
     run<2>("brick", d_frame, d_out, grid, cus);
     run<3>("brick_even", d_frame, d_out, grid, cus);
     run<4>("brick_x4", d_frame, d_out, grid, cus);
+    run<7>("brick_x2", d_frame, d_out, grid, cus);
+    run<8>("brick_x4_lds", d_frame, d_out, grid, cus);
     run<5>("window", d_frame, d_out, grid, cus);
     run<6>("frame", d_frame, d_out, grid, cus);
     CK(hipFree(d_frame));
