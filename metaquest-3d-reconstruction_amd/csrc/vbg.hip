@@ -370,7 +370,7 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
     //     windows at other occupancies, with the block zc check, one-correction division, ILP 4.
     //     DESIGN.md §4.1 has the measurements behind the choice.
     int var = v->kernel_variant;
-    if (var < 0 || var > 20) var = 0;
+    if (var < 0 || var > 22) var = 0;
     if (!MQR_AB && var != 1 && var != 2 && var != 4) var = 0;
     if (var != 1 && var != 2 && !lean_ok) var = 2;
     if (var == 5 && (v->R != 16 || W % 4 != 0 || W < 4 || (reinterpret_cast<uintptr_t>(depths) & 15))) var = 0;
@@ -442,6 +442,14 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
                 hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 7, 2, 7>), dim3(lean_grid), dim3(512), 0, s, list,
                                    lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H,
                                    W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
+            else if (var == 21 && strunc_one_correction_ok(sdf_trunc))  // default + one-correction s / trunc
+                hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 6, 2, 5, 1>), dim3(lean_grid), dim3(512), 0, s, list,
+                                   lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H,
+                                   W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
+            else if (var == 22 && strunc_one_correction_ok(sdf_trunc))  // 21 + zc checked per block, >= 5 waves / SIMD
+                hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 5, 2, 5, 1, true>), dim3(lean_grid), dim3(512), 0, s,
+                                   list, lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW,
+                                   H, W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
             else if (var == 10)  // variant 9 with s / sdf_trunc in one correction (verified for this sdf_trunc)
                 hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 8, 2, 3, 1>), dim3(lean_grid), dim3(512), 0, s, list,
                                    lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H,
