@@ -360,14 +360,15 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
     const bool lean_ok = !div_unsafe_host(sdf_trunc) && depth_scale == 1.0f && 4 * (HW + W) <= (int64_t{1} << 31);
     // Variants (mqr_vbg_set_variant, low byte; all bit-identical, tests/test_gpu_numerics.py):
     //   0 default: k_integrate_lean -- R = 16: brick map, 8-byte window depth reads (lean_gather_w,
-    //     >= 6 waves per SIMD, 2 interleaved voxel chains) when the frames allow them (even H W,
+    //     >= 7 waves per SIMD, 2 interleaved voxel chains) when the frames allow them (even H W,
     //     8-byte aligned stack), else variant 4;  R = 8: plate map, dword gathers;
     //   1 generic k_integrate (runtime R);  2 exact k_integrate_t;  4 k_integrate_lean with dword
     //     gathers at >= 8 waves per SIMD (the round-2 default);
     //   A/B library only (MQR_AB, vbg_ab.hpp): 3 plate map;  5 packed LDS tiles (k_integrate_lt);
     //     6 / 7 paired-lane gathers;  8 VALU-lean projection / update, 9 + zc checked per block, 10 +
-    //     one-correction s / trunc;  11 / 12 / 14 16-byte windows;  13 / 15 / 16 / 17 / 18 8-byte
-    //     windows at other occupancies, with the block zc check, one-correction division, ILP 4.
+    //     one-correction s / trunc;  11 / 12 / 14 / 19 16-byte windows;  13 / 16 / 17 / 18 / 20 / 21 /
+    //     22 8-byte windows at 6 waves / SIMD, with the block zc check, one-correction division, ILP 4,
+    //     in two halves (15 = the default).
     //     DESIGN.md §4.1 has the measurements behind the choice.
     int var = v->kernel_variant;
     if (var < 0 || var > 22) var = 0;
@@ -417,8 +418,8 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
                 hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 5, 1, 4>), dim3(lean_grid), dim3(512), 0, s, list,
                                    lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H,
                                    W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
-            else if (var == 15)  // 8-byte window gathers, >= 7 waves / SIMD
-                hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 7, 2, 5>), dim3(lean_grid), dim3(512), 0, s, list,
+            else if (var == 13)  // 8-byte window gathers, >= 6 waves / SIMD (no spill)
+                hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 6, 2, 5>), dim3(lean_grid), dim3(512), 0, s, list,
                                    lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H,
                                    W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
             else if (var == 16 || (var == 17 && !strunc_one_correction_ok(sdf_trunc)))
@@ -476,8 +477,9 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
                 hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 8, 2>), dim3(lean_grid), dim3(512), 0, s, list,
                                    lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H,
                                    W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
-            else  // default: 8-byte window reads
-                hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 6, 2, 5>), dim3(lean_grid), dim3(512), 0, s, list,
+            else  // default: 8-byte window reads, >= 7 waves / SIMD (three per-block address words
+                  // spill to scratch outside the frame loop; 1-2 % faster than 6 waves, variant 13)
+                hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 7, 2, 5>), dim3(lean_grid), dim3(512), 0, s, list,
                                    lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H,
                                    W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
             // exact fix-up of the blocks the fast kernel handed back (usually none: reads a zero count;
