@@ -24,6 +24,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include <mutex>
 #include <tuple>
@@ -834,7 +835,7 @@ __global__ __launch_bounds__(NT) void k_mc_emit(const int32_t* __restrict__ nb, 
                                                         const int32_t* __restrict__ toff,
                                                         const uint4* __restrict__ rows4,
                                                         const uint32_t* __restrict__ rowNt, float* pos, float* nrm,
-                                                        int32_t* tri, int64_t cap_v, int64_t cap_t) {
+                                                        int32_t* tri, int64_t cap_v, int64_t cap_t, int diag = 0) {
     using M = Mc<R, 1>;
     static_assert(NT >= 256, "one thread per triangle-table row");
     __shared__ uint32_t rowN[M::S2];
@@ -865,7 +866,13 @@ __global__ __launch_bounds__(NT) void k_mc_emit(const int32_t* __restrict__ nb, 
 
     int xb, yb, zb;
     unpack_key(bkeys[b], xb, yb, zb);
+#if MQR_AB  // A/B library only: timing of one half of the pass (wrong output on purpose)
+    if (diag != 2)
+#endif
     for (int i = tid; i < nvb; i += NT) mc_emit_vertex<M>(i, rows, nbrow, pool, pres, xb, yb, zb, voxel_size, vb0, pos, nrm);
+#if MQR_AB
+    if (diag != 1)
+#endif
     for (int i = tid; i < ntb; i += NT) mc_emit_tri<M>(i, rows, rowN, triC, triP, nbrow, nbvoff, rows4, vb0, tb0, tri);
 }
 
@@ -1284,7 +1291,12 @@ static int64_t spec_cap(int64_t hint) { return hint > 0 ? hint + hint / 4 + 4096
 
 template <int RT, class... A>
 static void launch_mc_emit(const mqr_vbg* v, int64_t n, A... args) {
+#if MQR_AB  // MQR_EMIT_DIAG=1: vertices only, 2: triangles only (timing diagnostics)
+    static const int diag = getenv("MQR_EMIT_DIAG") ? atoi(getenv("MQR_EMIT_DIAG")) : 0;
+    hipLaunchKernelGGL((k_mc_emit<RT>), dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, args..., diag);
+#else
     hipLaunchKernelGGL((k_mc_emit<RT>), dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, args...);
+#endif
 }
 
 template <int RT>
