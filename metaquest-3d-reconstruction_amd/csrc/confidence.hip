@@ -14,6 +14,7 @@
 // (mqr_check_div64, tests/test_gpu_numerics.py).
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -29,6 +30,10 @@ struct ConfFrame {
     double rfx, rfy;  // RN(1 / fx), RN(1 / fy)
     double Tcw[12];   // camera -> world, rows 0..2
     double Tinv[12];  // world -> camera (float32 np.linalg.inv of Tcw, widened)
+    // consistency filter bounds (consistency_bound_terms): ||Tinv - exact inverse of Tcw|| as
+    // rotation part (Frobenius) and translation part, and ||R^T R - I||_F of Tcw's rotation
+    double dR, dT, eR;
+    int ok;  // frame_ok (a neighbour that is not ok is skipped, as the reference skips failed loads)
 };
 
 // ---- correctly rounded float64 quotients without the v_div_scale / v_div_fixup wrapper ----------
@@ -116,6 +121,84 @@ __device__ inline int pixel_error_d2(const float* __restrict__ tgt, int H, int W
     return 1;
 }
 
+// The reference's consistency test err <= threshold (err = |pw - q| as float32, q the target pixel
+// back-projected at its interpolated depth zt and mapped to the world by Tcw) decided without the
+// back-projection whenever the answer is clear, exactly as the full computation decides it:
+//   q - pw = Tcw p' - pw with p' = (xt, yt, zt) the back-projection, which lies on the ray through
+//   pt = Tinv pw at depth zt up to rounding (xt = X zt / Z (1 + 5u) + ulp(uu) zt / fx), so with
+//   R = Tcw's rotation and Tinv = Tcw^-1 + E:
+//     |pw - q| = |R (pt - p' - E pw)| = |Z - zt| |pt| / Z (1 +- eR) +- (dR |pw| + dT) (1 + eR) +- tiny
+//   where dR = ||R_inv - R^-1||_F, dT = |t_inv - t*| and eR = ||R^T R - I||_F are the frame's
+//   (host-computed) defects of the float32 matrices.  With the band B around sqrt(d2_max) the
+//   pair is counted consistent when |Z - zt|^2 |pt|^2 <= (sd - B)^2 Z^2 and inconsistent when
+//   > (sd + B)^2 Z^2 (margins 1e-9 m and 1e-12 relative cover the fp64 roundings); only pairs
+//   inside the band take the full float64 back-projection (pixel_error_d2's tail).
+// Returns 0 = no finite error (not counted), 1 = consistent, 2 = inconsistent.
+__device__ inline int pixel_decide(const float* __restrict__ tgt, int H, int W, const ConfFrame& ft,
+                                   const double pw[3], double pw_norm, double depth_max, double sd, double d2_max) {
+    const float dmf = (float)depth_max;
+    if (!ft.ok) return 0;  // a neighbour that is not ok is skipped (frame_ok)
+    // (loading every frame parameter in one batch before the first branch measured 3 % slower: the
+    // scalar reads hit the scalar cache, and 98 SGPRs cost occupancy)
+    const double* Ti = ft.Tinv;
+    const double fx = ft.fx, fy = ft.fy, cx = ft.cx, cy = ft.cy, dR = ft.dR, dT = ft.dT, eR = ft.eR;
+    double pt[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+        pt[i] = Ti[i * 4 + 0] * pw[0] + Ti[i * 4 + 1] * pw[1] + Ti[i * 4 + 2] * pw[2] + Ti[i * 4 + 3];
+    const double X = pt[0], Y = pt[1], Z = pt[2];
+    if (!(Z > 0 && isfinite(Z) && Z <= depth_max && isfinite(X) && isfinite(Y))) return 0;
+    const double ax = X * fx, ay = Y * fy;
+    double qx, qy;
+    if (div64_safe(Z) && div64_safe(ax) && div64_safe(ay) && fabs(ax) <= 0x1p400 * Z && fabs(ay) <= 0x1p400 * Z) {
+        const Rcp64 rz = rcp64_refine(Z);
+        qx = div64_core(ax, rz);
+        qy = div64_core(ay, rz);
+    } else {
+        qx = ax / Z;
+        qy = ay / Z;
+    }
+    const double uu = qx + cx;
+    const double vv = qy + cy;
+    if (!(isfinite(uu) && isfinite(vv))) return 0;
+    const double max_coord = (double)((W > H ? W : H) * 10);
+    if (!(uu >= -max_coord && uu < max_coord && vv >= -max_coord && vv < max_coord)) return 0;
+    const int u0 = (int)floor(uu), v0 = (int)floor(vv), u1 = u0 + 1, v1 = v0 + 1;
+    if (!(u0 >= 0 && u1 < W && v0 >= 0 && v1 < H)) return 0;
+    // both rows' taps read before any test on them (short-circuit tests between the two reads made
+    // the compiler issue the second read after the first had returned)
+    float2 ab, cd;
+    const float* row0 = tgt + (int64_t)v0 * W + u0;
+    __builtin_memcpy(&ab, row0, sizeof(float2));
+    __builtin_memcpy(&cd, row0 + W, sizeof(float2));
+    const float Ia = ab.x, Ib = ab.y, Ic = cd.x, Id = cd.y;
+    const bool taps = (Ib > 0) & (Ib <= dmf) & (Ia > 0) & (Ia <= dmf) & (Ic > 0) & (Ic <= dmf) & (Id > 0) & (Id <= dmf);
+    if (!taps) return 0;
+    const double wa = ((double)u1 - uu) * ((double)v1 - vv);
+    const double wb = (uu - (double)u0) * ((double)v1 - vv);
+    const double wc = ((double)u1 - uu) * (vv - (double)v0);
+    const double wd = (uu - (double)u0) * (vv - (double)v0);
+    const float zt = (float)(wa * Ia + wb * Ib + wc * Ic + wd * Id);
+    if (!(zt > 0 && isfinite(zt))) return 0;
+    const double ztd = (double)zt;
+    // the filter
+    const double B = (dR * pw_norm + dT) * (1.0 + eR) + eR * (sd + 1.0) + 1e-9;
+    const double lo = sd - B, hi = sd + B;
+    const double dz = Z - ztd, S = X * X + Y * Y + Z * Z, Z2 = Z * Z;
+    const double lhs = dz * dz * S;
+    if (lo > 0 && lhs <= lo * lo * Z2 * (1.0 - 1e-12)) return 1;
+    if (lhs > hi * hi * Z2 * (1.0 + 1e-12)) return 2;
+    // inside the band: the reference's own float64 back-projection
+    const double xt = div64_by_rn_rcp((uu - ft.cx) * ztd, ft.fx, ft.rfx);
+    const double yt = div64_by_rn_rcp((vv - ft.cy) * ztd, ft.fy, ft.rfy);
+    double q[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+        q[i] = ft.Tcw[i * 4 + 0] * xt + ft.Tcw[i * 4 + 1] * yt + ft.Tcw[i * 4 + 2] * ztd + ft.Tcw[i * 4 + 3];
+    const double ex = pw[0] - q[0], ey = pw[1] - q[1], ez = pw[2] - q[2];
+    return ex * ex + ey * ey + ez * ez <= d2_max ? 1 : 2;
+}
+
 // depth_to_pointcloud_numpy for one pixel: returns 0 when the ref pixel is not in (0, depth_max].
 __device__ inline int ref_point(const ConfFrame& fr, int u, int v, float dref, double depth_max, double pw[3]) {
     if (!(dref > 0 && dref <= (float)depth_max)) return 0;
@@ -133,9 +216,12 @@ __device__ inline int ref_point(const ConfFrame& fr, int u, int v, float dref, d
 __global__ __launch_bounds__(256) void k_confidence(const float* __restrict__ depths, int N, int H, int W,
                                                     const ConfFrame* __restrict__ fr, const uint8_t* __restrict__ ok,
                                                     int ref_begin, int r, double depth_max, double d2_max,
-                                                    double* __restrict__ conf, int32_t* __restrict__ valid) {
+                                                    double sd, double* __restrict__ conf, int32_t* __restrict__ valid) {
     const int64_t HW = (int64_t)H * W;
-    const int ref = ref_begin + blockIdx.y;
+    // (grouping the grid as G reference frames per pixel tile, for L2 reuse of the neighbours' taps,
+    // measured no faster for G = 4 ... 64)
+    const int rloc = blockIdx.y;
+    const int ref = ref_begin + rloc;
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= HW) return;
     const int u = (int)(p % W), v = (int)(p / W);
@@ -143,16 +229,15 @@ __global__ __launch_bounds__(256) void k_confidence(const float* __restrict__ de
     int nv = 0, nc = 0;
     if (ref_point(fr[ref], u, v, depths[(int64_t)ref * HW + p], depth_max, pw)) {
         const int lo = max(0, ref - r), hi = min(N, ref + r + 1);
+        const double pw_norm = sqrt(pw[0] * pw[0] + pw[1] * pw[1] + pw[2] * pw[2]) * (1.0 + 1e-12);
         for (int t = lo; t < hi; ++t) {
-            if (t == ref || !ok[t]) continue;
-            double d2;
-            if (pixel_error_d2(depths + (int64_t)t * HW, H, W, fr[t], pw, depth_max, &d2)) {
-                ++nv;
-                if (d2 <= d2_max) ++nc;
-            }
+            if (t == ref) continue;
+            const int dcs = pixel_decide(depths + (int64_t)t * HW, H, W, fr[t], pw, pw_norm, depth_max, sd, d2_max);
+            nv += dcs != 0;
+            nc += dcs == 1;
         }
     }
-    const int64_t o = (int64_t)blockIdx.y * HW + p;
+    const int64_t o = (int64_t)rloc * HW + p;
     valid[o] = nv;
     conf[o] = nv == 0 ? 0.0 : (double)nc / (double)nv;
 }
@@ -204,12 +289,35 @@ void fill_frame(const float* K, const float* Tcw, const float* Tinv, ConfFrame& 
     f.fy = (double)K[4];
     f.cx = (double)K[2];
     f.cy = (double)K[5];
+    f.ok = 1;
     f.rfx = 1.0 / f.fx;  // correctly rounded (IEEE host division)
     f.rfy = 1.0 / f.fy;
     for (int k = 0; k < 12; ++k) {
         f.Tcw[k] = (double)Tcw[k];
         f.Tinv[k] = Tinv ? (double)Tinv[k] : 0.0;
     }
+    // consistency filter terms (pixel_decide): defects of the float32 matrices, in double, with slack
+    const double* T = f.Tcw;
+    const double a = T[0], b = T[1], c = T[2], d = T[4], e = T[5], g = T[6], h = T[8], i = T[9], j = T[10];
+    const double det = a * (e * j - g * i) - b * (d * j - g * h) + c * (d * i - e * h);
+    double inv[9] = {(e * j - g * i) / det, (c * i - b * j) / det, (b * g - c * e) / det,
+                     (g * h - d * j) / det, (a * j - c * h) / det, (c * d - a * g) / det,
+                     (d * i - e * h) / det, (b * h - a * i) / det, (a * e - b * d) / det};
+    double dR = 0.0, dT = 0.0, eR = 0.0;
+    for (int r = 0; r < 3; ++r) {
+        const double ts = -(inv[3 * r] * T[3] + inv[3 * r + 1] * T[7] + inv[3 * r + 2] * T[11]);
+        dT += (f.Tinv[4 * r + 3] - ts) * (f.Tinv[4 * r + 3] - ts);
+        for (int k = 0; k < 3; ++k) {
+            dR += (f.Tinv[4 * r + k] - inv[3 * r + k]) * (f.Tinv[4 * r + k] - inv[3 * r + k]);
+            double rtr = 0.0;  // (R^T R)_{rk}
+            for (int m = 0; m < 3; ++m) rtr += T[4 * m + r] * T[4 * m + k];
+            eR += (rtr - (r == k)) * (rtr - (r == k));
+        }
+    }
+    const bool finite = std::isfinite(det) && det != 0.0 && std::isfinite(dR) && std::isfinite(dT) && std::isfinite(eR);
+    f.dR = finite ? std::sqrt(dR) * 1.01 + 1e-12 : INFINITY;
+    f.dT = finite ? std::sqrt(dT) * 1.01 + 1e-12 : INFINITY;
+    f.eR = finite ? std::sqrt(eR) * 1.01 + 1e-12 : INFINITY;
 }
 
 // Largest double d2 >= 0 with (float)sqrt(d2) <= thr (binary search over the ordered bit patterns
@@ -254,6 +362,7 @@ int mqr_confidence(int device, const float* depths, int depth_loc, int N, int H,
     for (int i = 0; i < N; ++i) {
         fill_frame(K + 9 * i, T_cw + 16 * i, T_cw_inv + 16 * i, fr[i]);
         if (frame_ok) okv[i] = frame_ok[i] ? 1 : 0;
+        fr[i].ok = okv[i];
     }
     ConfFrame* dfr = nullptr;
     uint8_t* dok = nullptr;
@@ -275,8 +384,9 @@ int mqr_confidence(int device, const float* depths, int depth_loc, int N, int H,
         MQR_CHECK_HIP(hipMalloc(&dvalid, sizeof(int32_t) * nref * HW));
     }
     // (float) threshold: numpy compares the float32 error map against a weak Python float.
+    const double d2max = d2_threshold((float)error_threshold);
     hipLaunchKernelGGL(k_confidence, dim3((unsigned)((HW + 255) / 256), nref), dim3(256), 0, s, dsrc, N, H, W, dfr,
-                       dok, ref_begin, frame_range, depth_max, d2_threshold((float)error_threshold), dconf, dvalid);
+                       dok, ref_begin, frame_range, depth_max, d2max, d2max >= 0 ? std::sqrt(d2max) : NAN, dconf, dvalid);
     MQR_CHECK_HIP(hipGetLastError());
     if (out_loc != MQR_DEVICE) {
         MQR_CHECK_HIP(hipMemcpyAsync(conf, dconf, sizeof(double) * nref * HW, hipMemcpyDeviceToHost, s));
