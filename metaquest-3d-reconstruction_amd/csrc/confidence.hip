@@ -16,6 +16,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <vector>
 
 #include "mqr_common.hpp"
@@ -30,9 +31,10 @@ struct ConfFrame {
     double rfx, rfy;  // RN(1 / fx), RN(1 / fy)
     double Tcw[12];   // camera -> world, rows 0..2
     double Tinv[12];  // world -> camera (float32 np.linalg.inv of Tcw, widened)
-    // consistency filter bounds (consistency_bound_terms): ||Tinv - exact inverse of Tcw|| as
-    // rotation part (Frobenius) and translation part, and ||R^T R - I||_F of Tcw's rotation
-    double dR, dT, eR;
+    // consistency band terms (pixel_decide): c1 = dR (1 + eR), c0 = dT (1 + eR) + eR (sd + 1) + 1e-9
+    // from dR = ||R_inv - R^-1||_F, dT = |t_inv - t*| (Tinv against the exact inverse of Tcw) and
+    // eR = ||R^T R - I||_F of Tcw's rotation; +inf when they are not finite
+    double c1, c0;
     int ok;  // frame_ok (a neighbour that is not ok is skipped, as the reference skips failed loads)
 };
 
@@ -127,30 +129,40 @@ __device__ inline int pixel_error_d2(const float* __restrict__ tgt, int H, int W
 //   q - pw = Tcw p' - pw with p' = (xt, yt, zt) the back-projection, which lies on the ray through
 //   pt = Tinv pw at depth zt up to rounding (xt = X zt / Z (1 + 5u) + ulp(uu) zt / fx), so with
 //   R = Tcw's rotation and Tinv = Tcw^-1 + E:
-//     |pw - q| = |R (pt - p' - E pw)| = |Z - zt| |pt| / Z (1 +- eR) +- (dR |pw| + dT) (1 + eR) +- tiny
+//     |pw - q| = |Z - zt| |pt| / Z (1 +- eR) +- (dR |pw| + dT) (1 + eR) +- tiny
 //   where dR = ||R_inv - R^-1||_F, dT = |t_inv - t*| and eR = ||R^T R - I||_F are the frame's
-//   (host-computed) defects of the float32 matrices.  With the band B around sqrt(d2_max) the
-//   pair is counted consistent when |Z - zt|^2 |pt|^2 <= (sd - B)^2 Z^2 and inconsistent when
-//   > (sd + B)^2 Z^2 (margins 1e-9 m and 1e-12 relative cover the fp64 roundings); only pairs
-//   inside the band take the full float64 back-projection (pixel_error_d2's tail).
+//   (host-computed) defects of the float32 matrices.  With the band B = c1 |pw| + c0 around
+//   sd = sqrt(d2_max) (c1 = dR (1 + eR), c0 = dT (1 + eR) + eR (sd + 1) + 1e-9, maxima over the
+//   reference frame's neighbours, k_confidence) the pair is consistent when
+//   |Z - zt|^2 |pt|^2 <= lo2 Z^2 (lo2 = (sd - B)^2 (1 - 1e-12)) and inconsistent when > hi2 Z^2
+//   (hi2 = (sd + B)^2 (1 + 1e-12)); the margins cover the fp64 roundings.  Only pairs inside the band
+//   take the full float64 back-projection (pixel_error_d2's tail).  A NaN / infinite band (a frame
+//   whose defects are not finite) fails both compares and sends every pair to the exact tail.
+// The validity tests are pixel_error_d2's, restated without changing a decision:
+//   * Z <= zmax (= min(depth_max, DBL_MAX)) also rejects Z = inf;
+//   * X, Y are not tested: a non-finite X or Y gives a non-finite uu / vv, which fails the range test;
+//   * the range test 0 <= uu < W - 1, 0 <= vv < H - 1 is exactly floor(uu) >= 0, floor(uu) + 1 < W
+//     (and for v), and implies the |coord| < 10 max(W, H) and finiteness tests (NaN fails it);
+//   * (double)u1 = floor(uu) + 1 exactly.
 // Returns 0 = no finite error (not counted), 1 = consistent, 2 = inconsistent.
-__device__ inline int pixel_decide(const float* __restrict__ tgt, int H, int W, const ConfFrame& ft,
-                                   const double pw[3], double pw_norm, double depth_max, double sd, double d2_max) {
-    const float dmf = (float)depth_max;
+__device__ inline int pixel_decide(const float* __restrict__ tgt, int W, double wm1, double hm1, const ConfFrame& ft,
+                                   const double pw[3], double zmax, float dmf, double lo2, double hi2,
+                                   double d2_max) {
     if (!ft.ok) return 0;  // a neighbour that is not ok is skipped (frame_ok)
     // (loading every frame parameter in one batch before the first branch measured 3 % slower: the
     // scalar reads hit the scalar cache, and 98 SGPRs cost occupancy)
     const double* Ti = ft.Tinv;
-    const double fx = ft.fx, fy = ft.fy, cx = ft.cx, cy = ft.cy, dR = ft.dR, dT = ft.dT, eR = ft.eR;
-    double pt[3];
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-        pt[i] = Ti[i * 4 + 0] * pw[0] + Ti[i * 4 + 1] * pw[1] + Ti[i * 4 + 2] * pw[2] + Ti[i * 4 + 3];
-    const double X = pt[0], Y = pt[1], Z = pt[2];
-    if (!(Z > 0 && isfinite(Z) && Z <= depth_max && isfinite(X) && isfinite(Y))) return 0;
-    const double ax = X * fx, ay = Y * fy;
+    const double Z = Ti[8] * pw[0] + Ti[9] * pw[1] + Ti[10] * pw[2] + Ti[11];
+    if (!(Z > 0 && Z <= zmax)) return 0;
+    const double X = Ti[0] * pw[0] + Ti[1] * pw[1] + Ti[2] * pw[2] + Ti[3];
+    const double Y = Ti[4] * pw[0] + Ti[5] * pw[1] + Ti[6] * pw[2] + Ti[7];
+    const double ax = X * ft.fx, ay = Y * ft.fy;
+    const double aax = fabs(ax), aay = fabs(ay), zb = 0x1p400 * Z;
+    // div64_safe(Z) && div64_safe(ax) && div64_safe(ay) && |ax|, |ay| <= 2^400 Z, without short-circuit
+    const bool fast = (Z >= 0x1p-500) & (Z <= 0x1p500) & ((aax >= 0x1p-500) | (ax == 0.0)) &
+                      ((aay >= 0x1p-500) | (ay == 0.0)) & (aax <= zb) & (aay <= zb);
     double qx, qy;
-    if (div64_safe(Z) && div64_safe(ax) && div64_safe(ay) && fabs(ax) <= 0x1p400 * Z && fabs(ay) <= 0x1p400 * Z) {
+    if (__builtin_expect(fast, 1)) {
         const Rcp64 rz = rcp64_refine(Z);
         qx = div64_core(ax, rz);
         qy = div64_core(ay, rz);
@@ -158,13 +170,11 @@ __device__ inline int pixel_decide(const float* __restrict__ tgt, int H, int W, 
         qx = ax / Z;
         qy = ay / Z;
     }
-    const double uu = qx + cx;
-    const double vv = qy + cy;
-    if (!(isfinite(uu) && isfinite(vv))) return 0;
-    const double max_coord = (double)((W > H ? W : H) * 10);
-    if (!(uu >= -max_coord && uu < max_coord && vv >= -max_coord && vv < max_coord)) return 0;
-    const int u0 = (int)floor(uu), v0 = (int)floor(vv), u1 = u0 + 1, v1 = v0 + 1;
-    if (!(u0 >= 0 && u1 < W && v0 >= 0 && v1 < H)) return 0;
+    const double uu = qx + ft.cx;
+    const double vv = qy + ft.cy;
+    if (!((uu >= 0.0) & (uu < wm1) & (vv >= 0.0) & (vv < hm1))) return 0;
+    const double fu0 = floor(uu), fv0 = floor(vv);
+    const int u0 = (int)fu0, v0 = (int)fv0;
     // both rows' taps read before any test on them (short-circuit tests between the two reads made
     // the compiler issue the second read after the first had returned)
     float2 ab, cd;
@@ -174,20 +184,19 @@ __device__ inline int pixel_decide(const float* __restrict__ tgt, int H, int W, 
     const float Ia = ab.x, Ib = ab.y, Ic = cd.x, Id = cd.y;
     const bool taps = (Ib > 0) & (Ib <= dmf) & (Ia > 0) & (Ia <= dmf) & (Ic > 0) & (Ic <= dmf) & (Id > 0) & (Id <= dmf);
     if (!taps) return 0;
-    const double wa = ((double)u1 - uu) * ((double)v1 - vv);
-    const double wb = (uu - (double)u0) * ((double)v1 - vv);
-    const double wc = ((double)u1 - uu) * (vv - (double)v0);
-    const double wd = (uu - (double)u0) * (vv - (double)v0);
+    const double du1 = fu0 + 1.0, dv1 = fv0 + 1.0;
+    const double wa = (du1 - uu) * (dv1 - vv);
+    const double wb = (uu - fu0) * (dv1 - vv);
+    const double wc = (du1 - uu) * (vv - fv0);
+    const double wd = (uu - fu0) * (vv - fv0);
     const float zt = (float)(wa * Ia + wb * Ib + wc * Ic + wd * Id);
     if (!(zt > 0 && isfinite(zt))) return 0;
     const double ztd = (double)zt;
     // the filter
-    const double B = (dR * pw_norm + dT) * (1.0 + eR) + eR * (sd + 1.0) + 1e-9;
-    const double lo = sd - B, hi = sd + B;
-    const double dz = Z - ztd, S = X * X + Y * Y + Z * Z, Z2 = Z * Z;
-    const double lhs = dz * dz * S;
-    if (lo > 0 && lhs <= lo * lo * Z2 * (1.0 - 1e-12)) return 1;
-    if (lhs > hi * hi * Z2 * (1.0 + 1e-12)) return 2;
+    const double dz = Z - ztd, Z2 = Z * Z;
+    const double lhs = dz * dz * (X * X + Y * Y + Z2);
+    if (lhs <= lo2 * Z2) return 1;
+    if (lhs > hi2 * Z2) return 2;
     // inside the band: the reference's own float64 back-projection
     const double xt = div64_by_rn_rcp((uu - ft.cx) * ztd, ft.fx, ft.rfx);
     const double yt = div64_by_rn_rcp((vv - ft.cy) * ztd, ft.fy, ft.rfy);
@@ -214,9 +223,9 @@ __device__ inline int ref_point(const ConfFrame& fr, int u, int v, float dref, d
 // d2_max: the largest double d2 with (float)sqrt(d2) <= threshold (host, exact); the reference's
 // `err <= threshold` on the float32 error map is d2 <= d2_max (sqrt and both roundings monotone).
 __global__ __launch_bounds__(256) void k_confidence(const float* __restrict__ depths, int N, int H, int W,
-                                                    const ConfFrame* __restrict__ fr, const uint8_t* __restrict__ ok,
-                                                    int ref_begin, int r, double depth_max, double d2_max,
-                                                    double sd, double* __restrict__ conf, int32_t* __restrict__ valid) {
+                                                    const ConfFrame* __restrict__ fr, int ref_begin, int r,
+                                                    double depth_max, double d2_max, double sd,
+                                                    double* __restrict__ conf, int32_t* __restrict__ valid) {
     const int64_t HW = (int64_t)H * W;
     // (grouping the grid as G reference frames per pixel tile, for L2 reuse of the neighbours' taps,
     // measured no faster for G = 4 ... 64)
@@ -229,10 +238,24 @@ __global__ __launch_bounds__(256) void k_confidence(const float* __restrict__ de
     int nv = 0, nc = 0;
     if (ref_point(fr[ref], u, v, depths[(int64_t)ref * HW + p], depth_max, pw)) {
         const int lo = max(0, ref - r), hi = min(N, ref + r + 1);
+        // the consistency band (pixel_decide): the neighbours' largest defect terms, then per pixel
+        double c1 = 0.0, c0 = 0.0;
+        for (int t = lo; t < hi; ++t)
+            if (t != ref && fr[t].ok) {
+                c1 = fmax(c1, fr[t].c1);
+                c0 = fmax(c0, fr[t].c0);
+            }
         const double pw_norm = sqrt(pw[0] * pw[0] + pw[1] * pw[1] + pw[2] * pw[2]) * (1.0 + 1e-12);
+        const double B = c1 * pw_norm + c0;
+        const double blo = sd - B, bhi = sd + B;
+        const double lo2 = blo > 0 ? blo * blo * (1.0 - 1e-12) : -1.0;
+        const double hi2 = bhi * bhi * (1.0 + 1e-12);
+        const double zmax = fmin(depth_max, 0x1.fffffffffffffp1023);
+        const float dmf = (float)depth_max;
+        const double wm1 = (double)(W - 1), hm1 = (double)(H - 1);
         for (int t = lo; t < hi; ++t) {
             if (t == ref) continue;
-            const int dcs = pixel_decide(depths + (int64_t)t * HW, H, W, fr[t], pw, pw_norm, depth_max, sd, d2_max);
+            const int dcs = pixel_decide(depths + (int64_t)t * HW, W, wm1, hm1, fr[t], pw, zmax, dmf, lo2, hi2, d2_max);
             nv += dcs != 0;
             nc += dcs == 1;
         }
@@ -284,7 +307,7 @@ __global__ void k_check_div64(int mode, uint64_t seed, uint64_t count, double a_
 using namespace mqr;
 
 namespace {
-void fill_frame(const float* K, const float* Tcw, const float* Tinv, ConfFrame& f) {
+void fill_frame(const float* K, const float* Tcw, const float* Tinv, double sd, ConfFrame& f) {
     f.fx = (double)K[0];
     f.fy = (double)K[4];
     f.cx = (double)K[2];
@@ -315,9 +338,13 @@ void fill_frame(const float* K, const float* Tcw, const float* Tinv, ConfFrame& 
         }
     }
     const bool finite = std::isfinite(det) && det != 0.0 && std::isfinite(dR) && std::isfinite(dT) && std::isfinite(eR);
-    f.dR = finite ? std::sqrt(dR) * 1.01 + 1e-12 : INFINITY;
-    f.dT = finite ? std::sqrt(dT) * 1.01 + 1e-12 : INFINITY;
-    f.eR = finite ? std::sqrt(eR) * 1.01 + 1e-12 : INFINITY;
+    dR = std::sqrt(dR) * 1.01 + 1e-12;
+    dT = std::sqrt(dT) * 1.01 + 1e-12;
+    eR = std::sqrt(eR) * 1.01 + 1e-12;
+    // sd NaN (no consistent error possible): the band is irrelevant, every pair takes the exact tail
+    const double c1 = dR * (1.0 + eR), c0 = dT * (1.0 + eR) + eR * (sd + 1.0) + 1e-9;
+    f.c1 = finite && std::isfinite(c1) ? c1 : INFINITY;
+    f.c0 = finite && std::isfinite(c0) ? c0 : INFINITY;
 }
 
 // Largest double d2 >= 0 with (float)sqrt(d2) <= thr (binary search over the ordered bit patterns
@@ -340,6 +367,15 @@ double d2_threshold(float thr) {
     std::memcpy(&d, &lo, sizeof d);
     return d;
 }
+constexpr int kConfDevices = 64;
+struct ConfCache {
+    std::mutex mu;
+    hipStream_t s = nullptr;
+    ConfFrame* dfr = nullptr;  // device frame parameters, grow-only
+    ConfFrame* hfr = nullptr;  // pinned staging
+    int cap = 0;
+};
+ConfCache g_conf_cache[kConfDevices];
 }  // namespace
 
 extern "C" {
@@ -351,28 +387,41 @@ int mqr_confidence(int device, const float* depths, int depth_loc, int N, int H,
     MQR_REQUIRE(depths && K && T_cw && T_cw_inv && conf && valid, "null argument");
     MQR_REQUIRE(N > 0 && H > 0 && W > 0, "bad shape");
     MQR_REQUIRE(ref_begin >= 0 && ref_end <= N && ref_begin <= ref_end, "bad reference frame range");
+    MQR_REQUIRE(device >= 0 && device < kConfDevices, "bad device");
     MQR_CHECK_HIP(hipSetDevice(device));
     const int nref = ref_end - ref_begin;
     if (nref == 0) return 0;
     const int64_t HW = (int64_t)H * W;
-    hipStream_t s;
-    MQR_CHECK_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-    std::vector<ConfFrame> fr(N);
-    std::vector<uint8_t> okv(N, 1);
-    for (int i = 0; i < N; ++i) {
-        fill_frame(K + 9 * i, T_cw + 16 * i, T_cw_inv + 16 * i, fr[i]);
-        if (frame_ok) okv[i] = frame_ok[i] ? 1 : 0;
-        fr[i].ok = okv[i];
+    // (float) threshold: numpy compares the float32 error map against a weak Python float.
+    const double d2max = d2_threshold((float)error_threshold);
+    const double sd = d2max >= 0 ? std::sqrt(d2max) : NAN;
+    // per-device stream and frame-parameter buffers, kept between calls: a stream create / destroy and
+    // a hipMalloc / hipFree pair per call (hipFree synchronises the device) cost ~0.5 ms of a 13 ms call
+    ConfCache& cc = g_conf_cache[device];
+    std::lock_guard<std::mutex> lock(cc.mu);
+    if (!cc.s) MQR_CHECK_HIP(hipStreamCreateWithFlags(&cc.s, hipStreamNonBlocking));
+    if (cc.cap < N) {
+        if (cc.dfr) (void)hipFree(cc.dfr);
+        if (cc.hfr) (void)hipHostFree(cc.hfr);
+        cc.dfr = nullptr;
+        cc.hfr = nullptr;
+        cc.cap = 0;
+        MQR_CHECK_HIP(hipMalloc(&cc.dfr, sizeof(ConfFrame) * N));
+        MQR_CHECK_HIP(hipHostMalloc(&cc.hfr, sizeof(ConfFrame) * N, hipHostMallocDefault));
+        cc.cap = N;
     }
-    ConfFrame* dfr = nullptr;
-    uint8_t* dok = nullptr;
+    hipStream_t s = cc.s;
+    ConfFrame* fr = cc.hfr;
+    MQR_CHECK_HIP(hipStreamSynchronize(s));  // the previous call's upload has finished with hfr
+    for (int i = 0; i < N; ++i) {
+        fill_frame(K + 9 * i, T_cw + 16 * i, T_cw_inv + 16 * i, sd, fr[i]);
+        fr[i].ok = frame_ok ? (frame_ok[i] ? 1 : 0) : 1;
+    }
+    ConfFrame* dfr = cc.dfr;
     float* dd = nullptr;
     double* dconf = conf;
     int32_t* dvalid = valid;
-    MQR_CHECK_HIP(hipMalloc(&dfr, sizeof(ConfFrame) * N));
-    MQR_CHECK_HIP(hipMalloc(&dok, N));
-    MQR_CHECK_HIP(hipMemcpy(dfr, fr.data(), sizeof(ConfFrame) * N, hipMemcpyHostToDevice));
-    MQR_CHECK_HIP(hipMemcpy(dok, okv.data(), N, hipMemcpyHostToDevice));
+    MQR_CHECK_HIP(hipMemcpyAsync(dfr, fr, sizeof(ConfFrame) * N, hipMemcpyHostToDevice, s));
     const float* dsrc = depths;
     if (depth_loc != MQR_DEVICE) {
         MQR_CHECK_HIP(hipMalloc(&dd, sizeof(float) * N * HW));
@@ -383,10 +432,8 @@ int mqr_confidence(int device, const float* depths, int depth_loc, int N, int H,
         MQR_CHECK_HIP(hipMalloc(&dconf, sizeof(double) * nref * HW));
         MQR_CHECK_HIP(hipMalloc(&dvalid, sizeof(int32_t) * nref * HW));
     }
-    // (float) threshold: numpy compares the float32 error map against a weak Python float.
-    const double d2max = d2_threshold((float)error_threshold);
     hipLaunchKernelGGL(k_confidence, dim3((unsigned)((HW + 255) / 256), nref), dim3(256), 0, s, dsrc, N, H, W, dfr,
-                       dok, ref_begin, frame_range, depth_max, d2max, d2max >= 0 ? std::sqrt(d2max) : NAN, dconf, dvalid);
+                       ref_begin, frame_range, depth_max, d2max, sd, dconf, dvalid);
     MQR_CHECK_HIP(hipGetLastError());
     if (out_loc != MQR_DEVICE) {
         MQR_CHECK_HIP(hipMemcpyAsync(conf, dconf, sizeof(double) * nref * HW, hipMemcpyDeviceToHost, s));
@@ -398,9 +445,6 @@ int mqr_confidence(int device, const float* depths, int depth_loc, int N, int H,
         (void)hipFree(dvalid);
     }
     if (dd) (void)hipFree(dd);
-    (void)hipFree(dfr);
-    (void)hipFree(dok);
-    (void)hipStreamDestroy(s);
     return 0;
 }
 
@@ -438,8 +482,8 @@ int mqr_pixel_error_map(int device, const float* ref_depth, const float* tgt_dep
     MQR_CHECK_HIP(hipSetDevice(device));
     const int64_t HW = (int64_t)H * W;
     ConfFrame fr[2] = {};
-    fill_frame(K_ref, T_cw_ref, nullptr, fr[0]);
-    fill_frame(K_tgt, T_cw_tgt, T_cw_inv_tgt, fr[1]);
+    fill_frame(K_ref, T_cw_ref, nullptr, NAN, fr[0]);
+    fill_frame(K_tgt, T_cw_tgt, T_cw_inv_tgt, NAN, fr[1]);
     ConfFrame* dfr = nullptr;
     float *dr = nullptr, *dt = nullptr, *de = nullptr;
     MQR_CHECK_HIP(hipMalloc(&dfr, sizeof(fr)));
