@@ -53,3 +53,28 @@ def test_confidence_full_resolution_vs_oracle():
         assert np.array_equal(valid[i], ov)
         assert np.array_equal(conf[i], oc)
     assert valid.max() > 0
+
+
+@pytest.mark.parametrize("thr,dmax", [(0.08, 4.0), (0.0, 4.0), (-1.0, 4.0), (np.inf, 4.0), (1e30, 4.0),
+                                      (0.002, 4.0), (0.08, np.inf)])
+def test_confidence_band_edges_vs_oracle(thr, dmax):
+    """The consistency band (pixel_decide) against the oracle's full computation: thresholds at the
+    extremes (nothing / everything consistent, +inf) and small enough that many pairs fall inside the
+    band, unbounded depth_max, a non-rigid pose (large R^T R - I), a pose with a NaN entry and one with
+    an inverse off by 1 mm (large dT)."""
+    from mqr import synthetic
+    from mqr.confidence import confidence_maps
+    n = 16  # reference frames 5..10 see only finite-band neighbours (the band path proper)
+    seq = synthetic.make_sequence("room", n=n, height=120, width=160, f=131.25, noise=True, seed=11)
+    T = seq["T_cw"].astype(np.float32).copy()
+    T[1, :3, :3] *= np.float32(1.001)  # scaled rotation
+    T[14, 0, 3] = np.nan
+    Ti = np.linalg.inv(T.astype(np.float64)).astype(np.float32)
+    Ti[8, 1, 3] += np.float32(1e-3)
+    conf, valid = confidence_maps(seq["depth"], seq["K"], T, Ti, 0, n, 3, dmax, thr)
+    for i in range(n):
+        oc, ov = oracle.confidence(seq["depth"], seq["K"], T, Ti, i, 3, dmax, thr)
+        assert np.array_equal(valid[i], ov), i
+        assert np.array_equal(conf[i], oc), i
+    if thr == 0.08:
+        assert valid.max() > 0 and 0 < conf.mean() < 1
