@@ -185,6 +185,18 @@ __device__ inline int pixel_decide(const float* __restrict__ tgt, int W, double 
     const bool taps = (Ib > 0) & (Ib <= dmf) & (Ia > 0) & (Ia <= dmf) & (Ic > 0) & (Ic <= dmf) & (Id > 0) & (Id <= dmf);
     if (!taps) return 0;
     const double du1 = fu0 + 1.0, dv1 = fv0 + 1.0;
+    // the filter, on a float32 interpolation zf of the target depth: every weight and product is
+    // positive, so zf is within 7 * 2^-24 relative of the reference's sum and zt (its float32
+    // rounding) within 2^-24: |zf - zt| <= 2^-21 zt <= 2^-21 depth_max, covered by the band's
+    // 2^-18 depth_max * ray-length term (fill_frame).  The reference's tests zt > 0 and finite hold
+    // for positive finite taps (weights >= 0 summing to 1), so they cannot reject a pair here.
+    const float gu = (float)(du1 - uu), gv = (float)(dv1 - vv), fu = (float)(uu - fu0), fv = (float)(vv - fv0);
+    const float zf = __builtin_fmaf(fu * fv, Id, __builtin_fmaf(gu * fv, Ic, __builtin_fmaf(fu * gv, Ib, (gu * gv) * Ia)));
+    const double dz = Z - (double)zf, Z2 = Z * Z;
+    const double lhs = dz * dz * (X * X + Y * Y + Z2);
+    if (lhs <= lo2 * Z2) return 1;
+    if (lhs > hi2 * Z2) return 2;
+    // inside the band: the reference's own interpolation and float64 back-projection
     const double wa = (du1 - uu) * (dv1 - vv);
     const double wb = (uu - fu0) * (dv1 - vv);
     const double wc = (du1 - uu) * (vv - fv0);
@@ -192,12 +204,6 @@ __device__ inline int pixel_decide(const float* __restrict__ tgt, int W, double 
     const float zt = (float)(wa * Ia + wb * Ib + wc * Ic + wd * Id);
     if (!(zt > 0 && isfinite(zt))) return 0;
     const double ztd = (double)zt;
-    // the filter
-    const double dz = Z - ztd, Z2 = Z * Z;
-    const double lhs = dz * dz * (X * X + Y * Y + Z2);
-    if (lhs <= lo2 * Z2) return 1;
-    if (lhs > hi2 * Z2) return 2;
-    // inside the band: the reference's own float64 back-projection
     const double xt = div64_by_rn_rcp((uu - ft.cx) * ztd, ft.fx, ft.rfx);
     const double yt = div64_by_rn_rcp((vv - ft.cy) * ztd, ft.fy, ft.rfy);
     double q[3];
@@ -307,7 +313,7 @@ __global__ void k_check_div64(int mode, uint64_t seed, uint64_t count, double a_
 using namespace mqr;
 
 namespace {
-void fill_frame(const float* K, const float* Tcw, const float* Tinv, double sd, ConfFrame& f) {
+void fill_frame(const float* K, const float* Tcw, const float* Tinv, double sd, int H, int W, float dmf, ConfFrame& f) {
     f.fx = (double)K[0];
     f.fy = (double)K[4];
     f.cx = (double)K[2];
@@ -341,8 +347,13 @@ void fill_frame(const float* K, const float* Tcw, const float* Tinv, double sd, 
     dR = std::sqrt(dR) * 1.01 + 1e-12;
     dT = std::sqrt(dT) * 1.01 + 1e-12;
     eR = std::sqrt(eR) * 1.01 + 1e-12;
+    // |Z - zf| vs |Z - zt| (pixel_decide's float32 interpolation): 2^-18 depth_max times the longest
+    // ray |pt| / Z = sqrt(1 + ((u - cx) / fx)^2 + ((v - cy) / fy)^2) over the image (a corner)
+    const double ax = std::max(std::fabs(-f.cx), std::fabs((W - 1) - f.cx)) / std::fabs(f.fx);
+    const double ay = std::max(std::fabs(-f.cy), std::fabs((H - 1) - f.cy)) / std::fabs(f.fy);
+    const double zterm = 0x1p-18 * (double)dmf * std::sqrt(1.0 + ax * ax + ay * ay) * 1.01;
     // sd NaN (no consistent error possible): the band is irrelevant, every pair takes the exact tail
-    const double c1 = dR * (1.0 + eR), c0 = dT * (1.0 + eR) + eR * (sd + 1.0) + 1e-9;
+    const double c1 = dR * (1.0 + eR), c0 = (dT + zterm) * (1.0 + eR) + eR * (sd + 1.0) + 1e-9;
     f.c1 = finite && std::isfinite(c1) ? c1 : INFINITY;
     f.c0 = finite && std::isfinite(c0) ? c0 : INFINITY;
 }
@@ -414,7 +425,7 @@ int mqr_confidence(int device, const float* depths, int depth_loc, int N, int H,
     ConfFrame* fr = cc.hfr;
     MQR_CHECK_HIP(hipStreamSynchronize(s));  // the previous call's upload has finished with hfr
     for (int i = 0; i < N; ++i) {
-        fill_frame(K + 9 * i, T_cw + 16 * i, T_cw_inv + 16 * i, sd, fr[i]);
+        fill_frame(K + 9 * i, T_cw + 16 * i, T_cw_inv + 16 * i, sd, H, W, (float)depth_max, fr[i]);
         fr[i].ok = frame_ok ? (frame_ok[i] ? 1 : 0) : 1;
     }
     ConfFrame* dfr = cc.dfr;
@@ -482,8 +493,8 @@ int mqr_pixel_error_map(int device, const float* ref_depth, const float* tgt_dep
     MQR_CHECK_HIP(hipSetDevice(device));
     const int64_t HW = (int64_t)H * W;
     ConfFrame fr[2] = {};
-    fill_frame(K_ref, T_cw_ref, nullptr, NAN, fr[0]);
-    fill_frame(K_tgt, T_cw_tgt, T_cw_inv_tgt, NAN, fr[1]);
+    fill_frame(K_ref, T_cw_ref, nullptr, NAN, H, W, 0.f, fr[0]);
+    fill_frame(K_tgt, T_cw_tgt, T_cw_inv_tgt, NAN, H, W, 0.f, fr[1]);
     ConfFrame* dfr = nullptr;
     float *dr = nullptr, *dt = nullptr, *de = nullptr;
     MQR_CHECK_HIP(hipMalloc(&dfr, sizeof(fr)));
