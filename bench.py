@@ -4,8 +4,12 @@
 A "step" = integrate the rank's whole 500-frame depth sequence (640x480, procedural room = a
 512^3-voxel volume at 5 mm, R=16, depth_max 4 m, truncation 10 voxels) into an empty volume:
 per 64-frame batch one touch launch (hash insert) + one integrate launch, inputs resident in HBM.
-With N > 1 ranks every rank integrates its own 500 frames of an N*500-frame walk (weak scaling)
-and the step ends with the single RCCL merge of the partial volumes into rank 0.
+With N > 1 ranks the step is BASELINE's C4 (configs[3]): the fixed 2000-frame LEFT+RIGHT capture
+split over the ranks by contiguous frame ranges (strong scaling), each rank integrating its range,
+then the single RCCL exchange (mqr_reduce_rccl, sharded: owned slice + halo per rank); the line
+carries merge_phases_ms, the shards' parity against the oracle's pass over the whole capture, and
+a weak C2-per-rank sub-leg (`weak_c2`).  If RCCL cannot start on every rank the line fails (exit
+1, value null) -- no fallback transport is timed.
 
 Prints ONE JSON line (rank 0): value = frames integrated per second over all ranks, the mesh
 extraction time (weight_threshold 1.5, the pipeline's setting), the integrate kernel's roofline
@@ -65,7 +69,11 @@ def parse():
                          "rank, or the whole volume on rank 0")
     ap.add_argument("--strong", action="store_true",
                     help="C4: a fixed 2000-frame LEFT+RIGHT capture (1000 + 1000, stereo baseline 0.064 m) "
-                         "split over the ranks (strong scaling) instead of 500 frames per rank")
+                         "split over the ranks (strong scaling); the default for --gpus N > 1")
+    ap.add_argument("--weak", action="store_true",
+                    help="N > 1: C2 weak scaling (500 frames per rank) as the headline instead of the C4 split")
+    ap.add_argument("--weak-steps", type=int, default=50,
+                    help="N > 1 (C4 headline): timed steps of the weak C2-per-rank sub-leg (0: skip)")
     ap.add_argument("--strong-frames", type=int, default=1000, help="frames per side in --strong mode")
     ap.add_argument("--no-c5", action="store_true", help="skip the 1-GPU C5 leg (4000 frames @ 3 mm + colour)")
     ap.add_argument("--no-c4", action="store_true", help="skip the 1-GPU C4 leg (1000 + 1000 frames chained)")
@@ -477,13 +485,9 @@ def c4_leg(args, device, frames_per_side=1000, reps=3, parity=True):
     at 1.5 and its point cloud at 3.0 are checked against the oracle's volume of the same frames."""
     import numpy as np
     import torch
-    from mqr import synthetic
     from mqr.vbg import VoxelBlockGrid
     dev = int(device.index or 0)
-    left = synthetic.room_loop_poses(frames_per_side)
-    right = [(R_, t_ + R_[:, 0] * 0.064) for R_, t_ in left]
-    seq = synthetic.make_sequence_fast("room", poses=left + right, height=args.height, width=args.width, seed=4,
-                                       device=f"cuda:{dev}")
+    seq = c4_capture(args, dev, frames_per_side)
     depth = seq["depth_t"].contiguous()
     B, H, W = depth.shape
     K = seq["K"].astype(np.float64)
@@ -808,6 +812,64 @@ def log(msg):
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
+def c4_capture(args, dev, frames_per_side):
+    """BASELINE.json configs[3]'s capture: frames_per_side LEFT + as many RIGHT frames of the room
+    walk (0.064 m stereo baseline), 640x480, in reconstruct_scene.py:64-81's order (all LEFT, then
+    all RIGHT).  Seeded once for the whole capture, so every rank count shards the same frames."""
+    from mqr import synthetic
+    left = synthetic.room_loop_poses(frames_per_side)
+    right = [(R_, t_ + R_[:, 0] * 0.064) for R_, t_ in left]
+    return synthetic.make_sequence_fast("room", poses=left + right, height=args.height, width=args.width, seed=4,
+                                        device=f"cuda:{dev}")
+
+
+def sharded_parity(full_host, K, T, args, owned, meshes):
+    """The C4 shards merged over RCCL against the oracle's single sequential pass over the whole
+    capture (rank 0): the owned slices partition the oracle's block set, weights are identical, tsdf
+    within 1e-4 (the merge sums partial running averages: fp32 rounding differs from the sequential
+    update), and the shard meshes (owned cubes) have the oracle mesh's triangle count; whether the
+    triangle position multisets are also identical is reported (a rounding difference can move a vertex)."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from gpu_helpers import _key_order, mesh_signature
+    ref = oracle_volume(full_host, K, T, args.voxel, args)
+    ok_, ot, ow = ref.export()
+    gk = np.concatenate([o[0] for o in owned])
+    out = {"blocks": int(len(gk)), "oracle_blocks": int(len(ok_))}
+    ga, oa = _key_order(gk), _key_order(ok_)
+    out["keys_equal"] = gk.shape == ok_.shape and bool(np.array_equal(gk[ga], ok_[oa]))
+    if out["keys_equal"]:
+        gt = np.concatenate([o[1] for o in owned])
+        gw = np.concatenate([o[2] for o in owned])
+        weq, err = True, 0.0
+        for c in range(0, len(ga), 4096):
+            i, j = ga[c:c + 4096], oa[c:c + 4096]
+            weq = weq and bool(np.array_equal(gw[i], ow[j]))
+            m = gw[i] > 0
+            if m.any():
+                err = max(err, float(np.abs(gt[i][m] - ot[j][m]).max()))
+        out["weights_equal"], out["max_dtsdf"] = weq, err
+        del gt, gw
+    ov, _, otri = ref.extract_mesh(args.extract_threshold)
+    off, V, Tr = 0, [], []
+    for v, t in meshes:
+        V.append(v)
+        Tr.append(t + off)
+        off += len(v)
+    V, Tr = np.concatenate(V), np.concatenate(Tr)
+    out["mesh_threshold"] = args.extract_threshold
+    out["triangles"] = int(len(Tr))
+    out["triangle_count_equal"] = len(Tr) == len(otri)
+    if out["triangle_count_equal"]:
+        out["triangle_positions_equal"] = bool(np.array_equal(mesh_signature(V, Tr)[1], mesh_signature(ov, otri)[1]))
+    out["tolerance"] = 1e-4
+    out["comparison"] = ("owned slices of the RCCL-merged shards vs the oracle's sequential pass over all frames: "
+                         "keys/weights exact, tsdf within tolerance, triangle count exact")
+    out["all_ok"] = bool(out.get("keys_equal") and out.get("weights_equal") and out.get("max_dtsdf", 1) <= 1e-4
+                         and out["triangle_count_equal"])
+    return out
+
+
 def main():
     args = parse()
     rank = int(os.environ.get("RANK", 0))
@@ -815,7 +877,7 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", 0))
     import numpy as np
     import torch
-    if os.environ.get("MQR_BENCH_WRAP_DEVICES"):  # rehearsal on fewer GPUs than ranks
+    if os.environ.get("MQR_BENCH_WRAP_DEVICES"):  # rehearsal on fewer GPUs than ranks (gloo-staged merge)
         local %= torch.cuda.device_count()
     torch.cuda.set_device(local)
     dist = comm = None
@@ -824,22 +886,34 @@ def main():
         # RCCL inside libmqr_hip.so (mqr_reduce_rccl)
         import torch.distributed as dist
         dist.init_process_group("gloo")
+    # N > 1 measures BASELINE's C4 (a fixed 2000-frame L+R capture split over the ranks) unless --weak
+    strong = args.strong or (world > 1 and not args.weak)
 
     from mqr import synthetic
-    from mqr.distributed import make_comm, merge_rccl, shard_range
+    from mqr.distributed import make_comm, merge_rccl, merge_staged, shard_range
     from mqr.vbg import VoxelBlockGrid
 
-    if args.strong:
+    full_host = K_full = T_full = None
+    if strong:
         # C4: LEFT then RIGHT (reconstruct_scene.py:64-81 order), contiguous frame ranges per rank
-        left = synthetic.room_loop_poses(args.strong_frames)
-        right = [(R_, t_ + R_[:, 0] * 0.064) for R_, t_ in left]
+        full = c4_capture(args, local, args.strong_frames)
         lo, hi = shard_range(2 * args.strong_frames, rank, world)
-        poses = (left + right)[lo:hi]
+        if world == 1:
+            seq = full
+        else:
+            seq = {k: (v[lo:hi] if k in ("depth_t", "raw_t", "K", "T_wc", "T_cw") else v) for k, v in full.items()
+                   if k != "unity"}
+            seq["depth_t"] = seq["depth_t"].clone()
+            if rank == 0 and not (args.no_cpu or args.no_parity):
+                full_host = full["depth_t"].cpu().numpy()
+                K_full, T_full = full["K"].astype(np.float64), full["T_wc"].astype(np.float64)
+            del full
+            torch.cuda.empty_cache()
     else:
         # this rank's frames of an N*frames closed walk through the room (weak scaling)
         poses = synthetic.room_loop_poses(args.frames * world)[rank * args.frames:(rank + 1) * args.frames]
-    seq = synthetic.make_sequence_fast("room", poses=poses, height=args.height, width=args.width, seed=rank,
-                                       device=f"cuda:{local}")
+        seq = synthetic.make_sequence_fast("room", poses=poses, height=args.height, width=args.width, seed=rank,
+                                           device=f"cuda:{local}")
     depth_t = seq["depth_t"].contiguous()
     B, H, W = depth_t.shape
     K = seq["K"].astype(np.float64)
@@ -854,10 +928,10 @@ def main():
     merge_phases = []
     shard = {"out": None, "owned": 0}
     transport = None
-    if world > 1:
-        # RCCL inside libmqr; if it cannot start on every rank (the decision is agreed over gloo), the
-        # merge falls back to mqr.distributed.merge_to_root over the gloo group -- slower, but the
-        # scaling run still measures something, and the JSON says which transport ran
+    staged = bool(os.environ.get("MQR_BENCH_WRAP_DEVICES")) and world > torch.cuda.device_count()
+    if world > 1 and not staged:
+        # RCCL inside libmqr.  If it cannot start on every rank (agreed over gloo) the line fails:
+        # no value is printed for a run whose merge would not be the one measured.
         err = None
         try:
             comm = make_comm(local)
@@ -865,34 +939,42 @@ def main():
             comm, err = None, f"{type(e).__name__}: {e}"
         ok = torch.tensor([0 if comm is None else 1], dtype=torch.int32)
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-        if not int(ok.item()) and comm is not None:
-            comm.close()
-            comm = None
-        transport = "rccl (mqr_reduce_rccl)" if comm is not None else f"gloo fallback (merge_to_root): {err}"
+        if not int(ok.item()):
+            if comm is not None:
+                comm.close()
+            if rank == 0:
+                print(json.dumps({"metric": METRIC, "value": None, "unit": "frames/s", "n_gpus": world,
+                                  "merge_transport": f"RCCL failed to start on at least one rank: {err or 'peer'}",
+                                  "error": "no measurement: the RCCL merge could not run"}), flush=True)
+            dist.destroy_process_group()
+            sys.exit(1)
+        transport = "rccl (mqr_reduce_rccl)"
+    elif staged:
+        transport = "gloo-staged (mqr_xchg_*, rehearsal with several ranks per GPU; not a scaling measurement)"
+    if world > 1:
         log(f"rank {rank}: merge transport {transport}")
         shard["out"] = VoxelBlockGrid(voxel_size=args.voxel, block_resolution=args.block_resolution,
                                       block_count=args.block_count, device=local)
 
-    def step_integrate():
+    def merge():
+        t = time.perf_counter()
+        if comm is not None:
+            shard["out"], shard["owned"] = merge_rccl(vbg, comm, mode=args.merge, out=shard["out"])
+            merge_phases.append(comm.timing())
+        else:
+            shard["out"], shard["owned"] = merge_staged(vbg, mode=args.merge, out=shard["out"])
+        torch.cuda.synchronize()
+        merge_times.append(time.perf_counter() - t)
+
+    def step():
         vbg.reset()
         vbg.integrate_frames(dptr, K, T, depth_scale=1.0, depth_max=args.depth_max,
                              trunc_voxel_multiplier=args.trunc)
-
-    def step():
-        step_integrate()
         if world > 1:
-            t = time.perf_counter()
-            if comm is not None:
-                shard["out"], shard["owned"] = merge_rccl(vbg, comm, mode=args.merge, out=shard["out"])
-                merge_phases.append(comm.timing())
-            else:
-                from mqr.distributed import merge_to_root
-                merge_to_root(vbg, root=0)
-                shard["out"], shard["owned"] = vbg, (vbg.size() if rank == 0 else 0)
-            torch.cuda.synchronize()
-            merge_times.append(time.perf_counter() - t)
+            merge()
 
-    log(f"rank {rank}: {B} frames {H}x{W} generated; warm-up {args.warmup} steps")
+    log(f"rank {rank}: {B} frames {H}x{W} generated ({'C4 strong split' if strong else 'C2 per rank'}); "
+        f"warm-up {args.warmup} steps")
     for _ in range(args.warmup):
         step()
     merge_times.clear()
@@ -916,11 +998,14 @@ def main():
         e = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
+    merge_ms = (sum(merge_times) / len(merge_times) * 1e3) if merge_times else None
+    merge_phases_ms = ({k: sum(p[k] for p in merge_phases) / len(merge_phases) for k in merge_phases[0]}
+                       if merge_phases else None)
 
     blocks = vbg.size()
     R3_ = args.block_resolution ** 3
     ext_ms, (nv, nt) = (None, (0, 0))
-    sharded = None
+    sharded = sharded_par = weak_leg = None
     if world > 1:
         # every rank extracts its owned cubes (mqr_extract_mesh_owned); the mesh is the concatenation
         from mqr.distributed import extract_mesh_owned
@@ -939,6 +1024,54 @@ def main():
                            "included); triangles add up to the single-volume mesh"}
         blocks = sharded["union_blocks"]
         nv, nt = sharded["vertices_with_boundary_copies"], sharded["triangles"]
+        if strong and args.merge == "sharded" and not (args.no_cpu or args.no_parity):
+            # the last timed step's merged shards against the oracle's pass over the whole capture
+            k_, t_, w_ = shard["out"].export()
+            n_ = shard["owned"]
+            gathered = [None] * world if rank == 0 else None
+            dist.gather_object(((k_[:n_], t_[:n_], w_[:n_]), (m.vertices, m.triangles)), gathered, dst=0)
+            del k_, t_, w_
+            if rank == 0:
+                log("C4 sharded parity: oracle pass over the whole capture")
+                sharded_par = sharded_parity(full_host, K_full, T_full, args, [g[0] for g in gathered],
+                                             [g[1] for g in gathered])
+            del gathered
+            dist.barrier()
+        if strong and args.weak_steps > 0:
+            # sub-leg: C2 weak scaling (500 frames per rank of an N*500-frame walk), same merge
+            poses = synthetic.room_loop_poses(args.frames * world)[rank * args.frames:(rank + 1) * args.frames]
+            wseq = synthetic.make_sequence_fast("room", poses=poses, height=args.height, width=args.width,
+                                                seed=rank, device=f"cuda:{local}")
+            wd = wseq["depth_t"].contiguous()
+            wK, wT = wseq["K"].astype(np.float64), wseq["T_wc"].astype(np.float64)
+            wptr = (_DevPtr(wd.data_ptr()), wd.shape[0], H, W)
+
+            def wstep():
+                vbg.reset()
+                vbg.integrate_frames(wptr, wK, wT, depth_scale=1.0, depth_max=args.depth_max,
+                                     trunc_voxel_multiplier=args.trunc)
+                merge()
+
+            for _ in range(args.warmup):
+                wstep()
+            merge_times.clear()
+            dist.barrier()
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            for _ in range(args.weak_steps):
+                wstep()
+            torch.cuda.synchronize()
+            dist.barrier()
+            we = torch.tensor([time.perf_counter() - t1], dtype=torch.float64)
+            dist.all_reduce(we, op=dist.ReduceOp.MAX)
+            we = float(we.item())
+            weak_leg = {"workload": "C2 per rank (weak): 500 frames per GPU of an N*500-frame room walk + merge",
+                        "frames_per_gpu": int(wd.shape[0]), "steps": args.weak_steps,
+                        "value": wd.shape[0] * world * args.weak_steps / we, "unit": "frames/s",
+                        "ms_per_step": we / args.weak_steps * 1e3,
+                        "merge_ms": sum(merge_times) / len(merge_times) * 1e3, "union_blocks": shard["out"].size()
+                        if args.merge == "root" else None}
+            del wd, wseq
     elif rank == 0:
         ext_ms, (nv, nt) = extract_ms(vbg, args.extract_threshold, args.extract_reps)
 
@@ -959,6 +1092,8 @@ def main():
             log("parity check of the timed volume")
             parity = parity_check(vbg, ref_vol, args.extract_threshold, points_thr=3.0)
         del ref_vol
+    elif world > 1:
+        parity = sharded_par
 
     extras = {}
     if rank == 0 and world == 1 and not args.no_extras:
@@ -970,7 +1105,7 @@ def main():
         extras["raycast"] = raycast_leg(vbg, K, T, H, W, args.extract_threshold)
         extras["meshfilter"] = meshfilter_leg(vbg, args.extract_threshold)
         extras["c3"] = c3_leg(seq, vbg, args, dev)
-        if not args.strong and not args.no_c4:
+        if not strong and not args.no_c4:
             log("C4 leg (1000 + 1000 frames chained, parity)")
             extras["c4"] = c4_leg(args, dev, parity=not (args.no_cpu or args.no_parity))
         if not args.no_c5:
@@ -999,7 +1134,10 @@ def main():
     traffic, traffic_src = pmc_traffic(H, W, B)
 
     if rank == 0:
-        total_frames = (2 * args.strong_frames if args.strong else B * world) * args.steps
+        total_frames = (2 * args.strong_frames if strong else B * world) * args.steps
+        c4_name = ("C4 (SURVEY.md §8(d); BASELINE.json configs[3]): 2000-frame LEFT+RIGHT capture (1000 + 1000) "
+                   f"split over {world} GPU(s) by contiguous frame ranges, 640x480, 5 mm voxels, R=16, depth_max 4 m, "
+                   "trunc 10" + (f", merged over {transport} ({args.merge})" if world > 1 else ""))
         out = {
             "metric": METRIC,
             "value": total_frames / elapsed,
@@ -1009,27 +1147,24 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "strong" if args.strong else "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (procedural room, GPU ray-cast, sigma=0.002z noise + 1% dropout)",
-            "config": {"workload": ("C4 (SURVEY.md §8(d); BASELINE.json configs[3]): 2000-frame LEFT+RIGHT capture "
-                                    "split over the GPUs, 640x480, 5 mm voxels, R=16, depth_max 4 m, trunc 10, merged "
-                                    "over RCCL") if args.strong else
+            "config": {"workload": c4_name if strong else
                                    ("C2 (SURVEY.md §8(d); BASELINE.json configs[1]): 500-frame LEFT depth sequence "
                                     "per GPU, 640x480, hashed TSDF 5 mm voxels, 512^3 effective volume, R=16, "
                                     "depth_max 4 m, trunc 10"),
                        "frames_per_gpu": B, "height": H, "width": W, "voxel_size": args.voxel,
                        "block_resolution": args.block_resolution, "depth_max": args.depth_max,
                        "trunc_voxel_multiplier": args.trunc, "frame_batch": 64,
-                       "parallelism": f"frame-shard x{world}" + (
-                           (f" + libmqr RCCL merge ({args.merge})" if transport and transport.startswith("rccl")
-                            else " + gloo merge to rank 0 (fallback)") if world > 1 else "")},
+                       "parallelism": f"frame-shard x{world}" + (f" + libmqr merge ({args.merge}, {transport})"
+                                                                 if world > 1 else "")},
             "sharded_extract": sharded,
-            "merge_ms": (sum(merge_times) / len(merge_times) * 1e3) if merge_times else None,
-            "merge_phases_ms": ({k: sum(p[k] for p in merge_phases) / len(merge_phases) for k in merge_phases[0]}
-                                if merge_phases else None),
+            "merge_ms": merge_ms,
+            "merge_phases_ms": merge_phases_ms,
             "merge_transport": transport,
+            "weak_c2": weak_leg,
             "union_blocks": blocks if world > 1 else None,
             "extract_ms": ext_ms,
             "extract": {"weight_threshold": args.extract_threshold, "vertices": nv, "triangles": nt,

@@ -102,10 +102,23 @@ int mqr_vbg_unpack_weighted(mqr_vbg* v, const int32_t* union_keys, int64_t U, co
  * device; the host reads only block counts and list lengths.
  * mqr_comm_timing: the last merge's phases in ms -- [0] count + key all-gathers and the plan,
  * [1] output volume + gather of the outgoing blocks, [2] the RCCL exchange, [3] the merge kernels.
- * mqr_merge_local: the same plan and arithmetic for n volumes of one process on one device (the
- * merge reads each source's pool directly instead of receiving over RCCL; tests and timing).
- * mqr_merge_local_timing: the last mqr_merge_local's wall time per destination in ms (its plan,
- * output volume and merge kernels: one rank's share of a merge, without the transfer). */
+ * mqr_merge_local: the same exchange for n volumes of one process on one device, with device copies
+ * as the transport: every rank builds its own plan, packs its own send segments and merges its
+ * receive segments in rank order exactly as mqr_reduce_rccl does on that rank; before a byte moves,
+ * each sender's segment for d is checked against d's receive segment from it (length, and the
+ * source buffers both sides list, entry for entry; mismatch = status 4).  Tests and timing.
+ * mqr_merge_local_timing: the last mqr_merge_local's wall time per rank in ms (its plan, output
+ * volume, send-segment gather and merge kernels: one rank's share of a merge, without the transfer).
+ *
+ * mqr_xchg_*: the same exchange with the transport left to the caller (one process per rank; the
+ * tests carry the segments over gloo through host buffers).  gathered_keys: world*mx packed block
+ * keys (rank r's keys in buffer order at r*mx, padded with 0xFFFF...FF; packing as the int32 keys
+ * of mqr_vbg_export: ((x+2^20)<<42)|((y+2^20)<<21)|(z+2^20)).  create = plan + output volume
+ * (emptied) + send segments (+ the self segment in place); counts[world] = blocks per send segment
+ * (to each peer) and per receive segment (from each peer), floats_per_block = 2*R^3 ((tsdf,
+ * weight) interleaved); send_segment copies the segment for `peer` out, recv_segment copies the
+ * segment from `peer` in (peer != rank); finish merges in rank order.  `out` must outlive the
+ * handle. */
 #define MQR_MERGE_ROOT 0
 #define MQR_MERGE_SHARDED 1
 int mqr_comm_unique_id(uint8_t* id_out /* 128 bytes */);
@@ -115,6 +128,15 @@ int mqr_reduce_rccl(mqr_vbg* local, mqr_comm* comm, int mode, int root, mqr_vbg*
 int mqr_merge_local(mqr_vbg** locals, int n, int mode, int root, mqr_vbg** outs, int64_t* n_owned);
 int mqr_comm_timing(mqr_comm* comm, float* ms4);
 int mqr_merge_local_timing(float* ms, int n);
+typedef struct mqr_xchg mqr_xchg;
+int mqr_xchg_create(mqr_vbg* local, int world, int rank, int mode, int root, const uint64_t* gathered_keys,
+                    int64_t mx, int keys_loc, mqr_vbg* out, mqr_xchg** h);
+int mqr_xchg_counts(mqr_xchg* h, int64_t* send_blocks, int64_t* recv_blocks, int64_t* n_owned,
+                    int64_t* floats_per_block);
+int mqr_xchg_send_segment(mqr_xchg* h, int peer, float* dst, int loc);
+int mqr_xchg_recv_segment(mqr_xchg* h, int peer, const float* src, int loc);
+int mqr_xchg_finish(mqr_xchg* h, int64_t* n_owned);
+int mqr_xchg_destroy(mqr_xchg* h);
 
 /* vbg.extract_point_cloud(weight_threshold=3.0)   -- reconstruct_scene.py:90, refine_fragment_poses.py:39
  * vbg.extract_triangle_mesh(weight_threshold)       -- reconstruct_scene.py:105-108, 186-189 */

@@ -211,7 +211,10 @@ __device__ inline int pixel_decide(const float* __restrict__ tgt, int W, double 
     for (int i = 0; i < 3; ++i)
         q[i] = ft.Tcw[i * 4 + 0] * xt + ft.Tcw[i * 4 + 1] * yt + ft.Tcw[i * 4 + 2] * ztd + ft.Tcw[i * 4 + 3];
     const double ex = pw[0] - q[0], ey = pw[1] - q[1], ez = pw[2] - q[2];
-    return ex * ex + ey * ey + ez * ez <= d2_max ? 1 : 2;
+    const double d2 = ex * ex + ey * ey + ez * ez;
+    // a NaN error is not valid (valid_count += ~isnan(error_map), estimate_depth_confidences.py:66)
+    if (d2 != d2) return 0;
+    return d2 <= d2_max ? 1 : 2;
 }
 
 // depth_to_pointcloud_numpy for one pixel: returns 0 when the ref pixel is not in (0, depth_max].

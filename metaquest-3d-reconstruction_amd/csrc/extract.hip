@@ -848,7 +848,9 @@ __global__ __launch_bounds__(NT) void k_mc_emit(const int32_t* __restrict__ nb, 
     if (nvb == 0 && ntb == 0) return;  // block-uniform: nothing to write
     const int32_t vb0 = voff[b], tb0 = toff[b];
     // outputs past the speculative capacity: the host re-runs this pass into exact buffers
-    if ((int64_t)vb0 + nvb > cap_v || (int64_t)tb0 + ntb > cap_t) return;
+    // (int32 offsets: a total past 2^31 wraps them negative -- the host then fails the call after
+    // this speculative pass, which must not have written before the buffers' start)
+    if (vb0 < 0 || tb0 < 0 || (int64_t)vb0 + nvb > cap_v || (int64_t)tb0 + ntb > cap_t) return;
     const int tid = threadIdx.x;
     if (tid < 256) triP[tid] = mqr_tri_packed[tid];
     if (tid < 32) triC[tid] = mqr_tri_count_packed[tid];
@@ -940,7 +942,8 @@ __global__ __launch_bounds__(kMcThreads) void k_pt_emit(const int32_t* __restric
     const int64_t b = blockIdx.x;
     const int npb = count[b];
     if (npb == 0) return;  // block-uniform
-    if ((int64_t)off[b] + npb > cap) return;  // past the speculative capacity (the host re-runs)
+    if (off[b] < 0 || (int64_t)off[b] + npb > cap) return;  // past the speculative capacity (or a wrapped int32
+                                                           // offset): the host re-runs / fails the call
     const int tid = threadIdx.x;
     if (tid < 27) nbrow[tid] = nb[b * 27 + tid];
     for (int r = tid; r < M::R2; r += blockDim.x) rows[r] = rows4[b * M::R2 + r];

@@ -23,6 +23,14 @@
 //   entry), so a sender's segment for d and d's segment from that sender list the same blocks in
 //   the same (union) order.  The host reads two small count arrays per merge (block counts after
 //   the first all-gather, list lengths after the plan); nothing else leaves the device.
+//
+// Transports.  One rank's side of the exchange (plan, output volume, send segments, rank-ordered
+// merge of the receive segments) is `Exchange`; three transports move its segments:
+//   mqr_reduce_rccl   ncclSend / ncclRecv between processes (one per GPU);
+//   mqr_merge_local   device copies between the n volumes of one process (every rank still builds
+//                     its OWN plan and packs its OWN send segments; the pair lists are checked);
+//   mqr_xchg_*        the caller (host buffers over gloo, one process per rank, any device).
+// Only the ncclSend / ncclRecv call differs between them.
 #include <dlfcn.h>
 #include <rccl/rccl.h>
 
@@ -32,6 +40,7 @@
 #include <chrono>
 #include <climits>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <vector>
 
@@ -112,18 +121,17 @@ struct PlanScratch {
 };
 }  // namespace mqr
 
+namespace mqr {
+struct Exchange;
+}
+
 struct mqr_comm {
     int device = 0, rank = 0, world = 1;
     ncclComm_t nc = nullptr;
     hipStream_t s = nullptr;
-    // grow-only exchange buffers
-    void* sendbuf = nullptr;
-    size_t send_cap = 0;
-    void* recvbuf = nullptr;
-    size_t recv_cap = 0;
     void* small = nullptr;  // counts, padded keys
     size_t small_cap = 0;
-    mqr::PlanScratch plan;
+    mqr::Exchange* x = nullptr;  // plan, send / receive buffers (grow-only, reused across merges)
     // phase timing of the last merge (mqr_comm_timing): start, plan done, gathered, exchanged, merged
     hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
     float last_ms[4] = {0.f, 0.f, 0.f, 0.f};
@@ -153,26 +161,6 @@ __global__ void k_merge_blocks(const int32_t* __restrict__ dst, int64_t n, const
     float2* out = pool + (int64_t)dst[j] * R3;
     for (int p = threadIdx.x; p < R3; p += blockDim.x) {
         const float2 a = out[p], b = src[p];
-        if (b.y == 0.f) continue;
-        if (a.y == 0.f) {
-            out[p] = b;
-        } else {
-            const float w = a.y + b.y;
-            out[p] = make_float2((a.y * a.x + b.y * b.x) / w, w);
-        }
-    }
-}
-
-// Merge received entries straight from a source volume's pool (the one-process twin): entry j takes
-// source buffer src[j] into destination buffer dst[j], same arithmetic as k_merge_blocks.
-__global__ void k_merge_direct(const int32_t* __restrict__ src, const int32_t* __restrict__ dst, int64_t n,
-                               const float2* __restrict__ spool, int R3, float2* __restrict__ pool) {
-    const int64_t j = blockIdx.x;
-    if (j >= n) return;
-    const float2* in = spool + (int64_t)src[j] * R3;
-    float2* out = pool + (int64_t)dst[j] * R3;
-    for (int p = threadIdx.x; p < R3; p += blockDim.x) {
-        const float2 a = out[p], b = in[p];
         if (b.y == 0.f) continue;
         if (a.y == 0.f) {
             out[p] = b;
@@ -493,7 +481,115 @@ static int prepare_out(mqr_vbg* out, const uint64_t* dk, int64_t n) {
     return n > 0 ? activate_ordered(out, dk, n) : 0;
 }
 
+// One rank's side of the exchange, whatever carries the bytes (RCCL, device copies between the
+// volumes of one process, or host buffers over gloo): its plan, its output volume, the send
+// buffer (segments by destination, packed from the local pool by k_gather_blocks) and the receive
+// buffer (segments by source, merged in rank order by k_merge_blocks).  The segment accessors are
+// the ONLY description of what a transport moves: mqr_reduce_rccl hands them to ncclSend /
+// ncclRecv, mqr_merge_local to hipMemcpyAsync, mqr_xchg_* to the caller.
+struct Exchange {
+    PlanScratch plan;
+    PlanView pv;
+    PlanSummary H{};
+    int W = 1, me = 0, R3 = 0;
+    std::vector<size_t> soff, roff;  // block offsets of the segments
+    void* sendbuf = nullptr;
+    size_t send_cap = 0;
+    void* recvbuf = nullptr;
+    size_t recv_cap = 0;
+    Exchange() = default;
+    Exchange(const Exchange&) = delete;
+    Exchange& operator=(const Exchange&) = delete;
+    ~Exchange() {
+        if (sendbuf) (void)hipFree(sendbuf);
+        if (recvbuf) (void)hipFree(recvbuf);
+    }
+    size_t send_blocks(int d) const { return soff[d + 1] - soff[d]; }
+    size_t recv_blocks(int s) const { return roff[s + 1] - roff[s]; }
+    float2* send_seg(int d) const { return static_cast<float2*>(sendbuf) + soff[d] * R3; }
+    float2* recv_seg(int s) const { return static_cast<float2*>(recvbuf) + roff[s] * R3; }
+    size_t seg_floats(size_t blocks) const { return blocks * (size_t)R3 * 2; }
+};
+
+// Plan (identical on every rank) from the gathered keys dkeys[W * mx] (device), output volume,
+// send segments gathered from `local`, and the self segment copied into the receive buffer.
+// ev_plan / ev_gathered (nullable) are recorded after the plan and after the gather.
+static int xchg_prepare(Exchange& x, hipStream_t st, const uint64_t* dkeys, int W, int64_t mx, int me, int mode,
+                        int root, mqr_vbg* local, mqr_vbg* out, hipEvent_t ev_plan, hipEvent_t ev_gathered) {
+    x.W = W;
+    x.me = me;
+    x.R3 = (int)local->R3;
+    if (device_plan(x.plan, st, dkeys, W, mx, me, mode, root, x.pv)) return 1;
+    if (ev_plan) MQR_CHECK_HIP(hipEventRecord(ev_plan, st));
+    x.H = *x.pv.H;
+    x.soff.assign(W + 1, 0);
+    x.roff.assign(W + 1, 0);
+    for (int r = 0; r < W; ++r) {
+        x.soff[r + 1] = x.soff[r] + (size_t)x.H.cnt[0][r];
+        x.roff[r + 1] = x.roff[r] + (size_t)x.H.cnt[1][r];
+    }
+    const size_t ns = x.soff[W], nr = x.roff[W];
+    const size_t eb = sizeof(float2) * (size_t)x.R3;
+    if (prepare_out(out, x.pv.out_keys, x.H.n_out)) return 1;  // synchronous (out's stream)
+    if (grow(&x.sendbuf, &x.send_cap, std::max<size_t>(ns, 1) * eb) ||
+        grow(&x.recvbuf, &x.recv_cap, std::max<size_t>(nr, 1) * eb))
+        return 1;
+    if (ns)
+        hipLaunchKernelGGL(k_gather_blocks, dim3((unsigned)ns), dim3(256), 0, st, x.pv.send_idx, (int64_t)ns,
+                           local->pool, x.R3, static_cast<float2*>(x.sendbuf));
+    MQR_CHECK_HIP(hipGetLastError());
+    if (ev_gathered) MQR_CHECK_HIP(hipEventRecord(ev_gathered, st));
+    MQR_REQUIRE(x.send_blocks(me) == x.recv_blocks(me), "merge plan: self segment lengths differ");
+    if (x.send_blocks(me))
+        MQR_CHECK_HIP(hipMemcpyAsync(x.recv_seg(me), x.send_seg(me), eb * x.send_blocks(me), hipMemcpyDeviceToDevice,
+                                     st));
+    return 0;
+}
+
+// Received segments into the output volume, source by source in rank order (deterministic sums).
+static int xchg_merge(Exchange& x, hipStream_t st, mqr_vbg* out) {
+    for (int src = 0; src < x.W; ++src)
+        if (x.recv_blocks(src))
+            hipLaunchKernelGGL(k_merge_blocks, dim3((unsigned)x.recv_blocks(src)), dim3(256), 0, st,
+                               x.pv.recv_dst + x.roff[src], (int64_t)x.recv_blocks(src), x.recv_seg(src), x.R3,
+                               out->pool);
+    MQR_CHECK_HIP(hipGetLastError());
+    return 0;
+}
+
+// Every exit of an exchange waits for its stream first: async copies read host memory of the
+// call (counts, the pinned plan summary) and a failing rank must not leave kernels in flight.
+struct StreamDrain {
+    hipStream_t s;
+    ~StreamDrain() { (void)hipStreamSynchronize(s); }
+};
+// A stream the call created: drained, then destroyed (one guard, so the order cannot invert).
+struct OwnedStream {
+    hipStream_t s = nullptr;
+    ~OwnedStream() {
+        if (s) {
+            (void)hipStreamSynchronize(s);
+            (void)hipStreamDestroy(s);
+        }
+    }
+};
+
 }  // namespace mqr
+
+// Split-phase exchange with a caller-carried transport (the gloo / host-staged twin of
+// mqr_reduce_rccl, one process per rank): the same plan, segments and merge.
+struct mqr_xchg {
+    int device = 0, world = 1, rank = 0;
+    mqr_vbg* out = nullptr;
+    mqr::OwnedStream st;
+    mqr::Exchange x;
+    void* dkeys = nullptr;
+    bool finished = false;
+    ~mqr_xchg() {
+        if (st.s) (void)hipStreamSynchronize(st.s);
+        if (dkeys) (void)hipFree(dkeys);
+    }
+};
 
 using namespace mqr;
 
@@ -520,12 +616,14 @@ int mqr_comm_init(int device, int rank, int world, const uint8_t* id, mqr_comm**
     c->device = device;
     c->rank = rank;
     c->world = world;
+    c->x = new Exchange();
     ncclUniqueId uid;
     std::memcpy(uid.internal, id, NCCL_UNIQUE_ID_BYTES);
     ncclResult_t r = api->CommInitRank(&c->nc, world, uid, rank);
     if (r != ncclSuccess) {
         set_error(std::string("ncclCommInitRank: ") + api->GetErrorString(r));
-        delete c;
+        c->nc = nullptr;
+        mqr_comm_destroy(c);
         return 1;
     }
     bool ok = hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking) == hipSuccess;
@@ -545,8 +643,7 @@ int mqr_comm_destroy(mqr_comm* c) {
     if (c->s) (void)hipStreamSynchronize(c->s);
     RcclApi* api = rccl();
     if (api && c->nc) api->CommDestroy(c->nc);
-    if (c->sendbuf) (void)hipFree(c->sendbuf);
-    if (c->recvbuf) (void)hipFree(c->recvbuf);
+    delete c->x;
     if (c->small) (void)hipFree(c->small);
     for (hipEvent_t e : c->ev)
         if (e) (void)hipEventDestroy(e);
@@ -561,15 +658,6 @@ int mqr_comm_timing(mqr_comm* c, float* ms4) {
     return 0;
 }
 
-namespace {
-// Every exit of mqr_reduce_rccl waits for its stream first: async copies read host memory of the
-// call (counts, the pinned plan summary) and a failing rank must not leave kernels in flight.
-struct StreamDrain {
-    hipStream_t s;
-    ~StreamDrain() { (void)hipStreamSynchronize(s); }
-};
-}  // namespace
-
 int mqr_reduce_rccl(mqr_vbg* local, mqr_comm* c, int mode, int root, mqr_vbg* out, int64_t* n_owned) {
     MQR_REQUIRE(local && c && out && n_owned, "null argument");
     MQR_REQUIRE(local != out, "mqr_reduce_rccl: `out` must be a different volume than `local` (it is emptied first)");
@@ -582,8 +670,6 @@ int mqr_reduce_rccl(mqr_vbg* local, mqr_comm* c, int mode, int root, mqr_vbg* ou
     MQR_CHECK_HIP(hipSetDevice(c->device));
     *n_owned = 0;
     const int W = c->world, me = c->rank;
-    const int R3 = (int)local->R3;
-    const size_t eb = sizeof(float2) * R3;
     // host state the stream's async copies read: declared before the drain guard, so it outlives it
     int64_t n_me = 0;
     std::vector<int64_t> cnt(W);
@@ -606,40 +692,18 @@ int mqr_reduce_rccl(mqr_vbg* local, mqr_comm* c, int mode, int root, mqr_vbg* ou
     if (n_me)
         MQR_CHECK_HIP(hipMemcpyAsync(dmine, local->bkeys, sizeof(uint64_t) * n_me, hipMemcpyDeviceToDevice, c->s));
     MQR_CHECK_NCCL(api, api->AllGather(dmine, dkeys, mx, ncclUint64, c->nc, c->s));
-    // 2. the plan on the device (identical on every rank); the host reads the list lengths
-    PlanView pv;
-    if (device_plan(c->plan, c->s, dkeys, W, mx, me, mode, root, pv)) return 1;
-    MQR_CHECK_HIP(hipEventRecord(c->ev[1], c->s));
-    const PlanSummary H = *pv.H;
-    std::vector<size_t> soff(W + 1, 0), roff(W + 1, 0);
-    for (int r = 0; r < W; ++r) {
-        soff[r + 1] = soff[r] + (size_t)H.cnt[0][r];
-        roff[r + 1] = roff[r] + (size_t)H.cnt[1][r];
-    }
-    const size_t ns = soff[W], nr = roff[W];
-    if (prepare_out(out, pv.out_keys, H.n_out)) return 1;  // synchronous (out's stream)
-    // 3. gather my outgoing blocks (segments by destination), post the sparse all-to-all
-    if (grow(&c->sendbuf, &c->send_cap, std::max<size_t>(ns, 1) * eb) ||
-        grow(&c->recvbuf, &c->recv_cap, std::max<size_t>(nr, 1) * eb))
-        return 1;
-    float2* sb = static_cast<float2*>(c->sendbuf);
-    float2* rb = static_cast<float2*>(c->recvbuf);
-    if (ns)
-        hipLaunchKernelGGL(k_gather_blocks, dim3((unsigned)ns), dim3(256), 0, c->s, pv.send_idx, (int64_t)ns,
-                           local->pool, R3, sb);
-    MQR_CHECK_HIP(hipGetLastError());
-    MQR_CHECK_HIP(hipEventRecord(c->ev[2], c->s));
-    const size_t nself = soff[me + 1] - soff[me];
-    if (nself)
-        MQR_CHECK_HIP(hipMemcpyAsync(rb + roff[me] * R3, sb + soff[me] * R3, eb * nself, hipMemcpyDeviceToDevice, c->s));
+    // 2. plan (on the device, identical on every rank), output volume, send segments
+    Exchange& x = *c->x;
+    if (xchg_prepare(x, c->s, dkeys, W, mx, me, mode, root, local, out, c->ev[1], c->ev[2])) return 1;
+    // 3. the sparse all-to-all: segment for p -> p, segment from p <- p (the self segment is local)
     {
         ncclResult_t r = api->GroupStart();
         for (int p = 0; p < W && r == ncclSuccess; ++p) {
             if (p == me) continue;
-            if (soff[p + 1] > soff[p])
-                r = api->Send(sb + soff[p] * R3, (soff[p + 1] - soff[p]) * R3 * 2, ncclFloat32, p, c->nc, c->s);
-            if (r == ncclSuccess && roff[p + 1] > roff[p])
-                r = api->Recv(rb + roff[p] * R3, (roff[p + 1] - roff[p]) * R3 * 2, ncclFloat32, p, c->nc, c->s);
+            if (x.send_blocks(p))
+                r = api->Send(x.send_seg(p), x.seg_floats(x.send_blocks(p)), ncclFloat32, p, c->nc, c->s);
+            if (r == ncclSuccess && x.recv_blocks(p))
+                r = api->Recv(x.recv_seg(p), x.seg_floats(x.recv_blocks(p)), ncclFloat32, p, c->nc, c->s);
         }
         const ncclResult_t r2 = api->GroupEnd();
         if (r != ncclSuccess || r2 != ncclSuccess) {
@@ -648,13 +712,8 @@ int mqr_reduce_rccl(mqr_vbg* local, mqr_comm* c, int mode, int root, mqr_vbg* ou
         }
     }
     MQR_CHECK_HIP(hipEventRecord(c->ev[3], c->s));
-    // 4. merge the received entries source by source (rank order)
-    for (int src = 0; src < W; ++src)
-        if (roff[src + 1] > roff[src])
-            hipLaunchKernelGGL(k_merge_blocks, dim3((unsigned)(roff[src + 1] - roff[src])), dim3(256), 0, c->s,
-                               pv.recv_dst + roff[src], (int64_t)(roff[src + 1] - roff[src]), rb + roff[src] * R3, R3,
-                               out->pool);
-    MQR_CHECK_HIP(hipGetLastError());
+    // 4. merge the received segments source by source (rank order)
+    if (xchg_merge(x, c->s, out)) return 1;
     MQR_CHECK_HIP(hipEventRecord(c->ev[4], c->s));
     if (hipStreamSynchronize(c->s) != hipSuccess) {
         set_error("mqr_reduce_rccl: merge kernels failed");
@@ -662,7 +721,7 @@ int mqr_reduce_rccl(mqr_vbg* local, mqr_comm* c, int mode, int root, mqr_vbg* ou
     }
     for (int i = 0; i < 4; ++i)
         if (hipEventElapsedTime(&c->last_ms[i], c->ev[i], c->ev[i + 1]) != hipSuccess) c->last_ms[i] = -1.f;
-    *n_owned = H.n_owned;
+    *n_owned = x.H.n_owned;
     return 0;
 }
 
@@ -676,56 +735,85 @@ int mqr_merge_local(mqr_vbg** locals, int n, int mode, int root, mqr_vbg** outs,
         MQR_REQUIRE(locals[r] && outs[r], "null volume");
         MQR_REQUIRE(locals[r]->device == locals[0]->device && outs[r]->device == locals[0]->device,
                     "mqr_merge_local: all volumes on one device");
+        MQR_REQUIRE(locals[r]->R == locals[0]->R && outs[r]->R == locals[0]->R &&
+                        locals[r]->voxel_size == locals[0]->voxel_size &&
+                        outs[r]->voxel_size == locals[0]->voxel_size,
+                    "volume geometry differs");
         for (int q = 0; q < n; ++q) MQR_REQUIRE(outs[r] != locals[q], "mqr_merge_local: an output aliases an input");
+        for (int q = 0; q < r; ++q) MQR_REQUIRE(outs[r] != outs[q], "mqr_merge_local: two outputs are one volume");
     }
     MQR_CHECK_HIP(hipSetDevice(locals[0]->device));
-    const int R3 = (int)locals[0]->R3;
     int64_t mx = 1;
     for (int r = 0; r < n; ++r) {
         if (sync_all(locals[r])) return 1;
         mx = std::max<int64_t>(mx, locals[r]->pool_count);
     }
-    hipStream_t st = nullptr;
-    MQR_CHECK_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-    StreamDrain drain{st};
-    struct StreamFree {
-        hipStream_t s;
-        ~StreamFree() { (void)hipStreamDestroy(s); }
-    } sfree{st};
+    OwnedStream os;
+    MQR_CHECK_HIP(hipStreamCreateWithFlags(&os.s, hipStreamNonBlocking));
+    const hipStream_t st = os.s;
     // the all-gather, as device copies: rank r's keys at r mx, padded with kEmpty
     uint64_t* dkeys = nullptr;
     MQR_CHECK_HIP(hipMalloc(&dkeys, sizeof(uint64_t) * mx * n));
     struct DevFree {
         void* p;
-        ~DevFree() { if (p) (void)hipFree(p); }
+        ~DevFree() {
+            if (p) (void)hipFree(p);
+        }
     } kfree{dkeys};
     MQR_CHECK_HIP(hipMemsetAsync(dkeys, 0xff, sizeof(uint64_t) * mx * n, st));
     for (int r = 0; r < n; ++r)
         if (locals[r]->pool_count)
             MQR_CHECK_HIP(hipMemcpyAsync(dkeys + r * mx, locals[r]->bkeys, sizeof(uint64_t) * locals[r]->pool_count,
                                          hipMemcpyDeviceToDevice, st));
-    PlanScratch S;
+    MQR_CHECK_HIP(hipStreamSynchronize(st));
     t_local_ms.assign(n, 0.f);
-    MQR_CHECK_HIP(hipStreamSynchronize(st));  // the key copies are the all-gather's, not a destination's
+    // 1. every rank's own side, exactly as mqr_reduce_rccl runs it on that rank: its plan (me = s),
+    //    its output volume, its send segments packed from its own pool
+    std::vector<std::unique_ptr<Exchange>> X(n);
+    for (int s = 0; s < n; ++s) {
+        const auto t0 = std::chrono::steady_clock::now();
+        X[s].reset(new Exchange());
+        if (xchg_prepare(*X[s], st, dkeys, n, mx, s, mode, root, locals[s], outs[s], nullptr, nullptr)) return 1;
+        MQR_CHECK_HIP(hipStreamSynchronize(st));
+        t_local_ms[s] += std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
+    // 2. the transport: sender s's segment for d into d's segment from s.  Both ranks planned the
+    //    pair independently, so the segment lengths and the source buffers each side lists (s's
+    //    send_idx for d, d's recv_src for s) must agree entry for entry -- checked here, before any
+    //    byte moves.
+    std::vector<int32_t> a, b;
+    for (int d = 0; d < n; ++d)
+        for (int s = 0; s < n; ++s) {
+            const size_t m = X[s]->send_blocks(d);
+            if (m != X[d]->recv_blocks(s)) {
+                set_error("mqr_merge_local: rank " + std::to_string(s) + " sends " + std::to_string(m) +
+                          " blocks to rank " + std::to_string(d) + ", which expects " +
+                          std::to_string(X[d]->recv_blocks(s)));
+                return 4;
+            }
+            if (!m) continue;
+            a.resize(m);
+            b.resize(m);
+            MQR_CHECK_HIP(hipMemcpyAsync(a.data(), X[s]->pv.send_idx + X[s]->soff[d], 4 * m, hipMemcpyDeviceToHost, st));
+            MQR_CHECK_HIP(hipMemcpyAsync(b.data(), X[d]->pv.recv_src + X[d]->roff[s], 4 * m, hipMemcpyDeviceToHost, st));
+            MQR_CHECK_HIP(hipStreamSynchronize(st));
+            if (a != b) {
+                set_error("mqr_merge_local: rank " + std::to_string(s) + "'s segment for rank " + std::to_string(d) +
+                          " lists other blocks (or another order) than rank " + std::to_string(d) + " expects");
+                return 4;
+            }
+            if (s != d)
+                MQR_CHECK_HIP(hipMemcpyAsync(X[d]->recv_seg(s), X[s]->send_seg(d), sizeof(float2) * m * X[s]->R3,
+                                             hipMemcpyDeviceToDevice, st));
+        }
+    MQR_CHECK_HIP(hipStreamSynchronize(st));
+    // 3. every rank merges what it received, in source-rank order
     for (int d = 0; d < n; ++d) {
         const auto t0 = std::chrono::steady_clock::now();
-        // destination d's plan: its receive segments name, per source, the source's buffers
-        PlanView pv;
-        if (device_plan(S, st, dkeys, n, mx, d, mode, root, pv)) return 1;
-        const PlanSummary H = *pv.H;
-        if (prepare_out(outs[d], pv.out_keys, H.n_out)) return 1;
-        int64_t o = 0;
-        for (int src = 0; src < n; ++src) {
-            const int64_t m = H.cnt[1][src];
-            if (m)
-                hipLaunchKernelGGL(k_merge_direct, dim3((unsigned)m), dim3(256), 0, st, pv.recv_src + o,
-                                   pv.recv_dst + o, m, locals[src]->pool, R3, outs[d]->pool);
-            o += m;
-        }
-        MQR_CHECK_HIP(hipGetLastError());
-        MQR_CHECK_HIP(hipStreamSynchronize(st));  // the plan scratch is reused for the next destination
-        n_owned[d] = H.n_owned;
-        t_local_ms[d] = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        if (xchg_merge(*X[d], st, outs[d])) return 1;
+        MQR_CHECK_HIP(hipStreamSynchronize(st));
+        n_owned[d] = X[d]->H.n_owned;
+        t_local_ms[d] += std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }
     return 0;
 }
@@ -734,6 +822,94 @@ int mqr_merge_local_timing(float* ms, int n) {
     MQR_REQUIRE(ms && n >= 0, "bad arguments");
     MQR_REQUIRE((size_t)n <= t_local_ms.size(), "fewer destinations in the last mqr_merge_local");
     for (int i = 0; i < n; ++i) ms[i] = t_local_ms[i];
+    return 0;
+}
+
+int mqr_xchg_create(mqr_vbg* local, int world, int rank, int mode, int root, const uint64_t* gathered_keys,
+                    int64_t mx, int keys_loc, mqr_vbg* out, mqr_xchg** h) {
+    MQR_REQUIRE(local && out && gathered_keys && h, "null argument");
+    MQR_REQUIRE(local != out, "mqr_xchg_create: `out` must be a different volume than `local` (it is emptied first)");
+    MQR_REQUIRE(world >= 1 && world <= kMaxRanks && rank >= 0 && rank < world, "rank / world out of range (world <= 64)");
+    MQR_REQUIRE(mode == MQR_MERGE_ROOT || mode == MQR_MERGE_SHARDED, "unknown merge mode");
+    MQR_REQUIRE(root >= 0 && root < world, "root out of range");
+    MQR_REQUIRE(mx >= 1, "mx (padded keys per rank) must be >= 1");
+    MQR_REQUIRE(local->device == out->device, "volumes on one device");
+    MQR_REQUIRE(local->R == out->R && local->voxel_size == out->voxel_size, "volume geometry differs");
+    *h = nullptr;
+    MQR_CHECK_HIP(hipSetDevice(local->device));
+    if (sync_all(local)) return 1;
+    MQR_REQUIRE(local->pool_count <= mx, "mqr_xchg_create: mx is smaller than this rank's block count");
+    std::unique_ptr<mqr_xchg> xh(new mqr_xchg());
+    xh->device = local->device;
+    xh->world = world;
+    xh->rank = rank;
+    xh->out = out;
+    MQR_CHECK_HIP(hipStreamCreateWithFlags(&xh->st.s, hipStreamNonBlocking));
+    const size_t kb = sizeof(uint64_t) * (size_t)mx * world;
+    MQR_CHECK_HIP(hipMalloc(&xh->dkeys, kb));
+    MQR_CHECK_HIP(hipMemcpyAsync(xh->dkeys, gathered_keys, kb,
+                                 keys_loc == MQR_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, xh->st.s));
+    if (xchg_prepare(xh->x, xh->st.s, static_cast<const uint64_t*>(xh->dkeys), world, mx, rank, mode, root, local,
+                     out, nullptr, nullptr))
+        return 1;
+    MQR_CHECK_HIP(hipStreamSynchronize(xh->st.s));
+    *h = xh.release();
+    return 0;
+}
+
+int mqr_xchg_counts(mqr_xchg* h, int64_t* send_blocks, int64_t* recv_blocks, int64_t* n_owned, int64_t* floats_per_block) {
+    MQR_REQUIRE(h, "null argument");
+    for (int p = 0; p < h->world; ++p) {
+        if (send_blocks) send_blocks[p] = (int64_t)h->x.send_blocks(p);
+        if (recv_blocks) recv_blocks[p] = (int64_t)h->x.recv_blocks(p);
+    }
+    if (n_owned) *n_owned = h->x.H.n_owned;
+    if (floats_per_block) *floats_per_block = 2 * (int64_t)h->x.R3;
+    return 0;
+}
+
+int mqr_xchg_send_segment(mqr_xchg* h, int peer, float* dst, int loc) {
+    MQR_REQUIRE(h && peer >= 0 && peer < h->world, "bad arguments");
+    MQR_REQUIRE(!h->finished, "mqr_xchg_send_segment: exchange already finished");
+    const size_t m = h->x.send_blocks(peer);
+    if (!m) return 0;
+    MQR_REQUIRE(dst, "null destination");
+    MQR_CHECK_HIP(hipSetDevice(h->device));
+    MQR_CHECK_HIP(hipMemcpyAsync(dst, h->x.send_seg(peer), sizeof(float) * h->x.seg_floats(m),
+                                 loc == MQR_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, h->st.s));
+    MQR_CHECK_HIP(hipStreamSynchronize(h->st.s));
+    return 0;
+}
+
+int mqr_xchg_recv_segment(mqr_xchg* h, int peer, const float* src, int loc) {
+    MQR_REQUIRE(h && peer >= 0 && peer < h->world, "bad arguments");
+    MQR_REQUIRE(peer != h->rank, "mqr_xchg_recv_segment: the self segment is already in place");
+    MQR_REQUIRE(!h->finished, "mqr_xchg_recv_segment: exchange already finished");
+    const size_t m = h->x.recv_blocks(peer);
+    if (!m) return 0;
+    MQR_REQUIRE(src, "null source");
+    MQR_CHECK_HIP(hipSetDevice(h->device));
+    MQR_CHECK_HIP(hipMemcpyAsync(h->x.recv_seg(peer), src, sizeof(float) * h->x.seg_floats(m),
+                                 loc == MQR_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, h->st.s));
+    MQR_CHECK_HIP(hipStreamSynchronize(h->st.s));
+    return 0;
+}
+
+int mqr_xchg_finish(mqr_xchg* h, int64_t* n_owned) {
+    MQR_REQUIRE(h, "null argument");
+    MQR_REQUIRE(!h->finished, "mqr_xchg_finish: called twice");
+    MQR_CHECK_HIP(hipSetDevice(h->device));
+    if (xchg_merge(h->x, h->st.s, h->out)) return 1;
+    MQR_CHECK_HIP(hipStreamSynchronize(h->st.s));
+    h->finished = true;
+    if (n_owned) *n_owned = h->x.H.n_owned;
+    return 0;
+}
+
+int mqr_xchg_destroy(mqr_xchg* h) {
+    if (!h) return 0;
+    (void)hipSetDevice(h->device);
+    delete h;
     return 0;
 }
 

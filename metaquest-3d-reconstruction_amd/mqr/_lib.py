@@ -67,6 +67,13 @@ SIGNATURES = {
     "mqr_merge_local_timing": (ctypes.c_int, [_f32p, ctypes.c_int]),
     "mqr_merge_local": (ctypes.c_int, [ctypes.POINTER(_vp), ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                        ctypes.POINTER(_vp), _i64p]),
+    "mqr_xchg_create": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp,
+                                       ctypes.c_int64, ctypes.c_int, _vp, ctypes.POINTER(_vp)]),
+    "mqr_xchg_counts": (ctypes.c_int, [_vp, _i64p, _i64p, _i64p, _i64p]),
+    "mqr_xchg_send_segment": (ctypes.c_int, [_vp, ctypes.c_int, _vp, ctypes.c_int]),
+    "mqr_xchg_recv_segment": (ctypes.c_int, [_vp, ctypes.c_int, _vp, ctypes.c_int]),
+    "mqr_xchg_finish": (ctypes.c_int, [_vp, _i64p]),
+    "mqr_xchg_destroy": (ctypes.c_int, [_vp]),
     "mqr_geom_counts": (ctypes.c_int, [_vp, _i64p, _i64p]),
     "mqr_geom_copy": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_int]),
     "mqr_geom_free": (ctypes.c_int, [_vp]),

@@ -269,8 +269,9 @@ def merge_rccl(vbg, comm: RcclComm, mode: str = "sharded", root: int = 0, out=No
 
 
 def merge_local(vbgs, mode: str = "sharded", root: int = 0, outs=None):
-    """The merge of several volumes of one process on one device (the same device plan and merge
-    arithmetic; each destination reads the sources' pools directly instead of receiving over RCCL).
+    """mqr_reduce_rccl's exchange for several volumes of one process on one device, with device
+    copies as the transport: every rank plans, packs its send segments and merges in rank order as
+    it would over RCCL; sender / receiver segment lists are checked pair by pair (mqr_merge_local).
     Returns [(out volume, owned block count)] per input; outputs must not alias inputs."""
     import ctypes
     from . import _lib
@@ -283,9 +284,75 @@ def merge_local(vbgs, mode: str = "sharded", root: int = 0, outs=None):
     return list(zip(outs, owned.tolist()))
 
 
+def merge_staged(vbg, group=None, mode: str = "sharded", root: int = 0, out=None, check_counts: bool = True):
+    """mqr_reduce_rccl's exchange with the segments carried by torch.distributed over host buffers
+    (gloo): one process per rank, any device (several ranks may share one GPU, which RCCL refuses).
+    The plan, the send segments (packed from this rank's pool), the rank-ordered merge and the output
+    are libmqr's own (mqr_xchg_*); only the ncclSend / ncclRecv of the segments is replaced by
+    isend / irecv of host tensors.  With check_counts every rank's send count to each peer is
+    compared with that peer's receive count from it (an all-to-all of the counts) before any
+    segment moves.  Returns (out volume, owned block count)."""
+    import ctypes
+    import torch
+    import torch.distributed as dist
+    from . import _lib
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    out = out if out is not None else _empty_like(vbg)
+    local = np.ascontiguousarray(vbg.export_keys(), dtype=np.int32).reshape(-1, 3)
+    n = torch.tensor([len(local)], dtype=torch.int64)
+    counts = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(counts, n, group=group)
+    mx = max(1, max(int(c.item()) for c in counts))
+    mine = np.full(mx, -1, np.int64)  # 0xFFFF...FF padding (the library's empty key)
+    mine[:len(local)] = _packed(local)
+    gathered = [torch.empty(mx, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(gathered, torch.from_numpy(mine), group=group)
+    allk = np.ascontiguousarray(torch.cat(gathered).numpy())
+    h = ctypes.c_void_p()
+    _lib.call("mqr_xchg_create", vbg.handle, world, rank, MERGE_MODES[mode], int(root), _lib.ptr(allk), int(mx),
+              _lib.MQR_HOST, out.handle, ctypes.byref(h))
+    try:
+        sc, rc = np.zeros(world, np.int64), np.zeros(world, np.int64)
+        fpb = ctypes.c_int64()
+        _lib.call("mqr_xchg_counts", h, _lib.ptr(sc, _lib._i64p), _lib.ptr(rc, _lib._i64p), None, ctypes.byref(fpb))
+        if check_counts:
+            theirs = torch.empty(world, dtype=torch.int64)
+            dist.all_to_all_single(theirs, torch.from_numpy(sc.copy()), group=group)
+            if not np.array_equal(theirs.numpy(), rc):
+                raise RuntimeError(f"merge_staged: rank {rank} expects {rc.tolist()} blocks from the ranks, "
+                                   f"which send it {theirs.numpy().tolist()}")
+        ops, recvs = [], []
+        for p in range(world):
+            if p == rank:
+                continue
+            if sc[p]:
+                buf = np.empty(int(sc[p]) * fpb.value, np.float32)
+                _lib.call("mqr_xchg_send_segment", h, p, _lib.ptr(buf), _lib.MQR_HOST)
+                ops.append(dist.isend(torch.from_numpy(buf), dst=_global(group, p), group=group))
+            if rc[p]:
+                t = torch.empty(int(rc[p]) * fpb.value, dtype=torch.float32)
+                ops.append(dist.irecv(t, src=_global(group, p), group=group))
+                recvs.append((p, t))
+        for op in ops:
+            op.wait()
+        for p, t in recvs:
+            _lib.call("mqr_xchg_recv_segment", h, p, ctypes.c_void_p(t.data_ptr()), _lib.MQR_HOST)
+        owned = ctypes.c_int64()
+        _lib.call("mqr_xchg_finish", h, ctypes.byref(owned))
+    finally:
+        _lib._lib.mqr_xchg_destroy(h)
+    return out, owned.value
+
+
+def _global(group, r):
+    """Global rank of group rank r (torch.distributed's point-to-point calls take global ranks)."""
+    import torch.distributed as dist
+    return r if group is None else dist.get_global_rank(group, r)
+
+
 def merge_local_timing(n: int):
-    """Per-destination wall ms of the last merge_local (one rank's plan, output volume and merge
-    kernels, without the transfer)."""
+    """Per-rank wall ms of the last merge_local (one rank's plan, output volume, send-segment gather
+    and merge kernels, without the transfer)."""
     from . import _lib
     ms = np.zeros(n, np.float32)
     _lib.call("mqr_merge_local_timing", _lib.ptr(ms, _lib._f32p), int(n))

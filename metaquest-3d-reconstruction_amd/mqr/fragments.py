@@ -74,12 +74,18 @@ def _worker(args):
     import time
     i, io, ds, side, config = args
     t0 = time.perf_counter()
-    r = integrate_fragment_point_cloud(io, ds, side, config)
-    dt = time.perf_counter() - t0
-    if r is None:
-        return i, None, dt
-    side, pcd = r
-    return i, (side, pcd.points, pcd.normals), dt
+    # the reference's ParallelWorker (paralell_utils.py:11-19) turns ANY failure of a task into None
+    # for that task: library load / HIP context creation in a spawned worker or reading the cloud
+    # back must not abort the other fragments
+    try:
+        r = integrate_fragment_point_cloud(io, ds, side, config)
+        if r is None:
+            return i, None, time.perf_counter() - t0
+        side, pcd = r
+        return i, (side, pcd.points, pcd.normals), time.perf_counter() - t0
+    except Exception as e:  # noqa: BLE001
+        print(f"[Error] integrate_fragment_point_cloud failed for {getattr(side, 'name', side)}: {e}")
+        return i, None, time.perf_counter() - t0
 
 
 def _warm(_):

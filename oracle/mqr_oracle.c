@@ -695,7 +695,8 @@ int orc_confidence(const float* depths, const uint8_t* frame_valid, const float*
             if (t == ref || (frame_valid && !frame_valid[t])) continue;
             float e;
             if (pixel_error(depths + (int64_t)t * HW, H, W, K + 9 * ref, K + 9 * t, Tcw + 16 * ref, Tcw_inv + 16 * t,
-                            Tcw + 16 * t, depth_max, u, v, refd[p], &e)) {
+                            Tcw + 16 * t, depth_max, u, v, refd[p], &e) &&
+                !isnan(e)) {  /* valid_count += ~isnan(error_map) (estimate_depth_confidences.py:66) */
                 ++nv;
                 if (e <= thr) ++nc;
             }

@@ -60,17 +60,19 @@ def test_confidence_full_resolution_vs_oracle():
 def test_confidence_band_edges_vs_oracle(thr, dmax):
     """The consistency band (pixel_decide) against the oracle's full computation: thresholds at the
     extremes (nothing / everything consistent, +inf) and small enough that many pairs fall inside the
-    band, unbounded depth_max, a non-rigid pose (large R^T R - I), a pose with a NaN entry and one with
-    an inverse off by 1 mm (large dT)."""
+    band, unbounded depth_max, a non-rigid pose (large R^T R - I), a pose with a NaN entry, a NaN in
+    T_cw with a finite separately supplied inverse (the error is NaN: not valid) and an inverse off by
+    1 mm (large dT)."""
     from mqr import synthetic
     from mqr.confidence import confidence_maps
-    n = 16  # reference frames 5..10 see only finite-band neighbours (the band path proper)
+    n = 16  # reference frames 5..8 see only finite-band neighbours (the band path proper)
     seq = synthetic.make_sequence("room", n=n, height=120, width=160, f=131.25, noise=True, seed=11)
     T = seq["T_cw"].astype(np.float32).copy()
     T[1, :3, :3] *= np.float32(1.001)  # scaled rotation
     T[14, 0, 3] = np.nan
     Ti = np.linalg.inv(T.astype(np.float64)).astype(np.float32)
     Ti[8, 1, 3] += np.float32(1e-3)
+    T[12, 2, 3] = np.nan  # after the inverse: T_cw non-finite, T_cw_inv finite
     conf, valid = confidence_maps(seq["depth"], seq["K"], T, Ti, 0, n, 3, dmax, thr)
     for i in range(n):
         oc, ov = oracle.confidence(seq["depth"], seq["K"], T, Ti, i, 3, dmax, thr)

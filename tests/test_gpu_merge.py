@@ -1,4 +1,13 @@
-"""Multi-GPU merge in libmqr (mqr_reduce_rccl / mqr_merge_local) on one device.
+"""Multi-GPU merge in libmqr (mqr_reduce_rccl / mqr_merge_local / mqr_xchg_*) on one device.
+
+The exchange of mqr_reduce_rccl (per-rank plan, send segments packed by k_gather_blocks, receive
+segments merged in rank order through recv_dst) runs here over two other transports:
+* mqr_merge_local -- the n volumes of one process, device copies between the ranks' own send and
+  receive buffers; every sender / receiver pair's segment lists are checked entry for entry;
+* merge_staged (mqr_xchg_*) -- one PROCESS per rank (2, 3 and 8 processes sharing the GPU), the
+  segments carried over gloo through host buffers, each process planning on its own.
+Only the ncclSend / ncclRecv call itself is not exercised on a one-GPU box (RCCL refuses two ranks
+on one device).
 
 * root mode: N frame shards merged into one volume == one sequential pass (identical keys and
   weights, |dtsdf| <= 1e-4; voxels one shard saw alone are that shard's values bit for bit);
@@ -27,12 +36,12 @@ def seq():
     return synthetic.make_sequence("room", n=36, height=240, width=320, f=262.5, noise=True, seed=12)
 
 
-def _shards(seq, world, R=16, vs=0.01):
+def _shards(seq, world, R=16, vs=0.01, ranks=None):
     from mqr.distributed import shard_range
     from mqr.vbg import VoxelBlockGrid
     vols = []
     n = len(seq["K"])
-    for r in range(world):
+    for r in (range(world) if ranks is None else ranks):
         lo, hi = shard_range(n, r, world)
         v = VoxelBlockGrid(voxel_size=vs, block_resolution=R, block_count=64)
         v.integrate_frames(seq["depth"][lo:hi], seq["K"][lo:hi], seq["T_wc"][lo:hi], depth_scale=1.0,
@@ -49,7 +58,7 @@ def _oracle(seq, R=16, vs=0.01):
     return ref
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_root_merge_matches_single_pass(seq, world):
     from mqr.distributed import merge_local
     vols = _shards(seq, world)
@@ -73,7 +82,7 @@ def test_root_merge_matches_single_pass(seq, world):
         assert np.array_equal(tm[j][alone], t0[b][alone]) and np.array_equal(wm[j][alone], w0[b][alone])
 
 
-@pytest.mark.parametrize("world,R", [(2, 16), (3, 16), (4, 8)])
+@pytest.mark.parametrize("world,R", [(2, 16), (3, 16), (4, 8), (8, 16)])
 def test_sharded_meshes_concatenate_to_the_merged_mesh(seq, world, R):
     from mqr.distributed import extract_mesh_owned, merge_local
     vols = _shards(seq, world, R=R)
@@ -190,4 +199,84 @@ def test_rccl_two_gpus(seq):
         T.append(t + off)
         off += len(v)
     V, T = np.concatenate(V), np.concatenate(T)
+    assert np.array_equal(canon_triangles(V, T), canon_triangles(full.vertices, full.triangles))
+
+
+# ---------------------------------------------------------------- one process per rank (gloo-carried)
+def _staged_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from mqr import synthetic
+        from mqr.distributed import extract_mesh_owned, merge_staged
+        vol = _shards(synthetic.make_sequence("room", n=36, height=240, width=320, f=262.5, noise=True, seed=12),
+                      world, ranks=[rank])[0]
+        root = world - 1
+        out, n_root = merge_staged(vol, mode="root", root=root)
+        res = {"root": out.export() if rank == root else None, "n_root": n_root, "size_root": out.size()}
+        out2, n = merge_staged(vol, mode="sharded", out=out)  # the output volume is reused (emptied first)
+        m = extract_mesh_owned(out2, n, 1.5)
+        k, t, w = out2.export()
+        res.update(owned=(k[:n], t[:n], w[:n]), mesh=(m.vertices, m.triangles))
+        q.put((rank, res))
+    except Exception as e:  # noqa: BLE001
+        import traceback
+        q.put((rank, repr(e) + "\n" + traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_staged_processes_match_local_twin_and_single_pass(seq, world):
+    """`world` processes on the one GPU, each integrating its frame shard and running the exchange
+    on its own (plan, send segments, rank-ordered merge); segments over gloo.  The root volume is
+    bit-identical to the one-process twin's and within 1e-4 of the single pass; the shard meshes
+    concatenate to the merged mesh; owned blocks equal the merged volume's."""
+    import socket
+    import torch.multiprocessing as mp
+    from mqr.distributed import merge_local
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_staged_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    try:
+        res = dict(q.get(timeout=240) for _ in ps)
+    finally:
+        for p in ps:
+            p.join(60)
+            if p.is_alive():
+                p.kill()
+    for r in range(world):
+        assert not isinstance(res[r], str), res[r]
+    twin = merge_local(_shards(seq, world), mode="root", root=world - 1)[world - 1][0]
+    tk, tt, tw = twin.export()
+    rk, rt, rw = res[world - 1]["root"]
+    assert res[world - 1]["n_root"] == len(rk) == len(tk)
+    for r in range(world - 1):
+        assert res[r]["n_root"] == 0 and res[r]["size_root"] == 0
+    assert np.array_equal(rk, tk) and np.array_equal(rt, tt) and np.array_equal(rw, tw)  # same order, same bits
+    assert compare_volumes((rk, rt, rw), _oracle(seq).export(), TOL) < 1e-5
+    full = twin.extract_triangle_mesh(1.5)
+    off, V, T, K = 0, [], [], []
+    rpos = {tuple(k): i for i, k in enumerate(rk)}
+    for r in range(world):
+        v, t = res[r]["mesh"]
+        V.append(v)
+        T.append(t + off)
+        off += len(v)
+        k, ot, ow = res[r]["owned"]
+        K.append(k)
+        for b in range(len(k)):
+            j = rpos[tuple(k[b])]
+            assert np.array_equal(ot[b], rt[j]) and np.array_equal(ow[b], rw[j])
+    allk = np.concatenate(K)
+    assert len(allk) == len(rk) and len(np.unique(allk, axis=0)) == len(allk)
+    V, T = np.concatenate(V), np.concatenate(T)
+    assert len(T) == len(full.triangles) > 1000
     assert np.array_equal(canon_triangles(V, T), canon_triangles(full.vertices, full.triangles))
