@@ -1045,6 +1045,7 @@ def main():
             wd = wseq["depth_t"].contiguous()
             wK, wT = wseq["K"].astype(np.float64), wseq["T_wc"].astype(np.float64)
             wptr = (_DevPtr(wd.data_ptr()), wd.shape[0], H, W)
+            torch.cuda.synchronize()  # torch's stream wrote the frames; libmqr reads them on its own streams
 
             def wstep():
                 vbg.reset()

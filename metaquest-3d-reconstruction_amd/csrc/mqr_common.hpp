@@ -168,7 +168,8 @@ struct mqr_vbg {
     bool probe_one = false;    // batch touch probes one slot per new key (variant bit 0x1000, test hook)
     int batch_frames = mqr::kMaxBatch;  // frames per device batch (A/B: 32, variant bit 0x400)
     // profiling
-    int touch_ppt = 2;  // stride-4 pixels per k_touch thread
+    int touch_ppt = 2;  // stride-4 pixels per k_touch thread (strip touch, variant bits 16 / 17)
+    bool touch_frame = true;  // k_touch_frame: a frame per workgroup (default)
     bool profile = false;
     bool profile_touch = false;  // mqr_vbg_profile level 2: also time the touch launches
     std::vector<std::pair<hipEvent_t, hipEvent_t>> int_events, touch_events;

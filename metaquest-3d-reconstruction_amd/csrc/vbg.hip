@@ -582,7 +582,11 @@ static int touch_launch(mqr_vbg* v, int p, const float* dbase, int64_t HW, int H
     }
     if (n > 0)
     {
-        if (v->touch_ppt == 1)
+        if (v->touch_frame)  // default: a frame per workgroup, claims of the frame's distinct blocks only
+            hipLaunchKernelGGL((k_touch_frame<1024, 4096>), dim3(1, b), dim3(1024), 0, v->stream, dbase, HW, H, W,
+                               v->d_fp[p], dframe_dev(v, p), depth_scale, depth_max, sdf_trunc, block_size, t, max_probe,
+                               alloc, v->ctr(p), v->pool_ctr(), v->pool_cap, v->bkeys, v->lists[p], v->list_cap);
+        else if (v->touch_ppt == 1)
             hipLaunchKernelGGL(k_touch<1>, dim3((n + 255) / 256, b), dim3(256), 0, v->stream, dbase, HW, H, W,
                                v->d_fp[p], dframe_dev(v, p), depth_scale, depth_max, sdf_trunc, block_size, t, max_probe,
                                alloc, v->ctr(p), v->pool_ctr(), v->pool_cap, v->bkeys, v->lists[p], v->list_cap);
@@ -1086,6 +1090,7 @@ int mqr_vbg_set_variant(mqr_vbg* v, int variant) {
     v->touch_wait = (variant & 0x4000) != 0;  // bit 14: integrate always waits on a touch-stream event (A/B)
     v->xcd_order = (variant & 0x8000) != 0;   // bit 15: spatial per-XCD groups (k_xcd_order, A/B)
     v->touch_ppt = (variant & 0x10000) ? 1 : 2;  // bit 16: one stride-4 pixel per touch thread (A/B)
+    v->touch_frame = (variant & 0x30000) == 0;   // bit 17: the round-3 strip touch (k_touch<2>) instead of k_touch_frame
     return 0;
 }
 

@@ -277,6 +277,153 @@ __global__ __launch_bounds__(256) void k_touch(const float* __restrict__ depths,
     }
 }
 
+// The touch samples of one stride-4 pixel (Appendix A.2, the arithmetic of k_touch): up to 4 packed
+// keys, kEmpty where the pixel is invalid; consecutive equal keys are left to the caller.
+__device__ __forceinline__ int touch_pixel_keys(float draw, int x, int y, const FrameParams& fp, float depth_scale,
+                                                float depth_max, float sdf_trunc, float block_size, int* counters,
+                                                uint64_t (&key)[4]) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) key[s] = kEmpty;
+    const float d = draw / depth_scale;
+    if (!(d > 0 && d < depth_max)) return 0;
+    const float xc = ((float)x - fp.cx) * 1.0f / fp.fx;
+    const float yc = ((float)y - fp.cy) * 1.0f / fp.fy;
+    const float zc = 1.0f;
+    const float xg = xc * fp.pose[0] + yc * fp.pose[1] + zc * fp.pose[2] + fp.pose[3];
+    const float yg = xc * fp.pose[4] + yc * fp.pose[5] + zc * fp.pose[6] + fp.pose[7];
+    const float zg = xc * fp.pose[8] + yc * fp.pose[9] + zc * fp.pose[10] + fp.pose[11];
+    const float xo = fp.pose[3], yo = fp.pose[7], zo = fp.pose[11];
+    const float xd = xg - xo, yd = yg - yo, zd = zg - zo;
+    const float t_min = fmaxf(d - sdf_trunc, 0.0f);
+    const float t_max = fminf(d + sdf_trunc, depth_max);
+    const float t_step = (t_max - t_min) / 3;
+    float tt = t_min;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        const int xb = (int)floorf((xo + tt * xd) / block_size);
+        const int yb = (int)floorf((yo + tt * yd) / block_size);
+        const int zb = (int)floorf((zo + tt * zd) / block_size);
+        if (key_in_range(xb, yb, zb))
+            key[s] = pack_key(xb, yb, zb);
+        else
+            atomicOr(&counters[kOverflow], 8);
+        tt += t_step;
+    }
+    return 4;
+}
+
+// The table claim of a wave's keys (kEmpty = none): insert-or-find, pool buffers for new entries,
+// frame bit f, list appends.  Call with the whole wave converged.  Returns new frame bits (this lane).
+__device__ __forceinline__ int touch_claim(uint64_t k, int f, Table t, int64_t max_probe, int alloc, int* counters,
+                                           int* pool_ctr, int64_t pool_cap, uint64_t* bkeys, int32_t* list,
+                                           int64_t list_cap) {
+    int64_t slot = -1;
+    bool won = false, app = false;
+    int fresh = 0;
+    if (k != kEmpty) slot = table_claim(t, k, counters, won, max_probe);
+    if (alloc) wave_alloc(won, slot, k, t, counters, pool_ctr, pool_cap, bkeys);
+    if (slot >= 0) fresh = mark_slot_bit(t, slot, f, app);
+    wave_append(app, slot, counters, list, list_cap);
+    return fresh;
+}
+
+// compute_unique_block_coordinates for a batch with a FRAME per workgroup (blockIdx.y = batch frame;
+// gridDim.x workgroups split its stride-4 pixels, 1 by default).  Every sample's key goes into an LDS
+// set of the frame's blocks first; only the set's entries -- the frame's B_f distinct blocks, ~1 200
+// on the C2 walk -- are claimed in the global table, one device-coherent chain each (k_touch claims
+// per 512-pixel strip: ~4x as many chains for the same keys, and its 2 400 workgroups per batch hold
+// wave slots of the overlapped integrate).  A key that finds no LDS slot within kProbe probes, or
+// arrives after the set is 3/4 full, is claimed directly by its wave (the claim is idempotent: a
+// repeated key finds its slot and its frame bit already set), so a frame with more distinct blocks
+// than the set holds stays correct.
+template <int NT, int SEEN>
+__global__ __launch_bounds__(NT) void k_touch_frame(const float* __restrict__ depths, int64_t HW, int H, int W,
+                                                    const FrameParams* __restrict__ fps,
+                                                    const int64_t* __restrict__ depth_frame, float depth_scale,
+                                                    float depth_max, float sdf_trunc, float block_size, Table t,
+                                                    int64_t max_probe, int alloc, int* counters, int* pool_ctr,
+                                                    int64_t pool_cap, uint64_t* bkeys, int32_t* list,
+                                                    int64_t list_cap) {
+    static_assert(SEEN <= 65536 && (SEEN & (SEEN - 1)) == 0, "16-bit set indices, power of two");
+    constexpr int kProbe = 32, kFill = SEEN / 4 * 3;
+    __shared__ unsigned long long seen[SEEN];
+    __shared__ uint16_t uniq[SEEN];
+    __shared__ int wg_count[3];  // valid samples, new frame bits, set entries
+    for (int i = threadIdx.x; i < SEEN; i += NT) seen[i] = kEmpty;
+    if (threadIdx.x < 3) wg_count[threadIdx.x] = 0;
+    __syncthreads();
+    const int f = blockIdx.y;
+    const FrameParams fp = fps[f];
+    const int cols = W / 4, rows = H / 4, n = rows * cols;
+    const int lo = (int)((int64_t)n * blockIdx.x / gridDim.x), hi = (int)((int64_t)n * (blockIdx.x + 1) / gridDim.x);
+    const float* __restrict__ dep = depths + depth_frame[f] * HW;
+    int valid = 0, fresh = 0;
+    // uniform trip count (the spill claims need whole waves); the next pixel's depth is read ahead
+    int w = lo + (int)threadIdx.x;
+    float dnext = w < hi ? dep[(int64_t)((w / cols) * 4) * W + (w % cols) * 4] : 0.f;
+    for (int base = lo; base < hi; base += NT) {
+        const float draw = dnext;
+        const int wn = w + NT;
+        dnext = wn < hi ? dep[(int64_t)((wn / cols) * 4) * W + (wn % cols) * 4] : 0.f;
+        uint64_t key[4];
+        if (w < hi) valid += touch_pixel_keys(draw, (w % cols) * 4, (w / cols) * 4, fp, depth_scale, depth_max,
+                                              sdf_trunc, block_size, counters, key);
+        else
+#pragma unroll
+            for (int s = 0; s < 4; ++s) key[s] = kEmpty;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            uint64_t k = key[s];
+            if (s > 0 && key[s - 1] == k) k = kEmpty;
+            bool spill = false;
+            if (k != kEmpty) {
+                uint32_t h = (uint32_t)mix64(k) & (SEEN - 1);
+                spill = true;
+                for (int p = 0; p < kProbe; ++p) {
+                    const unsigned long long cur = seen[h];
+                    if (cur == k) {
+                        spill = false;
+                        break;
+                    }
+                    if (cur == kEmpty) {
+                        if (*(volatile int*)&wg_count[2] >= kFill) break;  // set nearly full: claim directly
+                        const unsigned long long old =
+                            atomicCAS(&seen[h], (unsigned long long)kEmpty, (unsigned long long)k);
+                        if (old == kEmpty) {
+                            uniq[atomicAdd(&wg_count[2], 1)] = (uint16_t)h;
+                            spill = false;
+                            break;
+                        }
+                        if (old == k) {
+                            spill = false;
+                            break;
+                        }
+                    }
+                    h = (h + 1) & (SEEN - 1);
+                }
+            }
+            if (__ballot(spill))  // wave-uniform
+                fresh += touch_claim(spill ? k : kEmpty, f, t, max_probe, alloc, counters, pool_ctr, pool_cap, bkeys,
+                                     list, list_cap);
+        }
+        w = wn;
+    }
+    wave_add(&wg_count[0], valid);
+    __syncthreads();
+    const int nu = min(wg_count[2], SEEN);
+    for (int base = 0; base < nu; base += NT) {  // uniform trip count
+        const int idx = base + (int)threadIdx.x;
+        fresh += touch_claim(idx < nu ? seen[uniq[idx]] : kEmpty, f, t, max_probe, alloc, counters, pool_ctr, pool_cap,
+                             bkeys, list, list_cap);
+    }
+    wave_add(&wg_count[1], fresh);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (wg_count[0]) atomicAdd(&counters[kFrameCounterBase + f], wg_count[0]);
+        if (wg_count[1]) atomicAdd(&counters[kFreshBase + f], wg_count[1]);
+    }
+}
+
 // Activate explicit keys (vbg.integrate(block_coords, ...)); marks frame bit 0.
 __global__ void k_activate(const int32_t* __restrict__ keys, int64_t n, Table t, int* counters, int* pool_ctr,
                            int64_t pool_cap, uint64_t* bkeys, int32_t* list, int64_t list_cap, int mark) {
