@@ -371,7 +371,7 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
     //     in two halves (15 = the default).
     //     DESIGN.md §4.1 has the measurements behind the choice.
     int var = v->kernel_variant;
-    if (var < 0 || var > 22) var = 0;
+    if (var < 0 || var > 26) var = 0;
     if (!MQR_AB && var != 1 && var != 2 && var != 4) var = 0;
     if (var != 1 && var != 2 && !lean_ok) var = 2;
     if (var == 5 && (v->R != 16 || W % 4 != 0 || W < 4 || (reinterpret_cast<uintptr_t>(depths) & 15))) var = 0;
@@ -382,7 +382,7 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
     const bool win16_ok = (HW % 4) == 0 && (reinterpret_cast<uintptr_t>(depths) & 15) == 0;
     if ((var == 11 || var == 12 || var == 14 || var == 19) && !win16_ok) var = 0;
     if (var == 0 && !(v->R == 16 && win8_ok)) var = 4;
-    if (var >= 13 && !win8_ok) var = 4;
+    if (var >= 13 && !win8_ok) var = 4;  // (23-26: 8-byte windows too)
     if (v->R != 16 && v->R != 8) var = 1;
     const int32_t* bad_list = v->bad[p];
     const bmask_t* bad_mask = reinterpret_cast<const bmask_t*>(v->bad[p] + v->list_cap);
@@ -451,6 +451,22 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
                 hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 5, 2, 5, 1, true>), dim3(lean_grid), dim3(512), 0, s,
                                    list, lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW,
                                    H, W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
+            else if (var == 23)  // default + next frame's parameters loaded during the current frame
+                hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 7, 2, 5, 0, false, 1>), dim3(lean_grid), dim3(512), 0,
+                                   s, list, lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths,
+                                   HW, H, W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
+            else if (var == 24)  // default + branchless in-image offset
+                hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 7, 2, 5, 0, false, 2>), dim3(lean_grid), dim3(512), 0,
+                                   s, list, lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths,
+                                   HW, H, W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
+            else if (var == 25)  // 23 + 24
+                hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 7, 2, 5, 0, false, 3>), dim3(lean_grid), dim3(512), 0,
+                                   s, list, lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths,
+                                   HW, H, W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
+            else if (var == 26)  // 25 at >= 6 waves / SIMD
+                hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 6, 2, 5, 0, false, 3>), dim3(lean_grid), dim3(512), 0,
+                                   s, list, lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths,
+                                   HW, H, W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
             else if (var == 10)  // variant 9 with s / sdf_trunc in one correction (verified for this sdf_trunc)
                 hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 8, 2, 3, 1>), dim3(lean_grid), dim3(512), 0, s, list,
                                    lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H,

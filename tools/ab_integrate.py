@@ -36,7 +36,7 @@ def main():
     B, H, W = d.shape
     K, T = seq["K"].astype(np.float64), seq["T_wc"].astype(np.float64)
     torch.cuda.synchronize()
-    variants = [int(x) for x in a.variants.split(",")]
+    variants = [int(x, 0) for x in a.variants.split(",")]
     shared = VoxelBlockGrid(voxel_size=0.005, block_resolution=16, block_count=40000, device=0)
     vols = {v: (VoxelBlockGrid(voxel_size=0.005, block_resolution=16, block_count=40000, device=0)
                 if a.separate else shared) for v in variants}

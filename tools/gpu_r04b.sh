@@ -27,3 +27,6 @@ python - <<'P'
 import json; d=json.load(open("gpurun_out/r04b_bench2.json"))
 print({k: d[k] for k in ("value","ms_per_step","merge_ms","merge_transport","scaling")}, d["parity"], d["weak_c2"])
 P
+MQR_HIP_LIB=tools/_ab/libmqr_ab.so timeout -k 10 300 python tools/ab_integrate.py --variants 0,23,24,25,26,0x20000 --rounds 7 --check \
+  > gpurun_out/r04b_ab.json 2> gpurun_out/r04b_ab.err || { tail -20 gpurun_out/r04b_ab.err; exit 1; }
+cat gpurun_out/r04b_ab.json
