@@ -160,6 +160,11 @@ int mqr_confidence(int device, const float* depths, int depth_loc, int N, int H,
                    const float* T_cw, const float* T_cw_inv, const uint8_t* frame_ok, int ref_begin, int ref_end,
                    int frame_range, double depth_max, double error_threshold, double* conf, int32_t* valid,
                    int out_loc);
+/* Diagnostic: enable (1) / disable (0) / keep (-1) per-pair stage counting of mqr_confidence on this
+ * device (a slower kernel build); last4 (nullable) = the last counted call's (pixel, neighbour) pairs
+ * with a valid reference pixel, and how many the float32 prefilter, the float64 band filter and the
+ * float64 back-projection decided. */
+int mqr_confidence_stats(int device, int enable, int64_t* last4);
 int mqr_pixel_error_map(int device, const float* ref_depth, const float* tgt_depth, int H, int W, const float* K_ref,
                         const float* K_tgt, const float* T_cw_ref, const float* T_cw_inv_tgt, const float* T_cw_tgt,
                         double depth_max, float* err_out);

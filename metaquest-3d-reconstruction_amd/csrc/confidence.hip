@@ -35,6 +35,12 @@ struct ConfFrame {
     // from dR = ||R_inv - R^-1||_F, dT = |t_inv - t*| (Tinv against the exact inverse of Tcw) and
     // eR = ||R^T R - I||_F of Tcw's rotation; +inf when they are not finite
     double c1, c0;
+    // float32 prefilter (pixel_decide32): the float32 Tinv and K entries as given, and per coordinate
+    // of Tinv pw the bound of the float32 evaluation's error, E = ea[c] m + eb[c] with m = max |pw|
+    // (ea = 8u sum |R row|, eb = 8u |t|, rounded up; u = 2^-24)
+    float Tf[12];
+    float fxf, fyf, cxf, cyf;
+    float ea[3], eb[3];
     int ok;  // frame_ok (a neighbour that is not ok is skipped, as the reference skips failed loads)
 };
 
@@ -144,7 +150,9 @@ __device__ inline int pixel_error_d2(const float* __restrict__ tgt, int H, int W
 //   * the range test 0 <= uu < W - 1, 0 <= vv < H - 1 is exactly floor(uu) >= 0, floor(uu) + 1 < W
 //     (and for v), and implies the |coord| < 10 max(W, H) and finiteness tests (NaN fails it);
 //   * (double)u1 = floor(uu) + 1 exactly.
-// Returns 0 = no finite error (not counted), 1 = consistent, 2 = inconsistent.
+// Returns 0 = no finite error (not counted), 1 = consistent, 2 = inconsistent, | kTail when decided by
+// the float64 back-projection.
+constexpr int kTail = 4;
 __device__ inline int pixel_decide(const float* __restrict__ tgt, int W, double wm1, double hm1, const ConfFrame& ft,
                                    const double pw[3], double zmax, float dmf, double lo2, double hi2,
                                    double d2_max) {
@@ -196,13 +204,14 @@ __device__ inline int pixel_decide(const float* __restrict__ tgt, int W, double 
     const double lhs = dz * dz * (X * X + Y * Y + Z2);
     if (lhs <= lo2 * Z2) return 1;
     if (lhs > hi2 * Z2) return 2;
-    // inside the band: the reference's own interpolation and float64 back-projection
+    // inside the band: the reference's own interpolation and float64 back-projection (kTail marks the
+    // decisions taken here, for mqr_confidence_stats)
     const double wa = (du1 - uu) * (dv1 - vv);
     const double wb = (uu - fu0) * (dv1 - vv);
     const double wc = (du1 - uu) * (vv - fv0);
     const double wd = (uu - fu0) * (vv - fv0);
     const float zt = (float)(wa * Ia + wb * Ib + wc * Ic + wd * Id);
-    if (!(zt > 0 && isfinite(zt))) return 0;
+    if (!(zt > 0 && isfinite(zt))) return kTail;
     const double ztd = (double)zt;
     const double xt = div64_by_rn_rcp((uu - ft.cx) * ztd, ft.fx, ft.rfx);
     const double yt = div64_by_rn_rcp((vv - ft.cy) * ztd, ft.fy, ft.rfy);
@@ -213,8 +222,99 @@ __device__ inline int pixel_decide(const float* __restrict__ tgt, int W, double 
     const double ex = pw[0] - q[0], ey = pw[1] - q[1], ez = pw[2] - q[2];
     const double d2 = ex * ex + ey * ey + ez * ez;
     // a NaN error is not valid (valid_count += ~isnan(error_map), estimate_depth_confidences.py:66)
-    if (d2 != d2) return 0;
-    return d2 <= d2_max ? 1 : 2;
+    if (d2 != d2) return kTail;
+    return kTail | (d2 <= d2_max ? 1 : 2);
+}
+
+// The same decision as pixel_decide from a float32 forward projection with rigorous error bounds:
+// returns 0 / 1 / 2 where every quantity it rests on is certain, -1 where it is not (the caller then
+// runs pixel_decide's float64 path from scratch).  With X, Y, Z the float32 Tinv pw (error <= E_c =
+// 8u (sum |R row| max|pw| + |t|): three FMAs with one rounding each, pw rounded to float32 once):
+//   * Z <= 0 or Z > zmax certain -> 0; Z's bracket straddling either bound -> -1;
+//   * uu = fx X / Z + cx (v_rcp_f32 within 1 ulp, two products, one sum) is within
+//     E_u = |fx| / Z (E_X + (|X| + E_X) E_Z / (Z - E_Z)) (1 + 8u) + 5u |qx| + 2u |uu| of the reference's
+//     float64 uu (whose own rounding, ~2^-50 relative, the 8u factors cover); likewise vv;
+//   * uu certainly < 0 or >= W - 1 (or vv) -> 0; floor(uu), floor(vv) certain when uu, vv lie at
+//     least E_u, E_v away from an integer, else -1 -- then the taps, the range test and the tap test are
+//     the reference's exactly;
+//   * the band filter of pixel_decide on float32 values: zf from float32 weights moves by at most
+//     E_u (|Ib - Ia| + |Id - Ic|) + E_v (|Ic - Ia| + |Id - Ib|) against the weights of the exact uu, vv
+//     (the band's zterm already covers the float32 interpolation itself); with E_dz = E_Z + that + u zf
+//     and E_P the bound of X^2 + Y^2 + Z^2, the pair is consistent when (|dz| + E_dz)^2 (P + E_P) <=
+//     lo2 (Z - E_Z)^2 and inconsistent when (|dz| - E_dz)^2 (P - E_P) > hi2 (Z + E_Z)^2, each side
+//     given 8u of rounding slack; otherwise -1.
+// Every test is written so that a NaN operand fails it (-> -1, the float64 path decides).
+// float32 neighbours of a double: the largest float <= x / the smallest float >= x (NaN stays NaN,
+// values past FLT_MAX go to FLT_MAX / +inf)
+__device__ __forceinline__ float float_step(float f, bool up) {  // adjacent float toward +-inf (f finite)
+    if (f == 0.0f) return up ? 0x1p-149f : -0x1p-149f;
+    const uint32_t b = __float_as_uint(f);
+    return __uint_as_float((f > 0.0f) == up ? b + 1 : b - 1);
+}
+__device__ __forceinline__ float round_down_f(double x) {
+    const float f = (float)x;
+    return (double)f > x ? float_step(f, false) : f;
+}
+__device__ __forceinline__ float round_up_f(double x) {
+    const float f = (float)x;
+    return (double)f < x ? float_step(f, true) : f;
+}
+struct Pix32 {
+    float p[3], m;     // pw as float32, max |pw| (rounded up)
+    float lo2, hi2;    // the band bounds, rounded down / up
+    float zlo, zhi;    // zmax rounded down / up
+};
+__device__ inline int pixel_decide32(const float* __restrict__ tgt, int W, int H, float wm1, float hm1, const ConfFrame& ft,
+                                     const Pix32& px, float dmf) {
+    constexpr float u = 0x1p-24f;
+    const float* T = ft.Tf;
+    const float X = __builtin_fmaf(T[0], px.p[0], __builtin_fmaf(T[1], px.p[1], __builtin_fmaf(T[2], px.p[2], T[3])));
+    const float Y = __builtin_fmaf(T[4], px.p[0], __builtin_fmaf(T[5], px.p[1], __builtin_fmaf(T[6], px.p[2], T[7])));
+    const float Z = __builtin_fmaf(T[8], px.p[0], __builtin_fmaf(T[9], px.p[1], __builtin_fmaf(T[10], px.p[2], T[11])));
+    const float EX = __builtin_fmaf(ft.ea[0], px.m, ft.eb[0]);
+    const float EY = __builtin_fmaf(ft.ea[1], px.m, ft.eb[1]);
+    const float EZ = __builtin_fmaf(ft.ea[2], px.m, ft.eb[2]);
+    // (comparisons of computed sums are made strict where rounding could otherwise flip them:
+    // RN(x) > c implies x > c and RN(x) < c implies x < c for a representable c)
+    const float zl = Z - EZ, zh = Z + EZ;
+    if (Z <= -EZ) return 0;           // Z <= 0 certain
+    if (zl > px.zhi) return 0;        // Z > zmax certain
+    if (!(zl > 0.0f && zh < px.zlo && EZ <= 0.125f * Z && Z >= 1e-6f)) return -1;
+    const float inv = __builtin_amdgcn_rcpf(Z);
+    const float qx = (X * ft.fxf) * inv, qy = (Y * ft.fyf) * inv;
+    const float uu = qx + ft.cxf, vv = qy + ft.cyf;
+    const float irl = inv * (1.0f + 2.0f * EZ * inv);  // >= 1 / (Z - E_Z) for E_Z <= Z / 8
+    const float ezr = EZ * irl;
+    const float Eu = __builtin_fabsf(ft.fxf) * inv * (EX + (__builtin_fabsf(X) + EX) * ezr) * (1.0f + 16.0f * u) +
+                     5.0f * u * __builtin_fabsf(qx) + 2.0f * u * __builtin_fabsf(uu);
+    const float Ev = __builtin_fabsf(ft.fyf) * inv * (EY + (__builtin_fabsf(Y) + EY) * ezr) * (1.0f + 16.0f * u) +
+                     5.0f * u * __builtin_fabsf(qy) + 2.0f * u * __builtin_fabsf(vv);
+    if ((uu + Eu < 0.0f) | (uu - Eu > wm1) | (vv + Ev < 0.0f) | (vv - Ev > hm1)) return 0;  // out of range certain
+    const float fu0 = __builtin_floorf(uu), fv0 = __builtin_floorf(vv);
+    const float ru = uu - fu0, rv = vv - fv0;  // exact (|uu|, |vv| < 2^23 here)
+    if (!((ru >= Eu) & (ru + Eu < 1.0f) & (rv >= Ev) & (rv + Ev < 1.0f) & (uu < 0x1p22f) & (vv < 0x1p22f))) return -1;
+    const int u0 = (int)fu0, v0 = (int)fv0;
+    if (!((u0 >= 0) & (u0 + 1 < W) & (v0 >= 0) & (v0 + 1 < H))) return 0;
+    float2 ab, cd;
+    const float* row0 = tgt + (int64_t)v0 * W + u0;
+    __builtin_memcpy(&ab, row0, sizeof(float2));
+    __builtin_memcpy(&cd, row0 + W, sizeof(float2));
+    const float Ia = ab.x, Ib = ab.y, Ic = cd.x, Id = cd.y;
+    const bool taps = (Ib > 0) & (Ib <= dmf) & (Ia > 0) & (Ia <= dmf) & (Ic > 0) & (Ic <= dmf) & (Id > 0) & (Id <= dmf);
+    if (!taps) return 0;
+    const float gu = (fu0 + 1.0f) - uu, gv = (fv0 + 1.0f) - vv, fu = ru, fv = rv;
+    const float zf = __builtin_fmaf(fu * fv, Id, __builtin_fmaf(gu * fv, Ic, __builtin_fmaf(fu * gv, Ib, (gu * gv) * Ia)));
+    const float Edz = EZ + Eu * (__builtin_fabsf(Ib - Ia) + __builtin_fabsf(Id - Ic)) +
+                      Ev * (__builtin_fabsf(Ic - Ia) + __builtin_fabsf(Id - Ib)) + 8.0f * u * zf;
+    const float dz = __builtin_fabsf(Z - zf);
+    const float P = __builtin_fmaf(X, X, __builtin_fmaf(Y, Y, Z * Z));
+    const float EP = 2.0f * (__builtin_fabsf(X) * EX + __builtin_fabsf(Y) * EY + Z * EZ) + (EX * EX + EY * EY + EZ * EZ) +
+                     8.0f * u * P;
+    const float a1 = dz + Edz;
+    if (a1 * a1 * (P + EP) * (1.0f + 16.0f * u) <= px.lo2 * (zl * zl) * (1.0f - 16.0f * u)) return 1;
+    const float a0 = dz - Edz;
+    if ((a0 > 0.0f) & (a0 * a0 * (P - EP) * (1.0f - 16.0f * u) > px.hi2 * (zh * zh) * (1.0f + 16.0f * u))) return 2;
+    return -1;
 }
 
 // depth_to_pointcloud_numpy for one pixel: returns 0 when the ref pixel is not in (0, depth_max].
@@ -231,21 +331,27 @@ __device__ inline int ref_point(const ConfFrame& fr, int u, int v, float dref, d
 
 // d2_max: the largest double d2 with (float)sqrt(d2) <= threshold (host, exact); the reference's
 // `err <= threshold` on the float32 error map is d2 <= d2_max (sqrt and both roundings monotone).
+// STATS: count the pairs per deciding stage into st[4] (pairs, float32 prefilter, float64 filter,
+// float64 back-projection) -- mqr_confidence_stats.
+template <bool STATS>
 __global__ __launch_bounds__(256) void k_confidence(const float* __restrict__ depths, int N, int H, int W,
                                                     const ConfFrame* __restrict__ fr, int ref_begin, int r,
                                                     double depth_max, double d2_max, double sd,
-                                                    double* __restrict__ conf, int32_t* __restrict__ valid) {
+                                                    double* __restrict__ conf, int32_t* __restrict__ valid,
+                                                    unsigned long long* __restrict__ st) {
     const int64_t HW = (int64_t)H * W;
     // (grouping the grid as G reference frames per pixel tile, for L2 reuse of the neighbours' taps,
     // measured no faster for G = 4 ... 64)
     const int rloc = blockIdx.y;
     const int ref = ref_begin + rloc;
-    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= HW) return;
+    const int64_t p0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (!STATS && p0 >= HW) return;  // (STATS: the wave reductions below need every lane)
+    const int64_t p = p0 < HW ? p0 : HW - 1;
     const int u = (int)(p % W), v = (int)(p / W);
     double pw[3];
     int nv = 0, nc = 0;
-    if (ref_point(fr[ref], u, v, depths[(int64_t)ref * HW + p], depth_max, pw)) {
+    uint32_t n_pairs = 0, n_f32 = 0, n_tail = 0;
+    if (p0 < HW && ref_point(fr[ref], u, v, depths[(int64_t)ref * HW + p], depth_max, pw)) {
         const int lo = max(0, ref - r), hi = min(N, ref + r + 1);
         // the consistency band (pixel_decide): the neighbours' largest defect terms, then per pixel
         double c1 = 0.0, c0 = 0.0;
@@ -262,13 +368,48 @@ __global__ __launch_bounds__(256) void k_confidence(const float* __restrict__ de
         const double zmax = fmin(depth_max, 0x1.fffffffffffffp1023);
         const float dmf = (float)depth_max;
         const double wm1 = (double)(W - 1), hm1 = (double)(H - 1);
+        Pix32 px;
+        float mx = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            px.p[i] = (float)pw[i];
+            mx = fmaxf(mx, __builtin_fabsf(px.p[i]));
+        }
+        px.m = mx * (1.0f + 0x1p-22f);
+        px.lo2 = lo2 >= 1e-12 ? round_down_f(lo2) : -1.0f;  // (no float32 underflow in the products)
+        px.hi2 = round_up_f(hi2);
+        px.zlo = round_down_f(zmax);
+        px.zhi = round_up_f(zmax);
+        const float wm1f = (float)(W - 1), hm1f = (float)(H - 1);
         for (int t = lo; t < hi; ++t) {
             if (t == ref) continue;
-            const int dcs = pixel_decide(depths + (int64_t)t * HW, W, wm1, hm1, fr[t], pw, zmax, dmf, lo2, hi2, d2_max);
+            const ConfFrame& ft = fr[t];
+            if (!ft.ok) continue;  // a neighbour that is not ok is skipped (frame_ok)
+            const float* tgt = depths + (int64_t)t * HW;
+            int dcs = pixel_decide32(tgt, W, H, wm1f, hm1f, ft, px, dmf);
+            if (STATS) {
+                ++n_pairs;
+                n_f32 += dcs >= 0;
+            }
+            if (dcs < 0) {
+                dcs = pixel_decide(tgt, W, wm1, hm1, ft, pw, zmax, dmf, lo2, hi2, d2_max);
+                if (STATS) n_tail += dcs >> 2;
+                dcs &= 3;
+            }
             nv += dcs != 0;
             nc += dcs == 1;
         }
     }
+    if (STATS) {
+        const uint32_t t[3] = {n_pairs, n_f32, n_tail};
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            uint32_t v = t[i];
+            for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+            if ((threadIdx.x & 63) == 0 && v) atomicAdd(&st[i == 0 ? 0 : i == 1 ? 1 : 3], (unsigned long long)v);
+        }
+    }
+    if (p0 >= HW) return;
     const int64_t o = (int64_t)rloc * HW + p;
     valid[o] = nv;
     conf[o] = nv == 0 ? 0.0 : (double)nc / (double)nv;
@@ -359,6 +500,20 @@ void fill_frame(const float* K, const float* Tcw, const float* Tinv, double sd, 
     const double c1 = dR * (1.0 + eR), c0 = (dT + zterm) * (1.0 + eR) + eR * (sd + 1.0) + 1e-9;
     f.c1 = finite && std::isfinite(c1) ? c1 : INFINITY;
     f.c0 = finite && std::isfinite(c0) ? c0 : INFINITY;
+    // float32 prefilter (pixel_decide32): the given float32 entries, and the error bound terms rounded
+    // up (8u = 2^-21; a non-finite entry makes them inf / NaN, which sends every pair to float64)
+    f.fxf = K[0];
+    f.fyf = K[4];
+    f.cxf = K[2];
+    f.cyf = K[5];
+    for (int k = 0; k < 12; ++k) f.Tf[k] = Tinv ? Tinv[k] : 0.0f;
+    for (int r = 0; r < 3; ++r) {
+        const double a = ((double)std::fabs(f.Tf[4 * r]) + std::fabs(f.Tf[4 * r + 1]) + std::fabs(f.Tf[4 * r + 2])) *
+                         0x1p-21 * (1.0 + 0x1p-20);
+        const double b = (double)std::fabs(f.Tf[4 * r + 3]) * 0x1p-21 * (1.0 + 0x1p-20) + 0x1p-126;
+        f.ea[r] = std::nextafter((float)a, INFINITY);
+        f.eb[r] = std::nextafter((float)b, INFINITY);
+    }
 }
 
 // Largest double d2 >= 0 with (float)sqrt(d2) <= thr (binary search over the ordered bit patterns
@@ -388,6 +543,9 @@ struct ConfCache {
     ConfFrame* dfr = nullptr;  // device frame parameters, grow-only
     ConfFrame* hfr = nullptr;  // pinned staging
     int cap = 0;
+    bool stats = false;                 // mqr_confidence_stats: count pairs per deciding stage
+    unsigned long long* dst = nullptr;  // device counters [4]
+    int64_t last[4] = {0, 0, 0, 0};     // pairs, float32 prefilter, float64 filter, float64 back-projection
 };
 ConfCache g_conf_cache[kConfDevices];
 }  // namespace
@@ -446,9 +604,25 @@ int mqr_confidence(int device, const float* depths, int depth_loc, int N, int H,
         MQR_CHECK_HIP(hipMalloc(&dconf, sizeof(double) * nref * HW));
         MQR_CHECK_HIP(hipMalloc(&dvalid, sizeof(int32_t) * nref * HW));
     }
-    hipLaunchKernelGGL(k_confidence, dim3((unsigned)((HW + 255) / 256), nref), dim3(256), 0, s, dsrc, N, H, W, dfr,
-                       ref_begin, frame_range, depth_max, d2max, sd, dconf, dvalid);
+    if (cc.stats) {
+        if (!cc.dst) MQR_CHECK_HIP(hipMalloc(&cc.dst, 4 * sizeof(unsigned long long)));
+        MQR_CHECK_HIP(hipMemsetAsync(cc.dst, 0, 4 * sizeof(unsigned long long), s));
+        hipLaunchKernelGGL(k_confidence<true>, dim3((unsigned)((HW + 255) / 256), nref), dim3(256), 0, s, dsrc, N, H, W,
+                           dfr, ref_begin, frame_range, depth_max, d2max, sd, dconf, dvalid, cc.dst);
+    } else {
+        hipLaunchKernelGGL(k_confidence<false>, dim3((unsigned)((HW + 255) / 256), nref), dim3(256), 0, s, dsrc, N, H, W,
+                           dfr, ref_begin, frame_range, depth_max, d2max, sd, dconf, dvalid, nullptr);
+    }
     MQR_CHECK_HIP(hipGetLastError());
+    if (cc.stats) {
+        unsigned long long h[4];
+        MQR_CHECK_HIP(hipMemcpyAsync(h, cc.dst, sizeof(h), hipMemcpyDeviceToHost, s));
+        MQR_CHECK_HIP(hipStreamSynchronize(s));
+        cc.last[0] = (int64_t)h[0];
+        cc.last[1] = (int64_t)h[1];
+        cc.last[3] = (int64_t)h[3];
+        cc.last[2] = cc.last[0] - cc.last[1] - cc.last[3];
+    }
     if (out_loc != MQR_DEVICE) {
         MQR_CHECK_HIP(hipMemcpyAsync(conf, dconf, sizeof(double) * nref * HW, hipMemcpyDeviceToHost, s));
         MQR_CHECK_HIP(hipMemcpyAsync(valid, dvalid, sizeof(int32_t) * nref * HW, hipMemcpyDeviceToHost, s));
@@ -459,6 +633,16 @@ int mqr_confidence(int device, const float* depths, int depth_loc, int N, int H,
         (void)hipFree(dvalid);
     }
     if (dd) (void)hipFree(dd);
+    return 0;
+}
+
+int mqr_confidence_stats(int device, int enable, int64_t* last4) {
+    MQR_REQUIRE(device >= 0 && device < kConfDevices, "bad device");
+    ConfCache& cc = g_conf_cache[device];
+    std::lock_guard<std::mutex> lock(cc.mu);
+    if (enable >= 0) cc.stats = enable != 0;
+    if (last4)
+        for (int i = 0; i < 4; ++i) last4[i] = cc.last[i];
     return 0;
 }
 

@@ -80,3 +80,37 @@ def test_confidence_band_edges_vs_oracle(thr, dmax):
         assert np.array_equal(conf[i], oc), i
     if thr == 0.08:
         assert valid.max() > 0 and 0 < conf.mean() < 1
+
+
+def test_confidence_float32_prefilter_stages_and_static_camera():
+    """The float32 prefilter (pixel_decide32) decides most pairs and defers the uncertain ones: the
+    stage counts add up, the maps are identical with counting on or off, and a static camera (every
+    neighbour's projection lands exactly on integer pixel coordinates: every floor() is uncertain in
+    float32, so every pair must take the float64 path) still matches the oracle bit for bit."""
+    import ctypes
+    from mqr import _lib, synthetic
+    from mqr.confidence import confidence_maps
+    seq = synthetic.make_sequence("room", n=12, height=120, width=160, f=131.25, noise=True, seed=21)
+    Ti = np.linalg.inv(seq["T_cw"])
+    last = np.zeros(4, np.int64)
+    base = confidence_maps(seq["depth"], seq["K"], seq["T_cw"], Ti, 0, 12, 10, 4.0, 0.08)
+    _lib.call("mqr_confidence_stats", 0, 1, None)
+    try:
+        counted = confidence_maps(seq["depth"], seq["K"], seq["T_cw"], Ti, 0, 12, 10, 4.0, 0.08)
+        _lib.call("mqr_confidence_stats", 0, -1, _lib.ptr(last, _lib._i64p))
+    finally:
+        _lib.call("mqr_confidence_stats", 0, 0, None)
+    assert np.array_equal(base[0], counted[0]) and np.array_equal(base[1], counted[1])
+    pairs, f32, f64, tail = (int(x) for x in last)
+    assert pairs > 0 and f32 + f64 + tail == pairs and f64 >= 0
+    assert f32 > 0.9 * pairs, last
+    # static camera: all poses equal (noise differs per frame)
+    T = np.repeat(seq["T_cw"][:1], 6, axis=0).astype(np.float32)
+    Ts = np.linalg.inv(T.astype(np.float64)).astype(np.float32)
+    d = seq["depth"][:6]
+    conf, valid = confidence_maps(d, seq["K"][:6], T, Ts, 0, 6, 3, 4.0, 0.08)
+    for i in range(6):
+        oc, ov = oracle.confidence(d, seq["K"][:6], T, Ts, i, 3, 4.0, 0.08)
+        assert np.array_equal(valid[i], ov), i
+        assert np.array_equal(conf[i], oc), i
+    assert valid.max() > 0
