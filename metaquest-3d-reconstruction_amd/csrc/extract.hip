@@ -824,18 +824,18 @@ __device__ __forceinline__ void mc_emit_tri(int i, const uint4* rows, const uint
 
 // Emission of a block with vertices or triangles, from the count pass's row records: vertices
 // (positions and normals from tsdf values gathered from the pool) and triangles at the offsets of
-// the scan, in (block, voxel, edge) / (block, cube, triangle) order.
+// the scan, in (block, voxel, edge) / (block, cube, triangle) order.  role 0: both (one workgroup per
+// block, vertices then triangles); 1: vertices only; 2: triangles only (k_mc_emit_split: a vertex and
+// a triangle workgroup per block, each with its own chain of dependent loads in flight).
 // (A merged vertex / triangle item loop and 512-thread blocks were measured: no change)
-template <int R, int NT = kMcThreads>
-__global__ __launch_bounds__(NT) void k_mc_emit(const int32_t* __restrict__ nb, const uint64_t* __restrict__ bkeys,
-                                                        const float2* __restrict__ pool, float voxel_size,
-                                                        const int32_t* __restrict__ vcount,
-                                                        const int32_t* __restrict__ tcount,
-                                                        const int32_t* __restrict__ voff,
-                                                        const int32_t* __restrict__ toff,
-                                                        const uint4* __restrict__ rows4,
-                                                        const uint32_t* __restrict__ rowNt, float* pos, float* nrm,
-                                                        int32_t* tri, int64_t cap_v, int64_t cap_t, int diag = 0) {
+template <int R, int NT>
+__device__ __forceinline__ void mc_emit_block(int64_t b, int role, const int32_t* __restrict__ nb,
+                                              const uint64_t* __restrict__ bkeys, const float2* __restrict__ pool,
+                                              float voxel_size, const int32_t* __restrict__ vcount,
+                                              const int32_t* __restrict__ tcount, const int32_t* __restrict__ voff,
+                                              const int32_t* __restrict__ toff, const uint4* __restrict__ rows4,
+                                              const uint32_t* __restrict__ rowNt, float* pos, float* nrm, int32_t* tri,
+                                              int64_t cap_v, int64_t cap_t) {
     using M = Mc<R, 1>;
     static_assert(NT >= 256, "one thread per triangle-table row");
     __shared__ uint32_t rowN[M::S2];
@@ -843,39 +843,67 @@ __global__ __launch_bounds__(NT) void k_mc_emit(const int32_t* __restrict__ nb, 
     __shared__ int32_t nbrow[27], nbvoff[27];
     __shared__ uint64_t triP[256];  // the triangle tables: lane-divergent lookups in a dependent loop
     __shared__ uint32_t triC[32];
-    const int64_t b = blockIdx.x;
-    const int nvb = vcount[b], ntb = tcount[b];
+    const int nvb = role == 2 ? 0 : vcount[b], ntb = role == 1 ? 0 : tcount[b];
     if (nvb == 0 && ntb == 0) return;  // block-uniform: nothing to write
     const int32_t vb0 = voff[b], tb0 = toff[b];
     // outputs past the speculative capacity: the host re-runs this pass into exact buffers
     // (int32 offsets: a total past 2^31 wraps them negative -- the host then fails the call after
     // this speculative pass, which must not have written before the buffers' start)
-    if (vb0 < 0 || tb0 < 0 || (int64_t)vb0 + nvb > cap_v || (int64_t)tb0 + ntb > cap_t) return;
+    if (vb0 < 0 || tb0 < 0 || (int64_t)vb0 + vcount[b] > cap_v || (int64_t)tb0 + tcount[b] > cap_t) return;
     const int tid = threadIdx.x;
-    if (tid < 256) triP[tid] = mqr_tri_packed[tid];
-    if (tid < 32) triC[tid] = mqr_tri_count_packed[tid];
+    if (ntb) {
+        if (tid < 256) triP[tid] = mqr_tri_packed[tid];
+        if (tid < 32) triC[tid] = mqr_tri_count_packed[tid];
+    }
     if (tid < 27) {
         const int32_t q = nb[b * 27 + tid];
         nbrow[tid] = q;
-        nbvoff[tid] = q >= 0 ? voff[q] : 0;
+        nbvoff[tid] = ntb && q >= 0 ? voff[q] : 0;
     }
     for (int r = tid; r < M::R2; r += NT) rows[r] = rows4[b * M::R2 + r];
     if (ntb)
         for (int q = tid; q < M::S2; q += NT) rowN[q] = rowNt[b * M::S2 + q];
     __syncthreads();
-    const int lane = tid & 63;
-    const uint32_t pres = (uint32_t)__ballot(lane < 27 && nbrow[lane < 27 ? lane : 0] >= 0);
-
-    int xb, yb, zb;
-    unpack_key(bkeys[b], xb, yb, zb);
-#if MQR_AB  // A/B library only: timing of one half of the pass (wrong output on purpose)
-    if (diag != 2)
-#endif
-    for (int i = tid; i < nvb; i += NT) mc_emit_vertex<M>(i, rows, nbrow, pool, pres, xb, yb, zb, voxel_size, vb0, pos, nrm);
-#if MQR_AB
-    if (diag != 1)
-#endif
+    if (nvb) {
+        const int lane = tid & 63;
+        const uint32_t pres = (uint32_t)__ballot(lane < 27 && nbrow[lane < 27 ? lane : 0] >= 0);
+        int xb, yb, zb;
+        unpack_key(bkeys[b], xb, yb, zb);
+        for (int i = tid; i < nvb; i += NT)
+            mc_emit_vertex<M>(i, rows, nbrow, pool, pres, xb, yb, zb, voxel_size, vb0, pos, nrm);
+    }
     for (int i = tid; i < ntb; i += NT) mc_emit_tri<M>(i, rows, rowN, triC, triP, nbrow, nbvoff, rows4, vb0, tb0, tri);
+}
+
+// diag (A/B library, MQR_EMIT_DIAG): 1 vertices only, 2 triangles only (timing of one half, wrong output)
+template <int R, int NT = kMcThreads>
+__global__ __launch_bounds__(NT) void k_mc_emit(const int32_t* __restrict__ nb, const uint64_t* __restrict__ bkeys,
+                                                const float2* __restrict__ pool, float voxel_size,
+                                                const int32_t* __restrict__ vcount, const int32_t* __restrict__ tcount,
+                                                const int32_t* __restrict__ voff, const int32_t* __restrict__ toff,
+                                                const uint4* __restrict__ rows4, const uint32_t* __restrict__ rowNt,
+                                                float* pos, float* nrm, int32_t* tri, int64_t cap_v, int64_t cap_t,
+                                                int diag = 0) {
+#if !MQR_AB
+    diag = 0;
+#endif
+    mc_emit_block<R, NT>(blockIdx.x, diag, nb, bkeys, pool, voxel_size, vcount, tcount, voff, toff, rows4,
+                         rowNt, pos, nrm, tri, cap_v, cap_t);
+}
+
+// Workgroup 2b emits block b's vertices, 2b + 1 its triangles.
+template <int R, int NT = kMcThreads>
+__global__ __launch_bounds__(NT) void k_mc_emit_split(const int32_t* __restrict__ nb, const uint64_t* __restrict__ bkeys,
+                                                      const float2* __restrict__ pool, float voxel_size,
+                                                      const int32_t* __restrict__ vcount,
+                                                      const int32_t* __restrict__ tcount,
+                                                      const int32_t* __restrict__ voff, const int32_t* __restrict__ toff,
+                                                      const uint4* __restrict__ rows4,
+                                                      const uint32_t* __restrict__ rowNt, float* pos, float* nrm,
+                                                      int32_t* tri, int64_t cap_v, int64_t cap_t, int diag = 0) {
+    (void)diag;
+    mc_emit_block<R, NT>(blockIdx.x >> 1, 1 + (blockIdx.x & 1), nb, bkeys, pool, voxel_size, vcount, tcount, voff, toff,
+                         rows4, rowNt, pos, nrm, tri, cap_v, cap_t);
 }
 
 // ---------------------------------------------------------------- point cloud (R = 8 / 16)
@@ -1296,10 +1324,13 @@ template <int RT, class... A>
 static void launch_mc_emit(const mqr_vbg* v, int64_t n, A... args) {
 #if MQR_AB  // MQR_EMIT_DIAG=1: vertices only, 2: triangles only (timing diagnostics)
     static const int diag = getenv("MQR_EMIT_DIAG") ? atoi(getenv("MQR_EMIT_DIAG")) : 0;
-    hipLaunchKernelGGL((k_mc_emit<RT>), dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, args..., diag);
 #else
-    hipLaunchKernelGGL((k_mc_emit<RT>), dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, args...);
+    constexpr int diag = 0;
 #endif
+    if (v->extract_mode == 1)  // a vertex and a triangle workgroup per block
+        hipLaunchKernelGGL((k_mc_emit_split<RT>), dim3((unsigned)(2 * n)), dim3(kMcThreads), 0, v->stream, args..., diag);
+    else
+        hipLaunchKernelGGL((k_mc_emit<RT>), dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, args..., diag);
 }
 
 template <int RT>

@@ -1107,6 +1107,7 @@ int mqr_vbg_set_variant(mqr_vbg* v, int variant) {
     v->xcd_order = (variant & 0x8000) != 0;   // bit 15: spatial per-XCD groups (k_xcd_order, A/B)
     v->touch_ppt = (variant & 0x10000) ? 1 : 2;  // bit 16: one stride-4 pixel per touch thread (A/B)
     v->touch_frame = (variant & 0x30000) == 0;   // bit 17: the round-3 strip touch (k_touch<2>) instead of k_touch_frame
+    v->extract_mode = (variant >> 20) & 0xf;      // bits 20-23: mesh emission configuration (tools/ab_extract.py)
     return 0;
 }
 

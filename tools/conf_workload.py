@@ -14,6 +14,7 @@ def main():
     import argparse
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--stats", action="store_true", help="also one counted call: pairs per deciding stage")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -39,10 +40,19 @@ def main():
         torch.cuda.synchronize()
         if i:
             times.append((time.perf_counter() - t0) * 1e3)
+    stages = None
+    if a.stats:
+        last = np.zeros(4, np.int64)
+        _lib.call("mqr_confidence_stats", 0, 1, None)
+        _lib.call("mqr_confidence", 0, ctypes.c_void_p(d.data_ptr()), 1, B, H, W, _lib.ptr(K32, _lib._f32p),
+                  _lib.ptr(T_cw, _lib._f32p), _lib.ptr(T_ci, _lib._f32p), None, 0, B, 10, 4.0, 0.08,
+                  ctypes.c_void_p(conf.data_ptr()), ctypes.c_void_p(valid.data_ptr()), 1)
+        _lib.call("mqr_confidence_stats", 0, 0, _lib.ptr(last, _lib._i64p))
+        stages = dict(zip(("pairs", "float32_prefilter", "float64_filter", "float64_backprojection"), last.tolist()))
     digest = hashlib.sha256(conf.cpu().numpy().tobytes() + valid.cpu().numpy().tobytes()).hexdigest()[:16]
     print(json.dumps({"ms_median": sorted(times)[len(times) // 2], "reps": a.reps, "valid_mean": float(valid.float().mean()),
                       "conf_mean": float(conf.mean()), "digest": digest,
-                      "single": os.environ.get("MQR_CONF_SINGLE") is not None}))
+                      "single": os.environ.get("MQR_CONF_SINGLE") is not None, "stages": stages}))
 
 
 if __name__ == "__main__":

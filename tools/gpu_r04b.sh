@@ -30,3 +30,7 @@ P
 MQR_HIP_LIB=tools/_ab/libmqr_ab.so timeout -k 10 300 python tools/ab_integrate.py --variants 0,23,24,25,26,0x20000 --rounds 7 --check \
   > gpurun_out/r04b_ab.json 2> gpurun_out/r04b_ab.err || { tail -20 gpurun_out/r04b_ab.err; exit 1; }
 cat gpurun_out/r04b_ab.json
+timeout -k 10 200 python tools/conf_workload.py --reps 5 --stats > gpurun_out/r04b_conf.json 2> gpurun_out/r04b_conf.err || { tail -20 gpurun_out/r04b_conf.err; exit 1; }
+cat gpurun_out/r04b_conf.json
+timeout -k 10 200 python tools/ab_extract.py --modes 0,1 --reps 15 > gpurun_out/r04b_abx.json 2> gpurun_out/r04b_abx.err || { tail -20 gpurun_out/r04b_abx.err; exit 1; }
+cat gpurun_out/r04b_abx.json
