@@ -154,13 +154,14 @@ def conf_binding():
     tools/conf_workload.py -> profiles/*_pmc_confidence.json): VALU issue share of the launch's
     cycles (fp64 instructions weighted at half rate), texture-addresser busy share, occupancy."""
     import glob
+    tag = build_tag(1)
     for path in reversed(sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_confidence.json")))):
         try:
             rec = json.load(open(path))
         except (OSError, ValueError):
             continue
         d = rec.get("derived")
-        if not d:
+        if not d or rec.get("confidence_src") != tag:  # only a record of this build's kernel
             continue
         valu, ta = d.get("valu_issue_frac_f64_at_half_rate"), d.get("ta_busy_frac")
         bound = ("VALU issue (fp64 at half rate)" if valu is not None and (ta is None or valu >= ta)
@@ -589,20 +590,32 @@ def meshfilter_leg(vbg, thr, min_count=2000, reps=3):
             "note": "mqr_mesh_filter_components, device-resident mesh in/out, wall time of the call, median"}
 
 
-def pmc_traffic(H, W, frames):
+def build_tag(which):
+    from mqr import _lib
+    try:
+        return _lib.build_tag(which)
+    except Exception:  # noqa: BLE001
+        return None
+
+
+def pmc_traffic(H, W, frames, variant_ran):
     """HBM bytes per integrate launch from the committed rocprofv3 --pmc passes of this workload
-    (tools/traffic_workload.py + tools/pmc_summary.py; FETCH_SIZE/WRITE_SIZE calibrated on k_pack)."""
+    (tools/traffic_workload.py + tools/pmc_summary.py; FETCH_SIZE/WRITE_SIZE calibrated on k_pack).
+    Quoted only from a record of THIS build's integrate sources (mqr_build_tag) and kernel variant:
+    a record of another kernel would describe a kernel that did not run (then None)."""
     import glob
+    tag = build_tag(0)
     recs = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
     for path in reversed(recs):
         try:
             rec = json.load(open(path))
             wl = rec["workload"]
-            if (wl["H"], wl["W"], wl["frames"]) == (H, W, frames):
+            if (wl["H"], wl["W"], wl["frames"]) == (H, W, frames) and rec.get("integrate_src") == tag and \
+                    rec.get("variant_ran") == variant_ran:
                 return rec["traffic_bytes_per_launch"], os.path.relpath(path, ROOT)
         except (OSError, KeyError, ValueError):
             continue
-    return None, None
+    return None, f"no counter record of this build (integrate_src {tag}, variant {variant_ran})"
 
 
 def gather_ceiling(avg_launch_ms, gathers_per_launch, cus, pattern="brick_x2"):
@@ -627,12 +640,13 @@ def gather_ceiling(avg_launch_ms, gathers_per_launch, cus, pattern="brick_x2"):
     return None
 
 
-def pmc_binding(avg_launch_ms):
+def pmc_binding(avg_launch_ms, variant_ran):
     """The integrate kernel's binding resource from the committed rocprofv3 counter passes of the
     default kernel (tools/pmc_ab.sh -> profiles/*_pmc_integrate_counters.json, entry "v0:..."):
     busy fractions of the texture addresser (TA), L1 tag lookups per CU-cycle, VALU issue share.
     The counters are per launch of this same workload; the live launch time rescales the rate."""
     import glob
+    tag = build_tag(0)
     for path in reversed(sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_integrate_counters.json")))):
         try:
             rec = json.load(open(path))
@@ -640,7 +654,9 @@ def pmc_binding(avg_launch_ms):
             continue
         for name, r in rec.items():
             d = r.get("derived")
-            if not name.startswith("v0:") or not d:
+            # only the default variant's counters of THIS build's integrate sources
+            if not name.startswith("v0:") or not d or r.get("integrate_src") != tag or \
+                    r.get("variant_ran") != variant_ran:
                 continue
             live_cycles = avg_launch_ms * 1e-3 * d["clock_ghz"] * 1e9 if avg_launch_ms else None
             return {"bound": "vector-memory gather path (TA address / TCP tag lookups)",
@@ -1132,7 +1148,11 @@ def main():
         if extras.get("confidence") is not None and args.conf_cpu_seconds > 0:
             extras["confidence"]["cpu_baseline"] = confidence_cpu(host_depth, K, T, args, args.conf_cpu_seconds)
 
-    traffic, traffic_src = pmc_traffic(H, W, B)
+    from mqr import _lib
+    _vr = ctypes.c_int(-1)
+    _lib.call("mqr_vbg_last_kernel", vbg.handle, ctypes.byref(_vr))
+    variant_ran = _vr.value
+    traffic, traffic_src = pmc_traffic(H, W, B, variant_ran)
 
     if rank == 0:
         total_frames = (2 * args.strong_frames if strong else B * world) * args.steps
@@ -1177,7 +1197,8 @@ def main():
             "raycast": extras.get("raycast"),
             "meshfilter": extras.get("meshfilter"),
             "host_input_frames_per_s": extras.get("host_input_frames_per_s"),
-            "roofline_binding": dict(pmc_binding(avg_ms) or {}, gather_ceiling=gather_ceiling(
+            "build": {"integrate_src": build_tag(0), "confidence_src": build_tag(1), "integrate_variant": variant_ran},
+            "roofline_binding": dict(pmc_binding(avg_ms, variant_ran) or {}, gather_ceiling=gather_ceiling(
                 avg_ms, st["frame_blocks"] * args.block_resolution ** 3 / 64 / launches,
                 torch.cuda.get_device_properties(local).multi_processor_count)),
             "roofline": {"bound": "hbm", "kernel": "k_integrate_lean", "achieved": achieved, "peak": HBM_PEAK_GBS,

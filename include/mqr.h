@@ -32,6 +32,12 @@ typedef struct mqr_scene mqr_scene;  /* triangle-mesh ray-casting scene (device 
 typedef struct mqr_comm mqr_comm;    /* RCCL communicator of one rank (one process per GPU) */
 
 int mqr_version(void);
+/* Build tags: which 0 = a hash of the integrate sources (vbg.hip, vbg_kernels.hpp, mqr_common.hpp),
+ * 1 = of the confidence sources, as compiled into this library; counter records under profiles/ carry
+ * the tag of the build they measured (bench.py quotes only matching ones).  mqr_vbg_last_kernel: the
+ * integrate variant (mqr_vbg_set_variant numbering) the volume's last launch actually used. */
+int mqr_build_tag(int which, char* buf, int cap);
+int mqr_vbg_last_kernel(mqr_vbg* v, int* variant);
 const char* mqr_last_error(void);
 int mqr_device_count(int* n);
 

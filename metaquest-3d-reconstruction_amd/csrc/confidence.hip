@@ -550,6 +550,13 @@ struct ConfCache {
 ConfCache g_conf_cache[kConfDevices];
 }  // namespace
 
+#ifndef MQR_SRC_TAG
+#define MQR_SRC_TAG "untagged"
+#endif
+namespace mqr {
+const char* confidence_src_tag() { return MQR_SRC_TAG; }
+}  // namespace mqr
+
 extern "C" {
 
 int mqr_confidence(int device, const float* depths, int depth_loc, int N, int H, int W, const float* K,

@@ -170,6 +170,7 @@ struct mqr_vbg {
     // profiling
     int touch_ppt = 2;  // stride-4 pixels per k_touch thread (strip touch, variant bits 16 / 17)
     bool touch_frame = true;  // k_touch_frame: a frame per workgroup (default)
+    int last_var = -1;        // integrate variant of the last launch, after fallbacks (mqr_vbg_last_kernel)
     int extract_mode = 0;     // mesh emission configuration (variant bits 20-23; 1 = vertex / triangle split)
     bool profile = false;
     bool profile_touch = false;  // mqr_vbg_profile level 2: also time the touch launches

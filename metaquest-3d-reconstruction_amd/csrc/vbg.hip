@@ -15,6 +15,7 @@
 // touch(b+1) runs on a second stream while integrate(b) runs (double-buffered batch state).
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <mutex>
 #include <unordered_map>
@@ -384,6 +385,7 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
     if (var == 0 && !(v->R == 16 && win8_ok)) var = 4;
     if (var >= 13 && !win8_ok) var = 4;  // (23-26: 8-byte windows too)
     if (v->R != 16 && v->R != 8) var = 1;
+    v->last_var = var;
     const int32_t* bad_list = v->bad[p];
     const bmask_t* bad_mask = reinterpret_cast<const bmask_t*>(v->bad[p] + v->list_cap);
     int* bad_count = counters + kBadCount;
@@ -681,6 +683,8 @@ static int touch_batch(mqr_vbg* v, int p, const float* dbase, int64_t HW, int H,
     return 0;
 }
 
+const char* confidence_src_tag();  // confidence.hip (the A/B library has no confidence tag of its own)
+
 static const char* kNoBlock =
     "No block is touched in TSDF volume, abort integration. Please check specified parameters, especially "
     "depth_scale and voxel_size";
@@ -693,6 +697,23 @@ using namespace mqr;
 extern "C" {
 
 int mqr_version(void) { return 100; }
+
+#ifndef MQR_SRC_TAG
+#define MQR_SRC_TAG "untagged"
+#endif
+int mqr_build_tag(int which, char* buf, int cap) {
+    MQR_REQUIRE(buf && cap > 0, "null argument");
+    MQR_REQUIRE(which == 0 || which == 1, "which: 0 = integrate sources, 1 = confidence sources");
+    const std::string t = which == 0 ? std::string(MQR_AB ? "ab-" : "") + MQR_SRC_TAG : std::string(confidence_src_tag());
+    std::snprintf(buf, (size_t)cap, "%s", t.c_str());
+    return 0;
+}
+
+int mqr_vbg_last_kernel(mqr_vbg* v, int* variant) {
+    MQR_REQUIRE(v && variant, "null argument");
+    *variant = v->last_var;
+    return 0;
+}
 const char* mqr_last_error(void) { return get_error(); }
 
 int mqr_device_count(int* n) {

@@ -35,6 +35,8 @@ class MqrStats(ctypes.Structure):
 SIGNATURES = {
     "mqr_version": (ctypes.c_int, []),
     "mqr_last_error": (ctypes.c_char_p, []),
+    "mqr_build_tag": (ctypes.c_int, [ctypes.c_int, ctypes.c_char_p, ctypes.c_int]),
+    "mqr_vbg_last_kernel": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int)]),
     "mqr_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
     "mqr_device_alloc": (ctypes.c_int, [ctypes.c_int, ctypes.c_int64, ctypes.POINTER(_vp)]),
     "mqr_device_free": (ctypes.c_int, [ctypes.c_int, _vp]),
@@ -199,6 +201,13 @@ def call(name, *args):
         msg = L.mqr_last_error().decode(errors="replace")
         raise MqrError(f"{name} failed ({rc}): {msg}", rc)
     return rc
+
+
+def build_tag(which: int) -> str:
+    """Hash of the integrate (0) / confidence (1) sources compiled into the loaded library."""
+    buf = ctypes.create_string_buffer(64)
+    call("mqr_build_tag", int(which), buf, 64)
+    return buf.value.decode()
 
 
 def device_count() -> int:

@@ -50,7 +50,11 @@ def main():
         _lib.call("mqr_confidence_stats", 0, 0, _lib.ptr(last, _lib._i64p))
         stages = dict(zip(("pairs", "float32_prefilter", "float64_filter", "float64_backprojection"), last.tolist()))
     digest = hashlib.sha256(conf.cpu().numpy().tobytes() + valid.cpu().numpy().tobytes()).hexdigest()[:16]
-    print(json.dumps({"ms_median": sorted(times)[len(times) // 2], "reps": a.reps, "valid_mean": float(valid.float().mean()),
+    rec = {"confidence_src": _lib.build_tag(1), "digest": digest}
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", "conf_workload.json"), "w") as f:
+        json.dump(rec, f)
+    print(json.dumps({"confidence_src": rec["confidence_src"], "ms_median": sorted(times)[len(times) // 2], "reps": a.reps, "valid_mean": float(valid.float().mean()),
                       "conf_mean": float(conf.mean()), "digest": digest,
                       "single": os.environ.get("MQR_CONF_SINGLE") is not None, "stages": stages}))
 

@@ -35,6 +35,13 @@ for path in glob.glob("/tmp/pmcab/**/*counter_collection.csv", recursive=True):
         if "Start_Timestamp" in g:
             res[short].setdefault("duration_ns_per_pass", []).append(
                 float((g["End_Timestamp"] - g["Start_Timestamp"]).mean()))
+# the build each variant's passes measured (tools/traffic_workload.py --out pmcab_v<var>)
+for short, r in res.items():
+    try:
+        wl = json.load(open(f"gpurun_out/pmcab_v{short[1:].split(':')[0]}/workload.json"))
+        r["integrate_src"], r["variant_ran"] = wl.get("integrate_src"), wl.get("variant_ran")
+    except (OSError, ValueError):
+        pass
 # derived per-launch rates: fraction of the launch's GPU cycles each unit was busy.  GRBM_GUI_ACTIVE
 # is summed over the 8 XCDs' graphics blocks: cycles of the launch = GRBM_GUI_ACTIVE / 8 (checked
 # against the pass's own kernel duration: ~2.2 GHz under this load).

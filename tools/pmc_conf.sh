@@ -27,6 +27,10 @@ for path in glob.glob("/tmp/pmcconf/**/*counter_collection.csv", recursive=True)
         res[c] = float(g["Counter_Value"].mean())
         res.setdefault("launches", int(len(g)))
         res.setdefault("duration_ns", float((g["End_Timestamp"] - g["Start_Timestamp"]).mean()))
+try:
+    res["confidence_src"] = json.load(open("gpurun_out/conf_workload.json")).get("confidence_src")
+except (OSError, ValueError):
+    res["confidence_src"] = None
 cyc = res.get("GRBM_GUI_ACTIVE", 0.0) / 8
 if cyc:
     f64 = sum(res.get(k, 0.0) for k in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64",

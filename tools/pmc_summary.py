@@ -30,12 +30,14 @@ def main(pmc_dir, out):
     n = fetch.loc[ik, "count"]
     raw_r = fetch.loc[ik, "mean"] * 1024.0
     raw_w = write.loc[ik, "mean"] * 1024.0
+    tk = next((k for k in fetch.index if k.startswith("k_touch")), None)
     rec = {"kernel": ik, "launches": int(n),
            "fetch_bytes_per_launch_raw": raw_r, "write_bytes_per_launch_raw": raw_w,
            "read_calibration": kr, "write_calibration": kw,
            "traffic_bytes_per_launch": raw_r * kr + raw_w * kw,
            "alg_bytes_per_launch": wl["alg_bytes_total"] / wl["integrate_launches"],
-           "touch_fetch_bytes_per_launch_raw": float(fetch.loc["k_touch", "mean"] * 1024.0),
+           "touch_fetch_bytes_per_launch_raw": float(fetch.loc[tk, "mean"] * 1024.0) if tk else None,
+           "integrate_src": wl.get("integrate_src"), "variant_ran": wl.get("variant_ran"),
            "workload": wl}
     rec["traffic_over_alg"] = rec["traffic_bytes_per_launch"] / rec["alg_bytes_per_launch"]
     json.dump(rec, open(out, "w"), indent=1)

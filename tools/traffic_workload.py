@@ -12,6 +12,11 @@ sys.path.insert(0, os.path.join(ROOT, "metaquest-3d-reconstruction_amd"))
 sys.path.insert(0, ROOT)
 
 
+def ctypes_int():
+    import ctypes
+    return ctypes.c_int(-1)
+
+
 def main():
     import argparse
     ap = argparse.ArgumentParser()
@@ -53,6 +58,11 @@ def main():
             "alg_bytes_total": 16 * R3 * st["union_blocks"] + 4 * H * W * st["frames"] + 16 * st["frame_blocks"],
             "pack_blocks": U, "pack_read_bytes": U * R3 * 8, "pack_write_bytes": U * R3 * 8}
     info["variant"] = a.variant
+    from mqr import _lib
+    lv = ctypes_int()
+    _lib.call("mqr_vbg_last_kernel", vbg.handle, lv)
+    info["variant_ran"] = lv.value
+    info["integrate_src"] = _lib.build_tag(0)  # the build this record measured (bench.py quotes matching ones)
     info["voxel_frames_per_launch"] = R3 * st["frame_blocks"] / max(st["integrate_launches"], 1)
     os.makedirs(os.path.join(ROOT, "gpurun_out", a.out), exist_ok=True)
     with open(os.path.join(ROOT, "gpurun_out", a.out, "workload.json"), "w") as f:
