@@ -98,6 +98,9 @@ constexpr int kFreshBase = kFrameCounterBase + kMaxBatch;  // per-frame new (blo
 constexpr int kNumGroups = 8;                               // workgroup groups that share an XCD
 constexpr int kGroupBase = kFreshBase + kMaxBatch;          // k_xcd_order: group g = [off[g], off[g+1])
 constexpr int kCountersTotal = kGroupBase + kNumGroups + 1;
+// device counter ints: 2 parity sets, the pool counter (+ spare), 2 shadow sets (k_gate: the copies a
+// speculatively launched integrate reads)
+constexpr int kCounterInts = 4 * kCountersTotal + 8;
 
 // ---------------------------------------------------------------- volume
 }  // namespace mqr
@@ -126,6 +129,9 @@ struct mqr_vbg {
     bool sys_fence = false;
     bool int_pending[2] = {false, false};
     bool lpt_ready[2] = {false, false};  // k_lpt_order already enqueued behind this parity's touch
+    bool ctr_clean[2] = {true, true};    // the parity's counters are zero (a reset cleared them)
+    bool spec_head = true;               // first batch of a call: integrate enqueued behind its touch (k_gate)
+    int64_t batch_n_max = 0;             // largest batch list seen (grid of a speculative integrate)
     hipEvent_t touch_ev(int p) const { return sys_fence ? ev_touch_sys[p] : ev_touch[p]; }
     hipEvent_t int_ev(int p) const { return sys_fence ? ev_int_sys[p] : ev_int[p]; }
     // the event that last closed parity p's integrate on its stream: int_ev(p), or, while profiling,
@@ -197,6 +203,7 @@ struct mqr_vbg {
     int* ctr(int parity) const { return counters + parity * mqr::kCountersTotal; }
     int* hctr(int parity) const { return h_counters + parity * mqr::kCountersTotal; }
     int* pool_ctr() const { return counters + 2 * mqr::kCountersTotal; }
+    int* shadow(int parity) const { return counters + 2 * mqr::kCountersTotal + 8 + parity * mqr::kCountersTotal; }
 };
 
 // Device-resident geometry result (extract.hip, meshfilter.hip); released by mqr_geom_free.

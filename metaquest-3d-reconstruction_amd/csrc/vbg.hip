@@ -227,16 +227,24 @@ static int upload_frames(mqr_vbg* v, int p, const double* K, const double* T, co
         make_frame_params(K + 9 * idx[f], T + 16 * idx[f], &v->h_fp[p][f]);
         h_dframe[f] = dframe[f];
     }
-    MQR_CHECK_HIP(hipMemcpyAsync(v->d_fp[p], v->h_fp[p], sizeof(FrameParams) * b, hipMemcpyHostToDevice, v->stream));
-    MQR_CHECK_HIP(hipMemcpyAsync(v->d_fp[p] + v->fp_cap, h_dframe, sizeof(int64_t) * b, hipMemcpyHostToDevice,
-                                 v->stream));
+    // one command when the two arrays are close (the parameters' unused tail travels along)
+    if (v->fp_cap <= 2 * kMaxBatch) {
+        MQR_CHECK_HIP(hipMemcpyAsync(v->d_fp[p], v->h_fp[p], sizeof(FrameParams) * v->fp_cap + sizeof(int64_t) * b,
+                                     hipMemcpyHostToDevice, v->stream));
+    } else {
+        MQR_CHECK_HIP(hipMemcpyAsync(v->d_fp[p], v->h_fp[p], sizeof(FrameParams) * b, hipMemcpyHostToDevice, v->stream));
+        MQR_CHECK_HIP(hipMemcpyAsync(v->d_fp[p] + v->fp_cap, h_dframe, sizeof(int64_t) * b, hipMemcpyHostToDevice,
+                                     v->stream));
+    }
     return 0;
 }
 
 // Counters of parity p: zero (pool counter untouched).
 static int reset_batch_counters(mqr_vbg* v, int p) {
     v->lpt_ready[p] = false;
-    MQR_CHECK_HIP(hipMemsetAsync(v->ctr(p), 0, sizeof(int) * kCountersTotal, v->stream));
+    if (!v->ctr_clean[p])  // (a volume reset already zeroed them: one queued command fewer at the step head)
+        MQR_CHECK_HIP(hipMemsetAsync(v->ctr(p), 0, sizeof(int) * kCountersTotal, v->stream));
+    v->ctr_clean[p] = false;
     return 0;
 }
 
@@ -314,15 +322,18 @@ static int enqueue_lpt(mqr_vbg* v, int p) {
 
 // Launch the integrate kernel for parity p on `stream2`, after touch(p) (event) completed.
 // first_new: the pool size before this batch's allocations (its blocks start at (0, 0)).
+// spec > 0: speculative launch (first batch of a call, counters not read yet): the kernels read the
+// shadow counters k_gate fills, the grid is `spec` workgroups (they loop over the list), and the
+// caller accounts the launch in the stats once the counters confirm it (spec_commit).
 static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, int H, int W, int nframes,
-                            float depth_scale, float depth_max, float sdf_trunc, int first_new) {
-    const int64_t n = std::min<int64_t>(v->hctr(p)[kListCount], v->list_cap);
+                            float depth_scale, float depth_max, float sdf_trunc, int first_new, int64_t spec = 0) {
+    const int64_t n = spec > 0 ? spec : std::min<int64_t>(v->hctr(p)[kListCount], v->list_cap);
     if (n == 0) return 0;
     hipStream_t s = v->pipelined ? v->stream2 : v->stream;
     const unsigned grid = (unsigned)std::min<int64_t>(n, 8192);
     const int64_t* depth_frame = dframe_dev(v, p);
     const Table t = v->table(p);
-    int* counters = v->ctr(p);
+    int* counters = spec > 0 ? v->shadow(p) : v->ctr(p);
     const int32_t* list = v->lists[p];
     const bmask_t* lmask = nullptr;
     // The host has just read this batch's counters (resolve_pool_overflow waits for them), so the
@@ -342,9 +353,13 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
     const int grouped = (v->xcd_order && lmask) ? 1 : 0;
     const unsigned lean_grid =
         grouped ? (unsigned)(kNumGroups * std::min<int64_t>((3 * n / 2 + kNumGroups - 1) / kNumGroups, 1024)) : grid;
-    if (v->pipelined && touch_wait) {
+    if (v->pipelined && (touch_wait || spec > 0)) {
         MQR_CHECK_HIP(hipEventRecord(v->touch_ev(p), v->stream));
         MQR_CHECK_HIP(hipStreamWaitEvent(s, v->touch_ev(p), 0));
+    }
+    if (spec > 0) {
+        hipLaunchKernelGGL(k_gate, dim3(1), dim3(64), 0, s, v->ctr(p), v->shadow(p), nframes);
+        MQR_CHECK_HIP(hipGetLastError());
     }
     const FrameParams* fp = v->d_fp[p];
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -525,10 +540,12 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
         MQR_CHECK_HIP(hipEventRecord(e1, s));
         v->int_done[p] = e1;
         v->int_events.emplace_back(e0, e1);
-        v->stats.integrate_launches += 1;
-        v->stats.union_blocks += n;
-        for (int f = 0; f < kMaxBatch; ++f) v->stats.frame_blocks += v->hctr(p)[kFreshBase + f];
-        v->stats.frames += nframes;
+        if (spec == 0) {
+            v->stats.integrate_launches += 1;
+            v->stats.union_blocks += n;
+            for (int f = 0; f < kMaxBatch; ++f) v->stats.frame_blocks += v->hctr(p)[kFreshBase + f];
+            v->stats.frames += nframes;
+        }
     }
     if (!v->profile) {
         MQR_CHECK_HIP(hipEventRecord(v->int_ev(p), s));
@@ -652,26 +669,39 @@ constexpr int64_t kMinHeadroom = 1 << 15;
 constexpr int64_t kMinTableLive = 1 << 19;  // ensure_table sizes for 2x live keys: 2^20 slots
 constexpr int64_t kProbeLimit = 128;
 
-// Touch (and allocate) frames [0, b) of the staged parity-p batch; pool overflow resolved.
-static int touch_batch(mqr_vbg* v, int p, const float* dbase, int64_t HW, int H, int W, int b, float depth_scale,
-                       float depth_max, float sdf_trunc, float block_size, int64_t max_touch) {
-    const int64_t worst = v->pool_count + b * max_touch;
+// Touch (and allocate) frames [0, b) of the staged parity-p batch, in two phases: the launch (table
+// sized, touch and longest-first order enqueued) and the resolution (counters read, pool overflow
+// resolved, a probe-limited table that filled up undone, grown and touched again).
+struct TouchState {
+    int64_t pool_before = 0, worst = 0;
+    bool limited = false;
+};
+static int touch_batch_launch(mqr_vbg* v, int p, const float* dbase, int64_t HW, int H, int W, int b,
+                              float depth_scale, float depth_max, float sdf_trunc, float block_size, int64_t max_touch,
+                              TouchState& ts) {
+    ts.worst = v->pool_count + b * max_touch;
     const int64_t headroom = v->table_worst ? b * max_touch
                                             : std::min<int64_t>(b * max_touch,
                                                                 std::max<int64_t>(kMinHeadroom, 4 * v->batch_new_max));
     if (ensure_table(v, std::max(kMinTableLive, v->pool_count + headroom))) return 1;
-    const bool limited = v->probe_one || v->tab.cap < next_pow2(2 * worst);
-    const int64_t pool_before = v->pool_count;
+    ts.limited = v->probe_one || v->tab.cap < next_pow2(2 * ts.worst);
+    ts.pool_before = v->pool_count;
     if (touch_launch(v, p, dbase, HW, H, W, b, depth_scale, depth_max, sdf_trunc, block_size, v->table(p), 1,
-                     limited ? (v->probe_one ? 1 : std::min(kProbeLimit, v->tab.cap)) : v->tab.cap))
+                     ts.limited ? (v->probe_one ? 1 : std::min(kProbeLimit, v->tab.cap)) : v->tab.cap))
         return 1;
     // the batch order is computed while the host waits for the counters (pool growth below only
     // rewrites buffer indices, which the order does not read)
     if (v->lpt_order && enqueue_lpt(v, p)) return 1;
+    return 0;
+}
+
+static int touch_batch_resolve(mqr_vbg* v, int p, const float* dbase, int64_t HW, int H, int W, int b,
+                               float depth_scale, float depth_max, float sdf_trunc, float block_size,
+                               const TouchState& ts) {
     bool full = false;
-    if (resolve_pool_overflow(v, p, limited ? &full : nullptr)) return 1;
+    if (resolve_pool_overflow(v, p, ts.limited ? &full : nullptr)) return 1;
     if (full) {
-        if (undo_touch(v, p, pool_before) || ensure_table(v, worst) || reset_batch_counters(v, p)) return 1;
+        if (undo_touch(v, p, ts.pool_before) || ensure_table(v, ts.worst) || reset_batch_counters(v, p)) return 1;
         if (touch_launch(v, p, dbase, HW, H, W, b, depth_scale, depth_max, sdf_trunc, block_size, v->table(p), 1,
                          v->tab.cap))
             return 1;
@@ -679,11 +709,18 @@ static int touch_batch(mqr_vbg* v, int p, const float* dbase, int64_t HW, int H,
         if (resolve_pool_overflow(v, p)) return 1;
         v->stats.table_retries += 1;
     }
-    v->batch_new_max = std::max(v->batch_new_max, v->pool_count - pool_before);
+    v->batch_new_max = std::max(v->batch_new_max, v->pool_count - ts.pool_before);
     return 0;
 }
 
-const char* confidence_src_tag();  // confidence.hip (the A/B library has no confidence tag of its own)
+static int touch_batch(mqr_vbg* v, int p, const float* dbase, int64_t HW, int H, int W, int b, float depth_scale,
+                       float depth_max, float sdf_trunc, float block_size, int64_t max_touch) {
+    TouchState ts;
+    return touch_batch_launch(v, p, dbase, HW, H, W, b, depth_scale, depth_max, sdf_trunc, block_size, max_touch, ts) ||
+           touch_batch_resolve(v, p, dbase, HW, H, W, b, depth_scale, depth_max, sdf_trunc, block_size, ts);
+}
+
+const char* confidence_src_tag();  // confidence.hip
 
 static const char* kNoBlock =
     "No block is touched in TSDF volume, abort integration. Please check specified parameters, especially "
@@ -761,7 +798,7 @@ int mqr_vbg_create(float voxel_size, int block_resolution, int64_t block_count, 
     v->voxel_size = voxel_size;
     v->R = block_resolution;
     v->R3 = (int64_t)block_resolution * block_resolution * block_resolution;
-    const size_t nctr = 2 * kCountersTotal + 8;
+    const size_t nctr = kCounterInts;
     // The touch stream gets the device's highest priority: touch(b+1) shares the CUs with
     // integrate(b), and integrate(b+1) cannot be enqueued before the host has read touch(b+1)'s
     // counters -- a touch starved by integrate waves would leave the device idle at every batch.
@@ -831,12 +868,13 @@ int mqr_vbg_reset(mqr_vbg* v) {
     if (sync_all(v)) return 1;
     // one launch, ordered on `stream` before anything that uses the volume next; the pool is not
     // cleared: a block starts at (0, 0) in the batch that allocates it (launch_integrate first_new)
-    const int nctr = 2 * kCountersTotal + 8;
+    const int nctr = kCounterInts;
     const int64_t cells = std::max<int64_t>(v->tab.cap, nctr);
     hipLaunchKernelGGL(k_reset_table, dim3((unsigned)((cells + 255) / 256)), dim3(256), 0, v->stream, v->tab, v->mask1,
                        v->counters, nctr);
     MQR_CHECK_HIP(hipGetLastError());
     v->pool_count = 0;
+    v->ctr_clean[0] = v->ctr_clean[1] = true;
     return 0;
 }
 
@@ -897,7 +935,43 @@ int mqr_integrate_frames(mqr_vbg* v, const float* depths, int depth_loc, int B, 
         }
         const int64_t pool_before = v->pool_count;
         if (upload_frames(v, p, K, T_wc, idx, b, dframe) || reset_batch_counters(v, p)) return 1;
-        if (touch_batch(v, p, dbase, HW, H, W, b, depth_scale, depth_max, sdf_trunc, block_size, max_touch)) return 1;
+        // The first batch of a call: its integrate is enqueued right behind its touch, gated on the
+        // device by the touch's own counters (k_gate), so the GPU does not idle while the host reads
+        // them.  Later batches' counters are read while the previous integrate runs anyway.
+        const bool spec = batch == 0 && v->spec_head && v->pipelined && !v->probe_one && v->batch_n_max > 0;
+        TouchState ts;
+        if (touch_batch_launch(v, p, dbase, HW, H, W, b, depth_scale, depth_max, sdf_trunc, block_size, max_touch, ts))
+            return 1;
+        if (spec) {
+            const int64_t grid = std::min<int64_t>(std::max<int64_t>(v->batch_n_max + v->batch_n_max / 4, 256), 8192);
+            const size_t ev_before = v->int_events.size();
+            if (launch_integrate(v, p, dbase, HW, H, W, b, depth_scale, depth_max, sdf_trunc, (int)pool_before, grid))
+                return 1;
+            if (read_counters(v, p)) return 1;  // the touch's counters (the integrate keeps running)
+            const int* c = v->hctr(p);
+            bool gated = c[kOverflow] != 0;
+            for (int f = 0; f < b; ++f) gated |= c[kFrameCounterBase + f] == 0;
+            if (!gated) {  // the speculative integrate is the batch's integrate (k_gate agreed)
+                v->pool_count = v->h_counters[2 * kCountersTotal];
+                v->batch_new_max = std::max(v->batch_new_max, v->pool_count - ts.pool_before);
+                const int64_t n = std::min<int64_t>(c[kListCount], v->list_cap);
+                v->batch_n_max = std::max(v->batch_n_max, n);
+                if (v->profile) {
+                    v->stats.integrate_launches += 1;
+                    v->stats.union_blocks += n;
+                    for (int f = 0; f < kMaxBatch; ++f) v->stats.frame_blocks += c[kFreshBase + f];
+                    v->stats.frames += b;
+                }
+                continue;
+            }
+            // gated: the integrate did nothing (and cleared no slot mark); redo the batch's tail the
+            // ordinary way once it has finished
+            MQR_CHECK_HIP(hipStreamSynchronize(v->stream2));
+            v->int_pending[p] = false;
+            if (v->profile && v->int_events.size() > ev_before) v->int_events.resize(ev_before);
+        }
+        if (touch_batch_resolve(v, p, dbase, HW, H, W, b, depth_scale, depth_max, sdf_trunc, block_size, ts)) return 1;
+        v->batch_n_max = std::max<int64_t>(v->batch_n_max, std::min<int64_t>(v->hctr(p)[kListCount], v->list_cap));
         int empty = -1;  // first frame of the batch that touched no block
         for (int f = 0; f < b && empty < 0; ++f)
             if (v->hctr(p)[kFrameCounterBase + f] == 0) empty = f;
@@ -1128,6 +1202,7 @@ int mqr_vbg_set_variant(mqr_vbg* v, int variant) {
     v->xcd_order = (variant & 0x8000) != 0;   // bit 15: spatial per-XCD groups (k_xcd_order, A/B)
     v->touch_ppt = (variant & 0x10000) ? 1 : 2;  // bit 16: one stride-4 pixel per touch thread (A/B)
     v->touch_frame = (variant & 0x30000) == 0;   // bit 17: the round-3 strip touch (k_touch<2>) instead of k_touch_frame
+    v->spec_head = (variant & 0x40000) == 0;     // bit 18: no speculative first-batch integrate (A/B)
     v->extract_mode = (variant >> 20) & 0xf;      // bits 20-23: mesh emission configuration (tools/ab_extract.py)
     return 0;
 }

@@ -1263,6 +1263,20 @@ __global__ void k_rehash(Table src, Table dst) {
 
 __global__ void k_set_counter(int* ctr, int value) { *ctr = value; }
 
+// Gate of a speculatively launched integrate (the first batch of a call is integrated right behind
+// its touch, before the host has read the touch's counters): copy the batch counters into the shadow
+// set the integrate and its fix-up read, with the list emptied when the touch needs the host (pool
+// overflow, full table, list overflow, key range, or a frame that touched nothing) -- the integrate
+// then does nothing and the host redoes the batch the ordinary way -- and the fix-up count zeroed.
+__global__ void k_gate(const int* __restrict__ ctr, int* __restrict__ shadow, int nframes) {
+    const int lane = threadIdx.x;  // one wave
+    bool empty = false;
+    for (int f = lane; f < nframes; f += 64) empty |= ctr[kFrameCounterBase + f] == 0;
+    const bool stop = __ballot(empty) != 0 || ctr[kOverflow] != 0;
+    for (int i = lane; i < kCountersTotal; i += 64)
+        shadow[i] = i == kListCount ? (stop ? 0 : ctr[kListCount]) : i == kBadCount ? 0 : ctr[i];
+}
+
 // Empty table: keys empty, values -1, both parities' slot masks 0; and `nctr` counters 0.
 __global__ void k_reset_table(Table t, bmask_t* mask1, int* counters, int nctr) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;

@@ -194,3 +194,40 @@ def test_sharded_merge_matches_single_pass(mqr_mod, room_seq):
         merged.unpack_weighted(dkeys.ptr.value, U, dsum.ptr.value)
         err = compare_volumes(merged.export(), full.export(), TOL)
         assert err < 1e-5
+
+
+def test_speculative_first_batch_gate(mqr_mod, room_seq):
+    """The first batch of a call is integrated right behind its touch, gated on the device by the
+    touch's counters (k_gate).  A volume that has integrated before (so the gate path is taken) gives
+    the same volume with the speculative head on and off (variant bit 18); a first batch whose pool
+    overflows (capacity 1 block) or holds a frame that touches nothing falls back to the ordinary path:
+    the result equals the oracle's and the error is raised as upstream does."""
+    from mqr import _lib
+    K = room_seq["K"].astype(np.float64)
+    T = room_seq["T_wc"].astype(np.float64)
+    d = room_seq["depth"]
+    kw = dict(depth_scale=1.0, depth_max=4.0, trunc_voxel_multiplier=10.0)
+    vols = []
+    for variant in (0, 0x40000):
+        v = mqr_mod.VoxelBlockGrid(voxel_size=0.01, block_resolution=16, block_count=4096)
+        _lib.call("mqr_vbg_set_variant", v.handle, variant)
+        v.integrate_frames(d[:4], K[:4], T[:4], **kw)  # sets the speculative grid estimate
+        v.reset()
+        v.integrate_frames(d, K, T, **kw)
+        vols.append(v)
+    assert compare_volumes(vols[0].export(), vols[1].export(), 0.0) == 0.0
+    ref = _oracle_run(room_seq, 0.01, 16, 4.0, 10.0)
+    compare_volumes(vols[0].export(), ref.export(), 0.0)
+    # pool overflow inside the speculative first batch: capacity 1 block
+    small = mqr_mod.VoxelBlockGrid(voxel_size=0.01, block_resolution=16, block_count=1)
+    small.integrate_frames(d[:1], K[:1], T[:1], **kw)
+    small.reset()
+    small.integrate_frames(d, K, T, **kw)
+    compare_volumes(small.export(), ref.export(), 0.0)
+    # a frame that touches nothing inside the first batch: frames before it integrated, then the error
+    dd = d.copy()
+    dd[3] = 0.0
+    vols[0].reset()
+    with pytest.raises(RuntimeError, match="No block is touched"):
+        vols[0].integrate_frames(dd, K, T, **kw)
+    compare_volumes(vols[0].export(), _oracle_run(room_seq, 0.01, 16, 4.0, 10.0, frames=[0, 1, 2]).export(), 0.0)
