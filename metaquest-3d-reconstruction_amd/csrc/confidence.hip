@@ -264,9 +264,21 @@ struct Pix32 {
     float lo2, hi2;    // the band bounds, rounded down / up
     float zlo, zhi;    // zmax rounded down / up
 };
-__device__ inline int pixel_decide32(const float* __restrict__ tgt, int W, int H, float wm1, float hm1, const ConfFrame& ft,
-                                     const Pix32& px, float dmf) {
+// Stage 1 of pixel_decide32 for one (pixel, neighbour) pair: the float32 projection, its error
+// bounds and the range / floor certainty tests, and -- for a pair that gets that far -- the two tap
+// rows' loads, issued here so that they are in flight while the next neighbour's stage 1 runs
+// (k_confidence pipelines the neighbour loop: the kernel is bound by these loads' latency, not by
+// its VALU work).  st: 0 decided (no finite error), 1 taps pending, -1 undecided (float64 path).
+struct Stage32 {
+    int st;
+    float Z, EZ, P, EP, uu, vv, Eu, Ev;  // (floor(uu), floor(vv) are recomputed in stage 2: registers)
+    float2 ab, cd;
+};
+__device__ __forceinline__ Stage32 decide32_stage1(const float* __restrict__ tgt, int W, int H, float wm1, float hm1,
+                                                   const ConfFrame& ft, const Pix32& px) {
     constexpr float u = 0x1p-24f;
+    Stage32 r;
+    r.st = 0;
     const float* T = ft.Tf;
     const float X = __builtin_fmaf(T[0], px.p[0], __builtin_fmaf(T[1], px.p[1], __builtin_fmaf(T[2], px.p[2], T[3])));
     const float Y = __builtin_fmaf(T[4], px.p[0], __builtin_fmaf(T[5], px.p[1], __builtin_fmaf(T[6], px.p[2], T[7])));
@@ -277,9 +289,12 @@ __device__ inline int pixel_decide32(const float* __restrict__ tgt, int W, int H
     // (comparisons of computed sums are made strict where rounding could otherwise flip them:
     // RN(x) > c implies x > c and RN(x) < c implies x < c for a representable c)
     const float zl = Z - EZ, zh = Z + EZ;
-    if (Z <= -EZ) return 0;           // Z <= 0 certain
-    if (zl > px.zhi) return 0;        // Z > zmax certain
-    if (!(zl > 0.0f && zh < px.zlo && EZ <= 0.125f * Z && Z >= 1e-6f)) return -1;
+    r.Z = Z;
+    r.EZ = EZ;
+    if (Z <= -EZ) return r;     // Z <= 0 certain
+    if (zl > px.zhi) return r;  // Z > zmax certain
+    r.st = -1;
+    if (!(zl > 0.0f && zh < px.zlo && EZ <= 0.125f * Z && Z >= 1e-6f)) return r;
     const float inv = __builtin_amdgcn_rcpf(Z);
     const float qx = (X * ft.fxf) * inv, qy = (Y * ft.fyf) * inv;
     const float uu = qx + ft.cxf, vv = qy + ft.cyf;
@@ -289,31 +304,53 @@ __device__ inline int pixel_decide32(const float* __restrict__ tgt, int W, int H
                      5.0f * u * __builtin_fabsf(qx) + 2.0f * u * __builtin_fabsf(uu);
     const float Ev = __builtin_fabsf(ft.fyf) * inv * (EY + (__builtin_fabsf(Y) + EY) * ezr) * (1.0f + 16.0f * u) +
                      5.0f * u * __builtin_fabsf(qy) + 2.0f * u * __builtin_fabsf(vv);
-    if ((uu + Eu < 0.0f) | (uu - Eu > wm1) | (vv + Ev < 0.0f) | (vv - Ev > hm1)) return 0;  // out of range certain
+    if ((uu + Eu < 0.0f) | (uu - Eu > wm1) | (vv + Ev < 0.0f) | (vv - Ev > hm1)) {  // out of range certain
+        r.st = 0;
+        return r;
+    }
     const float fu0 = __builtin_floorf(uu), fv0 = __builtin_floorf(vv);
     const float ru = uu - fu0, rv = vv - fv0;  // exact (|uu|, |vv| < 2^23 here)
-    if (!((ru >= Eu) & (ru + Eu < 1.0f) & (rv >= Ev) & (rv + Ev < 1.0f) & (uu < 0x1p22f) & (vv < 0x1p22f))) return -1;
+    if (!((ru >= Eu) & (ru + Eu < 1.0f) & (rv >= Ev) & (rv + Ev < 1.0f) & (uu < 0x1p22f) & (vv < 0x1p22f))) return r;
     const int u0 = (int)fu0, v0 = (int)fv0;
-    if (!((u0 >= 0) & (u0 + 1 < W) & (v0 >= 0) & (v0 + 1 < H))) return 0;
-    float2 ab, cd;
-    const float* row0 = tgt + (int64_t)v0 * W + u0;
-    __builtin_memcpy(&ab, row0, sizeof(float2));
-    __builtin_memcpy(&cd, row0 + W, sizeof(float2));
-    const float Ia = ab.x, Ib = ab.y, Ic = cd.x, Id = cd.y;
+    if (!((u0 >= 0) & (u0 + 1 < W) & (v0 >= 0) & (v0 + 1 < H))) {
+        r.st = 0;
+        return r;
+    }
+    r.st = 1;
+    r.P = __builtin_fmaf(X, X, __builtin_fmaf(Y, Y, Z * Z));
+    r.EP = 2.0f * (__builtin_fabsf(X) * EX + __builtin_fabsf(Y) * EY + Z * EZ) + (EX * EX + EY * EY + EZ * EZ) +
+           8.0f * u * r.P;
+    r.uu = uu;
+    r.vv = vv;
+    r.Eu = Eu;
+    r.Ev = Ev;
+    const float* row0 = tgt + (int64_t)v0 * W + u0;  // the two taps of a row in one 8-byte load
+    __builtin_memcpy(&r.ab, row0, sizeof(float2));
+    __builtin_memcpy(&r.cd, row0 + W, sizeof(float2));
+    return r;
+}
+
+// Stage 2: the tap test and the band filter on the float32 values (see the comment above); returns
+// 0 / 1 / 2, or -1 when the float64 path must decide.
+__device__ __forceinline__ int decide32_stage2(const Stage32& r, const Pix32& px, float dmf) {
+    constexpr float u = 0x1p-24f;
+    if (r.st <= 0) return r.st;
+    const float Ia = r.ab.x, Ib = r.ab.y, Ic = r.cd.x, Id = r.cd.y;
     const bool taps = (Ib > 0) & (Ib <= dmf) & (Ia > 0) & (Ia <= dmf) & (Ic > 0) & (Ic <= dmf) & (Id > 0) & (Id <= dmf);
     if (!taps) return 0;
-    const float gu = (fu0 + 1.0f) - uu, gv = (fv0 + 1.0f) - vv, fu = ru, fv = rv;
+    const float fu0 = __builtin_floorf(r.uu), fv0 = __builtin_floorf(r.vv);
+    const float fu = r.uu - fu0, fv = r.vv - fv0;
+    const float gu = (fu0 + 1.0f) - r.uu, gv = (fv0 + 1.0f) - r.vv;
     const float zf = __builtin_fmaf(fu * fv, Id, __builtin_fmaf(gu * fv, Ic, __builtin_fmaf(fu * gv, Ib, (gu * gv) * Ia)));
-    const float Edz = EZ + Eu * (__builtin_fabsf(Ib - Ia) + __builtin_fabsf(Id - Ic)) +
-                      Ev * (__builtin_fabsf(Ic - Ia) + __builtin_fabsf(Id - Ib)) + 8.0f * u * zf;
-    const float dz = __builtin_fabsf(Z - zf);
-    const float P = __builtin_fmaf(X, X, __builtin_fmaf(Y, Y, Z * Z));
-    const float EP = 2.0f * (__builtin_fabsf(X) * EX + __builtin_fabsf(Y) * EY + Z * EZ) + (EX * EX + EY * EY + EZ * EZ) +
-                     8.0f * u * P;
+    const float Edz = r.EZ + r.Eu * (__builtin_fabsf(Ib - Ia) + __builtin_fabsf(Id - Ic)) +
+                      r.Ev * (__builtin_fabsf(Ic - Ia) + __builtin_fabsf(Id - Ib)) + 8.0f * u * zf;
+    const float dz = __builtin_fabsf(r.Z - zf);
+    const float zl = r.Z - r.EZ, zh = r.Z + r.EZ;  // (the same roundings as in stage 1)
     const float a1 = dz + Edz;
-    if (a1 * a1 * (P + EP) * (1.0f + 16.0f * u) <= px.lo2 * (zl * zl) * (1.0f - 16.0f * u)) return 1;
+    if (a1 * a1 * (r.P + r.EP) * (1.0f + 16.0f * u) <= px.lo2 * (zl * zl) * (1.0f - 16.0f * u)) return 1;
     const float a0 = dz - Edz;
-    if ((a0 > 0.0f) & (a0 * a0 * (P - EP) * (1.0f - 16.0f * u) > px.hi2 * (zh * zh) * (1.0f + 16.0f * u))) return 2;
+    if ((a0 > 0.0f) & (a0 * a0 * (r.P - r.EP) * (1.0f - 16.0f * u) > px.hi2 * (zh * zh) * (1.0f + 16.0f * u)))
+        return 2;
     return -1;
 }
 
@@ -333,7 +370,7 @@ __device__ inline int ref_point(const ConfFrame& fr, int u, int v, float dref, d
 // `err <= threshold` on the float32 error map is d2 <= d2_max (sqrt and both roundings monotone).
 // STATS: count the pairs per deciding stage into st[4] (pairs, float32 prefilter, float64 filter,
 // float64 back-projection) -- mqr_confidence_stats.
-template <bool STATS>
+template <bool STATS, bool WIDE>
 __global__ __launch_bounds__(256) void k_confidence(const float* __restrict__ depths, int N, int H, int W,
                                                     const ConfFrame* __restrict__ fr, int ref_begin, int r,
                                                     double depth_max, double d2_max, double sd,
@@ -381,23 +418,49 @@ __global__ __launch_bounds__(256) void k_confidence(const float* __restrict__ de
         px.zlo = round_down_f(zmax);
         px.zhi = round_up_f(zmax);
         const float wm1f = (float)(W - 1), hm1f = (float)(H - 1);
-        for (int t = lo; t < hi; ++t) {
-            if (t == ref) continue;
-            const ConfFrame& ft = fr[t];
-            if (!ft.ok) continue;  // a neighbour that is not ok is skipped (frame_ok)
-            const float* tgt = depths + (int64_t)t * HW;
-            int dcs = pixel_decide32(tgt, W, H, wm1f, hm1f, ft, px, dmf);
-            if (STATS) {
-                ++n_pairs;
-                n_f32 += dcs >= 0;
+        // the neighbour loop, pipelined: stage 1 of the next neighbour (its projection, tests and tap
+        // loads) runs before stage 2 of the current one, so one pair's tap loads are in flight while
+        // the other's are computed; pairs the float32 path cannot decide are collected in `defer`
+        // (bit t - lo) and decided by the float64 path after the loop (outside the hot loop's registers)
+        // (WIDE: windows of more than 64 frames (r > 31), in chunks of 64 neighbours -- one defer bit each)
+#pragma clang loop unroll(disable)
+        for (int clo = lo; clo < hi; clo += 64) {
+            const int chi = WIDE ? min(hi, clo + 64) : hi;
+            auto next_t = [&](int t) {
+                for (++t; t < chi; ++t)
+                    if (t != ref && fr[t].ok) break;  // the reference frame and frames not ok are skipped
+                return t;
+            };
+            uint64_t defer = 0;
+            int t = next_t(clo - 1);
+            Stage32 cur;
+            if (t < chi) cur = decide32_stage1(depths + (int64_t)t * HW, W, H, wm1f, hm1f, fr[t], px);
+#pragma clang loop unroll(disable)
+            while (t < chi) {
+                const int t2 = next_t(t);
+                Stage32 nxt;
+                if (t2 < chi) nxt = decide32_stage1(depths + (int64_t)t2 * HW, W, H, wm1f, hm1f, fr[t2], px);
+                const int dcs = decide32_stage2(cur, px, dmf);
+                if (STATS) {
+                    ++n_pairs;
+                    n_f32 += dcs >= 0;
+                }
+                if (dcs < 0) defer |= 1ull << (t - clo);
+                nv += dcs > 0;
+                nc += dcs == 1;
+                t = t2;
+                cur = nxt;
             }
-            if (dcs < 0) {
-                dcs = pixel_decide(tgt, W, wm1, hm1, ft, pw, zmax, dmf, lo2, hi2, d2_max);
+            while (defer) {
+                const int td = clo + __builtin_ctzll(defer);
+                defer &= defer - 1;
+                int dcs = pixel_decide(depths + (int64_t)td * HW, W, wm1, hm1, fr[td], pw, zmax, dmf, lo2, hi2, d2_max);
                 if (STATS) n_tail += dcs >> 2;
                 dcs &= 3;
+                nv += dcs != 0;
+                nc += dcs == 1;
             }
-            nv += dcs != 0;
-            nc += dcs == 1;
+            if (!WIDE) break;
         }
     }
     if (STATS) {
@@ -611,14 +674,23 @@ int mqr_confidence(int device, const float* depths, int depth_loc, int N, int H,
         MQR_CHECK_HIP(hipMalloc(&dconf, sizeof(double) * nref * HW));
         MQR_CHECK_HIP(hipMalloc(&dvalid, sizeof(int32_t) * nref * HW));
     }
+    const dim3 grid((unsigned)((HW + 255) / 256), nref);
+    const bool wide = frame_range > 31;  // a window of more than 64 frames: chunked defer masks
     if (cc.stats) {
         if (!cc.dst) MQR_CHECK_HIP(hipMalloc(&cc.dst, 4 * sizeof(unsigned long long)));
         MQR_CHECK_HIP(hipMemsetAsync(cc.dst, 0, 4 * sizeof(unsigned long long), s));
-        hipLaunchKernelGGL(k_confidence<true>, dim3((unsigned)((HW + 255) / 256), nref), dim3(256), 0, s, dsrc, N, H, W,
-                           dfr, ref_begin, frame_range, depth_max, d2max, sd, dconf, dvalid, cc.dst);
+        if (wide)
+            hipLaunchKernelGGL((k_confidence<true, true>), grid, dim3(256), 0, s, dsrc, N, H, W, dfr, ref_begin,
+                               frame_range, depth_max, d2max, sd, dconf, dvalid, cc.dst);
+        else
+            hipLaunchKernelGGL((k_confidence<true, false>), grid, dim3(256), 0, s, dsrc, N, H, W, dfr, ref_begin,
+                               frame_range, depth_max, d2max, sd, dconf, dvalid, cc.dst);
+    } else if (wide) {
+        hipLaunchKernelGGL((k_confidence<false, true>), grid, dim3(256), 0, s, dsrc, N, H, W, dfr, ref_begin,
+                           frame_range, depth_max, d2max, sd, dconf, dvalid, nullptr);
     } else {
-        hipLaunchKernelGGL(k_confidence<false>, dim3((unsigned)((HW + 255) / 256), nref), dim3(256), 0, s, dsrc, N, H, W,
-                           dfr, ref_begin, frame_range, depth_max, d2max, sd, dconf, dvalid, nullptr);
+        hipLaunchKernelGGL((k_confidence<false, false>), grid, dim3(256), 0, s, dsrc, N, H, W, dfr, ref_begin,
+                           frame_range, depth_max, d2max, sd, dconf, dvalid, nullptr);
     }
     MQR_CHECK_HIP(hipGetLastError());
     if (cc.stats) {

@@ -825,9 +825,9 @@ __device__ __forceinline__ void mc_emit_tri(int i, const uint4* rows, const uint
 // Emission of a block with vertices or triangles, from the count pass's row records: vertices
 // (positions and normals from tsdf values gathered from the pool) and triangles at the offsets of
 // the scan, in (block, voxel, edge) / (block, cube, triangle) order.  role 0: both (one workgroup per
-// block, vertices then triangles); 1: vertices only; 2: triangles only (k_mc_emit_split: a vertex and
-// a triangle workgroup per block, each with its own chain of dependent loads in flight).
-// (A merged vertex / triangle item loop and 512-thread blocks were measured: no change)
+// block, vertices then triangles); 1: vertices only; 2: triangles only (timing diagnostics).
+// (A merged vertex / triangle item loop, 512-thread blocks and a vertex and a triangle workgroup per
+// block were measured: no change or slower)
 template <int R, int NT>
 __device__ __forceinline__ void mc_emit_block(int64_t b, int role, const int32_t* __restrict__ nb,
                                               const uint64_t* __restrict__ bkeys, const float2* __restrict__ pool,
@@ -889,21 +889,6 @@ __global__ __launch_bounds__(NT) void k_mc_emit(const int32_t* __restrict__ nb, 
 #endif
     mc_emit_block<R, NT>(blockIdx.x, diag, nb, bkeys, pool, voxel_size, vcount, tcount, voff, toff, rows4,
                          rowNt, pos, nrm, tri, cap_v, cap_t);
-}
-
-// Workgroup 2b emits block b's vertices, 2b + 1 its triangles.
-template <int R, int NT = kMcThreads>
-__global__ __launch_bounds__(NT) void k_mc_emit_split(const int32_t* __restrict__ nb, const uint64_t* __restrict__ bkeys,
-                                                      const float2* __restrict__ pool, float voxel_size,
-                                                      const int32_t* __restrict__ vcount,
-                                                      const int32_t* __restrict__ tcount,
-                                                      const int32_t* __restrict__ voff, const int32_t* __restrict__ toff,
-                                                      const uint4* __restrict__ rows4,
-                                                      const uint32_t* __restrict__ rowNt, float* pos, float* nrm,
-                                                      int32_t* tri, int64_t cap_v, int64_t cap_t, int diag = 0) {
-    (void)diag;
-    mc_emit_block<R, NT>(blockIdx.x >> 1, 1 + (blockIdx.x & 1), nb, bkeys, pool, voxel_size, vcount, tcount, voff, toff,
-                         rows4, rowNt, pos, nrm, tri, cap_v, cap_t);
 }
 
 // ---------------------------------------------------------------- point cloud (R = 8 / 16)
@@ -1327,10 +1312,7 @@ static void launch_mc_emit(const mqr_vbg* v, int64_t n, A... args) {
 #else
     constexpr int diag = 0;
 #endif
-    if (v->extract_mode == 1)  // a vertex and a triangle workgroup per block
-        hipLaunchKernelGGL((k_mc_emit_split<RT>), dim3((unsigned)(2 * n)), dim3(kMcThreads), 0, v->stream, args..., diag);
-    else
-        hipLaunchKernelGGL((k_mc_emit<RT>), dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, args..., diag);
+    hipLaunchKernelGGL((k_mc_emit<RT>), dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, args..., diag);
 }
 
 template <int RT>

@@ -175,9 +175,8 @@ struct mqr_vbg {
     int batch_frames = mqr::kMaxBatch;  // frames per device batch (A/B: 32, variant bit 0x400)
     // profiling
     int touch_ppt = 2;  // stride-4 pixels per k_touch thread (strip touch, variant bits 16 / 17)
-    bool touch_frame = true;  // k_touch_frame: a frame per workgroup (default)
+    bool touch_frame = false; // k_touch_frame: a frame per workgroup (variant bit 17, A/B)
     int last_var = -1;        // integrate variant of the last launch, after fallbacks (mqr_vbg_last_kernel)
-    int extract_mode = 0;     // mesh emission configuration (variant bits 20-23; 1 = vertex / triangle split)
     bool profile = false;
     bool profile_touch = false;  // mqr_vbg_profile level 2: also time the touch launches
     std::vector<std::pair<hipEvent_t, hipEvent_t>> int_events, touch_events;

@@ -387,7 +387,7 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
     //     in two halves (15 = the default).
     //     DESIGN.md §4.1 has the measurements behind the choice.
     int var = v->kernel_variant;
-    if (var < 0 || var > 26) var = 0;
+    if (var < 0 || var > 22) var = 0;
     if (!MQR_AB && var != 1 && var != 2 && var != 4) var = 0;
     if (var != 1 && var != 2 && !lean_ok) var = 2;
     if (var == 5 && (v->R != 16 || W % 4 != 0 || W < 4 || (reinterpret_cast<uintptr_t>(depths) & 15))) var = 0;
@@ -398,7 +398,7 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
     const bool win16_ok = (HW % 4) == 0 && (reinterpret_cast<uintptr_t>(depths) & 15) == 0;
     if ((var == 11 || var == 12 || var == 14 || var == 19) && !win16_ok) var = 0;
     if (var == 0 && !(v->R == 16 && win8_ok)) var = 4;
-    if (var >= 13 && !win8_ok) var = 4;  // (23-26: 8-byte windows too)
+    if (var >= 13 && !win8_ok) var = 4;
     if (v->R != 16 && v->R != 8) var = 1;
     v->last_var = var;
     const int32_t* bad_list = v->bad[p];
@@ -468,22 +468,6 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
                 hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 5, 2, 5, 1, true>), dim3(lean_grid), dim3(512), 0, s,
                                    list, lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW,
                                    H, W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
-            else if (var == 23)  // default + next frame's parameters loaded during the current frame
-                hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 7, 2, 5, 0, false, 1>), dim3(lean_grid), dim3(512), 0,
-                                   s, list, lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths,
-                                   HW, H, W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
-            else if (var == 24)  // default + branchless in-image offset
-                hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 7, 2, 5, 0, false, 2>), dim3(lean_grid), dim3(512), 0,
-                                   s, list, lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths,
-                                   HW, H, W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
-            else if (var == 25)  // 23 + 24
-                hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 7, 2, 5, 0, false, 3>), dim3(lean_grid), dim3(512), 0,
-                                   s, list, lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths,
-                                   HW, H, W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
-            else if (var == 26)  // 25 at >= 6 waves / SIMD
-                hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 6, 2, 5, 0, false, 3>), dim3(lean_grid), dim3(512), 0,
-                                   s, list, lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths,
-                                   HW, H, W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
             else if (var == 10)  // variant 9 with s / sdf_trunc in one correction (verified for this sdf_trunc)
                 hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 8, 2, 3, 1>), dim3(lean_grid), dim3(512), 0, s, list,
                                    lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H,
@@ -617,7 +601,7 @@ static int touch_launch(mqr_vbg* v, int p, const float* dbase, int64_t HW, int H
     }
     if (n > 0)
     {
-        if (v->touch_frame)  // default: a frame per workgroup, claims of the frame's distinct blocks only
+        if (v->touch_frame)  // A/B: a frame per workgroup, claims of the frame's distinct blocks only
             hipLaunchKernelGGL((k_touch_frame<1024, 4096>), dim3(1, b), dim3(1024), 0, v->stream, dbase, HW, H, W,
                                v->d_fp[p], dframe_dev(v, p), depth_scale, depth_max, sdf_trunc, block_size, t, max_probe,
                                alloc, v->ctr(p), v->pool_ctr(), v->pool_cap, v->bkeys, v->lists[p], v->list_cap);
@@ -1201,9 +1185,8 @@ int mqr_vbg_set_variant(mqr_vbg* v, int variant) {
     v->touch_wait = (variant & 0x4000) != 0;  // bit 14: integrate always waits on a touch-stream event (A/B)
     v->xcd_order = (variant & 0x8000) != 0;   // bit 15: spatial per-XCD groups (k_xcd_order, A/B)
     v->touch_ppt = (variant & 0x10000) ? 1 : 2;  // bit 16: one stride-4 pixel per touch thread (A/B)
-    v->touch_frame = (variant & 0x30000) == 0;   // bit 17: the round-3 strip touch (k_touch<2>) instead of k_touch_frame
+    v->touch_frame = (variant & 0x20000) != 0;   // bit 17: k_touch_frame (a frame per workgroup; A/B, 2.3x slower)
     v->spec_head = (variant & 0x40000) == 0;     // bit 18: no speculative first-batch integrate (A/B)
-    v->extract_mode = (variant >> 20) & 0xf;      // bits 20-23: mesh emission configuration (tools/ab_extract.py)
     return 0;
 }
 

@@ -881,85 +881,6 @@ __device__ __forceinline__ void lean_gather_w(float (&dv)[ZPER], bool& bad, cons
     }
 }
 
-// The frame state the 8-byte-window loop reads per frame (OPT variants of k_integrate_lean): held in
-// registers, so the next frame's can be loaded while the current one is processed (OPT & 1).
-struct LeanFrame {
-    float fx, fy, cx, cy;
-    float e[12];
-    int64_t dframe;
-};
-__device__ __forceinline__ LeanFrame lean_frame(const FrameParams* __restrict__ fps, const int64_t* __restrict__ depth_frame,
-                                                int f) {
-    LeanFrame r;
-    const FrameParams& fp = fps[f];
-    r.fx = fp.fx;
-    r.fy = fp.fy;
-    r.cx = fp.cx;
-    r.cy = fp.cy;
-#pragma unroll
-    for (int j = 0; j < 12; ++j) r.e[j] = fp.ext[j];
-    r.dframe = depth_frame[f];
-    return r;
-}
-
-// lean_gather_w<ZPER, ILP, 8> from a LeanFrame; BRANCHLESS: the in-image offset as a select of two
-// computed values (v_cvt_i32_f32 saturates out-of-range and NaN inputs, so the unselected value is
-// harmless) instead of the compiler's exec-mask branch (3 SALU + a branch per voxel-frame).
-template <int ZPER, int ILP, bool BRANCHLESS>
-__device__ __forceinline__ void lean_gather_f(float (&dv)[ZPER], bool& bad, const LeanFrame& fr,
-                                              __amdgpu_buffer_rsrc_t rs, const float (&xs)[ZPER],
-                                              const float (&ys)[ZPER], const float (&zs)[ZPER], uint32_t W4,
-                                              uint32_t past_end, uint32_t hm1_bits, uint32_t wm1_bits) {
-#pragma unroll
-    for (int k = 0; k < ZPER; ++k) {
-        const float ax = xs[k] * fr.e[0] + ys[k] * fr.e[1];
-        const float ay = xs[k] * fr.e[4] + ys[k] * fr.e[5];
-        const float az = xs[k] * fr.e[8] + ys[k] * fr.e[9];
-        const float xc = (ax + zs[k] * fr.e[2]) + fr.e[3];
-        const float yc = (ay + zs[k] * fr.e[6]) + fr.e[7];
-        const float zc = (az + zs[k] * fr.e[10]) + fr.e[11];
-        bad |= (__float_as_uint(zc) - 0x2D800000u) > 0x30000000u;  // not 2^-36 <= zc <= 2^60
-        const float inv_z = rcp_m(zc);
-        const float u = fr.fx * xc * inv_z + fr.cx;
-        const float v = fr.fy * yc * inv_z + fr.cy;
-        const bool in = (__float_as_uint(v) <= hm1_bits) && (__float_as_uint(u) <= wm1_bits);
-        uint32_t off;
-        if constexpr (BRANCHLESS) {
-            const uint32_t on = __umul24((uint32_t)__float2int_rz(v), W4) + ((uint32_t)__float2int_rz(u) << 2);
-            off = in ? on : past_end;
-        } else {
-            off = in ? __umul24((uint32_t)(int)v, W4) + ((uint32_t)(int)u << 2) : past_end;
-        }
-        const u32x2 q = __builtin_amdgcn_raw_buffer_load_b64(rs, off & ~7u, 0, 0);
-        dv[k] = __uint_as_float((off & 4u) ? q.y : q.x);
-        if ((k + 1) % ILP == 0) __builtin_amdgcn_sched_barrier(0);
-    }
-}
-
-template <int ZPER, int ILP = 1>
-__device__ __forceinline__ void lean_update_f(float2 (&tw)[ZPER], const float (&dv)[ZPER], const LeanFrame& fr,
-                                              const float (&xs)[ZPER], const float (&ys)[ZPER],
-                                              const float (&zs)[ZPER], float depth_max, float sdf_trunc, float y1t) {
-#pragma unroll
-    for (int k = 0; k < ZPER; ++k) {
-        const float az = xs[k] * fr.e[8] + ys[k] * fr.e[9];
-        const float zc = (az + zs[k] * fr.e[10]) + fr.e[11];
-        const float d = dv[k];
-        const float sdf = d - zc;
-        if (!(d <= 0) && !(d > depth_max) && !(sdf < -sdf_trunc)) {
-            float s;
-            asm("v_min_f32 %0, %1, %2" : "=v"(s) : "s"(sdf_trunc), "v"(sdf));
-            const float q0 = s * y1t;
-            const float q1 = __builtin_fmaf(__builtin_fmaf(-sdf_trunc, q0, s), y1t, q0);
-            const float sn = __builtin_fmaf(__builtin_fmaf(-sdf_trunc, q1, s), y1t, q1);
-            const float wgt = tw[k].y, wp = wgt + 1;
-            tw[k].x = (wgt * tw[k].x + sn) * rcp_m(wp);
-            tw[k].y = wp;
-        }
-        if ((k + 1) % ILP == 0) __builtin_amdgcn_sched_barrier(0);
-    }
-}
-
 // DIV1: s / sdf_trunc with one Markstein correction (the host enables it only for an sdf_trunc whose
 // every s in [0, sdf_trunc] it verified against IEEE division, strunc_one_correction_ok; the
 // sequence is odd in s, so negative s follow).
@@ -1062,10 +983,7 @@ __device__ void lean_gather_pair(float (&dv)[ZPER], bool& bad, const FrameParams
 #endif
 
 // PAIR (A/B library only, variant 6): the paired-lane gather of vbg_ab.hpp.
-// OPT (8-byte windows, PAIR = 5 only): bit 0 loads the next frame's parameters while the current frame
-// is processed (LeanFrame in registers), bit 1 computes the in-image offset without a branch.
-template <int R, int NT, int MAP = 0, int WPE = 1, int ILP = 1, int PAIR = 0, int DIV1 = 0, bool ZBLK = false,
-          int OPT = 0>
+template <int R, int NT, int MAP = 0, int WPE = 1, int ILP = 1, int PAIR = 0, int DIV1 = 0, bool ZBLK = false>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void k_integrate_lean(
     const int32_t* __restrict__ list, const bmask_t* __restrict__ lmask, int32_t* __restrict__ bad_out,
     int* __restrict__ counters, int64_t list_cap, Table t, float2* __restrict__ pool, float voxel_size,
@@ -1123,32 +1041,6 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
             if constexpr (PAIR == 3 || ZBLK) {  // block-level zc range check (block_zc_unsafe): skip the frame loop
                 static_assert(NT == 512, "one (frame, corner) per thread");
                 if (__syncthreads_or(block_zc_unsafe<R>(tid, mask, fps, xb, yb, zb, voxel_size))) bad = true, m = 0;
-            }
-            if constexpr (OPT != 0) {
-                static_assert(PAIR == 5, "OPT variants: 8-byte windows");
-                if (m) {
-                    LeanFrame cur = lean_frame(fps, depth_frame, __builtin_ctzll(m));
-                    m &= m - 1;
-                    for (;;) {
-                        LeanFrame nxt;
-                        const bool more = m != 0;
-                        if (OPT & 1) {  // issued now, waited for at the next iteration
-                            if (more) nxt = lean_frame(fps, depth_frame, __builtin_ctzll(m));
-                        }
-                        float dv[ZPER];
-                        lean_gather_f<ZPER, ILP, (OPT & 2) != 0>(dv, bad, cur, frame_rsrc(depths + cur.dframe * HW, bytes),
-                                                                 xs, ys, zs, W4, bytes, __float_as_uint(hm1),
-                                                                 __float_as_uint(wm1));
-                        lean_update_f<ZPER, ILP>(tw, dv, cur, xs, ys, zs, depth_max, sdf_trunc, y1t);
-                        if (!more) break;
-                        if (OPT & 1)
-                            cur = nxt;
-                        else
-                            cur = lean_frame(fps, depth_frame, __builtin_ctzll(m));
-                        m &= m - 1;
-                    }
-                }
-                m = 0;
             }
             while (m) {
                 const int f = __builtin_ctzll(m);

@@ -114,3 +114,18 @@ def test_confidence_float32_prefilter_stages_and_static_camera():
         assert np.array_equal(valid[i], ov), i
         assert np.array_equal(conf[i], oc), i
     assert valid.max() > 0
+
+
+def test_confidence_wide_window_vs_oracle():
+    """r > 31 (a window of more than 64 frames): the chunked float64-deferral path (k_confidence<WIDE>)
+    over 70 small frames against the oracle, reference frames at both ends and in the middle."""
+    from mqr import synthetic
+    from mqr.confidence import confidence_maps
+    seq = synthetic.make_sequence("room", n=70, height=48, width=64, f=52.5, noise=True, seed=23)
+    Ti = np.linalg.inv(seq["T_cw"])
+    conf, valid = confidence_maps(seq["depth"], seq["K"], seq["T_cw"], Ti, 0, 70, 40, 4.0, 0.08)
+    for i in (0, 35, 69):
+        oc, ov = oracle.confidence(seq["depth"], seq["K"], seq["T_cw"], Ti, i, 40, 4.0, 0.08)
+        assert np.array_equal(valid[i], ov), i
+        assert np.array_equal(conf[i], oc), i
+    assert valid.max() > 40

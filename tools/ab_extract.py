@@ -2,8 +2,8 @@
 """Interleaved A/B of extract_triangle_mesh configurations on the bench volume (C2, one process).
 
 python tools/ab_extract.py --modes 0 --reps 15
-mode = value of mqr_vbg_set_variant bits 20-23 for an extraction configuration under test (1: a vertex
-and a triangle workgroup per block) (round 3
+mode = value of mqr_vbg_set_variant bits 20-23 for an extraction configuration under test (round 4: a
+vertex and a triangle workgroup per block, 0.187 vs 0.179 ms, removed) (round 3
 measured a merged vertex / triangle item loop and 512-thread emission blocks this way: no change,
 profiles/r03_ab_integrate_windows.json; neither is in the library now, so mode 0 is the library).
 Prints per-mode median wall ms of mqr_extract_mesh (device-resident, the bench's extract_ms) and
