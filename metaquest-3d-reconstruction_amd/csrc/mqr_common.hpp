@@ -97,7 +97,8 @@ constexpr int kFrameCounterBase = 8;  // per-frame raw touch counts live at coun
 constexpr int kFreshBase = kFrameCounterBase + kMaxBatch;  // per-frame new (block, frame) marks
 constexpr int kNumGroups = 8;                               // workgroup groups that share an XCD
 constexpr int kGroupBase = kFreshBase + kMaxBatch;          // k_xcd_order: group g = [off[g], off[g+1])
-constexpr int kCountersTotal = kGroupBase + kNumGroups + 1;
+constexpr int kCollectBase = kGroupBase + kNumGroups + 1;   // two-phase touch: keys collected per frame
+constexpr int kCountersTotal = kCollectBase + kMaxBatch;
 // device counter ints: 2 parity sets, the pool counter (+ spare), 2 shadow sets (k_gate: the copies a
 // speculatively launched integrate reads)
 constexpr int kCounterInts = 4 * kCountersTotal + 8;
@@ -176,6 +177,9 @@ struct mqr_vbg {
     // profiling
     int touch_ppt = 2;  // stride-4 pixels per k_touch thread (strip touch, variant bits 16 / 17)
     bool touch_frame = false; // k_touch_frame: a frame per workgroup (variant bit 17, A/B)
+    bool touch_two_phase = false;  // k_touch<COLLECT> + k_touch_claim (variant bit 19, A/B)
+    uint64_t* collect = nullptr;   // two-phase touch: [2][kMaxBatch][collect_cap] packed keys
+    int64_t collect_cap = 0;       // keys per frame (4 (H/4) (W/4): every sample distinct)
     int last_var = -1;        // integrate variant of the last launch, after fallbacks (mqr_vbg_last_kernel)
     bool profile = false;
     bool profile_touch = false;  // mqr_vbg_profile level 2: also time the touch launches

@@ -599,7 +599,24 @@ static int touch_launch(mqr_vbg* v, int p, const float* dbase, int64_t HW, int H
         MQR_REQUIRE(e0 && e1, "profiling: event creation failed");
         MQR_CHECK_HIP(hipEventRecord(e0, v->stream));
     }
-    if (n > 0)
+    if (n > 0 && v->touch_two_phase) {  // A/B: strips collect their distinct keys, a workgroup per frame claims
+        const int64_t ccap = 4LL * n;
+        if (v->collect_cap < ccap) {
+            if (sync_all(v)) return 1;
+            if (v->collect) MQR_CHECK_HIP(hipFree(v->collect));
+            v->collect = nullptr;
+            v->collect_cap = 0;
+            MQR_CHECK_HIP(hipMalloc(&v->collect, sizeof(uint64_t) * 2 * kMaxBatch * ccap));
+            v->collect_cap = ccap;
+        }
+        uint64_t* col = v->collect + (int64_t)p * kMaxBatch * v->collect_cap;
+        hipLaunchKernelGGL((k_touch<2, true>), dim3((n + 511) / 512, b), dim3(256), 0, v->stream, dbase, HW, H, W,
+                           v->d_fp[p], dframe_dev(v, p), depth_scale, depth_max, sdf_trunc, block_size, t, max_probe,
+                           alloc, v->ctr(p), v->pool_ctr(), v->pool_cap, v->bkeys, v->lists[p], v->list_cap, col,
+                           v->collect_cap);
+        hipLaunchKernelGGL((k_touch_claim<1024, 4096>), dim3(1, b), dim3(1024), 0, v->stream, col, v->collect_cap, t,
+                           max_probe, alloc, v->ctr(p), v->pool_ctr(), v->pool_cap, v->bkeys, v->lists[p], v->list_cap);
+    } else if (n > 0)
     {
         if (v->touch_frame)  // A/B: a frame per workgroup, claims of the frame's distinct blocks only
             hipLaunchKernelGGL((k_touch_frame<1024, 4096>), dim3(1, b), dim3(1024), 0, v->stream, dbase, HW, H, W,
@@ -839,6 +856,7 @@ int mqr_vbg_destroy(mqr_vbg* v) {
     if (v->counters) (void)hipFree(v->counters);
     if (v->h_counters) (void)hipHostFree(v->h_counters);
     if (v->ex_scratch) (void)hipFree(v->ex_scratch);
+    if (v->collect) (void)hipFree(v->collect);
     if (v->h_ex) (void)hipHostFree(v->h_ex);
     if (v->stream) (void)hipStreamDestroy(v->stream);
     if (v->stream2) (void)hipStreamDestroy(v->stream2);
@@ -1187,6 +1205,7 @@ int mqr_vbg_set_variant(mqr_vbg* v, int variant) {
     v->touch_ppt = (variant & 0x10000) ? 1 : 2;  // bit 16: one stride-4 pixel per touch thread (A/B)
     v->touch_frame = (variant & 0x20000) != 0;   // bit 17: k_touch_frame (a frame per workgroup; A/B, 2.3x slower)
     v->spec_head = (variant & 0x40000) == 0;     // bit 18: no speculative first-batch integrate (A/B)
+    v->touch_two_phase = (variant & 0x80000) != 0;  // bit 19: two-phase touch (collect per strip, claim per frame)
     return 0;
 }
 

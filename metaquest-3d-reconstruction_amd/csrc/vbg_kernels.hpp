@@ -172,13 +172,17 @@ __device__ inline void wave_add(int* ctr, int v) {
 // compute_unique_block_coordinates for a batch: blockIdx.y = batch frame (bit), PPT stride-4 pixels
 // per thread (a workgroup covers 256 PPT consecutive ones), 4 samples each over
 // [max(d - trunc, 0), min(d + trunc, depth_max)] (Appendix A.2).
-template <int PPT>
+// COLLECT: phase 1 of the two-phase touch -- the workgroup's distinct keys are appended to the frame's
+// collect buffer (collect + f * ccap, count at counters[kCollectBase + f]) instead of being claimed;
+// k_touch_claim deduplicates them per frame and claims each of the frame's blocks once.
+template <int PPT, bool COLLECT = false>
 __global__ __launch_bounds__(256) void k_touch(const float* __restrict__ depths, int64_t HW, int H, int W,
                                                const FrameParams* __restrict__ fps,
                                                const int64_t* __restrict__ depth_frame, float depth_scale,
                                                float depth_max, float sdf_trunc, float block_size, Table t,
                                                int64_t max_probe, int alloc, int* counters, int* pool_ctr,
-                                               int64_t pool_cap, uint64_t* bkeys, int32_t* list, int64_t list_cap) {
+                                               int64_t pool_cap, uint64_t* bkeys, int32_t* list, int64_t list_cap,
+                                               uint64_t* __restrict__ collect = nullptr, int64_t ccap = 0) {
     // keys already inserted by this workgroup (a strip of one frame shares most of its blocks): only
     // a key's first occurrence probes the global table and sets the frame bit.  The first
     // occurrences are collected in LDS and then claimed all at once, one per thread: each claim is a
@@ -259,6 +263,17 @@ __global__ __launch_bounds__(256) void k_touch(const float* __restrict__ depths,
     wave_add(&wg_count[0], valid);
     __syncthreads();
     const int nu = wg_count[2];
+    if constexpr (COLLECT) {
+        __shared__ int cbase;
+        if (threadIdx.x == 0) {
+            cbase = nu ? atomicAdd(&counters[kCollectBase + f], nu) : 0;
+            if (wg_count[0]) atomicAdd(&counters[kFrameCounterBase + f], wg_count[0]);
+        }
+        __syncthreads();
+        uint64_t* dst = collect + (int64_t)f * ccap + cbase;
+        for (int i = threadIdx.x; i < nu; i += blockDim.x) dst[i] = seen[uniq[i]];  // (cbase + nu <= ccap: samples)
+        return;
+    }
     for (int base = 0; base < nu; base += blockDim.x) {  // uniform trip count: the wave_* calls need whole waves
         const int idx = base + (int)threadIdx.x;
         const uint64_t k = idx < nu ? seen[uniq[idx]] : kEmpty;
@@ -422,6 +437,73 @@ __global__ __launch_bounds__(NT) void k_touch_frame(const float* __restrict__ de
         if (wg_count[0]) atomicAdd(&counters[kFrameCounterBase + f], wg_count[0]);
         if (wg_count[1]) atomicAdd(&counters[kFreshBase + f], wg_count[1]);
     }
+}
+
+// Phase 2 of the two-phase touch: a workgroup per frame (blockIdx.y) reads the keys its strips
+// collected (each strip's distinct keys: ~4x the frame's B_f), deduplicates them in an LDS set and
+// claims each distinct block once (keys the set cannot take are claimed directly, as in k_touch_frame).
+template <int NT, int SEEN>
+__global__ __launch_bounds__(NT) void k_touch_claim(const uint64_t* __restrict__ collect, int64_t ccap, Table t,
+                                                    int64_t max_probe, int alloc, int* counters, int* pool_ctr,
+                                                    int64_t pool_cap, uint64_t* bkeys, int32_t* list, int64_t list_cap) {
+    static_assert(SEEN <= 65536 && (SEEN & (SEEN - 1)) == 0, "16-bit set indices, power of two");
+    constexpr int kProbe = 32, kFill = SEEN / 4 * 3;
+    __shared__ unsigned long long seen[SEEN];
+    __shared__ uint16_t uniq[SEEN];
+    __shared__ int wg_count[2];  // new frame bits, set entries
+    for (int i = threadIdx.x; i < SEEN; i += NT) seen[i] = kEmpty;
+    if (threadIdx.x < 2) wg_count[threadIdx.x] = 0;
+    __syncthreads();
+    const int f = blockIdx.y;
+    const int n = counters[kCollectBase + f];
+    const uint64_t* __restrict__ src = collect + (int64_t)f * ccap;
+    int fresh = 0;
+    for (int base = 0; base < n; base += NT) {  // uniform trip count (spill claims need whole waves)
+        const int i = base + (int)threadIdx.x;
+        const uint64_t k = i < n ? src[i] : kEmpty;
+        bool spill = false;
+        if (k != kEmpty) {
+            uint32_t h = (uint32_t)mix64(k) & (SEEN - 1);
+            spill = true;
+            for (int p = 0; p < kProbe; ++p) {
+                const unsigned long long cur = seen[h];
+                if (cur == k) {
+                    spill = false;
+                    break;
+                }
+                if (cur == kEmpty) {
+                    if (*(volatile int*)&wg_count[1] >= kFill) break;  // set nearly full: claim directly
+                    const unsigned long long old = atomicCAS(&seen[h], (unsigned long long)kEmpty, (unsigned long long)k);
+                    if (old == kEmpty) {
+                        uniq[atomicAdd(&wg_count[1], 1)] = (uint16_t)h;
+                        spill = false;
+                        break;
+                    }
+                    if (old == k) {
+                        spill = false;
+                        break;
+                    }
+                }
+                h = (h + 1) & (SEEN - 1);
+            }
+        }
+        if (__ballot(spill))  // wave-uniform
+            fresh += touch_claim(spill ? k : kEmpty, f, t, max_probe, alloc, counters, pool_ctr, pool_cap, bkeys, list,
+                                 list_cap);
+    }
+    __syncthreads();
+    const int nu = min(wg_count[1], SEEN);
+    for (int base = 0; base < nu; base += NT) {  // uniform trip count
+        const int idx = base + (int)threadIdx.x;
+        fresh += touch_claim(idx < nu ? seen[uniq[idx]] : kEmpty, f, t, max_probe, alloc, counters, pool_ctr, pool_cap,
+                             bkeys, list, list_cap);
+    }
+    __shared__ int fsum;
+    if (threadIdx.x == 0) fsum = 0;
+    __syncthreads();
+    wave_add(&fsum, fresh);
+    __syncthreads();
+    if (threadIdx.x == 0 && fsum) atomicAdd(&counters[kFreshBase + f], fsum);
 }
 
 // Activate explicit keys (vbg.integrate(block_coords, ...)); marks frame bit 0.
