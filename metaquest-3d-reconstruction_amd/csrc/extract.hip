@@ -692,6 +692,32 @@ __device__ inline void mc_edge_full(const int32_t* __restrict__ nbrow, const flo
     ne[2] = v[11] - v[12];
 }
 
+// mc_edge_full with a fast path for an edge whose 13 taps all lie inside the block (~60 % of the
+// edges at R = 16): one base address and constant offsets instead of a 27-neighbour lookup and a
+// 64-bit address per tap -- the same values, so the same results.
+template <class M>
+__device__ inline void mc_edge_taps(const int32_t* __restrict__ nbrow, const float2* __restrict__ pool, int x, int y,
+                                    int z, int axis, float& t_o, float& t_e, float* no, float* ne) {
+    constexpr int R = M::C - 1, DY = R, DZ = R * R;
+    const int ex = x + (axis == 0), ey = y + (axis == 1), ez = z + (axis == 2);
+    if (min(min(x, y), z) >= 1 && max(max(ex, ey), ez) <= R - 2) {
+        const float2* c = pool + (int64_t)nbrow[13] * M::R3 + (z * R + y) * R + x;
+        const float2* e = c + (axis == 0 ? 1 : axis == 1 ? DY : DZ);
+        const float vxp = c[1].x, vxm = c[-1].x, vyp = c[DY].x, vym = c[-DY].x, vzp = c[DZ].x, vzm = c[-DZ].x;
+        const float wxp = e[1].x, wxm = e[-1].x, wyp = e[DY].x, wym = e[-DY].x, wzp = e[DZ].x, wzm = e[-DZ].x;
+        t_o = c[0].x;
+        t_e = axis == 0 ? vxp : axis == 1 ? vyp : vzp;
+        no[0] = vxp - vxm;
+        no[1] = vyp - vym;
+        no[2] = vzp - vzm;
+        ne[0] = wxp - wxm;
+        ne[1] = wyp - wym;
+        ne[2] = wzp - wzm;
+    } else {
+        mc_edge_full<M>(nbrow, pool, x, y, z, axis, t_o, t_e, no, ne);
+    }
+}
+
 // The k-th output of a row whose outputs are ordered by (x, axis) with per-axis bit rows ex / ey /
 // ez: x = the largest x with (outputs below x) <= k, by binary search on prefix popcounts; k becomes
 // the rank of the output among voxel x's axes.
@@ -740,7 +766,7 @@ __device__ __forceinline__ void mc_emit_vertex(int i, const uint4* rows, const i
         uint32_t mm = m3;
         for (int j = 0; j < k; ++j) mm &= mm - 1;
         axis = __builtin_ctz(mm);
-        mc_edge_full<M>(nbrow, pool, x, y, z, axis, tsdf_o, tsdf_e, no, ne);
+        mc_edge_taps<M>(nbrow, pool, x, y, z, axis, tsdf_o, tsdf_e, no, ne);
     } else {
         tsdf_o = mc_tsdf<M>(nbrow, pool, x, y, z);
         mc_normal<M>(nbrow, pool, pres, x, y, z, no);
@@ -985,7 +1011,7 @@ __global__ __launch_bounds__(kMcThreads) void k_pt_emit(const int32_t* __restric
             uint32_t mm = m3;
             for (int j = 0; j < k; ++j) mm &= mm - 1;
             axis = __builtin_ctz(mm);
-            mc_edge_full<M>(nbrow, pool, x, y, z, axis, t_o, t_i, no, ni);
+            mc_edge_taps<M>(nbrow, pool, x, y, z, axis, t_o, t_i, no, ni);
         } else {
             t_o = mc_tsdf<M>(nbrow, pool, x, y, z);
             mc_normal<M>(nbrow, pool, pres, x, y, z, no);

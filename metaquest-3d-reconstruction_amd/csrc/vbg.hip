@@ -387,7 +387,7 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
     //     in two halves (15 = the default).
     //     DESIGN.md §4.1 has the measurements behind the choice.
     int var = v->kernel_variant;
-    if (var < 0 || var > 22) var = 0;
+    if (var < 0 || var > 23) var = 0;
     if (!MQR_AB && var != 1 && var != 2 && var != 4) var = 0;
     if (var != 1 && var != 2 && !lean_ok) var = 2;
     if (var == 5 && (v->R != 16 || W % 4 != 0 || W < 4 || (reinterpret_cast<uintptr_t>(depths) & 15))) var = 0;
@@ -468,6 +468,10 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
                 hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 5, 2, 5, 1, true>), dim3(lean_grid), dim3(512), 0, s,
                                    list, lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW,
                                    H, W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
+            else if (var == 23)  // default with the exact path in-kernel (exact_block_call): no fix-up launch
+                hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 7, 2, 5, 0, false, true>), dim3(lean_grid), dim3(512), 0,
+                                   s, list, lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths,
+                                   HW, H, W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
             else if (var == 10)  // variant 9 with s / sdf_trunc in one correction (verified for this sdf_trunc)
                 hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 8, 2, 3, 1>), dim3(lean_grid), dim3(512), 0, s, list,
                                    lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H,
@@ -499,11 +503,12 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
                 hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 7, 2, 5>), dim3(lean_grid), dim3(512), 0, s, list,
                                    lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H,
                                    W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
-            // exact fix-up of the blocks the fast kernel handed back (usually none: reads a zero count;
-            // redoing them inside the fast kernel costs it registers in the hot loop)
-            hipLaunchKernelGGL((k_integrate_t<16, 4, 512>), dim3(8), dim3(512), 0, s, bad_list, bad_mask, bad_count,
-                               v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp, depth_frame, depth_scale,
-                               depth_max, sdf_trunc, first_new);
+            // exact fix-up of the blocks the fast kernel handed back (usually none: reads a zero count);
+            // variant 23 redoes them in-kernel instead
+            if (var != 23)
+                hipLaunchKernelGGL((k_integrate_t<16, 4, 512>), dim3(8), dim3(512), 0, s, bad_list, bad_mask, bad_count,
+                                   v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp, depth_frame,
+                                   depth_scale, depth_max, sdf_trunc, first_new);
         }
     } else {  // R == 8
         if (var == 2) {

@@ -702,6 +702,17 @@ __device__ __forceinline__ void exact_block(float2* __restrict__ vox, bool fresh
         if (dirty & (1u << k)) vox[k * NT + tid] = tw[k];
 }
 
+template <int R, int NT>
+__device__ __attribute__((noinline)) void exact_block_call(float2* __restrict__ vox, bool fresh, bmask_t mask, int xb,
+                                                           int yb, int zb, float voxel_size,
+                                                           const float* __restrict__ depths, int64_t HW, int W,
+                                                           float hm1, float wm1, const FrameParams* __restrict__ fps,
+                                                           const int64_t* __restrict__ depth_frame, float depth_max,
+                                                           float sdf_trunc) {
+    exact_block<R, 4, NT>(vox, fresh, mask, xb, yb, zb, (int)threadIdx.x, voxel_size, depths, HW, W, hm1, wm1, fps,
+                          depth_frame, 1.0f, depth_max, sdf_trunc);
+}
+
 template <int R, int G, int NT>
 __global__ __launch_bounds__(NT) void k_integrate_t(const int32_t* __restrict__ list, const bmask_t* __restrict__ lmask,
                                                     const int* __restrict__ count, int64_t list_cap, Table t,
@@ -1065,7 +1076,18 @@ __device__ void lean_gather_pair(float (&dv)[ZPER], bool& bad, const FrameParams
 #endif
 
 // PAIR (A/B library only, variant 6): the paired-lane gather of vbg_ab.hpp.
-template <int R, int NT, int MAP = 0, int WPE = 1, int ILP = 1, int PAIR = 0, int DIV1 = 0, bool ZBLK = false>
+// FIXIN: a block whose operands leave the proven ranges is redone by the workgroup itself through the
+// exact path (exact_block, not inlined: its registers stay out of the frame loop's allocation) instead of
+// being handed to the fix-up launch -- no second launch behind every integrate.
+template <int R, int NT>
+__device__ __attribute__((noinline)) void exact_block_call(float2* __restrict__ vox, bool fresh, bmask_t mask, int xb,
+                                                           int yb, int zb, float voxel_size,
+                                                           const float* __restrict__ depths, int64_t HW, int W,
+                                                           float hm1, float wm1, const FrameParams* __restrict__ fps,
+                                                           const int64_t* __restrict__ depth_frame, float depth_max,
+                                                           float sdf_trunc);
+template <int R, int NT, int MAP = 0, int WPE = 1, int ILP = 1, int PAIR = 0, int DIV1 = 0, bool ZBLK = false,
+          bool FIXIN = false>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void k_integrate_lean(
     const int32_t* __restrict__ list, const bmask_t* __restrict__ lmask, int32_t* __restrict__ bad_out,
     int* __restrict__ counters, int64_t list_cap, Table t, float2* __restrict__ pool, float voxel_size,
@@ -1165,8 +1187,12 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
                 }
                 lean_update<ZPER, ILP>(tw, dv, fps[f], xs, ys, zs, depth_max, sdf_trunc, y1t);
             }
-            if (__syncthreads_or(bad)) {  // block-uniform: the exact fix-up launch redoes it from the pool
-                if (tid == 0) hand_off(bad_out, counters, list_cap, slot, mask);
+            if (__syncthreads_or(bad)) {  // block-uniform: the exact path redoes it from the pool
+                if constexpr (FIXIN)
+                    exact_block_call<R, NT>(pool + (int64_t)buf * R3, buf >= first_new, mask, xb, yb, zb, voxel_size,
+                                            depths, HW, W, hm1, wm1, fps, depth_frame, depth_max, sdf_trunc);
+                else if (tid == 0)
+                    hand_off(bad_out, counters, list_cap, slot, mask);
             } else {
 #pragma unroll
                 for (int k = 0; k < ZPER; ++k)
