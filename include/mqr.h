@@ -167,7 +167,7 @@ int mqr_confidence(int device, const float* depths, int depth_loc, int N, int H,
                    int frame_range, double depth_max, double error_threshold, double* conf, int32_t* valid,
                    int out_loc);
 /* Diagnostic: enable (1) / disable (0) / keep (-1) per-pair stage counting of mqr_confidence on this
- * device (a slower kernel build); last4 (nullable) = the last counted call's (pixel, neighbour) pairs
+ * device (a slower kernel build); 2 = a timing-only build without the tap loads (wrong maps); last4 (nullable) = the last counted call's (pixel, neighbour) pairs
  * with a valid reference pixel, and how many the float32 prefilter, the float64 band filter and the
  * float64 back-projection decided. */
 int mqr_confidence_stats(int device, int enable, int64_t* last4);

@@ -274,6 +274,7 @@ struct Stage32 {
     float Z, EZ, P, EP, uu, vv, Eu, Ev;  // (floor(uu), floor(vv) are recomputed in stage 2: registers)
     float2 ab, cd;
 };
+template <bool DIAG = false>  // DIAG (timing only, wrong results): no tap loads
 __device__ __forceinline__ Stage32 decide32_stage1(const float* __restrict__ tgt, int W, int H, float wm1, float hm1,
                                                    const ConfFrame& ft, const Pix32& px) {
     constexpr float u = 0x1p-24f;
@@ -324,6 +325,11 @@ __device__ __forceinline__ Stage32 decide32_stage1(const float* __restrict__ tgt
     r.vv = vv;
     r.Eu = Eu;
     r.Ev = Ev;
+    if (DIAG) {
+        r.ab = make_float2(1.0f + r.uu * 1e-30f, 1.0f);
+        r.cd = make_float2(1.0f, 1.0f + r.vv * 1e-30f);
+        return r;
+    }
     const float* row0 = tgt + (int64_t)v0 * W + u0;  // the two taps of a row in one 8-byte load
     __builtin_memcpy(&r.ab, row0, sizeof(float2));
     __builtin_memcpy(&r.cd, row0 + W, sizeof(float2));
@@ -370,7 +376,7 @@ __device__ inline int ref_point(const ConfFrame& fr, int u, int v, float dref, d
 // `err <= threshold` on the float32 error map is d2 <= d2_max (sqrt and both roundings monotone).
 // STATS: count the pairs per deciding stage into st[4] (pairs, float32 prefilter, float64 filter,
 // float64 back-projection) -- mqr_confidence_stats.
-template <bool STATS, bool WIDE>
+template <bool STATS, bool WIDE, bool DIAG = false>
 __global__ __launch_bounds__(256) void k_confidence(const float* __restrict__ depths, int N, int H, int W,
                                                     const ConfFrame* __restrict__ fr, int ref_begin, int r,
                                                     double depth_max, double d2_max, double sd,
@@ -434,12 +440,12 @@ __global__ __launch_bounds__(256) void k_confidence(const float* __restrict__ de
             uint64_t defer = 0;
             int t = next_t(clo - 1);
             Stage32 cur;
-            if (t < chi) cur = decide32_stage1(depths + (int64_t)t * HW, W, H, wm1f, hm1f, fr[t], px);
+            if (t < chi) cur = decide32_stage1<DIAG>(depths + (int64_t)t * HW, W, H, wm1f, hm1f, fr[t], px);
 #pragma clang loop unroll(disable)
             while (t < chi) {
                 const int t2 = next_t(t);
                 Stage32 nxt;
-                if (t2 < chi) nxt = decide32_stage1(depths + (int64_t)t2 * HW, W, H, wm1f, hm1f, fr[t2], px);
+                if (t2 < chi) nxt = decide32_stage1<DIAG>(depths + (int64_t)t2 * HW, W, H, wm1f, hm1f, fr[t2], px);
                 const int dcs = decide32_stage2(cur, px, dmf);
                 if (STATS) {
                     ++n_pairs;
@@ -607,6 +613,7 @@ struct ConfCache {
     ConfFrame* hfr = nullptr;  // pinned staging
     int cap = 0;
     bool stats = false;                 // mqr_confidence_stats: count pairs per deciding stage
+    bool diag = false;                  // mqr_confidence_stats enable = 2: no tap loads (timing only)
     unsigned long long* dst = nullptr;  // device counters [4]
     int64_t last[4] = {0, 0, 0, 0};     // pairs, float32 prefilter, float64 filter, float64 back-projection
 };
@@ -685,6 +692,9 @@ int mqr_confidence(int device, const float* depths, int depth_loc, int N, int H,
         else
             hipLaunchKernelGGL((k_confidence<true, false>), grid, dim3(256), 0, s, dsrc, N, H, W, dfr, ref_begin,
                                frame_range, depth_max, d2max, sd, dconf, dvalid, cc.dst);
+    } else if (cc.diag) {  // timing diagnostics only (wrong results): no tap loads
+        hipLaunchKernelGGL((k_confidence<false, false, true>), grid, dim3(256), 0, s, dsrc, N, H, W, dfr, ref_begin,
+                           frame_range, depth_max, d2max, sd, dconf, dvalid, nullptr);
     } else if (wide) {
         hipLaunchKernelGGL((k_confidence<false, true>), grid, dim3(256), 0, s, dsrc, N, H, W, dfr, ref_begin,
                            frame_range, depth_max, d2max, sd, dconf, dvalid, nullptr);
@@ -719,7 +729,10 @@ int mqr_confidence_stats(int device, int enable, int64_t* last4) {
     MQR_REQUIRE(device >= 0 && device < kConfDevices, "bad device");
     ConfCache& cc = g_conf_cache[device];
     std::lock_guard<std::mutex> lock(cc.mu);
-    if (enable >= 0) cc.stats = enable != 0;
+    if (enable >= 0) {
+        cc.stats = enable == 1;
+        cc.diag = enable == 2;
+    }
     if (last4)
         for (int i = 0; i < 4; ++i) last4[i] = cc.last[i];
     return 0;

@@ -15,6 +15,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--stats", action="store_true", help="also one counted call: pairs per deciding stage")
+    ap.add_argument("--diag", action="store_true", help="also the timing-only build without tap loads")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -40,6 +41,8 @@ def main():
         torch.cuda.synchronize()
         if i:
             times.append((time.perf_counter() - t0) * 1e3)
+    digest = hashlib.sha256(conf.cpu().numpy().tobytes() + valid.cpu().numpy().tobytes()).hexdigest()[:16]
+    vmean, cmean = float(valid.float().mean()), float(conf.mean())
     stages = None
     if a.stats:
         last = np.zeros(4, np.int64)
@@ -49,14 +52,27 @@ def main():
                   ctypes.c_void_p(conf.data_ptr()), ctypes.c_void_p(valid.data_ptr()), 1)
         _lib.call("mqr_confidence_stats", 0, 0, _lib.ptr(last, _lib._i64p))
         stages = dict(zip(("pairs", "float32_prefilter", "float64_filter", "float64_backprojection"), last.tolist()))
-    digest = hashlib.sha256(conf.cpu().numpy().tobytes() + valid.cpu().numpy().tobytes()).hexdigest()[:16]
+    diag_ms = None
+    if a.diag:
+        _lib.call("mqr_confidence_stats", 0, 2, None)
+        dt = []
+        for i in range(4):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            _lib.call("mqr_confidence", 0, ctypes.c_void_p(d.data_ptr()), 1, B, H, W, _lib.ptr(K32, _lib._f32p),
+                      _lib.ptr(T_cw, _lib._f32p), _lib.ptr(T_ci, _lib._f32p), None, 0, B, 10, 4.0, 0.08,
+                      ctypes.c_void_p(conf.data_ptr()), ctypes.c_void_p(valid.data_ptr()), 1)
+            torch.cuda.synchronize()
+            dt.append((time.perf_counter() - t0) * 1e3)
+        _lib.call("mqr_confidence_stats", 0, 0, None)
+        diag_ms = sorted(dt[1:])[1]
     rec = {"confidence_src": _lib.build_tag(1), "digest": digest}
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     with open(os.path.join(ROOT, "gpurun_out", "conf_workload.json"), "w") as f:
         json.dump(rec, f)
-    print(json.dumps({"confidence_src": rec["confidence_src"], "ms_median": sorted(times)[len(times) // 2], "reps": a.reps, "valid_mean": float(valid.float().mean()),
-                      "conf_mean": float(conf.mean()), "digest": digest,
-                      "single": os.environ.get("MQR_CONF_SINGLE") is not None, "stages": stages}))
+    print(json.dumps({"confidence_src": rec["confidence_src"], "ms_median": sorted(times)[len(times) // 2], "reps": a.reps, "valid_mean": vmean, "conf_mean": cmean, "digest": digest,
+                      "single": os.environ.get("MQR_CONF_SINGLE") is not None, "stages": stages,
+                      "no_tap_loads_ms": diag_ms}))
 
 
 if __name__ == "__main__":
