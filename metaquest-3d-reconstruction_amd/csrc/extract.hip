@@ -17,7 +17,7 @@
 //   k_mc_count  one workgroup per block: halo rows [-1, R]^3 rebuilt from the block's and its
 //               neighbours' bit planes, cube classification, vertex / triangle counts, per-row
 //               records (bases, owned edges / cubes) and sign rows for the emission pass
-//   k_scan_counts  exclusive scans of the per-block counts (one workgroup)
+//               and, by decoupled look-back in the same pass, the blocks' output offsets
 //   k_mc_emit   blocks with output only: vertices with tsdf values gathered from the pool,
 //               triangles at their global offsets (latency: ~4 dependent load phases per block)
 //   other R: the byte-tile kernels (k_mesh_count / k_mesh_emit) stage (tsdf, flags) tiles.
@@ -464,6 +464,42 @@ struct Mc {
     __device__ static int k27(int x, int y, int z) { return (blk(x) + 1) + 3 * (blk(y) + 1) + 9 * (blk(z) + 1); }
 };
 
+// ---- decoupled look-back: the per-block offsets inside the count pass ---------------------------
+// Block b publishes its two counts (vertices / points, triangles), then walks back over the words of
+// its predecessors until one carries an inclusive prefix; the exclusive prefix is the sum of what it
+// read.  A word packs flag (2 bits: 1 counts, 2 inclusive prefix) | t (31 bits) | v (31 bits), so one
+// 64-bit atomic load sees a consistent entry; k_mc_bits zeroes block b's word before the count pass.
+// Workgroups start in blockIdx order, so every predecessor is resident or done: the walk terminates.
+// Prefixes saturate at 2^31 - 1 (the host then refuses the mesh: int32 ids).
+constexpr uint64_t kLbMask = (1ull << 31) - 1;
+__device__ __forceinline__ uint64_t lb_word(uint64_t flag, int64_t v, int64_t t) {
+    const uint64_t vv = (uint64_t)min<int64_t>(v, (int64_t)kLbMask), tt = (uint64_t)min<int64_t>(t, (int64_t)kLbMask);
+    return flag << 62 | tt << 31 | vv;
+}
+__device__ inline void lookback_offsets(uint64_t* __restrict__ st, int64_t b, int64_t n, int v, int t,
+                                        int32_t* __restrict__ o0, int32_t* __restrict__ o1, int64_t* __restrict__ totals) {
+    int64_t ev = 0, et = 0;
+    if (b > 0) {
+        __hip_atomic_store(&st[b], lb_word(1, v, t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int64_t j = b - 1;;) {
+            const uint64_t w = __hip_atomic_load(&st[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint64_t flag = w >> 62;
+            if (flag == 0) continue;  // not published yet
+            ev += (int64_t)(w & kLbMask);
+            et += (int64_t)((w >> 31) & kLbMask);
+            if (flag == 2) break;
+            --j;
+        }
+    }
+    __hip_atomic_store(&st[b], lb_word(2, ev + v, et + t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    o0[b] = (int32_t)min<int64_t>(ev, (int64_t)kLbMask);
+    if (o1) o1[b] = (int32_t)min<int64_t>(et, (int64_t)kLbMask);
+    if (b == n - 1) {
+        totals[0] = ev + v;
+        totals[1] = et + t;
+    }
+}
+
 // ---- bits pass: every voxel read once, fully coalesced -------------------------------------------
 // Per block three bit planes of R^2 rows of R bits (u16, row = z R + y, bit = x): weight > thr
 // (V), tsdf < 0 (N), tsdf > 0 (P).  NaN sets neither N nor P, like the upstream comparisons.  The
@@ -473,7 +509,8 @@ struct Mc {
 template <int R>
 __global__ __launch_bounds__(kMcThreads) void k_mc_bits(const float2* __restrict__ pool, float thr,
                                                         uint16_t* __restrict__ bits, const uint64_t* __restrict__ bkeys,
-                                                        const Table t, int32_t* __restrict__ nb) {
+                                                        const Table t, int32_t* __restrict__ nb,
+                                                        uint64_t* __restrict__ lb) {
     constexpr int R2 = R * R, R3 = R2 * R, NIT = (R3 + kMcThreads - 1) / kMcThreads, RPB = 64 / R;
     constexpr uint64_t RM = (1ull << R) - 1;
     const int64_t b = blockIdx.x;
@@ -485,6 +522,7 @@ __global__ __launch_bounds__(kMcThreads) void k_mc_bits(const float2* __restrict
         const int i = it * kMcThreads + tid;
         v[it] = i < R3 ? src[i] : make_float2(0.f, 0.f);
     }
+    if (tid == 0) lb[b] = 0;  // the count pass's look-back word of this block
     if (tid < 27) {
         int x, y, z;
         unpack_key(bkeys[b], x, y, z);
@@ -613,7 +651,9 @@ __device__ inline int mc_row_tris(const uint32_t* rowN, uint32_t oc, int y, int 
 template <int R>
 __global__ __launch_bounds__(kMcThreads) void k_mc_count(const int32_t* __restrict__ nb, const uint16_t* __restrict__ bits,
                                                          int64_t tri_blocks, int32_t* vcount, int32_t* tcount,
-                                                         uint4* __restrict__ rows4, uint32_t* __restrict__ rowNt) {
+                                                         uint4* __restrict__ rows4, uint32_t* __restrict__ rowNt,
+                                                         uint64_t* __restrict__ lb, int32_t* __restrict__ voff,
+                                                         int32_t* __restrict__ toff, int64_t* __restrict__ totals) {
     using M = Mc<R, 1>;
     __shared__ uint32_t rowV[M::S2], rowN[M::S2], cs[M::C2];
     __shared__ int32_t nbrow[27];
@@ -641,6 +681,7 @@ __global__ __launch_bounds__(kMcThreads) void k_mc_count(const int32_t* __restri
     if (threadIdx.x == 0) {
         vcount[b] = vtot;
         tcount[b] = ttot;
+        lookback_offsets(lb, b, gridDim.x, vtot, ttot, voff, toff, totals);
     }
 }
 
@@ -925,7 +966,8 @@ __global__ __launch_bounds__(NT) void k_mc_emit(const int32_t* __restrict__ nb, 
 template <int R>
 __global__ __launch_bounds__(kMcThreads) void k_pt_count(const int32_t* __restrict__ nb, const uint16_t* __restrict__ bits,
                                                          const float2* __restrict__ pool, int32_t* __restrict__ count,
-                                                         uint4* __restrict__ rows4) {
+                                                         uint4* __restrict__ rows4, uint64_t* __restrict__ lb,
+                                                         int32_t* __restrict__ off, int64_t* __restrict__ totals) {
     using M = Mc<R, 1>;
     __shared__ uint32_t rowV[M::S2], rowN[M::S2], rowP[M::S2];
     __shared__ int32_t nbrow[27];
@@ -962,7 +1004,10 @@ __global__ __launch_bounds__(kMcThreads) void k_pt_count(const int32_t* __restri
     int tot;
     const int base = block_exclusive_scan(np, scratch, tot);
     if (r < M::R2) rows4[b * M::R2 + r] = make_uint4((uint32_t)base, m[0] | (m[1] << 16), m[2], 0u);
-    if (threadIdx.x == 0) count[b] = tot;
+    if (threadIdx.x == 0) {
+        count[b] = tot;
+        lookback_offsets(lb, b, gridDim.x, tot, 0, off, nullptr, totals);
+    }
 }
 
 // Points in (block, voxel, axis) order: position voxel_size (X + ratio e), normal interpolated
@@ -1108,91 +1153,6 @@ __global__ __launch_bounds__(kThreads) void k_points(const int32_t* __restrict__
     }
 }
 
-// Exclusive scans of the two per-block count arrays (vertices, triangles) in one workgroup of
-// kScanThreads; totals[0..1] = the sums.  (Two hipcub scans cost ~20 us of launches at these sizes.)
-// Tiles of kScanTile counts: coalesced loads, all of a thread's in flight, staged in LDS; each
-// thread scans kScanPer consecutive counts, wave and workgroup scans of the thread sums; results
-// back through LDS to coalesced stores; a running carry between tiles.
-constexpr int kScanThreads = 1024, kScanPer = 8, kScanTile = kScanThreads * kScanPer;
-__global__ __launch_bounds__(kScanThreads) void k_scan_counts(const int32_t* __restrict__ c0,
-                                                              const int32_t* __restrict__ c1, int64_t n,
-                                                              int32_t* __restrict__ o0, int32_t* __restrict__ o1,
-                                                              int64_t* __restrict__ totals) {
-    __shared__ int32_t t0[kScanTile], t1[kScanTile];
-    __shared__ int64_t ws0[kScanThreads / 64], ws1[kScanThreads / 64];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const bool two = c1 != nullptr;
-    int64_t carry0 = 0, carry1 = 0;
-    for (int64_t base = 0; base < n; base += kScanTile) {
-        int32_t v0[kScanPer], v1[kScanPer];
-#pragma unroll
-        for (int k = 0; k < kScanPer; ++k) {
-            const int64_t i = base + k * kScanThreads + tid;
-            v0[k] = i < n ? c0[i] : 0;
-            v1[k] = two && i < n ? c1[i] : 0;
-        }
-#pragma unroll
-        for (int k = 0; k < kScanPer; ++k) {
-            t0[k * kScanThreads + tid] = v0[k];
-            t1[k * kScanThreads + tid] = v1[k];
-        }
-        __syncthreads();
-        int64_t s0 = 0, s1 = 0;
-#pragma unroll
-        for (int k = 0; k < kScanPer; ++k) {
-            s0 += t0[tid * kScanPer + k];
-            s1 += t1[tid * kScanPer + k];
-        }
-        int64_t i0 = s0, i1 = s1;  // inclusive wave scans of the thread sums
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const int64_t a = __shfl_up(i0, d, 64), b = __shfl_up(i1, d, 64);
-            if (lane >= d) {
-                i0 += a;
-                i1 += b;
-            }
-        }
-        if (lane == 63) {
-            ws0[wave] = i0;
-            ws1[wave] = i1;
-        }
-        __syncthreads();
-        int64_t b0 = carry0, b1 = carry1, tot0 = 0, tot1 = 0;
-        for (int w = 0; w < kScanThreads / 64; ++w) {
-            if (w < wave) {
-                b0 += ws0[w];
-                b1 += ws1[w];
-            }
-            tot0 += ws0[w];
-            tot1 += ws1[w];
-        }
-        int64_t r0 = b0 + i0 - s0, r1 = b1 + i1 - s1;  // exclusive prefix of this thread's counts
-#pragma unroll
-        for (int k = 0; k < kScanPer; ++k) {
-            const int32_t a = t0[tid * kScanPer + k], b = t1[tid * kScanPer + k];
-            t0[tid * kScanPer + k] = (int32_t)r0;
-            t1[tid * kScanPer + k] = (int32_t)r1;
-            r0 += a;
-            r1 += b;
-        }
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < kScanPer; ++k) {
-            const int64_t i = base + k * kScanThreads + tid;
-            if (i < n) {
-                o0[i] = t0[k * kScanThreads + tid];
-                if (two) o1[i] = t1[k * kScanThreads + tid];
-            }
-        }
-        carry0 += tot0;
-        carry1 += tot1;
-        __syncthreads();  // the tile buffers and wave sums are reused
-    }
-    if (tid == 0) {
-        totals[0] = carry0;
-        totals[1] = carry1;
-    }
-}
 
 // ---------------------------------------------------------------- host side
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -1200,6 +1160,7 @@ static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 // Carve the grow-only per-volume scratch: nb[27n], 4 count/offset arrays of n, faces[3R^2 n], scan temp.
 struct ExScratch {
     int32_t *nb, *c0, *c1, *o0, *o1;
+    uint64_t* lb;    // look-back words of the count pass (one per block)
     uint32_t* faces;
     uint16_t* bits;  // k_mc_bits planes, 3 R^2 u16 per block (R = 8 / 16)
     void* tmp;
@@ -1219,7 +1180,8 @@ static int ex_scratch(mqr_vbg* v, int64_t n, bool mesh, ExScratch& e) {
                              : 0;
     const size_t sz_b = align256(sizeof(uint16_t) * 3 * v->R * v->R * n);
     tmp_bytes = std::max<size_t>(tmp_bytes, 2 * sizeof(int64_t));
-    const size_t need = sz_nb + 4 * sz_c + sz_f + sz_b + align256(tmp_bytes);
+    const size_t sz_lb = align256(sizeof(uint64_t) * n);
+    const size_t need = sz_nb + 4 * sz_c + sz_f + sz_b + sz_lb + align256(tmp_bytes);
     if (v->ex_scratch_bytes < need) {
         MQR_CHECK_HIP(hipStreamSynchronize(v->stream));
         if (v->ex_scratch) MQR_CHECK_HIP(hipFree(v->ex_scratch));
@@ -1242,6 +1204,8 @@ static int ex_scratch(mqr_vbg* v, int64_t n, bool mesh, ExScratch& e) {
     p += sz_f;
     e.bits = reinterpret_cast<uint16_t*>(p);
     p += sz_b;
+    e.lb = reinterpret_cast<uint64_t*>(p);
+    p += sz_lb;
     e.tmp = p;
     e.tmp_bytes = tmp_bytes;
     return 0;
@@ -1349,12 +1313,12 @@ static int mesh_passes(mqr_vbg* v, float thr, const ExScratch& e, mqr_geom* g, i
     uint32_t* rowNt = reinterpret_cast<uint32_t*>(rows4 + n * RR * RR);
     int64_t nv = 0, nt = 0;
     if constexpr (RT > 0) {
-        hipLaunchKernelGGL(k_mc_bits<RT>, dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, v->pool, thr, e.bits,
-                           v->bkeys, v->tab, e.nb);
-        hipLaunchKernelGGL(k_mc_count<RT>, dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, e.nb, e.bits, tri_blocks,
-                           e.c0, e.c1, rows4, rowNt);
         int64_t* tot = reinterpret_cast<int64_t*>(e.tmp);
-        hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(kScanThreads), 0, v->stream, e.c0, e.c1, n, e.o0, e.o1, tot);
+        hipLaunchKernelGGL(k_mc_bits<RT>, dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, v->pool, thr, e.bits,
+                           v->bkeys, v->tab, e.nb, e.lb);
+        // counts, row records and (decoupled look-back) the block offsets and totals in one pass
+        hipLaunchKernelGGL(k_mc_count<RT>, dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, e.nb, e.bits, tri_blocks,
+                           e.c0, e.c1, rows4, rowNt, e.lb, e.o0, e.o1, tot);
         MQR_CHECK_HIP(hipGetLastError());
         MQR_CHECK_HIP(hipMemcpyAsync(v->h_ex, tot, 2 * sizeof(int64_t), hipMemcpyDeviceToHost, v->stream));
         // With a previous extraction's counts, emit into buffers of that size (+ margin) without
@@ -1412,13 +1376,11 @@ static int point_passes(mqr_vbg* v, float thr, const ExScratch& e, mqr_geom* g) 
     int64_t np = 0;
     if constexpr (RT > 0) {
         uint4* rows4 = reinterpret_cast<uint4*>(e.faces);
-        hipLaunchKernelGGL(k_mc_bits<RT>, dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, v->pool, thr, e.bits,
-                           v->bkeys, v->tab, e.nb);
-        hipLaunchKernelGGL(k_pt_count<RT>, dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, e.nb, e.bits, v->pool,
-                           e.c0, rows4);
         int64_t* tot = reinterpret_cast<int64_t*>(e.tmp);
-        hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(kScanThreads), 0, v->stream, e.c0, (const int32_t*)nullptr, n,
-                           e.o0, (int32_t*)nullptr, tot);
+        hipLaunchKernelGGL(k_mc_bits<RT>, dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, v->pool, thr, e.bits,
+                           v->bkeys, v->tab, e.nb, e.lb);
+        hipLaunchKernelGGL(k_pt_count<RT>, dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, e.nb, e.bits, v->pool,
+                           e.c0, rows4, e.lb, e.o0, tot);
         MQR_CHECK_HIP(hipGetLastError());
         MQR_CHECK_HIP(hipMemcpyAsync(v->h_ex, tot, sizeof(int64_t), hipMemcpyDeviceToHost, v->stream));
         const int64_t cp = spec_cap(v->ex_hint[2]);  // speculative capacity, as in mesh_passes
