@@ -63,7 +63,20 @@ __host__ __device__ inline uint64_t mix64(uint64_t k) {
 // ---------------------------------------------------------------- hash table (device view)
 // Open addressing, linear probing, 64-bit keys claimed by atomicCAS.  vals = pool buffer
 // index (-1 none yet, -2 pool overflow), mask = frames of the current batch that touched it.
-typedef uint64_t bmask_t;  // one bit per frame of a device batch (<= kMaxBatch frames)
+// Slot mask of a device batch: bit f = frame f of the batch touched the block (f < kMaxBatch = 127);
+// bit 127 = the slot is on the batch list (set by whichever frame's mark first found its 64-bit word
+// empty and won the flag: two words, so "the whole mask was empty" is not one atomic).  Readers that
+// iterate frames strip it (bm_frames).
+typedef unsigned __int128 bmask_t;
+constexpr unsigned long long kListedBit = 1ull << 63;  // in word 1
+__host__ __device__ inline bmask_t bm_frames(bmask_t m) { return m & ~((bmask_t)kListedBit << 64); }
+__host__ __device__ inline int bm_popc(bmask_t m) {
+    return __builtin_popcountll((unsigned long long)m) + __builtin_popcountll((unsigned long long)(m >> 64));
+}
+__host__ __device__ inline int bm_ctz(bmask_t m) {  // m != 0
+    const unsigned long long lo = (unsigned long long)m;
+    return lo ? __builtin_ctzll(lo) : 64 + __builtin_ctzll((unsigned long long)(m >> 64));
+}
 struct Table {
     uint64_t* keys;
     int32_t* vals;
@@ -92,7 +105,8 @@ struct FrameParams {
 
 void make_frame_params(const double* K, const double* T_wc, FrameParams* fp);
 
-constexpr int kMaxBatch = 64;         // frames per device batch (one bit each in the slot mask)
+constexpr int kMaxBatch = 127;        // frames per device batch (one bit each in the slot mask)
+constexpr int kFirstBatch = 64;       // frames of a call's first batch (its touch runs before any integrate)
 constexpr int kFrameCounterBase = 8;  // per-frame raw touch counts live at counters[8 + f]
 constexpr int kFreshBase = kFrameCounterBase + kMaxBatch;  // per-frame new (block, frame) marks
 constexpr int kNumGroups = 8;                               // workgroup groups that share an XCD
@@ -173,7 +187,8 @@ struct mqr_vbg {
     bool touch_wait = false;   // integrate waits on a touch-stream event every batch (variant bit 0x4000, A/B)
     bool table_worst = false;  // table sized for every sample a new block (variant bit 0x2000, A/B)
     bool probe_one = false;    // batch touch probes one slot per new key (variant bit 0x1000, test hook)
-    int batch_frames = mqr::kMaxBatch;  // frames per device batch (A/B: 32, variant bit 0x400)
+    int batch_frames = mqr::kMaxBatch;  // frames per device batch (A/B: 32, variant bit 0x400; 64, bit 20)
+    int first_batch_frames = mqr::kFirstBatch;  // frames of a call's first batch
     // profiling
     int touch_ppt = 2;  // stride-4 pixels per k_touch thread (strip touch, variant bits 16 / 17)
     bool touch_frame = false; // k_touch_frame: a frame per workgroup (variant bit 17, A/B)

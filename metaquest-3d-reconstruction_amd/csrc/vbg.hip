@@ -8,7 +8,7 @@
 //   table  keys u64 / vals i32 / mask u64 x2 (batch parity), open addressing, capacity >= 2x live keys
 //   lists  slots touched by the current batch (appended once per batch, on first touch), x2
 //
-// Per batch of <= 64 frames: k_touch (one thread per stride-4 pixel per frame, 4 ray samples,
+// Per batch of <= 127 frames (the first of a call <= 64): k_touch (one thread per stride-4 pixel per frame, 4 ray samples,
 // hash insert, per-slot frame bitmask) -> host reads the batch counters (pool growth, empty-frame
 // error) -> k_integrate (one workgroup per touched block, every voxel applies that block's frames
 // in frame order = bit-identical to sequential per-frame integration).
@@ -920,10 +920,14 @@ int mqr_integrate_frames(mqr_vbg* v, const float* depths, int depth_loc, int B, 
         if (!frame_ok || frame_ok[i]) valid.push_back(i);
     int rc = 0;
     int batch = 0;
+    // batches of up to batch_frames frames (127), the first of a call shorter (64): its touch runs
+    // before any integrate, the later ones behind the previous batch's integrate
     const size_t nb = (size_t)std::max(1, std::min(v->batch_frames, kMaxBatch));
-    for (size_t s = 0; s < valid.size(); s += nb, ++batch) {
+    const size_t nb0 = (size_t)std::max(1, std::min(v->first_batch_frames, (int)nb));
+    int b = 0;
+    for (size_t s = 0; s < valid.size(); s += (size_t)b, ++batch) {
         const int p = v->pipelined ? (batch & 1) : 0;
-        const int b = (int)std::min<size_t>(nb, valid.size() - s);
+        b = (int)std::min<size_t>(batch == 0 ? nb0 : nb, valid.size() - s);
         const int* idx = valid.data() + s;
         if (ensure_fp(v, b)) return 1;
         if (depth_loc != MQR_DEVICE && ensure_depth(v, b * HW)) return 1;
@@ -1201,7 +1205,9 @@ int mqr_vbg_set_variant(mqr_vbg* v, int variant) {
     v->kernel_variant = variant & 0xff;
     v->pipelined = (variant & 0x100) == 0;  // bit 8: serialise touch and integrate (A/B of the overlap)
     v->lpt_order = (variant & 0x200) == 0;  // bit 9: integrate in touch order instead of longest-first
-    v->batch_frames = (variant & 0x400) ? 32 : kMaxBatch;  // bit 10: 32-frame batches (A/B)
+    // bit 10: 32-frame batches; bit 20: 64-frame batches (round 3); bit 21: no shorter first batch (A/Bs)
+    v->batch_frames = (variant & 0x400) ? 32 : (variant & 0x100000) ? 64 : kMaxBatch;
+    v->first_batch_frames = (variant & 0x200000) ? kMaxBatch : kFirstBatch;
     v->sys_fence = (variant & 0x800) != 0;  // bit 11: system-scope ordering / timing events (A/B)
     v->probe_one = (variant & 0x1000) != 0; // bit 12: force the full-table retry path (test hook)
     v->table_worst = (variant & 0x2000) != 0; // bit 13: size the table for the worst case (round-2 A/B)

@@ -55,7 +55,7 @@ __global__ __launch_bounds__(1024) void k_xcd_order(const int32_t* __restrict__ 
     };
     for (int i = tid; i < n; i += blockDim.x) {
         const int32_t s = list[i];
-        atomicAdd(&cellw[cell_of(t.keys[s])], __popcll(t.mask[s]));
+        atomicAdd(&cellw[cell_of(t.keys[s])], bm_popc(bm_frames(t.mask[s])));
     }
     __syncthreads();
     // exclusive scan of the 4096 cell weights: 4 per thread, wave shuffles, then the 16 wave totals
@@ -85,7 +85,7 @@ __global__ __launch_bounds__(1024) void k_xcd_order(const int32_t* __restrict__ 
     __syncthreads();
     for (int i = tid; i < n; i += blockDim.x) {
         const int32_t s = list[i];
-        const int w = __popcll(t.mask[s]);
+        const int w = bm_popc(bm_frames(t.mask[s]));
         const int c = cell_of(t.keys[s]);
         const int64_t start = (int64_t)cellw[c] + atomicAdd(&cellrun[c], w);
         const int g = total > 0 ? (int)min<int64_t>(kNumGroups - 1, ((2 * start + w) * kNumGroups) / (2 * (int64_t)total)) : 0;
@@ -108,8 +108,8 @@ __global__ __launch_bounds__(1024) void k_xcd_order(const int32_t* __restrict__ 
     __syncthreads();
     for (int i = tid; i < n; i += blockDim.x) {
         const int32_t s = list[i];
-        const bmask_t m = t.mask[s];
-        const int pos = atomicAdd(&ghist[gbyte[i]][__popcll(m)], 1);
+        const bmask_t m = bm_frames(t.mask[s]);
+        const int pos = atomicAdd(&ghist[gbyte[i]][bm_popc(m)], 1);
         out[pos] = s;
         out_mask[pos] = m;
     }
@@ -121,13 +121,20 @@ typedef __attribute__((address_space(3))) void lvoid_t;
 
 // Index of the j-th (from 0) set bit of m (m has more than j set bits).
 __device__ __forceinline__ int nth_bit(bmask_t m, int j) {
-    uint32_t w = (uint32_t)m;
+    uint64_t q = (uint64_t)m;
     int base = 0;
+    const int c64 = __popcll(q);
+    if (j >= c64) {
+        j -= c64;
+        base = 64;
+        q = (uint64_t)(m >> 64);
+    }
+    uint32_t w = (uint32_t)q;
     const int c = __popc(w);
     if (j >= c) {
         j -= c;
-        base = 32;
-        w = (uint32_t)(m >> 32);
+        base += 32;
+        w = (uint32_t)(q >> 32);
     }
 #pragma unroll
     for (int s = 16; s >= 1; s >>= 1) {
@@ -353,7 +360,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
     for (int64_t i = blockIdx.x; i < n; i += gridDim.x) {
         const int32_t slot = list[i];
         const int buf = __builtin_amdgcn_readfirstlane(t.vals[slot]);
-        const bmask_t mask = readfirstlane_u64(lmask ? lmask[i] : t.mask[slot]);
+        const bmask_t mask = readfirstlane_mask(lmask ? lmask[i] : bm_frames(t.mask[slot]));
         int xb, yb, zb;
         unpack_key(t.keys[slot], xb, yb, zb);
         if (buf < 0 || !mask) {  // block-uniform
@@ -375,10 +382,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
             xs[k] = xs0;
             ys[k] = (float)(yb * R + vy + dy) * voxel_size;
             zs[k] = (float)(zb * R + vz + dz) * voxel_size;
-            const float w = tw[k].y;  // rcp_m(w + 1) needs integer weights (a batch adds <= 64)
-            bad |= !(w >= 0.0f && w <= 0x1p23f && w == __builtin_truncf(w));
+            const float w = tw[k].y;  // rcp_m(w + 1) is exact for integer w <= 2^23 + 64: a batch adds <= 127
+            bad |= !(w >= 0.0f && w <= 0x1p23f - 64.0f && w == __builtin_truncf(w));
         }
-        tile_plan(sh, mask, __popcll(mask), xb, yb, zb, R, voxel_size, fps, H, W);
+        tile_plan(sh, mask, bm_popc(mask), xb, yb, zb, R, voxel_size, fps, H, W);
         const int ng = __builtin_amdgcn_readfirstlane(sh.ng);
         tile_stage(sh, 0, depths, HW, W, depth_frame);
         bmask_t m = mask;
@@ -389,7 +396,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
             const float* half = sh.tile[g & 1];
             const int j1 = __builtin_amdgcn_readfirstlane(sh.gstart[g + 1]);
             for (int j = __builtin_amdgcn_readfirstlane(sh.gstart[g]); j < j1; ++j) {
-                const int f = __builtin_ctzll(m);
+                const int f = bm_ctz(m);
                 m &= m - 1;
                 int4 r = sh.rect[j];
                 r = make_int4(__builtin_amdgcn_readfirstlane(r.x), __builtin_amdgcn_readfirstlane(r.y),

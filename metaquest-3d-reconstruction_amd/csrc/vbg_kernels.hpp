@@ -14,10 +14,29 @@
 namespace mqr {
 
 // ------------------------------------------------------------------ device helpers
-__device__ __forceinline__ bmask_t readfirstlane_u64(bmask_t v) {
+__device__ __forceinline__ uint64_t readfirstlane_u64(uint64_t v) {
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
     const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-    return (bmask_t)hi << 32 | lo;
+    return (uint64_t)hi << 32 | lo;
+}
+__device__ __forceinline__ bmask_t readfirstlane_mask(bmask_t v) {
+    return (bmask_t)readfirstlane_u64((uint64_t)(v >> 64)) << 64 | readfirstlane_u64((uint64_t)v);
+}
+
+// Frame bit f of a slot mask, word by word: returns the old value of f's word.  `first` when the slot
+// joins the batch list here: its word was empty and this mark won the listed flag (word 1, bit 63).
+__device__ __forceinline__ unsigned long long mask_set_frame(bmask_t* m, int f, bool& first) {
+    unsigned long long* w = reinterpret_cast<unsigned long long*>(m);
+    const unsigned long long bit = 1ull << (f & 63);
+    const unsigned long long old = atomicOr(&w[f >> 6], bit);
+    first = false;
+    if (old == 0 || (f >> 6 == 1 && old == kListedBit))  // the word held no frame bit yet
+        first = !(atomicOr(&w[1], kListedBit) & kListedBit);
+    return old;
+}
+__device__ __forceinline__ bool mask_has_frame(const bmask_t* m, int f) {
+    const unsigned long long* w = reinterpret_cast<const unsigned long long*>(m);
+    return (__hip_atomic_load(&w[f >> 6], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> (f & 63)) & 1;
 }
 
 __device__ inline int64_t table_find(const Table t, uint64_t k) {
@@ -67,19 +86,19 @@ __device__ inline int64_t table_insert(Table t, uint64_t k, bool alloc, int* cou
 // Sets frame bit f of the slot (appending the slot to the batch list at its first bit); returns
 // whether the bit was new -- the caller counts those per wave (kFrameBlocks).
 __device__ inline bool mark_slot(Table t, int64_t slot, int f, int* counters, int32_t* list, int64_t list_cap) {
-    const bmask_t bit = (bmask_t)1 << f;
     // every workgroup of a frame that sees the block marks it: read the word at L2 first and only
     // the workgroups that still find the bit clear issue the (same-address, serialised) atomic
-    if (__hip_atomic_load(&t.mask[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & bit) return false;
-    const bmask_t old = atomicOr((unsigned long long*)&t.mask[slot], (unsigned long long)bit);
-    if (old == 0) {
+    if (mask_has_frame(&t.mask[slot], f)) return false;
+    bool first;
+    const unsigned long long old = mask_set_frame(&t.mask[slot], f, first);
+    if (first) {
         const int pos = atomicAdd(&counters[kListCount], 1);
         if (pos < list_cap)
             list[pos] = (int32_t)slot;
         else
             atomicOr(&counters[kOverflow], 4);
     }
-    return !(old & bit);
+    return !((old >> (f & 63)) & 1);
 }
 
 // ---- wave-aggregated table updates of k_touch (call with the whole wave converged) ----------------
@@ -140,11 +159,9 @@ __device__ inline void wave_alloc(bool won, int64_t slot, uint64_t k, Table t, i
 
 // Frame bit f of the slot; `first` when the slot's batch mask was empty (the slot joins the list).
 __device__ inline bool mark_slot_bit(Table t, int64_t slot, int f, bool& first) {
-    const bmask_t bit = (bmask_t)1 << f;
-    if (__hip_atomic_load(&t.mask[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & bit) return false;
-    const bmask_t old = atomicOr((unsigned long long*)&t.mask[slot], (unsigned long long)bit);
-    first = old == 0;
-    return !(old & bit);
+    if (mask_has_frame(&t.mask[slot], f)) return false;
+    const unsigned long long old = mask_set_frame(&t.mask[slot], f, first);
+    return !((old >> (f & 63)) & 1);
 }
 
 // Batch-list appends of this wave's first-marked slots.
@@ -534,7 +551,7 @@ __global__ __launch_bounds__(256) void k_integrate(const int32_t* __restrict__ l
     for (int64_t i = blockIdx.x; i < n; i += gridDim.x) {
         const int32_t slot = list[i];
         const int buf = t.vals[slot];
-        const bmask_t mask = t.mask[slot];
+        const bmask_t mask = bm_frames(t.mask[slot]);
         int xb, yb, zb;
         unpack_key(t.keys[slot], xb, yb, zb);
         if (buf >= 0) {
@@ -549,7 +566,7 @@ __global__ __launch_bounds__(256) void k_integrate(const int32_t* __restrict__ l
                 bool dirty = fresh;
                 bmask_t m = mask;
                 while (m) {
-                    const int f = __builtin_ctzll(m);
+                    const int f = bm_ctz(m);
                     m &= m - 1;
                     const FrameParams& fp = fps[f];
                     const float xc = xs * fp.ext[0] + ys * fp.ext[1] + zs * fp.ext[2] + fp.ext[3];
@@ -625,7 +642,7 @@ __device__ __forceinline__ void integrate_column(float2 (&tw)[ZPER], uint32_t& d
                                                  bool unit_scale, float depth_max, float sdf_trunc) {
     bmask_t m = mask;
     while (m) {
-        const int f = __builtin_ctzll(m);
+        const int f = bm_ctz(m);
         m &= m - 1;
         const FrameParams& fp = fps[f];
         const float* __restrict__ dep = depths + depth_frame[f] * HW;
@@ -731,7 +748,7 @@ __global__ __launch_bounds__(NT) void k_integrate_t(const int32_t* __restrict__ 
     for (int64_t i = blockIdx.x; i < n; i += gridDim.x) {
         const int32_t slot = list[i];
         const int buf = t.vals[slot];
-        const bmask_t mask = readfirstlane_u64(lmask ? lmask[i] : t.mask[slot]);
+        const bmask_t mask = readfirstlane_mask(lmask ? lmask[i] : bm_frames(t.mask[slot]));
         int xb, yb, zb;
         unpack_key(t.keys[slot], xb, yb, zb);
         if (buf >= 0)
@@ -753,7 +770,7 @@ __global__ __launch_bounds__(1024) void k_lpt_order(const int32_t* __restrict__ 
     const int n = (int)min((int64_t)counters[kListCount], list_cap);
     if (threadIdx.x <= kMaxBatch) hist[threadIdx.x] = 0;
     __syncthreads();
-    for (int i = threadIdx.x; i < n; i += blockDim.x) atomicAdd(&hist[__popcll(mask[list[i]])], 1);
+    for (int i = threadIdx.x; i < n; i += blockDim.x) atomicAdd(&hist[bm_popc(bm_frames(mask[list[i]]))], 1);
     __syncthreads();
     if (threadIdx.x == 0) {
         int acc = 0;
@@ -766,8 +783,8 @@ __global__ __launch_bounds__(1024) void k_lpt_order(const int32_t* __restrict__ 
     __syncthreads();
     for (int i = threadIdx.x; i < n; i += blockDim.x) {
         const int32_t s = list[i];
-        const bmask_t m = mask[s];
-        const int pos = atomicAdd(&hist[__popcll(m)], 1);
+        const bmask_t m = bm_frames(mask[s]);
+        const int pos = atomicAdd(&hist[bm_popc(m)], 1);
         out[pos] = s;
         out_mask[pos] = m;
     }
@@ -1011,10 +1028,8 @@ __device__ __forceinline__ void lean_update_v(float2 (&tw)[ZPER], const float (&
 // A = max|x| |e8| + max|y| |e9| + max|z| |e10| + |e11| over the box.  A corner with Z - 2^-20 A <
 // 2^-36 or Z + 2^-20 A > 2^60 (or NaN) marks the block bad: the exact fix-up launch redoes it.
 template <int R>
-__device__ __forceinline__ bool block_zc_unsafe(int tid, bmask_t mask, const FrameParams* __restrict__ fps, int xb,
-                                                int yb, int zb, float voxel_size) {
-    const int j = tid >> 3, c = tid & 7;
-    if (j >= 64 || !((mask >> j) & 1)) return false;
+__device__ __forceinline__ bool block_zc_unsafe_frame(int j, int c, const FrameParams* __restrict__ fps, int xb, int yb,
+                                                      int zb, float voxel_size) {
     const FrameParams& fp = fps[j];
     const float xl = (float)(xb * R) * voxel_size, xh = (float)(xb * R + R - 1) * voxel_size;
     const float yl = (float)(yb * R) * voxel_size, yh = (float)(yb * R + R - 1) * voxel_size;
@@ -1027,6 +1042,16 @@ __device__ __forceinline__ bool block_zc_unsafe(int tid, bmask_t mask, const Fra
                      fmax(fabs((double)zl), fabs((double)zh)) * fabs(e10) + fabs(e11);
     const double err = A * 0x1p-20;
     return !(Z - err >= 0x1p-36 && Z + err <= 0x1p60);
+}
+
+template <int R>
+__device__ __forceinline__ bool block_zc_unsafe(int tid, bmask_t mask, const FrameParams* __restrict__ fps, int xb,
+                                                int yb, int zb, float voxel_size) {
+    const int c = tid & 7;
+    bool unsafe = false;
+    for (int j = tid >> 3; j < kMaxBatch; j += 64)  // 512 threads: 64 frames x 8 corners per round
+        if ((mask >> j) & 1) unsafe |= block_zc_unsafe_frame<R>(j, c, fps, xb, yb, zb, voxel_size);
+    return unsafe;
 }
 
 // Hand a block to the exact fix-up launch (its (slot, batch mask) appended to bad_out).
@@ -1118,7 +1143,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
     for (; i < iend; i += step) {
         const int32_t slot = list[i];
         const int buf = __builtin_amdgcn_readfirstlane(t.vals[slot]);
-        const bmask_t mask = readfirstlane_u64(lmask ? lmask[i] : t.mask[slot]);
+        const bmask_t mask = readfirstlane_mask(lmask ? lmask[i] : bm_frames(t.mask[slot]));
         int xb, yb, zb;
         unpack_key(t.keys[slot], xb, yb, zb);
         if (buf >= 0 && mask) {
@@ -1138,8 +1163,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
                 xs[k] = xs0;
                 ys[k] = (float)(yb * R + vy + dy) * voxel_size;
                 zs[k] = (float)(zb * R + vz + dz) * voxel_size;
-                const float w = tw[k].y;  // rcp_m(w + 1) needs integer weights (a batch adds <= 64)
-                bad |= !(w >= 0.0f && w <= 0x1p23f && w == __builtin_truncf(w));
+                const float w = tw[k].y;  // rcp_m(w + 1) is exact for integer w <= 2^23 + 64: a batch adds <= 127
+                bad |= !(w >= 0.0f && w <= 0x1p23f - 64.0f && w == __builtin_truncf(w));
             }
             bmask_t m = mask;
             if constexpr (PAIR == 3 || ZBLK) {  // block-level zc range check (block_zc_unsafe): skip the frame loop
@@ -1147,7 +1172,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
                 if (__syncthreads_or(block_zc_unsafe<R>(tid, mask, fps, xb, yb, zb, voxel_size))) bad = true, m = 0;
             }
             while (m) {
-                const int f = __builtin_ctzll(m);
+                const int f = bm_ctz(m);
                 m &= m - 1;
                 float dv[ZPER];
                 if constexpr (PAIR == 6 || PAIR == 7) {  // windows in two halves: <= 4 window loads in flight
