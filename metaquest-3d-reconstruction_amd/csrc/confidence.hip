@@ -336,6 +336,63 @@ __device__ __forceinline__ Stage32 decide32_stage1(const float* __restrict__ tgt
     return r;
 }
 
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+// decide32_stage1 without branches (BF): every lane evaluates the whole chain and the decision is
+// selected at the end; the two tap rows are read by buffer loads whose offset is past the frame's
+// end (reads 0, which fails the tap test) for lanes that do not reach them.  The same decisions as
+// decide32_stage1 (NaN operands still fail every test they meet); the frame's byte count 4HW + 4W
+// must fit 31 bits (host).
+__device__ __forceinline__ Stage32 decide32_stage1_bf(__amdgpu_buffer_rsrc_t rs, uint32_t W4, uint32_t past_end,
+                                                      int W, int H, float wm1, float hm1, const ConfFrame& ft,
+                                                      const Pix32& px) {
+    constexpr float u = 0x1p-24f;
+    Stage32 r;
+    const float* T = ft.Tf;
+    const float X = __builtin_fmaf(T[0], px.p[0], __builtin_fmaf(T[1], px.p[1], __builtin_fmaf(T[2], px.p[2], T[3])));
+    const float Y = __builtin_fmaf(T[4], px.p[0], __builtin_fmaf(T[5], px.p[1], __builtin_fmaf(T[6], px.p[2], T[7])));
+    const float Z = __builtin_fmaf(T[8], px.p[0], __builtin_fmaf(T[9], px.p[1], __builtin_fmaf(T[10], px.p[2], T[11])));
+    const float EX = __builtin_fmaf(ft.ea[0], px.m, ft.eb[0]);
+    const float EY = __builtin_fmaf(ft.ea[1], px.m, ft.eb[1]);
+    const float EZ = __builtin_fmaf(ft.ea[2], px.m, ft.eb[2]);
+    const float zl = Z - EZ, zh = Z + EZ;
+    r.Z = Z;
+    r.EZ = EZ;
+    const bool none_z = (Z <= -EZ) | (zl > px.zhi);
+    const bool ok_z = (zl > 0.0f) & (zh < px.zlo) & (EZ <= 0.125f * Z) & (Z >= 1e-6f);
+    const float inv = __builtin_amdgcn_rcpf(Z);
+    const float qx = (X * ft.fxf) * inv, qy = (Y * ft.fyf) * inv;
+    const float uu = qx + ft.cxf, vv = qy + ft.cyf;
+    const float irl = inv * (1.0f + 2.0f * EZ * inv);
+    const float ezr = EZ * irl;
+    const float Eu = __builtin_fabsf(ft.fxf) * inv * (EX + (__builtin_fabsf(X) + EX) * ezr) * (1.0f + 16.0f * u) +
+                     5.0f * u * __builtin_fabsf(qx) + 2.0f * u * __builtin_fabsf(uu);
+    const float Ev = __builtin_fabsf(ft.fyf) * inv * (EY + (__builtin_fabsf(Y) + EY) * ezr) * (1.0f + 16.0f * u) +
+                     5.0f * u * __builtin_fabsf(qy) + 2.0f * u * __builtin_fabsf(vv);
+    const bool out_rng = (uu + Eu < 0.0f) | (uu - Eu > wm1) | (vv + Ev < 0.0f) | (vv - Ev > hm1);
+    const float fu0 = __builtin_floorf(uu), fv0 = __builtin_floorf(vv);
+    const float ru = uu - fu0, rv = vv - fv0;
+    const bool sure = (ru >= Eu) & (ru + Eu < 1.0f) & (rv >= Ev) & (rv + Ev < 1.0f) & (uu < 0x1p22f) & (vv < 0x1p22f);
+    const int u0 = (int)fu0, v0 = (int)fv0;
+    const bool in_img = (u0 >= 0) & (u0 + 1 < W) & (v0 >= 0) & (v0 + 1 < H);
+    // none_z -> 0; else !ok_z -> -1; else out of range -> 0; else floor uncertain -> -1; else out of
+    // the image -> 0; else taps
+    const bool go = !none_z & ok_z & !out_rng & sure & in_img;
+    r.st = go ? 1 : (none_z | (ok_z & (out_rng | (sure & !in_img)))) ? 0 : -1;
+    r.P = __builtin_fmaf(X, X, __builtin_fmaf(Y, Y, Z * Z));
+    r.EP = 2.0f * (__builtin_fabsf(X) * EX + __builtin_fabsf(Y) * EY + Z * EZ) + (EX * EX + EY * EY + EZ * EZ) +
+           8.0f * u * r.P;
+    r.uu = uu;
+    r.vv = vv;
+    r.Eu = Eu;
+    r.Ev = Ev;
+    const uint32_t off = go ? __umul24((uint32_t)v0, W4) + ((uint32_t)u0 << 2) : past_end;
+    const u32x2 a = __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0);
+    const u32x2 c = __builtin_amdgcn_raw_buffer_load_b64(rs, off + W4, 0, 0);
+    r.ab = make_float2(__uint_as_float(a.x), __uint_as_float(a.y));
+    r.cd = make_float2(__uint_as_float(c.x), __uint_as_float(c.y));
+    return r;
+}
+
 // Stage 2: the tap test and the band filter on the float32 values (see the comment above); returns
 // 0 / 1 / 2, or -1 when the float64 path must decide.
 __device__ __forceinline__ int decide32_stage2(const Stage32& r, const Pix32& px, float dmf) {
@@ -376,7 +433,7 @@ __device__ inline int ref_point(const ConfFrame& fr, int u, int v, float dref, d
 // `err <= threshold` on the float32 error map is d2 <= d2_max (sqrt and both roundings monotone).
 // STATS: count the pairs per deciding stage into st[4] (pairs, float32 prefilter, float64 filter,
 // float64 back-projection) -- mqr_confidence_stats.
-template <bool STATS, bool WIDE, bool DIAG = false>
+template <bool STATS, bool WIDE, bool DIAG = false, bool BF = false>
 __global__ __launch_bounds__(256) void k_confidence(const float* __restrict__ depths, int N, int H, int W,
                                                     const ConfFrame* __restrict__ fr, int ref_begin, int r,
                                                     double depth_max, double d2_max, double sd,
@@ -440,12 +497,21 @@ __global__ __launch_bounds__(256) void k_confidence(const float* __restrict__ de
             uint64_t defer = 0;
             int t = next_t(clo - 1);
             Stage32 cur;
-            if (t < chi) cur = decide32_stage1<DIAG>(depths + (int64_t)t * HW, W, H, wm1f, hm1f, fr[t], px);
+            const uint32_t fbytes = 4u * (uint32_t)HW, W4 = 4u * (uint32_t)W;
+            auto stage1 = [&](int tt) {
+                if constexpr (BF)
+                    return decide32_stage1_bf(__builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(depths + (int64_t)tt * HW),
+                                                                                (short)0, (int)fbytes, 0x00020000),
+                                              W4, fbytes, W, H, wm1f, hm1f, fr[tt], px);
+                else
+                    return decide32_stage1<DIAG>(depths + (int64_t)tt * HW, W, H, wm1f, hm1f, fr[tt], px);
+            };
+            if (t < chi) cur = stage1(t);
 #pragma clang loop unroll(disable)
             while (t < chi) {
                 const int t2 = next_t(t);
                 Stage32 nxt;
-                if (t2 < chi) nxt = decide32_stage1<DIAG>(depths + (int64_t)t2 * HW, W, H, wm1f, hm1f, fr[t2], px);
+                if (t2 < chi) nxt = stage1(t2);
                 const int dcs = decide32_stage2(cur, px, dmf);
                 if (STATS) {
                     ++n_pairs;
@@ -614,6 +680,7 @@ struct ConfCache {
     int cap = 0;
     bool stats = false;                 // mqr_confidence_stats: count pairs per deciding stage
     bool diag = false;                  // mqr_confidence_stats enable = 2: no tap loads (timing only)
+    bool bf = false;                    // enable = 3: branch-free float32 stage 1 (A/B)
     unsigned long long* dst = nullptr;  // device counters [4]
     int64_t last[4] = {0, 0, 0, 0};     // pairs, float32 prefilter, float64 filter, float64 back-projection
 };
@@ -695,6 +762,9 @@ int mqr_confidence(int device, const float* depths, int depth_loc, int N, int H,
     } else if (cc.diag) {  // timing diagnostics only (wrong results): no tap loads
         hipLaunchKernelGGL((k_confidence<false, false, true>), grid, dim3(256), 0, s, dsrc, N, H, W, dfr, ref_begin,
                            frame_range, depth_max, d2max, sd, dconf, dvalid, nullptr);
+    } else if (cc.bf && !wide && 4 * (HW + W) < (int64_t{1} << 31)) {
+        hipLaunchKernelGGL((k_confidence<false, false, false, true>), grid, dim3(256), 0, s, dsrc, N, H, W, dfr,
+                           ref_begin, frame_range, depth_max, d2max, sd, dconf, dvalid, nullptr);
     } else if (wide) {
         hipLaunchKernelGGL((k_confidence<false, true>), grid, dim3(256), 0, s, dsrc, N, H, W, dfr, ref_begin,
                            frame_range, depth_max, d2max, sd, dconf, dvalid, nullptr);
@@ -732,6 +802,7 @@ int mqr_confidence_stats(int device, int enable, int64_t* last4) {
     if (enable >= 0) {
         cc.stats = enable == 1;
         cc.diag = enable == 2;
+        cc.bf = enable == 3;
     }
     if (last4)
         for (int i = 0; i < 4; ++i) last4[i] = cc.last[i];

@@ -14,5 +14,7 @@ MQR_HIP_LIB=tools/_ab/libmqr_ab.so timeout -k 10 300 python tools/ab_integrate.p
 cat gpurun_out/r04d_ab.json
 timeout -k 10 200 python tools/ab_extract.py --modes 0 --reps 15 > gpurun_out/r04d_abx.json 2> gpurun_out/r04d_abx.err || { tail -20 gpurun_out/r04d_abx.err; exit 1; }
 cat gpurun_out/r04d_abx.json
-timeout -k 10 200 python tools/conf_workload.py --reps 5 --diag > gpurun_out/r04d_conf.json 2> gpurun_out/r04d_conf.err || { tail -20 gpurun_out/r04d_conf.err; exit 1; }
+timeout -k 10 200 python tools/conf_workload.py --reps 5 --diag --ab 3 > gpurun_out/r04d_conf.json 2> gpurun_out/r04d_conf.err || { tail -20 gpurun_out/r04d_conf.err; exit 1; }
 cat gpurun_out/r04d_conf.json
+timeout -k 10 300 python bench.py > gpurun_out/r04d_bench.json 2> gpurun_out/r04d_bench.err || { tail -20 gpurun_out/r04d_bench.err; exit 1; }
+cat gpurun_out/r04d_bench.json
