@@ -384,10 +384,11 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
     //     6 / 7 paired-lane gathers;  8 VALU-lean projection / update, 9 + zc checked per block, 10 +
     //     one-correction s / trunc;  11 / 12 / 14 / 19 16-byte windows;  13 / 16 / 17 / 18 / 20 / 21 /
     //     22 8-byte windows at 6 waves / SIMD, with the block zc check, one-correction division, ILP 4,
-    //     in two halves (15 = the default).
+    //     in two halves (15 = the default);  23 default with the exact path in-kernel;  24 default with
+    //     wave slots wholly outside the image skipping their window load.
     //     DESIGN.md §4.1 has the measurements behind the choice.
     int var = v->kernel_variant;
-    if (var < 0 || var > 23) var = 0;
+    if (var < 0 || var > 24) var = 0;
     if (!MQR_AB && var != 1 && var != 2 && var != 4) var = 0;
     if (var != 1 && var != 2 && !lean_ok) var = 2;
     if (var == 5 && (v->R != 16 || W % 4 != 0 || W < 4 || (reinterpret_cast<uintptr_t>(depths) & 15))) var = 0;
@@ -472,6 +473,10 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
                 hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 7, 2, 5, 0, false, true>), dim3(lean_grid), dim3(512), 0,
                                    s, list, lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths,
                                    HW, H, W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
+            else if (var == 24)  // default + wave slots wholly outside the image skip their window load
+                hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 7, 2, 8>), dim3(lean_grid), dim3(512), 0, s, list,
+                                   lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H,
+                                   W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
             else if (var == 10)  // variant 9 with s / sdf_trunc in one correction (verified for this sdf_trunc)
                 hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 8, 2, 3, 1>), dim3(lean_grid), dim3(512), 0, s, list,
                                    lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H,

@@ -956,7 +956,9 @@ __device__ __forceinline__ void lean_gather_v(float (&dv)[ZPER], bool& bad, cons
 // multiple of the window (host): then an in-image window never crosses the end of the frame, and an
 // out-of-image lane's window at 4HW is wholly past the end (reads 0).
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-template <int ZPER, int ILP = 1, int WIN = 16, bool ZCHK = true, int K0 = 0, int K1 = ZPER>
+// SKIP: a voxel slot k whose 64 lanes all project outside the image issues no load (wave-uniform
+// branch on the ballot; dv = 0, which the update skips).
+template <int ZPER, int ILP = 1, int WIN = 16, bool ZCHK = true, int K0 = 0, int K1 = ZPER, bool SKIP = false>
 __device__ __forceinline__ void lean_gather_w(float (&dv)[ZPER], bool& bad, const FrameParams& fp,
                                               __amdgpu_buffer_rsrc_t rs, const float (&xs)[ZPER],
                                               const float (&ys)[ZPER], const float (&zs)[ZPER], uint32_t W4,
@@ -979,6 +981,13 @@ __device__ __forceinline__ void lean_gather_w(float (&dv)[ZPER], bool& bad, cons
         const float v = fy * yc * inv_z + cy;
         const bool in = (__float_as_uint(v) <= hm1_bits) && (__float_as_uint(u) <= wm1_bits);
         const uint32_t off = in ? __umul24((uint32_t)(int)v, W4) + ((uint32_t)(int)u << 2) : past_end;
+        if constexpr (SKIP) {
+            if (__builtin_amdgcn_ballot_w64(in) == 0) {
+                dv[k] = 0.0f;
+                if ((k + 1) % ILP == 0) __builtin_amdgcn_sched_barrier(0);
+                continue;
+            }
+        }
         if constexpr (WIN == 16) {
             const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(rs, off & ~15u, 0, 0);
             const uint32_t lo = (off & 8u) ? q.z : q.x, hi = (off & 8u) ? q.w : q.y;
@@ -1188,6 +1197,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
                                                                  __float_as_uint(hm1), __float_as_uint(wm1));
                     __builtin_amdgcn_sched_barrier(0);
                     lean_update_v<ZPER, ILP, DIV1, H2, ZPER>(tw, dv, fps[f], xs, ys, zs, depth_max, sdf_trunc, y1t);
+                    continue;
+                } else if constexpr (PAIR == 8) {  // 8-byte windows, out-of-image wave slots skipped
+                    lean_gather_w<ZPER, ILP, 8, !ZBLK, 0, ZPER, true>(dv, bad, fps[f],
+                                                                      frame_rsrc(depths + depth_frame[f] * HW, bytes),
+                                                                      xs, ys, zs, W4, bytes, __float_as_uint(hm1),
+                                                                      __float_as_uint(wm1));
+                    lean_update_v<ZPER, ILP, DIV1>(tw, dv, fps[f], xs, ys, zs, depth_max, sdf_trunc, y1t);
                     continue;
                 } else if constexpr (PAIR == 4 || PAIR == 5) {
                     lean_gather_w<ZPER, ILP, PAIR == 4 ? 16 : 8, !ZBLK>(dv, bad, fps[f], frame_rsrc(depths + depth_frame[f] * HW, bytes),
