@@ -212,7 +212,8 @@ int mqr_vbg_profile(mqr_vbg* v, int enable);
  * where its preconditions hold, 1 generic, 2 exact R-specialised, 3 lean with the plate map, 5 depth
  * from LDS tiles; all bit-identical, see launch_integrate in csrc/vbg.hip); bit 8 serialises touch and integrate, bit 9 keeps touch
  * order instead of longest-first, bit 10 uses 32-frame batches instead of 127 (the first of a call: 64;
- * bit 20: 64-frame batches, bit 21: no shorter first batch), bit 11 records
+ * bit 20: 64-frame batches, bit 21: no shorter first batch, bits 22 / 23: a first batch of 32 / 16),
+ * bit 11 records
  * system-scope ordering events, bit 12 probes one table slot per new key in the batch touch (forces
  * the full-table undo-and-retry path; test hook), bit 13 sizes the table for the worst case, bit 14 makes
  * every integrate launch wait on a touch-stream event, bit 15 runs the batch in spatial per-XCD groups

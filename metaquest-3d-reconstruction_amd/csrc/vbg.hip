@@ -1212,7 +1212,8 @@ int mqr_vbg_set_variant(mqr_vbg* v, int variant) {
     v->lpt_order = (variant & 0x200) == 0;  // bit 9: integrate in touch order instead of longest-first
     // bit 10: 32-frame batches; bit 20: 64-frame batches (round 3); bit 21: no shorter first batch (A/Bs)
     v->batch_frames = (variant & 0x400) ? 32 : (variant & 0x100000) ? 64 : kMaxBatch;
-    v->first_batch_frames = (variant & 0x200000) ? kMaxBatch : kFirstBatch;
+    // bits 22 / 23: a first batch of 32 / 16 frames (A/B of the step head)
+    v->first_batch_frames = (variant & 0x200000) ? kMaxBatch : (variant & 0x400000) ? 32 : (variant & 0x800000) ? 16 : kFirstBatch;
     v->sys_fence = (variant & 0x800) != 0;  // bit 11: system-scope ordering / timing events (A/B)
     v->probe_one = (variant & 0x1000) != 0; // bit 12: force the full-table retry path (test hook)
     v->table_worst = (variant & 0x2000) != 0; // bit 13: size the table for the worst case (round-2 A/B)

@@ -64,7 +64,22 @@ def project(keys, x, y, z, E, K):
     inimg = (u >= 0) & (v >= 0) & (u <= W - 1) & (v <= H - 1) & (zc > 0)
     ui = np.clip(np.nan_to_num(u), 0, W - 1).astype(np.int64)
     vi = np.clip(np.nan_to_num(v), 0, H - 1).astype(np.int64)
-    return zc, inimg, vi * W + ui
+    return zc, inimg, vi * W + ui, u, v
+
+
+TILE = int(os.environ.get("MQR_WS_TILE", "16"))
+
+
+def tile_max_dilated(d):
+    """Per TILE x TILE pixel tile: the largest valid depth (0 < d <= DMAX; -inf if none), then the
+    maximum over each tile's 3 x 3 tile neighbourhood."""
+    th, tw = -(-H // TILE), -(-W // TILE)
+    dd = np.where((d > 0) & (d <= DMAX), d, -np.inf).astype(np.float32)
+    pad = np.full((th * TILE, tw * TILE), -np.inf, np.float32)
+    pad[:H, :W] = dd
+    t = pad.reshape(th, TILE, tw, TILE).max(axis=(1, 3))
+    p = np.pad(t, 1, constant_values=-np.inf)
+    return np.max([p[i:i + th, j:j + tw] for i in range(3) for j in range(3)], axis=0)
 
 
 def main():
@@ -78,14 +93,21 @@ def main():
     bk = 4 * (yy // 8) + (zz // 4)        # and its voxel slot k
     brick = bw * 8 + bk
     tot = dict(voxel_frames=0, outside_image=0, invalid_depth=0, behind_surface=0, update=0)
-    bricks = dead_bricks = out_bricks = pairs = dead_pairs = 0
+    bricks = dead_bricks = out_bricks = pairs = dead_pairs = tile_bricks = 0
+    # lane 0 of each wave slot (brick id w * 8 + k): x = 8 (w % 2), y = 2 (w // 2) + 8 (k // 4), z = 4 (k % 4)
+    lane0 = np.zeros(64, np.int64)
+    for w in range(8):
+        for k in range(8):
+            x0, y0, z0 = 8 * (w % 2), 2 * (w // 2) + 8 * (k // 4), 4 * (k % 4)
+            lane0[w * 8 + k] = (z0 * R + y0) * R + x0
     quad = {name: [0, 0] for name in lane_maps()}
     for f in range(len(poses)):
         keys = oracle.touch(D[f], K[f], T[f], VS, R, 1.0, DMAX, 10.0)
         E = T[f].astype(np.float32)
+        tmd = tile_max_dilated(D[f])
         for c in range(0, len(keys), 256):
             kk = keys[c:c + 256]
-            zc, inimg, pix = project(kk, xx, yy, zz, E, K[f])
+            zc, inimg, pix, uu, vv = project(kk, xx, yy, zz, E, K[f])
             d = D[f].reshape(-1)[pix]
             dv = inimg & (d > 0) & (d <= DMAX)
             upd = dv & (d - zc >= -TAU)
@@ -99,6 +121,19 @@ def main():
             np.logical_or.at(ub, (rows, np.tile(brick, len(kk))), upd.ravel())
             ib = np.zeros((len(kk), 64), bool)
             np.logical_or.at(ib, (rows, np.tile(brick, len(kk))), inimg.ravel())
+            # tile cull: lane 0's pixel picks a tile; a lane is certainly not
+            # updating when outside the image, or within 16 px of lane 0's pixel (so its own tile is in
+            # the 3 x 3 neighbourhood) with zc - (neighbourhood max depth) > trunc
+            l0 = lane0[brick]                                      # per voxel: its slot's lane-0 voxel
+            u0, v0, in0 = uu[:, l0], vv[:, l0], inimg[:, l0]
+            t0 = np.where(in0, tmd[np.clip(np.nan_to_num(v0), 0, H - 1).astype(np.int64) // TILE,
+                                   np.clip(np.nan_to_num(u0), 0, W - 1).astype(np.int64) // TILE], np.inf)
+            with np.errstate(invalid="ignore"):
+                near = (np.abs(uu - u0) < TILE) & (np.abs(vv - v0) < TILE)
+                sure = (~inimg) | (near & (zc - t0 > TAU))
+            sb = np.ones((len(kk), 64), bool)
+            np.logical_and.at(sb, (rows, np.tile(brick, len(kk))), sure.ravel())
+            tile_bricks += int((sb & ib).sum())
             bricks += ub.size
             dead_bricks += int((~ub).sum())
             out_bricks += int((~ib).sum())
@@ -110,7 +145,7 @@ def main():
                 for w in range(8):
                     for k in range(8):
                         x, y, z = mp(w, LANE, k)
-                        _, inimg, pix = project(sub, x, y, z, E, K[f])
+                        _, inimg, pix, _, _ = project(sub, x, y, z, E, K[f])
                         q = np.sort(np.where(inimg, pix, -1).reshape(len(sub), 16, 4), axis=2)
                         distinct = (q[:, :, 1:] != q[:, :, :-1]).sum(2) + 1 - (q[:, :, 0] == -1)
                         quad[name][0] += int(distinct.sum())
@@ -120,6 +155,7 @@ def main():
            "fractions": {k: v / tot["voxel_frames"] for k, v in tot.items() if k != "voxel_frames"},
            "wave_bricks_without_update": dead_bricks / bricks,
            "wave_bricks_entirely_outside_image": out_bricks / bricks,
+           "wave_bricks_in_image_culled_by_tile_max": tile_bricks / bricks, "cull_tile_px": TILE,
            "block_frame_pairs_without_update": dead_pairs / pairs, "block_frame_pairs": pairs,
            "distinct_quad_pixels_per_64_lane_gather": {n: q / g for n, (q, g) in quad.items()}}
     print(json.dumps(out, indent=1))
