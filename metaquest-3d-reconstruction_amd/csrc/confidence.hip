@@ -362,22 +362,25 @@ __device__ __forceinline__ Stage32 decide32_stage1_bf(__amdgpu_buffer_rsrc_t rs,
     const float inv = __builtin_amdgcn_rcpf(Z);
     const float qx = (X * ft.fxf) * inv, qy = (Y * ft.fyf) * inv;
     const float uu = qx + ft.cxf, vv = qy + ft.cyf;
-    const float irl = inv * (1.0f + 2.0f * EZ * inv);
-    const float ezr = EZ * irl;
-    const float Eu = __builtin_fabsf(ft.fxf) * inv * (EX + (__builtin_fabsf(X) + EX) * ezr) * (1.0f + 16.0f * u) +
-                     5.0f * u * __builtin_fabsf(qx) + 2.0f * u * __builtin_fabsf(uu);
-    const float Ev = __builtin_fabsf(ft.fyf) * inv * (EY + (__builtin_fabsf(Y) + EY) * ezr) * (1.0f + 16.0f * u) +
-                     5.0f * u * __builtin_fabsf(qy) + 2.0f * u * __builtin_fabsf(vv);
-    const bool out_rng = (uu + Eu < 0.0f) | (uu - Eu > wm1) | (vv + Ev < 0.0f) | (vv - Ev > hm1);
+    // |uu - uu*| <= |fx| (E_X + |X| E_Z / Z) / (Z - E_Z) + rounding = (|fx| E_X + |fx X / Z| E_Z) / (Z - E_Z)
+    // + ...: the same bound as decide32_stage1's written with qx = fx X / Z (its float value within 3u,
+    // covered with the bound's own roundings by the 1 + 16u factor; every term is positive)
+    const float irl = inv * (1.0f + 2.0f * EZ * inv);  // >= 1 / (Z - E_Z) for E_Z <= Z / 8
+    const float Eu = __builtin_fmaf(__builtin_fabsf(ft.fxf), EX, __builtin_fabsf(qx) * EZ) * irl * (1.0f + 16.0f * u) +
+                     (5.0f * u * __builtin_fabsf(qx) + 2.0f * u * __builtin_fabsf(uu));
+    const float Ev = __builtin_fmaf(__builtin_fabsf(ft.fyf), EY, __builtin_fabsf(qy) * EZ) * irl * (1.0f + 16.0f * u) +
+                     (5.0f * u * __builtin_fabsf(qy) + 2.0f * u * __builtin_fabsf(vv));
     const float fu0 = __builtin_floorf(uu), fv0 = __builtin_floorf(vv);
-    const float ru = uu - fu0, rv = vv - fv0;
-    const bool sure = (ru >= Eu) & (ru + Eu < 1.0f) & (rv >= Ev) & (rv + Ev < 1.0f) & (uu < 0x1p22f) & (vv < 0x1p22f);
+    const float ru = uu - fu0, rv = vv - fv0;  // exact for every float
+    // floor certain: uu, vv at least E away from an integer (implies |uu|, |vv| < 2^23, where ru > 0 is
+    // possible, so the int conversions below cannot saturate; NaN fails it)
+    const bool sure = (ru >= Eu) & (ru + Eu < 1.0f) & (rv >= Ev) & (rv + Ev < 1.0f);
     const int u0 = (int)fu0, v0 = (int)fv0;
     const bool in_img = (u0 >= 0) & (u0 + 1 < W) & (v0 >= 0) & (v0 + 1 < H);
-    // none_z -> 0; else !ok_z -> -1; else out of range -> 0; else floor uncertain -> -1; else out of
-    // the image -> 0; else taps
-    const bool go = !none_z & ok_z & !out_rng & sure & in_img;
-    r.st = go ? 1 : (none_z | (ok_z & (out_rng | (sure & !in_img)))) ? 0 : -1;
+    // none_z -> 0; else !ok_z or the floors uncertain -> -1 (near the image border too: rare); else
+    // out of the image -> 0; else taps
+    const bool go = !none_z & ok_z & sure & in_img;
+    r.st = go ? 1 : (none_z | (ok_z & sure)) ? 0 : -1;
     r.P = __builtin_fmaf(X, X, __builtin_fmaf(Y, Y, Z * Z));
     r.EP = 2.0f * (__builtin_fabsf(X) * EX + __builtin_fabsf(Y) * EY + Z * EZ) + (EX * EX + EY * EY + EZ * EZ) +
            8.0f * u * r.P;
