@@ -398,12 +398,17 @@ __device__ __forceinline__ Stage32 decide32_stage1_bf(__amdgpu_buffer_rsrc_t rs,
 
 // Stage 2: the tap test and the band filter on the float32 values (see the comment above); returns
 // 0 / 1 / 2, or -1 when the float64 path must decide.
-__device__ __forceinline__ int decide32_stage2(const Stage32& r, const Pix32& px, float dmf) {
+// dmb: the bits of depth_max as float32 when it is > 0, else 0.  A tap passes the reference's
+// 0 < I <= depth_max exactly when bits(I) - 1 < dmb as unsigned integers: positive floats (and +inf)
+// order like their bits, +-0, negatives and NaNs fall outside -- four subtractions, two maxima and one
+// compare for the eight float compares.
+__device__ __forceinline__ int decide32_stage2(const Stage32& r, const Pix32& px, uint32_t dmb) {
     constexpr float u = 0x1p-24f;
     if (r.st <= 0) return r.st;
     const float Ia = r.ab.x, Ib = r.ab.y, Ic = r.cd.x, Id = r.cd.y;
-    const bool taps = (Ib > 0) & (Ib <= dmf) & (Ia > 0) & (Ia <= dmf) & (Ic > 0) & (Ic <= dmf) & (Id > 0) & (Id <= dmf);
-    if (!taps) return 0;
+    const uint32_t tmax = max(max(__float_as_uint(Ia) - 1u, __float_as_uint(Ib) - 1u),
+                              max(__float_as_uint(Ic) - 1u, __float_as_uint(Id) - 1u));
+    if (!(tmax < dmb)) return 0;
     const float fu0 = __builtin_floorf(r.uu), fv0 = __builtin_floorf(r.vv);
     const float fu = r.uu - fu0, fv = r.vv - fv0;
     const float gu = (fu0 + 1.0f) - r.uu, gv = (fv0 + 1.0f) - r.vv;
@@ -470,6 +475,7 @@ __global__ __launch_bounds__(256) void k_confidence(const float* __restrict__ de
         const double hi2 = bhi * bhi * (1.0 + 1e-12);
         const double zmax = fmin(depth_max, 0x1.fffffffffffffp1023);
         const float dmf = (float)depth_max;
+        const uint32_t dmb = dmf > 0.0f ? __float_as_uint(dmf) : 0u;
         const double wm1 = (double)(W - 1), hm1 = (double)(H - 1);
         Pix32 px;
         float mx = 0.0f;
@@ -515,7 +521,7 @@ __global__ __launch_bounds__(256) void k_confidence(const float* __restrict__ de
                 const int t2 = next_t(t);
                 Stage32 nxt;
                 if (t2 < chi) nxt = stage1(t2);
-                const int dcs = decide32_stage2(cur, px, dmf);
+                const int dcs = decide32_stage2(cur, px, dmb);
                 if (STATS) {
                     ++n_pairs;
                     n_f32 += dcs >= 0;
