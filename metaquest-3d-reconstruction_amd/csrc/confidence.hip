@@ -425,6 +425,29 @@ __device__ __forceinline__ int decide32_stage2(const Stage32& r, const Pix32& px
     return -1;
 }
 
+// decide32_stage2 without branches (BF): every lane consumes its taps (an early return left tap loads
+// in flight past the loop's back edge, and the compiler waited for them where their registers were
+// reused) and the decision is selected at the end -- the same decisions.
+__device__ __forceinline__ int decide32_stage2_bf(const Stage32& r, const Pix32& px, uint32_t dmb) {
+    constexpr float u = 0x1p-24f;
+    const float Ia = r.ab.x, Ib = r.ab.y, Ic = r.cd.x, Id = r.cd.y;
+    const uint32_t tmax = max(max(__float_as_uint(Ia) - 1u, __float_as_uint(Ib) - 1u),
+                              max(__float_as_uint(Ic) - 1u, __float_as_uint(Id) - 1u));
+    const float fu0 = __builtin_floorf(r.uu), fv0 = __builtin_floorf(r.vv);
+    const float fu = r.uu - fu0, fv = r.vv - fv0;
+    const float gu = (fu0 + 1.0f) - r.uu, gv = (fv0 + 1.0f) - r.vv;
+    const float zf = __builtin_fmaf(fu * fv, Id, __builtin_fmaf(gu * fv, Ic, __builtin_fmaf(fu * gv, Ib, (gu * gv) * Ia)));
+    const float Edz = r.EZ + r.Eu * (__builtin_fabsf(Ib - Ia) + __builtin_fabsf(Id - Ic)) +
+                      r.Ev * (__builtin_fabsf(Ic - Ia) + __builtin_fabsf(Id - Ib)) + 8.0f * u * zf;
+    const float dz = __builtin_fabsf(r.Z - zf);
+    const float zl = r.Z - r.EZ, zh = r.Z + r.EZ;
+    const float a1 = dz + Edz, a0 = dz - Edz;
+    const bool in_band_lo = a1 * a1 * (r.P + r.EP) * (1.0f + 16.0f * u) <= px.lo2 * (zl * zl) * (1.0f - 16.0f * u);
+    const bool out_band_hi = (a0 > 0.0f) & (a0 * a0 * (r.P - r.EP) * (1.0f - 16.0f * u) > px.hi2 * (zh * zh) * (1.0f + 16.0f * u));
+    const int d = in_band_lo ? 1 : out_band_hi ? 2 : -1;
+    return r.st <= 0 ? r.st : !(tmax < dmb) ? 0 : d;
+}
+
 // depth_to_pointcloud_numpy for one pixel: returns 0 when the ref pixel is not in (0, depth_max].
 __device__ inline int ref_point(const ConfFrame& fr, int u, int v, float dref, double depth_max, double pw[3]) {
     if (!(dref > 0 && dref <= (float)depth_max)) return 0;
@@ -495,9 +518,9 @@ __global__ __launch_bounds__(256) void k_confidence(const float* __restrict__ de
         // the other's are computed; pairs the float32 path cannot decide are collected in `defer`
         // (bit t - lo) and decided by the float64 path after the loop (outside the hot loop's registers)
         // (WIDE: windows of more than 64 frames (r > 31), in chunks of 64 neighbours -- one defer bit each)
-#pragma clang loop unroll(disable)
-        for (int clo = lo; clo < hi; clo += 64) {
-            const int chi = WIDE ? min(hi, clo + 64) : hi;
+        // (one chunk without WIDE: no outer loop, whose back edge made the compiler assume tap loads in
+        // flight at the top of the neighbour loop and wait for them)
+        auto run_chunk = [&](const int clo, const int chi) {
             auto next_t = [&](int t) {
                 for (++t; t < chi; ++t)
                     if (t != ref && fr[t].ok) break;  // the reference frame and frames not ok are skipped
@@ -505,7 +528,6 @@ __global__ __launch_bounds__(256) void k_confidence(const float* __restrict__ de
             };
             uint64_t defer = 0;
             int t = next_t(clo - 1);
-            Stage32 cur;
             const uint32_t fbytes = 4u * (uint32_t)HW, W4 = 4u * (uint32_t)W;
             auto stage1 = [&](int tt) {
                 if constexpr (BF)
@@ -515,22 +537,33 @@ __global__ __launch_bounds__(256) void k_confidence(const float* __restrict__ de
                 else
                     return decide32_stage1<DIAG>(depths + (int64_t)tt * HW, W, H, wm1f, hm1f, fr[tt], px);
             };
-            if (t < chi) cur = stage1(t);
-#pragma clang loop unroll(disable)
-            while (t < chi) {
-                const int t2 = next_t(t);
-                Stage32 nxt;
-                if (t2 < chi) nxt = stage1(t2);
-                const int dcs = decide32_stage2(cur, px, dmb);
+            auto account = [&](const Stage32& st, int tt) {
+                const int dcs = BF ? decide32_stage2_bf(st, px, dmb) : decide32_stage2(st, px, dmb);
                 if (STATS) {
                     ++n_pairs;
                     n_f32 += dcs >= 0;
                 }
-                if (dcs < 0) defer |= 1ull << (t - clo);
+                if (dcs < 0) defer |= 1ull << (tt - clo);
                 nv += dcs > 0;
                 nc += dcs == 1;
-                t = t2;
-                cur = nxt;
+            };
+            // unrolled by two with the stages' roles alternating, and stage 1 issued unconditionally (past
+            // the last neighbour it re-runs the current one, result unused): a `cur = nxt` copy of the tap
+            // registers, or loads issued on only one path, made the compiler wait at the end of every
+            // iteration for the loads it had just issued
+            if (t < chi) {
+                Stage32 a = stage1(t), b;
+#pragma clang loop unroll(disable)
+                while (true) {
+                    const int t2 = next_t(t);
+                    b = stage1(t2 < chi ? t2 : t);
+                    account(a, t);
+                    if (t2 >= chi) break;
+                    t = next_t(t2);
+                    a = stage1(t < chi ? t : t2);
+                    account(b, t2);
+                    if (t >= chi) break;
+                }
             }
             while (defer) {
                 const int td = clo + __builtin_ctzll(defer);
@@ -541,7 +574,12 @@ __global__ __launch_bounds__(256) void k_confidence(const float* __restrict__ de
                 nv += dcs != 0;
                 nc += dcs == 1;
             }
-            if (!WIDE) break;
+        };
+        if constexpr (WIDE) {
+#pragma clang loop unroll(disable)
+            for (int clo = lo; clo < hi; clo += 64) run_chunk(clo, min(hi, clo + 64));
+        } else {
+            run_chunk(lo, hi);
         }
     }
     if (STATS) {
