@@ -28,10 +28,10 @@ python - <<'P'
 import json; d=json.load(open("gpurun_out/ev_bench.json"))
 print({k: d[k] for k in ("value","ms_per_step","extract_ms")}, d["roofline"], d["parity"]["all_ok"], d["c4"]["parity"]["all_ok"], d["c5"]["parity"]["all_ok"], d["confidence"]["ms"], d["build"])
 P
-rm -rf gpurun_out/ev_prof
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/ev_prof -o run -- \
+rm -rf /tmp/ev_prof
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d /tmp/ev_prof -o run -- \
   python bench.py --no-cpu --no-extras --steps 50 --warmup 5 > gpurun_out/ev_prof_bench.json 2> gpurun_out/ev_prof_bench.err \
   || { tail -20 gpurun_out/ev_prof_bench.err; exit 1; }
-find gpurun_out/ev_prof -name "*kernel_stats.csv" -exec cp {} gpurun_out/profiles_new/${ROUND}_bench_kernel_stats.csv \;
+find /tmp/ev_prof -name "*kernel_stats.csv" -exec cp {} gpurun_out/profiles_new/${ROUND}_bench_kernel_stats.csv \;
 grep "mqr" gpurun_out/profiles_new/${ROUND}_bench_kernel_stats.csv | cut -c1-60,300-420 | head -14
 echo evidence done
