@@ -220,7 +220,8 @@ int mqr_vbg_profile(mqr_vbg* v, int enable);
  * (k_xcd_order; A/Bs), bit 16 gives the touch one stride-4 pixel per thread instead of two, bit 17
  * touches with a frame per workgroup (k_touch_frame, A/B), bit 18 turns off the speculative first-batch
  * integrate (k_gate; A/B), bit 19 touches in two phases (strips collect their distinct keys, a workgroup
- * per frame deduplicates and claims them; A/B).
+ * per frame deduplicates and claims them; A/B), bit 24 touches 8 frames per strip workgroup with one claim
+ * per (block, frame group) (k_touch_mf; A/B).
  * mqr_check_division: exhaustive bit-pattern check of the division shortcuts used on device against
  * IEEE division (which=0: 1/b via rcp_rn, 1: a/b via div_rn, 2: a/b via the bare core, 3: 1/b via
  * rcp_nm, 4: 1/b via rcp_m, over float bit patterns [lo_bits, lo_bits+count) as b or a); returns

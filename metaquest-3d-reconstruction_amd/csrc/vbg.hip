@@ -628,7 +628,12 @@ static int touch_launch(mqr_vbg* v, int p, const float* dbase, int64_t HW, int H
                            max_probe, alloc, v->ctr(p), v->pool_ctr(), v->pool_cap, v->bkeys, v->lists[p], v->list_cap);
     } else if (n > 0)
     {
-        if (v->touch_frame)  // A/B: a frame per workgroup, claims of the frame's distinct blocks only
+        if (v->touch_mf)  // A/B: 8 frames per strip workgroup, one claim per (block, frame group)
+            hipLaunchKernelGGL((k_touch_mf<8, 2, 2048>), dim3((n + 511) / 512, (b + 7) / 8), dim3(256), 0, v->stream,
+                               dbase, HW, H, W, v->d_fp[p], dframe_dev(v, p), b, depth_scale, depth_max, sdf_trunc,
+                               block_size, t, max_probe, alloc, v->ctr(p), v->pool_ctr(), v->pool_cap, v->bkeys,
+                               v->lists[p], v->list_cap);
+        else if (v->touch_frame)  // A/B: a frame per workgroup, claims of the frame's distinct blocks only
             hipLaunchKernelGGL((k_touch_frame<1024, 4096>), dim3(1, b), dim3(1024), 0, v->stream, dbase, HW, H, W,
                                v->d_fp[p], dframe_dev(v, p), depth_scale, depth_max, sdf_trunc, block_size, t, max_probe,
                                alloc, v->ctr(p), v->pool_ctr(), v->pool_cap, v->bkeys, v->lists[p], v->list_cap);
@@ -1223,6 +1228,7 @@ int mqr_vbg_set_variant(mqr_vbg* v, int variant) {
     v->touch_frame = (variant & 0x20000) != 0;   // bit 17: k_touch_frame (a frame per workgroup; A/B, 2.3x slower)
     v->spec_head = (variant & 0x40000) == 0;     // bit 18: no speculative first-batch integrate (A/B)
     v->touch_two_phase = (variant & 0x80000) != 0;  // bit 19: two-phase touch (collect per strip, claim per frame)
+    v->touch_mf = (variant & 0x1000000) != 0;  // bit 24: k_touch_mf (8 frames per strip workgroup)
     return 0;
 }
 

@@ -523,6 +523,148 @@ __global__ __launch_bounds__(NT) void k_touch_claim(const uint64_t* __restrict__
     if (threadIdx.x == 0 && fsum) atomicAdd(&counters[kFreshBase + f], fsum);
 }
 
+// compute_unique_block_coordinates for FPW consecutive frames per workgroup (blockIdx.y = frame group,
+// f0 = FPW blockIdx.y; a strip of 256 PPT stride-4 pixels as k_touch).  Consecutive frames of a walk
+// see mostly the same blocks in a strip, so the strip's keys of all FPW frames go into one LDS set with
+// a frame mask per entry, and each distinct block is claimed ONCE for the group: one device-coherent
+// chain (probe, mask word atomicOr of all its frame bits, list append) where k_touch runs one per
+// (block, frame).  FPW divides 64, so a group's bits lie in one mask word.  Keys the set cannot take
+// (probe limit, 3/4 full) are claimed directly for their frame, as in k_touch_frame.
+// Sets frame bits `bits` (one word: word index wi) of the slot; `first` when the slot had no frame bit.
+__device__ __forceinline__ unsigned long long mask_set_frames(bmask_t* m, int wi, unsigned long long bits, bool& first) {
+    unsigned long long* w = reinterpret_cast<unsigned long long*>(m);
+    const unsigned long long old = atomicOr(&w[wi], bits);
+    first = false;
+    if (old == 0 || (wi == 1 && old == kListedBit))  // the word held no frame bit yet
+        first = !(atomicOr(&w[1], kListedBit) & kListedBit);
+    return old;
+}
+template <int FPW, int PPT, int SEEN>
+__global__ __launch_bounds__(256) void k_touch_mf(const float* __restrict__ depths, int64_t HW, int H, int W,
+                                                  const FrameParams* __restrict__ fps,
+                                                  const int64_t* __restrict__ depth_frame, int nframes,
+                                                  float depth_scale, float depth_max, float sdf_trunc,
+                                                  float block_size, Table t, int64_t max_probe, int alloc,
+                                                  int* counters, int* pool_ctr, int64_t pool_cap, uint64_t* bkeys,
+                                                  int32_t* list, int64_t list_cap) {
+    static_assert(64 % FPW == 0 && FPW <= 32, "a group's frame bits in one mask word, a u32 LDS mask");
+    static_assert(SEEN <= 65536 && (SEEN & (SEEN - 1)) == 0, "16-bit set indices, power of two");
+    constexpr int NT = 256, kProbe = 32, kFill = SEEN / 4 * 3;
+    __shared__ unsigned long long seen[SEEN];
+    __shared__ uint32_t fmask[SEEN];
+    __shared__ uint16_t uniq[SEEN];
+    __shared__ int nset, cnt_valid[FPW], cnt_fresh[FPW];
+    for (int i = threadIdx.x; i < SEEN; i += NT) {
+        seen[i] = kEmpty;
+        fmask[i] = 0;
+    }
+    if (threadIdx.x < FPW) cnt_valid[threadIdx.x] = cnt_fresh[threadIdx.x] = 0;
+    if (threadIdx.x == 0) nset = 0;
+    __syncthreads();
+    const int f0 = blockIdx.y * FPW, nf = min(FPW, nframes - f0);
+    const int cols = W / 4, rows = H / 4, n = rows * cols;
+    int wpx[PPT];
+#pragma unroll
+    for (int jp = 0; jp < PPT; ++jp) wpx[jp] = (blockIdx.x * PPT + jp) * NT + threadIdx.x;
+    auto read_depths = [&](int j, float (&dd)[PPT]) {
+        const float* __restrict__ dep = depths + depth_frame[f0 + j] * HW;
+#pragma unroll
+        for (int jp = 0; jp < PPT; ++jp) {
+            const int w = wpx[jp];
+            dd[jp] = w < n ? dep[(int64_t)((w / cols) * 4) * W + (w % cols) * 4] : 0.f;
+        }
+    };
+    float dnext[PPT];
+    read_depths(0, dnext);
+    int fresh_direct[FPW];  // direct claims' new bits, per frame of the group (rare)
+#pragma unroll
+    for (int j = 0; j < FPW; ++j) fresh_direct[j] = 0;
+    for (int j = 0; j < nf; ++j) {  // uniform trip count (direct claims need whole waves)
+        float dd[PPT];
+#pragma unroll
+        for (int jp = 0; jp < PPT; ++jp) dd[jp] = dnext[jp];
+        if (j + 1 < nf) read_depths(j + 1, dnext);  // the next frame's reads in flight
+        const FrameParams& fp = fps[f0 + j];
+        int valid = 0;
+#pragma unroll
+        for (int jp = 0; jp < PPT; ++jp) {
+            const int w = wpx[jp];
+            uint64_t key[4];
+            if (w < n)
+                valid += touch_pixel_keys(dd[jp], (w % cols) * 4, (w / cols) * 4, fp, depth_scale, depth_max, sdf_trunc,
+                                          block_size, counters, key);
+            else
+#pragma unroll
+                for (int s = 0; s < 4; ++s) key[s] = kEmpty;
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                uint64_t k = key[s];
+                if (s > 0 && key[s - 1] == k) k = kEmpty;
+                bool spill = false;
+                if (k != kEmpty) {
+                    uint32_t h = (uint32_t)mix64(k) & (SEEN - 1);
+                    spill = true;
+                    for (int p = 0; p < kProbe; ++p) {
+                        const unsigned long long cur = seen[h];
+                        bool here = cur == k;
+                        if (!here && cur == kEmpty) {
+                            if (*(volatile int*)&nset >= kFill) break;  // set nearly full: claim directly
+                            const unsigned long long old =
+                                atomicCAS(&seen[h], (unsigned long long)kEmpty, (unsigned long long)k);
+                            if (old == kEmpty) uniq[atomicAdd(&nset, 1)] = (uint16_t)h;
+                            here = old == kEmpty || old == k;
+                        }
+                        if (here) {
+                            atomicOr(&fmask[h], 1u << j);
+                            spill = false;
+                            break;
+                        }
+                        h = (h + 1) & (SEEN - 1);
+                    }
+                }
+                if (__ballot(spill))  // wave-uniform
+                    fresh_direct[j] += touch_claim(spill ? k : kEmpty, f0 + j, t, max_probe, alloc, counters, pool_ctr,
+                                                   pool_cap, bkeys, list, list_cap);
+            }
+        }
+        wave_add(&cnt_valid[j], valid);
+    }
+#pragma unroll
+    for (int j = 0; j < FPW; ++j) wave_add(&cnt_fresh[j], fresh_direct[j]);
+    __syncthreads();
+    // one claim per distinct block of the group: all its frame bits in one atomicOr
+    const int nu = min(nset, SEEN), wi = f0 >> 6, sh = f0 & 63;
+    for (int base = 0; base < nu; base += NT) {  // uniform trip count
+        const int idx = base + (int)threadIdx.x;
+        const uint64_t k = idx < nu ? seen[uniq[idx]] : kEmpty;
+        const uint32_t fb = idx < nu ? fmask[uniq[idx]] : 0u;
+        int64_t slot = -1;
+        bool won = false, first = false;
+        if (k != kEmpty) slot = table_claim(t, k, counters, won, max_probe);
+        if (alloc) wave_alloc(won, slot, k, t, counters, pool_ctr, pool_cap, bkeys);
+        if (slot >= 0) {
+            const unsigned long long bits = (unsigned long long)fb << sh;
+            unsigned long long* w = reinterpret_cast<unsigned long long*>(&t.mask[slot]);
+            const unsigned long long cur = __hip_atomic_load(&w[wi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((cur & bits) != bits) {  // (every bit already set: another strip claimed them)
+                const unsigned long long old = mask_set_frames(&t.mask[slot], wi, bits, first);
+                unsigned long long nb = (bits & ~old) >> sh;
+                while (nb) {
+                    atomicAdd(&cnt_fresh[__builtin_ctzll(nb)], 1);
+                    nb &= nb - 1;
+                }
+            }
+        }
+        wave_append(first, slot, counters, list, list_cap);
+    }
+    __syncthreads();
+    if (threadIdx.x < nf) {
+        const int j = threadIdx.x;
+        if (cnt_valid[j]) atomicAdd(&counters[kFrameCounterBase + f0 + j], cnt_valid[j]);
+        if (cnt_fresh[j]) atomicAdd(&counters[kFreshBase + f0 + j], cnt_fresh[j]);
+    }
+}
+
 // Activate explicit keys (vbg.integrate(block_coords, ...)); marks frame bit 0.
 __global__ void k_activate(const int32_t* __restrict__ keys, int64_t n, Table t, int* counters, int* pool_ctr,
                            int64_t pool_cap, uint64_t* bkeys, int32_t* list, int64_t list_cap, int mark) {

@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 \
   --timeout-method thread > gpurun_out/r04d_tests.log 2>&1 || { tail -40 gpurun_out/r04d_tests.log; exit 1; }
 tail -2 gpurun_out/r04d_tests.log
-MQR_HIP_LIB=tools/_ab/libmqr_ab.so timeout -k 10 300 python tools/ab_integrate.py --variants 0,0x100000,0x200000,0x400000,0x800000,23,24,0x80000 --rounds 7 --check \
+MQR_HIP_LIB=tools/_ab/libmqr_ab.so timeout -k 10 300 python tools/ab_integrate.py --variants 0,0x100000,0x200000,0x400000,0x800000,23,24,0x80000,0x1000000 --rounds 7 --check \
   > gpurun_out/r04d_ab.json 2> gpurun_out/r04d_ab.err || { tail -20 gpurun_out/r04d_ab.err; exit 1; }
 cat gpurun_out/r04d_ab.json
 timeout -k 10 200 python tools/ab_extract.py --modes 0 --reps 15 > gpurun_out/r04d_abx.json 2> gpurun_out/r04d_abx.err || { tail -20 gpurun_out/r04d_abx.err; exit 1; }
