@@ -648,16 +648,30 @@ __device__ inline int mc_row_tris(const uint32_t* rowN, uint32_t oc, int y, int 
 // (owned crossing edges and owned surface cubes of the row) and the sign rows rowNt[b][q] of the
 // block's [-1, R]^3 tile (cube indices).  Emission of this block and of its -x / -y / -z
 // neighbours (triangles referencing vertices this block owns) read these instead of rebuilding them.
-template <int R>
+template <class M>
+__device__ __forceinline__ void mc_emit_vertex(int i, const uint4* rows, const int32_t* nbrow,
+                                               const float2* __restrict__ pool, uint32_t pres, int xb, int yb, int zb,
+                                               float voxel_size, int32_t vb0, float* pos, float* nrm);
+// VTX (A/B, mqr_vbg_set_variant bit 28): the block's vertices are emitted here, right after the
+// look-back gives the block its offset, into buffers of the previous extraction's size (cap_v; blocks
+// past it write nothing and the host re-runs the emission pass for everything) -- the emission pass
+// then does the triangles only.
+template <int R, bool VTX = false>
 __global__ __launch_bounds__(kMcThreads) void k_mc_count(const int32_t* __restrict__ nb, const uint16_t* __restrict__ bits,
                                                          int64_t tri_blocks, int32_t* vcount, int32_t* tcount,
                                                          uint4* __restrict__ rows4, uint32_t* __restrict__ rowNt,
                                                          uint64_t* __restrict__ lb, int32_t* __restrict__ voff,
-                                                         int32_t* __restrict__ toff, int64_t* __restrict__ totals) {
+                                                         int32_t* __restrict__ toff, int64_t* __restrict__ totals,
+                                                         const float2* __restrict__ pool = nullptr,
+                                                         const uint64_t* __restrict__ bkeys = nullptr,
+                                                         float voxel_size = 0.f, float* pos = nullptr,
+                                                         float* nrm = nullptr, int64_t cap_v = 0) {
     using M = Mc<R, 1>;
     __shared__ uint32_t rowV[M::S2], rowN[M::S2], cs[M::C2];
     __shared__ int32_t nbrow[27];
     __shared__ int scratch[16];
+    __shared__ uint4 rows[VTX ? M::R2 : 1];
+    __shared__ int32_t vb0_s;
     const int64_t b = blockIdx.x;
     if (threadIdx.x < 27) nbrow[threadIdx.x] = nb[b * 27 + threadIdx.x];
     __syncthreads();
@@ -676,12 +690,28 @@ __global__ __launch_bounds__(kMcThreads) void k_mc_count(const int32_t* __restri
     int vtot, ttot;
     const int vb = block_exclusive_scan(nv, scratch, vtot);
     const int tb = block_exclusive_scan(nt, scratch + 8, ttot);
-    if (r < M::R2) rows4[b * M::R2 + r] = make_uint4((uint32_t)vb, (uint32_t)tb, e.ex | (e.ey << 16), e.ez | (e.oc << 16));
+    if (r < M::R2) {
+        const uint4 rec = make_uint4((uint32_t)vb, (uint32_t)tb, e.ex | (e.ey << 16), e.ez | (e.oc << 16));
+        rows4[b * M::R2 + r] = rec;
+        if constexpr (VTX) rows[r] = rec;
+    }
     for (int q = threadIdx.x; q < M::S2; q += blockDim.x) rowNt[b * M::S2 + q] = rowN[q];
     if (threadIdx.x == 0) {
         vcount[b] = vtot;
         tcount[b] = ttot;
         lookback_offsets(lb, b, gridDim.x, vtot, ttot, voff, toff, totals);
+        if constexpr (VTX) vb0_s = voff[b];
+    }
+    if constexpr (VTX) {
+        __syncthreads();
+        const int32_t vb0 = vb0_s;
+        if (vtot == 0 || vb0 < 0 || (int64_t)vb0 + vtot > cap_v) return;  // block-uniform
+        const int lane = threadIdx.x & 63;
+        const uint32_t pres = (uint32_t)__ballot(lane < 27 && nbrow[lane < 27 ? lane : 0] >= 0);
+        int xb, yb, zb;
+        unpack_key(bkeys[b], xb, yb, zb);
+        for (int i = threadIdx.x; i < vtot; i += blockDim.x)
+            mc_emit_vertex<M>(i, rows, nbrow, pool, pres, xb, yb, zb, voxel_size, vb0, pos, nrm);
     }
 }
 
@@ -952,7 +982,7 @@ __global__ __launch_bounds__(NT) void k_mc_emit(const int32_t* __restrict__ nb, 
                                                 float* pos, float* nrm, int32_t* tri, int64_t cap_v, int64_t cap_t,
                                                 int diag = 0) {
 #if !MQR_AB
-    diag = 0;
+    if (diag != 2) diag = 0;  // 2: triangles only (the count pass emitted the vertices, bit 28)
 #endif
     mc_emit_block<R, NT>(blockIdx.x, diag, nb, bkeys, pool, voxel_size, vcount, tcount, voff, toff, rows4,
                          rowNt, pos, nrm, tri, cap_v, cap_t);
@@ -1296,11 +1326,12 @@ static int build_nb(mqr_vbg* v, int32_t* nb) {
 static int64_t spec_cap(int64_t hint) { return hint > 0 ? hint + hint / 4 + 4096 : 0; }
 
 template <int RT, class... A>
-static void launch_mc_emit(const mqr_vbg* v, int64_t n, A... args) {
+static void launch_mc_emit(const mqr_vbg* v, int64_t n, bool tri_only, A... args) {
 #if MQR_AB  // MQR_EMIT_DIAG=1: vertices only, 2: triangles only (timing diagnostics)
-    static const int diag = getenv("MQR_EMIT_DIAG") ? atoi(getenv("MQR_EMIT_DIAG")) : 0;
+    static const int diag_env = getenv("MQR_EMIT_DIAG") ? atoi(getenv("MQR_EMIT_DIAG")) : 0;
+    const int diag = tri_only ? 2 : diag_env;
 #else
-    constexpr int diag = 0;
+    const int diag = tri_only ? 2 : 0;
 #endif
     hipLaunchKernelGGL((k_mc_emit<RT>), dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, args..., diag);
 }
@@ -1316,19 +1347,27 @@ static int mesh_passes(mqr_vbg* v, float thr, const ExScratch& e, mqr_geom* g, i
         int64_t* tot = reinterpret_cast<int64_t*>(e.tmp);
         hipLaunchKernelGGL(k_mc_bits<RT>, dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, v->pool, thr, e.bits,
                            v->bkeys, v->tab, e.nb, e.lb);
-        // counts, row records and (decoupled look-back) the block offsets and totals in one pass
-        hipLaunchKernelGGL(k_mc_count<RT>, dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, e.nb, e.bits, tri_blocks,
-                           e.c0, e.c1, rows4, rowNt, e.lb, e.o0, e.o1, tot);
-        MQR_CHECK_HIP(hipGetLastError());
-        MQR_CHECK_HIP(hipMemcpyAsync(v->h_ex, tot, 2 * sizeof(int64_t), hipMemcpyDeviceToHost, v->stream));
         // With a previous extraction's counts, emit into buffers of that size (+ margin) without
         // waiting for this one's totals; blocks past the capacity write nothing and the pass is re-run
         // into exact buffers if the totals exceed it.  Without, wait for the totals first.
         int64_t cv = spec_cap(v->ex_hint[0]), ct = spec_cap(v->ex_hint[1]);
+        const bool spec = cv > 0 && ct > 0;
+        if (spec && alloc_geom(g, cv, ct)) return 1;
+        // counts, row records and (decoupled look-back) the block offsets and totals in one pass; with
+        // bit 28 (A/B) and speculative buffers also the vertices
+        const bool fused = spec && (v->ex_mode & 1);
+        if (fused)
+            hipLaunchKernelGGL((k_mc_count<RT, true>), dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, e.nb, e.bits,
+                               tri_blocks, e.c0, e.c1, rows4, rowNt, e.lb, e.o0, e.o1, tot, (const float2*)v->pool,
+                               (const uint64_t*)v->bkeys, v->voxel_size, g->pos, g->nrm, cv);
+        else
+            hipLaunchKernelGGL((k_mc_count<RT, false>), dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, e.nb, e.bits,
+                               tri_blocks, e.c0, e.c1, rows4, rowNt, e.lb, e.o0, e.o1, tot);
+        MQR_CHECK_HIP(hipGetLastError());
+        MQR_CHECK_HIP(hipMemcpyAsync(v->h_ex, tot, 2 * sizeof(int64_t), hipMemcpyDeviceToHost, v->stream));
         bool emitted = false;
-        if (cv > 0 && ct > 0) {
-            if (alloc_geom(g, cv, ct)) return 1;
-            launch_mc_emit<RT>(v, n, (const int32_t*)e.nb, (const uint64_t*)v->bkeys, (const float2*)v->pool,
+        if (spec) {
+            launch_mc_emit<RT>(v, n, fused, (const int32_t*)e.nb, (const uint64_t*)v->bkeys, (const float2*)v->pool,
                                v->voxel_size, (const int32_t*)e.c0, (const int32_t*)e.c1, (const int32_t*)e.o0,
                                (const int32_t*)e.o1, (const uint4*)rows4, (const uint32_t*)rowNt, g->pos, g->nrm,
                                g->tri, cv, ct);
@@ -1349,7 +1388,7 @@ static int mesh_passes(mqr_vbg* v, float thr, const ExScratch& e, mqr_geom* g, i
             g->blk = nullptr;
         }
         if (alloc_geom(g, nv, nt)) return 1;
-        launch_mc_emit<RT>(v, n, (const int32_t*)e.nb, (const uint64_t*)v->bkeys, (const float2*)v->pool, v->voxel_size,
+        launch_mc_emit<RT>(v, n, false, (const int32_t*)e.nb, (const uint64_t*)v->bkeys, (const float2*)v->pool, v->voxel_size,
                            (const int32_t*)e.c0, (const int32_t*)e.c1, (const int32_t*)e.o0, (const int32_t*)e.o1,
                            (const uint4*)rows4, (const uint32_t*)rowNt, g->pos, g->nrm, g->tri, nv, nt);
     } else {

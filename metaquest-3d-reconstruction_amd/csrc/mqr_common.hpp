@@ -193,6 +193,7 @@ struct mqr_vbg {
     int touch_ppt = 2;  // stride-4 pixels per k_touch thread (strip touch, variant bits 16 / 17)
     bool touch_frame = false; // k_touch_frame: a frame per workgroup (variant bit 17, A/B)
     bool touch_two_phase = false;  // k_touch<COLLECT> + k_touch_claim (variant bit 19, A/B)
+    int ex_mode = 0;  // extraction A/B (mqr_vbg_set_variant bits 28-30): 1 vertices emitted by the count pass
     bool touch_mf = false;  // k_touch_mf: 8 frames per strip workgroup, one claim per block (variant bit 24, A/B)
     uint64_t* collect = nullptr;   // two-phase touch: [2][kMaxBatch][collect_cap] packed keys
     int64_t collect_cap = 0;       // keys per frame (4 (H/4) (W/4): every sample distinct)

@@ -1229,6 +1229,7 @@ int mqr_vbg_set_variant(mqr_vbg* v, int variant) {
     v->spec_head = (variant & 0x40000) == 0;     // bit 18: no speculative first-batch integrate (A/B)
     v->touch_two_phase = (variant & 0x80000) != 0;  // bit 19: two-phase touch (collect per strip, claim per frame)
     v->touch_mf = (variant & 0x1000000) != 0;  // bit 24: k_touch_mf (8 frames per strip workgroup)
+    v->ex_mode = (variant >> 28) & 7;  // bits 28-30: extraction A/Bs (bit 28: vertices in the count pass)
     return 0;
 }
 

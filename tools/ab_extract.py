@@ -2,7 +2,8 @@
 """Interleaved A/B of extract_triangle_mesh configurations on the bench volume (C2, one process).
 
 python tools/ab_extract.py --modes 0 --reps 15
-mode = value of mqr_vbg_set_variant bits 20-23 for an extraction configuration under test (round 4: a
+mode = value of mqr_vbg_set_variant bits 28-30 for an extraction configuration under test (1: the count
+pass emits the vertices, round 4) (round 4 also: a
 vertex and a triangle workgroup per block, 0.187 vs 0.179 ms, removed) (round 3
 measured a merged vertex / triangle item loop and 512-thread emission blocks this way: no change,
 profiles/r03_ab_integrate_windows.json; neither is in the library now, so mode 0 is the library).
@@ -44,7 +45,7 @@ def main():
     outs = {}
     for r in range(a.reps + 1):
         for m in modes:
-            _lib.call("mqr_vbg_set_variant", vbg.handle, m << 20)
+            _lib.call("mqr_vbg_set_variant", vbg.handle, m << 28)
             g = ctypes.c_void_p()
             t0 = time.perf_counter()
             _lib.call("mqr_extract_mesh", vbg.handle, float(a.threshold), ctypes.byref(g))

@@ -12,7 +12,7 @@ tail -2 gpurun_out/r04d_tests.log
 MQR_HIP_LIB=tools/_ab/libmqr_ab.so timeout -k 10 300 python tools/ab_integrate.py --variants 0,0x100000,0x200000,0x400000,0x800000,23,24,0x80000,0x1000000 --rounds 7 --check \
   > gpurun_out/r04d_ab.json 2> gpurun_out/r04d_ab.err || { tail -20 gpurun_out/r04d_ab.err; exit 1; }
 cat gpurun_out/r04d_ab.json
-timeout -k 10 200 python tools/ab_extract.py --modes 0 --reps 15 > gpurun_out/r04d_abx.json 2> gpurun_out/r04d_abx.err || { tail -20 gpurun_out/r04d_abx.err; exit 1; }
+timeout -k 10 200 python tools/ab_extract.py --modes 0,1 --reps 15 > gpurun_out/r04d_abx.json 2> gpurun_out/r04d_abx.err || { tail -20 gpurun_out/r04d_abx.err; exit 1; }
 cat gpurun_out/r04d_abx.json
 timeout -k 10 200 python tools/conf_workload.py --reps 5 --diag --ab 3 > gpurun_out/r04d_conf.json 2> gpurun_out/r04d_conf.err || { tail -20 gpurun_out/r04d_conf.err; exit 1; }
 cat gpurun_out/r04d_conf.json
