@@ -381,9 +381,13 @@ __device__ __forceinline__ Stage32 decide32_stage1_bf(__amdgpu_buffer_rsrc_t rs,
     // out of the image -> 0; else taps
     const bool go = !none_z & ok_z & sure & in_img;
     r.st = go ? 1 : (none_z | (ok_z & sure)) ? 0 : -1;
+    // P = X^2 + Y^2 + Z^2 and, in EP, a RELATIVE bound rho of its error (stage 2 uses P (1 +- rho)):
+    // with E = max(E_X, E_Y, E_Z), |P* - P| <= 2 E (|X| + |Y| + Z) + 3 E^2 <= 2 sqrt(3) E sqrt(P) + 3 E^2
+    // and sqrt(P) >= Z, so rho = 2 sqrt(3) (E / Z) + 3 (E / Z)^2 + 8u (P's own roundings), E / Z <= E irl;
+    // 3.5 and 3.01 cover the roundings of rho itself
     r.P = __builtin_fmaf(X, X, __builtin_fmaf(Y, Y, Z * Z));
-    r.EP = 2.0f * (__builtin_fabsf(X) * EX + __builtin_fabsf(Y) * EY + Z * EZ) + (EX * EX + EY * EY + EZ * EZ) +
-           8.0f * u * r.P;
+    const float er = fmaxf(fmaxf(EX, EY), EZ) * irl;
+    r.EP = __builtin_fmaf(er, __builtin_fmaf(3.01f, er, 3.5f), 8.0f * u);
     r.uu = uu;
     r.vv = vv;
     r.Eu = Eu;
@@ -442,8 +446,9 @@ __device__ __forceinline__ int decide32_stage2_bf(const Stage32& r, const Pix32&
     const float dz = __builtin_fabsf(r.Z - zf);
     const float zl = r.Z - r.EZ, zh = r.Z + r.EZ;
     const float a1 = dz + Edz, a0 = dz - Edz;
-    const bool in_band_lo = a1 * a1 * (r.P + r.EP) * (1.0f + 16.0f * u) <= px.lo2 * (zl * zl) * (1.0f - 16.0f * u);
-    const bool out_band_hi = (a0 > 0.0f) & (a0 * a0 * (r.P - r.EP) * (1.0f - 16.0f * u) > px.hi2 * (zh * zh) * (1.0f + 16.0f * u));
+    const float Phi = __builtin_fmaf(r.P, r.EP, r.P), Plo = __builtin_fmaf(-r.P, r.EP, r.P);  // (EP: relative, BF)
+    const bool in_band_lo = a1 * a1 * Phi * (1.0f + 16.0f * u) <= px.lo2 * (zl * zl) * (1.0f - 16.0f * u);
+    const bool out_band_hi = (a0 > 0.0f) & (a0 * a0 * Plo * (1.0f - 16.0f * u) > px.hi2 * (zh * zh) * (1.0f + 16.0f * u));
     const int d = in_band_lo ? 1 : out_band_hi ? 2 : -1;
     return r.st <= 0 ? r.st : !(tmax < dmb) ? 0 : d;
 }
