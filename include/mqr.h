@@ -211,17 +211,14 @@ int mqr_vbg_profile(mqr_vbg* v, int enable);
 /* Test / tuning hooks.  mqr_vbg_set_variant: low byte = integrate kernel (0 default = lean kernel
  * where its preconditions hold, 1 generic, 2 exact R-specialised, 3 lean with the plate map, 5 depth
  * from LDS tiles; all bit-identical, see launch_integrate in csrc/vbg.hip); bit 8 serialises touch and integrate, bit 9 keeps touch
- * order instead of longest-first, bit 10 uses 32-frame batches instead of 127 (the first of a call: 64;
- * bit 20: 64-frame batches, bit 21: no shorter first batch, bits 22 / 23: a first batch of 32 / 16),
- * bit 11 records
+ * order instead of longest-first, bit 10 uses 32-frame batches instead of 127 (bit 20: 64-frame
+ * batches; bits 21 / 22 / 23: a first batch of 64 / 32 / 16 frames), bit 11 records
  * system-scope ordering events, bit 12 probes one table slot per new key in the batch touch (forces
  * the full-table undo-and-retry path; test hook), bit 13 sizes the table for the worst case, bit 14 makes
  * every integrate launch wait on a touch-stream event, bit 15 runs the batch in spatial per-XCD groups
- * (k_xcd_order; A/Bs), bit 16 gives the touch one stride-4 pixel per thread instead of two, bit 17
- * touches with a frame per workgroup (k_touch_frame, A/B), bit 18 turns off the speculative first-batch
- * integrate (k_gate; A/B), bit 19 touches in two phases (strips collect their distinct keys, a workgroup
- * per frame deduplicates and claims them; A/B), bit 24 touches 8 frames per strip workgroup with one claim
- * per (block, frame group) (k_touch_mf; A/B).
+ * (k_xcd_order; A/Bs), bit 16 gives the touch one stride-4 pixel per thread instead of two, bit 18 turns
+ * off the speculative first-batch integrate (k_gate; A/B); bits 28-30 select extraction A/Bs (bit 28:
+ * the count pass emits the vertices).
  * mqr_check_division: exhaustive bit-pattern check of the division shortcuts used on device against
  * IEEE division (which=0: 1/b via rcp_rn, 1: a/b via div_rn, 2: a/b via the bare core, 3: 1/b via
  * rcp_nm, 4: 1/b via rcp_m, over float bit patterns [lo_bits, lo_bits+count) as b or a); returns

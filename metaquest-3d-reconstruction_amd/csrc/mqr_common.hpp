@@ -106,13 +106,15 @@ struct FrameParams {
 void make_frame_params(const double* K, const double* T_wc, FrameParams* fp);
 
 constexpr int kMaxBatch = 127;        // frames per device batch (one bit each in the slot mask)
-constexpr int kFirstBatch = 64;       // frames of a call's first batch (its touch runs before any integrate)
+// frames of a call's first batch (its touch runs before any integrate): a full batch -- a 64-frame
+// first batch starts the first integrate sooner but adds a launch (2.551 vs 2.499 ms per C2 step,
+// profiles/r04_ab_integrate.json)
+constexpr int kFirstBatch = kMaxBatch;
 constexpr int kFrameCounterBase = 8;  // per-frame raw touch counts live at counters[8 + f]
 constexpr int kFreshBase = kFrameCounterBase + kMaxBatch;  // per-frame new (block, frame) marks
 constexpr int kNumGroups = 8;                               // workgroup groups that share an XCD
 constexpr int kGroupBase = kFreshBase + kMaxBatch;          // k_xcd_order: group g = [off[g], off[g+1])
-constexpr int kCollectBase = kGroupBase + kNumGroups + 1;   // two-phase touch: keys collected per frame
-constexpr int kCountersTotal = kCollectBase + kMaxBatch;
+constexpr int kCountersTotal = kGroupBase + kNumGroups + 1;
 // device counter ints: 2 parity sets, the pool counter (+ spare), 2 shadow sets (k_gate: the copies a
 // speculatively launched integrate reads)
 constexpr int kCounterInts = 4 * kCountersTotal + 8;
@@ -190,13 +192,8 @@ struct mqr_vbg {
     int batch_frames = mqr::kMaxBatch;  // frames per device batch (A/B: 32, variant bit 0x400; 64, bit 20)
     int first_batch_frames = mqr::kFirstBatch;  // frames of a call's first batch
     // profiling
-    int touch_ppt = 2;  // stride-4 pixels per k_touch thread (strip touch, variant bits 16 / 17)
-    bool touch_frame = false; // k_touch_frame: a frame per workgroup (variant bit 17, A/B)
-    bool touch_two_phase = false;  // k_touch<COLLECT> + k_touch_claim (variant bit 19, A/B)
+    int touch_ppt = 2;  // stride-4 pixels per k_touch thread (variant bit 16: one)
     int ex_mode = 0;  // extraction A/B (mqr_vbg_set_variant bits 28-30): 1 vertices emitted by the count pass
-    bool touch_mf = false;  // k_touch_mf: 8 frames per strip workgroup, one claim per block (variant bit 24, A/B)
-    uint64_t* collect = nullptr;   // two-phase touch: [2][kMaxBatch][collect_cap] packed keys
-    int64_t collect_cap = 0;       // keys per frame (4 (H/4) (W/4): every sample distinct)
     int last_var = -1;        // integrate variant of the last launch, after fallbacks (mqr_vbg_last_kernel)
     bool profile = false;
     bool profile_touch = false;  // mqr_vbg_profile level 2: also time the touch launches

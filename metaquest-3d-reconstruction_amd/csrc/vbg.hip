@@ -384,11 +384,12 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
     //     6 / 7 paired-lane gathers;  8 VALU-lean projection / update, 9 + zc checked per block, 10 +
     //     one-correction s / trunc;  11 / 12 / 14 / 19 16-byte windows;  13 / 16 / 17 / 18 / 20 / 21 /
     //     22 8-byte windows at 6 waves / SIMD, with the block zc check, one-correction division, ILP 4,
-    //     in two halves (15 = the default);  23 default with the exact path in-kernel;  24 default with
-    //     wave slots wholly outside the image skipping their window load.
+    //     in two halves (15 = the round-3 default: the same kernel with the exact path in a fix-up
+    //     launch);  23 = the default.  (24, a
+    //     ballot skip of out-of-image wave slots, ran 0.70 vs 0.48 ms per launch: removed.)
     //     DESIGN.md §4.1 has the measurements behind the choice.
     int var = v->kernel_variant;
-    if (var < 0 || var > 24) var = 0;
+    if (var < 0 || var > 23) var = 0;
     if (!MQR_AB && var != 1 && var != 2 && var != 4) var = 0;
     if (var != 1 && var != 2 && !lean_ok) var = 2;
     if (var == 5 && (v->R != 16 || W % 4 != 0 || W < 4 || (reinterpret_cast<uintptr_t>(depths) & 15))) var = 0;
@@ -469,12 +470,8 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
                 hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 5, 2, 5, 1, true>), dim3(lean_grid), dim3(512), 0, s,
                                    list, lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW,
                                    H, W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
-            else if (var == 23)  // default with the exact path in-kernel (exact_block_call): no fix-up launch
-                hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 7, 2, 5, 0, false, true>), dim3(lean_grid), dim3(512), 0,
-                                   s, list, lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths,
-                                   HW, H, W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
-            else if (var == 24)  // default + wave slots wholly outside the image skip their window load
-                hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 7, 2, 8>), dim3(lean_grid), dim3(512), 0, s, list,
+            else if (var == 15)  // the round-3 default: the exact path in a fix-up launch behind the kernel
+                hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 7, 2, 5>), dim3(lean_grid), dim3(512), 0, s, list,
                                    lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H,
                                    W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
             else if (var == 10)  // variant 9 with s / sdf_trunc in one correction (verified for this sdf_trunc)
@@ -504,13 +501,14 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
                                    lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H,
                                    W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
             else  // default: 8-byte window reads, >= 7 waves / SIMD (three per-block address words
-                  // spill to scratch outside the frame loop; 1-2 % faster than 6 waves, variant 13)
-                hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 7, 2, 5>), dim3(lean_grid), dim3(512), 0, s, list,
-                                   lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H,
-                                   W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
-            // exact fix-up of the blocks the fast kernel handed back (usually none: reads a zero count);
-            // variant 23 redoes them in-kernel instead
-            if (var != 23)
+                  // spill to scratch outside the frame loop; 1-2 % faster than 6 waves, variant 13); a block
+                  // whose operands leave the proven ranges is redone in-kernel by the exact path
+                  // (exact_block_call), so no fix-up launch follows (2.527 vs 2.551 ms per step, r04)
+                hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 7, 2, 5, 0, false, true>), dim3(lean_grid), dim3(512),
+                                   0, s, list, lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size,
+                                   depths, HW, H, W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
+            // exact fix-up of the blocks the other fast kernels handed back (usually none: reads a zero count)
+            if (var != 0 && var != 23)
                 hipLaunchKernelGGL((k_integrate_t<16, 4, 512>), dim3(8), dim3(512), 0, s, bad_list, bad_mask, bad_count,
                                    v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp, depth_frame,
                                    depth_scale, depth_max, sdf_trunc, first_new);
@@ -609,35 +607,11 @@ static int touch_launch(mqr_vbg* v, int p, const float* dbase, int64_t HW, int H
         MQR_REQUIRE(e0 && e1, "profiling: event creation failed");
         MQR_CHECK_HIP(hipEventRecord(e0, v->stream));
     }
-    if (n > 0 && v->touch_two_phase) {  // A/B: strips collect their distinct keys, a workgroup per frame claims
-        const int64_t ccap = 4LL * n;
-        if (v->collect_cap < ccap) {
-            if (sync_all(v)) return 1;
-            if (v->collect) MQR_CHECK_HIP(hipFree(v->collect));
-            v->collect = nullptr;
-            v->collect_cap = 0;
-            MQR_CHECK_HIP(hipMalloc(&v->collect, sizeof(uint64_t) * 2 * kMaxBatch * ccap));
-            v->collect_cap = ccap;
-        }
-        uint64_t* col = v->collect + (int64_t)p * kMaxBatch * v->collect_cap;
-        hipLaunchKernelGGL((k_touch<2, true>), dim3((n + 511) / 512, b), dim3(256), 0, v->stream, dbase, HW, H, W,
-                           v->d_fp[p], dframe_dev(v, p), depth_scale, depth_max, sdf_trunc, block_size, t, max_probe,
-                           alloc, v->ctr(p), v->pool_ctr(), v->pool_cap, v->bkeys, v->lists[p], v->list_cap, col,
-                           v->collect_cap);
-        hipLaunchKernelGGL((k_touch_claim<1024, 4096>), dim3(1, b), dim3(1024), 0, v->stream, col, v->collect_cap, t,
-                           max_probe, alloc, v->ctr(p), v->pool_ctr(), v->pool_cap, v->bkeys, v->lists[p], v->list_cap);
-    } else if (n > 0)
-    {
-        if (v->touch_mf)  // A/B: 8 frames per strip workgroup, one claim per (block, frame group)
-            hipLaunchKernelGGL((k_touch_mf<8, 2, 2048>), dim3((n + 511) / 512, (b + 7) / 8), dim3(256), 0, v->stream,
-                               dbase, HW, H, W, v->d_fp[p], dframe_dev(v, p), b, depth_scale, depth_max, sdf_trunc,
-                               block_size, t, max_probe, alloc, v->ctr(p), v->pool_ctr(), v->pool_cap, v->bkeys,
-                               v->lists[p], v->list_cap);
-        else if (v->touch_frame)  // A/B: a frame per workgroup, claims of the frame's distinct blocks only
-            hipLaunchKernelGGL((k_touch_frame<1024, 4096>), dim3(1, b), dim3(1024), 0, v->stream, dbase, HW, H, W,
-                               v->d_fp[p], dframe_dev(v, p), depth_scale, depth_max, sdf_trunc, block_size, t, max_probe,
-                               alloc, v->ctr(p), v->pool_ctr(), v->pool_cap, v->bkeys, v->lists[p], v->list_cap);
-        else if (v->touch_ppt == 1)
+    // (measured and removed, profiles/r04_ab_integrate.json and DESIGN.md §4.1: a frame per workgroup
+    // (k_touch_frame), a two-phase collect / claim touch, 8 frames per strip workgroup with one claim per
+    // (block, frame group))
+    if (n > 0) {
+        if (v->touch_ppt == 1)
             hipLaunchKernelGGL(k_touch<1>, dim3((n + 255) / 256, b), dim3(256), 0, v->stream, dbase, HW, H, W,
                                v->d_fp[p], dframe_dev(v, p), depth_scale, depth_max, sdf_trunc, block_size, t, max_probe,
                                alloc, v->ctr(p), v->pool_ctr(), v->pool_cap, v->bkeys, v->lists[p], v->list_cap);
@@ -871,7 +845,6 @@ int mqr_vbg_destroy(mqr_vbg* v) {
     if (v->counters) (void)hipFree(v->counters);
     if (v->h_counters) (void)hipHostFree(v->h_counters);
     if (v->ex_scratch) (void)hipFree(v->ex_scratch);
-    if (v->collect) (void)hipFree(v->collect);
     if (v->h_ex) (void)hipHostFree(v->h_ex);
     if (v->stream) (void)hipStreamDestroy(v->stream);
     if (v->stream2) (void)hipStreamDestroy(v->stream2);
@@ -1215,20 +1188,17 @@ int mqr_vbg_set_variant(mqr_vbg* v, int variant) {
     v->kernel_variant = variant & 0xff;
     v->pipelined = (variant & 0x100) == 0;  // bit 8: serialise touch and integrate (A/B of the overlap)
     v->lpt_order = (variant & 0x200) == 0;  // bit 9: integrate in touch order instead of longest-first
-    // bit 10: 32-frame batches; bit 20: 64-frame batches (round 3); bit 21: no shorter first batch (A/Bs)
+    // bit 10: 32-frame batches; bit 20: 64-frame batches (round 3) (A/Bs)
     v->batch_frames = (variant & 0x400) ? 32 : (variant & 0x100000) ? 64 : kMaxBatch;
-    // bits 22 / 23: a first batch of 32 / 16 frames (A/B of the step head)
-    v->first_batch_frames = (variant & 0x200000) ? kMaxBatch : (variant & 0x400000) ? 32 : (variant & 0x800000) ? 16 : kFirstBatch;
+    // bits 21 / 22 / 23: a first batch of 64 / 32 / 16 frames (A/B of the step head)
+    v->first_batch_frames = (variant & 0x200000) ? 64 : (variant & 0x400000) ? 32 : (variant & 0x800000) ? 16 : kFirstBatch;
     v->sys_fence = (variant & 0x800) != 0;  // bit 11: system-scope ordering / timing events (A/B)
     v->probe_one = (variant & 0x1000) != 0; // bit 12: force the full-table retry path (test hook)
     v->table_worst = (variant & 0x2000) != 0; // bit 13: size the table for the worst case (round-2 A/B)
     v->touch_wait = (variant & 0x4000) != 0;  // bit 14: integrate always waits on a touch-stream event (A/B)
     v->xcd_order = (variant & 0x8000) != 0;   // bit 15: spatial per-XCD groups (k_xcd_order, A/B)
     v->touch_ppt = (variant & 0x10000) ? 1 : 2;  // bit 16: one stride-4 pixel per touch thread (A/B)
-    v->touch_frame = (variant & 0x20000) != 0;   // bit 17: k_touch_frame (a frame per workgroup; A/B, 2.3x slower)
     v->spec_head = (variant & 0x40000) == 0;     // bit 18: no speculative first-batch integrate (A/B)
-    v->touch_two_phase = (variant & 0x80000) != 0;  // bit 19: two-phase touch (collect per strip, claim per frame)
-    v->touch_mf = (variant & 0x1000000) != 0;  // bit 24: k_touch_mf (8 frames per strip workgroup)
     v->ex_mode = (variant >> 28) & 7;  // bits 28-30: extraction A/Bs (bit 28: vertices in the count pass)
     return 0;
 }

@@ -189,17 +189,13 @@ __device__ inline void wave_add(int* ctr, int v) {
 // compute_unique_block_coordinates for a batch: blockIdx.y = batch frame (bit), PPT stride-4 pixels
 // per thread (a workgroup covers 256 PPT consecutive ones), 4 samples each over
 // [max(d - trunc, 0), min(d + trunc, depth_max)] (Appendix A.2).
-// COLLECT: phase 1 of the two-phase touch -- the workgroup's distinct keys are appended to the frame's
-// collect buffer (collect + f * ccap, count at counters[kCollectBase + f]) instead of being claimed;
-// k_touch_claim deduplicates them per frame and claims each of the frame's blocks once.
-template <int PPT, bool COLLECT = false>
+template <int PPT>
 __global__ __launch_bounds__(256) void k_touch(const float* __restrict__ depths, int64_t HW, int H, int W,
                                                const FrameParams* __restrict__ fps,
                                                const int64_t* __restrict__ depth_frame, float depth_scale,
                                                float depth_max, float sdf_trunc, float block_size, Table t,
                                                int64_t max_probe, int alloc, int* counters, int* pool_ctr,
-                                               int64_t pool_cap, uint64_t* bkeys, int32_t* list, int64_t list_cap,
-                                               uint64_t* __restrict__ collect = nullptr, int64_t ccap = 0) {
+                                               int64_t pool_cap, uint64_t* bkeys, int32_t* list, int64_t list_cap) {
     // keys already inserted by this workgroup (a strip of one frame shares most of its blocks): only
     // a key's first occurrence probes the global table and sets the frame bit.  The first
     // occurrences are collected in LDS and then claimed all at once, one per thread: each claim is a
@@ -280,17 +276,6 @@ __global__ __launch_bounds__(256) void k_touch(const float* __restrict__ depths,
     wave_add(&wg_count[0], valid);
     __syncthreads();
     const int nu = wg_count[2];
-    if constexpr (COLLECT) {
-        __shared__ int cbase;
-        if (threadIdx.x == 0) {
-            cbase = nu ? atomicAdd(&counters[kCollectBase + f], nu) : 0;
-            if (wg_count[0]) atomicAdd(&counters[kFrameCounterBase + f], wg_count[0]);
-        }
-        __syncthreads();
-        uint64_t* dst = collect + (int64_t)f * ccap + cbase;
-        for (int i = threadIdx.x; i < nu; i += blockDim.x) dst[i] = seen[uniq[i]];  // (cbase + nu <= ccap: samples)
-        return;
-    }
     for (int base = 0; base < nu; base += blockDim.x) {  // uniform trip count: the wave_* calls need whole waves
         const int idx = base + (int)threadIdx.x;
         const uint64_t k = idx < nu ? seen[uniq[idx]] : kEmpty;
@@ -306,362 +291,6 @@ __global__ __launch_bounds__(256) void k_touch(const float* __restrict__ depths,
     if (threadIdx.x == 0) {
         if (wg_count[0]) atomicAdd(&counters[kFrameCounterBase + f], wg_count[0]);
         if (wg_count[1]) atomicAdd(&counters[kFreshBase + f], wg_count[1]);  // spread: one word per frame
-    }
-}
-
-// The touch samples of one stride-4 pixel (Appendix A.2, the arithmetic of k_touch): up to 4 packed
-// keys, kEmpty where the pixel is invalid; consecutive equal keys are left to the caller.
-__device__ __forceinline__ int touch_pixel_keys(float draw, int x, int y, const FrameParams& fp, float depth_scale,
-                                                float depth_max, float sdf_trunc, float block_size, int* counters,
-                                                uint64_t (&key)[4]) {
-#pragma unroll
-    for (int s = 0; s < 4; ++s) key[s] = kEmpty;
-    const float d = draw / depth_scale;
-    if (!(d > 0 && d < depth_max)) return 0;
-    const float xc = ((float)x - fp.cx) * 1.0f / fp.fx;
-    const float yc = ((float)y - fp.cy) * 1.0f / fp.fy;
-    const float zc = 1.0f;
-    const float xg = xc * fp.pose[0] + yc * fp.pose[1] + zc * fp.pose[2] + fp.pose[3];
-    const float yg = xc * fp.pose[4] + yc * fp.pose[5] + zc * fp.pose[6] + fp.pose[7];
-    const float zg = xc * fp.pose[8] + yc * fp.pose[9] + zc * fp.pose[10] + fp.pose[11];
-    const float xo = fp.pose[3], yo = fp.pose[7], zo = fp.pose[11];
-    const float xd = xg - xo, yd = yg - yo, zd = zg - zo;
-    const float t_min = fmaxf(d - sdf_trunc, 0.0f);
-    const float t_max = fminf(d + sdf_trunc, depth_max);
-    const float t_step = (t_max - t_min) / 3;
-    float tt = t_min;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-        const int xb = (int)floorf((xo + tt * xd) / block_size);
-        const int yb = (int)floorf((yo + tt * yd) / block_size);
-        const int zb = (int)floorf((zo + tt * zd) / block_size);
-        if (key_in_range(xb, yb, zb))
-            key[s] = pack_key(xb, yb, zb);
-        else
-            atomicOr(&counters[kOverflow], 8);
-        tt += t_step;
-    }
-    return 4;
-}
-
-// The table claim of a wave's keys (kEmpty = none): insert-or-find, pool buffers for new entries,
-// frame bit f, list appends.  Call with the whole wave converged.  Returns new frame bits (this lane).
-__device__ __forceinline__ int touch_claim(uint64_t k, int f, Table t, int64_t max_probe, int alloc, int* counters,
-                                           int* pool_ctr, int64_t pool_cap, uint64_t* bkeys, int32_t* list,
-                                           int64_t list_cap) {
-    int64_t slot = -1;
-    bool won = false, app = false;
-    int fresh = 0;
-    if (k != kEmpty) slot = table_claim(t, k, counters, won, max_probe);
-    if (alloc) wave_alloc(won, slot, k, t, counters, pool_ctr, pool_cap, bkeys);
-    if (slot >= 0) fresh = mark_slot_bit(t, slot, f, app);
-    wave_append(app, slot, counters, list, list_cap);
-    return fresh;
-}
-
-// compute_unique_block_coordinates for a batch with a FRAME per workgroup (blockIdx.y = batch frame;
-// gridDim.x workgroups split its stride-4 pixels, 1 by default).  Every sample's key goes into an LDS
-// set of the frame's blocks first; only the set's entries -- the frame's B_f distinct blocks, ~1 200
-// on the C2 walk -- are claimed in the global table, one device-coherent chain each (k_touch claims
-// per 512-pixel strip: ~4x as many chains for the same keys, and its 2 400 workgroups per batch hold
-// wave slots of the overlapped integrate).  A key that finds no LDS slot within kProbe probes, or
-// arrives after the set is 3/4 full, is claimed directly by its wave (the claim is idempotent: a
-// repeated key finds its slot and its frame bit already set), so a frame with more distinct blocks
-// than the set holds stays correct.
-template <int NT, int SEEN>
-__global__ __launch_bounds__(NT) void k_touch_frame(const float* __restrict__ depths, int64_t HW, int H, int W,
-                                                    const FrameParams* __restrict__ fps,
-                                                    const int64_t* __restrict__ depth_frame, float depth_scale,
-                                                    float depth_max, float sdf_trunc, float block_size, Table t,
-                                                    int64_t max_probe, int alloc, int* counters, int* pool_ctr,
-                                                    int64_t pool_cap, uint64_t* bkeys, int32_t* list,
-                                                    int64_t list_cap) {
-    static_assert(SEEN <= 65536 && (SEEN & (SEEN - 1)) == 0, "16-bit set indices, power of two");
-    constexpr int kProbe = 32, kFill = SEEN / 4 * 3;
-    __shared__ unsigned long long seen[SEEN];
-    __shared__ uint16_t uniq[SEEN];
-    __shared__ int wg_count[3];  // valid samples, new frame bits, set entries
-    for (int i = threadIdx.x; i < SEEN; i += NT) seen[i] = kEmpty;
-    if (threadIdx.x < 3) wg_count[threadIdx.x] = 0;
-    __syncthreads();
-    const int f = blockIdx.y;
-    const FrameParams fp = fps[f];
-    const int cols = W / 4, rows = H / 4, n = rows * cols;
-    const int lo = (int)((int64_t)n * blockIdx.x / gridDim.x), hi = (int)((int64_t)n * (blockIdx.x + 1) / gridDim.x);
-    const float* __restrict__ dep = depths + depth_frame[f] * HW;
-    int valid = 0, fresh = 0;
-    // uniform trip count (the spill claims need whole waves); the next pixel's depth is read ahead
-    int w = lo + (int)threadIdx.x;
-    float dnext = w < hi ? dep[(int64_t)((w / cols) * 4) * W + (w % cols) * 4] : 0.f;
-    for (int base = lo; base < hi; base += NT) {
-        const float draw = dnext;
-        const int wn = w + NT;
-        dnext = wn < hi ? dep[(int64_t)((wn / cols) * 4) * W + (wn % cols) * 4] : 0.f;
-        uint64_t key[4];
-        if (w < hi) valid += touch_pixel_keys(draw, (w % cols) * 4, (w / cols) * 4, fp, depth_scale, depth_max,
-                                              sdf_trunc, block_size, counters, key);
-        else
-#pragma unroll
-            for (int s = 0; s < 4; ++s) key[s] = kEmpty;
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            uint64_t k = key[s];
-            if (s > 0 && key[s - 1] == k) k = kEmpty;
-            bool spill = false;
-            if (k != kEmpty) {
-                uint32_t h = (uint32_t)mix64(k) & (SEEN - 1);
-                spill = true;
-                for (int p = 0; p < kProbe; ++p) {
-                    const unsigned long long cur = seen[h];
-                    if (cur == k) {
-                        spill = false;
-                        break;
-                    }
-                    if (cur == kEmpty) {
-                        if (*(volatile int*)&wg_count[2] >= kFill) break;  // set nearly full: claim directly
-                        const unsigned long long old =
-                            atomicCAS(&seen[h], (unsigned long long)kEmpty, (unsigned long long)k);
-                        if (old == kEmpty) {
-                            uniq[atomicAdd(&wg_count[2], 1)] = (uint16_t)h;
-                            spill = false;
-                            break;
-                        }
-                        if (old == k) {
-                            spill = false;
-                            break;
-                        }
-                    }
-                    h = (h + 1) & (SEEN - 1);
-                }
-            }
-            if (__ballot(spill))  // wave-uniform
-                fresh += touch_claim(spill ? k : kEmpty, f, t, max_probe, alloc, counters, pool_ctr, pool_cap, bkeys,
-                                     list, list_cap);
-        }
-        w = wn;
-    }
-    wave_add(&wg_count[0], valid);
-    __syncthreads();
-    const int nu = min(wg_count[2], SEEN);
-    for (int base = 0; base < nu; base += NT) {  // uniform trip count
-        const int idx = base + (int)threadIdx.x;
-        fresh += touch_claim(idx < nu ? seen[uniq[idx]] : kEmpty, f, t, max_probe, alloc, counters, pool_ctr, pool_cap,
-                             bkeys, list, list_cap);
-    }
-    wave_add(&wg_count[1], fresh);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        if (wg_count[0]) atomicAdd(&counters[kFrameCounterBase + f], wg_count[0]);
-        if (wg_count[1]) atomicAdd(&counters[kFreshBase + f], wg_count[1]);
-    }
-}
-
-// Phase 2 of the two-phase touch: a workgroup per frame (blockIdx.y) reads the keys its strips
-// collected (each strip's distinct keys: ~4x the frame's B_f), deduplicates them in an LDS set and
-// claims each distinct block once (keys the set cannot take are claimed directly, as in k_touch_frame).
-template <int NT, int SEEN>
-__global__ __launch_bounds__(NT) void k_touch_claim(const uint64_t* __restrict__ collect, int64_t ccap, Table t,
-                                                    int64_t max_probe, int alloc, int* counters, int* pool_ctr,
-                                                    int64_t pool_cap, uint64_t* bkeys, int32_t* list, int64_t list_cap) {
-    static_assert(SEEN <= 65536 && (SEEN & (SEEN - 1)) == 0, "16-bit set indices, power of two");
-    constexpr int kProbe = 32, kFill = SEEN / 4 * 3;
-    __shared__ unsigned long long seen[SEEN];
-    __shared__ uint16_t uniq[SEEN];
-    __shared__ int wg_count[2];  // new frame bits, set entries
-    for (int i = threadIdx.x; i < SEEN; i += NT) seen[i] = kEmpty;
-    if (threadIdx.x < 2) wg_count[threadIdx.x] = 0;
-    __syncthreads();
-    const int f = blockIdx.y;
-    const int n = counters[kCollectBase + f];
-    const uint64_t* __restrict__ src = collect + (int64_t)f * ccap;
-    int fresh = 0;
-    for (int base = 0; base < n; base += NT) {  // uniform trip count (spill claims need whole waves)
-        const int i = base + (int)threadIdx.x;
-        const uint64_t k = i < n ? src[i] : kEmpty;
-        bool spill = false;
-        if (k != kEmpty) {
-            uint32_t h = (uint32_t)mix64(k) & (SEEN - 1);
-            spill = true;
-            for (int p = 0; p < kProbe; ++p) {
-                const unsigned long long cur = seen[h];
-                if (cur == k) {
-                    spill = false;
-                    break;
-                }
-                if (cur == kEmpty) {
-                    if (*(volatile int*)&wg_count[1] >= kFill) break;  // set nearly full: claim directly
-                    const unsigned long long old = atomicCAS(&seen[h], (unsigned long long)kEmpty, (unsigned long long)k);
-                    if (old == kEmpty) {
-                        uniq[atomicAdd(&wg_count[1], 1)] = (uint16_t)h;
-                        spill = false;
-                        break;
-                    }
-                    if (old == k) {
-                        spill = false;
-                        break;
-                    }
-                }
-                h = (h + 1) & (SEEN - 1);
-            }
-        }
-        if (__ballot(spill))  // wave-uniform
-            fresh += touch_claim(spill ? k : kEmpty, f, t, max_probe, alloc, counters, pool_ctr, pool_cap, bkeys, list,
-                                 list_cap);
-    }
-    __syncthreads();
-    const int nu = min(wg_count[1], SEEN);
-    for (int base = 0; base < nu; base += NT) {  // uniform trip count
-        const int idx = base + (int)threadIdx.x;
-        fresh += touch_claim(idx < nu ? seen[uniq[idx]] : kEmpty, f, t, max_probe, alloc, counters, pool_ctr, pool_cap,
-                             bkeys, list, list_cap);
-    }
-    __shared__ int fsum;
-    if (threadIdx.x == 0) fsum = 0;
-    __syncthreads();
-    wave_add(&fsum, fresh);
-    __syncthreads();
-    if (threadIdx.x == 0 && fsum) atomicAdd(&counters[kFreshBase + f], fsum);
-}
-
-// compute_unique_block_coordinates for FPW consecutive frames per workgroup (blockIdx.y = frame group,
-// f0 = FPW blockIdx.y; a strip of 256 PPT stride-4 pixels as k_touch).  Consecutive frames of a walk
-// see mostly the same blocks in a strip, so the strip's keys of all FPW frames go into one LDS set with
-// a frame mask per entry, and each distinct block is claimed ONCE for the group: one device-coherent
-// chain (probe, mask word atomicOr of all its frame bits, list append) where k_touch runs one per
-// (block, frame).  FPW divides 64, so a group's bits lie in one mask word.  Keys the set cannot take
-// (probe limit, 3/4 full) are claimed directly for their frame, as in k_touch_frame.
-// Sets frame bits `bits` (one word: word index wi) of the slot; `first` when the slot had no frame bit.
-__device__ __forceinline__ unsigned long long mask_set_frames(bmask_t* m, int wi, unsigned long long bits, bool& first) {
-    unsigned long long* w = reinterpret_cast<unsigned long long*>(m);
-    const unsigned long long old = atomicOr(&w[wi], bits);
-    first = false;
-    if (old == 0 || (wi == 1 && old == kListedBit))  // the word held no frame bit yet
-        first = !(atomicOr(&w[1], kListedBit) & kListedBit);
-    return old;
-}
-template <int FPW, int PPT, int SEEN>
-__global__ __launch_bounds__(256) void k_touch_mf(const float* __restrict__ depths, int64_t HW, int H, int W,
-                                                  const FrameParams* __restrict__ fps,
-                                                  const int64_t* __restrict__ depth_frame, int nframes,
-                                                  float depth_scale, float depth_max, float sdf_trunc,
-                                                  float block_size, Table t, int64_t max_probe, int alloc,
-                                                  int* counters, int* pool_ctr, int64_t pool_cap, uint64_t* bkeys,
-                                                  int32_t* list, int64_t list_cap) {
-    static_assert(64 % FPW == 0 && FPW <= 32, "a group's frame bits in one mask word, a u32 LDS mask");
-    static_assert(SEEN <= 65536 && (SEEN & (SEEN - 1)) == 0, "16-bit set indices, power of two");
-    constexpr int NT = 256, kProbe = 32, kFill = SEEN / 4 * 3;
-    __shared__ unsigned long long seen[SEEN];
-    __shared__ uint32_t fmask[SEEN];
-    __shared__ uint16_t uniq[SEEN];
-    __shared__ int nset, cnt_valid[FPW], cnt_fresh[FPW];
-    for (int i = threadIdx.x; i < SEEN; i += NT) {
-        seen[i] = kEmpty;
-        fmask[i] = 0;
-    }
-    if (threadIdx.x < FPW) cnt_valid[threadIdx.x] = cnt_fresh[threadIdx.x] = 0;
-    if (threadIdx.x == 0) nset = 0;
-    __syncthreads();
-    const int f0 = blockIdx.y * FPW, nf = min(FPW, nframes - f0);
-    const int cols = W / 4, rows = H / 4, n = rows * cols;
-    int wpx[PPT];
-#pragma unroll
-    for (int jp = 0; jp < PPT; ++jp) wpx[jp] = (blockIdx.x * PPT + jp) * NT + threadIdx.x;
-    auto read_depths = [&](int j, float (&dd)[PPT]) {
-        const float* __restrict__ dep = depths + depth_frame[f0 + j] * HW;
-#pragma unroll
-        for (int jp = 0; jp < PPT; ++jp) {
-            const int w = wpx[jp];
-            dd[jp] = w < n ? dep[(int64_t)((w / cols) * 4) * W + (w % cols) * 4] : 0.f;
-        }
-    };
-    float dnext[PPT];
-    read_depths(0, dnext);
-    int fresh_direct[FPW];  // direct claims' new bits, per frame of the group (rare)
-#pragma unroll
-    for (int j = 0; j < FPW; ++j) fresh_direct[j] = 0;
-    for (int j = 0; j < nf; ++j) {  // uniform trip count (direct claims need whole waves)
-        float dd[PPT];
-#pragma unroll
-        for (int jp = 0; jp < PPT; ++jp) dd[jp] = dnext[jp];
-        if (j + 1 < nf) read_depths(j + 1, dnext);  // the next frame's reads in flight
-        const FrameParams& fp = fps[f0 + j];
-        int valid = 0;
-#pragma unroll
-        for (int jp = 0; jp < PPT; ++jp) {
-            const int w = wpx[jp];
-            uint64_t key[4];
-            if (w < n)
-                valid += touch_pixel_keys(dd[jp], (w % cols) * 4, (w / cols) * 4, fp, depth_scale, depth_max, sdf_trunc,
-                                          block_size, counters, key);
-            else
-#pragma unroll
-                for (int s = 0; s < 4; ++s) key[s] = kEmpty;
-#pragma unroll
-            for (int s = 0; s < 4; ++s) {
-                uint64_t k = key[s];
-                if (s > 0 && key[s - 1] == k) k = kEmpty;
-                bool spill = false;
-                if (k != kEmpty) {
-                    uint32_t h = (uint32_t)mix64(k) & (SEEN - 1);
-                    spill = true;
-                    for (int p = 0; p < kProbe; ++p) {
-                        const unsigned long long cur = seen[h];
-                        bool here = cur == k;
-                        if (!here && cur == kEmpty) {
-                            if (*(volatile int*)&nset >= kFill) break;  // set nearly full: claim directly
-                            const unsigned long long old =
-                                atomicCAS(&seen[h], (unsigned long long)kEmpty, (unsigned long long)k);
-                            if (old == kEmpty) uniq[atomicAdd(&nset, 1)] = (uint16_t)h;
-                            here = old == kEmpty || old == k;
-                        }
-                        if (here) {
-                            atomicOr(&fmask[h], 1u << j);
-                            spill = false;
-                            break;
-                        }
-                        h = (h + 1) & (SEEN - 1);
-                    }
-                }
-                if (__ballot(spill))  // wave-uniform
-                    fresh_direct[j] += touch_claim(spill ? k : kEmpty, f0 + j, t, max_probe, alloc, counters, pool_ctr,
-                                                   pool_cap, bkeys, list, list_cap);
-            }
-        }
-        wave_add(&cnt_valid[j], valid);
-    }
-#pragma unroll
-    for (int j = 0; j < FPW; ++j) wave_add(&cnt_fresh[j], fresh_direct[j]);
-    __syncthreads();
-    // one claim per distinct block of the group: all its frame bits in one atomicOr
-    const int nu = min(nset, SEEN), wi = f0 >> 6, sh = f0 & 63;
-    for (int base = 0; base < nu; base += NT) {  // uniform trip count
-        const int idx = base + (int)threadIdx.x;
-        const uint64_t k = idx < nu ? seen[uniq[idx]] : kEmpty;
-        const uint32_t fb = idx < nu ? fmask[uniq[idx]] : 0u;
-        int64_t slot = -1;
-        bool won = false, first = false;
-        if (k != kEmpty) slot = table_claim(t, k, counters, won, max_probe);
-        if (alloc) wave_alloc(won, slot, k, t, counters, pool_ctr, pool_cap, bkeys);
-        if (slot >= 0) {
-            const unsigned long long bits = (unsigned long long)fb << sh;
-            unsigned long long* w = reinterpret_cast<unsigned long long*>(&t.mask[slot]);
-            const unsigned long long cur = __hip_atomic_load(&w[wi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if ((cur & bits) != bits) {  // (every bit already set: another strip claimed them)
-                const unsigned long long old = mask_set_frames(&t.mask[slot], wi, bits, first);
-                unsigned long long nb = (bits & ~old) >> sh;
-                while (nb) {
-                    atomicAdd(&cnt_fresh[__builtin_ctzll(nb)], 1);
-                    nb &= nb - 1;
-                }
-            }
-        }
-        wave_append(first, slot, counters, list, list_cap);
-    }
-    __syncthreads();
-    if (threadIdx.x < nf) {
-        const int j = threadIdx.x;
-        if (cnt_valid[j]) atomicAdd(&counters[kFrameCounterBase + f0 + j], cnt_valid[j]);
-        if (cnt_fresh[j]) atomicAdd(&counters[kFreshBase + f0 + j], cnt_fresh[j]);
     }
 }
 
@@ -1098,9 +727,7 @@ __device__ __forceinline__ void lean_gather_v(float (&dv)[ZPER], bool& bad, cons
 // multiple of the window (host): then an in-image window never crosses the end of the frame, and an
 // out-of-image lane's window at 4HW is wholly past the end (reads 0).
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-// SKIP: a voxel slot k whose 64 lanes all project outside the image issues no load (wave-uniform
-// branch on the ballot; dv = 0, which the update skips).
-template <int ZPER, int ILP = 1, int WIN = 16, bool ZCHK = true, int K0 = 0, int K1 = ZPER, bool SKIP = false>
+template <int ZPER, int ILP = 1, int WIN = 16, bool ZCHK = true, int K0 = 0, int K1 = ZPER>
 __device__ __forceinline__ void lean_gather_w(float (&dv)[ZPER], bool& bad, const FrameParams& fp,
                                               __amdgpu_buffer_rsrc_t rs, const float (&xs)[ZPER],
                                               const float (&ys)[ZPER], const float (&zs)[ZPER], uint32_t W4,
@@ -1123,13 +750,6 @@ __device__ __forceinline__ void lean_gather_w(float (&dv)[ZPER], bool& bad, cons
         const float v = fy * yc * inv_z + cy;
         const bool in = (__float_as_uint(v) <= hm1_bits) && (__float_as_uint(u) <= wm1_bits);
         const uint32_t off = in ? __umul24((uint32_t)(int)v, W4) + ((uint32_t)(int)u << 2) : past_end;
-        if constexpr (SKIP) {
-            if (__builtin_amdgcn_ballot_w64(in) == 0) {
-                dv[k] = 0.0f;
-                if ((k + 1) % ILP == 0) __builtin_amdgcn_sched_barrier(0);
-                continue;
-            }
-        }
         if constexpr (WIN == 16) {
             const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(rs, off & ~15u, 0, 0);
             const uint32_t lo = (off & 8u) ? q.z : q.x, hi = (off & 8u) ? q.w : q.y;
@@ -1339,13 +959,6 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
                                                                  __float_as_uint(hm1), __float_as_uint(wm1));
                     __builtin_amdgcn_sched_barrier(0);
                     lean_update_v<ZPER, ILP, DIV1, H2, ZPER>(tw, dv, fps[f], xs, ys, zs, depth_max, sdf_trunc, y1t);
-                    continue;
-                } else if constexpr (PAIR == 8) {  // 8-byte windows, out-of-image wave slots skipped
-                    lean_gather_w<ZPER, ILP, 8, !ZBLK, 0, ZPER, true>(dv, bad, fps[f],
-                                                                      frame_rsrc(depths + depth_frame[f] * HW, bytes),
-                                                                      xs, ys, zs, W4, bytes, __float_as_uint(hm1),
-                                                                      __float_as_uint(wm1));
-                    lean_update_v<ZPER, ILP, DIV1>(tw, dv, fps[f], xs, ys, zs, depth_max, sdf_trunc, y1t);
                     continue;
                 } else if constexpr (PAIR == 4 || PAIR == 5) {
                     lean_gather_w<ZPER, ILP, PAIR == 4 ? 16 : 8, !ZBLK>(dv, bad, fps[f], frame_rsrc(depths + depth_frame[f] * HW, bytes),
