@@ -42,6 +42,11 @@ struct ConfFrame {
     float fxf, fyf, cxf, cyf;
     float ea[3], eb[3];
     int ok;  // frame_ok (a neighbour that is not ok is skipped, as the reference skips failed loads)
+    // as a reference frame (host, per call): the largest c1 / c0 of its ok neighbours in the +-r window,
+    // and (windows of <= 64 frames) the window's neighbour mask -- bit i: frame max(0, ref - r) + i is
+    // ok and not the reference -- so the kernel walks its neighbours with a scalar bit scan
+    double wc1, wc0;
+    uint64_t wmask;
 };
 
 // ---- correctly rounded float64 quotients without the v_div_scale / v_div_fixup wrapper ----------
@@ -490,12 +495,7 @@ __global__ __launch_bounds__(256) void k_confidence(const float* __restrict__ de
     if (p0 < HW && ref_point(fr[ref], u, v, depths[(int64_t)ref * HW + p], depth_max, pw)) {
         const int lo = max(0, ref - r), hi = min(N, ref + r + 1);
         // the consistency band (pixel_decide): the neighbours' largest defect terms, then per pixel
-        double c1 = 0.0, c0 = 0.0;
-        for (int t = lo; t < hi; ++t)
-            if (t != ref && fr[t].ok) {
-                c1 = fmax(c1, fr[t].c1);
-                c0 = fmax(c0, fr[t].c0);
-            }
+        const double c1 = fr[ref].wc1, c0 = fr[ref].wc0;
         const double pw_norm = sqrt(pw[0] * pw[0] + pw[1] * pw[1] + pw[2] * pw[2]) * (1.0 + 1e-12);
         const double B = c1 * pw_norm + c0;
         const double blo = sd - B, bhi = sd + B;
@@ -556,7 +556,31 @@ __global__ __launch_bounds__(256) void k_confidence(const float* __restrict__ de
             // the last neighbour it re-runs the current one, result unused): a `cur = nxt` copy of the tap
             // registers, or loads issued on only one path, made the compiler wait at the end of every
             // iteration for the loads it had just issued
-            if (t < chi) {
+            if constexpr (!WIDE) {  // the neighbours from the window mask (scalar bit scan)
+                uint64_t m = fr[ref].wmask;
+                auto pop = [&]() {
+                    const int tt = clo + __builtin_ctzll(m);
+                    m &= m - 1;
+                    return tt;
+                };
+                if (m) {
+                    int ta = pop();
+                    Stage32 a = stage1(ta), b;
+#pragma clang loop unroll(disable)
+                    while (true) {
+                        const bool more = m != 0;
+                        const int tb = more ? pop() : ta;
+                        b = stage1(tb);
+                        account(a, ta);
+                        if (!more) break;
+                        const bool more2 = m != 0;
+                        ta = more2 ? pop() : tb;
+                        a = stage1(ta);
+                        account(b, tb);
+                        if (!more2) break;
+                    }
+                }
+            } else if (t < chi) {
                 Stage32 a = stage1(t), b;
 #pragma clang loop unroll(disable)
                 while (true) {
@@ -784,6 +808,20 @@ int mqr_confidence(int device, const float* depths, int depth_loc, int N, int H,
     for (int i = 0; i < N; ++i) {
         fill_frame(K + 9 * i, T_cw + 16 * i, T_cw_inv + 16 * i, sd, H, W, (float)depth_max, fr[i]);
         fr[i].ok = frame_ok ? (frame_ok[i] ? 1 : 0) : 1;
+    }
+    for (int i = ref_begin; i < ref_end; ++i) {  // the reference frames' window terms
+        const int lo = std::max(0, i - frame_range), hi = std::min(N, i + frame_range + 1);
+        double c1 = 0.0, c0 = 0.0;
+        uint64_t m = 0;
+        for (int t = lo; t < hi; ++t)
+            if (t != i && fr[t].ok) {
+                c1 = std::fmax(c1, fr[t].c1);
+                c0 = std::fmax(c0, fr[t].c0);
+                if (t - lo < 64) m |= 1ull << (t - lo);
+            }
+        fr[i].wc1 = c1;
+        fr[i].wc0 = c0;
+        fr[i].wmask = m;
     }
     ConfFrame* dfr = cc.dfr;
     float* dd = nullptr;
