@@ -40,6 +40,7 @@ struct ConfFrame {
     // (ea = 8u sum |R row|, eb = 8u |t|, rounded up; u = 2^-24)
     float Tf[12];
     float fxf, fyf, cxf, cyf;
+    float cxu, cyu;  // 2u |cx| (1 + 4u), 2u |cy| (1 + 4u): decide32_stage1_bf's bound of 2u |uu|, 2u |vv|
     float ea[3], eb[3];
     int ok;  // frame_ok (a neighbour that is not ok is skipped, as the reference skips failed loads)
     // as a reference frame (host, per call): the largest c1 / c0 of its ok neighbours in the +-r window,
@@ -268,6 +269,8 @@ struct Pix32 {
     float p[3], m;     // pw as float32, max |pw| (rounded up)
     float lo2, hi2;    // the band bounds, rounded down / up
     float zlo, zhi;    // zmax rounded down / up
+    float lo2s, hi2s;  // lo2 (1 - 16u) / (1 + 16u) rounded down, hi2 (1 + 16u) / (1 - 16u) rounded up
+                       // (decide32_stage2_bf: the slack for its products' roundings folded in)
 };
 // Stage 1 of pixel_decide32 for one (pixel, neighbour) pair: the float32 projection, its error
 // bounds and the range / floor certainty tests, and -- for a pair that gets that far -- the two tap
@@ -348,8 +351,7 @@ typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 // decide32_stage1 (NaN operands still fail every test they meet); the frame's byte count 4HW + 4W
 // must fit 31 bits (host).
 __device__ __forceinline__ Stage32 decide32_stage1_bf(__amdgpu_buffer_rsrc_t rs, uint32_t W4, uint32_t past_end,
-                                                      int W, int H, float wm1, float hm1, const ConfFrame& ft,
-                                                      const Pix32& px) {
+                                                      int W, int H, const ConfFrame& ft, const Pix32& px) {
     constexpr float u = 0x1p-24f;
     Stage32 r;
     const float* T = ft.Tf;
@@ -359,32 +361,32 @@ __device__ __forceinline__ Stage32 decide32_stage1_bf(__amdgpu_buffer_rsrc_t rs,
     const float EX = __builtin_fmaf(ft.ea[0], px.m, ft.eb[0]);
     const float EY = __builtin_fmaf(ft.ea[1], px.m, ft.eb[1]);
     const float EZ = __builtin_fmaf(ft.ea[2], px.m, ft.eb[2]);
-    const float zl = Z - EZ, zh = Z + EZ;
     r.Z = Z;
     r.EZ = EZ;
-    const bool none_z = (Z <= -EZ) | (zl > px.zhi);
-    const bool ok_z = (zl > 0.0f) & (zh < px.zlo) & (EZ <= 0.125f * Z) & (Z >= 1e-6f);
+    // Z <= 0 or Z > zmax certain -> 0; Z in (0, zmax] certain with E_Z <= Z / 8 and Z >= 1e-6 (then
+    // Z - E_Z >= 7 Z / 8 > 0) -> go on; else -1.  (fmaxf drops a NaN E_Z, whose Z + E_Z then fails.)
+    const bool none_z = (Z <= -EZ) | (Z - EZ > px.zhi);
+    const bool ok_z = (Z >= fmaxf(8.0f * EZ, 1e-6f)) & (Z + EZ < px.zlo);
     const float inv = __builtin_amdgcn_rcpf(Z);
     const float qx = (X * ft.fxf) * inv, qy = (Y * ft.fyf) * inv;
     const float uu = qx + ft.cxf, vv = qy + ft.cyf;
-    // |uu - uu*| <= |fx| (E_X + |X| E_Z / Z) / (Z - E_Z) + rounding = (|fx| E_X + |fx X / Z| E_Z) / (Z - E_Z)
-    // + ...: the same bound as decide32_stage1's written with qx = fx X / Z (its float value within 3u,
-    // covered with the bound's own roundings by the 1 + 16u factor; every term is positive)
-    const float irl = inv * (1.0f + 2.0f * EZ * inv);  // >= 1 / (Z - E_Z) for E_Z <= Z / 8
-    const float Eu = __builtin_fmaf(__builtin_fabsf(ft.fxf), EX, __builtin_fabsf(qx) * EZ) * irl * (1.0f + 16.0f * u) +
-                     (5.0f * u * __builtin_fabsf(qx) + 2.0f * u * __builtin_fabsf(uu));
-    const float Ev = __builtin_fmaf(__builtin_fabsf(ft.fyf), EY, __builtin_fabsf(qy) * EZ) * irl * (1.0f + 16.0f * u) +
-                     (5.0f * u * __builtin_fabsf(qy) + 2.0f * u * __builtin_fabsf(vv));
+    // |uu - uu*| <= (|fx| E_X + |fx X / Z| E_Z) / (Z - E_Z) + 5u |qx| + 2u |uu|  (decide32_stage1), with
+    // qx = fx X / Z in float within 3u and 2u |uu| <= 2u |qx| + 2u |cx| (1 + 4u): every term positive, the
+    // bound's own roundings inside its 1 + 16u factor (folded into irl)
+    const float irl = inv * __builtin_fmaf(2.0f * EZ, inv, 1.0f) * (1.0f + 16.0f * u);  // >= (1 + 16u) / (Z - E_Z)
+    const float aqx = __builtin_fabsf(qx), aqy = __builtin_fabsf(qy);
+    const float Eu = __builtin_fmaf(__builtin_fmaf(__builtin_fabsf(ft.fxf), EX, aqx * EZ), irl, __builtin_fmaf(7.5f * u, aqx, ft.cxu));
+    const float Ev = __builtin_fmaf(__builtin_fmaf(__builtin_fabsf(ft.fyf), EY, aqy * EZ), irl, __builtin_fmaf(7.5f * u, aqy, ft.cyu));
     const float fu0 = __builtin_floorf(uu), fv0 = __builtin_floorf(vv);
     const float ru = uu - fu0, rv = vv - fv0;  // exact for every float
     // floor certain: uu, vv at least E away from an integer (implies |uu|, |vv| < 2^23, where ru > 0 is
     // possible, so the int conversions below cannot saturate; NaN fails it)
     const bool sure = (ru >= Eu) & (ru + Eu < 1.0f) & (rv >= Ev) & (rv + Ev < 1.0f);
     const int u0 = (int)fu0, v0 = (int)fv0;
-    const bool in_img = (u0 >= 0) & (u0 + 1 < W) & (v0 >= 0) & (v0 + 1 < H);
+    const bool in_img = ((uint32_t)u0 < (uint32_t)(W - 1)) & ((uint32_t)v0 < (uint32_t)(H - 1));
     // none_z -> 0; else !ok_z or the floors uncertain -> -1 (near the image border too: rare); else
     // out of the image -> 0; else taps
-    const bool go = !none_z & ok_z & sure & in_img;
+    const bool go = ok_z & sure & in_img;
     r.st = go ? 1 : (none_z | (ok_z & sure)) ? 0 : -1;
     // P = X^2 + Y^2 + Z^2 and, in EP, a RELATIVE bound rho of its error (stage 2 uses P (1 +- rho)):
     // with E = max(E_X, E_Y, E_Z), |P* - P| <= 2 E (|X| + |Y| + Z) + 3 E^2 <= 2 sqrt(3) E sqrt(P) + 3 E^2
@@ -393,8 +395,8 @@ __device__ __forceinline__ Stage32 decide32_stage1_bf(__amdgpu_buffer_rsrc_t rs,
     r.P = __builtin_fmaf(X, X, __builtin_fmaf(Y, Y, Z * Z));
     const float er = fmaxf(fmaxf(EX, EY), EZ) * irl;
     r.EP = __builtin_fmaf(er, __builtin_fmaf(3.01f, er, 3.5f), 8.0f * u);
-    r.uu = uu;
-    r.vv = vv;
+    r.uu = ru;  // (the fractions: stage 2 interpolates with them)
+    r.vv = rv;
     r.Eu = Eu;
     r.Ev = Ev;
     const uint32_t off = go ? __umul24((uint32_t)v0, W4) + ((uint32_t)u0 << 2) : past_end;
@@ -440,22 +442,29 @@ __device__ __forceinline__ int decide32_stage2(const Stage32& r, const Pix32& px
 __device__ __forceinline__ int decide32_stage2_bf(const Stage32& r, const Pix32& px, uint32_t dmb) {
     constexpr float u = 0x1p-24f;
     const float Ia = r.ab.x, Ib = r.ab.y, Ic = r.cd.x, Id = r.cd.y;
-    const uint32_t tmax = max(max(__float_as_uint(Ia) - 1u, __float_as_uint(Ib) - 1u),
-                              max(__float_as_uint(Ic) - 1u, __float_as_uint(Id) - 1u));
-    const float fu0 = __builtin_floorf(r.uu), fv0 = __builtin_floorf(r.vv);
-    const float fu = r.uu - fu0, fv = r.vv - fv0;
-    const float gu = (fu0 + 1.0f) - r.uu, gv = (fv0 + 1.0f) - r.vv;
-    const float zf = __builtin_fmaf(fu * fv, Id, __builtin_fmaf(gu * fv, Ic, __builtin_fmaf(fu * gv, Ib, (gu * gv) * Ia)));
-    const float Edz = r.EZ + r.Eu * (__builtin_fabsf(Ib - Ia) + __builtin_fabsf(Id - Ic)) +
-                      r.Ev * (__builtin_fabsf(Ic - Ia) + __builtin_fabsf(Id - Ib)) + 8.0f * u * zf;
+    // the tap test: every tap in (0, depth_max] -- positive floats order like their bits, +0 is the
+    // smallest pattern, negatives and NaNs lie above every positive finite pattern
+    const uint32_t bA = __float_as_uint(Ia), bB = __float_as_uint(Ib), bC = __float_as_uint(Ic), bD = __float_as_uint(Id);
+    const uint32_t tmax = max(max(bA, bB), max(bC, bD)), tmin = min(min(bA, bB), min(bC, bD));
+    const bool taps = (tmin != 0u) & (tmax <= dmb) & (dmb != 0u);
+    // zf by three lerps on the fractions (r.uu, r.vv): within 4u max(I) <= 2^-22 depth_max of the exact
+    // interpolation at the float32 uu, vv -- inside the band's 2^-18 depth_max ray-length term, like the
+    // reference's own float32 rounding of zt; the weights' dependence on uu, vv is at most the taps'
+    // range per unit, so E_dz = E_Z + 2 (E_u + E_v) (max - min) + 8u zf
+    const float fu = r.uu, fv = r.vv;
+    const float z0 = __builtin_fmaf(fu, Ib - Ia, Ia), z1 = __builtin_fmaf(fu, Id - Ic, Ic);
+    const float zf = __builtin_fmaf(fv, z1 - z0, z0);
+    const float span = __uint_as_float(tmax) - __uint_as_float(tmin);
+    const float eu2 = r.Eu + r.Ev;
+    const float Edz = __builtin_fmaf(eu2 + eu2, span, __builtin_fmaf(8.0f * u, zf, r.EZ));
     const float dz = __builtin_fabsf(r.Z - zf);
     const float zl = r.Z - r.EZ, zh = r.Z + r.EZ;
     const float a1 = dz + Edz, a0 = dz - Edz;
-    const float Phi = __builtin_fmaf(r.P, r.EP, r.P), Plo = __builtin_fmaf(-r.P, r.EP, r.P);  // (EP: relative, BF)
-    const bool in_band_lo = a1 * a1 * Phi * (1.0f + 16.0f * u) <= px.lo2 * (zl * zl) * (1.0f - 16.0f * u);
-    const bool out_band_hi = (a0 > 0.0f) & (a0 * a0 * Plo * (1.0f - 16.0f * u) > px.hi2 * (zh * zh) * (1.0f + 16.0f * u));
+    const float Phi = __builtin_fmaf(r.P, r.EP, r.P), Plo = __builtin_fmaf(-r.P, r.EP, r.P);  // (EP: relative)
+    const bool in_band_lo = (a1 * a1) * Phi <= px.lo2s * (zl * zl);
+    const bool out_band_hi = (a0 > 0.0f) & ((a0 * a0) * Plo > px.hi2s * (zh * zh));
     const int d = in_band_lo ? 1 : out_band_hi ? 2 : -1;
-    return r.st <= 0 ? r.st : !(tmax < dmb) ? 0 : d;
+    return r.st <= 0 ? r.st : !taps ? 0 : d;
 }
 
 // depth_to_pointcloud_numpy for one pixel: returns 0 when the ref pixel is not in (0, depth_max].
@@ -517,6 +526,8 @@ __global__ __launch_bounds__(256) void k_confidence(const float* __restrict__ de
         px.hi2 = round_up_f(hi2);
         px.zlo = round_down_f(zmax);
         px.zhi = round_up_f(zmax);
+        px.lo2s = lo2 >= 1e-12 ? round_down_f(lo2 * ((1.0 - 0x1p-20) / (1.0 + 0x1p-20)) * (1.0 - 0x1p-40)) : -1.0f;
+        px.hi2s = round_up_f(hi2 * ((1.0 + 0x1p-20) / (1.0 - 0x1p-20)) * (1.0 + 0x1p-40));
         const float wm1f = (float)(W - 1), hm1f = (float)(H - 1);
         // the neighbour loop, pipelined: stage 1 of the next neighbour (its projection, tests and tap
         // loads) runs before stage 2 of the current one, so one pair's tap loads are in flight while
@@ -538,7 +549,7 @@ __global__ __launch_bounds__(256) void k_confidence(const float* __restrict__ de
                 if constexpr (BF)
                     return decide32_stage1_bf(__builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(depths + (int64_t)tt * HW),
                                                                                 (short)0, (int)fbytes, 0x00020000),
-                                              W4, fbytes, W, H, wm1f, hm1f, fr[tt], px);
+                                              W4, fbytes, W, H, fr[tt], px);
                 else
                     return decide32_stage1<DIAG>(depths + (int64_t)tt * HW, W, H, wm1f, hm1f, fr[tt], px);
             };
@@ -716,6 +727,8 @@ void fill_frame(const float* K, const float* Tcw, const float* Tinv, double sd, 
     f.fxf = K[0];
     f.fyf = K[4];
     f.cxf = K[2];
+    f.cxu = (float)(std::fabs((double)K[2]) * 0x1p-23 * (1.0 + 0x1p-22));
+    f.cyu = (float)(std::fabs((double)K[5]) * 0x1p-23 * (1.0 + 0x1p-22));
     f.cyf = K[5];
     for (int k = 0; k < 12; ++k) f.Tf[k] = Tinv ? Tinv[k] : 0.0f;
     for (int r = 0; r < 3; ++r) {
@@ -756,7 +769,7 @@ struct ConfCache {
     int cap = 0;
     bool stats = false;                 // mqr_confidence_stats: count pairs per deciding stage
     bool diag = false;                  // mqr_confidence_stats enable = 2: no tap loads (timing only)
-    bool bf = false;                    // enable = 3: branch-free float32 stage 1 (A/B)
+    bool branchy = false;               // enable = 4: the branchy float32 stages (A/B; 3 = the default)
     unsigned long long* dst = nullptr;  // device counters [4]
     int64_t last[4] = {0, 0, 0, 0};     // pairs, float32 prefilter, float64 filter, float64 back-projection
 };
@@ -840,27 +853,26 @@ int mqr_confidence(int device, const float* depths, int depth_loc, int N, int H,
     }
     const dim3 grid((unsigned)((HW + 255) / 256), nref);
     const bool wide = frame_range > 31;  // a window of more than 64 frames: chunked defer masks
+    // the branch-free float32 stages (default) address the frames with 32-bit byte offsets; the branchy
+    // ones (mode 4, the first round-4 form) remain for frames past that and for A/Bs
+    const bool bf = !cc.branchy && 4 * (HW + W) < (int64_t{1} << 31);
+    auto launch = [&](auto kern, unsigned long long* st) {
+        hipLaunchKernelGGL(kern, grid, dim3(256), 0, s, dsrc, N, H, W, dfr, ref_begin, frame_range, depth_max, d2max,
+                           sd, dconf, dvalid, st);
+    };
     if (cc.stats) {
         if (!cc.dst) MQR_CHECK_HIP(hipMalloc(&cc.dst, 4 * sizeof(unsigned long long)));
         MQR_CHECK_HIP(hipMemsetAsync(cc.dst, 0, 4 * sizeof(unsigned long long), s));
-        if (wide)
-            hipLaunchKernelGGL((k_confidence<true, true>), grid, dim3(256), 0, s, dsrc, N, H, W, dfr, ref_begin,
-                               frame_range, depth_max, d2max, sd, dconf, dvalid, cc.dst);
+        if (bf)
+            wide ? launch(k_confidence<true, true, false, true>, cc.dst) : launch(k_confidence<true, false, false, true>, cc.dst);
         else
-            hipLaunchKernelGGL((k_confidence<true, false>), grid, dim3(256), 0, s, dsrc, N, H, W, dfr, ref_begin,
-                               frame_range, depth_max, d2max, sd, dconf, dvalid, cc.dst);
+            wide ? launch(k_confidence<true, true>, cc.dst) : launch(k_confidence<true, false>, cc.dst);
     } else if (cc.diag) {  // timing diagnostics only (wrong results): no tap loads
-        hipLaunchKernelGGL((k_confidence<false, false, true>), grid, dim3(256), 0, s, dsrc, N, H, W, dfr, ref_begin,
-                           frame_range, depth_max, d2max, sd, dconf, dvalid, nullptr);
-    } else if (cc.bf && !wide && 4 * (HW + W) < (int64_t{1} << 31)) {
-        hipLaunchKernelGGL((k_confidence<false, false, false, true>), grid, dim3(256), 0, s, dsrc, N, H, W, dfr,
-                           ref_begin, frame_range, depth_max, d2max, sd, dconf, dvalid, nullptr);
-    } else if (wide) {
-        hipLaunchKernelGGL((k_confidence<false, true>), grid, dim3(256), 0, s, dsrc, N, H, W, dfr, ref_begin,
-                           frame_range, depth_max, d2max, sd, dconf, dvalid, nullptr);
+        launch(k_confidence<false, false, true>, nullptr);
+    } else if (bf) {
+        wide ? launch(k_confidence<false, true, false, true>, nullptr) : launch(k_confidence<false, false, false, true>, nullptr);
     } else {
-        hipLaunchKernelGGL((k_confidence<false, false>), grid, dim3(256), 0, s, dsrc, N, H, W, dfr, ref_begin,
-                           frame_range, depth_max, d2max, sd, dconf, dvalid, nullptr);
+        wide ? launch(k_confidence<false, true>, nullptr) : launch(k_confidence<false, false>, nullptr);
     }
     MQR_CHECK_HIP(hipGetLastError());
     if (cc.stats) {
@@ -892,7 +904,7 @@ int mqr_confidence_stats(int device, int enable, int64_t* last4) {
     if (enable >= 0) {
         cc.stats = enable == 1;
         cc.diag = enable == 2;
-        cc.bf = enable == 3;
+        cc.branchy = enable == 4;
     }
     if (last4)
         for (int i = 0; i < 4; ++i) last4[i] = cc.last[i];

@@ -465,12 +465,17 @@ struct Mc {
 };
 
 // ---- decoupled look-back: the per-block offsets inside the count pass ---------------------------
-// Block b publishes its two counts (vertices / points, triangles), then walks back over the words of
-// its predecessors until one carries an inclusive prefix; the exclusive prefix is the sum of what it
-// read.  A word packs flag (2 bits: 1 counts, 2 inclusive prefix) | t (31 bits) | v (31 bits), so one
-// 64-bit atomic load sees a consistent entry; k_mc_bits zeroes block b's word before the count pass.
-// Workgroups start in blockIdx order, so every predecessor is resident or done: the walk terminates.
-// Prefixes saturate at 2^31 - 1 (the host then refuses the mesh: int32 ids).
+// Block b publishes its two counts (vertices / points, triangles), then wave 0 reads the words of its
+// 64 nearest predecessors at once (one lane each) and sums back to the nearest one that carries an
+// inclusive prefix, retrying while a predecessor in that span has not published; without an inclusive
+// prefix in the window it adds the 64 counts and moves the window back.  (A one-word-at-a-time walk by
+// one thread made the C2 count pass 99 vs 31 us: each step is a cross-XCD round trip, and ~2 000
+// resident blocks each walked back over their unfinished predecessors.)  A word packs flag (2 bits:
+// 1 counts, 2 inclusive prefix) | t (31 bits) | v (31 bits), so one 64-bit atomic load sees a
+// consistent entry; k_mc_bits zeroes block b's word before the count pass.  Workgroups of lower index
+// are dispatched first on every XCD, so the lowest unfinished block is always resident: the walk
+// terminates.  Prefixes saturate at 2^31 - 1 (the host then refuses the mesh: int32 ids).
+// Call with the whole of wave 0.
 constexpr uint64_t kLbMask = (1ull << 31) - 1;
 __device__ __forceinline__ uint64_t lb_word(uint64_t flag, int64_t v, int64_t t) {
     const uint64_t vv = (uint64_t)min<int64_t>(v, (int64_t)kLbMask), tt = (uint64_t)min<int64_t>(t, (int64_t)kLbMask);
@@ -478,25 +483,44 @@ __device__ __forceinline__ uint64_t lb_word(uint64_t flag, int64_t v, int64_t t)
 }
 __device__ inline void lookback_offsets(uint64_t* __restrict__ st, int64_t b, int64_t n, int v, int t,
                                         int32_t* __restrict__ o0, int32_t* __restrict__ o1, int64_t* __restrict__ totals) {
+    const int lane = threadIdx.x & 63;
     int64_t ev = 0, et = 0;
     if (b > 0) {
-        __hip_atomic_store(&st[b], lb_word(1, v, t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        for (int64_t j = b - 1;;) {
-            const uint64_t w = __hip_atomic_load(&st[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0) __hip_atomic_store(&st[b], lb_word(1, v, t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int64_t j0 = b - 1;;) {
+            const int64_t j = j0 - lane;  // lane 0: the nearest predecessor of the window
+            // before block 0: an inclusive prefix of 0
+            const uint64_t w = j >= 0 ? __hip_atomic_load(&st[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                      : lb_word(2, 0, 0);
             const uint64_t flag = w >> 62;
-            if (flag == 0) continue;  // not published yet
-            ev += (int64_t)(w & kLbMask);
-            et += (int64_t)((w >> 31) & kLbMask);
-            if (flag == 2) break;
-            --j;
+            const uint64_t incl = __ballot(flag == 2), unpub = __ballot(flag == 0);
+            const int stop = incl ? __builtin_ctzll(incl) : 63;  // lanes [0, stop] are summed
+            const uint64_t need = stop == 63 ? ~0ull : (2ull << stop) - 1;
+            if (unpub & need) {  // a predecessor in the span has not published: read the window again
+                __builtin_amdgcn_s_sleep(1);
+                continue;
+            }
+            const bool mine = lane <= stop;
+            int64_t sv = mine ? (int64_t)(w & kLbMask) : 0, s_t = mine ? (int64_t)((w >> 31) & kLbMask) : 0;
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) {
+                sv += __shfl_xor(sv, o, 64);
+                s_t += __shfl_xor(s_t, o, 64);
+            }
+            ev += sv;
+            et += s_t;
+            if (incl) break;
+            j0 -= 64;
         }
     }
-    __hip_atomic_store(&st[b], lb_word(2, ev + v, et + t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    o0[b] = (int32_t)min<int64_t>(ev, (int64_t)kLbMask);
-    if (o1) o1[b] = (int32_t)min<int64_t>(et, (int64_t)kLbMask);
-    if (b == n - 1) {
-        totals[0] = ev + v;
-        totals[1] = et + t;
+    if (lane == 0) {
+        __hip_atomic_store(&st[b], lb_word(2, ev + v, et + t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        o0[b] = (int32_t)min<int64_t>(ev, (int64_t)kLbMask);
+        if (o1) o1[b] = (int32_t)min<int64_t>(et, (int64_t)kLbMask);
+        if (b == n - 1) {
+            totals[0] = ev + v;
+            totals[1] = et + t;
+        }
     }
 }
 
@@ -699,9 +723,10 @@ __global__ __launch_bounds__(kMcThreads) void k_mc_count(const int32_t* __restri
     if (threadIdx.x == 0) {
         vcount[b] = vtot;
         tcount[b] = ttot;
-        lookback_offsets(lb, b, gridDim.x, vtot, ttot, voff, toff, totals);
-        if constexpr (VTX) vb0_s = voff[b];
     }
+    if (threadIdx.x < 64) lookback_offsets(lb, b, gridDim.x, vtot, ttot, voff, toff, totals);
+    if constexpr (VTX)
+        if (threadIdx.x == 0) vb0_s = voff[b];
     if constexpr (VTX) {
         __syncthreads();
         const int32_t vb0 = vb0_s;
@@ -1034,10 +1059,8 @@ __global__ __launch_bounds__(kMcThreads) void k_pt_count(const int32_t* __restri
     int tot;
     const int base = block_exclusive_scan(np, scratch, tot);
     if (r < M::R2) rows4[b * M::R2 + r] = make_uint4((uint32_t)base, m[0] | (m[1] << 16), m[2], 0u);
-    if (threadIdx.x == 0) {
-        count[b] = tot;
-        lookback_offsets(lb, b, gridDim.x, tot, 0, off, nullptr, totals);
-    }
+    if (threadIdx.x == 0) count[b] = tot;
+    if (threadIdx.x < 64) lookback_offsets(lb, b, gridDim.x, tot, 0, off, nullptr, totals);
 }
 
 // Points in (block, voxel, axis) order: position voxel_size (X + ratio e), normal interpolated

@@ -17,7 +17,7 @@ def main():
     ap.add_argument("--stats", action="store_true", help="also one counted call: pairs per deciding stage")
     ap.add_argument("--diag", action="store_true", help="also the timing-only build without tap loads")
     ap.add_argument("--ab", default="", help="comma list of mqr_confidence_stats modes to time against the "
-                    "default (3 = branch-free float32 stage 1), each with its digest")
+                    "default (4 = the branchy float32 stages), each with its digest")
     a = ap.parse_args()
     import numpy as np
     import torch
