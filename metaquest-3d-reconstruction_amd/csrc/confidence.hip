@@ -578,15 +578,19 @@ __global__ __launch_bounds__(256) void k_confidence(const float* __restrict__ de
                     int ta = pop();
                     Stage32 a = stage1(ta), b;
 #pragma clang loop unroll(disable)
+                    // (sched_barrier: the scheduler otherwise hoisted the previous pair's stage 2 above the
+                    // next pair's loads and waited for its taps at the top of each half)
                     while (true) {
                         const bool more = m != 0;
                         const int tb = more ? pop() : ta;
                         b = stage1(tb);
+                        __builtin_amdgcn_sched_barrier(0);
                         account(a, ta);
                         if (!more) break;
                         const bool more2 = m != 0;
                         ta = more2 ? pop() : tb;
                         a = stage1(ta);
+                        __builtin_amdgcn_sched_barrier(0);
                         account(b, tb);
                         if (!more2) break;
                     }
