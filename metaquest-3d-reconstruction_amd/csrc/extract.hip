@@ -464,66 +464,6 @@ struct Mc {
     __device__ static int k27(int x, int y, int z) { return (blk(x) + 1) + 3 * (blk(y) + 1) + 9 * (blk(z) + 1); }
 };
 
-// ---- decoupled look-back: the per-block offsets inside the count pass ---------------------------
-// Block b publishes its two counts (vertices / points, triangles), then wave 0 reads the words of its
-// 64 nearest predecessors at once (one lane each) and sums back to the nearest one that carries an
-// inclusive prefix, retrying while a predecessor in that span has not published; without an inclusive
-// prefix in the window it adds the 64 counts and moves the window back.  (A one-word-at-a-time walk by
-// one thread made the C2 count pass 99 vs 31 us: each step is a cross-XCD round trip, and ~2 000
-// resident blocks each walked back over their unfinished predecessors.)  A word packs flag (2 bits:
-// 1 counts, 2 inclusive prefix) | t (31 bits) | v (31 bits), so one 64-bit atomic load sees a
-// consistent entry; k_mc_bits zeroes block b's word before the count pass.  Workgroups of lower index
-// are dispatched first on every XCD, so the lowest unfinished block is always resident: the walk
-// terminates.  Prefixes saturate at 2^31 - 1 (the host then refuses the mesh: int32 ids).
-// Call with the whole of wave 0.
-constexpr uint64_t kLbMask = (1ull << 31) - 1;
-__device__ __forceinline__ uint64_t lb_word(uint64_t flag, int64_t v, int64_t t) {
-    const uint64_t vv = (uint64_t)min<int64_t>(v, (int64_t)kLbMask), tt = (uint64_t)min<int64_t>(t, (int64_t)kLbMask);
-    return flag << 62 | tt << 31 | vv;
-}
-__device__ inline void lookback_offsets(uint64_t* __restrict__ st, int64_t b, int64_t n, int v, int t,
-                                        int32_t* __restrict__ o0, int32_t* __restrict__ o1, int64_t* __restrict__ totals) {
-    const int lane = threadIdx.x & 63;
-    int64_t ev = 0, et = 0;
-    if (b > 0) {
-        if (lane == 0) __hip_atomic_store(&st[b], lb_word(1, v, t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        for (int64_t j0 = b - 1;;) {
-            const int64_t j = j0 - lane;  // lane 0: the nearest predecessor of the window
-            // before block 0: an inclusive prefix of 0
-            const uint64_t w = j >= 0 ? __hip_atomic_load(&st[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                      : lb_word(2, 0, 0);
-            const uint64_t flag = w >> 62;
-            const uint64_t incl = __ballot(flag == 2), unpub = __ballot(flag == 0);
-            const int stop = incl ? __builtin_ctzll(incl) : 63;  // lanes [0, stop] are summed
-            const uint64_t need = stop == 63 ? ~0ull : (2ull << stop) - 1;
-            if (unpub & need) {  // a predecessor in the span has not published: read the window again
-                __builtin_amdgcn_s_sleep(1);
-                continue;
-            }
-            const bool mine = lane <= stop;
-            int64_t sv = mine ? (int64_t)(w & kLbMask) : 0, s_t = mine ? (int64_t)((w >> 31) & kLbMask) : 0;
-#pragma unroll
-            for (int o = 32; o >= 1; o >>= 1) {
-                sv += __shfl_xor(sv, o, 64);
-                s_t += __shfl_xor(s_t, o, 64);
-            }
-            ev += sv;
-            et += s_t;
-            if (incl) break;
-            j0 -= 64;
-        }
-    }
-    if (lane == 0) {
-        __hip_atomic_store(&st[b], lb_word(2, ev + v, et + t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        o0[b] = (int32_t)min<int64_t>(ev, (int64_t)kLbMask);
-        if (o1) o1[b] = (int32_t)min<int64_t>(et, (int64_t)kLbMask);
-        if (b == n - 1) {
-            totals[0] = ev + v;
-            totals[1] = et + t;
-        }
-    }
-}
-
 // ---- bits pass: every voxel read once, fully coalesced -------------------------------------------
 // Per block three bit planes of R^2 rows of R bits (u16, row = z R + y, bit = x): weight > thr
 // (V), tsdf < 0 (N), tsdf > 0 (P).  NaN sets neither N nor P, like the upstream comparisons.  The
@@ -533,8 +473,7 @@ __device__ inline void lookback_offsets(uint64_t* __restrict__ st, int64_t b, in
 template <int R>
 __global__ __launch_bounds__(kMcThreads) void k_mc_bits(const float2* __restrict__ pool, float thr,
                                                         uint16_t* __restrict__ bits, const uint64_t* __restrict__ bkeys,
-                                                        const Table t, int32_t* __restrict__ nb,
-                                                        uint64_t* __restrict__ lb) {
+                                                        const Table t, int32_t* __restrict__ nb) {
     constexpr int R2 = R * R, R3 = R2 * R, NIT = (R3 + kMcThreads - 1) / kMcThreads, RPB = 64 / R;
     constexpr uint64_t RM = (1ull << R) - 1;
     const int64_t b = blockIdx.x;
@@ -546,7 +485,6 @@ __global__ __launch_bounds__(kMcThreads) void k_mc_bits(const float2* __restrict
         const int i = it * kMcThreads + tid;
         v[it] = i < R3 ? src[i] : make_float2(0.f, 0.f);
     }
-    if (tid == 0) lb[b] = 0;  // the count pass's look-back word of this block
     if (tid < 27) {
         int x, y, z;
         unpack_key(bkeys[b], x, y, z);
@@ -672,30 +610,14 @@ __device__ inline int mc_row_tris(const uint32_t* rowN, uint32_t oc, int y, int 
 // (owned crossing edges and owned surface cubes of the row) and the sign rows rowNt[b][q] of the
 // block's [-1, R]^3 tile (cube indices).  Emission of this block and of its -x / -y / -z
 // neighbours (triangles referencing vertices this block owns) read these instead of rebuilding them.
-template <class M>
-__device__ __forceinline__ void mc_emit_vertex(int i, const uint4* rows, const int32_t* nbrow,
-                                               const float2* __restrict__ pool, uint32_t pres, int xb, int yb, int zb,
-                                               float voxel_size, int32_t vb0, float* pos, float* nrm);
-// VTX (A/B, mqr_vbg_set_variant bit 28): the block's vertices are emitted here, right after the
-// look-back gives the block its offset, into buffers of the previous extraction's size (cap_v; blocks
-// past it write nothing and the host re-runs the emission pass for everything) -- the emission pass
-// then does the triangles only.
-template <int R, bool VTX = false>
+template <int R>
 __global__ __launch_bounds__(kMcThreads) void k_mc_count(const int32_t* __restrict__ nb, const uint16_t* __restrict__ bits,
                                                          int64_t tri_blocks, int32_t* vcount, int32_t* tcount,
-                                                         uint4* __restrict__ rows4, uint32_t* __restrict__ rowNt,
-                                                         uint64_t* __restrict__ lb, int32_t* __restrict__ voff,
-                                                         int32_t* __restrict__ toff, int64_t* __restrict__ totals,
-                                                         const float2* __restrict__ pool = nullptr,
-                                                         const uint64_t* __restrict__ bkeys = nullptr,
-                                                         float voxel_size = 0.f, float* pos = nullptr,
-                                                         float* nrm = nullptr, int64_t cap_v = 0) {
+                                                         uint4* __restrict__ rows4, uint32_t* __restrict__ rowNt) {
     using M = Mc<R, 1>;
     __shared__ uint32_t rowV[M::S2], rowN[M::S2], cs[M::C2];
     __shared__ int32_t nbrow[27];
     __shared__ int scratch[16];
-    __shared__ uint4 rows[VTX ? M::R2 : 1];
-    __shared__ int32_t vb0_s;
     const int64_t b = blockIdx.x;
     if (threadIdx.x < 27) nbrow[threadIdx.x] = nb[b * 27 + threadIdx.x];
     __syncthreads();
@@ -714,29 +636,11 @@ __global__ __launch_bounds__(kMcThreads) void k_mc_count(const int32_t* __restri
     int vtot, ttot;
     const int vb = block_exclusive_scan(nv, scratch, vtot);
     const int tb = block_exclusive_scan(nt, scratch + 8, ttot);
-    if (r < M::R2) {
-        const uint4 rec = make_uint4((uint32_t)vb, (uint32_t)tb, e.ex | (e.ey << 16), e.ez | (e.oc << 16));
-        rows4[b * M::R2 + r] = rec;
-        if constexpr (VTX) rows[r] = rec;
-    }
+    if (r < M::R2) rows4[b * M::R2 + r] = make_uint4((uint32_t)vb, (uint32_t)tb, e.ex | (e.ey << 16), e.ez | (e.oc << 16));
     for (int q = threadIdx.x; q < M::S2; q += blockDim.x) rowNt[b * M::S2 + q] = rowN[q];
     if (threadIdx.x == 0) {
         vcount[b] = vtot;
         tcount[b] = ttot;
-    }
-    if (threadIdx.x < 64) lookback_offsets(lb, b, gridDim.x, vtot, ttot, voff, toff, totals);
-    if constexpr (VTX)
-        if (threadIdx.x == 0) vb0_s = voff[b];
-    if constexpr (VTX) {
-        __syncthreads();
-        const int32_t vb0 = vb0_s;
-        if (vtot == 0 || vb0 < 0 || (int64_t)vb0 + vtot > cap_v) return;  // block-uniform
-        const int lane = threadIdx.x & 63;
-        const uint32_t pres = (uint32_t)__ballot(lane < 27 && nbrow[lane < 27 ? lane : 0] >= 0);
-        int xb, yb, zb;
-        unpack_key(bkeys[b], xb, yb, zb);
-        for (int i = threadIdx.x; i < vtot; i += blockDim.x)
-            mc_emit_vertex<M>(i, rows, nbrow, pool, pres, xb, yb, zb, voxel_size, vb0, pos, nrm);
     }
 }
 
@@ -1007,10 +911,99 @@ __global__ __launch_bounds__(NT) void k_mc_emit(const int32_t* __restrict__ nb, 
                                                 float* pos, float* nrm, int32_t* tri, int64_t cap_v, int64_t cap_t,
                                                 int diag = 0) {
 #if !MQR_AB
-    if (diag != 2) diag = 0;  // 2: triangles only (the count pass emitted the vertices, bit 28)
+    diag = 0;
 #endif
     mc_emit_block<R, NT>(blockIdx.x, diag, nb, bkeys, pool, voxel_size, vcount, tcount, voff, toff, rows4,
                          rowNt, pos, nrm, tri, cap_v, cap_t);
+}
+
+
+// (A decoupled look-back inside the count pass, one word per step or 64 per step, made the C2 count
+// pass 99 / 77 us against 31 + 5 here: each step is a cross-XCD round trip.)
+// Exclusive scans of the two per-block count arrays (vertices, triangles) in one workgroup of
+// kScanThreads; totals[0..1] = the sums.  (Two hipcub scans cost ~20 us of launches at these sizes.)
+// Tiles of kScanTile counts: coalesced loads, all of a thread's in flight, staged in LDS; each
+// thread scans kScanPer consecutive counts, wave and workgroup scans of the thread sums; results
+// back through LDS to coalesced stores; a running carry between tiles.
+constexpr int kScanThreads = 1024, kScanPer = 8, kScanTile = kScanThreads * kScanPer;
+__global__ __launch_bounds__(kScanThreads) void k_scan_counts(const int32_t* __restrict__ c0,
+                                                              const int32_t* __restrict__ c1, int64_t n,
+                                                              int32_t* __restrict__ o0, int32_t* __restrict__ o1,
+                                                              int64_t* __restrict__ totals) {
+    __shared__ int32_t t0[kScanTile], t1[kScanTile];
+    __shared__ int64_t ws0[kScanThreads / 64], ws1[kScanThreads / 64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const bool two = c1 != nullptr;
+    int64_t carry0 = 0, carry1 = 0;
+    for (int64_t base = 0; base < n; base += kScanTile) {
+        int32_t v0[kScanPer], v1[kScanPer];
+#pragma unroll
+        for (int k = 0; k < kScanPer; ++k) {
+            const int64_t i = base + k * kScanThreads + tid;
+            v0[k] = i < n ? c0[i] : 0;
+            v1[k] = two && i < n ? c1[i] : 0;
+        }
+#pragma unroll
+        for (int k = 0; k < kScanPer; ++k) {
+            t0[k * kScanThreads + tid] = v0[k];
+            t1[k * kScanThreads + tid] = v1[k];
+        }
+        __syncthreads();
+        int64_t s0 = 0, s1 = 0;
+#pragma unroll
+        for (int k = 0; k < kScanPer; ++k) {
+            s0 += t0[tid * kScanPer + k];
+            s1 += t1[tid * kScanPer + k];
+        }
+        int64_t i0 = s0, i1 = s1;  // inclusive wave scans of the thread sums
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int64_t a = __shfl_up(i0, d, 64), b = __shfl_up(i1, d, 64);
+            if (lane >= d) {
+                i0 += a;
+                i1 += b;
+            }
+        }
+        if (lane == 63) {
+            ws0[wave] = i0;
+            ws1[wave] = i1;
+        }
+        __syncthreads();
+        int64_t b0 = carry0, b1 = carry1, tot0 = 0, tot1 = 0;
+        for (int w = 0; w < kScanThreads / 64; ++w) {
+            if (w < wave) {
+                b0 += ws0[w];
+                b1 += ws1[w];
+            }
+            tot0 += ws0[w];
+            tot1 += ws1[w];
+        }
+        int64_t r0 = b0 + i0 - s0, r1 = b1 + i1 - s1;  // exclusive prefix of this thread's counts
+#pragma unroll
+        for (int k = 0; k < kScanPer; ++k) {
+            const int32_t a = t0[tid * kScanPer + k], b = t1[tid * kScanPer + k];
+            t0[tid * kScanPer + k] = (int32_t)r0;
+            t1[tid * kScanPer + k] = (int32_t)r1;
+            r0 += a;
+            r1 += b;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kScanPer; ++k) {
+            const int64_t i = base + k * kScanThreads + tid;
+            if (i < n) {
+                o0[i] = t0[k * kScanThreads + tid];
+                if (two) o1[i] = t1[k * kScanThreads + tid];
+            }
+        }
+        carry0 += tot0;
+        carry1 += tot1;
+        __syncthreads();  // the tile buffers and wave sums are reused
+    }
+    if (tid == 0) {
+        totals[0] = carry0;
+        totals[1] = carry1;
+    }
 }
 
 // ---------------------------------------------------------------- point cloud (R = 8 / 16)
@@ -1021,8 +1014,7 @@ __global__ __launch_bounds__(NT) void k_mc_emit(const int32_t* __restrict__ nb, 
 template <int R>
 __global__ __launch_bounds__(kMcThreads) void k_pt_count(const int32_t* __restrict__ nb, const uint16_t* __restrict__ bits,
                                                          const float2* __restrict__ pool, int32_t* __restrict__ count,
-                                                         uint4* __restrict__ rows4, uint64_t* __restrict__ lb,
-                                                         int32_t* __restrict__ off, int64_t* __restrict__ totals) {
+                                                         uint4* __restrict__ rows4) {
     using M = Mc<R, 1>;
     __shared__ uint32_t rowV[M::S2], rowN[M::S2], rowP[M::S2];
     __shared__ int32_t nbrow[27];
@@ -1060,7 +1052,6 @@ __global__ __launch_bounds__(kMcThreads) void k_pt_count(const int32_t* __restri
     const int base = block_exclusive_scan(np, scratch, tot);
     if (r < M::R2) rows4[b * M::R2 + r] = make_uint4((uint32_t)base, m[0] | (m[1] << 16), m[2], 0u);
     if (threadIdx.x == 0) count[b] = tot;
-    if (threadIdx.x < 64) lookback_offsets(lb, b, gridDim.x, tot, 0, off, nullptr, totals);
 }
 
 // Points in (block, voxel, axis) order: position voxel_size (X + ratio e), normal interpolated
@@ -1213,7 +1204,6 @@ static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 // Carve the grow-only per-volume scratch: nb[27n], 4 count/offset arrays of n, faces[3R^2 n], scan temp.
 struct ExScratch {
     int32_t *nb, *c0, *c1, *o0, *o1;
-    uint64_t* lb;    // look-back words of the count pass (one per block)
     uint32_t* faces;
     uint16_t* bits;  // k_mc_bits planes, 3 R^2 u16 per block (R = 8 / 16)
     void* tmp;
@@ -1233,8 +1223,7 @@ static int ex_scratch(mqr_vbg* v, int64_t n, bool mesh, ExScratch& e) {
                              : 0;
     const size_t sz_b = align256(sizeof(uint16_t) * 3 * v->R * v->R * n);
     tmp_bytes = std::max<size_t>(tmp_bytes, 2 * sizeof(int64_t));
-    const size_t sz_lb = align256(sizeof(uint64_t) * n);
-    const size_t need = sz_nb + 4 * sz_c + sz_f + sz_b + sz_lb + align256(tmp_bytes);
+    const size_t need = sz_nb + 4 * sz_c + sz_f + sz_b + align256(tmp_bytes);
     if (v->ex_scratch_bytes < need) {
         MQR_CHECK_HIP(hipStreamSynchronize(v->stream));
         if (v->ex_scratch) MQR_CHECK_HIP(hipFree(v->ex_scratch));
@@ -1257,8 +1246,6 @@ static int ex_scratch(mqr_vbg* v, int64_t n, bool mesh, ExScratch& e) {
     p += sz_f;
     e.bits = reinterpret_cast<uint16_t*>(p);
     p += sz_b;
-    e.lb = reinterpret_cast<uint64_t*>(p);
-    p += sz_lb;
     e.tmp = p;
     e.tmp_bytes = tmp_bytes;
     return 0;
@@ -1349,12 +1336,11 @@ static int build_nb(mqr_vbg* v, int32_t* nb) {
 static int64_t spec_cap(int64_t hint) { return hint > 0 ? hint + hint / 4 + 4096 : 0; }
 
 template <int RT, class... A>
-static void launch_mc_emit(const mqr_vbg* v, int64_t n, bool tri_only, A... args) {
+static void launch_mc_emit(const mqr_vbg* v, int64_t n, A... args) {
 #if MQR_AB  // MQR_EMIT_DIAG=1: vertices only, 2: triangles only (timing diagnostics)
-    static const int diag_env = getenv("MQR_EMIT_DIAG") ? atoi(getenv("MQR_EMIT_DIAG")) : 0;
-    const int diag = tri_only ? 2 : diag_env;
+    static const int diag = getenv("MQR_EMIT_DIAG") ? atoi(getenv("MQR_EMIT_DIAG")) : 0;
 #else
-    const int diag = tri_only ? 2 : 0;
+    constexpr int diag = 0;
 #endif
     hipLaunchKernelGGL((k_mc_emit<RT>), dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, args..., diag);
 }
@@ -1369,28 +1355,21 @@ static int mesh_passes(mqr_vbg* v, float thr, const ExScratch& e, mqr_geom* g, i
     if constexpr (RT > 0) {
         int64_t* tot = reinterpret_cast<int64_t*>(e.tmp);
         hipLaunchKernelGGL(k_mc_bits<RT>, dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, v->pool, thr, e.bits,
-                           v->bkeys, v->tab, e.nb, e.lb);
+                           v->bkeys, v->tab, e.nb);
+        hipLaunchKernelGGL(k_mc_count<RT>, dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, e.nb, e.bits, tri_blocks,
+                           e.c0, e.c1, rows4, rowNt);
+        hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(kScanThreads), 0, v->stream, e.c0, e.c1, n, e.o0, e.o1, tot);
         // With a previous extraction's counts, emit into buffers of that size (+ margin) without
         // waiting for this one's totals; blocks past the capacity write nothing and the pass is re-run
         // into exact buffers if the totals exceed it.  Without, wait for the totals first.
         int64_t cv = spec_cap(v->ex_hint[0]), ct = spec_cap(v->ex_hint[1]);
         const bool spec = cv > 0 && ct > 0;
         if (spec && alloc_geom(g, cv, ct)) return 1;
-        // counts, row records and (decoupled look-back) the block offsets and totals in one pass; with
-        // bit 28 (A/B) and speculative buffers also the vertices
-        const bool fused = spec && (v->ex_mode & 1);
-        if (fused)
-            hipLaunchKernelGGL((k_mc_count<RT, true>), dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, e.nb, e.bits,
-                               tri_blocks, e.c0, e.c1, rows4, rowNt, e.lb, e.o0, e.o1, tot, (const float2*)v->pool,
-                               (const uint64_t*)v->bkeys, v->voxel_size, g->pos, g->nrm, cv);
-        else
-            hipLaunchKernelGGL((k_mc_count<RT, false>), dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, e.nb, e.bits,
-                               tri_blocks, e.c0, e.c1, rows4, rowNt, e.lb, e.o0, e.o1, tot);
         MQR_CHECK_HIP(hipGetLastError());
         MQR_CHECK_HIP(hipMemcpyAsync(v->h_ex, tot, 2 * sizeof(int64_t), hipMemcpyDeviceToHost, v->stream));
         bool emitted = false;
         if (spec) {
-            launch_mc_emit<RT>(v, n, fused, (const int32_t*)e.nb, (const uint64_t*)v->bkeys, (const float2*)v->pool,
+            launch_mc_emit<RT>(v, n, (const int32_t*)e.nb, (const uint64_t*)v->bkeys, (const float2*)v->pool,
                                v->voxel_size, (const int32_t*)e.c0, (const int32_t*)e.c1, (const int32_t*)e.o0,
                                (const int32_t*)e.o1, (const uint4*)rows4, (const uint32_t*)rowNt, g->pos, g->nrm,
                                g->tri, cv, ct);
@@ -1411,7 +1390,7 @@ static int mesh_passes(mqr_vbg* v, float thr, const ExScratch& e, mqr_geom* g, i
             g->blk = nullptr;
         }
         if (alloc_geom(g, nv, nt)) return 1;
-        launch_mc_emit<RT>(v, n, false, (const int32_t*)e.nb, (const uint64_t*)v->bkeys, (const float2*)v->pool, v->voxel_size,
+        launch_mc_emit<RT>(v, n, (const int32_t*)e.nb, (const uint64_t*)v->bkeys, (const float2*)v->pool, v->voxel_size,
                            (const int32_t*)e.c0, (const int32_t*)e.c1, (const int32_t*)e.o0, (const int32_t*)e.o1,
                            (const uint4*)rows4, (const uint32_t*)rowNt, g->pos, g->nrm, g->tri, nv, nt);
     } else {
@@ -1440,9 +1419,11 @@ static int point_passes(mqr_vbg* v, float thr, const ExScratch& e, mqr_geom* g) 
         uint4* rows4 = reinterpret_cast<uint4*>(e.faces);
         int64_t* tot = reinterpret_cast<int64_t*>(e.tmp);
         hipLaunchKernelGGL(k_mc_bits<RT>, dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, v->pool, thr, e.bits,
-                           v->bkeys, v->tab, e.nb, e.lb);
+                           v->bkeys, v->tab, e.nb);
         hipLaunchKernelGGL(k_pt_count<RT>, dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, e.nb, e.bits, v->pool,
-                           e.c0, rows4, e.lb, e.o0, tot);
+                           e.c0, rows4);
+        hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(kScanThreads), 0, v->stream, e.c0, (const int32_t*)nullptr, n,
+                           e.o0, (int32_t*)nullptr, tot);
         MQR_CHECK_HIP(hipGetLastError());
         MQR_CHECK_HIP(hipMemcpyAsync(v->h_ex, tot, sizeof(int64_t), hipMemcpyDeviceToHost, v->stream));
         const int64_t cp = spec_cap(v->ex_hint[2]);  // speculative capacity, as in mesh_passes

@@ -123,16 +123,12 @@ def test_points_match_oracle(mqr_mod, room_seq, thr):
     compare_points_normals(pcd.points, pcd.normals, op, on, 1e-6)
 
 
-@pytest.mark.parametrize("ex_mode", [0, 1])
-def test_repeated_extraction_speculative_capacity(mqr_mod, room_seq, ex_mode):
+def test_repeated_extraction_speculative_capacity(mqr_mod, room_seq):
     """The second and later extractions of a volume emit into buffers sized from the previous
     extraction's counts without waiting for the totals: a mesh / point cloud that grew past that
     capacity (2 frames, then 40) is re-emitted into exact buffers, one that fits (same volume again,
-    a higher threshold) is kept.  Every result equals the oracle.  ex_mode 1 (mqr_vbg_set_variant bit
-    28): the count pass emits the vertices into the speculative buffers."""
-    from mqr import _lib
+    a higher threshold) is kept.  Every result equals the oracle."""
     vbg = mqr_mod.VoxelBlockGrid(voxel_size=0.01, block_resolution=16, block_count=512)
-    _lib.call("mqr_vbg_set_variant", vbg.handle, ex_mode << 28)
     args = dict(depth_scale=1.0, depth_max=4.0, trunc_voxel_multiplier=10.0)
     vbg.integrate_frames(room_seq["depth"][:1], room_seq["K"][:1], room_seq["T_wc"][:1], **args)
     small = vbg.extract_triangle_mesh(weight_threshold=0.0)

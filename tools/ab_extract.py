@@ -2,8 +2,8 @@
 """Interleaved A/B of extract_triangle_mesh configurations on the bench volume (C2, one process).
 
 python tools/ab_extract.py --modes 0 --reps 15
-mode = value of mqr_vbg_set_variant bits 28-30 for an extraction configuration under test (1: the count
-pass emits the vertices, round 4) (round 4 also: a
+mode = value of mqr_vbg_set_variant bits 28-30 for an extraction configuration under test (round 4
+measured the count pass emitting the vertices, 0.264 vs 0.237 ms, and a
 vertex and a triangle workgroup per block, 0.187 vs 0.179 ms, removed) (round 3
 measured a merged vertex / triangle item loop and 512-thread emission blocks this way: no change,
 profiles/r03_ab_integrate_windows.json; neither is in the library now, so mode 0 is the library).
