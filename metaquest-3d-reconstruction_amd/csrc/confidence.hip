@@ -42,6 +42,7 @@ struct ConfFrame {
     float fxf, fyf, cxf, cyf;
     float cxu, cyu;  // 2u |cx| (1 + 4u), 2u |cy| (1 + 4u): decide32_stage1_bf's bound of 2u |uu|, 2u |vv|
     float ea[3], eb[3];
+    float eam, ebm;  // max(ea), max(eb): decide32_stage1_bf's one bound for all three coordinates
     int ok;  // frame_ok (a neighbour that is not ok is skipped, as the reference skips failed loads)
     // as a reference frame (host, per call): the largest c1 / c0 of its ok neighbours in the +-r window,
     // and (windows of <= 64 frames) the window's neighbour mask -- bit i: frame max(0, ref - r) + i is
@@ -358,9 +359,8 @@ __device__ __forceinline__ Stage32 decide32_stage1_bf(__amdgpu_buffer_rsrc_t rs,
     const float X = __builtin_fmaf(T[0], px.p[0], __builtin_fmaf(T[1], px.p[1], __builtin_fmaf(T[2], px.p[2], T[3])));
     const float Y = __builtin_fmaf(T[4], px.p[0], __builtin_fmaf(T[5], px.p[1], __builtin_fmaf(T[6], px.p[2], T[7])));
     const float Z = __builtin_fmaf(T[8], px.p[0], __builtin_fmaf(T[9], px.p[1], __builtin_fmaf(T[10], px.p[2], T[11])));
-    const float EX = __builtin_fmaf(ft.ea[0], px.m, ft.eb[0]);
-    const float EY = __builtin_fmaf(ft.ea[1], px.m, ft.eb[1]);
-    const float EZ = __builtin_fmaf(ft.ea[2], px.m, ft.eb[2]);
+    // one bound E >= E_X, E_Y, E_Z (the frame's largest row terms)
+    const float EZ = __builtin_fmaf(ft.eam, px.m, ft.ebm);
     r.Z = Z;
     r.EZ = EZ;
     // Z <= 0 or Z > zmax certain -> 0; Z in (0, zmax] certain with E_Z <= Z / 8 and Z >= 1e-6 (then
@@ -374,9 +374,10 @@ __device__ __forceinline__ Stage32 decide32_stage1_bf(__amdgpu_buffer_rsrc_t rs,
     // qx = fx X / Z in float within 3u and 2u |uu| <= 2u |qx| + 2u |cx| (1 + 4u): every term positive, the
     // bound's own roundings inside its 1 + 16u factor (folded into irl)
     const float irl = inv * __builtin_fmaf(2.0f * EZ, inv, 1.0f) * (1.0f + 16.0f * u);  // >= (1 + 16u) / (Z - E_Z)
+    const float ei = EZ * irl;  // E (1 + 16u) / (Z - E): with E_X = E_Y = E_Z = E, (|fx| E + |qx| E) irl = (|fx| + |qx|) ei
     const float aqx = __builtin_fabsf(qx), aqy = __builtin_fabsf(qy);
-    const float Eu = __builtin_fmaf(__builtin_fmaf(__builtin_fabsf(ft.fxf), EX, aqx * EZ), irl, __builtin_fmaf(7.5f * u, aqx, ft.cxu));
-    const float Ev = __builtin_fmaf(__builtin_fmaf(__builtin_fabsf(ft.fyf), EY, aqy * EZ), irl, __builtin_fmaf(7.5f * u, aqy, ft.cyu));
+    const float Eu = __builtin_fmaf(__builtin_fabsf(ft.fxf) + aqx, ei, __builtin_fmaf(7.5f * u, aqx, ft.cxu));
+    const float Ev = __builtin_fmaf(__builtin_fabsf(ft.fyf) + aqy, ei, __builtin_fmaf(7.5f * u, aqy, ft.cyu));
     const float fu0 = __builtin_floorf(uu), fv0 = __builtin_floorf(vv);
     const float ru = uu - fu0, rv = vv - fv0;  // exact for every float
     // floor certain: uu, vv at least E away from an integer (implies |uu|, |vv| < 2^23, where ru > 0 is
@@ -389,12 +390,11 @@ __device__ __forceinline__ Stage32 decide32_stage1_bf(__amdgpu_buffer_rsrc_t rs,
     const bool go = ok_z & sure & in_img;
     r.st = go ? 1 : (none_z | (ok_z & sure)) ? 0 : -1;
     // P = X^2 + Y^2 + Z^2 and, in EP, a RELATIVE bound rho of its error (stage 2 uses P (1 +- rho)):
-    // with E = max(E_X, E_Y, E_Z), |P* - P| <= 2 E (|X| + |Y| + Z) + 3 E^2 <= 2 sqrt(3) E sqrt(P) + 3 E^2
-    // and sqrt(P) >= Z, so rho = 2 sqrt(3) (E / Z) + 3 (E / Z)^2 + 8u (P's own roundings), E / Z <= E irl;
-    // 3.5 and 3.01 cover the roundings of rho itself
+    // |P* - P| <= 2 E (|X| + |Y| + Z) + 3 E^2 <= 2 sqrt(3) E sqrt(P) + 3 E^2 and sqrt(P) >= Z, so
+    // rho = 2 sqrt(3) (E / Z) + 3 (E / Z)^2 + 8u (P's own roundings), E / Z <= ei; 3.5 and 3.01 cover the
+    // roundings of rho itself
     r.P = __builtin_fmaf(X, X, __builtin_fmaf(Y, Y, Z * Z));
-    const float er = fmaxf(fmaxf(EX, EY), EZ) * irl;
-    r.EP = __builtin_fmaf(er, __builtin_fmaf(3.01f, er, 3.5f), 8.0f * u);
+    r.EP = __builtin_fmaf(ei, __builtin_fmaf(3.01f, ei, 3.5f), 8.0f * u);
     r.uu = ru;  // (the fractions: stage 2 interpolates with them)
     r.vv = rv;
     r.Eu = Eu;
@@ -742,6 +742,8 @@ void fill_frame(const float* K, const float* Tcw, const float* Tinv, double sd, 
         f.ea[r] = std::nextafter((float)a, INFINITY);
         f.eb[r] = std::nextafter((float)b, INFINITY);
     }
+    f.eam = std::fmax(std::fmax(f.ea[0], f.ea[1]), f.ea[2]);  // (fmax: a NaN entry is dropped, but then
+    f.ebm = std::fmax(std::fmax(f.eb[0], f.eb[1]), f.eb[2]);  //  Tf holds a NaN and every pair fails)
 }
 
 // Largest double d2 >= 0 with (float)sqrt(d2) <= thr (binary search over the ordered bit patterns
