@@ -373,8 +373,10 @@ __device__ __forceinline__ Stage32 decide32_stage1_bf(__amdgpu_buffer_rsrc_t rs,
     // |uu - uu*| <= (|fx| E_X + |fx X / Z| E_Z) / (Z - E_Z) + 5u |qx| + 2u |uu|  (decide32_stage1), with
     // qx = fx X / Z in float within 3u and 2u |uu| <= 2u |qx| + 2u |cx| (1 + 4u): every term positive, the
     // bound's own roundings inside its 1 + 16u factor (folded into irl)
-    const float irl = inv * __builtin_fmaf(2.0f * EZ, inv, 1.0f) * (1.0f + 16.0f * u);  // >= (1 + 16u) / (Z - E_Z)
-    const float ei = EZ * irl;  // E (1 + 16u) / (Z - E): with E_X = E_Y = E_Z = E, (|fx| E + |qx| E) irl = (|fx| + |qx|) ei
+    const float irl = inv * __builtin_fmaf(2.0f * EZ, inv, 1.0f);  // >= 1 / (Z - E_Z)
+    // E / (Z - E), E carrying the 1 + 16u slack (host): with E_X = E_Y = E_Z = E, (|fx| E + |qx| E) / (Z - E)
+    // (1 + 16u) <= (|fx| + |qx|) ei
+    const float ei = EZ * irl;
     const float aqx = __builtin_fabsf(qx), aqy = __builtin_fabsf(qy);
     const float Eu = __builtin_fmaf(__builtin_fabsf(ft.fxf) + aqx, ei, __builtin_fmaf(7.5f * u, aqx, ft.cxu));
     const float Ev = __builtin_fmaf(__builtin_fabsf(ft.fyf) + aqy, ei, __builtin_fmaf(7.5f * u, aqy, ft.cyu));
@@ -559,7 +561,8 @@ __global__ __launch_bounds__(256) void k_confidence(const float* __restrict__ de
                     ++n_pairs;
                     n_f32 += dcs >= 0;
                 }
-                if (dcs < 0) defer |= 1ull << (tt - clo);
+                if (__ballot(dcs < 0))  // (wave-uniform, rare: 0.4 % of pairs)
+                    if (dcs < 0) defer |= 1ull << (tt - clo);
                 nv += dcs > 0;
                 nc += dcs == 1;
             };
@@ -742,8 +745,11 @@ void fill_frame(const float* K, const float* Tcw, const float* Tinv, double sd, 
         f.ea[r] = std::nextafter((float)a, INFINITY);
         f.eb[r] = std::nextafter((float)b, INFINITY);
     }
-    f.eam = std::fmax(std::fmax(f.ea[0], f.ea[1]), f.ea[2]);  // (fmax: a NaN entry is dropped, but then
-    f.ebm = std::fmax(std::fmax(f.eb[0], f.eb[1]), f.eb[2]);  //  Tf holds a NaN and every pair fails)
+    // (fmax: a NaN entry is dropped, but then Tf holds a NaN and every pair fails); times 1 + 16u rounded
+    // up: the slack decide32_stage1_bf's E_u / E_v need for their own roundings, carried by E itself
+    // (a larger E is a valid bound wherever E is used)
+    f.eam = std::nextafter((float)(std::fmax(std::fmax(f.ea[0], f.ea[1]), f.ea[2]) * (1.0 + 0x1p-20)), INFINITY);
+    f.ebm = std::nextafter((float)(std::fmax(std::fmax(f.eb[0], f.eb[1]), f.eb[2]) * (1.0 + 0x1p-20)), INFINITY);
 }
 
 // Largest double d2 >= 0 with (float)sqrt(d2) <= thr (binary search over the ordered bit patterns
