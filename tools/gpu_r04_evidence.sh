@@ -9,7 +9,7 @@ mkdir -p gpurun_out/profiles_new
 export TMPDIR=/tmp
 ROUND=${ROUND:-r04}
 if [ -z "$SKIP_TESTS" ]; then
-  timeout -k 10 700 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > gpurun_out/ev_tests.log 2>&1 \
+  timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > gpurun_out/ev_tests.log 2>&1 \
     || { tail -40 gpurun_out/ev_tests.log; exit 1; }
   tail -2 gpurun_out/ev_tests.log
   timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/ev_smoke.log 2>&1 || { tail -20 gpurun_out/ev_smoke.log; exit 1; }
@@ -22,6 +22,9 @@ cp gpurun_out/pmc_ab.json gpurun_out/profiles_new/${ROUND}_pmc_integrate_counter
 timeout -k 10 400 bash tools/pmc_conf.sh > gpurun_out/ev_pmc_conf.log 2>&1 || { tail -20 gpurun_out/ev_pmc_conf.log; exit 1; }
 cp gpurun_out/pmc_conf.json gpurun_out/profiles_new/${ROUND}_pmc_confidence.json
 cp gpurun_out/profiles_new/${ROUND}_pmc_*.json profiles/
+timeout -k 10 200 python tools/conf_workload.py --reps 5 --stats --ab 4 > gpurun_out/profiles_new/${ROUND}_conf_workload.json 2> gpurun_out/ev_conf.err || { tail -20 gpurun_out/ev_conf.err; exit 1; }
+cat gpurun_out/profiles_new/${ROUND}_conf_workload.json
+timeout -k 10 200 python tools/ab_extract.py --modes 0 --reps 15 > gpurun_out/profiles_new/${ROUND}_extract_workload.json 2> gpurun_out/ev_abx.err || { tail -20 gpurun_out/ev_abx.err; exit 1; }
 timeout -k 10 500 python bench.py > gpurun_out/ev_bench.json 2> gpurun_out/ev_bench.err || { tail -20 gpurun_out/ev_bench.err; exit 1; }
 cp gpurun_out/ev_bench.json gpurun_out/profiles_new/${ROUND}_bench.json
 python - <<'P'
