@@ -561,7 +561,9 @@ __global__ __launch_bounds__(256) void k_confidence(const float* __restrict__ de
                     ++n_pairs;
                     n_f32 += dcs >= 0;
                 }
-                if (__ballot(dcs < 0))  // (wave-uniform, rare: 0.4 % of pairs)
+#if MQR_CONF_BALLOT_DEFER  // (A/B library: the update behind a wave-uniform ballot)
+                if (__ballot(dcs < 0))
+#endif
                     if (dcs < 0) defer |= 1ull << (tt - clo);
                 nv += dcs > 0;
                 nc += dcs == 1;
