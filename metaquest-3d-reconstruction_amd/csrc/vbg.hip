@@ -1194,9 +1194,15 @@ int mqr_vbg_set_variant(mqr_vbg* v, int variant) {
         int lo = 0, hi = 0;
         (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
         hipStream_t s1 = nullptr, s2 = nullptr;
-        if (hipStreamCreateWithPriority(&s1, hipStreamNonBlocking, ip ? lo : hi) != hipSuccess ||
-            hipStreamCreateWithPriority(&s2, hipStreamNonBlocking, ip ? hi : lo) != hipSuccess) {
+        // (the other stream at the default priority, as the volume creates them)
+        const bool ok1 = ip ? hipStreamCreateWithFlags(&s1, hipStreamNonBlocking) == hipSuccess
+                            : hipStreamCreateWithPriority(&s1, hipStreamNonBlocking, hi) == hipSuccess;
+        const bool ok2 = ip ? hipStreamCreateWithPriority(&s2, hipStreamNonBlocking, hi) == hipSuccess
+                            : hipStreamCreateWithFlags(&s2, hipStreamNonBlocking) == hipSuccess;
+        (void)lo;
+        if (!ok1 || !ok2) {
             if (s1) (void)hipStreamDestroy(s1);
+            if (s2) (void)hipStreamDestroy(s2);
             set_error("stream creation failed");
             return 1;
         }
