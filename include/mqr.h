@@ -217,8 +217,7 @@ int mqr_vbg_profile(mqr_vbg* v, int enable);
  * the full-table undo-and-retry path; test hook), bit 13 sizes the table for the worst case, bit 14 makes
  * every integrate launch wait on a touch-stream event, bit 15 runs the batch in spatial per-XCD groups
  * (k_xcd_order; A/Bs), bit 16 gives the touch one stride-4 pixel per thread instead of two, bit 18 turns
- * off the speculative first-batch integrate (k_gate; A/B), bit 25 gives the integrate stream the priority
- * instead of the touch stream (A/B).
+ * off the speculative first-batch integrate (k_gate; A/B).
  * mqr_check_division: exhaustive bit-pattern check of the division shortcuts used on device against
  * IEEE division (which=0: 1/b via rcp_rn, 1: a/b via div_rn, 2: a/b via the bare core, 3: 1/b via
  * rcp_nm, 4: 1/b via rcp_m, over float bit patterns [lo_bits, lo_bits+count) as b or a); returns

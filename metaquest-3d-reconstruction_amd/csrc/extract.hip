@@ -798,7 +798,7 @@ __device__ __forceinline__ void mc_emit_vertex(int i, const uint4* rows, const i
 // a +x / +y / +z neighbour's from rows4).
 template <class M>
 __device__ __forceinline__ void mc_emit_tri(int i, const uint4* rows, const uint32_t* rowN, const uint32_t* triC,
-                                            const uint64_t* triP, const int32_t* nbrow, const int32_t* nbvoff,
+                                            const uint64_t* triP, const int32_t* nbrow, const int32_t* __restrict__ voff,
                                             const uint4* __restrict__ rows4, int32_t vb0, int32_t tb0, int32_t* tri) {
     constexpr int R = M::C - 1;
     int lo = 0, hi = M::R2 - 1;
@@ -841,7 +841,9 @@ __device__ __forceinline__ void mc_emit_tri(int i, const uint4* rows, const uint
             } else {
                 const int lx = ox - dx * R, ly = oy - dy * R, lz = oz - dz * R;
                 const uint4 ow = rows4[(int64_t)nbuf * M::R2 + lz * R + ly];
-                vid = nbvoff[k27] + mc_vid(ow.x, ow.z & 0xffffu, ow.z >> 16, ow.w & 0xffffu, lx, axis);
+                // (the neighbour's block offset read here, beside its row record, not in the prologue:
+                // one dependent global round trip fewer before the block's first barrier)
+                vid = voff[nbuf] + mc_vid(ow.x, ow.z & 0xffffu, ow.z >> 16, ow.w & 0xffffu, lx, axis);
             }
         }
         tri[3 * t + (2 - j)] = vid;
@@ -866,7 +868,7 @@ __device__ __forceinline__ void mc_emit_block(int64_t b, int role, const int32_t
     static_assert(NT >= 256, "one thread per triangle-table row");
     __shared__ uint32_t rowN[M::S2];
     __shared__ uint4 rows[M::R2];  // vbase, tbase, ex | ey << 16, ez | oc << 16
-    __shared__ int32_t nbrow[27], nbvoff[27];
+    __shared__ int32_t nbrow[27];
     __shared__ uint64_t triP[256];  // the triangle tables: lane-divergent lookups in a dependent loop
     __shared__ uint32_t triC[32];
     const int nvb = role == 2 ? 0 : vcount[b], ntb = role == 1 ? 0 : tcount[b];
@@ -881,11 +883,7 @@ __device__ __forceinline__ void mc_emit_block(int64_t b, int role, const int32_t
         if (tid < 256) triP[tid] = mqr_tri_packed[tid];
         if (tid < 32) triC[tid] = mqr_tri_count_packed[tid];
     }
-    if (tid < 27) {
-        const int32_t q = nb[b * 27 + tid];
-        nbrow[tid] = q;
-        nbvoff[tid] = ntb && q >= 0 ? voff[q] : 0;
-    }
+    if (tid < 27) nbrow[tid] = nb[b * 27 + tid];
     for (int r = tid; r < M::R2; r += NT) rows[r] = rows4[b * M::R2 + r];
     if (ntb)
         for (int q = tid; q < M::S2; q += NT) rowN[q] = rowNt[b * M::S2 + q];
@@ -898,7 +896,7 @@ __device__ __forceinline__ void mc_emit_block(int64_t b, int role, const int32_t
         for (int i = tid; i < nvb; i += NT)
             mc_emit_vertex<M>(i, rows, nbrow, pool, pres, xb, yb, zb, voxel_size, vb0, pos, nrm);
     }
-    for (int i = tid; i < ntb; i += NT) mc_emit_tri<M>(i, rows, rowN, triC, triP, nbrow, nbvoff, rows4, vb0, tb0, tri);
+    for (int i = tid; i < ntb; i += NT) mc_emit_tri<M>(i, rows, rowN, triC, triP, nbrow, voff, rows4, vb0, tb0, tri);
 }
 
 // diag (A/B library, MQR_EMIT_DIAG): 1 vertices only, 2 triangles only (timing of one half, wrong output)

@@ -184,7 +184,6 @@ struct mqr_vbg {
 
     int kernel_variant = 0;    // integrate kernel configuration (launch_integrate in vbg.hip), 1 = generic
     bool pipelined = true;     // overlap touch(b+1) with integrate(b)
-    bool int_priority = false; // A/B (variant bit 25): the integrate stream, not the touch stream, gets the priority
     bool lpt_order = true;     // integrate blocks in longest-first order
     bool xcd_order = false;    // spatial groups per XCD (k_xcd_order; variant bit 0x8000, A/B)
     bool touch_wait = false;   // integrate waits on a touch-stream event every batch (variant bit 0x4000, A/B)
