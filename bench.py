@@ -3,7 +3,7 @@
 
 A "step" = integrate the rank's whole 500-frame depth sequence (640x480, procedural room = a
 512^3-voxel volume at 5 mm, R=16, depth_max 4 m, truncation 10 voxels) into an empty volume:
-per 64-frame batch one touch launch (hash insert) + one integrate launch, inputs resident in HBM.
+per batch of up to 127 frames one touch launch (hash insert) + one integrate launch, inputs resident in HBM.
 With N > 1 ranks the step is BASELINE's C4 (configs[3]): the fixed 2000-frame LEFT+RIGHT capture
 split over the ranks by contiguous frame ranges (strong scaling), each rank integrating its range,
 then the single RCCL exchange (mqr_reduce_rccl, sharded: owned slice + halo per rank); the line
@@ -1180,7 +1180,7 @@ def main():
                                     "depth_max 4 m, trunc 10"),
                        "frames_per_gpu": B, "height": H, "width": W, "voxel_size": args.voxel,
                        "block_resolution": args.block_resolution, "depth_max": args.depth_max,
-                       "trunc_voxel_multiplier": args.trunc, "frame_batch": 64,
+                       "trunc_voxel_multiplier": args.trunc, "frame_batch": 127,
                        "parallelism": f"frame-shard x{world}" + (f" + libmqr merge ({args.merge}, {transport})"
                                                                  if world > 1 else "")},
             "sharded_extract": sharded,
