@@ -888,27 +888,15 @@ __device__ __forceinline__ void mc_emit_block(int64_t b, int role, const int32_t
     if (ntb)
         for (int q = tid; q < M::S2; q += NT) rowN[q] = rowNt[b * M::S2 + q];
     __syncthreads();
-#if MQR_EMIT_SPLIT  // (A/B library) the first half of the waves emits the vertices, the second the triangles
-    constexpr int VT = NT / 2;
-    const bool vside = tid < VT;
-    const int t0 = vside ? tid : tid - VT;
-#else
-    constexpr int VT = NT;
-    constexpr bool vside = true;
-    const int t0 = tid;
-#endif
-    if (nvb && vside) {
+    if (nvb) {
         const int lane = tid & 63;
         const uint32_t pres = (uint32_t)__ballot(lane < 27 && nbrow[lane < 27 ? lane : 0] >= 0);
         int xb, yb, zb;
         unpack_key(bkeys[b], xb, yb, zb);
-        for (int i = t0; i < nvb; i += VT)
+        for (int i = tid; i < nvb; i += NT)
             mc_emit_vertex<M>(i, rows, nbrow, pool, pres, xb, yb, zb, voxel_size, vb0, pos, nrm);
     }
-#if MQR_EMIT_SPLIT
-    if (!vside)
-#endif
-        for (int i = t0; i < ntb; i += VT) mc_emit_tri<M>(i, rows, rowN, triC, triP, nbrow, voff, rows4, vb0, tb0, tri);
+    for (int i = tid; i < ntb; i += NT) mc_emit_tri<M>(i, rows, rowN, triC, triP, nbrow, voff, rows4, vb0, tb0, tri);
 }
 
 // diag (A/B library, MQR_EMIT_DIAG): 1 vertices only, 2 triangles only (timing of one half, wrong output)
