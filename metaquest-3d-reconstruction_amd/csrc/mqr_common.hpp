@@ -132,11 +132,6 @@ struct mqr_vbg {
     // batch parity; the hash table, pool and pool counter are shared.
     hipStream_t stream = nullptr;
     hipStream_t stream2 = nullptr;
-    // A/B (variant bit 25): the touches of a call's later batches on a stream restricted to a subset of
-    // the CUs (hipExtStreamCreateWithCUMask), ordered with `stream` by ev_mask
-    hipStream_t stream3 = nullptr;
-    hipEvent_t ev_mask[2] = {nullptr, nullptr};
-    bool touch_masked = false, touch_on_masked = false;
     // Ordering events between the two streams are recorded with a DEVICE-scope release
     // (hipEventDisableSystemFence): a default (system-scope) event makes the packet processor write
     // back and invalidate every XCD's L2 at the record -- ~20 us between consecutive integrate

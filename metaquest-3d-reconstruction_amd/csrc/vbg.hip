@@ -610,12 +610,7 @@ static int touch_launch(mqr_vbg* v, int p, const float* dbase, int64_t HW, int H
     // (measured and removed, profiles/r04_ab_integrate.json and DESIGN.md §4.1: a frame per workgroup
     // (k_touch_frame), a two-phase collect / claim touch, 8 frames per strip workgroup with one claim per
     // (block, frame group))
-    const bool masked = n > 0 && v->touch_on_masked && v->stream3;
-    hipStream_t ts = masked ? v->stream3 : v->stream;
-    if (masked) {
-        MQR_CHECK_HIP(hipEventRecord(v->ev_mask[0], v->stream));
-        MQR_CHECK_HIP(hipStreamWaitEvent(ts, v->ev_mask[0], 0));
-    }
+    hipStream_t ts = v->stream;
     if (n > 0) {
         if (v->touch_ppt == 1)
             hipLaunchKernelGGL(k_touch<1>, dim3((n + 255) / 256, b), dim3(256), 0, ts, dbase, HW, H, W,
@@ -625,10 +620,6 @@ static int touch_launch(mqr_vbg* v, int p, const float* dbase, int64_t HW, int H
             hipLaunchKernelGGL(k_touch<2>, dim3((n + 511) / 512, b), dim3(256), 0, ts, dbase, HW, H, W,
                                v->d_fp[p], dframe_dev(v, p), depth_scale, depth_max, sdf_trunc, block_size, t, max_probe,
                                alloc, v->ctr(p), v->pool_ctr(), v->pool_cap, v->bkeys, v->lists[p], v->list_cap);
-    }
-    if (masked) {
-        MQR_CHECK_HIP(hipEventRecord(v->ev_mask[1], ts));
-        MQR_CHECK_HIP(hipStreamWaitEvent(v->stream, v->ev_mask[1], 0));
     }
     MQR_CHECK_HIP(hipGetLastError());
     if (v->profile_touch) {
@@ -858,9 +849,6 @@ int mqr_vbg_destroy(mqr_vbg* v) {
     if (v->h_ex) (void)hipHostFree(v->h_ex);
     if (v->stream) (void)hipStreamDestroy(v->stream);
     if (v->stream2) (void)hipStreamDestroy(v->stream2);
-    if (v->stream3) (void)hipStreamDestroy(v->stream3);
-    for (hipEvent_t e : v->ev_mask)
-        if (e) (void)hipEventDestroy(e);
     delete v;
     return 0;
 }
@@ -947,11 +935,8 @@ int mqr_integrate_frames(mqr_vbg* v, const float* depths, int depth_loc, int B, 
         // them.  Later batches' counters are read while the previous integrate runs anyway.
         const bool spec = batch == 0 && v->spec_head && v->pipelined && !v->probe_one && v->batch_n_max > 0;
         TouchState ts;
-        v->touch_on_masked = batch > 0 && v->touch_masked;  // (A/B bit 25)
-        const int trc = touch_batch_launch(v, p, dbase, HW, H, W, b, depth_scale, depth_max, sdf_trunc, block_size,
-                                           max_touch, ts);
-        v->touch_on_masked = false;
-        if (trc) return 1;
+        if (touch_batch_launch(v, p, dbase, HW, H, W, b, depth_scale, depth_max, sdf_trunc, block_size, max_touch, ts))
+            return 1;
         if (spec) {
             const int64_t grid = std::min<int64_t>(std::max<int64_t>(v->batch_n_max + v->batch_n_max / 4, 256), 8192);
             const size_t ev_before = v->int_events.size();
@@ -1205,21 +1190,8 @@ int mqr_vbg_set_variant(mqr_vbg* v, int variant) {
     v->pipelined = (variant & 0x100) == 0;  // bit 8: serialise touch and integrate (A/B of the overlap)
     // (the integrate stream rather than the touch stream at the device's highest priority measured
     // 2.592 vs 2.587 ms per step: removed)
-    // bit 25 (A/B): the touches of a call's later batches on a stream restricted to the first
-    // MQR_TOUCH_CUS (default 32) CUs, so the overlapped integrate keeps the rest uncontended
-    v->touch_masked = (variant & 0x2000000) != 0;
-    if (v->touch_masked && !v->stream3) {
-        const char* env = getenv("MQR_TOUCH_CUS");
-        const int ncu = std::max(1, std::min(256, env ? atoi(env) : 32));
-        uint32_t mask[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        for (int i = 0; i < ncu; ++i) mask[i / 32] |= 1u << (i % 32);
-        if (hipExtStreamCreateWithCUMask(&v->stream3, 8, mask) != hipSuccess ||
-            hipEventCreateWithFlags(&v->ev_mask[0], hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess ||
-            hipEventCreateWithFlags(&v->ev_mask[1], hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess) {
-            set_error("CU-masked stream creation failed");
-            return 1;
-        }
-    }
+    // (the later batches' touches on a stream restricted to 32 / 64 / 128 CUs measured 3.07 / 2.72 /
+    // 2.61 vs 2.54-2.58 ms per step -- the overlapped touch barely slows the integrate: removed)
     v->lpt_order = (variant & 0x200) == 0;  // bit 9: integrate in touch order instead of longest-first
     // bit 10: 32-frame batches; bit 20: 64-frame batches (round 3) (A/Bs)
     v->batch_frames = (variant & 0x400) ? 32 : (variant & 0x100000) ? 64 : kMaxBatch;
