@@ -17,6 +17,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <type_traits>
 #include <vector>
 
 #include "mqr_common.hpp"
@@ -403,7 +404,7 @@ __device__ __forceinline__ Stage32 decide32_stage1_bf(__amdgpu_buffer_rsrc_t rs,
     r.Ev = Ev;
     const uint32_t off = go ? __umul24((uint32_t)v0, W4) + ((uint32_t)u0 << 2) : past_end;
     const u32x2 a = __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0);
-    const u32x2 c = __builtin_amdgcn_raw_buffer_load_b64(rs, off + W4, 0, 0);
+    const u32x2 c = __builtin_amdgcn_raw_buffer_load_b64(rs, off, W4, 0);  // (the next row: scalar offset)
     r.ab = make_float2(__uint_as_float(a.x), __uint_as_float(a.y));
     r.cd = make_float2(__uint_as_float(c.x), __uint_as_float(c.y));
     return r;
@@ -485,7 +486,8 @@ __device__ inline int ref_point(const ConfFrame& fr, int u, int v, float dref, d
 // `err <= threshold` on the float32 error map is d2 <= d2_max (sqrt and both roundings monotone).
 // STATS: count the pairs per deciding stage into st[4] (pairs, float32 prefilter, float64 filter,
 // float64 back-projection) -- mqr_confidence_stats.
-template <bool STATS, bool WIDE, bool DIAG = false, bool BF = false>
+// NARROW: a window of at most 32 frames (r <= 15): 32-bit deferral masks.
+template <bool STATS, bool WIDE, bool DIAG = false, bool BF = false, bool NARROW = false>
 __global__ __launch_bounds__(256) void k_confidence(const float* __restrict__ depths, int N, int H, int W,
                                                     const ConfFrame* __restrict__ fr, int ref_begin, int r,
                                                     double depth_max, double d2_max, double sd,
@@ -544,7 +546,8 @@ __global__ __launch_bounds__(256) void k_confidence(const float* __restrict__ de
                     if (t != ref && fr[t].ok) break;  // the reference frame and frames not ok are skipped
                 return t;
             };
-            uint64_t defer = 0;
+            using dmask_t = std::conditional_t<NARROW, uint32_t, uint64_t>;
+            dmask_t defer = 0;
             int t = next_t(clo - 1);
             const uint32_t fbytes = 4u * (uint32_t)HW, W4 = 4u * (uint32_t)W;
             auto stage1 = [&](int tt) {
@@ -564,7 +567,7 @@ __global__ __launch_bounds__(256) void k_confidence(const float* __restrict__ de
 #if MQR_CONF_BALLOT_DEFER  // (A/B library: the update behind a wave-uniform ballot)
                 if (__ballot(dcs < 0))
 #endif
-                    if (dcs < 0) defer |= 1ull << (tt - clo);
+                    if (dcs < 0) defer |= (dmask_t)1 << (tt - clo);
                 nv += dcs > 0;
                 nc += dcs == 1;
             };
@@ -615,7 +618,7 @@ __global__ __launch_bounds__(256) void k_confidence(const float* __restrict__ de
                 }
             }
             while (defer) {
-                const int td = clo + __builtin_ctzll(defer);
+                const int td = clo + (NARROW ? __builtin_ctz((uint32_t)defer) : __builtin_ctzll((uint64_t)defer));
                 defer &= defer - 1;
                 int dcs = pixel_decide(depths + (int64_t)td * HW, W, wm1, hm1, fr[td], pw, zmax, dmf, lo2, hi2, d2_max);
                 if (STATS) n_tail += dcs >> 2;
@@ -866,7 +869,8 @@ int mqr_confidence(int device, const float* depths, int depth_loc, int N, int H,
         MQR_CHECK_HIP(hipMalloc(&dvalid, sizeof(int32_t) * nref * HW));
     }
     const dim3 grid((unsigned)((HW + 255) / 256), nref);
-    const bool wide = frame_range > 31;  // a window of more than 64 frames: chunked defer masks
+    const bool wide = frame_range > 31;    // a window of more than 64 frames: chunked defer masks
+    const bool narrow = frame_range <= 15;  // at most 32 frames: 32-bit defer masks
     // the branch-free float32 stages (default) address the frames with 32-bit byte offsets; the branchy
     // ones (mode 4, the first round-4 form) remain for frames past that and for A/Bs
     const bool bf = !cc.branchy && 4 * (HW + W) < (int64_t{1} << 31);
@@ -878,13 +882,17 @@ int mqr_confidence(int device, const float* depths, int depth_loc, int N, int H,
         if (!cc.dst) MQR_CHECK_HIP(hipMalloc(&cc.dst, 4 * sizeof(unsigned long long)));
         MQR_CHECK_HIP(hipMemsetAsync(cc.dst, 0, 4 * sizeof(unsigned long long), s));
         if (bf)
-            wide ? launch(k_confidence<true, true, false, true>, cc.dst) : launch(k_confidence<true, false, false, true>, cc.dst);
+            wide ? launch(k_confidence<true, true, false, true>, cc.dst)
+                 : narrow ? launch(k_confidence<true, false, false, true, true>, cc.dst)
+                          : launch(k_confidence<true, false, false, true>, cc.dst);
         else
             wide ? launch(k_confidence<true, true>, cc.dst) : launch(k_confidence<true, false>, cc.dst);
     } else if (cc.diag) {  // timing diagnostics only (wrong results): no tap loads
         launch(k_confidence<false, false, true>, nullptr);
     } else if (bf) {
-        wide ? launch(k_confidence<false, true, false, true>, nullptr) : launch(k_confidence<false, false, false, true>, nullptr);
+        wide ? launch(k_confidence<false, true, false, true>, nullptr)
+             : narrow ? launch(k_confidence<false, false, false, true, true>, nullptr)
+                      : launch(k_confidence<false, false, false, true>, nullptr);
     } else {
         wide ? launch(k_confidence<false, true>, nullptr) : launch(k_confidence<false, false>, nullptr);
     }
