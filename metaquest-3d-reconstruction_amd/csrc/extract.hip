@@ -592,16 +592,21 @@ __device__ inline int mc_index(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
 }
 __device__ inline int mc_tri_count(int ci) { return (int)((mqr_tri_count_packed[ci >> 3] >> ((ci & 7) * 4)) & 0xFu); }
 
+// (nib: the per-cube counts as 4-bit fields, field x = the cube at origin x, for the emission pass)
 template <class M>
-__device__ inline int mc_row_tris(const uint32_t* rowN, uint32_t oc, int y, int z) {
+__device__ inline int mc_row_tris(const uint32_t* rowN, uint32_t oc, int y, int z, uint64_t* nib = nullptr) {
     const uint32_t a = rowN[M::q(y, z)], b = rowN[M::q(y + 1, z)], c = rowN[M::q(y, z + 1)];
     const uint32_t d = rowN[M::q(y + 1, z + 1)];
     int n = 0;
+    uint64_t w = 0;
     while (oc) {
         const int x = __builtin_ctz(oc);
         oc &= oc - 1;
-        n += mc_tri_count(mc_index(a >> (x + 1), b >> (x + 1), c >> (x + 1), d >> (x + 1)));
+        const int k = mc_tri_count(mc_index(a >> (x + 1), b >> (x + 1), c >> (x + 1), d >> (x + 1)));
+        n += k;
+        w |= (uint64_t)k << (4 * x);
     }
+    if (nib) *nib = w;
     return n;
 }
 
@@ -610,10 +615,12 @@ __device__ inline int mc_row_tris(const uint32_t* rowN, uint32_t oc, int y, int 
 // (owned crossing edges and owned surface cubes of the row) and the sign rows rowNt[b][q] of the
 // block's [-1, R]^3 tile (cube indices).  Emission of this block and of its -x / -y / -z
 // neighbours (triangles referencing vertices this block owns) read these instead of rebuilding them.
-template <int R>
+// NIB: also the rows' per-cube triangle counts (rowsT[b][row], mc_row_tris) for the emission pass.
+template <int R, bool NIB = false>
 __global__ __launch_bounds__(kMcThreads) void k_mc_count(const int32_t* __restrict__ nb, const uint16_t* __restrict__ bits,
                                                          int64_t tri_blocks, int32_t* vcount, int32_t* tcount,
-                                                         uint4* __restrict__ rows4, uint32_t* __restrict__ rowNt) {
+                                                         uint4* __restrict__ rows4, uint32_t* __restrict__ rowNt,
+                                                         uint64_t* __restrict__ rowsT = nullptr) {
     using M = Mc<R, 1>;
     __shared__ uint32_t rowV[M::S2], rowN[M::S2], cs[M::C2];
     __shared__ int32_t nbrow[27];
@@ -627,11 +634,13 @@ __global__ __launch_bounds__(kMcThreads) void k_mc_count(const int32_t* __restri
     const int r = threadIdx.x;
     RowEdges e{0, 0, 0, 0};
     int nv = 0, nt = 0;
+    uint64_t tw = 0;
     if (r < M::R2) {
         e = mc_row<M>(rowN, cs, r % R, r / R);
         if (b >= tri_blocks) e.oc = 0;  // halo block of a shard: its vertices, none of its cubes
         nv = __popc(e.ex) + __popc(e.ey) + __popc(e.ez);
-        nt = mc_row_tris<M>(rowN, e.oc, r % R, r / R);
+        nt = mc_row_tris<M>(rowN, e.oc, r % R, r / R, NIB ? &tw : nullptr);
+        if constexpr (NIB) rowsT[b * M::R2 + r] = tw;
     }
     int vtot, ttot;
     const int vb = block_exclusive_scan(nv, scratch, vtot);
@@ -743,16 +752,22 @@ __device__ inline int32_t mc_vid(uint32_t vbase, uint32_t ex, uint32_t ey, uint3
 
 // Vertex i of a block (emission pass): its row by binary search over the row vertex bases, its voxel
 // and edge by row_select, position and normal from the tsdf taps of the pool.
+// The last row whose vertex (F = 0) / triangle (F = 1) base is <= i, i.e. the (non-empty) row of output i.
+template <int R2, int F>
+__device__ __forceinline__ int row_search(const uint4* rows, int i) {
+    int lo = 0, hi = R2 - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if ((int)(F == 0 ? rows[mid].x : rows[mid].y) <= i) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+
 template <class M>
-__device__ __forceinline__ void mc_emit_vertex(int i, const uint4* rows, const int32_t* nbrow,
+__device__ __forceinline__ void mc_emit_vertex(int i, int lo, const uint4* rows, const int32_t* nbrow,
                                                const float2* __restrict__ pool, uint32_t pres, int xb, int yb, int zb,
                                                float voxel_size, int32_t vb0, float* pos, float* nrm) {
     constexpr int R = M::C - 1;
-    int lo = 0, hi = M::R2 - 1;  // last row whose vertex base is <= i (non-empty)
-    while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if ((int)rows[mid].x <= i) lo = mid; else hi = mid - 1;
-    }
     const uint4 rw = rows[lo];
     const uint32_t ex = rw.z & 0xffffu, ey = rw.z >> 16, ez = rw.w & 0xffffu;
     int k = i - (int)rw.x, x;
@@ -796,29 +811,42 @@ __device__ __forceinline__ void mc_emit_vertex(int i, const uint4* rows, const i
 // Triangle i of a block (emission pass): its cube by binary search over the row triangle bases and a
 // walk over the row's owned cubes, its three vertex ids from the row records (this block's in LDS,
 // a +x / +y / +z neighbour's from rows4).
-template <class M>
-__device__ __forceinline__ void mc_emit_tri(int i, const uint4* rows, const uint32_t* rowN, const uint32_t* triC,
-                                            const uint64_t* triP, const int32_t* nbrow, const int32_t* __restrict__ voff,
-                                            const uint4* __restrict__ rows4, int32_t vb0, int32_t tb0, int32_t* tri) {
+// (tcs: the rows' per-cube triangle counts (NIB) -- the cube found by skipping 4-bit fields in
+// registers instead of a walk with a table lookup per cube)
+template <class M, bool NIB>
+__device__ __forceinline__ void mc_emit_tri(int i, int lo, const uint4* rows, const uint64_t* tcs, const uint32_t* rowN,
+                                            const uint32_t* triC, const uint64_t* triP, const int32_t* nbrow,
+                                            const int32_t* __restrict__ voff, const uint4* __restrict__ rows4,
+                                            int32_t vb0, int32_t tb0, int32_t* tri) {
     constexpr int R = M::C - 1;
-    int lo = 0, hi = M::R2 - 1;
-    while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if ((int)rows[mid].y <= i) lo = mid; else hi = mid - 1;
-    }
     const uint4 rw = rows[lo];
     const int y = lo % R, z = lo / R;
     const uint32_t a = rowN[M::q(y, z)], bb = rowN[M::q(y + 1, z)], c = rowN[M::q(y, z + 1)];
     const uint32_t d = rowN[M::q(y + 1, z + 1)];
-    uint32_t oc = rw.w >> 16;
     int k = i - (int)rw.y, x = 0, ci = 0;
-    while (oc) {
-        x = __builtin_ctz(oc);
+    if constexpr (NIB) {
+        uint64_t w = tcs[lo];  // non-zero fields = the owned surface cubes; k < their sum
+        for (;;) {
+            const int s = __builtin_ctzll(w) & ~3;
+            w >>= s;
+            x += s >> 2;
+            const int n = (int)(w & 0xFu);
+            if (k < n) break;
+            k -= n;
+            w >>= 4;
+            ++x;
+        }
         ci = mc_index(a >> (x + 1), bb >> (x + 1), c >> (x + 1), d >> (x + 1));
-        const int n = (int)((triC[ci >> 3] >> ((ci & 7) * 4)) & 0xFu);
-        if (k < n) break;
-        k -= n;
-        oc &= oc - 1;
+    } else {
+        uint32_t oc = rw.w >> 16;
+        while (oc) {
+            x = __builtin_ctz(oc);
+            ci = mc_index(a >> (x + 1), bb >> (x + 1), c >> (x + 1), d >> (x + 1));
+            const int n = (int)((triC[ci >> 3] >> ((ci & 7) * 4)) & 0xFu);
+            if (k < n) break;
+            k -= n;
+            oc &= oc - 1;
+        }
     }
     const uint64_t te = triP[ci] >> (12 * k);
     const int64_t t = (int64_t)tb0 + i;
@@ -856,21 +884,28 @@ __device__ __forceinline__ void mc_emit_tri(int i, const uint4* rows, const uint
 // block, vertices then triangles); 1: vertices only; 2: triangles only (timing diagnostics).
 // (A merged vertex / triangle item loop, 512-thread blocks and a vertex and a triangle workgroup per
 // block were measured: no change or slower)
-template <int R, int NT>
+// MAP: blocks with at most kRowMap vertices / triangles find each output's row in an LDS byte map
+// (filled by one pass over the rows) instead of by a binary search over the row bases.
+constexpr int kRowMap = 2048;
+
+template <int R, int NT, bool NIB = false, bool MAP = false>
 __device__ __forceinline__ void mc_emit_block(int64_t b, int role, const int32_t* __restrict__ nb,
                                               const uint64_t* __restrict__ bkeys, const float2* __restrict__ pool,
                                               float voxel_size, const int32_t* __restrict__ vcount,
                                               const int32_t* __restrict__ tcount, const int32_t* __restrict__ voff,
                                               const int32_t* __restrict__ toff, const uint4* __restrict__ rows4,
                                               const uint32_t* __restrict__ rowNt, float* pos, float* nrm, int32_t* tri,
-                                              int64_t cap_v, int64_t cap_t) {
+                                              int64_t cap_v, int64_t cap_t, const uint64_t* __restrict__ rowsT) {
     using M = Mc<R, 1>;
     static_assert(NT >= 256, "one thread per triangle-table row");
+    static_assert(M::R2 <= 256, "row ids in bytes");
     __shared__ uint32_t rowN[M::S2];
     __shared__ uint4 rows[M::R2];  // vbase, tbase, ex | ey << 16, ez | oc << 16
     __shared__ int32_t nbrow[27];
     __shared__ uint64_t triP[256];  // the triangle tables: lane-divergent lookups in a dependent loop
     __shared__ uint32_t triC[32];
+    __shared__ uint64_t tcs[NIB ? M::R2 : 1];
+    __shared__ uint8_t vmap[MAP ? kRowMap : 1], tmap[MAP ? kRowMap : 1];
     const int nvb = role == 2 ? 0 : vcount[b], ntb = role == 1 ? 0 : tcount[b];
     if (nvb == 0 && ntb == 0) return;  // block-uniform: nothing to write
     const int32_t vb0 = voff[b], tb0 = toff[b];
@@ -885,34 +920,57 @@ __device__ __forceinline__ void mc_emit_block(int64_t b, int role, const int32_t
     }
     if (tid < 27) nbrow[tid] = nb[b * 27 + tid];
     for (int r = tid; r < M::R2; r += NT) rows[r] = rows4[b * M::R2 + r];
-    if (ntb)
+    if (ntb) {
         for (int q = tid; q < M::S2; q += NT) rowN[q] = rowNt[b * M::S2 + q];
+        if constexpr (NIB)
+            for (int r = tid; r < M::R2; r += NT) tcs[r] = rowsT[b * M::R2 + r];
+    }
     __syncthreads();
+    const bool vm = MAP && nvb <= kRowMap, tm = MAP && ntb <= kRowMap;  // block-uniform
+    if (vm || tm) {
+        for (int r = tid; r < M::R2; r += NT) {
+            const uint4 rw = rows[r];
+            if (vm) {
+                const int e = min(r + 1 < M::R2 ? (int)rows[r + 1].x : nvb, nvb);
+                for (int j = (int)rw.x; j < e; ++j) vmap[j] = (uint8_t)r;
+            }
+            if (tm) {
+                const int e = min(r + 1 < M::R2 ? (int)rows[r + 1].y : ntb, ntb);
+                for (int j = (int)rw.y; j < e; ++j) tmap[j] = (uint8_t)r;
+            }
+        }
+        __syncthreads();
+    }
     if (nvb) {
         const int lane = tid & 63;
         const uint32_t pres = (uint32_t)__ballot(lane < 27 && nbrow[lane < 27 ? lane : 0] >= 0);
         int xb, yb, zb;
         unpack_key(bkeys[b], xb, yb, zb);
-        for (int i = tid; i < nvb; i += NT)
-            mc_emit_vertex<M>(i, rows, nbrow, pool, pres, xb, yb, zb, voxel_size, vb0, pos, nrm);
+        for (int i = tid; i < nvb; i += NT) {
+            const int lo = vm ? (int)vmap[i] : row_search<M::R2, 0>(rows, i);
+            mc_emit_vertex<M>(i, lo, rows, nbrow, pool, pres, xb, yb, zb, voxel_size, vb0, pos, nrm);
+        }
     }
-    for (int i = tid; i < ntb; i += NT) mc_emit_tri<M>(i, rows, rowN, triC, triP, nbrow, voff, rows4, vb0, tb0, tri);
+    for (int i = tid; i < ntb; i += NT) {
+        const int lo = tm ? (int)tmap[i] : row_search<M::R2, 1>(rows, i);
+        mc_emit_tri<M, NIB>(i, lo, rows, tcs, rowN, triC, triP, nbrow, voff, rows4, vb0, tb0, tri);
+    }
 }
 
 // diag (A/B library, MQR_EMIT_DIAG): 1 vertices only, 2 triangles only (timing of one half, wrong output)
-template <int R, int NT = kMcThreads>
+template <int R, bool NIB = false, bool MAP = false, int NT = kMcThreads>
 __global__ __launch_bounds__(NT) void k_mc_emit(const int32_t* __restrict__ nb, const uint64_t* __restrict__ bkeys,
                                                 const float2* __restrict__ pool, float voxel_size,
                                                 const int32_t* __restrict__ vcount, const int32_t* __restrict__ tcount,
                                                 const int32_t* __restrict__ voff, const int32_t* __restrict__ toff,
                                                 const uint4* __restrict__ rows4, const uint32_t* __restrict__ rowNt,
                                                 float* pos, float* nrm, int32_t* tri, int64_t cap_v, int64_t cap_t,
-                                                int diag = 0) {
+                                                const uint64_t* __restrict__ rowsT, int diag = 0) {
 #if !MQR_AB
     diag = 0;
 #endif
-    mc_emit_block<R, NT>(blockIdx.x, diag, nb, bkeys, pool, voxel_size, vcount, tcount, voff, toff, rows4,
-                         rowNt, pos, nrm, tri, cap_v, cap_t);
+    mc_emit_block<R, NT, NIB, MAP>(blockIdx.x, diag, nb, bkeys, pool, voxel_size, vcount, tcount, voff, toff, rows4,
+                                   rowNt, pos, nrm, tri, cap_v, cap_t, rowsT);
 }
 
 
@@ -1214,9 +1272,10 @@ static int ex_scratch(mqr_vbg* v, int64_t n, bool mesh, ExScratch& e) {
                                                    (int)n, v->stream));
     const size_t sz_nb = align256(sizeof(int32_t) * 27 * n), sz_c = align256(sizeof(int32_t) * n);
     // mesh: the byte-tile path's face tables (3 R^2 u32 per block), or the bit-row path's row records
-    // (R^2 uint4) and sign rows ((R + 2)^2 u32) per block, whichever is larger
+    // (R^2 uint4), sign rows ((R + 2)^2 u32) and per-cube triangle counts (R^2 u64) per block,
+    // whichever is larger
     const size_t sz_f = mesh ? align256(std::max(sizeof(uint32_t) * 3 * v->R * v->R,
-                                                 sizeof(uint32_t) * (4 * v->R * v->R + (v->R + 2) * (v->R + 2))) *
+                                                 sizeof(uint32_t) * (6 * v->R * v->R + (v->R + 2) * (v->R + 2))) *
                                         n)
                              : 0;
     const size_t sz_b = align256(sizeof(uint16_t) * 3 * v->R * v->R * n);
@@ -1333,14 +1392,36 @@ static int build_nb(mqr_vbg* v, int32_t* nb) {
 // volume that is still being integrated.
 static int64_t spec_cap(int64_t hint) { return hint > 0 ? hint + hint / 4 + 4096 : 0; }
 
-template <int RT, class... A>
-static void launch_mc_emit(const mqr_vbg* v, int64_t n, A... args) {
+// Extraction configuration: bit 0 = NIB (k_mc_count), bit 1 = MAP (k_mc_emit); the A/B library
+// takes it from mqr_vbg_set_variant bits 28-30 (tools/ab_extract.py).
+[[maybe_unused]] constexpr int kExMode = 0;
+static int ex_mode(const mqr_vbg* v) {
+#if MQR_AB
+    return v->ex_mode;
+#else
+    (void)v;
+    return kExMode;
+#endif
+}
+
+template <int RT, bool NIB, bool MAP, class... A>
+static void launch_mc_emit_t(const mqr_vbg* v, int64_t n, A... args) {
 #if MQR_AB  // MQR_EMIT_DIAG=1: vertices only, 2: triangles only (timing diagnostics)
     static const int diag = getenv("MQR_EMIT_DIAG") ? atoi(getenv("MQR_EMIT_DIAG")) : 0;
 #else
     constexpr int diag = 0;
 #endif
-    hipLaunchKernelGGL((k_mc_emit<RT>), dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, args..., diag);
+    hipLaunchKernelGGL((k_mc_emit<RT, NIB, MAP>), dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, args..., diag);
+}
+
+template <int RT, class... A>
+static void launch_mc_emit(const mqr_vbg* v, int64_t n, A... args) {
+    switch (ex_mode(v) & 3) {
+        case 1: launch_mc_emit_t<RT, true, false>(v, n, args...); break;
+        case 2: launch_mc_emit_t<RT, false, true>(v, n, args...); break;
+        case 3: launch_mc_emit_t<RT, true, true>(v, n, args...); break;
+        default: launch_mc_emit_t<RT, false, false>(v, n, args...); break;
+    }
 }
 
 template <int RT>
@@ -1349,13 +1430,18 @@ static int mesh_passes(mqr_vbg* v, float thr, const ExScratch& e, mqr_geom* g, i
     constexpr int RR = RT > 0 ? RT : 16;
     uint4* rows4 = reinterpret_cast<uint4*>(e.faces);
     uint32_t* rowNt = reinterpret_cast<uint32_t*>(rows4 + n * RR * RR);
+    uint64_t* rowsT = reinterpret_cast<uint64_t*>(rowNt + n * (RR + 2) * (RR + 2));  // 8-byte aligned: (R + 2)^2 even
     int64_t nv = 0, nt = 0;
     if constexpr (RT > 0) {
         int64_t* tot = reinterpret_cast<int64_t*>(e.tmp);
         hipLaunchKernelGGL(k_mc_bits<RT>, dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, v->pool, thr, e.bits,
                            v->bkeys, v->tab, e.nb);
-        hipLaunchKernelGGL(k_mc_count<RT>, dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, e.nb, e.bits, tri_blocks,
-                           e.c0, e.c1, rows4, rowNt);
+        if (ex_mode(v) & 1)
+            hipLaunchKernelGGL((k_mc_count<RT, true>), dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, e.nb, e.bits,
+                               tri_blocks, e.c0, e.c1, rows4, rowNt, rowsT);
+        else
+            hipLaunchKernelGGL((k_mc_count<RT, false>), dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, e.nb, e.bits,
+                               tri_blocks, e.c0, e.c1, rows4, rowNt, rowsT);
         hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(kScanThreads), 0, v->stream, e.c0, e.c1, n, e.o0, e.o1, tot);
         // With a previous extraction's counts, emit into buffers of that size (+ margin) without
         // waiting for this one's totals; blocks past the capacity write nothing and the pass is re-run
@@ -1370,7 +1456,7 @@ static int mesh_passes(mqr_vbg* v, float thr, const ExScratch& e, mqr_geom* g, i
             launch_mc_emit<RT>(v, n, (const int32_t*)e.nb, (const uint64_t*)v->bkeys, (const float2*)v->pool,
                                v->voxel_size, (const int32_t*)e.c0, (const int32_t*)e.c1, (const int32_t*)e.o0,
                                (const int32_t*)e.o1, (const uint4*)rows4, (const uint32_t*)rowNt, g->pos, g->nrm,
-                               g->tri, cv, ct);
+                               g->tri, cv, ct, (const uint64_t*)rowsT);
             MQR_CHECK_HIP(hipGetLastError());
             emitted = true;
         }
@@ -1390,7 +1476,8 @@ static int mesh_passes(mqr_vbg* v, float thr, const ExScratch& e, mqr_geom* g, i
         if (alloc_geom(g, nv, nt)) return 1;
         launch_mc_emit<RT>(v, n, (const int32_t*)e.nb, (const uint64_t*)v->bkeys, (const float2*)v->pool, v->voxel_size,
                            (const int32_t*)e.c0, (const int32_t*)e.c1, (const int32_t*)e.o0, (const int32_t*)e.o1,
-                           (const uint4*)rows4, (const uint32_t*)rowNt, g->pos, g->nrm, g->tri, nv, nt);
+                           (const uint4*)rows4, (const uint32_t*)rowNt, g->pos, g->nrm, g->tri, nv, nt,
+                           (const uint64_t*)rowsT);
     } else {
         if (build_nb(v, e.nb)) return 1;
         hipLaunchKernelGGL(k_mesh_count<RT>, dim3((unsigned)n), dim3(kThreads), 0, v->stream, e.nb, n, v->pool, v->R,

@@ -1204,6 +1204,7 @@ int mqr_vbg_set_variant(mqr_vbg* v, int variant) {
     v->xcd_order = (variant & 0x8000) != 0;   // bit 15: spatial per-XCD groups (k_xcd_order, A/B)
     v->touch_ppt = (variant & 0x10000) ? 1 : 2;  // bit 16: one stride-4 pixel per touch thread (A/B)
     v->spec_head = (variant & 0x40000) == 0;     // bit 18: no speculative first-batch integrate (A/B)
+    v->ex_mode = (variant >> 28) & 7;            // bits 28-30: extraction configuration (A/B library only)
     return 0;
 }
 
