@@ -891,9 +891,8 @@ constexpr int kRowMap = 2048;
 template <int R, int NT, bool NIB = false, bool MAP = false>
 __device__ __forceinline__ void mc_emit_block(int64_t b, int role, const int32_t* __restrict__ nb,
                                               const uint64_t* __restrict__ bkeys, const float2* __restrict__ pool,
-                                              float voxel_size, const int32_t* __restrict__ vcount,
-                                              const int32_t* __restrict__ tcount, const int32_t* __restrict__ voff,
-                                              const int32_t* __restrict__ toff, const uint4* __restrict__ rows4,
+                                              float voxel_size, int nvb, int ntb, int32_t vb0, int32_t tb0,
+                                              const int32_t* __restrict__ voff, const uint4* __restrict__ rows4,
                                               const uint32_t* __restrict__ rowNt, float* pos, float* nrm, int32_t* tri,
                                               int64_t cap_v, int64_t cap_t, const uint64_t* __restrict__ rowsT) {
     using M = Mc<R, 1>;
@@ -906,13 +905,13 @@ __device__ __forceinline__ void mc_emit_block(int64_t b, int role, const int32_t
     __shared__ uint32_t triC[32];
     __shared__ uint64_t tcs[NIB ? M::R2 : 1];
     __shared__ uint8_t vmap[MAP ? kRowMap : 1], tmap[MAP ? kRowMap : 1];
-    const int nvb = role == 2 ? 0 : vcount[b], ntb = role == 1 ? 0 : tcount[b];
     if (nvb == 0 && ntb == 0) return;  // block-uniform: nothing to write
-    const int32_t vb0 = voff[b], tb0 = toff[b];
     // outputs past the speculative capacity: the host re-runs this pass into exact buffers
     // (int32 offsets: a total past 2^31 wraps them negative -- the host then fails the call after
     // this speculative pass, which must not have written before the buffers' start)
-    if (vb0 < 0 || tb0 < 0 || (int64_t)vb0 + vcount[b] > cap_v || (int64_t)tb0 + tcount[b] > cap_t) return;
+    if (vb0 < 0 || tb0 < 0 || (int64_t)vb0 + nvb > cap_v || (int64_t)tb0 + ntb > cap_t) return;
+    if (role == 1) ntb = 0;
+    if (role == 2) nvb = 0;
     const int tid = threadIdx.x;
     if (ntb) {
         if (tid < 256) triP[tid] = mqr_tri_packed[tid];
@@ -958,19 +957,33 @@ __device__ __forceinline__ void mc_emit_block(int64_t b, int role, const int32_t
 }
 
 // diag (A/B library, MQR_EMIT_DIAG): 1 vertices only, 2 triangles only (timing of one half, wrong output)
-template <int R, bool NIB = false, bool MAP = false, int NT = kMcThreads>
+// LST: workgroup i emits the i-th block with output of k_scan_counts' list (one record load)
+// instead of block i (its counts, then its offsets).
+template <int R, bool NIB = false, bool MAP = false, bool LST = false, int NT = kMcThreads>
 __global__ __launch_bounds__(NT) void k_mc_emit(const int32_t* __restrict__ nb, const uint64_t* __restrict__ bkeys,
                                                 const float2* __restrict__ pool, float voxel_size,
                                                 const int32_t* __restrict__ vcount, const int32_t* __restrict__ tcount,
                                                 const int32_t* __restrict__ voff, const int32_t* __restrict__ toff,
                                                 const uint4* __restrict__ rows4, const uint32_t* __restrict__ rowNt,
                                                 float* pos, float* nrm, int32_t* tri, int64_t cap_v, int64_t cap_t,
-                                                const uint64_t* __restrict__ rowsT, int diag = 0) {
+                                                const uint64_t* __restrict__ rowsT, const int4* __restrict__ recs,
+                                                const int64_t* __restrict__ nrecs, int diag = 0) {
 #if !MQR_AB
     diag = 0;
 #endif
-    mc_emit_block<R, NT, NIB, MAP>(blockIdx.x, diag, nb, bkeys, pool, voxel_size, vcount, tcount, voff, toff, rows4,
-                                   rowNt, pos, nrm, tri, cap_v, cap_t, rowsT);
+    if constexpr (LST) {
+        const int64_t nr = *nrecs;
+        const int4 rc = recs[blockIdx.x];  // (past nr: a stale record, unused)
+        if ((int64_t)blockIdx.x >= nr) return;
+        mc_emit_block<R, NT, NIB, MAP>(rc.x, diag, nb, bkeys, pool, voxel_size, rc.w & 0xffff, rc.w >> 16, rc.y, rc.z,
+                                       voff, rows4, rowNt, pos, nrm, tri, cap_v, cap_t, rowsT);
+    } else {
+        const int64_t b = blockIdx.x;
+        const int nvb = vcount[b], ntb = tcount[b];
+        if (nvb == 0 && ntb == 0) return;
+        mc_emit_block<R, NT, NIB, MAP>(b, diag, nb, bkeys, pool, voxel_size, nvb, ntb, voff[b], toff[b], voff, rows4,
+                                       rowNt, pos, nrm, tri, cap_v, cap_t, rowsT);
+    }
 }
 
 
@@ -982,15 +995,21 @@ __global__ __launch_bounds__(NT) void k_mc_emit(const int32_t* __restrict__ nb, 
 // thread scans kScanPer consecutive counts, wave and workgroup scans of the thread sums; results
 // back through LDS to coalesced stores; a running carry between tiles.
 constexpr int kScanThreads = 1024, kScanPer = 8, kScanTile = kScanThreads * kScanPer;
+// recs (optional, with c1): the blocks with output in block order, {block, o0, o1, c0 | c1 << 16}
+// (per-block counts < 2^16 at R <= 16), their number in totals[2] -- the emission pass's grid reads
+// one record per workgroup instead of the counts, then the offsets, of every block.
 __global__ __launch_bounds__(kScanThreads) void k_scan_counts(const int32_t* __restrict__ c0,
                                                               const int32_t* __restrict__ c1, int64_t n,
                                                               int32_t* __restrict__ o0, int32_t* __restrict__ o1,
-                                                              int64_t* __restrict__ totals) {
+                                                              int64_t* __restrict__ totals,
+                                                              int4* __restrict__ recs = nullptr) {
     __shared__ int32_t t0[kScanTile], t1[kScanTile];
     __shared__ int64_t ws0[kScanThreads / 64], ws1[kScanThreads / 64];
+    __shared__ int32_t ws2[kScanThreads / 64];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const bool two = c1 != nullptr;
+    const bool two = c1 != nullptr, lst = two && recs != nullptr;
     int64_t carry0 = 0, carry1 = 0;
+    int32_t carry2 = 0;
     for (int64_t base = 0; base < n; base += kScanTile) {
         int32_t v0[kScanPer], v1[kScanPer];
 #pragma unroll
@@ -1006,40 +1025,53 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_counts(const int32_t* __r
         }
         __syncthreads();
         int64_t s0 = 0, s1 = 0;
+        int32_t s2 = 0;  // blocks with output
 #pragma unroll
         for (int k = 0; k < kScanPer; ++k) {
-            s0 += t0[tid * kScanPer + k];
-            s1 += t1[tid * kScanPer + k];
+            const int32_t a = t0[tid * kScanPer + k], b = t1[tid * kScanPer + k];
+            s0 += a;
+            s1 += b;
+            s2 += (a | b) != 0;
         }
         int64_t i0 = s0, i1 = s1;  // inclusive wave scans of the thread sums
+        int32_t i2 = s2;
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
             const int64_t a = __shfl_up(i0, d, 64), b = __shfl_up(i1, d, 64);
+            const int32_t c = __shfl_up(i2, d, 64);
             if (lane >= d) {
                 i0 += a;
                 i1 += b;
+                i2 += c;
             }
         }
         if (lane == 63) {
             ws0[wave] = i0;
             ws1[wave] = i1;
+            ws2[wave] = i2;
         }
         __syncthreads();
         int64_t b0 = carry0, b1 = carry1, tot0 = 0, tot1 = 0;
+        int32_t b2 = carry2, tot2 = 0;
         for (int w = 0; w < kScanThreads / 64; ++w) {
             if (w < wave) {
                 b0 += ws0[w];
                 b1 += ws1[w];
+                b2 += ws2[w];
             }
             tot0 += ws0[w];
             tot1 += ws1[w];
+            tot2 += ws2[w];
         }
         int64_t r0 = b0 + i0 - s0, r1 = b1 + i1 - s1;  // exclusive prefix of this thread's counts
+        int32_t r2 = b2 + i2 - s2;
 #pragma unroll
         for (int k = 0; k < kScanPer; ++k) {
             const int32_t a = t0[tid * kScanPer + k], b = t1[tid * kScanPer + k];
             t0[tid * kScanPer + k] = (int32_t)r0;
             t1[tid * kScanPer + k] = (int32_t)r1;
+            if (lst && (a | b) != 0)
+                recs[r2++] = make_int4((int32_t)(base + tid * kScanPer + k), (int32_t)r0, (int32_t)r1, a | (b << 16));
             r0 += a;
             r1 += b;
         }
@@ -1054,11 +1086,13 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_counts(const int32_t* __r
         }
         carry0 += tot0;
         carry1 += tot1;
+        carry2 += tot2;
         __syncthreads();  // the tile buffers and wave sums are reused
     }
     if (tid == 0) {
         totals[0] = carry0;
         totals[1] = carry1;
+        if (lst) totals[2] = carry2;
     }
 }
 
@@ -1272,14 +1306,14 @@ static int ex_scratch(mqr_vbg* v, int64_t n, bool mesh, ExScratch& e) {
                                                    (int)n, v->stream));
     const size_t sz_nb = align256(sizeof(int32_t) * 27 * n), sz_c = align256(sizeof(int32_t) * n);
     // mesh: the byte-tile path's face tables (3 R^2 u32 per block), or the bit-row path's row records
-    // (R^2 uint4), sign rows ((R + 2)^2 u32) and per-cube triangle counts (R^2 u64) per block,
-    // whichever is larger
+    // (R^2 uint4), sign rows ((R + 2)^2 u32), per-cube triangle counts (R^2 u64) and the list
+    // record (int4) per block, whichever is larger
     const size_t sz_f = mesh ? align256(std::max(sizeof(uint32_t) * 3 * v->R * v->R,
-                                                 sizeof(uint32_t) * (6 * v->R * v->R + (v->R + 2) * (v->R + 2))) *
+                                                 sizeof(uint32_t) * (6 * v->R * v->R + (v->R + 2) * (v->R + 2) + 4)) *
                                         n)
                              : 0;
     const size_t sz_b = align256(sizeof(uint16_t) * 3 * v->R * v->R * n);
-    tmp_bytes = std::max<size_t>(tmp_bytes, 2 * sizeof(int64_t));
+    tmp_bytes = std::max<size_t>(tmp_bytes, 4 * sizeof(int64_t));  // k_scan_counts' totals
     const size_t need = sz_nb + 4 * sz_c + sz_f + sz_b + align256(tmp_bytes);
     if (v->ex_scratch_bytes < need) {
         MQR_CHECK_HIP(hipStreamSynchronize(v->stream));
@@ -1392,7 +1426,7 @@ static int build_nb(mqr_vbg* v, int32_t* nb) {
 // volume that is still being integrated.
 static int64_t spec_cap(int64_t hint) { return hint > 0 ? hint + hint / 4 + 4096 : 0; }
 
-// Extraction configuration: bit 0 = NIB (k_mc_count), bit 1 = MAP (k_mc_emit); the A/B library
+// Extraction configuration: bit 0 = NIB (k_mc_count), bit 1 = MAP, bit 2 = LST (k_mc_emit); the A/B library
 // takes it from mqr_vbg_set_variant bits 28-30 (tools/ab_extract.py).
 [[maybe_unused]] constexpr int kExMode = 0;
 static int ex_mode(const mqr_vbg* v) {
@@ -1404,24 +1438,32 @@ static int ex_mode(const mqr_vbg* v) {
 #endif
 }
 
-template <int RT, bool NIB, bool MAP, class... A>
+template <int RT, bool NIB, bool MAP, bool LST, class... A>
 static void launch_mc_emit_t(const mqr_vbg* v, int64_t n, A... args) {
 #if MQR_AB  // MQR_EMIT_DIAG=1: vertices only, 2: triangles only (timing diagnostics)
     static const int diag = getenv("MQR_EMIT_DIAG") ? atoi(getenv("MQR_EMIT_DIAG")) : 0;
 #else
     constexpr int diag = 0;
 #endif
-    hipLaunchKernelGGL((k_mc_emit<RT, NIB, MAP>), dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, args..., diag);
+    hipLaunchKernelGGL((k_mc_emit<RT, NIB, MAP, LST>), dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, args..., diag);
 }
 
 template <int RT, class... A>
 static void launch_mc_emit(const mqr_vbg* v, int64_t n, A... args) {
-    switch (ex_mode(v) & 3) {
-        case 1: launch_mc_emit_t<RT, true, false>(v, n, args...); break;
-        case 2: launch_mc_emit_t<RT, false, true>(v, n, args...); break;
-        case 3: launch_mc_emit_t<RT, true, true>(v, n, args...); break;
-        default: launch_mc_emit_t<RT, false, false>(v, n, args...); break;
+#if MQR_AB
+    switch (ex_mode(v)) {
+        case 1: launch_mc_emit_t<RT, true, false, false>(v, n, args...); return;
+        case 2: launch_mc_emit_t<RT, false, true, false>(v, n, args...); return;
+        case 3: launch_mc_emit_t<RT, true, true, false>(v, n, args...); return;
+        case 4: launch_mc_emit_t<RT, false, false, true>(v, n, args...); return;
+        case 5: launch_mc_emit_t<RT, true, false, true>(v, n, args...); return;
+        case 6: launch_mc_emit_t<RT, false, true, true>(v, n, args...); return;
+        case 7: launch_mc_emit_t<RT, true, true, true>(v, n, args...); return;
+        default: launch_mc_emit_t<RT, false, false, false>(v, n, args...); return;
     }
+#else
+    launch_mc_emit_t<RT, (kExMode & 1) != 0, (kExMode & 2) != 0, (kExMode & 4) != 0>(v, n, args...);
+#endif
 }
 
 template <int RT>
@@ -1431,6 +1473,7 @@ static int mesh_passes(mqr_vbg* v, float thr, const ExScratch& e, mqr_geom* g, i
     uint4* rows4 = reinterpret_cast<uint4*>(e.faces);
     uint32_t* rowNt = reinterpret_cast<uint32_t*>(rows4 + n * RR * RR);
     uint64_t* rowsT = reinterpret_cast<uint64_t*>(rowNt + n * (RR + 2) * (RR + 2));  // 8-byte aligned: (R + 2)^2 even
+    int4* recs = reinterpret_cast<int4*>(rowsT + n * RR * RR);  // 16-byte aligned: 4 (R + 2)^2 = 0 mod 16
     int64_t nv = 0, nt = 0;
     if constexpr (RT > 0) {
         int64_t* tot = reinterpret_cast<int64_t*>(e.tmp);
@@ -1442,7 +1485,8 @@ static int mesh_passes(mqr_vbg* v, float thr, const ExScratch& e, mqr_geom* g, i
         else
             hipLaunchKernelGGL((k_mc_count<RT, false>), dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, e.nb, e.bits,
                                tri_blocks, e.c0, e.c1, rows4, rowNt, rowsT);
-        hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(kScanThreads), 0, v->stream, e.c0, e.c1, n, e.o0, e.o1, tot);
+        hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(kScanThreads), 0, v->stream, e.c0, e.c1, n, e.o0, e.o1, tot,
+                           (ex_mode(v) & 4) ? recs : nullptr);
         // With a previous extraction's counts, emit into buffers of that size (+ margin) without
         // waiting for this one's totals; blocks past the capacity write nothing and the pass is re-run
         // into exact buffers if the totals exceed it.  Without, wait for the totals first.
@@ -1456,7 +1500,7 @@ static int mesh_passes(mqr_vbg* v, float thr, const ExScratch& e, mqr_geom* g, i
             launch_mc_emit<RT>(v, n, (const int32_t*)e.nb, (const uint64_t*)v->bkeys, (const float2*)v->pool,
                                v->voxel_size, (const int32_t*)e.c0, (const int32_t*)e.c1, (const int32_t*)e.o0,
                                (const int32_t*)e.o1, (const uint4*)rows4, (const uint32_t*)rowNt, g->pos, g->nrm,
-                               g->tri, cv, ct, (const uint64_t*)rowsT);
+                               g->tri, cv, ct, (const uint64_t*)rowsT, (const int4*)recs, (const int64_t*)(tot + 2));
             MQR_CHECK_HIP(hipGetLastError());
             emitted = true;
         }
@@ -1477,7 +1521,7 @@ static int mesh_passes(mqr_vbg* v, float thr, const ExScratch& e, mqr_geom* g, i
         launch_mc_emit<RT>(v, n, (const int32_t*)e.nb, (const uint64_t*)v->bkeys, (const float2*)v->pool, v->voxel_size,
                            (const int32_t*)e.c0, (const int32_t*)e.c1, (const int32_t*)e.o0, (const int32_t*)e.o1,
                            (const uint4*)rows4, (const uint32_t*)rowNt, g->pos, g->nrm, g->tri, nv, nt,
-                           (const uint64_t*)rowsT);
+                           (const uint64_t*)rowsT, (const int4*)recs, (const int64_t*)(tot + 2));
     } else {
         if (build_nb(v, e.nb)) return 1;
         hipLaunchKernelGGL(k_mesh_count<RT>, dim3((unsigned)n), dim3(kThreads), 0, v->stream, e.nb, n, v->pool, v->R,
@@ -1508,7 +1552,7 @@ static int point_passes(mqr_vbg* v, float thr, const ExScratch& e, mqr_geom* g) 
         hipLaunchKernelGGL(k_pt_count<RT>, dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, e.nb, e.bits, v->pool,
                            e.c0, rows4);
         hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(kScanThreads), 0, v->stream, e.c0, (const int32_t*)nullptr, n,
-                           e.o0, (int32_t*)nullptr, tot);
+                           e.o0, (int32_t*)nullptr, tot, (int4*)nullptr);
         MQR_CHECK_HIP(hipGetLastError());
         MQR_CHECK_HIP(hipMemcpyAsync(v->h_ex, tot, sizeof(int64_t), hipMemcpyDeviceToHost, v->stream));
         const int64_t cp = spec_cap(v->ex_hint[2]);  // speculative capacity, as in mesh_passes
