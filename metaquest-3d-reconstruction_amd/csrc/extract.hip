@@ -1428,7 +1428,7 @@ static int64_t spec_cap(int64_t hint) { return hint > 0 ? hint + hint / 4 + 4096
 
 // Extraction configuration: bit 0 = NIB (k_mc_count), bit 1 = MAP, bit 2 = LST (k_mc_emit); the A/B library
 // takes it from mqr_vbg_set_variant bits 28-30 (tools/ab_extract.py).
-[[maybe_unused]] constexpr int kExMode = 0;
+[[maybe_unused]] constexpr int kExMode = 3;  // NIB + MAP (tools/ab_extract.py)
 static int ex_mode(const mqr_vbg* v) {
 #if MQR_AB
     return v->ex_mode;

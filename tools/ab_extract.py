@@ -2,11 +2,13 @@
 """Interleaved A/B of extract_triangle_mesh configurations on the bench volume (C2, one process).
 
 python tools/ab_extract.py --modes 0 --reps 15
-mode = value of mqr_vbg_set_variant bits 28-30 for an extraction configuration under test (round 4
-measured the count pass emitting the vertices, 0.264 vs 0.237 ms, and a
+mode = value of mqr_vbg_set_variant bits 28-30 for an extraction configuration under test, A/B
+library only (extract.hip kExMode): bit 0 per-cube triangle counts from the count pass, bit 1 LDS row
+maps in the emission pass (both = 3, the library default), bit 2 emission over a compacted list of
+the blocks with output (round 4 also measured the count pass emitting the vertices, 0.264 vs 0.237 ms, and a
 vertex and a triangle workgroup per block, 0.187 vs 0.179 ms, removed) (round 3
 measured a merged vertex / triangle item loop and 512-thread emission blocks this way: no change,
-profiles/r03_ab_integrate_windows.json; neither is in the library now, so mode 0 is the library).
+profiles/r03_ab_integrate_windows.json; neither is in the library now).
 Prints per-mode median wall ms of mqr_extract_mesh (device-resident, the bench's extract_ms) and
 whether positions / normals / triangles equal the first mode's bit for bit.
 """
