@@ -25,6 +25,13 @@ cp gpurun_out/profiles_new/${ROUND}_pmc_*.json profiles/
 timeout -k 10 200 python tools/conf_workload.py --reps 5 --stats --ab 4 > gpurun_out/profiles_new/${ROUND}_conf_workload.json 2> gpurun_out/ev_conf.err || { tail -20 gpurun_out/ev_conf.err; exit 1; }
 cat gpurun_out/profiles_new/${ROUND}_conf_workload.json
 timeout -k 10 200 python tools/ab_extract.py --modes 0 --reps 15 > gpurun_out/profiles_new/${ROUND}_extract_workload.json 2> gpurun_out/ev_abx.err || { tail -20 gpurun_out/ev_abx.err; exit 1; }
+timeout -k 10 400 bash tools/pmc_extract.sh > gpurun_out/ev_pmc_extract.log 2>&1 || { tail -20 gpurun_out/ev_pmc_extract.log; exit 1; }
+cp gpurun_out/pmc_extract.json gpurun_out/profiles_new/${ROUND}_pmc_extract.json
+rm -rf /tmp/ev_exprof
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -f csv -d /tmp/ev_exprof -o run -- \
+  python tools/ab_extract.py --modes 0 --reps 15 > gpurun_out/ev_exprof.json 2> gpurun_out/ev_exprof.err \
+  || { tail -20 gpurun_out/ev_exprof.err; exit 1; }
+find /tmp/ev_exprof -name "*kernel_stats.csv" -exec cp {} gpurun_out/profiles_new/${ROUND}_extract_kernel_stats.csv \;
 timeout -k 10 500 python bench.py > gpurun_out/ev_bench.json 2> gpurun_out/ev_bench.err || { tail -20 gpurun_out/ev_bench.err; exit 1; }
 cp gpurun_out/ev_bench.json gpurun_out/profiles_new/${ROUND}_bench.json
 python - <<'P'
