@@ -281,6 +281,7 @@ struct Pix32 {
 // its VALU work).  st: 0 decided (no finite error), 1 taps pending, -1 undecided (float64 path).
 struct Stage32 {
     int st;
+    bool go, und;  // (BF: st == 1 / st == -1 as lane masks -- stage 2's decision stays in boolean form)
     float Z, EZ, P, EP, uu, vv, Eu, Ev;  // (floor(uu), floor(vv) are recomputed in stage 2: registers)
     float2 ab, cd;
 };
@@ -391,7 +392,8 @@ __device__ __forceinline__ Stage32 decide32_stage1_bf(__amdgpu_buffer_rsrc_t rs,
     // none_z -> 0; else !ok_z or the floors uncertain -> -1 (near the image border too: rare); else
     // out of the image -> 0; else taps
     const bool go = ok_z & sure & in_img;
-    r.st = go ? 1 : (none_z | (ok_z & sure)) ? 0 : -1;
+    r.go = go;
+    r.und = !(go | none_z | (ok_z & sure));
     // P = X^2 + Y^2 + Z^2 and, in EP, a RELATIVE bound rho of its error (stage 2 uses P (1 +- rho)):
     // |P* - P| <= 2 E (|X| + |Y| + Z) + 3 E^2 <= 2 sqrt(3) E sqrt(P) + 3 E^2 and sqrt(P) >= Z, so
     // rho = 2 sqrt(3) (E / Z) + 3 (E / Z)^2 + 8u (P's own roundings), E / Z <= ei; 3.5 and 3.01 cover the
@@ -441,8 +443,12 @@ __device__ __forceinline__ int decide32_stage2(const Stage32& r, const Pix32& px
 
 // decide32_stage2 without branches (BF): every lane consumes its taps (an early return left tap loads
 // in flight past the loop's back edge, and the compiler waited for them where their registers were
-// reused) and the decision is selected at the end -- the same decisions.
-__device__ __forceinline__ int decide32_stage2_bf(const Stage32& r, const Pix32& px, uint32_t dmb) {
+// reused) -- the same decisions, as lane masks: valid (decision > 0), consistent (== 1), deferred (< 0)
+// (the caller counts them with carry-in adds instead of selecting and re-testing an integer code)
+struct Dec32 {
+    bool valid, cons, dfr;
+};
+__device__ __forceinline__ Dec32 decide32_stage2_bf(const Stage32& r, const Pix32& px, uint32_t dmb) {
     constexpr float u = 0x1p-24f;
     const float Ia = r.ab.x, Ib = r.ab.y, Ic = r.cd.x, Id = r.cd.y;
     // the tap test: every tap in (0, depth_max] -- positive floats order like their bits, +0 is the
@@ -455,8 +461,10 @@ __device__ __forceinline__ int decide32_stage2_bf(const Stage32& r, const Pix32&
     // reference's own float32 rounding of zt; the weights' dependence on uu, vv is at most the taps'
     // range per unit, so E_dz = E_Z + 2 (E_u + E_v) (max - min) + 8u zf
     const float fu = r.uu, fv = r.vv;
-    const float z0 = __builtin_fmaf(fu, Ib - Ia, Ia), z1 = __builtin_fmaf(fu, Id - Ic, Ic);
-    const float zf = __builtin_fmaf(fv, z1 - z0, z0);
+    // (along v first: the row pairs (Ia, Ib), (Ic, Id) as loaded are the packed operands -- no
+    // register shuffle of the taps, whose copies at the loop's back edge waited for the loads)
+    const float za = __builtin_fmaf(fv, Ic - Ia, Ia), zb = __builtin_fmaf(fv, Id - Ib, Ib);
+    const float zf = __builtin_fmaf(fu, zb - za, za);
     const float span = __uint_as_float(tmax) - __uint_as_float(tmin);
     const float eu2 = r.Eu + r.Ev;
     const float Edz = __builtin_fmaf(eu2 + eu2, span, __builtin_fmaf(8.0f * u, zf, r.EZ));
@@ -466,8 +474,12 @@ __device__ __forceinline__ int decide32_stage2_bf(const Stage32& r, const Pix32&
     const float Phi = __builtin_fmaf(r.P, r.EP, r.P), Plo = __builtin_fmaf(-r.P, r.EP, r.P);  // (EP: relative)
     const bool in_band_lo = (a1 * a1) * Phi <= px.lo2s * (zl * zl);
     const bool out_band_hi = (a0 > 0.0f) & ((a0 * a0) * Plo > px.hi2s * (zh * zh));
-    const int d = in_band_lo ? 1 : out_band_hi ? 2 : -1;
-    return r.st <= 0 ? r.st : !taps ? 0 : d;
+    const bool gt = r.go & taps;
+    Dec32 d;
+    d.valid = gt & (in_band_lo | out_band_hi);
+    d.cons = gt & in_band_lo;
+    d.dfr = r.und | (gt & !(in_band_lo | out_band_hi));
+    return d;
 }
 
 // depth_to_pointcloud_numpy for one pixel: returns 0 when the ref pixel is not in (0, depth_max].
@@ -559,17 +571,28 @@ __global__ __launch_bounds__(256) void k_confidence(const float* __restrict__ de
                     return decide32_stage1<DIAG>(depths + (int64_t)tt * HW, W, H, wm1f, hm1f, fr[tt], px);
             };
             auto account = [&](const Stage32& st, int tt) {
-                const int dcs = BF ? decide32_stage2_bf(st, px, dmb) : decide32_stage2(st, px, dmb);
+                bool valid, cons, dfr;
+                if constexpr (BF) {
+                    const Dec32 d = decide32_stage2_bf(st, px, dmb);
+                    valid = d.valid;
+                    cons = d.cons;
+                    dfr = d.dfr;
+                } else {
+                    const int dcs = decide32_stage2(st, px, dmb);
+                    valid = dcs > 0;
+                    cons = dcs == 1;
+                    dfr = dcs < 0;
+                }
                 if (STATS) {
                     ++n_pairs;
-                    n_f32 += dcs >= 0;
+                    n_f32 += !dfr;
                 }
 #if MQR_CONF_BALLOT_DEFER  // (A/B library: the update behind a wave-uniform ballot)
-                if (__ballot(dcs < 0))
+                if (__ballot(dfr))
 #endif
-                    if (dcs < 0) defer |= (dmask_t)1 << (tt - clo);
-                nv += dcs > 0;
-                nc += dcs == 1;
+                    defer |= dfr ? (dmask_t)1 << (tt - clo) : (dmask_t)0;
+                nv += valid;
+                nc += cons;
             };
             // unrolled by two with the stages' roles alternating, and stage 1 issued unconditionally (past
             // the last neighbour it re-runs the current one, result unused): a `cur = nxt` copy of the tap
