@@ -44,6 +44,7 @@ struct ConfFrame {
     float cxu, cyu;  // 2u |cx| (1 + 4u), 2u |cy| (1 + 4u): decide32_stage1_bf's bound of 2u |uu|, 2u |vv|
     float ea[3], eb[3];
     float eam, ebm;  // max(ea), max(eb): decide32_stage1_bf's one bound for all three coordinates
+    float eam8, ebm8;  // 8 eam, max(8 ebm, 1e-6): its depth test Z >= max(8 E, 1e-6) in one fma (implied)
     int ok;  // frame_ok (a neighbour that is not ok is skipped, as the reference skips failed loads)
     // as a reference frame (host, per call): the largest c1 / c0 of its ok neighbours in the +-r window,
     // and (windows of <= 64 frames) the window's neighbour mask -- bit i: frame max(0, ref - r) + i is
@@ -368,17 +369,18 @@ __device__ __forceinline__ Stage32 decide32_stage1_bf(__amdgpu_buffer_rsrc_t rs,
     // Z <= 0 or Z > zmax certain -> 0; Z in (0, zmax] certain with E_Z <= Z / 8 and Z >= 1e-6 (then
     // Z - E_Z >= 7 Z / 8 > 0) -> go on; else -1.  (fmaxf drops a NaN E_Z, whose Z + E_Z then fails.)
     const bool none_z = (Z <= -EZ) | (Z - EZ > px.zhi);
-    const bool ok_z = (Z >= fmaxf(8.0f * EZ, 1e-6f)) & (Z + EZ < px.zlo);
+    const bool ok_z = (Z >= __builtin_fmaf(ft.eam8, px.m, ft.ebm8)) & (Z + EZ < px.zlo);  // Z >= max(8 E, 1e-6)
     const float inv = __builtin_amdgcn_rcpf(Z);
     const float qx = (X * ft.fxf) * inv, qy = (Y * ft.fyf) * inv;
     const float uu = qx + ft.cxf, vv = qy + ft.cyf;
     // |uu - uu*| <= (|fx| E_X + |fx X / Z| E_Z) / (Z - E_Z) + 5u |qx| + 2u |uu|  (decide32_stage1), with
     // qx = fx X / Z in float within 3u and 2u |uu| <= 2u |qx| + 2u |cx| (1 + 4u): every term positive, the
     // bound's own roundings inside its 1 + 16u factor (folded into irl)
-    const float irl = inv * __builtin_fmaf(2.0f * EZ, inv, 1.0f);  // >= 1 / (Z - E_Z)
-    // E / (Z - E), E carrying the 1 + 16u slack (host): with E_X = E_Y = E_Z = E, (|fx| E + |qx| E) / (Z - E)
-    // (1 + 16u) <= (|fx| + |qx|) ei
-    const float ei = EZ * irl;
+    // E / (Z - E) <= x (1 + 2x) for x = E / Z <= 1/8, evaluated as e1 (1 + 2 e1) with e1 = E inv (three
+    // roundings: rcp, product, fma), E carrying the 1 + 16u slack (host): with E_X = E_Y = E_Z = E,
+    // (|fx| E + |qx| E) / (Z - E) (1 + 16u) <= (|fx| + |qx|) ei
+    const float e1 = EZ * inv;
+    const float ei = __builtin_fmaf(e1 + e1, e1, e1);
     const float aqx = __builtin_fabsf(qx), aqy = __builtin_fabsf(qy);
     const float Eu = __builtin_fmaf(__builtin_fabsf(ft.fxf) + aqx, ei, __builtin_fmaf(7.5f * u, aqx, ft.cxu));
     const float Ev = __builtin_fmaf(__builtin_fabsf(ft.fyf) + aqy, ei, __builtin_fmaf(7.5f * u, aqy, ft.cyu));
@@ -455,7 +457,7 @@ __device__ __forceinline__ Dec32 decide32_stage2_bf(const Stage32& r, const Pix3
     // smallest pattern, negatives and NaNs lie above every positive finite pattern
     const uint32_t bA = __float_as_uint(Ia), bB = __float_as_uint(Ib), bC = __float_as_uint(Ic), bD = __float_as_uint(Id);
     const uint32_t tmax = max(max(bA, bB), max(bC, bD)), tmin = min(min(bA, bB), min(bC, bD));
-    const bool taps = (tmin != 0u) & (tmax <= dmb) & (dmb != 0u);
+    const bool taps = (tmin != 0u) & (tmax <= dmb);  // (dmb = 0: tmax <= 0 forces tmin = 0)
     // zf by three lerps on the fractions (r.uu, r.vv): within 4u max(I) <= 2^-22 depth_max of the exact
     // interpolation at the float32 uu, vv -- inside the band's 2^-18 depth_max ray-length term, like the
     // reference's own float32 rounding of zt; the weights' dependence on uu, vv is at most the taps'
@@ -590,7 +592,7 @@ __global__ __launch_bounds__(256) void k_confidence(const float* __restrict__ de
 #if MQR_CONF_BALLOT_DEFER  // (A/B library: the update behind a wave-uniform ballot)
                 if (__ballot(dfr))
 #endif
-                    defer |= dfr ? (dmask_t)1 << (tt - clo) : (dmask_t)0;
+                    defer |= (dmask_t)(dfr ? 1u : 0u) << (tt - clo);
                 nv += valid;
                 nc += cons;
             };
@@ -778,6 +780,10 @@ void fill_frame(const float* K, const float* Tcw, const float* Tinv, double sd, 
     // (a larger E is a valid bound wherever E is used)
     f.eam = std::nextafter((float)(std::fmax(std::fmax(f.ea[0], f.ea[1]), f.ea[2]) * (1.0 + 0x1p-20)), INFINITY);
     f.ebm = std::nextafter((float)(std::fmax(std::fmax(f.eb[0], f.eb[1]), f.eb[2]) * (1.0 + 0x1p-20)), INFINITY);
+    // RN(8 eam m + 8 ebm) = 8 RN(eam m + ebm) = 8 E (powers of two scale exactly), and with the 1e-6 floor
+    // in the addend RN(8 eam m + max(8 ebm, 1e-6)) >= max(8 E, 1e-6): the one-fma test implies the two
+    f.eam8 = 8.0f * f.eam;
+    f.ebm8 = std::fmax(8.0f * f.ebm, 1e-6f);
 }
 
 // Largest double d2 >= 0 with (float)sqrt(d2) <= thr (binary search over the ordered bit patterns
