@@ -995,19 +995,22 @@ __global__ __launch_bounds__(NT) void k_mc_emit(const int32_t* __restrict__ nb, 
 // thread scans kScanPer consecutive counts, wave and workgroup scans of the thread sums; results
 // back through LDS to coalesced stores; a running carry between tiles.
 constexpr int kScanThreads = 1024, kScanPer = 8, kScanTile = kScanThreads * kScanPer;
-// recs (optional, with c1): the blocks with output in block order, {block, o0, o1, c0 | c1 << 16}
+// LST (A/B mode, with c1): also the blocks with output in block order, {block, o0, o1, c0 | c1 << 16}
 // (per-block counts < 2^16 at R <= 16), their number in totals[2] -- the emission pass's grid reads
-// one record per workgroup instead of the counts, then the offsets, of every block.
+// one record per workgroup instead of the counts, then the offsets, of every block.  (A template
+// parameter: the list's third scan, compiled into every launch, made the kernel 5.4 -> 11.7 us.)
+template <bool LST = false>
 __global__ __launch_bounds__(kScanThreads) void k_scan_counts(const int32_t* __restrict__ c0,
                                                               const int32_t* __restrict__ c1, int64_t n,
                                                               int32_t* __restrict__ o0, int32_t* __restrict__ o1,
                                                               int64_t* __restrict__ totals,
-                                                              int4* __restrict__ recs = nullptr) {
+                                                              int4* __restrict__ recs) {
     __shared__ int32_t t0[kScanTile], t1[kScanTile];
     __shared__ int64_t ws0[kScanThreads / 64], ws1[kScanThreads / 64];
-    __shared__ int32_t ws2[kScanThreads / 64];
+    __shared__ int32_t ws2[LST ? kScanThreads / 64 : 1];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const bool two = c1 != nullptr, lst = two && recs != nullptr;
+    const bool two = c1 != nullptr;
+    constexpr bool lst = LST;
     int64_t carry0 = 0, carry1 = 0;
     int32_t carry2 = 0;
     for (int64_t base = 0; base < n; base += kScanTile) {
@@ -1025,30 +1028,31 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_counts(const int32_t* __r
         }
         __syncthreads();
         int64_t s0 = 0, s1 = 0;
-        int32_t s2 = 0;  // blocks with output
+        int32_t s2 = 0;  // blocks with output (LST)
 #pragma unroll
         for (int k = 0; k < kScanPer; ++k) {
             const int32_t a = t0[tid * kScanPer + k], b = t1[tid * kScanPer + k];
             s0 += a;
             s1 += b;
-            s2 += (a | b) != 0;
+            if constexpr (LST) s2 += (a | b) != 0;
         }
         int64_t i0 = s0, i1 = s1;  // inclusive wave scans of the thread sums
         int32_t i2 = s2;
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
             const int64_t a = __shfl_up(i0, d, 64), b = __shfl_up(i1, d, 64);
-            const int32_t c = __shfl_up(i2, d, 64);
+            int32_t c = 0;
+            if constexpr (LST) c = __shfl_up(i2, d, 64);
             if (lane >= d) {
                 i0 += a;
                 i1 += b;
-                i2 += c;
+                if constexpr (LST) i2 += c;
             }
         }
         if (lane == 63) {
             ws0[wave] = i0;
             ws1[wave] = i1;
-            ws2[wave] = i2;
+            if constexpr (LST) ws2[wave] = i2;
         }
         __syncthreads();
         int64_t b0 = carry0, b1 = carry1, tot0 = 0, tot1 = 0;
@@ -1057,11 +1061,11 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_counts(const int32_t* __r
             if (w < wave) {
                 b0 += ws0[w];
                 b1 += ws1[w];
-                b2 += ws2[w];
+                if constexpr (LST) b2 += ws2[w];
             }
             tot0 += ws0[w];
             tot1 += ws1[w];
-            tot2 += ws2[w];
+            if constexpr (LST) tot2 += ws2[w];
         }
         int64_t r0 = b0 + i0 - s0, r1 = b1 + i1 - s1;  // exclusive prefix of this thread's counts
         int32_t r2 = b2 + i2 - s2;
@@ -1485,8 +1489,12 @@ static int mesh_passes(mqr_vbg* v, float thr, const ExScratch& e, mqr_geom* g, i
         else
             hipLaunchKernelGGL((k_mc_count<RT, false>), dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, e.nb, e.bits,
                                tri_blocks, e.c0, e.c1, rows4, rowNt, rowsT);
-        hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(kScanThreads), 0, v->stream, e.c0, e.c1, n, e.o0, e.o1, tot,
-                           (ex_mode(v) & 4) ? recs : nullptr);
+        if (ex_mode(v) & 4)
+            hipLaunchKernelGGL(k_scan_counts<true>, dim3(1), dim3(kScanThreads), 0, v->stream, e.c0, e.c1, n, e.o0,
+                               e.o1, tot, recs);
+        else
+            hipLaunchKernelGGL(k_scan_counts<false>, dim3(1), dim3(kScanThreads), 0, v->stream, e.c0, e.c1, n, e.o0,
+                               e.o1, tot, (int4*)nullptr);
         // With a previous extraction's counts, emit into buffers of that size (+ margin) without
         // waiting for this one's totals; blocks past the capacity write nothing and the pass is re-run
         // into exact buffers if the totals exceed it.  Without, wait for the totals first.
@@ -1551,8 +1559,8 @@ static int point_passes(mqr_vbg* v, float thr, const ExScratch& e, mqr_geom* g) 
                            v->bkeys, v->tab, e.nb);
         hipLaunchKernelGGL(k_pt_count<RT>, dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, e.nb, e.bits, v->pool,
                            e.c0, rows4);
-        hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(kScanThreads), 0, v->stream, e.c0, (const int32_t*)nullptr, n,
-                           e.o0, (int32_t*)nullptr, tot, (int4*)nullptr);
+        hipLaunchKernelGGL(k_scan_counts<false>, dim3(1), dim3(kScanThreads), 0, v->stream, e.c0,
+                           (const int32_t*)nullptr, n, e.o0, (int32_t*)nullptr, tot, (int4*)nullptr);
         MQR_CHECK_HIP(hipGetLastError());
         MQR_CHECK_HIP(hipMemcpyAsync(v->h_ex, tot, sizeof(int64_t), hipMemcpyDeviceToHost, v->stream));
         const int64_t cp = spec_cap(v->ex_hint[2]);  // speculative capacity, as in mesh_passes
