@@ -17,3 +17,10 @@ timeout -k 10 200 rocprofv3 --kernel-trace --stats -f csv -d /tmp/q_exprof -o ru
 find /tmp/q_exprof -name "*kernel_stats.csv" -exec cp {} gpurun_out/r04q_extract_kernel_stats.csv \;
 cat gpurun_out/r04q_ab1.json gpurun_out/r04q_ab2.json gpurun_out/r04q_product.json
 grep "mqr" gpurun_out/r04q_extract_kernel_stats.csv | cut -c1-40,200-330
+# confidence: the working-tree kernel at 7 vs 8 waves per SIMD, 8 alternations
+: > gpurun_out/r04q_conf.jsonl
+for v in new w8 w8 new new w8 w8 new new w8 w8 new new w8 w8 new; do
+  MQR_HIP_LIB="$PWD/tools/_ab/libmqr_conf_$v.so" timeout -k 10 200 python -u tools/conf_workload.py --reps 7 > gpurun_out/r04q_tmp.json 2>> gpurun_out/r04q_conf.err || { tail -20 gpurun_out/r04q_conf.err; exit 1; }
+  python -c "import json,sys; d=json.load(open('gpurun_out/r04q_tmp.json')); print(json.dumps({'lib': '$v', 'ms': d['ms_median'], 'digest': d['digest'], 'src': d['confidence_src']}))" >> gpurun_out/r04q_conf.jsonl
+done
+cat gpurun_out/r04q_conf.jsonl
