@@ -501,8 +501,13 @@ __device__ inline int ref_point(const ConfFrame& fr, int u, int v, float dref, d
 // STATS: count the pairs per deciding stage into st[4] (pairs, float32 prefilter, float64 filter,
 // float64 back-projection) -- mqr_confidence_stats.
 // NARROW: a window of at most 32 frames (r <= 15): 32-bit deferral masks.
-template <bool STATS, bool WIDE, bool DIAG = false, bool BF = false, bool NARROW = false>
-__global__ __launch_bounds__(256) void k_confidence(const float* __restrict__ depths, int N, int H, int W,
+// W8: held to 8 waves per SIMD (the production instances: BF, !WIDE, !STATS) -- 61 instead of 68
+// VGPRs, nothing spilled: 6.84 vs 6.89 ms, 8 alternating processes each,
+// profiles/r04_ab_confidence_variants.json (the other instances would spill).  With SLP vectorisation,
+// 30 fewer VALU per two pairs but 76 VGPRs / 6 waves, it ran 7.4-7.8 ms: the loop's load latency, not
+// only its issue, counts.
+template <bool STATS, bool WIDE, bool DIAG = false, bool BF = false, bool NARROW = false, bool W8 = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W8 ? 8 : 1, 8))) void k_confidence(const float* __restrict__ depths, int N, int H, int W,
                                                     const ConfFrame* __restrict__ fr, int ref_begin, int r,
                                                     double depth_max, double d2_max, double sd,
                                                     double* __restrict__ conf, int32_t* __restrict__ valid,
@@ -920,8 +925,8 @@ int mqr_confidence(int device, const float* depths, int depth_loc, int N, int H,
         launch(k_confidence<false, false, true>, nullptr);
     } else if (bf) {
         wide ? launch(k_confidence<false, true, false, true>, nullptr)
-             : narrow ? launch(k_confidence<false, false, false, true, true>, nullptr)
-                      : launch(k_confidence<false, false, false, true>, nullptr);
+             : narrow ? launch(k_confidence<false, false, false, true, true, true>, nullptr)
+                      : launch(k_confidence<false, false, false, true, false, true>, nullptr);
     } else {
         wide ? launch(k_confidence<false, true>, nullptr) : launch(k_confidence<false, false>, nullptr);
     }

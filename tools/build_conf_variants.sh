@@ -14,6 +14,7 @@ git show ${OLD_REV:-HEAD}:metaquest-3d-reconstruction_amd/csrc/confidence.hip > 
 /opt/rocm/bin/hipcc $F -fno-slp-vectorize -DMQR_SRC_TAG=\"var-old\" -c build/var/confidence_old.hip -o build/var/c_old.o
 /opt/rocm/bin/hipcc $F -fno-slp-vectorize -DMQR_SRC_TAG=\"var-new\" -c confidence.hip -o build/var/c_new.o
 /opt/rocm/bin/hipcc $F -DMQR_SRC_TAG=\"var-slp\" -c confidence.hip -o build/var/c_slp.o
+# (the working tree's kernel carries amdgpu_waves_per_eu(8, 8) since round 4: then w8 = new)
 sed 's/__launch_bounds__(256) void k_confidence/__launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_confidence/' \
   confidence.hip > build/var/confidence_w8.hip
 grep -q "amdgpu_waves_per_eu(8, 8))) void k_confidence" build/var/confidence_w8.hip
