@@ -957,8 +957,9 @@ __device__ __forceinline__ void mc_emit_block(int64_t b, int role, const int32_t
 }
 
 // diag (A/B library, MQR_EMIT_DIAG): 1 vertices only, 2 triangles only (timing of one half, wrong output)
-// LST: workgroup i emits the i-th block with output of k_scan_counts' list (one record load)
-// instead of block i (its counts, then its offsets).
+// LST: a grid of at most 8 workgroups per CU walks k_scan_counts' list of the blocks with output
+// (one record load per block) instead of one workgroup per block (its counts, then its offsets; the
+// workgroups of blocks without output exit at once, and the launch's tail runs part-empty).
 template <int R, bool NIB = false, bool MAP = false, bool LST = false, int NT = kMcThreads>
 __global__ __launch_bounds__(NT) void k_mc_emit(const int32_t* __restrict__ nb, const uint64_t* __restrict__ bkeys,
                                                 const float2* __restrict__ pool, float voxel_size,
@@ -973,10 +974,12 @@ __global__ __launch_bounds__(NT) void k_mc_emit(const int32_t* __restrict__ nb, 
 #endif
     if constexpr (LST) {
         const int64_t nr = *nrecs;
-        const int4 rc = recs[blockIdx.x];  // (past nr: a stale record, unused)
-        if ((int64_t)blockIdx.x >= nr) return;
-        mc_emit_block<R, NT, NIB, MAP>(rc.x, diag, nb, bkeys, pool, voxel_size, rc.w & 0xffff, rc.w >> 16, rc.y, rc.z,
-                                       voff, rows4, rowNt, pos, nrm, tri, cap_v, cap_t, rowsT);
+        for (int64_t i = blockIdx.x; i < nr; i += gridDim.x) {
+            const int4 rc = recs[i];
+            mc_emit_block<R, NT, NIB, MAP>(rc.x, diag, nb, bkeys, pool, voxel_size, rc.w & 0xffff, rc.w >> 16, rc.y,
+                                           rc.z, voff, rows4, rowNt, pos, nrm, tri, cap_v, cap_t, rowsT);
+            __syncthreads();  // the block's LDS tiles are refilled by the next one
+        }
     } else {
         const int64_t b = blockIdx.x;
         const int nvb = vcount[b], ntb = tcount[b];
@@ -1449,7 +1452,14 @@ static void launch_mc_emit_t(const mqr_vbg* v, int64_t n, A... args) {
 #else
     constexpr int diag = 0;
 #endif
-    hipLaunchKernelGGL((k_mc_emit<RT, NIB, MAP, LST>), dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, args..., diag);
+    int64_t grid = n;
+    if constexpr (LST) {
+        static int cus = 0;
+        if (!cus && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, v->device) != hipSuccess) cus = 256;
+        grid = std::min<int64_t>(n, 8 * (int64_t)cus);
+    }
+    hipLaunchKernelGGL((k_mc_emit<RT, NIB, MAP, LST>), dim3((unsigned)grid), dim3(kMcThreads), 0, v->stream, args...,
+                       diag);
 }
 
 template <int RT, class... A>
