@@ -517,7 +517,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W8 ? 8 : 1,
     // measured no faster for G = 4 ... 64)
     const int rloc = blockIdx.y;
     const int ref = ref_begin + rloc;
-    const int64_t p0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+#ifndef MQR_CONF_XCD
+#define MQR_CONF_XCD 0
+#endif
+    // (MQR_CONF_XCD, A/B: workgroups go to the 8 XCDs round-robin; tile bx of a row of tiles divisible by
+    // 8 is remapped so that XCD x works on the x-th eighth of the image -- its neighbour taps then come
+    // from one band of each neighbour frame, which the XCD's own 4 MB L2 can hold)
+    unsigned bx = blockIdx.x;
+    if (MQR_CONF_XCD && (gridDim.x & 7u) == 0) bx = (bx & 7u) * (gridDim.x >> 3) + (bx >> 3);
+    const int64_t p0 = (int64_t)bx * blockDim.x + threadIdx.x;
     if (!STATS && p0 >= HW) return;  // (STATS: the wave reductions below need every lane)
     const int64_t p = p0 < HW ? p0 : HW - 1;
     const int u = (int)(p % W), v = (int)(p / W);

@@ -4,7 +4,9 @@
 #   old  the committed confidence.hip of git revision $OLD_REV (default HEAD), product flags
 #   new  the working-tree confidence.hip, product flags (-fno-slp-vectorize)
 #   slp  the working-tree confidence.hip with SLP vectorisation
-#   w8 / slpw8  new / slp with k_confidence held to 8 waves per SIMD (amdgpu_waves_per_eu(8, 8))
+#   (w8 / slpw8, new / slp held to 8 waves per SIMD, measured in round 4: the production instances now
+#   carry that attribute themselves)
+#   xcd  new with the XCD-banded tile order (MQR_CONF_XCD=1)
 set -e
 cd "$(dirname "$0")/../metaquest-3d-reconstruction_amd/csrc"
 make -s build/vbg.o build/extract.o build/ingest.o
@@ -14,13 +16,8 @@ git show ${OLD_REV:-HEAD}:metaquest-3d-reconstruction_amd/csrc/confidence.hip > 
 /opt/rocm/bin/hipcc $F -fno-slp-vectorize -DMQR_SRC_TAG=\"var-old\" -c build/var/confidence_old.hip -o build/var/c_old.o
 /opt/rocm/bin/hipcc $F -fno-slp-vectorize -DMQR_SRC_TAG=\"var-new\" -c confidence.hip -o build/var/c_new.o
 /opt/rocm/bin/hipcc $F -DMQR_SRC_TAG=\"var-slp\" -c confidence.hip -o build/var/c_slp.o
-# (the working tree's kernel carries amdgpu_waves_per_eu(8, 8) since round 4: then w8 = new)
-sed 's/__launch_bounds__(256) void k_confidence/__launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_confidence/' \
-  confidence.hip > build/var/confidence_w8.hip
-grep -q "amdgpu_waves_per_eu(8, 8))) void k_confidence" build/var/confidence_w8.hip
-/opt/rocm/bin/hipcc $F -fno-slp-vectorize -DMQR_SRC_TAG=\"var-w8\" -c build/var/confidence_w8.hip -o build/var/c_w8.o
-/opt/rocm/bin/hipcc $F -DMQR_SRC_TAG=\"var-slpw8\" -c build/var/confidence_w8.hip -o build/var/c_slpw8.o
-for v in old new slp w8 slpw8; do
+/opt/rocm/bin/hipcc $F -fno-slp-vectorize -DMQR_CONF_XCD=1 -DMQR_SRC_TAG=\"var-xcd\" -c confidence.hip -o build/var/c_xcd.o
+for v in old new slp xcd; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../../tools/_ab/libmqr_conf_$v.so \
     build/vbg.o build/extract.o build/ingest.o build/var/c_$v.o -Wl,-rpath,/opt/rocm/lib -ldl
 done
