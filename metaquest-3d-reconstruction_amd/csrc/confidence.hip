@@ -518,11 +518,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W8 ? 8 : 1,
     const int rloc = blockIdx.y;
     const int ref = ref_begin + rloc;
 #ifndef MQR_CONF_XCD
-#define MQR_CONF_XCD 0
+#define MQR_CONF_XCD 1
 #endif
-    // (MQR_CONF_XCD, A/B: workgroups go to the 8 XCDs round-robin; tile bx of a row of tiles divisible by
-    // 8 is remapped so that XCD x works on the x-th eighth of the image -- its neighbour taps then come
-    // from one band of each neighbour frame, which the XCD's own 4 MB L2 can hold)
+    // XCD bands: workgroups go to the 8 XCDs round-robin, so tile bx of a row of tiles divisible by 8 is
+    // remapped for XCD x to work on the x-th eighth of the image -- its neighbour taps then come from
+    // one band of each neighbour frame (~25 MB of window / 8), which the XCD's own 4 MB L2 can hold,
+    // instead of from the whole frames: 6.48-6.51 vs 7.01-7.10 ms, 6 alternating processes each,
+    // identical maps (profiles/r04_ab_confidence_variants.json r04r; MQR_CONF_XCD=0: the plain order)
     unsigned bx = blockIdx.x;
     if (MQR_CONF_XCD && (gridDim.x & 7u) == 0) bx = (bx & 7u) * (gridDim.x >> 3) + (bx >> 3);
     const int64_t p0 = (int64_t)bx * blockDim.x + threadIdx.x;

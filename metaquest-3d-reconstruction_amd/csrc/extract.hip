@@ -704,12 +704,27 @@ __device__ inline void mc_edge_full(const int32_t* __restrict__ nbrow, const flo
 // mc_edge_full with a fast path for an edge whose 13 taps all lie inside the block (~60 % of the
 // edges at R = 16): one base address and constant offsets instead of a 27-neighbour lookup and a
 // 64-bit address per tap -- the same values, so the same results.
+// (tsd: the block's tsdf values staged in LDS (STG) -- interior edges read their taps there)
 template <class M>
 __device__ inline void mc_edge_taps(const int32_t* __restrict__ nbrow, const float2* __restrict__ pool, int x, int y,
-                                    int z, int axis, float& t_o, float& t_e, float* no, float* ne) {
+                                    int z, int axis, float& t_o, float& t_e, float* no, float* ne,
+                                    const float* tsd = nullptr) {
     constexpr int R = M::C - 1, DY = R, DZ = R * R;
     const int ex = x + (axis == 0), ey = y + (axis == 1), ez = z + (axis == 2);
-    if (min(min(x, y), z) >= 1 && max(max(ex, ey), ez) <= R - 2) {
+    if (tsd && min(min(x, y), z) >= 1 && max(max(ex, ey), ez) <= R - 2) {
+        const float* c = tsd + (z * R + y) * R + x;
+        const float* e = c + (axis == 0 ? 1 : axis == 1 ? DY : DZ);
+        const float vxp = c[1], vxm = c[-1], vyp = c[DY], vym = c[-DY], vzp = c[DZ], vzm = c[-DZ];
+        const float wxp = e[1], wxm = e[-1], wyp = e[DY], wym = e[-DY], wzp = e[DZ], wzm = e[-DZ];
+        t_o = c[0];
+        t_e = axis == 0 ? vxp : axis == 1 ? vyp : vzp;
+        no[0] = vxp - vxm;
+        no[1] = vyp - vym;
+        no[2] = vzp - vzm;
+        ne[0] = wxp - wxm;
+        ne[1] = wyp - wym;
+        ne[2] = wzp - wzm;
+    } else if (min(min(x, y), z) >= 1 && max(max(ex, ey), ez) <= R - 2) {
         const float2* c = pool + (int64_t)nbrow[13] * M::R3 + (z * R + y) * R + x;
         const float2* e = c + (axis == 0 ? 1 : axis == 1 ? DY : DZ);
         const float vxp = c[1].x, vxm = c[-1].x, vyp = c[DY].x, vym = c[-DY].x, vzp = c[DZ].x, vzm = c[-DZ].x;
@@ -766,7 +781,8 @@ __device__ __forceinline__ int row_search(const uint4* rows, int i) {
 template <class M>
 __device__ __forceinline__ void mc_emit_vertex(int i, int lo, const uint4* rows, const int32_t* nbrow,
                                                const float2* __restrict__ pool, uint32_t pres, int xb, int yb, int zb,
-                                               float voxel_size, int32_t vb0, float* pos, float* nrm) {
+                                               float voxel_size, int32_t vb0, float* pos, float* nrm,
+                                               const float* tsd = nullptr) {
     constexpr int R = M::C - 1;
     const uint4 rw = rows[lo];
     const uint32_t ex = rw.z & 0xffffu, ey = rw.z >> 16, ez = rw.w & 0xffffu;
@@ -781,7 +797,7 @@ __device__ __forceinline__ void mc_emit_vertex(int i, int lo, const uint4* rows,
         uint32_t mm = m3;
         for (int j = 0; j < k; ++j) mm &= mm - 1;
         axis = __builtin_ctz(mm);
-        mc_edge_taps<M>(nbrow, pool, x, y, z, axis, tsdf_o, tsdf_e, no, ne);
+        mc_edge_taps<M>(nbrow, pool, x, y, z, axis, tsdf_o, tsdf_e, no, ne, tsd);
     } else {
         tsdf_o = mc_tsdf<M>(nbrow, pool, x, y, z);
         mc_normal<M>(nbrow, pool, pres, x, y, z, no);
@@ -888,7 +904,9 @@ __device__ __forceinline__ void mc_emit_tri(int i, int lo, const uint4* rows, co
 // (filled by one pass over the rows) instead of by a binary search over the row bases.
 constexpr int kRowMap = 2048;
 
-template <int R, int NT, bool NIB = false, bool MAP = false>
+// STG: a block with vertices and all 26 neighbours stages its own tsdf values in LDS (one coalesced
+// read of the block) and its interior edges read their 13 taps there instead of from the pool.
+template <int R, int NT, bool NIB = false, bool MAP = false, bool STG = false>
 __device__ __forceinline__ void mc_emit_block(int64_t b, int role, const int32_t* __restrict__ nb,
                                               const uint64_t* __restrict__ bkeys, const float2* __restrict__ pool,
                                               float voxel_size, int nvb, int ntb, int32_t vb0, int32_t tb0,
@@ -905,6 +923,7 @@ __device__ __forceinline__ void mc_emit_block(int64_t b, int role, const int32_t
     __shared__ uint32_t triC[32];
     __shared__ uint64_t tcs[NIB ? M::R2 : 1];
     __shared__ uint8_t vmap[MAP ? kRowMap : 1], tmap[MAP ? kRowMap : 1];
+    __shared__ float tsd[STG ? M::R3 : 1];
     if (nvb == 0 && ntb == 0) return;  // block-uniform: nothing to write
     // outputs past the speculative capacity: the host re-runs this pass into exact buffers
     // (int32 offsets: a total past 2^31 wraps them negative -- the host then fails the call after
@@ -918,6 +937,21 @@ __device__ __forceinline__ void mc_emit_block(int64_t b, int role, const int32_t
         if (tid < 32) triC[tid] = mqr_tri_count_packed[tid];
     }
     if (tid < 27) nbrow[tid] = nb[b * 27 + tid];
+    if constexpr (STG) {
+        if (nvb) {  // (block-uniform) the block's (tsdf, weight) pairs two at a time, all loads before the stores
+            static_assert(M::R3 % (2 * NT) == 0, "whole float4 rounds");
+            constexpr int K = M::R3 / (2 * NT);
+            const float4* src = reinterpret_cast<const float4*>(pool + b * M::R3);
+            float4 t4[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) t4[k] = src[k * NT + tid];
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                tsd[2 * (k * NT + tid)] = t4[k].x;
+                tsd[2 * (k * NT + tid) + 1] = t4[k].z;
+            }
+        }
+    }
     for (int r = tid; r < M::R2; r += NT) rows[r] = rows4[b * M::R2 + r];
     if (ntb) {
         for (int q = tid; q < M::S2; q += NT) rowN[q] = rowNt[b * M::S2 + q];
@@ -947,7 +981,7 @@ __device__ __forceinline__ void mc_emit_block(int64_t b, int role, const int32_t
         unpack_key(bkeys[b], xb, yb, zb);
         for (int i = tid; i < nvb; i += NT) {
             const int lo = vm ? (int)vmap[i] : row_search<M::R2, 0>(rows, i);
-            mc_emit_vertex<M>(i, lo, rows, nbrow, pool, pres, xb, yb, zb, voxel_size, vb0, pos, nrm);
+            mc_emit_vertex<M>(i, lo, rows, nbrow, pool, pres, xb, yb, zb, voxel_size, vb0, pos, nrm, STG ? tsd : nullptr);
         }
     }
     for (int i = tid; i < ntb; i += NT) {
@@ -957,10 +991,10 @@ __device__ __forceinline__ void mc_emit_block(int64_t b, int role, const int32_t
 }
 
 // diag (A/B library, MQR_EMIT_DIAG): 1 vertices only, 2 triangles only (timing of one half, wrong output)
-// LST: a grid of at most 8 workgroups per CU walks k_scan_counts' list of the blocks with output
-// (one record load per block) instead of one workgroup per block (its counts, then its offsets; the
-// workgroups of blocks without output exit at once, and the launch's tail runs part-empty).
-template <int R, bool NIB = false, bool MAP = false, bool LST = false, int NT = kMcThreads>
+// LST: workgroup i emits the i-th block with output of k_scan_counts' list (one record load)
+// instead of block i (its counts, then its offsets).  (A grid of at most 8 workgroups per CU walking
+// the list ran 0.206-0.208 vs 0.177-0.179 ms: the per-block chains serialised in each workgroup.)
+template <int R, bool NIB = false, bool MAP = false, bool LST = false, bool STG = false, int NT = kMcThreads>
 __global__ __launch_bounds__(NT) void k_mc_emit(const int32_t* __restrict__ nb, const uint64_t* __restrict__ bkeys,
                                                 const float2* __restrict__ pool, float voxel_size,
                                                 const int32_t* __restrict__ vcount, const int32_t* __restrict__ tcount,
@@ -974,17 +1008,15 @@ __global__ __launch_bounds__(NT) void k_mc_emit(const int32_t* __restrict__ nb, 
 #endif
     if constexpr (LST) {
         const int64_t nr = *nrecs;
-        for (int64_t i = blockIdx.x; i < nr; i += gridDim.x) {
-            const int4 rc = recs[i];
-            mc_emit_block<R, NT, NIB, MAP>(rc.x, diag, nb, bkeys, pool, voxel_size, rc.w & 0xffff, rc.w >> 16, rc.y,
-                                           rc.z, voff, rows4, rowNt, pos, nrm, tri, cap_v, cap_t, rowsT);
-            __syncthreads();  // the block's LDS tiles are refilled by the next one
-        }
+        const int4 rc = recs[blockIdx.x];  // (past nr: a stale record, unused)
+        if ((int64_t)blockIdx.x >= nr) return;
+        mc_emit_block<R, NT, NIB, MAP, STG>(rc.x, diag, nb, bkeys, pool, voxel_size, rc.w & 0xffff, rc.w >> 16, rc.y,
+                                            rc.z, voff, rows4, rowNt, pos, nrm, tri, cap_v, cap_t, rowsT);
     } else {
         const int64_t b = blockIdx.x;
         const int nvb = vcount[b], ntb = tcount[b];
         if (nvb == 0 && ntb == 0) return;
-        mc_emit_block<R, NT, NIB, MAP>(b, diag, nb, bkeys, pool, voxel_size, nvb, ntb, voff[b], toff[b], voff, rows4,
+        mc_emit_block<R, NT, NIB, MAP, STG>(b, diag, nb, bkeys, pool, voxel_size, nvb, ntb, voff[b], toff[b], voff, rows4,
                                        rowNt, pos, nrm, tri, cap_v, cap_t, rowsT);
     }
 }
@@ -1433,8 +1465,8 @@ static int build_nb(mqr_vbg* v, int32_t* nb) {
 // volume that is still being integrated.
 static int64_t spec_cap(int64_t hint) { return hint > 0 ? hint + hint / 4 + 4096 : 0; }
 
-// Extraction configuration: bit 0 = NIB (k_mc_count), bit 1 = MAP, bit 2 = LST (k_mc_emit); the A/B library
-// takes it from mqr_vbg_set_variant bits 28-30 (tools/ab_extract.py).
+// Extraction configuration: bit 0 = NIB (k_mc_count), bit 1 = MAP, bit 2 = LST, bit 3 = STG (k_mc_emit);
+// the A/B library takes it from mqr_vbg_set_extract_mode (below; tools/ab_extract.py).
 [[maybe_unused]] constexpr int kExMode = 3;  // NIB + MAP (tools/ab_extract.py)
 static int ex_mode(const mqr_vbg* v) {
 #if MQR_AB
@@ -1445,38 +1477,36 @@ static int ex_mode(const mqr_vbg* v) {
 #endif
 }
 
-template <int RT, bool NIB, bool MAP, bool LST, class... A>
+template <int RT, bool NIB, bool MAP, bool LST, bool STG, class... A>
 static void launch_mc_emit_t(const mqr_vbg* v, int64_t n, A... args) {
 #if MQR_AB  // MQR_EMIT_DIAG=1: vertices only, 2: triangles only (timing diagnostics)
     static const int diag = getenv("MQR_EMIT_DIAG") ? atoi(getenv("MQR_EMIT_DIAG")) : 0;
 #else
     constexpr int diag = 0;
 #endif
-    int64_t grid = n;
-    if constexpr (LST) {
-        static int cus = 0;
-        if (!cus && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, v->device) != hipSuccess) cus = 256;
-        grid = std::min<int64_t>(n, 8 * (int64_t)cus);
-    }
-    hipLaunchKernelGGL((k_mc_emit<RT, NIB, MAP, LST>), dim3((unsigned)grid), dim3(kMcThreads), 0, v->stream, args...,
-                       diag);
+    const int64_t grid = n;
+    hipLaunchKernelGGL((k_mc_emit<RT, NIB, MAP, LST, STG && RT == 16>), dim3((unsigned)grid), dim3(kMcThreads), 0,
+                       v->stream, args..., diag);
 }
 
 template <int RT, class... A>
 static void launch_mc_emit(const mqr_vbg* v, int64_t n, A... args) {
 #if MQR_AB
     switch (ex_mode(v)) {
-        case 1: launch_mc_emit_t<RT, true, false, false>(v, n, args...); return;
-        case 2: launch_mc_emit_t<RT, false, true, false>(v, n, args...); return;
-        case 3: launch_mc_emit_t<RT, true, true, false>(v, n, args...); return;
-        case 4: launch_mc_emit_t<RT, false, false, true>(v, n, args...); return;
-        case 5: launch_mc_emit_t<RT, true, false, true>(v, n, args...); return;
-        case 6: launch_mc_emit_t<RT, false, true, true>(v, n, args...); return;
-        case 7: launch_mc_emit_t<RT, true, true, true>(v, n, args...); return;
-        default: launch_mc_emit_t<RT, false, false, false>(v, n, args...); return;
+        case 1: launch_mc_emit_t<RT, true, false, false, false>(v, n, args...); return;
+        case 2: launch_mc_emit_t<RT, false, true, false, false>(v, n, args...); return;
+        case 3: launch_mc_emit_t<RT, true, true, false, false>(v, n, args...); return;
+        case 4: launch_mc_emit_t<RT, false, false, true, false>(v, n, args...); return;
+        case 5: launch_mc_emit_t<RT, true, false, true, false>(v, n, args...); return;
+        case 6: launch_mc_emit_t<RT, false, true, true, false>(v, n, args...); return;
+        case 7: launch_mc_emit_t<RT, true, true, true, false>(v, n, args...); return;
+        case 8: launch_mc_emit_t<RT, false, false, false, true>(v, n, args...); return;
+        case 11: launch_mc_emit_t<RT, true, true, false, true>(v, n, args...); return;
+        case 15: launch_mc_emit_t<RT, true, true, true, true>(v, n, args...); return;
+        default: launch_mc_emit_t<RT, false, false, false, false>(v, n, args...); return;
     }
 #else
-    launch_mc_emit_t<RT, (kExMode & 1) != 0, (kExMode & 2) != 0, (kExMode & 4) != 0>(v, n, args...);
+    launch_mc_emit_t<RT, (kExMode & 1) != 0, (kExMode & 2) != 0, (kExMode & 4) != 0, (kExMode & 8) != 0>(v, n, args...);
 #endif
 }
 
@@ -1617,6 +1647,15 @@ using namespace mqr;
 extern "C" {
 
 int mqr_extract_mesh(mqr_vbg* v, float thr, mqr_geom** out) { return mqr_extract_mesh_owned(v, thr, -1, out); }
+
+#if MQR_AB
+// A/B library only: the extraction configuration (kExMode bits) for tools/ab_extract.py.
+int mqr_vbg_set_extract_mode(mqr_vbg* v, int mode) {
+    MQR_REQUIRE(v && mode >= 0 && mode < 16, "bad extraction mode");
+    v->ex_mode = mode;
+    return 0;
+}
+#endif
 
 int mqr_extract_mesh_owned(mqr_vbg* v, float thr, int64_t n_owned, mqr_geom** out) {
     MQR_REQUIRE(v && out, "null argument");

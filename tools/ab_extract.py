@@ -2,10 +2,11 @@
 """Interleaved A/B of extract_triangle_mesh configurations on the bench volume (C2, one process).
 
 python tools/ab_extract.py --modes 0 --reps 15
-mode = value of mqr_vbg_set_variant bits 28-30 for an extraction configuration under test, A/B
-library only (extract.hip kExMode): bit 0 per-cube triangle counts from the count pass, bit 1 LDS row
+mode = an extraction configuration under test (mqr_vbg_set_extract_mode, A/B library only; the
+product library runs mode 0 = its kExMode, extract.hip): bit 0 per-cube triangle counts from the count pass, bit 1 LDS row
 maps in the emission pass (both = 3, the library default), bit 2 emission over a compacted list of
-the blocks with output (round 4 also measured the count pass emitting the vertices, 0.264 vs 0.237 ms, and a
+the blocks with output, bit 3 the block's
+tsdf staged in LDS for its interior vertex taps (round 4 also measured the count pass emitting the vertices, 0.264 vs 0.237 ms, and a
 vertex and a triangle workgroup per block, 0.187 vs 0.179 ms, removed) (round 3
 measured a merged vertex / triangle item loop and 512-thread emission blocks this way: no change,
 profiles/r03_ab_integrate_windows.json; neither is in the library now).
@@ -43,11 +44,15 @@ def main():
                          seq["T_wc"].astype(np.float64), depth_scale=1.0, depth_max=4.0, trunc_voxel_multiplier=10.0)
     torch.cuda.synchronize()
     modes = [int(x) for x in a.modes.split(",")]
+    ab = getattr(_lib.load(), "mqr_vbg_set_extract_mode", None) is not None
     times = {m: [] for m in modes}
     outs = {}
     for r in range(a.reps + 1):
         for m in modes:
-            _lib.call("mqr_vbg_set_variant", vbg.handle, m << 28)
+            if ab:
+                _lib.call("mqr_vbg_set_extract_mode", vbg.handle, m)
+            elif m:
+                raise SystemExit("extraction modes other than 0 need the A/B library (MQR_HIP_LIB=tools/_ab/libmqr_ab.so)")
             g = ctypes.c_void_p()
             t0 = time.perf_counter()
             _lib.call("mqr_extract_mesh", vbg.handle, float(a.threshold), ctypes.byref(g))

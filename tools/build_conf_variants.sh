@@ -6,7 +6,7 @@
 #   slp  the working-tree confidence.hip with SLP vectorisation
 #   (w8 / slpw8, new / slp held to 8 waves per SIMD, measured in round 4: the production instances now
 #   carry that attribute themselves)
-#   xcd  new with the XCD-banded tile order (MQR_CONF_XCD=1)
+#   xcd  new with the XCD-banded tile order (MQR_CONF_XCD=1, the default since round 4), plain: =0
 set -e
 cd "$(dirname "$0")/../metaquest-3d-reconstruction_amd/csrc"
 make -s build/vbg.o build/extract.o build/ingest.o
@@ -17,7 +17,8 @@ git show ${OLD_REV:-HEAD}:metaquest-3d-reconstruction_amd/csrc/confidence.hip > 
 /opt/rocm/bin/hipcc $F -fno-slp-vectorize -DMQR_SRC_TAG=\"var-new\" -c confidence.hip -o build/var/c_new.o
 /opt/rocm/bin/hipcc $F -DMQR_SRC_TAG=\"var-slp\" -c confidence.hip -o build/var/c_slp.o
 /opt/rocm/bin/hipcc $F -fno-slp-vectorize -DMQR_CONF_XCD=1 -DMQR_SRC_TAG=\"var-xcd\" -c confidence.hip -o build/var/c_xcd.o
-for v in old new slp xcd; do
+/opt/rocm/bin/hipcc $F -fno-slp-vectorize -DMQR_CONF_XCD=0 -DMQR_SRC_TAG=\"var-plain\" -c confidence.hip -o build/var/c_plain.o
+for v in old new slp xcd plain; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../../tools/_ab/libmqr_conf_$v.so \
     build/vbg.o build/extract.o build/ingest.o build/var/c_$v.o -Wl,-rpath,/opt/rocm/lib -ldl
 done
