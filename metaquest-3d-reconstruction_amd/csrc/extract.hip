@@ -615,8 +615,16 @@ __device__ inline int mc_row_tris(const uint32_t* rowN, uint32_t oc, int y, int 
 // (owned crossing edges and owned surface cubes of the row) and the sign rows rowNt[b][q] of the
 // block's [-1, R]^3 tile (cube indices).  Emission of this block and of its -x / -y / -z
 // neighbours (triangles referencing vertices this block owns) read these instead of rebuilding them.
+// XCD bands (XB): workgroups go to the 8 XCDs round-robin; workgroup i takes block xcd_band(i) so
+// that XCD x works on the x-th eighth of the pool (blocks allocated together -- often neighbours --
+// then share that XCD's L2 for their neighbours' planes, row records and taps).
+__device__ inline int64_t xcd_band(int64_t i, int64_t n) {
+    const int64_t q = n >> 3, r = n & 7, x = i & 7;
+    return x * q + min(x, r) + (i >> 3);
+}
+
 // NIB: also the rows' per-cube triangle counts (rowsT[b][row], mc_row_tris) for the emission pass.
-template <int R, bool NIB = false>
+template <int R, bool NIB = false, bool XB = false>
 __global__ __launch_bounds__(kMcThreads) void k_mc_count(const int32_t* __restrict__ nb, const uint16_t* __restrict__ bits,
                                                          int64_t tri_blocks, int32_t* vcount, int32_t* tcount,
                                                          uint4* __restrict__ rows4, uint32_t* __restrict__ rowNt,
@@ -625,7 +633,7 @@ __global__ __launch_bounds__(kMcThreads) void k_mc_count(const int32_t* __restri
     __shared__ uint32_t rowV[M::S2], rowN[M::S2], cs[M::C2];
     __shared__ int32_t nbrow[27];
     __shared__ int scratch[16];
-    const int64_t b = blockIdx.x;
+    const int64_t b = XB ? xcd_band(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
     if (threadIdx.x < 27) nbrow[threadIdx.x] = nb[b * 27 + threadIdx.x];
     __syncthreads();
     mc_stage_bits<M>(nbrow, bits, rowV, rowN, nullptr);
@@ -994,7 +1002,8 @@ __device__ __forceinline__ void mc_emit_block(int64_t b, int role, const int32_t
 // LST: workgroup i emits the i-th block with output of k_scan_counts' list (one record load)
 // instead of block i (its counts, then its offsets).  (A grid of at most 8 workgroups per CU walking
 // the list ran 0.206-0.208 vs 0.177-0.179 ms: the per-block chains serialised in each workgroup.)
-template <int R, bool NIB = false, bool MAP = false, bool LST = false, bool STG = false, int NT = kMcThreads>
+template <int R, bool NIB = false, bool MAP = false, bool LST = false, bool STG = false, bool XB = false,
+          int NT = kMcThreads>
 __global__ __launch_bounds__(NT) void k_mc_emit(const int32_t* __restrict__ nb, const uint64_t* __restrict__ bkeys,
                                                 const float2* __restrict__ pool, float voxel_size,
                                                 const int32_t* __restrict__ vcount, const int32_t* __restrict__ tcount,
@@ -1013,7 +1022,7 @@ __global__ __launch_bounds__(NT) void k_mc_emit(const int32_t* __restrict__ nb, 
         mc_emit_block<R, NT, NIB, MAP, STG>(rc.x, diag, nb, bkeys, pool, voxel_size, rc.w & 0xffff, rc.w >> 16, rc.y,
                                             rc.z, voff, rows4, rowNt, pos, nrm, tri, cap_v, cap_t, rowsT);
     } else {
-        const int64_t b = blockIdx.x;
+        const int64_t b = XB ? xcd_band(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
         const int nvb = vcount[b], ntb = tcount[b];
         if (nvb == 0 && ntb == 0) return;
         mc_emit_block<R, NT, NIB, MAP, STG>(b, diag, nb, bkeys, pool, voxel_size, nvb, ntb, voff[b], toff[b], voff, rows4,
@@ -1465,7 +1474,8 @@ static int build_nb(mqr_vbg* v, int32_t* nb) {
 // volume that is still being integrated.
 static int64_t spec_cap(int64_t hint) { return hint > 0 ? hint + hint / 4 + 4096 : 0; }
 
-// Extraction configuration: bit 0 = NIB (k_mc_count), bit 1 = MAP, bit 2 = LST, bit 3 = STG (k_mc_emit);
+// Extraction configuration: bit 0 = NIB (k_mc_count), bit 1 = MAP, bit 2 = LST, bit 3 = STG (k_mc_emit),
+// bit 4 = XB (XCD bands of the pool in k_mc_count and k_mc_emit);
 // the A/B library takes it from mqr_vbg_set_extract_mode (below; tools/ab_extract.py).
 [[maybe_unused]] constexpr int kExMode = 3;  // NIB + MAP (tools/ab_extract.py)
 static int ex_mode(const mqr_vbg* v) {
@@ -1477,7 +1487,7 @@ static int ex_mode(const mqr_vbg* v) {
 #endif
 }
 
-template <int RT, bool NIB, bool MAP, bool LST, bool STG, class... A>
+template <int RT, bool NIB, bool MAP, bool LST, bool STG, bool XB, class... A>
 static void launch_mc_emit_t(const mqr_vbg* v, int64_t n, A... args) {
 #if MQR_AB  // MQR_EMIT_DIAG=1: vertices only, 2: triangles only (timing diagnostics)
     static const int diag = getenv("MQR_EMIT_DIAG") ? atoi(getenv("MQR_EMIT_DIAG")) : 0;
@@ -1485,7 +1495,7 @@ static void launch_mc_emit_t(const mqr_vbg* v, int64_t n, A... args) {
     constexpr int diag = 0;
 #endif
     const int64_t grid = n;
-    hipLaunchKernelGGL((k_mc_emit<RT, NIB, MAP, LST, STG && RT == 16>), dim3((unsigned)grid), dim3(kMcThreads), 0,
+    hipLaunchKernelGGL((k_mc_emit<RT, NIB, MAP, LST, STG && RT == 16, XB>), dim3((unsigned)grid), dim3(kMcThreads), 0,
                        v->stream, args..., diag);
 }
 
@@ -1493,20 +1503,23 @@ template <int RT, class... A>
 static void launch_mc_emit(const mqr_vbg* v, int64_t n, A... args) {
 #if MQR_AB
     switch (ex_mode(v)) {
-        case 1: launch_mc_emit_t<RT, true, false, false, false>(v, n, args...); return;
-        case 2: launch_mc_emit_t<RT, false, true, false, false>(v, n, args...); return;
-        case 3: launch_mc_emit_t<RT, true, true, false, false>(v, n, args...); return;
-        case 4: launch_mc_emit_t<RT, false, false, true, false>(v, n, args...); return;
-        case 5: launch_mc_emit_t<RT, true, false, true, false>(v, n, args...); return;
-        case 6: launch_mc_emit_t<RT, false, true, true, false>(v, n, args...); return;
-        case 7: launch_mc_emit_t<RT, true, true, true, false>(v, n, args...); return;
-        case 8: launch_mc_emit_t<RT, false, false, false, true>(v, n, args...); return;
-        case 11: launch_mc_emit_t<RT, true, true, false, true>(v, n, args...); return;
-        case 15: launch_mc_emit_t<RT, true, true, true, true>(v, n, args...); return;
-        default: launch_mc_emit_t<RT, false, false, false, false>(v, n, args...); return;
+        case 1: launch_mc_emit_t<RT, true, false, false, false, false>(v, n, args...); return;
+        case 2: launch_mc_emit_t<RT, false, true, false, false, false>(v, n, args...); return;
+        case 3: launch_mc_emit_t<RT, true, true, false, false, false>(v, n, args...); return;
+        case 4: launch_mc_emit_t<RT, false, false, true, false, false>(v, n, args...); return;
+        case 5: launch_mc_emit_t<RT, true, false, true, false, false>(v, n, args...); return;
+        case 6: launch_mc_emit_t<RT, false, true, true, false, false>(v, n, args...); return;
+        case 7: launch_mc_emit_t<RT, true, true, true, false, false>(v, n, args...); return;
+        case 8: launch_mc_emit_t<RT, false, false, false, true, false>(v, n, args...); return;
+        case 11: launch_mc_emit_t<RT, true, true, false, true, false>(v, n, args...); return;
+        case 15: launch_mc_emit_t<RT, true, true, true, true, false>(v, n, args...); return;
+        case 19: launch_mc_emit_t<RT, true, true, false, false, true>(v, n, args...); return;
+        case 27: launch_mc_emit_t<RT, true, true, false, true, true>(v, n, args...); return;
+        default: launch_mc_emit_t<RT, false, false, false, false, false>(v, n, args...); return;
     }
 #else
-    launch_mc_emit_t<RT, (kExMode & 1) != 0, (kExMode & 2) != 0, (kExMode & 4) != 0, (kExMode & 8) != 0>(v, n, args...);
+    launch_mc_emit_t<RT, (kExMode & 1) != 0, (kExMode & 2) != 0, (kExMode & 4) != 0, (kExMode & 8) != 0,
+                     (kExMode & 16) != 0>(v, n, args...);
 #endif
 }
 
@@ -1523,12 +1536,15 @@ static int mesh_passes(mqr_vbg* v, float thr, const ExScratch& e, mqr_geom* g, i
         int64_t* tot = reinterpret_cast<int64_t*>(e.tmp);
         hipLaunchKernelGGL(k_mc_bits<RT>, dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, v->pool, thr, e.bits,
                            v->bkeys, v->tab, e.nb);
-        if (ex_mode(v) & 1)
-            hipLaunchKernelGGL((k_mc_count<RT, true>), dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, e.nb, e.bits,
-                               tri_blocks, e.c0, e.c1, rows4, rowNt, rowsT);
+        if ((ex_mode(v) & 17) == 17)
+            hipLaunchKernelGGL((k_mc_count<RT, true, true>), dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, e.nb,
+                               e.bits, tri_blocks, e.c0, e.c1, rows4, rowNt, rowsT);
+        else if (ex_mode(v) & 1)
+            hipLaunchKernelGGL((k_mc_count<RT, true, false>), dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, e.nb,
+                               e.bits, tri_blocks, e.c0, e.c1, rows4, rowNt, rowsT);
         else
-            hipLaunchKernelGGL((k_mc_count<RT, false>), dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, e.nb, e.bits,
-                               tri_blocks, e.c0, e.c1, rows4, rowNt, rowsT);
+            hipLaunchKernelGGL((k_mc_count<RT, false, false>), dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, e.nb,
+                               e.bits, tri_blocks, e.c0, e.c1, rows4, rowNt, rowsT);
         if (ex_mode(v) & 4)
             hipLaunchKernelGGL(k_scan_counts<true>, dim3(1), dim3(kScanThreads), 0, v->stream, e.c0, e.c1, n, e.o0,
                                e.o1, tot, recs);
@@ -1651,7 +1667,7 @@ int mqr_extract_mesh(mqr_vbg* v, float thr, mqr_geom** out) { return mqr_extract
 #if MQR_AB
 // A/B library only: the extraction configuration (kExMode bits) for tools/ab_extract.py.
 int mqr_vbg_set_extract_mode(mqr_vbg* v, int mode) {
-    MQR_REQUIRE(v && mode >= 0 && mode < 16, "bad extraction mode");
+    MQR_REQUIRE(v && mode >= 0 && mode < 32, "bad extraction mode");
     v->ex_mode = mode;
     return 0;
 }
