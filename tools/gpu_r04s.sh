@@ -7,8 +7,8 @@ cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest tests/test_gpu_confidence.py -x -q --timeout 240 --timeout-method thread > gpurun_out/r04s_tests.log 2>&1 || { tail -30 gpurun_out/r04s_tests.log; exit 1; }
 tail -1 gpurun_out/r04s_tests.log
-MQR_HIP_LIB="$PWD/tools/_ab/libmqr_ab.so" timeout -k 10 300 python -u tools/ab_extract.py --modes 3,11 --reps 21 > gpurun_out/r04s_ab1.json 2> gpurun_out/r04s_ab.err &&
-MQR_HIP_LIB="$PWD/tools/_ab/libmqr_ab.so" timeout -k 10 300 python -u tools/ab_extract.py --modes 11,3 --reps 21 > gpurun_out/r04s_ab2.json 2>> gpurun_out/r04s_ab.err || { tail -20 gpurun_out/r04s_ab.err; exit 1; }
+MQR_HIP_LIB="$PWD/tools/_ab/libmqr_ab.so" timeout -k 10 300 python -u tools/ab_extract.py --modes 3,11,19,27 --reps 21 > gpurun_out/r04s_ab1.json 2> gpurun_out/r04s_ab.err &&
+MQR_HIP_LIB="$PWD/tools/_ab/libmqr_ab.so" timeout -k 10 300 python -u tools/ab_extract.py --modes 27,19,11,3 --reps 21 > gpurun_out/r04s_ab2.json 2>> gpurun_out/r04s_ab.err || { tail -20 gpurun_out/r04s_ab.err; exit 1; }
 cat gpurun_out/r04s_ab1.json gpurun_out/r04s_ab2.json
 MQR_HIP_LIB="$PWD/tools/_ab/libmqr_ab.so" timeout -k 10 400 python -u tools/ab_integrate.py --variants 0,0x8000 --rounds 5 --check > gpurun_out/r04s_int.json 2> gpurun_out/r04s_int.err || { tail -20 gpurun_out/r04s_int.err; exit 1; }
 tail -5 gpurun_out/r04s_int.json
