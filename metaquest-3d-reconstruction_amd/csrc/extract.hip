@@ -615,16 +615,8 @@ __device__ inline int mc_row_tris(const uint32_t* rowN, uint32_t oc, int y, int 
 // (owned crossing edges and owned surface cubes of the row) and the sign rows rowNt[b][q] of the
 // block's [-1, R]^3 tile (cube indices).  Emission of this block and of its -x / -y / -z
 // neighbours (triangles referencing vertices this block owns) read these instead of rebuilding them.
-// XCD bands (XB): workgroups go to the 8 XCDs round-robin; workgroup i takes block xcd_band(i) so
-// that XCD x works on the x-th eighth of the pool (blocks allocated together -- often neighbours --
-// then share that XCD's L2 for their neighbours' planes, row records and taps).
-__device__ inline int64_t xcd_band(int64_t i, int64_t n) {
-    const int64_t q = n >> 3, r = n & 7, x = i & 7;
-    return x * q + min(x, r) + (i >> 3);
-}
-
 // NIB: also the rows' per-cube triangle counts (rowsT[b][row], mc_row_tris) for the emission pass.
-template <int R, bool NIB = false, bool XB = false>
+template <int R, bool NIB = false>
 __global__ __launch_bounds__(kMcThreads) void k_mc_count(const int32_t* __restrict__ nb, const uint16_t* __restrict__ bits,
                                                          int64_t tri_blocks, int32_t* vcount, int32_t* tcount,
                                                          uint4* __restrict__ rows4, uint32_t* __restrict__ rowNt,
@@ -633,7 +625,7 @@ __global__ __launch_bounds__(kMcThreads) void k_mc_count(const int32_t* __restri
     __shared__ uint32_t rowV[M::S2], rowN[M::S2], cs[M::C2];
     __shared__ int32_t nbrow[27];
     __shared__ int scratch[16];
-    const int64_t b = XB ? xcd_band(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
+    const int64_t b = blockIdx.x;
     if (threadIdx.x < 27) nbrow[threadIdx.x] = nb[b * 27 + threadIdx.x];
     __syncthreads();
     mc_stage_bits<M>(nbrow, bits, rowV, rowN, nullptr);
@@ -712,27 +704,12 @@ __device__ inline void mc_edge_full(const int32_t* __restrict__ nbrow, const flo
 // mc_edge_full with a fast path for an edge whose 13 taps all lie inside the block (~60 % of the
 // edges at R = 16): one base address and constant offsets instead of a 27-neighbour lookup and a
 // 64-bit address per tap -- the same values, so the same results.
-// (tsd: the block's tsdf values staged in LDS (STG) -- interior edges read their taps there)
 template <class M>
 __device__ inline void mc_edge_taps(const int32_t* __restrict__ nbrow, const float2* __restrict__ pool, int x, int y,
-                                    int z, int axis, float& t_o, float& t_e, float* no, float* ne,
-                                    const float* tsd = nullptr) {
+                                    int z, int axis, float& t_o, float& t_e, float* no, float* ne) {
     constexpr int R = M::C - 1, DY = R, DZ = R * R;
     const int ex = x + (axis == 0), ey = y + (axis == 1), ez = z + (axis == 2);
-    if (tsd && min(min(x, y), z) >= 1 && max(max(ex, ey), ez) <= R - 2) {
-        const float* c = tsd + (z * R + y) * R + x;
-        const float* e = c + (axis == 0 ? 1 : axis == 1 ? DY : DZ);
-        const float vxp = c[1], vxm = c[-1], vyp = c[DY], vym = c[-DY], vzp = c[DZ], vzm = c[-DZ];
-        const float wxp = e[1], wxm = e[-1], wyp = e[DY], wym = e[-DY], wzp = e[DZ], wzm = e[-DZ];
-        t_o = c[0];
-        t_e = axis == 0 ? vxp : axis == 1 ? vyp : vzp;
-        no[0] = vxp - vxm;
-        no[1] = vyp - vym;
-        no[2] = vzp - vzm;
-        ne[0] = wxp - wxm;
-        ne[1] = wyp - wym;
-        ne[2] = wzp - wzm;
-    } else if (min(min(x, y), z) >= 1 && max(max(ex, ey), ez) <= R - 2) {
+    if (min(min(x, y), z) >= 1 && max(max(ex, ey), ez) <= R - 2) {
         const float2* c = pool + (int64_t)nbrow[13] * M::R3 + (z * R + y) * R + x;
         const float2* e = c + (axis == 0 ? 1 : axis == 1 ? DY : DZ);
         const float vxp = c[1].x, vxm = c[-1].x, vyp = c[DY].x, vym = c[-DY].x, vzp = c[DZ].x, vzm = c[-DZ].x;
@@ -789,8 +766,7 @@ __device__ __forceinline__ int row_search(const uint4* rows, int i) {
 template <class M>
 __device__ __forceinline__ void mc_emit_vertex(int i, int lo, const uint4* rows, const int32_t* nbrow,
                                                const float2* __restrict__ pool, uint32_t pres, int xb, int yb, int zb,
-                                               float voxel_size, int32_t vb0, float* pos, float* nrm,
-                                               const float* tsd = nullptr) {
+                                               float voxel_size, int32_t vb0, float* pos, float* nrm) {
     constexpr int R = M::C - 1;
     const uint4 rw = rows[lo];
     const uint32_t ex = rw.z & 0xffffu, ey = rw.z >> 16, ez = rw.w & 0xffffu;
@@ -805,7 +781,7 @@ __device__ __forceinline__ void mc_emit_vertex(int i, int lo, const uint4* rows,
         uint32_t mm = m3;
         for (int j = 0; j < k; ++j) mm &= mm - 1;
         axis = __builtin_ctz(mm);
-        mc_edge_taps<M>(nbrow, pool, x, y, z, axis, tsdf_o, tsdf_e, no, ne, tsd);
+        mc_edge_taps<M>(nbrow, pool, x, y, z, axis, tsdf_o, tsdf_e, no, ne);
     } else {
         tsdf_o = mc_tsdf<M>(nbrow, pool, x, y, z);
         mc_normal<M>(nbrow, pool, pres, x, y, z, no);
@@ -912,13 +888,12 @@ __device__ __forceinline__ void mc_emit_tri(int i, int lo, const uint4* rows, co
 // (filled by one pass over the rows) instead of by a binary search over the row bases.
 constexpr int kRowMap = 2048;
 
-// STG: a block with vertices and all 26 neighbours stages its own tsdf values in LDS (one coalesced
-// read of the block) and its interior edges read their 13 taps there instead of from the pool.
-template <int R, int NT, bool NIB = false, bool MAP = false, bool STG = false>
+template <int R, int NT, bool NIB = false, bool MAP = false>
 __device__ __forceinline__ void mc_emit_block(int64_t b, int role, const int32_t* __restrict__ nb,
                                               const uint64_t* __restrict__ bkeys, const float2* __restrict__ pool,
-                                              float voxel_size, int nvb, int ntb, int32_t vb0, int32_t tb0,
-                                              const int32_t* __restrict__ voff, const uint4* __restrict__ rows4,
+                                              float voxel_size, const int32_t* __restrict__ vcount,
+                                              const int32_t* __restrict__ tcount, const int32_t* __restrict__ voff,
+                                              const int32_t* __restrict__ toff, const uint4* __restrict__ rows4,
                                               const uint32_t* __restrict__ rowNt, float* pos, float* nrm, int32_t* tri,
                                               int64_t cap_v, int64_t cap_t, const uint64_t* __restrict__ rowsT) {
     using M = Mc<R, 1>;
@@ -931,35 +906,19 @@ __device__ __forceinline__ void mc_emit_block(int64_t b, int role, const int32_t
     __shared__ uint32_t triC[32];
     __shared__ uint64_t tcs[NIB ? M::R2 : 1];
     __shared__ uint8_t vmap[MAP ? kRowMap : 1], tmap[MAP ? kRowMap : 1];
-    __shared__ float tsd[STG ? M::R3 : 1];
+    const int nvb = role == 2 ? 0 : vcount[b], ntb = role == 1 ? 0 : tcount[b];
     if (nvb == 0 && ntb == 0) return;  // block-uniform: nothing to write
+    const int32_t vb0 = voff[b], tb0 = toff[b];
     // outputs past the speculative capacity: the host re-runs this pass into exact buffers
     // (int32 offsets: a total past 2^31 wraps them negative -- the host then fails the call after
     // this speculative pass, which must not have written before the buffers' start)
-    if (vb0 < 0 || tb0 < 0 || (int64_t)vb0 + nvb > cap_v || (int64_t)tb0 + ntb > cap_t) return;
-    if (role == 1) ntb = 0;
-    if (role == 2) nvb = 0;
+    if (vb0 < 0 || tb0 < 0 || (int64_t)vb0 + vcount[b] > cap_v || (int64_t)tb0 + tcount[b] > cap_t) return;
     const int tid = threadIdx.x;
     if (ntb) {
         if (tid < 256) triP[tid] = mqr_tri_packed[tid];
         if (tid < 32) triC[tid] = mqr_tri_count_packed[tid];
     }
     if (tid < 27) nbrow[tid] = nb[b * 27 + tid];
-    if constexpr (STG) {
-        if (nvb) {  // (block-uniform) the block's (tsdf, weight) pairs two at a time, all loads before the stores
-            static_assert(M::R3 % (2 * NT) == 0, "whole float4 rounds");
-            constexpr int K = M::R3 / (2 * NT);
-            const float4* src = reinterpret_cast<const float4*>(pool + b * M::R3);
-            float4 t4[K];
-#pragma unroll
-            for (int k = 0; k < K; ++k) t4[k] = src[k * NT + tid];
-#pragma unroll
-            for (int k = 0; k < K; ++k) {
-                tsd[2 * (k * NT + tid)] = t4[k].x;
-                tsd[2 * (k * NT + tid) + 1] = t4[k].z;
-            }
-        }
-    }
     for (int r = tid; r < M::R2; r += NT) rows[r] = rows4[b * M::R2 + r];
     if (ntb) {
         for (int q = tid; q < M::S2; q += NT) rowN[q] = rowNt[b * M::S2 + q];
@@ -989,7 +948,7 @@ __device__ __forceinline__ void mc_emit_block(int64_t b, int role, const int32_t
         unpack_key(bkeys[b], xb, yb, zb);
         for (int i = tid; i < nvb; i += NT) {
             const int lo = vm ? (int)vmap[i] : row_search<M::R2, 0>(rows, i);
-            mc_emit_vertex<M>(i, lo, rows, nbrow, pool, pres, xb, yb, zb, voxel_size, vb0, pos, nrm, STG ? tsd : nullptr);
+            mc_emit_vertex<M>(i, lo, rows, nbrow, pool, pres, xb, yb, zb, voxel_size, vb0, pos, nrm);
         }
     }
     for (int i = tid; i < ntb; i += NT) {
@@ -999,35 +958,19 @@ __device__ __forceinline__ void mc_emit_block(int64_t b, int role, const int32_t
 }
 
 // diag (A/B library, MQR_EMIT_DIAG): 1 vertices only, 2 triangles only (timing of one half, wrong output)
-// LST: workgroup i emits the i-th block with output of k_scan_counts' list (one record load)
-// instead of block i (its counts, then its offsets).  (A grid of at most 8 workgroups per CU walking
-// the list ran 0.206-0.208 vs 0.177-0.179 ms: the per-block chains serialised in each workgroup.)
-template <int R, bool NIB = false, bool MAP = false, bool LST = false, bool STG = false, bool XB = false,
-          int NT = kMcThreads>
+template <int R, bool NIB = false, bool MAP = false, int NT = kMcThreads>
 __global__ __launch_bounds__(NT) void k_mc_emit(const int32_t* __restrict__ nb, const uint64_t* __restrict__ bkeys,
                                                 const float2* __restrict__ pool, float voxel_size,
                                                 const int32_t* __restrict__ vcount, const int32_t* __restrict__ tcount,
                                                 const int32_t* __restrict__ voff, const int32_t* __restrict__ toff,
                                                 const uint4* __restrict__ rows4, const uint32_t* __restrict__ rowNt,
                                                 float* pos, float* nrm, int32_t* tri, int64_t cap_v, int64_t cap_t,
-                                                const uint64_t* __restrict__ rowsT, const int4* __restrict__ recs,
-                                                const int64_t* __restrict__ nrecs, int diag = 0) {
+                                                const uint64_t* __restrict__ rowsT, int diag = 0) {
 #if !MQR_AB
     diag = 0;
 #endif
-    if constexpr (LST) {
-        const int64_t nr = *nrecs;
-        const int4 rc = recs[blockIdx.x];  // (past nr: a stale record, unused)
-        if ((int64_t)blockIdx.x >= nr) return;
-        mc_emit_block<R, NT, NIB, MAP, STG>(rc.x, diag, nb, bkeys, pool, voxel_size, rc.w & 0xffff, rc.w >> 16, rc.y,
-                                            rc.z, voff, rows4, rowNt, pos, nrm, tri, cap_v, cap_t, rowsT);
-    } else {
-        const int64_t b = XB ? xcd_band(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
-        const int nvb = vcount[b], ntb = tcount[b];
-        if (nvb == 0 && ntb == 0) return;
-        mc_emit_block<R, NT, NIB, MAP, STG>(b, diag, nb, bkeys, pool, voxel_size, nvb, ntb, voff[b], toff[b], voff, rows4,
-                                       rowNt, pos, nrm, tri, cap_v, cap_t, rowsT);
-    }
+    mc_emit_block<R, NT, NIB, MAP>(blockIdx.x, diag, nb, bkeys, pool, voxel_size, vcount, tcount, voff, toff, rows4,
+                                   rowNt, pos, nrm, tri, cap_v, cap_t, rowsT);
 }
 
 
@@ -1039,24 +982,15 @@ __global__ __launch_bounds__(NT) void k_mc_emit(const int32_t* __restrict__ nb, 
 // thread scans kScanPer consecutive counts, wave and workgroup scans of the thread sums; results
 // back through LDS to coalesced stores; a running carry between tiles.
 constexpr int kScanThreads = 1024, kScanPer = 8, kScanTile = kScanThreads * kScanPer;
-// LST (A/B mode, with c1): also the blocks with output in block order, {block, o0, o1, c0 | c1 << 16}
-// (per-block counts < 2^16 at R <= 16), their number in totals[2] -- the emission pass's grid reads
-// one record per workgroup instead of the counts, then the offsets, of every block.  (A template
-// parameter: the list's third scan, compiled into every launch, made the kernel 5.4 -> 11.7 us.)
-template <bool LST = false>
 __global__ __launch_bounds__(kScanThreads) void k_scan_counts(const int32_t* __restrict__ c0,
                                                               const int32_t* __restrict__ c1, int64_t n,
                                                               int32_t* __restrict__ o0, int32_t* __restrict__ o1,
-                                                              int64_t* __restrict__ totals,
-                                                              int4* __restrict__ recs) {
+                                                              int64_t* __restrict__ totals) {
     __shared__ int32_t t0[kScanTile], t1[kScanTile];
     __shared__ int64_t ws0[kScanThreads / 64], ws1[kScanThreads / 64];
-    __shared__ int32_t ws2[LST ? kScanThreads / 64 : 1];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const bool two = c1 != nullptr;
-    constexpr bool lst = LST;
     int64_t carry0 = 0, carry1 = 0;
-    int32_t carry2 = 0;
     for (int64_t base = 0; base < n; base += kScanTile) {
         int32_t v0[kScanPer], v1[kScanPer];
 #pragma unroll
@@ -1072,54 +1006,40 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_counts(const int32_t* __r
         }
         __syncthreads();
         int64_t s0 = 0, s1 = 0;
-        int32_t s2 = 0;  // blocks with output (LST)
 #pragma unroll
         for (int k = 0; k < kScanPer; ++k) {
-            const int32_t a = t0[tid * kScanPer + k], b = t1[tid * kScanPer + k];
-            s0 += a;
-            s1 += b;
-            if constexpr (LST) s2 += (a | b) != 0;
+            s0 += t0[tid * kScanPer + k];
+            s1 += t1[tid * kScanPer + k];
         }
         int64_t i0 = s0, i1 = s1;  // inclusive wave scans of the thread sums
-        int32_t i2 = s2;
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
             const int64_t a = __shfl_up(i0, d, 64), b = __shfl_up(i1, d, 64);
-            int32_t c = 0;
-            if constexpr (LST) c = __shfl_up(i2, d, 64);
             if (lane >= d) {
                 i0 += a;
                 i1 += b;
-                if constexpr (LST) i2 += c;
             }
         }
         if (lane == 63) {
             ws0[wave] = i0;
             ws1[wave] = i1;
-            if constexpr (LST) ws2[wave] = i2;
         }
         __syncthreads();
         int64_t b0 = carry0, b1 = carry1, tot0 = 0, tot1 = 0;
-        int32_t b2 = carry2, tot2 = 0;
         for (int w = 0; w < kScanThreads / 64; ++w) {
             if (w < wave) {
                 b0 += ws0[w];
                 b1 += ws1[w];
-                if constexpr (LST) b2 += ws2[w];
             }
             tot0 += ws0[w];
             tot1 += ws1[w];
-            if constexpr (LST) tot2 += ws2[w];
         }
         int64_t r0 = b0 + i0 - s0, r1 = b1 + i1 - s1;  // exclusive prefix of this thread's counts
-        int32_t r2 = b2 + i2 - s2;
 #pragma unroll
         for (int k = 0; k < kScanPer; ++k) {
             const int32_t a = t0[tid * kScanPer + k], b = t1[tid * kScanPer + k];
             t0[tid * kScanPer + k] = (int32_t)r0;
             t1[tid * kScanPer + k] = (int32_t)r1;
-            if (lst && (a | b) != 0)
-                recs[r2++] = make_int4((int32_t)(base + tid * kScanPer + k), (int32_t)r0, (int32_t)r1, a | (b << 16));
             r0 += a;
             r1 += b;
         }
@@ -1134,13 +1054,11 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_counts(const int32_t* __r
         }
         carry0 += tot0;
         carry1 += tot1;
-        carry2 += tot2;
         __syncthreads();  // the tile buffers and wave sums are reused
     }
     if (tid == 0) {
         totals[0] = carry0;
         totals[1] = carry1;
-        if (lst) totals[2] = carry2;
     }
 }
 
@@ -1354,14 +1272,14 @@ static int ex_scratch(mqr_vbg* v, int64_t n, bool mesh, ExScratch& e) {
                                                    (int)n, v->stream));
     const size_t sz_nb = align256(sizeof(int32_t) * 27 * n), sz_c = align256(sizeof(int32_t) * n);
     // mesh: the byte-tile path's face tables (3 R^2 u32 per block), or the bit-row path's row records
-    // (R^2 uint4), sign rows ((R + 2)^2 u32), per-cube triangle counts (R^2 u64) and the list
-    // record (int4) per block, whichever is larger
+    // (R^2 uint4), sign rows ((R + 2)^2 u32) and per-cube triangle counts (R^2 u64) per block,
+    // whichever is larger
     const size_t sz_f = mesh ? align256(std::max(sizeof(uint32_t) * 3 * v->R * v->R,
-                                                 sizeof(uint32_t) * (6 * v->R * v->R + (v->R + 2) * (v->R + 2) + 4)) *
+                                                 sizeof(uint32_t) * (6 * v->R * v->R + (v->R + 2) * (v->R + 2))) *
                                         n)
                              : 0;
     const size_t sz_b = align256(sizeof(uint16_t) * 3 * v->R * v->R * n);
-    tmp_bytes = std::max<size_t>(tmp_bytes, 4 * sizeof(int64_t));  // k_scan_counts' totals
+    tmp_bytes = std::max<size_t>(tmp_bytes, 2 * sizeof(int64_t));
     const size_t need = sz_nb + 4 * sz_c + sz_f + sz_b + align256(tmp_bytes);
     if (v->ex_scratch_bytes < need) {
         MQR_CHECK_HIP(hipStreamSynchronize(v->stream));
@@ -1474,9 +1392,12 @@ static int build_nb(mqr_vbg* v, int32_t* nb) {
 // volume that is still being integrated.
 static int64_t spec_cap(int64_t hint) { return hint > 0 ? hint + hint / 4 + 4096 : 0; }
 
-// Extraction configuration: bit 0 = NIB (k_mc_count), bit 1 = MAP, bit 2 = LST, bit 3 = STG (k_mc_emit),
-// bit 4 = XB (XCD bands of the pool in k_mc_count and k_mc_emit);
-// the A/B library takes it from mqr_vbg_set_extract_mode (below; tools/ab_extract.py).
+// Extraction configuration: bit 0 = NIB (k_mc_count), bit 1 = MAP (k_mc_emit); the A/B library
+// takes it from mqr_vbg_set_extract_mode (below; tools/ab_extract.py).  (Also measured in round 4
+// and removed, DESIGN.md §4.2: the emission over a compacted list of the blocks with output, by one
+// workgroup per listed block or by a grid of 8 workgroups per CU walking the list; the block's tsdf
+// staged in LDS for its interior vertices' taps; XCD bands of the pool in the count and emission
+// passes -- all neutral or slower.)
 [[maybe_unused]] constexpr int kExMode = 3;  // NIB + MAP (tools/ab_extract.py)
 static int ex_mode(const mqr_vbg* v) {
 #if MQR_AB
@@ -1487,40 +1408,24 @@ static int ex_mode(const mqr_vbg* v) {
 #endif
 }
 
-template <int RT, bool NIB, bool MAP, bool LST, bool STG, bool XB, class... A>
+template <int RT, bool NIB, bool MAP, class... A>
 static void launch_mc_emit_t(const mqr_vbg* v, int64_t n, A... args) {
 #if MQR_AB  // MQR_EMIT_DIAG=1: vertices only, 2: triangles only (timing diagnostics)
     static const int diag = getenv("MQR_EMIT_DIAG") ? atoi(getenv("MQR_EMIT_DIAG")) : 0;
 #else
     constexpr int diag = 0;
 #endif
-    const int64_t grid = n;
-    hipLaunchKernelGGL((k_mc_emit<RT, NIB, MAP, LST, STG && RT == 16, XB>), dim3((unsigned)grid), dim3(kMcThreads), 0,
-                       v->stream, args..., diag);
+    hipLaunchKernelGGL((k_mc_emit<RT, NIB, MAP>), dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, args..., diag);
 }
 
 template <int RT, class... A>
 static void launch_mc_emit(const mqr_vbg* v, int64_t n, A... args) {
-#if MQR_AB
-    switch (ex_mode(v)) {
-        case 1: launch_mc_emit_t<RT, true, false, false, false, false>(v, n, args...); return;
-        case 2: launch_mc_emit_t<RT, false, true, false, false, false>(v, n, args...); return;
-        case 3: launch_mc_emit_t<RT, true, true, false, false, false>(v, n, args...); return;
-        case 4: launch_mc_emit_t<RT, false, false, true, false, false>(v, n, args...); return;
-        case 5: launch_mc_emit_t<RT, true, false, true, false, false>(v, n, args...); return;
-        case 6: launch_mc_emit_t<RT, false, true, true, false, false>(v, n, args...); return;
-        case 7: launch_mc_emit_t<RT, true, true, true, false, false>(v, n, args...); return;
-        case 8: launch_mc_emit_t<RT, false, false, false, true, false>(v, n, args...); return;
-        case 11: launch_mc_emit_t<RT, true, true, false, true, false>(v, n, args...); return;
-        case 15: launch_mc_emit_t<RT, true, true, true, true, false>(v, n, args...); return;
-        case 19: launch_mc_emit_t<RT, true, true, false, false, true>(v, n, args...); return;
-        case 27: launch_mc_emit_t<RT, true, true, false, true, true>(v, n, args...); return;
-        default: launch_mc_emit_t<RT, false, false, false, false, false>(v, n, args...); return;
+    switch (ex_mode(v) & 3) {
+        case 1: launch_mc_emit_t<RT, true, false>(v, n, args...); break;
+        case 2: launch_mc_emit_t<RT, false, true>(v, n, args...); break;
+        case 3: launch_mc_emit_t<RT, true, true>(v, n, args...); break;
+        default: launch_mc_emit_t<RT, false, false>(v, n, args...); break;
     }
-#else
-    launch_mc_emit_t<RT, (kExMode & 1) != 0, (kExMode & 2) != 0, (kExMode & 4) != 0, (kExMode & 8) != 0,
-                     (kExMode & 16) != 0>(v, n, args...);
-#endif
 }
 
 template <int RT>
@@ -1530,27 +1435,18 @@ static int mesh_passes(mqr_vbg* v, float thr, const ExScratch& e, mqr_geom* g, i
     uint4* rows4 = reinterpret_cast<uint4*>(e.faces);
     uint32_t* rowNt = reinterpret_cast<uint32_t*>(rows4 + n * RR * RR);
     uint64_t* rowsT = reinterpret_cast<uint64_t*>(rowNt + n * (RR + 2) * (RR + 2));  // 8-byte aligned: (R + 2)^2 even
-    int4* recs = reinterpret_cast<int4*>(rowsT + n * RR * RR);  // 16-byte aligned: 4 (R + 2)^2 = 0 mod 16
     int64_t nv = 0, nt = 0;
     if constexpr (RT > 0) {
         int64_t* tot = reinterpret_cast<int64_t*>(e.tmp);
         hipLaunchKernelGGL(k_mc_bits<RT>, dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, v->pool, thr, e.bits,
                            v->bkeys, v->tab, e.nb);
-        if ((ex_mode(v) & 17) == 17)
-            hipLaunchKernelGGL((k_mc_count<RT, true, true>), dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, e.nb,
-                               e.bits, tri_blocks, e.c0, e.c1, rows4, rowNt, rowsT);
-        else if (ex_mode(v) & 1)
-            hipLaunchKernelGGL((k_mc_count<RT, true, false>), dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, e.nb,
-                               e.bits, tri_blocks, e.c0, e.c1, rows4, rowNt, rowsT);
+        if (ex_mode(v) & 1)
+            hipLaunchKernelGGL((k_mc_count<RT, true>), dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, e.nb, e.bits,
+                               tri_blocks, e.c0, e.c1, rows4, rowNt, rowsT);
         else
-            hipLaunchKernelGGL((k_mc_count<RT, false, false>), dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, e.nb,
-                               e.bits, tri_blocks, e.c0, e.c1, rows4, rowNt, rowsT);
-        if (ex_mode(v) & 4)
-            hipLaunchKernelGGL(k_scan_counts<true>, dim3(1), dim3(kScanThreads), 0, v->stream, e.c0, e.c1, n, e.o0,
-                               e.o1, tot, recs);
-        else
-            hipLaunchKernelGGL(k_scan_counts<false>, dim3(1), dim3(kScanThreads), 0, v->stream, e.c0, e.c1, n, e.o0,
-                               e.o1, tot, (int4*)nullptr);
+            hipLaunchKernelGGL((k_mc_count<RT, false>), dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, e.nb, e.bits,
+                               tri_blocks, e.c0, e.c1, rows4, rowNt, rowsT);
+        hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(kScanThreads), 0, v->stream, e.c0, e.c1, n, e.o0, e.o1, tot);
         // With a previous extraction's counts, emit into buffers of that size (+ margin) without
         // waiting for this one's totals; blocks past the capacity write nothing and the pass is re-run
         // into exact buffers if the totals exceed it.  Without, wait for the totals first.
@@ -1564,7 +1460,7 @@ static int mesh_passes(mqr_vbg* v, float thr, const ExScratch& e, mqr_geom* g, i
             launch_mc_emit<RT>(v, n, (const int32_t*)e.nb, (const uint64_t*)v->bkeys, (const float2*)v->pool,
                                v->voxel_size, (const int32_t*)e.c0, (const int32_t*)e.c1, (const int32_t*)e.o0,
                                (const int32_t*)e.o1, (const uint4*)rows4, (const uint32_t*)rowNt, g->pos, g->nrm,
-                               g->tri, cv, ct, (const uint64_t*)rowsT, (const int4*)recs, (const int64_t*)(tot + 2));
+                               g->tri, cv, ct, (const uint64_t*)rowsT);
             MQR_CHECK_HIP(hipGetLastError());
             emitted = true;
         }
@@ -1585,7 +1481,7 @@ static int mesh_passes(mqr_vbg* v, float thr, const ExScratch& e, mqr_geom* g, i
         launch_mc_emit<RT>(v, n, (const int32_t*)e.nb, (const uint64_t*)v->bkeys, (const float2*)v->pool, v->voxel_size,
                            (const int32_t*)e.c0, (const int32_t*)e.c1, (const int32_t*)e.o0, (const int32_t*)e.o1,
                            (const uint4*)rows4, (const uint32_t*)rowNt, g->pos, g->nrm, g->tri, nv, nt,
-                           (const uint64_t*)rowsT, (const int4*)recs, (const int64_t*)(tot + 2));
+                           (const uint64_t*)rowsT);
     } else {
         if (build_nb(v, e.nb)) return 1;
         hipLaunchKernelGGL(k_mesh_count<RT>, dim3((unsigned)n), dim3(kThreads), 0, v->stream, e.nb, n, v->pool, v->R,
@@ -1615,8 +1511,8 @@ static int point_passes(mqr_vbg* v, float thr, const ExScratch& e, mqr_geom* g) 
                            v->bkeys, v->tab, e.nb);
         hipLaunchKernelGGL(k_pt_count<RT>, dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, e.nb, e.bits, v->pool,
                            e.c0, rows4);
-        hipLaunchKernelGGL(k_scan_counts<false>, dim3(1), dim3(kScanThreads), 0, v->stream, e.c0,
-                           (const int32_t*)nullptr, n, e.o0, (int32_t*)nullptr, tot, (int4*)nullptr);
+        hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(kScanThreads), 0, v->stream, e.c0, (const int32_t*)nullptr, n,
+                           e.o0, (int32_t*)nullptr, tot);
         MQR_CHECK_HIP(hipGetLastError());
         MQR_CHECK_HIP(hipMemcpyAsync(v->h_ex, tot, sizeof(int64_t), hipMemcpyDeviceToHost, v->stream));
         const int64_t cp = spec_cap(v->ex_hint[2]);  // speculative capacity, as in mesh_passes
@@ -1667,7 +1563,7 @@ int mqr_extract_mesh(mqr_vbg* v, float thr, mqr_geom** out) { return mqr_extract
 #if MQR_AB
 // A/B library only: the extraction configuration (kExMode bits) for tools/ab_extract.py.
 int mqr_vbg_set_extract_mode(mqr_vbg* v, int mode) {
-    MQR_REQUIRE(v && mode >= 0 && mode < 32, "bad extraction mode");
+    MQR_REQUIRE(v && mode >= 0 && mode < 4, "bad extraction mode");
     v->ex_mode = mode;
     return 0;
 }

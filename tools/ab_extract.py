@@ -3,14 +3,13 @@
 
 python tools/ab_extract.py --modes 0 --reps 15
 mode = an extraction configuration under test (mqr_vbg_set_extract_mode, A/B library only; the
-product library runs mode 0 = its kExMode, extract.hip): bit 0 per-cube triangle counts from the count pass, bit 1 LDS row
-maps in the emission pass (both = 3, the library default), bit 2 emission over a compacted list of
-the blocks with output, bit 3 the block's
-tsdf staged in LDS for its interior vertex taps, bit 4 XCD bands of the pool in the count and emission
-passes (round 4 also measured the count pass emitting the vertices, 0.264 vs 0.237 ms, and a
-vertex and a triangle workgroup per block, 0.187 vs 0.179 ms, removed) (round 3
-measured a merged vertex / triangle item loop and 512-thread emission blocks this way: no change,
-profiles/r03_ab_integrate_windows.json; neither is in the library now).
+product library runs mode 0 = its kExMode, extract.hip): bit 0 per-cube triangle counts from the
+count pass, bit 1 LDS row maps in the emission pass (both = 3, the library default).  Round 4 also
+measured, and removed: an emission over a compacted list of the blocks with output, the block's tsdf
+staged in LDS for the interior vertex taps, XCD bands of the pool (profiles/r04_ab_extract.json),
+the count pass emitting the vertices (0.264 vs 0.237 ms) and a vertex and a triangle workgroup per
+block (0.187 vs 0.179 ms); round 3 measured a merged vertex / triangle item loop and 512-thread
+emission blocks this way: no change (profiles/r03_ab_integrate_windows.json).
 Prints per-mode median wall ms of mqr_extract_mesh (device-resident, the bench's extract_ms) and
 whether positions / normals / triangles equal the first mode's bit for bit.
 """
