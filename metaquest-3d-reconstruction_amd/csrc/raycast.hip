@@ -349,8 +349,16 @@ __global__ __launch_bounds__(256) void k_cast_pinhole(const float4* __restrict__
                                                       float* uvs, float* normals) {
     const int f = blockIdx.y;
     const int64_t HW = (int64_t)H * W;
+#ifndef MQR_RAY_XCD
+#define MQR_RAY_XCD 1
+#endif
+    // XCD bands: workgroups go to the 8 XCDs round-robin, so workgroup bx of a row of workgroups
+    // divisible by 8 is remapped for XCD x to cast the x-th eighth of the image (its rays then walk one
+    // part of the scene's BVH, which its own L2 can hold better than the whole tree)
+    unsigned bx = blockIdx.x;
+    if (MQR_RAY_XCD && (gridDim.x & 7u) == 0) bx = (bx & 7u) * (gridDim.x >> 3) + (bx >> 3);
     // 8x8 pixel tiles per wave keep a wave's rays coherent (same BVH paths)
-    const int64_t tile = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t tile = (int64_t)bx * 4 + (threadIdx.x >> 6);
     const int tiles_x = (W + 7) / 8;
     const int tx = (int)(tile % tiles_x), ty = (int)(tile / tiles_x);
     const int x = tx * 8 + (threadIdx.x & 7), y = ty * 8 + ((threadIdx.x >> 3) & 7);
