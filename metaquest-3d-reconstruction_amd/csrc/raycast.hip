@@ -349,14 +349,10 @@ __global__ __launch_bounds__(256) void k_cast_pinhole(const float4* __restrict__
                                                       float* uvs, float* normals) {
     const int f = blockIdx.y;
     const int64_t HW = (int64_t)H * W;
-#ifndef MQR_RAY_XCD
-#define MQR_RAY_XCD 1
-#endif
-    // XCD bands: workgroups go to the 8 XCDs round-robin, so workgroup bx of a row of workgroups
-    // divisible by 8 is remapped for XCD x to cast the x-th eighth of the image (its rays then walk one
-    // part of the scene's BVH, which its own L2 can hold better than the whole tree)
-    unsigned bx = blockIdx.x;
-    if (MQR_RAY_XCD && (gridDim.x & 7u) == 0) bx = (bx & 7u) * (gridDim.x >> 3) + (bx >> 3);
+    // (XCD bands -- workgroup bx remapped so that XCD bx mod 8 casts one eighth of the image -- ran
+    // 15.0-16.1 vs 13.2-13.4 ms for 64 C2 frames, identical hits: the bands' traversal costs differ,
+    // tools/raycast_workload.py, profiles/r04_ab_raycast_xcd.json)
+    const unsigned bx = blockIdx.x;
     // 8x8 pixel tiles per wave keep a wave's rays coherent (same BVH paths)
     const int64_t tile = (int64_t)bx * 4 + (threadIdx.x >> 6);
     const int tiles_x = (W + 7) / 8;

@@ -1,7 +1,8 @@
 #!/bin/bash
 # Libraries that differ only in the ray-casting object, for process-alternating A/B timing with
-# tools/raycast_workload.py (MQR_HIP_LIB=tools/_ab/libmqr_ray_<name>.so): xcd = MQR_RAY_XCD=1 (the
-# default), plain = MQR_RAY_XCD=0.
+# tools/raycast_workload.py (MQR_HIP_LIB=tools/_ab/libmqr_ray_<name>.so): xcd = MQR_RAY_XCD=1, plain =
+# MQR_RAY_XCD=0.  (Round 4 measured the XCD-banded order this way and removed it; the
+# macro is gone from raycast.hip, so both builds are now the plain order -- edit raycast.hip to A/B.)
 set -e
 cd "$(dirname "$0")/../metaquest-3d-reconstruction_amd/csrc"
 make -s $(for s in vbg extract confidence ingest meshfilter merge color; do echo build/$s.o; done)
