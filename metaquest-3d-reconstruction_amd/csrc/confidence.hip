@@ -534,13 +534,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W8 ? 8 : 1,
     double pw[3];
     int nv = 0, nc = 0;
     uint32_t n_pairs = 0, n_f32 = 0, n_tail = 0;
-#ifndef MQR_CONF_NT
-#define MQR_CONF_NT 0
-#endif
-    // (MQR_CONF_NT, A/B: the reference depth read and the two outputs streamed past the L2 -- which then
-    // keeps the XCD's band of the neighbour window)
-    const float dref = MQR_CONF_NT ? __builtin_nontemporal_load(depths + (int64_t)ref * HW + p) : depths[(int64_t)ref * HW + p];
-    if (p0 < HW && ref_point(fr[ref], u, v, dref, depth_max, pw)) {
+    if (p0 < HW && ref_point(fr[ref], u, v, depths[(int64_t)ref * HW + p], depth_max, pw)) {
         const int lo = max(0, ref - r), hi = min(N, ref + r + 1);
         // the consistency band (pixel_decide): the neighbours' largest defect terms, then per pixel
         const double c1 = fr[ref].wc1, c0 = fr[ref].wc0;
@@ -691,14 +685,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W8 ? 8 : 1,
     }
     if (p0 >= HW) return;
     const int64_t o = (int64_t)rloc * HW + p;
-    const double cv = nv == 0 ? 0.0 : (double)nc / (double)nv;
-    if (MQR_CONF_NT) {
-        __builtin_nontemporal_store(nv, valid + o);
-        __builtin_nontemporal_store(cv, conf + o);
-    } else {
-        valid[o] = nv;
-        conf[o] = cv;
-    }
+    valid[o] = nv;
+    conf[o] = nv == 0 ? 0.0 : (double)nc / (double)nv;
 }
 
 __global__ void k_error_map(const float* __restrict__ refd, const float* __restrict__ tgtd, int H, int W,

@@ -7,7 +7,8 @@
 #   (w8 / slpw8, new / slp held to 8 waves per SIMD, measured in round 4: the production instances now
 #   carry that attribute themselves)
 #   xcd  new with the XCD-banded tile order (MQR_CONF_XCD=1, the default since round 4), plain: =0
-#   nt   new with the reference depth read and the outputs non-temporal (MQR_CONF_NT=1)
+#   (nt, the reference depth read and the outputs non-temporal, was measured in round 4 at -0.5 %,
+#   within run-to-run spread, and not kept: r04v in profiles/r04_ab_confidence_variants.json)
 set -e
 cd "$(dirname "$0")/../metaquest-3d-reconstruction_amd/csrc"
 make -s build/vbg.o build/extract.o build/ingest.o
@@ -19,8 +20,7 @@ git show ${OLD_REV:-HEAD}:metaquest-3d-reconstruction_amd/csrc/confidence.hip > 
 /opt/rocm/bin/hipcc $F -DMQR_SRC_TAG=\"var-slp\" -c confidence.hip -o build/var/c_slp.o
 /opt/rocm/bin/hipcc $F -fno-slp-vectorize -DMQR_CONF_XCD=1 -DMQR_SRC_TAG=\"var-xcd\" -c confidence.hip -o build/var/c_xcd.o
 /opt/rocm/bin/hipcc $F -fno-slp-vectorize -DMQR_CONF_XCD=0 -DMQR_SRC_TAG=\"var-plain\" -c confidence.hip -o build/var/c_plain.o
-/opt/rocm/bin/hipcc $F -fno-slp-vectorize -DMQR_CONF_NT=1 -DMQR_SRC_TAG=\"var-nt\" -c confidence.hip -o build/var/c_nt.o
-for v in old new slp xcd plain nt; do
+for v in old new slp xcd plain; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../../tools/_ab/libmqr_conf_$v.so \
     build/vbg.o build/extract.o build/ingest.o build/var/c_$v.o -Wl,-rpath,/opt/rocm/lib -ldl
 done
