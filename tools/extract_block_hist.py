@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
-"""Per-block output counts of the C2 mesh in the emission pass's order (the mesh is emitted in
-(block, voxel, edge) / (block, cube, triangle) order, so runs of one block coordinate in the vertex /
-triangle arrays are the blocks, in pool order): how the emission workgroups' work is distributed and
-where the heavy blocks sit in the dispatch order."""
+"""Per-block triangle counts of the C2 mesh in the emission pass's order (triangles are emitted in
+(block, cube, triangle) order, so runs of one block coordinate are the blocks, in pool order): how
+the emission workgroups' triangle work is distributed and where the heavy blocks sit in the
+dispatch order."""
 import json
 import os
 import sys
@@ -38,26 +38,23 @@ def main():
     V = np.asarray(m.vertices, np.float64)
     T = np.asarray(m.triangles)
     bs = 0.005 * 16
-    # a vertex lies on an edge starting at its owning voxel: floor of (position / voxel - tiny) per axis
-    vblk = np.floor(V / bs - 1e-7).astype(np.int64)
+    # a triangle belongs to the block of its cube: the floor of its centroid's block coordinate
+    # (vertices are not attributed -- an edge vertex can sit on the far side of a block face)
     tblk = np.floor(V[T].mean(axis=1) / bs).astype(np.int64)
-    nv = runs(vblk)
     nt = runs(tblk)
-    out = {}
-    for name, a in (("vertices", nv), ("triangles", nt)):
-        a = np.sort(a)[::-1]
-        tot = a.sum()
-        out[name] = {"blocks": int(len(a)), "mean": float(a.mean()), "max": int(a[0]),
-                     "q50": float(np.percentile(a, 50)), "q90": float(np.percentile(a, 90)),
-                     "q99": float(np.percentile(a, 99)),
-                     "share_in_blocks_over_256": float(a[a > 256].sum() / tot),
-                     "share_in_blocks_over_512": float(a[a > 512].sum() / tot),
-                     "blocks_over_512": int((a > 512).sum()), "blocks_over_1024": int((a > 1024).sum())}
-    # position of the heavy triangle blocks in the dispatch (pool) order
+    a = np.sort(nt)[::-1]
+    tot = a.sum()
+    out = {"triangles": {"blocks": int(len(a)), "mean": float(a.mean()), "max": int(a[0]),
+                         "q50": float(np.percentile(a, 50)), "q90": float(np.percentile(a, 90)),
+                         "q99": float(np.percentile(a, 99)),
+                         "share_in_blocks_over_256": float(a[a > 256].sum() / tot),
+                         "share_in_blocks_over_512": float(a[a > 512].sum() / tot),
+                         "blocks_over_512": int((a > 512).sum()), "blocks_over_1024": int((a > 1024).sum())}}
+    # position of the heavy blocks in the dispatch (pool) order
     heavy = np.nonzero(nt > 512)[0]
-    out["heavy_triangle_blocks_position_quantiles"] = [float(x) for x in np.percentile(heavy / max(len(nt), 1), [0, 25, 50, 75, 100])] if len(heavy) else []
-    out["loop_iterations_256"] = {"vertex_max": int(np.ceil(nv.max() / 256)), "triangle_max": int(np.ceil(nt.max() / 256)),
-                                  "vertex_mean": float(np.ceil(nv / 256).mean()), "triangle_mean": float(np.ceil(nt / 256).mean())}
+    out["heavy_blocks_position_quantiles"] = ([float(x) for x in np.percentile(heavy / max(len(nt), 1), [0, 25, 50, 75, 100])]
+                                              if len(heavy) else [])
+    out["triangle_rounds_of_256"] = {"max": int(np.ceil(nt.max() / 256)), "mean": float(np.ceil(nt / 256).mean())}
     print(json.dumps(out))
 
 
