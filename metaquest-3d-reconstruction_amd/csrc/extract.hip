@@ -813,37 +813,10 @@ __device__ __forceinline__ void mc_emit_vertex(int i, int lo, const uint4* rows,
 // a +x / +y / +z neighbour's from rows4).
 // (tcs: the rows' per-cube triangle counts (NIB) -- the cube found by skipping 4-bit fields in
 // registers instead of a walk with a table lookup per cube)
-// The row records a block's triangles can need from its +x / +y / +z neighbours (PRE): the +x
-// neighbour's R^2 rows, R rows each of +y (ly = 0), +z (lz = 0), +xy, +xz, one row each of +yz, +xyz.
-template <int R>
-struct NbrRows {
-    static constexpr int R2 = R * R, N = R2 + 4 * R + 2;
-    // slot of neighbour row (lx, ly, lz) in the k27 direction (dx, dy, dz), and its row in that block
-    __device__ static int slot(int dx, int dy, int dz, int ly, int lz) {
-        if (dx && !dy && !dz) return lz * R + ly;
-        if (!dx && dy && !dz) return R2 + lz;
-        if (!dx && !dy && dz) return R2 + R + ly;
-        if (dx && dy && !dz) return R2 + 2 * R + lz;
-        if (dx && !dy && dz) return R2 + 3 * R + ly;
-        if (!dx && dy && dz) return R2 + 4 * R;
-        return R2 + 4 * R + 1;
-    }
-    __device__ static void of_slot(int j, int& k27, int& row) {
-        if (j < R2) { k27 = 2 + 3 + 9; row = j; }
-        else if (j < R2 + R) { k27 = 1 + 6 + 9; row = (j - R2) * R; }
-        else if (j < R2 + 2 * R) { k27 = 1 + 3 + 18; row = j - R2 - R; }
-        else if (j < R2 + 3 * R) { k27 = 2 + 6 + 9; row = (j - R2 - 2 * R) * R; }
-        else if (j < R2 + 4 * R) { k27 = 2 + 3 + 18; row = j - R2 - 3 * R; }
-        else if (j == R2 + 4 * R) { k27 = 1 + 6 + 18; row = 0; }
-        else { k27 = 2 + 6 + 18; row = 0; }
-    }
-};
-
-template <class M, bool NIB, bool PRE = false>
+template <class M, bool NIB>
 __device__ __forceinline__ void mc_emit_tri(int i, int lo, const uint4* rows, const uint64_t* tcs, const uint32_t* rowN,
                                             const uint32_t* triC, const uint64_t* triP, const int32_t* nbrow,
                                             const int32_t* __restrict__ voff, const uint4* __restrict__ rows4,
-                                            const uint4* nrow, const int32_t* nvo,
                                             int32_t vb0, int32_t tb0, int32_t* tri) {
     constexpr int R = M::C - 1;
     const uint4 rw = rows[lo];
@@ -895,15 +868,10 @@ __device__ __forceinline__ void mc_emit_tri(int i, int lo, const uint4* rows, co
                 vid = -1;  // cannot happen for a valid cube (all corners exist); stay in bounds
             } else {
                 const int lx = ox - dx * R, ly = oy - dy * R, lz = oz - dz * R;
-                if constexpr (PRE) {  // prefetched by the workgroup during its vertex loop
-                    const uint4 ow = nrow[NbrRows<R>::slot(dx, dy, dz, ly, lz)];
-                    vid = nvo[k27] + mc_vid(ow.x, ow.z & 0xffffu, ow.z >> 16, ow.w & 0xffffu, lx, axis);
-                } else {
-                    const uint4 ow = rows4[(int64_t)nbuf * M::R2 + lz * R + ly];
-                    // (the neighbour's block offset read here, beside its row record, not in the prologue:
-                    // one dependent global round trip fewer before the block's first barrier)
-                    vid = voff[nbuf] + mc_vid(ow.x, ow.z & 0xffffu, ow.z >> 16, ow.w & 0xffffu, lx, axis);
-                }
+                const uint4 ow = rows4[(int64_t)nbuf * M::R2 + lz * R + ly];
+                // (the neighbour's block offset read here, beside its row record, not in the prologue:
+                // one dependent global round trip fewer before the block's first barrier)
+                vid = voff[nbuf] + mc_vid(ow.x, ow.z & 0xffffu, ow.z >> 16, ow.w & 0xffffu, lx, axis);
             }
         }
         tri[3 * t + (2 - j)] = vid;
@@ -920,10 +888,7 @@ __device__ __forceinline__ void mc_emit_tri(int i, int lo, const uint4* rows, co
 // (filled by one pass over the rows) instead of by a binary search over the row bases.
 constexpr int kRowMap = 2048;
 
-// PRE: the row records the block's triangles need from its +x / +y / +z neighbours (NbrRows) and
-// their block offsets are loaded by the workgroup during its vertex loop and staged in LDS, so the
-// triangle loop makes no global round trip.
-template <int R, int NT, bool NIB = false, bool MAP = false, bool PRE = false>
+template <int R, int NT, bool NIB = false, bool MAP = false>
 __device__ __forceinline__ void mc_emit_block(int64_t b, int role, const int32_t* __restrict__ nb,
                                               const uint64_t* __restrict__ bkeys, const float2* __restrict__ pool,
                                               float voxel_size, const int32_t* __restrict__ vcount,
@@ -941,9 +906,6 @@ __device__ __forceinline__ void mc_emit_block(int64_t b, int role, const int32_t
     __shared__ uint32_t triC[32];
     __shared__ uint64_t tcs[NIB ? M::R2 : 1];
     __shared__ uint8_t vmap[MAP ? kRowMap : 1], tmap[MAP ? kRowMap : 1];
-    __shared__ uint4 nrow[PRE ? NbrRows<R>::N : 1];
-    __shared__ int32_t nvo[PRE ? 27 : 1];
-    static_assert(!PRE || NbrRows<R>::N <= 2 * NT, "two prefetched rows per thread");
     const int nvb = role == 2 ? 0 : vcount[b], ntb = role == 1 ? 0 : tcount[b];
     if (nvb == 0 && ntb == 0) return;  // block-uniform: nothing to write
     const int32_t vb0 = voff[b], tb0 = toff[b];
@@ -979,26 +941,6 @@ __device__ __forceinline__ void mc_emit_block(int64_t b, int role, const int32_t
         }
         __syncthreads();
     }
-    uint4 pr[2] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
-    int32_t pvo = 0;
-    if constexpr (PRE) {
-        if (ntb) {  // (block-uniform) issued here, stored to LDS after the vertex loop
-#pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                const int j = tid + k * NT;
-                if (j < NbrRows<R>::N) {
-                    int k27, row;
-                    NbrRows<R>::of_slot(j, k27, row);
-                    const int32_t nbuf = nbrow[k27];
-                    if (nbuf >= 0) pr[k] = rows4[(int64_t)nbuf * M::R2 + row];
-                }
-            }
-            if (tid < 27) {
-                const int32_t nbuf = nbrow[tid];
-                if (nbuf >= 0) pvo = voff[nbuf];
-            }
-        }
-    }
     if (nvb) {
         const int lane = tid & 63;
         const uint32_t pres = (uint32_t)__ballot(lane < 27 && nbrow[lane < 27 ? lane : 0] >= 0);
@@ -1009,23 +951,14 @@ __device__ __forceinline__ void mc_emit_block(int64_t b, int role, const int32_t
             mc_emit_vertex<M>(i, lo, rows, nbrow, pool, pres, xb, yb, zb, voxel_size, vb0, pos, nrm);
         }
     }
-    if constexpr (PRE) {
-        if (ntb) {
-#pragma unroll
-            for (int k = 0; k < 2; ++k)
-                if (tid + k * NT < NbrRows<R>::N) nrow[tid + k * NT] = pr[k];
-            if (tid < 27) nvo[tid] = pvo;
-            __syncthreads();
-        }
-    }
     for (int i = tid; i < ntb; i += NT) {
         const int lo = tm ? (int)tmap[i] : row_search<M::R2, 1>(rows, i);
-        mc_emit_tri<M, NIB, PRE>(i, lo, rows, tcs, rowN, triC, triP, nbrow, voff, rows4, nrow, nvo, vb0, tb0, tri);
+        mc_emit_tri<M, NIB>(i, lo, rows, tcs, rowN, triC, triP, nbrow, voff, rows4, vb0, tb0, tri);
     }
 }
 
 // diag (A/B library, MQR_EMIT_DIAG): 1 vertices only, 2 triangles only (timing of one half, wrong output)
-template <int R, bool NIB = false, bool MAP = false, bool PRE = false, int NT = kMcThreads>
+template <int R, bool NIB = false, bool MAP = false, int NT = kMcThreads>
 __global__ __launch_bounds__(NT) void k_mc_emit(const int32_t* __restrict__ nb, const uint64_t* __restrict__ bkeys,
                                                 const float2* __restrict__ pool, float voxel_size,
                                                 const int32_t* __restrict__ vcount, const int32_t* __restrict__ tcount,
@@ -1036,7 +969,7 @@ __global__ __launch_bounds__(NT) void k_mc_emit(const int32_t* __restrict__ nb, 
 #if !MQR_AB
     diag = 0;
 #endif
-    mc_emit_block<R, NT, NIB, MAP, PRE>(blockIdx.x, diag, nb, bkeys, pool, voxel_size, vcount, tcount, voff, toff, rows4,
+    mc_emit_block<R, NT, NIB, MAP>(blockIdx.x, diag, nb, bkeys, pool, voxel_size, vcount, tcount, voff, toff, rows4,
                                    rowNt, pos, nrm, tri, cap_v, cap_t, rowsT);
 }
 
@@ -1459,13 +1392,13 @@ static int build_nb(mqr_vbg* v, int32_t* nb) {
 // volume that is still being integrated.
 static int64_t spec_cap(int64_t hint) { return hint > 0 ? hint + hint / 4 + 4096 : 0; }
 
-// Extraction configuration: bit 0 = NIB (k_mc_count), bit 1 = MAP, bit 2 = PRE (k_mc_emit; 7 = all three
-// is the only configuration with PRE); the A/B library
+// Extraction configuration: bit 0 = NIB (k_mc_count), bit 1 = MAP (k_mc_emit); the A/B library
 // takes it from mqr_vbg_set_extract_mode (below; tools/ab_extract.py).  (Also measured in round 4
 // and removed, DESIGN.md §4.2: the emission over a compacted list of the blocks with output, by one
 // workgroup per listed block or by a grid of 8 workgroups per CU walking the list; the block's tsdf
 // staged in LDS for its interior vertices' taps; XCD bands of the pool in the count and emission
-// passes -- all neutral or slower.)
+// passes; the triangles' neighbour row records prefetched into LDS during the vertex loop -- all
+// neutral or slower.)
 [[maybe_unused]] constexpr int kExMode = 3;  // NIB + MAP (tools/ab_extract.py)
 static int ex_mode(const mqr_vbg* v) {
 #if MQR_AB
@@ -1476,24 +1409,23 @@ static int ex_mode(const mqr_vbg* v) {
 #endif
 }
 
-template <int RT, bool NIB, bool MAP, bool PRE, class... A>
+template <int RT, bool NIB, bool MAP, class... A>
 static void launch_mc_emit_t(const mqr_vbg* v, int64_t n, A... args) {
 #if MQR_AB  // MQR_EMIT_DIAG=1: vertices only, 2: triangles only (timing diagnostics)
     static const int diag = getenv("MQR_EMIT_DIAG") ? atoi(getenv("MQR_EMIT_DIAG")) : 0;
 #else
     constexpr int diag = 0;
 #endif
-    hipLaunchKernelGGL((k_mc_emit<RT, NIB, MAP, PRE>), dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, args..., diag);
+    hipLaunchKernelGGL((k_mc_emit<RT, NIB, MAP>), dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, args..., diag);
 }
 
 template <int RT, class... A>
 static void launch_mc_emit(const mqr_vbg* v, int64_t n, A... args) {
-    switch (ex_mode(v) & 7) {
-        case 1: launch_mc_emit_t<RT, true, false, false>(v, n, args...); break;
-        case 2: launch_mc_emit_t<RT, false, true, false>(v, n, args...); break;
-        case 3: launch_mc_emit_t<RT, true, true, false>(v, n, args...); break;
-        case 7: launch_mc_emit_t<RT, true, true, true>(v, n, args...); break;
-        default: launch_mc_emit_t<RT, false, false, false>(v, n, args...); break;
+    switch (ex_mode(v) & 3) {
+        case 1: launch_mc_emit_t<RT, true, false>(v, n, args...); break;
+        case 2: launch_mc_emit_t<RT, false, true>(v, n, args...); break;
+        case 3: launch_mc_emit_t<RT, true, true>(v, n, args...); break;
+        default: launch_mc_emit_t<RT, false, false>(v, n, args...); break;
     }
 }
 
@@ -1632,7 +1564,7 @@ int mqr_extract_mesh(mqr_vbg* v, float thr, mqr_geom** out) { return mqr_extract
 #if MQR_AB
 // A/B library only: the extraction configuration (kExMode bits) for tools/ab_extract.py.
 int mqr_vbg_set_extract_mode(mqr_vbg* v, int mode) {
-    MQR_REQUIRE(v && mode >= 0 && mode < 8, "bad extraction mode");
+    MQR_REQUIRE(v && mode >= 0 && mode < 4, "bad extraction mode");
     v->ex_mode = mode;
     return 0;
 }
