@@ -62,7 +62,8 @@ def parse():
     ap.add_argument("--conf-error", type=float, default=0.08)
     ap.add_argument("--no-extras", action="store_true", help="skip confidence / copy-peak / host-input legs")
     ap.add_argument("--no-parity", action="store_true", help="skip the oracle comparison of the timed volume")
-    ap.add_argument("--conf-cpu-seconds", type=float, default=10.0, help="bounded CPU sample of the confidence oracle")
+    ap.add_argument("--conf-cpu-seconds", type=float, default=20.0,
+                    help="bounded CPU sample of the confidence oracle (its maps are also the parity check)")
     ap.add_argument("--e2e-frames", type=int, default=500, help="frames of the on-disk C3 capture (0: skip the leg)")
     ap.add_argument("--merge", default="sharded", choices=["sharded", "root"],
                     help="N>1 volume merge inside libmqr over RCCL (mqr_reduce_rccl): owned slice + halo per "
@@ -77,6 +78,9 @@ def parse():
     ap.add_argument("--strong-frames", type=int, default=1000, help="frames per side in --strong mode")
     ap.add_argument("--no-c5", action="store_true", help="skip the 1-GPU C5 leg (4000 frames @ 3 mm + colour)")
     ap.add_argument("--no-c4", action="store_true", help="skip the 1-GPU C4 leg (1000 + 1000 frames chained)")
+    ap.add_argument("--touch-steps", type=int, default=20, help="profiled steps for touch_ms_per_launch (0: skip)")
+    ap.add_argument("--c5-only", action="store_true",
+                    help="run only the C5 leg and print its record (rocprof of the peak-HBM run)")
     return ap.parse_args()
 
 
@@ -148,7 +152,7 @@ def confidence_leg(depth_t, K, T_wc, args, device):
     return {"ref_frames": B, "window_r": args.conf_range, "ms": t * 1e3, "ref_frames_per_s": B / t,
             "alg_gbs": alg / t / 1e9, "depth_max": args.conf_depth_max, "error_threshold": args.conf_error,
             "binding": conf_binding(),
-            "note": "mqr_confidence over all frames, device-resident depth in/out, wall time of the call"}
+            "note": "mqr_confidence over all frames, device-resident depth in/out, wall time of the call"}, (conf, valid)
 
 
 def conf_binding():
@@ -207,7 +211,7 @@ def ingest_leg(B, H, W, device):
             "note": "mqr_decode_depth, device raw/conf/count in, depth out, wall time of the call"}
 
 
-def c3_leg(seq, vbg, args, device, reps=3):
+def c3_leg(seq, vbg, args, device, reps=3, parity=True):
     """C3 on the device, inputs resident in HBM: decode the raw NDC stack (mqr_decode_depth), the
     confidence of every frame (mqr_confidence, r = conf_range), decode again with the confidence
     mask (0.02 / 2, o3d_utils.py:141-142) and integrate the masked frames -- the pipeline's
@@ -261,10 +265,40 @@ def c3_leg(seq, vbg, args, device, reps=3):
         torch.cuda.synchronize()
         times.append(time.perf_counter() - t0)
     t = sorted(times)[len(times) // 2]
-    return {"frames": B, "ms": t * 1e3, "frames_per_s": B / t, "masked_fraction": float((masked == 0).float().mean()),
-            "blocks": vbg.size(), "window_r": args.conf_range,
-            "note": "device-resident raw NDC in: decode + confidence (all frames) + masked decode + integrate, "
-                    "wall time, median of 3"}
+    out = {"frames": B, "ms": t * 1e3, "frames_per_s": B / t, "masked_fraction": float((masked == 0).float().mean()),
+           "blocks": vbg.size(), "window_r": args.conf_range,
+           "note": "device-resident raw NDC in: decode + confidence (all frames) + masked decode + integrate, "
+                   "wall time, median of 3"}
+    if parity:
+        # the last run's outputs: the mask (o3d_utils.py:141-142 restated in torch on the leg's own decoded
+        # depth and maps, bit for bit on the integrated frames), the confidence maps of sampled reference
+        # frames against the oracle, and the masked volume against the oracle's volume of the same frames
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+        okb = torch.from_numpy(ok.astype(bool)).to(device)
+        want = torch.where((conf < 0.02) | (valid < 2), torch.zeros_like(depth), depth)
+        mask_equal = bool(torch.equal(masked[okb].view(torch.int32), want[okb].view(torch.int32)))
+        dh = depth.cpu().numpy()
+        sample = sorted({0, 1, B // 4, B // 2, 3 * B // 4, B - 2, B - 1})
+        conf_ok = True
+        for i in sample:
+            oc, ov = oracle.confidence(dh, K32.reshape(B, 3, 3), T_cw.reshape(B, 4, 4), T_ci.reshape(B, 4, 4), i,
+                                       int(args.conf_range), float(args.conf_depth_max), float(args.conf_error),
+                                       frame_valid=ok)
+            conf_ok = conf_ok and bool(np.array_equal(valid[i].cpu().numpy(), ov)) and bool(
+                np.array_equal(conf[i].cpu().numpy().view(np.uint64), oc.view(np.uint64)))
+        del dh
+        sel = np.flatnonzero(ok)
+        mh = masked.cpu().numpy()[sel]
+        ref = oracle_volume(mh, K[sel], T[sel], args.voxel, args)
+        del mh
+        out["parity"] = parity_check(vbg, ref, args.extract_threshold, points_thr=3.0)
+        out["parity"]["mask_equal"] = mask_equal
+        out["parity"]["confidence_frames_checked"] = sample
+        out["parity"]["confidence_equal"] = conf_ok
+        out["parity"]["all_ok"] = bool(out["parity"]["all_ok"] and mask_equal and conf_ok)
+        del ref
+    return out
 
 
 def dropin_e2e_leg(seq, frames, device, fragment_workers=4):
@@ -405,7 +439,18 @@ def c5_leg(args, device, frames_per_side=2000, voxel=0.003, key_every=40, parity
     class _P:
         ptr = ctypes.c_void_p(depth.data_ptr())
 
+    # pass 1: a fresh volume whose pool grows from 16384 blocks (reallocation + copy of the grown pool
+    # inside the timed call); passes 2-3: the same volume emptied (vbg.reset keeps the grown pool),
+    # with the integrate launches timed by HIP events for the roofline
     vbg = VoxelBlockGrid(voxel_size=voxel, block_resolution=16, block_count=16384, device=dev)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    vbg.integrate_frames((_P, B, H, W), K, T, depth_scale=1.0, depth_max=args.depth_max,
+                         trunc_voxel_multiplier=args.trunc)
+    torch.cuda.synchronize()
+    t_grow = time.perf_counter() - t0
+    vbg.stats(reset=True)
+    vbg.profile(True)
     times = []
     for _ in range(2):
         vbg.reset()
@@ -415,9 +460,29 @@ def c5_leg(args, device, frames_per_side=2000, voxel=0.003, key_every=40, parity
                              trunc_voxel_multiplier=args.trunc)
         torch.cuda.synchronize()
         times.append(time.perf_counter() - t0)
+    vbg.profile(False)
+    st = vbg.stats(reset=True)
     t_int = min(times)
     blocks = vbg.size()
     pool_gb = vbg.capacity() * 16 ** 3 * 8 / 1e9
+    R3 = 16 ** 3
+    launches = max(st["integrate_launches"], 1)
+    alg = (16 * R3 * st["union_blocks"] + 4 * H * W * st["frames"] + 16 * st["frame_blocks"]) / launches
+    avg_ms = st["integrate_ms"] / launches
+    int_roof = {"bound": "hbm", "kernel": "k_integrate_lean", "unit": "GB/s", "peak": HBM_PEAK_GBS,
+                "alg_bytes_per_launch": alg, "avg_launch_ms": avg_ms, "launches": st["integrate_launches"],
+                "achieved": alg / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else None,
+                "union_blocks_per_launch": st["union_blocks"] / launches,
+                "frame_blocks_per_frame": st["frame_blocks"] / max(st["frames"], 1),
+                "note": "16 R^3 U + 4 H W k + 16 sum B_f per launch (SURVEY §8(d)) / mean HIP-event launch time "
+                        "over the 2 timed passes"}
+    int_roof["frac"] = int_roof["achieved"] / HBM_PEAK_GBS if int_roof["achieved"] else None
+    # extraction on the device (the mqr_geom result stays in HBM), then the same with the host copy
+    ext_dev_ms, (dnv, dnt) = extract_ms(vbg, 1.5, 3)
+    ext_alg = 8 * R3 * blocks + 4 * 27 * blocks + 24 * dnv + 12 * dnt
+    ext_roof = {"bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS, "alg_bytes": ext_alg,
+                "achieved": ext_alg / (ext_dev_ms * 1e-3) / 1e9, "frac": ext_alg / (ext_dev_ms * 1e-3) / 1e9 /
+                HBM_PEAK_GBS, "note": "8 R^3 N + 108 N + 24 V + 12 T over the device-only extraction (median of 3)"}
     host = depth.cpu().numpy() if parity else None
     del depth, seq
     torch.cuda.empty_cache()
@@ -426,6 +491,7 @@ def c5_leg(args, device, frames_per_side=2000, voxel=0.003, key_every=40, parity
         t0 = time.perf_counter()
         mesh = vbg.extract_triangle_mesh(weight_threshold=1.5)
         ext.append(time.perf_counter() - t0)
+    mesh_bytes = mesh.vertices.nbytes + mesh.vertex_normals.nbytes + mesh.triangles.nbytes
     key = list(range(0, B, key_every))
     Ko = K[0]
     imgs = synthetic.render_color_torch("hall", Ko, [poses[i] for i in key], H, W, device=f"cuda:{dev}").cpu().numpy()
@@ -446,14 +512,18 @@ def c5_leg(args, device, frames_per_side=2000, voxel=0.003, key_every=40, parity
     err_fill = (float(np.abs(col[~seen] - synthetic.texture(mesh.vertices[~seen])).mean()) if (~seen).any()
                 else None)
     out = {"frames": B, "voxel_size": voxel, "integrate_ms": t_int * 1e3, "frames_per_s": B / t_int,
-           "blocks": blocks, "pool_gb": pool_gb, "extract_ms": sorted(ext)[1] * 1e3,
+           "integrate_ms_with_growth": t_grow * 1e3, "roofline": int_roof,
+           "blocks": blocks, "pool_gb": pool_gb, "extract_device_ms": ext_dev_ms, "extract_roofline": ext_roof,
+           "extract_ms": sorted(ext)[1] * 1e3, "extract_host_copy_bytes": mesh_bytes,
            "vertices": int(len(mesh.vertices)), "triangles": int(len(mesh.triangles)),
            "keyframes": len(key), "bvh_build_ms": bvh_s * 1e3, "colour_depth_cast_ms": cast_s * 1e3,
            "colour_ms": col_s * 1e3, "coloured_fraction": float(seen.mean()), "colour_mean_abs_err": err,
            "colour_mean_abs_err_knn_filled": err_fill,
            "generation_s": gen_s,
-           "note": "integrate: device-resident depth, best of 2 passes from an emptied volume (capacity grows "
-                   "from 16384 blocks); extract: host copy included, median of 3; colour: mqr_color_map (boundary "
+           "note": "integrate: device-resident depth, best of 2 passes into the emptied volume whose pool the "
+                   "first pass grew (integrate_ms_with_growth: that first pass, grown from 16384 blocks); "
+                   "extract_device_ms: result left in HBM; extract_ms: host copy included, median of 3; "
+                   "colour: mqr_color_map (boundary "
                    "masks, float64 means, 3-NN fill of unseen vertices), host arrays in/out (PCIe included), error vs "
                    "the analytic texture the colour frames were rendered with"}
     if parity:
@@ -801,9 +871,10 @@ def oracle_volume(depth_host, K, T, args_voxel, args, block_count=4096):
     return ref
 
 
-def confidence_cpu(depth_host, K, T_wc, args, budget_s):
+def confidence_cpu(depth_host, K, T_wc, args, budget_s, gpu_maps=None):
     """CPU baseline of the confidence leg: the oracle's build_confidence_map restatement (fp64,
-    OpenMP over pixels) on as many reference frames as fit in ~budget_s."""
+    OpenMP over pixels) on as many reference frames as fit in ~budget_s.  Every oracle map computed
+    is also compared bit for bit with the GPU leg's (conf, valid) of that frame (`parity`)."""
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
@@ -814,15 +885,35 @@ def confidence_cpu(depth_host, K, T_wc, args, budget_s):
     n = len(depth_host)
     t0 = time.perf_counter()
     done = 0
+    cmp_s = 0.0
+    veq = ceq = True
+    bad = []
     for i in np.linspace(0, n - 1, n).astype(int)[np.random.default_rng(0).permutation(n)]:
-        oracle.confidence(depth_host, K, T_cw, Ti, int(i), args.conf_range, args.conf_depth_max, args.conf_error)
+        oc, ov = oracle.confidence(depth_host, K, T_cw, Ti, int(i), args.conf_range, args.conf_depth_max,
+                                   args.conf_error)
         done += 1
-        if time.perf_counter() - t0 > budget_s:
+        if gpu_maps is not None:  # the comparison is not part of the timed baseline
+            tc = time.perf_counter()
+            gv = gpu_maps[1][int(i)].cpu().numpy()
+            gc = gpu_maps[0][int(i)].cpu().numpy()
+            v_ok, c_ok = bool(np.array_equal(gv, ov)), bool(np.array_equal(gc.view(np.uint64), oc.view(np.uint64)))
+            veq, ceq = veq and v_ok, ceq and c_ok
+            if not (v_ok and c_ok) and len(bad) < 16:
+                bad.append(int(i))
+            cmp_s += time.perf_counter() - tc
+        if time.perf_counter() - t0 - cmp_s > budget_s:
             break
-    dt = time.perf_counter() - t0
-    return {"value": done / dt, "unit": "ref frames/s", "cores": cores, "kind": "port",
-            "sample": f"{done} random reference frames of the sequence (r = {args.conf_range}), oracle.confidence "
-                      f"(oracle/mqr_oracle.c, OpenMP over pixels), {dt:.1f} s"}
+    dt = time.perf_counter() - t0 - cmp_s
+    out = {"value": done / dt, "unit": "ref frames/s", "cores": cores, "kind": "port",
+           "sample": f"{done} random reference frames of the sequence (r = {args.conf_range}), oracle.confidence "
+                     f"(oracle/mqr_oracle.c, OpenMP over pixels), {dt:.1f} s"}
+    parity = None
+    if gpu_maps is not None:
+        parity = {"frames_compared": done, "frames_total": n, "valid_equal": veq, "conf_equal": ceq,
+                  "mismatched_frames": bad, "all_ok": bool(veq and ceq and done > 0),
+                  "comparison": "valid_count (int32) and confidence (float64 bit patterns) of every reference frame "
+                                "the CPU baseline computed, against the GPU leg's maps of the same call"}
+    return out, parity
 
 
 def log(msg):
@@ -898,6 +989,10 @@ def main():
     if os.environ.get("MQR_BENCH_WRAP_DEVICES"):  # rehearsal on fewer GPUs than ranks (gloo-staged merge)
         local %= torch.cuda.device_count()
     torch.cuda.set_device(local)
+    if args.c5_only:
+        print(json.dumps({"c5": c5_leg(args, torch.device("cuda", local), parity=not (args.no_cpu or args.no_parity))}),
+              flush=True)
+        return
     dist = comm = None
     if world > 1:
         # control plane only (barriers, the RCCL id, max-over-ranks timing); volume data moves over
@@ -1012,6 +1107,17 @@ def main():
     log(f"rank {rank}: {args.steps} timed steps in {elapsed:.3f} s")
     vbg.profile(False)
     st = vbg.stats(reset=True)
+    # the touch launches' times (HIP events on the touch stream) from a separate profiled pass of the
+    # same step: recorded inside the timed steps they would add two event commands per batch
+    tst = None
+    if args.touch_steps > 0:
+        vbg.profile(True, touch=True)
+        for _ in range(args.touch_steps):
+            vbg.reset()
+            vbg.integrate_frames(dptr, K, T, depth_scale=1.0, depth_max=args.depth_max,
+                                 trunc_voxel_multiplier=args.trunc)
+        tst = vbg.stats(reset=True)
+        vbg.profile(False)
     if dist:
         e = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
@@ -1062,8 +1168,8 @@ def main():
                                                 seed=rank, device=f"cuda:{local}")
             wd = wseq["depth_t"].contiguous()
             wK, wT = wseq["K"].astype(np.float64), wseq["T_wc"].astype(np.float64)
+            # no synchronize: libmqr orders its streams after torch's current stream (include/mqr.h)
             wptr = (_DevPtr(wd.data_ptr()), wd.shape[0], H, W)
-            torch.cuda.synchronize()  # torch's stream wrote the frames; libmqr reads them on its own streams
 
             def wstep():
                 vbg.reset()
@@ -1115,15 +1221,16 @@ def main():
         parity = sharded_par
 
     extras = {}
+    conf_maps = None
     if rank == 0 and world == 1 and not args.no_extras:
         dev = torch.device("cuda", local)
         log("extra legs: copy peak, confidence, ingest, raycast, mesh filter, C3, drop-in")
         extras["hbm_copy_gbs"] = copy_peak_gbs(dev)
-        extras["confidence"] = confidence_leg(depth_t, K, T, args, dev)
+        extras["confidence"], conf_maps = confidence_leg(depth_t, K, T, args, dev)
         extras["ingest"] = ingest_leg(B, H, W, dev)
         extras["raycast"] = raycast_leg(vbg, K, T, H, W, args.extract_threshold)
         extras["meshfilter"] = meshfilter_leg(vbg, args.extract_threshold)
-        extras["c3"] = c3_leg(seq, vbg, args, dev)
+        extras["c3"] = c3_leg(seq, vbg, args, dev, parity=not (args.no_cpu or args.no_parity))
         if not strong and not args.no_c4:
             log("C4 leg (1000 + 1000 frames chained, parity)")
             extras["c4"] = c4_leg(args, dev, parity=not (args.no_cpu or args.no_parity))
@@ -1148,7 +1255,10 @@ def main():
 
     if host_depth is not None:
         if extras.get("confidence") is not None and args.conf_cpu_seconds > 0:
-            extras["confidence"]["cpu_baseline"] = confidence_cpu(host_depth, K, T, args, args.conf_cpu_seconds)
+            log("confidence CPU baseline + parity of the GPU maps")
+            extras["confidence"]["cpu_baseline"], extras["confidence"]["parity"] = confidence_cpu(
+                host_depth, K, T, args, args.conf_cpu_seconds, conf_maps)
+    conf_maps = None
 
     from mqr import _lib
     _vr = ctypes.c_int(-1)
@@ -1211,7 +1321,12 @@ def main():
                          "launches": st["integrate_launches"], "union_blocks_per_launch":
                              st["union_blocks"] / launches, "frame_blocks_per_frame":
                              st["frame_blocks"] / max(st["frames"], 1),
-                         "touch_ms_per_launch": (st["touch_ms"] / st["touch_launches"]) if st["touch_launches"] else None},
+                         "touch_ms_per_launch": (tst["touch_ms"] / tst["touch_launches"]) if tst and
+                         tst["touch_launches"] else None,
+                         "touch_launches_per_step": (tst["touch_launches"] / args.touch_steps) if tst else None,
+                         "touch_note": f"k_touch launch time (HIP events on the touch stream) over {args.touch_steps} "
+                                       "profiled steps after the timed ones; the first touch of a step runs alone, the "
+                                       "others beside the previous batch's integrate"},
             "cpu_baseline": cpu,
             "parity": parity,
             "c3": extras.get("c3"),

@@ -9,6 +9,13 @@
  *   - plain pointers and sizes only; `loc` arguments say where a buffer lives:
  *     MQR_HOST (caller-owned host memory, read/written during the call only) or
  *     MQR_DEVICE (device pointer on the volume's device, e.g. from mqr_device_alloc);
+ *   - stream ordering of MQR_DEVICE buffers: the library runs on its own non-blocking HIP streams.
+ *     Every call that reads or writes caller device buffers first makes those streams wait for all
+ *     work enqueued so far on the calling thread's CALLER STREAM (mqr_set_stream; default: the null
+ *     stream), so a kernel or copy the caller enqueued there that writes an input -- or still reads a
+ *     buffer the call overwrites -- is complete before the library touches it.  No host wait is
+ *     involved (an event and a stream wait).  Every call has finished with its buffers when it
+ *     returns: outputs are complete and visible to any stream afterwards;
  *   - matrices are row-major: K = 3x3 intrinsic (Open3D convention, cx already flipped),
  *     T_wc = 4x4 world->camera extrinsic, both float64 as the reference passes them
  *     (o3d_utils.py:203-210);
@@ -40,6 +47,12 @@ int mqr_build_tag(int which, char* buf, int cap);
 int mqr_vbg_last_kernel(mqr_vbg* v, int* variant);
 const char* mqr_last_error(void);
 int mqr_device_count(int* n);
+/* The calling thread's caller stream (a hipStream_t; NULL = the null stream, the default): see
+ * "stream ordering" above.  A PyTorch caller passes torch.cuda.current_stream().cuda_stream (the
+ * Python layer does this by itself); the stream must belong to the device of the calls that follow
+ * (status 2 otherwise).  mqr_get_stream reads the current setting. */
+int mqr_set_stream(void* stream);
+int mqr_get_stream(void** stream);
 
 /* Device memory helpers (so callers can keep inputs resident in HBM without any framework). */
 int mqr_device_alloc(int device, int64_t bytes, void** ptr);

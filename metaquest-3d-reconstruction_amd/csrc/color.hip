@@ -386,6 +386,10 @@ int mqr_color_vertices(int device, const float* vertices, int64_t nv, int vloc, 
     }
     hipStream_t s = nullptr;
     MQR_CHECK_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    if ((vloc == MQR_DEVICE || img_loc == MQR_DEVICE || out_loc == MQR_DEVICE) && order_after_caller(device, s)) {
+        (void)hipStreamDestroy(s);
+        return 2;
+    }
     std::vector<void*> owned;
     int rc = 0;
     auto dev = [&](const void* h, size_t bytes, bool host) -> const void* {
@@ -455,6 +459,10 @@ int mqr_color_map(int device, const float* vertices, int64_t nv, int vloc, const
     }
     hipStream_t s = nullptr;
     MQR_CHECK_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    if ((vloc == MQR_DEVICE || img_loc == MQR_DEVICE || out_loc == MQR_DEVICE) && order_after_caller(device, s)) {
+        (void)hipStreamDestroy(s);
+        return 2;
+    }
     std::vector<void*> owned;
     auto alloc = [&](size_t bytes) -> void* {
         void* p = nullptr;

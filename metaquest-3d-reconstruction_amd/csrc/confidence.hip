@@ -879,6 +879,7 @@ int mqr_confidence(int device, const float* depths, int depth_loc, int N, int H,
     hipStream_t s = cc.s;
     ConfFrame* fr = cc.hfr;
     MQR_CHECK_HIP(hipStreamSynchronize(s));  // the previous call's upload has finished with hfr
+    if ((depth_loc == MQR_DEVICE || out_loc == MQR_DEVICE) && order_after_caller(device, s)) return 2;
     for (int i = 0; i < N; ++i) {
         fill_frame(K + 9 * i, T_cw + 16 * i, T_cw_inv + 16 * i, sd, H, W, (float)depth_max, fr[i]);
         fr[i].ok = frame_ok ? (frame_ok[i] ? 1 : 0) : 1;

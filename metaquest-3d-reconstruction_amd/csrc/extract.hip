@@ -26,7 +26,10 @@
 #include <algorithm>
 #include <cstdlib>
 
+#include <atomic>
+#include <cstring>
 #include <mutex>
+#include <thread>
 #include <tuple>
 #include <vector>
 
@@ -1632,13 +1635,102 @@ int mqr_geom_counts(mqr_geom* g, int64_t* nv, int64_t* nt) {
     return 0;
 }
 
+}  // extern "C"
+
+namespace mqr {
+// Device -> pageable host copies of large results (mqr_geom_copy).  hipMemcpy into pageable memory
+// stages through the runtime's pinned buffers on the calling thread: ~10 GB/s for the 1 GB C5 mesh,
+// the destination's first-touch page faults included (BENCH_r04 c5.extract_ms 102.9 ms).  Here
+// kD2HThreads host threads each own a stream and two pinned staging chunks: chunk k + T's DMA runs
+// while the thread copies chunk k out of the other buffer (and first-touches its destination pages),
+// and the threads' chunks interleave through the range.  The staging is kept per device (2 x 8 MB per
+// thread, pinned) and serialised by a mutex: one large copy at a time per process.
+constexpr int kD2HThreads = 8;
+constexpr size_t kD2HChunk = size_t(8) << 20;
+constexpr size_t kD2HMin = size_t(32) << 20;  // smaller copies: one hipMemcpy
+constexpr int kD2HDevices = 64;
+struct D2HStage {
+    hipStream_t s = nullptr;
+    void* buf[2] = {nullptr, nullptr};
+    hipEvent_t ev[2] = {nullptr, nullptr};
+};
+static std::mutex g_d2h_mu;
+static D2HStage g_d2h[kD2HDevices][kD2HThreads];
+
+static int d2h_parallel(int device, void* dst, const void* src, size_t bytes) {
+    MQR_REQUIRE(device >= 0 && device < kD2HDevices, "device index out of range");
+    std::lock_guard<std::mutex> lk(g_d2h_mu);
+    const size_t nchunks = (bytes + kD2HChunk - 1) / kD2HChunk;
+    const int T = (int)std::min<size_t>(kD2HThreads, nchunks);
+    std::atomic<int> failed{0};
+    std::vector<std::string> errs(T);
+    auto work = [&](int t) {
+        D2HStage& st = g_d2h[device][t];
+        auto fail = [&](const char* what, hipError_t e) {
+            errs[t] = std::string("mqr_geom_copy: ") + what + ": " + hipGetErrorString(e);
+            failed.store(1);
+        };
+        hipError_t e = hipSetDevice(device);
+        if (e == hipSuccess && !st.s) e = hipStreamCreateWithFlags(&st.s, hipStreamNonBlocking);
+        for (int b = 0; b < 2 && e == hipSuccess; ++b) {
+            if (!st.buf[b]) e = hipHostMalloc(&st.buf[b], kD2HChunk, hipHostMallocDefault);
+            if (e == hipSuccess && !st.ev[b]) e = hipEventCreateWithFlags(&st.ev[b], hipEventDisableTiming);
+        }
+        if (e != hipSuccess) return fail("staging setup", e);
+        auto len_of = [&](size_t k) { return std::min(kD2HChunk, bytes - k * kD2HChunk); };
+        auto issue = [&](size_t k, int b) {
+            hipError_t r = hipMemcpyAsync(st.buf[b], static_cast<const char*>(src) + k * kD2HChunk, len_of(k),
+                                          hipMemcpyDeviceToHost, st.s);
+            if (r == hipSuccess) r = hipEventRecord(st.ev[b], st.s);
+            return r;
+        };
+        int b = 0;
+        if ((e = issue((size_t)t, 0)) != hipSuccess) return fail("hipMemcpyAsync", e);
+        for (size_t k = (size_t)t; k < nchunks; k += (size_t)T) {
+            if (k + T < nchunks && (e = issue(k + T, b ^ 1)) != hipSuccess) {
+                (void)hipStreamSynchronize(st.s);
+                return fail("hipMemcpyAsync", e);
+            }
+            if ((e = hipEventSynchronize(st.ev[b])) != hipSuccess) {
+                (void)hipStreamSynchronize(st.s);
+                return fail("hipEventSynchronize", e);
+            }
+            std::memcpy(static_cast<char*>(dst) + k * kD2HChunk, st.buf[b], len_of(k));
+            if (failed.load()) break;
+            b ^= 1;
+        }
+        (void)hipStreamSynchronize(st.s);  // a chunk issued ahead of a failure on another thread
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < T; ++t) th.emplace_back(work, t);
+    work(0);
+    for (auto& x : th) x.join();
+    for (int t = 0; t < T; ++t)
+        if (!errs[t].empty()) {
+            set_error(errs[t]);
+            return 1;
+        }
+    return 0;
+}
+
+static int geom_copy_one(int device, void* dst, const void* src, size_t bytes, hipMemcpyKind k) {
+    if (k == hipMemcpyDeviceToHost && bytes >= kD2HMin) return d2h_parallel(device, dst, src, bytes);
+    MQR_CHECK_HIP(hipMemcpy(dst, src, bytes, k));
+    return 0;
+}
+}  // namespace mqr
+
+extern "C" {
+
 int mqr_geom_copy(mqr_geom* g, float* positions, float* normals, int32_t* triangles, int loc) {
     MQR_REQUIRE(g, "null geometry");
     MQR_CHECK_HIP(hipSetDevice(g->device));
     const hipMemcpyKind k = loc == MQR_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
-    if (positions && g->nv) MQR_CHECK_HIP(hipMemcpy(positions, g->pos, sizeof(float) * 3 * g->nv, k));
-    if (normals && g->nv) MQR_CHECK_HIP(hipMemcpy(normals, g->nrm, sizeof(float) * 3 * g->nv, k));
-    if (triangles && g->nt) MQR_CHECK_HIP(hipMemcpy(triangles, g->tri, sizeof(int32_t) * 3 * g->nt, k));
+    // hipMemcpy orders after the null stream only: the caller's stream may still use the buffers
+    if (loc == MQR_DEVICE && caller_stream()) MQR_CHECK_HIP(hipStreamSynchronize(caller_stream()));
+    if (positions && g->nv && geom_copy_one(g->device, positions, g->pos, sizeof(float) * 3 * g->nv, k)) return 1;
+    if (normals && g->nv && geom_copy_one(g->device, normals, g->nrm, sizeof(float) * 3 * g->nv, k)) return 1;
+    if (triangles && g->nt && geom_copy_one(g->device, triangles, g->tri, sizeof(int32_t) * 3 * g->nt, k)) return 1;
     return 0;
 }
 

@@ -191,6 +191,7 @@ int mqr_decode_depth(int device, const float* raw, int raw_loc, int N, int H, in
     const size_t b_vc = stage_mask ? align256(sizeof(int32_t) * total) : 0;
     const size_t b_out = stage_out ? align256(sizeof(float) * total) : 0;
     if (decode_ctx_reserve(c, std::max<size_t>(b_raw + b_conf + b_vc + b_out, 256), N)) return 1;
+    if ((!stage_raw || (any_mask && !stage_mask) || !stage_out) && order_after_caller(device, c.s)) return 2;
     for (int f = 0; f < N; ++f) {
         const double nr = nears[f], fa = fars[f];
         DecodeFrame& d = c.h_fr[f];

@@ -845,10 +845,30 @@ int mqr_xchg_create(mqr_vbg* local, int world, int rank, int mode, int root, con
     xh->rank = rank;
     xh->out = out;
     MQR_CHECK_HIP(hipStreamCreateWithFlags(&xh->st.s, hipStreamNonBlocking));
+    if (keys_loc == MQR_DEVICE && order_after_caller(xh->device, xh->st.s)) return 2;
     const size_t kb = sizeof(uint64_t) * (size_t)mx * world;
     MQR_CHECK_HIP(hipMalloc(&xh->dkeys, kb));
     MQR_CHECK_HIP(hipMemcpyAsync(xh->dkeys, gathered_keys, kb,
                                  keys_loc == MQR_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, xh->st.s));
+    // This rank's row must be its own keys in buffer order, padded with kEmpty: the plan's send lists
+    // index the local pool through it (k_gather_blocks reads buffer `send_idx`), so a foreign or
+    // reordered row would read past pool_count or merge blocks into the wrong places.
+    {
+        const int64_t n = local->pool_count;
+        std::vector<uint64_t> row((size_t)mx), mine((size_t)n);
+        MQR_CHECK_HIP(hipMemcpyAsync(row.data(), static_cast<const uint64_t*>(xh->dkeys) + (size_t)rank * mx,
+                                     sizeof(uint64_t) * mx, hipMemcpyDeviceToHost, xh->st.s));
+        if (n) MQR_CHECK_HIP(hipMemcpyAsync(mine.data(), local->bkeys, sizeof(uint64_t) * n, hipMemcpyDeviceToHost,
+                                            xh->st.s));
+        MQR_CHECK_HIP(hipStreamSynchronize(xh->st.s));
+        bool ok = std::equal(mine.begin(), mine.end(), row.begin());
+        for (int64_t i = n; ok && i < mx; ++i) ok = row[(size_t)i] == kEmpty;
+        if (!ok) {
+            set_error("mqr_xchg_create: row " + std::to_string(rank) + " of gathered_keys is not this rank's " +
+                      std::to_string(n) + " block keys in buffer order padded with 0xFF..FF");
+            return 4;
+        }
+    }
     if (xchg_prepare(xh->x, xh->st.s, static_cast<const uint64_t*>(xh->dkeys), world, mx, rank, mode, root, local,
                      out, nullptr, nullptr))
         return 1;
@@ -875,6 +895,7 @@ int mqr_xchg_send_segment(mqr_xchg* h, int peer, float* dst, int loc) {
     if (!m) return 0;
     MQR_REQUIRE(dst, "null destination");
     MQR_CHECK_HIP(hipSetDevice(h->device));
+    if (loc == MQR_DEVICE && order_after_caller(h->device, h->st.s)) return 2;
     MQR_CHECK_HIP(hipMemcpyAsync(dst, h->x.send_seg(peer), sizeof(float) * h->x.seg_floats(m),
                                  loc == MQR_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, h->st.s));
     MQR_CHECK_HIP(hipStreamSynchronize(h->st.s));
@@ -889,6 +910,7 @@ int mqr_xchg_recv_segment(mqr_xchg* h, int peer, const float* src, int loc) {
     if (!m) return 0;
     MQR_REQUIRE(src, "null source");
     MQR_CHECK_HIP(hipSetDevice(h->device));
+    if (loc == MQR_DEVICE && order_after_caller(h->device, h->st.s)) return 2;
     MQR_CHECK_HIP(hipMemcpyAsync(h->x.recv_seg(peer), src, sizeof(float) * h->x.seg_floats(m),
                                  loc == MQR_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, h->st.s));
     MQR_CHECK_HIP(hipStreamSynchronize(h->st.s));

@@ -721,6 +721,7 @@ int mqr_mesh_filter_components(int device, const float* vertices, const float* n
     MQR_REQUIRE(c.open(device, (size_t)(128 * nt + 96 * nv) + ((size_t)32 << 20)) == 0,
                 "mesh filter: device allocation failed");
     const hipMemcpyKind k = loc == MQR_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    if (loc == MQR_DEVICE && order_after_caller(device, c.s)) return 2;
     Mesh m;
     m.nv = nv;
     m.nt = nt;

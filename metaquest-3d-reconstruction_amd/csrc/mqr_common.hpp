@@ -242,5 +242,12 @@ void* geom_block_alloc(int device, size_t bytes, size_t* cap);
 void geom_block_release(int device, void* p, size_t cap);
 int grow_pool(mqr_vbg* v, int64_t need);
 int sync_all(mqr_vbg* v);
+// Caller-stream ordering (mqr_set_stream, include/mqr.h): the library streams `a` (and `b`) wait for
+// every command the calling thread's caller stream holds so far.  Called by each entry point that
+// reads or writes caller MQR_DEVICE buffers, before its first command on them (the current device
+// must be `device`).  Every entry point drains its own streams before it returns, so outputs need
+// no ordering in the other direction.
+int order_after_caller(int device, hipStream_t a, hipStream_t b = nullptr);
+hipStream_t caller_stream();  // the calling thread's caller stream (nullptr: the null stream)
 int activate_ordered(mqr_vbg* v, const uint64_t* dkeys, int64_t n);  // empty volume, buffer i = key i
 }  // namespace mqr

@@ -602,6 +602,7 @@ int mqr_scene_add_triangles(mqr_scene* s, const float* vertices, int64_t nv, con
     g.nv = nv;
     g.nt = nt;
     const hipMemcpyKind k = loc == MQR_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    if (loc == MQR_DEVICE && order_after_caller(s->device, s->stream)) return 2;
     MQR_CHECK_HIP(hipMalloc(&g.v, sizeof(float) * 3 * std::max<int64_t>(nv, 1)));
     MQR_CHECK_HIP(hipMalloc(&g.t, sizeof(int32_t) * 3 * std::max<int64_t>(nt, 1)));
     if (nv) MQR_CHECK_HIP(hipMemcpyAsync(g.v, vertices, sizeof(float) * 3 * nv, k, s->stream));
@@ -627,6 +628,7 @@ int mqr_scene_cast_pinhole(mqr_scene* s, const double* K, const double* T_wc, in
     MQR_CHECK_HIP(hipSetDevice(s->device));
     if (build(s)) return 1;
     const int64_t HW = (int64_t)H * W, total = HW * n_frames;
+    if (out_loc == MQR_DEVICE && order_after_caller(s->device, s->stream)) return 2;
     std::vector<PinholeFrame> hf(n_frames);
     for (int f = 0; f < n_frames; ++f) hf[f] = pinhole(K + 9 * f, T_wc + 16 * f);
     PinholeFrame* d_fr = nullptr;
@@ -690,6 +692,7 @@ int mqr_scene_cast_rays(mqr_scene* s, const float* rays, int64_t nrays, int rays
     MQR_CHECK_HIP(hipSetDevice(s->device));
     if (build(s)) return 1;
     if (nrays == 0) return 0;
+    if ((rays_loc == MQR_DEVICE || out_loc == MQR_DEVICE) && order_after_caller(s->device, s->stream)) return 2;
     std::vector<void*> owned;
     auto dalloc = [&](size_t bytes) {
         void* p = nullptr;

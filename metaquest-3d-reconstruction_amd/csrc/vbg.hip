@@ -32,6 +32,42 @@ static thread_local std::string g_err;
 void set_error(const std::string& msg) { g_err = msg; }
 const char* get_error() { return g_err.c_str(); }
 
+// mqr_set_stream: the calling thread's caller stream (nullptr = the null stream) and one ordering
+// event per device.  The event is recorded with a device-scope release: the producer (a kernel or a
+// copy the caller enqueued) and the consumer (a library kernel) are on the same device, and the
+// consumer's dispatch acquires as every kernel launch does.  The events are never destroyed: a
+// thread-exit destructor could run after the HIP runtime has been torn down.
+static constexpr int kOrderDevices = 64;
+static thread_local hipStream_t t_caller_stream = nullptr;
+static thread_local hipEvent_t t_order_ev[kOrderDevices] = {};
+
+hipStream_t caller_stream() { return t_caller_stream; }
+
+int order_after_caller(int device, hipStream_t a, hipStream_t b) {
+    MQR_REQUIRE(device >= 0 && device < kOrderDevices, "device index out of range");
+    if (t_caller_stream) {
+        hipDevice_t sd = -1;
+        if (hipStreamGetDevice(t_caller_stream, &sd) != hipSuccess || sd != device) {
+            (void)hipGetLastError();
+            set_error("the caller stream given to mqr_set_stream belongs to device " + std::to_string((int)sd) +
+                      ", the call works on device " + std::to_string(device) +
+                      ": pass a stream of that device (torch: torch.cuda.set_device / torch.cuda.stream)");
+            return 2;
+        }
+    }
+    hipEvent_t& e = t_order_ev[device];
+    if (!e) MQR_CHECK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventDisableSystemFence));
+    if (hipEventRecord(e, t_caller_stream) != hipSuccess) {
+        (void)hipGetLastError();  // not left behind for a later launch check
+        set_error("the caller stream given to mqr_set_stream cannot be waited on from device " +
+                  std::to_string(device) + " (a stream of another device, or destroyed)");
+        return 2;
+    }
+    MQR_CHECK_HIP(hipStreamWaitEvent(a, e, 0));
+    if (b) MQR_CHECK_HIP(hipStreamWaitEvent(b, e, 0));
+    return 0;
+}
+
 void make_frame_params(const double* K, const double* T, FrameParams* fp) {
     fp->fx = (float)K[0];
     fp->fy = (float)K[4];
@@ -744,6 +780,17 @@ int mqr_vbg_last_kernel(mqr_vbg* v, int* variant) {
 }
 const char* mqr_last_error(void) { return get_error(); }
 
+int mqr_set_stream(void* stream) {
+    t_caller_stream = static_cast<hipStream_t>(stream);
+    return 0;
+}
+
+int mqr_get_stream(void** stream) {
+    MQR_REQUIRE(stream, "null argument");
+    *stream = t_caller_stream;
+    return 0;
+}
+
 int mqr_device_count(int* n) {
     MQR_CHECK_HIP(hipGetDeviceCount(n));
     return 0;
@@ -763,6 +810,9 @@ int mqr_device_free(int device, void* ptr) {
 
 int mqr_memcpy(void* dst, int dst_loc, const void* src, int src_loc, int64_t bytes, int device) {
     MQR_CHECK_HIP(hipSetDevice(device));
+    // hipMemcpy orders after the null stream only: wait for the caller stream's work on the buffers
+    if ((dst_loc == MQR_DEVICE || src_loc == MQR_DEVICE) && t_caller_stream)
+        MQR_CHECK_HIP(hipStreamSynchronize(t_caller_stream));
     hipMemcpyKind kind = dst_loc == MQR_DEVICE ? (src_loc == MQR_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice)
                                                : (src_loc == MQR_DEVICE ? hipMemcpyDeviceToHost : hipMemcpyHostToHost);
     MQR_CHECK_HIP(hipMemcpy(dst, src, (size_t)bytes, kind));
@@ -895,6 +945,8 @@ int mqr_integrate_frames(mqr_vbg* v, const float* depths, int depth_loc, int B, 
     MQR_REQUIRE(v && depths && K && T_wc, "null argument");
     MQR_REQUIRE(B >= 0 && H > 0 && W > 0, "bad frame shape");
     MQR_CHECK_HIP(hipSetDevice(v->device));
+    // device frames: both streams read them (touch, integrate) -- ordered after the caller's writes
+    if (depth_loc == MQR_DEVICE && order_after_caller(v->device, v->stream, v->stream2)) return 2;
     const int64_t HW = (int64_t)H * W;
     const float sdf_trunc = v->voxel_size * trunc_mult;
     const float block_size = v->voxel_size * v->R;
@@ -999,6 +1051,7 @@ int mqr_touch(mqr_vbg* v, const float* depth, int depth_loc, int H, int W, const
     MQR_REQUIRE(v && depth && K && T_wc && keys_out && n_out, "null argument");
     MQR_CHECK_HIP(hipSetDevice(v->device));
     if (sync_all(v)) return 1;
+    if (depth_loc == MQR_DEVICE && order_after_caller(v->device, v->stream)) return 2;
     const int64_t HW = (int64_t)H * W;
     const int64_t max_touch = 4LL * (H / 4) * (W / 4);
     const int64_t want = next_pow2(2 * std::max<int64_t>(max_touch, 1));
@@ -1046,6 +1099,7 @@ int mqr_integrate(mqr_vbg* v, const int32_t* keys, int64_t n, const float* depth
     MQR_CHECK_HIP(hipSetDevice(v->device));
     if (n == 0) return 0;
     if (sync_all(v)) return 1;
+    if (depth_loc == MQR_DEVICE && order_after_caller(v->device, v->stream, v->stream2)) return 2;
     const int64_t HW = (int64_t)H * W;
     if (ensure_table(v, v->pool_count + n)) return 1;
     const float* dptr = depth;
@@ -1081,6 +1135,7 @@ int mqr_vbg_export(mqr_vbg* v, int32_t* keys, float* tsdf, float* weight, int lo
     if (sync_all(v)) return 1;
     const int64_t n = v->pool_count;
     if (n == 0) return 0;
+    if (loc == MQR_DEVICE && order_after_caller(v->device, v->stream)) return 2;  // the caller may still read them
     int32_t* dk = keys;
     float* dt = tsdf;
     float* dw = weight;
@@ -1124,6 +1179,8 @@ int mqr_vbg_import(mqr_vbg* v, const int32_t* keys, const float* tsdf, const flo
     MQR_REQUIRE(v && ((keys && tsdf && weight) || n == 0), "null argument");
     MQR_CHECK_HIP(hipSetDevice(v->device));
     if (n == 0) return 0;
+    if (sync_all(v)) return 1;
+    if (loc == MQR_DEVICE && order_after_caller(v->device, v->stream)) return 2;
     const int32_t* dk = keys;
     const float* dt = tsdf;
     const float* dw = weight;
@@ -1160,6 +1217,7 @@ int mqr_vbg_pack_weighted(mqr_vbg* v, const int32_t* union_keys, int64_t U, floa
     MQR_CHECK_HIP(hipSetDevice(v->device));
     if (U == 0) return 0;
     if (sync_all(v)) return 1;
+    if (order_after_caller(v->device, v->stream)) return 2;
     hipLaunchKernelGGL(k_pack, dim3((unsigned)U), dim3(256), 0, v->stream, union_keys, U, v->tab, v->pool, (int)v->R3,
                        reinterpret_cast<float2*>(packed));
     MQR_CHECK_HIP(hipGetLastError());
@@ -1171,6 +1229,8 @@ int mqr_vbg_unpack_weighted(mqr_vbg* v, const int32_t* union_keys, int64_t U, co
     MQR_REQUIRE(v && (U == 0 || (union_keys && packed)), "null argument");
     MQR_CHECK_HIP(hipSetDevice(v->device));
     if (U == 0) return 0;
+    if (sync_all(v)) return 1;
+    if (order_after_caller(v->device, v->stream)) return 2;
     if (activate_device_keys(v, union_keys, U)) return 1;
     hipLaunchKernelGGL(k_unpack, dim3((unsigned)U), dim3(256), 0, v->stream, union_keys, U, v->tab, v->pool,
                        (int)v->R3, reinterpret_cast<const float2*>(packed));

@@ -7,6 +7,8 @@ from __future__ import annotations
 
 import ctypes
 import os
+import sys
+import threading
 
 import numpy as np
 
@@ -38,6 +40,8 @@ SIGNATURES = {
     "mqr_build_tag": (ctypes.c_int, [ctypes.c_int, ctypes.c_char_p, ctypes.c_int]),
     "mqr_vbg_last_kernel": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int)]),
     "mqr_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+    "mqr_set_stream": (ctypes.c_int, [_vp]),
+    "mqr_get_stream": (ctypes.c_int, [ctypes.POINTER(_vp)]),
     "mqr_device_alloc": (ctypes.c_int, [ctypes.c_int, ctypes.c_int64, ctypes.POINTER(_vp)]),
     "mqr_device_free": (ctypes.c_int, [ctypes.c_int, _vp]),
     "mqr_memcpy": (ctypes.c_int, [_vp, ctypes.c_int, _vp, ctypes.c_int, ctypes.c_int64, ctypes.c_int]),
@@ -194,8 +198,42 @@ def load(path: str = LIB_PATH):
     return L
 
 
+# Entry points that may read or write caller device buffers: before each, the thread's caller stream
+# (include/mqr.h "stream ordering") is set to torch's current stream, so tensors torch is still
+# writing on any stream -- the default one or a side stream under ``torch.cuda.stream(s)`` -- are
+# complete before the library reads them.
+ORDERED = frozenset({
+    "mqr_touch", "mqr_integrate", "mqr_integrate_frames", "mqr_vbg_export", "mqr_vbg_import",
+    "mqr_vbg_pack_weighted", "mqr_vbg_unpack_weighted", "mqr_xchg_create", "mqr_xchg_send_segment",
+    "mqr_xchg_recv_segment", "mqr_geom_copy", "mqr_confidence", "mqr_decode_depth", "mqr_color_vertices",
+    "mqr_color_map", "mqr_scene_add_triangles", "mqr_scene_cast_pinhole", "mqr_scene_cast_rays",
+    "mqr_mesh_filter_components", "mqr_memcpy",
+})
+_tls = threading.local()
+
+
+def torch_stream() -> int:
+    """torch's current stream (its handle) once torch has initialised HIP in this process, else 0
+    (the null stream -- nothing torch-side can be pending)."""
+    torch = sys.modules.get("torch")
+    if torch is None or not torch.cuda.is_initialized():
+        return 0
+    return int(torch.cuda.current_stream().cuda_stream)
+
+
+def set_stream(stream: int):
+    """Make `stream` (a hipStream_t handle, 0 = null stream) this thread's caller stream."""
+    if getattr(_tls, "stream", None) != stream:
+        rc = load().mqr_set_stream(ctypes.c_void_p(stream or None))
+        if rc != 0:
+            raise MqrError(f"mqr_set_stream failed ({rc})", rc)
+        _tls.stream = stream
+
+
 def call(name, *args):
     L = load()
+    if name in ORDERED:
+        set_stream(torch_stream())
     rc = getattr(L, name)(*args)
     if rc != 0:
         msg = L.mqr_last_error().decode(errors="replace")

@@ -284,14 +284,15 @@ def merge_local(vbgs, mode: str = "sharded", root: int = 0, outs=None):
     return list(zip(outs, owned.tolist()))
 
 
-def merge_staged(vbg, group=None, mode: str = "sharded", root: int = 0, out=None, check_counts: bool = True):
+def merge_staged(vbg, group=None, mode: str = "sharded", root: int = 0, out=None):
     """mqr_reduce_rccl's exchange with the segments carried by torch.distributed over host buffers
     (gloo): one process per rank, any device (several ranks may share one GPU, which RCCL refuses).
     The plan, the send segments (packed from this rank's pool), the rank-ordered merge and the output
     are libmqr's own (mqr_xchg_*); only the ncclSend / ncclRecv of the segments is replaced by
-    isend / irecv of host tensors.  With check_counts every rank's send count to each peer is
-    compared with that peer's receive count from it (an all-to-all of the counts) before any
-    segment moves.  Returns (out volume, owned block count)."""
+    isend / irecv of host tensors.  Every rank's send count to each peer is compared with that
+    peer's receive count from it (an all-to-all of the counts) before any segment moves, and
+    mqr_xchg_create checks that this rank's row of the gathered keys is its own.  Returns (out
+    volume, owned block count)."""
     import ctypes
     import torch
     import torch.distributed as dist
@@ -315,12 +316,11 @@ def merge_staged(vbg, group=None, mode: str = "sharded", root: int = 0, out=None
         sc, rc = np.zeros(world, np.int64), np.zeros(world, np.int64)
         fpb = ctypes.c_int64()
         _lib.call("mqr_xchg_counts", h, _lib.ptr(sc, _lib._i64p), _lib.ptr(rc, _lib._i64p), None, ctypes.byref(fpb))
-        if check_counts:
-            theirs = torch.empty(world, dtype=torch.int64)
-            dist.all_to_all_single(theirs, torch.from_numpy(sc.copy()), group=group)
-            if not np.array_equal(theirs.numpy(), rc):
-                raise RuntimeError(f"merge_staged: rank {rank} expects {rc.tolist()} blocks from the ranks, "
-                                   f"which send it {theirs.numpy().tolist()}")
+        theirs = torch.empty(world, dtype=torch.int64)
+        dist.all_to_all_single(theirs, torch.from_numpy(sc.copy()), group=group)
+        if not np.array_equal(theirs.numpy(), rc):
+            raise RuntimeError(f"merge_staged: rank {rank} expects {rc.tolist()} blocks from the ranks, "
+                               f"which send it {theirs.numpy().tolist()}")
         ops, recvs = [], []
         for p in range(world):
             if p == rank:

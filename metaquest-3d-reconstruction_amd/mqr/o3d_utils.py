@@ -26,7 +26,7 @@ from .meshfilter import filter_mesh_components  # noqa: F401  (re-exported: o3d_
 from .raycasting import raycast_in_color_view  # noqa: F401  (re-exported: o3d_utils.py:324-341)
 from .vbg import VoxelBlockGrid
 
-CHUNK = 64  # frames per host->device hand-off (device batches are <= 64 frames)
+CHUNK = 127  # frames per host->device hand-off: one full device batch (kMaxBatch, csrc/mqr_common.hpp)
 
 
 def compute_o3d_intrinsic_matrices(dataset) -> np.ndarray:

@@ -146,18 +146,21 @@ def test_c2_room_320x320(vbg_mod):
 
 
 def test_c3_confidence_mask_integrate(vbg_mod, c2_seq):
-    """C3: confidence of every frame (r = 10) on the GPU, checked against the oracle on reference
-    frames at both window edges and in the middle; then the masked sequence integrates
+    """C3: confidence of every frame (r = 10) on the GPU, checked against the oracle on ALL 500
+    reference frames (the float32 prefilter decides ~99.6 % of the (pixel, neighbour) pairs: every
+    frame's maps must stay bit-identical, not a sample); then the masked sequence integrates
     identically on both sides."""
     from mqr.confidence import confidence_maps
     seq = c2_seq
     depth, K, Tcw = seq["depth"], seq["K"], seq["T_cw"]
     Ti = np.linalg.inv(Tcw)
     conf, valid = confidence_maps(depth, K, Tcw, Ti, 0, len(depth), 10, 4.0, 0.08)
-    for i in (0, 9, 10, 250, 490, 499):
+    bad = []
+    for i in range(len(depth)):
         oc, ov = oracle.confidence(depth, K, Tcw, Ti, i, 10, 4.0, 0.08)
-        assert np.array_equal(valid[i], ov), i
-        assert np.array_equal(conf[i], oc), i
+        if not (np.array_equal(valid[i], ov) and np.array_equal(conf[i], oc)):
+            bad.append(i)
+    assert not bad, f"confidence maps differ from the oracle at reference frames {bad[:20]}"
     masked = depth.copy()
     masked[conf < 0.02] = 0.0  # o3d_utils.py:141-142 with the pipeline's thresholds
     masked[valid < 2] = 0.0

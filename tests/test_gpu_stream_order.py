@@ -1,0 +1,137 @@
+"""Stream ordering at the C-ABI boundary (include/mqr.h "stream ordering", mqr_set_stream).
+
+libmqr runs on its own non-blocking HIP streams.  A caller that hands it a device tensor torch has
+just written on a side stream -- with no synchronize in between -- must get the result of the
+written frames, never of the bytes that were there before.  Each test delays the side stream by a
+spin kernel, enqueues the write behind it and calls the library at once (inside
+``torch.cuda.stream(s)``, so the Python layer passes s as the caller stream); the outputs are
+compared with the CPU oracle.  Without the ordering the library would read the frames ~50 ms before
+they land (round 4's N>1 rehearsal abort, gpurun_out/r04a_bench2.err: "No block is touched")."""
+import ctypes
+
+import numpy as np
+import pytest
+
+import oracle  # the test-only checker (tests/conftest.py puts oracle/ on the path)
+
+pytestmark = pytest.mark.gpu
+
+_SPIN = 100_000_000  # spin-kernel cycles (~40-50 ms at the MI355X shader clock)
+
+
+class _Dev:
+    def __init__(self, t):
+        self.ptr = ctypes.c_void_p(t.data_ptr())
+
+
+def _late_copy(torch, host, s):
+    """A device tensor whose contents land on stream `s` only after a spin kernel: poisoned first
+    (NaN, which touches nothing), then the host frames copied in behind the spin."""
+    dev = torch.full(host.shape, float("nan"), dtype=torch.float32, device="cuda")
+    pinned = torch.from_numpy(host).pin_memory()
+    torch.cuda.synchronize()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        torch.cuda._sleep(_SPIN)
+        dev.copy_(pinned, non_blocking=True)
+    dev.record_stream(s)
+    return dev
+
+
+def test_integrate_frames_after_side_stream_write():
+    import torch
+    from gpu_helpers import compare_volumes
+    from mqr import synthetic
+    from mqr.vbg import VoxelBlockGrid
+    seq = synthetic.make_sequence("room", n=24, height=240, width=320, f=262.5, noise=True, seed=7)
+    B, H, W = seq["depth"].shape
+    K, T = seq["K"].astype(np.float64), seq["T_wc"].astype(np.float64)
+    s = torch.cuda.Stream()
+    dev = _late_copy(torch, np.ascontiguousarray(seq["depth"], np.float32), s)
+    vbg = VoxelBlockGrid(voxel_size=0.01, block_resolution=16, block_count=256, device="cuda:0")
+    with torch.cuda.stream(s):  # no synchronize: the library orders itself after s
+        vbg.integrate_frames((_Dev(dev), B, H, W), K, T, depth_scale=1.0, depth_max=4.0, trunc_voxel_multiplier=10.0)
+    ref = oracle.OracleVBG(0.01, 16, 256)
+    for i in range(B):
+        ref.integrate_frame(seq["depth"][i], K[i], T[i], 1.0, 4.0, 10.0)
+    assert compare_volumes(vbg.export(), ref.export(), 0.0) == 0.0
+
+
+def test_default_stream_write_is_ordered_too():
+    """The same with torch's default stream as the writer (the caller stream is then the null stream)."""
+    import torch
+    from gpu_helpers import compare_volumes
+    from mqr import synthetic
+    from mqr.vbg import VoxelBlockGrid
+    seq = synthetic.make_sequence("sphere", n=8, height=120, width=160, f=131.25, noise=True, seed=3)
+    B, H, W = seq["depth"].shape
+    K, T = seq["K"].astype(np.float64), seq["T_wc"].astype(np.float64)
+    dev = torch.full((B, H, W), float("nan"), dtype=torch.float32, device="cuda")
+    pinned = torch.from_numpy(np.ascontiguousarray(seq["depth"], np.float32)).pin_memory()
+    torch.cuda.synchronize()
+    torch.cuda._sleep(_SPIN)
+    dev.copy_(pinned, non_blocking=True)
+    vbg = VoxelBlockGrid(voxel_size=0.02, block_resolution=16, block_count=64, device="cuda:0")
+    vbg.integrate_frames((_Dev(dev), B, H, W), K, T, depth_scale=1.0, depth_max=3.0, trunc_voxel_multiplier=4.0)
+    ref = oracle.OracleVBG(0.02, 16, 64)
+    for i in range(B):
+        ref.integrate_frame(seq["depth"][i], K[i], T[i], 1.0, 3.0, 4.0)
+    assert compare_volumes(vbg.export(), ref.export(), 0.0) == 0.0
+
+
+def test_confidence_and_decode_after_side_stream_write():
+    import torch
+    from mqr import _lib, synthetic
+    seq = synthetic.make_sequence("room", n=6, height=120, width=160, f=131.25, noise=True, seed=5)
+    B, H, W = seq["depth"].shape
+    Tcw = seq["T_cw"].astype(np.float32)
+    Tci = np.linalg.inv(seq["T_cw"]).astype(np.float32)
+    K32 = np.ascontiguousarray(seq["K"], np.float32)
+    s = torch.cuda.Stream()
+    # confidence maps of frames that land late on s, written into tensors torch still clears on s
+    dev = _late_copy(torch, np.ascontiguousarray(seq["depth"], np.float32), s)
+    with torch.cuda.stream(s):
+        conf = torch.full((B, H, W), -1.0, dtype=torch.float64, device="cuda")
+        valid = torch.full((B, H, W), -1, dtype=torch.int32, device="cuda")
+        _lib.call("mqr_confidence", 0, ctypes.c_void_p(dev.data_ptr()), _lib.MQR_DEVICE, B, H, W,
+                  _lib.ptr(K32, _lib._f32p), _lib.ptr(np.ascontiguousarray(Tcw.reshape(B, 16)), _lib._f32p),
+                  _lib.ptr(np.ascontiguousarray(Tci.reshape(B, 16)), _lib._f32p), None, 0, B, 2, 3.0, 0.05,
+                  ctypes.c_void_p(conf.data_ptr()), ctypes.c_void_p(valid.data_ptr()), _lib.MQR_DEVICE)
+        c, v = conf.cpu().numpy(), valid.cpu().numpy()
+    for i in (0, B // 2, B - 1):
+        oc, ov = oracle.confidence(seq["depth"], seq["K"], seq["T_cw"], np.linalg.inv(seq["T_cw"]), i, 2, 3.0, 0.05)
+        assert np.array_equal(v[i], ov) and np.array_equal(c[i], oc), f"confidence of frame {i} differs"
+    # device ingestion of raw NDC buffers that land late on s
+    raw = np.ascontiguousarray(seq["raw"], np.float32)
+    draw = _late_copy(torch, raw, s)
+    nears = np.full(B, 0.1, np.float64)
+    fars = np.full(B, np.inf, np.float64)
+    ok = np.zeros(B, np.uint8)
+    with torch.cuda.stream(s):
+        out = torch.zeros((B, H, W), dtype=torch.float32, device="cuda")
+        _lib.call("mqr_decode_depth", 0, ctypes.c_void_p(draw.data_ptr()), _lib.MQR_DEVICE, B, H, W,
+                  _lib.ptr(nears, _lib._f64p), _lib.ptr(fars, _lib._f64p), None, None, None, None, _lib.MQR_HOST,
+                  0.0, 0, ctypes.c_void_p(out.data_ptr()), _lib.MQR_DEVICE, _lib.ptr(ok, _lib._u8p))
+        got = out.cpu().numpy()
+    ref = np.empty_like(got)
+    ref_ok = np.zeros(B, np.uint8)
+    _lib.call("mqr_decode_depth", 0, _lib.ptr(raw), _lib.MQR_HOST, B, H, W, _lib.ptr(nears, _lib._f64p),
+              _lib.ptr(fars, _lib._f64p), None, None, None, None, _lib.MQR_HOST, 0.0, 0, _lib.ptr(ref),
+              _lib.MQR_HOST, _lib.ptr(ref_ok, _lib._u8p))
+    assert np.array_equal(ok, ref_ok)
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+
+
+def test_caller_stream_is_set_per_call():
+    """The Python layer passes torch's current stream before every ordered entry point."""
+    import torch
+    from mqr import _lib
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        _lib.set_stream(_lib.torch_stream())
+        got = ctypes.c_void_p()
+        _lib.call("mqr_get_stream", ctypes.byref(got))
+        assert (got.value or 0) == s.cuda_stream
+    _lib.set_stream(_lib.torch_stream())
+    _lib.call("mqr_get_stream", ctypes.byref(got))
+    assert (got.value or 0) == torch.cuda.current_stream().cuda_stream

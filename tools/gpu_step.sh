@@ -1,0 +1,79 @@
+#!/bin/bash
+# One parameterised GPU call (replaces round 4's per-iteration tools/gpu_r04*.sh scripts).
+#   STEPS="tests bench n2 ..." bash tools/gpu_step.sh      (run under gpurun, from the repo root)
+# Steps, run in the order given, each under its own time limit, the call ending at the first failure:
+#   tests       the whole `pytest -m gpu` suite                      -> gpurun_out/${TAG}_gpu_tests.log
+#   tests:F     pytest -m gpu on the test files F (comma separated)   -> gpurun_out/${TAG}_gpu_tests.log
+#   smoke       __graft_entry__.smoke()                               -> gpurun_out/${TAG}_smoke.log
+#   bench       the default bench line (N = 1)                        -> gpurun_out/${TAG}_bench.json
+#   benchq      a short bench (no C4 / C5 / drop-in legs)             -> gpurun_out/${TAG}_benchq.json
+#   n2          2-rank rehearsal on one GPU (gloo-staged merge)        -> gpurun_out/${TAG}_bench_n2.json
+#   prof        rocprofv3 --kernel-trace --stats of the C2 bench      -> gpurun_out/${TAG}_bench_kernel_stats.csv
+#   profc5      the same over the C5 leg alone                        -> gpurun_out/${TAG}_c5_kernel_stats.csv
+#   traffic     FETCH_SIZE / WRITE_SIZE passes (tools/pmc_traffic.sh) -> profiles/${TAG}_pmc_traffic.json
+#   abint:V     tools/ab_integrate.py over integrate variants V (comma separated, A/B library)
+#   abext:M     tools/ab_extract.py over extraction modes M (A/B library)
+#   conf        tools/conf_workload.py (the confidence kernel alone)
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+TAG=${TAG:-r05}
+PYT="python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu"
+for step in ${STEPS:-tests}; do
+  echo "== $step ($(date +%H:%M:%S))"
+  case "$step" in
+    tests)
+      timeout -k 10 900 $PYT tests > gpurun_out/${TAG}_gpu_tests.log 2>&1 || { tail -40 gpurun_out/${TAG}_gpu_tests.log; exit 1; }
+      tail -1 gpurun_out/${TAG}_gpu_tests.log ;;
+    tests:*)
+      files=$(echo "${step#tests:}" | tr ',' ' ')
+      timeout -k 10 900 $PYT $files > gpurun_out/${TAG}_gpu_tests.log 2>&1 || { tail -40 gpurun_out/${TAG}_gpu_tests.log; exit 1; }
+      tail -1 gpurun_out/${TAG}_gpu_tests.log ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1 || { tail -20 gpurun_out/${TAG}_smoke.log; exit 1; }
+      tail -1 gpurun_out/${TAG}_smoke.log ;;
+    bench)
+      timeout -k 10 900 python bench.py > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err || { tail -30 gpurun_out/${TAG}_bench.err; exit 1; }
+      tail -c 400 gpurun_out/${TAG}_bench.json ;;
+    benchq)
+      timeout -k 10 600 python bench.py --no-c4 --no-c5 --e2e-frames 0 > gpurun_out/${TAG}_benchq.json 2> gpurun_out/${TAG}_benchq.err || { tail -30 gpurun_out/${TAG}_benchq.err; exit 1; }
+      tail -c 400 gpurun_out/${TAG}_benchq.json ;;
+    n2)
+      MQR_BENCH_WRAP_DEVICES=1 timeout -k 10 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+        --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 10 --warmup 2 --weak-steps 10 \
+        > gpurun_out/${TAG}_bench_n2.json 2> gpurun_out/${TAG}_bench_n2.err || { tail -40 gpurun_out/${TAG}_bench_n2.err; exit 1; }
+      tail -c 600 gpurun_out/${TAG}_bench_n2.json ;;
+    prof)
+      rm -rf gpurun_out/prof
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/prof -o run -- \
+        python bench.py --no-cpu --no-extras --steps 50 --warmup 5 --touch-steps 0 > gpurun_out/${TAG}_prof_bench.json 2> gpurun_out/${TAG}_prof_bench.err \
+        || { tail -20 gpurun_out/${TAG}_prof_bench.err; exit 1; }
+      find gpurun_out/prof -name "*kernel_stats.csv" -exec cp {} gpurun_out/${TAG}_bench_kernel_stats.csv \;
+      grep "mqr" gpurun_out/${TAG}_bench_kernel_stats.csv | cut -c1-70 | head -12 ;;
+    profc5)
+      rm -rf gpurun_out/profc5
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/profc5 -o run -- \
+        python bench.py --c5-only --no-parity > gpurun_out/${TAG}_prof_c5.json 2> gpurun_out/${TAG}_prof_c5.err \
+        || { tail -20 gpurun_out/${TAG}_prof_c5.err; exit 1; }
+      find gpurun_out/profc5 -name "*kernel_stats.csv" -exec cp {} gpurun_out/${TAG}_c5_kernel_stats.csv \;
+      grep "mqr" gpurun_out/${TAG}_c5_kernel_stats.csv | cut -c1-70 | head -16 ;;
+    traffic)
+      ROUND=$TAG timeout -k 10 600 bash tools/pmc_traffic.sh > gpurun_out/${TAG}_pmc_traffic.log 2>&1 || { tail -20 gpurun_out/${TAG}_pmc_traffic.log; exit 1; }
+      mkdir -p gpurun_out/profiles_new && cp profiles/${TAG}_pmc_traffic.json profiles/${TAG}_pmc_fetch.csv profiles/${TAG}_pmc_write.csv gpurun_out/profiles_new/
+      grep -E "traffic_bytes_per_launch|traffic_over_alg" profiles/${TAG}_pmc_traffic.json ;;
+    abint:*)
+      MQR_HIP_LIB="$PWD/tools/_ab/libmqr_ab.so" timeout -k 10 600 python -u tools/ab_integrate.py --check --rounds 7 --variants "${step#abint:}" \
+        > gpurun_out/${TAG}_abint.json 2> gpurun_out/${TAG}_abint.err || { tail -20 gpurun_out/${TAG}_abint.err; exit 1; }
+      cat gpurun_out/${TAG}_abint.json ;;
+    abext:*)
+      MQR_HIP_LIB="$PWD/tools/_ab/libmqr_ab.so" timeout -k 10 600 python -u tools/ab_extract.py --modes "${step#abext:}" --reps 21 \
+        > gpurun_out/${TAG}_abext.json 2> gpurun_out/${TAG}_abext.err || { tail -20 gpurun_out/${TAG}_abext.err; exit 1; }
+      cat gpurun_out/${TAG}_abext.json ;;
+    conf)
+      timeout -k 10 300 python -u tools/conf_workload.py > gpurun_out/${TAG}_conf.json 2> gpurun_out/${TAG}_conf.err || { tail -20 gpurun_out/${TAG}_conf.err; exit 1; }
+      cat gpurun_out/${TAG}_conf.json ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "steps done"
