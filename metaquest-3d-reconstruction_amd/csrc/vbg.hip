@@ -425,7 +425,7 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
     //     ballot skip of out-of-image wave slots, ran 0.70 vs 0.48 ms per launch: removed.)
     //     DESIGN.md §4.1 has the measurements behind the choice.
     int var = v->kernel_variant;
-    if (var < 0 || var > 23) var = 0;
+    if (var < 0 || var > 31) var = 0;
     if (!MQR_AB && var != 1 && var != 2 && var != 4) var = 0;
     if (var != 1 && var != 2 && !lean_ok) var = 2;
     if (var == 5 && (v->R != 16 || W % 4 != 0 || W < 4 || (reinterpret_cast<uintptr_t>(depths) & 15))) var = 0;
@@ -452,6 +452,24 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
                                depth_frame, depth_scale, depth_max, sdf_trunc, first_new);
         } else {
 #if MQR_AB
+            // k_integrate_win (8-byte windows): 24 = the default's plain frame loop, 25 = software-pipelined
+            // frames at >= 6 waves / SIMD, 26 / 27 = 1024 threads (4 voxels each) pipelined / plain at >= 8,
+            // 28 = pipelined forced to >= 7 waves / SIMD; 29 / 30 = half-frame pipeline, 512 threads at >= 7
+            // waves / 1024 threads at >= 8, 31 = half-frame pipeline, 512 threads at >= 6 waves
+            if (var >= 24 && var <= 31) {
+                auto win = [&](auto kern, unsigned nt) {
+                    hipLaunchKernelGGL(kern, dim3(grid), dim3(nt), 0, s, list, lmask, counters, v->list_cap, t, v->pool,
+                                       v->voxel_size, depths, HW, H, W, fp, depth_frame, depth_max, sdf_trunc, first_new);
+                };
+                if (var == 24) win(k_integrate_win<512, 7, 0>, 512);
+                else if (var == 25) win(k_integrate_win<512, 6, 1>, 512);
+                else if (var == 26) win(k_integrate_win<1024, 8, 1>, 1024);
+                else if (var == 27) win(k_integrate_win<1024, 8, 0>, 1024);
+                else if (var == 28) win(k_integrate_win<512, 7, 1>, 512);
+                else if (var == 29) win(k_integrate_win<512, 7, 2>, 512);
+                else if (var == 30) win(k_integrate_win<1024, 8, 2>, 1024);
+                else win(k_integrate_win<512, 6, 2>, 512);
+            } else
             if (var == 8)  // VALU-lean projection / update (lean_gather_v)
                 hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 8, 2, 2>), dim3(lean_grid), dim3(512), 0, s, list,
                                    lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H,
@@ -544,7 +562,7 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
                                    0, s, list, lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size,
                                    depths, HW, H, W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
             // exact fix-up of the blocks the other fast kernels handed back (usually none: reads a zero count)
-            if (var != 0 && var != 23)
+            if (var != 0 && var != 23 && var < 24)
                 hipLaunchKernelGGL((k_integrate_t<16, 4, 512>), dim3(8), dim3(512), 0, s, bad_list, bad_mask, bad_count,
                                    v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp, depth_frame,
                                    depth_scale, depth_max, sdf_trunc, first_new);

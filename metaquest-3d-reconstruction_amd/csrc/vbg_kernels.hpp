@@ -1001,6 +1001,164 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
     }
 }
 
+// ---- window-read integrate with a software-pipelined frame loop (R = 16) -------------------------------
+// k_integrate_lean<16, 512, brick, WPE, 2, 8-byte windows, FIXIN>'s arithmetic (lean_gather_w /
+// lean_update_v: bit-identical), with the brick map generalised to NT threads and, for PIPE, the frame
+// loop unrolled by two with the roles of two depth-register sets alternating: frame f_next's projection
+// and window loads are issued BEFORE frame f's running-average update, so a wave keeps one frame's loads
+// in flight while it updates the previous one (the plain loop issues frame f's loads and at once waits
+// for them in frame f's update: nothing of f + 1 is in flight).  The per-voxel update order stays frame
+// order.  NT = 512: 8 voxels per thread (+8 VGPRs for the second set); NT = 1024: 4 voxels per thread.
+// Map: lane l of wave w owns x = l % 8 + 8 (w % 2), y = (l / 8) % 2 + 2 (w / 2), z = l / 16 (a wave's
+// voxels k form an 8 x 2 x 4 brick); voxel k sits at (x, y + 8 (k / 4), z + 4 (k % 4)) for NT = 512
+// and at (x, y, z + 4 k) for NT = 1024.
+template <int NT>
+__host__ __device__ constexpr int win_dy(int k) { return NT == 512 ? 8 * (k >> 2) : 0; }
+template <int NT>
+__host__ __device__ constexpr int win_dz(int k) { return NT == 512 ? 4 * (k & 3) : 4 * k; }
+
+template <int NT, int WPE, int PIPE>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void k_integrate_win(
+    const int32_t* __restrict__ list, const bmask_t* __restrict__ lmask, int* __restrict__ counters, int64_t list_cap,
+    Table t, float2* __restrict__ pool, float voxel_size, const float* __restrict__ depths, int64_t HW, int H, int W,
+    const FrameParams* __restrict__ fps, const int64_t* __restrict__ depth_frame, float depth_max, float sdf_trunc,
+    int first_new) {
+    constexpr int R = 16, R2 = R * R, R3 = R2 * R;
+    constexpr int ZPER = R3 / NT;
+    static_assert(NT == 512 || NT == 1024, "brick map for 512 or 1024 threads");
+    const int64_t n = min((int64_t)counters[kListCount], list_cap);
+    const float hm1 = (float)H - 1.0f, wm1 = (float)W - 1.0f;
+    const uint32_t W4 = 4u * (uint32_t)W, bytes = 4u * (uint32_t)HW;
+    const uint32_t hb = __float_as_uint(hm1), wb = __float_as_uint(wm1);
+    const float y0t = __builtin_amdgcn_rcpf(sdf_trunc);
+    const float y1t = __builtin_fmaf(__builtin_fmaf(-sdf_trunc, y0t, 1.0f), y0t, y0t);
+    const int tid = threadIdx.x;
+    const int l = tid & 63, w = tid >> 6;
+    const int vx = (l & 7) + 8 * (w & 1), vy = ((l >> 3) & 1) + 2 * (w >> 1), vz = l >> 4;
+    const uint32_t voff = 8u * (uint32_t)(vx + R * vy + R2 * vz);  // byte offset of voxel 0 in its block
+    for (int64_t i = blockIdx.x; i < n; i += gridDim.x) {
+        const int32_t slot = list[i];
+        const int buf = __builtin_amdgcn_readfirstlane(t.vals[slot]);
+        const bmask_t mask = readfirstlane_mask(lmask ? lmask[i] : bm_frames(t.mask[slot]));
+        int xb, yb, zb;
+        unpack_key(t.keys[slot], xb, yb, zb);
+        if (buf >= 0 && mask) {
+            const __amdgpu_buffer_rsrc_t vox = __builtin_amdgcn_make_buffer_rsrc(
+                pool + (int64_t)buf * R3, (short)0, (int)(R3 * sizeof(float2)), 0x00020000);
+            float2 tw[ZPER];
+            float xs[ZPER], ys[ZPER], zs[ZPER];
+            bool bad = false;
+            const float xs0 = (float)(xb * R + vx) * voxel_size;
+#pragma unroll
+            for (int k = 0; k < ZPER; ++k) {
+                const int dy = win_dy<NT>(k), dz = win_dz<NT>(k);
+                // a block allocated by this batch (buffer >= first_new) starts at (0, 0)
+                tw[k] = buf >= first_new ? make_float2(0.f, 0.f)
+                                         : pool_load(vox, voff, (R * dy + R2 * dz) * (int)sizeof(float2));
+                xs[k] = xs0;
+                ys[k] = (float)(yb * R + vy + dy) * voxel_size;
+                zs[k] = (float)(zb * R + vz + dz) * voxel_size;
+                const float wv = tw[k].y;  // rcp_m(w + 1) is exact for integer w <= 2^23 + 64
+                bad |= !(wv >= 0.0f && wv <= 0x1p23f - 64.0f && wv == __builtin_truncf(wv));
+            }
+            auto gather = [&](float (&dv)[ZPER], int f) {
+                lean_gather_w<ZPER, 2, 8>(dv, bad, fps[f], frame_rsrc(depths + depth_frame[f] * HW, bytes), xs, ys, zs,
+                                          W4, bytes, hb, wb);
+            };
+            auto update = [&](const float (&dv)[ZPER], int f) {
+                lean_update_v<ZPER, 2, 0>(tw, dv, fps[f], xs, ys, zs, depth_max, sdf_trunc, y1t);
+            };
+            bmask_t m = mask;
+            float da[ZPER];
+            if constexpr (PIPE == 2) {
+                // half-frame pipeline: the voxels in two halves h0 / h1 and one depth-register set; steady
+                // state per frame f: gather h0(f), update h1(f_prev), gather h1(f), update h0(f) -- each
+                // half's update runs while the other half's loads are in flight
+                constexpr int H2 = ZPER / 2;
+                auto g0 = [&](int f) {
+                    lean_gather_w<ZPER, 2, 8, true, 0, H2>(da, bad, fps[f], frame_rsrc(depths + depth_frame[f] * HW, bytes),
+                                                           xs, ys, zs, W4, bytes, hb, wb);
+                };
+                auto g1 = [&](int f) {
+                    lean_gather_w<ZPER, 2, 8, true, H2, ZPER>(da, bad, fps[f],
+                                                              frame_rsrc(depths + depth_frame[f] * HW, bytes), xs, ys,
+                                                              zs, W4, bytes, hb, wb);
+                };
+                auto u0 = [&](int f) {
+                    lean_update_v<ZPER, 2, 0, 0, H2>(tw, da, fps[f], xs, ys, zs, depth_max, sdf_trunc, y1t);
+                };
+                auto u1 = [&](int f) {
+                    lean_update_v<ZPER, 2, 0, H2, ZPER>(tw, da, fps[f], xs, ys, zs, depth_max, sdf_trunc, y1t);
+                };
+                int fp = bm_ctz(m);
+                m &= m - 1;
+                g0(fp);
+                __builtin_amdgcn_sched_barrier(0);
+                g1(fp);
+                __builtin_amdgcn_sched_barrier(0);
+                u0(fp);
+                while (m) {
+                    const int f = bm_ctz(m);
+                    m &= m - 1;
+                    __builtin_amdgcn_sched_barrier(0);
+                    g0(f);
+                    __builtin_amdgcn_sched_barrier(0);
+                    u1(fp);
+                    __builtin_amdgcn_sched_barrier(0);
+                    g1(f);
+                    __builtin_amdgcn_sched_barrier(0);
+                    u0(f);
+                    fp = f;
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                u1(fp);
+            } else if constexpr (PIPE) {
+                float db[ZPER];
+                int fa = bm_ctz(m);
+                m &= m - 1;
+                gather(da, fa);
+                for (;;) {
+                    if (!m) {
+                        update(da, fa);
+                        break;
+                    }
+                    const int fb = bm_ctz(m);
+                    m &= m - 1;
+                    gather(db, fb);  // frame fb's loads in flight ...
+                    __builtin_amdgcn_sched_barrier(0);
+                    update(da, fa);  // ... while frame fa is applied
+                    if (!m) {
+                        update(db, fb);
+                        break;
+                    }
+                    fa = bm_ctz(m);
+                    m &= m - 1;
+                    gather(da, fa);
+                    __builtin_amdgcn_sched_barrier(0);
+                    update(db, fb);
+                }
+            } else {
+                while (m) {
+                    const int f = bm_ctz(m);
+                    m &= m - 1;
+                    gather(da, f);
+                    update(da, f);
+                }
+            }
+            if (__syncthreads_or(bad)) {  // block-uniform: the exact path redoes it from the pool
+                exact_block_call<R, NT>(pool + (int64_t)buf * R3, buf >= first_new, mask, xb, yb, zb, voxel_size, depths,
+                                        HW, W, hm1, wm1, fps, depth_frame, depth_max, sdf_trunc);
+            } else {
+#pragma unroll
+                for (int k = 0; k < ZPER; ++k)
+                    pool_store(vox, voff, (R * win_dy<NT>(k) + R2 * win_dz<NT>(k)) * (int)sizeof(float2), tw[k]);
+            }
+        }
+        __syncthreads();
+        if (tid == 0) t.mask[slot] = 0;
+    }
+}
+
 // Exhaustive-check kernels for the division shortcut (tests/test_gpu_numerics.py).
 // mode 0: rcp_rn, 1: rcp_nm, 2: rcp_m.
 __global__ void k_check_rcp(int mode, uint32_t lo_bits, uint64_t count, uint32_t* mismatches, uint32_t* first_bad) {

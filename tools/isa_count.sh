@@ -11,7 +11,7 @@ python3 - "$OUT/k.s" "$PAT" <<'EOF'
 import re, sys
 text = open(sys.argv[1]).read()
 pat = re.compile(sys.argv[2])
-for m in re.finditer(r"^(_Z\S+):\s*\n(.*?)^\.Lfunc_end\d+:", text, re.S | re.M):
+for m in re.finditer(r"^(_Z\S+):[^\n]*\n(.*?)^\.Lfunc_end\d+:", text, re.S | re.M):
     name, body = m.group(1), m.group(2)
     if not pat.search(name):
         continue
