@@ -1293,7 +1293,8 @@ static int ex_scratch(mqr_vbg* v, int64_t n, bool mesh, ExScratch& e) {
         MQR_CHECK_HIP(hipMalloc(&v->ex_scratch, cap));
         v->ex_scratch_bytes = cap;
     }
-    if (!v->h_ex) MQR_CHECK_HIP(hipHostMalloc(&v->h_ex, 4 * sizeof(int64_t), hipHostMallocDefault));
+    // fine-grained (coherent) pinned memory: k_scan_counts writes the totals straight into it (ex_mode bit 2)
+    if (!v->h_ex) MQR_CHECK_HIP(hipHostMalloc(&v->h_ex, 4 * sizeof(int64_t), hipHostMallocCoherent));
     char* p = static_cast<char*>(v->ex_scratch);
     e.nb = reinterpret_cast<int32_t*>(p);
     p += sz_nb;
@@ -1395,17 +1396,19 @@ static int build_nb(mqr_vbg* v, int32_t* nb) {
 // volume that is still being integrated.
 static int64_t spec_cap(int64_t hint) { return hint > 0 ? hint + hint / 4 + 4096 : 0; }
 
-// Extraction configuration: bit 0 = NIB (k_mc_count), bit 1 = MAP (k_mc_emit); the A/B library
-// takes it from mqr_vbg_set_extract_mode (below; tools/ab_extract.py).  (Also measured in round 4
+// Extraction configuration: bit 0 = NIB (k_mc_count), bit 1 = MAP (k_mc_emit), bit 2 = the scan writes
+// the totals straight into pinned host memory (without: a D2H copy enqueued between the scan and the
+// emission pass, whose latency the emission waited behind); the A/B library takes it from
+// mqr_vbg_set_extract_mode (below; tools/ab_extract.py; a negative mode = the library default).  (Also measured in round 4
 // and removed, DESIGN.md §4.2: the emission over a compacted list of the blocks with output, by one
 // workgroup per listed block or by a grid of 8 workgroups per CU walking the list; the block's tsdf
 // staged in LDS for its interior vertices' taps; XCD bands of the pool in the count and emission
 // passes; the triangles' neighbour row records prefetched into LDS during the vertex loop -- all
 // neutral or slower.)
-[[maybe_unused]] constexpr int kExMode = 3;  // NIB + MAP (tools/ab_extract.py)
+[[maybe_unused]] constexpr int kExMode = 7;  // NIB + MAP + direct totals (tools/ab_extract.py)
 static int ex_mode(const mqr_vbg* v) {
 #if MQR_AB
-    return v->ex_mode;
+    return v->ex_mode < 0 ? kExMode : v->ex_mode;
 #else
     (void)v;
     return kExMode;
@@ -1450,7 +1453,9 @@ static int mesh_passes(mqr_vbg* v, float thr, const ExScratch& e, mqr_geom* g, i
         else
             hipLaunchKernelGGL((k_mc_count<RT, false>), dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, e.nb, e.bits,
                                tri_blocks, e.c0, e.c1, rows4, rowNt, rowsT);
-        hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(kScanThreads), 0, v->stream, e.c0, e.c1, n, e.o0, e.o1, tot);
+        const bool direct = ex_mode(v) & 4;
+        hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(kScanThreads), 0, v->stream, e.c0, e.c1, n, e.o0, e.o1,
+                           direct ? v->h_ex : tot);
         // With a previous extraction's counts, emit into buffers of that size (+ margin) without
         // waiting for this one's totals; blocks past the capacity write nothing and the pass is re-run
         // into exact buffers if the totals exceed it.  Without, wait for the totals first.
@@ -1458,7 +1463,7 @@ static int mesh_passes(mqr_vbg* v, float thr, const ExScratch& e, mqr_geom* g, i
         const bool spec = cv > 0 && ct > 0;
         if (spec && alloc_geom(g, cv, ct)) return 1;
         MQR_CHECK_HIP(hipGetLastError());
-        MQR_CHECK_HIP(hipMemcpyAsync(v->h_ex, tot, 2 * sizeof(int64_t), hipMemcpyDeviceToHost, v->stream));
+        if (!direct) MQR_CHECK_HIP(hipMemcpyAsync(v->h_ex, tot, 2 * sizeof(int64_t), hipMemcpyDeviceToHost, v->stream));
         bool emitted = false;
         if (spec) {
             launch_mc_emit<RT>(v, n, (const int32_t*)e.nb, (const uint64_t*)v->bkeys, (const float2*)v->pool,
@@ -1515,10 +1520,11 @@ static int point_passes(mqr_vbg* v, float thr, const ExScratch& e, mqr_geom* g) 
                            v->bkeys, v->tab, e.nb);
         hipLaunchKernelGGL(k_pt_count<RT>, dim3((unsigned)n), dim3(kMcThreads), 0, v->stream, e.nb, e.bits, v->pool,
                            e.c0, rows4);
+        const bool direct = ex_mode(v) & 4;
         hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(kScanThreads), 0, v->stream, e.c0, (const int32_t*)nullptr, n,
-                           e.o0, (int32_t*)nullptr, tot);
+                           e.o0, (int32_t*)nullptr, direct ? v->h_ex : tot);
         MQR_CHECK_HIP(hipGetLastError());
-        MQR_CHECK_HIP(hipMemcpyAsync(v->h_ex, tot, sizeof(int64_t), hipMemcpyDeviceToHost, v->stream));
+        if (!direct) MQR_CHECK_HIP(hipMemcpyAsync(v->h_ex, tot, sizeof(int64_t), hipMemcpyDeviceToHost, v->stream));
         const int64_t cp = spec_cap(v->ex_hint[2]);  // speculative capacity, as in mesh_passes
         if (cp > 0) {
             if (alloc_geom(g, cp, 0)) return 1;
@@ -1567,7 +1573,7 @@ int mqr_extract_mesh(mqr_vbg* v, float thr, mqr_geom** out) { return mqr_extract
 #if MQR_AB
 // A/B library only: the extraction configuration (kExMode bits) for tools/ab_extract.py.
 int mqr_vbg_set_extract_mode(mqr_vbg* v, int mode) {
-    MQR_REQUIRE(v && mode >= 0 && mode < 4, "bad extraction mode");
+    MQR_REQUIRE(v && mode < 8, "bad extraction mode");
     v->ex_mode = mode;
     return 0;
 }

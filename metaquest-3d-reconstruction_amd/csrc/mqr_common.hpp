@@ -193,7 +193,7 @@ struct mqr_vbg {
     int first_batch_frames = mqr::kFirstBatch;  // frames of a call's first batch
     // profiling
     int touch_ppt = 2;  // stride-4 pixels per k_touch thread (variant bit 16: one)
-    int ex_mode = 0;    // extraction configuration under A/B (variant bits 28-30, tools/ab_extract.py)
+    int ex_mode = -1;   // extraction configuration under A/B (-1: the library default kExMode; tools/ab_extract.py)
     int last_var = -1;        // integrate variant of the last launch, after fallbacks (mqr_vbg_last_kernel)
     bool profile = false;
     bool profile_touch = false;  // mqr_vbg_profile level 2: also time the touch launches

@@ -425,7 +425,7 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
     //     ballot skip of out-of-image wave slots, ran 0.70 vs 0.48 ms per launch: removed.)
     //     DESIGN.md §4.1 has the measurements behind the choice.
     int var = v->kernel_variant;
-    if (var < 0 || var > 31) var = 0;
+    if (var < 0 || var > 35) var = 0;
     if (!MQR_AB && var != 1 && var != 2 && var != 4) var = 0;
     if (var != 1 && var != 2 && !lean_ok) var = 2;
     if (var == 5 && (v->R != 16 || W % 4 != 0 || W < 4 || (reinterpret_cast<uintptr_t>(depths) & 15))) var = 0;
@@ -455,8 +455,9 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
             // k_integrate_win (8-byte windows): 24 = the default's plain frame loop, 25 = software-pipelined
             // frames at >= 6 waves / SIMD, 26 / 27 = 1024 threads (4 voxels each) pipelined / plain at >= 8,
             // 28 = pipelined forced to >= 7 waves / SIMD; 29 / 30 = half-frame pipeline, 512 threads at >= 7
-            // waves / 1024 threads at >= 8, 31 = half-frame pipeline, 512 threads at >= 6 waves
-            if (var >= 24 && var <= 31) {
+            // waves / 1024 threads at >= 8, 31 = half-frame pipeline, 512 threads at >= 6 waves;
+            // timing diagnostics (wrong results): 32 / 33 = 24 with DIAG 1 / 2, 34 / 35 = 31 with DIAG 1 / 2
+            if (var >= 24 && var <= 35) {
                 auto win = [&](auto kern, unsigned nt) {
                     hipLaunchKernelGGL(kern, dim3(grid), dim3(nt), 0, s, list, lmask, counters, v->list_cap, t, v->pool,
                                        v->voxel_size, depths, HW, H, W, fp, depth_frame, depth_max, sdf_trunc, first_new);
@@ -468,7 +469,11 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
                 else if (var == 28) win(k_integrate_win<512, 7, 1>, 512);
                 else if (var == 29) win(k_integrate_win<512, 7, 2>, 512);
                 else if (var == 30) win(k_integrate_win<1024, 8, 2>, 1024);
-                else win(k_integrate_win<512, 6, 2>, 512);
+                else if (var == 31) win(k_integrate_win<512, 6, 2>, 512);
+                else if (var == 32) win(k_integrate_win<512, 7, 0, 1>, 512);
+                else if (var == 33) win(k_integrate_win<512, 7, 0, 2>, 512);
+                else if (var == 34) win(k_integrate_win<512, 6, 2, 1>, 512);
+                else win(k_integrate_win<512, 6, 2, 2>, 512);
             } else
             if (var == 8)  // VALU-lean projection / update (lean_gather_v)
                 hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 8, 2, 2>), dim3(lean_grid), dim3(512), 0, s, list,
@@ -1282,7 +1287,7 @@ int mqr_vbg_set_variant(mqr_vbg* v, int variant) {
     v->xcd_order = (variant & 0x8000) != 0;   // bit 15: spatial per-XCD groups (k_xcd_order, A/B)
     v->touch_ppt = (variant & 0x10000) ? 1 : 2;  // bit 16: one stride-4 pixel per touch thread (A/B)
     v->spec_head = (variant & 0x40000) == 0;     // bit 18: no speculative first-batch integrate (A/B)
-    v->ex_mode = (variant >> 28) & 7;            // bits 28-30: extraction configuration (A/B library only)
+    // (the extraction configuration is set by mqr_vbg_set_extract_mode alone, A/B library only)
     return 0;
 }
 

@@ -727,7 +727,7 @@ __device__ __forceinline__ void lean_gather_v(float (&dv)[ZPER], bool& bad, cons
 // multiple of the window (host): then an in-image window never crosses the end of the frame, and an
 // out-of-image lane's window at 4HW is wholly past the end (reads 0).
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-template <int ZPER, int ILP = 1, int WIN = 16, bool ZCHK = true, int K0 = 0, int K1 = ZPER>
+template <int ZPER, int ILP = 1, int WIN = 16, bool ZCHK = true, int K0 = 0, int K1 = ZPER, int DIAGV = 0>
 __device__ __forceinline__ void lean_gather_w(float (&dv)[ZPER], bool& bad, const FrameParams& fp,
                                               __amdgpu_buffer_rsrc_t rs, const float (&xs)[ZPER],
                                               const float (&ys)[ZPER], const float (&zs)[ZPER], uint32_t W4,
@@ -745,7 +745,8 @@ __device__ __forceinline__ void lean_gather_w(float (&dv)[ZPER], bool& bad, cons
         const float yc = (ay + zs[k] * e[6]) + e[7];
         const float zc = (az + zs[k] * e[10]) + e[11];
         if (ZCHK) bad |= (__float_as_uint(zc) - 0x2D800000u) > 0x30000000u;  // not 2^-36 <= zc <= 2^60
-        const float inv_z = rcp_m(zc);
+        // DIAGV (timing diagnostics of the A/B library only, wrong results): the bare v_rcp
+        const float inv_z = DIAGV == 1 ? __builtin_amdgcn_rcpf(zc) : rcp_m(zc);
         const float u = fx * xc * inv_z + cx;
         const float v = fy * yc * inv_z + cy;
         const bool in = (__float_as_uint(v) <= hm1_bits) && (__float_as_uint(u) <= wm1_bits);
@@ -765,7 +766,7 @@ __device__ __forceinline__ void lean_gather_w(float (&dv)[ZPER], bool& bad, cons
 // DIV1: s / sdf_trunc with one Markstein correction (the host enables it only for an sdf_trunc whose
 // every s in [0, sdf_trunc] it verified against IEEE division, strunc_one_correction_ok; the
 // sequence is odd in s, so negative s follow).
-template <int ZPER, int ILP = 1, int DIV1 = 0, int K0 = 0, int K1 = ZPER>
+template <int ZPER, int ILP = 1, int DIV1 = 0, int K0 = 0, int K1 = ZPER, int DIAGV = 0>
 __device__ __forceinline__ void lean_update_v(float2 (&tw)[ZPER], const float (&dv)[ZPER], const FrameParams& fp,
                                               const float (&xs)[ZPER], const float (&ys)[ZPER],
                                               const float (&zs)[ZPER], float depth_max, float sdf_trunc, float y1t) {
@@ -780,10 +781,10 @@ __device__ __forceinline__ void lean_update_v(float2 (&tw)[ZPER], const float (&
             float s;
             asm("v_min_f32 %0, %1, %2" : "=v"(s) : "s"(sdf_trunc), "v"(sdf));
             const float q0 = s * y1t;
-            const float q1 = __builtin_fmaf(__builtin_fmaf(-sdf_trunc, q0, s), y1t, q0);
-            const float sn = DIV1 ? q1 : __builtin_fmaf(__builtin_fmaf(-sdf_trunc, q1, s), y1t, q1);
+            const float q1 = DIAGV == 1 ? q0 : __builtin_fmaf(__builtin_fmaf(-sdf_trunc, q0, s), y1t, q0);
+            const float sn = DIV1 || DIAGV == 1 ? q1 : __builtin_fmaf(__builtin_fmaf(-sdf_trunc, q1, s), y1t, q1);
             const float wgt = tw[k].y, wp = wgt + 1;
-            tw[k].x = (wgt * tw[k].x + sn) * rcp_m(wp);
+            tw[k].x = (wgt * tw[k].x + sn) * (DIAGV == 1 ? __builtin_amdgcn_rcpf(wp) : rcp_m(wp));
             tw[k].y = wp;
         }
         if ((k + 1) % ILP == 0) __builtin_amdgcn_sched_barrier(0);
@@ -1017,7 +1018,11 @@ __host__ __device__ constexpr int win_dy(int k) { return NT == 512 ? 8 * (k >> 2
 template <int NT>
 __host__ __device__ constexpr int win_dz(int k) { return NT == 512 ? 4 * (k & 3) : 4 * k; }
 
-template <int NT, int WPE, int PIPE>
+// DIAG (A/B library timing diagnostics, wrong results): 1 = the bare v_rcp for 1 / zc and 1 / (w + 1) and
+// one product for s / sdf_trunc (about a third of the frame loop's VALU work gone); 2 = every frame's depth
+// read from the batch's first frame (a 1.2 MB working set that stays in L2: the refetch of each XCD's
+// frames from the MALL taken away).
+template <int NT, int WPE, int PIPE, int DIAG = 0>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void k_integrate_win(
     const int32_t* __restrict__ list, const bmask_t* __restrict__ lmask, int* __restrict__ counters, int64_t list_cap,
     Table t, float2* __restrict__ pool, float voxel_size, const float* __restrict__ depths, int64_t HW, int H, int W,
@@ -1061,12 +1066,15 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
                 const float wv = tw[k].y;  // rcp_m(w + 1) is exact for integer w <= 2^23 + 64
                 bad |= !(wv >= 0.0f && wv <= 0x1p23f - 64.0f && wv == __builtin_truncf(wv));
             }
+            const int64_t f0 = depth_frame[bm_ctz(mask)];
+            auto dframe = [&](int f) { return DIAG == 2 ? f0 : depth_frame[f]; };
             auto gather = [&](float (&dv)[ZPER], int f) {
-                lean_gather_w<ZPER, 2, 8>(dv, bad, fps[f], frame_rsrc(depths + depth_frame[f] * HW, bytes), xs, ys, zs,
-                                          W4, bytes, hb, wb);
+                lean_gather_w<ZPER, 2, 8, true, 0, ZPER, DIAG == 1>(dv, bad, fps[f],
+                                                                   frame_rsrc(depths + dframe(f) * HW, bytes), xs, ys,
+                                                                   zs, W4, bytes, hb, wb);
             };
             auto update = [&](const float (&dv)[ZPER], int f) {
-                lean_update_v<ZPER, 2, 0>(tw, dv, fps[f], xs, ys, zs, depth_max, sdf_trunc, y1t);
+                lean_update_v<ZPER, 2, 0, 0, ZPER, DIAG == 1>(tw, dv, fps[f], xs, ys, zs, depth_max, sdf_trunc, y1t);
             };
             bmask_t m = mask;
             float da[ZPER];
@@ -1076,19 +1084,20 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
                 // half's update runs while the other half's loads are in flight
                 constexpr int H2 = ZPER / 2;
                 auto g0 = [&](int f) {
-                    lean_gather_w<ZPER, 2, 8, true, 0, H2>(da, bad, fps[f], frame_rsrc(depths + depth_frame[f] * HW, bytes),
-                                                           xs, ys, zs, W4, bytes, hb, wb);
+                    lean_gather_w<ZPER, 2, 8, true, 0, H2, DIAG == 1>(da, bad, fps[f],
+                                                                     frame_rsrc(depths + dframe(f) * HW, bytes), xs, ys,
+                                                                     zs, W4, bytes, hb, wb);
                 };
                 auto g1 = [&](int f) {
-                    lean_gather_w<ZPER, 2, 8, true, H2, ZPER>(da, bad, fps[f],
-                                                              frame_rsrc(depths + depth_frame[f] * HW, bytes), xs, ys,
-                                                              zs, W4, bytes, hb, wb);
+                    lean_gather_w<ZPER, 2, 8, true, H2, ZPER, DIAG == 1>(da, bad, fps[f],
+                                                                        frame_rsrc(depths + dframe(f) * HW, bytes), xs,
+                                                                        ys, zs, W4, bytes, hb, wb);
                 };
                 auto u0 = [&](int f) {
-                    lean_update_v<ZPER, 2, 0, 0, H2>(tw, da, fps[f], xs, ys, zs, depth_max, sdf_trunc, y1t);
+                    lean_update_v<ZPER, 2, 0, 0, H2, DIAG == 1>(tw, da, fps[f], xs, ys, zs, depth_max, sdf_trunc, y1t);
                 };
                 auto u1 = [&](int f) {
-                    lean_update_v<ZPER, 2, 0, H2, ZPER>(tw, da, fps[f], xs, ys, zs, depth_max, sdf_trunc, y1t);
+                    lean_update_v<ZPER, 2, 0, H2, ZPER, DIAG == 1>(tw, da, fps[f], xs, ys, zs, depth_max, sdf_trunc, y1t);
                 };
                 int fp = bm_ctz(m);
                 m &= m - 1;

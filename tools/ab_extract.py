@@ -1,10 +1,12 @@
 #!/usr/bin/env python3
 """Interleaved A/B of extract_triangle_mesh configurations on the bench volume (C2, one process).
 
-python tools/ab_extract.py --modes 0 --reps 15
-mode = an extraction configuration under test (mqr_vbg_set_extract_mode, A/B library only; the
-product library runs mode 0 = its kExMode, extract.hip): bit 0 per-cube triangle counts from the
-count pass, bit 1 LDS row maps in the emission pass (both = 3, the library default).  Round 4 also
+python tools/ab_extract.py --modes 3,7 --reps 15
+mode = an extraction configuration under test (mqr_vbg_set_extract_mode, A/B library only; -1 = the
+library default kExMode, extract.hip, the only mode of the product library): bit 0 per-cube triangle
+counts from the count pass, bit 1 LDS row maps in the emission pass, bit 2 the scan's totals written
+straight into pinned host memory instead of a D2H copy between the scan and the emission pass (all
+three = 7, the default since round 5).  Round 4 also
 measured, and removed: an emission over a compacted list of the blocks with output, the block's tsdf
 staged in LDS for the interior vertex taps, XCD bands of the pool (profiles/r04_ab_extract.json),
 the count pass emitting the vertices (0.264 vs 0.237 ms) and a vertex and a triangle workgroup per
@@ -27,7 +29,7 @@ sys.path.insert(0, ROOT)
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--modes", default="0")
+    ap.add_argument("--modes", default="-1")
     ap.add_argument("--reps", type=int, default=15)
     ap.add_argument("--threshold", type=float, default=1.5)
     a = ap.parse_args()
@@ -51,8 +53,8 @@ def main():
         for m in modes:
             if ab:
                 _lib.call("mqr_vbg_set_extract_mode", vbg.handle, m)
-            elif m:
-                raise SystemExit("extraction modes other than 0 need the A/B library (MQR_HIP_LIB=tools/_ab/libmqr_ab.so)")
+            elif m != -1:
+                raise SystemExit("extraction modes other than -1 need the A/B library (MQR_HIP_LIB=tools/_ab/libmqr_ab.so)")
             g = ctypes.c_void_p()
             t0 = time.perf_counter()
             _lib.call("mqr_extract_mesh", vbg.handle, float(a.threshold), ctypes.byref(g))
