@@ -425,7 +425,7 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
     //     ballot skip of out-of-image wave slots, ran 0.70 vs 0.48 ms per launch: removed.)
     //     DESIGN.md §4.1 has the measurements behind the choice.
     int var = v->kernel_variant;
-    if (var < 0 || var > 35) var = 0;
+    if (var < 0 || var > 39) var = 0;
     if (!MQR_AB && var != 1 && var != 2 && var != 4) var = 0;
     if (var != 1 && var != 2 && !lean_ok) var = 2;
     if (var == 5 && (v->R != 16 || W % 4 != 0 || W < 4 || (reinterpret_cast<uintptr_t>(depths) & 15))) var = 0;
@@ -457,7 +457,9 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
             // 28 = pipelined forced to >= 7 waves / SIMD; 29 / 30 = half-frame pipeline, 512 threads at >= 7
             // waves / 1024 threads at >= 8, 31 = half-frame pipeline, 512 threads at >= 6 waves;
             // timing diagnostics (wrong results): 32 / 33 = 24 with DIAG 1 / 2, 34 / 35 = 31 with DIAG 1 / 2
-            if (var >= 24 && var <= 35) {
+            // packed FP32 (k_integrate_pk): 36 / 37 = plain / half-frame pipeline at >= 7 waves, 38 / 39 = half-frame
+            // pipeline / plain at >= 6
+            if (var >= 24 && var <= 39) {
                 auto win = [&](auto kern, unsigned nt) {
                     hipLaunchKernelGGL(kern, dim3(grid), dim3(nt), 0, s, list, lmask, counters, v->list_cap, t, v->pool,
                                        v->voxel_size, depths, HW, H, W, fp, depth_frame, depth_max, sdf_trunc, first_new);
@@ -473,7 +475,11 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
                 else if (var == 32) win(k_integrate_win<512, 7, 0, 1>, 512);
                 else if (var == 33) win(k_integrate_win<512, 7, 0, 2>, 512);
                 else if (var == 34) win(k_integrate_win<512, 6, 2, 1>, 512);
-                else win(k_integrate_win<512, 6, 2, 2>, 512);
+                else if (var == 35) win(k_integrate_win<512, 6, 2, 2>, 512);
+                else if (var == 36) win(k_integrate_pk<7, 0>, 512);
+                else if (var == 37) win(k_integrate_pk<7, 2>, 512);
+                else if (var == 38) win(k_integrate_pk<6, 2>, 512);
+                else win(k_integrate_pk<6, 0>, 512);
             } else
             if (var == 8)  // VALU-lean projection / update (lean_gather_v)
                 hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 8, 2, 2>), dim3(lean_grid), dim3(512), 0, s, list,

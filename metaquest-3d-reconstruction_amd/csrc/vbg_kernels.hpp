@@ -1168,6 +1168,180 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
     }
 }
 
+// ---- packed-FP32 integrate (R = 16, NT = 512) --------------------------------------------------------------
+// k_integrate_win's float operations two voxels at a time: voxels (2p, 2p + 1) of a thread share x and y and
+// differ in z, so their transform, projection, reciprocal corrections and running-average update map onto
+// gfx950's packed FP32 instructions (v_pk_mul_f32 / v_pk_add_f32 / v_pk_fma_f32: two IEEE round-to-nearest
+// results, exactly the scalar instructions' -- no contraction is introduced, the fma calls are the scalar
+// code's own).  v_rcp, the float -> int conversions, the in-image tests and the window addressing stay scalar.
+// Voxel state as pairs: tt[p] = (tsdf 2p, tsdf 2p+1), ww[p] = (weight 2p, weight 2p+1).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 splat2(float a) { return (f32x2){a, a}; }
+__device__ __forceinline__ f32x2 fma2(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f32x2 rcp_m2(f32x2 b) {  // rcp_m elementwise: v_rcp x 2, Markstein correction packed
+    const f32x2 y0 = {__builtin_amdgcn_rcpf(b.x), __builtin_amdgcn_rcpf(b.y)};
+    return fma2(fma2(-b, y0, splat2(1.0f)), y0, y0);
+}
+
+// Pairs [P0, P1): projection + 8-byte window read of both voxels of each pair (lean_gather_w's operations).
+template <int NP, int P0, int P1>
+__device__ __forceinline__ void pk_gather(float (&dv)[2 * NP], bool& bad, const FrameParams& fp,
+                                          __amdgpu_buffer_rsrc_t rs, float xs0, const float (&ysp)[NP],
+                                          const f32x2 (&zz)[NP], uint32_t W4, uint32_t past_end, uint32_t hb,
+                                          uint32_t wb) {
+    float e[12];
+#pragma unroll
+    for (int j = 0; j < 12; ++j) e[j] = fp.ext[j];
+#pragma unroll
+    for (int p = P0; p < P1; ++p) {
+        const float ax = xs0 * e[0] + ysp[p] * e[1];  // shared by the pairs of one y (merged)
+        const float ay = xs0 * e[4] + ysp[p] * e[5];
+        const float az = xs0 * e[8] + ysp[p] * e[9];
+        const f32x2 xc = (splat2(ax) + zz[p] * splat2(e[2])) + splat2(e[3]);
+        const f32x2 yc = (splat2(ay) + zz[p] * splat2(e[6])) + splat2(e[7]);
+        const f32x2 zc = (splat2(az) + zz[p] * splat2(e[10])) + splat2(e[11]);
+        bad |= (__float_as_uint(zc.x) - 0x2D800000u) > 0x30000000u;  // not 2^-36 <= zc <= 2^60
+        bad |= (__float_as_uint(zc.y) - 0x2D800000u) > 0x30000000u;
+        const f32x2 inv_z = rcp_m2(zc);
+        const f32x2 u = (splat2(fp.fx) * xc) * inv_z + splat2(fp.cx);
+        const f32x2 v = (splat2(fp.fy) * yc) * inv_z + splat2(fp.cy);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const float uh = h ? u.y : u.x, vh = h ? v.y : v.x;
+            const bool in = (__float_as_uint(vh) <= hb) && (__float_as_uint(uh) <= wb);
+            const uint32_t off = in ? __umul24((uint32_t)(int)vh, W4) + ((uint32_t)(int)uh << 2) : past_end;
+            const u32x2 q = __builtin_amdgcn_raw_buffer_load_b64(rs, off & ~7u, 0, 0);
+            dv[2 * p + h] = __uint_as_float((off & 4u) ? q.y : q.x);
+        }
+        __builtin_amdgcn_sched_barrier(0);  // one pair's chain at a time (registers)
+    }
+}
+
+// Pairs [P0, P1): lean_update_v's running-average update, both voxels of a pair in packed form; a pair is
+// skipped when no lane updates either voxel (the scalar code's per-voxel branch, per pair).
+template <int NP, int P0, int P1>
+__device__ __forceinline__ void pk_update(f32x2 (&tt)[NP], f32x2 (&ww)[NP], const float (&dv)[2 * NP],
+                                          const FrameParams& fp, float xs0, const float (&ysp)[NP],
+                                          const f32x2 (&zz)[NP], float depth_max, float sdf_trunc, float y1t) {
+    const float e8 = fp.ext[8], e9 = fp.ext[9], e10 = fp.ext[10], e11 = fp.ext[11];
+#pragma unroll
+    for (int p = P0; p < P1; ++p) {
+        const float az = xs0 * e8 + ysp[p] * e9;
+        const f32x2 zc = (splat2(az) + zz[p] * splat2(e10)) + splat2(e11);
+        const f32x2 d = {dv[2 * p], dv[2 * p + 1]};
+        const f32x2 sdf = d - zc;
+        const bool up0 = !(d.x <= 0) && !(d.x > depth_max) && !(sdf.x < -sdf_trunc);
+        const bool up1 = !(d.y <= 0) && !(d.y > depth_max) && !(sdf.y < -sdf_trunc);
+        if (up0 || up1) {
+            f32x2 s;
+            asm("v_min_f32 %0, %1, %2" : "=v"(s.x) : "s"(sdf_trunc), "v"(sdf.x));
+            asm("v_min_f32 %0, %1, %2" : "=v"(s.y) : "s"(sdf_trunc), "v"(sdf.y));
+            const f32x2 T = splat2(sdf_trunc), Y = splat2(y1t);
+            const f32x2 q0 = s * Y;
+            const f32x2 q1 = fma2(fma2(-T, q0, s), Y, q0);
+            const f32x2 sn = fma2(fma2(-T, q1, s), Y, q1);
+            const f32x2 wgt = ww[p], wp = wgt + splat2(1.0f);
+            const f32x2 nt = (wgt * tt[p] + sn) * rcp_m2(wp);
+            tt[p].x = up0 ? nt.x : tt[p].x;
+            tt[p].y = up1 ? nt.y : tt[p].y;
+            ww[p].x = up0 ? wp.x : ww[p].x;
+            ww[p].y = up1 ? wp.y : ww[p].y;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+// The packed-FP32 kernel: k_integrate_win<512, WPE, PIPE in {0, 2}>'s structure over pk_gather / pk_update.
+template <int WPE, int PIPE>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void k_integrate_pk(
+    const int32_t* __restrict__ list, const bmask_t* __restrict__ lmask, int* __restrict__ counters, int64_t list_cap,
+    Table t, float2* __restrict__ pool, float voxel_size, const float* __restrict__ depths, int64_t HW, int H, int W,
+    const FrameParams* __restrict__ fps, const int64_t* __restrict__ depth_frame, float depth_max, float sdf_trunc,
+    int first_new) {
+    constexpr int NT = 512, R = 16, R2 = R * R, R3 = R2 * R;
+    constexpr int ZPER = R3 / NT, NP = ZPER / 2;
+    const int64_t n = min((int64_t)counters[kListCount], list_cap);
+    const float hm1 = (float)H - 1.0f, wm1 = (float)W - 1.0f;
+    const uint32_t W4 = 4u * (uint32_t)W, bytes = 4u * (uint32_t)HW;
+    const uint32_t hb = __float_as_uint(hm1), wb = __float_as_uint(wm1);
+    const float y0t = __builtin_amdgcn_rcpf(sdf_trunc);
+    const float y1t = __builtin_fmaf(__builtin_fmaf(-sdf_trunc, y0t, 1.0f), y0t, y0t);
+    const int tid = threadIdx.x;
+    const int l = tid & 63, w = tid >> 6;
+    const int vx = (l & 7) + 8 * (w & 1), vy = ((l >> 3) & 1) + 2 * (w >> 1), vz = l >> 4;
+    const uint32_t voff = 8u * (uint32_t)(vx + R * vy + R2 * vz);
+    for (int64_t i = blockIdx.x; i < n; i += gridDim.x) {
+        const int32_t slot = list[i];
+        const int buf = __builtin_amdgcn_readfirstlane(t.vals[slot]);
+        const bmask_t mask = readfirstlane_mask(lmask ? lmask[i] : bm_frames(t.mask[slot]));
+        int xb, yb, zb;
+        unpack_key(t.keys[slot], xb, yb, zb);
+        if (buf >= 0 && mask) {
+            const __amdgpu_buffer_rsrc_t vox = __builtin_amdgcn_make_buffer_rsrc(
+                pool + (int64_t)buf * R3, (short)0, (int)(R3 * sizeof(float2)), 0x00020000);
+            f32x2 tt[NP], ww[NP], zz[NP];
+            float ysp[NP];
+            bool bad = false;
+            const float xs0 = (float)(xb * R + vx) * voxel_size;
+#pragma unroll
+            for (int p = 0; p < NP; ++p) {
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int k = 2 * p + h;
+                    const int dy = win_dy<NT>(k), dz = win_dz<NT>(k);
+                    const float2 v = buf >= first_new ? make_float2(0.f, 0.f)
+                                                      : pool_load(vox, voff, (R * dy + R2 * dz) * (int)sizeof(float2));
+                    if (h) tt[p].y = v.x, ww[p].y = v.y, zz[p].y = (float)(zb * R + vz + dz) * voxel_size;
+                    else tt[p].x = v.x, ww[p].x = v.y, zz[p].x = (float)(zb * R + vz + dz) * voxel_size;
+                    bad |= !(v.y >= 0.0f && v.y <= 0x1p23f - 64.0f && v.y == __builtin_truncf(v.y));
+                }
+                ysp[p] = (float)(yb * R + vy + win_dy<NT>(2 * p)) * voxel_size;
+            }
+            auto frs = [&](int f) { return frame_rsrc(depths + depth_frame[f] * HW, bytes); };
+            bmask_t m = mask;
+            float da[ZPER];
+            if constexpr (PIPE == 2) {
+                constexpr int H2 = NP / 2;
+                int fp = bm_ctz(m);
+                m &= m - 1;
+                pk_gather<NP, 0, H2>(da, bad, fps[fp], frs(fp), xs0, ysp, zz, W4, bytes, hb, wb);
+                pk_gather<NP, H2, NP>(da, bad, fps[fp], frs(fp), xs0, ysp, zz, W4, bytes, hb, wb);
+                pk_update<NP, 0, H2>(tt, ww, da, fps[fp], xs0, ysp, zz, depth_max, sdf_trunc, y1t);
+                while (m) {
+                    const int f = bm_ctz(m);
+                    m &= m - 1;
+                    pk_gather<NP, 0, H2>(da, bad, fps[f], frs(f), xs0, ysp, zz, W4, bytes, hb, wb);
+                    pk_update<NP, H2, NP>(tt, ww, da, fps[fp], xs0, ysp, zz, depth_max, sdf_trunc, y1t);
+                    pk_gather<NP, H2, NP>(da, bad, fps[f], frs(f), xs0, ysp, zz, W4, bytes, hb, wb);
+                    pk_update<NP, 0, H2>(tt, ww, da, fps[f], xs0, ysp, zz, depth_max, sdf_trunc, y1t);
+                    fp = f;
+                }
+                pk_update<NP, H2, NP>(tt, ww, da, fps[fp], xs0, ysp, zz, depth_max, sdf_trunc, y1t);
+            } else {
+                while (m) {
+                    const int f = bm_ctz(m);
+                    m &= m - 1;
+                    pk_gather<NP, 0, NP>(da, bad, fps[f], frs(f), xs0, ysp, zz, W4, bytes, hb, wb);
+                    pk_update<NP, 0, NP>(tt, ww, da, fps[f], xs0, ysp, zz, depth_max, sdf_trunc, y1t);
+                }
+            }
+            if (__syncthreads_or(bad)) {
+                exact_block_call<R, NT>(pool + (int64_t)buf * R3, buf >= first_new, mask, xb, yb, zb, voxel_size, depths,
+                                        HW, W, hm1, wm1, fps, depth_frame, depth_max, sdf_trunc);
+            } else {
+#pragma unroll
+                for (int k = 0; k < ZPER; ++k) {
+                    const f32x2 a = tt[k >> 1], b = ww[k >> 1];
+                    pool_store(vox, voff, (R * win_dy<NT>(k) + R2 * win_dz<NT>(k)) * (int)sizeof(float2),
+                               (k & 1) ? make_float2(a.y, b.y) : make_float2(a.x, b.x));
+                }
+            }
+        }
+        __syncthreads();
+        if (tid == 0) t.mask[slot] = 0;
+    }
+}
+
 // Exhaustive-check kernels for the division shortcut (tests/test_gpu_numerics.py).
 // mode 0: rcp_rn, 1: rcp_nm, 2: rcp_m.
 __global__ void k_check_rcp(int mode, uint32_t lo_bits, uint64_t count, uint32_t* mismatches, uint32_t* first_bad) {

@@ -28,15 +28,15 @@ def test_ab_integrate_variants_equal_generic():
 
 def test_ab_extraction_modes_bit_identical():
     """The A/B library's extraction configurations (tools/ab_extract.py modes: per-cube triangle
-    counts from the count pass, LDS row maps, both = the shipped default) emit the same mesh bit for
-    bit on the C2 volume."""
+    counts from the count pass, LDS row maps, the scan's totals written straight to pinned memory; all
+    three = the shipped default 7) emit the same mesh bit for bit on the C2 volume."""
     import json
     assert os.path.exists(AB_LIB), f"{AB_LIB} missing: run __graft_entry__.build()"
     env = dict(os.environ, MQR_HIP_LIB=AB_LIB)
-    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tools", "ab_extract.py"), "--modes", "0,1,2,3",
+    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tools", "ab_extract.py"), "--modes", "0,1,2,3,4,7",
                         "--reps", "1"], cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     res = json.loads(r.stdout.strip().splitlines()[-1])["modes"]
-    assert set(res) == {"0", "1", "2", "3"}
+    assert set(res) == {"0", "1", "2", "3", "4", "7"}
     assert all(m["bit_identical_to_first"] for m in res.values()), res
     assert res["0"]["triangles"] > 1_000_000
