@@ -40,6 +40,7 @@
 #include <chrono>
 #include <climits>
 #include <cstring>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <vector>
@@ -769,10 +770,19 @@ int mqr_merge_local(mqr_vbg** locals, int n, int mode, int root, mqr_vbg** outs,
     t_local_ms.assign(n, 0.f);
     // 1. every rank's own side, exactly as mqr_reduce_rccl runs it on that rank: its plan (me = s),
     //    its output volume, its send segments packed from its own pool
-    std::vector<std::unique_ptr<Exchange>> X(n);
+    // the ranks' Exchange objects (plan scratch, send / receive buffers: grow-only) are kept per device
+    // across calls, so a repeated merge allocates nothing and the per-rank times exclude hipMalloc; never
+    // destroyed (a static destructor could run after the HIP runtime's teardown)
+    static std::mutex cache_mu;
+    static auto* cache = new std::map<int, std::vector<std::unique_ptr<Exchange>>>();
+    std::lock_guard<std::mutex> cache_lock(cache_mu);
+    std::vector<std::unique_ptr<Exchange>>& X = (*cache)[locals[0]->device];
+    if ((int)X.size() < n) X.resize(n);
+    for (int s = 0; s < n; ++s) {
+        if (!X[s]) X[s].reset(new Exchange());
+    }
     for (int s = 0; s < n; ++s) {
         const auto t0 = std::chrono::steady_clock::now();
-        X[s].reset(new Exchange());
         if (xchg_prepare(*X[s], st, dkeys, n, mx, s, mode, root, locals[s], outs[s], nullptr, nullptr)) return 1;
         MQR_CHECK_HIP(hipStreamSynchronize(st));
         t_local_ms[s] += std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();

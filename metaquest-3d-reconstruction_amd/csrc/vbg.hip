@@ -8,7 +8,8 @@
 //   table  keys u64 / vals i32 / mask u64 x2 (batch parity), open addressing, capacity >= 2x live keys
 //   lists  slots touched by the current batch (appended once per batch, on first touch), x2
 //
-// Per batch of <= 127 frames (the first of a call <= 64): k_touch (one thread per stride-4 pixel per frame, 4 ray samples,
+// Per batch of <= 127 frames (the first of a call a full batch too; variant bits 21-23 shorten it for A/Bs): k_touch
+// (two stride-4 pixels per thread per frame, 4 ray samples,
 // hash insert, per-slot frame bitmask) -> host reads the batch counters (pool growth, empty-frame
 // error) -> k_integrate (one workgroup per touched block, every voxel applies that block's frames
 // in frame order = bit-identical to sequential per-frame integration).
@@ -360,7 +361,7 @@ static int enqueue_lpt(mqr_vbg* v, int p) {
 // first_new: the pool size before this batch's allocations (its blocks start at (0, 0)).
 // spec > 0: speculative launch (first batch of a call, counters not read yet): the kernels read the
 // shadow counters k_gate fills, the grid is `spec` workgroups (they loop over the list), and the
-// caller accounts the launch in the stats once the counters confirm it (spec_commit).
+// caller (mqr_integrate_frames) accounts the launch in the stats once the counters confirm it.
 static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, int H, int W, int nframes,
                             float depth_scale, float depth_max, float sdf_trunc, int first_new, int64_t spec = 0) {
     const int64_t n = spec > 0 ? spec : std::min<int64_t>(v->hctr(p)[kListCount], v->list_cap);
@@ -985,7 +986,8 @@ int mqr_integrate_frames(mqr_vbg* v, const float* depths, int depth_loc, int B, 
         if (!frame_ok || frame_ok[i]) valid.push_back(i);
     int rc = 0;
     int batch = 0;
-    // batches of up to batch_frames frames (127), the first of a call shorter (64): its touch runs
+    // batches of up to batch_frames frames (127), the first of a call a full batch as well
+    // (first_batch_frames; variant bits 21-23 shorten it for A/Bs): its touch runs
     // before any integrate, the later ones behind the previous batch's integrate
     const size_t nb = (size_t)std::max(1, std::min(v->batch_frames, kMaxBatch));
     const size_t nb0 = (size_t)std::max(1, std::min(v->first_batch_frames, (int)nb));
