@@ -10,6 +10,7 @@
 #   n2          2-rank rehearsal on one GPU (gloo-staged merge)        -> gpurun_out/${TAG}_bench_n2.json
 #   prof        rocprofv3 --kernel-trace --stats of the C2 bench      -> gpurun_out/${TAG}_bench_kernel_stats.csv
 #   profc5      the same over the C5 leg alone                        -> gpurun_out/${TAG}_c5_kernel_stats.csv
+#   xtrace      kernel trace of 30 extractions: wall vs device span vs gaps -> gpurun_out/${TAG}_extract_timeline.json
 #   traffic     FETCH_SIZE / WRITE_SIZE passes (tools/pmc_traffic.sh) -> profiles/${TAG}_pmc_traffic.json
 #   abint:V     tools/ab_integrate.py over integrate variants V (comma separated, A/B library)
 #   abext:M     tools/ab_extract.py over extraction modes M (A/B library)
@@ -58,6 +59,12 @@ for step in ${STEPS:-tests}; do
         || { tail -20 gpurun_out/${TAG}_prof_c5.err; exit 1; }
       find gpurun_out/profc5 -name "*kernel_stats.csv" -exec cp {} gpurun_out/${TAG}_c5_kernel_stats.csv \;
       grep "mqr" gpurun_out/${TAG}_c5_kernel_stats.csv | cut -c1-70 | head -16 ;;
+    xtrace)
+      rm -rf gpurun_out/xt
+      timeout -k 10 300 rocprofv3 --kernel-trace -f csv -d gpurun_out/xt -o run -- \
+        python tools/extract_timeline.py --run --walls gpurun_out/xt_walls.json > gpurun_out/${TAG}_xt.log 2>&1 || { tail -20 gpurun_out/${TAG}_xt.log; exit 1; }
+      python tools/extract_timeline.py --analyze "$(find gpurun_out/xt -name '*kernel_trace.csv' | head -1)" gpurun_out/xt_walls.json \
+        > gpurun_out/${TAG}_extract_timeline.json && cat gpurun_out/${TAG}_extract_timeline.json ;;
     traffic)
       ROUND=$TAG timeout -k 10 600 bash tools/pmc_traffic.sh > gpurun_out/${TAG}_pmc_traffic.log 2>&1 || { tail -20 gpurun_out/${TAG}_pmc_traffic.log; exit 1; }
       mkdir -p gpurun_out/profiles_new && cp profiles/${TAG}_pmc_traffic.json profiles/${TAG}_pmc_fetch.csv profiles/${TAG}_pmc_write.csv gpurun_out/profiles_new/
