@@ -245,6 +245,83 @@ static int ensure_depth(mqr_vbg* v, int64_t floats) {
     return ok;
 }
 
+#if MQR_AB
+// The A/B library's integrate variants (launch_integrate's variant list; kernels in vbg_ab.hpp).  *fixup: the
+// caller runs the exact fix-up launch behind the kernel (the kernels that hand blocks back).
+static int launch_integrate_ab(mqr_vbg* v, int var, hipStream_t s, unsigned grid, unsigned lean_grid, int grouped,
+                               const int32_t* list, const bmask_t* lmask, int* counters, const Table& t,
+                               const float* depths, int64_t HW, int H, int W, const FrameParams* fp,
+                               const int64_t* depth_frame, float depth_max, float sdf_trunc, int first_new,
+                               int32_t* bad_out, bool* fixup) {
+    // k_integrate_lean_ab<16, 512, MAP, WPE, ILP, PAIR, DIV1, ZBLK, FIXIN>
+    auto lean = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(lean_grid), dim3(512), 0, s, list, lmask, bad_out, counters, v->list_cap, t,
+                           v->pool, v->voxel_size, depths, HW, H, W, fp, depth_frame, depth_max, sdf_trunc, first_new,
+                           grouped);
+    };
+    auto win = [&](auto kern, unsigned nt) {
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(nt), 0, s, list, lmask, counters, v->list_cap, t, v->pool,
+                           v->voxel_size, depths, HW, H, W, fp, depth_frame, depth_max, sdf_trunc, first_new);
+    };
+    *fixup = var <= 22;
+    switch (var) {
+        case 3: lean(k_integrate_lean_ab<16, 512>); break;  // plate map
+        case 5:
+            hipLaunchKernelGGL((k_integrate_lt<1>), dim3(grid), dim3(512), 0, s, list, lmask, bad_out, counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp, depth_frame,
+                               depth_max, sdf_trunc, first_new);
+            break;
+        case 6: lean(k_integrate_lean_ab<16, 512, 1, 8, 1, 1>); break;  // paired gathers, 8 waves (spills)
+        case 7: lean(k_integrate_lean_ab<16, 512, 1, 6, 1, 1>); break;  // paired gathers, 6 waves
+        case 8: lean(k_integrate_lean_ab<16, 512, 1, 8, 2, 2>); break;  // VALU-lean projection / update
+        case 9: lean(k_integrate_lean_ab<16, 512, 1, 8, 2, 3>); break;  // + zc checked per block
+        case 10:                                                         // + one-correction s / trunc
+            if (strunc_one_correction_ok(sdf_trunc)) lean(k_integrate_lean_ab<16, 512, 1, 8, 2, 3, 1>);
+            else lean(k_integrate_lean_ab<16, 512, 1, 8, 2, 3>);
+            break;
+        case 11: lean(k_integrate_lean_ab<16, 512, 1, 5, 2, 4>); break;  // 16-byte windows, >= 5 waves
+        case 12: lean(k_integrate_lean_ab<16, 512, 1, 4, 2, 4>); break;  // 16-byte windows, >= 4 waves
+        case 13: lean(k_integrate_lean_ab<16, 512, 1, 6, 2, 5>); break;  // 8-byte windows, >= 6 waves
+        case 14: lean(k_integrate_lean_ab<16, 512, 1, 5, 1, 4>); break;  // 16-byte windows, ILP 1
+        case 15: lean(k_integrate_lean_ab<16, 512, 1, 7, 2, 5>); break;  // the round-3 default (fix-up launch)
+        case 16: lean(k_integrate_lean_ab<16, 512, 1, 6, 2, 5, 0, true>); break;  // zc checked per block
+        case 17:                                                                  // 16 + one-correction
+            if (strunc_one_correction_ok(sdf_trunc)) lean(k_integrate_lean_ab<16, 512, 1, 6, 2, 5, 1, true>);
+            else lean(k_integrate_lean_ab<16, 512, 1, 6, 2, 5, 0, true>);
+            break;
+        case 18: lean(k_integrate_lean_ab<16, 512, 1, 6, 4, 5>); break;  // 4 interleaved voxel chains
+        case 19: lean(k_integrate_lean_ab<16, 512, 1, 6, 2, 6>); break;  // 16-byte windows in two halves
+        case 20: lean(k_integrate_lean_ab<16, 512, 1, 7, 2, 7>); break;  // 8-byte windows in two halves
+        case 21:                                                          // default + one-correction
+            if (strunc_one_correction_ok(sdf_trunc)) lean(k_integrate_lean_ab<16, 512, 1, 6, 2, 5, 1>);
+            else lean(k_integrate_lean_ab<16, 512, 1, 7, 2, 5>);
+            break;
+        case 22:  // 21 + zc checked per block, >= 5 waves
+            if (strunc_one_correction_ok(sdf_trunc)) lean(k_integrate_lean_ab<16, 512, 1, 5, 2, 5, 1, true>);
+            else lean(k_integrate_lean_ab<16, 512, 1, 7, 2, 5>);
+            break;
+        case 23: lean(k_integrate_lean_ab<16, 512, 1, 7, 2, 5, 0, false, true>); break;  // the round-4 default
+        case 24: win(k_integrate_win_ab<512, 7, 0>, 512); break;    // plain frame loop
+        case 25: win(k_integrate_win_ab<512, 6, 1>, 512); break;    // frames pipelined, >= 6 waves
+        case 26: win(k_integrate_win_ab<1024, 8, 1>, 1024); break;  // 1024 threads, frames pipelined
+        case 27: win(k_integrate_win_ab<1024, 8, 0>, 1024); break;  // 1024 threads, plain
+        case 28: win(k_integrate_win_ab<512, 7, 1>, 512); break;    // frames pipelined, >= 7 waves
+        case 29: win(k_integrate_win_ab<512, 7, 2>, 512); break;    // half-frame pipeline, >= 7 waves
+        case 30: win(k_integrate_win_ab<1024, 8, 2>, 1024); break;  // half-frame pipeline, 1024 threads
+        case 31: win(k_integrate_win_ab<512, 6, 2>, 512); break;    // half-frame pipeline, >= 6 waves
+        case 32: win(k_integrate_win_ab<512, 7, 0, 1>, 512); break;  // timing diagnostics (wrong results)
+        case 33: win(k_integrate_win_ab<512, 7, 0, 2>, 512); break;
+        case 34: win(k_integrate_win_ab<512, 6, 2, 1>, 512); break;
+        case 35: win(k_integrate_win_ab<512, 6, 2, 2>, 512); break;
+        case 36: win(k_integrate_pk<7, 0>, 512); break;  // packed FP32
+        case 37: win(k_integrate_pk<7, 2>, 512); break;
+        case 38: win(k_integrate_pk<6, 2>, 512); break;
+        case 39: win(k_integrate_pk<6, 0>, 512); break;
+        default: set_error("integrate variant " + std::to_string(var) + " unknown"); return 2;
+    }
+    return 0;
+}
+#endif
+
 // Host twin of den_unsafe(): true unless 2^-60 <= |x| <= 2^60.
 static bool div_unsafe_host(float x) {
     const float m = std::fabs(x);
@@ -387,8 +464,8 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
     }
     v->lpt_ready[p] = false;
     // the lean kernels run k_xcd_order's groups on the workgroups that share an XCD
-    const int grouped = (v->xcd_order && lmask) ? 1 : 0;
-    const unsigned lean_grid =
+    [[maybe_unused]] const int grouped = (v->xcd_order && lmask) ? 1 : 0;
+    [[maybe_unused]] const unsigned lean_grid =
         grouped ? (unsigned)(kNumGroups * std::min<int64_t>((3 * n / 2 + kNumGroups - 1) / kNumGroups, 1024)) : grid;
     if (v->pipelined && (touch_wait || spec > 0)) {
         MQR_CHECK_HIP(hipEventRecord(v->touch_ev(p), v->stream));
@@ -406,25 +483,26 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
         MQR_REQUIRE(e0 && e1, "profiling: event creation failed");
         MQR_CHECK_HIP(hipEventRecord(e0, s));
     }
-    // The fast kernels (k_integrate_lean, k_integrate_lt) evaluate s / sdf_trunc through the division
+    // The fast kernels (k_integrate_win, k_integrate_lean) evaluate s / sdf_trunc through the division
     // core (div_rn_core: exact while the denominator is in [2^-60, 2^60]), take depth in metres
     // (depth_scale 1: Open3D's d / 1 is d), and address the frame with 32-bit byte offsets that
     // must stay past 4HW for out-of-image voxels.  Otherwise the exact k_integrate_t runs alone.
     const bool lean_ok = !div_unsafe_host(sdf_trunc) && depth_scale == 1.0f && 4 * (HW + W) <= (int64_t{1} << 31);
     // Variants (mqr_vbg_set_variant, low byte; all bit-identical, tests/test_gpu_numerics.py):
-    //   0 default: k_integrate_lean -- R = 16: brick map, 8-byte window depth reads (lean_gather_w,
-    //     >= 7 waves per SIMD, 2 interleaved voxel chains) when the frames allow them (even H W,
-    //     8-byte aligned stack), else variant 4;  R = 8: plate map, dword gathers;
-    //   1 generic k_integrate (runtime R);  2 exact k_integrate_t;  4 k_integrate_lean with dword
-    //     gathers at >= 8 waves per SIMD (the round-2 default);
-    //   A/B library only (MQR_AB, vbg_ab.hpp): 3 plate map;  5 packed LDS tiles (k_integrate_lt);
-    //     6 / 7 paired-lane gathers;  8 VALU-lean projection / update, 9 + zc checked per block, 10 +
-    //     one-correction s / trunc;  11 / 12 / 14 / 19 16-byte windows;  13 / 16 / 17 / 18 / 20 / 21 /
-    //     22 8-byte windows at 6 waves / SIMD, with the block zc check, one-correction division, ILP 4,
-    //     in two halves (15 = the round-3 default: the same kernel with the exact path in a fix-up
-    //     launch);  23 = the default.  (24, a
-    //     ballot skip of out-of-image wave slots, ran 0.70 vs 0.48 ms per launch: removed.)
-    //     DESIGN.md §4.1 has the measurements behind the choice.
+    //   0 default -- R = 16: k_integrate_win (brick map, 8-byte window depth reads, >= 7 waves per SIMD,
+    //     blocks outside the proven ranges redone in-kernel) when the frames allow the window reads (even
+    //     H W, 8-byte aligned stack), else variant 4;  R = 8: k_integrate_lean, plate map, dword gathers;
+    //   1 generic k_integrate (runtime R);  2 exact k_integrate_t;  4 k_integrate_lean with dword gathers
+    //     at >= 8 waves per SIMD (the round-2 default) + the exact fix-up launch;
+    //   A/B library only (MQR_AB, vbg_ab.hpp; DESIGN.md §4.1 has the measurements): 3 plate map;  5 packed
+    //     LDS tiles (k_integrate_lt);  6 / 7 paired-lane gathers;  8 VALU-lean projection / update, 9 + zc
+    //     checked per block, 10 + one-correction s / trunc;  11 / 12 / 14 / 19 16-byte windows;  13 / 16 /
+    //     17 / 18 / 20 / 21 / 22 8-byte windows at 6 waves / SIMD, with the block zc check, one-correction
+    //     division, ILP 4, in two halves;  15 = the round-3 default (the exact path in a fix-up launch);
+    //     23 = the round-4 default (k_integrate_lean_ab with the same arithmetic as 0);  24-31 the frame
+    //     loop software-pipelined / 1024-thread workgroups (k_integrate_win_ab);  32-35 timing diagnostics
+    //     (wrong results);  36-39 packed FP32 (k_integrate_pk).  (24 of round 4, a ballot skip of
+    //     out-of-image wave slots, ran 0.70 vs 0.48 ms per launch: removed.)
     int var = v->kernel_variant;
     if (var < 0 || var > 39) var = 0;
     if (!MQR_AB && var != 1 && var != 2 && var != 4) var = 0;
@@ -443,6 +521,7 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
     const int32_t* bad_list = v->bad[p];
     const bmask_t* bad_mask = reinterpret_cast<const bmask_t*>(v->bad[p] + v->list_cap);
     int* bad_count = counters + kBadCount;
+    bool fixup = false;  // the exact fix-up launch over the blocks a fast kernel handed back
     if (var == 1) {
         hipLaunchKernelGGL(k_integrate, dim3(grid), dim3(256), 0, s, list, counters, v->list_cap, t, v->pool, v->R,
                            v->voxel_size, depths, HW, H, W, fp, depth_frame, depth_scale, depth_max, sdf_trunc, first_new);
@@ -451,133 +530,21 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
             hipLaunchKernelGGL((k_integrate_t<16, 4, 512>), dim3(grid), dim3(512), 0, s, list, lmask,
                                counters + kListCount, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp,
                                depth_frame, depth_scale, depth_max, sdf_trunc, first_new);
+        } else if (var == 4) {  // dword gathers (frames the window reads cannot take)
+            hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 8, 2>), dim3(grid), dim3(512), 0, s, list, lmask,
+                               v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp,
+                               depth_frame, depth_max, sdf_trunc, first_new);
+            fixup = true;
+        } else if (var == 0) {
+            hipLaunchKernelGGL(k_integrate_win<7>, dim3(grid), dim3(512), 0, s, list, lmask, counters, v->list_cap, t,
+                               v->pool, v->voxel_size, depths, HW, H, W, fp, depth_frame, depth_max, sdf_trunc,
+                               first_new);
         } else {
 #if MQR_AB
-            // k_integrate_win (8-byte windows): 24 = the default's plain frame loop, 25 = software-pipelined
-            // frames at >= 6 waves / SIMD, 26 / 27 = 1024 threads (4 voxels each) pipelined / plain at >= 8,
-            // 28 = pipelined forced to >= 7 waves / SIMD; 29 / 30 = half-frame pipeline, 512 threads at >= 7
-            // waves / 1024 threads at >= 8, 31 = half-frame pipeline, 512 threads at >= 6 waves;
-            // timing diagnostics (wrong results): 32 / 33 = 24 with DIAG 1 / 2, 34 / 35 = 31 with DIAG 1 / 2
-            // packed FP32 (k_integrate_pk): 36 / 37 = plain / half-frame pipeline at >= 7 waves, 38 / 39 = half-frame
-            // pipeline / plain at >= 6
-            if (var >= 24 && var <= 39) {
-                auto win = [&](auto kern, unsigned nt) {
-                    hipLaunchKernelGGL(kern, dim3(grid), dim3(nt), 0, s, list, lmask, counters, v->list_cap, t, v->pool,
-                                       v->voxel_size, depths, HW, H, W, fp, depth_frame, depth_max, sdf_trunc, first_new);
-                };
-                if (var == 24) win(k_integrate_win<512, 7, 0>, 512);
-                else if (var == 25) win(k_integrate_win<512, 6, 1>, 512);
-                else if (var == 26) win(k_integrate_win<1024, 8, 1>, 1024);
-                else if (var == 27) win(k_integrate_win<1024, 8, 0>, 1024);
-                else if (var == 28) win(k_integrate_win<512, 7, 1>, 512);
-                else if (var == 29) win(k_integrate_win<512, 7, 2>, 512);
-                else if (var == 30) win(k_integrate_win<1024, 8, 2>, 1024);
-                else if (var == 31) win(k_integrate_win<512, 6, 2>, 512);
-                else if (var == 32) win(k_integrate_win<512, 7, 0, 1>, 512);
-                else if (var == 33) win(k_integrate_win<512, 7, 0, 2>, 512);
-                else if (var == 34) win(k_integrate_win<512, 6, 2, 1>, 512);
-                else if (var == 35) win(k_integrate_win<512, 6, 2, 2>, 512);
-                else if (var == 36) win(k_integrate_pk<7, 0>, 512);
-                else if (var == 37) win(k_integrate_pk<7, 2>, 512);
-                else if (var == 38) win(k_integrate_pk<6, 2>, 512);
-                else win(k_integrate_pk<6, 0>, 512);
-            } else
-            if (var == 8)  // VALU-lean projection / update (lean_gather_v)
-                hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 8, 2, 2>), dim3(lean_grid), dim3(512), 0, s, list,
-                                   lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H,
-                                   W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
-            else if (var == 9 || (var == 10 && !strunc_one_correction_ok(sdf_trunc)))
-                // variant 8 with the zc range checked once per block (block_zc_unsafe)
-                hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 8, 2, 3>), dim3(lean_grid), dim3(512), 0, s, list,
-                                   lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H,
-                                   W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
-            else if (var == 11)  // 16-byte window gathers (lean_gather_w), >= 5 waves / SIMD
-                hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 5, 2, 4>), dim3(lean_grid), dim3(512), 0, s, list,
-                                   lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H,
-                                   W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
-            else if (var == 12)  // 16-byte window gathers, >= 4 waves / SIMD
-                hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 4, 2, 4>), dim3(lean_grid), dim3(512), 0, s, list,
-                                   lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H,
-                                   W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
-            else if (var == 14)  // 16-byte window gathers, ILP 1, >= 5 waves / SIMD
-                hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 5, 1, 4>), dim3(lean_grid), dim3(512), 0, s, list,
-                                   lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H,
-                                   W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
-            else if (var == 13)  // 8-byte window gathers, >= 6 waves / SIMD (no spill)
-                hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 6, 2, 5>), dim3(lean_grid), dim3(512), 0, s, list,
-                                   lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H,
-                                   W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
-            else if (var == 16 || (var == 17 && !strunc_one_correction_ok(sdf_trunc)))
-                // 8-byte windows, zc checked per block
-                hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 6, 2, 5, 0, true>), dim3(lean_grid), dim3(512), 0, s,
-                                   list, lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW,
-                                   H, W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
-            else if (var == 17)  // 16 + one-correction s / sdf_trunc
-                hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 6, 2, 5, 1, true>), dim3(lean_grid), dim3(512), 0, s,
-                                   list, lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW,
-                                   H, W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
-            else if (var == 18)  // 8-byte windows, 4 interleaved voxel chains
-                hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 6, 4, 5>), dim3(lean_grid), dim3(512), 0, s, list,
-                                   lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H,
-                                   W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
-            else if (var == 19)  // 16-byte windows in two halves (<= 4 window loads in flight), >= 6 waves / SIMD
-                hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 6, 2, 6>), dim3(lean_grid), dim3(512), 0, s, list,
-                                   lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H,
-                                   W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
-            else if (var == 20)  // 8-byte windows in two halves, >= 7 waves / SIMD
-                hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 7, 2, 7>), dim3(lean_grid), dim3(512), 0, s, list,
-                                   lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H,
-                                   W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
-            else if (var == 21 && strunc_one_correction_ok(sdf_trunc))  // default + one-correction s / trunc
-                hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 6, 2, 5, 1>), dim3(lean_grid), dim3(512), 0, s, list,
-                                   lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H,
-                                   W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
-            else if (var == 22 && strunc_one_correction_ok(sdf_trunc))  // 21 + zc checked per block, >= 5 waves / SIMD
-                hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 5, 2, 5, 1, true>), dim3(lean_grid), dim3(512), 0, s,
-                                   list, lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW,
-                                   H, W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
-            else if (var == 15)  // the round-3 default: the exact path in a fix-up launch behind the kernel
-                hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 7, 2, 5>), dim3(lean_grid), dim3(512), 0, s, list,
-                                   lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H,
-                                   W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
-            else if (var == 10)  // variant 9 with s / sdf_trunc in one correction (verified for this sdf_trunc)
-                hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 8, 2, 3, 1>), dim3(lean_grid), dim3(512), 0, s, list,
-                                   lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H,
-                                   W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
-            else if (var == 6)  // paired gather at 8 waves / SIMD (spills) or 6 (variant 7)
-                hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 8, 1, 1>), dim3(lean_grid), dim3(512), 0, s, list,
-                                   lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H,
-                                   W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
-            else if (var == 7)
-                hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 6, 1, 1>), dim3(lean_grid), dim3(512), 0, s, list,
-                                   lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H,
-                                   W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
-            else if (var == 5)
-                hipLaunchKernelGGL((k_integrate_lt<1>), dim3(grid), dim3(512), 0, s, list, lmask, v->bad[p], counters,
-                                   v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp, depth_frame,
-                                   depth_max, sdf_trunc, first_new);
-            else if (var == 3)
-                hipLaunchKernelGGL((k_integrate_lean<16, 512>), dim3(lean_grid), dim3(512), 0, s, list, lmask,
-                                   v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp,
-                                   depth_frame, depth_max, sdf_trunc, first_new, grouped);
-            else
+            if (launch_integrate_ab(v, var, s, grid, lean_grid, grouped, list, lmask, counters, t, depths, HW, H, W, fp,
+                                    depth_frame, depth_max, sdf_trunc, first_new, v->bad[p], &fixup))
+                return 1;
 #endif
-            if (var == 4)  // dword gathers (round-2 default; frames the window reads cannot take)
-                hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 8, 2>), dim3(lean_grid), dim3(512), 0, s, list,
-                                   lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H,
-                                   W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
-            else  // default: 8-byte window reads, >= 7 waves / SIMD (three per-block address words
-                  // spill to scratch outside the frame loop; 1-2 % faster than 6 waves, variant 13); a block
-                  // whose operands leave the proven ranges is redone in-kernel by the exact path
-                  // (exact_block_call), so no fix-up launch follows (2.527 vs 2.551 ms per step, r04)
-                hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 7, 2, 5, 0, false, true>), dim3(lean_grid), dim3(512),
-                                   0, s, list, lmask, v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size,
-                                   depths, HW, H, W, fp, depth_frame, depth_max, sdf_trunc, first_new, grouped);
-            // exact fix-up of the blocks the other fast kernels handed back (usually none: reads a zero count)
-            if (var != 0 && var != 23 && var < 24)
-                hipLaunchKernelGGL((k_integrate_t<16, 4, 512>), dim3(8), dim3(512), 0, s, bad_list, bad_mask, bad_count,
-                                   v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp, depth_frame,
-                                   depth_scale, depth_max, sdf_trunc, first_new);
         }
     } else {  // R == 8
         if (var == 2) {
@@ -585,14 +552,18 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
                                counters + kListCount, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp,
                                depth_frame, depth_scale, depth_max, sdf_trunc, first_new);
         } else {
-            hipLaunchKernelGGL((k_integrate_lean<8, 256>), dim3(lean_grid), dim3(256), 0, s, list, lmask, v->bad[p],
+            hipLaunchKernelGGL((k_integrate_lean<8, 256>), dim3(grid), dim3(256), 0, s, list, lmask, v->bad[p],
                                counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp, depth_frame,
-                               depth_max, sdf_trunc, first_new, grouped);
+                               depth_max, sdf_trunc, first_new);
             hipLaunchKernelGGL((k_integrate_t<8, 2, 256>), dim3(8), dim3(256), 0, s, bad_list, bad_mask, bad_count,
                                v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp, depth_frame, depth_scale,
                                depth_max, sdf_trunc, first_new);
         }
     }
+    if (fixup)  // (usually no block: reads a zero count)
+        hipLaunchKernelGGL((k_integrate_t<16, 4, 512>), dim3(8), dim3(512), 0, s, bad_list, bad_mask, bad_count,
+                           v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp, depth_frame, depth_scale,
+                           depth_max, sdf_trunc, first_new);
     MQR_CHECK_HIP(hipGetLastError());
     if (v->profile) {
         MQR_CHECK_HIP(hipEventRecord(e1, s));

@@ -490,4 +490,553 @@ __device__ void lean_gather_pair(float (&dv)[ZPER], bool& bad, const FrameParams
     }
 }
 
+// ---- VALU-lean projection / update (PAIR = 2, 3) ---------------------------------------------------
+// The same float operations as lean_gather / lean_update with fewer instructions around them:
+//  * in-image test as two unsigned compares of the float bits: 0 <= u <= W - 1 holds exactly when
+//    bits(u) <= bits(W - 1) for every u but -0.0 (sign bit) -- the host replaces a -0.0 principal
+//    point by +0.0, which changes no u and no pixel (x + -0 = x + +0 unless x = -0, and (int)-0 =
+//    (int)+0), so u = -0.0 cannot occur; NaN and negative values compare above the bound;
+//  * min(sdf, trunc) as one v_min_f32: sdf comes out of a subtraction, so it is never a signalling
+//    NaN and IEEE-mode v_min_f32 returns trunc for a NaN sdf, as fminf does (the compiler's fminf adds
+//    a canonicalising v_max_f32 in front);
+//  * (PAIR = 3) the zc range checked once per block and batch (block_zc_unsafe), not per voxel-frame.
+// The depth read stays a gather by every lane through the raw view (out-of-image lanes read 0 past
+// the end): reading under the in-image exec mask kept 8 lane masks live across the gathers, which
+// the compiler spilled to VGPR booleans (3 VALU per voxel-frame) and made the update wait for all 8
+// gathers.
+template <int ZPER, int ILP = 1, bool ZCHK = true>
+__device__ __forceinline__ void lean_gather_v(float (&dv)[ZPER], bool& bad, const FrameParams& fp,
+                                              __amdgpu_buffer_rsrc_t rs, const float (&xs)[ZPER],
+                                              const float (&ys)[ZPER], const float (&zs)[ZPER], uint32_t W4,
+                                              uint32_t past_end, uint32_t hm1_bits, uint32_t wm1_bits) {
+    float e[12];
+#pragma unroll
+    for (int j = 0; j < 12; ++j) e[j] = fp.ext[j];
+    const float fx = fp.fx, fy = fp.fy, cx = fp.cx, cy = fp.cy;
+#pragma unroll
+    for (int k = 0; k < ZPER; ++k) {
+        const float ax = xs[k] * e[0] + ys[k] * e[1];
+        const float ay = xs[k] * e[4] + ys[k] * e[5];
+        const float az = xs[k] * e[8] + ys[k] * e[9];
+        const float xc = (ax + zs[k] * e[2]) + e[3];
+        const float yc = (ay + zs[k] * e[6]) + e[7];
+        const float zc = (az + zs[k] * e[10]) + e[11];
+        if (ZCHK) bad |= (__float_as_uint(zc) - 0x2D800000u) > 0x30000000u;  // not 2^-36 <= zc <= 2^60
+        const float inv_z = rcp_m(zc);
+        const float u = fx * xc * inv_z + cx;
+        const float v = fy * yc * inv_z + cy;
+        const bool in = (__float_as_uint(v) <= hm1_bits) && (__float_as_uint(u) <= wm1_bits);
+        const uint32_t off = in ? __umul24((uint32_t)(int)v, W4) + ((uint32_t)(int)u << 2) : past_end;
+        dv[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
+        if ((k + 1) % ILP == 0) __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+
+// The zc range check of lean_gather (2^-36 <= zc <= 2^60, where rcp_m is exact) once per block and
+// batch instead of per voxel-frame (PAIR = 3): thread (frame j = tid / 8, corner c = tid % 8) bounds
+// zc at one corner of the block's voxel-coordinate box.  The voxel coordinates are the float values
+// fl((float)i * voxel_size), monotone in i, so every voxel lies in the box of the corner values; the
+// exact affine Z = x e8 + y e9 + z e10 + e11 takes its extremes over the box at the corners; the
+// float32 evaluation (three products, three sums) differs from Z by at most gamma_4 A < 2^-21 A,
+// A = max|x| |e8| + max|y| |e9| + max|z| |e10| + |e11| over the box.  A corner with Z - 2^-20 A <
+// 2^-36 or Z + 2^-20 A > 2^60 (or NaN) marks the block bad: the exact fix-up launch redoes it.
+template <int R>
+__device__ __forceinline__ bool block_zc_unsafe_frame(int j, int c, const FrameParams* __restrict__ fps, int xb, int yb,
+                                                      int zb, float voxel_size) {
+    const FrameParams& fp = fps[j];
+    const float xl = (float)(xb * R) * voxel_size, xh = (float)(xb * R + R - 1) * voxel_size;
+    const float yl = (float)(yb * R) * voxel_size, yh = (float)(yb * R + R - 1) * voxel_size;
+    const float zl = (float)(zb * R) * voxel_size, zh = (float)(zb * R + R - 1) * voxel_size;
+    const double e8 = fp.ext[8], e9 = fp.ext[9], e10 = fp.ext[10], e11 = fp.ext[11];
+    const double x = (c & 1) ? xh : xl, y = (c & 2) ? yh : yl, z = (c & 4) ? zh : zl;
+    const double Z = x * e8 + y * e9 + z * e10 + e11;
+    const double A = fmax(fabs((double)xl), fabs((double)xh)) * fabs(e8) +
+                     fmax(fabs((double)yl), fabs((double)yh)) * fabs(e9) +
+                     fmax(fabs((double)zl), fabs((double)zh)) * fabs(e10) + fabs(e11);
+    const double err = A * 0x1p-20;
+    return !(Z - err >= 0x1p-36 && Z + err <= 0x1p60);
+}
+
+template <int R>
+__device__ __forceinline__ bool block_zc_unsafe(int tid, bmask_t mask, const FrameParams* __restrict__ fps, int xb,
+                                                int yb, int zb, float voxel_size) {
+    const int c = tid & 7;
+    bool unsafe = false;
+    for (int j = tid >> 3; j < kMaxBatch; j += 64)  // 512 threads: 64 frames x 8 corners per round
+        if ((mask >> j) & 1) unsafe |= block_zc_unsafe_frame<R>(j, c, fps, xb, yb, zb, voxel_size);
+    return unsafe;
+}
+
+
+// A/B: the round-2..4 lean integrate with all its measured variants (the product keeps k_integrate_lean with
+// dword gathers and k_integrate_win).  Lean integrate, unit depth scale only (host: sdf_trunc in the division core's range).  Block per
+// workgroup, voxels per lean_map<MAP>; every voxel of a block not handed off is written back.
+// WPE: minimum waves per SIMD the register allocation must allow; ILP: voxel chains the scheduler
+// may interleave (lean_gather / lean_update).
+
+// PAIR (A/B library only, variant 6): the paired-lane gather of vbg_ab.hpp.
+// FIXIN: a block whose operands leave the proven ranges is redone by the workgroup itself through the
+// exact path (exact_block, not inlined: its registers stay out of the frame loop's allocation) instead of
+// being handed to the fix-up launch -- no second launch behind every integrate.
+template <int R, int NT>
+__device__ __attribute__((noinline)) void exact_block_call(float2* __restrict__ vox, bool fresh, bmask_t mask, int xb,
+                                                           int yb, int zb, float voxel_size,
+                                                           const float* __restrict__ depths, int64_t HW, int W,
+                                                           float hm1, float wm1, const FrameParams* __restrict__ fps,
+                                                           const int64_t* __restrict__ depth_frame, float depth_max,
+                                                           float sdf_trunc);
+template <int R, int NT, int MAP = 0, int WPE = 1, int ILP = 1, int PAIR = 0, int DIV1 = 0, bool ZBLK = false,
+          bool FIXIN = false>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void k_integrate_lean_ab(
+    const int32_t* __restrict__ list, const bmask_t* __restrict__ lmask, int32_t* __restrict__ bad_out,
+    int* __restrict__ counters, int64_t list_cap, Table t, float2* __restrict__ pool, float voxel_size,
+    const float* __restrict__ depths, int64_t HW, int H, int W, const FrameParams* __restrict__ fps,
+    const int64_t* __restrict__ depth_frame, float depth_max, float sdf_trunc, int first_new, int grouped) {
+    constexpr int R2 = R * R;
+    constexpr int R3 = R2 * R;
+    constexpr int ZPER = R3 / NT;
+    static_assert(R3 % NT == 0 && NT % R2 == 0, "NT must divide R^3 and be a multiple of R^2");
+    static_assert(MAP == 0 || (R == 16 && NT == 512), "the brick map is for R = 16, NT = 512");
+    const int64_t n = min((int64_t)counters[kListCount], list_cap);
+    const float hf = (float)H, hm1 = (float)H - 1.0f, wm1 = (float)W - 1.0f;
+    const uint32_t W4 = 4u * (uint32_t)W, bytes = 4u * (uint32_t)HW;
+    const float y0t = __builtin_amdgcn_rcpf(sdf_trunc);
+    const float y1t = __builtin_fmaf(__builtin_fmaf(-sdf_trunc, y0t, 1.0f), y0t, y0t);
+    const int tid = threadIdx.x;
+    int vx, vy, vz;
+    lean_map<R, NT, MAP>(tid, vx, vy, vz);
+    const uint32_t voff = 8u * (uint32_t)(vx + R * vy + R2 * vz);  // byte offset of voxel 0 in its block
+    // grouped (k_xcd_order): the workgroups with blockIdx % 8 == g run group g (grid % 8 == 0)
+    int64_t i = blockIdx.x, iend = n, step = gridDim.x;
+    if (grouped) {
+        const int g = blockIdx.x % kNumGroups;
+        i = counters[kGroupBase + g] + blockIdx.x / kNumGroups;
+        iend = counters[kGroupBase + g + 1];
+        step = gridDim.x / kNumGroups;
+    }
+    for (; i < iend; i += step) {
+        const int32_t slot = list[i];
+        const int buf = __builtin_amdgcn_readfirstlane(t.vals[slot]);
+        const bmask_t mask = readfirstlane_mask(lmask ? lmask[i] : bm_frames(t.mask[slot]));
+        int xb, yb, zb;
+        unpack_key(t.keys[slot], xb, yb, zb);
+        if (buf >= 0 && mask) {
+            const __amdgpu_buffer_rsrc_t vox = __builtin_amdgcn_make_buffer_rsrc(
+                pool + (int64_t)buf * R3, (short)0, (int)(R3 * sizeof(float2)), 0x00020000);
+            float2 tw[ZPER];
+            float xs[ZPER], ys[ZPER], zs[ZPER];
+            bool bad = false;
+            const float xs0 = (float)(xb * R + vx) * voxel_size;
+#pragma unroll
+            for (int k = 0; k < ZPER; ++k) {
+                const int dy = lean_dy<R, NT, MAP>(k), dz = lean_dz<R, NT, MAP>(k);
+                // a block allocated by this batch (buffer >= first_new) starts at (0, 0): the pool is
+                // not cleared on reset or growth
+                tw[k] = buf >= first_new ? make_float2(0.f, 0.f)
+                                         : pool_load(vox, voff, (R * dy + R2 * dz) * (int)sizeof(float2));
+                xs[k] = xs0;
+                ys[k] = (float)(yb * R + vy + dy) * voxel_size;
+                zs[k] = (float)(zb * R + vz + dz) * voxel_size;
+                const float w = tw[k].y;  // rcp_m(w + 1) is exact for integer w <= 2^23 + 64: a batch adds <= 127
+                bad |= !(w >= 0.0f && w <= 0x1p23f - 64.0f && w == __builtin_truncf(w));
+            }
+            bmask_t m = mask;
+            if constexpr (PAIR == 3 || ZBLK) {  // block-level zc range check (block_zc_unsafe): skip the frame loop
+                static_assert(NT == 512, "one (frame, corner) per thread");
+                if (__syncthreads_or(block_zc_unsafe<R>(tid, mask, fps, xb, yb, zb, voxel_size))) bad = true, m = 0;
+            }
+            while (m) {
+                const int f = bm_ctz(m);
+                m &= m - 1;
+                float dv[ZPER];
+                if constexpr (PAIR == 6 || PAIR == 7) {  // windows in two halves: <= 4 window loads in flight
+                    constexpr int H2 = ZPER / 2;
+                    const __amdgpu_buffer_rsrc_t rsf = frame_rsrc(depths + depth_frame[f] * HW, bytes);
+                    constexpr int WB = PAIR == 6 ? 16 : 8;
+                    lean_gather_w<ZPER, ILP, WB, true, 0, H2>(dv, bad, fps[f], rsf, xs, ys, zs, W4, bytes,
+                                                              __float_as_uint(hm1), __float_as_uint(wm1));
+                    __builtin_amdgcn_sched_barrier(0);
+                    lean_update_v<ZPER, ILP, DIV1, 0, H2>(tw, dv, fps[f], xs, ys, zs, depth_max, sdf_trunc, y1t);
+                    __builtin_amdgcn_sched_barrier(0);
+                    lean_gather_w<ZPER, ILP, WB, true, H2, ZPER>(dv, bad, fps[f], rsf, xs, ys, zs, W4, bytes,
+                                                                 __float_as_uint(hm1), __float_as_uint(wm1));
+                    __builtin_amdgcn_sched_barrier(0);
+                    lean_update_v<ZPER, ILP, DIV1, H2, ZPER>(tw, dv, fps[f], xs, ys, zs, depth_max, sdf_trunc, y1t);
+                    continue;
+                } else if constexpr (PAIR == 4 || PAIR == 5) {
+                    lean_gather_w<ZPER, ILP, PAIR == 4 ? 16 : 8, !ZBLK>(dv, bad, fps[f], frame_rsrc(depths + depth_frame[f] * HW, bytes),
+                                                                  xs, ys, zs, W4, bytes, __float_as_uint(hm1),
+                                                                  __float_as_uint(wm1));
+                    lean_update_v<ZPER, ILP, DIV1>(tw, dv, fps[f], xs, ys, zs, depth_max, sdf_trunc, y1t);
+                    continue;
+                } else if constexpr (PAIR == 2 || PAIR == 3) {
+                    lean_gather_v<ZPER, ILP, PAIR == 2>(dv, bad, fps[f], frame_rsrc(depths + depth_frame[f] * HW, bytes),
+                                                         xs, ys, zs, W4, bytes, __float_as_uint(hm1), __float_as_uint(wm1));
+                    lean_update_v<ZPER, ILP, DIV1>(tw, dv, fps[f], xs, ys, zs, depth_max, sdf_trunc, y1t);
+                    continue;
+                } else if constexpr (PAIR) {
+                    static_assert(MAP == 1, "pairs are the x-adjacent lanes of the brick map");
+                    lean_gather_pair<ZPER, ILP>(dv, bad, fps[f], frame_rsrc(depths + depth_frame[f] * HW, bytes), xs,
+                                                ys, zs, W4, hf, hm1, wm1, bytes);
+                } else {
+                    lean_gather<ZPER, ILP>(dv, bad, fps[f], frame_rsrc(depths + depth_frame[f] * HW, bytes), xs, ys,
+                                           zs, W4, hf, hm1, wm1);
+                }
+                lean_update<ZPER, ILP>(tw, dv, fps[f], xs, ys, zs, depth_max, sdf_trunc, y1t);
+            }
+            if (__syncthreads_or(bad)) {  // block-uniform: the exact path redoes it from the pool
+                if constexpr (FIXIN)
+                    exact_block_call<R, NT>(pool + (int64_t)buf * R3, buf >= first_new, mask, xb, yb, zb, voxel_size,
+                                            depths, HW, W, hm1, wm1, fps, depth_frame, depth_max, sdf_trunc);
+                else if (tid == 0)
+                    hand_off(bad_out, counters, list_cap, slot, mask);
+            } else {
+#pragma unroll
+                for (int k = 0; k < ZPER; ++k)
+                    pool_store(vox, voff, (R * lean_dy<R, NT, MAP>(k) + R2 * lean_dz<R, NT, MAP>(k)) * (int)sizeof(float2),
+                               tw[k]);
+            }
+        }
+        __syncthreads();
+        if (tid == 0) t.mask[slot] = 0;
+    }
+}
+
+// ---- A/B: k_integrate_win with a software-pipelined frame loop, 1024-thread workgroups, timing diagnostics -------------------------------
+// k_integrate_lean<16, 512, brick, WPE, 2, 8-byte windows, FIXIN>'s arithmetic (lean_gather_w /
+// lean_update_v: bit-identical), with the brick map generalised to NT threads and, for PIPE, the frame
+// loop unrolled by two with the roles of two depth-register sets alternating: frame f_next's projection
+// and window loads are issued BEFORE frame f's running-average update, so a wave keeps one frame's loads
+// in flight while it updates the previous one (the plain loop issues frame f's loads and at once waits
+// for them in frame f's update: nothing of f + 1 is in flight).  The per-voxel update order stays frame
+// order.  NT = 512: 8 voxels per thread (+8 VGPRs for the second set); NT = 1024: 4 voxels per thread.
+// Map: lane l of wave w owns x = l % 8 + 8 (w % 2), y = (l / 8) % 2 + 2 (w / 2), z = l / 16 (a wave's
+// voxels k form an 8 x 2 x 4 brick); voxel k sits at (x, y + 8 (k / 4), z + 4 (k % 4)) for NT = 512
+// and at (x, y, z + 4 k) for NT = 1024.
+
+// DIAG (A/B library timing diagnostics, wrong results): 1 = the bare v_rcp for 1 / zc and 1 / (w + 1) and
+// one product for s / sdf_trunc (about a third of the frame loop's VALU work gone); 2 = every frame's depth
+// read from the batch's first frame (a 1.2 MB working set that stays in L2: the refetch of each XCD's
+// frames from the MALL taken away).
+template <int NT, int WPE, int PIPE, int DIAG = 0>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void k_integrate_win_ab(
+    const int32_t* __restrict__ list, const bmask_t* __restrict__ lmask, int* __restrict__ counters, int64_t list_cap,
+    Table t, float2* __restrict__ pool, float voxel_size, const float* __restrict__ depths, int64_t HW, int H, int W,
+    const FrameParams* __restrict__ fps, const int64_t* __restrict__ depth_frame, float depth_max, float sdf_trunc,
+    int first_new) {
+    constexpr int R = 16, R2 = R * R, R3 = R2 * R;
+    constexpr int ZPER = R3 / NT;
+    static_assert(NT == 512 || NT == 1024, "brick map for 512 or 1024 threads");
+    const int64_t n = min((int64_t)counters[kListCount], list_cap);
+    const float hm1 = (float)H - 1.0f, wm1 = (float)W - 1.0f;
+    const uint32_t W4 = 4u * (uint32_t)W, bytes = 4u * (uint32_t)HW;
+    const uint32_t hb = __float_as_uint(hm1), wb = __float_as_uint(wm1);
+    const float y0t = __builtin_amdgcn_rcpf(sdf_trunc);
+    const float y1t = __builtin_fmaf(__builtin_fmaf(-sdf_trunc, y0t, 1.0f), y0t, y0t);
+    const int tid = threadIdx.x;
+    const int l = tid & 63, w = tid >> 6;
+    const int vx = (l & 7) + 8 * (w & 1), vy = ((l >> 3) & 1) + 2 * (w >> 1), vz = l >> 4;
+    const uint32_t voff = 8u * (uint32_t)(vx + R * vy + R2 * vz);  // byte offset of voxel 0 in its block
+    for (int64_t i = blockIdx.x; i < n; i += gridDim.x) {
+        const int32_t slot = list[i];
+        const int buf = __builtin_amdgcn_readfirstlane(t.vals[slot]);
+        const bmask_t mask = readfirstlane_mask(lmask ? lmask[i] : bm_frames(t.mask[slot]));
+        int xb, yb, zb;
+        unpack_key(t.keys[slot], xb, yb, zb);
+        if (buf >= 0 && mask) {
+            const __amdgpu_buffer_rsrc_t vox = __builtin_amdgcn_make_buffer_rsrc(
+                pool + (int64_t)buf * R3, (short)0, (int)(R3 * sizeof(float2)), 0x00020000);
+            float2 tw[ZPER];
+            float xs[ZPER], ys[ZPER], zs[ZPER];
+            bool bad = false;
+            const float xs0 = (float)(xb * R + vx) * voxel_size;
+#pragma unroll
+            for (int k = 0; k < ZPER; ++k) {
+                const int dy = win_dy<NT>(k), dz = win_dz<NT>(k);
+                // a block allocated by this batch (buffer >= first_new) starts at (0, 0)
+                tw[k] = buf >= first_new ? make_float2(0.f, 0.f)
+                                         : pool_load(vox, voff, (R * dy + R2 * dz) * (int)sizeof(float2));
+                xs[k] = xs0;
+                ys[k] = (float)(yb * R + vy + dy) * voxel_size;
+                zs[k] = (float)(zb * R + vz + dz) * voxel_size;
+                const float wv = tw[k].y;  // rcp_m(w + 1) is exact for integer w <= 2^23 + 64
+                bad |= !(wv >= 0.0f && wv <= 0x1p23f - 64.0f && wv == __builtin_truncf(wv));
+            }
+            const int64_t f0 = depth_frame[bm_ctz(mask)];
+            auto dframe = [&](int f) { return DIAG == 2 ? f0 : depth_frame[f]; };
+            auto gather = [&](float (&dv)[ZPER], int f) {
+                lean_gather_w<ZPER, 2, 8, true, 0, ZPER, DIAG == 1>(dv, bad, fps[f],
+                                                                   frame_rsrc(depths + dframe(f) * HW, bytes), xs, ys,
+                                                                   zs, W4, bytes, hb, wb);
+            };
+            auto update = [&](const float (&dv)[ZPER], int f) {
+                lean_update_v<ZPER, 2, 0, 0, ZPER, DIAG == 1>(tw, dv, fps[f], xs, ys, zs, depth_max, sdf_trunc, y1t);
+            };
+            bmask_t m = mask;
+            float da[ZPER];
+            if constexpr (PIPE == 2) {
+                // half-frame pipeline: the voxels in two halves h0 / h1 and one depth-register set; steady
+                // state per frame f: gather h0(f), update h1(f_prev), gather h1(f), update h0(f) -- each
+                // half's update runs while the other half's loads are in flight
+                constexpr int H2 = ZPER / 2;
+                auto g0 = [&](int f) {
+                    lean_gather_w<ZPER, 2, 8, true, 0, H2, DIAG == 1>(da, bad, fps[f],
+                                                                     frame_rsrc(depths + dframe(f) * HW, bytes), xs, ys,
+                                                                     zs, W4, bytes, hb, wb);
+                };
+                auto g1 = [&](int f) {
+                    lean_gather_w<ZPER, 2, 8, true, H2, ZPER, DIAG == 1>(da, bad, fps[f],
+                                                                        frame_rsrc(depths + dframe(f) * HW, bytes), xs,
+                                                                        ys, zs, W4, bytes, hb, wb);
+                };
+                auto u0 = [&](int f) {
+                    lean_update_v<ZPER, 2, 0, 0, H2, DIAG == 1>(tw, da, fps[f], xs, ys, zs, depth_max, sdf_trunc, y1t);
+                };
+                auto u1 = [&](int f) {
+                    lean_update_v<ZPER, 2, 0, H2, ZPER, DIAG == 1>(tw, da, fps[f], xs, ys, zs, depth_max, sdf_trunc, y1t);
+                };
+                int fp = bm_ctz(m);
+                m &= m - 1;
+                g0(fp);
+                __builtin_amdgcn_sched_barrier(0);
+                g1(fp);
+                __builtin_amdgcn_sched_barrier(0);
+                u0(fp);
+                while (m) {
+                    const int f = bm_ctz(m);
+                    m &= m - 1;
+                    __builtin_amdgcn_sched_barrier(0);
+                    g0(f);
+                    __builtin_amdgcn_sched_barrier(0);
+                    u1(fp);
+                    __builtin_amdgcn_sched_barrier(0);
+                    g1(f);
+                    __builtin_amdgcn_sched_barrier(0);
+                    u0(f);
+                    fp = f;
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                u1(fp);
+            } else if constexpr (PIPE) {
+                float db[ZPER];
+                int fa = bm_ctz(m);
+                m &= m - 1;
+                gather(da, fa);
+                for (;;) {
+                    if (!m) {
+                        update(da, fa);
+                        break;
+                    }
+                    const int fb = bm_ctz(m);
+                    m &= m - 1;
+                    gather(db, fb);  // frame fb's loads in flight ...
+                    __builtin_amdgcn_sched_barrier(0);
+                    update(da, fa);  // ... while frame fa is applied
+                    if (!m) {
+                        update(db, fb);
+                        break;
+                    }
+                    fa = bm_ctz(m);
+                    m &= m - 1;
+                    gather(da, fa);
+                    __builtin_amdgcn_sched_barrier(0);
+                    update(db, fb);
+                }
+            } else {
+                while (m) {
+                    const int f = bm_ctz(m);
+                    m &= m - 1;
+                    gather(da, f);
+                    update(da, f);
+                }
+            }
+            if (__syncthreads_or(bad)) {  // block-uniform: the exact path redoes it from the pool
+                exact_block_call<R, NT>(pool + (int64_t)buf * R3, buf >= first_new, mask, xb, yb, zb, voxel_size, depths,
+                                        HW, W, hm1, wm1, fps, depth_frame, depth_max, sdf_trunc);
+            } else {
+#pragma unroll
+                for (int k = 0; k < ZPER; ++k)
+                    pool_store(vox, voff, (R * win_dy<NT>(k) + R2 * win_dz<NT>(k)) * (int)sizeof(float2), tw[k]);
+            }
+        }
+        __syncthreads();
+        if (tid == 0) t.mask[slot] = 0;
+    }
+}
+
+// ---- packed-FP32 integrate (R = 16, NT = 512) --------------------------------------------------------------
+// k_integrate_win's float operations two voxels at a time: voxels (2p, 2p + 1) of a thread share x and y and
+// differ in z, so their transform, projection, reciprocal corrections and running-average update map onto
+// gfx950's packed FP32 instructions (v_pk_mul_f32 / v_pk_add_f32 / v_pk_fma_f32: two IEEE round-to-nearest
+// results, exactly the scalar instructions' -- no contraction is introduced, the fma calls are the scalar
+// code's own).  v_rcp, the float -> int conversions, the in-image tests and the window addressing stay scalar.
+// Voxel state as pairs: tt[p] = (tsdf 2p, tsdf 2p+1), ww[p] = (weight 2p, weight 2p+1).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 splat2(float a) { return (f32x2){a, a}; }
+__device__ __forceinline__ f32x2 fma2(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f32x2 rcp_m2(f32x2 b) {  // rcp_m elementwise: v_rcp x 2, Markstein correction packed
+    const f32x2 y0 = {__builtin_amdgcn_rcpf(b.x), __builtin_amdgcn_rcpf(b.y)};
+    return fma2(fma2(-b, y0, splat2(1.0f)), y0, y0);
+}
+
+// Pairs [P0, P1): projection + 8-byte window read of both voxels of each pair (lean_gather_w's operations).
+template <int NP, int P0, int P1>
+__device__ __forceinline__ void pk_gather(float (&dv)[2 * NP], bool& bad, const FrameParams& fp,
+                                          __amdgpu_buffer_rsrc_t rs, float xs0, const float (&ysp)[NP],
+                                          const f32x2 (&zz)[NP], uint32_t W4, uint32_t past_end, uint32_t hb,
+                                          uint32_t wb) {
+    float e[12];
+#pragma unroll
+    for (int j = 0; j < 12; ++j) e[j] = fp.ext[j];
+#pragma unroll
+    for (int p = P0; p < P1; ++p) {
+        const float ax = xs0 * e[0] + ysp[p] * e[1];  // shared by the pairs of one y (merged)
+        const float ay = xs0 * e[4] + ysp[p] * e[5];
+        const float az = xs0 * e[8] + ysp[p] * e[9];
+        const f32x2 xc = (splat2(ax) + zz[p] * splat2(e[2])) + splat2(e[3]);
+        const f32x2 yc = (splat2(ay) + zz[p] * splat2(e[6])) + splat2(e[7]);
+        const f32x2 zc = (splat2(az) + zz[p] * splat2(e[10])) + splat2(e[11]);
+        bad |= (__float_as_uint(zc.x) - 0x2D800000u) > 0x30000000u;  // not 2^-36 <= zc <= 2^60
+        bad |= (__float_as_uint(zc.y) - 0x2D800000u) > 0x30000000u;
+        const f32x2 inv_z = rcp_m2(zc);
+        const f32x2 u = (splat2(fp.fx) * xc) * inv_z + splat2(fp.cx);
+        const f32x2 v = (splat2(fp.fy) * yc) * inv_z + splat2(fp.cy);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const float uh = h ? u.y : u.x, vh = h ? v.y : v.x;
+            const bool in = (__float_as_uint(vh) <= hb) && (__float_as_uint(uh) <= wb);
+            const uint32_t off = in ? __umul24((uint32_t)(int)vh, W4) + ((uint32_t)(int)uh << 2) : past_end;
+            const u32x2 q = __builtin_amdgcn_raw_buffer_load_b64(rs, off & ~7u, 0, 0);
+            dv[2 * p + h] = __uint_as_float((off & 4u) ? q.y : q.x);
+        }
+        __builtin_amdgcn_sched_barrier(0);  // one pair's chain at a time (registers)
+    }
+}
+
+// Pairs [P0, P1): lean_update_v's running-average update, both voxels of a pair in packed form; a pair is
+// skipped when no lane updates either voxel (the scalar code's per-voxel branch, per pair).
+template <int NP, int P0, int P1>
+__device__ __forceinline__ void pk_update(f32x2 (&tt)[NP], f32x2 (&ww)[NP], const float (&dv)[2 * NP],
+                                          const FrameParams& fp, float xs0, const float (&ysp)[NP],
+                                          const f32x2 (&zz)[NP], float depth_max, float sdf_trunc, float y1t) {
+    const float e8 = fp.ext[8], e9 = fp.ext[9], e10 = fp.ext[10], e11 = fp.ext[11];
+#pragma unroll
+    for (int p = P0; p < P1; ++p) {
+        const float az = xs0 * e8 + ysp[p] * e9;
+        const f32x2 zc = (splat2(az) + zz[p] * splat2(e10)) + splat2(e11);
+        const f32x2 d = {dv[2 * p], dv[2 * p + 1]};
+        const f32x2 sdf = d - zc;
+        const bool up0 = !(d.x <= 0) && !(d.x > depth_max) && !(sdf.x < -sdf_trunc);
+        const bool up1 = !(d.y <= 0) && !(d.y > depth_max) && !(sdf.y < -sdf_trunc);
+        if (up0 || up1) {
+            f32x2 s;
+            asm("v_min_f32 %0, %1, %2" : "=v"(s.x) : "s"(sdf_trunc), "v"(sdf.x));
+            asm("v_min_f32 %0, %1, %2" : "=v"(s.y) : "s"(sdf_trunc), "v"(sdf.y));
+            const f32x2 T = splat2(sdf_trunc), Y = splat2(y1t);
+            const f32x2 q0 = s * Y;
+            const f32x2 q1 = fma2(fma2(-T, q0, s), Y, q0);
+            const f32x2 sn = fma2(fma2(-T, q1, s), Y, q1);
+            const f32x2 wgt = ww[p], wp = wgt + splat2(1.0f);
+            const f32x2 nt = (wgt * tt[p] + sn) * rcp_m2(wp);
+            tt[p].x = up0 ? nt.x : tt[p].x;
+            tt[p].y = up1 ? nt.y : tt[p].y;
+            ww[p].x = up0 ? wp.x : ww[p].x;
+            ww[p].y = up1 ? wp.y : ww[p].y;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+// The packed-FP32 kernel: k_integrate_win<512, WPE, PIPE in {0, 2}>'s structure over pk_gather / pk_update.
+template <int WPE, int PIPE>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void k_integrate_pk(
+    const int32_t* __restrict__ list, const bmask_t* __restrict__ lmask, int* __restrict__ counters, int64_t list_cap,
+    Table t, float2* __restrict__ pool, float voxel_size, const float* __restrict__ depths, int64_t HW, int H, int W,
+    const FrameParams* __restrict__ fps, const int64_t* __restrict__ depth_frame, float depth_max, float sdf_trunc,
+    int first_new) {
+    constexpr int NT = 512, R = 16, R2 = R * R, R3 = R2 * R;
+    constexpr int ZPER = R3 / NT, NP = ZPER / 2;
+    const int64_t n = min((int64_t)counters[kListCount], list_cap);
+    const float hm1 = (float)H - 1.0f, wm1 = (float)W - 1.0f;
+    const uint32_t W4 = 4u * (uint32_t)W, bytes = 4u * (uint32_t)HW;
+    const uint32_t hb = __float_as_uint(hm1), wb = __float_as_uint(wm1);
+    const float y0t = __builtin_amdgcn_rcpf(sdf_trunc);
+    const float y1t = __builtin_fmaf(__builtin_fmaf(-sdf_trunc, y0t, 1.0f), y0t, y0t);
+    const int tid = threadIdx.x;
+    const int l = tid & 63, w = tid >> 6;
+    const int vx = (l & 7) + 8 * (w & 1), vy = ((l >> 3) & 1) + 2 * (w >> 1), vz = l >> 4;
+    const uint32_t voff = 8u * (uint32_t)(vx + R * vy + R2 * vz);
+    for (int64_t i = blockIdx.x; i < n; i += gridDim.x) {
+        const int32_t slot = list[i];
+        const int buf = __builtin_amdgcn_readfirstlane(t.vals[slot]);
+        const bmask_t mask = readfirstlane_mask(lmask ? lmask[i] : bm_frames(t.mask[slot]));
+        int xb, yb, zb;
+        unpack_key(t.keys[slot], xb, yb, zb);
+        if (buf >= 0 && mask) {
+            const __amdgpu_buffer_rsrc_t vox = __builtin_amdgcn_make_buffer_rsrc(
+                pool + (int64_t)buf * R3, (short)0, (int)(R3 * sizeof(float2)), 0x00020000);
+            f32x2 tt[NP], ww[NP], zz[NP];
+            float ysp[NP];
+            bool bad = false;
+            const float xs0 = (float)(xb * R + vx) * voxel_size;
+#pragma unroll
+            for (int p = 0; p < NP; ++p) {
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int k = 2 * p + h;
+                    const int dy = win_dy<NT>(k), dz = win_dz<NT>(k);
+                    const float2 v = buf >= first_new ? make_float2(0.f, 0.f)
+                                                      : pool_load(vox, voff, (R * dy + R2 * dz) * (int)sizeof(float2));
+                    if (h) tt[p].y = v.x, ww[p].y = v.y, zz[p].y = (float)(zb * R + vz + dz) * voxel_size;
+                    else tt[p].x = v.x, ww[p].x = v.y, zz[p].x = (float)(zb * R + vz + dz) * voxel_size;
+                    bad |= !(v.y >= 0.0f && v.y <= 0x1p23f - 64.0f && v.y == __builtin_truncf(v.y));
+                }
+                ysp[p] = (float)(yb * R + vy + win_dy<NT>(2 * p)) * voxel_size;
+            }
+            auto frs = [&](int f) { return frame_rsrc(depths + depth_frame[f] * HW, bytes); };
+            bmask_t m = mask;
+            float da[ZPER];
+            if constexpr (PIPE == 2) {
+                constexpr int H2 = NP / 2;
+                int fp = bm_ctz(m);
+                m &= m - 1;
+                pk_gather<NP, 0, H2>(da, bad, fps[fp], frs(fp), xs0, ysp, zz, W4, bytes, hb, wb);
+                pk_gather<NP, H2, NP>(da, bad, fps[fp], frs(fp), xs0, ysp, zz, W4, bytes, hb, wb);
+                pk_update<NP, 0, H2>(tt, ww, da, fps[fp], xs0, ysp, zz, depth_max, sdf_trunc, y1t);
+                while (m) {
+                    const int f = bm_ctz(m);
+                    m &= m - 1;
+                    pk_gather<NP, 0, H2>(da, bad, fps[f], frs(f), xs0, ysp, zz, W4, bytes, hb, wb);
+                    pk_update<NP, H2, NP>(tt, ww, da, fps[fp], xs0, ysp, zz, depth_max, sdf_trunc, y1t);
+                    pk_gather<NP, H2, NP>(da, bad, fps[f], frs(f), xs0, ysp, zz, W4, bytes, hb, wb);
+                    pk_update<NP, 0, H2>(tt, ww, da, fps[f], xs0, ysp, zz, depth_max, sdf_trunc, y1t);
+                    fp = f;
+                }
+                pk_update<NP, H2, NP>(tt, ww, da, fps[fp], xs0, ysp, zz, depth_max, sdf_trunc, y1t);
+            } else {
+                while (m) {
+                    const int f = bm_ctz(m);
+                    m &= m - 1;
+                    pk_gather<NP, 0, NP>(da, bad, fps[f], frs(f), xs0, ysp, zz, W4, bytes, hb, wb);
+                    pk_update<NP, 0, NP>(tt, ww, da, fps[f], xs0, ysp, zz, depth_max, sdf_trunc, y1t);
+                }
+            }
+            if (__syncthreads_or(bad)) {
+                exact_block_call<R, NT>(pool + (int64_t)buf * R3, buf >= first_new, mask, xb, yb, zb, voxel_size, depths,
+                                        HW, W, hm1, wm1, fps, depth_frame, depth_max, sdf_trunc);
+            } else {
+#pragma unroll
+                for (int k = 0; k < ZPER; ++k) {
+                    const f32x2 a = tt[k >> 1], b = ww[k >> 1];
+                    pool_store(vox, voff, (R * win_dy<NT>(k) + R2 * win_dz<NT>(k)) * (int)sizeof(float2),
+                               (k & 1) ? make_float2(a.y, b.y) : make_float2(a.x, b.x));
+                }
+            }
+        }
+        __syncthreads();
+        if (tid == 0) t.mask[slot] = 0;
+    }
+}
+
 }  // namespace mqr
