@@ -469,7 +469,7 @@ def c5_leg(args, device, frames_per_side=2000, voxel=0.003, key_every=40, parity
     launches = max(st["integrate_launches"], 1)
     alg = (16 * R3 * st["union_blocks"] + 4 * H * W * st["frames"] + 16 * st["frame_blocks"]) / launches
     avg_ms = st["integrate_ms"] / launches
-    int_roof = {"bound": "hbm", "kernel": "k_integrate_lean", "unit": "GB/s", "peak": HBM_PEAK_GBS,
+    int_roof = {"bound": "hbm", "kernel": "k_integrate_win", "unit": "GB/s", "peak": HBM_PEAK_GBS,
                 "alg_bytes_per_launch": alg, "avg_launch_ms": avg_ms, "launches": st["integrate_launches"],
                 "achieved": alg / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else None,
                 "union_blocks_per_launch": st["union_blocks"] / launches,
@@ -1313,7 +1313,7 @@ def main():
             "roofline_binding": dict(pmc_binding(avg_ms, variant_ran) or {}, gather_ceiling=gather_ceiling(
                 avg_ms, st["frame_blocks"] * args.block_resolution ** 3 / 64 / launches,
                 torch.cuda.get_device_properties(local).multi_processor_count)),
-            "roofline": {"bound": "hbm", "kernel": "k_integrate_lean", "achieved": achieved, "peak": HBM_PEAK_GBS,
+            "roofline": {"bound": "hbm", "kernel": "k_integrate_win", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "peak_measured_copy": extras.get("hbm_copy_gbs"),
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_source": traffic_src,

@@ -12,6 +12,7 @@
 #   profc5      the same over the C5 leg alone                        -> gpurun_out/${TAG}_c5_kernel_stats.csv
 #   xtrace      kernel trace of 30 extractions: wall vs device span vs gaps -> gpurun_out/${TAG}_extract_timeline.json
 #   traffic     FETCH_SIZE / WRITE_SIZE passes (tools/pmc_traffic.sh) -> profiles/${TAG}_pmc_traffic.json
+#   pmcint      SQ / TA / TCP counters of the default integrate kernel (tools/pmc_ab.sh) -> profiles_new/
 #   abint:V     tools/ab_integrate.py over integrate variants V (comma separated, A/B library)
 #   abext:M     tools/ab_extract.py over extraction modes M (A/B library)
 #   conf        tools/conf_workload.py (the confidence kernel alone)
@@ -69,6 +70,10 @@ for step in ${STEPS:-tests}; do
       ROUND=$TAG timeout -k 10 600 bash tools/pmc_traffic.sh > gpurun_out/${TAG}_pmc_traffic.log 2>&1 || { tail -20 gpurun_out/${TAG}_pmc_traffic.log; exit 1; }
       mkdir -p gpurun_out/profiles_new && cp profiles/${TAG}_pmc_traffic.json profiles/${TAG}_pmc_fetch.csv profiles/${TAG}_pmc_write.csv gpurun_out/profiles_new/
       grep -E "traffic_bytes_per_launch|traffic_over_alg" profiles/${TAG}_pmc_traffic.json ;;
+    pmcint)
+      VARIANTS="0" timeout -k 10 700 bash tools/pmc_ab.sh > gpurun_out/${TAG}_pmc_ab.log 2>&1 || { tail -20 gpurun_out/${TAG}_pmc_ab.log; exit 1; }
+      mkdir -p gpurun_out/profiles_new && cp gpurun_out/pmc_ab.json gpurun_out/profiles_new/${TAG}_pmc_integrate_counters.json
+      head -c 600 gpurun_out/pmc_ab.json ;;
     abint:*)
       MQR_HIP_LIB="$PWD/tools/_ab/libmqr_ab.so" timeout -k 10 600 python -u tools/ab_integrate.py --check --rounds 7 --variants "${step#abint:}" \
         > gpurun_out/${TAG}_abint.json 2> gpurun_out/${TAG}_abint.err || { tail -20 gpurun_out/${TAG}_abint.err; exit 1; }
