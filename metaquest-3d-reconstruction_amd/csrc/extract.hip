@@ -1585,7 +1585,7 @@ int mqr_extract_mesh_owned(mqr_vbg* v, float thr, int64_t n_owned, mqr_geom** ou
     MQR_REQUIRE(n_owned < 0 || v->R == 16 || v->R == 8, "owned-block extraction supports block_resolution 8 / 16");
     const int64_t tri_blocks = n_owned < 0 ? INT64_MAX : n_owned;
     MQR_CHECK_HIP(hipSetDevice(v->device));
-    if (sync_all(v)) return 1;  // an integrate may still be running on the second stream
+    if (order_after_integrate(v)) return 1;  // an integrate may still be running on the second stream
     const int64_t n = v->pool_count;
     mqr_geom* g = new mqr_geom();
     g->device = v->device;
@@ -1612,7 +1612,7 @@ int mqr_extract_points(mqr_vbg* v, float thr, mqr_geom** out) {
     MQR_REQUIRE(v && out, "null argument");
     MQR_REQUIRE(v->R <= kMaxR, "extract_point_cloud supports block_resolution <= 16");
     MQR_CHECK_HIP(hipSetDevice(v->device));
-    if (sync_all(v)) return 1;
+    if (order_after_integrate(v)) return 1;
     const int64_t n = v->pool_count;
     mqr_geom* g = new mqr_geom();
     g->device = v->device;

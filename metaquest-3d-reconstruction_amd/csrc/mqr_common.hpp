@@ -242,6 +242,9 @@ void* geom_block_alloc(int device, size_t bytes, size_t* cap);
 void geom_block_release(int device, void* p, size_t cap);
 int grow_pool(mqr_vbg* v, int64_t need);
 int sync_all(mqr_vbg* v);
+// Work enqueued on the volume's `stream` from here on runs after any integrate still in flight on its second
+// stream (a device-side wait; no host synchronisation when nothing is in flight, the usual case).
+int order_after_integrate(mqr_vbg* v);
 // Caller-stream ordering (mqr_set_stream, include/mqr.h): the library streams `a` (and `b`) wait for
 // every command the calling thread's caller stream holds so far.  Called by each entry point that
 // reads or writes caller MQR_DEVICE buffers, before its first command on them (the current device

@@ -121,6 +121,12 @@ int sync_all(mqr_vbg* v) {
     return 0;
 }
 
+int order_after_integrate(mqr_vbg* v) {
+    for (int p = 0; p < 2; ++p)
+        if (v->int_pending[p]) MQR_CHECK_HIP(hipStreamWaitEvent(v->stream, v->int_done[p], 0));
+    return 0;
+}
+
 static int ensure_lists(mqr_vbg* v, int64_t cap) {
     if (v->list_cap >= cap) return 0;
     if (sync_all(v)) return 1;

@@ -52,6 +52,7 @@ for step in ${STEPS:-tests}; do
         python bench.py --no-cpu --no-extras --steps 50 --warmup 5 --touch-steps 0 > gpurun_out/${TAG}_prof_bench.json 2> gpurun_out/${TAG}_prof_bench.err \
         || { tail -20 gpurun_out/${TAG}_prof_bench.err; exit 1; }
       find gpurun_out/prof -name "*kernel_stats.csv" -exec cp {} gpurun_out/${TAG}_bench_kernel_stats.csv \;
+      rm -rf gpurun_out/prof  # (traces: gpurun copies back at most 64 MiB of gpurun_out/)
       grep "mqr" gpurun_out/${TAG}_bench_kernel_stats.csv | cut -c1-70 | head -12 ;;
     profc5)
       rm -rf gpurun_out/profc5
@@ -59,13 +60,15 @@ for step in ${STEPS:-tests}; do
         python bench.py --c5-only --no-parity > gpurun_out/${TAG}_prof_c5.json 2> gpurun_out/${TAG}_prof_c5.err \
         || { tail -20 gpurun_out/${TAG}_prof_c5.err; exit 1; }
       find gpurun_out/profc5 -name "*kernel_stats.csv" -exec cp {} gpurun_out/${TAG}_c5_kernel_stats.csv \;
+      rm -rf gpurun_out/profc5
       grep "mqr" gpurun_out/${TAG}_c5_kernel_stats.csv | cut -c1-70 | head -16 ;;
     xtrace)
       rm -rf gpurun_out/xt
       timeout -k 10 300 rocprofv3 --kernel-trace -f csv -d gpurun_out/xt -o run -- \
         python tools/extract_timeline.py --run --walls gpurun_out/xt_walls.json > gpurun_out/${TAG}_xt.log 2>&1 || { tail -20 gpurun_out/${TAG}_xt.log; exit 1; }
       python tools/extract_timeline.py --analyze "$(find gpurun_out/xt -name '*kernel_trace.csv' | head -1)" gpurun_out/xt_walls.json \
-        > gpurun_out/${TAG}_extract_timeline.json && cat gpurun_out/${TAG}_extract_timeline.json ;;
+        > gpurun_out/${TAG}_extract_timeline.json && cat gpurun_out/${TAG}_extract_timeline.json
+      rm -rf gpurun_out/xt ;;
     traffic)
       ROUND=$TAG timeout -k 10 600 bash tools/pmc_traffic.sh > gpurun_out/${TAG}_pmc_traffic.log 2>&1 || { tail -20 gpurun_out/${TAG}_pmc_traffic.log; exit 1; }
       mkdir -p gpurun_out/profiles_new && cp profiles/${TAG}_pmc_traffic.json profiles/${TAG}_pmc_fetch.csv profiles/${TAG}_pmc_write.csv gpurun_out/profiles_new/
@@ -73,6 +76,7 @@ for step in ${STEPS:-tests}; do
     pmcint)
       VARIANTS="0" timeout -k 10 700 bash tools/pmc_ab.sh > gpurun_out/${TAG}_pmc_ab.log 2>&1 || { tail -20 gpurun_out/${TAG}_pmc_ab.log; exit 1; }
       mkdir -p gpurun_out/profiles_new && cp gpurun_out/pmc_ab.json gpurun_out/profiles_new/${TAG}_pmc_integrate_counters.json
+      rm -rf /tmp/pmcab
       head -c 600 gpurun_out/pmc_ab.json ;;
     abint:*)
       MQR_HIP_LIB="$PWD/tools/_ab/libmqr_ab.so" timeout -k 10 600 python -u tools/ab_integrate.py --check --rounds 7 --variants "${step#abint:}" \
