@@ -1653,7 +1653,6 @@ namespace mqr {
 // thread, pinned) and serialised by a mutex: one large copy at a time per process.
 constexpr int kD2HThreads = 8;
 constexpr size_t kD2HChunk = size_t(8) << 20;
-constexpr size_t kD2HMin = size_t(32) << 20;  // smaller copies: one hipMemcpy
 constexpr int kD2HDevices = 64;
 struct D2HStage {
     hipStream_t s = nullptr;
@@ -1663,11 +1662,13 @@ struct D2HStage {
 static std::mutex g_d2h_mu;
 static D2HStage g_d2h[kD2HDevices][kD2HThreads];
 
-static int d2h_parallel(int device, void* dst, const void* src, size_t bytes) {
+int d2h_parallel(int device, void* dst, const void* src, size_t bytes) {
     MQR_REQUIRE(device >= 0 && device < kD2HDevices, "device index out of range");
     std::lock_guard<std::mutex> lk(g_d2h_mu);
     const size_t nchunks = (bytes + kD2HChunk - 1) / kD2HChunk;
-    const int T = (int)std::min<size_t>(kD2HThreads, nchunks);
+    // MQR_D2H_THREADS (1..8): fewer host threads, for tools/d2h_probe.py
+    static const int env_threads = getenv("MQR_D2H_THREADS") ? std::max(1, std::min(kD2HThreads, atoi(getenv("MQR_D2H_THREADS")))) : kD2HThreads;
+    const int T = (int)std::min<size_t>(env_threads, nchunks);
     std::atomic<int> failed{0};
     std::vector<std::string> errs(T);
     auto work = [&](int t) {
@@ -1720,7 +1721,7 @@ static int d2h_parallel(int device, void* dst, const void* src, size_t bytes) {
 }
 
 static int geom_copy_one(int device, void* dst, const void* src, size_t bytes, hipMemcpyKind k) {
-    if (k == hipMemcpyDeviceToHost && bytes >= kD2HMin) return d2h_parallel(device, dst, src, bytes);
+    if (k == hipMemcpyDeviceToHost && bytes >= kD2HParallelMin) return d2h_parallel(device, dst, src, bytes);
     MQR_CHECK_HIP(hipMemcpy(dst, src, bytes, k));
     return 0;
 }

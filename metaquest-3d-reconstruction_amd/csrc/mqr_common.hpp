@@ -252,5 +252,9 @@ int order_after_integrate(mqr_vbg* v);
 // no ordering in the other direction.
 int order_after_caller(int device, hipStream_t a, hipStream_t b = nullptr);
 hipStream_t caller_stream();  // the calling thread's caller stream (nullptr: the null stream)
+// Large device -> pageable host copies by several host threads through pinned staging (extract.hip);
+// mqr_geom_copy and mqr_memcpy use it from kD2HParallelMin bytes on.
+constexpr size_t kD2HParallelMin = size_t(32) << 20;
+int d2h_parallel(int device, void* dst, const void* src, size_t bytes);
 int activate_ordered(mqr_vbg* v, const uint64_t* dkeys, int64_t n);  // empty volume, buffer i = key i
 }  // namespace mqr

@@ -822,6 +822,7 @@ int mqr_memcpy(void* dst, int dst_loc, const void* src, int src_loc, int64_t byt
         MQR_CHECK_HIP(hipStreamSynchronize(t_caller_stream));
     hipMemcpyKind kind = dst_loc == MQR_DEVICE ? (src_loc == MQR_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice)
                                                : (src_loc == MQR_DEVICE ? hipMemcpyDeviceToHost : hipMemcpyHostToHost);
+    if (kind == hipMemcpyDeviceToHost && bytes >= (int64_t)kD2HParallelMin) return d2h_parallel(device, dst, src, (size_t)bytes);
     MQR_CHECK_HIP(hipMemcpy(dst, src, (size_t)bytes, kind));
     return 0;
 }

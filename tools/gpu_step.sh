@@ -15,6 +15,7 @@
 #   pmcint      SQ / TA / TCP counters of the default integrate kernel (tools/pmc_ab.sh) -> profiles_new/
 #   abint:V     tools/ab_integrate.py over integrate variants V (comma separated, A/B library)
 #   abext:M     tools/ab_extract.py over extraction modes M (A/B library)
+#   d2h         device -> host copy ceilings (tools/d2h_probe.py) with 1 / 4 / 8 staging threads
 #   conf        tools/conf_workload.py (the confidence kernel alone)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -86,6 +87,11 @@ for step in ${STEPS:-tests}; do
       MQR_HIP_LIB="$PWD/tools/_ab/libmqr_ab.so" timeout -k 10 600 python -u tools/ab_extract.py --modes "${step#abext:}" --reps 21 \
         > gpurun_out/${TAG}_abext.json 2> gpurun_out/${TAG}_abext.err || { tail -20 gpurun_out/${TAG}_abext.err; exit 1; }
       cat gpurun_out/${TAG}_abext.json ;;
+    d2h)
+      for t in 1 4 8; do
+        MQR_D2H_THREADS=$t timeout -k 10 120 python -u tools/d2h_probe.py >> gpurun_out/${TAG}_d2h.jsonl 2> gpurun_out/${TAG}_d2h.err || { tail -20 gpurun_out/${TAG}_d2h.err; exit 1; }
+      done
+      cat gpurun_out/${TAG}_d2h.jsonl ;;
     conf)
       timeout -k 10 300 python -u tools/conf_workload.py > gpurun_out/${TAG}_conf.json 2> gpurun_out/${TAG}_conf.err || { tail -20 gpurun_out/${TAG}_conf.err; exit 1; }
       cat gpurun_out/${TAG}_conf.json ;;
