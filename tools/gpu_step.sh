@@ -16,6 +16,7 @@
 #   abint:V     tools/ab_integrate.py over integrate variants V (comma separated, A/B library)
 #   abext:M     tools/ab_extract.py over extraction modes M (A/B library)
 #   d2h         device -> host copy ceilings (tools/d2h_probe.py) with 1 / 4 / 8 staging threads
+#   chunkab     drop-in integrate() with 64- vs 127-frame hand-offs (tools/dropin_ab.py)
 #   conf        tools/conf_workload.py (the confidence kernel alone)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -92,6 +93,9 @@ for step in ${STEPS:-tests}; do
         MQR_D2H_THREADS=$t timeout -k 10 120 python -u tools/d2h_probe.py >> gpurun_out/${TAG}_d2h.jsonl 2> gpurun_out/${TAG}_d2h.err || { tail -20 gpurun_out/${TAG}_d2h.err; exit 1; }
       done
       cat gpurun_out/${TAG}_d2h.jsonl ;;
+    chunkab)
+      timeout -k 10 600 python -u tools/dropin_ab.py > gpurun_out/${TAG}_chunk_ab.json 2> gpurun_out/${TAG}_chunk_ab.err || { tail -20 gpurun_out/${TAG}_chunk_ab.err; exit 1; }
+      cat gpurun_out/${TAG}_chunk_ab.json ;;
     conf)
       timeout -k 10 300 python -u tools/conf_workload.py > gpurun_out/${TAG}_conf.json 2> gpurun_out/${TAG}_conf.err || { tail -20 gpurun_out/${TAG}_conf.err; exit 1; }
       cat gpurun_out/${TAG}_conf.json ;;
