@@ -202,15 +202,22 @@ __device__ inline float from_ordered(uint32_t u) {
     return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
 }
 
-__global__ void k_cm_bounds(const float* __restrict__ V, const int32_t* __restrict__ ids, int64_t n,
-                            uint32_t* __restrict__ bb /* min x y z (ordered), max x y z */) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// Bounds of the sampled vertices: grid-stride with a capped grid, wave then workgroup reduction, one
+// atomic per bound word and workgroup (256 threads).
+__global__ __launch_bounds__(256) void k_cm_bounds(const float* __restrict__ V, const int32_t* __restrict__ ids,
+                                                   int64_t n, uint32_t* __restrict__ bb /* min x y z (ordered), max */) {
+    __shared__ uint32_t part[4][6];
     uint32_t lo[3] = {~0u, ~0u, ~0u}, hi[3] = {0u, 0u, 0u};
-    if (i < n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const int32_t v = ids[i];
 #pragma unroll
-        for (int a = 0; a < 3; ++a) lo[a] = hi[a] = ordered_u32(V[3 * (int64_t)v + a]);
+        for (int a = 0; a < 3; ++a) {
+            const uint32_t o = ordered_u32(V[3 * (int64_t)v + a]);
+            lo[a] = min(lo[a], o);
+            hi[a] = max(hi[a], o);
+        }
     }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
         uint32_t l = lo[a], h = hi[a];
@@ -218,10 +225,18 @@ __global__ void k_cm_bounds(const float* __restrict__ V, const int32_t* __restri
             l = min(l, (uint32_t)__shfl_xor((int)l, o, 64));
             h = max(h, (uint32_t)__shfl_xor((int)h, o, 64));
         }
-        if ((threadIdx.x & 63) == 0) {
-            atomicMin(&bb[a], l);
-            atomicMax(&bb[3 + a], h);
+        if (lane == 0) {
+            part[wave][a] = l;
+            part[wave][3 + a] = h;
         }
+    }
+    __syncthreads();
+    if (threadIdx.x < 6) {
+        const int c = threadIdx.x;
+        uint32_t r = part[0][c];
+        for (int w = 1; w < 4; ++w) r = c < 3 ? min(r, part[w][c]) : max(r, part[w][c]);
+        if (c < 3) atomicMin(&bb[c], r);
+        else atomicMax(&bb[c], r);
     }
 }
 
@@ -287,25 +302,38 @@ __device__ inline double box_d2(const double q[3], float4 lo, float4 hi) {
     return s;
 }
 
-template <int KMAX>
+// The knn (3) nearest sampled vertices of every unseen vertex (exact: float64 squared distances of the
+// float32 positions, ties by vertex index, the oracle's k-d tree rule), then the mean of their colours.
+// K = knn at compile time: the running best list lives in registers (static indices, an unrolled
+// insertion), and the traversal stack in LDS (stack-major: lane t's entry sp at stk[sp][t], conflict-free);
+// the round-4 form kept a 64 x int64 stack and a KMAX = 8 list with dynamic indices in scratch (64 ms for
+// C5's 17.5 M unseen vertices, profiles/r05_c5_kernel_stats.csv).  A nearest-first DFS holds at most one
+// pending sibling per level plus the current pair: depth + 1 <= 29 entries for P <= 2^27 buckets.
+constexpr int kKnnStack = 32;
+template <int K>
 __global__ __launch_bounds__(256) void k_cm_knn_fill(const float* __restrict__ V, const int32_t* __restrict__ qids,
                                                      int64_t nq, const int32_t* __restrict__ sorted, int64_t n,
                                                      int64_t P, const float4* __restrict__ lo,
                                                      const float4* __restrict__ hi, const double* __restrict__ avg,
-                                                     int knn, float* __restrict__ out) {
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+                                                     float* __restrict__ out) {
+    __shared__ int32_t stk[kKnnStack][256];
+    const int lane = threadIdx.x;
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + lane;
     if (t >= nq) return;
     const int32_t qv = qids[t];
     const double q[3] = {V[3 * (int64_t)qv], V[3 * (int64_t)qv + 1], V[3 * (int64_t)qv + 2]};
-    double bd[KMAX];
-    int32_t bi[KMAX];
-    int nb = 0;
-    int64_t stack[64];
+    double bd[K];
+    int32_t bi[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        bd[k] = __builtin_inf();  // an empty slot sorts after every real candidate
+        bi[k] = 0x7fffffff;
+    }
     int sp = 0;
-    stack[sp++] = 1;
+    stk[sp++][lane] = 1;
     while (sp) {
-        const int64_t node = stack[--sp];
-        if (nb == knn && box_d2(q, lo[node], hi[node]) > bd[nb - 1]) continue;
+        const int32_t node = stk[--sp][lane];
+        if (box_d2(q, lo[node], hi[node]) > bd[K - 1]) continue;  // (never while the list has room: inf)
         if (node >= P) {  // bucket
             const int64_t b = node - P;
             for (int64_t j = b * kBucket; j < min(n, (b + 1) * kBucket); ++j) {
@@ -313,32 +341,38 @@ __global__ __launch_bounds__(256) void k_cm_knn_fill(const float* __restrict__ V
                 const double dx = q[0] - (double)V[3 * (int64_t)v], dy = q[1] - (double)V[3 * (int64_t)v + 1];
                 const double dz = q[2] - (double)V[3 * (int64_t)v + 2];
                 const double d2 = dx * dx + dy * dy + dz * dz;
-                if (nb == knn && !(d2 < bd[nb - 1] || (d2 == bd[nb - 1] && v < bi[nb - 1]))) continue;
-                int k = nb < knn ? nb++ : nb - 1;
-                while (k > 0 && (d2 < bd[k - 1] || (d2 == bd[k - 1] && v < bi[k - 1]))) {
-                    bd[k] = bd[k - 1];
-                    bi[k] = bi[k - 1];
-                    --k;
+                auto before = [&](int k) { return d2 < bd[k] || (d2 == bd[k] && v < bi[k]); };  // new precedes k
+                if (!before(K - 1)) continue;
+                // insert at its rank among the K kept, sorted by (d2, index); the last one drops out.  From
+                // the end, with static indices: slot k takes slot k - 1's entry if the new one precedes it,
+                // else the new entry if it precedes slot k's, else keeps its own
+#pragma unroll
+                for (int k = K - 1; k >= 0; --k) {
+                    if (k > 0 && before(k - 1)) {
+                        bd[k] = bd[k - 1];
+                        bi[k] = bi[k - 1];
+                    } else if (before(k)) {
+                        bd[k] = d2;
+                        bi[k] = v;
+                    }
                 }
-                bd[k] = d2;
-                bi[k] = v;
             }
         } else {  // nearer child popped first
-            const int64_t a = 2 * node, c = a + 1;
+            const int32_t a = 2 * node, c = a + 1;
             const double da = box_d2(q, lo[a], hi[a]), dc = box_d2(q, lo[c], hi[c]);
-            if (da <= dc) {
-                stack[sp++] = c;
-                stack[sp++] = a;
-            } else {
-                stack[sp++] = a;
-                stack[sp++] = c;
-            }
+            stk[sp++][lane] = da <= dc ? c : a;
+            stk[sp++][lane] = da <= dc ? a : c;
         }
     }
+    int nb = 0;
     double c[3] = {0.0, 0.0, 0.0};
-    for (int k = 0; k < nb; ++k)
 #pragma unroll
-        for (int a = 0; a < 3; ++a) c[a] += avg[3 * (int64_t)bi[k] + a];
+    for (int k = 0; k < K; ++k)
+        if (bd[k] != __builtin_inf()) {
+            ++nb;
+#pragma unroll
+            for (int a = 0; a < 3; ++a) c[a] += avg[3 * (int64_t)bi[k] + a];
+        }
     if (nb > 0)
 #pragma unroll
         for (int a = 0; a < 3; ++a) c[a] /= (double)nb;
@@ -549,7 +583,7 @@ int mqr_color_map(int device, const float* vertices, int64_t nv, int vloc, const
                 const uint32_t init[6] = {~0u, ~0u, ~0u, 0u, 0u, 0u};
                 const unsigned gs = (unsigned)((nseen + 255) / 256);
                 if (hipMemcpyAsync(bb, init, sizeof init, hipMemcpyHostToDevice, s) != hipSuccess) fail("mqr_color_map: copy");
-                hipLaunchKernelGGL(k_cm_bounds, dim3(gs), dim3(256), 0, s, dV, ids, nseen, bb);
+                hipLaunchKernelGGL(k_cm_bounds, dim3(std::min(gs, 4096u)), dim3(256), 0, s, dV, ids, nseen, bb);
                 hipLaunchKernelGGL(k_cm_morton, dim3(gs), dim3(256), 0, s, dV, ids, nseen, bb, keys);
                 if (hipcub::DeviceRadixSort::SortPairs(tmps, tbs, keys, keys + nseen, ids, sorted, (int)nseen, 0, 63, s) !=
                     hipSuccess)
@@ -559,8 +593,21 @@ int mqr_color_map(int device, const float* vertices, int64_t nv, int vloc, const
                 for (int64_t first = P / 2; first >= 1; first /= 2)
                     hipLaunchKernelGGL(k_cm_level, dim3((unsigned)((first + 255) / 256)), dim3(256), 0, s, first, first,
                                        blo, bhi);
-                hipLaunchKernelGGL(k_cm_knn_fill<8>, dim3((unsigned)((nunseen + 255) / 256)), dim3(256), 0, s, dV,
-                                   ids + nv, nunseen, sorted, nseen, P, blo, bhi, avg, knn, dO);
+                const dim3 gq((unsigned)((nunseen + 255) / 256));
+                auto fill = [&](auto kern) {
+                    hipLaunchKernelGGL(kern, gq, dim3(256), 0, s, dV, ids + nv, nunseen, sorted, nseen, P, blo, bhi,
+                                       avg, dO);
+                };
+                switch (knn) {  // knn in [1, 8] (checked on entry)
+                    case 1: fill(k_cm_knn_fill<1>); break;
+                    case 2: fill(k_cm_knn_fill<2>); break;
+                    case 3: fill(k_cm_knn_fill<3>); break;
+                    case 4: fill(k_cm_knn_fill<4>); break;
+                    case 5: fill(k_cm_knn_fill<5>); break;
+                    case 6: fill(k_cm_knn_fill<6>); break;
+                    case 7: fill(k_cm_knn_fill<7>); break;
+                    default: fill(k_cm_knn_fill<8>); break;
+                }
             }
         }
         if (!rc && hipGetLastError() != hipSuccess) fail("mqr_color_map: kernel launch failed");

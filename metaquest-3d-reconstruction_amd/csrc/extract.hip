@@ -1650,8 +1650,11 @@ namespace mqr {
 // kD2HThreads host threads each own a stream and two pinned staging chunks: chunk k + T's DMA runs
 // while the thread copies chunk k out of the other buffer (and first-touches its destination pages),
 // and the threads' chunks interleave through the range.  The staging is kept per device (2 x 8 MB per
-// thread, pinned) and serialised by a mutex: one large copy at a time per process.
-constexpr int kD2HThreads = 8;
+// thread, pinned) and serialised by a mutex: one large copy at a time per process.  1 GiB on an MI355X
+// box (tools/d2h_probe.py, profiles/r05_d2h_probe.jsonl): DMA into pinned memory 57 GB/s; this path into
+// a FRESH pageable array 10.2 / 16.6 / 13.5 GB/s with 1 / 4 / 8 threads (the kernel zeroing the pages on
+// first touch bounds it: one thread first-touches at ~20 GB/s), into touched pages 27.6 / 42.0 / 23.9.
+constexpr int kD2HThreads = 4;
 constexpr size_t kD2HChunk = size_t(8) << 20;
 constexpr int kD2HDevices = 64;
 struct D2HStage {
@@ -1660,14 +1663,15 @@ struct D2HStage {
     hipEvent_t ev[2] = {nullptr, nullptr};
 };
 static std::mutex g_d2h_mu;
-static D2HStage g_d2h[kD2HDevices][kD2HThreads];
+static D2HStage g_d2h[kD2HDevices][8];
 
 int d2h_parallel(int device, void* dst, const void* src, size_t bytes) {
     MQR_REQUIRE(device >= 0 && device < kD2HDevices, "device index out of range");
     std::lock_guard<std::mutex> lk(g_d2h_mu);
     const size_t nchunks = (bytes + kD2HChunk - 1) / kD2HChunk;
-    // MQR_D2H_THREADS (1..8): fewer host threads, for tools/d2h_probe.py
-    static const int env_threads = getenv("MQR_D2H_THREADS") ? std::max(1, std::min(kD2HThreads, atoi(getenv("MQR_D2H_THREADS")))) : kD2HThreads;
+    // MQR_D2H_THREADS (1..8): another thread count, for tools/d2h_probe.py
+    static const int env_threads =
+        getenv("MQR_D2H_THREADS") ? std::max(1, std::min(8, atoi(getenv("MQR_D2H_THREADS")))) : kD2HThreads;
     const int T = (int)std::min<size_t>(env_threads, nchunks);
     std::atomic<int> failed{0};
     std::vector<std::string> errs(T);

@@ -55,8 +55,7 @@ struct BuildTri {
 
 // Gather every geometry's triangles into one array (prim id / geom id kept) and accumulate the
 // centroid bounds (ordered-int atomics).
-// Centroid bounds: a wave-wide min / max first, then one atomic per wave and axis (2 M per-thread
-// atomics on the same 6 words serialised this kernel to ~2 ms).
+// Centroid bounds: a wave-wide min / max, then a workgroup-wide one (block_bounds_atomic).
 __device__ inline uint32_t wave_min_u32(uint32_t x) {
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) x = min(x, (uint32_t)__shfl_xor((int)x, o, 64));
@@ -68,12 +67,39 @@ __device__ inline uint32_t wave_max_u32(uint32_t x) {
     return x;
 }
 
-__global__ void k_gather_tris(const float* __restrict__ v, const int32_t* __restrict__ t, int64_t nt, int64_t nv,
-                              int64_t base, uint32_t geom, BuildTri* tris, uint32_t* prim, uint32_t* gid,
-                              uint32_t* cbounds /* 6: min xyz, max xyz (ordered) */, int* bad) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// Min / max of a workgroup's per-thread bounds (256 threads) into out[0..2] / out[3..5] by one atomic per
+// word and workgroup.
+__device__ inline void block_bounds_atomic(uint32_t (&lo)[3], uint32_t (&hi)[3], uint32_t* out) {
+    __shared__ uint32_t part[4][6];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const uint32_t wl = wave_min_u32(lo[a]), wh = wave_max_u32(hi[a]);
+        if (lane == 0) {
+            part[wave][a] = wl;
+            part[wave][3 + a] = wh;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < 6) {
+        const int c = threadIdx.x;
+        uint32_t r = part[0][c];
+        for (int w = 1; w < 4; ++w) r = c < 3 ? min(r, part[w][c]) : max(r, part[w][c]);
+        if (c < 3) atomicMin(&out[c], r);
+        else atomicMax(&out[c], r);
+    }
+}
+
+// Grid-stride over the triangles (a capped grid: one atomic per bound word and WORKGROUP -- per-wave
+// atomics on the same six words serialised this kernel to 44 ms for C5's 41 M triangles,
+// profiles/r05_c5_kernel_stats.csv).  256 threads per workgroup.
+constexpr unsigned kGatherGrid = 4096;
+__global__ __launch_bounds__(256) void k_gather_tris(const float* __restrict__ v, const int32_t* __restrict__ t,
+                                                     int64_t nt, int64_t nv, int64_t base, uint32_t geom, BuildTri* tris,
+                                                     uint32_t* prim, uint32_t* gid,
+                                                     uint32_t* cbounds /* 6: min xyz, max xyz (ordered) */, int* bad) {
     uint32_t lo[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, hi[3] = {0u, 0u, 0u};
-    if (i < nt) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nt; i += (int64_t)gridDim.x * blockDim.x) {
         BuildTri b;
         float c[3] = {0.f, 0.f, 0.f};
         for (int k = 0; k < 3; ++k) {
@@ -90,15 +116,13 @@ __global__ void k_gather_tris(const float* __restrict__ v, const int32_t* __rest
         tris[base + i] = b;
         prim[base + i] = (uint32_t)i;
         gid[base + i] = geom;
-        for (int a = 0; a < 3; ++a) lo[a] = hi[a] = f2ord(c[a] * (1.0f / 3.0f));
-    }
-    for (int a = 0; a < 3; ++a) {
-        const uint32_t wl = wave_min_u32(lo[a]), wh = wave_max_u32(hi[a]);
-        if ((threadIdx.x & 63) == 0) {
-            atomicMin(&cbounds[a], wl);
-            atomicMax(&cbounds[3 + a], wh);
+        for (int a = 0; a < 3; ++a) {
+            const uint32_t o = f2ord(c[a] * (1.0f / 3.0f));
+            lo[a] = min(lo[a], o);
+            hi[a] = max(hi[a], o);
         }
     }
+    block_bounds_atomic(lo, hi, cbounds);
 }
 
 __device__ inline uint64_t spread21(uint32_t x) {
@@ -441,7 +465,8 @@ static int build(mqr_scene* s) {
     for (size_t g = 0; g < s->geoms.size(); ++g) {
         const auto& G = s->geoms[g];
         if (G.nt == 0) continue;
-        hipLaunchKernelGGL(k_gather_tris, dim3((unsigned)((G.nt + 255) / 256)), dim3(256), 0, st, G.v, G.t, G.nt,
+        hipLaunchKernelGGL(k_gather_tris, dim3((unsigned)std::min<int64_t>((G.nt + 255) / 256, kGatherGrid)), dim3(256), 0,
+                           st, G.v, G.t, G.nt,
                            G.nv, base, (uint32_t)g, tris, prim, gid, cb, bad);
         RC_HIP(hipGetLastError());
         base += G.nt;

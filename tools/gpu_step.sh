@@ -7,6 +7,7 @@
 #   smoke       __graft_entry__.smoke()                               -> gpurun_out/${TAG}_smoke.log
 #   bench       the default bench line (N = 1)                        -> gpurun_out/${TAG}_bench.json
 #   benchq      a short bench (no C4 / C5 / drop-in legs)             -> gpurun_out/${TAG}_benchq.json
+#   c5          the C5 leg alone, parity included (bench.py --c5-only)   -> gpurun_out/${TAG}_c5.json
 #   n2          2-rank rehearsal on one GPU (gloo-staged merge)        -> gpurun_out/${TAG}_bench_n2.json
 #   prof        rocprofv3 --kernel-trace --stats of the C2 bench      -> gpurun_out/${TAG}_bench_kernel_stats.csv
 #   profc5      the same over the C5 leg alone                        -> gpurun_out/${TAG}_c5_kernel_stats.csv
@@ -43,6 +44,9 @@ for step in ${STEPS:-tests}; do
     benchq)
       timeout -k 10 600 python bench.py --no-c4 --no-c5 --e2e-frames 0 > gpurun_out/${TAG}_benchq.json 2> gpurun_out/${TAG}_benchq.err || { tail -30 gpurun_out/${TAG}_benchq.err; exit 1; }
       tail -c 400 gpurun_out/${TAG}_benchq.json ;;
+    c5)
+      timeout -k 10 900 python bench.py --c5-only > gpurun_out/${TAG}_c5.json 2> gpurun_out/${TAG}_c5.err || { tail -30 gpurun_out/${TAG}_c5.err; exit 1; }
+      tail -c 1500 gpurun_out/${TAG}_c5.json ;;
     n2)
       MQR_BENCH_WRAP_DEVICES=1 timeout -k 10 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
         --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 10 --warmup 2 --weak-steps 10 \
