@@ -322,6 +322,11 @@ static int launch_integrate_ab(mqr_vbg* v, int var, hipStream_t s, unsigned grid
         case 37: win(k_integrate_pk<7, 2>, 512); break;
         case 38: win(k_integrate_pk<6, 2>, 512); break;
         case 39: win(k_integrate_pk<6, 0>, 512); break;
+        // branch-free forms: 40 window offsets selected, 41 updates selected, 42 both, 43 both at >= 6 waves
+        case 40: win(k_integrate_win_ab<512, 7, 0, 0, 1>, 512); break;
+        case 41: win(k_integrate_win_ab<512, 7, 0, 0, 2>, 512); break;
+        case 42: win(k_integrate_win_ab<512, 7, 0, 0, 3>, 512); break;
+        case 43: win(k_integrate_win_ab<512, 6, 0, 0, 3>, 512); break;
         default: set_error("integrate variant " + std::to_string(var) + " unknown"); return 2;
     }
     return 0;
@@ -507,10 +512,10 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
     //     division, ILP 4, in two halves;  15 = the round-3 default (the exact path in a fix-up launch);
     //     23 = the round-4 default (k_integrate_lean_ab with the same arithmetic as 0);  24-31 the frame
     //     loop software-pipelined / 1024-thread workgroups (k_integrate_win_ab);  32-35 timing diagnostics
-    //     (wrong results);  36-39 packed FP32 (k_integrate_pk).  (24 of round 4, a ballot skip of
+    //     (wrong results);  36-39 packed FP32 (k_integrate_pk);  40-43 branch-free window offsets / updates.  (24 of round 4, a ballot skip of
     //     out-of-image wave slots, ran 0.70 vs 0.48 ms per launch: removed.)
     int var = v->kernel_variant;
-    if (var < 0 || var > 39) var = 0;
+    if (var < 0 || var > 43) var = 0;
     if (!MQR_AB && var != 1 && var != 2 && var != 4) var = 0;
     if (var != 1 && var != 2 && !lean_ok) var = 2;
     if (var == 5 && (v->R != 16 || W % 4 != 0 || W < 4 || (reinterpret_cast<uintptr_t>(depths) & 15))) var = 0;

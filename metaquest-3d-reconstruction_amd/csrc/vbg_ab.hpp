@@ -719,7 +719,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
 // one product for s / sdf_trunc (about a third of the frame loop's VALU work gone); 2 = every frame's depth
 // read from the batch's first frame (a 1.2 MB working set that stays in L2: the refetch of each XCD's
 // frames from the MALL taken away).
-template <int NT, int WPE, int PIPE, int DIAG = 0>
+// BF: bit 0 = branch-free window offsets, bit 1 = branch-free updates (lean_gather_w / lean_update_v DIAGV
+// bits 1 / 2).
+template <int NT, int WPE, int PIPE, int DIAG = 0, int BF = 0>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void k_integrate_win_ab(
     const int32_t* __restrict__ list, const bmask_t* __restrict__ lmask, int* __restrict__ counters, int64_t list_cap,
     Table t, float2* __restrict__ pool, float voxel_size, const float* __restrict__ depths, int64_t HW, int H, int W,
@@ -766,12 +768,12 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
             const int64_t f0 = depth_frame[bm_ctz(mask)];
             auto dframe = [&](int f) { return DIAG == 2 ? f0 : depth_frame[f]; };
             auto gather = [&](float (&dv)[ZPER], int f) {
-                lean_gather_w<ZPER, 2, 8, true, 0, ZPER, DIAG == 1>(dv, bad, fps[f],
+                lean_gather_w<ZPER, 2, 8, true, 0, ZPER, (DIAG == 1 ? 1 : 0) | (BF << 1)>(dv, bad, fps[f],
                                                                    frame_rsrc(depths + dframe(f) * HW, bytes), xs, ys,
                                                                    zs, W4, bytes, hb, wb);
             };
             auto update = [&](const float (&dv)[ZPER], int f) {
-                lean_update_v<ZPER, 2, 0, 0, ZPER, DIAG == 1>(tw, dv, fps[f], xs, ys, zs, depth_max, sdf_trunc, y1t);
+                lean_update_v<ZPER, 2, 0, 0, ZPER, (DIAG == 1 ? 1 : 0) | (BF << 1)>(tw, dv, fps[f], xs, ys, zs, depth_max, sdf_trunc, y1t);
             };
             bmask_t m = mask;
             float da[ZPER];
@@ -781,20 +783,20 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE, 8))) vo
                 // half's update runs while the other half's loads are in flight
                 constexpr int H2 = ZPER / 2;
                 auto g0 = [&](int f) {
-                    lean_gather_w<ZPER, 2, 8, true, 0, H2, DIAG == 1>(da, bad, fps[f],
+                    lean_gather_w<ZPER, 2, 8, true, 0, H2, (DIAG == 1 ? 1 : 0) | (BF << 1)>(da, bad, fps[f],
                                                                      frame_rsrc(depths + dframe(f) * HW, bytes), xs, ys,
                                                                      zs, W4, bytes, hb, wb);
                 };
                 auto g1 = [&](int f) {
-                    lean_gather_w<ZPER, 2, 8, true, H2, ZPER, DIAG == 1>(da, bad, fps[f],
+                    lean_gather_w<ZPER, 2, 8, true, H2, ZPER, (DIAG == 1 ? 1 : 0) | (BF << 1)>(da, bad, fps[f],
                                                                         frame_rsrc(depths + dframe(f) * HW, bytes), xs,
                                                                         ys, zs, W4, bytes, hb, wb);
                 };
                 auto u0 = [&](int f) {
-                    lean_update_v<ZPER, 2, 0, 0, H2, DIAG == 1>(tw, da, fps[f], xs, ys, zs, depth_max, sdf_trunc, y1t);
+                    lean_update_v<ZPER, 2, 0, 0, H2, (DIAG == 1 ? 1 : 0) | (BF << 1)>(tw, da, fps[f], xs, ys, zs, depth_max, sdf_trunc, y1t);
                 };
                 auto u1 = [&](int f) {
-                    lean_update_v<ZPER, 2, 0, H2, ZPER, DIAG == 1>(tw, da, fps[f], xs, ys, zs, depth_max, sdf_trunc, y1t);
+                    lean_update_v<ZPER, 2, 0, H2, ZPER, (DIAG == 1 ? 1 : 0) | (BF << 1)>(tw, da, fps[f], xs, ys, zs, depth_max, sdf_trunc, y1t);
                 };
                 int fp = bm_ctz(m);
                 m &= m - 1;

@@ -703,12 +703,15 @@ __device__ __forceinline__ void lean_gather_w(float (&dv)[ZPER], bool& bad, cons
         const float yc = (ay + zs[k] * e[6]) + e[7];
         const float zc = (az + zs[k] * e[10]) + e[11];
         if (ZCHK) bad |= (__float_as_uint(zc) - 0x2D800000u) > 0x30000000u;  // not 2^-36 <= zc <= 2^60
-        // DIAGV (timing diagnostics of the A/B library only, wrong results): the bare v_rcp
-        const float inv_z = DIAGV == 1 ? __builtin_amdgcn_rcpf(zc) : rcp_m(zc);
+        // DIAGV (A/B library only): bit 0 = timing diagnostics (wrong results): the bare v_rcp; bit 1 = the
+        // in-image offset computed for every lane and selected (the compiler otherwise branches around it)
+        const float inv_z = (DIAGV & 1) ? __builtin_amdgcn_rcpf(zc) : rcp_m(zc);
         const float u = fx * xc * inv_z + cx;
         const float v = fy * yc * inv_z + cy;
         const bool in = (__float_as_uint(v) <= hm1_bits) && (__float_as_uint(u) <= wm1_bits);
-        const uint32_t off = in ? __umul24((uint32_t)(int)v, W4) + ((uint32_t)(int)u << 2) : past_end;
+        uint32_t off_in = __umul24((uint32_t)(int)v, W4) + ((uint32_t)(int)u << 2);
+        if constexpr ((DIAGV & 2) != 0) asm volatile("" : "+v"(off_in));
+        const uint32_t off = in ? off_in : past_end;
         if constexpr (WIN == 16) {
             const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(rs, off & ~15u, 0, 0);
             const uint32_t lo = (off & 8u) ? q.z : q.x, hi = (off & 8u) ? q.w : q.y;
@@ -735,15 +738,20 @@ __device__ __forceinline__ void lean_update_v(float2 (&tw)[ZPER], const float (&
         const float zc = (az + zs[k] * e10) + e11;
         const float d = dv[k];
         const float sdf = d - zc;
-        if (!(d <= 0) && !(d > depth_max) && !(sdf < -sdf_trunc)) {
+        const bool up = !(d <= 0) && !(d > depth_max) && !(sdf < -sdf_trunc);
+        // DIAGV bit 2 (A/B library only): every lane evaluates the update and selects (no branch per voxel)
+        if ((DIAGV & 4) != 0 || up) {
             float s;
             asm("v_min_f32 %0, %1, %2" : "=v"(s) : "s"(sdf_trunc), "v"(sdf));
             const float q0 = s * y1t;
-            const float q1 = DIAGV == 1 ? q0 : __builtin_fmaf(__builtin_fmaf(-sdf_trunc, q0, s), y1t, q0);
-            const float sn = DIV1 || DIAGV == 1 ? q1 : __builtin_fmaf(__builtin_fmaf(-sdf_trunc, q1, s), y1t, q1);
-            const float wgt = tw[k].y, wp = wgt + 1;
-            tw[k].x = (wgt * tw[k].x + sn) * (DIAGV == 1 ? __builtin_amdgcn_rcpf(wp) : rcp_m(wp));
-            tw[k].y = wp;
+            const float q1 = (DIAGV & 1) ? q0 : __builtin_fmaf(__builtin_fmaf(-sdf_trunc, q0, s), y1t, q0);
+            const float sn = DIV1 || (DIAGV & 1) ? q1 : __builtin_fmaf(__builtin_fmaf(-sdf_trunc, q1, s), y1t, q1);
+            const float wgt = tw[k].y;
+            float wp = wgt + 1;
+            float nt = (wgt * tw[k].x + sn) * ((DIAGV & 1) ? __builtin_amdgcn_rcpf(wp) : rcp_m(wp));
+            if constexpr ((DIAGV & 4) != 0) asm volatile("" : "+v"(nt), "+v"(wp));
+            tw[k].x = up ? nt : tw[k].x;
+            tw[k].y = up ? wp : wgt;
         }
         if ((k + 1) % ILP == 0) __builtin_amdgcn_sched_barrier(0);
     }

@@ -26,7 +26,11 @@ from .meshfilter import filter_mesh_components  # noqa: F401  (re-exported: o3d_
 from .raycasting import raycast_in_color_view  # noqa: F401  (re-exported: o3d_utils.py:324-341)
 from .vbg import VoxelBlockGrid
 
-CHUNK = 127  # frames per host->device hand-off: one full device batch (kMaxBatch, csrc/mqr_common.hpp)
+# frames per host->device hand-off.  Not a full device batch (127, kMaxBatch): this loop is bound by the
+# host (file reads, npz loads, the staged arrays), and 127-frame hand-offs ran 17 % slower than 64-frame
+# ones on the bench's on-disk capture -- 0.629 vs 0.535 s for 500 frames, identical volumes
+# (tools/dropin_ab.py, profiles/r05_ab_dropin_chunk.json)
+CHUNK = 64
 
 
 def compute_o3d_intrinsic_matrices(dataset) -> np.ndarray:
