@@ -327,6 +327,7 @@ static int launch_integrate_ab(mqr_vbg* v, int var, hipStream_t s, unsigned grid
         case 41: win(k_integrate_win_ab<512, 7, 0, 0, 2>, 512); break;
         case 42: win(k_integrate_win_ab<512, 7, 0, 0, 3>, 512); break;
         case 43: win(k_integrate_win_ab<512, 6, 0, 0, 3>, 512); break;
+        case 44: win(k_integrate_win_r4<7>, 512); break;  // the round-4 default's source
         default: set_error("integrate variant " + std::to_string(var) + " unknown"); return 2;
     }
     return 0;
@@ -515,7 +516,7 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
     //     (wrong results);  36-39 packed FP32 (k_integrate_pk);  40-43 branch-free window offsets / updates.  (24 of round 4, a ballot skip of
     //     out-of-image wave slots, ran 0.70 vs 0.48 ms per launch: removed.)
     int var = v->kernel_variant;
-    if (var < 0 || var > 43) var = 0;
+    if (var < 0 || var > 44) var = 0;
     if (!MQR_AB && var != 1 && var != 2 && var != 4) var = 0;
     if (var != 1 && var != 2 && !lean_ok) var = 2;
     if (var == 5 && (v->R != 16 || W % 4 != 0 || W < 4 || (reinterpret_cast<uintptr_t>(depths) & 15))) var = 0;

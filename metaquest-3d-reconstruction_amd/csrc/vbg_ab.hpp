@@ -1041,4 +1041,137 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
     }
 }
 
+// ---- A/B: the round-4 default's exact source (lean_gather_w / lean_update_v as of round 4, before the
+// round-5 restructuring of the window offset and update), for the same-process comparison (variant 44)
+template <int ZPER, int ILP = 1, int WIN = 16, bool ZCHK = true, int K0 = 0, int K1 = ZPER>
+__device__ __forceinline__ void lean_gather_w_r4(float (&dv)[ZPER], bool& bad, const FrameParams& fp,
+                                              __amdgpu_buffer_rsrc_t rs, const float (&xs)[ZPER],
+                                              const float (&ys)[ZPER], const float (&zs)[ZPER], uint32_t W4,
+                                              uint32_t past_end, uint32_t hm1_bits, uint32_t wm1_bits) {
+    float e[12];
+#pragma unroll
+    for (int j = 0; j < 12; ++j) e[j] = fp.ext[j];
+    const float fx = fp.fx, fy = fp.fy, cx = fp.cx, cy = fp.cy;
+#pragma unroll
+    for (int k = K0; k < K1; ++k) {
+        const float ax = xs[k] * e[0] + ys[k] * e[1];
+        const float ay = xs[k] * e[4] + ys[k] * e[5];
+        const float az = xs[k] * e[8] + ys[k] * e[9];
+        const float xc = (ax + zs[k] * e[2]) + e[3];
+        const float yc = (ay + zs[k] * e[6]) + e[7];
+        const float zc = (az + zs[k] * e[10]) + e[11];
+        if (ZCHK) bad |= (__float_as_uint(zc) - 0x2D800000u) > 0x30000000u;  // not 2^-36 <= zc <= 2^60
+        const float inv_z = rcp_m(zc);
+        const float u = fx * xc * inv_z + cx;
+        const float v = fy * yc * inv_z + cy;
+        const bool in = (__float_as_uint(v) <= hm1_bits) && (__float_as_uint(u) <= wm1_bits);
+        const uint32_t off = in ? __umul24((uint32_t)(int)v, W4) + ((uint32_t)(int)u << 2) : past_end;
+        if constexpr (WIN == 16) {
+            const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(rs, off & ~15u, 0, 0);
+            const uint32_t lo = (off & 8u) ? q.z : q.x, hi = (off & 8u) ? q.w : q.y;
+            dv[k] = __uint_as_float((off & 4u) ? hi : lo);
+        } else {
+            const u32x2 q = __builtin_amdgcn_raw_buffer_load_b64(rs, off & ~7u, 0, 0);
+            dv[k] = __uint_as_float((off & 4u) ? q.y : q.x);
+        }
+        if ((k + 1) % ILP == 0) __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+// DIV1: s / sdf_trunc with one Markstein correction (the host enables it only for an sdf_trunc whose
+// every s in [0, sdf_trunc] it verified against IEEE division, strunc_one_correction_ok; the
+// sequence is odd in s, so negative s follow).
+template <int ZPER, int ILP = 1, int DIV1 = 0, int K0 = 0, int K1 = ZPER>
+__device__ __forceinline__ void lean_update_v_r4(float2 (&tw)[ZPER], const float (&dv)[ZPER], const FrameParams& fp,
+                                              const float (&xs)[ZPER], const float (&ys)[ZPER],
+                                              const float (&zs)[ZPER], float depth_max, float sdf_trunc, float y1t) {
+    const float e8 = fp.ext[8], e9 = fp.ext[9], e10 = fp.ext[10], e11 = fp.ext[11];
+#pragma unroll
+    for (int k = K0; k < K1; ++k) {
+        const float az = xs[k] * e8 + ys[k] * e9;
+        const float zc = (az + zs[k] * e10) + e11;
+        const float d = dv[k];
+        const float sdf = d - zc;
+        if (!(d <= 0) && !(d > depth_max) && !(sdf < -sdf_trunc)) {
+            float s;
+            asm("v_min_f32 %0, %1, %2" : "=v"(s) : "s"(sdf_trunc), "v"(sdf));
+            const float q0 = s * y1t;
+            const float q1 = __builtin_fmaf(__builtin_fmaf(-sdf_trunc, q0, s), y1t, q0);
+            const float sn = DIV1 ? q1 : __builtin_fmaf(__builtin_fmaf(-sdf_trunc, q1, s), y1t, q1);
+            const float wgt = tw[k].y, wp = wgt + 1;
+            tw[k].x = (wgt * tw[k].x + sn) * rcp_m(wp);
+            tw[k].y = wp;
+        }
+        if ((k + 1) % ILP == 0) __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+
+template <int WPE>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void k_integrate_win_r4(
+    const int32_t* __restrict__ list, const bmask_t* __restrict__ lmask, int* __restrict__ counters, int64_t list_cap,
+    Table t, float2* __restrict__ pool, float voxel_size, const float* __restrict__ depths, int64_t HW, int H, int W,
+    const FrameParams* __restrict__ fps, const int64_t* __restrict__ depth_frame, float depth_max, float sdf_trunc,
+    int first_new) {
+    constexpr int NT = 512, R = 16, R2 = R * R, R3 = R2 * R;
+    constexpr int ZPER = R3 / NT;
+    const int64_t n = min((int64_t)counters[kListCount], list_cap);
+    const float hm1 = (float)H - 1.0f, wm1 = (float)W - 1.0f;
+    const uint32_t W4 = 4u * (uint32_t)W, bytes = 4u * (uint32_t)HW;
+    const uint32_t hb = __float_as_uint(hm1), wb = __float_as_uint(wm1);
+    const float y0t = __builtin_amdgcn_rcpf(sdf_trunc);
+    const float y1t = __builtin_fmaf(__builtin_fmaf(-sdf_trunc, y0t, 1.0f), y0t, y0t);
+    const int tid = threadIdx.x;
+    const int l = tid & 63, w = tid >> 6;
+    const int vx = (l & 7) + 8 * (w & 1), vy = ((l >> 3) & 1) + 2 * (w >> 1), vz = l >> 4;
+    const uint32_t voff = 8u * (uint32_t)(vx + R * vy + R2 * vz);  // byte offset of voxel 0 in its block
+    for (int64_t i = blockIdx.x; i < n; i += gridDim.x) {
+        const int32_t slot = list[i];
+        const int buf = __builtin_amdgcn_readfirstlane(t.vals[slot]);
+        const bmask_t mask = readfirstlane_mask(lmask ? lmask[i] : bm_frames(t.mask[slot]));
+        int xb, yb, zb;
+        unpack_key(t.keys[slot], xb, yb, zb);
+        if (buf >= 0 && mask) {
+            const __amdgpu_buffer_rsrc_t vox = __builtin_amdgcn_make_buffer_rsrc(
+                pool + (int64_t)buf * R3, (short)0, (int)(R3 * sizeof(float2)), 0x00020000);
+            float2 tw[ZPER];
+            float xs[ZPER], ys[ZPER], zs[ZPER];
+            bool bad = false;
+            const float xs0 = (float)(xb * R + vx) * voxel_size;
+#pragma unroll
+            for (int k = 0; k < ZPER; ++k) {
+                const int dy = win_dy<NT>(k), dz = win_dz<NT>(k);
+                // a block allocated by this batch (buffer >= first_new) starts at (0, 0): the pool is not
+                // cleared on reset or growth
+                tw[k] = buf >= first_new ? make_float2(0.f, 0.f)
+                                         : pool_load(vox, voff, (R * dy + R2 * dz) * (int)sizeof(float2));
+                xs[k] = xs0;
+                ys[k] = (float)(yb * R + vy + dy) * voxel_size;
+                zs[k] = (float)(zb * R + vz + dz) * voxel_size;
+                const float wv = tw[k].y;  // rcp_m(w + 1) is exact for integer w <= 2^23 + 64: a batch adds <= 127
+                bad |= !(wv >= 0.0f && wv <= 0x1p23f - 64.0f && wv == __builtin_truncf(wv));
+            }
+            bmask_t m = mask;
+            while (m) {
+                const int f = bm_ctz(m);
+                m &= m - 1;
+                float dv[ZPER];
+                lean_gather_w_r4<ZPER, 2, 8>(dv, bad, fps[f], frame_rsrc(depths + depth_frame[f] * HW, bytes), xs, ys, zs,
+                                          W4, bytes, hb, wb);
+                lean_update_v_r4<ZPER, 2, 0>(tw, dv, fps[f], xs, ys, zs, depth_max, sdf_trunc, y1t);
+            }
+            if (__syncthreads_or(bad)) {  // block-uniform: the exact path redoes it from the pool
+                exact_block_call<R, NT>(pool + (int64_t)buf * R3, buf >= first_new, mask, xb, yb, zb, voxel_size, depths,
+                                        HW, W, hm1, wm1, fps, depth_frame, depth_max, sdf_trunc);
+            } else {
+#pragma unroll
+                for (int k = 0; k < ZPER; ++k)
+                    pool_store(vox, voff, (R * win_dy<NT>(k) + R2 * win_dz<NT>(k)) * (int)sizeof(float2), tw[k]);
+            }
+        }
+        __syncthreads();
+        if (tid == 0) t.mask[slot] = 0;
+    }
+}
+
 }  // namespace mqr
