@@ -507,6 +507,33 @@ def c5_leg(args, device, frames_per_side=2000, voxel=0.003, key_every=40, parity
     t0 = time.perf_counter()
     col, cnt = color_map(mesh.vertices, imgs, cad, K[key], T[key], device=dev)
     col_s = time.perf_counter() - t0
+    # the same cast and colouring with every input and output resident in HBM (the kernels' own time;
+    # the host-array calls above include the PCIe copies of ~0.8 GB)
+    from mqr import _lib as _l
+    nk = len(key)
+    d_t = torch.empty(nk * H * W, dtype=torch.float32, device=f"cuda:{dev}")
+    d_v = torch.from_numpy(np.ascontiguousarray(mesh.vertices, np.float32)).to(f"cuda:{dev}")
+    d_im = torch.from_numpy(np.ascontiguousarray(imgs, np.uint8)).to(f"cuda:{dev}")
+    d_col = torch.empty((len(mesh.vertices), 3), dtype=torch.float32, device=f"cuda:{dev}")
+    d_cnt = torch.empty(len(mesh.vertices), dtype=torch.int32, device=f"cuda:{dev}")
+    Kk = np.ascontiguousarray(K[key], np.float64)
+    Tk = np.ascontiguousarray(T[key], np.float64)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    _l.call("mqr_scene_cast_pinhole", scene._h, _l.ptr(Kk, _l._f64p), _l.ptr(Tk, _l._f64p), nk, H, W,
+            ctypes.c_void_p(d_t.data_ptr()), None, None, None, None, _l.MQR_DEVICE)
+    cast_dev_s = time.perf_counter() - t0
+    col_dev = []
+    for _ in range(2):
+        t0 = time.perf_counter()
+        _l.call("mqr_color_map", dev, ctypes.c_void_p(d_v.data_ptr()), len(mesh.vertices), _l.MQR_DEVICE,
+                ctypes.c_void_p(d_im.data_ptr()), ctypes.c_void_p(d_t.data_ptr()), _l.MQR_DEVICE, nk, H, W,
+                _l.ptr(Kk, _l._f64p), _l.ptr(Tk, _l._f64p), 2.5, 0.03, 10, 0.1, 3, 3.0, 3,
+                ctypes.c_void_p(d_col.data_ptr()), ctypes.c_void_p(d_cnt.data_ptr()), _l.MQR_DEVICE)
+        col_dev.append(time.perf_counter() - t0)
+    device_equal = bool(np.array_equal(d_t.cpu().numpy().reshape(cad.shape), cad) and
+                        np.array_equal(d_col.cpu().numpy(), col) and np.array_equal(d_cnt.cpu().numpy(), cnt))
+    del d_t, d_v, d_im, d_col, d_cnt
     seen = cnt > 0
     err = float(np.abs(col[seen] - synthetic.texture(mesh.vertices[seen])).mean()) if seen.any() else None
     err_fill = (float(np.abs(col[~seen] - synthetic.texture(mesh.vertices[~seen])).mean()) if (~seen).any()
@@ -517,7 +544,9 @@ def c5_leg(args, device, frames_per_side=2000, voxel=0.003, key_every=40, parity
            "extract_ms": sorted(ext)[1] * 1e3, "extract_host_copy_bytes": mesh_bytes,
            "vertices": int(len(mesh.vertices)), "triangles": int(len(mesh.triangles)),
            "keyframes": len(key), "bvh_build_ms": bvh_s * 1e3, "colour_depth_cast_ms": cast_s * 1e3,
-           "colour_ms": col_s * 1e3, "coloured_fraction": float(seen.mean()), "colour_mean_abs_err": err,
+           "colour_ms": col_s * 1e3, "colour_depth_cast_device_ms": cast_dev_s * 1e3,
+           "colour_device_ms": min(col_dev) * 1e3, "colour_device_path_equal": device_equal,
+           "coloured_fraction": float(seen.mean()), "colour_mean_abs_err": err,
            "colour_mean_abs_err_knn_filled": err_fill,
            "generation_s": gen_s,
            "note": "integrate: device-resident depth, best of 2 passes into the emptied volume whose pool the "
@@ -525,7 +554,8 @@ def c5_leg(args, device, frames_per_side=2000, voxel=0.003, key_every=40, parity
                    "extract_device_ms: result left in HBM; extract_ms: host copy included, median of 3; "
                    "colour: mqr_color_map (boundary "
                    "masks, float64 means, 3-NN fill of unseen vertices), host arrays in/out (PCIe included), error vs "
-                   "the analytic texture the colour frames were rendered with"}
+                   "the analytic texture the colour frames were rendered with; *_device_ms: the same cast / colouring "
+                   "with inputs and outputs in HBM (colour: best of 2), results equal to the host-array calls"}
     if parity:
         # the volume of the last timed pass, its mesh (the one coloured above) and point cloud, and the
         # per-vertex colours, against the oracle on the same 4000 frames (LEFT then RIGHT)

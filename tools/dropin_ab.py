@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--chunks", default="64,127")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--frames", type=int, default=500)
+    ap.add_argument("--profile", action="store_true", help="cProfile one integrate() per chunk size (main thread)")
     a = ap.parse_args()
     import numpy as np
     from mqr import o3d_utils, synthetic
@@ -44,6 +45,20 @@ def main():
                   voxel_size=0.005, block_resolution=16, block_count=40000, depth_max=4.0,
                   trunc_voxel_multiplier=10.0, device=0)
         chunks = [int(c) for c in a.chunks.split(",")]
+        if a.profile:
+            import cProfile
+            import io as _io
+            import pstats
+            o3d_utils.integrate(ds, io, Side.LEFT, **kw)  # warm-up
+            for c in chunks:
+                o3d_utils.CHUNK = c
+                pr = cProfile.Profile()
+                pr.enable()
+                o3d_utils.integrate(ds, io, Side.LEFT, **kw)
+                pr.disable()
+                buf = _io.StringIO()
+                pstats.Stats(pr, stream=buf).sort_stats("tottime").print_stats(14)
+                print(f"== CHUNK {c}\n" + buf.getvalue(), file=sys.stderr)
         times = {c: [] for c in chunks}
         vols = {}
         for r in range(a.rounds + 1):

@@ -100,6 +100,9 @@ for step in ${STEPS:-tests}; do
     chunkab)
       timeout -k 10 600 python -u tools/dropin_ab.py > gpurun_out/${TAG}_chunk_ab.json 2> gpurun_out/${TAG}_chunk_ab.err || { tail -20 gpurun_out/${TAG}_chunk_ab.err; exit 1; }
       cat gpurun_out/${TAG}_chunk_ab.json ;;
+    chunkprof)
+      timeout -k 10 600 python -u tools/dropin_ab.py --profile --rounds 1 > gpurun_out/${TAG}_chunk_prof.json 2> gpurun_out/${TAG}_chunk_prof.txt || { tail -20 gpurun_out/${TAG}_chunk_prof.txt; exit 1; }
+      grep -A22 "== CHUNK" gpurun_out/${TAG}_chunk_prof.txt | cut -c1-150 ;;
     conf)
       timeout -k 10 300 python -u tools/conf_workload.py > gpurun_out/${TAG}_conf.json 2> gpurun_out/${TAG}_conf.err || { tail -20 gpurun_out/${TAG}_conf.err; exit 1; }
       cat gpurun_out/${TAG}_conf.json ;;
