@@ -280,3 +280,33 @@ def test_staged_processes_match_local_twin_and_single_pass(seq, world):
     V, T = np.concatenate(V), np.concatenate(T)
     assert len(T) == len(full.triangles) > 1000
     assert np.array_equal(canon_triangles(V, T), canon_triangles(full.vertices, full.triangles))
+
+
+def test_xchg_create_checks_the_callers_key_row(seq):
+    """mqr_xchg_create refuses (status 4) a gathered-keys row that is not the rank's own keys in buffer
+    order padded with 0xFF..FF: the plan's send lists index the local pool through it."""
+    import ctypes
+    from mqr import _lib
+    from mqr.distributed import MERGE_MODES, _empty_like, _packed
+    vols = _shards(seq, 2)
+    mine = _packed(vols[0].export_keys())
+    other = _packed(vols[1].export_keys())
+    mx = max(len(mine), len(other)) + 3
+    out = _empty_like(vols[0])
+
+    def create(row0):
+        allk = np.full(2 * mx, -1, np.int64)
+        allk[:len(row0)] = row0
+        allk[mx:mx + len(other)] = other
+        h = ctypes.c_void_p()
+        rc = _lib.load().mqr_xchg_create(vols[0].handle, 2, 0, MERGE_MODES["root"], 0, _lib.ptr(allk), mx,
+                                          _lib.MQR_HOST, out.handle, ctypes.byref(h))
+        if h.value:
+            _lib.load().mqr_xchg_destroy(h)
+        return rc
+
+    assert create(mine) == 0
+    assert create(mine[::-1].copy()) == 4                           # another order
+    assert create(mine[:-1]) == 4                                   # a key missing (padding in its place)
+    assert create(np.concatenate([mine, other[:1]])) == 4          # a foreign key in the padding
+    assert "not this rank's" in _lib.load().mqr_last_error().decode()
