@@ -15,6 +15,7 @@ The swap in the reference is one import line:
 from __future__ import annotations
 
 import sys
+import threading
 from concurrent.futures import ThreadPoolExecutor
 from typing import Optional
 
@@ -31,6 +32,37 @@ from .vbg import VoxelBlockGrid
 # ones on the bench's on-disk capture -- 0.629 vs 0.535 s for 500 frames, identical volumes
 # (tools/dropin_ab.py, profiles/r05_ab_dropin_chunk.json)
 CHUNK = 64
+
+
+class _HostStage:
+    """Reusable host staging of one chunk of raw frames and their confidence maps (pageable, so no
+    pinning cost; reused, so its pages are faulted in once instead of per chunk)."""
+
+    def __init__(self, B, H, W, with_conf):
+        self.key = (B, H, W, with_conf)
+        self.raw = np.empty((B, H, W), np.float32)
+        self.conf = np.empty((B, H, W), np.float64) if with_conf else None
+        self.vc = np.empty((B, H, W), np.int32) if with_conf else None
+
+
+# per thread: the two alternating sets of the last shape used, kept across integrate() calls (the fragment
+# path calls integrate() once per 100 frames)
+_TLS = threading.local()
+
+
+def _host_stage(turn, B, H, W, with_conf) -> _HostStage:
+    stages = getattr(_TLS, "stages", None)
+    if stages is None:
+        stages = _TLS.stages = [None, None]
+    st = stages[turn]
+    if st is None or st.key != (B, H, W, with_conf):
+        st = stages[turn] = _HostStage(B, H, W, with_conf)
+    return st
+
+
+def release_host_staging():
+    """Free this thread's drop-in integrate() host staging (~16 B per pixel per staged frame, two chunks)."""
+    _TLS.stages = None
 
 
 def compute_o3d_intrinsic_matrices(dataset) -> np.ndarray:
@@ -115,7 +147,49 @@ def integrate(dataset, depth_data_io, side, use_confidence_filtered_depth: bool,
         hi = min(n, lo + CHUNK)
         return lo, hi, [it for it in io_pool().map(load_one, range(lo, hi)) if it is not None]
 
+    def load_chunk_staged(lo, st):
+        """load_chunk for a chunk of one frame size: the I/O threads read every frame straight into
+        the reusable staging set `st` (raw buffer, and the confidence maps when masking) -- no
+        per-chunk allocations, stacking or copies on the main thread.  A missing file leaves a zero
+        raw buffer, which the device decode flags invalid (frame_ok 0: skipped, as the reference
+        skips a missing frame)."""
+        hi = min(n, lo + CHUNK)
+
+        def one(j):
+            i = lo + j
+            raw = read_raw(dataset.timestamps[i], dataset.widths[i], dataset.heights[i])
+            if raw is None:
+                st.raw[j] = 0.0
+                return False
+            st.raw[j] = raw
+            if not use_confidence_filtered_depth:
+                return False
+            cm = depth_data_io.load_confidence_map(side=side, timestamp=dataset.timestamps[i])
+            if cm is None:
+                print(f"[Warning] Confidence map not found for timestamp {dataset.timestamps[i]}")
+                return False
+            st.conf[j] = cm.confidence_map
+            st.vc[j] = cm.valid_count
+            return True
+
+        has = np.array(list(io_pool().map(one, range(hi - lo))), bool)
+        return lo, hi, (st, has)
+
     stage = {}  # (H, W) -> DeviceBuffer of CHUNK decoded frames
+
+    def device_buffer(H, W):
+        from ._lib import DeviceBuffer
+        buf = stage.get((H, W))
+        if buf is None:
+            buf = stage[(H, W)] = DeviceBuffer(4 * CHUNK * H * W, vbg.device_id)
+        return buf
+
+    def integrate_decoded(idx, buf, ok, H, W):
+        if ok.any():
+            K = intrinsics[idx].astype(np.float64)
+            T = extrinsic_wc[idx].astype(np.float64)
+            vbg.integrate_frames((buf, len(idx), H, W), K, T, frame_ok=ok.astype(np.uint8), depth_scale=1.0,
+                                 depth_max=float(depth_max), trunc_voxel_multiplier=float(trunc_voxel_multiplier))
 
     def run(idx, frames, cms, H, W):
         K = intrinsics[idx].astype(np.float64)
@@ -124,12 +198,9 @@ def integrate(dataset, depth_data_io, side, use_confidence_filtered_depth: bool,
         if read_raw is None:
             vbg.integrate_frames(np.stack(frames), K, T, **kw)
             return
-        from ._lib import DeviceBuffer
         from .ingest import decode_depth_frames
         B = len(idx)
-        buf = stage.get((H, W))
-        if buf is None:
-            buf = stage[(H, W)] = DeviceBuffer(4 * CHUNK * H * W, vbg.device_id)
+        buf = device_buffer(H, W)
         has = np.array([cm is not None for cm in cms], bool)
         conf = vc = None
         if has.any():
@@ -144,28 +215,57 @@ def integrate(dataset, depth_data_io, side, use_confidence_filtered_depth: bool,
                                     confidence_threshold=confidence_threshold,
                                     valid_count_threshold=valid_count_threshold, device=vbg.device_id,
                                     out_ptr=buf.ptr)
-        if ok.any():
-            vbg.integrate_frames((buf, B, H, W), K, T, frame_ok=ok.astype(np.uint8), **kw)
+        integrate_decoded(idx, buf, ok, H, W)
+
+    def run_staged(lo, hi, st, has):
+        from .ingest import decode_depth_frames
+        B = hi - lo
+        H, W = st.raw.shape[1:]
+        idx = np.arange(lo, hi)
+        buf = device_buffer(H, W)
+        any_mask = bool(has.any())
+        _, ok = decode_depth_frames(st.raw[:B], [dataset.nears[i] for i in idx], [dataset.fars[i] for i in idx],
+                                    conf=st.conf[:B] if any_mask else None, valid_count=st.vc[:B] if any_mask else None,
+                                    has_mask=has if any_mask else None, confidence_threshold=confidence_threshold,
+                                    valid_count_threshold=valid_count_threshold, device=vbg.device_id,
+                                    out_ptr=buf.ptr)
+        integrate_decoded(idx, buf, ok, H, W)
+
+    def uniform(lo):  # every frame of the chunk at lo has one size (the usual capture)
+        hi = min(n, lo + CHUNK)
+        return len({(int(dataset.heights[i]), int(dataset.widths[i])) for i in range(lo, hi)}) == 1
+
+    def submit(pool, lo, turn):
+        if read_raw is not None and uniform(lo):
+            st = _host_stage(turn, CHUNK, int(dataset.heights[lo]), int(dataset.widths[lo]), use_confidence_filtered_depth)
+            return pool.submit(load_chunk_staged, lo, st)
+        return pool.submit(load_chunk, lo)
 
     bar = None
     if show_progress:
         from tqdm import tqdm
         bar = tqdm(total=n, desc=desc, file=sys.stderr, dynamic_ncols=True, mininterval=0.1)
     with ThreadPoolExecutor(max_workers=1) as pool:
-        fut = pool.submit(load_chunk, 0) if n else None
+        # two staging sets alternate: the I/O threads fill chunk i + 1's while chunk i's is decoded
+        turn = 0
+        fut = submit(pool, 0, turn) if n else None
         while fut is not None:
             lo, hi, items = fut.result()
-            fut = pool.submit(load_chunk, hi) if hi < n else None
-            # consecutive runs of one frame size, in dataset order (the running average is order-dependent)
-            j = 0
-            while j < len(items):
-                k = j + 1
-                while k < len(items) and items[k][1].shape == items[j][1].shape:
-                    k += 1
-                sel = items[j:k]
-                run(np.array([i for i, _, _ in sel]), [f for _, f, _ in sel], [c for _, _, c in sel],
-                    *sel[0][1].shape)
-                j = k
+            turn ^= 1
+            fut = submit(pool, hi, turn) if hi < n else None
+            if isinstance(items, tuple):
+                run_staged(lo, hi, *items)
+            else:
+                # consecutive runs of one frame size, in dataset order (the running average is order-dependent)
+                j = 0
+                while j < len(items):
+                    k = j + 1
+                    while k < len(items) and items[k][1].shape == items[j][1].shape:
+                        k += 1
+                    sel = items[j:k]
+                    run(np.array([i for i, _, _ in sel]), [f for _, f, _ in sel], [c for _, _, c in sel],
+                        *sel[0][1].shape)
+                    j = k
             if bar is not None:
                 bar.update(hi - lo)
     if bar is not None:
