@@ -704,14 +704,21 @@ __device__ __forceinline__ void lean_gather_w(float (&dv)[ZPER], bool& bad, cons
         const float zc = (az + zs[k] * e[10]) + e[11];
         if (ZCHK) bad |= (__float_as_uint(zc) - 0x2D800000u) > 0x30000000u;  // not 2^-36 <= zc <= 2^60
         // DIAGV (A/B library only): bit 0 = timing diagnostics (wrong results): the bare v_rcp; bit 1 = the
-        // in-image offset computed for every lane and selected (the compiler otherwise branches around it)
+        // in-image offset computed for every lane and selected.  The default form lets the compiler branch
+        // around the offset of out-of-image lanes: 0.595-0.603 vs 0.638-0.647 ms per launch for a form it
+        // compiled without those branches (profiles/r05_ab_integrate_branchfree.json, variant 44 vs 0).
         const float inv_z = (DIAGV & 1) ? __builtin_amdgcn_rcpf(zc) : rcp_m(zc);
         const float u = fx * xc * inv_z + cx;
         const float v = fy * yc * inv_z + cy;
         const bool in = (__float_as_uint(v) <= hm1_bits) && (__float_as_uint(u) <= wm1_bits);
-        uint32_t off_in = __umul24((uint32_t)(int)v, W4) + ((uint32_t)(int)u << 2);
-        if constexpr ((DIAGV & 2) != 0) asm volatile("" : "+v"(off_in));
-        const uint32_t off = in ? off_in : past_end;
+        uint32_t off;
+        if constexpr ((DIAGV & 2) != 0) {
+            uint32_t off_in = __umul24((uint32_t)(int)v, W4) + ((uint32_t)(int)u << 2);
+            asm volatile("" : "+v"(off_in));
+            off = in ? off_in : past_end;
+        } else {
+            off = in ? __umul24((uint32_t)(int)v, W4) + ((uint32_t)(int)u << 2) : past_end;
+        }
         if constexpr (WIN == 16) {
             const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(rs, off & ~15u, 0, 0);
             const uint32_t lo = (off & 8u) ? q.z : q.x, hi = (off & 8u) ? q.w : q.y;
@@ -738,9 +745,19 @@ __device__ __forceinline__ void lean_update_v(float2 (&tw)[ZPER], const float (&
         const float zc = (az + zs[k] * e10) + e11;
         const float d = dv[k];
         const float sdf = d - zc;
-        const bool up = !(d <= 0) && !(d > depth_max) && !(sdf < -sdf_trunc);
-        // DIAGV bit 2 (A/B library only): every lane evaluates the update and selects (no branch per voxel)
-        if ((DIAGV & 4) != 0 || up) {
+        if constexpr ((DIAGV & 4) == 0) {
+            if (!(d <= 0) && !(d > depth_max) && !(sdf < -sdf_trunc)) {
+                float s;
+                asm("v_min_f32 %0, %1, %2" : "=v"(s) : "s"(sdf_trunc), "v"(sdf));
+                const float q0 = s * y1t;
+                const float q1 = (DIAGV & 1) ? q0 : __builtin_fmaf(__builtin_fmaf(-sdf_trunc, q0, s), y1t, q0);
+                const float sn = DIV1 || (DIAGV & 1) ? q1 : __builtin_fmaf(__builtin_fmaf(-sdf_trunc, q1, s), y1t, q1);
+                const float wgt = tw[k].y, wp = wgt + 1;
+                tw[k].x = (wgt * tw[k].x + sn) * ((DIAGV & 1) ? __builtin_amdgcn_rcpf(wp) : rcp_m(wp));
+                tw[k].y = wp;
+            }
+        } else {  // DIAGV bit 2 (A/B library only): every lane evaluates the update and selects (no branch)
+            const bool up = !(d <= 0) && !(d > depth_max) && !(sdf < -sdf_trunc);
             float s;
             asm("v_min_f32 %0, %1, %2" : "=v"(s) : "s"(sdf_trunc), "v"(sdf));
             const float q0 = s * y1t;
@@ -749,7 +766,7 @@ __device__ __forceinline__ void lean_update_v(float2 (&tw)[ZPER], const float (&
             const float wgt = tw[k].y;
             float wp = wgt + 1;
             float nt = (wgt * tw[k].x + sn) * ((DIAGV & 1) ? __builtin_amdgcn_rcpf(wp) : rcp_m(wp));
-            if constexpr ((DIAGV & 4) != 0) asm volatile("" : "+v"(nt), "+v"(wp));
+            asm volatile("" : "+v"(nt), "+v"(wp));
             tw[k].x = up ? nt : tw[k].x;
             tw[k].y = up ? wp : wgt;
         }
