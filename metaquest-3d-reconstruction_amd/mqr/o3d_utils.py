@@ -27,11 +27,12 @@ from .meshfilter import filter_mesh_components  # noqa: F401  (re-exported: o3d_
 from .raycasting import raycast_in_color_view  # noqa: F401  (re-exported: o3d_utils.py:324-341)
 from .vbg import VoxelBlockGrid
 
-# frames per host->device hand-off.  Not a full device batch (127, kMaxBatch): this loop is bound by the
-# host (file reads, npz loads, the staged arrays), and 127-frame hand-offs ran 17 % slower than 64-frame
-# ones on the bench's on-disk capture -- 0.629 vs 0.535 s for 500 frames, identical volumes
-# (tools/dropin_ab.py, profiles/r05_ab_dropin_chunk.json)
-CHUNK = 64
+# frames per host->device hand-off: a full device batch (kMaxBatch).  With the chunk read straight into
+# reused host staging sets, 127-frame hand-offs take 0.362 s against 0.420 s for 64-frame ones on the
+# bench's 500-frame on-disk capture, identical volumes (tools/dropin_ab.py,
+# profiles/r05_ab_dropin_chunk_staged.json); before that staging, 127 was the slower size (0.629 vs
+# 0.535 s, profiles/r05_ab_dropin_chunk.json)
+CHUNK = 127
 
 
 class _HostStage:
@@ -237,7 +238,7 @@ def integrate(dataset, depth_data_io, side, use_confidence_filtered_depth: bool,
 
     def submit(pool, lo, turn):
         if read_raw is not None and uniform(lo):
-            st = _host_stage(turn, CHUNK, int(dataset.heights[lo]), int(dataset.widths[lo]), use_confidence_filtered_depth)
+            st = _host_stage(turn, min(CHUNK, n), int(dataset.heights[lo]), int(dataset.widths[lo]), use_confidence_filtered_depth)
             return pool.submit(load_chunk_staged, lo, st)
         return pool.submit(load_chunk, lo)
 

@@ -33,10 +33,15 @@ def _capture(tmp_path, n=14, seed=31):
     return io, ds, Side
 
 
+@pytest.mark.parametrize("chunk", [4, 127])
 @pytest.mark.parametrize("use_conf", [False, True])
-def test_integrate_dropin_matches_oracle(tmp_path, use_conf, capsys):
+def test_integrate_dropin_matches_oracle(tmp_path, use_conf, chunk, capsys, monkeypatch):
+    """chunk 4: several hand-offs, so both alternating host staging sets are reused (and the missing
+    file / invalid buffer / missing confidence map land in different chunks)."""
     from gpu_helpers import compare_volumes
+    from mqr import o3d_utils
     from mqr.o3d_utils import _masked_depth, compute_o3d_intrinsic_matrices, integrate
+    monkeypatch.setattr(o3d_utils, "CHUNK", chunk)
     io, ds, Side = _capture(tmp_path)
     kw = dict(use_confidence_filtered_depth=use_conf, confidence_threshold=0.2, valid_count_threshold=2)
     vbg = integrate(ds, io, Side.LEFT, voxel_size=0.01, block_resolution=16, block_count=500, depth_max=4.0,
@@ -72,16 +77,20 @@ def test_integrate_dropin_chains_volumes(tmp_path):
     assert compare_volumes(a.export(), b.export(), 0.0) == 0.0
 
 
-def test_integrate_dropin_ragged_frame_sizes(tmp_path):
+@pytest.mark.parametrize("chunk", [4, 127])
+def test_integrate_dropin_ragged_frame_sizes(tmp_path, chunk, monkeypatch):
     """Frames of different sizes in one capture (the descriptor CSV gives each frame's width and
     height, depth_data_io.py:187-188): runs of one size go to the device in dataset order, and the
-    volume equals frame-by-frame integration."""
+    volume equals frame-by-frame integration.  chunk 4 mixes one-size chunks (staged path) with a
+    chunk that spans both sizes (list path)."""
     import pandas as pd
     from gpu_helpers import compare_volumes
     from mqr import synthetic
     from mqr.dataio import DepthDataIO
     from mqr.models import Side
+    from mqr import o3d_utils
     from mqr.o3d_utils import _masked_depth, compute_o3d_intrinsic_matrices, integrate
+    monkeypatch.setattr(o3d_utils, "CHUNK", chunk)
     parts = [("a", 240, 320, 262.5, 1_000_000, 5), ("b", 120, 160, 131.25, 2_000_000, 4),
              ("c", 240, 320, 262.5, 3_000_000, 3)]
     frames = []
