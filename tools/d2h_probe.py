@@ -2,7 +2,8 @@
 """Device -> host copy ceilings on this box (the C5 mesh copy, bench c5.extract_ms): 1 GiB from HBM into
 (a) torch pinned memory, (b) a fresh pageable torch tensor (.cpu()), (c) mqr_memcpy into a fresh numpy
 array (first-touch page faults inside the copy) and (d) into the same array again (pages present), and
-(e) the cost of first-touching a fresh array alone (np.empty + fill, one thread).
+(e) the cost of first-touching a fresh array alone (np.empty + fill, one thread), and (f) mqr_memcpy into a
+fresh mqr._lib.host_empty array (2 MiB-aligned MADV_HUGEPAGE mapping, what the library's callers use).
 MQR_D2H_THREADS sets the host threads of libmqr's staged copy (default 8).  Prints one JSON line."""
 import ctypes
 import json
@@ -47,6 +48,12 @@ def main():
     out["mqr_touched_gbs"] = gbs(time.perf_counter() - t0)
     out["values_ok"] = ok and bool(np.all(a[:: 1 << 16] == 1.0))
     del a
+    h = _lib.host_empty(n, np.float32)
+    t0 = time.perf_counter()
+    _lib.call("mqr_memcpy", _lib.ptr(h), _lib.MQR_HOST, ctypes.c_void_p(dev.data_ptr()), _lib.MQR_DEVICE, nbytes, 0)
+    out["mqr_fresh_host_empty_gbs"] = gbs(time.perf_counter() - t0)
+    out["values_ok"] = out["values_ok"] and bool(np.all(h[:: 1 << 16] == 1.0) and h[-1] == 1.0)
+    del h
     t0 = time.perf_counter()
     b = np.empty(n, np.float32)
     b.fill(0.0)
