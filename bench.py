@@ -84,6 +84,17 @@ def parse():
     return ap.parse_args()
 
 
+def _vmstat():
+    """Host page-fault / huge-page / compaction counters (/proc/vmstat) around the host copies."""
+    keys = ("thp_fault_alloc", "thp_fault_fallback", "compact_stall", "compact_fail", "compact_success",
+            "pgfault", "pgmajfault")
+    try:
+        with open("/proc/vmstat") as f:
+            return {k: int(v) for k, v in (ln.split() for ln in f) if k in keys}
+    except OSError:
+        return {}
+
+
 def extract_ms(vbg, thr, reps):
     from mqr import _lib
     times, counts = [], (0, 0)
@@ -98,6 +109,39 @@ def extract_ms(vbg, thr, reps):
         _lib.call("mqr_geom_free", g)
     times.sort()
     return times[len(times) // 2], counts
+
+
+def extract_phases(vbg, thr, reps):
+    """VoxelBlockGrid._geom's steps timed one by one (ms): the extraction (result in HBM), the three host
+    destination allocations, mqr_geom_copy (device -> host, 3 arrays), mqr_geom_free, and the release of
+    the host arrays (not part of an extraction: the unmap of ~1 GB)."""
+    import numpy as np
+    from mqr import _lib
+    out = []
+    for _ in range(reps):
+        ph = {}
+        g = ctypes.c_void_p()
+        t0 = time.perf_counter()
+        _lib.call("mqr_extract_mesh", vbg.handle, float(thr), ctypes.byref(g))
+        t1 = time.perf_counter()
+        nv, nt = ctypes.c_int64(), ctypes.c_int64()
+        _lib.call("mqr_geom_counts", g, ctypes.byref(nv), ctypes.byref(nt))
+        pos = np.empty((nv.value, 3), np.float32)
+        nrm = np.empty((nv.value, 3), np.float32)
+        tri = np.empty((nt.value, 3), np.int32)
+        t2 = time.perf_counter()
+        _lib.call("mqr_geom_copy", g, _lib.ptr(pos), _lib.ptr(nrm), _lib.ptr(tri), _lib.MQR_HOST)
+        t3 = time.perf_counter()
+        _lib.call("mqr_geom_free", g)
+        t4 = time.perf_counter()
+        nbytes = pos.nbytes + nrm.nbytes + tri.nbytes
+        ph = {"extract": (t1 - t0) * 1e3, "alloc": (t2 - t1) * 1e3, "copy": (t3 - t2) * 1e3,
+              "free": (t4 - t3) * 1e3, "copy_gbs": nbytes / (t3 - t2) / 1e9}
+        t5 = time.perf_counter()
+        del pos, nrm, tri
+        ph["release"] = (time.perf_counter() - t5) * 1e3
+        out.append(ph)
+    return out
 
 
 def copy_peak_gbs(device, nbytes=2 << 30, reps=5):
@@ -490,10 +534,15 @@ def c5_leg(args, device, frames_per_side=2000, voxel=0.003, key_every=40, parity
     del depth, seq
     torch.cuda.empty_cache()
     ext = []
+    vm0 = _vmstat()
+    mesh = None
     for _ in range(3):
+        mesh = None  # release the previous result (a ~1 GB unmap) outside the timed call
         t0 = time.perf_counter()
         mesh = vbg.extract_triangle_mesh(weight_threshold=1.5)
         ext.append(time.perf_counter() - t0)
+    vm1 = _vmstat()
+    ext_phases = extract_phases(vbg, 1.5, 3)
     mesh_bytes = mesh.vertices.nbytes + mesh.vertex_normals.nbytes + mesh.triangles.nbytes
     key = list(range(0, B, key_every))
     Ko = K[0]
@@ -544,7 +593,9 @@ def c5_leg(args, device, frames_per_side=2000, voxel=0.003, key_every=40, parity
     out = {"frames": B, "voxel_size": voxel, "integrate_ms": t_int * 1e3, "frames_per_s": B / t_int,
            "integrate_ms_with_growth": t_grow * 1e3, "roofline": int_roof,
            "blocks": blocks, "pool_gb": pool_gb, "extract_device_ms": ext_dev_ms, "extract_roofline": ext_roof,
-           "extract_ms": sorted(ext)[1] * 1e3, "extract_host_copy_bytes": mesh_bytes,
+           "extract_ms": sorted(ext)[1] * 1e3, "extract_runs_ms": [x * 1e3 for x in ext],
+           "extract_vmstat_delta": {k: vm1[k] - vm0[k] for k in vm0 if k in vm1}, "extract_phases_ms": ext_phases,
+           "extract_host_copy_bytes": mesh_bytes,
            "vertices": int(len(mesh.vertices)), "triangles": int(len(mesh.triangles)),
            "keyframes": len(key), "bvh_build_ms": bvh_s * 1e3, "colour_depth_cast_ms": cast_s * 1e3,
            "colour_ms": col_s * 1e3, "colour_depth_cast_device_ms": cast_dev_s * 1e3,

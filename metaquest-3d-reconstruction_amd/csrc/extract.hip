@@ -1644,83 +1644,111 @@ int mqr_geom_counts(mqr_geom* g, int64_t* nv, int64_t* nt) {
 }  // extern "C"
 
 namespace mqr {
-// Device -> pageable host copies of large results (mqr_geom_copy).  hipMemcpy into pageable memory
-// stages through the runtime's pinned buffers on the calling thread: ~10 GB/s for the 1 GB C5 mesh,
-// the destination's first-touch page faults included (BENCH_r04 c5.extract_ms 102.9 ms).  Here
-// kD2HThreads host threads each own a stream and two pinned staging chunks: chunk k + T's DMA runs
-// while the thread copies chunk k out of the other buffer (and first-touches its destination pages),
-// and the threads' chunks interleave through the range.  The staging is kept per device (2 x 8 MB per
-// thread, pinned) and serialised by a mutex: one large copy at a time per process.  1 GiB on an MI355X
-// box (tools/d2h_probe.py, profiles/r05_d2h_probe.jsonl): DMA into pinned memory 57 GB/s; this path into
-// a FRESH pageable array 10.2 / 16.6 / 13.5 GB/s with 1 / 4 / 8 threads (the kernel zeroing the pages on
-// first touch bounds it: one thread first-touches at ~20 GB/s), into touched pages 27.6 / 42.0 / 23.9.
-constexpr int kD2HThreads = 4;
+// Device -> pageable host copies of large results (mqr_geom_copy, mqr_memcpy).  hipMemcpy into pageable
+// memory stages through the runtime's pinned buffers on the calling thread: ~10 GB/s for the 1 GB C5 mesh
+// (BENCH_r04 c5.extract_ms 102.9 ms).  Here a copy kernel moves the range chunk by chunk into a ring of
+// pinned slots (GPU stores over the fabric: 54.7 GB/s into pinned memory, SDMA 57.1, tools/d2h_modes.hip)
+// on a stream the process already runs, and kD2HThreads host threads copy each slot out as its event
+// completes (first-touching the destination pages in parallel).  Round 5's first version gave every host
+// thread its own stream and DMA: the same ~41 GB/s once set up, but its set-up cost the process's first
+// large copy 46.6 ms (first 48 MB copy, vs 1.6 ms for the second, tools/d2h_probe.py) -- four stream
+// creations 50 ms and the copy engine's first use 16-19 ms on an MI355X box (tools/d2h_setup_probe.hip,
+// profiles/r05_d2h_setup_probe.json).  The ring (one pinned allocation per device) is kept and the calls
+// are serialised by a mutex: one large copy at a time per process.
+constexpr int kD2HThreads = 8;  // 1 GiB into a fresh array: 44.4 GB/s with 4, 51.1 with 8 (profiles/r05_d2h_probe.jsonl)
+constexpr int kD2HSlots = 8;
 constexpr size_t kD2HChunk = size_t(8) << 20;
 constexpr int kD2HDevices = 64;
-struct D2HStage {
-    hipStream_t s = nullptr;
-    void* buf[2] = {nullptr, nullptr};
-    hipEvent_t ev[2] = {nullptr, nullptr};
+struct D2HRing {
+    char* buf = nullptr;
+    hipEvent_t ev[kD2HSlots] = {};
 };
 static std::mutex g_d2h_mu;
-static D2HStage g_d2h[kD2HDevices][8];
+static D2HRing g_d2h[kD2HDevices];
+
+__global__ __launch_bounds__(256) void k_copy_out16(uint4* __restrict__ dst, const uint4* __restrict__ src, size_t n16) {
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (size_t)gridDim.x * 256) dst[i] = src[i];
+}
+
+__global__ __launch_bounds__(256) void k_copy_out1(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, size_t n) {
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) dst[i] = src[i];
+}
 
 int d2h_parallel(int device, void* dst, const void* src, size_t bytes) {
     MQR_REQUIRE(device >= 0 && device < kD2HDevices, "device index out of range");
     std::lock_guard<std::mutex> lk(g_d2h_mu);
+    D2HRing& r = g_d2h[device];
+    if (!r.buf) {
+        MQR_CHECK_HIP(hipHostMalloc(reinterpret_cast<void**>(&r.buf), kD2HSlots * kD2HChunk, hipHostMallocDefault));
+        for (auto& e : r.ev) MQR_CHECK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    // the caller's stream when it is this device's (mqr_set_stream; its earlier work on `src` is then
+    // ordered), else the null stream
+    hipStream_t s = nullptr;
+    if (caller_stream()) {
+        hipDevice_t sd = -1;
+        if (hipStreamGetDevice(caller_stream(), &sd) == hipSuccess && sd == device) s = caller_stream();
+        (void)hipGetLastError();
+    }
     const size_t nchunks = (bytes + kD2HChunk - 1) / kD2HChunk;
     // MQR_D2H_THREADS (1..8): another thread count, for tools/d2h_probe.py
     static const int env_threads =
         getenv("MQR_D2H_THREADS") ? std::max(1, std::min(8, atoi(getenv("MQR_D2H_THREADS")))) : kD2HThreads;
     const int T = (int)std::min<size_t>(env_threads, nchunks);
+    const bool aligned = (reinterpret_cast<uintptr_t>(src) & 15) == 0;
+    auto len_of = [&](size_t k) { return std::min(kD2HChunk, bytes - k * kD2HChunk); };
+    std::atomic<int64_t> issued{0};  // chunks whose copy and event are queued
+    std::atomic<int64_t> slot_done[kD2HSlots];  // the last chunk copied out of each slot
+    for (auto& d : slot_done) d.store(-1);
     std::atomic<int> failed{0};
-    std::vector<std::string> errs(T);
-    auto work = [&](int t) {
-        D2HStage& st = g_d2h[device][t];
-        auto fail = [&](const char* what, hipError_t e) {
-            errs[t] = std::string("mqr_geom_copy: ") + what + ": " + hipGetErrorString(e);
-            failed.store(1);
-        };
-        hipError_t e = hipSetDevice(device);
-        if (e == hipSuccess && !st.s) e = hipStreamCreateWithFlags(&st.s, hipStreamNonBlocking);
-        for (int b = 0; b < 2 && e == hipSuccess; ++b) {
-            if (!st.buf[b]) e = hipHostMalloc(&st.buf[b], kD2HChunk, hipHostMallocDefault);
-            if (e == hipSuccess && !st.ev[b]) e = hipEventCreateWithFlags(&st.ev[b], hipEventDisableTiming);
-        }
-        if (e != hipSuccess) return fail("staging setup", e);
-        auto len_of = [&](size_t k) { return std::min(kD2HChunk, bytes - k * kD2HChunk); };
-        auto issue = [&](size_t k, int b) {
-            hipError_t r = hipMemcpyAsync(st.buf[b], static_cast<const char*>(src) + k * kD2HChunk, len_of(k),
-                                          hipMemcpyDeviceToHost, st.s);
-            if (r == hipSuccess) r = hipEventRecord(st.ev[b], st.s);
-            return r;
-        };
-        int b = 0;
-        if ((e = issue((size_t)t, 0)) != hipSuccess) return fail("hipMemcpyAsync", e);
+    std::vector<std::string> errs(T + 1);
+    auto out = [&](int t) {  // host thread t: chunks t, t + T, ... out of their slots
         for (size_t k = (size_t)t; k < nchunks; k += (size_t)T) {
-            if (k + T < nchunks && (e = issue(k + T, b ^ 1)) != hipSuccess) {
-                (void)hipStreamSynchronize(st.s);
-                return fail("hipMemcpyAsync", e);
+            while (issued.load(std::memory_order_acquire) <= (int64_t)k && !failed.load()) std::this_thread::yield();
+            if (failed.load()) return;
+            const int slot = (int)(k % kD2HSlots);
+            hipError_t e = hipEventSynchronize(r.ev[slot]);
+            if (e != hipSuccess) {
+                errs[t] = std::string("d2h copy: hipEventSynchronize: ") + hipGetErrorString(e);
+                failed.store(1);
+                return;
             }
-            if ((e = hipEventSynchronize(st.ev[b])) != hipSuccess) {
-                (void)hipStreamSynchronize(st.s);
-                return fail("hipEventSynchronize", e);
-            }
-            std::memcpy(static_cast<char*>(dst) + k * kD2HChunk, st.buf[b], len_of(k));
-            if (failed.load()) break;
-            b ^= 1;
+            std::memcpy(static_cast<char*>(dst) + k * kD2HChunk, r.buf + slot * kD2HChunk, len_of(k));
+            slot_done[slot].store((int64_t)k, std::memory_order_release);
         }
-        (void)hipStreamSynchronize(st.s);  // a chunk issued ahead of a failure on another thread
     };
     std::vector<std::thread> th;
-    for (int t = 1; t < T; ++t) th.emplace_back(work, t);
-    work(0);
-    for (auto& x : th) x.join();
-    for (int t = 0; t < T; ++t)
-        if (!errs[t].empty()) {
-            set_error(errs[t]);
-            return 1;
+    for (int t = 0; t < T; ++t) th.emplace_back(out, t);
+    for (size_t k = 0; k < nchunks && !failed.load(); ++k) {  // this thread queues the chunk copies
+        const int slot = (int)(k % kD2HSlots);
+        if (k >= (size_t)kD2HSlots)
+            while (slot_done[slot].load(std::memory_order_acquire) != (int64_t)(k - kD2HSlots) && !failed.load())
+                std::this_thread::yield();
+        if (failed.load()) break;
+        const char* from = static_cast<const char*>(src) + k * kD2HChunk;
+        char* to = r.buf + slot * kD2HChunk;
+        const size_t len = len_of(k), n16 = aligned ? len / 16 : 0, tail = len - 16 * n16;
+        if (n16) k_copy_out16<<<1024, 256, 0, s>>>(reinterpret_cast<uint4*>(to), reinterpret_cast<const uint4*>(from), n16);
+        if (tail) k_copy_out1<<<(unsigned)std::min<size_t>(1024, (tail + 255) / 256), 256, 0, s>>>(
+                      reinterpret_cast<uint8_t*>(to) + 16 * n16, reinterpret_cast<const uint8_t*>(from) + 16 * n16, tail);
+        hipError_t e = hipGetLastError();
+        if (e == hipSuccess) e = hipEventRecord(r.ev[slot], s);
+        if (e != hipSuccess) {
+            errs[T] = std::string("d2h copy: chunk copy launch: ") + hipGetErrorString(e);
+            failed.store(1);
+            break;
         }
+        issued.store((int64_t)k + 1, std::memory_order_release);
+    }
+    for (auto& x : th) x.join();
+    if (failed.load()) {
+        (void)hipStreamSynchronize(s);  // no slot write left in flight for the next call
+        for (auto& m : errs)
+            if (!m.empty()) {
+                set_error(m);
+                return 1;
+            }
+    }
     return 0;
 }
 

@@ -6,7 +6,6 @@ raises.  (The CPU restatement under oracle/ is test infrastructure only.)
 from __future__ import annotations
 
 import ctypes
-import mmap
 import os
 import sys
 import threading
@@ -264,32 +263,6 @@ def ptr(a: np.ndarray, t=None):
     return a.ctypes.data_as(t)
 
 
-# Large device -> host destinations (meshes, point clouds, exports) come from an anonymous mapping aligned
-# to 2 MiB and advised MADV_HUGEPAGE: the copy's first touch then faults 2 MiB pages instead of 4 KiB ones.
-# 1 GiB through the staged copy on an MI355X box (tools/d2h_modes.hip, tools/d2h_probe.py,
-# profiles/r05_d2h_modes.jsonl): 43.5 GB/s into such a mapping, 15.2 GB/s into a fresh np.empty array
-# (glibc's mapping is not 2 MiB aligned and numpy's advice did not give the copy huge pages), 50.7 GB/s
-# into pages already present.  Same threshold as the library's parallel staged copy (kD2HParallelMin).
-HOST_HUGE_MIN = 32 << 20
-_HUGE = 2 << 20
-
-
-def host_empty(shape, dtype) -> np.ndarray:
-    """np.empty for a device -> host copy destination (huge-page backed when >= HOST_HUGE_MIN bytes)."""
-    dt = np.dtype(dtype)
-    shape = tuple(int(x) for x in (shape if isinstance(shape, (tuple, list)) else (shape,)))
-    n = int(np.prod(shape, dtype=np.int64)) * dt.itemsize
-    if n < HOST_HUGE_MIN or not hasattr(mmap, "MADV_HUGEPAGE"):
-        return np.empty(shape, dt)
-    mm = mmap.mmap(-1, n + _HUGE)
-    view = ctypes.c_char.from_buffer(mm)
-    base = ctypes.addressof(view)
-    del view  # (releases the export: the array below keeps the mapping alive)
-    off = (-base) % _HUGE
-    mm.madvise(mmap.MADV_HUGEPAGE, off, n)
-    return np.frombuffer(mm, dt, count=n // dt.itemsize, offset=off).reshape(shape)
-
-
 class DeviceBuffer:
     """Raw HBM allocation owned by Python (keeps inputs resident without any framework)."""
 
@@ -308,7 +281,7 @@ class DeviceBuffer:
         return buf
 
     def to_array(self, shape, dtype):
-        out = host_empty(shape, dtype)
+        out = np.empty(shape, dtype)
         call("mqr_memcpy", ptr(out), MQR_HOST, self.ptr, MQR_DEVICE, out.nbytes, self.device)
         return out
 

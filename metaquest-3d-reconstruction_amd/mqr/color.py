@@ -53,8 +53,8 @@ def color_vertices(vertices, images, depths, K, T_wc, max_depth=MAX_DEPTH,
     d = np.ascontiguousarray(depths, dtype=np.float32).reshape(N, H, W)
     Kd = np.ascontiguousarray(K, dtype=np.float64).reshape(N, 9)
     Td = np.ascontiguousarray(T_wc, dtype=np.float64).reshape(N, 16)
-    out = _lib.host_empty((len(V), 3), np.float32)
-    cnt = _lib.host_empty(len(V), np.int32)
+    out = np.empty((len(V), 3), np.float32)
+    cnt = np.empty(len(V), np.int32)
     call("mqr_color_vertices", int(device), ptr(V), len(V), MQR_HOST, ptr(im), ptr(d), MQR_HOST, N, H, W,
          ptr(Kd, _lib._f64p), ptr(Td, _lib._f64p), float(max_depth), float(visibility_threshold), int(margin),
          ptr(out), ptr(cnt), MQR_HOST)
@@ -75,8 +75,8 @@ def color_map(vertices, images, t_hit, K, T_wc, max_depth=MAX_DEPTH, visibility_
     d = np.ascontiguousarray(t_hit, dtype=np.float32).reshape(N, H, W)
     Kd = np.ascontiguousarray(K, dtype=np.float64).reshape(N, 9)
     Td = np.ascontiguousarray(T_wc, dtype=np.float64).reshape(N, 16)
-    out = _lib.host_empty((len(V), 3), np.float32)
-    cnt = _lib.host_empty(len(V), np.int32)
+    out = np.empty((len(V), 3), np.float32)
+    cnt = np.empty(len(V), np.int32)
     call("mqr_color_map", int(device), ptr(V), len(V), MQR_HOST, ptr(im), ptr(d), MQR_HOST, N, H, W,
          ptr(Kd, _lib._f64p), ptr(Td, _lib._f64p), float(max_depth), float(visibility_threshold), int(margin),
          float(discontinuity_threshold), int(half_dilation), float(depth_trunc), int(knn), ptr(out), ptr(cnt), MQR_HOST)

@@ -47,9 +47,9 @@ def filter_mesh_components_gpu(vertices, normals, triangles, min_triangle_count:
     try:
         nv, nt = ctypes.c_int64(), ctypes.c_int64()
         call("mqr_geom_counts", g, ctypes.byref(nv), ctypes.byref(nt))
-        pos = _lib.host_empty((nv.value, 3), np.float32)
-        nrm = _lib.host_empty((nv.value, 3), np.float32)
-        tri = _lib.host_empty((nt.value, 3), np.int32)
+        pos = np.empty((nv.value, 3), np.float32)
+        nrm = np.empty((nv.value, 3), np.float32)
+        tri = np.empty((nt.value, 3), np.int32)
         call("mqr_geom_copy", g, ptr(pos), ptr(nrm), ptr(tri) if nt.value else None, MQR_HOST)
     finally:
         call("mqr_geom_free", g)

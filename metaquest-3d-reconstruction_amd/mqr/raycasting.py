@@ -105,11 +105,11 @@ class RaycastingScene:
         return Tensor(rays)
 
     def _outputs(self, n, full):
-        t = _lib.host_empty(n, np.float32)
+        t = np.empty(n, np.float32)
         if not full:
             return t, None, None, None, None
-        return (t, _lib.host_empty(n, np.uint32), _lib.host_empty(n, np.uint32), _lib.host_empty((n, 2), np.float32),
-                _lib.host_empty((n, 3), np.float32))
+        return (t, np.empty(n, np.uint32), np.empty(n, np.uint32), np.empty((n, 2), np.float32),
+                np.empty((n, 3), np.float32))
 
     @staticmethod
     def _p(a):

@@ -199,9 +199,9 @@ class VoxelBlockGrid:
         try:
             nv, nt = ctypes.c_int64(), ctypes.c_int64()
             call("mqr_geom_counts", g, ctypes.byref(nv), ctypes.byref(nt))
-            pos = _lib.host_empty((nv.value, 3), np.float32)
-            nrm = _lib.host_empty((nv.value, 3), np.float32)
-            tri = _lib.host_empty((nt.value, 3), np.int32)
+            pos = np.empty((nv.value, 3), np.float32)
+            nrm = np.empty((nv.value, 3), np.float32)
+            tri = np.empty((nt.value, 3), np.int32)
             call("mqr_geom_copy", g, ptr(pos), ptr(nrm), ptr(tri) if nt.value else None, MQR_HOST)
         finally:
             call("mqr_geom_free", g)
@@ -220,9 +220,9 @@ class VoxelBlockGrid:
         """(keys (N,3) int32, tsdf (N,R,R,R) f32, weight (N,R,R,R) f32) in buffer order."""
         n = self.size()
         R = self.block_resolution
-        keys = _lib.host_empty((n, 3), np.int32)
-        tsdf = _lib.host_empty((n, R, R, R), np.float32)
-        wgt = _lib.host_empty((n, R, R, R), np.float32)
+        keys = np.empty((n, 3), np.int32)
+        tsdf = np.empty((n, R, R, R), np.float32)
+        wgt = np.empty((n, R, R, R), np.float32)
         if n:
             call("mqr_vbg_export", self._h, ptr(keys), ptr(tsdf), ptr(wgt), MQR_HOST)
         return keys, tsdf, wgt

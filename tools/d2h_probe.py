@@ -2,8 +2,10 @@
 """Device -> host copy ceilings on this box (the C5 mesh copy, bench c5.extract_ms): 1 GiB from HBM into
 (a) torch pinned memory, (b) a fresh pageable torch tensor (.cpu()), (c) mqr_memcpy into a fresh numpy
 array (first-touch page faults inside the copy) and (d) into the same array again (pages present), and
-(e) the cost of first-touching a fresh array alone (np.empty + fill, one thread), and (f) mqr_memcpy into a
-fresh mqr._lib.host_empty array (2 MiB-aligned MADV_HUGEPAGE mapping, what the library's callers use).
+(e) the cost of first-touching a fresh array alone (np.empty + fill, one thread), (f) mqr_memcpy into a
+fresh 2 MiB-aligned private MADV_HUGEPAGE mapping and (g) into a second fresh np.empty array.  (c) is the
+process's first large copy and also pays the staging set-up (pinned buffers, streams, threads): compare
+(g), not (c), with (f).
 MQR_D2H_THREADS sets the host threads of libmqr's staged copy (default 8).  Prints one JSON line."""
 import ctypes
 import json
@@ -13,6 +15,19 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "metaquest-3d-reconstruction_amd"))
+
+
+def huge_empty(nbytes):
+    """float32 array over a 2 MiB-aligned private anonymous mapping advised MADV_HUGEPAGE (MAP_PRIVATE:
+    Python's default anonymous mmap is shared memory, whose huge pages follow shmem_enabled)."""
+    import mmap
+    import numpy as np
+    mm = mmap.mmap(-1, nbytes + (2 << 20), flags=mmap.MAP_PRIVATE)
+    view = ctypes.c_char.from_buffer(mm)
+    off = (-ctypes.addressof(view)) % (2 << 20)
+    del view
+    mm.madvise(mmap.MADV_HUGEPAGE, off, nbytes)
+    return np.frombuffer(mm, np.float32, nbytes // 4, off)
 
 
 def main():
@@ -38,6 +53,13 @@ def main():
     x = dev.cpu()
     out["torch_pageable_fresh_gbs"] = gbs(time.perf_counter() - t0)
     del x
+    small = np.empty((48 << 20) // 4, np.float32)  # above the parallel threshold (32 MiB)
+    for name in ("first_48mb_copy_ms", "second_48mb_copy_ms"):
+        t0 = time.perf_counter()
+        _lib.call("mqr_memcpy", _lib.ptr(small), _lib.MQR_HOST, ctypes.c_void_p(dev.data_ptr()), _lib.MQR_DEVICE,
+                  small.nbytes, 0)
+        out[name] = (time.perf_counter() - t0) * 1e3
+    del small
     a = np.empty(n, np.float32)
     t0 = time.perf_counter()
     _lib.call("mqr_memcpy", _lib.ptr(a), _lib.MQR_HOST, ctypes.c_void_p(dev.data_ptr()), _lib.MQR_DEVICE, nbytes, 0)
@@ -48,12 +70,13 @@ def main():
     out["mqr_touched_gbs"] = gbs(time.perf_counter() - t0)
     out["values_ok"] = ok and bool(np.all(a[:: 1 << 16] == 1.0))
     del a
-    h = _lib.host_empty(n, np.float32)
-    t0 = time.perf_counter()
-    _lib.call("mqr_memcpy", _lib.ptr(h), _lib.MQR_HOST, ctypes.c_void_p(dev.data_ptr()), _lib.MQR_DEVICE, nbytes, 0)
-    out["mqr_fresh_host_empty_gbs"] = gbs(time.perf_counter() - t0)
-    out["values_ok"] = out["values_ok"] and bool(np.all(h[:: 1 << 16] == 1.0) and h[-1] == 1.0)
-    del h
+    for name in ("mqr_fresh_hugepage_gbs", "mqr_second_fresh_gbs"):
+        h = huge_empty(nbytes) if name == "mqr_fresh_hugepage_gbs" else np.empty(n, np.float32)
+        t0 = time.perf_counter()
+        _lib.call("mqr_memcpy", _lib.ptr(h), _lib.MQR_HOST, ctypes.c_void_p(dev.data_ptr()), _lib.MQR_DEVICE, nbytes, 0)
+        out[name] = gbs(time.perf_counter() - t0)
+        out["values_ok"] = out["values_ok"] and bool(np.all(h[:: 1 << 16] == 1.0) and h[-1] == 1.0)
+        del h
     t0 = time.perf_counter()
     b = np.empty(n, np.float32)
     b.fill(0.0)
