@@ -431,7 +431,7 @@ int mqr_color_vertices(int device, const float* vertices, int64_t nv, int vloc, 
         void* p = nullptr;
         if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
         owned.push_back(p);
-        if (hipMemcpyAsync(p, h, bytes, hipMemcpyHostToDevice, s) != hipSuccess) return nullptr;
+        if (copy_to_device(device, p, h, bytes, s)) return nullptr;
         return p;
     };
     const int64_t HW = (int64_t)H * W;
@@ -458,9 +458,8 @@ int mqr_color_vertices(int device, const float* vertices, int64_t nv, int vloc, 
             rc = 1;
         }
         if (!rc && out_loc != MQR_DEVICE &&
-            (hipMemcpyAsync(colors_out, dO, sizeof(float) * 3 * nv, hipMemcpyDeviceToHost, s) != hipSuccess ||
-             (counts_out && hipMemcpyAsync(counts_out, dN, sizeof(int32_t) * nv, hipMemcpyDeviceToHost, s) !=
-                                hipSuccess))) {
+            (copy_to_host(device, colors_out, dO, sizeof(float) * 3 * nv, s) ||
+             (counts_out && copy_to_host(device, counts_out, dN, sizeof(int32_t) * nv, s)))) {
             set_error("mqr_color_vertices: copy back failed");
             rc = 1;
         }
@@ -507,7 +506,7 @@ int mqr_color_map(int device, const float* vertices, int64_t nv, int vloc, const
     auto dev = [&](const void* h, size_t bytes, bool host) -> const void* {
         if (!host) return h;
         void* p = alloc(bytes);
-        if (!p || hipMemcpyAsync(p, h, bytes, hipMemcpyHostToDevice, s) != hipSuccess) return nullptr;
+        if (!p || copy_to_device(device, p, h, bytes, s)) return nullptr;
         return p;
     };
     int rc = 0;
@@ -612,8 +611,8 @@ int mqr_color_map(int device, const float* vertices, int64_t nv, int vloc, const
         }
         if (!rc && hipGetLastError() != hipSuccess) fail("mqr_color_map: kernel launch failed");
         if (!rc && out_loc != MQR_DEVICE &&
-            (hipMemcpyAsync(colors_out, dO, sizeof(float) * 3 * nv, hipMemcpyDeviceToHost, s) != hipSuccess ||
-             (counts_out && hipMemcpyAsync(counts_out, cnt, sizeof(int32_t) * nv, hipMemcpyDeviceToHost, s) != hipSuccess)))
+            (copy_to_host(device, colors_out, dO, sizeof(float) * 3 * nv, s) ||
+             (counts_out && copy_to_host(device, counts_out, cnt, sizeof(int32_t) * nv, s))))
             fail("mqr_color_map: copy back failed");
         if (!rc && out_loc == MQR_DEVICE && counts_out &&
             hipMemcpyAsync(counts_out, cnt, sizeof(int32_t) * nv, hipMemcpyDeviceToDevice, s) != hipSuccess)

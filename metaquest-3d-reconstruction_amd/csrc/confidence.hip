@@ -906,7 +906,10 @@ int mqr_confidence(int device, const float* depths, int depth_loc, int N, int H,
     const float* dsrc = depths;
     if (depth_loc != MQR_DEVICE) {
         MQR_CHECK_HIP(hipMalloc(&dd, sizeof(float) * N * HW));
-        MQR_CHECK_HIP(hipMemcpy(dd, depths, sizeof(float) * N * HW, hipMemcpyHostToDevice));
+        if (copy_to_device(device, dd, depths, sizeof(float) * N * HW, s)) {
+            (void)hipFree(dd);
+            return 1;
+        }
         dsrc = dd;
     }
     if (out_loc != MQR_DEVICE) {
@@ -951,17 +954,17 @@ int mqr_confidence(int device, const float* depths, int depth_loc, int N, int H,
         cc.last[3] = (int64_t)h[3];
         cc.last[2] = cc.last[0] - cc.last[1] - cc.last[3];
     }
-    if (out_loc != MQR_DEVICE) {
-        MQR_CHECK_HIP(hipMemcpyAsync(conf, dconf, sizeof(double) * nref * HW, hipMemcpyDeviceToHost, s));
-        MQR_CHECK_HIP(hipMemcpyAsync(valid, dvalid, sizeof(int32_t) * nref * HW, hipMemcpyDeviceToHost, s));
-    }
-    MQR_CHECK_HIP(hipStreamSynchronize(s));
+    int rc = 0;
+    if (out_loc != MQR_DEVICE)
+        rc = copy_to_host(device, conf, dconf, sizeof(double) * nref * HW, s) ||
+             copy_to_host(device, valid, dvalid, sizeof(int32_t) * nref * HW, s);
+    if (!rc) MQR_CHECK_HIP(hipStreamSynchronize(s));
     if (out_loc != MQR_DEVICE) {
         (void)hipFree(dconf);
         (void)hipFree(dvalid);
     }
     if (dd) (void)hipFree(dd);
-    return 0;
+    return rc;
 }
 
 int mqr_confidence_stats(int device, int enable, int64_t* last4) {

@@ -1674,7 +1674,29 @@ __global__ __launch_bounds__(256) void k_copy_out1(uint8_t* __restrict__ dst, co
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) dst[i] = src[i];
 }
 
-int d2h_parallel(int device, void* dst, const void* src, size_t bytes) {
+hipStream_t copy_stream(int device) {
+    if (caller_stream()) {
+        hipDevice_t sd = -1;
+        const bool same = hipStreamGetDevice(caller_stream(), &sd) == hipSuccess && sd == device;
+        (void)hipGetLastError();
+        if (same) return caller_stream();
+    }
+    return nullptr;
+}
+
+static void launch_copy(char* to, const char* from, size_t len, hipStream_t s) {
+    const bool aligned = ((reinterpret_cast<uintptr_t>(to) | reinterpret_cast<uintptr_t>(from)) & 15) == 0;
+    const size_t n16 = aligned ? len / 16 : 0, tail = len - 16 * n16;
+    if (n16) k_copy_out16<<<1024, 256, 0, s>>>(reinterpret_cast<uint4*>(to), reinterpret_cast<const uint4*>(from), n16);
+    if (tail)
+        k_copy_out1<<<(unsigned)std::min<size_t>(1024, (tail + 255) / 256), 256, 0, s>>>(
+            reinterpret_cast<uint8_t*>(to) + 16 * n16, reinterpret_cast<const uint8_t*>(from) + 16 * n16, tail);
+}
+
+// One ring transfer: the GPU fills slot k % S with chunk k, host thread k % T copies it out once its
+// event completes; this thread queues the GPU copies in chunk order, each into a slot whose previous
+// chunk has been copied out.
+static int ring_copy(int device, char* dst, const char* src, size_t bytes, hipStream_t s) {
     MQR_REQUIRE(device >= 0 && device < kD2HDevices, "device index out of range");
     std::lock_guard<std::mutex> lk(g_d2h_mu);
     D2HRing& r = g_d2h[device];
@@ -1682,59 +1704,45 @@ int d2h_parallel(int device, void* dst, const void* src, size_t bytes) {
         MQR_CHECK_HIP(hipHostMalloc(reinterpret_cast<void**>(&r.buf), kD2HSlots * kD2HChunk, hipHostMallocDefault));
         for (auto& e : r.ev) MQR_CHECK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
-    // the caller's stream when it is this device's (mqr_set_stream; its earlier work on `src` is then
-    // ordered), else the null stream
-    hipStream_t s = nullptr;
-    if (caller_stream()) {
-        hipDevice_t sd = -1;
-        if (hipStreamGetDevice(caller_stream(), &sd) == hipSuccess && sd == device) s = caller_stream();
-        (void)hipGetLastError();
-    }
     const size_t nchunks = (bytes + kD2HChunk - 1) / kD2HChunk;
     // MQR_D2H_THREADS (1..8): another thread count, for tools/d2h_probe.py
     static const int env_threads =
         getenv("MQR_D2H_THREADS") ? std::max(1, std::min(8, atoi(getenv("MQR_D2H_THREADS")))) : kD2HThreads;
     const int T = (int)std::min<size_t>(env_threads, nchunks);
-    const bool aligned = (reinterpret_cast<uintptr_t>(src) & 15) == 0;
     auto len_of = [&](size_t k) { return std::min(kD2HChunk, bytes - k * kD2HChunk); };
-    std::atomic<int64_t> issued{0};  // chunks whose copy and event are queued
-    std::atomic<int64_t> slot_done[kD2HSlots];  // the last chunk copied out of each slot
-    for (auto& d : slot_done) d.store(-1);
+    std::atomic<int64_t> issued{0};            // chunks whose GPU copy and event are queued
+    std::atomic<int64_t> host_done[kD2HSlots];  // the last chunk copied out of each slot
+    for (auto& d : host_done) d.store(-1);
     std::atomic<int> failed{0};
     std::vector<std::string> errs(T + 1);
-    auto out = [&](int t) {  // host thread t: chunks t, t + T, ... out of their slots
+    auto host_side = [&](int t) {
         for (size_t k = (size_t)t; k < nchunks; k += (size_t)T) {
             while (issued.load(std::memory_order_acquire) <= (int64_t)k && !failed.load()) std::this_thread::yield();
             if (failed.load()) return;
             const int slot = (int)(k % kD2HSlots);
             hipError_t e = hipEventSynchronize(r.ev[slot]);
             if (e != hipSuccess) {
-                errs[t] = std::string("d2h copy: hipEventSynchronize: ") + hipGetErrorString(e);
+                errs[t] = std::string("host copy: hipEventSynchronize: ") + hipGetErrorString(e);
                 failed.store(1);
                 return;
             }
-            std::memcpy(static_cast<char*>(dst) + k * kD2HChunk, r.buf + slot * kD2HChunk, len_of(k));
-            slot_done[slot].store((int64_t)k, std::memory_order_release);
+            std::memcpy(dst + k * kD2HChunk, r.buf + slot * kD2HChunk, len_of(k));
+            host_done[slot].store((int64_t)k, std::memory_order_release);
         }
     };
     std::vector<std::thread> th;
-    for (int t = 0; t < T; ++t) th.emplace_back(out, t);
-    for (size_t k = 0; k < nchunks && !failed.load(); ++k) {  // this thread queues the chunk copies
+    for (int t = 0; t < T; ++t) th.emplace_back(host_side, t);
+    for (size_t k = 0; k < nchunks && !failed.load(); ++k) {
         const int slot = (int)(k % kD2HSlots);
         if (k >= (size_t)kD2HSlots)
-            while (slot_done[slot].load(std::memory_order_acquire) != (int64_t)(k - kD2HSlots) && !failed.load())
+            while (host_done[slot].load(std::memory_order_acquire) != (int64_t)(k - kD2HSlots) && !failed.load())
                 std::this_thread::yield();
         if (failed.load()) break;
-        const char* from = static_cast<const char*>(src) + k * kD2HChunk;
-        char* to = r.buf + slot * kD2HChunk;
-        const size_t len = len_of(k), n16 = aligned ? len / 16 : 0, tail = len - 16 * n16;
-        if (n16) k_copy_out16<<<1024, 256, 0, s>>>(reinterpret_cast<uint4*>(to), reinterpret_cast<const uint4*>(from), n16);
-        if (tail) k_copy_out1<<<(unsigned)std::min<size_t>(1024, (tail + 255) / 256), 256, 0, s>>>(
-                      reinterpret_cast<uint8_t*>(to) + 16 * n16, reinterpret_cast<const uint8_t*>(from) + 16 * n16, tail);
+        launch_copy(r.buf + slot * kD2HChunk, src + k * kD2HChunk, len_of(k), s);
         hipError_t e = hipGetLastError();
         if (e == hipSuccess) e = hipEventRecord(r.ev[slot], s);
         if (e != hipSuccess) {
-            errs[T] = std::string("d2h copy: chunk copy launch: ") + hipGetErrorString(e);
+            errs[T] = std::string("host copy: chunk copy launch: ") + hipGetErrorString(e);
             failed.store(1);
             break;
         }
@@ -1748,6 +1756,39 @@ int d2h_parallel(int device, void* dst, const void* src, size_t bytes) {
                 set_error(m);
                 return 1;
             }
+    }
+    return 0;
+}
+
+int d2h_parallel(int device, void* dst, const void* src, size_t bytes) {
+    return copy_to_host(device, dst, src, bytes, copy_stream(device));
+}
+
+// page-locked host memory (hipHostMalloc / hipHostRegister, e.g. torch's pin_memory()): the DMA engine
+// reads or writes it directly, no staging
+static bool host_pinned(const void* p) {
+    hipPointerAttribute_t a{};
+    const bool pinned = hipPointerGetAttributes(&a, p) == hipSuccess && a.type == hipMemoryTypeHost;
+    (void)hipGetLastError();
+    return pinned;
+}
+
+int copy_to_host(int device, void* dst, const void* src, size_t bytes, hipStream_t s) {
+    if (bytes >= kD2HParallelMin && !host_pinned(dst)) return ring_copy(device, static_cast<char*>(dst), static_cast<const char*>(src), bytes, s);
+    if (bytes) {
+        MQR_CHECK_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s));
+        MQR_CHECK_HIP(hipStreamSynchronize(s));
+    }
+    return 0;
+}
+
+// uploads: HIP's own pageable path already runs at the link's rate from present pages (1 GiB: 55.8 GB/s,
+// against 44.1 through a ring like the one above, profiles/r05_d2h_probe.jsonl)
+int copy_to_device(int device, void* dst, const void* src, size_t bytes, hipStream_t s) {
+    (void)device;
+    if (bytes) {
+        MQR_CHECK_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
+        MQR_CHECK_HIP(hipStreamSynchronize(s));
     }
     return 0;
 }

@@ -209,17 +209,17 @@ int mqr_decode_depth(int device, const float* raw, int raw_loc, int N, int H, in
     char* sp = c.scratch;
     const float* d_raw = raw;
     if (stage_raw) {
-        MQR_CHECK_HIP(hipMemcpyAsync(sp, raw, sizeof(float) * total, hipMemcpyHostToDevice, c.s));
+        if (copy_to_device(device, sp, raw, sizeof(float) * total, c.s)) return 1;
         d_raw = reinterpret_cast<const float*>(sp);
         sp += b_raw;
     }
     const double* d_conf = conf;
     const int32_t* d_vc = valid_count;
     if (stage_mask) {
-        MQR_CHECK_HIP(hipMemcpyAsync(sp, conf, sizeof(double) * total, hipMemcpyHostToDevice, c.s));
+        if (copy_to_device(device, sp, conf, sizeof(double) * total, c.s)) return 1;
         d_conf = reinterpret_cast<const double*>(sp);
         sp += b_conf;
-        MQR_CHECK_HIP(hipMemcpyAsync(sp, valid_count, sizeof(int32_t) * total, hipMemcpyHostToDevice, c.s));
+        if (copy_to_device(device, sp, valid_count, sizeof(int32_t) * total, c.s)) return 1;
         d_vc = reinterpret_cast<const int32_t*>(sp);
         sp += b_vc;
     }
@@ -242,7 +242,7 @@ int mqr_decode_depth(int device, const float* raw, int raw_loc, int N, int H, in
                            d_vc, conf_thr, count_thr, d_out, c.d_flags);
     MQR_CHECK_HIP(hipGetLastError());
     MQR_CHECK_HIP(hipMemcpyAsync(c.h_flags, c.d_flags, sizeof(uint32_t) * N, hipMemcpyDeviceToHost, c.s));
-    if (stage_out) MQR_CHECK_HIP(hipMemcpyAsync(depth_out, d_out, sizeof(float) * total, hipMemcpyDeviceToHost, c.s));
+    if (stage_out && copy_to_host(device, depth_out, d_out, sizeof(float) * total, c.s)) return 1;
     MQR_CHECK_HIP(hipStreamSynchronize(c.s));
     for (int f = 0; f < N; ++f) {
         const uint32_t fl = c.h_flags[f];

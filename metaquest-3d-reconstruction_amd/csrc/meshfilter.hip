@@ -729,9 +729,15 @@ int mqr_mesh_filter_components(int device, const float* vertices, const float* n
     m.nrm = normals ? c.alloc<float>(3 * nv) : nullptr;
     m.tri = c.alloc<int32_t>(3 * nt);
     MQR_REQUIRE(m.pos && m.tri && (!normals || m.nrm), "mesh filter: device allocation failed");
-    if (nv) MQR_CHECK_HIP(hipMemcpyAsync(m.pos, vertices, sizeof(float) * 3 * nv, k, c.s));
-    if (nv && normals) MQR_CHECK_HIP(hipMemcpyAsync(m.nrm, normals, sizeof(float) * 3 * nv, k, c.s));
-    if (nt) MQR_CHECK_HIP(hipMemcpyAsync(m.tri, triangles, sizeof(int32_t) * 3 * nt, k, c.s));
+    if (loc == MQR_DEVICE) {
+        if (nv) MQR_CHECK_HIP(hipMemcpyAsync(m.pos, vertices, sizeof(float) * 3 * nv, k, c.s));
+        if (nv && normals) MQR_CHECK_HIP(hipMemcpyAsync(m.nrm, normals, sizeof(float) * 3 * nv, k, c.s));
+        if (nt) MQR_CHECK_HIP(hipMemcpyAsync(m.tri, triangles, sizeof(int32_t) * 3 * nt, k, c.s));
+    } else if (copy_to_device(device, m.pos, vertices, sizeof(float) * 3 * nv, c.s) ||
+               (normals && copy_to_device(device, m.nrm, normals, sizeof(float) * 3 * nv, c.s)) ||
+               copy_to_device(device, m.tri, triangles, sizeof(int32_t) * 3 * nt, c.s)) {
+        return 1;
+    }
     if (nt > 0) {
         // ---- cluster_connected_triangles
         const int64_t ne = 3 * nt;

@@ -256,5 +256,12 @@ hipStream_t caller_stream();  // the calling thread's caller stream (nullptr: th
 // mqr_geom_copy and mqr_memcpy use it from kD2HParallelMin bytes on.
 constexpr size_t kD2HParallelMin = size_t(32) << 20;
 int d2h_parallel(int device, void* dst, const void* src, size_t bytes);
+// Host <-> device copies ordered on stream s, complete on return (the bytes are in place and the host
+// buffer is free).  Downloads of kD2HParallelMin bytes or more into pageable memory go through the pinned
+// ring, everything else is hipMemcpyAsync + a stream synchronize.  copy_stream(): the caller's stream
+// (mqr_set_stream) when it is `device`'s, else null.
+int copy_to_host(int device, void* dst, const void* src, size_t bytes, hipStream_t s);
+int copy_to_device(int device, void* dst, const void* src, size_t bytes, hipStream_t s);
+hipStream_t copy_stream(int device);
 int activate_ordered(mqr_vbg* v, const uint64_t* dkeys, int64_t n);  // empty volume, buffer i = key i
 }  // namespace mqr

@@ -630,9 +630,16 @@ int mqr_scene_add_triangles(mqr_scene* s, const float* vertices, int64_t nv, con
     if (loc == MQR_DEVICE && order_after_caller(s->device, s->stream)) return 2;
     MQR_CHECK_HIP(hipMalloc(&g.v, sizeof(float) * 3 * std::max<int64_t>(nv, 1)));
     MQR_CHECK_HIP(hipMalloc(&g.t, sizeof(int32_t) * 3 * std::max<int64_t>(nt, 1)));
-    if (nv) MQR_CHECK_HIP(hipMemcpyAsync(g.v, vertices, sizeof(float) * 3 * nv, k, s->stream));
-    if (nt) MQR_CHECK_HIP(hipMemcpyAsync(g.t, triangles, sizeof(int32_t) * 3 * nt, k, s->stream));
-    MQR_CHECK_HIP(hipStreamSynchronize(s->stream));
+    if (loc == MQR_DEVICE) {
+        if (nv) MQR_CHECK_HIP(hipMemcpyAsync(g.v, vertices, sizeof(float) * 3 * nv, k, s->stream));
+        if (nt) MQR_CHECK_HIP(hipMemcpyAsync(g.t, triangles, sizeof(int32_t) * 3 * nt, k, s->stream));
+        MQR_CHECK_HIP(hipStreamSynchronize(s->stream));
+    } else if (copy_to_device(s->device, g.v, vertices, sizeof(float) * 3 * nv, s->stream) ||
+               copy_to_device(s->device, g.t, triangles, sizeof(int32_t) * 3 * nt, s->stream)) {
+        (void)hipFree(g.v);
+        (void)hipFree(g.t);
+        return 1;
+    }
     if (geom_id) *geom_id = (uint32_t)s->geoms.size();
     s->geoms.push_back(g);
     s->built = false;
@@ -692,12 +699,12 @@ int mqr_scene_cast_pinhole(mqr_scene* s, const double* K, const double* T_wc, in
         }
     }
     if (!rc && out_loc != MQR_DEVICE) {
-        const hipMemcpyKind k = hipMemcpyDeviceToHost;
-        if (hipMemcpyAsync(t_hit, d_t, sizeof(float) * total, k, s->stream) ||
-            (geom_ids && hipMemcpyAsync(geom_ids, d_g, sizeof(uint32_t) * total, k, s->stream)) ||
-            (prim_ids && hipMemcpyAsync(prim_ids, d_p, sizeof(uint32_t) * total, k, s->stream)) ||
-            (uvs && hipMemcpyAsync(uvs, d_uv, sizeof(float) * 2 * total, k, s->stream)) ||
-            (normals && hipMemcpyAsync(normals, d_n, sizeof(float) * 3 * total, k, s->stream))) {
+        const int dv = s->device;
+        if (copy_to_host(dv, t_hit, d_t, sizeof(float) * total, s->stream) ||
+            (geom_ids && copy_to_host(dv, geom_ids, d_g, sizeof(uint32_t) * total, s->stream)) ||
+            (prim_ids && copy_to_host(dv, prim_ids, d_p, sizeof(uint32_t) * total, s->stream)) ||
+            (uvs && copy_to_host(dv, uvs, d_uv, sizeof(float) * 2 * total, s->stream)) ||
+            (normals && copy_to_host(dv, normals, d_n, sizeof(float) * 3 * total, s->stream))) {
             set_error("cast_pinhole: copy back failed");
             rc = 1;
         }
@@ -730,7 +737,7 @@ int mqr_scene_cast_rays(mqr_scene* s, const float* rays, int64_t nrays, int rays
     bool ok = true;
     if (rays_loc != MQR_DEVICE) {
         float* p = (float*)dalloc(sizeof(float) * 6 * nrays);
-        ok = p && hipMemcpyAsync(p, rays, sizeof(float) * 6 * nrays, hipMemcpyHostToDevice, s->stream) == hipSuccess;
+        ok = p && copy_to_device(s->device, p, rays, sizeof(float) * 6 * nrays, s->stream) == 0;
         d_r = p;
     }
     if (out_loc != MQR_DEVICE) {
@@ -754,12 +761,12 @@ int mqr_scene_cast_rays(mqr_scene* s, const float* rays, int64_t nrays, int rays
         }
     }
     if (!rc && out_loc != MQR_DEVICE) {
-        const hipMemcpyKind k = hipMemcpyDeviceToHost;
-        if (hipMemcpyAsync(t_hit, d_t, sizeof(float) * nrays, k, s->stream) ||
-            (geom_ids && hipMemcpyAsync(geom_ids, d_g, sizeof(uint32_t) * nrays, k, s->stream)) ||
-            (prim_ids && hipMemcpyAsync(prim_ids, d_p, sizeof(uint32_t) * nrays, k, s->stream)) ||
-            (uvs && hipMemcpyAsync(uvs, d_uv, sizeof(float) * 2 * nrays, k, s->stream)) ||
-            (normals && hipMemcpyAsync(normals, d_n, sizeof(float) * 3 * nrays, k, s->stream))) {
+        const int dv = s->device;
+        if (copy_to_host(dv, t_hit, d_t, sizeof(float) * nrays, s->stream) ||
+            (geom_ids && copy_to_host(dv, geom_ids, d_g, sizeof(uint32_t) * nrays, s->stream)) ||
+            (prim_ids && copy_to_host(dv, prim_ids, d_p, sizeof(uint32_t) * nrays, s->stream)) ||
+            (uvs && copy_to_host(dv, uvs, d_uv, sizeof(float) * 2 * nrays, s->stream)) ||
+            (normals && copy_to_host(dv, normals, d_n, sizeof(float) * 3 * nrays, s->stream))) {
             set_error("cast_rays: copy back failed");
             rc = 1;
         }

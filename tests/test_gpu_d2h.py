@@ -1,8 +1,10 @@
-"""Large device -> host copies (csrc/extract.hip d2h_parallel: a copy kernel into a ring of pinned slots,
-host threads copying the slots out), used by mqr_memcpy and mqr_geom_copy from 32 MiB on.  Byte-exact
-against torch's own copy for: more chunks than ring slots, lengths that are not a multiple of the chunk
-or of 16 bytes, a source that is not 16-byte aligned (byte-copy path), a destination offset inside a
-larger host array, and a copy ordered behind a torch side stream's write (mqr_set_stream)."""
+"""Large host <-> device copies.  Downloads into pageable memory from 32 MiB on go through
+csrc/extract.hip ring_copy (copy kernels into a ring of pinned slots, host threads copying them out),
+used by mqr_memcpy, mqr_geom_copy and the host-array outputs of colouring, ray casting, confidence and
+decoding; uploads use HIP's pageable path.  Byte-exact against torch's own copy for: more chunks than
+ring slots, lengths that are not a multiple of the chunk or of 16 bytes, sources / destinations that are
+not 16-byte aligned (byte-copy path), offsets inside larger arrays, page-locked host buffers (direct DMA),
+and copies ordered behind a torch side stream's write (mqr_set_stream)."""
 import ctypes
 
 import numpy as np
@@ -61,3 +63,32 @@ def test_large_d2h_copy_ordered_after_caller_stream():
         _lib.call("mqr_memcpy", ctypes.c_void_p(out.ctypes.data), _lib.MQR_HOST, ctypes.c_void_p(src.data_ptr()),
                   _lib.MQR_DEVICE, n, 0)
     assert (out == 7).all()
+
+
+@pytest.mark.parametrize("nbytes,dst_off", [(32 * MIB, 0), (200 * MIB + 12, 0), (97 * MIB + 5, 3), (64 * MIB, 16)])
+def test_large_h2d_copy_exact(nbytes, dst_off):
+    import torch
+    from mqr import _lib
+    rng = np.random.default_rng(nbytes)
+    host = rng.integers(0, 256, nbytes + 11, dtype=np.uint8)
+    dev = torch.full((nbytes + dst_off + 64,), 0xEE, dtype=torch.uint8, device="cuda")
+    _lib.call("mqr_memcpy", ctypes.c_void_p(dev.data_ptr() + dst_off), _lib.MQR_DEVICE,
+              ctypes.c_void_p(host.ctypes.data + 11), _lib.MQR_HOST, nbytes, 0)
+    back = dev.cpu().numpy()
+    assert np.array_equal(back[dst_off:dst_off + nbytes], host[11:])
+    assert (back[:dst_off] == 0xEE).all() and (back[dst_off + nbytes:] == 0xEE).all()
+
+
+def test_large_copies_pinned_host_buffers():
+    import torch
+    from mqr import _lib
+    n = 72 * MIB + 4
+    src = torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda")
+    pin = torch.empty(n, dtype=torch.uint8).pin_memory()
+    _lib.call("mqr_memcpy", ctypes.c_void_p(pin.data_ptr()), _lib.MQR_HOST, ctypes.c_void_p(src.data_ptr()),
+              _lib.MQR_DEVICE, n, 0)
+    assert torch.equal(pin, src.cpu())
+    dst = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    _lib.call("mqr_memcpy", ctypes.c_void_p(dst.data_ptr()), _lib.MQR_DEVICE, ctypes.c_void_p(pin.data_ptr()),
+              _lib.MQR_HOST, n, 0)
+    assert torch.equal(dst, src)
