@@ -379,11 +379,13 @@ def dropin_e2e_leg(seq, frames, device, fragment_workers=4):
                   voxel_size=0.005, block_resolution=16, block_count=40000, depth_max=4.0,
                   trunc_voxel_multiplier=10.0, device=int(device.index or 0))
         integrate(ds, io, Side.LEFT, **kw)  # warm-up (allocations, page cache)
-        runs = []
+        from mqr import o3d_utils
+        runs, splits = [], []
         for _ in range(5):  # median of 5: a single host-bound run varies by +-20 %
             t0 = time.perf_counter()
             vbg = integrate(ds, io, Side.LEFT, **kw)
             runs.append(time.perf_counter() - t0)
+            splits.append(dict(o3d_utils.last_integrate_times.__dict__))
             blocks = vbg.size()
             del vbg
         t_int = float(np.median(runs))
@@ -391,7 +393,7 @@ def dropin_e2e_leg(seq, frames, device, fragment_workers=4):
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
     return {"frames": n, "confidence_s": t_conf, "confidence_frames_per_s": n / t_conf, "integrate_s": t_int,
-            "integrate_runs_s": runs, "integrate_frames_per_s": n / t_int, "frames_per_s": n / (t_conf + t_int), "blocks": blocks,
+            "integrate_runs_s": runs, "integrate_splits_s": splits, "integrate_frames_per_s": n / t_int, "frames_per_s": n / (t_conf + t_int), "blocks": blocks,
             "fragments": frag,
             "note": "on-disk capture (raw + descriptor CSV), estimate_depth_confidences (writes npz) then "
                     "o3d_utils.integrate with confidence masking (median of 5 runs); host file I/O + PCIe included"}

@@ -203,6 +203,24 @@ int mqr_decode_depth(int device, const float* raw, int raw_loc, int N, int H, in
                      const uint8_t* has_mask, int mask_loc, double conf_thr, int count_thr, float* depth_out,
                      int out_loc, uint8_t* frame_ok);
 
+/* Host reads of the drop-in integrate.  Replaces, for n frames, the raw depth
+ * read of DepthDataIO.load_depth_map (np.fromfile of H*W little-endian float32,
+ * scripts/dataio/depth_data_io.py:33-53) and load_confidence_map (np.load of the np.savez npz:
+ * confidence_map <f8 HxW, valid_count <i4 HxW; depth_data_io.py:91-104): `threads` native threads pread
+ * the files straight into raw_out[n][H][W] and, when conf_paths is non-null, conf_out / vc_out[n][H][W]
+ * (conf_paths[f] may be null: no confidence read for that frame).  Host-only (no device work).
+ * status[f] is a set of MQR_FRAME_* bits.  A missing or unreadable raw file leaves zeros in raw_out
+ * (decoded invalid); *_OTHER (wrong size, a compressed / non-standard npz, another dtype or shape, a read
+ * error) is left to the caller's own loader, which then raises or logs exactly as the reference does. */
+#define MQR_FRAME_RAW_OK 1
+#define MQR_FRAME_RAW_MISSING 2
+#define MQR_FRAME_RAW_OTHER 4
+#define MQR_FRAME_CONF_OK 8
+#define MQR_FRAME_CONF_MISSING 16
+#define MQR_FRAME_CONF_OTHER 32
+int mqr_read_frames(int n, const char* const* raw_paths, const char* const* conf_paths, int H, int W,
+                    float* raw_out, double* conf_out, int32_t* vc_out, uint8_t* status, int threads);
+
 /* Kernel timing (HIP events on the volume's own stream).  enable=1 starts recording every
  * integrate-kernel launch; stats: launches, total kernel ms, union blocks, frame-blocks
  * (sum of per-frame touched blocks), frames, and the same for touch. */

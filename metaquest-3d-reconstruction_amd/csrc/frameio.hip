@@ -1,0 +1,221 @@
+// Host reads of the drop-in integrate: per frame, the raw NDC depth file
+// (H*W little-endian float32; reference dataio/depth_data_io.py:33-53 via np.fromfile) and the confidence
+// npz written by np.savez (members confidence_map <f8 HxW and valid_count <i4 HxW;
+// depth_data_io.py:91-115), read by native threads with pread straight into the caller's arrays.
+//
+// np.savez stores members uncompressed, so each member's array bytes are one contiguous file range:
+// the zip central directory gives the member's local header, the local header its data start, the .npy
+// header the dtype / order / shape and the data offset.  Anything else -- a compressed or otherwise
+// unexpected archive, another dtype or shape, a raw file of the wrong size, a read error -- is reported
+// per frame and left to the caller's own loader, so error behaviour stays the reference's.
+// Round 5: the Python loader (np.load per npz on 8 I/O threads) bounded the drop-in integrate at
+// 0.28-0.53 s of waiting per 500-frame call against 0.05-0.08 s of device hand-off (bench
+// dropin_e2e.integrate_splits_s).
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cerrno>
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "mqr_common.hpp"
+
+namespace {
+
+struct Fd {
+    int fd = -1;
+    explicit Fd(const char* p) : fd(::open(p, O_RDONLY | O_CLOEXEC)) {}
+    ~Fd() {
+        if (fd >= 0) ::close(fd);
+    }
+};
+
+bool pread_all(int fd, void* dst, size_t n, int64_t off) {
+    char* p = static_cast<char*>(dst);
+    while (n) {
+        const ssize_t r = ::pread(fd, p, n, (off_t)off);
+        if (r < 0 && errno == EINTR) continue;
+        if (r <= 0) return false;
+        p += r;
+        n -= (size_t)r;
+        off += r;
+    }
+    return true;
+}
+
+uint16_t u16(const unsigned char* p) { return (uint16_t)(p[0] | (p[1] << 8)); }
+uint32_t u32(const unsigned char* p) { return (uint32_t)u16(p) | ((uint32_t)u16(p + 2) << 16); }
+uint64_t u64(const unsigned char* p) { return (uint64_t)u32(p) | ((uint64_t)u32(p + 4) << 32); }
+
+// The .npy header dict: {'descr': '<f8', 'fortran_order': False, 'shape': (H, W), }
+bool npy_header_ok(const std::string& h, const char* descr, int H, int W) {
+    auto value_after = [&](const char* key) -> std::string {
+        const size_t k = h.find(key);
+        if (k == std::string::npos) return "";
+        size_t c = h.find(':', k);
+        if (c == std::string::npos) return "";
+        ++c;
+        while (c < h.size() && h[c] == ' ') ++c;
+        return h.substr(c);
+    };
+    const std::string d = value_after("'descr'");
+    if (d.compare(0, strlen(descr) + 2, std::string("'") + descr + "'") != 0) return false;
+    if (value_after("'fortran_order'").compare(0, 5, "False") != 0) return false;
+    const std::string s = value_after("'shape'");
+    long a = -1, b = -1;
+    if (s.empty() || s[0] != '(' || sscanf(s.c_str(), "(%ld, %ld)", &a, &b) != 2) return false;
+    const size_t close = s.find(')');
+    return close != std::string::npos && a == H && b == W &&
+           std::count(s.begin(), s.begin() + (std::ptrdiff_t)close, ',') == 1;
+}
+
+// Locate the array bytes of member `name` (stored) in the zip at fd: file offset of the data, or -1.
+struct Member {
+    std::string name;
+    int64_t data_off = -1;
+    int64_t size = -1;
+};
+
+bool zip_members(int fd, int64_t fsize, std::vector<Member>& want) {
+    // end of central directory: the last 22..(22 + 65535) bytes
+    const int64_t tail = std::min<int64_t>(fsize, 22 + 65535);
+    std::vector<unsigned char> t((size_t)tail);
+    if (!pread_all(fd, t.data(), t.size(), fsize - tail)) return false;
+    int64_t e = -1;
+    for (int64_t i = tail - 22; i >= 0; --i)
+        if (u32(&t[(size_t)i]) == 0x06054b50u) {
+            e = i;
+            break;
+        }
+    if (e < 0) return false;
+    uint64_t entries = u16(&t[(size_t)e + 10]), cd_size = u32(&t[(size_t)e + 12]), cd_off = u32(&t[(size_t)e + 16]);
+    if (entries == 0xFFFF || cd_size == 0xFFFFFFFFu || cd_off == 0xFFFFFFFFu) {  // zip64 end record
+        if (e < 20 || u32(&t[(size_t)e - 20]) != 0x07064b50u) return false;
+        const uint64_t z64 = u64(&t[(size_t)e - 20 + 8]);
+        unsigned char r[56];
+        if (!pread_all(fd, r, sizeof r, (int64_t)z64) || u32(r) != 0x06064b50u) return false;
+        entries = u64(r + 32);
+        cd_size = u64(r + 40);
+        cd_off = u64(r + 48);
+    }
+    if (cd_off + cd_size > (uint64_t)fsize || cd_size > (uint64_t(1) << 24)) return false;
+    std::vector<unsigned char> cd((size_t)cd_size);
+    if (!pread_all(fd, cd.data(), cd.size(), (int64_t)cd_off)) return false;
+    size_t p = 0;
+    for (uint64_t k = 0; k < entries; ++k) {
+        if (p + 46 > cd.size() || u32(&cd[p]) != 0x02014b50u) return false;
+        const uint16_t method = u16(&cd[p + 10]), nlen = u16(&cd[p + 28]), xlen = u16(&cd[p + 30]),
+                       clen = u16(&cd[p + 32]);
+        uint64_t csize = u32(&cd[p + 20]), usize = u32(&cd[p + 24]), loff = u32(&cd[p + 42]);
+        if (p + 46 + nlen + xlen + clen > cd.size()) return false;
+        const std::string name(reinterpret_cast<const char*>(&cd[p + 46]), nlen);
+        // zip64 extra field: the 0xFFFFFFFF fields, in order usize, csize, offset
+        for (size_t x = p + 46 + nlen; x + 4 <= p + 46 + nlen + xlen;) {
+            const uint16_t id = u16(&cd[x]), len = u16(&cd[x + 2]);
+            if (id == 0x0001) {
+                size_t q = x + 4;
+                if (usize == 0xFFFFFFFFu && q + 8 <= x + 4 + len) usize = u64(&cd[q]), q += 8;
+                if (csize == 0xFFFFFFFFu && q + 8 <= x + 4 + len) csize = u64(&cd[q]), q += 8;
+                if (loff == 0xFFFFFFFFu && q + 8 <= x + 4 + len) loff = u64(&cd[q]), q += 8;
+            }
+            x += 4 + len;
+        }
+        for (Member& m : want)
+            if (m.name == name) {
+                if (method != 0 || csize != usize) return false;  // compressed (np.savez_compressed)
+                unsigned char lh[30];
+                if (!pread_all(fd, lh, sizeof lh, (int64_t)loff) || u32(lh) != 0x04034b50u) return false;
+                m.data_off = (int64_t)loff + 30 + u16(lh + 26) + u16(lh + 28);
+                m.size = (int64_t)usize;
+            }
+        p += 46 + nlen + xlen + clen;
+    }
+    for (const Member& m : want)
+        if (m.data_off < 0 || m.data_off + m.size > fsize) return false;
+    return true;
+}
+
+// The array bytes of one .npy member at [off, off + size): checks the header, reads H*W*item bytes.
+bool read_npy(int fd, const Member& m, const char* descr, size_t item, int H, int W, void* dst) {
+    unsigned char pre[12];
+    if (m.size < 10 || !pread_all(fd, pre, 10, m.data_off)) return false;
+    if (memcmp(pre, "\x93NUMPY", 6) != 0) return false;
+    int64_t hl, hoff;
+    if (pre[6] == 1) {
+        hl = u16(pre + 8);
+        hoff = 10;
+    } else if (pre[6] == 2 || pre[6] == 3) {
+        if (m.size < 12 || !pread_all(fd, pre, 12, m.data_off)) return false;
+        hl = u32(pre + 8);
+        hoff = 12;
+    } else {
+        return false;
+    }
+    const size_t bytes = item * (size_t)H * (size_t)W;
+    if (hl > 65536 || hoff + hl + (int64_t)bytes != m.size) return false;
+    std::string h((size_t)hl, '\0');
+    if (!pread_all(fd, &h[0], (size_t)hl, m.data_off + hoff)) return false;
+    if (!npy_header_ok(h, descr, H, W)) return false;
+    return pread_all(fd, dst, bytes, m.data_off + hoff + hl);
+}
+
+}  // namespace
+
+extern "C" {
+
+int mqr_read_frames(int n, const char* const* raw_paths, const char* const* conf_paths, int H, int W, float* raw_out,
+                    double* conf_out, int32_t* vc_out, uint8_t* status, int threads) {
+    MQR_REQUIRE(n >= 0 && H > 0 && W > 0, "bad sizes");
+    MQR_REQUIRE(n == 0 || (raw_paths && raw_out && status), "null argument");
+    MQR_REQUIRE(!conf_paths || (conf_out && vc_out), "confidence paths without output arrays");
+    const size_t HW = (size_t)H * (size_t)W;
+    std::atomic<int> next{0};
+    auto work = [&] {
+        for (int f; (f = next.fetch_add(1)) < n;) {
+            uint8_t st = 0;
+            float* raw = raw_out + (size_t)f * HW;
+            {
+                Fd fd(raw_paths[f]);
+                struct stat sb {};
+                if (fd.fd < 0) {
+                    st |= errno == ENOENT ? MQR_FRAME_RAW_MISSING : MQR_FRAME_RAW_OTHER;
+                } else if (fstat(fd.fd, &sb) != 0 || (size_t)sb.st_size != 4 * HW || !pread_all(fd.fd, raw, 4 * HW, 0)) {
+                    st |= MQR_FRAME_RAW_OTHER;
+                } else {
+                    st |= MQR_FRAME_RAW_OK;
+                }
+                if (!(st & MQR_FRAME_RAW_OK)) memset(raw, 0, 4 * HW);  // no frame: zeros, decoded invalid
+            }
+            if (conf_paths && conf_paths[f]) {
+                Fd fd(conf_paths[f]);
+                struct stat sb {};
+                if (fd.fd < 0) {
+                    st |= errno == ENOENT ? MQR_FRAME_CONF_MISSING : MQR_FRAME_CONF_OTHER;
+                } else {
+                    std::vector<Member> m(2);
+                    m[0].name = "confidence_map.npy";
+                    m[1].name = "valid_count.npy";
+                    const bool ok = fstat(fd.fd, &sb) == 0 && zip_members(fd.fd, sb.st_size, m) &&
+                                    read_npy(fd.fd, m[0], "<f8", 8, H, W, conf_out + (size_t)f * HW) &&
+                                    read_npy(fd.fd, m[1], "<i4", 4, H, W, vc_out + (size_t)f * HW);
+                    st |= ok ? MQR_FRAME_CONF_OK : MQR_FRAME_CONF_OTHER;
+                }
+            }
+            status[f] = st;
+        }
+    };
+    const int T = std::max(1, std::min({threads > 0 ? threads : 8, 64, std::max(n, 1)}));
+    std::vector<std::thread> th;
+    for (int t = 1; t < T; ++t) th.emplace_back(work);
+    work();
+    for (auto& x : th) x.join();
+    return 0;
+}
+
+}  // extern "C"

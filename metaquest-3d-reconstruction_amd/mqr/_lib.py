@@ -89,6 +89,8 @@ SIGNATURES = {
     "mqr_confidence_stats": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _i64p]),
     "mqr_pixel_error_map": (ctypes.c_int, [ctypes.c_int, _f32p, _f32p, ctypes.c_int, ctypes.c_int, _f32p, _f32p,
                                            _f32p, _f32p, _f32p, ctypes.c_double, _f32p]),
+    "mqr_read_frames": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_char_p),
+                                       ctypes.c_int, ctypes.c_int, _vp, _vp, _vp, _vp, ctypes.c_int]),
     "mqr_decode_depth": (ctypes.c_int, [ctypes.c_int, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                         _f64p, _f64p, _u8p, _vp, _vp, _u8p, ctypes.c_int, ctypes.c_double,
                                         ctypes.c_int, _vp, ctypes.c_int, _u8p]),
@@ -121,6 +123,11 @@ SIGNATURES = {
 }
 
 _lib = None
+
+
+# mqr_read_frames status bits (include/mqr.h)
+MQR_FRAME_RAW_OK, MQR_FRAME_RAW_MISSING, MQR_FRAME_RAW_OTHER = 1, 2, 4
+MQR_FRAME_CONF_OK, MQR_FRAME_CONF_MISSING, MQR_FRAME_CONF_OTHER = 8, 16, 32
 
 
 class MqrError(RuntimeError):

@@ -14,14 +14,17 @@ The swap in the reference is one import line:
 """
 from __future__ import annotations
 
+import ctypes
+import os
 import sys
 import threading
+import time
 from concurrent.futures import ThreadPoolExecutor
 from typing import Optional
 
 import numpy as np
 
-from ._io import io_pool
+from ._io import io_pool, io_threads
 from .geometry import Image
 from .meshfilter import filter_mesh_components  # noqa: F401  (re-exported: o3d_utils.py:241-321)
 from .raycasting import raycast_in_color_view  # noqa: F401  (re-exported: o3d_utils.py:324-341)
@@ -107,6 +110,28 @@ def _raw_reader(depth_data_io, side):
     return None
 
 
+def _frame_paths(depth_data_io, side):
+    """(raw path fn, confidence npz path fn) of timestamp when the frames are read by the standard loaders
+    -- this package's DepthDataIO (methods not overridden) or the reference's (its depth_path_config:
+    get_depth_map_path / get_depth_confidence_map_path, depth_data_io.py:33-53, 91-104) -- so that the
+    native reader (mqr_read_frames) reads exactly those files; None otherwise or with MQR_NATIVE_IO=0."""
+    if os.environ.get("MQR_NATIVE_IO") == "0":
+        return None
+    from .dataio import DepthDataIO
+    if isinstance(depth_data_io, DepthDataIO):
+        cls = type(depth_data_io)
+        if cls.load_raw_depth is DepthDataIO.load_raw_depth and cls.load_confidence_map is DepthDataIO.load_confidence_map:
+            p = depth_data_io.paths
+            return (lambda ts: p.depth_map_path(side, ts)), (lambda ts: p.confidence_path(side, ts))
+        return None
+    cfg = getattr(depth_data_io, "depth_path_config", None)
+    if (not hasattr(depth_data_io, "load_raw_depth") and cfg is not None and hasattr(cfg, "get_depth_map_path")
+            and hasattr(cfg, "get_depth_confidence_map_path")):
+        return ((lambda ts: cfg.get_depth_map_path(side=side, timestamp=ts)),
+                (lambda ts: cfg.get_depth_confidence_map_path(side=side, timestamp=ts)))
+    return None
+
+
 def load_depth_map(depth_data_io, side, index: int, dataset, device, use_confidence_filtered_depth: bool,
                    confidence_threshold: float, valid_count_threshold: int) -> Optional[Image]:
     d = _masked_depth(depth_data_io, side, index, dataset, use_confidence_filtered_depth, confidence_threshold,
@@ -114,17 +139,26 @@ def load_depth_map(depth_data_io, side, index: int, dataset, device, use_confide
     return None if d is None else Image(d, device=device)
 
 
+# wall-clock split of the last integrate() call on this thread (seconds): volume creation, the main thread
+# waiting for the I/O threads' chunks, and the device hand-off (decode + mask + batched integrate calls)
+last_integrate_times = threading.local()
+
+
 def integrate(dataset, depth_data_io, side, use_confidence_filtered_depth: bool, confidence_threshold: float,
               valid_count_threshold: int, voxel_size: float, block_resolution: int, block_count: int,
               depth_max: float, trunc_voxel_multiplier: float, device, show_progress: bool = False,
               desc: Optional[str] = None, vbg_opt: Optional[VoxelBlockGrid] = None) -> VoxelBlockGrid:
+    times = {"create": 0.0, "wait_io": 0.0, "device": 0.0, "chunks": 0}
+    t_c = time.perf_counter()
     vbg = vbg_opt if vbg_opt is not None else VoxelBlockGrid(
         attr_names=("tsdf", "weight"), attr_dtypes=("float32", "float32"), attr_channels=((1), (1)),
         voxel_size=voxel_size, block_resolution=block_resolution, block_count=block_count, device=device)
+    times["create"] = time.perf_counter() - t_c
     n = len(dataset.timestamps)
     extrinsic_wc = dataset.transforms.extrinsics_wc
     intrinsics = compute_o3d_intrinsic_matrices(dataset)
     read_raw = _raw_reader(depth_data_io, side)
+    native = _frame_paths(depth_data_io, side) if read_raw is not None else None
 
     def load_one(i):
         if read_raw is None:
@@ -154,26 +188,73 @@ def integrate(dataset, depth_data_io, side, use_confidence_filtered_depth: bool,
         per-chunk allocations, stacking or copies on the main thread.  A missing file leaves a zero
         raw buffer, which the device decode flags invalid (frame_ok 0: skipped, as the reference
         skips a missing frame)."""
+        from .dataio import DepthDataIO
         hi = min(n, lo + CHUNK)
 
-        def one(j):
+        def one(j):  # 1: masked, 0: unmasked, -1: unmasked, confidence map not found (warned below)
             i = lo + j
             raw = read_raw(dataset.timestamps[i], dataset.widths[i], dataset.heights[i])
             if raw is None:
                 st.raw[j] = 0.0
-                return False
+                return 0
             st.raw[j] = raw
-            if not use_confidence_filtered_depth:
-                return False
+            # the reference loads the confidence map only for a valid depth map (o3d_utils.py:109-142)
+            if not use_confidence_filtered_depth or not DepthDataIO.is_depth_map_valid(raw):
+                return 0
             cm = depth_data_io.load_confidence_map(side=side, timestamp=dataset.timestamps[i])
             if cm is None:
-                print(f"[Warning] Confidence map not found for timestamp {dataset.timestamps[i]}")
-                return False
+                return -1
             st.conf[j] = cm.confidence_map
             st.vc[j] = cm.valid_count
-            return True
+            return 1
 
-        has = np.array(list(io_pool().map(one, range(hi - lo))), bool)
+        res = list(io_pool().map(one, range(hi - lo)))
+        for j, r in enumerate(res):  # in frame order, as the reference's loop prints them
+            if r < 0:
+                print(f"[Warning] Confidence map not found for timestamp {dataset.timestamps[lo + j]}")
+        return lo, hi, (st, np.array([r > 0 for r in res], bool))
+
+    def load_chunk_native(lo, st):
+        """load_chunk_staged through mqr_read_frames: native threads pread the raw files and the npz
+        members straight into `st`.  Frames the reader leaves to Python (a raw file of the wrong size, a
+        confidence npz it does not parse) go through the standard loaders here, in frame order, and the
+        confidence messages are printed only for frames whose depth map is valid -- the reference loads
+        the confidence map only after is_depth_map_valid passed (o3d_utils.py:109-142)."""
+        from . import _lib
+        from .dataio import DepthDataIO
+        hi = min(n, lo + CHUNK)
+        B = hi - lo
+        H, W = st.raw.shape[1:]
+        raw_path, conf_path = native
+        ts = [dataset.timestamps[i] for i in range(lo, hi)]
+        raws = (ctypes.c_char_p * B)(*[os.fsencode(str(raw_path(t))) for t in ts])
+        confs = (ctypes.c_char_p * B)(*[os.fsencode(str(conf_path(t))) for t in ts]) if use_confidence_filtered_depth else None
+        status = np.zeros(B, np.uint8)
+        _lib.call("mqr_read_frames", B, raws, confs, H, W, _lib.ptr(st.raw), _lib.ptr(st.conf) if confs else None,
+                  _lib.ptr(st.vc) if confs else None, _lib.ptr(status), io_threads())
+        has = np.zeros(B, bool)
+        for j in range(B):
+            s = int(status[j])
+            if s & _lib.MQR_FRAME_RAW_OTHER:
+                raw = read_raw(ts[j], dataset.widths[lo + j], dataset.heights[lo + j])  # raises as the reference
+                if raw is None:
+                    continue
+                st.raw[j] = raw
+                s |= _lib.MQR_FRAME_RAW_OK
+            if not (s & _lib.MQR_FRAME_RAW_OK) or not use_confidence_filtered_depth:
+                continue
+            if s & _lib.MQR_FRAME_CONF_OK:
+                has[j] = True
+                continue
+            if not DepthDataIO.is_depth_map_valid(st.raw[j]):
+                continue
+            cm = None if s & _lib.MQR_FRAME_CONF_MISSING else depth_data_io.load_confidence_map(side=side, timestamp=ts[j])
+            if cm is None:
+                print(f"[Warning] Confidence map not found for timestamp {ts[j]}")
+                continue
+            st.conf[j] = cm.confidence_map
+            st.vc[j] = cm.valid_count
+            has[j] = True
         return lo, hi, (st, has)
 
     stage = {}  # (H, W) -> DeviceBuffer of CHUNK decoded frames
@@ -239,7 +320,7 @@ def integrate(dataset, depth_data_io, side, use_confidence_filtered_depth: bool,
     def submit(pool, lo, turn):
         if read_raw is not None and uniform(lo):
             st = _host_stage(turn, min(CHUNK, n), int(dataset.heights[lo]), int(dataset.widths[lo]), use_confidence_filtered_depth)
-            return pool.submit(load_chunk_staged, lo, st)
+            return pool.submit(load_chunk_native if native is not None else load_chunk_staged, lo, st)
         return pool.submit(load_chunk, lo)
 
     bar = None
@@ -251,7 +332,10 @@ def integrate(dataset, depth_data_io, side, use_confidence_filtered_depth: bool,
         turn = 0
         fut = submit(pool, 0, turn) if n else None
         while fut is not None:
+            t0 = time.perf_counter()
             lo, hi, items = fut.result()
+            t1 = time.perf_counter()
+            times["wait_io"] += t1 - t0
             turn ^= 1
             fut = submit(pool, hi, turn) if hi < n else None
             if isinstance(items, tuple):
@@ -267,10 +351,13 @@ def integrate(dataset, depth_data_io, side, use_confidence_filtered_depth: bool,
                     run(np.array([i for i, _, _ in sel]), [f for _, f, _ in sel], [c for _, _, c in sel],
                         *sel[0][1].shape)
                     j = k
+            times["device"] += time.perf_counter() - t1
+            times["chunks"] += 1
             if bar is not None:
                 bar.update(hi - lo)
     if bar is not None:
         bar.close()
     for b in stage.values():
         b.free()
+    last_integrate_times.__dict__.update(times)
     return vbg

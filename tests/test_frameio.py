@@ -1,0 +1,86 @@
+"""mqr_read_frames (csrc/frameio.hip): the drop-in integrate's native reader of raw depth files and np.savez
+confidence npz (reference dataio/depth_data_io.py:33-53, 91-115).  Host-only, so it runs here without a
+GPU: every frame it reports read must equal np.fromfile / np.load of the same file, and every file it
+cannot take (missing, wrong size, compressed, another dtype or shape, truncated) must be reported, not
+guessed."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+
+def _lib():
+    from mqr import _lib
+    try:
+        _lib.load()
+    except Exception as e:  # pragma: no cover - the library is built by __graft_entry__.build()
+        pytest.skip(f"libmqr_hip.so not loadable here: {e}")
+    return _lib
+
+
+def _read(lib, raws, confs, H, W, threads):
+    n = len(raws)
+    raw = np.full((n, H, W), np.nan, np.float32)
+    conf = np.full((n, H, W), np.nan, np.float64)
+    vc = np.full((n, H, W), -7, np.int32)
+    st = np.zeros(n, np.uint8)
+    rp = (ctypes.c_char_p * n)(*[os.fsencode(str(p)) for p in raws])
+    cp = (ctypes.c_char_p * n)(*[None if p is None else os.fsencode(str(p)) for p in confs]) if confs else None
+    lib.call("mqr_read_frames", n, rp, cp, H, W, lib.ptr(raw), lib.ptr(conf) if cp else None,
+             lib.ptr(vc) if cp else None, lib.ptr(st), threads)
+    return raw, conf, vc, st
+
+
+@pytest.mark.parametrize("threads", [1, 4])
+def test_read_frames_matches_numpy_and_reports_the_rest(tmp_path, threads):
+    lib = _lib()
+    H, W = 24, 40
+    rng = np.random.default_rng(3)
+    raws, confs, expect = [], [], []
+    for i in range(12):
+        r = rng.random((H, W), dtype=np.float32)
+        c = rng.random((H, W))
+        v = rng.integers(0, 9, (H, W)).astype(np.int32)
+        rp, cp = tmp_path / f"{i}.raw", tmp_path / f"{i}.npz"
+        r.astype("<f4").tofile(rp)
+        np.savez(cp, confidence_map=c, valid_count=v)
+        raws.append(rp)
+        confs.append(cp)
+        expect.append((r, c, v))
+    os.unlink(raws[1])                                                   # raw missing
+    np.zeros(H * W + 3, "<f4").tofile(raws[2])                           # raw of the wrong size
+    os.unlink(confs[3])                                                  # confidence missing
+    np.savez_compressed(confs[4], confidence_map=expect[4][1], valid_count=expect[4][2])   # compressed
+    np.savez(confs[5], confidence_map=expect[5][1].astype(np.float32), valid_count=expect[5][2])  # dtype
+    np.savez(confs[6], confidence_map=expect[6][1][:, :-1].copy(), valid_count=expect[6][2])    # shape
+    with open(confs[7], "r+b") as f:                                     # truncated
+        f.truncate(os.path.getsize(confs[7]) // 2)
+    np.savez(confs[8], valid_count=expect[8][2])                         # member missing
+    np.savez(confs[9], confidence_map=np.asfortranarray(expect[9][1]), valid_count=expect[9][2])  # F order
+    confs[10] = None                                                     # no confidence asked for
+    raw, conf, vc, st = _read(lib, raws, confs, H, W, threads)
+    ok_raw, miss_raw, oth_raw = lib.MQR_FRAME_RAW_OK, lib.MQR_FRAME_RAW_MISSING, lib.MQR_FRAME_RAW_OTHER
+    ok_c, miss_c, oth_c = lib.MQR_FRAME_CONF_OK, lib.MQR_FRAME_CONF_MISSING, lib.MQR_FRAME_CONF_OTHER
+    want = {0: ok_raw | ok_c, 1: miss_raw | ok_c, 2: oth_raw | ok_c, 3: ok_raw | miss_c, 4: ok_raw | oth_c,
+            5: ok_raw | oth_c, 6: ok_raw | oth_c, 7: ok_raw | oth_c, 8: ok_raw | oth_c, 9: ok_raw | oth_c,
+            10: ok_raw, 11: ok_raw | ok_c}
+    assert {i: int(s) for i, s in enumerate(st)} == want
+    for i, (r, c, v) in enumerate(expect):
+        if st[i] & ok_raw:
+            assert np.array_equal(raw[i], np.fromfile(raws[i], "<f4").reshape(H, W))
+        else:
+            assert (raw[i] == 0).all()  # no frame: zeros (decoded invalid)
+        if st[i] & ok_c:
+            d = np.load(confs[i])
+            assert np.array_equal(conf[i], d["confidence_map"]) and np.array_equal(vc[i], d["valid_count"])
+
+
+def test_read_frames_without_confidence_and_empty(tmp_path):
+    lib = _lib()
+    H, W = 8, 8
+    p = tmp_path / "a.raw"
+    np.arange(64, dtype="<f4").tofile(p)
+    raw, _, _, st = _read(lib, [p], None, H, W, 2)
+    assert st[0] == lib.MQR_FRAME_RAW_OK and np.array_equal(raw[0].ravel(), np.arange(64, dtype=np.float32))
+    lib.call("mqr_read_frames", 0, None, None, H, W, None, None, None, None, 2)

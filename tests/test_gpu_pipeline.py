@@ -1,8 +1,9 @@
 """The drop-in boundary end to end: mqr.o3d_utils.integrate(dataset, depth_data_io, side, ...)
-(reference o3d_utils.py:153-238) on a capture written in the reference's layout, with device
-ingestion (raw files -> mqr_decode_depth -> batched touch/integrate), against the CPU oracle fed
-by the numpy decode path frame by frame.  Covers missing files, invalid buffers, confidence
-masking and a missing confidence map.  Bit-identical volumes."""
+(reference o3d_utils.py:153-238) on a capture written in the reference's layout, with native file
+reads (mqr_read_frames) and device ingestion (raw files -> mqr_decode_depth -> batched touch/integrate),
+against the CPU oracle fed by the numpy decode path frame by frame.  Covers missing files, invalid
+buffers, confidence masking, missing confidence maps (warned only for valid frames) and the Python
+readers (MQR_NATIVE_IO=0).  Bit-identical volumes."""
 import numpy as np
 import pytest
 
@@ -22,8 +23,8 @@ def _capture(tmp_path, n=14, seed=31):
     assert len(ds) == n
     rng = np.random.default_rng(seed)
     for i, ts in enumerate(ds.timestamps):
-        if i == 6:
-            continue  # no confidence map: warn, integrate unmasked
+        if i in (6, 9):
+            continue  # no confidence map: warn (6) and integrate unmasked; 9 is invalid, so no warning
         conf = rng.random((240, 320))
         vc = rng.integers(0, 8, (240, 320)).astype(np.int32)
         io.save_confidence_map(Side.LEFT, int(ts), ConfidenceMap(conf, vc))
@@ -33,21 +34,25 @@ def _capture(tmp_path, n=14, seed=31):
     return io, ds, Side
 
 
+@pytest.mark.parametrize("native_io", [True, False])
 @pytest.mark.parametrize("chunk", [4, 127])
 @pytest.mark.parametrize("use_conf", [False, True])
-def test_integrate_dropin_matches_oracle(tmp_path, use_conf, chunk, capsys, monkeypatch):
+def test_integrate_dropin_matches_oracle(tmp_path, use_conf, chunk, native_io, capsys, monkeypatch):
     """chunk 4: several hand-offs, so both alternating host staging sets are reused (and the missing
     file / invalid buffer / missing confidence map land in different chunks)."""
     from gpu_helpers import compare_volumes
     from mqr import o3d_utils
     from mqr.o3d_utils import _masked_depth, compute_o3d_intrinsic_matrices, integrate
     monkeypatch.setattr(o3d_utils, "CHUNK", chunk)
+    if not native_io:
+        monkeypatch.setenv("MQR_NATIVE_IO", "0")
     io, ds, Side = _capture(tmp_path)
     kw = dict(use_confidence_filtered_depth=use_conf, confidence_threshold=0.2, valid_count_threshold=2)
     vbg = integrate(ds, io, Side.LEFT, voxel_size=0.01, block_resolution=16, block_count=500, depth_max=4.0,
                     trunc_voxel_multiplier=10.0, device="CUDA:0", **kw)
     out = capsys.readouterr().out
-    assert ("[Warning] Confidence map not found" in out) == use_conf
+    # the reference reads a frame's confidence map only after its depth map passed is_depth_map_valid
+    assert out.count("[Warning] Confidence map not found") == (1 if use_conf else 0)
     ref = oracle.OracleVBG(0.01, 16, 256)
     K = compute_o3d_intrinsic_matrices(ds).astype(np.float64)
     T = ds.transforms.extrinsics_wc.astype(np.float64)

@@ -60,6 +60,7 @@ def main():
                 pstats.Stats(pr, stream=buf).sort_stats("tottime").print_stats(14)
                 print(f"== CHUNK {c}\n" + buf.getvalue(), file=sys.stderr)
         times = {c: [] for c in chunks}
+        splits = {}
         vols = {}
         for r in range(a.rounds + 1):
             for c in chunks:
@@ -69,6 +70,7 @@ def main():
                 dt = time.perf_counter() - t0
                 if r:
                     times[c].append(dt)
+                    splits.setdefault(c, []).append(dict(o3d_utils.last_integrate_times.__dict__))
                 if r == a.rounds:
                     k, t, w = vbg.export()
                     o = np.lexsort(k.T[::-1])
@@ -83,7 +85,7 @@ def main():
         same = k0.shape == k1.shape and (k0 == k1).all() and (w0 == w1).all() and (t0_.view(np.uint32) == t1.view(np.uint32)).all()
         med = float(np.median(times[c]))
         out["chunks"][c] = {"integrate_s": med, "integrate_frames_per_s": len(ds) / med, "all_s": times[c],
-                            "volume_identical_to_first": bool(same)}
+                            "volume_identical_to_first": bool(same), "splits_s": splits[c]}
     print(json.dumps(out), flush=True)
 
 
