@@ -368,9 +368,11 @@ def dropin_e2e_leg(seq, frames, device, fragment_workers=4):
         n = len(ds)
         cfg = DepthConfidenceEstimationConfig(target_frame_range=10, depth_max=4.0, error_threshold=0.08,
                                               skip_if_output_dir_exists=False, device=int(device.index or 0))
+        from mqr import confidence as _conf
         t0 = time.perf_counter()
         estimate_depth_confidences(io, cfg, sides=[Side.LEFT])
         t_conf = time.perf_counter() - t0
+        conf_split = dict(_conf.last_confidence_times.__dict__)
         # reconstruct_scene.py:27-53: confidences first (UNITY poses converted inside), then the
         # integrator gets the dataset with OPEN3D camera poses
         ds.transforms = ds.transforms.convert_coordinate_system(target_coordinate_system=CoordinateSystem.OPEN3D,
@@ -392,7 +394,7 @@ def dropin_e2e_leg(seq, frames, device, fragment_workers=4):
         frag = fragments_leg(io, ds, fragment_workers) if fragment_workers > 0 else None
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
-    return {"frames": n, "confidence_s": t_conf, "confidence_frames_per_s": n / t_conf, "integrate_s": t_int,
+    return {"frames": n, "confidence_s": t_conf, "confidence_split_s": conf_split, "confidence_frames_per_s": n / t_conf, "integrate_s": t_int,
             "integrate_runs_s": runs, "integrate_splits_s": splits, "integrate_frames_per_s": n / t_int, "frames_per_s": n / (t_conf + t_int), "blocks": blocks,
             "fragments": frag,
             "note": "on-disk capture (raw + descriptor CSV), estimate_depth_confidences (writes npz) then "

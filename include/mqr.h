@@ -221,6 +221,19 @@ int mqr_decode_depth(int device, const float* raw, int raw_loc, int N, int H, in
 int mqr_read_frames(int n, const char* const* raw_paths, const char* const* conf_paths, int H, int W,
                     float* raw_out, double* conf_out, int32_t* vc_out, uint8_t* status, int threads);
 
+/* The confidence maps' writer (SURVEY §8 C3 outputs): for n frames, np.savez(paths[f],
+ * confidence_map=conf[f], valid_count=valid[f]) as the reference saves them
+ * (scripts/dataio/depth_data_io.py:106-115) -- a zip of stored members confidence_map.npy (<f8 H x W) and
+ * valid_count.npy (<i4 H x W), .npy format 1.0 headers, zip64 local extra fields and CRC-32 like
+ * np.savez's -- written by `threads` native threads from the caller's arrays.  Host-only.
+ * paths[f] may be null (no file for that frame).  status[f]: 0, or the errno of the failed open / write
+ * (the caller reports that frame). */
+int mqr_write_confidence_npz(int n, const char* const* paths, const double* conf, const int32_t* valid, int H, int W,
+                             int32_t* status, int threads);
+/* CRC-32 (zip / zlib) of len bytes continuing from crc (0 to start): the writer's checksum, exported for
+ * its tests. */
+uint32_t mqr_crc32(uint32_t crc, const void* data, int64_t len);
+
 /* Kernel timing (HIP events on the volume's own stream).  enable=1 starts recording every
  * integrate-kernel launch; stats: launches, total kernel ms, union blocks, frame-blocks
  * (sum of per-frame touched blocks), frames, and the same for touch. */

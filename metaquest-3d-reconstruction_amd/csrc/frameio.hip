@@ -12,8 +12,11 @@
 // 0.28-0.53 s of waiting per 500-frame call against 0.05-0.08 s of device hand-off (bench
 // dropin_e2e.integrate_splits_s).
 #include <fcntl.h>
+#include <immintrin.h>
 #include <sys/stat.h>
+#include <sys/uio.h>
 #include <unistd.h>
+#include <zlib.h>
 
 #include <algorithm>
 #include <atomic>
@@ -165,9 +168,231 @@ bool read_npy(int fd, const Member& m, const char* descr, size_t item, int H, in
     return pread_all(fd, dst, bytes, m.data_off + hoff + hl);
 }
 
+// CRC-32 (zip / gzip polynomial, reflected) by carry-less multiplication: four 128-bit lanes folded
+// 64 bytes at a time, folded to 128 bits, then 64, then Barrett-reduced (Gopal et al., "Fast CRC
+// Computation for Generic Polynomials Using PCLMULQDQ Instruction", Intel 2009; constants x^k mod P for
+// the bit-reflected P = 0x104C11DB7).  len >= 64 and a multiple of 16; crc in and out pre-inverted.
+#define MQR_CLMUL __attribute__((target("pclmul,sse4.1"), always_inline)) inline
+MQR_CLMUL __m128i ld(const unsigned char* q) { return _mm_loadu_si128(reinterpret_cast<const __m128i*>(q)); }
+MQR_CLMUL __m128i fold(__m128i a, __m128i k, __m128i next) {
+    return _mm_xor_si128(_mm_xor_si128(_mm_clmulepi64_si128(a, k, 0x11), _mm_clmulepi64_si128(a, k, 0x00)), next);
+}
+
+__attribute__((target("pclmul,sse4.1"))) uint32_t crc32_fold(const unsigned char* p, size_t len, uint32_t crc) {
+    alignas(16) static const uint64_t k12[2] = {0x0154442bd4ull, 0x01c6e41596ull};
+    alignas(16) static const uint64_t k34[2] = {0x01751997d0ull, 0x00ccaa009eull};
+    alignas(16) static const uint64_t k50[2] = {0x0163cd6124ull, 0ull};
+    alignas(16) static const uint64_t pmu[2] = {0x01db710641ull, 0x01f7011641ull};
+    __m128i a0 = _mm_xor_si128(ld(p), _mm_cvtsi32_si128((int)crc)), a1 = ld(p + 16), a2 = ld(p + 32), a3 = ld(p + 48);
+    __m128i k = _mm_load_si128(reinterpret_cast<const __m128i*>(k12));
+    p += 64;
+    len -= 64;
+    for (; len >= 64; p += 64, len -= 64) {
+        a0 = fold(a0, k, ld(p));
+        a1 = fold(a1, k, ld(p + 16));
+        a2 = fold(a2, k, ld(p + 32));
+        a3 = fold(a3, k, ld(p + 48));
+    }
+    k = _mm_load_si128(reinterpret_cast<const __m128i*>(k34));
+    a0 = fold(a0, k, a1);
+    a0 = fold(a0, k, a2);
+    a0 = fold(a0, k, a3);
+    for (; len >= 16; p += 16, len -= 16) a0 = fold(a0, k, ld(p));
+    const __m128i lo32 = _mm_setr_epi32(-1, 0, -1, 0);
+    __m128i t = _mm_clmulepi64_si128(a0, k, 0x10);  // 128 -> 64 bits
+    a0 = _mm_xor_si128(_mm_srli_si128(a0, 8), t);
+    k = _mm_loadl_epi64(reinterpret_cast<const __m128i*>(k50));
+    t = _mm_srli_si128(a0, 4);
+    a0 = _mm_xor_si128(_mm_clmulepi64_si128(_mm_and_si128(a0, lo32), k, 0x00), t);
+    k = _mm_load_si128(reinterpret_cast<const __m128i*>(pmu));  // Barrett reduction to 32 bits
+    t = _mm_clmulepi64_si128(_mm_and_si128(a0, lo32), k, 0x10);
+    t = _mm_clmulepi64_si128(_mm_and_si128(t, lo32), k, 0x00);
+    return (uint32_t)_mm_extract_epi32(_mm_xor_si128(a0, t), 1);
+}
+
+uint32_t crc32_of(uint32_t crc, const void* data, size_t len) {
+    const unsigned char* p = static_cast<const unsigned char*>(data);
+    if (len >= 64 && __builtin_cpu_supports("pclmul") && __builtin_cpu_supports("sse4.1")) {
+        const size_t body = len & ~(size_t)15;
+        crc = ~crc32_fold(p, body, ~crc);
+        p += body;
+        len -= body;
+    }
+    while (len) {  // zlib for the tail (and without PCLMULQDQ)
+        const uInt n = (uInt)std::min<size_t>(len, 1u << 30);
+        crc = (uint32_t)crc32(crc, p, n);
+        p += n;
+        len -= n;
+    }
+    return crc;
+}
+
+bool pwrite_all(int fd, const void* src, size_t n, int64_t off) {
+    const char* p = static_cast<const char*>(src);
+    while (n) {
+        const ssize_t r = ::pwrite(fd, p, n, (off_t)off);
+        if (r < 0 && errno == EINTR) continue;
+        if (r <= 0) return false;
+        p += r;
+        n -= (size_t)r;
+        off += r;
+    }
+    return true;
+}
+
+void put16(std::string& s, uint16_t v) { s.push_back((char)(v & 0xFF)), s.push_back((char)(v >> 8)); }
+void put32(std::string& s, uint32_t v) { put16(s, (uint16_t)(v & 0xFFFF)), put16(s, (uint16_t)(v >> 16)); }
+void put64(std::string& s, uint64_t v) { put32(s, (uint32_t)(v & 0xFFFFFFFFu)), put32(s, (uint32_t)(v >> 32)); }
+
+// .npy format 1.0 header of a C-order H x W array, padded with spaces to a 64-byte multiple (numpy's
+// ARRAY_ALIGN) and ended by a newline
+std::string npy_header(const char* descr, int H, int W) {
+    std::string d = std::string("{'descr': '") + descr + "', 'fortran_order': False, 'shape': (" + std::to_string(H) +
+                    ", " + std::to_string(W) + "), }";
+    const size_t total = (10 + d.size() + 1 + 63) / 64 * 64;
+    d.append(total - 10 - d.size() - 1, ' ');
+    d.push_back('\n');
+    std::string h("\x93NUMPY\x01\x00", 8);
+    put16(h, (uint16_t)d.size());
+    return h + d;
+}
+
+// One np.savez-layout npz: stored members in the given order, each a local header with a zip64 extra
+// field (np.savez opens its members with force_zip64), then the central directory and end record.
+struct NpzMember {
+    const char* name;
+    std::string npy;  // .npy header
+    const void* data;
+    size_t bytes;
+};
+
+int write_npz(const char* path, NpzMember* m, int nm) {
+    int64_t off = 0;
+    std::vector<int64_t> lh_off(nm);
+    std::vector<uint32_t> crc(nm);
+    std::vector<std::string> lh(nm);
+    for (int i = 0; i < nm; ++i) {
+        crc[i] = crc32_of(crc32_of(0, m[i].npy.data(), m[i].npy.size()), m[i].data, m[i].bytes);
+        const uint64_t size = m[i].npy.size() + m[i].bytes;
+        std::string& h = lh[i];
+        put32(h, 0x04034b50u);
+        put16(h, 45);  // version needed: zip64
+        put16(h, 0);   // flags
+        put16(h, 0);   // stored
+        put16(h, 0);   // time
+        put16(h, (1 << 5) | 1);  // date 1980-01-01
+        put32(h, crc[i]);
+        put32(h, 0xFFFFFFFFu);
+        put32(h, 0xFFFFFFFFu);
+        put16(h, (uint16_t)strlen(m[i].name));
+        put16(h, 20);
+        h += m[i].name;
+        put16(h, 0x0001);
+        put16(h, 16);
+        put64(h, size);
+        put64(h, size);
+        lh_off[i] = off;
+        off += (int64_t)(h.size() + size);
+    }
+    std::string cd;
+    for (int i = 0; i < nm; ++i) {
+        const uint64_t size = m[i].npy.size() + m[i].bytes;
+        const bool big = size >= 0xFFFFFFFFull || (uint64_t)lh_off[i] >= 0xFFFFFFFFull;
+        put32(cd, 0x02014b50u);
+        put16(cd, 45);
+        put16(cd, 45);
+        put16(cd, 0);
+        put16(cd, 0);
+        put16(cd, 0);
+        put16(cd, (1 << 5) | 1);
+        put32(cd, crc[i]);
+        put32(cd, big ? 0xFFFFFFFFu : (uint32_t)size);
+        put32(cd, big ? 0xFFFFFFFFu : (uint32_t)size);
+        put16(cd, (uint16_t)strlen(m[i].name));
+        put16(cd, big ? 28 : 0);
+        put16(cd, 0);  // comment
+        put16(cd, 0);  // disk
+        put16(cd, 0);  // internal attributes
+        put32(cd, 0600u << 16);  // external attributes (unix mode, as zipfile writes them)
+        put32(cd, big ? 0xFFFFFFFFu : (uint32_t)lh_off[i]);
+        cd += m[i].name;
+        if (big) {
+            put16(cd, 0x0001);
+            put16(cd, 24);
+            put64(cd, size);
+            put64(cd, size);
+            put64(cd, (uint64_t)lh_off[i]);
+        }
+    }
+    const int64_t cd_off = off;
+    std::string end;
+    if (cd_off >= 0xFFFFFFFFll) {  // zip64 end record + locator
+        put32(end, 0x06064b50u);
+        put64(end, 44);
+        put16(end, 45);
+        put16(end, 45);
+        put32(end, 0);
+        put32(end, 0);
+        put64(end, (uint64_t)nm);
+        put64(end, (uint64_t)nm);
+        put64(end, cd.size());
+        put64(end, (uint64_t)cd_off);
+        put32(end, 0x07064b50u);
+        put32(end, 0);
+        put64(end, (uint64_t)(cd_off + (int64_t)cd.size()));
+        put32(end, 1);
+    }
+    put32(end, 0x06054b50u);
+    put16(end, 0);
+    put16(end, 0);
+    put16(end, (uint16_t)nm);
+    put16(end, (uint16_t)nm);
+    put32(end, (uint32_t)cd.size());
+    put32(end, cd_off >= 0xFFFFFFFFll ? 0xFFFFFFFFu : (uint32_t)cd_off);
+    put16(end, 0);
+    const int fd = ::open(path, O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+    if (fd < 0) return errno ? errno : EIO;
+    bool ok = true;
+    for (int i = 0; i < nm && ok; ++i) {
+        ok = pwrite_all(fd, lh[i].data(), lh[i].size(), lh_off[i]) &&
+             pwrite_all(fd, m[i].npy.data(), m[i].npy.size(), lh_off[i] + (int64_t)lh[i].size()) &&
+             pwrite_all(fd, m[i].data, m[i].bytes, lh_off[i] + (int64_t)(lh[i].size() + m[i].npy.size()));
+    }
+    ok = ok && pwrite_all(fd, cd.data(), cd.size(), cd_off) &&
+         pwrite_all(fd, end.data(), end.size(), cd_off + (int64_t)cd.size());
+    const int err = ok ? 0 : (errno ? errno : EIO);
+    if (::close(fd) != 0 && ok) return errno ? errno : EIO;
+    return err;
+}
+
 }  // namespace
 
 extern "C" {
+
+uint32_t mqr_crc32(uint32_t crc, const void* data, int64_t len) { return len > 0 ? crc32_of(crc, data, (size_t)len) : crc; }
+
+int mqr_write_confidence_npz(int n, const char* const* paths, const double* conf, const int32_t* valid, int H, int W,
+                             int32_t* status, int threads) {
+    MQR_REQUIRE(n >= 0 && H > 0 && W > 0, "bad sizes");
+    MQR_REQUIRE(n == 0 || (paths && conf && valid && status), "null argument");
+    const size_t HW = (size_t)H * (size_t)W;
+    const std::string h_conf = npy_header("<f8", H, W), h_valid = npy_header("<i4", H, W);
+    std::atomic<int> next{0};
+    auto work = [&] {
+        for (int f; (f = next.fetch_add(1)) < n;) {
+            NpzMember m[2] = {{"confidence_map.npy", h_conf, conf + (size_t)f * HW, 8 * HW},
+                              {"valid_count.npy", h_valid, valid + (size_t)f * HW, 4 * HW}};
+            status[f] = paths[f] ? write_npz(paths[f], m, 2) : 0;  // null path: no file for this frame
+        }
+    };
+    const int T = std::max(1, std::min({threads > 0 ? threads : 8, 64, std::max(n, 1)}));
+    std::vector<std::thread> th;
+    for (int t = 1; t < T; ++t) th.emplace_back(work);
+    work();
+    for (auto& x : th) x.join();
+    return 0;
+}
+
 
 int mqr_read_frames(int n, const char* const* raw_paths, const char* const* conf_paths, int H, int W, float* raw_out,
                     double* conf_out, int32_t* vc_out, uint8_t* status, int threads) {

@@ -89,6 +89,9 @@ SIGNATURES = {
     "mqr_confidence_stats": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _i64p]),
     "mqr_pixel_error_map": (ctypes.c_int, [ctypes.c_int, _f32p, _f32p, ctypes.c_int, ctypes.c_int, _f32p, _f32p,
                                            _f32p, _f32p, _f32p, ctypes.c_double, _f32p]),
+    "mqr_write_confidence_npz": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p), _vp, _vp, ctypes.c_int,
+                                                ctypes.c_int, _vp, ctypes.c_int]),
+    "mqr_crc32": (ctypes.c_uint32, [ctypes.c_uint32, _vp, ctypes.c_int64]),
     "mqr_read_frames": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_char_p),
                                        ctypes.c_int, ctypes.c_int, _vp, _vp, _vp, _vp, ctypes.c_int]),
     "mqr_decode_depth": (ctypes.c_int, [ctypes.c_int, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,

@@ -15,6 +15,9 @@ existing per-frame files are kept, a side whose directory exists is skipped when
 from __future__ import annotations
 
 import ctypes
+import os
+import threading
+import time
 from dataclasses import dataclass
 from typing import Optional
 
@@ -27,6 +30,10 @@ from .models import ConfidenceMap, CoordinateSystem, Side
 from .o3d_utils import compute_o3d_intrinsic_matrices
 
 REF_CHUNK = 64
+
+# wall-clock split (seconds) of the last estimate_depth_confidences call on this thread: the resume scan,
+# frame decoding (prefetch), the confidence calls (upload + kernel + download), waiting for npz writes
+last_confidence_times = threading.local()
 
 
 @dataclass
@@ -120,12 +127,153 @@ def _report(side, idx, timestamp, e):
     traceback.print_exception(type(e), e, e.__traceback__)
 
 
+# decoded frames of a side kept in HBM by the native path (bytes); larger captures take the windowed path
+RESIDENT_MAX_BYTES = 48 << 30
+_READ_CHUNK = 127
+
+
+def _native_paths(depth_data_io, side, dataset):
+    """(raw path fn, confidence path fn) when the side can run device-resident: frames read, decoded and
+    saved by the standard code (this package's DepthDataIO with those methods not overridden, or the
+    reference's DepthDataIO through its path config), one frame size, and the decoded frames within
+    RESIDENT_MAX_BYTES; else None."""
+    from .dataio import DepthDataIO
+    from .o3d_utils import _frame_paths
+    paths = _frame_paths(depth_data_io, side)
+    if paths is None:
+        return None
+    methods = ("load_depth_map", "load_depth_map_by_index", "save_confidence_map", "is_depth_map_valid")
+    if set(methods) & set(getattr(depth_data_io, "__dict__", {})):  # replaced on the instance
+        return None
+    if isinstance(depth_data_io, DepthDataIO):
+        cls = type(depth_data_io)
+        if any(getattr(cls, m) is not getattr(DepthDataIO, m) for m in methods):
+            return None
+    if len(dataset) == 0 or len(set(zip(np.asarray(dataset.widths).tolist(), np.asarray(dataset.heights).tolist()))) != 1:
+        return None
+    if 4 * len(dataset) * int(dataset.widths[0]) * int(dataset.heights[0]) > RESIDENT_MAX_BYTES:
+        return None
+    return paths
+
+
+def _estimate_side_native(depth_data_io, config, side, dataset, todo, K, T_cw, T_inv, paths, times) -> bool:
+    """One side, device-resident: the raw files read by native threads (mqr_read_frames), decoded on the
+    GPU once into an HBM array of all frames (mqr_decode_depth: the reference's is_depth_map_valid and
+    convert_depth_to_linear, bit for bit), the confidence kernel run on device windows of it, each run's
+    maps downloaded and written by native threads (mqr_write_confidence_npz: np.savez's files) while the
+    next run computes.  Returns False, before anything is written, when a raw file needs the Python
+    reader (wrong size, unreadable): the caller then takes the standard path for the side."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from ._io import io_threads
+    from ._lib import DeviceBuffer, MQR_DEVICE
+    from .ingest import decode_depth_frames
+    raw_path, conf_path = paths
+    n = len(dataset)
+    H, W = int(dataset.heights[0]), int(dataset.widths[0])
+    HW = H * W
+    dev = int(getattr(config, "device", 0))
+    r = int(config.target_frame_range)
+    ts = dataset.timestamps
+    t0 = time.perf_counter()
+    depth = DeviceBuffer(4 * n * HW, dev)
+    ok = np.zeros(n, bool)
+    stages = [np.empty((min(_READ_CHUNK, n), H, W), np.float32) for _ in range(2)]
+
+    def read(c0, st):
+        c1 = min(n, c0 + _READ_CHUNK)
+        status = np.zeros(c1 - c0, np.uint8)
+        names = (ctypes.c_char_p * (c1 - c0))(*[os.fsencode(str(raw_path(ts[i]))) for i in range(c0, c1)])
+        call("mqr_read_frames", c1 - c0, names, None, H, W, ptr(st), None, None, ptr(status), io_threads())
+        return c0, c1, st, status
+
+    with ThreadPoolExecutor(max_workers=1) as reader:
+        fut = reader.submit(read, 0, stages[0])
+        turn = 0
+        while fut is not None:
+            c0, c1, st, status = fut.result()
+            if (status & _lib.MQR_FRAME_RAW_OTHER).any():
+                depth.free()
+                return False
+            turn ^= 1
+            fut = reader.submit(read, c1, stages[turn]) if c1 < n else None
+            _, ok[c0:c1] = decode_depth_frames(st[:c1 - c0], [dataset.nears[i] for i in range(c0, c1)],
+                                               [dataset.fars[i] for i in range(c0, c1)], device=dev,
+                                               out_ptr=depth.ptr.value + 4 * c0 * HW)
+    times["decode"] += time.perf_counter() - t0
+    Kf = np.ascontiguousarray(K, dtype=np.float32).reshape(n, 9)
+    Tc = np.ascontiguousarray(T_cw, dtype=np.float32).reshape(n, 16)
+    Ti = np.ascontiguousarray(T_inv, dtype=np.float32).reshape(n, 16)
+    ok8 = ok.astype(np.uint8)
+    if todo:
+        conf_path(ts[todo[0]]).parent.mkdir(parents=True, exist_ok=True)
+
+    def write(a, names, conf, valid):
+        status = np.zeros(len(names), np.int32)
+        arr = (ctypes.c_char_p * len(names))(*names)
+        call("mqr_write_confidence_npz", len(names), arr, ptr(conf), ptr(valid), H, W, ptr(status), io_threads())
+        return a, status
+
+    pending = []
+
+    def settle(keep):
+        t_s = time.perf_counter()
+        while len(pending) > keep:
+            fw = pending.pop(0)
+            try:
+                a, status = fw.result()
+            except Exception as e:  # noqa: BLE001 -- the whole run's writes failed
+                a, status = None, e
+            if isinstance(status, Exception):
+                continue
+            for j in np.nonzero(status)[0]:
+                i = a + int(j)
+                e = OSError(int(status[j]), os.strerror(int(status[j])), str(conf_path(ts[i])))
+                _report(side, i, ts[i], e)
+        times["write_wait"] += time.perf_counter() - t_s
+
+    with ThreadPoolExecutor(max_workers=1) as writer:
+        for c0 in range(0, len(todo), REF_CHUNK):
+            chunk = [i for i in todo[c0:c0 + REF_CHUNK] if ok[i]]  # invalid refs: no output
+            j = 0
+            while j < len(chunk):  # runs spanning < REF_CHUNK indices, as the standard path groups them
+                k = j + 1
+                while k < len(chunk) and chunk[k] - chunk[j] < REF_CHUNK:
+                    k += 1
+                refs = chunk[j:k]
+                j = k
+                a, b = refs[0], refs[-1] + 1
+                lo, hi = max(0, a - r), min(n, b + r)
+                conf = np.empty((b - a, H, W), np.float64)
+                valid = np.empty((b - a, H, W), np.int32)
+                t_c = time.perf_counter()
+                try:
+                    call("mqr_confidence", dev, ctypes.c_void_p(depth.ptr.value + 4 * lo * HW), MQR_DEVICE, hi - lo,
+                         H, W, ptr(Kf[lo:hi], _lib._f32p), ptr(Tc[lo:hi], _lib._f32p), ptr(Ti[lo:hi], _lib._f32p),
+                         ptr(ok8[lo:hi], _lib._u8p), a - lo, b - lo, r, float(config.depth_max),
+                         float(config.error_threshold), ptr(conf), ptr(valid), MQR_HOST)
+                except Exception as e:  # noqa: BLE001 -- every reference frame of the run failed
+                    for i in refs:
+                        _report(side, i, ts[i], e)
+                    continue
+                finally:
+                    times["compute"] += time.perf_counter() - t_c
+                want = set(refs)
+                names = [os.fsencode(str(conf_path(ts[i]))) if i in want else None for i in range(a, b)]
+                pending.append(writer.submit(write, a, names, conf, valid))
+                settle(2)  # at most two runs' maps held for writing
+        settle(0)
+    depth.free()
+    return True
+
+
 def estimate_depth_confidences(depth_data_io, config: DepthConfidenceEstimationConfig, sides=None):
     """Per side: skip if the output directory exists (``skip_if_output_dir_exists``), keep existing
     per-frame files, compute the rest in chunks of REF_CHUNK reference frames.  Frames are decoded
     once each and held only while a chunk's window [first - r, last + r] needs them.  As in the
     reference (estimate_depth_confidences.py:98-117), an error while building or saving one
     reference frame's map is printed and that frame is skipped; the other frames go on."""
+    times = {"scan": 0.0, "decode": 0.0, "compute": 0.0, "write_wait": 0.0}
     for side in (sides or list(Side)):
         if config.skip_if_output_dir_exists and depth_data_io.exists_depth_confidence_map_dir(side=side):
             print(f"[{side.name}] Skipping confidence map estimation: output directory already exists. "
@@ -140,8 +288,14 @@ def estimate_depth_confidences(depth_data_io, config: DepthConfidenceEstimationC
                                                             is_camera=True).extrinsics_cw
         T_inv = np.linalg.inv(T_cw)
         r = int(config.target_frame_range)
+        t0 = time.perf_counter()
         todo = [i for i in range(n) if depth_data_io.load_confidence_map(side=side, timestamp=dataset.timestamps[i])
                 is None]
+        times["scan"] += time.perf_counter() - t0
+        native = _native_paths(depth_data_io, side, dataset) if todo else None
+        if native is not None and _estimate_side_native(depth_data_io, config, side, dataset, todo, K, T_cw, T_inv,
+                                                        native, times):
+            continue
         cache = {}  # index -> decoded frame (None: missing / invalid), frames of the current window only
         pool = io_pool()
         writes = []  # (frame index, npz write in flight on the I/O threads)
@@ -159,6 +313,7 @@ def estimate_depth_confidences(depth_data_io, config: DepthConfidenceEstimationC
 
         def settle(keep):  # wait for all but the last `keep` writes, reporting failures per frame
             nonlocal writes
+            t_s = time.perf_counter()
             cut = max(0, len(writes) - keep)
             for i, w in writes[:cut]:
                 try:
@@ -166,10 +321,13 @@ def estimate_depth_confidences(depth_data_io, config: DepthConfidenceEstimationC
                 except Exception as e:  # noqa: BLE001 -- the reference catches everything per frame
                     _report(side, i, dataset.timestamps[i], e)
             writes = writes[cut:]
+            times["write_wait"] += time.perf_counter() - t_s
 
         for c0 in range(0, len(todo), REF_CHUNK):
             part = todo[c0:c0 + REF_CHUNK]
+            t_p = time.perf_counter()
             prefetch(part[0] - r, part[-1] + r + 1)
+            times["decode"] += time.perf_counter() - t_p
             chunk = [i for i in part if frame(i) is not None]  # invalid refs: no output
             for i in [k for k in cache if chunk and k < chunk[0] - r]:
                 del cache[i]
@@ -184,6 +342,7 @@ def estimate_depth_confidences(depth_data_io, config: DepthConfidenceEstimationC
                 lo, hi = max(0, a - r), min(n, b + r)
                 win = [frame(i) for i in range(lo, hi)]
                 ok = np.array([f is not None for f in win])
+                t_c = time.perf_counter()
                 try:
                     conf, valid = confidence_maps(_canvas_stack(win), K[lo:hi], T_cw[lo:hi], T_inv[lo:hi], a - lo,
                                                   b - lo, r, config.depth_max, config.error_threshold, ok,
@@ -192,6 +351,8 @@ def estimate_depth_confidences(depth_data_io, config: DepthConfidenceEstimationC
                     for i in refs:
                         _report(side, i, dataset.timestamps[i], e)
                     continue
+                finally:
+                    times["compute"] += time.perf_counter() - t_c
                 for i in refs:
                     h, w = frame(i).shape
                     cm = ConfidenceMap(np.ascontiguousarray(conf[i - a, :h, :w]),
@@ -201,3 +362,4 @@ def estimate_depth_confidences(depth_data_io, config: DepthConfidenceEstimationC
                 if len(writes) > 2 * REF_CHUNK:  # bound the maps held for writing
                     settle(REF_CHUNK)
         settle(0)
+    last_confidence_times.__dict__.update(times)

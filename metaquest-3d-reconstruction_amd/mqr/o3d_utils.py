@@ -120,7 +120,8 @@ def _frame_paths(depth_data_io, side):
     from .dataio import DepthDataIO
     if isinstance(depth_data_io, DepthDataIO):
         cls = type(depth_data_io)
-        if cls.load_raw_depth is DepthDataIO.load_raw_depth and cls.load_confidence_map is DepthDataIO.load_confidence_map:
+        if (cls.load_raw_depth is DepthDataIO.load_raw_depth and cls.load_confidence_map is DepthDataIO.load_confidence_map
+                and not {"load_raw_depth", "load_confidence_map"} & set(vars(depth_data_io))):
             p = depth_data_io.paths
             return (lambda ts: p.depth_map_path(side, ts)), (lambda ts: p.confidence_path(side, ts))
         return None

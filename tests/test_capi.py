@@ -10,7 +10,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def _declared():
     src = open(os.path.join(ROOT, "include", "mqr.h")).read()
-    return sorted(set(re.findall(r"^\s*(?:const\s+char\s*\*|int)\s+(mqr_\w+)\s*\(", src, flags=re.M)))
+    return sorted(set(re.findall(r"^\s*(?:const\s+char\s*\*|int|uint32_t)\s+(mqr_\w+)\s*\(", src, flags=re.M)))
 
 
 def test_header_declares_the_boundary():

@@ -1,8 +1,9 @@
-"""mqr_read_frames (csrc/frameio.hip): the drop-in integrate's native reader of raw depth files and np.savez
-confidence npz (reference dataio/depth_data_io.py:33-53, 91-115).  Host-only, so it runs here without a
-GPU: every frame it reports read must equal np.fromfile / np.load of the same file, and every file it
+"""csrc/frameio.hip: mqr_read_frames, the native reader of raw depth files and np.savez confidence npz
+(reference dataio/depth_data_io.py:33-53, 91-104), and mqr_write_confidence_npz, the native np.savez of
+the confidence maps (depth_data_io.py:106-115) with its CRC-32.  Host-only, so they run here without a
+GPU: every frame the reader reports read must equal np.fromfile / np.load of the same file, every file it
 cannot take (missing, wrong size, compressed, another dtype or shape, truncated) must be reported, not
-guessed."""
+guessed; the writer's files must load with np.load and hold the members np.savez writes, byte for byte."""
 import ctypes
 import os
 
@@ -84,3 +85,56 @@ def test_read_frames_without_confidence_and_empty(tmp_path):
     raw, _, _, st = _read(lib, [p], None, H, W, 2)
     assert st[0] == lib.MQR_FRAME_RAW_OK and np.array_equal(raw[0].ravel(), np.arange(64, dtype=np.float32))
     lib.call("mqr_read_frames", 0, None, None, H, W, None, None, None, None, 2)
+
+
+def test_crc32_matches_zlib():
+    import zlib
+    lib = _lib()
+    rng = np.random.default_rng(5)
+    for n in list(range(0, 200)) + [1000, 4095, 65536 + 17, 3 << 20]:
+        b = rng.integers(0, 256, n, dtype=np.uint8)
+        for start in (0, 0x12345678):
+            got = lib.load().mqr_crc32(start, b.ctypes.data if n else None, n)
+            assert got == zlib.crc32(b.tobytes(), start), (n, start)
+
+
+@pytest.mark.parametrize("threads", [1, 3])
+def test_write_confidence_npz_roundtrip(tmp_path, threads):
+    """The native writer's files load with np.load (CRC-checked by zipfile), hold the arrays bit for bit,
+    pass zipfile's own test, and read back through mqr_read_frames; an unwritable path is reported."""
+    import zipfile
+    lib = _lib()
+    H, W, n = 30, 50, 5
+    rng = np.random.default_rng(7)
+    conf = rng.random((n, H, W))
+    conf[0, 0, 0] = np.nan
+    valid = rng.integers(-5, 30, (n, H, W)).astype(np.int32)
+    paths = [tmp_path / f"{i}.npz" for i in range(n)]
+    paths[3] = tmp_path / "no_such_dir" / "3.npz"
+    st = np.full(n, -1, np.int32)
+    pp = (ctypes.c_char_p * (n + 1))(*[os.fsencode(str(p)) for p in paths], None)  # null path: skipped
+    conf = np.concatenate([conf, conf[:1]])
+    valid = np.concatenate([valid, valid[:1]])
+    st = np.full(n + 1, -1, np.int32)
+    lib.call("mqr_write_confidence_npz", n + 1, pp, lib.ptr(conf), lib.ptr(valid), H, W, lib.ptr(st), threads)
+    assert st[3] != 0 and all(st[i] == 0 for i in range(n + 1) if i != 3)
+    assert sorted(p.name for p in tmp_path.iterdir()) == ["0.npz", "1.npz", "2.npz", "4.npz"]
+    for i in (0, 1, 2, 4):
+        with zipfile.ZipFile(paths[i]) as z:
+            assert z.testzip() is None and z.namelist() == ["confidence_map.npy", "valid_count.npy"]
+        d = np.load(paths[i])
+        assert d["confidence_map"].dtype == np.float64 and d["valid_count"].dtype == np.int32
+        assert np.array_equal(d["confidence_map"], conf[i], equal_nan=True)
+        assert np.array_equal(d["valid_count"], valid[i])
+        ref = tmp_path / f"ref{i}.npz"
+        np.savez(ref, confidence_map=conf[i], valid_count=valid[i])
+        with zipfile.ZipFile(ref) as a, zipfile.ZipFile(paths[i]) as b:  # same members, same bytes
+            for name in a.namelist():
+                assert a.read(name) == b.read(name)
+    ok = [0, 1, 2, 4]
+    raws = [tmp_path / f"r{i}.raw" for i in ok]
+    for r in raws:
+        np.zeros((H, W), "<f4").tofile(r)
+    _, c2, v2, st2 = _read(lib, raws, [paths[i] for i in ok], H, W, 2)
+    assert (st2 & lib.MQR_FRAME_CONF_OK).all()
+    assert np.array_equal(c2, conf[ok], equal_nan=True) and np.array_equal(v2, valid[ok])

@@ -6,7 +6,9 @@ vectors, tests/test_oracle_golden.py).
 Covers: the dir-level skip (``skip_if_output_dir_exists``), an existing per-frame file kept as is
 (resume rule :94-96), a frame missing / invalid after the dataset was cached (no output for it,
 skipped as a neighbour), reference-frame chunks that cross the 64-frame REF_CHUNK boundary and
-windows clipped at both ends of the sequence.
+windows clipped at both ends of the sequence -- on the device-resident path (native reads, frames
+decoded once into HBM, native npz writes) and on the standard one (MQR_NATIVE_IO=0), and a write
+failure on each, reported per frame with the reference's message.
 """
 import numpy as np
 import pytest
@@ -53,8 +55,11 @@ def _config(skip):
                                            skip_if_output_dir_exists=skip)
 
 
-def test_driver_outputs_match_oracle(capture):
+@pytest.mark.parametrize("native_io", [True, False])
+def test_driver_outputs_match_oracle(capture, native_io, monkeypatch):
     from mqr.confidence import REF_CHUNK, estimate_depth_confidences
+    if not native_io:
+        monkeypatch.setenv("MQR_NATIVE_IO", "0")
     from mqr.dataio import DepthDataIO
     from mqr.models import ConfidenceMap
     path, seq, io, ds, Side = capture
@@ -177,3 +182,18 @@ def test_driver_reports_a_failing_frame_and_goes_on(capture, capsys, monkeypatch
     conf_dir = path / "left_depth_confidence"
     assert len(list(conf_dir.glob("*.npz"))) == N - 1
     assert io.load_confidence_map(Side.LEFT, bad) is None
+
+
+def test_driver_native_write_failure_reported(capture, capsys):
+    """On the device-resident path a file that cannot be written (here a directory in its place) is
+    reported with the reference's message and errno, and every other frame is written."""
+    from mqr.confidence import estimate_depth_confidences
+    path, seq, io, ds, Side = capture
+    bad = int(ds.timestamps[9])
+    (path / "left_depth_confidence" / f"{bad}.npz").mkdir(parents=True)
+    estimate_depth_confidences(io, _config(skip=False), sides=[Side.LEFT])
+    out = capsys.readouterr().out
+    assert f"[Error] build_and_save_confidence_map failed for LEFT frame 9 (timestamp {bad}): [Errno 21]" in out
+    conf_dir = path / "left_depth_confidence"
+    assert len(list(conf_dir.glob("*.npz"))) == N  # N - 1 files and the directory named like the 10th
+    assert io.load_confidence_map(Side.LEFT, int(ds.timestamps[10])) is not None
