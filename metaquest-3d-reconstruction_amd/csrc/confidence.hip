@@ -833,7 +833,26 @@ struct ConfCache {
     bool branchy = false;               // enable = 4: the branchy float32 stages (A/B; 3 = the default)
     unsigned long long* dst = nullptr;  // device counters [4]
     int64_t last[4] = {0, 0, 0, 0};     // pairs, float32 prefilter, float64 filter, float64 back-projection
+    // grow-only device staging of host-array calls (uploaded depths; conf + valid before their download):
+    // a hipMalloc / hipFree pair of ~240 MB per 64-frame call cost more than the kernel
+    void* d_in = nullptr;
+    size_t d_in_cap = 0;
+    void* d_out = nullptr;
+    size_t d_out_cap = 0;
 };
+
+int grow(void** p, size_t* cap, size_t want) {
+    if (*cap >= want) return 0;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    if (hipMalloc(p, want) != hipSuccess) {
+        (void)hipGetLastError();
+        return 1;
+    }
+    *cap = want;
+    return 0;
+}
 ConfCache g_conf_cache[kConfDevices];
 }  // namespace
 
@@ -905,16 +924,17 @@ int mqr_confidence(int device, const float* depths, int depth_loc, int N, int H,
     MQR_CHECK_HIP(hipMemcpyAsync(dfr, fr, sizeof(ConfFrame) * N, hipMemcpyHostToDevice, s));
     const float* dsrc = depths;
     if (depth_loc != MQR_DEVICE) {
-        MQR_CHECK_HIP(hipMalloc(&dd, sizeof(float) * N * HW));
-        if (copy_to_device(device, dd, depths, sizeof(float) * N * HW, s)) {
-            (void)hipFree(dd);
-            return 1;
-        }
+        MQR_REQUIRE(grow(&cc.d_in, &cc.d_in_cap, sizeof(float) * N * HW) == 0, "mqr_confidence: device allocation failed");
+        dd = static_cast<float*>(cc.d_in);
+        if (copy_to_device(device, dd, depths, sizeof(float) * N * HW, s)) return 1;
         dsrc = dd;
     }
     if (out_loc != MQR_DEVICE) {
-        MQR_CHECK_HIP(hipMalloc(&dconf, sizeof(double) * nref * HW));
-        MQR_CHECK_HIP(hipMalloc(&dvalid, sizeof(int32_t) * nref * HW));
+        const size_t bc = (sizeof(double) * nref * HW + 255) & ~(size_t)255;
+        MQR_REQUIRE(grow(&cc.d_out, &cc.d_out_cap, bc + sizeof(int32_t) * nref * HW) == 0,
+                    "mqr_confidence: device allocation failed");
+        dconf = static_cast<double*>(cc.d_out);
+        dvalid = reinterpret_cast<int32_t*>(static_cast<char*>(cc.d_out) + bc);
     }
     const dim3 grid((unsigned)((HW + 255) / 256), nref);
     const bool wide = frame_range > 31;    // a window of more than 64 frames: chunked defer masks
@@ -959,11 +979,6 @@ int mqr_confidence(int device, const float* depths, int depth_loc, int N, int H,
         rc = copy_to_host(device, conf, dconf, sizeof(double) * nref * HW, s) ||
              copy_to_host(device, valid, dvalid, sizeof(int32_t) * nref * HW, s);
     if (!rc) MQR_CHECK_HIP(hipStreamSynchronize(s));
-    if (out_loc != MQR_DEVICE) {
-        (void)hipFree(dconf);
-        (void)hipFree(dvalid);
-    }
-    if (dd) (void)hipFree(dd);
     return rc;
 }
 

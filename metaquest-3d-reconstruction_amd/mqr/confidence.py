@@ -215,6 +215,10 @@ def _estimate_side_native(depth_data_io, config, side, dataset, todo, K, T_cw, T
         return a, status
 
     pending = []
+    # three host sets of maps: the run computing and the at most two runs being written (settle(2));
+    # reused, so their pages are faulted in once
+    outs = [(np.empty((REF_CHUNK, H, W), np.float64), np.empty((REF_CHUNK, H, W), np.int32)) for _ in range(3)]
+    runs = 0
 
     def settle(keep):
         t_s = time.perf_counter()
@@ -244,8 +248,8 @@ def _estimate_side_native(depth_data_io, config, side, dataset, todo, K, T_cw, T
                 j = k
                 a, b = refs[0], refs[-1] + 1
                 lo, hi = max(0, a - r), min(n, b + r)
-                conf = np.empty((b - a, H, W), np.float64)
-                valid = np.empty((b - a, H, W), np.int32)
+                conf, valid = (x[:b - a] for x in outs[runs % 3])
+                runs += 1
                 t_c = time.perf_counter()
                 try:
                     call("mqr_confidence", dev, ctypes.c_void_p(depth.ptr.value + 4 * lo * HW), MQR_DEVICE, hi - lo,
