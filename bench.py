@@ -544,6 +544,7 @@ def c5_leg(args, device, frames_per_side=2000, voxel=0.003, key_every=40, parity
         mesh = None  # release the previous result (a ~1 GB unmap) outside the timed call
         t0 = time.perf_counter()
         mesh = vbg.extract_triangle_mesh(weight_threshold=1.5)
+        _ = (mesh.vertices, mesh.vertex_normals, mesh.triangles)  # the host copies (the mesh is left in HBM)
         ext.append(time.perf_counter() - t0)
     vm1 = _vmstat()
     ext_phases = extract_phases(vbg, 1.5, 3)
@@ -594,6 +595,22 @@ def c5_leg(args, device, frames_per_side=2000, voxel=0.003, key_every=40, parity
     device_equal = bool(np.array_equal(d_t.cpu().numpy().reshape(cad.shape), cad) and
                         np.array_equal(d_col.cpu().numpy(), col) and np.array_equal(d_cnt.cpu().numpy(), cnt))
     del d_t, d_v, d_im, d_col, d_cnt
+    # the whole colour tail as the pipeline runs it (project_vertex_colors: BVH, colour-view casts, colours):
+    # on the mesh the extraction left in HBM, and on host arrays of the same mesh (every array over PCIe)
+    from mqr.color import project_vertex_colors
+    mesh_dev = vbg.extract_triangle_mesh(weight_threshold=1.5)
+    mesh_host = mesh_dev.cpu()
+    pipe = {"device_resident": [], "host_arrays": []}
+    for _ in range(2):
+        for name, m in (("device_resident", mesh_dev), ("host_arrays", mesh_host)):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            pc, pn = project_vertex_colors(m, imgs, K[key], T[key], device=dev)
+            pipe[name].append(time.perf_counter() - t0)
+            pipe_equal = bool(np.array_equal(pc, col) and np.array_equal(pn, cnt))
+            if not pipe_equal:
+                break
+    del mesh_dev, mesh_host
     seen = cnt > 0
     err = float(np.abs(col[seen] - synthetic.texture(mesh.vertices[seen])).mean()) if seen.any() else None
     err_fill = (float(np.abs(col[~seen] - synthetic.texture(mesh.vertices[~seen])).mean()) if (~seen).any()
@@ -606,7 +623,8 @@ def c5_leg(args, device, frames_per_side=2000, voxel=0.003, key_every=40, parity
            "extract_host_copy_bytes": mesh_bytes,
            "vertices": int(len(mesh.vertices)), "triangles": int(len(mesh.triangles)),
            "keyframes": len(key), "bvh_build_ms": bvh_s * 1e3, "colour_depth_cast_ms": cast_s * 1e3,
-           "colour_ms": col_s * 1e3, "colour_runs_ms": [x * 1e3 for x in col_runs], "colour_depth_cast_device_ms": cast_dev_s * 1e3,
+           "colour_ms": col_s * 1e3, "colour_runs_ms": [x * 1e3 for x in col_runs],
+           "colour_pipeline_ms": {k: min(v) * 1e3 for k, v in pipe.items()}, "colour_pipeline_equal": pipe_equal, "colour_depth_cast_device_ms": cast_dev_s * 1e3,
            "colour_device_ms": min(col_dev) * 1e3, "colour_device_path_equal": device_equal,
            "coloured_fraction": float(seen.mean()), "colour_mean_abs_err": err,
            "colour_mean_abs_err_knn_filled": err_fill,

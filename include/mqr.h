@@ -168,6 +168,12 @@ int mqr_geom_counts(mqr_geom* g, int64_t* n_vertices, int64_t* n_triangles);
 /* Copy to caller buffers (positions / normals n*3 float32, triangles n*3 int32); NULL skips. */
 int mqr_geom_copy(mqr_geom* g, float* positions, float* normals, int32_t* triangles, int loc);
 int mqr_geom_free(mqr_geom* g);
+/* The geometry's arrays in place (device pointers on its device, null when empty; valid until
+ * mqr_geom_free, and only after the call that produced it returned): positions / normals float32
+ * [nv][3], triangles int32 [nt][3].  Lets a caller keep the result in HBM, as Open3D's tensor geometry
+ * on a CUDA device stays there, and hand it to MQR_DEVICE inputs (mqr_scene_add_triangles,
+ * mqr_mesh_filter_components, mqr_color_map) without a host round trip. */
+int mqr_geom_device_ptrs(mqr_geom* g, void** positions, void** normals, void** triangles);
 
 /* build_confidence_map / compute_pixel_error_map
  * (confidence_estimation/estimate_depth_confidences.py:15-79, compute_pixel_error_map.py:120-220)

@@ -1814,6 +1814,14 @@ int mqr_geom_copy(mqr_geom* g, float* positions, float* normals, int32_t* triang
     return 0;
 }
 
+int mqr_geom_device_ptrs(mqr_geom* g, void** positions, void** normals, void** triangles) {
+    MQR_REQUIRE(g, "null geometry");
+    if (positions) *positions = g->nv ? g->pos : nullptr;
+    if (normals) *normals = g->nv ? g->nrm : nullptr;
+    if (triangles) *triangles = g->nt ? g->tri : nullptr;
+    return 0;
+}
+
 int mqr_geom_free(mqr_geom* g) {
     if (!g) return 0;
     (void)hipSetDevice(g->device);

@@ -81,6 +81,7 @@ SIGNATURES = {
     "mqr_xchg_finish": (ctypes.c_int, [_vp, _i64p]),
     "mqr_xchg_destroy": (ctypes.c_int, [_vp]),
     "mqr_geom_counts": (ctypes.c_int, [_vp, _i64p, _i64p]),
+    "mqr_geom_device_ptrs": (ctypes.c_int, [_vp, ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_vp)]),
     "mqr_geom_copy": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_int]),
     "mqr_geom_free": (ctypes.c_int, [_vp]),
     "mqr_confidence": (ctypes.c_int, [ctypes.c_int, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _f32p,

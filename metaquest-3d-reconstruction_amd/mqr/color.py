@@ -66,20 +66,37 @@ def color_map(vertices, images, t_hit, K, T_wc, max_depth=MAX_DEPTH, visibility_
               depth_trunc=DEPTH_TRUNC, knn=KNN, device=0):
     """run_rigid_optimizer's vertex colours with the poses as given.  t_hit (N,H,W) float32: the
     keyframes' raycast_in_color_view depth (inf on a miss).  Returns (colours (V,3) float32,
-    counts (V,) int32 = keyframes averaged; 0 where the colour comes from the knn fill)."""
-    V = np.ascontiguousarray(vertices, dtype=np.float32).reshape(-1, 3)
+    counts (V,) int32 = keyframes averaged; 0 where the colour comes from the knn fill).  Vertices and
+    t_hit already in HBM on `device` (a mesh from this package's extraction, a cast's t_hit Tensor) are
+    used in place."""
+    from .geometry import device_ptr
+    from ._lib import MQR_DEVICE, DeviceBuffer
     im = np.ascontiguousarray(images, dtype=np.uint8)
     if im.ndim != 4 or im.shape[3] != 3:
         raise ValueError(f"images must be (N,H,W,3) uint8, got {im.shape}")
     N, H, W = im.shape[:3]
-    d = np.ascontiguousarray(t_hit, dtype=np.float32).reshape(N, H, W)
+    dv = device_ptr(vertices, device) if getattr(vertices, "dtype", None) == np.float32 else None
+    if dv is not None and vertices.shape[-1:] == (3,):
+        nv, vptr, vloc = int(np.prod(vertices.shape[:-1])), ctypes.c_void_p(dv[0]), MQR_DEVICE
+    else:
+        V = np.ascontiguousarray(vertices, dtype=np.float32).reshape(-1, 3)
+        nv, vptr, vloc = len(V), ptr(V), MQR_HOST
+    dt = device_ptr(t_hit, device) if getattr(t_hit, "dtype", None) == np.float32 else None
+    keep = None
+    if dt is not None and int(np.prod(t_hit.shape)) == N * H * W:  # images go up beside the resident depths
+        keep = DeviceBuffer.from_array(im, int(device))
+        iptr, tptr, iloc = keep.ptr, ctypes.c_void_p(dt[0]), MQR_DEVICE
+    else:
+        d = np.ascontiguousarray(t_hit, dtype=np.float32).reshape(N, H, W)
+        iptr, tptr, iloc = ptr(im), ptr(d), MQR_HOST
     Kd = np.ascontiguousarray(K, dtype=np.float64).reshape(N, 9)
     Td = np.ascontiguousarray(T_wc, dtype=np.float64).reshape(N, 16)
-    out = np.empty((len(V), 3), np.float32)
-    cnt = np.empty(len(V), np.int32)
-    call("mqr_color_map", int(device), ptr(V), len(V), MQR_HOST, ptr(im), ptr(d), MQR_HOST, N, H, W,
+    out = np.empty((nv, 3), np.float32)
+    cnt = np.empty(nv, np.int32)
+    call("mqr_color_map", int(device), vptr, nv, vloc, iptr, tptr, iloc, N, H, W,
          ptr(Kd, _lib._f64p), ptr(Td, _lib._f64p), float(max_depth), float(visibility_threshold), int(margin),
          float(discontinuity_threshold), int(half_dilation), float(depth_trunc), int(knn), ptr(out), ptr(cnt), MQR_HOST)
+    del keep
     return out, cnt
 
 
@@ -87,14 +104,18 @@ def project_vertex_colors(mesh, images, K, T_wc, device=0, complete=True, **kw):
     """Ray-cast each keyframe's colour-aligned depth from `mesh` (raycast_in_color_view), then colour
     the vertices: color_map (complete=True) or the visibility-and-average primitive color_vertices.
     Returns (colours, counts)."""
-    from .raycasting import RaycastingScene, _mesh_arrays
-    v, t = _mesh_arrays(mesh)
+    from .raycasting import RaycastingScene, _device_mesh, _mesh_arrays
     im = np.asarray(images)
     N, H, W = im.shape[:3]
     scene = RaycastingScene(device=device)
-    scene.add_triangles(v, t)
+    if _device_mesh(mesh, None, device) is not None:  # the mesh stays in HBM from extraction to colours
+        v = mesh.vertex.positions
+        scene.add_triangles(mesh)
+    else:
+        v, t = _mesh_arrays(mesh)
+        scene.add_triangles(v, t)
     depth = scene.cast_pinhole(np.asarray(K, np.float64).reshape(N, 3, 3), np.asarray(T_wc, np.float64).reshape(N, 4, 4),
-                               W, H)["t_hit"].numpy()
+                               W, H)["t_hit"]
     if complete:
         return color_map(v, im, depth, K, T_wc, device=device, **kw)
-    return color_vertices(v, im, depth, K, T_wc, device=device, **kw)
+    return color_vertices(v, im, depth.numpy(), K, T_wc, device=device, **kw)

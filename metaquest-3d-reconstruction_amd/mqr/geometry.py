@@ -8,43 +8,138 @@ The reference consumes Open3D tensor geometry:
 These classes expose the same attribute paths over numpy arrays; ``to_legacy()`` returns a real
 Open3D legacy object when ``open3d`` is importable and otherwise returns ``self`` (which offers
 ``points`` / ``vertices`` / ``triangles`` / ``*_normals`` arrays and a binary PLY writer).
+
+Results of the device path (extraction, mesh filtering, ray casts) stay in HBM, as Open3D's tensor
+geometry on a CUDA device does: their Tensors hold a device array and copy it to the host once, on
+the first host access (``.numpy()``, indexing, ``.cpu()``, ``to_legacy()``, pickling).  Consumers of
+this package (``RaycastingScene.add_triangles``, ``filter_mesh_components``, ``color_map``) take the
+device arrays in place, so extract -> filter -> cast -> colour moves no mesh over PCIe.
 """
 from __future__ import annotations
+
+import ctypes
 
 import numpy as np
 
 
-class Tensor:
-    """Minimal host tensor facade (``.numpy()``, ``.shape``, ``.dtype``, indexing)."""
+class DeviceArray:
+    """A C-order array in HBM: device pointer, shape, numpy dtype, device index, and the object that owns
+    the memory (kept alive with the array)."""
 
-    def __init__(self, array: np.ndarray):
-        self._a = np.asarray(array)
+    def __init__(self, owner, ptr: int, shape, dtype, device_id: int):
+        self.owner = owner
+        self.ptr = int(ptr or 0)
+        self.shape = tuple(int(x) for x in shape)
+        self.dtype = np.dtype(dtype)
+        self.device_id = int(device_id)
+
+    @property
+    def nbytes(self) -> int:
+        return int(np.prod(self.shape, dtype=np.int64)) * self.dtype.itemsize
+
+    def host(self) -> np.ndarray:
+        from . import _lib
+        out = np.empty(self.shape, self.dtype)
+        if out.nbytes:
+            _lib.call("mqr_memcpy", ctypes.c_void_p(out.ctypes.data), _lib.MQR_HOST, ctypes.c_void_p(self.ptr),
+                      _lib.MQR_DEVICE, out.nbytes, self.device_id)
+        return out
+
+
+class Tensor:
+    """Minimal tensor facade (``.numpy()``, ``.shape``, ``.dtype``, indexing) over a host array or a
+    DeviceArray (copied to the host once, on first host access)."""
+
+    def __init__(self, array):
+        if isinstance(array, DeviceArray):
+            self._a, self._d = None, array
+        else:
+            self._a, self._d = np.asarray(array), None
 
     def numpy(self) -> np.ndarray:
+        if self._a is None:
+            self._a = self._d.host()
         return self._a
+
+    def device_array(self):
+        """The DeviceArray behind this tensor, or None for a host tensor."""
+        return self._d
+
+    @property
+    def is_cuda(self) -> bool:
+        return self._d is not None
 
     @property
     def shape(self):
-        return self._a.shape
+        return self._d.shape if self._a is None else self._a.shape
 
     @property
     def dtype(self):
-        return self._a.dtype
+        return self._d.dtype if self._a is None else self._a.dtype
 
     def __len__(self):
-        return len(self._a)
+        return self.shape[0]
 
     def __getitem__(self, i):
-        return self._a[i]
+        return self.numpy()[i]
 
     def __array__(self, dtype=None, copy=None):
-        return self._a if dtype is None else self._a.astype(dtype)
+        a = self.numpy()
+        return a if dtype is None else a.astype(dtype)
 
     def cpu(self):
-        return self
+        return self if self._d is None else Tensor(self.numpy())
+
+    def __getstate__(self):  # across processes: host arrays only
+        return {"_a": self.numpy(), "_d": None}
 
     def __repr__(self):
-        return f"mqr.Tensor(shape={self._a.shape}, dtype={self._a.dtype})"
+        where = "HBM" if self._d is not None else "host"
+        return f"mqr.Tensor(shape={self.shape}, dtype={self.dtype}, {where})"
+
+
+class DeviceGeom:
+    """Owner of one mqr_geom result (extraction / mesh filter): its arrays stay in HBM until the last
+    Tensor over them is gone.  ``tensors()`` -> (positions, normals, triangles) Tensors over them."""
+
+    def __init__(self, handle, device_id: int):
+        from . import _lib
+        self._h = handle
+        self.device_id = int(device_id)
+        nv, nt = ctypes.c_int64(), ctypes.c_int64()
+        _lib.call("mqr_geom_counts", handle, ctypes.byref(nv), ctypes.byref(nt))
+        self.nv, self.nt = int(nv.value), int(nt.value)
+        p, n, t = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+        _lib.call("mqr_geom_device_ptrs", handle, ctypes.byref(p), ctypes.byref(n), ctypes.byref(t))
+        self._ptrs = (p.value or 0, n.value or 0, t.value or 0)
+
+    def tensors(self):
+        p, n, t = self._ptrs
+        return (Tensor(DeviceArray(self, p, (self.nv, 3), np.float32, self.device_id)),
+                Tensor(DeviceArray(self, n, (self.nv, 3), np.float32, self.device_id)),
+                Tensor(DeviceArray(self, t, (self.nt, 3), np.int32, self.device_id)))
+
+    def __del__(self):
+        try:
+            from . import _lib
+            if self._h is not None and self._h.value and _lib._lib is not None:
+                _lib._lib.mqr_geom_free(self._h)
+            self._h = None
+        except Exception:
+            pass
+
+
+def device_ptr(x, device_id=None):
+    """(pointer, device index) of a tensor / array held in HBM (a device-backed Tensor or DeviceArray),
+    else None; with device_id given, None unless it lives on that device."""
+    d = x.device_array() if isinstance(x, Tensor) else x if isinstance(x, DeviceArray) else None
+    if d is None or (device_id is not None and d.device_id != int(device_id)):
+        return None
+    return d.ptr, d.device_id
+
+
+def _tensor(x):
+    return x if isinstance(x, Tensor) else Tensor(x)
 
 
 class Image:
@@ -157,9 +252,14 @@ def read_ply(path):
 
 
 class PointCloud:
-    def __init__(self, positions: np.ndarray, normals: np.ndarray, device=None):
-        self.point = _AttrMap(positions=Tensor(positions), normals=Tensor(normals))
+    def __init__(self, positions, normals, device=None):
+        self.point = _AttrMap(positions=_tensor(positions), normals=_tensor(normals))
         self.device = device
+
+    @classmethod
+    def from_device(cls, geom: DeviceGeom, device=None):
+        p, n, _ = geom.tensors()
+        return cls(p, n, device=device)
 
     @property
     def points(self):
@@ -170,7 +270,7 @@ class PointCloud:
         return self.point.normals.numpy()
 
     def cpu(self):
-        return self
+        return PointCloud(self.point.positions.cpu(), self.point.normals.cpu(), device="CPU:0")
 
     def to(self, device):
         self.device = device
@@ -190,10 +290,14 @@ class PointCloud:
 
 
 class TriangleMesh:
-    def __init__(self, vertices: np.ndarray, normals: np.ndarray, triangles: np.ndarray, device=None):
-        self.vertex = _AttrMap(positions=Tensor(vertices), normals=Tensor(normals))
-        self.triangle = _AttrMap(indices=Tensor(triangles))
+    def __init__(self, vertices, normals, triangles, device=None):
+        self.vertex = _AttrMap(positions=_tensor(vertices), normals=_tensor(normals))
+        self.triangle = _AttrMap(indices=_tensor(triangles))
         self.device = device
+
+    @classmethod
+    def from_device(cls, geom: DeviceGeom, device=None):
+        return cls(*geom.tensors(), device=device)
 
     @property
     def vertices(self):
@@ -208,7 +312,8 @@ class TriangleMesh:
         return self.triangle.indices.numpy()
 
     def cpu(self):
-        return self
+        return TriangleMesh(self.vertex.positions.cpu(), self.vertex.normals.cpu(), self.triangle.indices.cpu(),
+                            device="CPU:0")
 
     def to(self, device):
         self.device = device

@@ -11,7 +11,9 @@ depth (reconstruct_scene.py:197-201; o3d_utils.py:324-341; optimize_color_pose.p
 The BVH is built on the device (libmqr_hip.so, csrc/raycast.hip) at the first query after the
 geometry changed.  ``cast_pinhole`` is the fused path (rays generated on the device, identical
 to create_rays_pinhole + cast_rays).  t_hit is inf where a ray hits nothing; ids are
-0xFFFFFFFF (``INVALID_ID``) there.
+0xFFFFFFFF (``INVALID_ID``) there.  A mesh already in HBM (this package's extraction or mesh filter)
+is added in place, and the cast results stay in HBM as Open3D's do on a CUDA device (copied to the
+host on the first ``.numpy()``), so ``color_map`` can take them without a round trip.
 """
 from __future__ import annotations
 
@@ -22,7 +24,7 @@ import numpy as np
 
 from . import _lib
 from ._lib import MQR_HOST, call, ptr
-from .geometry import Tensor
+from .geometry import DeviceArray, Tensor, device_ptr
 
 INVALID_ID = 0xFFFFFFFF
 
@@ -38,6 +40,22 @@ def _mesh_arrays(mesh_or_vertices, triangles=None):
     t = t.numpy() if hasattr(t, "numpy") else np.asarray(t)
     return (np.ascontiguousarray(v, dtype=np.float32).reshape(-1, 3),
             np.ascontiguousarray(t, dtype=np.int32).reshape(-1, 3))
+
+
+def _device_mesh(mesh_or_vertices, triangles, device_id):
+    """((vertex ptr, nv), (triangle ptr, nt)) when positions (float32 (n,3)) and indices (int32 (m,3)) are
+    Tensors in HBM on `device_id`, else None."""
+    if triangles is not None:
+        v, t = mesh_or_vertices, triangles
+    elif hasattr(mesh_or_vertices, "vertex") and hasattr(mesh_or_vertices, "triangle"):
+        v, t = mesh_or_vertices.vertex.positions, mesh_or_vertices.triangle.indices
+    else:
+        return None
+    pv, pt = device_ptr(v, device_id), device_ptr(t, device_id)
+    if pv is None or pt is None or v.dtype != np.float32 or t.dtype != np.int32 or v.shape[-1:] != (3,) \
+            or t.shape[-1:] != (3,):
+        return None
+    return (pv[0], int(np.prod(v.shape[:-1]))), (pt[0], int(np.prod(t.shape[:-1])))
 
 
 def _pinhole_params(K, T):
@@ -77,8 +95,15 @@ class RaycastingScene:
             pass
 
     def add_triangles(self, vertex_positions, triangle_indices=None) -> int:
-        v, t = _mesh_arrays(vertex_positions, triangle_indices)
         gid = ctypes.c_uint32()
+        dev = _device_mesh(vertex_positions, triangle_indices, self.device_id)
+        if dev is not None:  # the mesh is in HBM on this scene's device: no host round trip
+            (pv, nv), (pt, nt) = dev
+            call("mqr_scene_add_triangles", self._h, ctypes.c_void_p(pv), nv, ctypes.c_void_p(pt), nt, _lib.MQR_DEVICE,
+                 ctypes.byref(gid))
+            self._ngeom += 1
+            return int(gid.value)
+        v, t = _mesh_arrays(vertex_positions, triangle_indices)
         call("mqr_scene_add_triangles", self._h, ptr(v), v.shape[0], ptr(t), t.shape[0], MQR_HOST,
              ctypes.byref(gid))
         self._ngeom += 1
@@ -105,30 +130,34 @@ class RaycastingScene:
         return Tensor(rays)
 
     def _outputs(self, n, full):
-        t = np.empty(n, np.float32)
-        if not full:
-            return t, None, None, None, None
-        return (t, np.empty(n, np.uint32), np.empty(n, np.uint32), np.empty((n, 2), np.float32),
-                np.empty((n, 3), np.float32))
+        """Device buffers for the cast's results: (t_hit, geometry ids, primitive ids, uvs, normals)."""
+        from ._lib import DeviceBuffer
+        specs = [(np.float32, ())] + ([(np.uint32, ()), (np.uint32, ()), (np.float32, (2,)), (np.float32, (3,))]
+                                      if full else [])
+        out = [(DeviceBuffer(max(4, n * np.dtype(dt).itemsize * int(np.prod(k, dtype=np.int64))), self.device_id),
+                dt, k) for dt, k in specs]
+        return out + [None] * (5 - len(out))
 
     @staticmethod
-    def _p(a):
-        return None if a is None else ptr(a)
+    def _p(o):
+        return None if o is None else o[0].ptr
+
+    def _tensors(self, outs, shape, full):
+        """The results as Tensors over their device buffers (host copies on first access)."""
+        names = ["t_hit"] + (["geometry_ids", "primitive_ids", "primitive_uvs", "primitive_normals"] if full else [])
+        return {nm: Tensor(DeviceArray(buf, buf.ptr.value, shape + k, dt, self.device_id))
+                for nm, (buf, dt, k) in zip(names, outs)}
 
     def cast_rays(self, rays, nthreads: int = 0, full: bool = True) -> dict:
         r = rays.numpy() if hasattr(rays, "numpy") else np.asarray(rays)
         shape = r.shape[:-1]
         r = np.ascontiguousarray(r, dtype=np.float32).reshape(-1, 6)
         n = r.shape[0]
-        t, g, p, uv, nr = self._outputs(n, full)
-        call("mqr_scene_cast_rays", self._h, ptr(r), n, MQR_HOST, ptr(t), self._p(g), self._p(p), self._p(uv),
-             self._p(nr), MQR_HOST)
-        out = {"t_hit": Tensor(t.reshape(shape))}
-        if full:
-            out.update(geometry_ids=Tensor(g.reshape(shape)), primitive_ids=Tensor(p.reshape(shape)),
-                       primitive_uvs=Tensor(uv.reshape(shape + (2,))),
-                       primitive_normals=Tensor(nr.reshape(shape + (3,))))
-        return out
+        outs = self._outputs(n, full)
+        t, g, p, uv, nr = outs
+        call("mqr_scene_cast_rays", self._h, ptr(r), n, MQR_HOST, self._p(t), self._p(g), self._p(p), self._p(uv),
+             self._p(nr), _lib.MQR_DEVICE)
+        return self._tensors([o for o in outs if o is not None], tuple(shape), full)
 
     def cast_pinhole(self, intrinsics, extrinsics, width_px: int, height_px: int, full: bool = False) -> dict:
         """Fused create_rays_pinhole + cast_rays for one camera (K (3,3), T_wc (4,4)) or a stack
@@ -140,16 +169,12 @@ class RaycastingScene:
         T = T.reshape(-1, 4, 4)
         nf = K.shape[0]
         n = nf * height_px * width_px
-        t, g, p, uv, nr = self._outputs(n, full)
+        outs = self._outputs(n, full)
+        t, g, p, uv, nr = outs
         call("mqr_scene_cast_pinhole", self._h, ptr(K, _lib._f64p), ptr(T, _lib._f64p), nf, int(height_px),
-             int(width_px), ptr(t), self._p(g), self._p(p), self._p(uv), self._p(nr), MQR_HOST)
+             int(width_px), self._p(t), self._p(g), self._p(p), self._p(uv), self._p(nr), _lib.MQR_DEVICE)
         shape = (height_px, width_px) if single else (nf, height_px, width_px)
-        out = {"t_hit": Tensor(t.reshape(shape))}
-        if full:
-            out.update(geometry_ids=Tensor(g.reshape(shape)), primitive_ids=Tensor(p.reshape(shape)),
-                       primitive_uvs=Tensor(uv.reshape(shape + (2,))),
-                       primitive_normals=Tensor(nr.reshape(shape + (3,))))
-        return out
+        return self._tensors([o for o in outs if o is not None], shape, full)
 
 
 def raycast_in_color_view(scene: RaycastingScene, dataset, batch: int = 16):

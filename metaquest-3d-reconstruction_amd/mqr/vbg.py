@@ -189,6 +189,8 @@ class VoxelBlockGrid:
 
     # -- extraction --------------------------------------------------------------------------------
     def _geom(self, fn, thr):
+        """The extraction's result, left in HBM (DeviceGeom): host arrays are copied on first access."""
+        from .geometry import DeviceGeom
         g = ctypes.c_void_p()
         try:
             call(fn, self._h, float(thr), ctypes.byref(g))
@@ -197,23 +199,19 @@ class VoxelBlockGrid:
                 _lib._lib.mqr_geom_free(g)
             raise
         try:
-            nv, nt = ctypes.c_int64(), ctypes.c_int64()
-            call("mqr_geom_counts", g, ctypes.byref(nv), ctypes.byref(nt))
-            pos = np.empty((nv.value, 3), np.float32)
-            nrm = np.empty((nv.value, 3), np.float32)
-            tri = np.empty((nt.value, 3), np.int32)
-            call("mqr_geom_copy", g, ptr(pos), ptr(nrm), ptr(tri) if nt.value else None, MQR_HOST)
-        finally:
-            call("mqr_geom_free", g)
-        return pos, nrm, tri
+            return DeviceGeom(g, self.device_id)
+        except Exception:
+            _lib._lib.mqr_geom_free(g)
+            raise
 
     def extract_point_cloud(self, weight_threshold=3.0, estimated_point_number=-1):
-        pos, nrm, _ = self._geom("mqr_extract_points", weight_threshold)
-        return PointCloud(pos, nrm, device=self.device)
+        """Open3D returns the cloud on the volume's device; so does this (positions / normals in HBM,
+        copied to the host on first host access)."""
+        return PointCloud.from_device(self._geom("mqr_extract_points", weight_threshold), device=self.device)
 
     def extract_triangle_mesh(self, weight_threshold=3.0, estimated_vertex_number=-1):
-        pos, nrm, tri = self._geom("mqr_extract_mesh", weight_threshold)
-        return TriangleMesh(pos, nrm, tri, device=self.device)
+        """The mesh on the volume's device, as Open3D returns it (arrays in HBM until a host access)."""
+        return TriangleMesh.from_device(self._geom("mqr_extract_mesh", weight_threshold), device=self.device)
 
     # -- contents ----------------------------------------------------------------------------------
     def export(self):
