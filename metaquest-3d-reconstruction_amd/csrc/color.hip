@@ -265,18 +265,21 @@ __global__ void k_cm_morton(const float* __restrict__ V, const int32_t* __restri
     keys[i] = spread21(c[0]) | spread21(c[1]) << 1 | spread21(c[2]) << 2;
 }
 
-// leaf boxes (bucket b = sorted points [kBucket b, kBucket (b + 1)) ); empty leaves get an inverted box
+// leaf boxes (bucket b = sorted points [kBucket b, kBucket (b + 1)) ); empty leaves get an inverted box.
+// Also the points themselves in that order, packed (x, y, z, vertex index bits), for the leaf scans.
 __global__ void k_cm_leaf_boxes(const float* __restrict__ V, const int32_t* __restrict__ sorted, int64_t n, int64_t P,
-                                float4* __restrict__ lo, float4* __restrict__ hi) {
+                                float4* __restrict__ lo, float4* __restrict__ hi, float4* __restrict__ pts) {
     const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= P) return;
     float l[3] = {INFINITY, INFINITY, INFINITY}, h[3] = {-INFINITY, -INFINITY, -INFINITY};
     for (int64_t j = b * kBucket; j < min(n, (b + 1) * kBucket); ++j) {
         const int32_t v = sorted[j];
+        const float p[3] = {V[3 * (int64_t)v], V[3 * (int64_t)v + 1], V[3 * (int64_t)v + 2]};
+        pts[j] = make_float4(p[0], p[1], p[2], __int_as_float(v));
 #pragma unroll
         for (int a = 0; a < 3; ++a) {
-            l[a] = fminf(l[a], V[3 * (int64_t)v + a]);
-            h[a] = fmaxf(h[a], V[3 * (int64_t)v + a]);
+            l[a] = fminf(l[a], p[a]);
+            h[a] = fmaxf(h[a], p[a]);
         }
     }
     lo[P + b] = make_float4(l[0], l[1], l[2], 0.f);
@@ -291,37 +294,46 @@ __global__ void k_cm_level(int64_t first, int64_t count, float4* __restrict__ lo
     hi[n] = make_float4(fmaxf(hi[a].x, hi[b].x), fmaxf(hi[a].y, hi[b].y), fmaxf(hi[a].z, hi[b].z), 0.f);
 }
 
-__device__ inline double box_d2(const double q[3], float4 lo, float4 hi) {
-    const double l[3] = {lo.x, lo.y, lo.z}, h[3] = {hi.x, hi.y, hi.z};
-    double s = 0.0;
+// A lower bound of the squared distance from q to a box, in float32: every operation is correctly rounded
+// (relative error <= 2^-24 each, <= 2^-21 for the whole sum of three squares of differences), so shrinking
+// by 2^-18 leaves a bound below the exact value; underflow only lowers it.  Pruning on it skips no box the
+// exact float64 test would keep, and the visiting order cannot change the result (the list is a total
+// order on (d2, index)).
+__device__ inline float box_d2_lb(const float q[3], float4 lo, float4 hi) {
+    const float l[3] = {lo.x, lo.y, lo.z}, h[3] = {hi.x, hi.y, hi.z};
+    float s = 0.f;
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
-        const double t = fmax(fmax(l[a] - q[a], q[a] - h[a]), 0.0);
+        const float t = fmaxf(fmaxf(l[a] - q[a], q[a] - h[a]), 0.f);
         s += t * t;
     }
-    return s;
+    return s * (1.0f - 0x1p-18f);
 }
 
 // The knn (3) nearest sampled vertices of every unseen vertex (exact: float64 squared distances of the
 // float32 positions, ties by vertex index, the oracle's k-d tree rule), then the mean of their colours.
 // K = knn at compile time: the running best list lives in registers (static indices, an unrolled
-// insertion), and the traversal stack in LDS (stack-major: lane t's entry sp at stk[sp][t], conflict-free);
-// the round-4 form kept a 64 x int64 stack and a KMAX = 8 list with dynamic indices in scratch (64 ms for
-// C5's 17.5 M unseen vertices, profiles/r05_c5_kernel_stats.csv).  A nearest-first DFS holds at most one
-// pending sibling per level plus the current pair: depth + 1 <= 29 entries for P <= 2^27 buckets.
-constexpr int kKnnStack = 32;
+// insertion), and the traversal stack in LDS (stack-major: lane t's entry sp at stk[sp * 256 + t],
+// conflict-free), sized by the host to the tree's depth + 2 (a nearest-first DFS holds at most one pending
+// sibling per level plus the current pair): 20 entries for C5's 2^18 buckets instead of a fixed 32, so
+// more workgroups fit a CU's LDS.  Boxes are pruned and ordered in float32 on a proven lower bound
+// (box_d2_lb); candidates are compared exactly in float64.  The round-4 form kept a 64 x int64 stack and a
+// KMAX = 8 list with dynamic indices in scratch (64 ms for C5's 17.5 M unseen vertices), the first
+// round-5 form float64 box tests and a 32-entry stack (44.5 ms, profiles/r05_c5_kernel_stats.csv).
 template <int K>
 __global__ __launch_bounds__(256) void k_cm_knn_fill(const float* __restrict__ V, const int32_t* __restrict__ qids,
-                                                     int64_t nq, const int32_t* __restrict__ sorted, int64_t n,
+                                                     int64_t nq, const float4* __restrict__ pts, int64_t n,
                                                      int64_t P, const float4* __restrict__ lo,
                                                      const float4* __restrict__ hi, const double* __restrict__ avg,
                                                      float* __restrict__ out) {
-    __shared__ int32_t stk[kKnnStack][256];
+    extern __shared__ int32_t stk_lds[];
+    int32_t* stk = stk_lds + threadIdx.x;  // entry e of this lane at stk[256 e]
     const int lane = threadIdx.x;
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + lane;
     if (t >= nq) return;
     const int32_t qv = qids[t];
-    const double q[3] = {V[3 * (int64_t)qv], V[3 * (int64_t)qv + 1], V[3 * (int64_t)qv + 2]};
+    const float qf[3] = {V[3 * (int64_t)qv], V[3 * (int64_t)qv + 1], V[3 * (int64_t)qv + 2]};
+    const double q[3] = {qf[0], qf[1], qf[2]};
     double bd[K];
     int32_t bi[K];
 #pragma unroll
@@ -329,17 +341,22 @@ __global__ __launch_bounds__(256) void k_cm_knn_fill(const float* __restrict__ V
         bd[k] = __builtin_inf();  // an empty slot sorts after every real candidate
         bi[k] = 0x7fffffff;
     }
+    (void)lane;
     int sp = 0;
-    stk[sp++][lane] = 1;
+    stk[256 * sp++] = 1;
     while (sp) {
-        const int32_t node = stk[--sp][lane];
-        if (box_d2(q, lo[node], hi[node]) > bd[K - 1]) continue;  // (never while the list has room: inf)
+        const int32_t node = stk[256 * --sp];
+        if ((double)box_d2_lb(qf, lo[node], hi[node]) > bd[K - 1]) continue;  // (never while the list has room)
         if (node >= P) {  // bucket
             const int64_t b = node - P;
             for (int64_t j = b * kBucket; j < min(n, (b + 1) * kBucket); ++j) {
-                const int32_t v = sorted[j];
-                const double dx = q[0] - (double)V[3 * (int64_t)v], dy = q[1] - (double)V[3 * (int64_t)v + 1];
-                const double dz = q[2] - (double)V[3 * (int64_t)v + 2];
+                const float4 pt = pts[j];
+                // float32 lower bound first (box_d2_lb's argument): most points of a visited bucket cannot
+                // enter the list, and those skip the float64 distance
+                const float fx = qf[0] - pt.x, fy = qf[1] - pt.y, fz = qf[2] - pt.z;
+                if ((double)((fx * fx + fy * fy + fz * fz) * (1.0f - 0x1p-18f)) > bd[K - 1]) continue;
+                const int32_t v = __float_as_int(pt.w);
+                const double dx = q[0] - (double)pt.x, dy = q[1] - (double)pt.y, dz = q[2] - (double)pt.z;
                 const double d2 = dx * dx + dy * dy + dz * dz;
                 auto before = [&](int k) { return d2 < bd[k] || (d2 == bd[k] && v < bi[k]); };  // new precedes k
                 if (!before(K - 1)) continue;
@@ -359,9 +376,9 @@ __global__ __launch_bounds__(256) void k_cm_knn_fill(const float* __restrict__ V
             }
         } else {  // nearer child popped first
             const int32_t a = 2 * node, c = a + 1;
-            const double da = box_d2(q, lo[a], hi[a]), dc = box_d2(q, lo[c], hi[c]);
-            stk[sp++][lane] = da <= dc ? c : a;
-            stk[sp++][lane] = da <= dc ? a : c;
+            const float da = box_d2_lb(qf, lo[a], hi[a]), dc = box_d2_lb(qf, lo[c], hi[c]);
+            stk[256 * sp++] = da <= dc ? c : a;
+            stk[256 * sp++] = da <= dc ? a : c;
         }
     }
     int nb = 0;
@@ -571,8 +588,9 @@ int mqr_color_map(int device, const float* vertices, int64_t nv, int vloc, const
             int32_t* sorted = static_cast<int32_t*>(alloc(sizeof(int32_t) * nseen));
             float4* blo = static_cast<float4*>(alloc(sizeof(float4) * 2 * P));
             float4* bhi = static_cast<float4*>(alloc(sizeof(float4) * 2 * P));
+            float4* pts = static_cast<float4*>(alloc(sizeof(float4) * nseen));
             size_t tbs = 0;
-            if (!bb || !keys || !sorted || !blo || !bhi ||
+            if (!bb || !keys || !sorted || !blo || !bhi || !pts ||
                 hipcub::DeviceRadixSort::SortPairs(nullptr, tbs, keys, keys + nseen, ids, sorted, (int)nseen, 0, 63, s) !=
                     hipSuccess)
                 fail("mqr_color_map: knn allocation failed");
@@ -588,13 +606,16 @@ int mqr_color_map(int device, const float* vertices, int64_t nv, int vloc, const
                     hipSuccess)
                     fail("mqr_color_map: sort failed");
                 hipLaunchKernelGGL(k_cm_leaf_boxes, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, dV, sorted, nseen,
-                                   P, blo, bhi);
+                                   P, blo, bhi, pts);
                 for (int64_t first = P / 2; first >= 1; first /= 2)
                     hipLaunchKernelGGL(k_cm_level, dim3((unsigned)((first + 255) / 256)), dim3(256), 0, s, first, first,
                                        blo, bhi);
                 const dim3 gq((unsigned)((nunseen + 255) / 256));
+                int depth = 0;  // levels below the root of the P-leaf tree
+                while ((int64_t{1} << depth) < P) ++depth;
+                const size_t lds = sizeof(int32_t) * 256 * (size_t)(depth + 2);
                 auto fill = [&](auto kern) {
-                    hipLaunchKernelGGL(kern, gq, dim3(256), 0, s, dV, ids + nv, nunseen, sorted, nseen, P, blo, bhi,
+                    hipLaunchKernelGGL(kern, gq, dim3(256), lds, s, dV, ids + nv, nunseen, pts, nseen, P, blo, bhi,
                                        avg, dO);
                 };
                 switch (knn) {  // knn in [1, 8] (checked on entry)
