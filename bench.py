@@ -1352,13 +1352,17 @@ def main():
             extras["dropin_e2e"] = dropin_e2e_leg(seq, min(args.e2e_frames, B), dev)
         # PCIe-inclusive: the same step from host (numpy) frames, H2D inside integrate_frames
         host = depth_t.cpu().numpy()
-        vbg.reset()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        vbg.integrate_frames(host, K, T, depth_scale=1.0, depth_max=args.depth_max,
-                             trunc_voxel_multiplier=args.trunc)
-        torch.cuda.synchronize()
-        extras["host_input_frames_per_s"] = B / (time.perf_counter() - t0)
+        best = None
+        for _ in range(3):  # best of 3 (a single run varies with the host's copy path)
+            vbg.reset()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            vbg.integrate_frames(host, K, T, depth_scale=1.0, depth_max=args.depth_max,
+                                 trunc_voxel_multiplier=args.trunc)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            best = dt if best is None else min(best, dt)
+        extras["host_input_frames_per_s"] = B / best
     ext_alg = None
     if ext_ms:
         ext_alg = (8 * R3_ * blocks + 4 * 27 * blocks + 24 * nv + 12 * nt) / (ext_ms * 1e-3) / 1e9
