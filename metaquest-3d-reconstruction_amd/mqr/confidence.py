@@ -177,6 +177,8 @@ def _estimate_side_native(depth_data_io, config, side, dataset, todo, K, T_cw, T
     ts = dataset.timestamps
     t0 = time.perf_counter()
     depth = DeviceBuffer(4 * n * HW, dev)
+    times["alloc"] = times.get("alloc", 0.0) + time.perf_counter() - t0
+    t0 = time.perf_counter()
     ok = np.zeros(n, bool)
     stages = [np.empty((min(_READ_CHUNK, n), H, W), np.float32) for _ in range(2)]
 
@@ -267,7 +269,9 @@ def _estimate_side_native(depth_data_io, config, side, dataset, todo, K, T_cw, T
                 pending.append(writer.submit(write, a, names, conf, valid))
                 settle(2)  # at most two runs' maps held for writing
         settle(0)
+    t0 = time.perf_counter()
     depth.free()
+    times["free"] = times.get("free", 0.0) + time.perf_counter() - t0
     return True
 
 
@@ -277,12 +281,14 @@ def estimate_depth_confidences(depth_data_io, config: DepthConfidenceEstimationC
     once each and held only while a chunk's window [first - r, last + r] needs them.  As in the
     reference (estimate_depth_confidences.py:98-117), an error while building or saving one
     reference frame's map is printed and that frame is skipped; the other frames go on."""
-    times = {"scan": 0.0, "decode": 0.0, "compute": 0.0, "write_wait": 0.0}
+    times = {"scan": 0.0, "decode": 0.0, "compute": 0.0, "write_wait": 0.0, "total": 0.0}
+    t_all = time.perf_counter()
     for side in (sides or list(Side)):
         if config.skip_if_output_dir_exists and depth_data_io.exists_depth_confidence_map_dir(side=side):
             print(f"[{side.name}] Skipping confidence map estimation: output directory already exists. "
                   "Set skip_if_output_dir_exists = False to force re-estimation.")
             continue
+        t0 = time.perf_counter()
         dataset = depth_data_io.load_depth_dataset(side=side)
         n = len(dataset)
         if n == 0:
@@ -292,6 +298,7 @@ def estimate_depth_confidences(depth_data_io, config: DepthConfidenceEstimationC
                                                             is_camera=True).extrinsics_cw
         T_inv = np.linalg.inv(T_cw)
         r = int(config.target_frame_range)
+        times["prep"] = times.get("prep", 0.0) + time.perf_counter() - t0
         t0 = time.perf_counter()
         todo = [i for i in range(n) if depth_data_io.load_confidence_map(side=side, timestamp=dataset.timestamps[i])
                 is None]
@@ -366,4 +373,5 @@ def estimate_depth_confidences(depth_data_io, config: DepthConfidenceEstimationC
                 if len(writes) > 2 * REF_CHUNK:  # bound the maps held for writing
                     settle(REF_CHUNK)
         settle(0)
+    times["total"] = time.perf_counter() - t_all
     last_confidence_times.__dict__.update(times)
