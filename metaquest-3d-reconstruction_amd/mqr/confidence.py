@@ -131,6 +131,23 @@ def _report(side, idx, timestamp, e):
 RESIDENT_MAX_BYTES = 48 << 30
 _READ_CHUNK = 127
 
+# per thread: the native path's three host sets of maps, kept across calls -- freeing them (~0.7 GB at
+# 640 x 480) cost ~50 ms per call and re-faulting them slowed every download (tools/conf_driver_prof.py)
+_TLS = threading.local()
+
+
+def _map_sets(H, W):
+    sets = getattr(_TLS, "map_sets", None)
+    if sets is None or sets[0][0].shape[1:] != (H, W):
+        sets = _TLS.map_sets = [(np.empty((REF_CHUNK, H, W), np.float64), np.empty((REF_CHUNK, H, W), np.int32))
+                                for _ in range(3)]
+    return sets
+
+
+def release_host_maps():
+    """Free this thread's cached host map sets of estimate_depth_confidences (12 B per pixel, 3 x REF_CHUNK)."""
+    _TLS.map_sets = None
+
 
 def _native_paths(depth_data_io, side, dataset):
     """(raw path fn, confidence path fn) when the side can run device-resident: frames read, decoded and
@@ -219,7 +236,7 @@ def _estimate_side_native(depth_data_io, config, side, dataset, todo, K, T_cw, T
     pending = []
     # three host sets of maps: the run computing and the at most two runs being written (settle(2));
     # reused, so their pages are faulted in once
-    outs = [(np.empty((REF_CHUNK, H, W), np.float64), np.empty((REF_CHUNK, H, W), np.int32)) for _ in range(3)]
+    outs = _map_sets(H, W)
     runs = 0
 
     def settle(keep):
