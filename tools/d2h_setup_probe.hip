@@ -1,6 +1,6 @@
 // What does the first large device -> host copy of a process pay for?  (tools/d2h_probe.py: the first
 // 48 MB mqr_memcpy took 46.6 ms, the second 1.6 ms.)  After the context exists (hipMalloc + one kernel),
-// times each set-up step d2h_parallel performs on its first call: stream creation, pinned staging
+// times each set-up step the first round-5 d2h_parallel performed on its first call: stream creation, pinned staging
 // allocation (8 x 8 MB, or one 64 MB block), event creation, and the first D2H copy on each new stream.
 // One JSON line.   hipcc --offload-arch=gfx950 -O2 -o tools/_ab/d2h_setup_probe tools/d2h_setup_probe.hip
 #include <hip/hip_runtime.h>
