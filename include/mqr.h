@@ -208,6 +208,12 @@ int mqr_decode_depth(int device, const float* raw, int raw_loc, int N, int H, in
                      const double* fars, const uint8_t* strong, const double* conf, const int32_t* valid_count,
                      const uint8_t* has_mask, int mask_loc, double conf_thr, int count_thr, float* depth_out,
                      int out_loc, uint8_t* frame_ok);
+/* The same decode with the confidence mask given as one byte per pixel (mask[N][H][W], mask_loc; nonzero =
+ * depth 0 where has_mask[f]), e.g. as mqr_read_frames_masked computes it from the npz: 1 byte per pixel to
+ * stage instead of 12. */
+int mqr_decode_depth_masked(int device, const float* raw, int raw_loc, int N, int H, int W, const double* nears,
+                            const double* fars, const uint8_t* strong, const uint8_t* mask, const uint8_t* has_mask,
+                            int mask_loc, float* depth_out, int out_loc, uint8_t* frame_ok);
 
 /* Host reads of the drop-in integrate.  Replaces, for n frames, the raw depth
  * read of DepthDataIO.load_depth_map (np.fromfile of H*W little-endian float32,
@@ -226,6 +232,12 @@ int mqr_decode_depth(int device, const float* raw, int raw_loc, int N, int H, in
 #define MQR_FRAME_CONF_OTHER 32
 int mqr_read_frames(int n, const char* const* raw_paths, const char* const* conf_paths, int H, int W,
                     float* raw_out, double* conf_out, int32_t* vc_out, uint8_t* status, int threads);
+/* The same reads with the confidence maps reduced while they are read to the mask byte the decode applies:
+ * mask_out[f][y][x] = (confidence_map < conf_thr) | (valid_count < count_thr) (o3d_utils.py:131-142),
+ * for mqr_decode_depth_masked. */
+int mqr_read_frames_masked(int n, const char* const* raw_paths, const char* const* conf_paths, int H, int W,
+                           double conf_thr, int count_thr, float* raw_out, uint8_t* mask_out, uint8_t* status,
+                           int threads);
 
 /* The confidence maps' writer (SURVEY §8 C3 outputs): for n frames, np.savez(paths[f],
  * confidence_map=conf[f], valid_count=valid[f]) as the reference saves them

@@ -144,8 +144,9 @@ bool zip_members(int fd, int64_t fsize, std::vector<Member>& want) {
     return true;
 }
 
-// The array bytes of one .npy member at [off, off + size): checks the header, reads H*W*item bytes.
-bool read_npy(int fd, const Member& m, const char* descr, size_t item, int H, int W, void* dst) {
+// The file offset of the array bytes of one .npy member at [off, off + size) after checking its header
+// (dtype, C order, shape H x W, size), or -1.
+int64_t npy_data_off(int fd, const Member& m, const char* descr, size_t item, int H, int W) {
     unsigned char pre[12];
     if (m.size < 10 || !pread_all(fd, pre, 10, m.data_off)) return false;
     if (memcmp(pre, "\x93NUMPY", 6) != 0) return false;
@@ -158,14 +159,40 @@ bool read_npy(int fd, const Member& m, const char* descr, size_t item, int H, in
         hl = u32(pre + 8);
         hoff = 12;
     } else {
-        return false;
+        return -1;
     }
     const size_t bytes = item * (size_t)H * (size_t)W;
-    if (hl > 65536 || hoff + hl + (int64_t)bytes != m.size) return false;
+    if (hl > 65536 || hoff + hl + (int64_t)bytes != m.size) return -1;
     std::string h((size_t)hl, '\0');
-    if (!pread_all(fd, &h[0], (size_t)hl, m.data_off + hoff)) return false;
-    if (!npy_header_ok(h, descr, H, W)) return false;
-    return pread_all(fd, dst, bytes, m.data_off + hoff + hl);
+    if (!pread_all(fd, &h[0], (size_t)hl, m.data_off + hoff)) return -1;
+    if (!npy_header_ok(h, descr, H, W)) return -1;
+    return m.data_off + hoff + hl;
+}
+
+// Reads the H*W*item array bytes of one .npy member into dst.
+bool read_npy(int fd, const Member& m, const char* descr, size_t item, int H, int W, void* dst) {
+    const int64_t off = npy_data_off(fd, m, descr, item, H, W);
+    return off >= 0 && pread_all(fd, dst, item * (size_t)H * (size_t)W, off);
+}
+
+// The confidence mask of one frame, one byte per pixel: (confidence_map < conf_thr) | (valid_count <
+// count_thr), the comparison the decode applies (ingest.hip decode_px; reference o3d_utils.py:47-50 via
+// dataio/depth_data_io.py:125-131).  Both members are read in blocks through a thread-local buffer.
+bool read_mask(int fd, const Member* m, int H, int W, double conf_thr, int count_thr, uint8_t* mask) {
+    const size_t HW = (size_t)H * (size_t)W;
+    const int64_t oc = npy_data_off(fd, m[0], "<f8", 8, H, W), ov = npy_data_off(fd, m[1], "<i4", 4, H, W);
+    if (oc < 0 || ov < 0) return false;
+    constexpr size_t kBlock = 32768;  // pixels per read: 256 KiB of confidence
+    thread_local std::vector<double> cb(kBlock);
+    thread_local std::vector<int32_t> vb(kBlock);
+    for (size_t p = 0; p < HW; p += kBlock) {
+        const size_t k = std::min(kBlock, HW - p);
+        if (!pread_all(fd, cb.data(), 8 * k, oc + 8 * (int64_t)p) ||
+            !pread_all(fd, vb.data(), 4 * k, ov + 4 * (int64_t)p))
+            return false;
+        for (size_t i = 0; i < k; ++i) mask[p + i] = (uint8_t)((cb[i] < conf_thr) | (vb[i] < count_thr));
+    }
+    return true;
 }
 
 // CRC-32 (zip / gzip polynomial, reflected) by carry-less multiplication: four 128-bit lanes folded
@@ -394,11 +421,12 @@ int mqr_write_confidence_npz(int n, const char* const* paths, const double* conf
 }
 
 
-int mqr_read_frames(int n, const char* const* raw_paths, const char* const* conf_paths, int H, int W, float* raw_out,
-                    double* conf_out, int32_t* vc_out, uint8_t* status, int threads) {
+// Both readers: the maps themselves (conf_out / vc_out) or the mask byte per pixel (mask_out).
+static int read_frames(int n, const char* const* raw_paths, const char* const* conf_paths, int H, int W,
+                       float* raw_out, double* conf_out, int32_t* vc_out, uint8_t* mask_out, double conf_thr,
+                       int count_thr, uint8_t* status, int threads) {
     MQR_REQUIRE(n >= 0 && H > 0 && W > 0, "bad sizes");
     MQR_REQUIRE(n == 0 || (raw_paths && raw_out && status), "null argument");
-    MQR_REQUIRE(!conf_paths || (conf_out && vc_out), "confidence paths without output arrays");
     const size_t HW = (size_t)H * (size_t)W;
     std::atomic<int> next{0};
     auto work = [&] {
@@ -427,8 +455,10 @@ int mqr_read_frames(int n, const char* const* raw_paths, const char* const* conf
                     m[0].name = "confidence_map.npy";
                     m[1].name = "valid_count.npy";
                     const bool ok = fstat(fd.fd, &sb) == 0 && zip_members(fd.fd, sb.st_size, m) &&
-                                    read_npy(fd.fd, m[0], "<f8", 8, H, W, conf_out + (size_t)f * HW) &&
-                                    read_npy(fd.fd, m[1], "<i4", 4, H, W, vc_out + (size_t)f * HW);
+                                    (mask_out ? read_mask(fd.fd, m.data(), H, W, conf_thr, count_thr,
+                                                          mask_out + (size_t)f * HW)
+                                              : read_npy(fd.fd, m[0], "<f8", 8, H, W, conf_out + (size_t)f * HW) &&
+                                                    read_npy(fd.fd, m[1], "<i4", 4, H, W, vc_out + (size_t)f * HW));
                     st |= ok ? MQR_FRAME_CONF_OK : MQR_FRAME_CONF_OTHER;
                 }
             }
@@ -441,6 +471,20 @@ int mqr_read_frames(int n, const char* const* raw_paths, const char* const* conf
     work();
     for (auto& x : th) x.join();
     return 0;
+}
+
+int mqr_read_frames(int n, const char* const* raw_paths, const char* const* conf_paths, int H, int W, float* raw_out,
+                    double* conf_out, int32_t* vc_out, uint8_t* status, int threads) {
+    MQR_REQUIRE(!conf_paths || (conf_out && vc_out), "confidence paths without output arrays");
+    return read_frames(n, raw_paths, conf_paths, H, W, raw_out, conf_out, vc_out, nullptr, 0.0, 0, status, threads);
+}
+
+int mqr_read_frames_masked(int n, const char* const* raw_paths, const char* const* conf_paths, int H, int W,
+                           double conf_thr, int count_thr, float* raw_out, uint8_t* mask_out, uint8_t* status,
+                           int threads) {
+    MQR_REQUIRE(!conf_paths || mask_out, "confidence paths without a mask array");
+    return read_frames(n, raw_paths, conf_paths, H, W, raw_out, nullptr, nullptr, mask_out, conf_thr, count_thr,
+                       status, threads);
 }
 
 }  // extern "C"

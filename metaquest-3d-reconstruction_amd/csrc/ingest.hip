@@ -59,13 +59,16 @@ __device__ __forceinline__ float decode_px(float d, const DecodeFrame& fr, doubl
 // Workgroups stride over 4-pixel groups of one frame (blockIdx.y): 16-byte raw / count / depth
 // accesses and two 16-byte confidence loads, so every wave moves whole 1 KiB (raw) or 2 KiB
 // (confidence) runs.  VEC = false: scalar tail path for frames whose size is not a multiple of 4.
-template <bool VEC>
+// BYTES: the mask comes as one byte per pixel (mqr_decode_depth_masked, e.g. from mqr_read_frames_masked)
+// instead of the confidence / count maps.
+template <bool VEC, bool BYTES = false>
 __global__ __launch_bounds__(256) void k_decode_depth(const float* __restrict__ raw, int64_t HW,
                                                       const DecodeFrame* __restrict__ frames,
                                                       const double* __restrict__ conf,
                                                       const int32_t* __restrict__ vcount, double conf_thr,
                                                       int count_thr, float* __restrict__ out,
-                                                      uint32_t* __restrict__ flags) {
+                                                      uint32_t* __restrict__ flags,
+                                                      const uint8_t* __restrict__ mask8 = nullptr) {
     const int f = blockIdx.y;
     const DecodeFrame fr = frames[f];
     const int64_t base = (int64_t)f * HW;
@@ -78,7 +81,18 @@ __global__ __launch_bounds__(256) void k_decode_depth(const float* __restrict__ 
         for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
             const float4 d = r4[i];
             float4 z;
-            if (fr.mask) {
+            if (BYTES) {
+                const uchar4 m = fr.mask ? reinterpret_cast<const uchar4*>(mask8 + base)[i] : make_uchar4(0, 0, 0, 0);
+                // the decode runs for the validity flags even where the mask zeroes the depth
+                z.x = decode_px<false>(d.x, fr, 0.0, 0, conf_thr, count_thr, fl);
+                z.y = decode_px<false>(d.y, fr, 0.0, 0, conf_thr, count_thr, fl);
+                z.z = decode_px<false>(d.z, fr, 0.0, 0, conf_thr, count_thr, fl);
+                z.w = decode_px<false>(d.w, fr, 0.0, 0, conf_thr, count_thr, fl);
+                if (m.x) z.x = 0.0f;
+                if (m.y) z.y = 0.0f;
+                if (m.z) z.z = 0.0f;
+                if (m.w) z.w = 0.0f;
+            } else if (fr.mask) {
                 const double2* c2 = reinterpret_cast<const double2*>(conf + base) + 2 * i;
                 const double2 ca = c2[0], cb = c2[1];
                 const int4 v = reinterpret_cast<const int4*>(vcount + base)[i];
@@ -97,8 +111,13 @@ __global__ __launch_bounds__(256) void k_decode_depth(const float* __restrict__ 
     } else {
         for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < HW; i += stride) {
             const float d = raw[base + i];
-            out[base + i] = fr.mask ? decode_px<true>(d, fr, conf[base + i], vcount[base + i], conf_thr, count_thr, fl)
-                                    : decode_px<false>(d, fr, 0.0, 0, conf_thr, count_thr, fl);
+            if (BYTES) {
+                const float z = decode_px<false>(d, fr, 0.0, 0, conf_thr, count_thr, fl);
+                out[base + i] = fr.mask && mask8[base + i] ? 0.0f : z;
+            } else {
+                out[base + i] = fr.mask ? decode_px<true>(d, fr, conf[base + i], vcount[base + i], conf_thr, count_thr, fl)
+                                        : decode_px<false>(d, fr, 0.0, 0, conf_thr, count_thr, fl);
+            }
         }
     }
     // workgroup-level OR (wave shuffle, then LDS), then ONE device atomic per workgroup.  A device
@@ -167,28 +186,27 @@ static size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
 using namespace mqr;
 
-extern "C" {
-
-int mqr_decode_depth(int device, const float* raw, int raw_loc, int N, int H, int W, const double* nears,
-                     const double* fars, const uint8_t* strong, const double* conf, const int32_t* valid_count,
-                     const uint8_t* has_mask, int mask_loc, double conf_thr, int count_thr, float* depth_out,
-                     int out_loc, uint8_t* frame_ok) {
+// The decode with the mask as confidence / count maps (mask8 null) or as one byte per pixel (mask8).
+static int decode_impl(int device, const float* raw, int raw_loc, int N, int H, int W, const double* nears,
+                       const double* fars, const uint8_t* strong, const double* conf, const int32_t* valid_count,
+                       const uint8_t* mask8, const uint8_t* has_mask, int mask_loc, double conf_thr, int count_thr,
+                       float* depth_out, int out_loc, uint8_t* frame_ok) {
     MQR_REQUIRE(raw && nears && fars && depth_out && frame_ok, "null argument");
     MQR_REQUIRE(N >= 0 && H > 0 && W > 0, "bad frame shape");
     MQR_REQUIRE(device >= 0 && device < 64, "device index out of range");
     if (N == 0) return 0;
     const bool any_mask = has_mask && std::any_of(has_mask, has_mask + N, [](uint8_t m) { return m != 0; });
-    MQR_REQUIRE(!any_mask || (conf && valid_count), "mask requested without confidence maps");
+    MQR_REQUIRE(!any_mask || mask8 || (conf && valid_count), "mask requested without confidence maps");
     MQR_CHECK_HIP(hipSetDevice(device));
     const int64_t HW = (int64_t)H * W, total = HW * N;
     DecodeCtx& c = g_decode[device];
     std::lock_guard<std::mutex> lock(c.mu);
-    // scratch layout: [raw f32][conf f64][count i32][out f32], only the parts that are staged
+    // scratch layout: [raw f32][conf f64][count i32] or [mask u8] [out f32], only the parts that are staged
     const bool stage_raw = raw_loc != MQR_DEVICE, stage_mask = any_mask && mask_loc != MQR_DEVICE,
                stage_out = out_loc != MQR_DEVICE;
     const size_t b_raw = stage_raw ? align256(sizeof(float) * total) : 0;
-    const size_t b_conf = stage_mask ? align256(sizeof(double) * total) : 0;
-    const size_t b_vc = stage_mask ? align256(sizeof(int32_t) * total) : 0;
+    const size_t b_conf = stage_mask && !mask8 ? align256(sizeof(double) * total) : 0;
+    const size_t b_vc = stage_mask ? align256((mask8 ? 1 : sizeof(int32_t)) * total) : 0;
     const size_t b_out = stage_out ? align256(sizeof(float) * total) : 0;
     if (decode_ctx_reserve(c, std::max<size_t>(b_raw + b_conf + b_vc + b_out, 256), N)) return 1;
     if ((!stage_raw || (any_mask && !stage_mask) || !stage_out) && order_after_caller(device, c.s)) return 2;
@@ -215,7 +233,12 @@ int mqr_decode_depth(int device, const float* raw, int raw_loc, int N, int H, in
     }
     const double* d_conf = conf;
     const int32_t* d_vc = valid_count;
-    if (stage_mask) {
+    const uint8_t* d_m8 = mask8;
+    if (stage_mask && mask8) {
+        if (copy_to_device(device, sp, mask8, total, c.s)) return 1;
+        d_m8 = reinterpret_cast<const uint8_t*>(sp);
+        sp += b_vc;
+    } else if (stage_mask) {
         if (copy_to_device(device, sp, conf, sizeof(double) * total, c.s)) return 1;
         d_conf = reinterpret_cast<const double*>(sp);
         sp += b_conf;
@@ -228,18 +251,25 @@ int mqr_decode_depth(int device, const float* raw, int raw_loc, int N, int H, in
     MQR_CHECK_HIP(hipMemsetAsync(c.d_flags, 0, sizeof(uint32_t) * N, c.s));
     auto aligned = [](const void* p, size_t a) { return (reinterpret_cast<uintptr_t>(p) & (a - 1)) == 0; };
     const bool vec = HW % 4 == 0 && aligned(d_raw, 16) && aligned(d_out, 16) &&
-                     (!any_mask || (aligned(d_conf, 32) && aligned(d_vc, 16)));
+                     (!any_mask || (mask8 ? aligned(d_m8, 4) : (aligned(d_conf, 32) && aligned(d_vc, 16))));
     const int64_t work = vec ? HW / 4 : HW;
     // ~4096 workgroups in all (16 per CU), each a long grid-stride run over its frame: enough
     // to fill the chip with few enough workgroups that the per-frame flag atomics stay rare
     const int64_t per_frame = std::max<int64_t>(1, (4096 + N - 1) / N);
     const unsigned gx = (unsigned)std::min<int64_t>((work + 255) / 256, per_frame);
-    if (vec)
-        hipLaunchKernelGGL(k_decode_depth<true>, dim3(gx, (unsigned)N), dim3(256), 0, c.s, d_raw, HW, c.d_fr, d_conf,
-                           d_vc, conf_thr, count_thr, d_out, c.d_flags);
+    const dim3 grid(gx, (unsigned)N);
+    if (mask8 && vec)
+        hipLaunchKernelGGL((k_decode_depth<true, true>), grid, dim3(256), 0, c.s, d_raw, HW, c.d_fr, nullptr, nullptr,
+                           conf_thr, count_thr, d_out, c.d_flags, d_m8);
+    else if (mask8)
+        hipLaunchKernelGGL((k_decode_depth<false, true>), grid, dim3(256), 0, c.s, d_raw, HW, c.d_fr, nullptr, nullptr,
+                           conf_thr, count_thr, d_out, c.d_flags, d_m8);
+    else if (vec)
+        hipLaunchKernelGGL((k_decode_depth<true, false>), grid, dim3(256), 0, c.s, d_raw, HW, c.d_fr, d_conf, d_vc,
+                           conf_thr, count_thr, d_out, c.d_flags, nullptr);
     else
-        hipLaunchKernelGGL(k_decode_depth<false>, dim3(gx, (unsigned)N), dim3(256), 0, c.s, d_raw, HW, c.d_fr, d_conf,
-                           d_vc, conf_thr, count_thr, d_out, c.d_flags);
+        hipLaunchKernelGGL((k_decode_depth<false, false>), grid, dim3(256), 0, c.s, d_raw, HW, c.d_fr, d_conf, d_vc,
+                           conf_thr, count_thr, d_out, c.d_flags, nullptr);
     MQR_CHECK_HIP(hipGetLastError());
     MQR_CHECK_HIP(hipMemcpyAsync(c.h_flags, c.d_flags, sizeof(uint32_t) * N, hipMemcpyDeviceToHost, c.s));
     if (stage_out && copy_to_host(device, depth_out, d_out, sizeof(float) * total, c.s)) return 1;
@@ -249,6 +279,26 @@ int mqr_decode_depth(int device, const float* raw, int raw_loc, int N, int H, in
         frame_ok[f] = (fl & kAnyNonZero) && (fl & kAnyNonOne) && !(fl & (kAnyNaN | kAnyNotGE0));
     }
     return 0;
+}
+
+extern "C" {
+
+int mqr_decode_depth(int device, const float* raw, int raw_loc, int N, int H, int W, const double* nears,
+                     const double* fars, const uint8_t* strong, const double* conf, const int32_t* valid_count,
+                     const uint8_t* has_mask, int mask_loc, double conf_thr, int count_thr, float* depth_out,
+                     int out_loc, uint8_t* frame_ok) {
+    return decode_impl(device, raw, raw_loc, N, H, W, nears, fars, strong, conf, valid_count, nullptr, has_mask,
+                       mask_loc, conf_thr, count_thr, depth_out, out_loc, frame_ok);
+}
+
+int mqr_decode_depth_masked(int device, const float* raw, int raw_loc, int N, int H, int W, const double* nears,
+                            const double* fars, const uint8_t* strong, const uint8_t* mask, const uint8_t* has_mask,
+                            int mask_loc, float* depth_out, int out_loc, uint8_t* frame_ok) {
+    const bool any_mask = has_mask && N > 0 && std::any_of(has_mask, has_mask + N, [](uint8_t m) { return m != 0; });
+    MQR_REQUIRE(!any_mask || mask, "mask requested without a mask array");
+    static const uint8_t kNone = 0;
+    return decode_impl(device, raw, raw_loc, N, H, W, nears, fars, strong, nullptr, nullptr, any_mask ? mask : &kNone,
+                       any_mask ? has_mask : nullptr, mask_loc, 0.0, 0, depth_out, out_loc, frame_ok);
 }
 
 }  // extern "C"

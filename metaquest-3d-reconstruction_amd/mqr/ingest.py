@@ -14,6 +14,7 @@ keep the decode in float32.  The kernel reproduces both, per frame, from the ope
 """
 from __future__ import annotations
 
+import math
 from typing import Optional, Sequence
 
 import numpy as np
@@ -30,11 +31,20 @@ def _strong(x) -> int:
     return 0
 
 
+def count_threshold(valid_count_threshold) -> int:
+    """The int32 threshold t' with (count < t') == (count < valid_count_threshold) for every int32 count,
+    as numpy compares an int32 map with a Python int or float threshold."""
+    return int(min(max(math.ceil(valid_count_threshold), -(2 ** 31)), 2 ** 31 - 1))
+
+
 def decode_depth_frames(raw, nears: Sequence, fars: Sequence, conf: Optional[np.ndarray] = None,
                         valid_count: Optional[np.ndarray] = None, has_mask: Optional[Sequence[bool]] = None,
                         confidence_threshold: float = 0.0, valid_count_threshold: int = 0, device: int = 0,
-                        out_ptr: Optional[int] = None):
+                        out_ptr: Optional[int] = None, mask: Optional[np.ndarray] = None):
     """raw: (N,H,W) float32 numpy array, or a tuple (device_ptr, N, H, W) of raw buffers in HBM.
+    The confidence mask of the frames selected by `has_mask` comes either as the maps (`conf`,
+    `valid_count` and the thresholds) or, already reduced, as `mask` ((N,H,W) uint8 host array, nonzero =
+    depth 0; mqr_decode_depth_masked: 1 byte per pixel to stage instead of 12).
 
     Returns (depth, frame_ok): depth is a (N,H,W) float32 numpy array, or None when `out_ptr`
     (a device pointer with room for N*H*W floats) received it; frame_ok is (N,) bool."""
@@ -54,11 +64,6 @@ def decode_depth_frames(raw, nears: Sequence, fars: Sequence, conf: Optional[np.
     f64 = np.array([float(x) for x in fars], np.float64)
     mask_arg = None
     conf_arg = vc_arg = None
-    if has_mask is not None and np.any(has_mask):
-        mask = np.ascontiguousarray(np.asarray(has_mask, dtype=np.uint8).reshape(N))
-        conf = np.ascontiguousarray(conf, dtype=np.float64).reshape(N, H, W)
-        valid_count = np.ascontiguousarray(valid_count, dtype=np.int32).reshape(N, H, W)
-        mask_arg, conf_arg, vc_arg = ptr(mask, _lib._u8p), ptr(conf), ptr(valid_count)
     ok = np.zeros(N, np.uint8)
     out = None
     if out_ptr is None:
@@ -66,9 +71,25 @@ def decode_depth_frames(raw, nears: Sequence, fars: Sequence, conf: Optional[np.
         out_arg, out_loc = ptr(out), MQR_HOST
     else:
         out_arg, out_loc = ctypes_ptr(out_ptr), MQR_DEVICE
+    if mask is not None:
+        m8 = None
+        if has_mask is not None and np.any(has_mask):
+            mask_arg = ptr(np.ascontiguousarray(np.asarray(has_mask, dtype=np.uint8).reshape(N)), _lib._u8p)
+            m8 = np.asarray(mask)
+            if m8.dtype != np.uint8 or m8.shape != (N, H, W) or not m8.flags.c_contiguous:
+                raise ValueError("mask must be a C-contiguous (N, H, W) uint8 array")
+        call("mqr_decode_depth_masked", int(device), raw_arg, raw_loc, N, H, W, ptr(n64, _lib._f64p),
+             ptr(f64, _lib._f64p), ptr(strong, _lib._u8p), None if m8 is None else ptr(m8), mask_arg, MQR_HOST,
+             out_arg, out_loc, ptr(ok, _lib._u8p))
+        return out, ok.astype(bool)
+    if has_mask is not None and np.any(has_mask):
+        mask = np.ascontiguousarray(np.asarray(has_mask, dtype=np.uint8).reshape(N))
+        conf = np.ascontiguousarray(conf, dtype=np.float64).reshape(N, H, W)
+        valid_count = np.ascontiguousarray(valid_count, dtype=np.int32).reshape(N, H, W)
+        mask_arg, conf_arg, vc_arg = ptr(mask, _lib._u8p), ptr(conf), ptr(valid_count)
     call("mqr_decode_depth", int(device), raw_arg, raw_loc, N, H, W, ptr(n64, _lib._f64p), ptr(f64, _lib._f64p),
          ptr(strong, _lib._u8p), conf_arg, vc_arg, mask_arg, MQR_HOST, float(confidence_threshold),
-         int(valid_count_threshold), out_arg, out_loc, ptr(ok, _lib._u8p))
+         count_threshold(valid_count_threshold), out_arg, out_loc, ptr(ok, _lib._u8p))
     return out, ok.astype(bool)
 
 

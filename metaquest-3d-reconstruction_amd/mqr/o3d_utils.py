@@ -25,6 +25,7 @@ from typing import Optional
 import numpy as np
 
 from ._io import io_pool, io_threads
+from .ingest import count_threshold
 from .geometry import Image
 from .meshfilter import filter_mesh_components  # noqa: F401  (re-exported: o3d_utils.py:241-321)
 from .raycasting import raycast_in_color_view  # noqa: F401  (re-exported: o3d_utils.py:324-341)
@@ -39,14 +40,15 @@ CHUNK = 127
 
 
 class _HostStage:
-    """Reusable host staging of one chunk of raw frames and their confidence maps (pageable, so no
-    pinning cost; reused, so its pages are faulted in once instead of per chunk)."""
+    """Reusable host staging of one chunk of raw frames and their confidence masks, one byte per pixel:
+    (confidence_map < threshold) | (valid_count < threshold), reduced as the maps are read (pageable, so no
+    pinning cost; reused, so its pages are faulted in once instead of per chunk).  5 B per pixel go to
+    the device instead of the 16 B of raw + confidence_map + valid_count."""
 
     def __init__(self, B, H, W, with_conf):
         self.key = (B, H, W, with_conf)
         self.raw = np.empty((B, H, W), np.float32)
-        self.conf = np.empty((B, H, W), np.float64) if with_conf else None
-        self.vc = np.empty((B, H, W), np.int32) if with_conf else None
+        self.mask = np.empty((B, H, W), np.uint8) if with_conf else None
 
 
 # per thread: the two alternating sets of the last shape used, kept across integrate() calls (the fragment
@@ -65,7 +67,7 @@ def _host_stage(turn, B, H, W, with_conf) -> _HostStage:
 
 
 def release_host_staging():
-    """Free this thread's drop-in integrate() host staging (~16 B per pixel per staged frame, two chunks)."""
+    """Free this thread's drop-in integrate() host staging (5 B per pixel per staged frame, two chunks)."""
     _TLS.stages = None
 
 
@@ -183,6 +185,11 @@ def integrate(dataset, depth_data_io, side, use_confidence_filtered_depth: bool,
         hi = min(n, lo + CHUNK)
         return lo, hi, [it for it in io_pool().map(load_one, range(lo, hi)) if it is not None]
 
+    def put_mask(st, j, cm):  # the reference's two masking comparisons (o3d_utils.py:131-142), as numpy makes them
+        m = st.mask[j].view(np.bool_)
+        np.less(cm.confidence_map, confidence_threshold, out=m)
+        m |= cm.valid_count < valid_count_threshold
+
     def load_chunk_staged(lo, st):
         """load_chunk for a chunk of one frame size: the I/O threads read every frame straight into
         the reusable staging set `st` (raw buffer, and the confidence maps when masking) -- no
@@ -205,8 +212,7 @@ def integrate(dataset, depth_data_io, side, use_confidence_filtered_depth: bool,
             cm = depth_data_io.load_confidence_map(side=side, timestamp=dataset.timestamps[i])
             if cm is None:
                 return -1
-            st.conf[j] = cm.confidence_map
-            st.vc[j] = cm.valid_count
+            put_mask(st, j, cm)
             return 1
 
         res = list(io_pool().map(one, range(hi - lo)))
@@ -216,8 +222,8 @@ def integrate(dataset, depth_data_io, side, use_confidence_filtered_depth: bool,
         return lo, hi, (st, np.array([r > 0 for r in res], bool))
 
     def load_chunk_native(lo, st):
-        """load_chunk_staged through mqr_read_frames: native threads pread the raw files and the npz
-        members straight into `st`.  Frames the reader leaves to Python (a raw file of the wrong size, a
+        """load_chunk_staged through mqr_read_frames_masked: native threads pread the raw files into `st`
+        and reduce the npz members to the mask bytes as they read them.  Frames the reader leaves to Python (a raw file of the wrong size, a
         confidence npz it does not parse) go through the standard loaders here, in frame order, and the
         confidence messages are printed only for frames whose depth map is valid -- the reference loads
         the confidence map only after is_depth_map_valid passed (o3d_utils.py:109-142)."""
@@ -231,8 +237,9 @@ def integrate(dataset, depth_data_io, side, use_confidence_filtered_depth: bool,
         raws = (ctypes.c_char_p * B)(*[os.fsencode(str(raw_path(t))) for t in ts])
         confs = (ctypes.c_char_p * B)(*[os.fsencode(str(conf_path(t))) for t in ts]) if use_confidence_filtered_depth else None
         status = np.zeros(B, np.uint8)
-        _lib.call("mqr_read_frames", B, raws, confs, H, W, _lib.ptr(st.raw), _lib.ptr(st.conf) if confs else None,
-                  _lib.ptr(st.vc) if confs else None, _lib.ptr(status), io_threads())
+        _lib.call("mqr_read_frames_masked", B, raws, confs, H, W, float(confidence_threshold),
+                  count_threshold(valid_count_threshold), _lib.ptr(st.raw), _lib.ptr(st.mask) if confs else None,
+                  _lib.ptr(status), io_threads())
         has = np.zeros(B, bool)
         for j in range(B):
             s = int(status[j])
@@ -253,8 +260,7 @@ def integrate(dataset, depth_data_io, side, use_confidence_filtered_depth: bool,
             if cm is None:
                 print(f"[Warning] Confidence map not found for timestamp {ts[j]}")
                 continue
-            st.conf[j] = cm.confidence_map
-            st.vc[j] = cm.valid_count
+            put_mask(st, j, cm)
             has[j] = True
         return lo, hi, (st, has)
 
@@ -308,10 +314,8 @@ def integrate(dataset, depth_data_io, side, use_confidence_filtered_depth: bool,
         buf = device_buffer(H, W)
         any_mask = bool(has.any())
         _, ok = decode_depth_frames(st.raw[:B], [dataset.nears[i] for i in idx], [dataset.fars[i] for i in idx],
-                                    conf=st.conf[:B] if any_mask else None, valid_count=st.vc[:B] if any_mask else None,
-                                    has_mask=has if any_mask else None, confidence_threshold=confidence_threshold,
-                                    valid_count_threshold=valid_count_threshold, device=vbg.device_id,
-                                    out_ptr=buf.ptr)
+                                    mask=st.mask[:B] if any_mask else None,
+                                    has_mask=has if any_mask else None, device=vbg.device_id, out_ptr=buf.ptr)
         integrate_decoded(idx, buf, ok, H, W)
 
     def uniform(lo):  # every frame of the chunk at lo has one size (the usual capture)

@@ -138,3 +138,42 @@ def test_write_confidence_npz_roundtrip(tmp_path, threads):
     _, c2, v2, st2 = _read(lib, raws, [paths[i] for i in ok], H, W, 2)
     assert (st2 & lib.MQR_FRAME_CONF_OK).all()
     assert np.array_equal(c2, conf[ok], equal_nan=True) and np.array_equal(v2, valid[ok])
+
+
+@pytest.mark.parametrize("shape", [(24, 40), (210, 330)])   # the second spans several 32768-pixel read blocks
+def test_read_frames_masked_matches_the_decode_mask(tmp_path, shape):
+    """mqr_read_frames_masked: the same statuses and raw frames as mqr_read_frames, and per frame read the
+    mask byte (confidence_map < conf_thr) | (valid_count < count_thr) that load_depth_map applies
+    (reference o3d_utils.py:131-142) -- NaN confidence never masks, as in the comparison numpy makes."""
+    lib = _lib()
+    H, W = shape
+    rng = np.random.default_rng(11)
+    raws, confs = [], []
+    for i in range(6):
+        c = rng.random((H, W))
+        c[rng.random((H, W)) < 0.05] = np.nan
+        c[0, :3] = (-np.inf, np.inf, 0.02)
+        v = rng.integers(-2, 6, (H, W)).astype(np.int32)
+        rp, cp = tmp_path / f"{i}.raw", tmp_path / f"{i}.npz"
+        rng.random((H, W), dtype=np.float32).astype("<f4").tofile(rp)
+        np.savez(cp, confidence_map=c, valid_count=v)
+        raws.append(rp)
+        confs.append(cp)
+    os.unlink(confs[2])
+    np.savez_compressed(confs[3], confidence_map=np.zeros((H, W)), valid_count=np.zeros((H, W), np.int32))
+    confs[4] = None
+    raw0, _, _, st0 = _read(lib, raws, confs, H, W, 2)
+    n = len(raws)
+    raw = np.full((n, H, W), np.nan, np.float32)
+    mask = np.full((n, H, W), 7, np.uint8)
+    st = np.zeros(n, np.uint8)
+    rp = (ctypes.c_char_p * n)(*[os.fsencode(str(p)) for p in raws])
+    cp = (ctypes.c_char_p * n)(*[None if p is None else os.fsencode(str(p)) for p in confs])
+    thr, vthr = 0.02, 2
+    lib.call("mqr_read_frames_masked", n, rp, cp, H, W, thr, vthr, lib.ptr(raw), lib.ptr(mask), lib.ptr(st), 3)
+    assert np.array_equal(st, st0) and np.array_equal(raw, raw0)
+    for i in range(n):
+        if st[i] & lib.MQR_FRAME_CONF_OK:
+            d = np.load(confs[i])
+            want = (d["confidence_map"] < thr) | (d["valid_count"] < vthr)
+            assert np.array_equal(mask[i], want.astype(np.uint8))

@@ -73,3 +73,39 @@ def test_decode_rejects_unsupported_scalar_types():
     from mqr.ingest import decode_depth_frames
     with pytest.raises(TypeError):
         decode_depth_frames(np.zeros((1, 4, 4), np.float32), [np.float32(0.1)], [np.inf])
+
+
+@pytest.mark.parametrize("shape", [(480, 640), (37, 53)])   # vector path, and the scalar path (H*W % 4 != 0)
+def test_decode_byte_mask_equals_the_map_mask(shape):
+    """mqr_decode_depth_masked with the mask byte (conf < thr) | (count < thr) gives the bits and the
+    validity of mqr_decode_depth with the maps; a float count threshold compares as numpy does."""
+    from mqr.depth_utils import convert_depth_to_linear
+    from mqr.ingest import decode_depth_frames
+    rng = np.random.default_rng(9)
+    H, W = shape
+    N = 5
+    raw = rng.random((N, H, W)).astype(np.float32)
+    raw[:, ::7, ::5] = 1.0
+    raw[2] = 0.0
+    conf = rng.random((N, H, W))
+    conf[0, 0, :5] = np.nan
+    vc = rng.integers(0, 6, (N, H, W)).astype(np.int32)
+    has = np.array([1, 0, 1, 1, 1], bool)
+    nears = [np.float64(0.1), 0.1, np.float64(0.1), np.float64(0.05), 0.2]
+    fars = [np.float64(np.inf), np.inf, np.float64(np.inf), np.float64(50.0), 100.0]
+    for vthr in (2, 2.5):
+        m8 = ((conf < 0.3) | (vc < vthr)).astype(np.uint8)
+        a, ok_a = decode_depth_frames(raw, nears, fars, conf=conf, valid_count=vc, has_mask=has,
+                                      confidence_threshold=0.3, valid_count_threshold=vthr)
+        b, ok_b = decode_depth_frames(raw, nears, fars, mask=m8, has_mask=has)
+        assert np.array_equal(ok_a, ok_b) and ok_b.tolist() == [True, True, False, True, True]
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+        for f in range(N):
+            ref = convert_depth_to_linear(raw[f], nears[f], fars[f])
+            if has[f]:
+                ref[conf[f] < 0.3] = 0.0
+                ref[vc[f] < vthr] = 0.0
+            assert np.array_equal(b[f].view(np.uint32), ref.view(np.uint32)), (vthr, f)
+    c, ok_c = decode_depth_frames(raw, nears, fars, mask=np.ones((N, H, W), np.uint8), has_mask=None)
+    d, _ = decode_depth_frames(raw, nears, fars)
+    assert np.array_equal(c.view(np.uint32), d.view(np.uint32)) and np.array_equal(ok_c, ok_a)
