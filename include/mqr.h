@@ -185,6 +185,16 @@ int mqr_confidence(int device, const float* depths, int depth_loc, int N, int H,
                    const float* T_cw, const float* T_cw_inv, const uint8_t* frame_ok, int ref_begin, int ref_end,
                    int frame_range, double depth_max, double error_threshold, double* conf, int32_t* valid,
                    int out_loc);
+/* mqr_confidence for host output as two bytes per pixel: counts[r][y][x] = valid_count | consistent_count
+ * << 8 of reference frame ref_begin + r (csrc/confpack.hip: the maps computed into HBM, reduced on the device,
+ * each pair checked to give back the map's exact float64 bits; 2 bytes cross the link instead of 12).
+ * *packed = 1 on success; 0 when a pixel does not fit (more than 255 valid neighbours) -- counts is then
+ * unspecified and the caller uses mqr_confidence.  The pairs expand to the maps in
+ * mqr_write_confidence_npz_counts. */
+int mqr_confidence_counts(int device, const float* depths, int depth_loc, int N, int H, int W, const float* K,
+                          const float* T_cw, const float* T_cw_inv, const uint8_t* frame_ok, int ref_begin,
+                          int ref_end, int frame_range, double depth_max, double error_threshold, uint16_t* counts,
+                          int* packed);
 /* Diagnostic: enable (1) / disable (0) / keep (-1) per-pair stage counting of mqr_confidence on this
  * device (a slower kernel build); 2 = a timing-only build without the tap loads (wrong maps); last4 (nullable) = the last counted call's (pixel, neighbour) pairs
  * with a valid reference pixel, and how many the float32 prefilter, the float64 band filter and the
@@ -248,6 +258,11 @@ int mqr_read_frames_masked(int n, const char* const* raw_paths, const char* cons
  * (the caller reports that frame). */
 int mqr_write_confidence_npz(int n, const char* const* paths, const double* conf, const int32_t* valid, int H, int W,
                              int32_t* status, int threads);
+/* The same files from the confidence maps' two counts per pixel: counts[f][y][x] = valid_count |
+ * consistent_count << 8 (as mqr_confidence_counts downloads them); confidence_map = consistent / valid in
+ * float64, 0 where valid is 0 (estimate_depth_confidences.py:72-74), expanded by the writer threads. */
+int mqr_write_confidence_npz_counts(int n, const char* const* paths, const uint16_t* counts, int H, int W,
+                                    int32_t* status, int threads);
 /* CRC-32 (zip / zlib) of len bytes continuing from crc (0 to start): the writer's checksum, exported for
  * its tests. */
 uint32_t mqr_crc32(uint32_t crc, const void* data, int64_t len);

@@ -24,6 +24,7 @@
 #include <cstdint>
 #include <cstring>
 #include <string>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -190,7 +191,7 @@ bool read_mask(int fd, const Member* m, int H, int W, double conf_thr, int count
         if (!pread_all(fd, cb.data(), 8 * k, oc + 8 * (int64_t)p) ||
             !pread_all(fd, vb.data(), 4 * k, ov + 4 * (int64_t)p))
             return false;
-        for (size_t i = 0; i < k; ++i) mask[p + i] = (uint8_t)((cb[i] < conf_thr) | (vb[i] < count_thr));
+        for (size_t i = 0; i < k; ++i) mask[p + i] = (uint8_t)((int)(cb[i] < conf_thr) | (int)(vb[i] < count_thr));
     }
     return true;
 }
@@ -463,6 +464,49 @@ static int read_frames(int n, const char* const* raw_paths, const char* const* c
                 }
             }
             status[f] = st;
+        }
+    };
+    const int T = std::max(1, std::min({threads > 0 ? threads : 8, 64, std::max(n, 1)}));
+    std::vector<std::thread> th;
+    for (int t = 1; t < T; ++t) th.emplace_back(work);
+    work();
+    for (auto& x : th) x.join();
+    return 0;
+}
+
+int mqr_write_confidence_npz_counts(int n, const char* const* paths, const uint16_t* counts, int H, int W,
+                                    int32_t* status, int threads) {
+    MQR_REQUIRE(n >= 0 && H > 0 && W > 0, "bad sizes");
+    MQR_REQUIRE(n == 0 || (paths && counts && status), "null argument");
+    // confidence_map of a (valid, consistent) pair: np.true_divide(consistent, valid) -- the correctly
+    // rounded float64 quotient -- and 0 where valid is 0 (estimate_depth_confidences.py:72-74)
+    static double table[1 << 16];
+    static std::once_flag once;
+    std::call_once(once, [] {
+        for (int c = 0; c < (1 << 16); ++c) {
+            const int v = c & 0xFF, k = c >> 8;
+            table[c] = v ? (double)k / (double)v : 0.0;
+        }
+    });
+    const size_t HW = (size_t)H * (size_t)W;
+    const std::string h_conf = npy_header("<f8", H, W), h_valid = npy_header("<i4", H, W);
+    std::atomic<int> next{0};
+    auto work = [&] {
+        std::vector<double> conf(HW);
+        std::vector<int32_t> valid(HW);
+        for (int f; (f = next.fetch_add(1)) < n;) {
+            if (!paths[f]) {
+                status[f] = 0;
+                continue;
+            }
+            const uint16_t* c = counts + (size_t)f * HW;
+            for (size_t i = 0; i < HW; ++i) {
+                conf[i] = table[c[i]];
+                valid[i] = c[i] & 0xFF;
+            }
+            NpzMember m[2] = {{"confidence_map.npy", h_conf, conf.data(), 8 * HW},
+                              {"valid_count.npy", h_valid, valid.data(), 4 * HW}};
+            status[f] = write_npz(paths[f], m, 2);
         }
     };
     const int T = std::max(1, std::min({threads > 0 ? threads : 8, 64, std::max(n, 1)}));

@@ -87,12 +87,18 @@ SIGNATURES = {
     "mqr_confidence": (ctypes.c_int, [ctypes.c_int, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _f32p,
                                       _f32p, _f32p, _u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double,
                                       ctypes.c_double, _vp, _vp, ctypes.c_int]),
+    "mqr_confidence_counts": (ctypes.c_int, [ctypes.c_int, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                             ctypes.c_int, _f32p, _f32p, _f32p, _u8p, ctypes.c_int, ctypes.c_int,
+                                             ctypes.c_int, ctypes.c_double, ctypes.c_double, _vp,
+                                             ctypes.POINTER(ctypes.c_int)]),
     "mqr_confidence_stats": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _i64p]),
     "mqr_pixel_error_map": (ctypes.c_int, [ctypes.c_int, _f32p, _f32p, ctypes.c_int, ctypes.c_int, _f32p, _f32p,
                                            _f32p, _f32p, _f32p, ctypes.c_double, _f32p]),
     "mqr_write_confidence_npz": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p), _vp, _vp, ctypes.c_int,
                                                 ctypes.c_int, _vp, ctypes.c_int]),
     "mqr_crc32": (ctypes.c_uint32, [ctypes.c_uint32, _vp, ctypes.c_int64]),
+    "mqr_write_confidence_npz_counts": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p), _vp,
+                                                       ctypes.c_int, ctypes.c_int, _vp, ctypes.c_int]),
     "mqr_read_frames": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_char_p),
                                        ctypes.c_int, ctypes.c_int, _vp, _vp, _vp, _vp, ctypes.c_int]),
     "mqr_read_frames_masked": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p),
@@ -222,7 +228,7 @@ def load(path: str = LIB_PATH):
 ORDERED = frozenset({
     "mqr_touch", "mqr_integrate", "mqr_integrate_frames", "mqr_vbg_export", "mqr_vbg_import",
     "mqr_vbg_pack_weighted", "mqr_vbg_unpack_weighted", "mqr_xchg_create", "mqr_xchg_send_segment",
-    "mqr_xchg_recv_segment", "mqr_geom_copy", "mqr_confidence", "mqr_decode_depth", "mqr_decode_depth_masked",
+    "mqr_xchg_recv_segment", "mqr_geom_copy", "mqr_confidence", "mqr_confidence_counts", "mqr_decode_depth", "mqr_decode_depth_masked",
     "mqr_color_vertices",
     "mqr_color_map", "mqr_scene_add_triangles", "mqr_scene_cast_pinhole", "mqr_scene_cast_rays",
     "mqr_mesh_filter_components", "mqr_memcpy",

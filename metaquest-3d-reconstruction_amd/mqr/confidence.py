@@ -127,25 +127,38 @@ def _report(side, idx, timestamp, e):
     traceback.print_exception(type(e), e, e.__traceback__)
 
 
+# the native path downloads the maps as (valid, consistent) byte pairs (mqr_confidence_counts) when a window's
+# neighbour count fits a byte; False: the maps themselves (A/B, tools/conf_ab.py)
+COUNT_PAIRS = True
+
 # decoded frames of a side kept in HBM by the native path (bytes); larger captures take the windowed path
 RESIDENT_MAX_BYTES = 48 << 30
 _READ_CHUNK = 127
 
-# per thread: the native path's three host sets of maps, kept across calls -- freeing them (~0.7 GB at
-# 640 x 480) cost ~50 ms per call and re-faulting them slowed every download (tools/conf_driver_prof.py)
+# per thread: the native path's three host sets of count pairs (or of maps), kept across calls -- freeing
+# the maps (~0.7 GB at 640 x 480) cost ~50 ms per call and re-faulting them slowed every download
+# (tools/conf_driver_prof.py)
 _TLS = threading.local()
 
 
-def _map_sets(H, W):
-    sets = getattr(_TLS, "map_sets", None)
+def _map_sets(H, W, counts: bool):
+    cache = getattr(_TLS, "map_sets", None)
+    if cache is None:
+        cache = _TLS.map_sets = {}
+    sets = cache.get(counts)
     if sets is None or sets[0][0].shape[1:] != (H, W):
-        sets = _TLS.map_sets = [(np.empty((REF_CHUNK, H, W), np.float64), np.empty((REF_CHUNK, H, W), np.int32))
-                                for _ in range(3)]
+        if counts:
+            sets = [(np.empty((REF_CHUNK, H, W), np.uint16),) for _ in range(3)]
+        else:
+            sets = [(np.empty((REF_CHUNK, H, W), np.float64), np.empty((REF_CHUNK, H, W), np.int32))
+                    for _ in range(3)]
+        cache[counts] = sets
     return sets
 
 
 def release_host_maps():
-    """Free this thread's cached host map sets of estimate_depth_confidences (12 B per pixel, 3 x REF_CHUNK)."""
+    """Free this thread's cached host sets of estimate_depth_confidences (3 x REF_CHUNK frames of 2 B per pixel,
+    or 12 B when a window holds more than 255 neighbours)."""
     _TLS.map_sets = None
 
 
@@ -227,16 +240,22 @@ def _estimate_side_native(depth_data_io, config, side, dataset, todo, K, T_cw, T
     if todo:
         conf_path(ts[todo[0]]).parent.mkdir(parents=True, exist_ok=True)
 
-    def write(a, names, conf, valid):
+    def write(a, names, maps):
         status = np.zeros(len(names), np.int32)
         arr = (ctypes.c_char_p * len(names))(*names)
-        call("mqr_write_confidence_npz", len(names), arr, ptr(conf), ptr(valid), H, W, ptr(status), io_threads())
+        if len(maps) == 1:  # count pairs, expanded to the maps by the writer threads
+            call("mqr_write_confidence_npz_counts", len(names), arr, ptr(maps[0]), H, W, ptr(status), io_threads())
+        else:
+            call("mqr_write_confidence_npz", len(names), arr, ptr(maps[0]), ptr(maps[1]), H, W, ptr(status),
+                 io_threads())
         return a, status
 
     pending = []
-    # three host sets of maps: the run computing and the at most two runs being written (settle(2));
-    # reused, so their pages are faulted in once
-    outs = _map_sets(H, W)
+    # three host sets: the run computing and the at most two runs being written (settle(2)); reused, so
+    # their pages are faulted in once.  Count pairs (mqr_confidence_counts: 2 B per pixel downloaded instead
+    # of the maps' 12) whenever a window's neighbour count fits a byte.
+    use_counts = COUNT_PAIRS and 2 * r <= 255
+    outs = _map_sets(H, W, use_counts)
     runs = 0
 
     def settle(keep):
@@ -267,14 +286,21 @@ def _estimate_side_native(depth_data_io, config, side, dataset, todo, K, T_cw, T
                 j = k
                 a, b = refs[0], refs[-1] + 1
                 lo, hi = max(0, a - r), min(n, b + r)
-                conf, valid = (x[:b - a] for x in outs[runs % 3])
+                maps = tuple(x[:b - a] for x in outs[runs % 3])
                 runs += 1
                 t_c = time.perf_counter()
+                args = (dev, ctypes.c_void_p(depth.ptr.value + 4 * lo * HW), MQR_DEVICE, hi - lo, H, W,
+                        ptr(Kf[lo:hi], _lib._f32p), ptr(Tc[lo:hi], _lib._f32p), ptr(Ti[lo:hi], _lib._f32p),
+                        ptr(ok8[lo:hi], _lib._u8p), a - lo, b - lo, r, float(config.depth_max),
+                        float(config.error_threshold))
                 try:
-                    call("mqr_confidence", dev, ctypes.c_void_p(depth.ptr.value + 4 * lo * HW), MQR_DEVICE, hi - lo,
-                         H, W, ptr(Kf[lo:hi], _lib._f32p), ptr(Tc[lo:hi], _lib._f32p), ptr(Ti[lo:hi], _lib._f32p),
-                         ptr(ok8[lo:hi], _lib._u8p), a - lo, b - lo, r, float(config.depth_max),
-                         float(config.error_threshold), ptr(conf), ptr(valid), MQR_HOST)
+                    packed = ctypes.c_int(0)
+                    if use_counts:
+                        call("mqr_confidence_counts", *args, ptr(maps[0]), ctypes.byref(packed))
+                    if not packed.value:  # the maps themselves
+                        if use_counts:  # (a pixel with more than 255 valid neighbours: not reached for 2r <= 255)
+                            maps = (np.empty((b - a, H, W), np.float64), np.empty((b - a, H, W), np.int32))
+                        call("mqr_confidence", *args, ptr(maps[0]), ptr(maps[1]), MQR_HOST)
                 except Exception as e:  # noqa: BLE001 -- every reference frame of the run failed
                     for i in refs:
                         _report(side, i, ts[i], e)
@@ -283,7 +309,7 @@ def _estimate_side_native(depth_data_io, config, side, dataset, todo, K, T_cw, T
                     times["compute"] += time.perf_counter() - t_c
                 want = set(refs)
                 names = [os.fsencode(str(conf_path(ts[i]))) if i in want else None for i in range(a, b)]
-                pending.append(writer.submit(write, a, names, conf, valid))
+                pending.append(writer.submit(write, a, names, maps))
                 settle(2)  # at most two runs' maps held for writing
         settle(0)
     t0 = time.perf_counter()

@@ -177,3 +177,36 @@ def test_read_frames_masked_matches_the_decode_mask(tmp_path, shape):
             d = np.load(confs[i])
             want = (d["confidence_map"] < thr) | (d["valid_count"] < vthr)
             assert np.array_equal(mask[i], want.astype(np.uint8))
+
+
+@pytest.mark.parametrize("threads", [1, 4])
+def test_write_confidence_npz_counts_equals_np_savez_of_the_maps(tmp_path, threads):
+    """mqr_write_confidence_npz_counts: files byte-identical (members) to np.savez of the maps the
+    reference builds from the two counts -- confidence_map = np.true_divide(consistent, valid), 0 where
+    valid is 0, valid_count int32 (estimate_depth_confidences.py:41-79) -- for every (valid, consistent)
+    pair of the byte range; a null path writes nothing."""
+    import zipfile
+    lib = _lib()
+    H, W = 256, 257
+    v, k = np.meshgrid(np.arange(256), np.arange(257), indexing="ij")
+    k = np.minimum(k, v)
+    n = 3
+    valid = np.stack([v, np.roll(v, 1, 0), np.roll(v, 5, 1)]).astype(np.int32)
+    cons = np.stack([k, np.roll(k, 1, 0), np.roll(k, 5, 1)]).astype(np.int32)
+    counts = (valid | cons << 8).astype(np.uint16)
+    paths = [tmp_path / f"{i}.npz" for i in range(n)]
+    pp = (ctypes.c_char_p * (n + 1))(*[os.fsencode(str(p)) for p in paths], None)
+    counts = np.concatenate([counts, counts[:1]])
+    st = np.full(n + 1, -1, np.int32)
+    lib.call("mqr_write_confidence_npz_counts", n + 1, pp, lib.ptr(counts), H, W, lib.ptr(st), threads)
+    assert (st == 0).all() and sorted(p.name for p in tmp_path.iterdir()) == ["0.npz", "1.npz", "2.npz"]
+    for i in range(n):
+        with np.errstate(divide="ignore", invalid="ignore"):
+            conf = np.true_divide(cons[i], valid[i])
+        conf[valid[i] == 0] = 0.0
+        ref = tmp_path / f"ref{i}.npz"
+        np.savez(ref, confidence_map=conf, valid_count=valid[i])
+        with zipfile.ZipFile(ref) as a, zipfile.ZipFile(paths[i]) as b:
+            assert b.testzip() is None and a.namelist() == b.namelist()
+            for name in a.namelist():
+                assert a.read(name) == b.read(name)

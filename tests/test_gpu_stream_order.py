@@ -135,3 +135,35 @@ def test_caller_stream_is_set_per_call():
     _lib.set_stream(_lib.torch_stream())
     _lib.call("mqr_get_stream", ctypes.byref(got))
     assert (got.value or 0) == torch.cuda.current_stream().cuda_stream
+
+
+def test_confidence_counts_after_side_stream_write():
+    """mqr_confidence_counts (the maps as (valid, consistent) byte pairs, csrc/confpack.hip) on frames that
+    land late on a side stream: the pairs expand to the oracle's maps exactly -- confidence_map =
+    consistent / valid in float64, 0 where valid is 0 -- for every reference frame."""
+    import torch
+    from mqr import _lib, synthetic
+    seq = synthetic.make_sequence("room", n=9, height=120, width=160, f=131.25, noise=True, seed=6)
+    B, H, W = seq["depth"].shape
+    Tcw = np.ascontiguousarray(seq["T_cw"].astype(np.float32).reshape(B, 16))
+    Tci = np.ascontiguousarray(np.linalg.inv(seq["T_cw"]).astype(np.float32).reshape(B, 16))
+    K32 = np.ascontiguousarray(seq["K"], np.float32)
+    s = torch.cuda.Stream()
+    dev = _late_copy(torch, np.ascontiguousarray(seq["depth"], np.float32), s)
+    r, a, b = 3, 1, B - 1
+    counts = np.full((b - a, H, W), 0xFFFF, np.uint16)
+    packed = ctypes.c_int(-1)
+    with torch.cuda.stream(s):
+        _lib.call("mqr_confidence_counts", 0, ctypes.c_void_p(dev.data_ptr()), _lib.MQR_DEVICE, B, H, W,
+                  _lib.ptr(K32, _lib._f32p), _lib.ptr(Tcw, _lib._f32p), _lib.ptr(Tci, _lib._f32p), None, a, b, r,
+                  3.0, 0.05, _lib.ptr(counts), ctypes.byref(packed))
+    assert packed.value == 1
+    valid = (counts & 0xFF).astype(np.int32)
+    cons = (counts >> 8).astype(np.int32)
+    assert (cons <= valid).all() and valid.max() <= 2 * r
+    for i in range(a, b):
+        oc, ov = oracle.confidence(seq["depth"], seq["K"], seq["T_cw"], np.linalg.inv(seq["T_cw"]), i, r, 3.0, 0.05)
+        with np.errstate(divide="ignore", invalid="ignore"):
+            c = np.true_divide(cons[i - a], valid[i - a])
+        c[valid[i - a] == 0] = 0.0
+        assert np.array_equal(valid[i - a], ov) and np.array_equal(c.view(np.uint64), oc.view(np.uint64)), i
