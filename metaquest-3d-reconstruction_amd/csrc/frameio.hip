@@ -24,6 +24,7 @@
 #include <cstdint>
 #include <cstring>
 #include <string>
+#include <functional>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -287,20 +288,52 @@ std::string npy_header(const char* descr, int H, int W) {
 
 // One np.savez-layout npz: stored members in the given order, each a local header with a zip64 extra
 // field (np.savez opens its members with force_zip64), then the central directory and end record.
+// A member's array bytes come from `data`, or, when `fill` is set, are produced block by block: fill(off, n,
+// dst) writes bytes [off, off + n) of the array to dst (whole items), each block checksummed and written
+// while it is in cache.
 struct NpzMember {
     const char* name;
     std::string npy;  // .npy header
     const void* data;
     size_t bytes;
+    std::function<void(size_t, size_t, void*)> fill = nullptr;
 };
 
+// The CRC of the header + array of member m, written at data_off (the array) -- from the caller's bytes or
+// through fill's blocks.
+bool put_member_data(int fd, const NpzMember& m, int64_t data_off, uint32_t& crc) {
+    crc = crc32_of(0, m.npy.data(), m.npy.size());
+    if (!m.fill) {
+        crc = crc32_of(crc, m.data, m.bytes);
+        return pwrite_all(fd, m.data, m.bytes, data_off);
+    }
+    constexpr size_t kBlock = size_t(1) << 17;
+    thread_local std::vector<uint64_t> blk(kBlock / 8);
+    for (size_t o = 0; o < m.bytes; o += kBlock) {
+        const size_t k = std::min(kBlock, m.bytes - o);
+        m.fill(o, k, blk.data());
+        crc = crc32_of(crc, blk.data(), k);
+        if (!pwrite_all(fd, blk.data(), k, data_off + (int64_t)o)) return false;
+    }
+    return true;
+}
+
 int write_npz(const char* path, NpzMember* m, int nm) {
+    const int fd = ::open(path, O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+    if (fd < 0) return errno ? errno : EIO;
+    // the array bytes first (their CRCs go into the headers), then the headers, directory and end record
     int64_t off = 0;
     std::vector<int64_t> lh_off(nm);
     std::vector<uint32_t> crc(nm);
     std::vector<std::string> lh(nm);
+    bool ok = true;
     for (int i = 0; i < nm; ++i) {
-        crc[i] = crc32_of(crc32_of(0, m[i].npy.data(), m[i].npy.size()), m[i].data, m[i].bytes);
+        lh_off[i] = off;
+        const size_t lh_size = 30 + strlen(m[i].name) + 20;
+        ok = ok && put_member_data(fd, m[i], off + (int64_t)(lh_size + m[i].npy.size()), crc[i]);
+        off += (int64_t)(lh_size + m[i].npy.size() + m[i].bytes);
+    }
+    for (int i = 0; i < nm; ++i) {
         const uint64_t size = m[i].npy.size() + m[i].bytes;
         std::string& h = lh[i];
         put32(h, 0x04034b50u);
@@ -319,8 +352,6 @@ int write_npz(const char* path, NpzMember* m, int nm) {
         put16(h, 16);
         put64(h, size);
         put64(h, size);
-        lh_off[i] = off;
-        off += (int64_t)(h.size() + size);
     }
     std::string cd;
     for (int i = 0; i < nm; ++i) {
@@ -378,13 +409,9 @@ int write_npz(const char* path, NpzMember* m, int nm) {
     put32(end, (uint32_t)cd.size());
     put32(end, cd_off >= 0xFFFFFFFFll ? 0xFFFFFFFFu : (uint32_t)cd_off);
     put16(end, 0);
-    const int fd = ::open(path, O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
-    if (fd < 0) return errno ? errno : EIO;
-    bool ok = true;
     for (int i = 0; i < nm && ok; ++i) {
         ok = pwrite_all(fd, lh[i].data(), lh[i].size(), lh_off[i]) &&
-             pwrite_all(fd, m[i].npy.data(), m[i].npy.size(), lh_off[i] + (int64_t)lh[i].size()) &&
-             pwrite_all(fd, m[i].data, m[i].bytes, lh_off[i] + (int64_t)(lh[i].size() + m[i].npy.size()));
+             pwrite_all(fd, m[i].npy.data(), m[i].npy.size(), lh_off[i] + (int64_t)lh[i].size());
     }
     ok = ok && pwrite_all(fd, cd.data(), cd.size(), cd_off) &&
          pwrite_all(fd, end.data(), end.size(), cd_off + (int64_t)cd.size());
@@ -492,20 +519,24 @@ int mqr_write_confidence_npz_counts(int n, const char* const* paths, const uint1
     const std::string h_conf = npy_header("<f8", H, W), h_valid = npy_header("<i4", H, W);
     std::atomic<int> next{0};
     auto work = [&] {
-        std::vector<double> conf(HW);
-        std::vector<int32_t> valid(HW);
         for (int f; (f = next.fetch_add(1)) < n;) {
             if (!paths[f]) {
                 status[f] = 0;
                 continue;
             }
             const uint16_t* c = counts + (size_t)f * HW;
-            for (size_t i = 0; i < HW; ++i) {
-                conf[i] = table[c[i]];
-                valid[i] = c[i] & 0xFF;
-            }
-            NpzMember m[2] = {{"confidence_map.npy", h_conf, conf.data(), 8 * HW},
-                              {"valid_count.npy", h_valid, valid.data(), 4 * HW}};
+            // the maps expanded block by block into the writer's cache-resident buffer
+            NpzMember m[2] = {{"confidence_map.npy", h_conf, nullptr, 8 * HW,
+                               [c](size_t off, size_t nb, void* dst) {
+                                   double* d = static_cast<double*>(dst);
+                                   const uint16_t* s = c + off / 8;
+                                   for (size_t i = 0; i < nb / 8; ++i) d[i] = table[s[i]];
+                               }},
+                              {"valid_count.npy", h_valid, nullptr, 4 * HW, [c](size_t off, size_t nb, void* dst) {
+                                   int32_t* d = static_cast<int32_t*>(dst);
+                                   const uint16_t* s = c + off / 4;
+                                   for (size_t i = 0; i < nb / 4; ++i) d[i] = s[i] & 0xFF;
+                               }}};
             status[f] = write_npz(paths[f], m, 2);
         }
     };

@@ -34,17 +34,29 @@ def main():
                                               skip_if_output_dir_exists=False, device=0)
         estimate_depth_confidences(io_, cfg, sides=[Side.LEFT])  # warm-up
         shutil.rmtree(os.path.join(tmp, "left_depth_confidence"), ignore_errors=True)
+        import gc
+        gc_ms = []
+        gc_t = {}
+
+        def on_gc(phase, info):  # the collector's own passes during the profiled call
+            if phase == "start":
+                gc_t["t"] = time.perf_counter()
+            else:
+                gc_ms.append((info["generation"], (time.perf_counter() - gc_t["t"]) * 1e3))
+        gc.callbacks.append(on_gc)
         pr = cProfile.Profile()
         t0 = time.perf_counter()
         pr.enable()
         estimate_depth_confidences(io_, cfg, sides=[Side.LEFT])
         pr.disable()
         wall = time.perf_counter() - t0
+        gc.callbacks.remove(on_gc)
         for key in ("cumulative", "tottime"):
             buf = io.StringIO()
             pstats.Stats(pr, stream=buf).sort_stats(key).print_stats(22)
             print(f"== {key}\n" + buf.getvalue(), file=sys.stderr)
-        print(json.dumps({"wall_s": wall, "split_s": dict(confidence.last_confidence_times.__dict__)}), flush=True)
+        print(json.dumps({"wall_s": wall, "split_s": dict(confidence.last_confidence_times.__dict__),
+                          "gc_passes_ms": gc_ms}), flush=True)
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
 
