@@ -200,10 +200,12 @@ def _native_paths(depth_data_io, side, dataset):
 def _estimate_side_native(depth_data_io, config, side, dataset, todo, K, T_cw, T_inv, paths, times) -> bool:
     """One side, device-resident: the raw files read by native threads (mqr_read_frames), decoded on the
     GPU once into an HBM array of all frames (mqr_decode_depth: the reference's is_depth_map_valid and
-    convert_depth_to_linear, bit for bit), the confidence kernel run on device windows of it, each run's
-    maps downloaded and written by native threads (mqr_write_confidence_npz: np.savez's files) while the
-    next run computes.  Returns False, before anything is written, when a raw file needs the Python
-    reader (wrong size, unreadable): the caller then takes the standard path for the side."""
+    convert_depth_to_linear, bit for bit), the confidence kernel run on device windows of it as soon as a
+    window is decoded, each run's maps downloaded and written by native threads (mqr_write_confidence_npz:
+    np.savez's files) while the next frames are read and the next run computes.  Returns False when a raw
+    file needs the Python reader: a file of the wrong size before anything is written; a read error later
+    leaves the runs already written (windows read in full, so their files are what the standard path writes)
+    -- the caller then takes the standard path for the side."""
     from concurrent.futures import ThreadPoolExecutor
 
     from ._io import io_threads
@@ -217,39 +219,32 @@ def _estimate_side_native(depth_data_io, config, side, dataset, todo, K, T_cw, T
     r = int(config.target_frame_range)
     ts = dataset.timestamps
     t0 = time.perf_counter()
+    raw_names = [os.fsencode(str(raw_path(t))) for t in ts]
+    for name in raw_names:  # a raw file of the wrong size: the standard path reads (or rejects) it
+        try:
+            if os.stat(name).st_size != 4 * HW:
+                return False
+        except FileNotFoundError:
+            pass  # missing: decoded invalid, as the reference skips it
+    times["scan"] += time.perf_counter() - t0
+    t0 = time.perf_counter()
     depth = DeviceBuffer(4 * n * HW, dev)
     times["alloc"] = times.get("alloc", 0.0) + time.perf_counter() - t0
-    t0 = time.perf_counter()
     ok = np.zeros(n, bool)
     stages = _raw_stages(min(_READ_CHUNK, n), H, W)
+    Kf = np.ascontiguousarray(K, dtype=np.float32).reshape(n, 9)
+    Tc = np.ascontiguousarray(T_cw, dtype=np.float32).reshape(n, 16)
+    Ti = np.ascontiguousarray(T_inv, dtype=np.float32).reshape(n, 16)
+    ok8 = np.zeros(n, np.uint8)
+    if todo:
+        conf_path(ts[todo[0]]).parent.mkdir(parents=True, exist_ok=True)
 
     def read(c0, st):
         c1 = min(n, c0 + _READ_CHUNK)
         status = np.zeros(c1 - c0, np.uint8)
-        names = (ctypes.c_char_p * (c1 - c0))(*[os.fsencode(str(raw_path(ts[i]))) for i in range(c0, c1)])
+        names = (ctypes.c_char_p * (c1 - c0))(*raw_names[c0:c1])
         call("mqr_read_frames", c1 - c0, names, None, H, W, ptr(st), None, None, ptr(status), io_threads())
         return c0, c1, st, status
-
-    with ThreadPoolExecutor(max_workers=1) as reader:
-        fut = reader.submit(read, 0, stages[0])
-        turn = 0
-        while fut is not None:
-            c0, c1, st, status = fut.result()
-            if (status & _lib.MQR_FRAME_RAW_OTHER).any():
-                depth.free()
-                return False
-            turn ^= 1
-            fut = reader.submit(read, c1, stages[turn]) if c1 < n else None
-            _, ok[c0:c1] = decode_depth_frames(st[:c1 - c0], [dataset.nears[i] for i in range(c0, c1)],
-                                               [dataset.fars[i] for i in range(c0, c1)], device=dev,
-                                               out_ptr=depth.ptr.value + 4 * c0 * HW)
-    times["decode"] += time.perf_counter() - t0
-    Kf = np.ascontiguousarray(K, dtype=np.float32).reshape(n, 9)
-    Tc = np.ascontiguousarray(T_cw, dtype=np.float32).reshape(n, 16)
-    Ti = np.ascontiguousarray(T_inv, dtype=np.float32).reshape(n, 16)
-    ok8 = ok.astype(np.uint8)
-    if todo:
-        conf_path(ts[todo[0]]).parent.mkdir(parents=True, exist_ok=True)
 
     def write(a, names, maps):
         status = np.zeros(len(names), np.int32)
@@ -268,6 +263,7 @@ def _estimate_side_native(depth_data_io, config, side, dataset, todo, K, T_cw, T
     use_counts = COUNT_PAIRS and 2 * r <= 255
     outs = _map_sets(H, W, use_counts)
     runs = 0
+    next_c0 = 0  # the first chunk of `todo` not computed yet
 
     def settle(keep):
         t_s = time.perf_counter()
@@ -285,8 +281,12 @@ def _estimate_side_native(depth_data_io, config, side, dataset, todo, K, T_cw, T
                 _report(side, i, ts[i], e)
         times["write_wait"] += time.perf_counter() - t_s
 
-    with ThreadPoolExecutor(max_workers=1) as writer:
-        for c0 in range(0, len(todo), REF_CHUNK):
+    def compute_ready(limit):
+        """The chunks of `todo` whose windows lie in the frames decoded so far ([0, limit))."""
+        nonlocal next_c0, runs
+        while next_c0 < len(todo) and (limit == n or todo[min(len(todo), next_c0 + REF_CHUNK) - 1] + r + 1 <= limit):
+            c0 = next_c0
+            next_c0 += REF_CHUNK
             chunk = [i for i in todo[c0:c0 + REF_CHUNK] if ok[i]]  # invalid refs: no output
             j = 0
             while j < len(chunk):  # runs spanning < REF_CHUNK indices, as the standard path groups them
@@ -322,6 +322,25 @@ def _estimate_side_native(depth_data_io, config, side, dataset, todo, K, T_cw, T
                 names = [os.fsencode(str(conf_path(ts[i]))) if i in want else None for i in range(a, b)]
                 pending.append(writer.submit(write, a, names, maps))
                 settle(2)  # at most two runs' maps held for writing
+
+    with ThreadPoolExecutor(max_workers=1) as reader, ThreadPoolExecutor(max_workers=1) as writer:
+        fut = reader.submit(read, 0, stages[0])
+        turn = 0
+        while fut is not None:
+            t0 = time.perf_counter()
+            c0, c1, st, status = fut.result()
+            if (status & _lib.MQR_FRAME_RAW_OTHER).any():
+                settle(0)
+                depth.free()
+                return False
+            turn ^= 1
+            fut = reader.submit(read, c1, stages[turn]) if c1 < n else None
+            _, ok[c0:c1] = decode_depth_frames(st[:c1 - c0], [dataset.nears[i] for i in range(c0, c1)],
+                                               [dataset.fars[i] for i in range(c0, c1)], device=dev,
+                                               out_ptr=depth.ptr.value + 4 * c0 * HW)
+            ok8[c0:c1] = ok[c0:c1]
+            times["decode"] += time.perf_counter() - t0
+            compute_ready(c1)
         settle(0)
     t0 = time.perf_counter()
     depth.free()
