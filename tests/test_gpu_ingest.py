@@ -109,3 +109,27 @@ def test_decode_byte_mask_equals_the_map_mask(shape):
     c, ok_c = decode_depth_frames(raw, nears, fars, mask=np.ones((N, H, W), np.uint8), has_mask=None)
     d, _ = decode_depth_frames(raw, nears, fars)
     assert np.array_equal(c.view(np.uint32), d.view(np.uint32)) and np.array_equal(ok_c, ok_a)
+
+
+def test_decode_byte_mask_device_resident():
+    """mqr_decode_depth_masked with raw frames, mask bytes and output all in HBM (MQR_DEVICE)."""
+    import ctypes
+    from mqr import _lib
+    from mqr._lib import DeviceBuffer
+    from mqr.ingest import decode_depth_frames
+    rng = np.random.default_rng(12)
+    N, H, W = 3, 60, 80
+    raw = rng.random((N, H, W)).astype(np.float32)
+    m8 = (rng.random((N, H, W)) < 0.3).astype(np.uint8)
+    has = np.array([1, 0, 1], np.uint8)
+    nears = np.full(N, 0.1, np.float64)
+    fars = np.full(N, np.inf, np.float64)
+    r_buf, m_buf, o_buf = DeviceBuffer.from_array(raw), DeviceBuffer.from_array(m8), DeviceBuffer(raw.nbytes)
+    ok = np.zeros(N, np.uint8)
+    _lib.call("mqr_decode_depth_masked", 0, r_buf.ptr, _lib.MQR_DEVICE, N, H, W, _lib.ptr(nears, _lib._f64p),
+              _lib.ptr(fars, _lib._f64p), None, m_buf.ptr, _lib.ptr(has, _lib._u8p), _lib.MQR_DEVICE, o_buf.ptr,
+              _lib.MQR_DEVICE, _lib.ptr(ok, _lib._u8p))
+    got = o_buf.to_array(raw.shape, np.float32)
+    ref, ref_ok = decode_depth_frames(raw, [0.1] * N, [np.inf] * N, mask=m8, has_mask=has.astype(bool))
+    assert np.array_equal(ok.astype(bool), ref_ok) and np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+    assert (got[0][m8[0] != 0] == 0).all() and np.array_equal(got[1], ref[1])
