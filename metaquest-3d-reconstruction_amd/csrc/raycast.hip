@@ -36,6 +36,8 @@ struct mqr_scene {
     int64_t ntri = 0;
     float4* leaf = nullptr;     // [ntri][3]: (v0, prim id bits), (e1, geom id bits), (e2, 0)
     float4* node = nullptr;     // [ntri-1][4]: lo0, hi0, lo1, hi1 (w of lo0/lo1 = child index bits)
+    void* bvh_blk = nullptr;    // leaf and node: one block of the device-block cache (geom_block_alloc)
+    size_t bvh_cap = 0;
 };
 
 namespace mqr {
@@ -407,12 +409,15 @@ __global__ __launch_bounds__(256) void k_cast_rays(const float4* __restrict__ no
 
 // ------------------------------------------------------------------ host
 static void free_built(mqr_scene* s) {
-    if (s->leaf) (void)hipFree(s->leaf);
-    if (s->node) (void)hipFree(s->node);
+    geom_block_release(s->device, s->bvh_blk, s->bvh_cap);
+    s->bvh_blk = nullptr;
+    s->bvh_cap = 0;
     s->leaf = nullptr;
     s->node = nullptr;
     s->built = false;
 }
+
+static size_t al256(size_t x) { return (x + 255) & ~size_t(255); }
 
 static int build(mqr_scene* s) {
     if (s->built) return 0;
@@ -422,18 +427,49 @@ static int build(mqr_scene* s) {
     MQR_REQUIRE(n > 0, "raycasting scene has no triangles");
     MQR_REQUIRE(n < (int64_t)1 << 30, "raycasting scene too large (>= 2^30 triangles)");
     hipStream_t st = s->stream;
-    BuildTri* tris = nullptr;
-    uint32_t *prim = nullptr, *gid = nullptr, *cb = nullptr, *idx = nullptr, *idx_sorted = nullptr;
-    uint64_t *keys = nullptr, *keys_sorted = nullptr;
-    int32_t *child = nullptr, *parent = nullptr;
-    int *arrivals = nullptr, *bad = nullptr;
-    void* tmp = nullptr;
-    size_t tmp_bytes = 0;
     int rc = 0;
+    // Every temporary of the build carved from one block of the process's device-block cache
+    // (geom_block_alloc), and the scene's leaf / node arrays from another: a rebuild or the next scene's
+    // build reuses them instead of 15 hipMalloc / hipFree pairs: 2.93 -> 1.01 ms per build of a 2.1 M-triangle
+    // mesh, the kernels' own 1.06 ms (tools/bvh_build_probe.py, profiles/r05_bvh_build_probe.json).
+    const int64_t m1 = std::max<int64_t>(n - 1, 1);
+    size_t sort_bytes = 0, depth_sort_bytes = 0;
+    MQR_CHECK_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, sort_bytes, (const uint64_t*)nullptr, (uint64_t*)nullptr,
+                                                     (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n, 0, 63, st));
+    MQR_CHECK_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, depth_sort_bytes, (const uint32_t*)nullptr,
+                                                     (uint32_t*)nullptr, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                                     (int)m1, 0, 8, st));
+    const size_t tmp_bytes = std::max(sort_bytes, depth_sort_bytes) + 16;
+    const size_t sizes[] = {al256(sizeof(BuildTri) * n), al256(4 * n), al256(4 * n), al256(4 * 6), al256(4 * n),
+                            al256(4 * n), al256(8 * n), al256(8 * n), al256(8 * m1), al256(8 * n),
+                            al256(4 * std::max<int64_t>(m1, 512)), al256(4), al256(tmp_bytes)};
+    size_t total = 0;
+    for (size_t z : sizes) total += z;
+    size_t blk_cap = 0;
+    void* blk = geom_block_alloc(s->device, total, &blk_cap);
+    MQR_REQUIRE(blk, "raycasting scene: device allocation failed");
+    char* q = static_cast<char*>(blk);
+    auto carve = [&](int i) {
+        char* r = q;
+        q += sizes[i];
+        return r;
+    };
+    BuildTri* tris = reinterpret_cast<BuildTri*>(carve(0));
+    uint32_t* prim = reinterpret_cast<uint32_t*>(carve(1));
+    uint32_t* gid = reinterpret_cast<uint32_t*>(carve(2));
+    uint32_t* cb = reinterpret_cast<uint32_t*>(carve(3));
+    uint32_t* idx = reinterpret_cast<uint32_t*>(carve(4));
+    uint32_t* idx_sorted = reinterpret_cast<uint32_t*>(carve(5));
+    uint64_t* keys = reinterpret_cast<uint64_t*>(carve(6));
+    uint64_t* keys_sorted = reinterpret_cast<uint64_t*>(carve(7));
+    int32_t* child = reinterpret_cast<int32_t*>(carve(8));
+    int32_t* parent = reinterpret_cast<int32_t*>(carve(9));
+    int* arrivals = reinterpret_cast<int*>(carve(10));
+    int* bad = reinterpret_cast<int*>(carve(11));
+    void* tmp = carve(12);
     auto cleanup = [&]() {
-        for (void* p : {(void*)tris, (void*)prim, (void*)gid, (void*)cb, (void*)idx, (void*)idx_sorted, (void*)keys,
-                        (void*)keys_sorted, (void*)child, (void*)parent, (void*)arrivals, (void*)bad, tmp})
-            if (p) (void)hipFree(p);
+        (void)hipStreamSynchronize(st);  // (the block goes back to the cache: no kernel of this build may still use it)
+        geom_block_release(s->device, blk, blk_cap);
     };
 #define RC_HIP(expr)                                                           \
     do {                                                                       \
@@ -444,18 +480,6 @@ static int build(mqr_scene* s) {
             return 1;                                                          \
         }                                                                      \
     } while (0)
-    RC_HIP(hipMalloc(&tris, sizeof(BuildTri) * n));
-    RC_HIP(hipMalloc(&prim, sizeof(uint32_t) * n));
-    RC_HIP(hipMalloc(&gid, sizeof(uint32_t) * n));
-    RC_HIP(hipMalloc(&cb, sizeof(uint32_t) * 6));
-    RC_HIP(hipMalloc(&idx, sizeof(uint32_t) * n));
-    RC_HIP(hipMalloc(&idx_sorted, sizeof(uint32_t) * n));
-    RC_HIP(hipMalloc(&keys, sizeof(uint64_t) * n));
-    RC_HIP(hipMalloc(&keys_sorted, sizeof(uint64_t) * n));
-    RC_HIP(hipMalloc(&child, sizeof(int32_t) * 2 * std::max<int64_t>(n - 1, 1)));
-    RC_HIP(hipMalloc(&parent, sizeof(int32_t) * (2 * n)));
-    RC_HIP(hipMalloc(&arrivals, sizeof(int) * std::max<int64_t>(n - 1, 1)));
-    RC_HIP(hipMalloc(&bad, sizeof(int)));
     const uint32_t init[6] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0u, 0u, 0u};
     RC_HIP(hipMemcpyAsync(cb, init, sizeof(init), hipMemcpyHostToDevice, st));
     RC_HIP(hipMemsetAsync(bad, 0, sizeof(int), st));
@@ -474,12 +498,19 @@ static int build(mqr_scene* s) {
     const unsigned gb = (unsigned)((n + 255) / 256);
     hipLaunchKernelGGL(k_morton, dim3(gb), dim3(256), 0, st, tris, n, cb, keys, idx);
     RC_HIP(hipGetLastError());
-    RC_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, keys, keys_sorted, idx, idx_sorted, (int)n, 0, 63,
-                                              st));
-    RC_HIP(hipMalloc(&tmp, tmp_bytes + 16));
-    RC_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, keys, keys_sorted, idx, idx_sorted, (int)n, 0, 63, st));
-    RC_HIP(hipMalloc(&s->leaf, sizeof(float4) * 3 * n));
-    RC_HIP(hipMalloc(&s->node, sizeof(float4) * 4 * std::max<int64_t>(n - 1, 1)));
+    size_t sb = sort_bytes;
+    RC_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, sb, keys, keys_sorted, idx, idx_sorted, (int)n, 0, 63, st));
+    {
+        const size_t sl = al256(sizeof(float4) * 3 * n);
+        s->bvh_blk = geom_block_alloc(s->device, sl + sizeof(float4) * 4 * m1, &s->bvh_cap);
+        if (!s->bvh_blk) {
+            set_error("raycasting scene: device allocation failed");
+            cleanup();
+            return 1;
+        }
+        s->leaf = static_cast<float4*>(s->bvh_blk);
+        s->node = reinterpret_cast<float4*>(static_cast<char*>(s->bvh_blk) + sl);
+    }
     if (n > 1) {
         hipLaunchKernelGGL(k_radix_tree, dim3((unsigned)((n - 1 + 255) / 256)), dim3(256), 0, st, keys_sorted, n,
                            child, parent);
@@ -495,26 +526,12 @@ static int build(mqr_scene* s) {
         uint32_t* depth_s = depth + m;
         uint32_t* ids = reinterpret_cast<uint32_t*>(keys_sorted);
         uint32_t* ids_s = ids + m;
-        int* lvl = arrivals;  // 512 ints: start[256], end[256] (arrivals has n - 1 >= 512 slots or is regrown)
-        if (m < 512) {
-            RC_HIP(hipFree(arrivals));
-            arrivals = nullptr;
-            RC_HIP(hipMalloc(&arrivals, sizeof(int) * 512));
-            lvl = arrivals;
-        }
+        int* lvl = arrivals;  // 512 ints: start[256], end[256] (arrivals has max(n - 1, 512) slots)
         RC_HIP(hipMemsetAsync(lvl, 0, sizeof(int) * 512, st));
         const unsigned gm = (unsigned)((m + 255) / 256);
         hipLaunchKernelGGL(k_node_depth, dim3(gm), dim3(256), 0, st, parent, m, depth, ids, bad);
         RC_HIP(hipGetLastError());
-        size_t sb = 0;
-        RC_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, sb, depth, depth_s, ids, ids_s, (int)m, 0, 8, st));
-        if (sb > tmp_bytes + 16) {
-            RC_HIP(hipFree(tmp));
-            tmp = nullptr;
-            RC_HIP(hipMalloc(&tmp, sb));
-        } else {
-            sb = tmp_bytes + 16;
-        }
+        sb = depth_sort_bytes;
         RC_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, sb, depth, depth_s, ids, ids_s, (int)m, 0, 8, st));
         hipLaunchKernelGGL(k_level_bounds, dim3(gm), dim3(256), 0, st, depth_s, m, lvl, lvl + 256);
         RC_HIP(hipGetLastError());
