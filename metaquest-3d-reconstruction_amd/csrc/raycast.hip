@@ -419,6 +419,24 @@ static void free_built(mqr_scene* s) {
 
 static size_t al256(size_t x) { return (x + 255) & ~size_t(255); }
 
+// A cast's device staging: one block of the device-block cache (geom_block_alloc) carved into 256-byte
+// aligned pieces, returned to the cache at scope exit -- after the call's stream synchronisation -- instead
+// of a hipMalloc / hipFree pair per array per call.
+struct CachedBlock {
+    int device;
+    void* p = nullptr;
+    size_t cap = 0, used = 0;
+    CachedBlock(int d, size_t bytes) : device(d) { p = geom_block_alloc(d, std::max<size_t>(bytes, 256), &cap); }
+    ~CachedBlock() { geom_block_release(device, p, cap); }
+    CachedBlock(const CachedBlock&) = delete;
+    CachedBlock& operator=(const CachedBlock&) = delete;
+    void* take(size_t b) {
+        char* r = static_cast<char*>(p) + used;
+        used += al256(b);
+        return r;
+    }
+};
+
 static int build(mqr_scene* s) {
     if (s->built) return 0;
     free_built(s);
@@ -680,22 +698,21 @@ int mqr_scene_cast_pinhole(mqr_scene* s, const double* K, const double* T_wc, in
     if (out_loc == MQR_DEVICE && order_after_caller(s->device, s->stream)) return 2;
     std::vector<PinholeFrame> hf(n_frames);
     for (int f = 0; f < n_frames; ++f) hf[f] = pinhole(K + 9 * f, T_wc + 16 * f);
-    PinholeFrame* d_fr = nullptr;
     float *d_t = t_hit, *d_uv = uvs, *d_n = normals;
     uint32_t *d_g = geom_ids, *d_p = prim_ids;
-    std::vector<void*> owned;
-    auto dalloc = [&](size_t bytes) {
-        void* p = nullptr;
-        if (hipMalloc(&p, bytes) == hipSuccess) owned.push_back(p);
-        return p;
-    };
-    bool ok = (d_fr = (PinholeFrame*)dalloc(sizeof(PinholeFrame) * n_frames)) != nullptr;
-    if (out_loc != MQR_DEVICE) {
-        ok = ok && (d_t = (float*)dalloc(sizeof(float) * total));
-        if (geom_ids) ok = ok && (d_g = (uint32_t*)dalloc(sizeof(uint32_t) * total));
-        if (prim_ids) ok = ok && (d_p = (uint32_t*)dalloc(sizeof(uint32_t) * total));
-        if (uvs) ok = ok && (d_uv = (float*)dalloc(sizeof(float) * 2 * total));
-        if (normals) ok = ok && (d_n = (float*)dalloc(sizeof(float) * 3 * total));
+    const bool host_out = out_loc != MQR_DEVICE;
+    const size_t per_px = host_out ? 4 + (geom_ids ? 4 : 0) + (prim_ids ? 4 : 0) + (uvs ? 8 : 0) +
+                                         (normals ? 12 : 0)
+                                   : 0;
+    CachedBlock blk(s->device, al256(sizeof(PinholeFrame) * n_frames) + per_px * total + 5 * 256);
+    bool ok = blk.p != nullptr;
+    PinholeFrame* d_fr = ok ? (PinholeFrame*)blk.take(sizeof(PinholeFrame) * n_frames) : nullptr;
+    if (ok && host_out) {
+        d_t = (float*)blk.take(sizeof(float) * total);
+        if (geom_ids) d_g = (uint32_t*)blk.take(sizeof(uint32_t) * total);
+        if (prim_ids) d_p = (uint32_t*)blk.take(sizeof(uint32_t) * total);
+        if (uvs) d_uv = (float*)blk.take(sizeof(float) * 2 * total);
+        if (normals) d_n = (float*)blk.take(sizeof(float) * 3 * total);
     }
     int rc = 0;
     if (!ok) {
@@ -730,7 +747,6 @@ int mqr_scene_cast_pinhole(mqr_scene* s, const double* K, const double* T_wc, in
         set_error("cast_pinhole: kernel failed");
         rc = 1;
     }
-    for (void* p : owned) (void)hipFree(p);
     return rc;
 }
 
@@ -742,27 +758,26 @@ int mqr_scene_cast_rays(mqr_scene* s, const float* rays, int64_t nrays, int rays
     if (build(s)) return 1;
     if (nrays == 0) return 0;
     if ((rays_loc == MQR_DEVICE || out_loc == MQR_DEVICE) && order_after_caller(s->device, s->stream)) return 2;
-    std::vector<void*> owned;
-    auto dalloc = [&](size_t bytes) {
-        void* p = nullptr;
-        if (hipMalloc(&p, bytes) == hipSuccess) owned.push_back(p);
-        return p;
-    };
     const float* d_r = rays;
     float *d_t = t_hit, *d_uv = uvs, *d_n = normals;
     uint32_t *d_g = geom_ids, *d_p = prim_ids;
-    bool ok = true;
-    if (rays_loc != MQR_DEVICE) {
-        float* p = (float*)dalloc(sizeof(float) * 6 * nrays);
-        ok = p && copy_to_device(s->device, p, rays, sizeof(float) * 6 * nrays, s->stream) == 0;
+    const bool host_in = rays_loc != MQR_DEVICE, host_out = out_loc != MQR_DEVICE;
+    const size_t per_ray = (host_in ? 24 : 0) + (host_out ? 4 + (geom_ids ? 4 : 0) + (prim_ids ? 4 : 0) +
+                                                             (uvs ? 8 : 0) + (normals ? 12 : 0)
+                                                       : 0);
+    CachedBlock blk(s->device, per_ray * (size_t)nrays + 6 * 256);
+    bool ok = blk.p != nullptr;
+    if (ok && host_in) {
+        float* p = (float*)blk.take(sizeof(float) * 6 * nrays);
+        ok = copy_to_device(s->device, p, rays, sizeof(float) * 6 * nrays, s->stream) == 0;
         d_r = p;
     }
-    if (out_loc != MQR_DEVICE) {
-        ok = ok && (d_t = (float*)dalloc(sizeof(float) * nrays));
-        if (geom_ids) ok = ok && (d_g = (uint32_t*)dalloc(sizeof(uint32_t) * nrays));
-        if (prim_ids) ok = ok && (d_p = (uint32_t*)dalloc(sizeof(uint32_t) * nrays));
-        if (uvs) ok = ok && (d_uv = (float*)dalloc(sizeof(float) * 2 * nrays));
-        if (normals) ok = ok && (d_n = (float*)dalloc(sizeof(float) * 3 * nrays));
+    if (ok && host_out) {
+        d_t = (float*)blk.take(sizeof(float) * nrays);
+        if (geom_ids) d_g = (uint32_t*)blk.take(sizeof(uint32_t) * nrays);
+        if (prim_ids) d_p = (uint32_t*)blk.take(sizeof(uint32_t) * nrays);
+        if (uvs) d_uv = (float*)blk.take(sizeof(float) * 2 * nrays);
+        if (normals) d_n = (float*)blk.take(sizeof(float) * 3 * nrays);
     }
     int rc = 0;
     if (!ok) {
@@ -792,7 +807,6 @@ int mqr_scene_cast_rays(mqr_scene* s, const float* rays, int64_t nrays, int rays
         set_error("cast_rays: kernel failed");
         rc = 1;
     }
-    for (void* p : owned) (void)hipFree(p);
     return rc;
 }
 

@@ -40,7 +40,30 @@ def main():
         _lib.call("mqr_scene_build", s)
         walls.append((time.perf_counter() - t0) * 1e3)
         L.mqr_scene_destroy(s)
-    print(json.dumps({"triangles": int(t.shape[0]), "build_ms": walls}), flush=True)
+    # pinhole casts of the last scene shape: 64 VGA frames looking down at the grid, t_hit to the host
+    s = ctypes.c_void_p()
+    _lib.call("mqr_scene_create", 0, ctypes.byref(s))
+    gid = ctypes.c_uint32()
+    _lib.call("mqr_scene_add_triangles", s, _lib.ptr(v), v.shape[0], _lib.ptr(t), t.shape[0], _lib.MQR_HOST,
+              ctypes.byref(gid))
+    F, H, W = 64, 480, 640
+    K = np.tile(np.array([[500.0, 0, 320], [0, 500.0, 240], [0, 0, 1]]), (F, 1, 1))
+    T = np.tile(np.eye(4), (F, 1, 1))
+    T[:, 0, 3] = np.linspace(1.0, 3.0, F)
+    T[:, 1, 3] = 2.0
+    T[:, 2, 3] = 2.0
+    T[:, 1, 1] = T[:, 2, 2] = -1.0  # looking down -z
+    Kc, Tc = np.ascontiguousarray(K), np.ascontiguousarray(T)
+    th = np.empty((F, H, W), np.float32)
+    casts = []
+    for _ in range(7):
+        t0 = time.perf_counter()
+        _lib.call("mqr_scene_cast_pinhole", s, _lib.ptr(Kc, _lib._f64p), _lib.ptr(Tc, _lib._f64p), F, H, W,
+                  _lib.ptr(th), None, None, None, None, _lib.MQR_HOST)
+        casts.append((time.perf_counter() - t0) * 1e3)
+    L.mqr_scene_destroy(s)
+    print(json.dumps({"lib": os.environ.get("MQR_HIP_LIB", "default"), "triangles": int(t.shape[0]),
+                      "build_ms": walls, "cast64_ms": casts, "hit_fraction": float(np.isfinite(th).mean())}), flush=True)
 
 
 if __name__ == "__main__":
