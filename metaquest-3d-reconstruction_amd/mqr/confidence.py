@@ -348,6 +348,29 @@ def _estimate_side_native(depth_data_io, config, side, dataset, todo, K, T_cw, T
     return True
 
 
+def _todo(depth_data_io, side, dataset):
+    """The frames without a loadable confidence map (load_confidence_map(...) is None, as the reference
+    selects them).  With this package's DepthDataIO and its standard loader and paths, one listing of the
+    confidence directory stands in for the per-frame existence checks: only frames whose file is present go
+    through load_confidence_map (~10 us of path building and stat per frame otherwise)."""
+    from .dataio import DepthDataIO, DepthPaths
+    from .o3d_utils import _frame_paths
+    ts = dataset.timestamps
+    load = depth_data_io.load_confidence_map
+    if (isinstance(depth_data_io, DepthDataIO) and type(depth_data_io.paths) is DepthPaths
+            and _frame_paths(depth_data_io, side) is not None):
+        try:
+            present = set(os.listdir(depth_data_io.paths.confidence_dir(side)))
+        except FileNotFoundError:
+            present = set()
+        except OSError:
+            present = None
+        if present is not None:
+            return [i for i, t in enumerate(ts)
+                    if f"{int(t)}.npz" not in present or load(side=side, timestamp=t) is None]
+    return [i for i, t in enumerate(ts) if load(side=side, timestamp=t) is None]
+
+
 def estimate_depth_confidences(depth_data_io, config: DepthConfidenceEstimationConfig, sides=None):
     """Per side: skip if the output directory exists (``skip_if_output_dir_exists``), keep existing
     per-frame files, compute the rest in chunks of REF_CHUNK reference frames.  Frames are decoded
@@ -373,8 +396,7 @@ def estimate_depth_confidences(depth_data_io, config: DepthConfidenceEstimationC
         r = int(config.target_frame_range)
         times["prep"] = times.get("prep", 0.0) + time.perf_counter() - t0
         t0 = time.perf_counter()
-        todo = [i for i in range(n) if depth_data_io.load_confidence_map(side=side, timestamp=dataset.timestamps[i])
-                is None]
+        todo = _todo(depth_data_io, side, dataset)
         times["scan"] += time.perf_counter() - t0
         native = _native_paths(depth_data_io, side, dataset) if todo else None
         if native is not None and _estimate_side_native(depth_data_io, config, side, dataset, todo, K, T_cw, T_inv,
