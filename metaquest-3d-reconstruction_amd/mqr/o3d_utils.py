@@ -37,6 +37,9 @@ from .vbg import VoxelBlockGrid
 # profiles/r05_ab_dropin_chunk_staged.json); before that staging, 127 was the slower size (0.629 vs
 # 0.535 s, profiles/r05_ab_dropin_chunk.json)
 CHUNK = 127
+# frames of the first hand-off: nothing overlaps the first chunk's reads, so a short first chunk starts the
+# device sooner (A/B: profiles/r05_ab_dropin_first_chunk.json)
+FIRST_CHUNK = 32
 
 
 class _HostStage:
@@ -163,6 +166,9 @@ def integrate(dataset, depth_data_io, side, use_confidence_filtered_depth: bool,
     read_raw = _raw_reader(depth_data_io, side)
     native = _frame_paths(depth_data_io, side) if read_raw is not None else None
 
+    def chunk_end(lo):  # chunks: [0, FIRST_CHUNK), then CHUNK frames each
+        return min(n, lo + (min(FIRST_CHUNK, CHUNK) if lo == 0 else CHUNK))
+
     def load_one(i):
         if read_raw is None:
             d = _masked_depth(depth_data_io, side, i, dataset, use_confidence_filtered_depth,
@@ -182,7 +188,7 @@ def integrate(dataset, depth_data_io, side, use_confidence_filtered_depth: bool,
         """Host side of one chunk: file reads only (decode + mask run on the device), or the
         caller's own DataIO decode when it exposes no raw-buffer access; frames read by the I/O
         threads, results in frame order."""
-        hi = min(n, lo + CHUNK)
+        hi = chunk_end(lo)
         return lo, hi, [it for it in io_pool().map(load_one, range(lo, hi)) if it is not None]
 
     def put_mask(st, j, cm):  # the reference's two masking comparisons (o3d_utils.py:131-142), as numpy makes them
@@ -197,7 +203,7 @@ def integrate(dataset, depth_data_io, side, use_confidence_filtered_depth: bool,
         raw buffer, which the device decode flags invalid (frame_ok 0: skipped, as the reference
         skips a missing frame)."""
         from .dataio import DepthDataIO
-        hi = min(n, lo + CHUNK)
+        hi = chunk_end(lo)
 
         def one(j):  # 1: masked, 0: unmasked, -1: unmasked, confidence map not found (warned below)
             i = lo + j
@@ -229,7 +235,7 @@ def integrate(dataset, depth_data_io, side, use_confidence_filtered_depth: bool,
         the confidence map only after is_depth_map_valid passed (o3d_utils.py:109-142)."""
         from . import _lib
         from .dataio import DepthDataIO
-        hi = min(n, lo + CHUNK)
+        hi = chunk_end(lo)
         B = hi - lo
         H, W = st.raw.shape[1:]
         raw_path, conf_path = native
@@ -319,7 +325,7 @@ def integrate(dataset, depth_data_io, side, use_confidence_filtered_depth: bool,
         integrate_decoded(idx, buf, ok, H, W)
 
     def uniform(lo):  # every frame of the chunk at lo has one size (the usual capture)
-        hi = min(n, lo + CHUNK)
+        hi = chunk_end(lo)
         return len({(int(dataset.heights[i]), int(dataset.widths[i])) for i in range(lo, hi)}) == 1
 
     def submit(pool, lo, turn):

@@ -19,6 +19,7 @@ sys.path.insert(0, os.path.join(ROOT, "metaquest-3d-reconstruction_amd"))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--chunks", default="64,127")
+    ap.add_argument("--firsts", default="", help="FIRST_CHUNK values to cross with the chunk sizes (default: the module's)")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--frames", type=int, default=500)
     ap.add_argument("--profile", action="store_true", help="cProfile one integrate() per chunk size (main thread)")
@@ -59,12 +60,17 @@ def main():
                 buf = _io.StringIO()
                 pstats.Stats(pr, stream=buf).sort_stats("tottime").print_stats(14)
                 print(f"== CHUNK {c}\n" + buf.getvalue(), file=sys.stderr)
-        times = {c: [] for c in chunks}
+        firsts = [int(f) for f in a.firsts.split(",")] if a.firsts else [o3d_utils.FIRST_CHUNK]
+        configs = [(c, f) for c in chunks for f in firsts]
+        key = (lambda c, f: str(c)) if len(firsts) == 1 else (lambda c, f: f"{c}/first{f}")
+        times = {key(c, f): [] for c, f in configs}
         splits = {}
         vols = {}
         for r in range(a.rounds + 1):
-            for c in chunks:
+            for c, f in configs:
                 o3d_utils.CHUNK = c
+                o3d_utils.FIRST_CHUNK = f
+                c = key(c, f)
                 t0 = time.perf_counter()
                 vbg = o3d_utils.integrate(ds, io, Side.LEFT, **kw)
                 dt = time.perf_counter() - t0
@@ -78,9 +84,9 @@ def main():
                 del vbg
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
-    k0, t0_, w0 = vols[chunks[0]]
+    k0, t0_, w0 = vols[key(*configs[0])]
     out = {"frames": len(ds), "rounds": a.rounds, "chunks": {}}
-    for c in chunks:
+    for c in (key(c, f) for c, f in configs):
         k1, t1, w1 = vols[c]
         same = k0.shape == k1.shape and (k0 == k1).all() and (w0 == w1).all() and (t0_.view(np.uint32) == t1.view(np.uint32)).all()
         med = float(np.median(times[c]))
