@@ -19,6 +19,7 @@ Every call goes through libmqr_hip.so; there is no CPU path.
 from __future__ import annotations
 
 import ctypes
+import threading
 
 import numpy as np
 
@@ -80,6 +81,24 @@ def _mat(m, shape) -> np.ndarray:
     return a
 
 
+# Released grids kept for reuse: creating and destroying a grid (its HBM pool and hash table, its streams)
+# cost ~2.6 ms per fresh volume, which the fragment path pays once per 100 frames (tools/fragment_probe.py).
+# A released grid that never grew is reset (the state of a new grid, mqr_vbg_reset) and handed to the next
+# VoxelBlockGrid of the same voxel size, resolution, block count and device.  At most SPARE_GRIDS are kept.
+SPARE_GRIDS = 1
+_spares = []  # [(key, handle)]
+_spares_lock = threading.Lock()
+
+
+def release_spare_grids():
+    """Destroy the kept released grids (their HBM is freed)."""
+    with _spares_lock:
+        hs = [h for _, h in _spares]
+        _spares.clear()
+    for h in hs:
+        _lib._lib.mqr_vbg_destroy(h)
+
+
 class VoxelBlockGrid:
     def __init__(self, attr_names=("tsdf", "weight"), attr_dtypes=None, attr_channels=None, voxel_size=0.01,
                  block_resolution=16, block_count=50_000, device=None):
@@ -91,17 +110,33 @@ class VoxelBlockGrid:
         self.block_resolution = int(block_resolution)
         self.device = device
         self.device_id = parse_device(device)
-        h = ctypes.c_void_p()
-        call("mqr_vbg_create", self.voxel_size, self.block_resolution, int(block_count), self.device_id,
-             ctypes.byref(h))
+        self._key = (self.voxel_size, self.block_resolution, int(block_count), self.device_id)
+        with _spares_lock:
+            i = next((j for j, (k, _) in enumerate(_spares) if k == self._key), None)
+            h = _spares.pop(i)[1] if i is not None else None
+        if h is None:
+            h = ctypes.c_void_p()
+            call("mqr_vbg_create", self.voxel_size, self.block_resolution, int(block_count), self.device_id,
+                 ctypes.byref(h))
         self._h = h
 
     # -- lifetime -----------------------------------------------------------------------------
     def __del__(self):
         h = getattr(self, "_h", None)
-        if h is not None and h.value and _lib._lib is not None:
-            _lib._lib.mqr_vbg_destroy(h)
-            self._h = None
+        if h is None or not h.value or _lib._lib is None:
+            return
+        self._h = None
+        key = None if getattr(self, "_profiled", False) else getattr(self, "_key", None)
+        cap = ctypes.c_int64(-1)
+        # (the integrate configuration back to a new grid's default, then emptied)
+        if (key is not None and SPARE_GRIDS > 0 and _lib._lib.mqr_vbg_capacity(h, ctypes.byref(cap)) == 0
+                and cap.value == key[2] and _lib._lib.mqr_vbg_set_variant(h, 0) == 0
+                and _lib._lib.mqr_vbg_reset(h) == 0):
+            with _spares_lock:
+                if len(_spares) < SPARE_GRIDS:
+                    _spares.append((key, h))
+                    return
+        _lib._lib.mqr_vbg_destroy(h)
 
     @property
     def handle(self):
@@ -255,6 +290,7 @@ class VoxelBlockGrid:
     def profile(self, enable=True, touch=False):
         """Per-launch timing events (stats()['integrate_ms']); touch=True also times the touch launches."""
         call("mqr_vbg_profile", self._h, (2 if touch else 1) if enable else 0)
+        self._profiled = True  # (its timing state stays with it: not kept for reuse)
 
     def stats(self, reset=False) -> dict:
         s = MqrStats()

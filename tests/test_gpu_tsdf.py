@@ -231,3 +231,34 @@ def test_speculative_first_batch_gate(mqr_mod, room_seq):
     with pytest.raises(RuntimeError, match="No block is touched"):
         vols[0].integrate_frames(dd, K, T, **kw)
     compare_volumes(vols[0].export(), _oracle_run(room_seq, 0.01, 16, 4.0, 10.0, frames=[0, 1, 2]).export(), 0.0)
+
+
+def test_released_grid_is_reused_as_a_new_one(mqr_mod, room_seq):
+    """A released grid of the same configuration is handed to the next VoxelBlockGrid (mqr.vbg SPARE_GRIDS):
+    it must come back empty, with the default integrate configuration, and integrate exactly as a new grid;
+    a grid that grew is not kept."""
+    from mqr import vbg as vbg_mod
+    from mqr import _lib
+    vbg_mod.release_spare_grids()
+    K = room_seq["K"].astype(np.float64)
+    T = room_seq["T_wc"].astype(np.float64)
+    kw = dict(depth_scale=1.0, depth_max=4.0, trunc_voxel_multiplier=10.0)
+    a = mqr_mod.VoxelBlockGrid(voxel_size=0.01, block_resolution=16, block_count=4096)
+    _lib.call("mqr_vbg_set_variant", a.handle, 0x400)  # 32-frame batches: must not carry over
+    a.integrate_frames(room_seq["depth"][:20], K[:20], T[:20], **kw)
+    ref = a.export()
+    h = a.handle.value
+    del a
+    b = mqr_mod.VoxelBlockGrid(voxel_size=0.01, block_resolution=16, block_count=4096)
+    assert b.handle.value == h and b.size() == 0  # the released grid, emptied
+    b.integrate_frames(room_seq["depth"][:20], K[:20], T[:20], **kw)
+    assert compare_volumes(b.export(), ref, 0.0) == 0.0
+    c = mqr_mod.VoxelBlockGrid(voxel_size=0.01, block_resolution=16, block_count=4096)
+    assert c.handle.value != h  # (b still alive: a new grid)
+    del b, c
+    g = mqr_mod.VoxelBlockGrid(voxel_size=0.01, block_resolution=16, block_count=16)  # grows past 16 blocks
+    g.integrate_frames(room_seq["depth"][:20], K[:20], T[:20], **kw)
+    vbg_mod.release_spare_grids()
+    del g
+    assert not vbg_mod._spares  # grown: destroyed, not kept
+    vbg_mod.release_spare_grids()
