@@ -84,8 +84,10 @@ def _mat(m, shape) -> np.ndarray:
 # Released grids kept for reuse: creating and destroying a grid (its HBM pool and hash table, its streams)
 # cost ~2.6 ms per fresh volume, which the fragment path pays once per 100 frames (tools/fragment_probe.py).
 # A released grid that never grew is reset (the state of a new grid, mqr_vbg_reset) and handed to the next
-# VoxelBlockGrid of the same voxel size, resolution, block count and device.  At most SPARE_GRIDS are kept.
+# VoxelBlockGrid of the same voxel size, resolution, block count and device.  At most SPARE_GRIDS are kept,
+# and only grids whose pool is at most SPARE_MAX_BYTES (a large volume's HBM is not held back).
 SPARE_GRIDS = 1
+SPARE_MAX_BYTES = 4 << 30
 _spares = []  # [(key, handle)]
 _spares_lock = threading.Lock()
 
@@ -129,7 +131,8 @@ class VoxelBlockGrid:
         key = None if getattr(self, "_profiled", False) else getattr(self, "_key", None)
         cap = ctypes.c_int64(-1)
         # (the integrate configuration back to a new grid's default, then emptied)
-        if (key is not None and SPARE_GRIDS > 0 and _lib._lib.mqr_vbg_capacity(h, ctypes.byref(cap)) == 0
+        if (key is not None and SPARE_GRIDS > 0 and key[2] * key[1] ** 3 * 8 <= SPARE_MAX_BYTES
+                and _lib._lib.mqr_vbg_capacity(h, ctypes.byref(cap)) == 0
                 and cap.value == key[2] and _lib._lib.mqr_vbg_set_variant(h, 0) == 0
                 and _lib._lib.mqr_vbg_reset(h) == 0):
             with _spares_lock:
