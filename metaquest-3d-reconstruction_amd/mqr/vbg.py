@@ -128,17 +128,20 @@ class VoxelBlockGrid:
         if h is None or not h.value or _lib._lib is None:
             return
         self._h = None
-        key = None if getattr(self, "_profiled", False) else getattr(self, "_key", None)
-        cap = ctypes.c_int64(-1)
-        # (the integrate configuration back to a new grid's default, then emptied)
-        if (key is not None and SPARE_GRIDS > 0 and key[2] * key[1] ** 3 * 8 <= SPARE_MAX_BYTES
-                and _lib._lib.mqr_vbg_capacity(h, ctypes.byref(cap)) == 0
-                and cap.value == key[2] and _lib._lib.mqr_vbg_set_variant(h, 0) == 0
-                and _lib._lib.mqr_vbg_reset(h) == 0):
-            with _spares_lock:
-                if len(_spares) < SPARE_GRIDS:
-                    _spares.append((key, h))
-                    return
+        try:  # (at interpreter exit the module's globals may already be gone: then just destroy)
+            key = None if getattr(self, "_profiled", False) else getattr(self, "_key", None)
+            cap = ctypes.c_int64(-1)
+            # (the integrate configuration back to a new grid's default, then emptied)
+            if (key is not None and SPARE_GRIDS > 0 and key[2] * key[1] ** 3 * 8 <= SPARE_MAX_BYTES
+                    and _lib._lib.mqr_vbg_capacity(h, ctypes.byref(cap)) == 0
+                    and cap.value == key[2] and _lib._lib.mqr_vbg_set_variant(h, 0) == 0
+                    and _lib._lib.mqr_vbg_reset(h) == 0):
+                with _spares_lock:
+                    if len(_spares) < SPARE_GRIDS:
+                        _spares.append((key, h))
+                        return
+        except Exception:  # noqa: BLE001
+            pass
         _lib._lib.mqr_vbg_destroy(h)
 
     @property
