@@ -23,9 +23,11 @@
 
 #include <cmath>
 #include <mutex>
+#include <memory>
 #include <vector>
 
 #include "mqr_common.hpp"
+#include "device_block.hpp"
 
 namespace mqr {
 
@@ -441,17 +443,18 @@ int mqr_color_vertices(int device, const float* vertices, int64_t nv, int vloc, 
         (void)hipStreamDestroy(s);
         return 2;
     }
-    std::vector<void*> owned;
     int rc = 0;
+    const int64_t HW = (int64_t)H * W;
+    const bool hv = vloc != MQR_DEVICE, hi = img_loc != MQR_DEVICE, ho = out_loc != MQR_DEVICE;
+    // device staging from the device-block cache (device_block.hpp), returned after the final synchronisation
+    CachedBlock blk(device, (hv ? 12 * (size_t)nv : 0) + (hi ? 7 * (size_t)HW * N : 0) +
+                                sizeof(ColorCam) * std::max(N, 1) + (ho ? 16 * (size_t)nv : 0) + 6 * 256);
     auto dev = [&](const void* h, size_t bytes, bool host) -> const void* {
         if (!host) return h;
-        void* p = nullptr;
-        if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
-        owned.push_back(p);
-        if (copy_to_device(device, p, h, bytes, s)) return nullptr;
+        void* p = blk.take(bytes);
+        if (!p || copy_to_device(device, p, h, bytes, s)) return nullptr;
         return p;
     };
-    const int64_t HW = (int64_t)H * W;
     const float* dV = static_cast<const float*>(dev(vertices, sizeof(float) * 3 * nv, vloc != MQR_DEVICE));
     const uint8_t* dI = static_cast<const uint8_t*>(dev(images, (size_t)3 * HW * N, img_loc != MQR_DEVICE));
     const float* dD = static_cast<const float*>(dev(depths, sizeof(float) * HW * N, img_loc != MQR_DEVICE));
@@ -459,8 +462,7 @@ int mqr_color_vertices(int device, const float* vertices, int64_t nv, int vloc, 
     float* dO = colors_out;
     int32_t* dN = counts_out;
     if (out_loc != MQR_DEVICE) {
-        void* p = nullptr;
-        if (hipMalloc(&p, (sizeof(float) * 3 + sizeof(int32_t)) * nv) == hipSuccess) owned.push_back(p);
+        void* p = blk.take((sizeof(float) * 3 + sizeof(int32_t)) * nv);
         dO = static_cast<float*>(p);
         dN = p ? reinterpret_cast<int32_t*>(static_cast<float*>(p) + 3 * nv) : nullptr;
     }
@@ -485,7 +487,6 @@ int mqr_color_vertices(int device, const float* vertices, int64_t nv, int vloc, 
         set_error("mqr_color_vertices: kernel failed");
         rc = 1;
     }
-    for (void* p : owned) (void)hipFree(p);
     (void)hipStreamDestroy(s);
     return rc;
 }
@@ -513,13 +514,26 @@ int mqr_color_map(int device, const float* vertices, int64_t nv, int vloc, const
         (void)hipStreamDestroy(s);
         return 2;
     }
-    std::vector<void*> owned;
-    auto alloc = [&](size_t bytes) -> void* {
-        void* p = nullptr;
-        if (hipMalloc(&p, std::max<size_t>(bytes, 16)) != hipSuccess) return nullptr;
-        owned.push_back(p);
-        return p;
-    };
+    // device staging from the device-block cache (device_block.hpp): the visibility pass's arrays in one
+    // block, the knn pass's (sized once the seen vertices are counted) in a second; both returned after
+    // the final synchronisation
+    const int64_t HW0 = (int64_t)H * W, NHW0 = HW0 * N;
+    size_t tb_sel = 0;
+    {
+        hipcub::CountingInputIterator<int32_t> it0(0);
+        if (hipcub::DeviceSelect::Flagged(nullptr, tb_sel, it0, (const uint8_t*)nullptr, (int32_t*)nullptr,
+                                          (int64_t*)nullptr, (int)nv, s) != hipSuccess) {
+            (void)hipStreamDestroy(s);
+            set_error("mqr_color_map: select sizing failed");
+            return 1;
+        }
+    }
+    const bool hv = vloc != MQR_DEVICE, hi = img_loc != MQR_DEVICE;
+    CachedBlock blk(device, (hv ? 12 * (size_t)nv : 0) + (hi ? 7 * (size_t)NHW0 : 0) + sizeof(ColorCam) * std::max(N, 1) +
+                                10 * (size_t)NHW0 + (24 + 4 + 12 + 1 + 1 + 8) * (size_t)nv + 16 + tb_sel + 16 * 256);
+    std::unique_ptr<CachedBlock> blk_knn;
+    CachedBlock* cur = &blk;
+    auto alloc = [&](size_t bytes) -> void* { return cur->take(std::max<size_t>(bytes, 16)); };
     auto dev = [&](const void* h, size_t bytes, bool host) -> const void* {
         if (!host) return h;
         void* p = alloc(bytes);
@@ -562,10 +576,8 @@ int mqr_color_map(int device, const float* vertices, int64_t nv, int vloc, const
         hipLaunchKernelGGL(k_cm_vertices, dim3(gv), dim3(256), 0, s, dV, nv, dI, dT, mask, dC, N, H, W, max_depth,
                            visibility_threshold, margin, (float)depth_trunc, avg, cnt);
         hipLaunchKernelGGL(k_cm_flags, dim3(gv), dim3(256), 0, s, cnt, nv, fseen, funseen);
-        size_t tb = 0;
+        size_t tb = tb_sel;
         hipcub::CountingInputIterator<int32_t> it(0);
-        if (hipcub::DeviceSelect::Flagged(nullptr, tb, it, fseen, ids, nsel, (int)nv, s) != hipSuccess)
-            fail("mqr_color_map: select sizing failed");
         void* tmp = rc ? nullptr : alloc(tb);
         if (!rc && (!tmp || hipcub::DeviceSelect::Flagged(tmp, tb, it, fseen, ids, nsel, (int)nv, s) != hipSuccess ||
                     hipcub::DeviceSelect::Flagged(tmp, tb, it, funseen, ids + nv, nsel + 1, (int)nv, s) != hipSuccess))
@@ -583,17 +595,21 @@ int mqr_color_map(int device, const float* vertices, int64_t nv, int vloc, const
             const int64_t nb = (nseen + kBucket - 1) / kBucket;
             int64_t P = 1;
             while (P < nb) P <<= 1;
+            size_t tbs = 0;
+            if (hipcub::DeviceRadixSort::SortPairs(nullptr, tbs, (const uint64_t*)nullptr, (uint64_t*)nullptr,
+                                                   (const int32_t*)nullptr, (int32_t*)nullptr, (int)nseen, 0, 63, s) !=
+                hipSuccess)
+                fail("mqr_color_map: knn allocation failed");
+            blk_knn.reset(new CachedBlock(device, 24 + 16 * (size_t)nseen + 4 * (size_t)nseen + 64 * (size_t)P +
+                                                      16 * (size_t)nseen + tbs + 8 * 256));
+            cur = blk_knn.get();
             uint32_t* bb = static_cast<uint32_t*>(alloc(6 * sizeof(uint32_t)));
             uint64_t* keys = static_cast<uint64_t*>(alloc(sizeof(uint64_t) * 2 * nseen));
             int32_t* sorted = static_cast<int32_t*>(alloc(sizeof(int32_t) * nseen));
             float4* blo = static_cast<float4*>(alloc(sizeof(float4) * 2 * P));
             float4* bhi = static_cast<float4*>(alloc(sizeof(float4) * 2 * P));
             float4* pts = static_cast<float4*>(alloc(sizeof(float4) * nseen));
-            size_t tbs = 0;
-            if (!bb || !keys || !sorted || !blo || !bhi || !pts ||
-                hipcub::DeviceRadixSort::SortPairs(nullptr, tbs, keys, keys + nseen, ids, sorted, (int)nseen, 0, 63, s) !=
-                    hipSuccess)
-                fail("mqr_color_map: knn allocation failed");
+            if (!rc && (!bb || !keys || !sorted || !blo || !bhi || !pts)) fail("mqr_color_map: knn allocation failed");
             void* tmps = rc ? nullptr : alloc(tbs);
             if (!rc && !tmps) fail("mqr_color_map: knn allocation failed");
             if (!rc) {
@@ -640,7 +656,6 @@ int mqr_color_map(int device, const float* vertices, int64_t nv, int vloc, const
             fail("mqr_color_map: copy failed");
     }
     if (hipStreamSynchronize(s) != hipSuccess && !rc) fail("mqr_color_map: kernel failed");
-    for (void* p : owned) (void)hipFree(p);
     (void)hipStreamDestroy(s);
     return rc;
 }

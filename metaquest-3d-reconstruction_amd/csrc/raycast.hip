@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "mqr_common.hpp"
+#include "device_block.hpp"
 
 struct mqr_scene {
     int device = 0;
@@ -419,23 +420,6 @@ static void free_built(mqr_scene* s) {
 
 static size_t al256(size_t x) { return (x + 255) & ~size_t(255); }
 
-// A cast's device staging: one block of the device-block cache (geom_block_alloc) carved into 256-byte
-// aligned pieces, returned to the cache at scope exit -- after the call's stream synchronisation -- instead
-// of a hipMalloc / hipFree pair per array per call.
-struct CachedBlock {
-    int device;
-    void* p = nullptr;
-    size_t cap = 0, used = 0;
-    CachedBlock(int d, size_t bytes) : device(d) { p = geom_block_alloc(d, std::max<size_t>(bytes, 256), &cap); }
-    ~CachedBlock() { geom_block_release(device, p, cap); }
-    CachedBlock(const CachedBlock&) = delete;
-    CachedBlock& operator=(const CachedBlock&) = delete;
-    void* take(size_t b) {
-        char* r = static_cast<char*>(p) + used;
-        used += al256(b);
-        return r;
-    }
-};
 
 static int build(mqr_scene* s) {
     if (s->built) return 0;
