@@ -296,7 +296,7 @@ int mqr_decode_depth_masked(int device, const float* raw, int raw_loc, int N, in
                             int mask_loc, float* depth_out, int out_loc, uint8_t* frame_ok) {
     const bool any_mask = has_mask && N > 0 && std::any_of(has_mask, has_mask + N, [](uint8_t m) { return m != 0; });
     MQR_REQUIRE(!any_mask || mask, "mask requested without a mask array");
-    static const uint8_t kNone = 0;
+    static const uint8_t kNone = 0;  // (a non-null placeholder selecting the byte-mask kernel: never read, no frame masked)
     return decode_impl(device, raw, raw_loc, N, H, W, nears, fars, strong, nullptr, nullptr, any_mask ? mask : &kNone,
                        any_mask ? has_mask : nullptr, mask_loc, 0.0, 0, depth_out, out_loc, frame_ok);
 }
