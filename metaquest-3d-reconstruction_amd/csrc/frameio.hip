@@ -150,14 +150,14 @@ bool zip_members(int fd, int64_t fsize, std::vector<Member>& want) {
 // (dtype, C order, shape H x W, size), or -1.
 int64_t npy_data_off(int fd, const Member& m, const char* descr, size_t item, int H, int W) {
     unsigned char pre[12];
-    if (m.size < 10 || !pread_all(fd, pre, 10, m.data_off)) return false;
-    if (memcmp(pre, "\x93NUMPY", 6) != 0) return false;
+    if (m.size < 10 || !pread_all(fd, pre, 10, m.data_off)) return -1;
+    if (memcmp(pre, "\x93NUMPY", 6) != 0) return -1;
     int64_t hl, hoff;
     if (pre[6] == 1) {
         hl = u16(pre + 8);
         hoff = 10;
     } else if (pre[6] == 2 || pre[6] == 3) {
-        if (m.size < 12 || !pread_all(fd, pre, 12, m.data_off)) return false;
+        if (m.size < 12 || !pread_all(fd, pre, 12, m.data_off)) return -1;
         hl = u32(pre + 8);
         hoff = 12;
     } else {

@@ -6,6 +6,7 @@ cannot take (missing, wrong size, compressed, another dtype or shape, truncated)
 guessed; the writer's files must load with np.load and hold the members np.savez writes, byte for byte."""
 import ctypes
 import os
+import zipfile
 
 import numpy as np
 import pytest
@@ -39,7 +40,7 @@ def test_read_frames_matches_numpy_and_reports_the_rest(tmp_path, threads):
     H, W = 24, 40
     rng = np.random.default_rng(3)
     raws, confs, expect = [], [], []
-    for i in range(12):
+    for i in range(13):
         r = rng.random((H, W), dtype=np.float32)
         c = rng.random((H, W))
         v = rng.integers(0, 9, (H, W)).astype(np.int32)
@@ -60,12 +61,15 @@ def test_read_frames_matches_numpy_and_reports_the_rest(tmp_path, threads):
     np.savez(confs[8], valid_count=expect[8][2])                         # member missing
     np.savez(confs[9], confidence_map=np.asfortranarray(expect[9][1]), valid_count=expect[9][2])  # F order
     confs[10] = None                                                     # no confidence asked for
+    with zipfile.ZipFile(confs[12], "w", zipfile.ZIP_STORED) as z:       # members that are not .npy
+        z.writestr("confidence_map.npy", b"\x00" * (128 + 8 * H * W))
+        z.writestr("valid_count.npy", b"\x00" * (128 + 4 * H * W))
     raw, conf, vc, st = _read(lib, raws, confs, H, W, threads)
     ok_raw, miss_raw, oth_raw = lib.MQR_FRAME_RAW_OK, lib.MQR_FRAME_RAW_MISSING, lib.MQR_FRAME_RAW_OTHER
     ok_c, miss_c, oth_c = lib.MQR_FRAME_CONF_OK, lib.MQR_FRAME_CONF_MISSING, lib.MQR_FRAME_CONF_OTHER
     want = {0: ok_raw | ok_c, 1: miss_raw | ok_c, 2: oth_raw | ok_c, 3: ok_raw | miss_c, 4: ok_raw | oth_c,
             5: ok_raw | oth_c, 6: ok_raw | oth_c, 7: ok_raw | oth_c, 8: ok_raw | oth_c, 9: ok_raw | oth_c,
-            10: ok_raw, 11: ok_raw | ok_c}
+            10: ok_raw, 11: ok_raw | ok_c, 12: ok_raw | oth_c}
     assert {i: int(s) for i, s in enumerate(st)} == want
     for i, (r, c, v) in enumerate(expect):
         if st[i] & ok_raw:
