@@ -39,7 +39,7 @@ class _DevPtr:
         self.ptr = ctypes.c_void_p(p)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=400)
@@ -81,7 +81,98 @@ def parse():
     ap.add_argument("--touch-steps", type=int, default=20, help="profiled steps for touch_ms_per_launch (0: skip)")
     ap.add_argument("--c5-only", action="store_true",
                     help="run only the C5 leg and print its record (rocprof of the peak-HBM run)")
-    return ap.parse_args()
+    ap.add_argument("--launch-timeout", type=float, default=3000.0,
+                    help="--gpus N > 1 without WORLD_SIZE: overall limit on the N self-launched ranks (s)")
+    return ap.parse_args(argv)
+
+
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv, child=None, timeout=3000.0, out=None, grace=10.0):
+    """`bench.py --gpus N` (N > 1) started without WORLD_SIZE: start N fresh rank processes of this
+    script on this node (RANK = LOCAL_RANK = i, WORLD_SIZE = N, MASTER_ADDR 127.0.0.1, a free
+    MASTER_PORT), relay rank 0's stdout (its JSON line) and return the worst exit code.  The parent
+    imports no torch and touches no GPU (it starts children, it never execs).  When a rank fails, or
+    `timeout` passes, the others are terminated (SIGTERM to each rank's process group, SIGKILL after
+    `grace` s).  `child` replaces `[python, bench.py]` (the launcher test's stub)."""
+    import signal
+    import subprocess
+    import threading
+    out = out or sys.stdout
+    cmd = list(child) if child else [sys.executable, "-u", os.path.abspath(__file__)]
+    port = str(_free_port())
+    procs = []
+    printed = threading.Event()
+
+    def relay(stream):
+        for line in stream:
+            out.write(line)
+            out.flush()
+            if line.lstrip().startswith("{"):
+                printed.set()
+
+    def stop_all(sig):
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, sig)
+                except (ProcessLookupError, PermissionError):
+                    pass
+
+    prev = signal.getsignal(signal.SIGTERM)
+    signal.signal(signal.SIGTERM, lambda *_: (stop_all(signal.SIGTERM), sys.exit(143)))
+    relay_thread = None
+    try:
+        for r in range(n):
+            env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                       GROUP_RANK="0", NODE_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+            procs.append(subprocess.Popen(cmd + list(argv), env=env, start_new_session=True,
+                                          stdout=subprocess.PIPE if r == 0 else sys.stderr.fileno(), text=True))
+            if r == 0:
+                relay_thread = threading.Thread(target=relay, args=(procs[0].stdout,), daemon=True)
+                relay_thread.start()
+        t_end = time.monotonic() + timeout
+        failed = timed_out = False
+        while any(p.poll() is None for p in procs):
+            if not failed and any(p.poll() not in (None, 0) for p in procs):
+                failed = True
+                bad = [(i, p.returncode) for i, p in enumerate(procs) if p.returncode not in (None, 0)]
+                print(f"[bench launcher] rank(s) failed {bad}: terminating the others", file=sys.stderr, flush=True)
+                stop_all(signal.SIGTERM)
+                t_end = min(t_end, time.monotonic() + grace)
+            elif time.monotonic() > t_end:
+                if not (failed or timed_out):
+                    timed_out = True
+                    print(f"[bench launcher] {timeout:.0f} s limit: terminating the ranks", file=sys.stderr,
+                          flush=True)
+                    stop_all(signal.SIGTERM)
+                    t_end = time.monotonic() + grace
+                else:
+                    stop_all(signal.SIGKILL)
+            time.sleep(0.05)
+        if relay_thread is not None:
+            relay_thread.join(5.0)
+    finally:
+        stop_all(signal.SIGKILL)
+        signal.signal(signal.SIGTERM, prev)
+    codes = [p.returncode for p in procs]
+    worst = 0
+    for c in codes:
+        c = 128 - c if c < 0 else c  # killed by a signal: 128 + signal number
+        worst = max(worst, c)
+    if timed_out:
+        worst = max(worst, 124)
+    if worst and not printed.is_set():
+        out.write(json.dumps({"metric": METRIC, "value": None, "unit": "frames/s", "n_gpus": n,
+                              "error": f"self-launched ranks exited {codes}" + (" (time limit)" if timed_out else "")})
+                  + "\n")
+        out.flush()
+    return worst
 
 
 def _vmstat():
@@ -1101,6 +1192,16 @@ def sharded_parity(full_host, K, T, args, owned, meshes):
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:
+            # no launcher around us: start the N ranks here, before anything touches the GPU
+            sys.exit(launch_ranks(args.gpus, sys.argv[1:], timeout=args.launch_timeout))
+    elif int(os.environ["WORLD_SIZE"]) != args.gpus:
+        if int(os.environ.get("RANK", 0)) == 0:
+            print(json.dumps({"metric": METRIC, "value": None, "unit": "frames/s", "n_gpus": args.gpus,
+                              "error": f"--gpus {args.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']}"}),
+                  flush=True)
+        sys.exit(1)
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))

@@ -9,6 +9,8 @@
 #   benchq      a short bench (no C4 / C5 / drop-in legs)             -> gpurun_out/${TAG}_benchq.json
 #   c5          the C5 leg alone, parity included (bench.py --c5-only)   -> gpurun_out/${TAG}_c5.json
 #   n2          2-rank rehearsal on one GPU (gloo-staged merge)        -> gpurun_out/${TAG}_bench_n2.json
+#   n2self      the same, bench.py --gpus 2 starting its own ranks (no torchrun) -> gpurun_out/${TAG}_bench_n2_selflaunch.json
+#   mbytes      C4 exchange bytes / zero-weight voxels / per-rank times at 2, 4, 8 ranks (tools/merge_bytes.py)
 #   prof        rocprofv3 --kernel-trace --stats of the C2 bench      -> gpurun_out/${TAG}_bench_kernel_stats.csv
 #   profc5      the same over the C5 leg alone                        -> gpurun_out/${TAG}_c5_kernel_stats.csv
 #   xtrace      kernel trace of 30 extractions: wall vs device span vs gaps -> gpurun_out/${TAG}_extract_timeline.json
@@ -23,7 +25,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-TAG=${TAG:-r05}
+TAG=${TAG:-r06}
 PYT="python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu"
 for step in ${STEPS:-tests}; do
   echo "== $step ($(date +%H:%M:%S))"
@@ -52,6 +54,13 @@ for step in ${STEPS:-tests}; do
         --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 10 --warmup 2 --weak-steps 10 \
         > gpurun_out/${TAG}_bench_n2.json 2> gpurun_out/${TAG}_bench_n2.err || { tail -40 gpurun_out/${TAG}_bench_n2.err; exit 1; }
       tail -c 600 gpurun_out/${TAG}_bench_n2.json ;;
+    n2self)
+      MQR_BENCH_WRAP_DEVICES=1 timeout -k 10 900 python bench.py --gpus 2 --steps 10 --warmup 2 --weak-steps 10 \
+        > gpurun_out/${TAG}_bench_n2_selflaunch.json 2> gpurun_out/${TAG}_bench_n2_selflaunch.err || { tail -40 gpurun_out/${TAG}_bench_n2_selflaunch.err; exit 1; }
+      tail -c 600 gpurun_out/${TAG}_bench_n2_selflaunch.json ;;
+    mbytes)
+      timeout -k 10 600 python tools/merge_bytes.py > gpurun_out/${TAG}_merge_bytes.json 2> gpurun_out/${TAG}_merge_bytes.err || { tail -30 gpurun_out/${TAG}_merge_bytes.err; exit 1; }
+      tail -8 gpurun_out/${TAG}_merge_bytes.err ;;
     prof)
       rm -rf gpurun_out/prof
       timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/prof -o run -- \
