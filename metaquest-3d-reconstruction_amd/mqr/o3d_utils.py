@@ -83,7 +83,7 @@ def compute_o3d_intrinsic_matrices(dataset) -> np.ndarray:
 
 
 def _masked_depth(depth_data_io, side, index, dataset, use_confidence_filtered_depth, confidence_threshold,
-                  valid_count_threshold) -> Optional[np.ndarray]:
+                  valid_count_threshold, warn=print) -> Optional[np.ndarray]:
     depth = depth_data_io.load_depth_map(side=side, timestamp=dataset.timestamps[index],
                                          width=dataset.widths[index], height=dataset.heights[index],
                                          near=dataset.nears[index], far=dataset.fars[index])
@@ -92,7 +92,7 @@ def _masked_depth(depth_data_io, side, index, dataset, use_confidence_filtered_d
     if use_confidence_filtered_depth:
         cm = depth_data_io.load_confidence_map(side=side, timestamp=dataset.timestamps[index])
         if cm is None:
-            print(f"[Warning] Confidence map not found for timestamp {dataset.timestamps[index]}")
+            warn(f"[Warning] Confidence map not found for timestamp {dataset.timestamps[index]}")
         else:
             depth[cm.confidence_map < confidence_threshold] = 0.0
             depth[cm.valid_count < valid_count_threshold] = 0.0
@@ -138,6 +138,17 @@ def _frame_paths(depth_data_io, side):
     return None
 
 
+class _Raised:
+    """A frame whose read raised (in an I/O thread).  The reference's per-frame loop has integrated
+    every frame before it and printed their messages when the exception leaves integrate()
+    (o3d_utils.py:188-236): the chunk's frames before it are integrated, its messages printed, then
+    the exception is re-raised on the calling thread; nothing of that frame or after it is read or
+    printed (no further chunk is started)."""
+
+    def __init__(self, index, exc):
+        self.index, self.exc = index, exc
+
+
 def load_depth_map(depth_data_io, side, index: int, dataset, device, use_confidence_filtered_depth: bool,
                    confidence_threshold: float, valid_count_threshold: int) -> Optional[Image]:
     d = _masked_depth(depth_data_io, side, index, dataset, use_confidence_filtered_depth, confidence_threshold,
@@ -154,6 +165,7 @@ def integrate(dataset, depth_data_io, side, use_confidence_filtered_depth: bool,
               valid_count_threshold: int, voxel_size: float, block_resolution: int, block_count: int,
               depth_max: float, trunc_voxel_multiplier: float, device, show_progress: bool = False,
               desc: Optional[str] = None, vbg_opt: Optional[VoxelBlockGrid] = None) -> VoxelBlockGrid:
+    from .dataio import DepthDataIO
     times = {"create": 0.0, "wait_io": 0.0, "device": 0.0, "chunks": 0}
     t_c = time.perf_counter()
     vbg = vbg_opt if vbg_opt is not None else VoxelBlockGrid(
@@ -170,26 +182,41 @@ def integrate(dataset, depth_data_io, side, use_confidence_filtered_depth: bool,
         return min(n, lo + (min(FIRST_CHUNK, CHUNK) if lo == 0 else CHUNK))
 
     def load_one(i):
-        if read_raw is None:
-            d = _masked_depth(depth_data_io, side, i, dataset, use_confidence_filtered_depth,
-                              confidence_threshold, valid_count_threshold)
-            return None if d is None else (i, d, None)
-        raw = read_raw(dataset.timestamps[i], dataset.widths[i], dataset.heights[i])
-        if raw is None:
-            return None
-        cm = None
-        if use_confidence_filtered_depth:
-            cm = depth_data_io.load_confidence_map(side=side, timestamp=dataset.timestamps[i])
-            if cm is None:
-                print(f"[Warning] Confidence map not found for timestamp {dataset.timestamps[i]}")
-        return i, raw, cm
+        """(item or None, this frame's messages), or _Raised."""
+        msgs = []
+        try:
+            if read_raw is None:
+                d = _masked_depth(depth_data_io, side, i, dataset, use_confidence_filtered_depth,
+                                  confidence_threshold, valid_count_threshold, warn=msgs.append)
+                return (None if d is None else (i, d, None)), msgs
+            raw = read_raw(dataset.timestamps[i], dataset.widths[i], dataset.heights[i])
+            if raw is None:
+                return None, msgs
+            cm = None
+            # the reference loads the confidence map only for a valid depth map (o3d_utils.py:109-142);
+            # an invalid one is dropped by the device decode
+            if use_confidence_filtered_depth and DepthDataIO.is_depth_map_valid(raw):
+                cm = depth_data_io.load_confidence_map(side=side, timestamp=dataset.timestamps[i])
+                if cm is None:
+                    msgs.append(f"[Warning] Confidence map not found for timestamp {dataset.timestamps[i]}")
+            return (i, raw, cm), msgs
+        except Exception as e:  # noqa: BLE001 -- re-raised on the calling thread after the prefix
+            return _Raised(i, e)
 
     def load_chunk(lo):
         """Host side of one chunk: file reads only (decode + mask run on the device), or the
         caller's own DataIO decode when it exposes no raw-buffer access; frames read by the I/O
-        threads, results in frame order."""
+        threads, results in frame order, cut at the first frame whose read raised."""
         hi = chunk_end(lo)
-        return lo, hi, [it for it in io_pool().map(load_one, range(lo, hi)) if it is not None]
+        items, msgs, err = [], [], None
+        for r in io_pool().map(load_one, range(lo, hi)):
+            if isinstance(r, _Raised):
+                err = r
+                break
+            if r[0] is not None:
+                items.append(r[0])
+            msgs += r[1]
+        return lo, hi, items, msgs, err
 
     def put_mask(st, j, cm):  # the reference's two masking comparisons (o3d_utils.py:131-142), as numpy makes them
         m = st.mask[j].view(np.bool_)
@@ -202,39 +229,41 @@ def integrate(dataset, depth_data_io, side, use_confidence_filtered_depth: bool,
         per-chunk allocations, stacking or copies on the main thread.  A missing file leaves a zero
         raw buffer, which the device decode flags invalid (frame_ok 0: skipped, as the reference
         skips a missing frame)."""
-        from .dataio import DepthDataIO
         hi = chunk_end(lo)
 
         def one(j):  # 1: masked, 0: unmasked, -1: unmasked, confidence map not found (warned below)
             i = lo + j
-            raw = read_raw(dataset.timestamps[i], dataset.widths[i], dataset.heights[i])
-            if raw is None:
-                st.raw[j] = 0.0
-                return 0
-            st.raw[j] = raw
-            # the reference loads the confidence map only for a valid depth map (o3d_utils.py:109-142)
-            if not use_confidence_filtered_depth or not DepthDataIO.is_depth_map_valid(raw):
-                return 0
-            cm = depth_data_io.load_confidence_map(side=side, timestamp=dataset.timestamps[i])
-            if cm is None:
-                return -1
-            put_mask(st, j, cm)
-            return 1
+            try:
+                raw = read_raw(dataset.timestamps[i], dataset.widths[i], dataset.heights[i])
+                if raw is None:
+                    st.raw[j] = 0.0
+                    return 0
+                st.raw[j] = raw
+                # the reference loads the confidence map only for a valid depth map (o3d_utils.py:109-142)
+                if not use_confidence_filtered_depth or not DepthDataIO.is_depth_map_valid(raw):
+                    return 0
+                cm = depth_data_io.load_confidence_map(side=side, timestamp=dataset.timestamps[i])
+                if cm is None:
+                    return -1
+                put_mask(st, j, cm)
+                return 1
+            except Exception as e:  # noqa: BLE001 -- re-raised on the calling thread after the prefix
+                return _Raised(i, e)
 
         res = list(io_pool().map(one, range(hi - lo)))
-        for j, r in enumerate(res):  # in frame order, as the reference's loop prints them
-            if r < 0:
-                print(f"[Warning] Confidence map not found for timestamp {dataset.timestamps[lo + j]}")
-        return lo, hi, (st, np.array([r > 0 for r in res], bool))
+        err = next((r for r in res if isinstance(r, _Raised)), None)
+        if err is not None:  # the chunk ends before the frame that raised
+            res = res[:err.index - lo]
+        # in frame order, as the reference's loop prints them (on the calling thread, chunk by chunk)
+        msgs = [f"[Warning] Confidence map not found for timestamp {dataset.timestamps[lo + j]}"
+                for j, r in enumerate(res) if r < 0]
+        return lo, lo + len(res), (st, np.array([r > 0 for r in res], bool)), msgs, err
 
     def load_chunk_native(lo, st):
         """load_chunk_staged through mqr_read_frames_masked: native threads pread the raw files into `st`
-        and reduce the npz members to the mask bytes as they read them.  Frames the reader leaves to Python (a raw file of the wrong size, a
-        confidence npz it does not parse) go through the standard loaders here, in frame order, and the
-        confidence messages are printed only for frames whose depth map is valid -- the reference loads
-        the confidence map only after is_depth_map_valid passed (o3d_utils.py:109-142)."""
+        and reduce the npz members to the mask bytes as they read them (on the I/O thread).  The frames
+        the reader leaves to Python are finished by finish_native on the calling thread."""
         from . import _lib
-        from .dataio import DepthDataIO
         hi = chunk_end(lo)
         B = hi - lo
         H, W = st.raw.shape[1:]
@@ -246,29 +275,44 @@ def integrate(dataset, depth_data_io, side, use_confidence_filtered_depth: bool,
         _lib.call("mqr_read_frames_masked", B, raws, confs, H, W, float(confidence_threshold),
                   count_threshold(valid_count_threshold), _lib.ptr(st.raw), _lib.ptr(st.mask) if confs else None,
                   _lib.ptr(status), io_threads())
+        return lo, hi, ("native", st, status), [], None
+
+    def finish_native(lo, hi, st, status):
+        """The frames mqr_read_frames_masked left to Python (a raw file of the wrong size, a confidence
+        npz it does not parse) through the standard loaders, in frame order, on the calling thread:
+        confidence messages are printed only for frames whose depth map is valid -- the reference loads
+        the confidence map only after is_depth_map_valid passed (o3d_utils.py:109-142) -- and a frame
+        whose read raises ends the chunk there (returned as _Raised).  Returns (hi, has, err)."""
+        from . import _lib
+        B = hi - lo
         has = np.zeros(B, bool)
         for j in range(B):
             s = int(status[j])
-            if s & _lib.MQR_FRAME_RAW_OTHER:
-                raw = read_raw(ts[j], dataset.widths[lo + j], dataset.heights[lo + j])  # raises as the reference
-                if raw is None:
+            i = lo + j
+            try:
+                if s & _lib.MQR_FRAME_RAW_OTHER:
+                    raw = read_raw(dataset.timestamps[i], dataset.widths[i], dataset.heights[i])  # raises as the reference
+                    if raw is None:
+                        continue
+                    st.raw[j] = raw
+                    s |= _lib.MQR_FRAME_RAW_OK
+                if not (s & _lib.MQR_FRAME_RAW_OK) or not use_confidence_filtered_depth:
                     continue
-                st.raw[j] = raw
-                s |= _lib.MQR_FRAME_RAW_OK
-            if not (s & _lib.MQR_FRAME_RAW_OK) or not use_confidence_filtered_depth:
-                continue
-            if s & _lib.MQR_FRAME_CONF_OK:
-                has[j] = True
-                continue
-            if not DepthDataIO.is_depth_map_valid(st.raw[j]):
-                continue
-            cm = None if s & _lib.MQR_FRAME_CONF_MISSING else depth_data_io.load_confidence_map(side=side, timestamp=ts[j])
+                if s & _lib.MQR_FRAME_CONF_OK:
+                    has[j] = True
+                    continue
+                if not DepthDataIO.is_depth_map_valid(st.raw[j]):
+                    continue
+                cm = (None if s & _lib.MQR_FRAME_CONF_MISSING else
+                      depth_data_io.load_confidence_map(side=side, timestamp=dataset.timestamps[i]))
+            except Exception as e:  # noqa: BLE001 -- re-raised by the caller after the prefix
+                return i, has[:j], _Raised(i, e)
             if cm is None:
-                print(f"[Warning] Confidence map not found for timestamp {ts[j]}")
+                print(f"[Warning] Confidence map not found for timestamp {dataset.timestamps[i]}")
                 continue
             put_mask(st, j, cm)
             has[j] = True
-        return lo, hi, (st, has)
+        return hi, has, None
 
     stage = {}  # (H, W) -> DeviceBuffer of CHUNK decoded frames
 
@@ -344,13 +388,24 @@ def integrate(dataset, depth_data_io, side, use_confidence_filtered_depth: bool,
         fut = submit(pool, 0, turn) if n else None
         while fut is not None:
             t0 = time.perf_counter()
-            lo, hi, items = fut.result()
+            lo, hi, items, msgs, err = fut.result()
             t1 = time.perf_counter()
             times["wait_io"] += t1 - t0
             turn ^= 1
-            fut = submit(pool, hi, turn) if hi < n else None
+            # the next chunk's reads overlap this chunk's device work -- unless a read raised in this one
+            end = chunk_end(lo)
+            fut = submit(pool, end, turn) if end < n and err is None else None
+            for m in msgs:  # this chunk's messages, in frame order, before its frames are integrated
+                print(m)
+            if isinstance(items, tuple) and items[0] == "native":
+                hi, has, err = finish_native(lo, hi, items[1], items[2])
+                if err is not None and fut is not None:  # never read past the frame that raised
+                    fut.cancel()
+                    fut = None
+                items = (items[1], has)
             if isinstance(items, tuple):
-                run_staged(lo, hi, *items)
+                if hi > lo:
+                    run_staged(lo, hi, *items)
             else:
                 # consecutive runs of one frame size, in dataset order (the running average is order-dependent)
                 j = 0
@@ -366,6 +421,12 @@ def integrate(dataset, depth_data_io, side, use_confidence_filtered_depth: bool,
             times["chunks"] += 1
             if bar is not None:
                 bar.update(hi - lo)
+            if err is not None:
+                if bar is not None:
+                    bar.close()
+                for b in stage.values():
+                    b.free()
+                raise err.exc
     if bar is not None:
         bar.close()
     for b in stage.values():

@@ -121,3 +121,44 @@ def test_integrate_dropin_ragged_frame_sizes(tmp_path, chunk, monkeypatch):
         assert d is not None and d.shape == (ds.heights[i], ds.widths[i])
         ref.integrate_frame(d, K[i], T[i], 1.0, 4.0, 10.0)
     assert compare_volumes(vbg.export(), ref.export(), 0.0) == 0.0
+
+
+@pytest.mark.parametrize("native_io", [True, False])
+@pytest.mark.parametrize("chunk", [4, 127])
+def test_integrate_dropin_failure_prefix(tmp_path, chunk, native_io, capsys, monkeypatch):
+    """A frame whose read raises mid-chunk (a raw file of the wrong size: the reference's
+    np.fromfile(...).reshape raises ValueError, depth_data_io.py:46): the exception leaves integrate()
+    with every earlier frame integrated and nothing of it or after it, and only the earlier frames'
+    messages printed -- the reference's per-frame loop (o3d_utils.py:188-236).  Frame 6 (after the
+    failing frame 5) has no confidence map: its warning must not appear."""
+    from gpu_helpers import compare_volumes
+    from mqr import o3d_utils
+    from mqr.o3d_utils import _masked_depth, compute_o3d_intrinsic_matrices, integrate
+    from mqr.vbg import VoxelBlockGrid
+    monkeypatch.setattr(o3d_utils, "CHUNK", chunk)
+    if not native_io:
+        monkeypatch.setenv("MQR_NATIVE_IO", "0")
+    io, ds, Side = _capture(tmp_path)
+    files = sorted((tmp_path / "left_depth").glob("*.raw"))
+    fail = 5
+    np.zeros(240 * 320 + 7, "<f4").tofile(files[fail - 1])  # files[3] was deleted: index fail - 1 is frame 5
+    assert ds.timestamps[fail] == int(files[fail - 1].stem)
+    kw = dict(use_confidence_filtered_depth=True, confidence_threshold=0.2, valid_count_threshold=2)
+    vbg = VoxelBlockGrid(voxel_size=0.01, block_resolution=16, block_count=500, device=0)
+    capsys.readouterr()
+    with pytest.raises(ValueError):
+        integrate(ds, io, Side.LEFT, voxel_size=0.01, block_resolution=16, block_count=500, depth_max=4.0,
+                  trunc_voxel_multiplier=10.0, device="CUDA:0", vbg_opt=vbg, **kw)
+    assert "Confidence map not found" not in capsys.readouterr().out
+    ref = oracle.OracleVBG(0.01, 16, 256)
+    K = compute_o3d_intrinsic_matrices(ds).astype(np.float64)
+    T = ds.transforms.extrinsics_wc.astype(np.float64)
+    used = 0
+    for i in range(fail):
+        d = _masked_depth(io, Side.LEFT, i, ds, **kw)
+        if d is not None:
+            ref.integrate_frame(d, K[i], T[i], 1.0, 4.0, 10.0)
+            used += 1
+    assert used == fail - 1  # frame 3 is missing
+    assert vbg.size() > 0
+    assert compare_volumes(vbg.export(), ref.export(), 0.0) == 0.0
