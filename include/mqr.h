@@ -49,8 +49,9 @@ const char* mqr_last_error(void);
 int mqr_device_count(int* n);
 /* The calling thread's caller stream (a hipStream_t; NULL = the null stream, the default): see
  * "stream ordering" above.  A PyTorch caller passes torch.cuda.current_stream().cuda_stream (the
- * Python layer does this by itself); the stream must belong to the device of the calls that follow
- * (status 2 otherwise).  mqr_get_stream reads the current setting. */
+ * Python layer does this by itself).  A caller stream of another device than the call's is drained on
+ * the host instead (hipStreamSynchronize; no cross-device stream wait); an invalid one is status 2.
+ * mqr_get_stream reads the current setting. */
 int mqr_set_stream(void* stream);
 int mqr_get_stream(void** stream);
 
@@ -59,6 +60,9 @@ int mqr_device_alloc(int device, int64_t bytes, void** ptr);
 int mqr_device_free(int device, void* ptr);
 int mqr_memcpy(void* dst, int dst_loc, const void* src, int src_loc, int64_t bytes, int device);
 int mqr_device_synchronize(int device);
+/* hipMemGetInfo of `device`: free and total HBM bytes (the Python layer keeps a released volume for
+ * reuse only while enough stays free). */
+int mqr_device_mem_info(int device, int64_t* free_bytes, int64_t* total_bytes);
 
 /* o3d.t.geometry.VoxelBlockGrid(attr_names=('tsdf','weight'), attr_dtypes=(f32,f32), attr_channels=(1,1),
  *                               voxel_size, block_resolution, block_count, device)

@@ -48,12 +48,16 @@ int order_after_caller(int device, hipStream_t a, hipStream_t b) {
     MQR_REQUIRE(device >= 0 && device < kOrderDevices, "device index out of range");
     if (t_caller_stream) {
         hipDevice_t sd = -1;
-        if (hipStreamGetDevice(t_caller_stream, &sd) != hipSuccess || sd != device) {
+        if (hipStreamGetDevice(t_caller_stream, &sd) != hipSuccess) {
             (void)hipGetLastError();
-            set_error("the caller stream given to mqr_set_stream belongs to device " + std::to_string((int)sd) +
-                      ", the call works on device " + std::to_string(device) +
-                      ": pass a stream of that device (torch: torch.cuda.set_device / torch.cuda.stream)");
+            set_error("the caller stream given to mqr_set_stream is not a valid stream (destroyed?)");
             return 2;
+        }
+        if (sd != device) {
+            // a stream of another device (e.g. torch's current stream on cuda:0 while the call works on a
+            // volume on device 1): no device-side wait across devices -- drain it on the host instead
+            MQR_CHECK_HIP(hipStreamSynchronize(t_caller_stream));
+            return 0;
         }
     }
     hipEvent_t& e = t_order_ev[device];
@@ -830,6 +834,16 @@ int mqr_memcpy(void* dst, int dst_loc, const void* src, int src_loc, int64_t byt
                                                : (src_loc == MQR_DEVICE ? hipMemcpyDeviceToHost : hipMemcpyHostToHost);
     if (kind == hipMemcpyDeviceToHost && bytes >= (int64_t)kD2HParallelMin) return d2h_parallel(device, dst, src, (size_t)bytes);
     MQR_CHECK_HIP(hipMemcpy(dst, src, (size_t)bytes, kind));
+    return 0;
+}
+
+int mqr_device_mem_info(int device, int64_t* free_bytes, int64_t* total_bytes) {
+    MQR_REQUIRE(free_bytes && total_bytes, "null argument");
+    MQR_CHECK_HIP(hipSetDevice(device));
+    size_t f = 0, t = 0;
+    MQR_CHECK_HIP(hipMemGetInfo(&f, &t));
+    *free_bytes = (int64_t)f;
+    *total_bytes = (int64_t)t;
     return 0;
 }
 

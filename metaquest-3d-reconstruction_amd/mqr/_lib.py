@@ -46,6 +46,7 @@ SIGNATURES = {
     "mqr_device_free": (ctypes.c_int, [ctypes.c_int, _vp]),
     "mqr_memcpy": (ctypes.c_int, [_vp, ctypes.c_int, _vp, ctypes.c_int, ctypes.c_int64, ctypes.c_int]),
     "mqr_device_synchronize": (ctypes.c_int, [ctypes.c_int]),
+    "mqr_device_mem_info": (ctypes.c_int, [ctypes.c_int, _i64p, _i64p]),
     "mqr_vbg_create": (ctypes.c_int, [ctypes.c_float, ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.POINTER(_vp)]),
     "mqr_vbg_destroy": (ctypes.c_int, [_vp]),
     "mqr_vbg_reset": (ctypes.c_int, [_vp]),

@@ -179,7 +179,7 @@ def _native_paths(depth_data_io, side, dataset):
     reference's DepthDataIO through its path config), one frame size, and the decoded frames within
     RESIDENT_MAX_BYTES; else None."""
     from .dataio import DepthDataIO
-    from .o3d_utils import _frame_paths
+    from .o3d_utils import _frame_paths, _reference_methods_intact
     paths = _frame_paths(depth_data_io, side)
     if paths is None:
         return None
@@ -190,6 +190,8 @@ def _native_paths(depth_data_io, side, dataset):
         cls = type(depth_data_io)
         if any(getattr(cls, m) is not getattr(DepthDataIO, m) for m in methods):
             return None
+    elif not _reference_methods_intact(depth_data_io, methods):  # a subclass of the reference's overrides one
+        return None
     if len(dataset) == 0 or len(set(zip(np.asarray(dataset.widths).tolist(), np.asarray(dataset.heights).tolist()))) != 1:
         return None
     if 4 * len(dataset) * int(dataset.widths[0]) * int(dataset.heights[0]) > RESIDENT_MAX_BYTES:

@@ -115,6 +115,20 @@ def _raw_reader(depth_data_io, side):
     return None
 
 
+def _reference_methods_intact(depth_data_io, methods) -> bool:
+    """False when one of `methods` is replaced on the instance, or overridden by a subclass of the
+    reference's DepthDataIO (scripts/dataio/depth_data_io.py; a class of that name in the MRO): then the
+    native readers / writers must not stand in for it.  A duck type of the reference's shape (no such
+    base) keeps its methods as the standard ones."""
+    if set(methods) & set(getattr(depth_data_io, "__dict__", {})):
+        return False
+    mro = type(depth_data_io).__mro__
+    base = next((c for c in mro if c.__name__ == "DepthDataIO"), None)
+    if base is None:
+        return True
+    return not any(m in c.__dict__ for c in mro[:mro.index(base)] for m in methods)
+
+
 def _frame_paths(depth_data_io, side):
     """(raw path fn, confidence npz path fn) of timestamp when the frames are read by the standard loaders
     -- this package's DepthDataIO (methods not overridden) or the reference's (its depth_path_config:
@@ -132,7 +146,8 @@ def _frame_paths(depth_data_io, side):
         return None
     cfg = getattr(depth_data_io, "depth_path_config", None)
     if (not hasattr(depth_data_io, "load_raw_depth") and cfg is not None and hasattr(cfg, "get_depth_map_path")
-            and hasattr(cfg, "get_depth_confidence_map_path")):
+            and hasattr(cfg, "get_depth_confidence_map_path")
+            and _reference_methods_intact(depth_data_io, ("load_depth_map", "load_confidence_map"))):
         return ((lambda ts: cfg.get_depth_map_path(side=side, timestamp=ts)),
                 (lambda ts: cfg.get_depth_confidence_map_path(side=side, timestamp=ts)))
     return None

@@ -84,12 +84,24 @@ def _mat(m, shape) -> np.ndarray:
 # Released grids kept for reuse: creating and destroying a grid (its HBM pool and hash table, its streams)
 # cost ~2.6 ms per fresh volume, which the fragment path pays once per 100 frames (tools/fragment_probe.py).
 # A released grid that never grew is reset (the state of a new grid, mqr_vbg_reset) and handed to the next
-# VoxelBlockGrid of the same voxel size, resolution, block count and device.  At most SPARE_GRIDS are kept,
-# and only grids whose pool is at most SPARE_MAX_BYTES (a large volume's HBM is not held back).
+# VoxelBlockGrid of the same voxel size, resolution, block count and device.  Budget per process: at most
+# SPARE_GRIDS kept in total, only grids whose pool is at most SPARE_MAX_BYTES (the reference's default
+# 50 000-block grid at R = 16 is 1.64 GB; a large volume's HBM is not held back), and only while at least
+# SPARE_MIN_FREE of the device's HBM stays free (hipMemGetInfo).  A create that fails while spares are
+# held releases them and tries once more.  A 4-process fragment pool on one GPU thus holds <= 8 GiB.
 SPARE_GRIDS = 1
-SPARE_MAX_BYTES = 4 << 30
+SPARE_MAX_BYTES = 2 << 30
+SPARE_MIN_FREE = 0.25
 _spares = []  # [(key, handle)]
 _spares_lock = threading.Lock()
+
+
+def _hbm_headroom(device) -> bool:
+    """At least SPARE_MIN_FREE of `device`'s HBM is free (a spare grid is kept only then)."""
+    free, total = ctypes.c_int64(), ctypes.c_int64()
+    if _lib._lib.mqr_device_mem_info(int(device), ctypes.byref(free), ctypes.byref(total)) != 0 or total.value <= 0:
+        return False
+    return free.value >= SPARE_MIN_FREE * total.value
 
 
 def release_spare_grids():
@@ -118,8 +130,18 @@ class VoxelBlockGrid:
             h = _spares.pop(i)[1] if i is not None else None
         if h is None:
             h = ctypes.c_void_p()
-            call("mqr_vbg_create", self.voxel_size, self.block_resolution, int(block_count), self.device_id,
-                 ctypes.byref(h))
+            try:
+                call("mqr_vbg_create", self.voxel_size, self.block_resolution, int(block_count), self.device_id,
+                     ctypes.byref(h))
+            except _lib.MqrError:
+                with _spares_lock:
+                    held = bool(_spares)
+                if not held:
+                    raise
+                release_spare_grids()  # their HBM may be what the new grid lacks
+                h = ctypes.c_void_p()
+                call("mqr_vbg_create", self.voxel_size, self.block_resolution, int(block_count), self.device_id,
+                     ctypes.byref(h))
         self._h = h
 
     # -- lifetime -----------------------------------------------------------------------------
@@ -133,6 +155,7 @@ class VoxelBlockGrid:
             cap = ctypes.c_int64(-1)
             # (the integrate configuration back to a new grid's default, then emptied)
             if (key is not None and SPARE_GRIDS > 0 and key[2] * key[1] ** 3 * 8 <= SPARE_MAX_BYTES
+                    and _hbm_headroom(key[3])
                     and _lib._lib.mqr_vbg_capacity(h, ctypes.byref(cap)) == 0
                     and cap.value == key[2] and _lib._lib.mqr_vbg_set_variant(h, 0) == 0
                     and _lib._lib.mqr_vbg_reset(h) == 0):

@@ -100,3 +100,54 @@ def test_dropin_failure_prefix(tmp_path, capsys, monkeypatch, fakes, chunk, nati
     assert isinstance(err, ValueError)
     assert frames == [i for i in range(fail) if i not in (3, 9)]
     assert out.count("[Warning] Confidence map not found") == (1 if fail > 6 else 0)
+
+
+def test_native_paths_respect_subclass_overrides(tmp_path):
+    """A subclass of the reference's DepthDataIO that overrides a loader or the saver at class level
+    keeps its override: the native readers / writers are not used for it."""
+    from mqr.confidence import _native_paths
+    from mqr.o3d_utils import _frame_paths
+    io, ds, Side, _ = _capture(tmp_path)
+
+    class _Paths:
+        def get_depth_map_path(self, side, timestamp):
+            return io.paths.depth_map_path(side, timestamp)
+
+        def get_depth_confidence_map_path(self, side, timestamp):
+            return io.paths.confidence_path(side, timestamp)
+
+    class DepthDataIO:  # the reference's class name (scripts/dataio/depth_data_io.py)
+        def __init__(self):
+            self.depth_path_config = _Paths()
+
+        def load_depth_map(self, side, timestamp, width, height, near, far):
+            return io.load_depth_map(side, timestamp, width, height, near, far)
+
+        def load_depth_map_by_index(self, side, dataset, index):
+            return io.load_depth_map_by_index(side, dataset, index)
+
+        def is_depth_map_valid(self, depth_map):
+            return io.is_depth_map_valid(depth_map)
+
+        def load_confidence_map(self, side, timestamp):
+            return io.load_confidence_map(side, timestamp)
+
+        def save_confidence_map(self, side, timestamp, confidence_map):
+            return io.save_confidence_map(side, timestamp, confidence_map)
+
+    class Loads(DepthDataIO):
+        def load_confidence_map(self, side, timestamp):
+            return None
+
+    class Saves(DepthDataIO):
+        def save_confidence_map(self, side, timestamp, confidence_map):
+            pass
+
+    assert _frame_paths(DepthDataIO(), Side.LEFT) is not None
+    assert _frame_paths(Loads(), Side.LEFT) is None
+    assert _frame_paths(Saves(), Side.LEFT) is not None       # integrate() reads only
+    assert _native_paths(DepthDataIO(), Side.LEFT, ds) is not None
+    assert _native_paths(Saves(), Side.LEFT, ds) is None
+    inst = DepthDataIO()
+    inst.load_confidence_map = lambda side, timestamp: None   # replaced on the instance
+    assert _frame_paths(inst, Side.LEFT) is None
