@@ -751,6 +751,196 @@ def c5_leg(args, device, frames_per_side=2000, voxel=0.003, key_every=40, parity
     return out
 
 
+def c5_sharded_leg(args, rank, world, dev, merge_fn, dist, parity=True, frames_per_side=2000, voxel=0.003,
+                   key_every=40):
+    """C5 in its multi-GPU form (BASELINE.json configs[4]; reconstruct_scene.py:64-122, 181-225): the
+    2000 + 2000 frame hall walk at 3 mm (c5_leg's capture, seeded once, so every rank count shards the
+    same frames) split over the ranks by contiguous frame ranges; each rank integrates its range into
+    its own volume (pool grown from 16384 blocks by a first, untimed pass), ONE exchange (merge_fn:
+    mqr_reduce_rccl, or the gloo-staged twin in a rehearsal) leaves every rank its owned slice of the
+    block union plus a one-block halo, every rank extracts its owned cubes' mesh at 1.5
+    (mqr_extract_mesh_owned) and colours its shard mesh from every key_every-th frame.  Colour-aligned
+    depth: each rank casts the keyframe views against its shard mesh and the per-pixel MIN over ranks
+    (an all-reduce over the gloo control plane, host-staged) is the cast against the whole mesh -- the
+    triangles partition the mesh, and the closest hit of a union is the least of its parts'.  The
+    3-NN fill of unseen vertices draws on the shard's own sampled vertices (the one deviation from
+    colouring the concatenated mesh in one call).
+
+    Parity (rank 0 gathers the owned slices point to point): the merged owned slices against the
+    oracle's sequential pass over all 4000 frames (keys and weights exact, tsdf within 1e-4), the
+    shard meshes' triangle count against the oracle mesh's, and every rank's colours bit for bit
+    against the oracle's colour_map on the same shard vertices and reduced depth."""
+    import numpy as np
+    import torch
+    from mqr import synthetic
+    from mqr.color import color_map
+    from mqr.distributed import extract_mesh_owned, shard_range
+    from mqr.raycasting import RaycastingScene
+    from mqr.vbg import VoxelBlockGrid
+    H, W = args.height, args.width
+    left = synthetic.hall_loop_poses(frames_per_side)
+    right = [(R_, t_ + R_[:, 0] * 0.064) for R_, t_ in left]
+    poses = left + right
+    B = len(poses)
+    t0 = time.perf_counter()
+    seq = synthetic.make_sequence_fast("hall", poses=poses, height=H, width=W, seed=5, device=f"cuda:{dev}")
+    gen_s = time.perf_counter() - t0
+    K, T = seq["K"].astype(np.float64), seq["T_wc"].astype(np.float64)
+    lo, hi = shard_range(B, rank, world)
+    host = seq["depth_t"].cpu().numpy() if (parity and rank == 0) else None
+    part = seq["depth_t"][lo:hi].contiguous().clone()
+    del seq
+    torch.cuda.empty_cache()
+
+    class _P:
+        ptr = ctypes.c_void_p(part.data_ptr())
+
+    vbg = VoxelBlockGrid(voxel_size=voxel, block_resolution=16, block_count=16384, device=dev)
+    kw = dict(depth_scale=1.0, depth_max=args.depth_max, trunc_voxel_multiplier=args.trunc)
+    vbg.integrate_frames((_P, hi - lo, H, W), K[lo:hi], T[lo:hi], **kw)  # grows the pool (untimed)
+
+    def wall_max(fn):
+        dist.barrier()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        r = fn()
+        torch.cuda.synchronize()
+        e = torch.tensor([time.perf_counter() - t], dtype=torch.float64)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        return r, float(e.item()) * 1e3
+
+    def integrate():
+        vbg.reset()
+        vbg.integrate_frames((_P, hi - lo, H, W), K[lo:hi], T[lo:hi], **kw)
+
+    _, int_ms = wall_max(integrate)
+    stats = {}
+    (out, owned), merge_ms = wall_max(lambda: merge_fn(vbg, stats))
+    del vbg
+    mesh, ext_ms = wall_max(lambda: extract_mesh_owned(out, owned, 1.5))
+    key = list(range(0, B, key_every))
+    imgs = synthetic.render_color_torch("hall", K[0], [poses[i] for i in key], H, W, device=f"cuda:{dev}").cpu().numpy()
+
+    def cast():
+        if len(mesh.triangles) == 0:
+            return np.full((len(key), H, W), np.inf, np.float32)
+        scene = RaycastingScene(device=dev)
+        scene.add_triangles(mesh.vertices, mesh.triangles)
+        return np.ascontiguousarray(scene.cast_pinhole(K[key], T[key], W, H)["t_hit"].numpy(), np.float32)
+
+    cad_local, cast_ms = wall_max(cast)
+
+    def reduce_min():
+        t = torch.from_numpy(cad_local)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return t.numpy()
+
+    cad, reduce_ms = wall_max(reduce_min)
+    def colour():
+        if len(mesh.vertices) == 0:
+            return np.zeros((0, 3), np.float32), np.zeros(0, np.int32)
+        return color_map(mesh.vertices, imgs, cad, K[key], T[key], device=dev)
+
+    (col, cnt), col_ms = wall_max(colour)
+    st = torch.tensor([len(mesh.triangles), len(mesh.vertices), owned, stats.get("sent_bytes", 0),
+                       stats.get("recv_bytes", 0)], dtype=torch.float64)
+    allst = [torch.zeros_like(st) for _ in range(world)]
+    dist.all_gather(allst, st)
+    allst = torch.stack(allst)
+    rec = {"frames": B, "voxel_size": voxel, "frames_per_gpu": [shard_range(B, r, world)[1] - shard_range(B, r, world)[0]
+                                                               for r in range(world)],
+           "integrate_ms_max": int_ms, "merge_ms_max": merge_ms, "frames_per_s": B / ((int_ms + merge_ms) * 1e-3),
+           "extract_owned_ms_max": ext_ms, "colour_depth_cast_ms_max": cast_ms, "colour_depth_min_reduce_ms": reduce_ms,
+           "colour_ms_max": col_ms, "triangles": int(allst[:, 0].sum()),
+           "vertices_with_boundary_copies": int(allst[:, 1].sum()), "union_blocks": int(allst[:, 2].sum()),
+           "merge_max_sent_bytes": float(allst[:, 3].max()), "merge_max_recv_bytes": float(allst[:, 4].max()),
+           "keyframes": len(key), "generation_s": gen_s,
+           "note": "frames_per_s = 4000 / (integrate + merge), each the max over ranks of a barrier-bracketed "
+                   "wall time; extraction (host copy of the shard mesh included), colour-view casts, the "
+                   "host-staged MIN all-reduce of the cast depth and the colouring timed after it"}
+    if parity:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle
+        from gpu_helpers import _key_order
+        cores, _ = host_cores()
+        # every rank's colours vs the oracle on the same inputs (ranks share the host cores)
+        oracle.set_threads(max(1, cores // world))
+        if len(mesh.vertices):
+            oc, on = oracle.color_map(mesh.vertices, imgs, cad, K[key], T[key])
+            col_ok = bool(np.array_equal(col, oc) and np.array_equal(cnt, on))
+            del oc, on
+        else:
+            col_ok = True
+        k_, t_, w_ = out.export()
+        k_, t_, w_ = k_[:owned], t_[:owned], w_[:owned]
+        R3 = 16 ** 3
+        if rank == 0:
+            log("C5 sharded parity: oracle pass over the whole capture")
+            oracle.set_threads(cores)
+            ref = oracle_volume(host, K, T, voxel, args, block_count=16384)
+            del host
+            ok_, ot, ow = ref.export()
+            _, _, otri = ref.extract_mesh(1.5)
+            n_otri = len(otri)
+            del ref, otri
+            oa = _key_order(ok_)
+            ok_, ot, ow = ok_[oa], ot[oa].reshape(-1, R3), ow[oa].reshape(-1, R3)
+            okp = (ok_[:, 0].astype(np.int64) + (1 << 20)) << 42 | (ok_[:, 1].astype(np.int64) + (1 << 20)) << 21 | \
+                (ok_[:, 2].astype(np.int64) + (1 << 20))
+            seen, weq, err = 0, True, 0.0
+            for r in range(world):
+                if r == 0:
+                    rk, rt, rw = k_, t_.reshape(-1, R3), w_.reshape(-1, R3)
+                else:
+                    n = torch.zeros(1, dtype=torch.int64)
+                    dist.recv(n, src=r)
+                    n = int(n.item())
+                    rk, rt, rw = torch.empty((n, 3), dtype=torch.int32), torch.empty((n, R3)), torch.empty((n, R3))
+                    for x in (rk, rt, rw):
+                        dist.recv(x, src=r)
+                    rk, rt, rw = rk.numpy(), rt.numpy(), rw.numpy()
+                rp = (rk[:, 0].astype(np.int64) + (1 << 20)) << 42 | (rk[:, 1].astype(np.int64) + (1 << 20)) << 21 | \
+                    (rk[:, 2].astype(np.int64) + (1 << 20))
+                j = np.searchsorted(okp, rp)
+                found = (j < len(okp)) & (okp[np.minimum(j, len(okp) - 1)] == rp)
+                if not found.all():
+                    weq = False
+                    break
+                seen += len(rp)
+                for c in range(0, len(j), 4096):
+                    jj = j[c:c + 4096]
+                    weq = weq and bool(np.array_equal(rw[c:c + 4096], ow[jj]))
+                    m = rw[c:c + 4096] > 0
+                    if m.any():
+                        err = max(err, float(np.abs(rt[c:c + 4096][m] - ot[jj][m]).max()))
+            keys_ok = weq and seen == len(okp)
+            res = torch.tensor([float(keys_ok), float(weq), err, float(n_otri)], dtype=torch.float64)
+        else:
+            dist.send(torch.tensor([len(k_)], dtype=torch.int64), dst=0)
+            for x in (k_, t_.reshape(-1, R3), w_.reshape(-1, R3)):
+                dist.send(torch.from_numpy(np.ascontiguousarray(x)), dst=0)
+            res = torch.zeros(4, dtype=torch.float64)
+        del k_, t_, w_
+        dist.broadcast(res, src=0)
+        cok = torch.tensor([1 if col_ok else 0], dtype=torch.int32)
+        dist.all_reduce(cok, op=dist.ReduceOp.MIN)
+        tri_ok = int(res[3].item()) == rec["triangles"]
+        rec["parity"] = {"keys_equal": bool(res[0].item()), "weights_equal": bool(res[1].item()),
+                         "max_dtsdf": float(res[2].item()), "tolerance": 1e-4,
+                         "oracle_triangles": int(res[3].item()), "triangle_count_equal": tri_ok,
+                         "colours_equal": bool(cok.item()),
+                         "comparison": "owned slices of the merged shards vs the oracle's sequential pass over all "
+                                       "4000 frames (keys / weights exact, tsdf within tolerance), shard triangle counts "
+                                       "summed vs the oracle mesh at 1.5, every rank's colours and counts bit for bit vs "
+                                       "oracle.color_map on its shard vertices with the reduced colour-view depth"}
+        rec["parity"]["all_ok"] = bool(rec["parity"]["keys_equal"] and rec["parity"]["weights_equal"]
+                                       and rec["parity"]["max_dtsdf"] <= 1e-4 and tri_ok and rec["parity"]["colours_equal"])
+    del out, mesh, part
+    torch.cuda.empty_cache()
+    return rec
+
+
 def c4_leg(args, device, frames_per_side=1000, reps=3, parity=True):
     """C4 on one GPU (BASELINE.json configs[3], the N = 1 point): 1000 LEFT + 1000 RIGHT frames of
     the room walk (0.064 m stereo baseline), 640x480, 5 mm, integrated as reconstruct_scene.py:64-81
@@ -1218,8 +1408,10 @@ def main():
     if world > 1:
         # control plane only (barriers, the RCCL id, max-over-ranks timing); volume data moves over
         # RCCL inside libmqr_hip.so (mqr_reduce_rccl)
+        import datetime
         import torch.distributed as dist
-        dist.init_process_group("gloo")
+        # a rank stuck in a collective (its peer died) fails after 10 minutes instead of gloo's 30
+        dist.init_process_group("gloo", timeout=datetime.timedelta(minutes=10))
     # N > 1 measures BASELINE's C4 (a fixed 2000-frame L+R capture split over the ranks) unless --weak
     strong = args.strong or (world > 1 and not args.weak)
 
@@ -1296,9 +1488,11 @@ def main():
             shard["out"], shard["owned"] = merge_rccl(vbg, comm, mode=args.merge, out=shard["out"])
             merge_phases.append(comm.timing())
         else:
-            shard["out"], shard["owned"] = merge_staged(vbg, mode=args.merge, out=shard["out"])
+            shard["out"], shard["owned"] = merge_staged(vbg, mode=args.merge, out=shard["out"], stats=shard)
         torch.cuda.synchronize()
         merge_times.append(time.perf_counter() - t)
+        if comm is not None:
+            shard.update(comm.counts())
 
     def step():
         vbg.reset()
@@ -1344,13 +1538,25 @@ def main():
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
     merge_ms = (sum(merge_times) / len(merge_times) * 1e3) if merge_times else None
+    merge_bytes = None
+    if dist and "sent_bytes" in shard:
+        # what each rank's exchange moved to / from its peers (self segment excluded), last timed step
+        mb = torch.tensor([shard["sent_bytes"], shard["recv_bytes"], shard["sent_blocks"], shard["recv_blocks"]],
+                          dtype=torch.float64)
+        allmb = [torch.zeros_like(mb) for _ in range(world)]
+        dist.all_gather(allmb, mb)
+        allmb = torch.stack(allmb)
+        merge_bytes = {"sent_bytes_per_rank": allmb[:, 0].tolist(), "recv_bytes_per_rank": allmb[:, 1].tolist(),
+                       "max_sent_bytes": float(allmb[:, 0].max()), "max_recv_bytes": float(allmb[:, 1].max()),
+                       "total_bytes": float(allmb[:, 0].sum()), "bytes_per_block": 8 * args.block_resolution ** 3,
+                       "note": "(tsdf, weight) float32 of whole blocks to each peer, the local self segment excluded"}
     merge_phases_ms = ({k: sum(p[k] for p in merge_phases) / len(merge_phases) for k in merge_phases[0]}
                        if merge_phases else None)
 
     blocks = vbg.size()
     R3_ = args.block_resolution ** 3
     ext_ms, (nv, nt) = (None, (0, 0))
-    sharded = sharded_par = weak_leg = None
+    sharded = sharded_par = weak_leg = c5_sharded = None
     if world > 1:
         # every rank extracts its owned cubes (mqr_extract_mesh_owned); the mesh is the concatenation
         from mqr.distributed import extract_mesh_owned
@@ -1418,6 +1624,23 @@ def main():
                         "merge_ms": sum(merge_times) / len(merge_times) * 1e3, "union_blocks": shard["out"].size()
                         if args.merge == "root" else None}
             del wd, wseq
+        if not args.no_c5:
+            # C5's multi-GPU form: 4000 hall frames at 3 mm sharded, one exchange, owned-cube meshes, colour
+            def c5_merge(v, st):
+                if comm is not None:
+                    o = merge_rccl(v, comm, mode="sharded")
+                    st.update(comm.counts())
+                    return o
+                return merge_staged(v, mode="sharded", stats=st)
+
+            log(f"rank {rank}: C5 sharded sub-leg")
+            try:
+                c5_sharded = c5_sharded_leg(args, rank, world, local, c5_merge, dist,
+                                            parity=not (args.no_cpu or args.no_parity))
+            except Exception as e:  # noqa: BLE001 -- reported in the line; the C4 headline stands
+                log(f"rank {rank}: C5 sharded sub-leg failed: {type(e).__name__}: {e}")
+                c5_sharded = {"error": f"rank {rank}: {type(e).__name__}: {e}"}
+            torch.cuda.empty_cache()
     elif rank == 0:
         ext_ms, (nv, nt) = extract_ms(vbg, args.extract_threshold, args.extract_reps)
 
@@ -1522,6 +1745,7 @@ def main():
             "merge_ms": merge_ms,
             "merge_phases_ms": merge_phases_ms,
             "merge_transport": transport,
+            "merge_bytes_per_rank": merge_bytes,
             "weak_c2": weak_leg,
             "union_blocks": blocks if world > 1 else None,
             "extract_ms": ext_ms,
@@ -1557,6 +1781,7 @@ def main():
             "c3": extras.get("c3"),
             "c4": extras.get("c4"),
             "c5": extras.get("c5"),
+            "c5_sharded": c5_sharded,
             "dropin_e2e": extras.get("dropin_e2e"),
         }
         print(json.dumps(out), flush=True)

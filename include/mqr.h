@@ -150,6 +150,10 @@ int mqr_comm_destroy(mqr_comm* comm);
 int mqr_reduce_rccl(mqr_vbg* local, mqr_comm* comm, int mode, int root, mqr_vbg* out, int64_t* n_owned);
 int mqr_merge_local(mqr_vbg** locals, int n, int mode, int root, mqr_vbg** outs, int64_t* n_owned);
 int mqr_comm_timing(mqr_comm* comm, float* ms4);
+/* Segment sizes of the last mqr_reduce_rccl on `comm`: blocks sent to / received from each rank
+ * (world entries each; the own rank's entry is the local self segment, not carried by RCCL) and the
+ * floats per block (2 R^3).  Zeros before the first merge. */
+int mqr_comm_counts(mqr_comm* comm, int64_t* send_blocks, int64_t* recv_blocks, int64_t* floats_per_block);
 int mqr_merge_local_timing(float* ms, int n);
 typedef struct mqr_xchg mqr_xchg;
 int mqr_xchg_create(mqr_vbg* local, int world, int rank, int mode, int root, const uint64_t* gathered_keys,

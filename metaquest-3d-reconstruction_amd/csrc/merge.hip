@@ -659,6 +659,18 @@ int mqr_comm_timing(mqr_comm* c, float* ms4) {
     return 0;
 }
 
+int mqr_comm_counts(mqr_comm* c, int64_t* send_blocks, int64_t* recv_blocks, int64_t* floats_per_block) {
+    MQR_REQUIRE(c, "null argument");
+    const Exchange& x = *c->x;
+    const bool run = (int)x.soff.size() == c->world + 1;  // a merge has run on this communicator
+    for (int p = 0; p < c->world; ++p) {
+        if (send_blocks) send_blocks[p] = run ? (int64_t)x.send_blocks(p) : 0;
+        if (recv_blocks) recv_blocks[p] = run ? (int64_t)x.recv_blocks(p) : 0;
+    }
+    if (floats_per_block) *floats_per_block = 2 * (int64_t)x.R3;
+    return 0;
+}
+
 int mqr_reduce_rccl(mqr_vbg* local, mqr_comm* c, int mode, int root, mqr_vbg* out, int64_t* n_owned) {
     MQR_REQUIRE(local && c && out && n_owned, "null argument");
     MQR_REQUIRE(local != out, "mqr_reduce_rccl: `out` must be a different volume than `local` (it is emptied first)");

@@ -229,6 +229,16 @@ class RcclComm:
         _lib.call("mqr_comm_timing", self._h, ms)
         return {"plan_ms": ms[0], "out_and_gather_ms": ms[1], "exchange_ms": ms[2], "merge_kernels_ms": ms[3]}
 
+    def counts(self) -> dict:
+        """Segment sizes of the last merge: blocks sent to / received from each rank (the own rank's
+        entry is the local self segment) and bytes per block."""
+        import ctypes
+        from . import _lib
+        sc, rc = np.zeros(self.world, np.int64), np.zeros(self.world, np.int64)
+        fpb = ctypes.c_int64()
+        _lib.call("mqr_comm_counts", self._h, _lib.ptr(sc, _lib._i64p), _lib.ptr(rc, _lib._i64p), ctypes.byref(fpb))
+        return _segment_stats(sc, rc, 4 * fpb.value, self.rank)
+
     def close(self):
         from . import _lib
         if getattr(self, "_h", None) is not None and self._h.value and _lib._lib is not None:
@@ -240,6 +250,16 @@ class RcclComm:
             self.close()
         except Exception:
             pass
+
+
+def _segment_stats(send_blocks, recv_blocks, bytes_per_block, rank) -> dict:
+    """What one rank's merge moved between ranks (its self segment excluded)."""
+    sc = np.asarray(send_blocks, np.int64).copy()
+    rc = np.asarray(recv_blocks, np.int64).copy()
+    sc[rank] = rc[rank] = 0
+    return {"sent_blocks": int(sc.sum()), "recv_blocks": int(rc.sum()), "sent_bytes": int(sc.sum()) * bytes_per_block,
+            "recv_bytes": int(rc.sum()) * bytes_per_block, "peers_sent_to": int((sc > 0).sum()),
+            "max_segment_bytes": int(max(sc.max(), rc.max()) * bytes_per_block) if len(sc) else 0}
 
 
 def make_comm(device: int, group=None) -> RcclComm:
@@ -284,7 +304,7 @@ def merge_local(vbgs, mode: str = "sharded", root: int = 0, outs=None):
     return list(zip(outs, owned.tolist()))
 
 
-def merge_staged(vbg, group=None, mode: str = "sharded", root: int = 0, out=None):
+def merge_staged(vbg, group=None, mode: str = "sharded", root: int = 0, out=None, stats=None):
     """mqr_reduce_rccl's exchange with the segments carried by torch.distributed over host buffers
     (gloo): one process per rank, any device (several ranks may share one GPU, which RCCL refuses).
     The plan, the send segments (packed from this rank's pool), the rank-ordered merge and the output
@@ -292,7 +312,7 @@ def merge_staged(vbg, group=None, mode: str = "sharded", root: int = 0, out=None
     isend / irecv of host tensors.  Every rank's send count to each peer is compared with that
     peer's receive count from it (an all-to-all of the counts) before any segment moves, and
     mqr_xchg_create checks that this rank's row of the gathered keys is its own.  Returns (out
-    volume, owned block count)."""
+    volume, owned block count); `stats` (a dict) receives the segment sizes (_segment_stats)."""
     import ctypes
     import torch
     import torch.distributed as dist
@@ -321,6 +341,8 @@ def merge_staged(vbg, group=None, mode: str = "sharded", root: int = 0, out=None
         if not np.array_equal(theirs.numpy(), rc):
             raise RuntimeError(f"merge_staged: rank {rank} expects {rc.tolist()} blocks from the ranks, "
                                f"which send it {theirs.numpy().tolist()}")
+        if stats is not None:
+            stats.update(_segment_stats(sc, rc, 4 * fpb.value, rank))
         ops, recvs = [], []
         for p in range(world):
             if p == rank:
