@@ -262,7 +262,7 @@ static int launch_integrate_ab(mqr_vbg* v, int var, hipStream_t s, unsigned grid
                                const int32_t* list, const bmask_t* lmask, int* counters, const Table& t,
                                const float* depths, int64_t HW, int H, int W, const FrameParams* fp,
                                const int64_t* depth_frame, float depth_max, float sdf_trunc, int first_new,
-                               int32_t* bad_out, bool* fixup) {
+                               int32_t* bad_out, bool* fixup, int nframes) {
     // k_integrate_lean_ab<16, 512, MAP, WPE, ILP, PAIR, DIV1, ZBLK, FIXIN>
     auto lean = [&](auto kern) {
         hipLaunchKernelGGL(kern, dim3(lean_grid), dim3(512), 0, s, list, lmask, bad_out, counters, v->list_cap, t,
@@ -332,6 +332,33 @@ static int launch_integrate_ab(mqr_vbg* v, int var, hipStream_t s, unsigned grid
         case 42: win(k_integrate_win_ab<512, 7, 0, 0, 3>, 512); break;
         case 43: win(k_integrate_win_ab<512, 6, 0, 0, 3>, 512); break;
         case 44: win(k_integrate_win_r4<7>, 512); break;  // the round-4 default's source
+        case 45:    // lane-level tile proofs (k_tile_records + k_integrate_tp), >= 7 waves
+        case 46: {  // the same at >= 6 waves
+            // per device, grow-only (A/B library only): the batch's 8 x 4 tile records, 8 B each
+            static void* rec_buf[64] = {};
+            static size_t rec_cap[64] = {};
+            const int TW = (W + 7) / 8, TH = (H + 3) / 4;
+            const size_t need = sizeof(uint2) * (size_t)TW * TH * (size_t)std::max(nframes, 1);
+            MQR_REQUIRE(v->device >= 0 && v->device < 64, "device index out of range");
+            if (rec_cap[v->device] < need) {
+                if (rec_buf[v->device]) MQR_CHECK_HIP(hipFree(rec_buf[v->device]));
+                rec_buf[v->device] = nullptr;
+                rec_cap[v->device] = 0;
+                MQR_CHECK_HIP(hipMalloc(&rec_buf[v->device], need));
+                rec_cap[v->device] = need;
+            }
+            uint2* recs = static_cast<uint2*>(rec_buf[v->device]);
+            hipLaunchKernelGGL(k_tile_records, dim3((unsigned)((TW * TH + 7) / 8), (unsigned)nframes), dim3(256), 0, s,
+                               depths, HW, H, W, depth_frame, depth_max, TW, TH, recs);
+            auto tp = [&](auto kern) {
+                hipLaunchKernelGGL(kern, dim3(grid), dim3(512), 0, s, list, lmask, counters, v->list_cap, t, v->pool,
+                                   v->voxel_size, depths, HW, H, W, fp, depth_frame, depth_max, sdf_trunc, first_new,
+                                   recs, TW, TH);
+            };
+            if (var == 45) tp(k_integrate_tp<7>);
+            else tp(k_integrate_tp<6>);
+            break;
+        }
         default: set_error("integrate variant " + std::to_string(var) + " unknown"); return 2;
     }
     return 0;
@@ -517,10 +544,11 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
     //     division, ILP 4, in two halves;  15 = the round-3 default (the exact path in a fix-up launch);
     //     23 = the round-4 default (k_integrate_lean_ab with the same arithmetic as 0);  24-31 the frame
     //     loop software-pipelined / 1024-thread workgroups (k_integrate_win_ab);  32-35 timing diagnostics
-    //     (wrong results);  36-39 packed FP32 (k_integrate_pk);  40-43 branch-free window offsets / updates.  (24 of round 4, a ballot skip of
+    //     (wrong results);  36-39 packed FP32 (k_integrate_pk);  40-43 branch-free window offsets / updates;  44 the
+    //     round-4 source;  45 / 46 lane-level tile proofs (k_tile_records + k_integrate_tp, >= 7 / 6 waves).  (24 of round 4, a ballot skip of
     //     out-of-image wave slots, ran 0.70 vs 0.48 ms per launch: removed.)
     int var = v->kernel_variant;
-    if (var < 0 || var > 44) var = 0;
+    if (var < 0 || var > 46) var = 0;
     if (!MQR_AB && var != 1 && var != 2 && var != 4) var = 0;
     if (var != 1 && var != 2 && !lean_ok) var = 2;
     if (var == 5 && (v->R != 16 || W % 4 != 0 || W < 4 || (reinterpret_cast<uintptr_t>(depths) & 15))) var = 0;
@@ -558,7 +586,7 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
         } else {
 #if MQR_AB
             if (launch_integrate_ab(v, var, s, grid, lean_grid, grouped, list, lmask, counters, t, depths, HW, H, W, fp,
-                                    depth_frame, depth_max, sdf_trunc, first_new, v->bad[p], &fixup))
+                                    depth_frame, depth_max, sdf_trunc, first_new, v->bad[p], &fixup, nframes))
                 return 1;
 #endif
         }

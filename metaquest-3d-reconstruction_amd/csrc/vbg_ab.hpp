@@ -1174,4 +1174,178 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
     }
 }
 
+
+// ---- A/B: lane-level tile proofs (verdict r05 item 3) ------------------------------------------------------
+// Per 8 x 4 pixel tile of every batch frame, an 8-byte record (k_tile_records): bit p of word 0 = pixel
+// (p % 8, p / 8) of the tile passes the update's depth test !(d <= 0) && !(d > depth_max) (NaN passes it),
+// word 1 = lo | hi << 16: binary16 bounds, lo <= every valid non-NaN depth of the tile (rounded down; +inf
+// if none), hi >= every one of them (rounded up; -inf if none, +inf if the tile holds a NaN).  In the frame
+// loop a lane reads its tile's record first (lanes of a wave mostly share one or two tiles) and is decided
+// without its pixel when
+//   bit 0                     -> no update (the update's own depth test fails): depth 0 stands in;
+//   fl(lo - zc) >= sdf_trunc  -> sdf >= sdf_trunc for every valid pixel of the tile (monotone rounding), so
+//                                s = sdf_trunc: a NaN depth stands in, which takes exactly that update;
+//   fl(hi - zc) < -sdf_trunc  -> sdf < -sdf_trunc: no update (depth 0).
+// Only the other lanes issue the 8-byte window read (exec-masked: a wave with none skips the load).  The
+// running-average update is lean_update_v unchanged, so the volume is bit-identical to k_integrate_win's.
+// tools/tile_proof_stats.py estimated 36 % of in-image lane-frames decided, 21 % of wave slots without a
+// pixel read, 0.66x the distinct windows, at the cost of one more (mostly one-address) load per voxel-frame.
+__device__ __forceinline__ uint32_t half_bits_down(float x) {  // binary16 bits of the largest half <= x (x >= 0 or +-inf)
+    if (!(x < 65504.0f)) return x == __builtin_inff() ? 0x7C00u : 0x7BFFu;
+    const _Float16 h = (_Float16)x;
+    uint32_t b = (uint32_t)__builtin_bit_cast(uint16_t, h);
+    if ((float)h > x) b = b == 0 ? 0x8001u : b - 1;  // x >= 0: only finite positive values round up
+    return b;
+}
+__device__ __forceinline__ uint32_t half_bits_up(float x) {  // binary16 bits of the smallest half >= x (x >= 0 or +-inf)
+    if (x == -__builtin_inff()) return 0xFC00u;
+    if (!(x <= 65504.0f)) return 0x7C00u;
+    const _Float16 h = (_Float16)x;
+    uint32_t b = (uint32_t)__builtin_bit_cast(uint16_t, h);
+    if ((float)h < x) b = b + 1;  // x >= 0 here: the next half up (65504 rounds to itself)
+    return b;
+}
+__device__ __forceinline__ float half_from_bits(uint32_t b) {
+    return (float)__builtin_bit_cast(_Float16, (uint16_t)b);
+}
+
+// One wave per two tiles (lanes 0-31 / 32-63), 8 tiles per 256-thread workgroup; blockIdx.y = batch frame.
+__global__ __launch_bounds__(256) void k_tile_records(const float* __restrict__ depths, int64_t HW, int H, int W,
+                                                      const int64_t* __restrict__ depth_frame, float depth_max,
+                                                      int TW, int TH, uint2* __restrict__ rec) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int tile = (blockIdx.x * 4 + wave) * 2 + (lane >> 5);
+    const int p = lane & 31;
+    const int ntiles = TW * TH;
+    const int tx = tile % TW, ty = tile / TW;
+    const int px = tx * 8 + (p & 7), py = ty * 4 + (p >> 3);
+    const bool in = tile < ntiles && px < W && py < H;
+    const float d = in ? depths[depth_frame[blockIdx.y] * HW + (int64_t)py * W + px] : 0.0f;
+    const bool valid = in && !(d <= 0.0f) && !(d > depth_max);
+    const bool fin = valid && d == d;
+    const uint64_t vb = __ballot(valid), nb = __ballot(valid && d != d);
+    float lo = fin ? d : __builtin_inff(), hi = fin ? d : -__builtin_inff();
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) {
+        lo = __builtin_fminf(lo, __shfl_xor(lo, o));
+        hi = __builtin_fmaxf(hi, __shfl_xor(hi, o));
+    }
+    if (p == 0 && tile < ntiles) {
+        const uint32_t half = lane >> 5;
+        const uint32_t m = (uint32_t)(vb >> (32 * half));
+        if ((uint32_t)(nb >> (32 * half))) hi = __builtin_inff();
+        rec[(int64_t)blockIdx.y * ntiles + tile] = make_uint2(m, half_bits_down(lo) | (half_bits_up(hi) << 16));
+    }
+}
+
+// lean_gather_w<ZPER, 2, 8> with the tile proofs in front of the window read.
+template <int ZPER>
+__device__ __forceinline__ void tp_gather(float (&dv)[ZPER], bool& bad, const FrameParams& fp,
+                                          __amdgpu_buffer_rsrc_t rs, __amdgpu_buffer_rsrc_t rr,
+                                          const float (&xs)[ZPER], const float (&ys)[ZPER], const float (&zs)[ZPER],
+                                          uint32_t W4, uint32_t past_end, uint32_t rec_end, uint32_t TW8,
+                                          uint32_t hm1_bits, uint32_t wm1_bits, float sdf_trunc) {
+    float e[12];
+#pragma unroll
+    for (int j = 0; j < 12; ++j) e[j] = fp.ext[j];
+    const float fx = fp.fx, fy = fp.fy, cx = fp.cx, cy = fp.cy;
+#pragma unroll
+    for (int k = 0; k < ZPER; ++k) {
+        const float ax = xs[k] * e[0] + ys[k] * e[1];
+        const float ay = xs[k] * e[4] + ys[k] * e[5];
+        const float az = xs[k] * e[8] + ys[k] * e[9];
+        const float xc = (ax + zs[k] * e[2]) + e[3];
+        const float yc = (ay + zs[k] * e[6]) + e[7];
+        const float zc = (az + zs[k] * e[10]) + e[11];
+        bad |= (__float_as_uint(zc) - 0x2D800000u) > 0x30000000u;
+        const float inv_z = rcp_m(zc);
+        const float u = fx * xc * inv_z + cx;
+        const float v = fy * yc * inv_z + cy;
+        const bool in = (__float_as_uint(v) <= hm1_bits) && (__float_as_uint(u) <= wm1_bits);
+        const uint32_t ui = (uint32_t)(int)u, vi = (uint32_t)(int)v;
+        const uint32_t roff = in ? __umul24(vi >> 2, TW8) + ((ui >> 3) << 3) : rec_end;
+        const u32x2 r = __builtin_amdgcn_raw_buffer_load_b64(rr, roff, 0, 0);
+        const bool valid = (r.x >> (((vi & 3u) << 3) | (ui & 7u))) & 1u;  // out of the image: r = 0
+        const bool clamp = valid && (half_from_bits(r.y & 0xFFFFu) - zc >= sdf_trunc);
+        const bool behind = valid && (half_from_bits(r.y >> 16) - zc < -sdf_trunc);
+        float d = clamp ? __builtin_nanf("") : 0.0f;
+        if (valid && !clamp && !behind) {
+            const uint32_t off = __umul24(vi, W4) + (ui << 2);
+            const u32x2 q = __builtin_amdgcn_raw_buffer_load_b64(rs, off & ~7u, 0, 0);
+            d = __uint_as_float((off & 4u) ? q.y : q.x);
+        }
+        dv[k] = d;
+        if ((k + 1) % 2 == 0) __builtin_amdgcn_sched_barrier(0);
+    }
+    (void)past_end;
+}
+
+template <int WPE>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void k_integrate_tp(
+    const int32_t* __restrict__ list, const bmask_t* __restrict__ lmask, int* __restrict__ counters, int64_t list_cap,
+    Table t, float2* __restrict__ pool, float voxel_size, const float* __restrict__ depths, int64_t HW, int H, int W,
+    const FrameParams* __restrict__ fps, const int64_t* __restrict__ depth_frame, float depth_max, float sdf_trunc,
+    int first_new, const uint2* __restrict__ recs, int TW, int TH) {
+    constexpr int NT = 512, R = 16, R2 = R * R, R3 = R2 * R;
+    constexpr int ZPER = R3 / NT;
+    const int64_t n = min((int64_t)counters[kListCount], list_cap);
+    const float hm1 = (float)H - 1.0f, wm1 = (float)W - 1.0f;
+    const uint32_t W4 = 4u * (uint32_t)W, bytes = 4u * (uint32_t)HW;
+    const uint32_t rec_bytes = 8u * (uint32_t)(TW * TH), TW8 = 8u * (uint32_t)TW;
+    const uint32_t hb = __float_as_uint(hm1), wb = __float_as_uint(wm1);
+    const float y0t = __builtin_amdgcn_rcpf(sdf_trunc);
+    const float y1t = __builtin_fmaf(__builtin_fmaf(-sdf_trunc, y0t, 1.0f), y0t, y0t);
+    const int tid = threadIdx.x;
+    const int l = tid & 63, w = tid >> 6;
+    const int vx = (l & 7) + 8 * (w & 1), vy = ((l >> 3) & 1) + 2 * (w >> 1), vz = l >> 4;
+    const uint32_t voff = 8u * (uint32_t)(vx + R * vy + R2 * vz);
+    for (int64_t i = blockIdx.x; i < n; i += gridDim.x) {
+        const int32_t slot = list[i];
+        const int buf = __builtin_amdgcn_readfirstlane(t.vals[slot]);
+        const bmask_t mask = readfirstlane_mask(lmask ? lmask[i] : bm_frames(t.mask[slot]));
+        int xb, yb, zb;
+        unpack_key(t.keys[slot], xb, yb, zb);
+        if (buf >= 0 && mask) {
+            const __amdgpu_buffer_rsrc_t vox = __builtin_amdgcn_make_buffer_rsrc(
+                pool + (int64_t)buf * R3, (short)0, (int)(R3 * sizeof(float2)), 0x00020000);
+            float2 tw[ZPER];
+            float xs[ZPER], ys[ZPER], zs[ZPER];
+            bool bad = false;
+            const float xs0 = (float)(xb * R + vx) * voxel_size;
+#pragma unroll
+            for (int k = 0; k < ZPER; ++k) {
+                const int dy = win_dy<NT>(k), dz = win_dz<NT>(k);
+                tw[k] = buf >= first_new ? make_float2(0.f, 0.f)
+                                         : pool_load(vox, voff, (R * dy + R2 * dz) * (int)sizeof(float2));
+                xs[k] = xs0;
+                ys[k] = (float)(yb * R + vy + dy) * voxel_size;
+                zs[k] = (float)(zb * R + vz + dz) * voxel_size;
+                const float wv = tw[k].y;
+                bad |= !(wv >= 0.0f && wv <= 0x1p23f - 64.0f && wv == __builtin_truncf(wv));
+            }
+            bmask_t m = mask;
+            while (m) {
+                const int f = bm_ctz(m);
+                m &= m - 1;
+                float dv[ZPER];
+                const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+                    const_cast<uint2*>(recs + (int64_t)f * TW * TH), (short)0, (int)rec_bytes, 0x00020000);
+                tp_gather<ZPER>(dv, bad, fps[f], frame_rsrc(depths + depth_frame[f] * HW, bytes), rr, xs, ys, zs, W4,
+                                bytes, rec_bytes, TW8, hb, wb, sdf_trunc);
+                lean_update_v<ZPER, 2, 0>(tw, dv, fps[f], xs, ys, zs, depth_max, sdf_trunc, y1t);
+            }
+            if (__syncthreads_or(bad)) {
+                exact_block_call<R, NT>(pool + (int64_t)buf * R3, buf >= first_new, mask, xb, yb, zb, voxel_size, depths,
+                                        HW, W, hm1, wm1, fps, depth_frame, depth_max, sdf_trunc);
+            } else {
+#pragma unroll
+                for (int k = 0; k < ZPER; ++k)
+                    pool_store(vox, voff, (R * win_dy<NT>(k) + R2 * win_dz<NT>(k)) * (int)sizeof(float2), tw[k]);
+            }
+        }
+        __syncthreads();
+        if (tid == 0) t.mask[slot] = 0;
+    }
+}
+
 }  // namespace mqr
