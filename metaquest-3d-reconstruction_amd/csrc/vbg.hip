@@ -333,7 +333,11 @@ static int launch_integrate_ab(mqr_vbg* v, int var, hipStream_t s, unsigned grid
         case 43: win(k_integrate_win_ab<512, 6, 0, 0, 3>, 512); break;
         case 44: win(k_integrate_win_r4<7>, 512); break;  // the round-4 default's source
         case 45:    // lane-level tile proofs (k_tile_records + k_integrate_tp), >= 7 waves
-        case 46: {  // the same at >= 6 waves
+        case 46:    // the same at >= 6 waves
+        case 47:    // record loads of all 8 voxels first, >= 7 waves
+        case 48:    // the same at >= 5 waves
+        case 49:    // 45 branch-free: every lane issues the window read, decided lanes past the end
+        case 50: {  // 47 branch-free
             // per device, grow-only (A/B library only): the batch's 8 x 4 tile records, 8 B each
             static void* rec_buf[64] = {};
             static size_t rec_cap[64] = {};
@@ -356,7 +360,11 @@ static int launch_integrate_ab(mqr_vbg* v, int var, hipStream_t s, unsigned grid
                                    recs, TW, TH);
             };
             if (var == 45) tp(k_integrate_tp<7>);
-            else tp(k_integrate_tp<6>);
+            else if (var == 46) tp(k_integrate_tp<6>);
+            else if (var == 47) tp(k_integrate_tp<7, 1>);
+            else if (var == 48) tp(k_integrate_tp<5, 1>);
+            else if (var == 49) tp(k_integrate_tp<7, 0, 1>);
+            else tp(k_integrate_tp<7, 1, 1>);
             break;
         }
         default: set_error("integrate variant " + std::to_string(var) + " unknown"); return 2;
@@ -545,10 +553,11 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
     //     23 = the round-4 default (k_integrate_lean_ab with the same arithmetic as 0);  24-31 the frame
     //     loop software-pipelined / 1024-thread workgroups (k_integrate_win_ab);  32-35 timing diagnostics
     //     (wrong results);  36-39 packed FP32 (k_integrate_pk);  40-43 branch-free window offsets / updates;  44 the
-    //     round-4 source;  45 / 46 lane-level tile proofs (k_tile_records + k_integrate_tp, >= 7 / 6 waves).  (24 of round 4, a ballot skip of
+    //     round-4 source;  45 / 46 lane-level tile proofs (k_tile_records + k_integrate_tp, >= 7 / 6 waves), 47 / 48 with
+    //     the eight record loads issued first (>= 7 / 5 waves), 49 / 50 = 45 / 47 branch-free.  (24 of round 4, a ballot skip of
     //     out-of-image wave slots, ran 0.70 vs 0.48 ms per launch: removed.)
     int var = v->kernel_variant;
-    if (var < 0 || var > 46) var = 0;
+    if (var < 0 || var > 50) var = 0;
     if (!MQR_AB && var != 1 && var != 2 && var != 4) var = 0;
     if (var != 1 && var != 2 && !lean_ok) var = 2;
     if (var == 5 && (v->R != 16 || W % 4 != 0 || W < 4 || (reinterpret_cast<uintptr_t>(depths) & 15))) var = 0;

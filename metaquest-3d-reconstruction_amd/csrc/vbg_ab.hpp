@@ -1239,7 +1239,7 @@ __global__ __launch_bounds__(256) void k_tile_records(const float* __restrict__ 
 }
 
 // lean_gather_w<ZPER, 2, 8> with the tile proofs in front of the window read.
-template <int ZPER>
+template <int ZPER, int BF = 0>
 __device__ __forceinline__ void tp_gather(float (&dv)[ZPER], bool& bad, const FrameParams& fp,
                                           __amdgpu_buffer_rsrc_t rs, __amdgpu_buffer_rsrc_t rr,
                                           const float (&xs)[ZPER], const float (&ys)[ZPER], const float (&zs)[ZPER],
@@ -1269,7 +1269,12 @@ __device__ __forceinline__ void tp_gather(float (&dv)[ZPER], bool& bad, const Fr
         const bool clamp = valid && (half_from_bits(r.y & 0xFFFFu) - zc >= sdf_trunc);
         const bool behind = valid && (half_from_bits(r.y >> 16) - zc < -sdf_trunc);
         float d = clamp ? __builtin_nanf("") : 0.0f;
-        if (valid && !clamp && !behind) {
+        if constexpr (BF) {  // every lane issues the read; decided lanes read past the end (one address)
+            const bool need = valid && !clamp && !behind;
+            const uint32_t off = need ? __umul24(vi, W4) + (ui << 2) : past_end;
+            const u32x2 q = __builtin_amdgcn_raw_buffer_load_b64(rs, off & ~7u, 0, 0);
+            d = need ? __uint_as_float((off & 4u) ? q.y : q.x) : d;
+        } else if (valid && !clamp && !behind) {
             const uint32_t off = __umul24(vi, W4) + (ui << 2);
             const u32x2 q = __builtin_amdgcn_raw_buffer_load_b64(rs, off & ~7u, 0, 0);
             d = __uint_as_float((off & 4u) ? q.y : q.x);
@@ -1277,10 +1282,70 @@ __device__ __forceinline__ void tp_gather(float (&dv)[ZPER], bool& bad, const Fr
         dv[k] = d;
         if ((k + 1) % 2 == 0) __builtin_amdgcn_sched_barrier(0);
     }
-    (void)past_end;
 }
 
-template <int WPE>
+// TWO_PHASE: the 8 voxels' record loads issued together first (one memory round trip for all of them),
+// then the projection recomputed (an empty asm hides its operands, so the compiler does not keep the first
+// pass's values live) for the decisions and the window reads.
+template <int ZPER, int BF = 0>
+__device__ __forceinline__ void tp_gather2(float (&dv)[ZPER], bool& bad, const FrameParams& fp,
+                                           __amdgpu_buffer_rsrc_t rs, __amdgpu_buffer_rsrc_t rr,
+                                           const float (&xs)[ZPER], const float (&ys)[ZPER], const float (&zs)[ZPER],
+                                           uint32_t W4, uint32_t past_end, uint32_t rec_end, uint32_t TW8,
+                                           uint32_t hm1_bits, uint32_t wm1_bits, float sdf_trunc) {
+    float e[12];
+#pragma unroll
+    for (int j = 0; j < 12; ++j) e[j] = fp.ext[j];
+    const float fx = fp.fx, fy = fp.fy, cx = fp.cx, cy = fp.cy;
+    u32x2 r[ZPER];
+#pragma unroll
+    for (int k = 0; k < ZPER; ++k) {
+        const float xc = ((xs[k] * e[0] + ys[k] * e[1]) + zs[k] * e[2]) + e[3];
+        const float yc = ((xs[k] * e[4] + ys[k] * e[5]) + zs[k] * e[6]) + e[7];
+        const float zc = ((xs[k] * e[8] + ys[k] * e[9]) + zs[k] * e[10]) + e[11];
+        const float inv_z = rcp_m(zc);
+        const float u = fx * xc * inv_z + cx;
+        const float v = fy * yc * inv_z + cy;
+        const bool in = (__float_as_uint(v) <= hm1_bits) && (__float_as_uint(u) <= wm1_bits);
+        const uint32_t roff = in ? __umul24((uint32_t)(int)v >> 2, TW8) + (((uint32_t)(int)u >> 3) << 3) : rec_end;
+        r[k] = __builtin_amdgcn_raw_buffer_load_b64(rr, roff, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int k = 0; k < ZPER; ++k) {
+        float x = xs[k], y = ys[k], z = zs[k];
+        asm volatile("" : "+v"(x), "+v"(y), "+v"(z));
+        const float ax = x * e[0] + y * e[1];
+        const float ay = x * e[4] + y * e[5];
+        const float az = x * e[8] + y * e[9];
+        const float xc = (ax + z * e[2]) + e[3];
+        const float yc = (ay + z * e[6]) + e[7];
+        const float zc = (az + z * e[10]) + e[11];
+        bad |= (__float_as_uint(zc) - 0x2D800000u) > 0x30000000u;
+        const float inv_z = rcp_m(zc);
+        const float u = fx * xc * inv_z + cx;
+        const float v = fy * yc * inv_z + cy;
+        const uint32_t ui = (uint32_t)(int)u, vi = (uint32_t)(int)v;
+        const bool valid = (r[k].x >> (((vi & 3u) << 3) | (ui & 7u))) & 1u;  // out of the image: r = 0
+        const bool clamp = valid && (half_from_bits(r[k].y & 0xFFFFu) - zc >= sdf_trunc);
+        const bool behind = valid && (half_from_bits(r[k].y >> 16) - zc < -sdf_trunc);
+        float d = clamp ? __builtin_nanf("") : 0.0f;
+        if constexpr (BF) {
+            const bool need = valid && !clamp && !behind;
+            const uint32_t off = need ? __umul24(vi, W4) + (ui << 2) : past_end;
+            const u32x2 q = __builtin_amdgcn_raw_buffer_load_b64(rs, off & ~7u, 0, 0);
+            d = need ? __uint_as_float((off & 4u) ? q.y : q.x) : d;
+        } else if (valid && !clamp && !behind) {
+            const uint32_t off = __umul24(vi, W4) + (ui << 2);
+            const u32x2 q = __builtin_amdgcn_raw_buffer_load_b64(rs, off & ~7u, 0, 0);
+            d = __uint_as_float((off & 4u) ? q.y : q.x);
+        }
+        dv[k] = d;
+        if ((k + 1) % 2 == 0) __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+template <int WPE, int TWO_PHASE = 0, int BF = 0>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void k_integrate_tp(
     const int32_t* __restrict__ list, const bmask_t* __restrict__ lmask, int* __restrict__ counters, int64_t list_cap,
     Table t, float2* __restrict__ pool, float voxel_size, const float* __restrict__ depths, int64_t HW, int H, int W,
@@ -1330,8 +1395,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
                 float dv[ZPER];
                 const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
                     const_cast<uint2*>(recs + (int64_t)f * TW * TH), (short)0, (int)rec_bytes, 0x00020000);
-                tp_gather<ZPER>(dv, bad, fps[f], frame_rsrc(depths + depth_frame[f] * HW, bytes), rr, xs, ys, zs, W4,
-                                bytes, rec_bytes, TW8, hb, wb, sdf_trunc);
+                if constexpr (TWO_PHASE)
+                    tp_gather2<ZPER, BF>(dv, bad, fps[f], frame_rsrc(depths + depth_frame[f] * HW, bytes), rr, xs, ys,
+                                         zs, W4, bytes, rec_bytes, TW8, hb, wb, sdf_trunc);
+                else
+                    tp_gather<ZPER, BF>(dv, bad, fps[f], frame_rsrc(depths + depth_frame[f] * HW, bytes), rr, xs, ys, zs,
+                                        W4, bytes, rec_bytes, TW8, hb, wb, sdf_trunc);
                 lean_update_v<ZPER, 2, 0>(tw, dv, fps[f], xs, ys, zs, depth_max, sdf_trunc, y1t);
             }
             if (__syncthreads_or(bad)) {

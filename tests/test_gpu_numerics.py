@@ -55,7 +55,7 @@ INTEGRATE_VARIANTS = {16: (0, 2, 4, 0x100, 0x104, 0x200, 0x400, 0x800, 0x10000, 
                       8: (0, 2, 0x100)}
 if AB:
     INTEGRATE_VARIANTS = {16: (0, 3, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25,
-                               26, 27, 28, 29, 30, 31, 36, 37, 38, 39, 40, 41, 44, 45, 46, 0x105, 0x605, 0x106, 0x108, 0x10b, 0x10d, 0x111, 0x8000, 0x8003, 0x8008, 0x800a, 0x800b, 0x800d, 0x8011), 8: (0, 0x8000)}
+                               26, 27, 28, 29, 30, 31, 36, 37, 38, 39, 40, 41, 44, 45, 46, 47, 48, 49, 50, 0x105, 0x605, 0x106, 0x108, 0x10b, 0x10d, 0x111, 0x8000, 0x8003, 0x8008, 0x800a, 0x800b, 0x800d, 0x8011), 8: (0, 0x8000)}
 
 
 def test_specialised_integrate_equals_generic():
