@@ -889,6 +889,7 @@ def c5_sharded_leg(args, rank, world, dev, merge_fn, dist, parity=True, frames_p
             okp = (ok_[:, 0].astype(np.int64) + (1 << 20)) << 42 | (ok_[:, 1].astype(np.int64) + (1 << 20)) << 21 | \
                 (ok_[:, 2].astype(np.int64) + (1 << 20))
             seen, weq, err, flips, flip_max = 0, True, 0.0, 0, 0.0
+            parts = []  # every rank's owned slice: the merged volume, for the oracle's extraction of it
             for r in range(world):
                 if r == 0:
                     rk, rt, rw = k_, t_.reshape(-1, R3), w_.reshape(-1, R3)
@@ -908,6 +909,7 @@ def c5_sharded_leg(args, rank, world, dev, merge_fn, dist, parity=True, frames_p
                     weq = False
                     break
                 seen += len(rp)
+                parts.append((rk, rt, rw))
                 for c in range(0, len(j), 4096):
                     jj = j[c:c + 4096]
                     weq = weq and bool(np.array_equal(rw[c:c + 4096], ow[jj]))
@@ -922,33 +924,50 @@ def c5_sharded_leg(args, rank, world, dev, merge_fn, dist, parity=True, frames_p
                             flips += int(f.sum())
                             flip_max = max(flip_max, float(np.maximum(np.abs(a[f]), np.abs(b[f])).max()))
             keys_ok = weq and seen == len(okp)
-            res = torch.tensor([float(keys_ok), float(weq), err, float(n_otri), float(flips), flip_max],
-                               dtype=torch.float64)
+            del ok_, ot, ow, okp
+            # the oracle's marching cubes over the merged volume itself (the owned slices put together):
+            # equal to the shard meshes' summed triangle count when the owned-cube extraction is exact, so
+            # any difference from the oracle's own mesh lies in the merged tsdf, not in the extraction
+            n_mtri = -1
+            if parts:
+                mv = oracle.OracleVBG(voxel, 16, sum(len(q[0]) for q in parts))
+                mv.import_blocks(np.concatenate([q[0] for q in parts]), np.concatenate([q[1] for q in parts]),
+                                 np.concatenate([q[2] for q in parts]))
+                del parts
+                n_mtri = len(mv.extract_mesh(1.5)[2])
+                del mv
+            res = torch.tensor([float(keys_ok), float(weq), err, float(n_otri), float(flips), flip_max,
+                                float(n_mtri)], dtype=torch.float64)
         else:
             dist.send(torch.tensor([len(k_)], dtype=torch.int64), dst=0)
             for x in (k_, t_.reshape(-1, R3), w_.reshape(-1, R3)):
                 dist.send(torch.from_numpy(np.ascontiguousarray(x)), dst=0)
-            res = torch.zeros(6, dtype=torch.float64)
+            res = torch.zeros(7, dtype=torch.float64)
         del k_, t_, w_
         dist.broadcast(res, src=0)
         cok = torch.tensor([1 if col_ok else 0], dtype=torch.int32)
         dist.all_reduce(cok, op=dist.ReduceOp.MIN)
         tri_ok = int(res[3].item()) == rec["triangles"]
         flips, flip_max = int(res[4].item()), float(res[5].item())
+        merged_exact = int(res[6].item()) == rec["triangles"]
         rec["parity"] = {"keys_equal": bool(res[0].item()), "weights_equal": bool(res[1].item()),
                          "max_dtsdf": float(res[2].item()), "tolerance": 1e-4,
                          "oracle_triangles": int(res[3].item()), "triangle_count_equal": tri_ok,
                          "triangle_count_diff": rec["triangles"] - int(res[3].item()),
                          "tsdf_sign_flips": flips, "max_abs_tsdf_at_sign_flips": flip_max,
+                         "oracle_triangles_of_merged_volume": int(res[6].item()),
+                         "merged_mesh_count_exact": merged_exact,
                          "colours_equal": bool(cok.item()),
                          "comparison": "owned slices of the merged shards vs the oracle's sequential pass over all "
                                        "4000 frames (keys / weights exact, tsdf within tolerance), shard triangle counts "
-                                       "summed vs the oracle mesh at 1.5 (exact, or every voxel whose tsdf sign differs "
+                                       "summed vs the oracle mesh at 1.5 (exact, or: exactly the oracle's extraction of "
+                                       "the merged owned slices, and every voxel whose tsdf sign differs from the oracle's "
                                        "within the tolerance of 0), every rank's colours and counts bit for bit vs "
                                        "oracle.color_map on its shard vertices with the reduced colour-view depth"}
         # the triangle count is exact unless the merge's rounding moved a voxel's tsdf across 0 -- then
-        # every such voxel must lie within the tolerance of 0 (its sign is not determined at 1e-4)
-        rec["parity"]["triangle_count_explained"] = bool(tri_ok or (flips > 0 and flip_max <= 1e-4))
+        # the shard meshes must be exactly the oracle's mesh of the merged volume, and every such voxel must
+        # lie within the tolerance of 0 (its sign is not determined at 1e-4)
+        rec["parity"]["triangle_count_explained"] = bool(merged_exact and (tri_ok or (flips > 0 and flip_max <= 1e-4)))
         rec["parity"]["all_ok"] = bool(rec["parity"]["keys_equal"] and rec["parity"]["weights_equal"]
                                        and rec["parity"]["max_dtsdf"] <= 1e-4 and rec["parity"]["triangle_count_explained"]
                                        and rec["parity"]["colours_equal"])
@@ -1396,17 +1415,29 @@ def sharded_parity(full_host, K, T, args, owned, meshes):
     return out
 
 
+def _json_stdout():
+    """The JSON line is the only thing this process writes to stdout.  Native libraries write to
+    file descriptor 1 behind Python's back (gloo's "[Gloo] Rank 0 is connected to ..." lines, RCCL's
+    and ROCm's messages); fd 1 is pointed at stderr and the line goes out through a private
+    duplicate of the original stdout."""
+    sys.stdout.flush()
+    fd = os.dup(1)
+    os.dup2(2, 1)
+    return os.fdopen(fd, "w", buffering=1)
+
+
 def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ:
         if args.gpus > 1:
             # no launcher around us: start the N ranks here, before anything touches the GPU
             sys.exit(launch_ranks(args.gpus, sys.argv[1:], timeout=args.launch_timeout))
-    elif int(os.environ["WORLD_SIZE"]) != args.gpus:
+    out_json = _json_stdout()
+    if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) != args.gpus:
         if int(os.environ.get("RANK", 0)) == 0:
             print(json.dumps({"metric": METRIC, "value": None, "unit": "frames/s", "n_gpus": args.gpus,
                               "error": f"--gpus {args.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']}"}),
-                  flush=True)
+                  file=out_json, flush=True)
         sys.exit(1)
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
@@ -1418,7 +1449,7 @@ def main():
     torch.cuda.set_device(local)
     if args.c5_only:
         print(json.dumps({"c5": c5_leg(args, torch.device("cuda", local), parity=not (args.no_cpu or args.no_parity))}),
-              flush=True)
+              file=out_json, flush=True)
         return
     dist = comm = None
     if world > 1:
@@ -1487,7 +1518,7 @@ def main():
             if rank == 0:
                 print(json.dumps({"metric": METRIC, "value": None, "unit": "frames/s", "n_gpus": world,
                                   "merge_transport": f"RCCL failed to start on at least one rank: {err or 'peer'}",
-                                  "error": "no measurement: the RCCL merge could not run"}), flush=True)
+                                  "error": "no measurement: the RCCL merge could not run"}), file=out_json, flush=True)
             dist.destroy_process_group()
             sys.exit(1)
         transport = "rccl (mqr_reduce_rccl)"
@@ -1800,7 +1831,7 @@ def main():
             "c5_sharded": c5_sharded,
             "dropin_e2e": extras.get("dropin_e2e"),
         }
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=out_json, flush=True)
     if comm is not None:
         comm.close()
     if dist:

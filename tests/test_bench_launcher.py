@@ -96,3 +96,17 @@ def test_bench_rejects_a_world_size_other_than_gpus():
     assert p.returncode == 1
     rec = json.loads(p.stdout.strip().splitlines()[-1])
     assert rec["value"] is None and "WORLD_SIZE=2" in rec["error"]
+
+
+def test_rank_stdout_carries_only_the_json_line():
+    """Native libraries write to fd 1 behind Python's back (gloo's connection log): in a rank process
+    bench._json_stdout points fd 1 at stderr, so stdout holds the JSON line alone."""
+    code = ("import os, sys, json; sys.path.insert(0, %r); import bench\n"
+            "out = bench._json_stdout()\n"
+            "os.write(1, b'[Gloo] Rank 0 is connected to 1 peer ranks\\n')\n"
+            "print('python log line')\n"
+            "print(json.dumps({'value': 1.0}), file=out, flush=True)\n") % ROOT
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
+    assert p.returncode == 0, p.stderr
+    assert p.stdout.splitlines() == ['{"value": 1.0}'], p.stdout
+    assert "[Gloo]" in p.stderr and "python log line" in p.stderr
