@@ -14,8 +14,13 @@
  *     work enqueued so far on the calling thread's CALLER STREAM (mqr_set_stream; default: the null
  *     stream), so a kernel or copy the caller enqueued there that writes an input -- or still reads a
  *     buffer the call overwrites -- is complete before the library touches it.  No host wait is
- *     involved (an event and a stream wait).  Every call has finished with its buffers when it
- *     returns: outputs are complete and visible to any stream afterwards;
+ *     involved (an event and a stream wait).  Every call but one has finished with its buffers when
+ *     it returns: outputs are complete and visible to any stream afterwards.  The exception is
+ *     mqr_integrate_frames on MQR_DEVICE frames, which returns once its last integrate is queued:
+ *     the caller stream is then made to wait (device-side) for that integrate, so whatever the
+ *     caller enqueues there next -- overwriting or freeing the frames included -- runs after the
+ *     library's reads; every later call on the volume orders itself behind it (a host-side reader
+ *     of the frames synchronizes the caller stream first, as it would for a kernel of its own);
  *   - matrices are row-major: K = 3x3 intrinsic (Open3D convention, cx already flipped),
  *     T_wc = 4x4 world->camera extrinsic, both float64 as the reference passes them
  *     (o3d_utils.py:203-210);
@@ -92,7 +97,10 @@ int mqr_integrate(mqr_vbg* v, const int32_t* keys, int64_t n, const float* depth
  * order, batched on device (results identical to B sequential touch+integrate calls).
  * depths: B*H*W float32 metric depth (0 = invalid), K: B*9, T_wc: B*16 (host float64).
  * frame_ok (host, may be NULL): frames with frame_ok[i]==0 are skipped (missing/invalid loads).
- * Returns 3 if a valid frame touches no block (upstream raises). */
+ * Returns 3 if a valid frame touches no block (upstream raises).  Every batch's touch counters are
+ * read on the host before its integrate is launched, so errors are reported by this call; with
+ * MQR_DEVICE frames the call returns with the last integrate still running (see "stream ordering"
+ * above), with MQR_HOST frames after it has finished. */
 int mqr_integrate_frames(mqr_vbg* v, const float* depths, int depth_loc, int B, int H, int W, const double* K,
                          const double* T_wc, const uint8_t* frame_ok, float depth_scale, float depth_max,
                          float trunc_mult);

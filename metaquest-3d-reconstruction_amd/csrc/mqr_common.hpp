@@ -148,6 +148,9 @@ struct mqr_vbg {
     bool lpt_ready[2] = {false, false};  // k_lpt_order already enqueued behind this parity's touch
     bool ctr_clean[2] = {true, true};    // the parity's counters are zero (a reset cleared them)
     bool spec_head = true;               // first batch of a call: integrate enqueued behind its touch (k_gate)
+    // mqr_integrate_frames on device frames returns once its last integrate is queued (the caller's stream
+    // waits for it; the volume's next user orders behind it on the device) instead of draining the streams
+    bool async_return = true;
     int64_t batch_n_max = 0;             // largest batch list seen (grid of a speculative integrate)
     hipEvent_t touch_ev(int p) const { return sys_fence ? ev_touch_sys[p] : ev_touch[p]; }
     hipEvent_t int_ev(int p) const { return sys_fence ? ev_int_sys[p] : ev_int[p]; }
@@ -248,9 +251,13 @@ int order_after_integrate(mqr_vbg* v);
 // Caller-stream ordering (mqr_set_stream, include/mqr.h): the library streams `a` (and `b`) wait for
 // every command the calling thread's caller stream holds so far.  Called by each entry point that
 // reads or writes caller MQR_DEVICE buffers, before its first command on them (the current device
-// must be `device`).  Every entry point drains its own streams before it returns, so outputs need
-// no ordering in the other direction.
+// must be `device`).  Every entry point but one drains its own streams before it returns, so outputs
+// need no ordering in the other direction; mqr_integrate_frames on device frames instead makes the caller
+// stream wait for its last integrate (order_caller_after_integrate).
 int order_after_caller(int device, hipStream_t a, hipStream_t b = nullptr);
+// The caller stream waits (device-side) for every integrate of `v` still in flight: what the caller
+// enqueues there next -- e.g. overwriting the frames just integrated -- runs after the library's reads.
+int order_caller_after_integrate(mqr_vbg* v);
 hipStream_t caller_stream();  // the calling thread's caller stream (nullptr: the null stream)
 // Large device -> pageable host copies by several host threads through pinned staging (extract.hip);
 // mqr_geom_copy and mqr_memcpy use it from kD2HParallelMin bytes on.

@@ -131,6 +131,22 @@ int order_after_integrate(mqr_vbg* v) {
     return 0;
 }
 
+int order_caller_after_integrate(mqr_vbg* v) {
+    hipStream_t cs = t_caller_stream;
+    if (cs) {
+        hipDevice_t sd = -1;
+        if (hipStreamGetDevice(cs, &sd) != hipSuccess || sd != v->device) {
+            (void)hipGetLastError();
+            return sync_all(v);  // a stream of another device (or none valid): no device-side wait -- drain
+        }
+    }
+    // both parities: integrates run in order on their stream, but a call of one batch leaves only its
+    // own parity pending and an earlier call may have left the other
+    for (int p = 0; p < 2; ++p)
+        if (v->int_pending[p]) MQR_CHECK_HIP(hipStreamWaitEvent(cs, v->int_done[p], 0));
+    return 0;
+}
+
 static int ensure_lists(mqr_vbg* v, int64_t cap) {
     if (v->list_cap >= cap) return 0;
     if (sync_all(v)) return 1;
@@ -971,7 +987,9 @@ int mqr_vbg_destroy(mqr_vbg* v) {
 int mqr_vbg_reset(mqr_vbg* v) {
     MQR_REQUIRE(v, "null volume");
     MQR_CHECK_HIP(hipSetDevice(v->device));
-    if (sync_all(v)) return 1;
+    // behind an integrate still in flight (mqr_integrate_frames on device frames returns before it ends):
+    // a device-side wait on `stream`, no host wait
+    if (order_after_integrate(v)) return 1;
     // one launch, ordered on `stream` before anything that uses the volume next; the pool is not
     // cleared: a block starts at (0, 0) in the batch that allocates it (launch_integrate first_new)
     const int nctr = kCounterInts;
@@ -1111,6 +1129,14 @@ int mqr_integrate_frames(mqr_vbg* v, const float* depths, int depth_loc, int B, 
             break;
         }
         if (launch_integrate(v, p, dbase, HW, H, W, b, depth_scale, depth_max, sdf_trunc, (int)pool_before)) return 1;
+    }
+    if (rc == 0 && depth_loc == MQR_DEVICE && v->async_return) {
+        // Device frames, no error: every batch's counters have been read (pool growth, empty frames), so
+        // nothing is left to decide on the host -- return with the last integrate queued.  The caller's
+        // stream waits for it (its next write to the frames is ordered after the library's reads); the
+        // volume's next user orders behind it on the device (order_after_integrate, wait_parity_free) or
+        // drains it (sync_all).  Host frames stay synchronous: the caller's array is read by copies.
+        return order_caller_after_integrate(v);
     }
     if (sync_all(v)) return 1;
     if (rc) set_error(kNoBlock);  // the prefix re-run may have overwritten the message
@@ -1335,6 +1361,7 @@ int mqr_vbg_set_variant(mqr_vbg* v, int variant) {
     v->xcd_order = (variant & 0x8000) != 0;   // bit 15: spatial per-XCD groups (k_xcd_order, A/B)
     v->touch_ppt = (variant & 0x10000) ? 1 : 2;  // bit 16: one stride-4 pixel per touch thread (A/B)
     v->spec_head = (variant & 0x40000) == 0;     // bit 18: no speculative first-batch integrate (A/B)
+    v->async_return = (variant & 0x1000000) == 0; // bit 24: integrate_frames drains its streams before returning (A/B)
     // (the extraction configuration is set by mqr_vbg_set_extract_mode alone, A/B library only)
     return 0;
 }

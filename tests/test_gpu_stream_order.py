@@ -167,3 +167,92 @@ def test_confidence_counts_after_side_stream_write():
             c = np.true_divide(cons[i - a], valid[i - a])
         c[valid[i - a] == 0] = 0.0
         assert np.array_equal(valid[i - a], ov) and np.array_equal(c.view(np.uint64), oc.view(np.uint64)), i
+
+
+# ---- the other direction: mqr_integrate_frames on device frames returns with its last integrate queued
+def _room(n=127, seed=11):
+    from mqr import synthetic
+    seq = synthetic.make_sequence("room", n=n, height=240, width=320, f=262.5, noise=True, seed=seed)
+    return np.ascontiguousarray(seq["depth"], np.float32), seq["K"].astype(np.float64), seq["T_wc"].astype(np.float64)
+
+
+def _oracle(depth, K, T, vs=0.01, dmax=4.0, tm=10.0, ref=None):
+    ref = ref if ref is not None else oracle.OracleVBG(vs, 16, 256)
+    for i in range(len(depth)):
+        ref.integrate_frame(depth[i], K[i], T[i], 1.0, dmax, tm)
+    return ref
+
+
+@pytest.mark.parametrize("side_stream", [False, True])
+def test_caller_overwrite_right_after_integrate_frames_is_ordered(side_stream):
+    """The caller poisons the frames on its stream the moment integrate_frames returns (no
+    synchronize): the write must wait for the library's reads, so the volume is the oracle's over the
+    frames as they were.  A long call (254 frames, two batches in flight at the return) makes the
+    race wide if the ordering were missing."""
+    import torch
+    from gpu_helpers import compare_volumes
+    from mqr.vbg import VoxelBlockGrid
+    depth, K, T = _room(254)
+    B, H, W = depth.shape
+    dev = torch.from_numpy(depth).cuda()
+    torch.cuda.synchronize()
+    vbg = VoxelBlockGrid(voxel_size=0.01, block_resolution=16, block_count=256, device="cuda:0")
+    s = torch.cuda.Stream() if side_stream else torch.cuda.current_stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        vbg.integrate_frames((_Dev(dev), B, H, W), K, T, depth_scale=1.0, depth_max=4.0, trunc_voxel_multiplier=10.0)
+        dev.fill_(0.7)  # a wall at 0.7 m in every frame: touches other blocks than the room
+    dev.record_stream(s)
+    ref = _oracle(depth, K, T)
+    assert compare_volumes(vbg.export(), ref.export(), 0.0) == 0.0
+    torch.cuda.synchronize()
+    assert float(dev.max()) == float(np.float32(0.7))
+
+
+def test_reset_extract_and_second_call_after_an_unfinished_integrate():
+    """reset, a second integrate_frames and extraction issued while the previous integrate still runs:
+    each orders itself behind it on the device (no host wait), and the results are the oracle's."""
+    import torch
+    from gpu_helpers import compare_volumes
+    from mqr.vbg import VoxelBlockGrid
+    d1, K1, T1 = _room(127, seed=11)
+    d2, K2, T2 = _room(100, seed=12)
+    B1, H, W = d1.shape
+    t1, t2 = torch.from_numpy(d1).cuda(), torch.from_numpy(d2).cuda()
+    torch.cuda.synchronize()
+    kw = dict(depth_scale=1.0, depth_max=4.0, trunc_voxel_multiplier=10.0)
+    vbg = VoxelBlockGrid(voxel_size=0.01, block_resolution=16, block_count=256, device="cuda:0")
+    # (a) reset behind an unfinished integrate, then the second sequence alone
+    vbg.integrate_frames((_Dev(t1), B1, H, W), K1, T1, **kw)
+    vbg.reset()
+    vbg.integrate_frames((_Dev(t2), len(d2), H, W), K2, T2, **kw)
+    ref2 = _oracle(d2, K2, T2)
+    assert compare_volumes(vbg.export(), ref2.export(), 0.0) == 0.0
+    # (b) two calls back to back (the second's touch behind the first's integrate), then the mesh at once
+    vbg.reset()
+    vbg.integrate_frames((_Dev(t1), B1, H, W), K1, T1, **kw)
+    vbg.integrate_frames((_Dev(t2), len(d2), H, W), K2, T2, **kw)
+    mesh = vbg.extract_triangle_mesh(weight_threshold=1.5)
+    ref12 = _oracle(d2, K2, T2, ref=_oracle(d1, K1, T1))
+    assert compare_volumes(vbg.export(), ref12.export(), 0.0) == 0.0
+    _, _, otri = ref12.extract_mesh(1.5)
+    assert mesh.triangles.shape[0] == otri.shape[0]
+
+
+def test_synchronous_return_variant_is_identical():
+    """Variant bit 24 (the A/B of the asynchronous return) drains the streams before returning: same volume."""
+    import torch
+    from mqr import _lib
+    from mqr.vbg import VoxelBlockGrid
+    depth, K, T = _room(60, seed=13)
+    B, H, W = depth.shape
+    t = torch.from_numpy(depth).cuda()
+    torch.cuda.synchronize()
+    out = []
+    for variant in (0, 0x1000000):
+        vbg = VoxelBlockGrid(voxel_size=0.01, block_resolution=16, block_count=256, device="cuda:0")
+        _lib.call("mqr_vbg_set_variant", vbg.handle, variant)
+        vbg.integrate_frames((_Dev(t), B, H, W), K, T, depth_scale=1.0, depth_max=4.0, trunc_voxel_multiplier=10.0)
+        out.append(vbg.export())
+    from gpu_helpers import compare_volumes
+    assert compare_volumes(out[0], out[1], 0.0) == 0.0  # (block order is the touch's arrival order)

@@ -21,6 +21,7 @@
 #   d2h         device -> host copy ceilings (tools/d2h_probe.py) with 1 / 4 / 8 staging threads
 #   chunkab     drop-in integrate() with 64- vs 127-frame hand-offs (tools/dropin_ab.py)
 #   conf        tools/conf_workload.py (the confidence kernel alone)
+#   abasync[:V] integrate_frames returning with its last integrate queued vs draining, or variants V (tools/ab_async.py)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
@@ -69,6 +70,14 @@ for step in ${STEPS:-tests}; do
       find gpurun_out/prof -name "*kernel_stats.csv" -exec cp {} gpurun_out/${TAG}_bench_kernel_stats.csv \;
       rm -rf gpurun_out/prof  # (traces: gpurun copies back at most 64 MiB of gpurun_out/)
       grep "mqr" gpurun_out/${TAG}_bench_kernel_stats.csv | cut -c1-70 | head -12 ;;
+    steptrace)
+      rm -rf gpurun_out/st
+      timeout -k 10 400 rocprofv3 --kernel-trace -f csv -d gpurun_out/st -o run -- \
+        python bench.py --no-cpu --no-extras --no-c4 --no-c5 --e2e-frames 0 --steps 50 --warmup 5 --touch-steps 0 \
+        > gpurun_out/${TAG}_st_bench.json 2> gpurun_out/${TAG}_st_bench.err || { tail -20 gpurun_out/${TAG}_st_bench.err; exit 1; }
+      cp "$(find gpurun_out/st -name '*kernel_trace.csv' | head -1)" gpurun_out/${TAG}_step_trace.csv
+      rm -rf gpurun_out/st
+      python tools/step_head.py gpurun_out/${TAG}_step_trace.csv --steps 40 > gpurun_out/${TAG}_step_head.json && cat gpurun_out/${TAG}_step_head.json ;;
     profc5)
       rm -rf gpurun_out/profc5
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/profc5 -o run -- \
@@ -112,6 +121,10 @@ for step in ${STEPS:-tests}; do
     chunkprof)
       timeout -k 10 600 python -u tools/dropin_ab.py --profile --rounds 1 > gpurun_out/${TAG}_chunk_prof.json 2> gpurun_out/${TAG}_chunk_prof.txt || { tail -20 gpurun_out/${TAG}_chunk_prof.txt; exit 1; }
       grep -A22 "== CHUNK" gpurun_out/${TAG}_chunk_prof.txt | cut -c1-150 ;;
+    abasync|abasync:*)
+      V=0,0x1000000; [ "$step" != abasync ] && V="${step#abasync:}"
+      timeout -k 10 400 python -u tools/ab_async.py --rounds 7 --steps 100 --variants "$V" > gpurun_out/${TAG}_ab_async.json 2> gpurun_out/${TAG}_ab_async.err || { tail -20 gpurun_out/${TAG}_ab_async.err; exit 1; }
+      cat gpurun_out/${TAG}_ab_async.json ;;
     conf)
       timeout -k 10 300 python -u tools/conf_workload.py > gpurun_out/${TAG}_conf.json 2> gpurun_out/${TAG}_conf.err || { tail -20 gpurun_out/${TAG}_conf.err; exit 1; }
       cat gpurun_out/${TAG}_conf.json ;;
