@@ -486,7 +486,9 @@ static int resolve_pool_overflow(mqr_vbg* v, int p, bool* table_full = nullptr) 
 
 // Longest-first order of parity p's batch list (k_lpt_order reads the list length on the device, so
 // the batch touch enqueues it before the host has read the counters).
-static int enqueue_lpt(mqr_vbg* v, int p) {
+// nframes: the batch's frame count -- the order kernel also fills the shadow counters a speculative
+// integrate of the batch reads (k_gate's work; launch_integrate then launches no gate).
+static int enqueue_lpt(mqr_vbg* v, int p, int nframes) {
     bmask_t* om = reinterpret_cast<bmask_t*>(v->lpt[p] + v->list_cap);
 #if MQR_AB
     if (v->xcd_order)
@@ -495,7 +497,7 @@ static int enqueue_lpt(mqr_vbg* v, int p) {
     else
 #endif
         hipLaunchKernelGGL(k_lpt_order, dim3(1), dim3(1024), 0, v->stream, v->lists[p], v->ctr(p), v->list_cap,
-                           v->table(p).mask, v->lpt[p], om);
+                           v->table(p).mask, v->lpt[p], om, v->shadow(p), nframes);
     MQR_CHECK_HIP(hipGetLastError());
     v->lpt_ready[p] = true;
     return 0;
@@ -521,13 +523,15 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
     // touch -- and an order enqueued behind it -- completed: integrate needs no device-side wait on
     // the touch stream, only for an order enqueued here, after that read.
     bool touch_wait = v->touch_wait;
+    bool gated_by_order = false;  // k_lpt_order filled the shadow counters (no k_gate launch)
     if (v->lpt_order && n > 1) {  // on the touch stream: overlaps the previous integrate
         if (!v->lpt_ready[p]) {
-            if (enqueue_lpt(v, p)) return 1;
+            if (enqueue_lpt(v, p, nframes)) return 1;
             touch_wait = true;
         }
         list = v->lpt[p];
         lmask = reinterpret_cast<bmask_t*>(v->lpt[p] + v->list_cap);
+        gated_by_order = !v->xcd_order;
     }
     v->lpt_ready[p] = false;
     // the lean kernels run k_xcd_order's groups on the workgroups that share an XCD
@@ -538,7 +542,7 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
         MQR_CHECK_HIP(hipEventRecord(v->touch_ev(p), v->stream));
         MQR_CHECK_HIP(hipStreamWaitEvent(s, v->touch_ev(p), 0));
     }
-    if (spec > 0) {
+    if (spec > 0 && !gated_by_order) {
         hipLaunchKernelGGL(k_gate, dim3(1), dim3(64), 0, s, v->ctr(p), v->shadow(p), nframes);
         MQR_CHECK_HIP(hipGetLastError());
     }
@@ -788,7 +792,7 @@ static int touch_batch_launch(mqr_vbg* v, int p, const float* dbase, int64_t HW,
         return 1;
     // the batch order is computed while the host waits for the counters (pool growth below only
     // rewrites buffer indices, which the order does not read)
-    if (v->lpt_order && enqueue_lpt(v, p)) return 1;
+    if (v->lpt_order && enqueue_lpt(v, p, b)) return 1;
     return 0;
 }
 
@@ -802,7 +806,7 @@ static int touch_batch_resolve(mqr_vbg* v, int p, const float* dbase, int64_t HW
         if (touch_launch(v, p, dbase, HW, H, W, b, depth_scale, depth_max, sdf_trunc, block_size, v->table(p), 1,
                          v->tab.cap))
             return 1;
-        if (v->lpt_order && enqueue_lpt(v, p)) return 1;
+        if (v->lpt_order && enqueue_lpt(v, p, b)) return 1;
         if (resolve_pool_overflow(v, p)) return 1;
         v->stats.table_retries += 1;
     }
@@ -1028,8 +1032,9 @@ int mqr_integrate_frames(mqr_vbg* v, const float* depths, int depth_loc, int B, 
     MQR_REQUIRE(v && depths && K && T_wc, "null argument");
     MQR_REQUIRE(B >= 0 && H > 0 && W > 0, "bad frame shape");
     MQR_CHECK_HIP(hipSetDevice(v->device));
-    // device frames: both streams read them (touch, integrate) -- ordered after the caller's writes
-    if (depth_loc == MQR_DEVICE && order_after_caller(v->device, v->stream, v->stream2)) return 2;
+    // device frames: both streams read them (touch, integrate) -- ordered after the caller's writes, from
+    // the first batch's touch on (its frame-parameter upload and counter clear need not wait for them)
+    bool caller_ordered = depth_loc != MQR_DEVICE;
     const int64_t HW = (int64_t)H * W;
     const float sdf_trunc = v->voxel_size * trunc_mult;
     const float block_size = v->voxel_size * v->R;
@@ -1075,6 +1080,10 @@ int mqr_integrate_frames(mqr_vbg* v, const float* depths, int depth_loc, int B, 
         // device by the touch's own counters (k_gate), so the GPU does not idle while the host reads
         // them.  Later batches' counters are read while the previous integrate runs anyway.
         const bool spec = batch == 0 && v->spec_head && v->pipelined && !v->probe_one && v->batch_n_max > 0;
+        if (!caller_ordered) {
+            if (order_after_caller(v->device, v->stream, v->stream2)) return 2;
+            caller_ordered = true;
+        }
         TouchState ts;
         if (touch_batch_launch(v, p, dbase, HW, H, W, b, depth_scale, depth_max, sdf_trunc, block_size, max_touch, ts))
             return 1;

@@ -534,12 +534,24 @@ __global__ __launch_bounds__(NT) void k_integrate_t(const int32_t* __restrict__ 
 // that touched each block (popcount of its slot mask), descending.  The integrate grid then ends on
 // short blocks instead of whichever long blocks the touch order happened to put last.  One
 // workgroup; order within a bin is arbitrary (blocks are independent, results unchanged).
+// shadow (nullable): k_gate's work for a speculative integrate of the batch's `nframes` frames, done
+// here -- the kernel runs right behind the touch anyway -- so the integrate needs no gate launch.
+__device__ __forceinline__ void gate_counters(const int* __restrict__ ctr, int* __restrict__ shadow, bool stop) {
+    for (int i = threadIdx.x; i < kCountersTotal; i += blockDim.x)
+        shadow[i] = i == kListCount ? (stop ? 0 : ctr[kListCount]) : i == kBadCount ? 0 : ctr[i];
+}
+
 __global__ __launch_bounds__(1024) void k_lpt_order(const int32_t* __restrict__ list, const int* __restrict__ counters,
                                                     int64_t list_cap, const bmask_t* __restrict__ mask,
-                                                    int32_t* __restrict__ out, bmask_t* __restrict__ out_mask) {
+                                                    int32_t* __restrict__ out, bmask_t* __restrict__ out_mask,
+                                                    int* __restrict__ shadow = nullptr, int nframes = 0) {
     __shared__ int hist[kMaxBatch + 1];
     const int n = (int)min((int64_t)counters[kListCount], list_cap);
     if (threadIdx.x <= kMaxBatch) hist[threadIdx.x] = 0;
+    if (shadow) {
+        const bool empty = (int)threadIdx.x < nframes && counters[kFrameCounterBase + threadIdx.x] == 0;
+        gate_counters(counters, shadow, __syncthreads_or(empty) != 0 || counters[kOverflow] != 0);
+    }
     __syncthreads();
     for (int i = threadIdx.x; i < n; i += blockDim.x) atomicAdd(&hist[bm_popc(bm_frames(mask[list[i]]))], 1);
     __syncthreads();
@@ -1040,9 +1052,7 @@ __global__ void k_gate(const int* __restrict__ ctr, int* __restrict__ shadow, in
     const int lane = threadIdx.x;  // one wave
     bool empty = false;
     for (int f = lane; f < nframes; f += 64) empty |= ctr[kFrameCounterBase + f] == 0;
-    const bool stop = __ballot(empty) != 0 || ctr[kOverflow] != 0;
-    for (int i = lane; i < kCountersTotal; i += 64)
-        shadow[i] = i == kListCount ? (stop ? 0 : ctr[kListCount]) : i == kBadCount ? 0 : ctr[i];
+    gate_counters(ctr, shadow, __ballot(empty) != 0 || ctr[kOverflow] != 0);
 }
 
 // Empty table: keys empty, values -1, both parities' slot masks 0; and `nctr` counters 0.
