@@ -289,6 +289,10 @@ static int launch_integrate_ab(mqr_vbg* v, int var, hipStream_t s, unsigned grid
         hipLaunchKernelGGL(kern, dim3(grid), dim3(nt), 0, s, list, lmask, counters, v->list_cap, t, v->pool,
                            v->voxel_size, depths, HW, H, W, fp, depth_frame, depth_max, sdf_trunc, first_new);
     };
+    auto wx = [&](auto kern) {  // k_integrate_wx: the window kernel's arguments plus the fix-up list
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(512), 0, s, list, lmask, bad_out, counters, v->list_cap, t, v->pool,
+                           v->voxel_size, depths, HW, H, W, fp, depth_frame, depth_max, sdf_trunc, first_new);
+    };
     *fixup = var <= 22;
     switch (var) {
         case 3: lean(k_integrate_lean_ab<16, 512>); break;  // plate map
@@ -383,6 +387,15 @@ static int launch_integrate_ab(mqr_vbg* v, int var, hipStream_t s, unsigned grid
             else tp(k_integrate_tp<7, 1, 1>);
             break;
         }
+        // round 6: register-pressure forms of the default (k_integrate_wx<WPE, MODE>: MODE 1 halves, 2 fix-up launch)
+        case 51: wx(k_integrate_wx<6, 0>); break;
+        case 52: wx(k_integrate_wx<7, 1>); break;
+        case 53: wx(k_integrate_wx<8, 1>); break;
+        case 54: wx(k_integrate_wx<6, 1>); break;
+        case 55: *fixup = true; wx(k_integrate_wx<7, 2>); break;
+        case 56: *fixup = true; wx(k_integrate_wx<6, 2>); break;
+        case 57: *fixup = true; wx(k_integrate_wx<8, 3>); break;
+        case 58: *fixup = true; wx(k_integrate_wx<7, 3>); break;
         default: set_error("integrate variant " + std::to_string(var) + " unknown"); return 2;
     }
     return 0;
@@ -577,7 +590,7 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
     //     the eight record loads issued first (>= 7 / 5 waves), 49 / 50 = 45 / 47 branch-free.  (24 of round 4, a ballot skip of
     //     out-of-image wave slots, ran 0.70 vs 0.48 ms per launch: removed.)
     int var = v->kernel_variant;
-    if (var < 0 || var > 50) var = 0;
+    if (var < 0 || var > 58) var = 0;
     if (!MQR_AB && var != 1 && var != 2 && var != 4) var = 0;
     if (var != 1 && var != 2 && !lean_ok) var = 2;
     if (var == 5 && (v->R != 16 || W % 4 != 0 || W < 4 || (reinterpret_cast<uintptr_t>(depths) & 15))) var = 0;

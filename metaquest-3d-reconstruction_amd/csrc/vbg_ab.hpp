@@ -1417,4 +1417,87 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
     }
 }
 
+// ---- round 6: register-pressure forms of k_integrate_win (A/B variants 51-58) ---------------------------------
+// The shipped kernel at 72 VGPRs keeps 7 of its 8 voxels' (tsdf, weight) pairs in scratch inside the frame
+// loop (14 scratch loads / stores per wave-frame beside the 8 window reads), and a 512-thread workgroup gets 3
+// workgroups per CU -- 6 waves per SIMD -- whether the budget allows 6 or 7.  MODE bit 0: the frame's 8 voxels
+// in two halves (gather 0-3, update 0-3, gather 4-7, update 4-7: half the window reads in flight, half the
+// registers for them); bit 1: no in-kernel exact path (a block outside the proven ranges is handed to the exact
+// fix-up launch, hand_off, like k_integrate_lean) -- no call, so no registers saved across one.
+template <int WPE, int MODE>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void k_integrate_wx(
+    const int32_t* __restrict__ list, const bmask_t* __restrict__ lmask, int32_t* __restrict__ bad_out,
+    int* __restrict__ counters, int64_t list_cap, Table t, float2* __restrict__ pool, float voxel_size,
+    const float* __restrict__ depths, int64_t HW, int H, int W, const FrameParams* __restrict__ fps,
+    const int64_t* __restrict__ depth_frame, float depth_max, float sdf_trunc, int first_new) {
+    constexpr int NT = 512, R = 16, R2 = R * R, R3 = R2 * R;
+    constexpr int ZPER = R3 / NT;
+    const int64_t n = min((int64_t)counters[kListCount], list_cap);
+    const float hm1 = (float)H - 1.0f, wm1 = (float)W - 1.0f;
+    const uint32_t W4 = 4u * (uint32_t)W, bytes = 4u * (uint32_t)HW;
+    const uint32_t hb = __float_as_uint(hm1), wb = __float_as_uint(wm1);
+    const float y0t = __builtin_amdgcn_rcpf(sdf_trunc);
+    const float y1t = __builtin_fmaf(__builtin_fmaf(-sdf_trunc, y0t, 1.0f), y0t, y0t);
+    const int tid = threadIdx.x;
+    const int l = tid & 63, w = tid >> 6;
+    const int vx = (l & 7) + 8 * (w & 1), vy = ((l >> 3) & 1) + 2 * (w >> 1), vz = l >> 4;
+    const uint32_t voff = 8u * (uint32_t)(vx + R * vy + R2 * vz);
+    for (int64_t i = blockIdx.x; i < n; i += gridDim.x) {
+        const int32_t slot = list[i];
+        const int buf = __builtin_amdgcn_readfirstlane(t.vals[slot]);
+        const bmask_t mask = readfirstlane_mask(lmask ? lmask[i] : bm_frames(t.mask[slot]));
+        int xb, yb, zb;
+        unpack_key(t.keys[slot], xb, yb, zb);
+        if (buf >= 0 && mask) {
+            const __amdgpu_buffer_rsrc_t vox = __builtin_amdgcn_make_buffer_rsrc(
+                pool + (int64_t)buf * R3, (short)0, (int)(R3 * sizeof(float2)), 0x00020000);
+            float2 tw[ZPER];
+            float xs[ZPER], ys[ZPER], zs[ZPER];
+            bool bad = false;
+            const float xs0 = (float)(xb * R + vx) * voxel_size;
+#pragma unroll
+            for (int k = 0; k < ZPER; ++k) {
+                const int dy = win_dy<NT>(k), dz = win_dz<NT>(k);
+                tw[k] = buf >= first_new ? make_float2(0.f, 0.f)
+                                         : pool_load(vox, voff, (R * dy + R2 * dz) * (int)sizeof(float2));
+                xs[k] = xs0;
+                ys[k] = (float)(yb * R + vy + dy) * voxel_size;
+                zs[k] = (float)(zb * R + vz + dz) * voxel_size;
+                const float wv = tw[k].y;
+                bad |= !(wv >= 0.0f && wv <= 0x1p23f - 64.0f && wv == __builtin_truncf(wv));
+            }
+            bmask_t m = mask;
+            while (m) {
+                const int f = bm_ctz(m);
+                m &= m - 1;
+                float dv[ZPER];
+                const __amdgpu_buffer_rsrc_t rs = frame_rsrc(depths + depth_frame[f] * HW, bytes);
+                if constexpr ((MODE & 1) != 0) {
+                    lean_gather_w<ZPER, 2, 8, true, 0, ZPER / 2>(dv, bad, fps[f], rs, xs, ys, zs, W4, bytes, hb, wb);
+                    lean_update_v<ZPER, 2, 0, 0, ZPER / 2>(tw, dv, fps[f], xs, ys, zs, depth_max, sdf_trunc, y1t);
+                    lean_gather_w<ZPER, 2, 8, true, ZPER / 2, ZPER>(dv, bad, fps[f], rs, xs, ys, zs, W4, bytes, hb, wb);
+                    lean_update_v<ZPER, 2, 0, ZPER / 2, ZPER>(tw, dv, fps[f], xs, ys, zs, depth_max, sdf_trunc, y1t);
+                } else {
+                    lean_gather_w<ZPER, 2, 8>(dv, bad, fps[f], rs, xs, ys, zs, W4, bytes, hb, wb);
+                    lean_update_v<ZPER, 2, 0>(tw, dv, fps[f], xs, ys, zs, depth_max, sdf_trunc, y1t);
+                }
+            }
+            if (__syncthreads_or(bad)) {
+                if constexpr ((MODE & 2) != 0) {
+                    if (tid == 0) hand_off(bad_out, counters, list_cap, slot, mask);
+                } else {
+                    exact_block_call<R, NT>(pool + (int64_t)buf * R3, buf >= first_new, mask, xb, yb, zb, voxel_size,
+                                            depths, HW, W, hm1, wm1, fps, depth_frame, depth_max, sdf_trunc);
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < ZPER; ++k)
+                    pool_store(vox, voff, (R * win_dy<NT>(k) + R2 * win_dz<NT>(k)) * (int)sizeof(float2), tw[k]);
+            }
+        }
+        __syncthreads();
+        if (tid == 0) t.mask[slot] = 0;
+    }
+}
+
 }  // namespace mqr
