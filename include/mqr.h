@@ -163,6 +163,10 @@ int mqr_comm_timing(mqr_comm* comm, float* ms4);
  * floats per block (2 R^3).  Zeros before the first merge. */
 int mqr_comm_counts(mqr_comm* comm, int64_t* send_blocks, int64_t* recv_blocks, int64_t* floats_per_block);
 int mqr_merge_local_timing(float* ms, int n);
+/* How every transport merges the received segments (process-wide, for A/Bs and tests): 0 (default) one
+ * fused pass per output block folding its entries in rank order in registers; 1 the round-5 form, one
+ * pass over the output per source rank.  The two give the same bits. */
+int mqr_merge_set_per_source(int on);
 typedef struct mqr_xchg mqr_xchg;
 int mqr_xchg_create(mqr_vbg* local, int world, int rank, int mode, int root, const uint64_t* gathered_keys,
                     int64_t mx, int keys_loc, mqr_vbg* out, mqr_xchg** h);

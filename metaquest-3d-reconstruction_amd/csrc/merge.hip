@@ -37,8 +37,10 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <climits>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -169,6 +171,73 @@ __global__ void k_merge_blocks(const int32_t* __restrict__ dst, int64_t n, const
             const float w = a.y + b.y;
             out[p] = make_float2((a.y * a.x + b.y * b.x) / w, w);
         }
+    }
+}
+
+// Fused merge (the default): one workgroup per output buffer folds all of its received entries in
+// source-rank order in registers -- the same operations in the same order as the k_merge_blocks launch per
+// source, so the same bits -- reading each entry once and writing the buffer once, where the per-source
+// launches read and rewrite the output buffer for every source that holds it (at 8 ranks a buffer has ~4).
+// Entries come as a CSR over output buffers (k_csr_count / scan / k_csr_fill: `list` holds receive
+// indices in arbitrary order, sorted here); the rank's own entries are read straight from its send
+// segment (receive indices [self_lo, self_hi) <-> send index self_send + j - self_lo), so the self
+// segment is not copied.
+__global__ void k_csr_count(const int32_t* __restrict__ dst, int64_t n, int32_t* __restrict__ cnt) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < n) atomicAdd(&cnt[dst[j]], 1);
+}
+
+__global__ void k_csr_fill(const int32_t* __restrict__ dst, int64_t n, const int32_t* __restrict__ start,
+                           int32_t* __restrict__ fill, int32_t* __restrict__ list) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < n) {
+        const int32_t d = dst[j];
+        list[start[d] + atomicAdd(&fill[d], 1)] = (int32_t)j;
+    }
+}
+
+static std::atomic<bool> g_merge_per_source{false};  // A/B and test hook: mqr_merge_set_per_source
+constexpr int kMergeMaxEntries = 64;  // a buffer receives at most one entry per rank (kMaxRanks)
+
+__global__ __launch_bounds__(256) void k_merge_fused(const int32_t* __restrict__ start, const int32_t* __restrict__ list,
+                                                     int64_t n_out, const float2* __restrict__ recv,
+                                                     const float2* __restrict__ send, int64_t self_lo, int64_t self_hi,
+                                                     int64_t self_send, int R3, float2* __restrict__ pool) {
+    __shared__ int32_t ent[kMergeMaxEntries];
+    __shared__ int n_ent;
+    const int64_t d = blockIdx.x;
+    if (d >= n_out) return;
+    if (threadIdx.x == 0) {
+        const int b = start[d], e = start[d + 1];
+        int m = 0;
+        for (int k = b; k < e && m < kMergeMaxEntries; ++k) {  // insertion sort: source-rank (= receive index) order
+            const int32_t v = list[k];
+            int q = m++;
+            while (q > 0 && ent[q - 1] > v) {
+                ent[q] = ent[q - 1];
+                --q;
+            }
+            ent[q] = v;
+        }
+        n_ent = m;
+    }
+    __syncthreads();
+    const int m = n_ent;
+    float2* out = pool + d * R3;
+    for (int p = threadIdx.x; p < R3; p += blockDim.x) {
+        float2 a = make_float2(0.f, 0.f);  // the output buffer as activate_ordered leaves it
+        for (int k = 0; k < m; ++k) {
+            const int64_t j = ent[k];
+            const float2 b = (j >= self_lo && j < self_hi) ? send[(self_send + (j - self_lo)) * R3 + p] : recv[j * R3 + p];
+            if (b.y == 0.f) continue;
+            if (a.y == 0.f) {
+                a = b;
+            } else {
+                const float w = a.y + b.y;
+                a = make_float2((a.y * a.x + b.y * b.x) / w, w);
+            }
+        }
+        out[p] = a;
     }
 }
 
@@ -498,12 +567,16 @@ struct Exchange {
     size_t send_cap = 0;
     void* recvbuf = nullptr;
     size_t recv_cap = 0;
+    void* csr = nullptr;  // fused merge: start[n_out + 1], fill[n_out], list[nr]
+    size_t csr_cap = 0;
+    bool fused = true;    // k_merge_fused (false: one k_merge_blocks launch per source, mqr_merge_set_per_source)
     Exchange() = default;
     Exchange(const Exchange&) = delete;
     Exchange& operator=(const Exchange&) = delete;
     ~Exchange() {
         if (sendbuf) (void)hipFree(sendbuf);
         if (recvbuf) (void)hipFree(recvbuf);
+        if (csr) (void)hipFree(csr);
     }
     size_t send_blocks(int d) const { return soff[d + 1] - soff[d]; }
     size_t recv_blocks(int s) const { return roff[s + 1] - roff[s]; }
@@ -541,7 +614,8 @@ static int xchg_prepare(Exchange& x, hipStream_t st, const uint64_t* dkeys, int 
     MQR_CHECK_HIP(hipGetLastError());
     if (ev_gathered) MQR_CHECK_HIP(hipEventRecord(ev_gathered, st));
     MQR_REQUIRE(x.send_blocks(me) == x.recv_blocks(me), "merge plan: self segment lengths differ");
-    if (x.send_blocks(me))
+    x.fused = !g_merge_per_source.load();
+    if (x.send_blocks(me) && !x.fused)  // (the fused merge reads the rank's own entries from its send segment)
         MQR_CHECK_HIP(hipMemcpyAsync(x.recv_seg(me), x.send_seg(me), eb * x.send_blocks(me), hipMemcpyDeviceToDevice,
                                      st));
     return 0;
@@ -549,6 +623,34 @@ static int xchg_prepare(Exchange& x, hipStream_t st, const uint64_t* dkeys, int 
 
 // Received segments into the output volume, source by source in rank order (deterministic sums).
 static int xchg_merge(Exchange& x, hipStream_t st, mqr_vbg* out) {
+    if (x.fused) {
+        const int64_t n_out = x.H.n_out, nr = (int64_t)x.roff[x.W];
+        if (n_out == 0) return 0;
+        MQR_REQUIRE(x.W <= kMergeMaxEntries, "merge: too many ranks");
+        size_t tb = 0;
+        MQR_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (const int32_t*)nullptr, (int32_t*)nullptr,
+                                                       (int)(n_out + 1), st));
+        const size_t o_cnt = 4 * (size_t)(n_out + 1), o_list = 2 * o_cnt,
+                     o_tmp = (o_list + 4 * (size_t)std::max<int64_t>(nr, 1) + 255) & ~size_t(255);
+        if (grow(&x.csr, &x.csr_cap, o_tmp + tb)) return 1;
+        char* c = static_cast<char*>(x.csr);
+        int32_t* start = reinterpret_cast<int32_t*>(c);        // [n_out + 1]
+        int32_t* cnt = reinterpret_cast<int32_t*>(c + o_cnt);  // [n_out + 1]: counts (last 0), then fill cursors
+        int32_t* list = reinterpret_cast<int32_t*>(c + o_list);
+        MQR_CHECK_HIP(hipMemsetAsync(cnt, 0, o_cnt, st));
+        const unsigned g = (unsigned)((std::max<int64_t>(nr, 1) + 255) / 256);
+        if (nr) hipLaunchKernelGGL(k_csr_count, dim3(g), dim3(256), 0, st, x.pv.recv_dst, nr, cnt);
+        size_t t = tb;  // start[n_out] = nr
+        MQR_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(c + o_tmp, t, cnt, start, (int)(n_out + 1), st));
+        MQR_CHECK_HIP(hipMemsetAsync(cnt, 0, 4 * (size_t)n_out, st));
+        if (nr) hipLaunchKernelGGL(k_csr_fill, dim3(g), dim3(256), 0, st, x.pv.recv_dst, nr, start, cnt, list);
+        const int me = x.me;
+        hipLaunchKernelGGL(k_merge_fused, dim3((unsigned)n_out), dim3(256), 0, st, start, list, n_out,
+                           static_cast<const float2*>(x.recvbuf), static_cast<const float2*>(x.sendbuf),
+                           (int64_t)x.roff[me], (int64_t)x.roff[me + 1], (int64_t)x.soff[me], x.R3, out->pool);
+        MQR_CHECK_HIP(hipGetLastError());
+        return 0;
+    }
     for (int src = 0; src < x.W; ++src)
         if (x.recv_blocks(src))
             hipLaunchKernelGGL(k_merge_blocks, dim3((unsigned)x.recv_blocks(src)), dim3(256), 0, st,
@@ -837,6 +939,11 @@ int mqr_merge_local(mqr_vbg** locals, int n, int mode, int root, mqr_vbg** outs,
         n_owned[d] = X[d]->H.n_owned;
         t_local_ms[d] += std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }
+    return 0;
+}
+
+int mqr_merge_set_per_source(int on) {
+    g_merge_per_source.store(on != 0);
     return 0;
 }
 

@@ -73,6 +73,7 @@ SIGNATURES = {
     "mqr_comm_timing": (ctypes.c_int, [_vp, _f32p]),
     "mqr_comm_counts": (ctypes.c_int, [_vp, _i64p, _i64p, _i64p]),
     "mqr_merge_local_timing": (ctypes.c_int, [_f32p, ctypes.c_int]),
+    "mqr_merge_set_per_source": (ctypes.c_int, [ctypes.c_int]),
     "mqr_merge_local": (ctypes.c_int, [ctypes.POINTER(_vp), ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                        ctypes.POINTER(_vp), _i64p]),
     "mqr_xchg_create": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp,

@@ -381,6 +381,13 @@ def merge_local_timing(n: int):
     return ms.tolist()
 
 
+def set_merge_per_source(on: bool):
+    """Process-wide merge form (mqr_merge_set_per_source): False (default) = one fused pass per output
+    block, True = the round-5 pass per source rank.  Same bits; for A/Bs and tests."""
+    from . import _lib
+    _lib.call("mqr_merge_set_per_source", 1 if on else 0)
+
+
 def extract_mesh_owned(vbg, n_owned: int, weight_threshold: float = 1.5):
     """A shard's mesh: triangles of the cubes whose origin lies in its owned blocks, the vertices
     they reference (re-indexed; vertices on the shard boundary also appear in the neighbour's mesh)."""

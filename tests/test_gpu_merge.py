@@ -116,6 +116,25 @@ def test_sharded_meshes_concatenate_to_the_merged_mesh(seq, world, R):
             assert np.array_equal(t[b], rt[j]) and np.array_equal(w[b], rw[j])
 
 
+@pytest.mark.parametrize("world,mode", [(2, "sharded"), (3, "root"), (8, "sharded"), (8, "root")])
+def test_fused_merge_equals_per_source_merge(seq, world, mode):
+    """The fused merge (one pass per output block, entries folded in rank order) against the round-5 merge
+    (one pass over the output per source rank, mqr_merge_set_per_source): every rank's output, bit for bit."""
+    from mqr.distributed import merge_local, set_merge_per_source
+    vols = _shards(seq, world)
+    fused = [(o.export(), n) for o, n in merge_local(vols, mode=mode)]
+    set_merge_per_source(True)
+    try:
+        per_src = [(o.export(), n) for o, n in merge_local(vols, mode=mode)]
+    finally:
+        set_merge_per_source(False)
+    assert len(fused) == len(per_src)
+    for (a, na), (b, nb) in zip(fused, per_src):
+        assert na == nb
+        for x, y in zip(a, b):  # both outputs are activated in plan order: same buffer order
+            assert np.array_equal(x, y)
+
+
 def test_rccl_world_one(seq):
     """mqr_reduce_rccl through a real RCCL communicator (world size 1: the send to self)."""
     from mqr.distributed import RcclComm, merge_rccl

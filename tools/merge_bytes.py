@@ -74,7 +74,7 @@ def main():
     a = ap.parse_args()
     from bench import _DevPtr
     from mqr import synthetic
-    from mqr.distributed import merge_local, merge_local_timing, shard_range
+    from mqr.distributed import merge_local, merge_local_timing, set_merge_per_source, shard_range
     from mqr.vbg import VoxelBlockGrid
     left = synthetic.room_loop_poses(a.frames_per_side)
     right = [(R_, t_ + R_[:, 0] * 0.064) for R_, t_ in left]
@@ -108,24 +108,35 @@ def main():
         U, per = plan_counts(keys, zeros, R3)
         # one rank's own share of the exchange without the transfer (plan, output volume, send gather,
         # merge kernels): mqr_merge_local's per-destination wall times, median of 3 after a warm-up
-        outs, reps = None, []
-        for _ in range(4):
-            got = merge_local(vols, mode="sharded", outs=outs)
-            outs = [o for o, _ in got]
-            reps.append(merge_local_timing(W))
-        own_ms = [sorted(rr[i] for rr in reps[1:])[1] for i in range(W)]
+        # (and the same with the round-5 merge, one pass over the output per source: mqr_merge_set_per_source)
+        def own_times(per_source):
+            set_merge_per_source(per_source)
+            try:
+                outs_, reps = None, []
+                for _ in range(6):
+                    got_ = merge_local(vols, mode="sharded", outs=outs_)
+                    outs_ = [o for o, _ in got_]
+                    reps.append(merge_local_timing(W))
+            finally:
+                set_merge_per_source(False)
+            return [sorted(rr[i] for rr in reps[1:])[2] for i in range(W)], outs_, got_
+        own_ps, _, _ = own_times(True)
+        own_ms, outs, got = own_times(False)
         sent = sum(p["sent_blocks"] for p in per) * R3
         zf = sum(p["sent_zero_weight_frac"] * p["sent_blocks"] for p in per) * R3 / max(sent, 1)
         for r in range(W):
             per[r]["integrate_ms"] = int_ms[r]
             per[r]["merge_own_ms"] = own_ms[r]
+            per[r]["merge_own_ms_per_source"] = own_ps[r]
         res["per_world"][W] = {"union_blocks": U, "ranks": per,
                                "max_sent_bytes": max(p["sent_bytes"] for p in per),
                                "max_recv_bytes": max(p["recv_bytes"] for p in per),
                                "max_integrate_ms": max(int_ms), "max_merge_own_ms": max(own_ms),
+                               "max_merge_own_ms_per_source": max(own_ps),
                                "sent_zero_weight_frac": zf}
         print(f"W={W}: U={U} max sent {res['per_world'][W]['max_sent_bytes'] / 1e6:.1f} MB, "
-              f"zero-weight {zf:.3f}, integrate {max(int_ms):.2f} ms, own merge {max(own_ms):.2f} ms",
+              f"zero-weight {zf:.3f}, integrate {max(int_ms):.2f} ms, own merge {max(own_ms):.2f} ms "
+              f"(per-source merge {max(own_ps):.2f})",
               file=sys.stderr, flush=True)
         del vols, outs, got
         torch.cuda.empty_cache()
