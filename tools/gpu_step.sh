@@ -12,6 +12,7 @@
 #   n2self      the same, bench.py --gpus 2 starting its own ranks (no torchrun) -> gpurun_out/${TAG}_bench_n2_selflaunch.json
 #   mbytes      C4 exchange bytes / zero-weight voxels / per-rank times at 2, 4, 8 ranks (tools/merge_bytes.py)
 #   prof        rocprofv3 --kernel-trace --stats of the C2 bench      -> gpurun_out/${TAG}_bench_kernel_stats.csv
+#   mprof       rocprofv3 kernel trace + stats of tools/time_merge.py (8 ranks on one GPU)
 #   profc5      the same over the C5 leg alone                        -> gpurun_out/${TAG}_c5_kernel_stats.csv
 #   xtrace      kernel trace of 30 extractions: wall vs device span vs gaps -> gpurun_out/${TAG}_extract_timeline.json
 #   traffic     FETCH_SIZE / WRITE_SIZE passes (tools/pmc_traffic.sh) -> profiles/${TAG}_pmc_traffic.json
@@ -78,6 +79,15 @@ for step in ${STEPS:-tests}; do
       cp "$(find gpurun_out/st -name '*kernel_trace.csv' | head -1)" gpurun_out/${TAG}_step_trace.csv
       rm -rf gpurun_out/st
       python tools/step_head.py gpurun_out/${TAG}_step_trace.csv --steps 40 > gpurun_out/${TAG}_step_head.json && cat gpurun_out/${TAG}_step_head.json ;;
+    mprof)
+      rm -rf gpurun_out/mp
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/mp -o run -- \
+        python tools/time_merge.py --ranks 8 --reps 5 > gpurun_out/${TAG}_time_merge.json 2> gpurun_out/${TAG}_time_merge.err \
+        || { tail -20 gpurun_out/${TAG}_time_merge.err; exit 1; }
+      find gpurun_out/mp -name "*kernel_stats.csv" -exec cp {} gpurun_out/${TAG}_merge_kernel_stats.csv \;
+      python tools/merge_trace.py "$(find gpurun_out/mp -name '*kernel_trace.csv' | head -1)" > gpurun_out/${TAG}_merge_timeline.json
+      rm -rf gpurun_out/mp
+      cat gpurun_out/${TAG}_time_merge.json; head -c 3000 gpurun_out/${TAG}_merge_timeline.json ;;
     profc5)
       rm -rf gpurun_out/profc5
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/profc5 -o run -- \
