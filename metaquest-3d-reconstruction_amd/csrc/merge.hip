@@ -178,56 +178,51 @@ __global__ void k_merge_blocks(const int32_t* __restrict__ dst, int64_t n, const
 // source-rank order in registers -- the same operations in the same order as the k_merge_blocks launch per
 // source, so the same bits -- reading each entry once and writing the buffer once, where the per-source
 // launches read and rewrite the output buffer for every source that holds it (at 8 ranks a buffer has ~4).
-// Entries come as a CSR over output buffers (k_csr_count / scan / k_csr_fill: `list` holds receive
-// indices in arbitrary order, sorted here); the rank's own entries are read straight from its send
-// segment (receive indices [self_lo, self_hi) <-> send index self_send + j - self_lo), so the self
-// segment is not copied.
-__global__ void k_csr_count(const int32_t* __restrict__ dst, int64_t n, int32_t* __restrict__ cnt) {
-    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j < n) atomicAdd(&cnt[dst[j]], 1);
-}
-
-__global__ void k_csr_fill(const int32_t* __restrict__ dst, int64_t n, const int32_t* __restrict__ start,
-                           int32_t* __restrict__ fill, int32_t* __restrict__ list) {
-    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j < n) {
-        const int32_t d = dst[j];
-        list[start[d] + atomicAdd(&fill[d], 1)] = (int32_t)j;
-    }
-}
-
+// A buffer gets at most one entry per source, so its entries sit in a dense [n_out][W] table of receive
+// indices (-1: none), filled by one scatter over the receive lists (k_merge_entries); the rank's own
+// entries are read straight from its send segment (receive indices [roff[me], roff[me+1]) <-> send index
+// soff[me] + j - roff[me]), so the self segment is not copied.  Every output buffer gets at least one entry
+// (it is in the plan because some rank holds the block), so every voxel is written and the output pool
+// needs no zeroing.
 static std::atomic<bool> g_merge_per_source{false};  // A/B and test hook: mqr_merge_set_per_source
-constexpr int kMergeMaxEntries = 64;  // a buffer receives at most one entry per rank (kMaxRanks)
+constexpr int kMergeMaxEntries = 64;                  // a buffer gets at most one entry per rank (kMaxRanks)
 
-__global__ __launch_bounds__(256) void k_merge_fused(const int32_t* __restrict__ start, const int32_t* __restrict__ list,
-                                                     int64_t n_out, const float2* __restrict__ recv,
-                                                     const float2* __restrict__ send, int64_t self_lo, int64_t self_hi,
-                                                     int64_t self_send, int R3, float2* __restrict__ pool) {
-    __shared__ int32_t ent[kMergeMaxEntries];
-    __shared__ int n_ent;
+struct SegOffsets {
+    int64_t off[kMergeMaxEntries + 1];  // receive segment s = [off[s], off[s + 1])
+};
+
+__global__ void k_merge_entries(const int32_t* __restrict__ dst, int64_t n, SegOffsets seg, int W,
+                                int32_t* __restrict__ ent) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    int s = 0;
+    while (s + 1 < W && seg.off[s + 1] <= j) ++s;
+    ent[(int64_t)dst[j] * W + s] = (int32_t)j;
+}
+
+__global__ __launch_bounds__(256) void k_merge_fused(const int32_t* __restrict__ ent, int W, int64_t n_out,
+                                                     const float2* __restrict__ recv, const float2* __restrict__ send,
+                                                     int64_t self_lo, int64_t self_hi, int64_t self_send, int R3,
+                                                     float2* __restrict__ pool) {
+    __shared__ int32_t e[kMergeMaxEntries];
+    __shared__ int n_e;
     const int64_t d = blockIdx.x;
     if (d >= n_out) return;
-    if (threadIdx.x == 0) {
-        const int b = start[d], e = start[d + 1];
+    if (threadIdx.x == 0) {  // the buffer's entries in source order
         int m = 0;
-        for (int k = b; k < e && m < kMergeMaxEntries; ++k) {  // insertion sort: source-rank (= receive index) order
-            const int32_t v = list[k];
-            int q = m++;
-            while (q > 0 && ent[q - 1] > v) {
-                ent[q] = ent[q - 1];
-                --q;
-            }
-            ent[q] = v;
+        for (int s = 0; s < W; ++s) {
+            const int32_t j = ent[d * W + s];
+            if (j >= 0) e[m++] = j;
         }
-        n_ent = m;
+        n_e = m;
     }
     __syncthreads();
-    const int m = n_ent;
+    const int m = n_e;
     float2* out = pool + d * R3;
     for (int p = threadIdx.x; p < R3; p += blockDim.x) {
-        float2 a = make_float2(0.f, 0.f);  // the output buffer as activate_ordered leaves it
+        float2 a = make_float2(0.f, 0.f);  // the buffer as the per-source form starts it (zeroed)
         for (int k = 0; k < m; ++k) {
-            const int64_t j = ent[k];
+            const int64_t j = e[k];
             const float2 b = (j >= self_lo && j < self_hi) ? send[(self_send + (j - self_lo)) * R3 + p] : recv[j * R3 + p];
             if (b.y == 0.f) continue;
             if (a.y == 0.f) {
@@ -546,9 +541,9 @@ static int grow(void** p, size_t* cap, size_t need) {
 }
 
 // Output volume of one rank: empty it, activate its keys in order (owned first).
-static int prepare_out(mqr_vbg* out, const uint64_t* dk, int64_t n) {
+static int prepare_out(mqr_vbg* out, const uint64_t* dk, int64_t n, bool fused) {
     if (mqr_vbg_reset(out)) return 1;
-    return n > 0 ? activate_ordered(out, dk, n) : 0;
+    return activate_ordered(out, dk, n, fused);
 }
 
 // One rank's side of the exchange, whatever carries the bytes (RCCL, device copies between the
@@ -567,7 +562,7 @@ struct Exchange {
     size_t send_cap = 0;
     void* recvbuf = nullptr;
     size_t recv_cap = 0;
-    void* csr = nullptr;  // fused merge: start[n_out + 1], fill[n_out], list[nr]
+    void* csr = nullptr;  // fused merge: the [n_out][W] entry table
     size_t csr_cap = 0;
     bool fused = true;    // k_merge_fused (false: one k_merge_blocks launch per source, mqr_merge_set_per_source)
     Exchange() = default;
@@ -604,7 +599,10 @@ static int xchg_prepare(Exchange& x, hipStream_t st, const uint64_t* dkeys, int 
     }
     const size_t ns = x.soff[W], nr = x.roff[W];
     const size_t eb = sizeof(float2) * (size_t)x.R3;
-    if (prepare_out(out, x.pv.out_keys, x.H.n_out)) return 1;  // synchronous (out's stream)
+    x.fused = !g_merge_per_source.load();
+    // (fused: the output's activation is not waited for -- the merge writes only pool buffers, and
+    // activate_ordered_check reads its table-full flag after the merge)
+    if (prepare_out(out, x.pv.out_keys, x.H.n_out, x.fused)) return 1;
     if (grow(&x.sendbuf, &x.send_cap, std::max<size_t>(ns, 1) * eb) ||
         grow(&x.recvbuf, &x.recv_cap, std::max<size_t>(nr, 1) * eb))
         return 1;
@@ -614,7 +612,6 @@ static int xchg_prepare(Exchange& x, hipStream_t st, const uint64_t* dkeys, int 
     MQR_CHECK_HIP(hipGetLastError());
     if (ev_gathered) MQR_CHECK_HIP(hipEventRecord(ev_gathered, st));
     MQR_REQUIRE(x.send_blocks(me) == x.recv_blocks(me), "merge plan: self segment lengths differ");
-    x.fused = !g_merge_per_source.load();
     if (x.send_blocks(me) && !x.fused)  // (the fused merge reads the rank's own entries from its send segment)
         MQR_CHECK_HIP(hipMemcpyAsync(x.recv_seg(me), x.send_seg(me), eb * x.send_blocks(me), hipMemcpyDeviceToDevice,
                                      st));
@@ -627,25 +624,16 @@ static int xchg_merge(Exchange& x, hipStream_t st, mqr_vbg* out) {
         const int64_t n_out = x.H.n_out, nr = (int64_t)x.roff[x.W];
         if (n_out == 0) return 0;
         MQR_REQUIRE(x.W <= kMergeMaxEntries, "merge: too many ranks");
-        size_t tb = 0;
-        MQR_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (const int32_t*)nullptr, (int32_t*)nullptr,
-                                                       (int)(n_out + 1), st));
-        const size_t o_cnt = 4 * (size_t)(n_out + 1), o_list = 2 * o_cnt,
-                     o_tmp = (o_list + 4 * (size_t)std::max<int64_t>(nr, 1) + 255) & ~size_t(255);
-        if (grow(&x.csr, &x.csr_cap, o_tmp + tb)) return 1;
-        char* c = static_cast<char*>(x.csr);
-        int32_t* start = reinterpret_cast<int32_t*>(c);        // [n_out + 1]
-        int32_t* cnt = reinterpret_cast<int32_t*>(c + o_cnt);  // [n_out + 1]: counts (last 0), then fill cursors
-        int32_t* list = reinterpret_cast<int32_t*>(c + o_list);
-        MQR_CHECK_HIP(hipMemsetAsync(cnt, 0, o_cnt, st));
-        const unsigned g = (unsigned)((std::max<int64_t>(nr, 1) + 255) / 256);
-        if (nr) hipLaunchKernelGGL(k_csr_count, dim3(g), dim3(256), 0, st, x.pv.recv_dst, nr, cnt);
-        size_t t = tb;  // start[n_out] = nr
-        MQR_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(c + o_tmp, t, cnt, start, (int)(n_out + 1), st));
-        MQR_CHECK_HIP(hipMemsetAsync(cnt, 0, 4 * (size_t)n_out, st));
-        if (nr) hipLaunchKernelGGL(k_csr_fill, dim3(g), dim3(256), 0, st, x.pv.recv_dst, nr, start, cnt, list);
+        if (grow(&x.csr, &x.csr_cap, sizeof(int32_t) * (size_t)n_out * x.W)) return 1;
+        int32_t* ent = static_cast<int32_t*>(x.csr);
+        MQR_CHECK_HIP(hipMemsetAsync(ent, 0xff, sizeof(int32_t) * (size_t)n_out * x.W, st));
+        SegOffsets seg{};
+        for (int r = 0; r <= x.W; ++r) seg.off[r] = (int64_t)x.roff[r];
+        if (nr)
+            hipLaunchKernelGGL(k_merge_entries, dim3((unsigned)((nr + 255) / 256)), dim3(256), 0, st, x.pv.recv_dst, nr,
+                               seg, x.W, ent);
         const int me = x.me;
-        hipLaunchKernelGGL(k_merge_fused, dim3((unsigned)n_out), dim3(256), 0, st, start, list, n_out,
+        hipLaunchKernelGGL(k_merge_fused, dim3((unsigned)n_out), dim3(256), 0, st, ent, x.W, n_out,
                            static_cast<const float2*>(x.recvbuf), static_cast<const float2*>(x.sendbuf),
                            (int64_t)x.roff[me], (int64_t)x.roff[me + 1], (int64_t)x.soff[me], x.R3, out->pool);
         MQR_CHECK_HIP(hipGetLastError());
@@ -834,6 +822,7 @@ int mqr_reduce_rccl(mqr_vbg* local, mqr_comm* c, int mode, int root, mqr_vbg* ou
         set_error("mqr_reduce_rccl: merge kernels failed");
         return 1;
     }
+    if (activate_ordered_check(out)) return 1;
     for (int i = 0; i < 4; ++i)
         if (hipEventElapsedTime(&c->last_ms[i], c->ev[i], c->ev[i + 1]) != hipSuccess) c->last_ms[i] = -1.f;
     *n_owned = x.H.n_owned;
@@ -936,6 +925,7 @@ int mqr_merge_local(mqr_vbg** locals, int n, int mode, int root, mqr_vbg** outs,
         const auto t0 = std::chrono::steady_clock::now();
         if (xchg_merge(*X[d], st, outs[d])) return 1;
         MQR_CHECK_HIP(hipStreamSynchronize(st));
+        if (activate_ordered_check(outs[d])) return 1;
         n_owned[d] = X[d]->H.n_owned;
         t_local_ms[d] += std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }
@@ -1052,6 +1042,7 @@ int mqr_xchg_finish(mqr_xchg* h, int64_t* n_owned) {
     MQR_CHECK_HIP(hipSetDevice(h->device));
     if (xchg_merge(h->x, h->st.s, h->out)) return 1;
     MQR_CHECK_HIP(hipStreamSynchronize(h->st.s));
+    if (activate_ordered_check(h->out)) return 1;
     h->finished = true;
     if (n_owned) *n_owned = h->x.H.n_owned;
     return 0;

@@ -151,6 +151,7 @@ struct mqr_vbg {
     // mqr_integrate_frames on device frames returns once its last integrate is queued (the caller's stream
     // waits for it; the volume's next user orders behind it on the device) instead of draining the streams
     bool async_return = true;
+    bool act_check = false;  // activate_ordered's table-full check is still to be read (activate_ordered_check)
     int64_t batch_n_max = 0;             // largest batch list seen (grid of a speculative integrate)
     hipEvent_t touch_ev(int p) const { return sys_fence ? ev_touch_sys[p] : ev_touch[p]; }
     hipEvent_t int_ev(int p) const { return sys_fence ? ev_int_sys[p] : ev_int[p]; }
@@ -270,5 +271,6 @@ int d2h_parallel(int device, void* dst, const void* src, size_t bytes);
 int copy_to_host(int device, void* dst, const void* src, size_t bytes, hipStream_t s);
 int copy_to_device(int device, void* dst, const void* src, size_t bytes, hipStream_t s);
 hipStream_t copy_stream(int device);
-int activate_ordered(mqr_vbg* v, const uint64_t* dkeys, int64_t n);  // empty volume, buffer i = key i
+int activate_ordered(mqr_vbg* v, const uint64_t* dkeys, int64_t n, bool merge_writes_all);  // empty volume, buffer i = key i
+int activate_ordered_check(mqr_vbg* v);  // its table-full check (deferred when merge_writes_all)
 }  // namespace mqr

@@ -697,25 +697,50 @@ static void drain_events(mqr_vbg* v) {
 }
 
 // Fill an EMPTY volume with `n` distinct packed keys (device), buffer i = keys[i], pool counter n.
-int activate_ordered(mqr_vbg* v, const uint64_t* dkeys, int64_t n) {
+// merge_writes_all: the caller's merge writes every voxel of the n buffers (k_merge_fused) -- the pool is
+// not zeroed first, and the table-full check is deferred: the counters are copied to the host behind the
+// activation and activate_ordered_check reads them after the caller's final synchronize, so the host
+// does not wait here.  Otherwise the buffers start at (0, 0) (k_merge_blocks accumulates into them) and
+// the check is made before returning.
+int activate_ordered(mqr_vbg* v, const uint64_t* dkeys, int64_t n, bool merge_writes_all) {
     if (v->pool_count != 0) {
         set_error("internal: ordered activation needs an empty volume");
         return 1;
     }
+    v->act_check = false;
     if (n == 0) return 0;
-    if (sync_all(v) || ensure_table(v, n) || grow_pool(v, n) || reset_batch_counters(v, 0)) return 1;
-    // the merge accumulates into these buffers (k_merge_blocks): they start at (0, 0)
-    MQR_CHECK_HIP(hipMemsetAsync(v->pool, 0, sizeof(float2) * n * v->R3, v->stream));
+    // (ensure_table / grow_pool drain the volume's streams before they reallocate; everything else is
+    // ordered on `stream` behind the reset)
+    if (ensure_table(v, n) || grow_pool(v, n) || reset_batch_counters(v, 0)) return 1;
+    if (!merge_writes_all) MQR_CHECK_HIP(hipMemsetAsync(v->pool, 0, sizeof(float2) * n * v->R3, v->stream));
     hipLaunchKernelGGL(k_activate_ordered, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, v->stream, dkeys, n,
                        v->tab, v->bkeys, v->ctr(0));
     hipLaunchKernelGGL(k_set_counter, dim3(1), dim3(1), 0, v->stream, v->pool_ctr(), (int)n);
     MQR_CHECK_HIP(hipGetLastError());
+    v->pool_count = n;
+    if (merge_writes_all) {
+        MQR_CHECK_HIP(hipMemcpyAsync(v->hctr(0), v->ctr(0), sizeof(int) * kCountersTotal, hipMemcpyDeviceToHost,
+                                     v->stream));
+        MQR_CHECK_HIP(hipEventRecord(v->ev_host[0], v->stream));
+        v->act_check = true;
+        return 0;
+    }
     if (read_counters(v, 0)) return 1;
     if (v->hctr(0)[kOverflow] & 2) {
         set_error("internal: block table full");
         return 1;
     }
-    v->pool_count = n;
+    return 0;
+}
+
+int activate_ordered_check(mqr_vbg* v) {
+    if (!v->act_check) return 0;  // checked by activate_ordered itself, or nothing activated
+    v->act_check = false;
+    MQR_CHECK_HIP(hipEventSynchronize(v->ev_host[0]));
+    if (v->hctr(0)[kOverflow] & 2) {
+        set_error("internal: block table full");
+        return 1;
+    }
     return 0;
 }
 
