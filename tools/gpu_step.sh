@@ -12,6 +12,7 @@
 #   n2self      the same, bench.py --gpus 2 starting its own ranks (no torchrun) -> gpurun_out/${TAG}_bench_n2_selflaunch.json
 #   mbytes      C4 exchange bytes / zero-weight voxels / per-rank times at 2, 4, 8 ranks (tools/merge_bytes.py)
 #   prof        rocprofv3 --kernel-trace --stats of the C2 bench      -> gpurun_out/${TAG}_bench_kernel_stats.csv
+#   shardtrace[:W:R] one C4 shard's reset + integrate passes under a kernel trace (tools/shard_steps.py + step_head.py)
 #   mprof       rocprofv3 kernel trace + stats of tools/time_merge.py (8 ranks on one GPU)
 #   profc5      the same over the C5 leg alone                        -> gpurun_out/${TAG}_c5_kernel_stats.csv
 #   xtrace      kernel trace of 30 extractions: wall vs device span vs gaps -> gpurun_out/${TAG}_extract_timeline.json
@@ -88,6 +89,18 @@ for step in ${STEPS:-tests}; do
       python tools/merge_trace.py "$(find gpurun_out/mp -name '*kernel_trace.csv' | head -1)" > gpurun_out/${TAG}_merge_timeline.json
       rm -rf gpurun_out/mp
       cat gpurun_out/${TAG}_time_merge.json; head -c 3000 gpurun_out/${TAG}_merge_timeline.json ;;
+    shardtrace|shardtrace:*)
+      WR=8:3; [ "$step" != shardtrace ] && WR="${step#shardtrace:}"
+      rm -rf gpurun_out/sh
+      timeout -k 10 300 rocprofv3 --kernel-trace -f csv -d gpurun_out/sh -o run -- \
+        python tools/shard_steps.py --world "${WR%%:*}" --rank "${WR##*:}" --steps 40 > gpurun_out/${TAG}_shard_steps.json 2> gpurun_out/${TAG}_shard_steps.err \
+        || { tail -20 gpurun_out/${TAG}_shard_steps.err; exit 1; }
+      python tools/step_head.py "$(find gpurun_out/sh -name '*kernel_trace.csv' | head -1)" --steps 30 > gpurun_out/${TAG}_shard_head.json
+      rm -rf gpurun_out/sh
+      cat gpurun_out/${TAG}_shard_steps.json gpurun_out/${TAG}_shard_head.json ;;
+    shardall)
+      timeout -k 10 300 python tools/shard_steps.py --all --steps 40 > gpurun_out/${TAG}_shard_all.json 2> gpurun_out/${TAG}_shard_all.err || { tail -20 gpurun_out/${TAG}_shard_all.err; exit 1; }
+      grep "W=" gpurun_out/${TAG}_shard_all.err ;;
     profc5)
       rm -rf gpurun_out/profc5
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/profc5 -o run -- \
