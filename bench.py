@@ -1595,8 +1595,11 @@ def main():
         allmb = torch.stack(allmb)
         merge_bytes = {"sent_bytes_per_rank": allmb[:, 0].tolist(), "recv_bytes_per_rank": allmb[:, 1].tolist(),
                        "max_sent_bytes": float(allmb[:, 0].max()), "max_recv_bytes": float(allmb[:, 1].max()),
-                       "total_bytes": float(allmb[:, 0].sum()), "bytes_per_block": 8 * args.block_resolution ** 3,
-                       "note": "(tsdf, weight) float32 of whole blocks to each peer, the local self segment excluded"}
+                       "total_bytes": float(allmb[:, 0].sum()),
+                       "bytes_per_block": shard.get("bytes_per_block", 8 * args.block_resolution ** 3),
+                       "note": "whole blocks to each peer, the local self segment excluded: tsdf float32 with the "
+                               "weights as uint16 (6 B per voxel) when every rank's weights fit, else float32 "
+                               "(tsdf, weight) pairs (8 B per voxel)"}
     merge_phases_ms = ({k: sum(p[k] for p in merge_phases) / len(merge_phases) for k in merge_phases[0]}
                        if merge_phases else None)
 

@@ -160,12 +160,18 @@ int mqr_merge_local(mqr_vbg** locals, int n, int mode, int root, mqr_vbg** outs,
 int mqr_comm_timing(mqr_comm* comm, float* ms4);
 /* Segment sizes of the last mqr_reduce_rccl on `comm`: blocks sent to / received from each rank
  * (world entries each; the own rank's entry is the local self segment, not carried by RCCL) and the
- * floats per block (2 R^3).  Zeros before the first merge. */
+ * 4-byte words per block (2 R^3, or 1.5 R^3 with uint16 weights).  Zeros before the first merge. */
 int mqr_comm_counts(mqr_comm* comm, int64_t* send_blocks, int64_t* recv_blocks, int64_t* floats_per_block);
 int mqr_merge_local_timing(float* ms, int n);
-/* How every transport merges the received segments (process-wide, for A/Bs and tests): 0 (default) one
- * fused pass per output block folding its entries in rank order in registers; 1 the round-5 form, one
- * pass over the output per source rank.  The two give the same bits. */
+/* Merge A/B and test hooks (process-wide).  Bit 0: how every transport merges the received segments --
+ * 0 (default) one fused pass per output block folding its entries in rank order in registers, 1 the
+ * round-5 form, one pass over the output per source rank.  Bit 1: mqr_merge_local sends float32 weights
+ * even where uint16 would hold them.  Segment format: a block travels as its R^3 (tsdf, weight) float32
+ * pairs, or -- when every rank's weights are integers <= 65535, which the library knows from each volume's
+ * frame count (volumes filled by import or unpack count as unknown) -- as R^3 float32 tsdf then R^3
+ * uint16 weights (6 B instead of 8 B per voxel); mqr_comm_counts / mqr_xchg_counts report the 4-byte
+ * words per block of the format used (2 R^3 or 1.5 R^3; the caller-carried transport always uses float32
+ * pairs).  Every combination gives the same bits. */
 int mqr_merge_set_per_source(int on);
 typedef struct mqr_xchg mqr_xchg;
 int mqr_xchg_create(mqr_vbg* local, int world, int rank, int mode, int root, const uint64_t* gathered_keys,

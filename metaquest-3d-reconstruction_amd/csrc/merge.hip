@@ -143,27 +143,52 @@ struct mqr_comm {
 namespace mqr {
 
 // ------------------------------------------------------------------ kernels
-// (tsdf, weight) of listed local buffers into consecutive [R3] float2 entries.
+// Segment formats.  PK = 0: a block is its R3 (tsdf, weight) float2 pairs, the pool's own layout (8 B per
+// voxel).  PK = 1: R3 float tsdf, then R3 uint16 weights (6 B per voxel) -- used when every rank's
+// weights are integers <= 65535 (each rank's wbound; all ranks decide alike from the gathered bounds),
+// which uint16 holds exactly, so the merge reads the same values either way.
+template <int PK>
+__device__ __forceinline__ float2 seg_load(const char* __restrict__ blk, int p, int R3) {
+    if constexpr (PK == 0) {
+        return reinterpret_cast<const float2*>(blk)[p];
+    } else {
+        return make_float2(reinterpret_cast<const float*>(blk)[p],
+                           (float)reinterpret_cast<const uint16_t*>(blk + 4 * (size_t)R3)[p]);
+    }
+}
+__host__ __device__ constexpr size_t seg_block_bytes(int pk, int R3) { return (size_t)R3 * (pk ? 6 : 8); }
+
+// (tsdf, weight) of listed local buffers into consecutive segment blocks.
+template <int PK>
 __global__ void k_gather_blocks(const int32_t* __restrict__ bufs, int64_t n, const float2* __restrict__ pool, int R3,
-                                float2* __restrict__ out) {
+                                char* __restrict__ out) {
     const int64_t j = blockIdx.x;
     if (j >= n) return;
     const float2* src = pool + (int64_t)bufs[j] * R3;
-    float2* dst = out + j * R3;
-    for (int p = threadIdx.x; p < R3; p += blockDim.x) dst[p] = src[p];
+    char* dst = out + j * seg_block_bytes(PK, R3);
+    for (int p = threadIdx.x; p < R3; p += blockDim.x) {
+        const float2 v = src[p];
+        if constexpr (PK == 0) {
+            reinterpret_cast<float2*>(dst)[p] = v;
+        } else {
+            reinterpret_cast<float*>(dst)[p] = v.x;
+            reinterpret_cast<uint16_t*>(dst + 4 * (size_t)R3)[p] = (uint16_t)v.y;
+        }
+    }
 }
 
 // Merge received entries into destination buffers: a voxel with no weight yet takes the entry as
 // is, one with weight merges by the running-average identity; entries with zero weight change
 // nothing.  One launch per source rank, in rank order; a buffer appears at most once per source.
-__global__ void k_merge_blocks(const int32_t* __restrict__ dst, int64_t n, const float2* __restrict__ in, int R3,
+template <int PK>
+__global__ void k_merge_blocks(const int32_t* __restrict__ dst, int64_t n, const char* __restrict__ in, int R3,
                                float2* __restrict__ pool) {
     const int64_t j = blockIdx.x;
     if (j >= n) return;
-    const float2* src = in + j * R3;
+    const char* src = in + j * seg_block_bytes(PK, R3);
     float2* out = pool + (int64_t)dst[j] * R3;
     for (int p = threadIdx.x; p < R3; p += blockDim.x) {
-        const float2 a = out[p], b = src[p];
+        const float2 a = out[p], b = seg_load<PK>(src, p, R3);
         if (b.y == 0.f) continue;
         if (a.y == 0.f) {
             out[p] = b;
@@ -185,6 +210,7 @@ __global__ void k_merge_blocks(const int32_t* __restrict__ dst, int64_t n, const
 // (it is in the plan because some rank holds the block), so every voxel is written and the output pool
 // needs no zeroing.
 static std::atomic<bool> g_merge_per_source{false};  // A/B and test hook: mqr_merge_set_per_source
+static std::atomic<bool> g_merge_f32_segments{false};  // A/B and test hook: mqr_merge_set_per_source bit 1
 constexpr int kMergeMaxEntries = 64;                  // a buffer gets at most one entry per rank (kMaxRanks)
 
 struct SegOffsets {
@@ -200,8 +226,9 @@ __global__ void k_merge_entries(const int32_t* __restrict__ dst, int64_t n, SegO
     ent[(int64_t)dst[j] * W + s] = (int32_t)j;
 }
 
+template <int PK>
 __global__ __launch_bounds__(256) void k_merge_fused(const int32_t* __restrict__ ent, int W, int64_t n_out,
-                                                     const float2* __restrict__ recv, const float2* __restrict__ send,
+                                                     const char* __restrict__ recv, const char* __restrict__ send,
                                                      int64_t self_lo, int64_t self_hi, int64_t self_send, int R3,
                                                      float2* __restrict__ pool) {
     __shared__ int32_t e[kMergeMaxEntries];
@@ -223,7 +250,9 @@ __global__ __launch_bounds__(256) void k_merge_fused(const int32_t* __restrict__
         float2 a = make_float2(0.f, 0.f);  // the buffer as the per-source form starts it (zeroed)
         for (int k = 0; k < m; ++k) {
             const int64_t j = e[k];
-            const float2 b = (j >= self_lo && j < self_hi) ? send[(self_send + (j - self_lo)) * R3 + p] : recv[j * R3 + p];
+            const size_t bb = seg_block_bytes(PK, R3);
+            const char* blk = (j >= self_lo && j < self_hi) ? send + (self_send + (j - self_lo)) * bb : recv + j * bb;
+            const float2 b = seg_load<PK>(blk, p, R3);
             if (b.y == 0.f) continue;
             if (a.y == 0.f) {
                 a = b;
@@ -557,6 +586,7 @@ struct Exchange {
     PlanView pv;
     PlanSummary H{};
     int W = 1, me = 0, R3 = 0;
+    int pk = 0;                       // segment format (seg_load): 0 float2 pairs, 1 uint16 weights
     std::vector<size_t> soff, roff;  // block offsets of the segments
     void* sendbuf = nullptr;
     size_t send_cap = 0;
@@ -575,19 +605,21 @@ struct Exchange {
     }
     size_t send_blocks(int d) const { return soff[d + 1] - soff[d]; }
     size_t recv_blocks(int s) const { return roff[s + 1] - roff[s]; }
-    float2* send_seg(int d) const { return static_cast<float2*>(sendbuf) + soff[d] * R3; }
-    float2* recv_seg(int s) const { return static_cast<float2*>(recvbuf) + roff[s] * R3; }
-    size_t seg_floats(size_t blocks) const { return blocks * (size_t)R3 * 2; }
+    size_t block_bytes() const { return seg_block_bytes(pk, R3); }
+    char* send_seg(int d) const { return static_cast<char*>(sendbuf) + soff[d] * block_bytes(); }
+    char* recv_seg(int s) const { return static_cast<char*>(recvbuf) + roff[s] * block_bytes(); }
+    size_t seg_bytes(size_t blocks) const { return blocks * block_bytes(); }
 };
 
 // Plan (identical on every rank) from the gathered keys dkeys[W * mx] (device), output volume,
 // send segments gathered from `local`, and the self segment copied into the receive buffer.
 // ev_plan / ev_gathered (nullable) are recorded after the plan and after the gather.
 static int xchg_prepare(Exchange& x, hipStream_t st, const uint64_t* dkeys, int W, int64_t mx, int me, int mode,
-                        int root, mqr_vbg* local, mqr_vbg* out, hipEvent_t ev_plan, hipEvent_t ev_gathered) {
+                        int root, mqr_vbg* local, mqr_vbg* out, hipEvent_t ev_plan, hipEvent_t ev_gathered, int pk) {
     x.W = W;
     x.me = me;
     x.R3 = (int)local->R3;
+    x.pk = pk;
     if (device_plan(x.plan, st, dkeys, W, mx, me, mode, root, x.pv)) return 1;
     if (ev_plan) MQR_CHECK_HIP(hipEventRecord(ev_plan, st));
     x.H = *x.pv.H;
@@ -598,7 +630,7 @@ static int xchg_prepare(Exchange& x, hipStream_t st, const uint64_t* dkeys, int 
         x.roff[r + 1] = x.roff[r] + (size_t)x.H.cnt[1][r];
     }
     const size_t ns = x.soff[W], nr = x.roff[W];
-    const size_t eb = sizeof(float2) * (size_t)x.R3;
+    const size_t eb = x.block_bytes();
     x.fused = !g_merge_per_source.load();
     // (fused: the output's activation is not waited for -- the merge writes only pool buffers, and
     // activate_ordered_check reads its table-full flag after the merge)
@@ -606,9 +638,14 @@ static int xchg_prepare(Exchange& x, hipStream_t st, const uint64_t* dkeys, int 
     if (grow(&x.sendbuf, &x.send_cap, std::max<size_t>(ns, 1) * eb) ||
         grow(&x.recvbuf, &x.recv_cap, std::max<size_t>(nr, 1) * eb))
         return 1;
-    if (ns)
-        hipLaunchKernelGGL(k_gather_blocks, dim3((unsigned)ns), dim3(256), 0, st, x.pv.send_idx, (int64_t)ns,
-                           local->pool, x.R3, static_cast<float2*>(x.sendbuf));
+    if (ns) {
+        if (x.pk)
+            hipLaunchKernelGGL(k_gather_blocks<1>, dim3((unsigned)ns), dim3(256), 0, st, x.pv.send_idx, (int64_t)ns,
+                               local->pool, x.R3, static_cast<char*>(x.sendbuf));
+        else
+            hipLaunchKernelGGL(k_gather_blocks<0>, dim3((unsigned)ns), dim3(256), 0, st, x.pv.send_idx, (int64_t)ns,
+                               local->pool, x.R3, static_cast<char*>(x.sendbuf));
+    }
     MQR_CHECK_HIP(hipGetLastError());
     if (ev_gathered) MQR_CHECK_HIP(hipEventRecord(ev_gathered, st));
     MQR_REQUIRE(x.send_blocks(me) == x.recv_blocks(me), "merge plan: self segment lengths differ");
@@ -616,6 +653,20 @@ static int xchg_prepare(Exchange& x, hipStream_t st, const uint64_t* dkeys, int 
         MQR_CHECK_HIP(hipMemcpyAsync(x.recv_seg(me), x.send_seg(me), eb * x.send_blocks(me), hipMemcpyDeviceToDevice,
                                      st));
     return 0;
+}
+
+// Segment format from every rank's weight bound (wbound: -1 unknown): uint16 weights when all are known
+// and <= 65535 (and R^3 even, so a segment is whole 4-byte words); the output's bound is their sum.
+static int seg_format(const int64_t* wb, int W, int R3, int64_t* out_bound) {
+    bool known = true;
+    int64_t mxb = 0, sum = 0;
+    for (int r = 0; r < W; ++r) {
+        known = known && wb[r] >= 0;
+        mxb = std::max(mxb, wb[r]);
+        sum += std::max<int64_t>(wb[r], 0);
+    }
+    *out_bound = known ? sum : -1;
+    return (known && mxb <= 65535 && R3 % 2 == 0) ? 1 : 0;
 }
 
 // Received segments into the output volume, source by source in rank order (deterministic sums).
@@ -633,17 +684,20 @@ static int xchg_merge(Exchange& x, hipStream_t st, mqr_vbg* out) {
             hipLaunchKernelGGL(k_merge_entries, dim3((unsigned)((nr + 255) / 256)), dim3(256), 0, st, x.pv.recv_dst, nr,
                                seg, x.W, ent);
         const int me = x.me;
-        hipLaunchKernelGGL(k_merge_fused, dim3((unsigned)n_out), dim3(256), 0, st, ent, x.W, n_out,
-                           static_cast<const float2*>(x.recvbuf), static_cast<const float2*>(x.sendbuf),
+        auto fused = x.pk ? k_merge_fused<1> : k_merge_fused<0>;
+        hipLaunchKernelGGL(fused, dim3((unsigned)n_out), dim3(256), 0, st, ent, x.W, n_out,
+                           static_cast<const char*>(x.recvbuf), static_cast<const char*>(x.sendbuf),
                            (int64_t)x.roff[me], (int64_t)x.roff[me + 1], (int64_t)x.soff[me], x.R3, out->pool);
         MQR_CHECK_HIP(hipGetLastError());
         return 0;
     }
     for (int src = 0; src < x.W; ++src)
-        if (x.recv_blocks(src))
-            hipLaunchKernelGGL(k_merge_blocks, dim3((unsigned)x.recv_blocks(src)), dim3(256), 0, st,
+        if (x.recv_blocks(src)) {
+            auto per_source = x.pk ? k_merge_blocks<1> : k_merge_blocks<0>;
+            hipLaunchKernelGGL(per_source, dim3((unsigned)x.recv_blocks(src)), dim3(256), 0, st,
                                x.pv.recv_dst + x.roff[src], (int64_t)x.recv_blocks(src), x.recv_seg(src), x.R3,
                                out->pool);
+        }
     MQR_CHECK_HIP(hipGetLastError());
     return 0;
 }
@@ -757,7 +811,7 @@ int mqr_comm_counts(mqr_comm* c, int64_t* send_blocks, int64_t* recv_blocks, int
         if (send_blocks) send_blocks[p] = run ? (int64_t)x.send_blocks(p) : 0;
         if (recv_blocks) recv_blocks[p] = run ? (int64_t)x.recv_blocks(p) : 0;
     }
-    if (floats_per_block) *floats_per_block = 2 * (int64_t)x.R3;
+    if (floats_per_block) *floats_per_block = (int64_t)(x.block_bytes() / 4);
     return 0;
 }
 
@@ -774,20 +828,30 @@ int mqr_reduce_rccl(mqr_vbg* local, mqr_comm* c, int mode, int root, mqr_vbg* ou
     *n_owned = 0;
     const int W = c->world, me = c->rank;
     // host state the stream's async copies read: declared before the drain guard, so it outlives it
-    int64_t n_me = 0;
-    std::vector<int64_t> cnt(W);
+    int64_t mine[2] = {0, 0};
+    std::vector<int64_t> cnt(2 * W);
     StreamDrain drain{c->s};
     if (sync_all(local)) return 1;  // the local volume's integration is complete
-    n_me = local->pool_count;
+    mine[0] = local->pool_count;
+    mine[1] = local->wbound;
+    const int64_t n_me = mine[0];
     MQR_CHECK_HIP(hipEventRecord(c->ev[0], c->s));
-    // 1. all-gather block counts (host: the padding), then the padded packed keys
-    if (grow(&c->small, &c->small_cap, sizeof(int64_t) * 2 * W)) return 1;
+    // 1. all-gather (block count, weight bound) pairs (host: the padding, the segment format), then the
+    //    padded packed keys
+    if (grow(&c->small, &c->small_cap, sizeof(int64_t) * 2 * (W + 1))) return 1;
     int64_t* dcnt = static_cast<int64_t*>(c->small);
-    MQR_CHECK_HIP(hipMemcpyAsync(dcnt + W, &n_me, sizeof(int64_t), hipMemcpyHostToDevice, c->s));
-    MQR_CHECK_NCCL(api, api->AllGather(dcnt + W, dcnt, 1, ncclInt64, c->nc, c->s));
-    MQR_CHECK_HIP(hipMemcpyAsync(cnt.data(), dcnt, sizeof(int64_t) * W, hipMemcpyDeviceToHost, c->s));
+    MQR_CHECK_HIP(hipMemcpyAsync(dcnt + 2 * W, mine, sizeof(mine), hipMemcpyHostToDevice, c->s));
+    MQR_CHECK_NCCL(api, api->AllGather(dcnt + 2 * W, dcnt, 2, ncclInt64, c->nc, c->s));
+    MQR_CHECK_HIP(hipMemcpyAsync(cnt.data(), dcnt, sizeof(int64_t) * 2 * W, hipMemcpyDeviceToHost, c->s));
     MQR_CHECK_HIP(hipStreamSynchronize(c->s));
-    const int64_t mx = std::max<int64_t>(1, *std::max_element(cnt.begin(), cnt.end()));
+    int64_t mx = 1;
+    std::vector<int64_t> wb(W);
+    for (int r = 0; r < W; ++r) {
+        mx = std::max(mx, cnt[2 * r]);
+        wb[r] = cnt[2 * r + 1];
+    }
+    int64_t out_bound = -1;
+    const int pk = seg_format(wb.data(), W, (int)local->R3, &out_bound);
     if (grow(&c->small, &c->small_cap, sizeof(uint64_t) * mx * (W + 1))) return 1;
     uint64_t* dkeys = static_cast<uint64_t*>(c->small);
     uint64_t* dmine = dkeys + mx * W;
@@ -797,16 +861,17 @@ int mqr_reduce_rccl(mqr_vbg* local, mqr_comm* c, int mode, int root, mqr_vbg* ou
     MQR_CHECK_NCCL(api, api->AllGather(dmine, dkeys, mx, ncclUint64, c->nc, c->s));
     // 2. plan (on the device, identical on every rank), output volume, send segments
     Exchange& x = *c->x;
-    if (xchg_prepare(x, c->s, dkeys, W, mx, me, mode, root, local, out, c->ev[1], c->ev[2])) return 1;
+    if (xchg_prepare(x, c->s, dkeys, W, mx, me, mode, root, local, out, c->ev[1], c->ev[2], pk)) return 1;
+    out->wbound = out_bound;
     // 3. the sparse all-to-all: segment for p -> p, segment from p <- p (the self segment is local)
     {
         ncclResult_t r = api->GroupStart();
         for (int p = 0; p < W && r == ncclSuccess; ++p) {
             if (p == me) continue;
             if (x.send_blocks(p))
-                r = api->Send(x.send_seg(p), x.seg_floats(x.send_blocks(p)), ncclFloat32, p, c->nc, c->s);
+                r = api->Send(x.send_seg(p), x.seg_bytes(x.send_blocks(p)), ncclUint8, p, c->nc, c->s);
             if (r == ncclSuccess && x.recv_blocks(p))
-                r = api->Recv(x.recv_seg(p), x.seg_floats(x.recv_blocks(p)), ncclFloat32, p, c->nc, c->s);
+                r = api->Recv(x.recv_seg(p), x.seg_bytes(x.recv_blocks(p)), ncclUint8, p, c->nc, c->s);
         }
         const ncclResult_t r2 = api->GroupEnd();
         if (r != ncclSuccess || r2 != ncclSuccess) {
@@ -871,6 +936,11 @@ int mqr_merge_local(mqr_vbg** locals, int n, int mode, int root, mqr_vbg** outs,
                                          hipMemcpyDeviceToDevice, st));
     MQR_CHECK_HIP(hipStreamSynchronize(st));
     t_local_ms.assign(n, 0.f);
+    std::vector<int64_t> wb(n);
+    for (int r = 0; r < n; ++r) wb[r] = locals[r]->wbound;
+    int64_t out_bound = -1;
+    const int pk = g_merge_f32_segments.load() ? 0 : seg_format(wb.data(), n, (int)locals[0]->R3, &out_bound);
+    if (g_merge_f32_segments.load()) seg_format(wb.data(), n, (int)locals[0]->R3, &out_bound);  // (the bound only)
     // 1. every rank's own side, exactly as mqr_reduce_rccl runs it on that rank: its plan (me = s),
     //    its output volume, its send segments packed from its own pool
     // the ranks' Exchange objects (plan scratch, send / receive buffers: grow-only) are kept per device
@@ -886,7 +956,8 @@ int mqr_merge_local(mqr_vbg** locals, int n, int mode, int root, mqr_vbg** outs,
     }
     for (int s = 0; s < n; ++s) {
         const auto t0 = std::chrono::steady_clock::now();
-        if (xchg_prepare(*X[s], st, dkeys, n, mx, s, mode, root, locals[s], outs[s], nullptr, nullptr)) return 1;
+        if (xchg_prepare(*X[s], st, dkeys, n, mx, s, mode, root, locals[s], outs[s], nullptr, nullptr, pk)) return 1;
+        outs[s]->wbound = out_bound;
         MQR_CHECK_HIP(hipStreamSynchronize(st));
         t_local_ms[s] += std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }
@@ -916,7 +987,7 @@ int mqr_merge_local(mqr_vbg** locals, int n, int mode, int root, mqr_vbg** outs,
                 return 4;
             }
             if (s != d)
-                MQR_CHECK_HIP(hipMemcpyAsync(X[d]->recv_seg(s), X[s]->send_seg(d), sizeof(float2) * m * X[s]->R3,
+                MQR_CHECK_HIP(hipMemcpyAsync(X[d]->recv_seg(s), X[s]->send_seg(d), X[s]->seg_bytes(m),
                                              hipMemcpyDeviceToDevice, st));
         }
     MQR_CHECK_HIP(hipStreamSynchronize(st));
@@ -933,7 +1004,8 @@ int mqr_merge_local(mqr_vbg** locals, int n, int mode, int root, mqr_vbg** outs,
 }
 
 int mqr_merge_set_per_source(int on) {
-    g_merge_per_source.store(on != 0);
+    g_merge_per_source.store((on & 1) != 0);
+    g_merge_f32_segments.store((on & 2) != 0);
     return 0;
 }
 
@@ -989,8 +1061,9 @@ int mqr_xchg_create(mqr_vbg* local, int world, int rank, int mode, int root, con
         }
     }
     if (xchg_prepare(xh->x, xh->st.s, static_cast<const uint64_t*>(xh->dkeys), world, mx, rank, mode, root, local,
-                     out, nullptr, nullptr))
+                     out, nullptr, nullptr, 0))  // (the caller carries float32 pairs)
         return 1;
+    out->wbound = -1;  // (the caller's transport does not carry the ranks' bounds)
     MQR_CHECK_HIP(hipStreamSynchronize(xh->st.s));
     *h = xh.release();
     return 0;
@@ -1003,7 +1076,7 @@ int mqr_xchg_counts(mqr_xchg* h, int64_t* send_blocks, int64_t* recv_blocks, int
         if (recv_blocks) recv_blocks[p] = (int64_t)h->x.recv_blocks(p);
     }
     if (n_owned) *n_owned = h->x.H.n_owned;
-    if (floats_per_block) *floats_per_block = 2 * (int64_t)h->x.R3;
+    if (floats_per_block) *floats_per_block = (int64_t)(h->x.block_bytes() / 4);
     return 0;
 }
 
@@ -1015,7 +1088,7 @@ int mqr_xchg_send_segment(mqr_xchg* h, int peer, float* dst, int loc) {
     MQR_REQUIRE(dst, "null destination");
     MQR_CHECK_HIP(hipSetDevice(h->device));
     if (loc == MQR_DEVICE && order_after_caller(h->device, h->st.s)) return 2;
-    MQR_CHECK_HIP(hipMemcpyAsync(dst, h->x.send_seg(peer), sizeof(float) * h->x.seg_floats(m),
+    MQR_CHECK_HIP(hipMemcpyAsync(dst, h->x.send_seg(peer), h->x.seg_bytes(m),
                                  loc == MQR_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, h->st.s));
     MQR_CHECK_HIP(hipStreamSynchronize(h->st.s));
     return 0;
@@ -1030,7 +1103,7 @@ int mqr_xchg_recv_segment(mqr_xchg* h, int peer, const float* src, int loc) {
     MQR_REQUIRE(src, "null source");
     MQR_CHECK_HIP(hipSetDevice(h->device));
     if (loc == MQR_DEVICE && order_after_caller(h->device, h->st.s)) return 2;
-    MQR_CHECK_HIP(hipMemcpyAsync(h->x.recv_seg(peer), src, sizeof(float) * h->x.seg_floats(m),
+    MQR_CHECK_HIP(hipMemcpyAsync(h->x.recv_seg(peer), src, h->x.seg_bytes(m),
                                  loc == MQR_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, h->st.s));
     MQR_CHECK_HIP(hipStreamSynchronize(h->st.s));
     return 0;

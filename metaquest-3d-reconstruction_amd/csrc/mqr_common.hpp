@@ -166,6 +166,9 @@ struct mqr_vbg {
     uint64_t* bkeys = nullptr; // [pool_cap] packed key of each buffer
     int64_t pool_cap = 0;
     int64_t pool_count = 0;    // host mirror (valid after each batch)
+    // Upper bound of any voxel's weight (every integrated frame adds at most 1): the merge sends weights as
+    // uint16 when every rank's bound is <= 65535.  -1 = unknown (imported or unpacked contents).
+    int64_t wbound = 0;
     int64_t batch_new_max = 0; // most blocks one integrate batch has allocated (sizes the table headroom)
 
     int32_t* lists[2] = {nullptr, nullptr};  // batch slot lists, capacity list_cap each

@@ -1041,6 +1041,7 @@ int mqr_vbg_reset(mqr_vbg* v) {
                        v->counters, nctr);
     MQR_CHECK_HIP(hipGetLastError());
     v->pool_count = 0;
+    v->wbound = 0;
     v->ctr_clean[0] = v->ctr_clean[1] = true;
     return 0;
 }
@@ -1081,6 +1082,7 @@ int mqr_integrate_frames(mqr_vbg* v, const float* depths, int depth_loc, int B, 
     std::vector<int> valid;
     for (int i = 0; i < B; ++i)
         if (!frame_ok || frame_ok[i]) valid.push_back(i);
+    if (v->wbound >= 0) v->wbound += (int64_t)valid.size();  // (an upper bound even if the call fails part-way)
     int rc = 0;
     int batch = 0;
     // batches of up to batch_frames frames (127), the first of a call a full batch as well
@@ -1243,6 +1245,7 @@ int mqr_integrate(mqr_vbg* v, const int32_t* keys, int64_t n, const float* depth
     MQR_REQUIRE(v && depth && K && T_wc && (keys || n == 0), "null argument");
     MQR_CHECK_HIP(hipSetDevice(v->device));
     if (n == 0) return 0;
+    if (v->wbound >= 0) v->wbound += 1;
     if (sync_all(v)) return 1;
     if (depth_loc == MQR_DEVICE && order_after_caller(v->device, v->stream, v->stream2)) return 2;
     const int64_t HW = (int64_t)H * W;
@@ -1324,6 +1327,7 @@ int mqr_vbg_import(mqr_vbg* v, const int32_t* keys, const float* tsdf, const flo
     MQR_REQUIRE(v && ((keys && tsdf && weight) || n == 0), "null argument");
     MQR_CHECK_HIP(hipSetDevice(v->device));
     if (n == 0) return 0;
+    v->wbound = -1;  // arbitrary weights: the merge keeps them float32
     if (sync_all(v)) return 1;
     if (loc == MQR_DEVICE && order_after_caller(v->device, v->stream)) return 2;
     const int32_t* dk = keys;
@@ -1374,6 +1378,7 @@ int mqr_vbg_unpack_weighted(mqr_vbg* v, const int32_t* union_keys, int64_t U, co
     MQR_REQUIRE(v && (U == 0 || (union_keys && packed)), "null argument");
     MQR_CHECK_HIP(hipSetDevice(v->device));
     if (U == 0) return 0;
+    v->wbound = -1;
     if (sync_all(v)) return 1;
     if (order_after_caller(v->device, v->stream)) return 2;
     if (activate_device_keys(v, union_keys, U)) return 1;

@@ -257,7 +257,8 @@ def _segment_stats(send_blocks, recv_blocks, bytes_per_block, rank) -> dict:
     sc = np.asarray(send_blocks, np.int64).copy()
     rc = np.asarray(recv_blocks, np.int64).copy()
     sc[rank] = rc[rank] = 0
-    return {"sent_blocks": int(sc.sum()), "recv_blocks": int(rc.sum()), "sent_bytes": int(sc.sum()) * bytes_per_block,
+    return {"bytes_per_block": int(bytes_per_block),
+            "sent_blocks": int(sc.sum()), "recv_blocks": int(rc.sum()), "sent_bytes": int(sc.sum()) * bytes_per_block,
             "recv_bytes": int(rc.sum()) * bytes_per_block, "peers_sent_to": int((sc > 0).sum()),
             "max_segment_bytes": int(max(sc.max(), rc.max()) * bytes_per_block) if len(sc) else 0}
 
@@ -381,11 +382,12 @@ def merge_local_timing(n: int):
     return ms.tolist()
 
 
-def set_merge_per_source(on: bool):
-    """Process-wide merge form (mqr_merge_set_per_source): False (default) = one fused pass per output
-    block, True = the round-5 pass per source rank.  Same bits; for A/Bs and tests."""
+def set_merge_per_source(on: bool, f32_segments: bool = False):
+    """Process-wide merge A/B hooks (mqr_merge_set_per_source): on = the round-5 pass per source rank
+    instead of one fused pass per output block; f32_segments = merge_local sends float32 weights even
+    where uint16 holds them.  Same bits; for A/Bs and tests."""
     from . import _lib
-    _lib.call("mqr_merge_set_per_source", 1 if on else 0)
+    _lib.call("mqr_merge_set_per_source", (1 if on else 0) | (2 if f32_segments else 0))
 
 
 def extract_mesh_owned(vbg, n_owned: int, weight_threshold: float = 1.5):

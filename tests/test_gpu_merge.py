@@ -161,6 +161,51 @@ def test_rccl_world_one(seq):
         comm.close()
 
 
+def test_segment_format_follows_the_weight_bounds(seq):
+    """Segments carry uint16 weights when every rank's weights are integers <= 65535 (integrated volumes)
+    and float32 pairs otherwise (an imported volume's weights are unknown); the RCCL path at world size 1
+    reports the format in its counts, and the merged volume is the same either way."""
+    from mqr.distributed import RcclComm, merge_rccl
+    from mqr.vbg import VoxelBlockGrid
+    vol = _shards(seq, 1)[0]
+    R3 = 16 ** 3
+    comm = RcclComm(0, 0, 1, RcclComm.unique_id())
+    try:
+        out, _ = merge_rccl(vol, comm, mode="root")
+        assert comm.counts()["bytes_per_block"] == 6 * R3  # uint16 weights
+        a = out.export()
+        imp = VoxelBlockGrid(voxel_size=0.01, block_resolution=16, block_count=64)
+        imp.import_blocks(*vol.export())
+        out2, _ = merge_rccl(imp, comm, mode="root")
+        assert comm.counts()["bytes_per_block"] == 8 * R3  # float32 pairs
+        assert compare_volumes(out2.export(), a, 0.0) == 0.0
+        assert compare_volumes(a, vol.export(), 0.0) == 0.0
+    finally:
+        comm.close()
+
+
+@pytest.mark.parametrize("world,mode", [(3, "sharded"), (8, "root")])
+def test_uint16_weight_segments_equal_float32_segments(seq, world, mode):
+    """merge_local with uint16-weight segments (the default for integrated volumes) against float32 pairs
+    (mqr_merge_set_per_source bit 1), fused and per-source merges: every output bit for bit."""
+    from mqr.distributed import merge_local, set_merge_per_source
+    vols = _shards(seq, world)
+    outs = {}
+    try:
+        for per_source in (False, True):
+            for f32 in (False, True):
+                set_merge_per_source(per_source, f32)
+                outs[(per_source, f32)] = [(o.export(), n) for o, n in merge_local(vols, mode=mode)]
+    finally:
+        set_merge_per_source(False, False)
+    ref = outs[(False, False)]
+    for key, got in outs.items():
+        for (a, na), (b, nb) in zip(ref, got):
+            assert na == nb, key
+            for x, y in zip(a, b):
+                assert np.array_equal(x, y), key
+
+
 def _rccl_worker(rank, world, port, q):
     import torch
     import torch.distributed as dist

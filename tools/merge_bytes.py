@@ -61,6 +61,9 @@ def plan_counts(keys_per_rank, zeros_per_rank, R3):
     for r in range(W):
         out[r]["recv_blocks"] = int(recv[r])
         out[r]["recv_bytes"] = int(recv[r]) * R3 * 8
+        # the segments as the library sends integrated volumes: tsdf float32 + weight uint16 (6 B per voxel)
+        out[r]["sent_bytes_uint16_weights"] = out[r]["sent_bytes"] // 8 * 6
+        out[r]["recv_bytes_uint16_weights"] = out[r]["recv_bytes"] // 8 * 6
     return U, out
 
 
@@ -130,6 +133,8 @@ def main():
             per[r]["merge_own_ms_per_source"] = own_ps[r]
         res["per_world"][W] = {"union_blocks": U, "ranks": per,
                                "max_sent_bytes": max(p["sent_bytes"] for p in per),
+                               "max_sent_bytes_uint16_weights": max(p["sent_bytes_uint16_weights"] for p in per),
+                               "max_recv_bytes_uint16_weights": max(p["recv_bytes_uint16_weights"] for p in per),
                                "max_recv_bytes": max(p["recv_bytes"] for p in per),
                                "max_integrate_ms": max(int_ms), "max_merge_own_ms": max(own_ms),
                                "max_merge_own_ms_per_source": max(own_ps),
