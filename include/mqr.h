@@ -60,7 +60,8 @@ int mqr_device_count(int* n);
 int mqr_set_stream(void* stream);
 int mqr_get_stream(void** stream);
 
-/* Device memory helpers (so callers can keep inputs resident in HBM without any framework). */
+/* Device memory helpers (so callers can keep inputs resident in HBM without any framework).
+ * mqr_device_free waits for the device first (work in flight may still read the buffer). */
 int mqr_device_alloc(int device, int64_t bytes, void** ptr);
 int mqr_device_free(int device, void* ptr);
 int mqr_memcpy(void* dst, int dst_loc, const void* src, int src_loc, int64_t bytes, int device);

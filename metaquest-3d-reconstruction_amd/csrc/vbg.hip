@@ -917,6 +917,9 @@ int mqr_device_alloc(int device, int64_t bytes, void** ptr) {
 
 int mqr_device_free(int device, void* ptr) {
     MQR_CHECK_HIP(hipSetDevice(device));
+    // the buffer may still be read by work in flight on the library's streams (an integrate_frames on
+    // device frames returns before its last integrate ends): the whole device first
+    MQR_CHECK_HIP(hipDeviceSynchronize());
     MQR_CHECK_HIP(hipFree(ptr));
     return 0;
 }
