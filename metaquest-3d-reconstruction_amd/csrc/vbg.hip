@@ -397,6 +397,9 @@ static int launch_integrate_ab(mqr_vbg* v, int var, hipStream_t s, unsigned grid
         case 57: *fixup = true; wx(k_integrate_wx<8, 3>); break;
         case 58: *fixup = true; wx(k_integrate_wx<7, 3>); break;
         case 59: *fixup = true; wx(k_integrate_wx<8, 2>); break;
+        case 60: wx(k_integrate_wx<7, 4>); break;  // the default + a workgroup barrier per frame
+        case 61: wx(k_integrate_wx<6, 4>); break;
+        case 62: *fixup = true; wx(k_integrate_wx<8, 6>); break;
         default: set_error("integrate variant " + std::to_string(var) + " unknown"); return 2;
     }
     return 0;
@@ -591,7 +594,7 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
     //     the eight record loads issued first (>= 7 / 5 waves), 49 / 50 = 45 / 47 branch-free.  (24 of round 4, a ballot skip of
     //     out-of-image wave slots, ran 0.70 vs 0.48 ms per launch: removed.)
     int var = v->kernel_variant;
-    if (var < 0 || var > 59) var = 0;
+    if (var < 0 || var > 62) var = 0;
     if (!MQR_AB && var != 1 && var != 2 && var != 4) var = 0;
     if (var != 1 && var != 2 && !lean_ok) var = 2;
     if (var == 5 && (v->R != 16 || W % 4 != 0 || W < 4 || (reinterpret_cast<uintptr_t>(depths) & 15))) var = 0;

@@ -1423,7 +1423,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
 // workgroups per CU -- 6 waves per SIMD -- whether the budget allows 6 or 7.  MODE bit 0: the frame's 8 voxels
 // in two halves (gather 0-3, update 0-3, gather 4-7, update 4-7: half the window reads in flight, half the
 // registers for them); bit 1: no in-kernel exact path (a block outside the proven ranges is handed to the exact
-// fix-up launch, hand_off, like k_integrate_lean) -- no call, so no registers saved across one.
+// fix-up launch, hand_off, like k_integrate_lean) -- no call, so no registers saved across one; bit 2: a
+// workgroup barrier after every frame.
 template <int WPE, int MODE>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void k_integrate_wx(
     const int32_t* __restrict__ list, const bmask_t* __restrict__ lmask, int32_t* __restrict__ bad_out,
@@ -1481,6 +1482,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
                     lean_gather_w<ZPER, 2, 8>(dv, bad, fps[f], rs, xs, ys, zs, W4, bytes, hb, wb);
                     lean_update_v<ZPER, 2, 0>(tw, dv, fps[f], xs, ys, zs, depth_max, sdf_trunc, y1t);
                 }
+                // MODE bit 2: the workgroup's 8 waves kept in step frame by frame (they read the same image
+                // region of the same frame, so the L1 can serve one wave's windows to the next)
+                if constexpr ((MODE & 4) != 0) __syncthreads();
             }
             if (__syncthreads_or(bad)) {
                 if constexpr ((MODE & 2) != 0) {
