@@ -1530,6 +1530,9 @@ def main():
                                       block_count=args.block_count, device=local)
 
     def merge():
+        # (the integrate returns with its last launch queued and the merge waits for it anyway: waiting
+        # here first keeps that wait out of merge_ms)
+        torch.cuda.synchronize()
         t = time.perf_counter()
         if comm is not None:
             shard["out"], shard["owned"] = merge_rccl(vbg, comm, mode=args.merge, out=shard["out"])
