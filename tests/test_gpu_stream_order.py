@@ -256,3 +256,18 @@ def test_synchronous_return_variant_is_identical():
         out.append(vbg.export())
     from gpu_helpers import compare_volumes
     assert compare_volumes(out[0], out[1], 0.0) == 0.0  # (block order is the touch's arrival order)
+
+
+def test_device_buffer_freed_right_after_integrate_frames():
+    """A library-allocated frame buffer (mqr_device_alloc) freed the moment integrate_frames returns:
+    mqr_device_free waits for the device, so the in-flight integrate still reads the frames."""
+    from gpu_helpers import compare_volumes
+    from mqr._lib import DeviceBuffer
+    from mqr.vbg import VoxelBlockGrid
+    depth, K, T = _room(200, seed=14)
+    B, H, W = depth.shape
+    buf = DeviceBuffer.from_array(depth)
+    vbg = VoxelBlockGrid(voxel_size=0.01, block_resolution=16, block_count=256, device="cuda:0")
+    vbg.integrate_frames((buf, B, H, W), K, T, depth_scale=1.0, depth_max=4.0, trunc_voxel_multiplier=10.0)
+    buf.free()
+    assert compare_volumes(vbg.export(), _oracle(depth, K, T).export(), 0.0) == 0.0
