@@ -1530,9 +1530,9 @@ def main():
                                       block_count=args.block_count, device=local)
 
     def merge():
-        # (the integrate returns with its last launch queued and the merge waits for it anyway: waiting
-        # here first keeps that wait out of merge_ms)
-        torch.cuda.synchronize()
+        # (integrate_frames returns with its last launch queued; the merge's all-gathers and plan overlap
+        # it and only its send gather waits for it -- so this wall time includes that wait, and
+        # merge_phases_ms is the merge's own device time)
         t = time.perf_counter()
         if comm is not None:
             shard["out"], shard["owned"] = merge_rccl(vbg, comm, mode=args.merge, out=shard["out"])
@@ -1796,6 +1796,9 @@ def main():
                                                                  if world > 1 else "")},
             "sharded_extract": sharded,
             "merge_ms": merge_ms,
+            "merge_ms_note": ("wall time of the merge call per step; it overlaps the rank's last integrate launch "
+                              "(all-gathers and plan) and waits for it before the send gather, so it includes that "
+                              "wait; merge_phases_ms are the merge's own device phases") if world > 1 else None,
             "merge_phases_ms": merge_phases_ms,
             "merge_transport": transport,
             "merge_bytes_per_rank": merge_bytes,

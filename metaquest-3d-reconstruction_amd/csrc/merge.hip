@@ -138,6 +138,7 @@ struct mqr_comm {
     // phase timing of the last merge (mqr_comm_timing): start, plan done, gathered, exchanged, merged
     hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
     float last_ms[4] = {0.f, 0.f, 0.f, 0.f};
+    hipEvent_t order = nullptr;  // the local volume's touch stream, waited for on `s` (no host wait)
 };
 
 namespace mqr {
@@ -611,6 +612,16 @@ struct Exchange {
     size_t seg_bytes(size_t blocks) const { return blocks * block_bytes(); }
 };
 
+// `st` waits (on the device) for the integrates still in flight on a volume: integrate_frames on device
+// frames returns with its last integrate queued, and the merge overlaps its all-gathers, plan and output
+// activation with it -- only the send gather, the first reader of the pool, waits.  (After a sync_all,
+// as in mqr_merge_local and mqr_xchg_create, nothing is pending and this enqueues nothing.)
+static int order_after_volume_integrates(mqr_vbg* v, hipStream_t st) {
+    for (int p = 0; p < 2; ++p)
+        if (v->int_pending[p]) MQR_CHECK_HIP(hipStreamWaitEvent(st, v->int_done[p], 0));
+    return 0;
+}
+
 // Plan (identical on every rank) from the gathered keys dkeys[W * mx] (device), output volume,
 // send segments gathered from `local`, and the self segment copied into the receive buffer.
 // ev_plan / ev_gathered (nullable) are recorded after the plan and after the gather.
@@ -638,6 +649,7 @@ static int xchg_prepare(Exchange& x, hipStream_t st, const uint64_t* dkeys, int 
     if (grow(&x.sendbuf, &x.send_cap, std::max<size_t>(ns, 1) * eb) ||
         grow(&x.recvbuf, &x.recv_cap, std::max<size_t>(nr, 1) * eb))
         return 1;
+    if (order_after_volume_integrates(local, st)) return 1;
     if (ns) {
         if (x.pk)
             hipLaunchKernelGGL(k_gather_blocks<1>, dim3((unsigned)ns), dim3(256), 0, st, x.pv.send_idx, (int64_t)ns,
@@ -792,6 +804,7 @@ int mqr_comm_destroy(mqr_comm* c) {
     if (c->small) (void)hipFree(c->small);
     for (hipEvent_t e : c->ev)
         if (e) (void)hipEventDestroy(e);
+    if (c->order) (void)hipEventDestroy(c->order);
     if (c->s) (void)hipStreamDestroy(c->s);
     delete c;
     return 0;
@@ -831,7 +844,13 @@ int mqr_reduce_rccl(mqr_vbg* local, mqr_comm* c, int mode, int root, mqr_vbg* ou
     int64_t mine[2] = {0, 0};
     std::vector<int64_t> cnt(2 * W);
     StreamDrain drain{c->s};
-    if (sync_all(local)) return 1;  // the local volume's integration is complete
+    // The local volume's block set is final once its integrate_frames returned (the host read every
+    // batch's touch counters), but its last integrate may still be running: `s` waits here for the
+    // volume's touch stream only (keys, and anything else enqueued there, e.g. a reset), and for the
+    // integrates just before the send gather (xchg_prepare), so the exchange's first half overlaps them.
+    if (!c->order) MQR_CHECK_HIP(hipEventCreateWithFlags(&c->order, hipEventDisableTiming | hipEventDisableSystemFence));
+    MQR_CHECK_HIP(hipEventRecord(c->order, local->stream));
+    MQR_CHECK_HIP(hipStreamWaitEvent(c->s, c->order, 0));
     mine[0] = local->pool_count;
     mine[1] = local->wbound;
     const int64_t n_me = mine[0];

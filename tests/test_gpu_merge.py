@@ -374,3 +374,33 @@ def test_xchg_create_checks_the_callers_key_row(seq):
     assert create(mine[:-1]) == 4                                   # a key missing (padding in its place)
     assert create(np.concatenate([mine, other[:1]])) == 4          # a foreign key in the padding
     assert "not this rank's" in _lib.load().mqr_last_error().decode()
+
+
+def test_rccl_merge_right_after_device_frame_integrate(seq):
+    """integrate_frames on device frames returns with its last integrate running; mqr_reduce_rccl issued at
+    once overlaps its all-gathers and plan with it and waits only before the send gather: the merged volume
+    (world size 1: the volume itself) is the oracle's."""
+    import ctypes
+    import torch
+    from mqr.distributed import RcclComm, merge_rccl
+    from mqr.vbg import VoxelBlockGrid
+
+    class _Dev:
+        def __init__(self, t):
+            self.ptr = ctypes.c_void_p(t.data_ptr())
+
+    d = torch.from_numpy(np.ascontiguousarray(seq["depth"], np.float32)).cuda()
+    torch.cuda.synchronize()
+    B, H, W = d.shape
+    comm = RcclComm(0, 0, 1, RcclComm.unique_id())
+    try:
+        vol = VoxelBlockGrid(voxel_size=0.01, block_resolution=16, block_count=64)
+        out = None
+        for _ in range(2):  # twice: the second merge follows a reset and re-integration of the same volume
+            vol.reset()
+            vol.integrate_frames((_Dev(d), B, H, W), seq["K"].astype(np.float64), seq["T_wc"].astype(np.float64),
+                                 depth_scale=1.0, depth_max=4.0, trunc_voxel_multiplier=10.0)
+            out, n = merge_rccl(vol, comm, mode="root", out=out)
+            assert compare_volumes(out.export(), _oracle(seq).export(), 0.0) == 0.0
+    finally:
+        comm.close()

@@ -98,6 +98,9 @@ for step in ${STEPS:-tests}; do
       python tools/step_head.py "$(find gpurun_out/sh -name '*kernel_trace.csv' | head -1)" --steps 30 > gpurun_out/${TAG}_shard_head.json
       rm -rf gpurun_out/sh
       cat gpurun_out/${TAG}_shard_steps.json gpurun_out/${TAG}_shard_head.json ;;
+    shardmerge)
+      timeout -k 10 300 python tools/shard_steps.py --merge --steps 30 > gpurun_out/${TAG}_shard_merge.json 2> gpurun_out/${TAG}_shard_merge.err || { tail -20 gpurun_out/${TAG}_shard_merge.err; exit 1; }
+      cat gpurun_out/${TAG}_shard_merge.json ;;
     shardall)
       timeout -k 10 300 python tools/shard_steps.py --all --steps 40 > gpurun_out/${TAG}_shard_all.json 2> gpurun_out/${TAG}_shard_all.err || { tail -20 gpurun_out/${TAG}_shard_all.err; exit 1; }
       grep "W=" gpurun_out/${TAG}_shard_all.err ;;

@@ -24,6 +24,9 @@ def main():
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--frames-per-side", type=int, default=1000)
     ap.add_argument("--all", action="store_true")
+    ap.add_argument("--merge", action="store_true",
+                    help="each pass also merges the shard through RCCL at world size 1 (root), alternating "
+                         "rounds with a synchronize before the merge (no overlap with the integrate's last launch)")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -59,6 +62,40 @@ def main():
         print(json.dumps({"workload": "C4 capture, bench.py's contiguous split; per rank K passes of reset + "
                           "integrate_frames back to back (the bench's timed loop, asynchronous return)",
                           "steps": a.steps, "per_world": res}), flush=True)
+        return
+    if a.merge:
+        import torch.distributed as dist
+        from mqr.distributed import make_comm, merge_rccl
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29543")
+        dist.init_process_group("gloo", rank=0, world_size=1)
+        comm = make_comm(0)
+        lo, hi = shard_range(2 * a.frames_per_side, a.rank, a.world)
+        dd = full["depth_t"][lo:hi].contiguous()
+        KK, TT = full["K"][lo:hi].astype(np.float64), full["T_wc"][lo:hi].astype(np.float64)
+        v = VoxelBlockGrid(voxel_size=args.voxel, block_resolution=16, block_count=args.block_count, device=0)
+        kw = dict(depth_scale=1.0, depth_max=args.depth_max, trunc_voxel_multiplier=args.trunc)
+        ar = (bench._DevPtr(dd.data_ptr()), *dd.shape)
+        out = None
+        res = {"overlap": [], "sync_first": []}
+        for rnd in range(8):
+            for mode in ("overlap", "sync_first"):
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for _ in range(a.steps):
+                    v.reset()
+                    v.integrate_frames(ar, KK, TT, **kw)
+                    if mode == "sync_first":
+                        torch.cuda.synchronize()
+                    out, _ = merge_rccl(v, comm, mode="root", out=out)
+                torch.cuda.synchronize()
+                if rnd:
+                    res[mode].append((time.perf_counter() - t0) / a.steps * 1e3)
+        comm.close()
+        dist.destroy_process_group()
+        print(json.dumps({"workload": f"C4 shard {a.rank} of {a.world} ({hi - lo} frames): reset + integrate_frames + "
+                          "merge_rccl (world size 1, root) per pass", "ms_per_pass_median":
+                          {k: float(np.median(x)) for k, x in res.items()}, "ms_per_pass": res}), flush=True)
         return
     lo, hi = shard_range(2 * a.frames_per_side, a.rank, a.world)
     d = full["depth_t"][lo:hi].contiguous()
