@@ -18,6 +18,7 @@
 #   xtrace      kernel trace of 30 extractions: wall vs device span vs gaps -> gpurun_out/${TAG}_extract_timeline.json
 #   traffic     FETCH_SIZE / WRITE_SIZE passes (tools/pmc_traffic.sh) -> profiles/${TAG}_pmc_traffic.json
 #   pmcint      SQ / TA / TCP counters of the default integrate kernel (tools/pmc_ab.sh) -> profiles_new/
+#   pmcconf     counter passes of the confidence kernel (tools/pmc_conf.sh) -> profiles_new/${TAG}_pmc_confidence.json
 #   abint:V     tools/ab_integrate.py over integrate variants V (comma separated, A/B library)
 #   abext:M     tools/ab_extract.py over extraction modes M (A/B library)
 #   d2h         device -> host copy ceilings (tools/d2h_probe.py) with 1 / 4 / 8 staging threads
@@ -128,6 +129,11 @@ for step in ${STEPS:-tests}; do
       mkdir -p gpurun_out/profiles_new && cp gpurun_out/pmc_ab.json gpurun_out/profiles_new/${TAG}_pmc_integrate_counters.json
       rm -rf /tmp/pmcab
       head -c 600 gpurun_out/pmc_ab.json ;;
+    pmcconf)
+      timeout -k 10 600 bash tools/pmc_conf.sh > gpurun_out/${TAG}_pmc_conf.log 2>&1 || { tail -20 gpurun_out/${TAG}_pmc_conf.log; exit 1; }
+      mkdir -p gpurun_out/profiles_new && cp gpurun_out/pmc_conf.json gpurun_out/profiles_new/${TAG}_pmc_confidence.json
+      rm -rf /tmp/pmcconf
+      head -c 400 gpurun_out/pmc_conf.json ;;
     abint:*)
       MQR_HIP_LIB="$PWD/tools/_ab/libmqr_ab.so" timeout -k 10 600 python -u tools/ab_integrate.py --check --rounds 7 --variants "${step#abint:}" \
         > gpurun_out/${TAG}_abint.json 2> gpurun_out/${TAG}_abint.err || { tail -20 gpurun_out/${TAG}_abint.err; exit 1; }
