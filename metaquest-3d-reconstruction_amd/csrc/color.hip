@@ -195,6 +195,9 @@ __global__ __launch_bounds__(256) void k_cm_vertices(const float* __restrict__ V
 // ---- knn over the sampled vertices: Morton-sorted buckets of kBucket points under an implicit
 // complete binary tree of bucket boxes (heap order, leaves at P + b); exact search in float64.
 constexpr int kBucket = 16;
+#ifndef MQR_KNN_WAVE
+#define MQR_KNN_WAVE 1  // k_cm_knn_fill_wave (1) or the per-lane traversal k_cm_knn_fill (0): A/B builds
+#endif
 
 __device__ inline uint32_t ordered_u32(float f) {
     const uint32_t u = __float_as_uint(f);
@@ -397,6 +400,100 @@ __global__ __launch_bounds__(256) void k_cm_knn_fill(const float* __restrict__ V
         for (int a = 0; a < 3; ++a) c[a] /= (double)nb;
 #pragma unroll
     for (int a = 0; a < 3; ++a) out[3 * (int64_t)qv + a] = (float)c[a];
+}
+
+// The same search with the traversal shared by a wave (MQR_KNN_WAVE): the wave's 64 queries -- neighbours in
+// vertex order, so close in space -- walk one stack of nodes together (node indices wave-uniform, read by
+// scalar loads), a node is skipped only when every lane's bound prunes it, and each lane keeps its own
+// exact best list.  A lane may so test nodes it would have pruned alone: that only offers it candidates
+// its own search would have rejected or met anyway, and the kept list is a total order on (d2, index), so
+// the result is the same.  Inactive lanes (past the query count) prune everything.
+template <int K>
+__global__ __launch_bounds__(256) void k_cm_knn_fill_wave(const float* __restrict__ V, const int32_t* __restrict__ qids,
+                                                          int64_t nq, const float4* __restrict__ pts, int64_t n,
+                                                          int64_t P, const float4* __restrict__ lo,
+                                                          const float4* __restrict__ hi,
+                                                          const double* __restrict__ avg, float* __restrict__ out) {
+    extern __shared__ int32_t stk_lds[];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    int32_t* stk = stk_lds + wave * 64;
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool active = t < nq;
+    const int32_t qv = active ? qids[t] : 0;
+    float qf[3] = {0.f, 0.f, 0.f};
+    if (active) {
+        qf[0] = V[3 * (int64_t)qv];
+        qf[1] = V[3 * (int64_t)qv + 1];
+        qf[2] = V[3 * (int64_t)qv + 2];
+    }
+    const double q[3] = {qf[0], qf[1], qf[2]};
+    double bd[K];
+    int32_t bi[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        bd[k] = active ? __builtin_inf() : -1.0;  // an inactive lane prunes every node
+        bi[k] = 0x7fffffff;
+    }
+    if (__ballot(active) == 0) return;  // (wave-uniform)
+    int sp = 0;
+    if (lane == 0) stk[0] = 1;
+    sp = 1;
+    while (sp) {
+        __builtin_amdgcn_wave_barrier();
+        const int32_t node = __builtin_amdgcn_readfirstlane(stk[--sp]);
+        const float4 nlo = lo[node], nhi = hi[node];
+        if (!__ballot((double)box_d2_lb(qf, nlo, nhi) <= bd[K - 1])) continue;
+        if (node >= P) {  // bucket
+            const int64_t b = node - P;
+            const int64_t e = min(n, (b + 1) * kBucket);
+            for (int64_t j = b * kBucket; j < e; ++j) {
+                const float4 pt = pts[j];
+                const float fx = qf[0] - pt.x, fy = qf[1] - pt.y, fz = qf[2] - pt.z;
+                if ((double)((fx * fx + fy * fy + fz * fz) * (1.0f - 0x1p-18f)) > bd[K - 1]) continue;
+                const int32_t v = __float_as_int(pt.w);
+                const double dx = q[0] - (double)pt.x, dy = q[1] - (double)pt.y, dz = q[2] - (double)pt.z;
+                const double d2 = dx * dx + dy * dy + dz * dz;
+                auto before = [&](int k) { return d2 < bd[k] || (d2 == bd[k] && v < bi[k]); };
+                if (!before(K - 1)) continue;
+#pragma unroll
+                for (int k = K - 1; k >= 0; --k) {
+                    if (k > 0 && before(k - 1)) {
+                        bd[k] = bd[k - 1];
+                        bi[k] = bi[k - 1];
+                    } else if (before(k)) {
+                        bd[k] = d2;
+                        bi[k] = v;
+                    }
+                }
+            }
+        } else {  // both children, the one nearer for most lanes popped first
+            const int32_t a = 2 * node, c = a + 1;
+            const float da = box_d2_lb(qf, lo[a], hi[a]), dc = box_d2_lb(qf, lo[c], hi[c]);
+            const uint64_t m = __ballot(active && da <= dc), act = __ballot(active);
+            const bool a_first = 2 * __popcll(m) >= __popcll(act);
+            __builtin_amdgcn_wave_barrier();
+            if (lane == 0) {
+                stk[sp] = a_first ? c : a;
+                stk[sp + 1] = a_first ? a : c;
+            }
+            sp += 2;
+        }
+    }
+    if (!active) return;
+    int nb = 0;
+    double cc[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+        if (bd[k] != __builtin_inf()) {
+            ++nb;
+#pragma unroll
+            for (int a = 0; a < 3; ++a) cc[a] += avg[3 * (int64_t)bi[k] + a];
+        }
+    if (nb > 0)
+#pragma unroll
+        for (int a = 0; a < 3; ++a) cc[a] /= (double)nb;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) out[3 * (int64_t)qv + a] = (float)cc[a];
 }
 
 __global__ void k_cm_out_seen(const double* __restrict__ avg, const int32_t* __restrict__ counts, int64_t nv,
@@ -629,20 +726,21 @@ int mqr_color_map(int device, const float* vertices, int64_t nv, int vloc, const
                 const dim3 gq((unsigned)((nunseen + 255) / 256));
                 int depth = 0;  // levels below the root of the P-leaf tree
                 while ((int64_t{1} << depth) < P) ++depth;
-                const size_t lds = sizeof(int32_t) * 256 * (size_t)(depth + 2);
+                const bool wave = MQR_KNN_WAVE && depth + 2 <= 64;  // (the wave stack holds 64 entries)
+                const size_t lds = wave ? sizeof(int32_t) * 4 * 64 : sizeof(int32_t) * 256 * (size_t)(depth + 2);
                 auto fill = [&](auto kern) {
                     hipLaunchKernelGGL(kern, gq, dim3(256), lds, s, dV, ids + nv, nunseen, pts, nseen, P, blo, bhi,
                                        avg, dO);
                 };
                 switch (knn) {  // knn in [1, 8] (checked on entry)
-                    case 1: fill(k_cm_knn_fill<1>); break;
-                    case 2: fill(k_cm_knn_fill<2>); break;
-                    case 3: fill(k_cm_knn_fill<3>); break;
-                    case 4: fill(k_cm_knn_fill<4>); break;
-                    case 5: fill(k_cm_knn_fill<5>); break;
-                    case 6: fill(k_cm_knn_fill<6>); break;
-                    case 7: fill(k_cm_knn_fill<7>); break;
-                    default: fill(k_cm_knn_fill<8>); break;
+                    case 1: wave ? fill(k_cm_knn_fill_wave<1>) : fill(k_cm_knn_fill<1>); break;
+                    case 2: wave ? fill(k_cm_knn_fill_wave<2>) : fill(k_cm_knn_fill<2>); break;
+                    case 3: wave ? fill(k_cm_knn_fill_wave<3>) : fill(k_cm_knn_fill<3>); break;
+                    case 4: wave ? fill(k_cm_knn_fill_wave<4>) : fill(k_cm_knn_fill<4>); break;
+                    case 5: wave ? fill(k_cm_knn_fill_wave<5>) : fill(k_cm_knn_fill<5>); break;
+                    case 6: wave ? fill(k_cm_knn_fill_wave<6>) : fill(k_cm_knn_fill<6>); break;
+                    case 7: wave ? fill(k_cm_knn_fill_wave<7>) : fill(k_cm_knn_fill<7>); break;
+                    default: wave ? fill(k_cm_knn_fill_wave<8>) : fill(k_cm_knn_fill<8>); break;
                 }
             }
         }
