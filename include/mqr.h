@@ -47,9 +47,12 @@ int mqr_version(void);
 /* Build tags: which 0 = a hash of the integrate sources (vbg.hip, vbg_kernels.hpp, mqr_common.hpp),
  * 1 = of the confidence sources, as compiled into this library; counter records under profiles/ carry
  * the tag of the build they measured (bench.py quotes only matching ones).  mqr_vbg_last_kernel: the
- * integrate variant (mqr_vbg_set_variant numbering) the volume's last launch actually used. */
+ * integrate variant (mqr_vbg_set_variant numbering) the volume's last launch actually used.
+ * mqr_vbg_flips: how many mqr_vbg_reset calls swapped in the volume's second table / pool set instead of
+ * waiting for an integrate still in flight (see mqr_vbg_reset). */
 int mqr_build_tag(int which, char* buf, int cap);
 int mqr_vbg_last_kernel(mqr_vbg* v, int* variant);
+int mqr_vbg_flips(mqr_vbg* v, int64_t* n);
 const char* mqr_last_error(void);
 int mqr_device_count(int* n);
 /* The calling thread's caller stream (a hipStream_t; NULL = the null stream, the default): see
@@ -76,7 +79,11 @@ int mqr_device_mem_info(int device, int64_t* free_bytes, int64_t* total_bytes);
  * block_count is the initial capacity; the volume grows automatically like Open3D's hash map. */
 int mqr_vbg_create(float voxel_size, int block_resolution, int64_t block_count, int device, mqr_vbg** out);
 int mqr_vbg_destroy(mqr_vbg* v);
-/* Empty the volume in place (keeps its allocations): the state of a freshly created grid. */
+/* Empty the volume in place (keeps its allocations): the state of a freshly created grid.  Ordered on the
+ * device: when an integrate of an asynchronously returning mqr_integrate_frames is still in flight, the
+ * volume swaps in a second hash table / block pool set (allocated once, at the current capacities, while the
+ * volume's pool is within 2 GiB and a quarter of the device's HBM stays free) and clears that one, so the
+ * next call's first touch overlaps the unfinished integrate; otherwise the clear queues behind it. */
 int mqr_vbg_reset(mqr_vbg* v);
 int mqr_vbg_size(mqr_vbg* v, int64_t* n_blocks);
 int mqr_vbg_capacity(mqr_vbg* v, int64_t* block_capacity);
@@ -321,7 +328,9 @@ int mqr_vbg_profile(mqr_vbg* v, int enable);
  * the full-table undo-and-retry path; test hook), bit 13 sizes the table for the worst case, bit 14 makes
  * every integrate launch wait on a touch-stream event, bit 15 runs the batch in spatial per-XCD groups
  * (k_xcd_order; A/Bs), bit 16 gives the touch one stride-4 pixel per thread instead of two, bit 18 turns
- * off the speculative first-batch integrate (k_gate; A/B).
+ * off the speculative first-batch integrate (k_gate; A/B), bit 24 makes mqr_integrate_frames on device frames
+ * drain its streams before returning (A/B), bit 25 makes mqr_vbg_reset wait for an integrate in flight
+ * instead of swapping in the second table / pool set (A/B).
  * mqr_check_division: exhaustive bit-pattern check of the division shortcuts used on device against
  * IEEE division (which=0: 1/b via rcp_rn, 1: a/b via div_rn, 2: a/b via the bare core, 3: 1/b via
  * rcp_nm, 4: 1/b via rcp_m, over float bit patterns [lo_bits, lo_bits+count) as b or a); returns

@@ -171,6 +171,25 @@ struct mqr_vbg {
     int64_t wbound = 0;
     int64_t batch_new_max = 0; // most blocks one integrate batch has allocated (sizes the table headroom)
 
+    // Second table / pool set.  mqr_vbg_reset while an integrate is still in flight swaps the sets instead of
+    // ordering the clear behind that integrate: the next call's touch then overlaps the previous call's last
+    // integrate.  set_ev marks, on stream2, the last integrate that used a set while it was
+    // current; a set swapped back in is cleared behind it.  Kept only for volumes within kAltMaxBytes and
+    // while the device keeps a quarter of its HBM free; variant bit 25 turns the swap off.
+    struct VolSet {
+        mqr::Table tab{};
+        mqr::bmask_t* mask1 = nullptr;
+        float2* pool = nullptr;
+        uint64_t* bkeys = nullptr;
+        int64_t pool_cap = 0;
+        hipEvent_t ev = nullptr;
+        bool ev_live = false;
+    } alt;
+    hipEvent_t set_ev = nullptr;  // the current set's event (swapped with alt.ev)
+    bool set_ev_live = false;
+    bool flip_reset = true;
+    int64_t flips = 0;  // resets that swapped the sets (mqr_vbg_flips)
+
     int32_t* lists[2] = {nullptr, nullptr};  // batch slot lists, capacity list_cap each
     int32_t* lpt[2] = {nullptr, nullptr};    // the same lists reordered (k_lpt_order / k_xcd_order): slots,
                                              // then their masks, then a group byte per entry (scratch)

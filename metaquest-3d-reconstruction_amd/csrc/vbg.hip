@@ -1001,6 +1001,8 @@ int mqr_vbg_create(float voxel_size, int block_resolution, int64_t block_count, 
     return 0;
 }
 
+static void free_alt(mqr_vbg* v);  // (the second table / pool set, below mqr_vbg_reset's helpers)
+
 int mqr_vbg_destroy(mqr_vbg* v) {
     if (!v) return 0;
     (void)hipSetDevice(v->device);
@@ -1009,6 +1011,9 @@ int mqr_vbg_destroy(mqr_vbg* v) {
     drain_events(v);
     free_table(v->tab);
     free_table(v->ftab);
+    free_alt(v);
+    for (hipEvent_t e : {v->set_ev, v->alt.ev})
+        if (e) (void)hipEventDestroy(e);
     if (v->mask1) (void)hipFree(v->mask1);
     if (v->pool) (void)hipFree(v->pool);
     if (v->bkeys) (void)hipFree(v->bkeys);
@@ -1033,22 +1038,127 @@ int mqr_vbg_destroy(mqr_vbg* v) {
     return 0;
 }
 
+// ---- the second table / pool set (mqr_vbg_reset behind an unfinished integrate) ----
+constexpr int64_t kAltMaxBytes = int64_t{2} << 30;  // volumes whose pool is larger wait instead
+
+static void swap_sets(mqr_vbg* v) {
+    std::swap(v->tab, v->alt.tab);
+    std::swap(v->mask1, v->alt.mask1);
+    std::swap(v->pool, v->alt.pool);
+    std::swap(v->bkeys, v->alt.bkeys);
+    std::swap(v->pool_cap, v->alt.pool_cap);
+    std::swap(v->set_ev, v->alt.ev);
+    std::swap(v->set_ev_live, v->alt.ev_live);
+}
+
+static void free_alt(mqr_vbg* v) {
+    free_table(v->alt.tab);
+    if (v->alt.mask1) (void)hipFree(v->alt.mask1);
+    if (v->alt.pool) (void)hipFree(v->alt.pool);
+    if (v->alt.bkeys) (void)hipFree(v->alt.bkeys);
+    v->alt.mask1 = nullptr;
+    v->alt.pool = nullptr;
+    v->alt.bkeys = nullptr;
+    v->alt.pool_cap = 0;
+}
+
+// The second set at the current set's capacities (fresh allocations: a reset discards contents).  *ok is
+// false when the budget does not allow it -- the reset then waits as before.
+static int ensure_alt(mqr_vbg* v, bool* ok) {
+    *ok = false;
+    const bool pool_fits = v->alt.pool && v->alt.pool_cap >= v->pool_cap;
+    const bool tab_fits = v->alt.tab.keys && v->alt.tab.cap >= v->tab.cap;
+    if (pool_fits && tab_fits) {
+        *ok = true;
+        return 0;
+    }
+    const int64_t pool_bytes = (int64_t)sizeof(float2) * v->pool_cap * v->R3 + (int64_t)sizeof(uint64_t) * v->pool_cap;
+    const int64_t tab_bytes = (int64_t)(sizeof(uint64_t) + sizeof(int32_t) + 2 * sizeof(bmask_t)) * v->tab.cap;
+    if (pool_bytes > kAltMaxBytes) return 0;
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    const int64_t need = (pool_fits ? 0 : pool_bytes) + (tab_fits ? 0 : tab_bytes);
+    if ((int64_t)free_b - need < (int64_t)(total_b / 4)) return 0;
+    // the set's last readers (an integrate before its event) are done before its memory is replaced
+    if (v->alt.ev_live) MQR_CHECK_HIP(hipEventSynchronize(v->alt.ev));
+    if (!v->alt.ev) MQR_CHECK_HIP(hipEventCreateWithFlags(&v->alt.ev, hipEventDisableTiming | hipEventDisableSystemFence));
+    if (!v->set_ev) MQR_CHECK_HIP(hipEventCreateWithFlags(&v->set_ev, hipEventDisableTiming | hipEventDisableSystemFence));
+    v->alt.ev_live = false;
+    bool fail = false;
+    if (!pool_fits) {
+        if (v->alt.pool) (void)hipFree(v->alt.pool);
+        if (v->alt.bkeys) (void)hipFree(v->alt.bkeys);
+        v->alt.pool = nullptr;
+        v->alt.bkeys = nullptr;
+        v->alt.pool_cap = 0;
+        fail = hipMalloc(&v->alt.pool, sizeof(float2) * v->pool_cap * v->R3) != hipSuccess ||
+               hipMalloc(&v->alt.bkeys, sizeof(uint64_t) * v->pool_cap) != hipSuccess;
+        if (!fail) v->alt.pool_cap = v->pool_cap;
+    }
+    if (!fail && !tab_fits) {
+        free_table(v->alt.tab);
+        if (v->alt.mask1) (void)hipFree(v->alt.mask1);
+        v->alt.mask1 = nullptr;
+        Table nt{};
+        fail = hipMalloc(&nt.keys, sizeof(uint64_t) * v->tab.cap) != hipSuccess ||
+               hipMalloc(&nt.vals, sizeof(int32_t) * v->tab.cap) != hipSuccess ||
+               hipMalloc(&nt.mask, sizeof(bmask_t) * v->tab.cap) != hipSuccess ||
+               hipMalloc(&v->alt.mask1, sizeof(bmask_t) * v->tab.cap) != hipSuccess;
+        nt.cap = v->tab.cap;
+        v->alt.tab = nt;  // (freed by free_alt on failure; k_reset_table clears it when swapped in)
+    }
+    if (fail) {
+        (void)hipGetLastError();
+        free_alt(v);
+        return 0;
+    }
+    *ok = true;
+    return 0;
+}
+
 int mqr_vbg_reset(mqr_vbg* v) {
     MQR_REQUIRE(v, "null volume");
     MQR_CHECK_HIP(hipSetDevice(v->device));
-    // behind an integrate still in flight (mqr_integrate_frames on device frames returns before it ends):
-    // a device-side wait on `stream`, no host wait
-    if (order_after_integrate(v)) return 1;
+    uint32_t segs = 0x1f;  // every counter segment (k_reset_table)
+    const bool inflight = v->pipelined && (v->int_pending[0] || v->int_pending[1]);
+    bool flip = false;
+    if (inflight && v->flip_reset && ensure_alt(v, &flip)) return 1;
+    if (flip) {
+        // an integrate of the current set is still in flight (mqr_integrate_frames on device frames returns
+        // before it ends): mark the set's last reader on the integrate stream and swap in the other set,
+        // cleared behind the integrate that last read it -- the next touch need not wait for this one
+        MQR_CHECK_HIP(hipEventRecord(v->set_ev, v->stream2));
+        v->set_ev_live = true;
+        swap_sets(v);
+        if (v->set_ev_live) MQR_CHECK_HIP(hipStreamWaitEvent(v->stream, v->set_ev, 0));
+        // the in-flight parity's counters (and shadows) are still read: cleared by reset_batch_counters,
+        // after wait_parity_free, when that parity is next used
+        for (int p = 0; p < 2; ++p)
+            if (v->int_pending[p]) segs &= ~((1u << p) | (1u << (3 + p)));
+        ++v->flips;
+    } else {
+        // behind an integrate still in flight: a device-side wait on `stream`, no host wait
+        if (order_after_integrate(v)) return 1;
+    }
     // one launch, ordered on `stream` before anything that uses the volume next; the pool is not
     // cleared: a block starts at (0, 0) in the batch that allocates it (launch_integrate first_new)
-    const int nctr = kCounterInts;
-    const int64_t cells = std::max<int64_t>(v->tab.cap, nctr);
+    const int64_t cells = std::max<int64_t>(v->tab.cap, kCounterInts);
     hipLaunchKernelGGL(k_reset_table, dim3((unsigned)((cells + 255) / 256)), dim3(256), 0, v->stream, v->tab, v->mask1,
-                       v->counters, nctr);
+                       v->counters, segs);
     MQR_CHECK_HIP(hipGetLastError());
     v->pool_count = 0;
     v->wbound = 0;
-    v->ctr_clean[0] = v->ctr_clean[1] = true;
+    v->ctr_clean[0] = (segs & 1u) != 0;
+    v->ctr_clean[1] = (segs & 2u) != 0;
+    return 0;
+}
+
+int mqr_vbg_flips(mqr_vbg* v, int64_t* n) {
+    MQR_REQUIRE(v && n, "null argument");
+    *n = v->flips;
     return 0;
 }
 
@@ -1421,6 +1531,7 @@ int mqr_vbg_set_variant(mqr_vbg* v, int variant) {
     v->touch_ppt = (variant & 0x10000) ? 1 : 2;  // bit 16: one stride-4 pixel per touch thread (A/B)
     v->spec_head = (variant & 0x40000) == 0;     // bit 18: no speculative first-batch integrate (A/B)
     v->async_return = (variant & 0x1000000) == 0; // bit 24: integrate_frames drains its streams before returning (A/B)
+    v->flip_reset = (variant & 0x2000000) == 0;   // bit 25: reset waits for an in-flight integrate (no set swap, A/B)
     // (the extraction configuration is set by mqr_vbg_set_extract_mode alone, A/B library only)
     return 0;
 }

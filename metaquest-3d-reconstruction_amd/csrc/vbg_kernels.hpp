@@ -1055,8 +1055,10 @@ __global__ void k_gate(const int* __restrict__ ctr, int* __restrict__ shadow, in
     gate_counters(ctr, shadow, __ballot(empty) != 0 || ctr[kOverflow] != 0);
 }
 
-// Empty table: keys empty, values -1, both parities' slot masks 0; and `nctr` counters 0.
-__global__ void k_reset_table(Table t, bmask_t* mask1, int* counters, int nctr) {
+// Empty table: keys empty, values -1, both parities' slot masks 0; and the counter segments `segs` selects
+// zeroed (bit 0 / 1: parity 0 / 1, bit 2: the pool counter and its spare ints, bit 3 / 4: the parities'
+// shadow sets -- a reset that swapped the volume's sets leaves an in-flight integrate's parity alone).
+__global__ void k_reset_table(Table t, bmask_t* mask1, int* counters, uint32_t segs) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < t.cap) {
         t.keys[i] = kEmpty;
@@ -1064,7 +1066,11 @@ __global__ void k_reset_table(Table t, bmask_t* mask1, int* counters, int nctr) 
         t.mask[i] = 0;
         mask1[i] = 0;
     }
-    if (i < nctr) counters[i] = 0;
+    if (i < kCounterInts) {
+        const int seg = i < kCountersTotal ? 0 : i < 2 * kCountersTotal ? 1 : i < 2 * kCountersTotal + 8 ? 2
+                      : i < 3 * kCountersTotal + 8 ? 3 : 4;
+        if ((segs >> seg) & 1u) counters[i] = 0;
+    }
 }
 
 __global__ void k_fixup_alloc(Table t, int* counters, int* pool_ctr, int64_t pool_cap, uint64_t* bkeys) {

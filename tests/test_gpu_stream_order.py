@@ -271,3 +271,58 @@ def test_device_buffer_freed_right_after_integrate_frames():
     vbg.integrate_frames((buf, B, H, W), K, T, depth_scale=1.0, depth_max=4.0, trunc_voxel_multiplier=10.0)
     buf.free()
     assert compare_volumes(vbg.export(), _oracle(depth, K, T).export(), 0.0) == 0.0
+
+
+def _flips(vbg):
+    from mqr import _lib
+    n = ctypes.c_int64(-1)
+    _lib.call("mqr_vbg_flips", vbg.handle, ctypes.byref(n))
+    return n.value
+
+
+@pytest.mark.parametrize("variant", [0, 0x2000000])
+def test_reset_behind_an_unfinished_integrate_swaps_sets(variant):
+    """reset while an integrate is in flight swaps in the volume's second table / pool set instead of waiting
+    (variant 0; bit 25 waits).  The calls alternate a long and a short sequence with no synchronize, so each
+    reset finds the previous call's last integrate running: a set swapped back in must be cleared only after
+    the integrate that last read it (the long one, two calls earlier), and the second set -- allocated at the
+    capacities of the first, which grows in the first call -- must be replaced when the first grows past it.
+    Every volume and mesh is the oracle's, the capacity is kept across the swaps, and the swap count says
+    which path ran."""
+    import torch
+    from gpu_helpers import compare_volumes
+    from mqr.vbg import VoxelBlockGrid
+    from mqr import _lib
+    d1, K1, T1 = _room(254, seed=21)
+    d2, K2, T2 = _room(90, seed=22)
+    B1, H, W = d1.shape
+    t1, t2 = torch.from_numpy(d1).cuda(), torch.from_numpy(d2).cuda()
+    torch.cuda.synchronize()
+    kw = dict(depth_scale=1.0, depth_max=4.0, trunc_voxel_multiplier=10.0)
+    a = (_Dev(t1), B1, H, W), K1, T1
+    b = (_Dev(t2), len(d2), H, W), K2, T2
+    vbg = VoxelBlockGrid(voxel_size=0.01, block_resolution=16, block_count=64, device="cuda:0")
+    _lib.call("mqr_vbg_set_variant", vbg.handle, variant)
+    for frames, K, T in (a, b, a, b, a):  # resets 2-5 each behind the previous call's unfinished integrate
+        vbg.reset()
+        vbg.integrate_frames(frames, K, T, **kw)
+    ref1, ref2 = _oracle(d1, K1, T1), _oracle(d2, K2, T2)
+    mesh = vbg.extract_triangle_mesh(weight_threshold=1.5)
+    assert compare_volumes(vbg.export(), ref1.export(), 0.0) == 0.0
+    assert mesh.triangles.shape[0] == ref1.extract_mesh(1.5)[2].shape[0]
+    cap = vbg.capacity()
+    assert cap >= vbg.size()
+    vbg.integrate_frames(*b, **kw)  # onto the first sequence (the mask / counter state after the swaps)
+    assert compare_volumes(vbg.export(), _oracle(d2, K2, T2, ref=_oracle(d1, K1, T1)).export(), 0.0) == 0.0
+    vbg.reset()  # nothing in flight (export drained): an in-place clear
+    vbg.integrate_frames(*b, **kw)
+    vbg.reset()
+    vbg.integrate_frames(*a, **kw)
+    assert compare_volumes(vbg.export(), ref1.export(), 0.0) == 0.0
+    assert vbg.capacity() >= cap
+    flips = _flips(vbg)
+    if variant:
+        assert flips == 0
+    else:
+        assert flips == 5, flips  # 4 in the loop + the one behind the short call
+    del ref2
