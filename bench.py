@@ -77,6 +77,9 @@ def parse(argv=None):
                     help="N > 1 (C4 headline): timed steps of the weak C2-per-rank sub-leg (0: skip)")
     ap.add_argument("--strong-frames", type=int, default=1000, help="frames per side in --strong mode")
     ap.add_argument("--no-c5", action="store_true", help="skip the 1-GPU C5 leg (4000 frames @ 3 mm + colour)")
+    ap.add_argument("--no-resident", action="store_true",
+                    help="pass the timed step's frames as MQR_DEVICE (the caller stream waits for each pass's last "
+                         "integrate) instead of MQR_DEVICE_RESIDENT (A/B)")
     ap.add_argument("--no-c4", action="store_true", help="skip the 1-GPU C4 leg (1000 + 1000 frames chained)")
     ap.add_argument("--touch-steps", type=int, default=20, help="profiled steps for touch_ms_per_launch (0: skip)")
     ap.add_argument("--c5-only", action="store_true",
@@ -1544,10 +1547,15 @@ def main():
         if comm is not None:
             shard.update(comm.counts())
 
+    # The frames are generated once and never written again: MQR_DEVICE_RESIDENT (include/mqr.h), so a pass's
+    # first touch can run beside the previous pass's last integrate.  Every pass still resets the volume and
+    # integrates all B frames; the timed region ends with a synchronize.
+    resident = not args.no_resident
+
     def step():
         vbg.reset()
         vbg.integrate_frames(dptr, K, T, depth_scale=1.0, depth_max=args.depth_max,
-                             trunc_voxel_multiplier=args.trunc)
+                             trunc_voxel_multiplier=args.trunc, resident=resident)
         if world > 1:
             merge()
 
@@ -1792,6 +1800,7 @@ def main():
                        "frames_per_gpu": B, "height": H, "width": W, "voxel_size": args.voxel,
                        "block_resolution": args.block_resolution, "depth_max": args.depth_max,
                        "trunc_voxel_multiplier": args.trunc, "frame_batch": 127,
+                       "frames": "MQR_DEVICE" if args.no_resident else "MQR_DEVICE_RESIDENT (generated once, unchanged)",
                        "parallelism": f"frame-shard x{world}" + (f" + libmqr merge ({args.merge}, {transport})"
                                                                  if world > 1 else "")},
             "sharded_extract": sharded,

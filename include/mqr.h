@@ -20,7 +20,13 @@
  *     the caller stream is then made to wait (device-side) for that integrate, so whatever the
  *     caller enqueues there next -- overwriting or freeing the frames included -- runs after the
  *     library's reads; every later call on the volume orders itself behind it (a host-side reader
- *     of the frames synchronizes the caller stream first, as it would for a kernel of its own);
+ *     of the frames synchronizes the caller stream first, as it would for a kernel of its own).
+ *     mqr_integrate_frames also takes MQR_DEVICE_RESIDENT frames: device frames the caller keeps
+ *     allocated and unchanged until the device (or the volume, by any call that drains it) has been
+ *     synchronized -- e.g. a capture uploaded once and integrated pass after pass.  Reads are ordered
+ *     after the caller stream as for MQR_DEVICE, but the caller stream is not made to wait for the
+ *     call's integrates, so the next call's first touch -- itself behind the caller stream -- can run
+ *     beside this call's last integrate instead of after it;
  *   - matrices are row-major: K = 3x3 intrinsic (Open3D convention, cx already flipped),
  *     T_wc = 4x4 world->camera extrinsic, both float64 as the reference passes them
  *     (o3d_utils.py:203-210);
@@ -37,6 +43,7 @@ extern "C" {
 
 #define MQR_HOST 0
 #define MQR_DEVICE 1
+#define MQR_DEVICE_RESIDENT 2 /* mqr_integrate_frames only: see "stream ordering" above */
 
 typedef struct mqr_vbg mqr_vbg;    /* voxel-block-hashed TSDF volume resident in HBM */
 typedef struct mqr_geom mqr_geom;  /* extracted point cloud or triangle mesh (device-resident) */
@@ -107,8 +114,8 @@ int mqr_integrate(mqr_vbg* v, const int32_t* keys, int64_t n, const float* depth
  * frame_ok (host, may be NULL): frames with frame_ok[i]==0 are skipped (missing/invalid loads).
  * Returns 3 if a valid frame touches no block (upstream raises).  Every batch's touch counters are
  * read on the host before its integrate is launched, so errors are reported by this call; with
- * MQR_DEVICE frames the call returns with the last integrate still running (see "stream ordering"
- * above), with MQR_HOST frames after it has finished. */
+ * MQR_DEVICE / MQR_DEVICE_RESIDENT frames the call returns with the last integrate still running (see
+ * "stream ordering" above), with MQR_HOST frames after it has finished. */
 int mqr_integrate_frames(mqr_vbg* v, const float* depths, int depth_loc, int B, int H, int W, const double* K,
                          const double* T_wc, const uint8_t* frame_ok, float depth_scale, float depth_max,
                          float trunc_mult);

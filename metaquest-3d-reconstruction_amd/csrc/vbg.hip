@@ -1187,7 +1187,13 @@ int mqr_integrate_frames(mqr_vbg* v, const float* depths, int depth_loc, int B, 
                          float trunc_mult) {
     MQR_REQUIRE(v && depths && K && T_wc, "null argument");
     MQR_REQUIRE(B >= 0 && H > 0 && W > 0, "bad frame shape");
+    MQR_REQUIRE(depth_loc == MQR_HOST || depth_loc == MQR_DEVICE || depth_loc == MQR_DEVICE_RESIDENT,
+                "depth_loc must be MQR_HOST, MQR_DEVICE or MQR_DEVICE_RESIDENT");
     MQR_CHECK_HIP(hipSetDevice(v->device));
+    // resident device frames (include/mqr.h): the caller keeps them unchanged until it synchronizes, so its
+    // stream is not made to wait for this call's integrates at the return
+    const bool resident = depth_loc == MQR_DEVICE_RESIDENT;
+    if (resident) depth_loc = MQR_DEVICE;
     // device frames: both streams read them (touch, integrate) -- ordered after the caller's writes, from
     // the first batch's touch on (its frame-parameter upload and counter clear need not wait for them)
     bool caller_ordered = depth_loc != MQR_DEVICE;
@@ -1302,7 +1308,9 @@ int mqr_integrate_frames(mqr_vbg* v, const float* depths, int depth_loc, int B, 
         // stream waits for it (its next write to the frames is ordered after the library's reads); the
         // volume's next user orders behind it on the device (order_after_integrate, wait_parity_free) or
         // drains it (sync_all).  Host frames stay synchronous: the caller's array is read by copies.
-        return order_caller_after_integrate(v);
+        // Resident frames: no caller-stream wait -- the caller's next work (the next call's touch included,
+        // which orders itself after the caller stream) need not queue behind this call's last integrate.
+        return resident ? 0 : order_caller_after_integrate(v);
     }
     if (sync_all(v)) return 1;
     if (rc) set_error(kNoBlock);  // the prefix re-run may have overwritten the message

@@ -17,6 +17,7 @@ LIB_PATH = os.environ.get("MQR_HIP_LIB", os.path.join(_HERE, "libmqr_hip.so"))
 
 MQR_HOST = 0
 MQR_DEVICE = 1
+MQR_DEVICE_RESIDENT = 2  # mqr_integrate_frames: device frames kept unchanged until the caller synchronizes
 
 _f32p = ctypes.POINTER(ctypes.c_float)
 _f64p = ctypes.POINTER(ctypes.c_double)

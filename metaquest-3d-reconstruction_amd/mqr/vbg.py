@@ -24,7 +24,7 @@ import threading
 import numpy as np
 
 from . import _lib
-from ._lib import MQR_DEVICE, MQR_HOST, MqrStats, call, ptr
+from ._lib import MQR_DEVICE, MQR_DEVICE_RESIDENT, MQR_HOST, MqrStats, call, ptr
 from .geometry import Image, PointCloud, Tensor, TriangleMesh
 
 # Open3D defaults for the keyword arguments the reference relies on.
@@ -230,14 +230,17 @@ class VoxelBlockGrid:
 
     # -- batched whole-sequence entry ---------------------------------------------------------------
     def integrate_frames(self, depths, intrinsics, extrinsics, frame_ok=None, depth_scale=1.0, depth_max=3.0,
-                         trunc_voxel_multiplier=8.0):
+                         trunc_voxel_multiplier=8.0, resident=False):
         """touch + integrate for every frame in order (== sequential per-frame calls, bit for bit).
 
         depths: (B,H,W) float32 host array, or an ``_lib.DeviceBuffer`` holding B*H*W floats (then
-        pass ``depths=(buffer, B, H, W)``); intrinsics (B,3,3), extrinsics (B,4,4) world->camera."""
+        pass ``depths=(buffer, B, H, W)``); intrinsics (B,3,3), extrinsics (B,4,4) world->camera.
+        resident=True (device frames only): the caller keeps the frames allocated and unchanged until it
+        synchronizes the device (MQR_DEVICE_RESIDENT, include/mqr.h), so its stream does not wait for the
+        call's integrates and the next call's first touch can overlap them."""
         if isinstance(depths, tuple):
             buf, B, H, W = depths
-            dptr, loc = buf.ptr, MQR_DEVICE
+            dptr, loc = buf.ptr, (MQR_DEVICE_RESIDENT if resident else MQR_DEVICE)
             keep = None
         else:
             keep = np.ascontiguousarray(depths, dtype=np.float32)

@@ -326,3 +326,40 @@ def test_reset_behind_an_unfinished_integrate_swaps_sets(variant):
     else:
         assert flips == 5, flips  # 4 in the loop + the one behind the short call
     del ref2
+
+
+def test_resident_frames_back_to_back_passes():
+    """MQR_DEVICE_RESIDENT frames (integrate_frames(resident=True)): the caller stream is not made to wait
+    for the call's integrates, so the next call's touch may run beside the previous call's last integrate
+    (the overlap itself is measured by tools/ab_async.py and the bench trace, not here).  Reset passes over
+    resident frames -- mixed with an MQR_DEVICE pass, on a side caller stream and the default one, two
+    captures alternating with no synchronize -- leave the oracle's volumes."""
+    import torch
+    from gpu_helpers import compare_volumes
+    from mqr.vbg import VoxelBlockGrid
+    d1, K1, T1 = _room(254, seed=31)
+    d2, K2, T2 = _room(127, seed=32)
+    B1, H, W = d1.shape
+    t1, t2 = torch.from_numpy(d1).cuda(), torch.from_numpy(d2).cuda()
+    torch.cuda.synchronize()
+    kw = dict(depth_scale=1.0, depth_max=4.0, trunc_voxel_multiplier=10.0, resident=True)
+    a = (_Dev(t1), B1, H, W), K1, T1
+    b = (_Dev(t2), len(d2), H, W), K2, T2
+    vbg = VoxelBlockGrid(voxel_size=0.01, block_resolution=16, block_count=256, device="cuda:0")
+    s = torch.cuda.Stream()  # a side caller stream, then the default one
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        vbg.integrate_frames(*a, **kw)
+        vbg.reset()
+        vbg.integrate_frames(*a, **dict(kw, resident=False))
+        vbg.reset()
+        vbg.integrate_frames(*a, **kw)
+    torch.cuda.current_stream().wait_stream(s)
+    for frames, K, T in (b, a, b, a):
+        vbg.reset()
+        vbg.integrate_frames(frames, K, T, **kw)
+    vbg.integrate_frames(*b, **kw)  # onto the first capture, still without a synchronize
+    torch.cuda.synchronize()
+    ref = _oracle(d2, K2, T2, ref=_oracle(d1, K1, T1))
+    assert compare_volumes(vbg.export(), ref.export(), 0.0) == 0.0
+    assert _flips(vbg) >= 5

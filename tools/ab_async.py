@@ -6,7 +6,7 @@ asynchronous return of mqr_integrate_frames on device frames (variant 0: the cal
 integrate queued) vs the synchronous one (variant bit 24: the streams drained before returning).
 Prints one JSON object (median ms per step per variant).
 
-python tools/ab_async.py --rounds 7 --steps 100 [--variants 0,0x1000000,0x400000]
+python tools/ab_async.py --rounds 7 --steps 100 [--variants 0,0x1000000,0x400000,r0]   (r: resident frames)
 """
 import argparse
 import json
@@ -37,7 +37,10 @@ def main():
     K, T = seq["K"].astype(np.float64), seq["T_wc"].astype(np.float64)
     torch.cuda.synchronize()
     names = {0: "async", 0x1000000: "sync"}
-    modes = {names.get(int(v, 0), v): int(v, 0) for v in a.variants.split(",")}
+    # a variant prefixed "r" passes the frames as MQR_DEVICE_RESIDENT (integrate_frames(resident=True))
+    modes = {(("resident" if v == "r0" else v) if v.startswith("r") else names.get(int(v, 0), v)):
+             int(v.lstrip("r"), 0) for v in a.variants.split(",")}
+    resident = {m: m.startswith("r") for m in modes}
     vols = {m: VoxelBlockGrid(voxel_size=0.005, block_resolution=16, block_count=40000, device=0) for m in modes}
     for m, v in modes.items():
         _lib.call("mqr_vbg_set_variant", vols[m].handle, v)
@@ -51,7 +54,7 @@ def main():
             t0 = time.perf_counter()
             for _ in range(a.steps):
                 vbg.reset()
-                vbg.integrate_frames(arg, K, T, **kw)
+                vbg.integrate_frames(arg, K, T, resident=resident[m], **kw)
             torch.cuda.synchronize()
             dt = (time.perf_counter() - t0) / a.steps * 1e3
             if r:

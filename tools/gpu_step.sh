@@ -11,6 +11,7 @@
 #   n2          2-rank rehearsal on one GPU (gloo-staged merge)        -> gpurun_out/${TAG}_bench_n2.json
 #   n2self      the same, bench.py --gpus 2 starting its own ranks (no torchrun) -> gpurun_out/${TAG}_bench_n2_selflaunch.json
 #   mbytes      C4 exchange bytes / zero-weight voxels / per-rank times at 2, 4, 8 ranks (tools/merge_bytes.py)
+#   steptrace   kernel trace of the C2 loop: step head (tools/step_head.py) and integrate-stream gaps (tools/integrate_gaps.py)
 #   prof        rocprofv3 --kernel-trace --stats of the C2 bench      -> gpurun_out/${TAG}_bench_kernel_stats.csv
 #   shardtrace[:W:R] one C4 shard's reset + integrate passes under a kernel trace (tools/shard_steps.py + step_head.py)
 #   mprof       rocprofv3 kernel trace + stats of tools/time_merge.py (8 ranks on one GPU)
@@ -80,7 +81,8 @@ for step in ${STEPS:-tests}; do
         > gpurun_out/${TAG}_st_bench.json 2> gpurun_out/${TAG}_st_bench.err || { tail -20 gpurun_out/${TAG}_st_bench.err; exit 1; }
       cp "$(find gpurun_out/st -name '*kernel_trace.csv' | head -1)" gpurun_out/${TAG}_step_trace.csv
       rm -rf gpurun_out/st
-      python tools/step_head.py gpurun_out/${TAG}_step_trace.csv --steps 40 > gpurun_out/${TAG}_step_head.json && cat gpurun_out/${TAG}_step_head.json ;;
+      python tools/step_head.py gpurun_out/${TAG}_step_trace.csv --steps 40 > gpurun_out/${TAG}_step_head.json && cat gpurun_out/${TAG}_step_head.json
+      python tools/integrate_gaps.py gpurun_out/${TAG}_step_trace.csv > gpurun_out/${TAG}_integrate_gaps.json && cat gpurun_out/${TAG}_integrate_gaps.json ;;
     mprof)
       rm -rf gpurun_out/mp
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/mp -o run -- \
