@@ -170,6 +170,11 @@ struct mqr_vbg {
     // uint16 when every rank's bound is <= 65535.  -1 = unknown (imported or unpacked contents).
     int64_t wbound = 0;
     int64_t batch_new_max = 0; // most blocks one integrate batch has allocated (sizes the table headroom)
+    // Weight bound of the next integrate launch (set by its caller: the weights before the call plus the frames
+    // up to the batch's end; -1 unknown): the default kernel's LDS table of (w, 1 / (w + 1)) has this many
+    // entries (k_integrate_wt; without a bound, or above kRtabMax, k_integrate_win runs).
+    int64_t launch_wbound = -1;
+    bool rtab = true;  // variant bit 26 clears it (A/B)
 
     // Second table / pool set.  mqr_vbg_reset while an integrate is still in flight swaps the sets instead of
     // ordering the clear behind that integrate: the next call's touch then overlaps the previous call's last

@@ -400,6 +400,14 @@ static int launch_integrate_ab(mqr_vbg* v, int var, hipStream_t s, unsigned grid
         case 60: wx(k_integrate_wx<7, 4>); break;  // the default + a workgroup barrier per frame
         case 61: wx(k_integrate_wx<6, 4>); break;
         case 62: *fixup = true; wx(k_integrate_wx<8, 6>); break;
+        case 64: {  // the default's LDS-table kernel at >= 6 waves per SIMD (k_integrate_wt<6>)
+            const int tcount = (int)v->launch_wbound;
+            hipLaunchKernelGGL(k_integrate_wt<6>, dim3(grid), dim3(512), sizeof(float2) * (size_t)tcount, s, list, lmask,
+                               bad_out, counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp,
+                               depth_frame, depth_max, sdf_trunc, first_new, tcount);
+            *fixup = true;
+            break;
+        }
         default: set_error("integrate variant " + std::to_string(var) + " unknown"); return 2;
     }
     return 0;
@@ -594,7 +602,10 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
     //     the eight record loads issued first (>= 7 / 5 waves), 49 / 50 = 45 / 47 branch-free.  (24 of round 4, a ballot skip of
     //     out-of-image wave slots, ran 0.70 vs 0.48 ms per launch: removed.)
     int var = v->kernel_variant;
-    if (var < 0 || var > 62) var = 0;
+    if (var < 0 || var > 64 || var == 63) var = 0;
+    // the LDS-table kernels (default, 64) need a known weight bound whose table fits a workgroup's LDS share
+    const bool rtab_ok = v->rtab && v->launch_wbound >= 1 && v->launch_wbound <= kRtabMax;
+    if (var == 64 && !rtab_ok) var = 0;
     if (!MQR_AB && var != 1 && var != 2 && var != 4) var = 0;
     if (var != 1 && var != 2 && !lean_ok) var = 2;
     if (var == 5 && (v->R != 16 || W % 4 != 0 || W < 4 || (reinterpret_cast<uintptr_t>(depths) & 15))) var = 0;
@@ -624,6 +635,12 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
             hipLaunchKernelGGL((k_integrate_lean<16, 512, 1, 8, 2>), dim3(grid), dim3(512), 0, s, list, lmask,
                                v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp,
                                depth_frame, depth_max, sdf_trunc, first_new);
+            fixup = true;
+        } else if (var == 0 && rtab_ok) {  // the update through the (w, 1 / (w + 1)) table
+            const int tcount = (int)v->launch_wbound;
+            hipLaunchKernelGGL(k_integrate_wt<7>, dim3(grid), dim3(512), sizeof(float2) * (size_t)tcount, s, list, lmask,
+                               v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp,
+                               depth_frame, depth_max, sdf_trunc, first_new, tcount);
             fixup = true;
         } else if (var == 0) {
             hipLaunchKernelGGL(k_integrate_win<7>, dim3(grid), dim3(512), 0, s, list, lmask, counters, v->list_cap, t,
@@ -1204,6 +1221,7 @@ int mqr_integrate_frames(mqr_vbg* v, const float* depths, int depth_loc, int B, 
     std::vector<int> valid;
     for (int i = 0; i < B; ++i)
         if (!frame_ok || frame_ok[i]) valid.push_back(i);
+    const int64_t wb0 = v->wbound;  // weights before the call: a batch ending at frame e keeps them <= wb0 + e
     if (v->wbound >= 0) v->wbound += (int64_t)valid.size();  // (an upper bound even if the call fails part-way)
     int rc = 0;
     int batch = 0;
@@ -1250,6 +1268,7 @@ int mqr_integrate_frames(mqr_vbg* v, const float* depths, int depth_loc, int B, 
         TouchState ts;
         if (touch_batch_launch(v, p, dbase, HW, H, W, b, depth_scale, depth_max, sdf_trunc, block_size, max_touch, ts))
             return 1;
+        v->launch_wbound = wb0 >= 0 ? wb0 + (int64_t)s + b : -1;  // this batch's weight bound (the LDS table)
         if (spec) {
             const int64_t grid = std::min<int64_t>(std::max<int64_t>(v->batch_n_max + v->batch_n_max / 4, 256), 8192);
             const size_t ev_before = v->int_events.size();
@@ -1291,6 +1310,7 @@ int mqr_integrate_frames(mqr_vbg* v, const float* depths, int depth_loc, int B, 
             rc = 3;
             if (undo_touch(v, p, pool_before)) return 1;
             if (empty > 0) {
+                v->launch_wbound = wb0 >= 0 ? wb0 + (int64_t)s + empty : -1;
                 if (upload_frames(v, p, K, T_wc, idx, empty, dframe) || reset_batch_counters(v, p)) return 1;
                 if (touch_batch(v, p, dbase, HW, H, W, empty, depth_scale, depth_max, sdf_trunc, block_size,
                                 max_touch))
@@ -1394,6 +1414,7 @@ int mqr_integrate(mqr_vbg* v, const int32_t* keys, int64_t n, const float* depth
         (void)hipFree(dkeys);
         return 1;
     }
+    v->launch_wbound = v->wbound;
     int rc = launch_integrate(v, 0, dptr, HW, H, W, 1, depth_scale, depth_max, v->voxel_size * trunc_mult,
                               (int)pool_before);
     if (sync_all(v)) rc = 1;
@@ -1540,6 +1561,7 @@ int mqr_vbg_set_variant(mqr_vbg* v, int variant) {
     v->spec_head = (variant & 0x40000) == 0;     // bit 18: no speculative first-batch integrate (A/B)
     v->async_return = (variant & 0x1000000) == 0; // bit 24: integrate_frames drains its streams before returning (A/B)
     v->flip_reset = (variant & 0x2000000) == 0;   // bit 25: reset waits for an in-flight integrate (no set swap, A/B)
+    v->rtab = (variant & 0x4000000) == 0;         // bit 26: k_integrate_win instead of the LDS-table kernel (A/B)
     // (the extraction configuration is set by mqr_vbg_set_extract_mode alone, A/B library only)
     return 0;
 }

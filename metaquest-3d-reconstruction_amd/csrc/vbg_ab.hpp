@@ -1504,4 +1504,5 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
     }
 }
 
+
 }  // namespace mqr

@@ -49,13 +49,14 @@ def test_shortened_reciprocals_exact(which, lo, hi):
 # tests below also cover the A/B kernels the shipped library leaves out (variants 3 and 5, bit 0x8000)
 AB = os.environ.get("MQR_AB_TEST") == "1"
 # 0x10000: one pixel per touch thread, 0x40000: no speculative first-batch integrate, 0x100000: 64-frame
-# batches, 0x200000 / 0x400000 / 0x800000: a first batch of 64 / 32 / 16 frames
+# batches, 0x200000 / 0x400000 / 0x800000: a first batch of 64 / 32 / 16 frames, 0x4000000: the default
+# kernel without its LDS weight table (k_integrate_win)
 INTEGRATE_VARIANTS = {16: (0, 2, 4, 0x100, 0x104, 0x200, 0x400, 0x800, 0x10000, 0x40000, 0x100000, 0x200000,
-                           0x400000, 0x800000),
+                           0x400000, 0x800000, 0x4000000),
                       8: (0, 2, 0x100)}
 if AB:
     INTEGRATE_VARIANTS = {16: (0, 3, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25,
-                               26, 27, 28, 29, 30, 31, 36, 37, 38, 39, 40, 41, 44, 45, 46, 47, 48, 49, 50, 0x105, 0x605, 0x106, 0x108, 0x10b, 0x10d, 0x111, 0x8000, 0x8003, 0x8008, 0x800a, 0x800b, 0x800d, 0x8011), 8: (0, 0x8000)}
+                               26, 27, 28, 29, 30, 31, 36, 37, 38, 39, 40, 41, 44, 45, 46, 47, 48, 49, 50, 64, 0x4000000, 0x105, 0x605, 0x106, 0x108, 0x10b, 0x10d, 0x111, 0x8000, 0x8003, 0x8008, 0x800a, 0x800b, 0x800d, 0x8011), 8: (0, 0x8000)}
 
 
 def test_specialised_integrate_equals_generic():
@@ -289,3 +290,36 @@ def test_confidence_float64_quotients_match_ieee(mode, a_max, b_lo, b_hi):
     _lib.call("mqr_check_div64", 0, mode, 12345 + mode, 1 << 31, a_max, b_lo, b_hi, ctypes.byref(mm),
               _lib.ptr(bad, _lib._f64p))
     assert mm.value == 0, f"{mm.value} mismatches, e.g. a={bad[0]!r} b={bad[1]!r}"
+
+
+def test_weight_table_across_calls_and_unknown_bounds():
+    """The default kernel's LDS table of (w, 1 / (w + 1)) is sized per batch from the weights before the call
+    plus the frames up to the batch's end.  Weights carried over several calls (one of them two batches long,
+    the second batch starting at the previous batches' bound), a volume whose weights are unknown after an
+    import (no bound: k_integrate_win runs) and the table-less kernel (bit 26) all equal the generic kernel."""
+    from gpu_helpers import compare_volumes
+    from mqr import _lib, synthetic
+    from mqr.vbg import VoxelBlockGrid
+    seq = synthetic.make_sequence("room", n=70, height=120, width=160, f=131.25, noise=True, seed=23)
+    d, K, T = seq["depth"], seq["K"], seq["T_wc"]
+    kw = dict(depth_scale=1.0, depth_max=4.0, trunc_voxel_multiplier=10.0)
+    calls = [(slice(0, 20),), (slice(10, 30),), (slice(0, 70), slice(0, 70))]  # the last: 140 frames, two batches
+    out = {}
+    for variant in (1, 0, 0x4000000):
+        v = VoxelBlockGrid(voxel_size=0.02, block_resolution=16, block_count=64)
+        _lib.call("mqr_vbg_set_variant", v.handle, variant)
+        for parts in calls:
+            dd = np.concatenate([d[p] for p in parts])
+            v.integrate_frames(dd, np.concatenate([K[p] for p in parts]), np.concatenate([T[p] for p in parts]), **kw)
+        out[variant] = v.export()
+        # then through an import (weight bound unknown) and two more calls
+        w = VoxelBlockGrid(voxel_size=0.02, block_resolution=16, block_count=64)
+        _lib.call("mqr_vbg_set_variant", w.handle, variant)
+        w.import_blocks(*out[variant])
+        for _ in range(2):
+            w.integrate_frames(d[:40], K[:40], T[:40], **kw)
+        out[(variant, "imported")] = w.export()
+    assert float(out[1][2].max()) > 30  # weights carried past the first two calls' frame counts
+    for variant in (0, 0x4000000):
+        compare_volumes(out[1], out[variant], 0.0)
+        compare_volumes(out[(1, "imported")], out[(variant, "imported")], 0.0)
