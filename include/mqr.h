@@ -338,7 +338,8 @@ int mqr_vbg_profile(mqr_vbg* v, int enable);
  * off the speculative first-batch integrate (k_gate; A/B), bit 24 makes mqr_integrate_frames on device frames
  * drain its streams before returning (A/B), bit 25 makes mqr_vbg_reset wait for an integrate in flight
  * instead of swapping in the second table / pool set (A/B), bit 26 runs the default integrate without its LDS
- * table of (w, 1 / (w + 1)) (k_integrate_win instead of k_integrate_wt; A/B).
+ * table of (w, 1 / (w + 1)) (k_integrate_win instead of k_integrate_wt; A/B), bit 27 keeps k_integrate_wt's two
+ * Markstein corrections of s / sdf_trunc where one is verified exact for the volume's sdf_trunc (A/B).
  * mqr_check_division: exhaustive bit-pattern check of the division shortcuts used on device against
  * IEEE division (which=0: 1/b via rcp_rn, 1: a/b via div_rn, 2: a/b via the bare core, 3: 1/b via
  * rcp_nm, 4: 1/b via rcp_m, over float bit patterns [lo_bits, lo_bits+count) as b or a); returns

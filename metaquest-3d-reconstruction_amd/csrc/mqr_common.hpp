@@ -175,6 +175,7 @@ struct mqr_vbg {
     // entries (k_integrate_wt; without a bound, or above kRtabMax, k_integrate_win runs).
     int64_t launch_wbound = -1;
     bool rtab = true;  // variant bit 26 clears it (A/B)
+    bool div1 = true;  // one-correction s / sdf_trunc where verified (strunc_one_correction_ok); bit 27 clears it
 
     // Second table / pool set.  mqr_vbg_reset while an integrate is still in flight swaps the sets instead of
     // ordering the clear behind that integrate: the next call's touch then overlaps the previous call's last

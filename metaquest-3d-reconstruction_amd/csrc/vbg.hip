@@ -238,10 +238,10 @@ static int ensure_depth(mqr_vbg* v, int64_t floats) {
     return 0;
 }
 
-// Whether one Markstein correction gives IEEE s / t for every s in [-t, t] (lean_update_v<DIV1>):
+// Whether one Markstein correction gives IEEE s / t for every s in [-t, t] (k_integrate_wt<.., 1>, lean_update_v<DIV1>):
 // k_check_strunc over the ~1e9 floats of [+0, t] once per t per process (a few ms; the sequence is
 // odd in s).  Cached; on any error the answer is false (two corrections stay).
-[[maybe_unused]] static bool strunc_one_correction_ok(float t) {
+static bool strunc_one_correction_ok(float t) {
     static std::mutex mu;
     static std::unordered_map<uint32_t, bool> cache;
     const uint32_t tb = __builtin_bit_cast(uint32_t, t);
@@ -638,9 +638,11 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
             fixup = true;
         } else if (var == 0 && rtab_ok) {  // the update through the (w, 1 / (w + 1)) table
             const int tcount = (int)v->launch_wbound;
-            hipLaunchKernelGGL(k_integrate_wt<7>, dim3(grid), dim3(512), sizeof(float2) * (size_t)tcount, s, list, lmask,
-                               v->bad[p], counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp,
-                               depth_frame, depth_max, sdf_trunc, first_new, tcount);
+            // s / sdf_trunc with one correction where that is verified exact for this sdf_trunc (bit 27: never)
+            auto kern = v->div1 && strunc_one_correction_ok(sdf_trunc) ? k_integrate_wt<7, 1> : k_integrate_wt<7, 0>;
+            hipLaunchKernelGGL(kern, dim3(grid), dim3(512), sizeof(float2) * (size_t)tcount, s, list, lmask, v->bad[p],
+                               counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp, depth_frame,
+                               depth_max, sdf_trunc, first_new, tcount);
             fixup = true;
         } else if (var == 0) {
             hipLaunchKernelGGL(k_integrate_win<7>, dim3(grid), dim3(512), 0, s, list, lmask, counters, v->list_cap, t,
@@ -1562,6 +1564,7 @@ int mqr_vbg_set_variant(mqr_vbg* v, int variant) {
     v->async_return = (variant & 0x1000000) == 0; // bit 24: integrate_frames drains its streams before returning (A/B)
     v->flip_reset = (variant & 0x2000000) == 0;   // bit 25: reset waits for an in-flight integrate (no set swap, A/B)
     v->rtab = (variant & 0x4000000) == 0;         // bit 26: k_integrate_win instead of the LDS-table kernel (A/B)
+    v->div1 = (variant & 0x8000000) == 0;         // bit 27: the LDS-table kernel keeps two quotient corrections (A/B)
     // (the extraction configuration is set by mqr_vbg_set_extract_mode alone, A/B library only)
     return 0;
 }

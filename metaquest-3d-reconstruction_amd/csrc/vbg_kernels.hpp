@@ -998,7 +998,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
 // LDS read overlaps the quotient.
 constexpr int kRtabMax = 6000;  // table entries: 48 KB of LDS, 3 workgroups per CU still fit
 
-template <int WPE>
+// DIV1: s / sdf_trunc with one Markstein correction (host: strunc_one_correction_ok verified it for this
+// sdf_trunc over every s in [-t, t]), as lean_update_v<DIV1>.
+template <int WPE, int DIV1 = 0>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void k_integrate_wt(
     const int32_t* __restrict__ list, const bmask_t* __restrict__ lmask, int32_t* __restrict__ bad_out,
     int* __restrict__ counters, int64_t list_cap,
@@ -1070,7 +1072,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
                         asm("v_min_f32 %0, %1, %2" : "=v"(s) : "s"(sdf_trunc), "v"(sdf));
                         const float q0 = s * y1t;
                         const float q1 = __builtin_fmaf(__builtin_fmaf(-sdf_trunc, q0, s), y1t, q0);
-                        const float sn = __builtin_fmaf(__builtin_fmaf(-sdf_trunc, q1, s), y1t, q1);
+                        const float sn = DIV1 ? q1 : __builtin_fmaf(__builtin_fmaf(-sdf_trunc, q1, s), y1t, q1);
                         ts[k] = (e.x * ts[k] + sn) * e.y;
                         wa[k] += 8u;
                     }

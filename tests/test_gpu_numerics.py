@@ -52,7 +52,7 @@ AB = os.environ.get("MQR_AB_TEST") == "1"
 # batches, 0x200000 / 0x400000 / 0x800000: a first batch of 64 / 32 / 16 frames, 0x4000000: the default
 # kernel without its LDS weight table (k_integrate_win)
 INTEGRATE_VARIANTS = {16: (0, 2, 4, 0x100, 0x104, 0x200, 0x400, 0x800, 0x10000, 0x40000, 0x100000, 0x200000,
-                           0x400000, 0x800000, 0x4000000),
+                           0x400000, 0x800000, 0x4000000, 0x8000000),
                       8: (0, 2, 0x100)}
 if AB:
     INTEGRATE_VARIANTS = {16: (0, 3, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25,
@@ -305,7 +305,7 @@ def test_weight_table_across_calls_and_unknown_bounds():
     kw = dict(depth_scale=1.0, depth_max=4.0, trunc_voxel_multiplier=10.0)
     calls = [(slice(0, 20),), (slice(10, 30),), (slice(0, 70), slice(0, 70))]  # the last: 140 frames, two batches
     out = {}
-    for variant in (1, 0, 0x4000000):
+    for variant in (1, 0, 0x4000000, 0x8000000):
         v = VoxelBlockGrid(voxel_size=0.02, block_resolution=16, block_count=64)
         _lib.call("mqr_vbg_set_variant", v.handle, variant)
         for parts in calls:
@@ -320,6 +320,6 @@ def test_weight_table_across_calls_and_unknown_bounds():
             w.integrate_frames(d[:40], K[:40], T[:40], **kw)
         out[(variant, "imported")] = w.export()
     assert float(out[1][2].max()) > 30  # weights carried past the first two calls' frame counts
-    for variant in (0, 0x4000000):
+    for variant in (0, 0x4000000, 0x8000000):
         compare_volumes(out[1], out[variant], 0.0)
         compare_volumes(out[(1, "imported")], out[(variant, "imported")], 0.0)
