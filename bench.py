@@ -614,7 +614,7 @@ def c5_leg(args, device, frames_per_side=2000, voxel=0.003, key_every=40, parity
     launches = max(st["integrate_launches"], 1)
     alg = (16 * R3 * st["union_blocks"] + 4 * H * W * st["frames"] + 16 * st["frame_blocks"]) / launches
     avg_ms = st["integrate_ms"] / launches
-    int_roof = {"bound": "hbm", "kernel": "k_integrate_win", "unit": "GB/s", "peak": HBM_PEAK_GBS,
+    int_roof = {"bound": "hbm", "kernel": last_kernel_name(vbg), "unit": "GB/s", "peak": HBM_PEAK_GBS,
                 "alg_bytes_per_launch": alg, "avg_launch_ms": avg_ms, "launches": st["integrate_launches"],
                 "achieved": alg / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else None,
                 "union_blocks_per_launch": st["union_blocks"] / launches,
@@ -1099,6 +1099,14 @@ def meshfilter_leg(vbg, thr, min_count=2000, reps=3):
             "triangles_out": int(stats[6]), "min_triangle_count": min_count, "ms": ms,
             "mtris_per_s": nt / ms / 1e3,
             "note": "mqr_mesh_filter_components, device-resident mesh in/out, wall time of the call, median"}
+
+
+def last_kernel_name(vbg):
+    """The main kernel of the volume's last integrate launch (mqr_vbg_last_kernel_name)."""
+    from mqr import _lib
+    buf = ctypes.create_string_buffer(64)
+    _lib.call("mqr_vbg_last_kernel_name", vbg.handle, buf, 64)
+    return buf.value.decode()
 
 
 def build_tag(which):
@@ -1773,6 +1781,7 @@ def main():
     _vr = ctypes.c_int(-1)
     _lib.call("mqr_vbg_last_kernel", vbg.handle, ctypes.byref(_vr))
     variant_ran = _vr.value
+    kernel_ran = last_kernel_name(vbg)
     traffic, traffic_src = pmc_traffic(H, W, B, variant_ran)
 
     if rank == 0:
@@ -1827,7 +1836,7 @@ def main():
             "roofline_binding": dict(pmc_binding(avg_ms, variant_ran) or {}, gather_ceiling=gather_ceiling(
                 avg_ms, st["frame_blocks"] * args.block_resolution ** 3 / 64 / launches,
                 torch.cuda.get_device_properties(local).multi_processor_count)),
-            "roofline": {"bound": "hbm", "kernel": "k_integrate_win", "achieved": achieved, "peak": HBM_PEAK_GBS,
+            "roofline": {"bound": "hbm", "kernel": kernel_ran, "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "peak_measured_copy": extras.get("hbm_copy_gbs"),
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_source": traffic_src,

@@ -59,6 +59,8 @@ int mqr_version(void);
  * waiting for an integrate still in flight (see mqr_vbg_reset). */
 int mqr_build_tag(int which, char* buf, int cap);
 int mqr_vbg_last_kernel(mqr_vbg* v, int* variant);
+/* The name of the main kernel the volume's last integrate launch ran (e.g. "k_integrate_wt<7, 1>"). */
+int mqr_vbg_last_kernel_name(mqr_vbg* v, char* buf, int cap);
 int mqr_vbg_flips(mqr_vbg* v, int64_t* n);
 const char* mqr_last_error(void);
 int mqr_device_count(int* n);

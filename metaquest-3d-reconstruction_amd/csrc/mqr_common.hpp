@@ -227,6 +227,7 @@ struct mqr_vbg {
     int touch_ppt = 2;  // stride-4 pixels per k_touch thread (variant bit 16: one)
     int ex_mode = -1;   // extraction configuration under A/B (-1: the library default kExMode; tools/ab_extract.py)
     int last_var = -1;        // integrate variant of the last launch, after fallbacks (mqr_vbg_last_kernel)
+    const char* last_kname = "";  // its main kernel (mqr_vbg_last_kernel_name)
     bool profile = false;
     bool profile_touch = false;  // mqr_vbg_profile level 2: also time the touch launches
     std::vector<std::pair<hipEvent_t, hipEvent_t>> int_events, touch_events;

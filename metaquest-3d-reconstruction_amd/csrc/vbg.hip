@@ -619,6 +619,8 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
     if (var >= 13 && !win8_ok) var = 4;
     if (v->R != 16 && v->R != 8) var = 1;
     v->last_var = var;
+    v->last_kname = var == 1 ? "k_integrate" : var == 2 ? "k_integrate_t" : var == 4 || v->R == 8 ? "k_integrate_lean"
+                                                                                                   : "k_integrate_ab";
     const int32_t* bad_list = v->bad[p];
     const bmask_t* bad_mask = reinterpret_cast<const bmask_t*>(v->bad[p] + v->list_cap);
     int* bad_count = counters + kBadCount;
@@ -639,12 +641,15 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
         } else if (var == 0 && rtab_ok) {  // the update through the (w, 1 / (w + 1)) table
             const int tcount = (int)v->launch_wbound;
             // s / sdf_trunc with one correction where that is verified exact for this sdf_trunc (bit 27: never)
-            auto kern = v->div1 && strunc_one_correction_ok(sdf_trunc) ? k_integrate_wt<7, 1> : k_integrate_wt<7, 0>;
+            const bool one = v->div1 && strunc_one_correction_ok(sdf_trunc);
+            auto kern = one ? k_integrate_wt<7, 1> : k_integrate_wt<7, 0>;
+            v->last_kname = one ? "k_integrate_wt<7, 1>" : "k_integrate_wt<7, 0>";
             hipLaunchKernelGGL(kern, dim3(grid), dim3(512), sizeof(float2) * (size_t)tcount, s, list, lmask, v->bad[p],
                                counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp, depth_frame,
                                depth_max, sdf_trunc, first_new, tcount);
             fixup = true;
         } else if (var == 0) {
+            v->last_kname = "k_integrate_win<7>";
             hipLaunchKernelGGL(k_integrate_win<7>, dim3(grid), dim3(512), 0, s, list, lmask, counters, v->list_cap, t,
                                v->pool, v->voxel_size, depths, HW, H, W, fp, depth_frame, depth_max, sdf_trunc,
                                first_new);
@@ -911,6 +916,12 @@ int mqr_build_tag(int which, char* buf, int cap) {
 int mqr_vbg_last_kernel(mqr_vbg* v, int* variant) {
     MQR_REQUIRE(v && variant, "null argument");
     *variant = v->last_var;
+    return 0;
+}
+
+int mqr_vbg_last_kernel_name(mqr_vbg* v, char* buf, int cap) {
+    MQR_REQUIRE(v && buf && cap > 0, "null argument");
+    std::snprintf(buf, (size_t)cap, "%s", v->last_kname);
     return 0;
 }
 const char* mqr_last_error(void) { return get_error(); }

@@ -41,6 +41,7 @@ SIGNATURES = {
     "mqr_build_tag": (ctypes.c_int, [ctypes.c_int, ctypes.c_char_p, ctypes.c_int]),
     "mqr_vbg_last_kernel": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int)]),
     "mqr_vbg_flips": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int64)]),
+    "mqr_vbg_last_kernel_name": (ctypes.c_int, [_vp, ctypes.c_char_p, ctypes.c_int]),
     "mqr_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
     "mqr_set_stream": (ctypes.c_int, [_vp]),
     "mqr_get_stream": (ctypes.c_int, [ctypes.POINTER(_vp)]),

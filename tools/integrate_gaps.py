@@ -19,7 +19,7 @@ def main():
     ap.add_argument("--per-step", type=int, default=4)
     a = ap.parse_args()
     df = pd.read_csv(a.trace, usecols=["Kernel_Name", "Start_Timestamp", "End_Timestamp"]).sort_values("Start_Timestamp")
-    is_int = df.Kernel_Name.str.contains("k_integrate_(?:win|lean)")
+    is_int = df.Kernel_Name.str.contains("k_integrate_(?:wt|win|lean)")
     integ = df[is_int].tail(a.launches)
     other = df[~is_int]
     s = integ.Start_Timestamp.to_numpy(np.int64)

@@ -19,7 +19,7 @@ def main():
     for i in range(max(0, len(starts) - n - 1), len(starts) - 1):
         s, e = starts[i], starts[i + 1]
         d = df[(df.Start_Timestamp >= s) & (df.Start_Timestamp < e)]
-        integ = d[d.Kernel_Name.str.contains("k_integrate_(?:win|lean)")]
+        integ = d[d.Kernel_Name.str.contains("k_integrate_(?:wt|win|lean)")]
         touch = d[d.Kernel_Name.str.contains("k_touch")]
         lpt = d[d.Kernel_Name.str.contains("k_lpt_order")]
         gate = d[d.Kernel_Name.str.contains("k_gate")]
