@@ -400,6 +400,18 @@ static int launch_integrate_ab(mqr_vbg* v, int var, hipStream_t s, unsigned grid
         case 60: wx(k_integrate_wx<7, 4>); break;  // the default + a workgroup barrier per frame
         case 61: wx(k_integrate_wx<6, 4>); break;
         case 62: *fixup = true; wx(k_integrate_wx<8, 6>); break;
+        case 65: case 66: case 67: {  // the default's kernel with OPT 1 / 2 / 3 (k_integrate_wt<7, DIV1, OPT>)
+            const int tcount = (int)v->launch_wbound;
+            const bool one = v->div1 && strunc_one_correction_ok(sdf_trunc);
+            auto kern = var == 65 ? (one ? k_integrate_wt<7, 1, 1> : k_integrate_wt<7, 0, 1>)
+                      : var == 66 ? (one ? k_integrate_wt<7, 1, 2> : k_integrate_wt<7, 0, 2>)
+                                  : (one ? k_integrate_wt<7, 1, 3> : k_integrate_wt<7, 0, 3>);
+            hipLaunchKernelGGL(kern, dim3(grid), dim3(512), sizeof(float2) * (size_t)tcount, s, list, lmask, bad_out,
+                               counters, v->list_cap, t, v->pool, v->voxel_size, depths, HW, H, W, fp, depth_frame,
+                               depth_max, sdf_trunc, first_new, tcount);
+            *fixup = true;
+            break;
+        }
         case 64: {  // the default's LDS-table kernel at >= 6 waves per SIMD (k_integrate_wt<6>)
             const int tcount = (int)v->launch_wbound;
             hipLaunchKernelGGL(k_integrate_wt<6>, dim3(grid), dim3(512), sizeof(float2) * (size_t)tcount, s, list, lmask,
@@ -602,10 +614,10 @@ static int launch_integrate(mqr_vbg* v, int p, const float* depths, int64_t HW, 
     //     the eight record loads issued first (>= 7 / 5 waves), 49 / 50 = 45 / 47 branch-free.  (24 of round 4, a ballot skip of
     //     out-of-image wave slots, ran 0.70 vs 0.48 ms per launch: removed.)
     int var = v->kernel_variant;
-    if (var < 0 || var > 64 || var == 63) var = 0;
+    if (var < 0 || var > 67 || var == 63) var = 0;
     // the LDS-table kernels (default, 64) need a known weight bound whose table fits a workgroup's LDS share
     const bool rtab_ok = v->rtab && v->launch_wbound >= 1 && v->launch_wbound <= kRtabMax;
-    if (var == 64 && !rtab_ok) var = 0;
+    if (var >= 64 && !rtab_ok) var = 0;
     if (!MQR_AB && var != 1 && var != 2 && var != 4) var = 0;
     if (var != 1 && var != 2 && !lean_ok) var = 2;
     if (var == 5 && (v->R != 16 || W % 4 != 0 || W < 4 || (reinterpret_cast<uintptr_t>(depths) & 15))) var = 0;

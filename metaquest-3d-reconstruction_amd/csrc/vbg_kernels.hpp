@@ -999,8 +999,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
 constexpr int kRtabMax = 6000;  // table entries: 48 KB of LDS, 3 workgroups per CU still fit
 
 // DIV1: s / sdf_trunc with one Markstein correction (host: strunc_one_correction_ok verified it for this
-// sdf_trunc over every s in [-t, t]), as lean_update_v<DIV1>.
-template <int WPE, int DIV1 = 0>
+// sdf_trunc over every s in [-t, t]), as lean_update_v<DIV1>.  OPT (A/B library only): bit 0 keeps the table
+// entries' LDS addresses themselves (no base add per read), bit 1 selects the pixel's dword of its 8-byte
+// window by one 64-bit shift (v_lshrrev_b64 by 8 * the byte offset; the shifter takes its low 6 bits).
+typedef __attribute__((address_space(3))) const float2 lds_float2;
+template <int WPE, int DIV1 = 0, int OPT = 0>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void k_integrate_wt(
     const int32_t* __restrict__ list, const bmask_t* __restrict__ lmask, int32_t* __restrict__ bad_out,
     int* __restrict__ counters, int64_t list_cap,
@@ -1023,6 +1026,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
     const int vx = (l & 7) + 8 * (w & 1), vy = ((l >> 3) & 1) + 2 * (w >> 1), vz = l >> 4;
     const uint32_t voff = 8u * (uint32_t)(vx + R * vy + R2 * vz);
     const char* tbase = reinterpret_cast<const char*>(rtab);
+    const uint32_t lbase = (OPT & 1) ? (uint32_t)(uintptr_t)(lds_float2*)rtab : 0u;  // LDS address of entry 0
     for (int64_t i = blockIdx.x; i < n; i += gridDim.x) {
         const int32_t slot = list[i];
         const int buf = __builtin_amdgcn_readfirstlane(t.vals[slot]);
@@ -1048,26 +1052,68 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
                 zs[k] = (float)(zb * R + vz + dz) * voxel_size;
                 bad |= !(tw.y >= 0.0f && tw.y <= wlim && tw.y == __builtin_truncf(tw.y));
                 ts[k] = tw.x;
-                wa[k] = 8u * (uint32_t)(bad ? 0.0f : tw.y);
+                wa[k] = lbase + 8u * (uint32_t)(bad ? 0.0f : tw.y);
             }
             bmask_t m = mask;
             while (m) {
                 const int f = bm_ctz(m);
                 m &= m - 1;
                 float dv[ZPER];
-                lean_gather_w<ZPER, 2, 8>(dv, bad, fps[f], frame_rsrc(depths + depth_frame[f] * HW, bytes), xs, ys, zs,
-                                          W4, bytes, hb, wb);
+                u32x2 qv[ZPER];
+                uint32_t shv[ZPER];
+                if constexpr ((OPT & 2) != 0) {  // lean_gather_w<ZPER, 2, 8>'s operations, the window kept whole
+                    const FrameParams& g = fps[f];
+                    const __amdgpu_buffer_rsrc_t rs = frame_rsrc(depths + depth_frame[f] * HW, bytes);
+                    float e[12];
+#pragma unroll
+                    for (int j = 0; j < 12; ++j) e[j] = g.ext[j];
+#pragma unroll
+                    for (int k = 0; k < ZPER; ++k) {
+                        const float ax = xs[k] * e[0] + ys[k] * e[1];
+                        const float ay = xs[k] * e[4] + ys[k] * e[5];
+                        const float az = xs[k] * e[8] + ys[k] * e[9];
+                        const float xc = (ax + zs[k] * e[2]) + e[3];
+                        const float yc = (ay + zs[k] * e[6]) + e[7];
+                        const float zc = (az + zs[k] * e[10]) + e[11];
+                        bad |= (__float_as_uint(zc) - 0x2D800000u) > 0x30000000u;
+                        const float inv_z = rcp_m(zc);
+                        const float u = g.fx * xc * inv_z + g.cx;
+                        const float v = g.fy * yc * inv_z + g.cy;
+                        const bool in = (__float_as_uint(v) <= hb) && (__float_as_uint(u) <= wb);
+                        const uint32_t off = in ? __umul24((uint32_t)(int)v, W4) + ((uint32_t)(int)u << 2) : bytes;
+                        qv[k] = __builtin_amdgcn_raw_buffer_load_b64(rs, off & ~7u, 0, 0);
+                        shv[k] = off << 3;
+                        if ((k + 1) % 2 == 0) __builtin_amdgcn_sched_barrier(0);
+                    }
+                } else {
+                    lean_gather_w<ZPER, 2, 8>(dv, bad, fps[f], frame_rsrc(depths + depth_frame[f] * HW, bytes), xs, ys,
+                                              zs, W4, bytes, hb, wb);
+                }
                 const FrameParams& fp = fps[f];
                 const float e8 = fp.ext[8], e9 = fp.ext[9], e10 = fp.ext[10], e11 = fp.ext[11];
 #pragma unroll
                 for (int k = 0; k < ZPER; ++k) {
                     const float az = xs[k] * e8 + ys[k] * e9;
                     const float zc = (az + zs[k] * e10) + e11;
-                    const float d = dv[k];
+                    float d;
+                    if constexpr ((OPT & 2) != 0) {
+                        uint64_t r;
+                        const uint64_t q64 = ((uint64_t)qv[k].y << 32) | qv[k].x;
+                        asm("v_lshrrev_b64 %0, %1, %2" : "=v"(r) : "v"(shv[k]), "v"(q64));
+                        d = __uint_as_float((uint32_t)r);
+                    } else {
+                        d = dv[k];
+                    }
                     const float sdf = d - zc;
                     if (!(d <= 0) && !(d > depth_max) && !(sdf < -sdf_trunc)) {
                         // the entry read first: its LDS latency overlaps the quotient
-                        const float2 e = *reinterpret_cast<const float2*>(tbase + wa[k]);  // (w, 1 / (w + 1))
+                        float2 e;  // (w, 1 / (w + 1))
+                        if constexpr ((OPT & 1) != 0) {
+                            lds_float2* px = (lds_float2*)(uintptr_t)wa[k];
+                            e = make_float2(px->x, px->y);
+                        } else {
+                            e = *reinterpret_cast<const float2*>(tbase + wa[k]);
+                        }
                         float s;
                         asm("v_min_f32 %0, %1, %2" : "=v"(s) : "s"(sdf_trunc), "v"(sdf));
                         const float q0 = s * y1t;
@@ -1085,7 +1131,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
 #pragma unroll
                 for (int k = 0; k < ZPER; ++k)
                     pool_store(vox, voff, (R * win_dy<NT>(k) + R2 * win_dz<NT>(k)) * (int)sizeof(float2),
-                               make_float2(ts[k], (float)(wa[k] >> 3)));
+                               make_float2(ts[k], (float)((wa[k] - lbase) >> 3)));
             }
         }
         __syncthreads();
